@@ -1,0 +1,201 @@
+#!/usr/bin/env python
+"""bench.py — NLP callback throughput (constraint + Jacobian evaluations per second) on MI355X.
+
+Workload (BASELINE.json configs[1], SURVEY.md section 8(d) cfg 2): OcpFes DingModelFrequency, 10 pulses at
+10 Hz, final time 1 s, n_shooting 20, end-force 100 N objective, bioptim default transcription RK1 x 10
+multiple shooting.  One "instance-evaluation" = g (40 continuity rows) + J_g (120 values) of one OCP
+instance.  Each GPU evaluates a resident batch of B instances (synthetic decision vectors, seeded) per
+step with ONE libcfx call (cfx_eval_all, device pointers, SoA layout) = one kernel launch.
+
+Multi-GPU (torchrun): instances are independent, so each rank owns its own batch (weak scaling, no
+data-path collective); only the timing max-reduction crosses ranks.
+
+Prints ONE JSON line on rank 0 with the roofline of the shooting kernel (achieved algorithmic HBM GB/s
+from HIP events on the launch stream vs 8 TB/s) and the CPU baseline (the plain-C oracle port of the
+as-written reference evaluation, OpenMP, timed on a bounded sample on this host).
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import pathlib
+import sys
+import time
+
+import numpy as np
+
+ROOT = pathlib.Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+METRIC = "NLP callback evals/s (constraint+Jac) and wall-clock to Ipopt-equiv convergence"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--batch", type=int, default=1 << 20, help="instances per GPU")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline sample budget (0: skip)")
+    return ap.parse_args()
+
+
+def build_problem():
+    from cocofest_amd import ModelMaker, OcpFes, OdeSolver
+
+    model = ModelMaker.create_model("ding2003", stim_time=[round(0.1 * i, 1) for i in range(10)],
+                                    sum_stim_truncation=20)
+    return OcpFes.prepare_ocp(model=model, final_time=1, objective={"end_node_tracking": 100},
+                              ode_solver=OdeSolver.RK1(n_integration_steps=10), n_shooting=20)
+
+
+def synthetic_soa(ocp, B, seed, device):
+    """SoA decision vectors (nv, B): Cn ~ U(0, 1.5), F ~ U(0, 250) at every node."""
+    import torch
+
+    gen = torch.Generator(device=device)
+    gen.manual_seed(seed)
+    v = torch.rand((ocp.nv, B), generator=gen, dtype=torch.float64, device=device)
+    scale = torch.tensor([1.5, 250.0] * (ocp.nv // 2), dtype=torch.float64, device=device)[:, None]
+    return v * scale
+
+
+def pmc_traffic():
+    """HBM bytes per launch of the shooting kernel from the committed rocprofv3 PMC summary, if any."""
+    f = ROOT / "profiles" / "pmc_traffic.json"
+    if not f.exists():
+        return None
+    try:
+        return json.loads(f.read_text()).get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def cpu_baseline(ocp, budget_s):
+    """The plain-C port of the reference's as-written evaluation (oracle/c), all usable host cores, on a
+    bounded sample of the same workload."""
+    from oracle import c_oracle, fes_oracle as O
+
+    threads = min(16, len(os.sched_getaffinity(0)))
+    pb = O.Problem(name="ding2003", c=O.model_constants("ding2003"), n_shooting=ocp.n_shooting, final_time=1.0,
+                   truncation=20, rows=ocp.stim_rows, scheme="RK1", n_steps=10)
+    rng = np.random.default_rng(0)
+    chunk = 4096
+    v = rng.uniform(0.0, 1.0, (chunk, pb.nv)) * np.tile([1.5, 250.0], pb.nv // 2)
+    c_oracle.shooting(pb, v[:64], threads=threads)  # warm-up / load
+    done, t0 = 0, time.perf_counter()
+    while True:
+        c_oracle.shooting(pb, v, threads=threads)
+        done += chunk
+        el = time.perf_counter() - t0
+        if el >= budget_s:
+            break
+    return {"value": done / el, "unit": "instance-evals/s", "cores": threads, "kind": "port",
+            "sample": f"{done} instances of cfg2 (g + J_g, as-written calcium sum: 2T-1 exp per RK stage), "
+                      f"oracle/c/fes_oracle.c, OpenMP {threads} threads, {el:.1f} s"}
+
+
+def main():
+    args = parse()
+    import torch
+
+    from cocofest_amd import _cfx
+
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local = int(os.environ.get("LOCAL_RANK", 0))
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    ocp = build_problem()
+    B = args.batch
+    h = ocp.nlp(batch=B, layout="soa", device=local)
+    v = synthetic_soa(ocp, B, seed=1234 + rank, device=f"cuda:{local}")
+    g = torch.empty((h.ng, B), dtype=torch.float64, device=f"cuda:{local}")
+    jac = torch.empty((h.nnz_jac, B), dtype=torch.float64, device=f"cuda:{local}")
+
+    for _ in range(args.warmup):
+        h.eval_all(v, g=g, jac=jac)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record()
+    for _ in range(args.steps):
+        h.eval_all(v, g=g, jac=jac)
+    ev1.record()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    kern_ms = ev0.elapsed_time(ev1) / args.steps  # one kernel launch per step, on this stream
+
+    t = torch.tensor([wall], dtype=torch.float64, device=f"cuda:{local}")
+    if dist:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    wall_max = float(t.item())
+    ms_per_step = wall_max / args.steps * 1e3
+    value = world * B / (wall_max / args.steps)
+
+    bytes_per_instance = 8 * (h.nv + h.ng + h.nnz_jac)  # read v, write g and J_g values
+    achieved = bytes_per_instance * B / (kern_ms * 1e-3) / 1e9
+    traffic = pmc_traffic()
+
+    out = None
+    if rank == 0:
+        cpu = cpu_baseline(ocp, args.cpu_seconds) if (world == 1 and args.cpu_seconds > 0) else None
+        out = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "instance-evals/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms_per_step,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (seeded decision vectors around physiological states)",
+            "config": {
+                "workload": "cfg2: OcpFes DingModelFrequency n_stim=10 @10Hz, final_time=1s, n_shooting=20, "
+                            "end_node_tracking=100N, RK1 x 10 multiple shooting; one step = g + J_g of every instance",
+                "batch_per_gpu": B,
+                "nv": h.nv, "ng": h.ng, "nnz_jac": h.nnz_jac,
+                "layout": "SoA (element-major, instance-minor), device-resident",
+                "parallelism": f"instances sharded over {world} GPU(s), no data-path collective",
+            },
+            "roofline": {
+                "bound": "hbm",
+                "kernel": "cfx::k_shooting<DING2003, RK1, D=2>",
+                "achieved": achieved,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS,
+                "traffic": traffic,
+                "bytes_per_instance": bytes_per_instance,
+                "kernel_ms": kern_ms,
+            },
+            "cpu_baseline": cpu,
+        }
+    h.close()
+    if dist:
+        dist.barrier()
+        dist.destroy_process_group()
+    if out is not None:
+        print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,31 @@
+"""cocofest_amd — MI355X-native NLP-evaluation engine for cocofest's FES optimal-control problems.
+
+The public names mirror the reference package (Ipuch/cocofest) for the accelerated path: the six FES
+models, ``ModelMaker``, ``OcpFes``, ``IvpFes``, ``FourierSeries`` and the bioptim-style ``OdeSolver`` /
+``ObjectiveFcn`` / ``ObjectiveList`` / ``Node`` the reference's call sites use.  All NLP callbacks and
+integrations execute in libcfx (hand-written HIP for gfx950) — there is no CPU evaluation path.
+"""
+
+from ._cfx import CfxError, Handle, load_library
+from .fes_models import (
+    DingModelFrequency,
+    DingModelFrequencyWithFatigue,
+    DingModelPulseIntensityFrequency,
+    DingModelPulseIntensityFrequencyWithFatigue,
+    DingModelPulseWidthFrequency,
+    DingModelPulseWidthFrequencyWithFatigue,
+    FesModel,
+    ModelMaker,
+)
+from .fourier import FourierSeries
+from .ivp import IvpFes
+from .ocp import FesOcp, Node, Objective, ObjectiveFcn, ObjectiveList, OcpFes
+from .ode_solver import ControlType, OdeSolver
+
+__all__ = [
+    "CfxError", "Handle", "load_library", "DingModelFrequency", "DingModelFrequencyWithFatigue",
+    "DingModelPulseIntensityFrequency", "DingModelPulseIntensityFrequencyWithFatigue",
+    "DingModelPulseWidthFrequency", "DingModelPulseWidthFrequencyWithFatigue", "FesModel", "ModelMaker",
+    "FourierSeries", "IvpFes", "FesOcp", "Node", "Objective", "ObjectiveFcn", "ObjectiveList", "OcpFes",
+    "ControlType", "OdeSolver",
+]

@@ -1,0 +1,287 @@
+"""ctypes binding of libcfx (include/cfx.h).
+
+The shared library is built in-tree (``cocofest_amd/libcfx.so``, see ``cocofest_amd/csrc/Makefile``).
+There is no CPU fallback: if the library is missing, or no HIP device is visible when a handle is
+created, a ``CfxError`` is raised.
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+import os
+import pathlib
+
+import numpy as np
+
+LIB_PATH = pathlib.Path(__file__).with_name("libcfx.so")
+
+ABI_VERSION = 1
+OK, EINVAL, EHIP, ENOMEM, EUNSUPPORTED, ENODEV = 0, -1, -2, -3, -4, -5
+MODEL_IDS = {
+    "ding2003": 0,
+    "ding2003_with_fatigue": 1,
+    "ding2007": 2,
+    "ding2007_with_fatigue": 3,
+    "hmed2018": 4,
+    "hmed2018_with_fatigue": 5,
+}
+RK1, RK2, RK4 = 1, 2, 4
+LAYOUT_AOS, LAYOUT_SOA = 0, 1
+DEVICE = 1
+OBJ_LAGRANGE, OBJ_MAYER = 0, 1
+VAR_STATE, VAR_CONTROL = 0, 1
+
+
+class CfxError(RuntimeError):
+    """Error raised by libcfx (carries the integer code)."""
+
+    def __init__(self, code, msg):
+        super().__init__(f"libcfx error {code}: {msg}")
+        self.code = code
+
+
+class Constants(C.Structure):
+    _fields_ = [(n, C.c_double) for n in (
+        "tauc", "r0_km_relationship", "a_rest", "tau1_rest", "tau2", "km_rest",
+        "a_scale", "pd0", "pdt", "ar", "bs", "Is", "cr",
+        "alpha_a", "alpha_tau1", "alpha_km", "tau_fat", "fl", "fv", "fp")]
+
+
+class Objective(C.Structure):
+    _fields_ = [
+        ("kind", C.c_int32), ("var_kind", C.c_int32), ("var_index", C.c_int32),
+        ("node_first", C.c_int32), ("node_last", C.c_int32),
+        ("weight", C.c_double), ("target", C.POINTER(C.c_double)), ("target_value", C.c_double),
+    ]
+
+
+class Problem(C.Structure):
+    _fields_ = [
+        ("abi_version", C.c_int32), ("model", C.c_int32), ("scheme", C.c_int32), ("n_steps", C.c_int32),
+        ("n_shooting", C.c_int32), ("truncation", C.c_int32), ("n_params", C.c_int32), ("layout", C.c_int32),
+        ("batch", C.c_int64), ("final_time", C.c_double),
+        ("stim_rows", C.POINTER(C.c_double)), ("last_stim_idx", C.POINTER(C.c_int32)),
+        ("intensity_floor", C.c_double), ("constants", Constants),
+        ("n_objectives", C.c_int32), ("objectives", C.POINTER(Objective)), ("device", C.c_int32),
+    ]
+
+
+class Sizes(C.Structure):
+    _fields_ = [("nv", C.c_int64), ("ng", C.c_int64), ("nnz_jac", C.c_int64), ("nnz_hess", C.c_int64),
+                ("nx", C.c_int32), ("nu", C.c_int32)]
+
+
+# exported symbols and their signatures (must match include/cfx.h)
+_P = C.c_void_p
+_D = C.POINTER(C.c_double)
+SIGNATURES = {
+    "cfx_create": (C.c_int, [C.POINTER(Problem), C.POINTER(_P)]),
+    "cfx_destroy": (None, [_P]),
+    "cfx_get_sizes": (C.c_int, [_P, C.POINTER(Sizes)]),
+    "cfx_set_stream": (C.c_int, [_P, _P]),
+    "cfx_synchronize": (C.c_int, [_P]),
+    "cfx_last_error": (C.c_char_p, [_P]),
+    "cfx_abi_version": (C.c_int, []),
+    "cfx_device_count": (C.c_int, []),
+    "cfx_jac_structure": (C.c_int, [_P, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
+    "cfx_hess_structure": (C.c_int, [_P, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
+    "cfx_eval_g": (C.c_int, [_P, _P, _P, C.c_uint32]),
+    "cfx_eval_jac_g": (C.c_int, [_P, _P, _P, C.c_uint32]),
+    "cfx_eval_f": (C.c_int, [_P, _P, _P, C.c_uint32]),
+    "cfx_eval_grad_f": (C.c_int, [_P, _P, _P, C.c_uint32]),
+    "cfx_eval_h": (C.c_int, [_P, _P, _P, _P, _P, C.c_uint32]),
+    "cfx_eval_all": (C.c_int, [_P, _P, _P, _P, _P, _P, C.c_uint32]),
+    "cfx_integrate": (C.c_int, [_P, _P, _P, _P, C.c_uint32]),
+}
+
+_lib = None
+
+
+def load_library(path: str | os.PathLike | None = None):
+    """Load libcfx.so (once) and declare every exported signature; raise if it is missing."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = pathlib.Path(path) if path else LIB_PATH
+    if not p.exists():
+        raise CfxError(ENODEV, f"{p} not found: build it with `make -C cocofest_amd/csrc` (no CPU fallback)")
+    lib = C.CDLL(str(p))
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.cfx_abi_version() != ABI_VERSION:
+        raise CfxError(EINVAL, "libcfx ABI version mismatch")
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def _ptr(a):
+    """Address of a numpy array / torch tensor (None -> NULL)."""
+    if a is None:
+        return None
+    if isinstance(a, np.ndarray):
+        return a.ctypes.data
+    return a.data_ptr()
+
+
+class Handle:
+    """One libcfx handle: a batch of B instances of one transcribed FES problem on one GPU.
+
+    Host numpy arrays are copied to the GPU and back synchronously; torch CUDA tensors (float64,
+    contiguous) are used in place and the call is enqueued on torch's current stream.
+    """
+
+    def __init__(self, *, model_id, constants: dict, scheme, n_steps, n_shooting, truncation, final_time,
+                 stim_rows, batch, layout=LAYOUT_SOA, n_params=0, last_stim_idx=None, intensity_floor=0.0,
+                 objectives=(), device=0):
+        self.lib = load_library()
+        self._keep = []
+        rows = np.ascontiguousarray(stim_rows, dtype=np.float64).reshape(-1)
+        self._keep.append(rows)
+        pb = Problem()
+        pb.abi_version = ABI_VERSION
+        pb.model = model_id
+        pb.scheme = scheme
+        pb.n_steps = n_steps
+        pb.n_shooting = n_shooting
+        pb.truncation = truncation
+        pb.n_params = n_params
+        pb.layout = layout
+        pb.batch = batch
+        pb.final_time = final_time
+        pb.stim_rows = rows.ctypes.data_as(_D)
+        if last_stim_idx is not None:
+            li = np.ascontiguousarray(last_stim_idx, dtype=np.int32)
+            self._keep.append(li)
+            pb.last_stim_idx = li.ctypes.data_as(C.POINTER(C.c_int32))
+        pb.intensity_floor = intensity_floor
+        cst = Constants()
+        for name, _ in Constants._fields_:
+            setattr(cst, name, float(constants.get(name, 0.0)))
+        pb.constants = cst
+        objs = (Objective * max(1, len(objectives)))()
+        for i, o in enumerate(objectives):
+            objs[i].kind = o["kind"]
+            objs[i].var_kind = o["var_kind"]
+            objs[i].var_index = o["var_index"]
+            objs[i].node_first = o["node_first"]
+            objs[i].node_last = o["node_last"]
+            objs[i].weight = o["weight"]
+            if o.get("target") is not None:
+                t = np.ascontiguousarray(o["target"], dtype=np.float64)
+                self._keep.append(t)
+                objs[i].target = t.ctypes.data_as(_D)
+            objs[i].target_value = float(o.get("target_value", 0.0))
+        self._keep.append(objs)
+        pb.n_objectives = len(objectives)
+        pb.objectives = objs
+        pb.device = device
+        h = C.c_void_p()
+        rc = self.lib.cfx_create(C.byref(pb), C.byref(h))
+        if rc != OK:
+            raise CfxError(rc, self.lib.cfx_last_error(None).decode())
+        self.h = h
+        sz = Sizes()
+        self._check(self.lib.cfx_get_sizes(self.h, C.byref(sz)))
+        self.nv, self.ng, self.nnz_jac, self.nnz_hess = sz.nv, sz.ng, sz.nnz_jac, sz.nnz_hess
+        self.nx, self.nu = sz.nx, sz.nu
+        self.batch, self.layout, self.n_shooting, self.n_steps = batch, layout, n_shooting, n_steps
+        self.device = device
+
+    def _check(self, rc):
+        if rc != OK:
+            raise CfxError(rc, self.lib.cfx_last_error(self.h).decode())
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.cfx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- structure ----
+    def jac_structure(self):
+        r = np.empty(self.nnz_jac, dtype=np.int32)
+        c = np.empty(self.nnz_jac, dtype=np.int32)
+        self._check(self.lib.cfx_jac_structure(self.h, r.ctypes.data_as(C.POINTER(C.c_int32)),
+                                               c.ctypes.data_as(C.POINTER(C.c_int32))))
+        return r, c
+
+    def hess_structure(self):
+        r = np.empty(self.nnz_hess, dtype=np.int32)
+        c = np.empty(self.nnz_hess, dtype=np.int32)
+        self._check(self.lib.cfx_hess_structure(self.h, r.ctypes.data_as(C.POINTER(C.c_int32)),
+                                                c.ctypes.data_as(C.POINTER(C.c_int32))))
+        return r, c
+
+    # ---- evaluation ----
+    @staticmethod
+    def _flags(*arrays):
+        dev = [a for a in arrays if a is not None and not isinstance(a, np.ndarray)]
+        if dev and len(dev) != len([a for a in arrays if a is not None]):
+            raise CfxError(EINVAL, "mix of host and device buffers in one call")
+        for a in dev:
+            if not a.is_contiguous() or str(a.dtype) != "torch.float64":
+                raise CfxError(EINVAL, "device buffers must be contiguous float64 tensors")
+        return DEVICE if dev else 0
+
+    def set_stream(self, stream_ptr):
+        self._check(self.lib.cfx_set_stream(self.h, stream_ptr))
+
+    def _torch_stream(self, flags):
+        if flags & DEVICE:
+            import torch
+
+            self._check(self.lib.cfx_set_stream(self.h, torch.cuda.current_stream().cuda_stream))
+
+    def _shape(self, n):
+        return (self.batch, n) if self.layout == LAYOUT_AOS else (n, self.batch)
+
+    def eval_all(self, v, g=None, jac=None, f=None, grad=None):
+        fl = self._flags(v, g, jac, f, grad)
+        self._torch_stream(fl)
+        self._check(self.lib.cfx_eval_all(self.h, _ptr(v), _ptr(g), _ptr(jac), _ptr(f), _ptr(grad), fl))
+
+    def eval_g(self, v, g=None):
+        g = np.empty(self._shape(self.ng)) if g is None else g
+        self.eval_all(v, g=g)
+        return g
+
+    def eval_jac_g(self, v, jac=None):
+        jac = np.empty(self._shape(self.nnz_jac)) if jac is None else jac
+        self.eval_all(v, jac=jac)
+        return jac
+
+    def eval_f(self, v, f=None):
+        f = np.empty(self.batch) if f is None else f
+        self.eval_all(v, f=f)
+        return f
+
+    def eval_grad_f(self, v, grad=None):
+        grad = np.empty(self._shape(self.nv)) if grad is None else grad
+        self.eval_all(v, grad=grad)
+        return grad
+
+    def eval_h(self, v, obj_factor, lam, hess=None):
+        hess = np.empty(self._shape(self.nnz_hess)) if hess is None else hess
+        fl = self._flags(v, obj_factor, lam, hess)
+        self._torch_stream(fl)
+        self._check(self.lib.cfx_eval_h(self.h, _ptr(v), _ptr(obj_factor), _ptr(lam), _ptr(hess), fl))
+        return hess
+
+    def integrate(self, x0=None, u=None, traj=None):
+        n = (self.n_shooting * self.n_steps + 1) * self.nx
+        traj = np.empty(self._shape(n)) if traj is None else traj
+        fl = self._flags(x0, u, traj)
+        self._torch_stream(fl)
+        self._check(self.lib.cfx_integrate(self.h, _ptr(x0), _ptr(u), _ptr(traj), fl))
+        return traj
+
+    def synchronize(self):
+        self._check(self.lib.cfx_synchronize(self.h))

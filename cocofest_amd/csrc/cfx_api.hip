@@ -1,0 +1,526 @@
+// cfx_api.hip — the C ABI of libcfx (include/cfx.h): problem set-up on the host, stimulation
+// coefficient tables, sparsity, buffer staging, and the launches of the gfx950 kernels.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/cfx.h"
+#include "cfx_aux.h"
+#include "cfx_launch.h"
+
+using namespace cfx;
+
+namespace {
+
+thread_local std::string g_create_error;
+
+enum Slot { S_V = 0, S_A1, S_A2, S_G, S_J, S_F, S_GRAD, S_OUT, S_COUNT };
+
+struct DevBuf {
+    double* p = nullptr;
+    size_t n = 0;
+};
+
+}  // namespace
+
+struct cfx_handle {
+    cfx_problem prob{};
+    std::vector<double> rows;
+    std::vector<int32_t> last_idx;
+    std::vector<cfx_objective> objs;
+    cfx_sizes sz{};
+    int model = 0, scheme = 1, tmax = 1, stages = 1;
+    KParams kp{};
+    int device = 0;
+    hipStream_t own_stream = nullptr, stream = nullptr;
+    double* d_tab = nullptr;
+    double* d_rest = nullptr;
+    DevObjective* d_obj = nullptr;
+    double* d_targets = nullptr;
+    int32_t* d_sl_param = nullptr;
+    int32_t* d_sl_joff = nullptr;
+    int n_obj = 0;
+    std::vector<int32_t> jrow, jcol, hrow, hcol;
+    DevBuf main[S_COUNT], stage[S_COUNT];
+    std::string err;
+};
+
+#define CFX_HIP(h, call)                                                                      \
+    do {                                                                                      \
+        hipError_t e_ = (call);                                                               \
+        if (e_ != hipSuccess) {                                                               \
+            (h)->err = std::string(#call) + ": " + hipGetErrorString(e_);                     \
+            return CFX_EHIP;                                                                  \
+        }                                                                                     \
+    } while (0)
+
+static int fail(cfx_handle* h, int code, const std::string& msg) {
+    h->err = msg;
+    return code;
+}
+
+// ------------------------------------------------------------------------------------------------------
+// stimulation coefficients (cocofest/models/ding2003.py:200-252; hmed2018.py:97-98)
+// ------------------------------------------------------------------------------------------------------
+static void build_tables(const cfx_handle* h, std::vector<double>& tab) {
+    const cfx_problem& p = h->prob;
+    const cfx_constants& c = p.constants;
+    const int N = p.n_shooting, m = p.n_steps, T = p.truncation, S = h->stages;
+    const double dt = p.final_time / N;
+    const double hh = dt / m;
+    const double r0 = c.km_rest + c.r0_km_relationship;
+    const bool hmed = is_int(h->model);
+    const int Q = m * S;
+    tab.assign((size_t)N * Q * (hmed ? h->tmax : 1), 0.0);
+    std::vector<double> ri(T);
+    for (int k = 0; k < N; ++k) {
+        const double* row = &h->rows[(size_t)k * T];
+        for (int i = 0; i < T; ++i) ri[i] = i == 0 ? 1.0 : 1.0 + (r0 - 1.0) * std::exp(-(row[i] - row[i - 1]) / c.tauc);
+        const double t0 = k * dt;
+        for (int j = 0; j < m; ++j) {
+            const double tj = t0 + j * hh;
+            for (int s = 0; s < S; ++s) {
+                double t = tj;
+                if (S == 2 && s == 1) t = tj + hh / 2;
+                if (S == 4 && (s == 1 || s == 2)) t = tj + hh / 2;
+                if (S == 4 && s == 3) t = tj + hh;
+                const size_t q = (size_t)k * Q + (size_t)j * S + s;
+                if (hmed) {
+                    for (int i = 0; i < T; ++i) tab[q * h->tmax + i] = ri[i] * std::exp(-(t - row[i]) / c.tauc);
+                } else {
+                    double sum = 0.0;
+                    for (int i = 0; i < T; ++i) sum = sum + ri[i] * std::exp(-(t - row[i]) / c.tauc);
+                    tab[q] = sum;
+                }
+            }
+        }
+    }
+}
+
+static double* ensure(cfx_handle* h, DevBuf& b, size_t count, int* rc) {
+    if (b.n < count) {
+        if (b.p) (void)hipFree(b.p);
+        b.p = nullptr;
+        b.n = 0;
+        hipError_t e = hipMalloc((void**)&b.p, count * sizeof(double));
+        if (e != hipSuccess) {
+            h->err = std::string("hipMalloc: ") + hipGetErrorString(e);
+            *rc = CFX_ENOMEM;
+            return nullptr;
+        }
+        b.n = count;
+    }
+    return b.p;
+}
+
+static dim3 tgrid(int64_t B, int64_t len) { return dim3((unsigned)((B + 63) / 64), (unsigned)((len + 63) / 64)); }
+
+// Device SoA view of an input buffer of `len` doubles per instance.
+static const double* stage_in(cfx_handle* h, int slot, const double* ptr, int64_t len, uint32_t flags, int* rc) {
+    const int64_t B = h->prob.batch;
+    const bool dev = flags & CFX_DEVICE;
+    const bool aos = h->prob.layout == CFX_LAYOUT_AOS && len > 1;
+    if (dev && !aos) return ptr;
+    const size_t n = (size_t)B * len;
+    double* m = ensure(h, h->main[slot], n, rc);
+    if (!m) return nullptr;
+    const double* src = ptr;
+    if (!dev) {
+        double* target = aos ? ensure(h, h->stage[slot], n, rc) : m;
+        if (!target) return nullptr;
+        if (hipMemcpyAsync(target, ptr, n * sizeof(double), hipMemcpyHostToDevice, h->stream) != hipSuccess) {
+            *rc = CFX_EHIP;
+            h->err = "hipMemcpyAsync H2D failed";
+            return nullptr;
+        }
+        if (!aos) return m;
+        src = target;
+    }
+    hipLaunchKernelGGL(k_aos_to_soa, tgrid(B, len), dim3(256), 0, h->stream, src, m, B, len);
+    return m;
+}
+
+// Device SoA buffer an output is written to.
+static double* stage_out(cfx_handle* h, int slot, double* ptr, int64_t len, uint32_t flags, int* rc) {
+    const bool dev = flags & CFX_DEVICE;
+    const bool aos = h->prob.layout == CFX_LAYOUT_AOS && len > 1;
+    if (dev && !aos) return ptr;
+    return ensure(h, h->main[slot], (size_t)h->prob.batch * len, rc);
+}
+
+static int finish_out(cfx_handle* h, int slot, double* soa, double* ptr, int64_t len, uint32_t flags) {
+    const int64_t B = h->prob.batch;
+    const bool dev = flags & CFX_DEVICE;
+    const bool aos = h->prob.layout == CFX_LAYOUT_AOS && len > 1;
+    const size_t n = (size_t)B * len;
+    if (dev && !aos) return CFX_OK;
+    double* src = soa;
+    if (aos) {
+        int rc = CFX_OK;
+        double* dst = dev ? ptr : ensure(h, h->stage[slot], n, &rc);
+        if (!dst) return rc;
+        hipLaunchKernelGGL(k_soa_to_aos, tgrid(B, len), dim3(256), 0, h->stream, soa, dst, B, len);
+        if (dev) return CFX_OK;
+        src = dst;
+    }
+    CFX_HIP(h, hipMemcpyAsync(ptr, src, n * sizeof(double), hipMemcpyDeviceToHost, h->stream));
+    return CFX_OK;
+}
+
+static int sync_if_host(cfx_handle* h, uint32_t flags) {
+    if (!(flags & CFX_DEVICE)) CFX_HIP(h, hipStreamSynchronize(h->stream));
+    CFX_HIP(h, hipGetLastError());
+    return CFX_OK;
+}
+
+// ------------------------------------------------------------------------------------------------------
+// lifetime
+// ------------------------------------------------------------------------------------------------------
+static int create_fail(cfx_handle* h, int code, const std::string& msg) {
+    g_create_error = msg;
+    if (h) cfx_destroy(h);
+    return code;
+}
+
+extern "C" int cfx_abi_version(void) { return CFX_ABI_VERSION; }
+
+extern "C" int cfx_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+extern "C" int cfx_create(const cfx_problem* p, cfx_handle** out) {
+    if (!p || !out) return create_fail(nullptr, CFX_EINVAL, "cfx_create: NULL argument");
+    *out = nullptr;
+    if (p->abi_version != CFX_ABI_VERSION) return create_fail(nullptr, CFX_EINVAL, "cfx_create: ABI version mismatch");
+    if (p->model < CFX_DING2003 || p->model > CFX_HMED2018_FATIGUE)
+        return create_fail(nullptr, CFX_EINVAL, "cfx_create: unknown model");
+    if (p->scheme != CFX_RK1 && p->scheme != CFX_RK2 && p->scheme != CFX_RK4)
+        return create_fail(nullptr, CFX_EUNSUPPORTED, "cfx_create: scheme must be CFX_RK1, CFX_RK2 or CFX_RK4");
+    if (p->n_steps < 1 || p->n_shooting < 1 || p->batch < 1 || !(p->final_time > 0.0))
+        return create_fail(nullptr, CFX_EINVAL, "cfx_create: n_steps, n_shooting, batch and final_time must be positive");
+    if (p->truncation < 1 || p->truncation > 32)
+        return create_fail(nullptr, CFX_EUNSUPPORTED, "cfx_create: truncation must be in [1, 32]");
+    if (p->layout != CFX_LAYOUT_AOS && p->layout != CFX_LAYOUT_SOA)
+        return create_fail(nullptr, CFX_EINVAL, "cfx_create: unknown layout");
+    if (!p->stim_rows) return create_fail(nullptr, CFX_EINVAL, "cfx_create: stim_rows is NULL");
+    const bool hmed = p->model >= CFX_HMED2018;
+    if (p->n_params < 0 || (p->n_params > 0 && (!hmed || !p->last_stim_idx)))
+        return create_fail(nullptr, CFX_EINVAL,
+                           "cfx_create: intensity parameters need a Hmed2018 model and last_stim_idx");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1)
+        return create_fail(nullptr, CFX_ENODEV, "cfx_create: no HIP device available (libcfx has no CPU path)");
+    if (p->device < 0 || p->device >= ndev) return create_fail(nullptr, CFX_ENODEV, "cfx_create: bad device ordinal");
+
+    cfx_handle* h = new cfx_handle();
+    h->prob = *p;
+    h->model = p->model;
+    h->scheme = p->scheme;
+    h->stages = stages_of(p->scheme);
+    h->device = p->device;
+    const int N = p->n_shooting, T = p->truncation;
+    h->rows.assign(p->stim_rows, p->stim_rows + (size_t)(N + 1) * T);
+    if (p->n_params > 0) {
+        h->last_idx.assign(p->last_stim_idx, p->last_stim_idx + N);
+        for (int k = 0; k < N; ++k)
+            if (h->last_idx[k] >= p->n_params)
+                return create_fail(h, CFX_EINVAL, "cfx_create: last_stim_idx out of the parameter range");
+    }
+    h->prob.stim_rows = nullptr;
+    h->prob.last_stim_idx = nullptr;
+    h->tmax = hmed ? tmax_bucket(T) : 1;
+
+    const int nx = is_fatigue(h->model) ? 5 : 2;
+    const int nu = is_pw(h->model) ? 1 : (hmed ? T : 0);
+    const int nz = nx + nu;
+    const int n_slide = (hmed && p->n_params > 0) ? T : 0;
+    const int ngk = nx + n_slide;
+
+    // objectives
+    std::vector<DevObjective> dobj;
+    std::vector<double> targets;
+    for (int t = 0; t < p->n_objectives; ++t) {
+        const cfx_objective& o = p->objectives[t];
+        const bool st = o.var_kind == CFX_VAR_STATE;
+        const int lim = st ? N : N - 1;
+        if ((o.var_kind != CFX_VAR_STATE && o.var_kind != CFX_VAR_CONTROL) || o.var_index < 0 ||
+            o.var_index >= (st ? nx : nu) || o.node_first < 0 || o.node_last > lim || o.node_first > o.node_last ||
+            (o.kind != CFX_OBJ_LAGRANGE && o.kind != CFX_OBJ_MAYER))
+            return create_fail(h, CFX_EINVAL, "cfx_create: invalid objective term " + std::to_string(t));
+        DevObjective d{};
+        d.var_kind = st ? 0 : 1;
+        d.var_index = o.var_index;
+        d.node_first = o.node_first;
+        d.node_last = o.node_last;
+        d.w_eff = o.weight * (o.kind == CFX_OBJ_LAGRANGE ? p->final_time / N : 1.0);
+        d.target_value = o.target_value;
+        d.target_off = -1;
+        if (o.target) {
+            d.target_off = (int32_t)targets.size();
+            targets.insert(targets.end(), o.target, o.target + N + 1);
+        }
+        dobj.push_back(d);
+    }
+    h->n_obj = (int)dobj.size();
+    h->prob.objectives = nullptr;
+
+    // sizes + sparsity
+    h->sz.nx = nx;
+    h->sz.nu = nu;
+    h->sz.nv = (int64_t)N * nz + nx + p->n_params;
+    h->sz.ng = (int64_t)N * ngk;
+    const int nnzk = nx * (nz + 1);
+    const int nhk = nz * (nz + 1) / 2;
+    for (int k = 0; k < N; ++k) {
+        for (int r = 0; r < nx; ++r) {
+            for (int c = 0; c < nz; ++c) {
+                h->jrow.push_back(k * ngk + r);
+                h->jcol.push_back(k * nz + c);
+            }
+            h->jrow.push_back(k * ngk + r);
+            h->jcol.push_back((k + 1) * nz + r);
+        }
+    }
+    std::vector<int32_t> sl_param, sl_joff;
+    const int p_off = N * nz + nx;
+    if (n_slide) {
+        for (int k = 0; k < N; ++k) {
+            const int idx = h->last_idx[k];
+            const int first = idx + 1 - T;
+            for (int j = 0; j < T; ++j) {
+                const int pi = first + j;
+                const bool valid = pi >= 0 && pi <= idx;
+                sl_param.push_back(valid ? pi : -1);
+                sl_joff.push_back((int32_t)h->jrow.size());
+                h->jrow.push_back(k * ngk + nx + j);
+                h->jcol.push_back(k * nz + nx + j);
+                if (valid) {
+                    h->jrow.push_back(k * ngk + nx + j);
+                    h->jcol.push_back(p_off + pi);
+                }
+            }
+        }
+    }
+    h->sz.nnz_jac = (int64_t)h->jrow.size();
+    for (int k = 0; k < N; ++k)
+        for (int i = 0; i < nz; ++i)
+            for (int j = 0; j <= i; ++j) {
+                h->hrow.push_back(k * nz + i);
+                h->hcol.push_back(k * nz + j);
+            }
+    for (int r = 0; r < nx; ++r) {
+        h->hrow.push_back(N * nz + r);
+        h->hcol.push_back(N * nz + r);
+    }
+    h->sz.nnz_hess = (int64_t)h->hrow.size();
+
+    // kernel parameters
+    const cfx_constants& c = p->constants;
+    KParams& kp = h->kp;
+    kp.B = p->batch;
+    kp.nx = nx;
+    kp.N = N;
+    kp.m = p->n_steps;
+    kp.nu = nu;
+    kp.nz = nz;
+    kp.T = T;
+    kp.Q = p->n_steps * h->stages;
+    kp.ngk = ngk;
+    kp.nnzk = nnzk;
+    kp.nhk = nhk;
+    kp.n_slide = n_slide;
+    kp.n_params = p->n_params;
+    kp.dt = p->final_time / N;
+    kp.h = kp.dt / p->n_steps;
+    kp.inv_tauc = 1.0 / c.tauc;
+    kp.tau2 = c.tau2;
+    kp.km_rest = c.km_rest;
+    kp.tau1_rest = c.tau1_rest;
+    kp.a_rest = c.a_rest;
+    kp.a_scale = c.a_scale;
+    kp.pd0 = c.pd0;
+    kp.pdt = c.pdt;
+    kp.ar = c.ar;
+    kp.bs = c.bs;
+    kp.Is = c.Is;
+    kp.cr = c.cr;
+    kp.alpha_a = c.alpha_a;
+    kp.alpha_tau1 = c.alpha_tau1;
+    kp.alpha_km = c.alpha_km;
+    kp.inv_tau_fat = is_fatigue(h->model) ? 1.0 / c.tau_fat : 0.0;
+    kp.a_fat_rest = is_pw(h->model) ? c.a_scale : c.a_rest;
+    kp.mult = c.fl * c.fv + c.fp;
+
+    if (hipSetDevice(h->device) != hipSuccess) return create_fail(h, CFX_EHIP, "cfx_create: hipSetDevice failed");
+    if (hipStreamCreateWithFlags(&h->own_stream, hipStreamNonBlocking) != hipSuccess)
+        return create_fail(h, CFX_EHIP, "cfx_create: hipStreamCreate failed");
+    h->stream = h->own_stream;
+
+    std::vector<double> tab;
+    build_tables(h, tab);
+    std::vector<double> rest(nx, 0.0);
+    if (nx == 5) {
+        rest[2] = kp.a_fat_rest;
+        rest[3] = c.tau1_rest;
+        rest[4] = c.km_rest;
+    }
+    auto upload = [&](void** dst, const void* src, size_t bytes) -> bool {
+        if (bytes == 0) return true;
+        if (hipMalloc(dst, bytes) != hipSuccess) return false;
+        return hipMemcpy(*dst, src, bytes, hipMemcpyHostToDevice) == hipSuccess;
+    };
+    if (!upload((void**)&h->d_tab, tab.data(), tab.size() * sizeof(double)) ||
+        !upload((void**)&h->d_rest, rest.data(), rest.size() * sizeof(double)) ||
+        !upload((void**)&h->d_obj, dobj.data(), dobj.size() * sizeof(DevObjective)) ||
+        !upload((void**)&h->d_targets, targets.data(), targets.size() * sizeof(double)) ||
+        !upload((void**)&h->d_sl_param, sl_param.data(), sl_param.size() * sizeof(int32_t)) ||
+        !upload((void**)&h->d_sl_joff, sl_joff.data(), sl_joff.size() * sizeof(int32_t)))
+        return create_fail(h, CFX_ENOMEM, "cfx_create: device allocation/upload failed");
+    kp.tab = h->d_tab;
+    kp.rest = h->d_rest;
+    *out = h;
+    return CFX_OK;
+}
+
+extern "C" void cfx_destroy(cfx_handle* h) {
+    if (!h) return;
+    (void)hipSetDevice(h->device);
+    if (h->stream) (void)hipStreamSynchronize(h->stream);
+    for (int s = 0; s < S_COUNT; ++s) {
+        if (h->main[s].p) (void)hipFree(h->main[s].p);
+        if (h->stage[s].p) (void)hipFree(h->stage[s].p);
+    }
+    for (void* p : {(void*)h->d_tab, (void*)h->d_rest, (void*)h->d_obj, (void*)h->d_targets, (void*)h->d_sl_param,
+                    (void*)h->d_sl_joff})
+        if (p) (void)hipFree(p);
+    if (h->own_stream) (void)hipStreamDestroy(h->own_stream);
+    delete h;
+}
+
+extern "C" int cfx_get_sizes(const cfx_handle* h, cfx_sizes* out) {
+    if (!h || !out) return CFX_EINVAL;
+    *out = h->sz;
+    return CFX_OK;
+}
+
+extern "C" int cfx_set_stream(cfx_handle* h, void* stream) {
+    if (!h) return CFX_EINVAL;
+    h->stream = stream ? (hipStream_t)stream : h->own_stream;
+    return CFX_OK;
+}
+
+extern "C" int cfx_synchronize(cfx_handle* h) {
+    if (!h) return CFX_EINVAL;
+    CFX_HIP(h, hipStreamSynchronize(h->stream));
+    return CFX_OK;
+}
+
+extern "C" const char* cfx_last_error(const cfx_handle* h) { return h ? h->err.c_str() : g_create_error.c_str(); }
+
+extern "C" int cfx_jac_structure(const cfx_handle* h, int32_t* row, int32_t* col) {
+    if (!h || !row || !col) return CFX_EINVAL;
+    std::memcpy(row, h->jrow.data(), h->jrow.size() * sizeof(int32_t));
+    std::memcpy(col, h->jcol.data(), h->jcol.size() * sizeof(int32_t));
+    return CFX_OK;
+}
+
+extern "C" int cfx_hess_structure(const cfx_handle* h, int32_t* row, int32_t* col) {
+    if (!h || !row || !col) return CFX_EINVAL;
+    std::memcpy(row, h->hrow.data(), h->hrow.size() * sizeof(int32_t));
+    std::memcpy(col, h->hcol.data(), h->hcol.size() * sizeof(int32_t));
+    return CFX_OK;
+}
+
+// ------------------------------------------------------------------------------------------------------
+// evaluation
+// ------------------------------------------------------------------------------------------------------
+static hipError_t launch_shooting(cfx_handle* h, bool derivs, const double* V, double* G, double* J) {
+    if (is_int(h->model)) return launch_shooting_hmed(h->model, h->scheme, derivs, h->tmax, h->kp, V, G, J, h->stream);
+    return launch_shooting_ding(h->model, h->scheme, derivs, h->kp, V, G, J, h->stream);
+}
+
+extern "C" int cfx_eval_all(cfx_handle* h, const double* v, double* g, double* jac, double* f, double* grad,
+                            uint32_t flags) {
+    if (!h || !v) return CFX_EINVAL;
+    CFX_HIP(h, hipSetDevice(h->device));
+    int rc = CFX_OK;
+    const int64_t B = h->prob.batch;
+    const double* V = stage_in(h, S_V, v, h->sz.nv, flags, &rc);
+    if (!V) return rc;
+    double* G = g ? stage_out(h, S_G, g, h->sz.ng, flags, &rc) : nullptr;
+    double* J = jac ? stage_out(h, S_J, jac, h->sz.nnz_jac, flags, &rc) : nullptr;
+    double* F = f ? stage_out(h, S_F, f, 1, flags, &rc) : nullptr;
+    double* GR = grad ? stage_out(h, S_GRAD, grad, h->sz.nv, flags, &rc) : nullptr;
+    if (rc != CFX_OK) return rc;
+    if (G || J) {
+        CFX_HIP(h, launch_shooting(h, J != nullptr, V, G, J));
+        if (h->kp.n_slide)
+            hipLaunchKernelGGL(k_slide, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, h->stream, h->kp, h->d_sl_param,
+                               h->d_sl_joff, h->prob.intensity_floor, V, G, J);
+    }
+    if (F || GR) {
+        if (GR) CFX_HIP(h, hipMemsetAsync(GR, 0, (size_t)B * h->sz.nv * sizeof(double), h->stream));
+        hipLaunchKernelGGL(k_objective, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, h->stream, h->kp, h->n_obj,
+                           h->d_obj, h->d_targets, V, F, GR);
+    }
+    CFX_HIP(h, hipGetLastError());
+    if (G && (rc = finish_out(h, S_G, G, g, h->sz.ng, flags)) != CFX_OK) return rc;
+    if (J && (rc = finish_out(h, S_J, J, jac, h->sz.nnz_jac, flags)) != CFX_OK) return rc;
+    if (F && (rc = finish_out(h, S_F, F, f, 1, flags)) != CFX_OK) return rc;
+    if (GR && (rc = finish_out(h, S_GRAD, GR, grad, h->sz.nv, flags)) != CFX_OK) return rc;
+    return sync_if_host(h, flags);
+}
+
+extern "C" int cfx_eval_g(cfx_handle* h, const double* v, double* g, uint32_t flags) {
+    if (!g) return h ? fail(h, CFX_EINVAL, "cfx_eval_g: g is NULL") : CFX_EINVAL;
+    return cfx_eval_all(h, v, g, nullptr, nullptr, nullptr, flags);
+}
+
+extern "C" int cfx_eval_jac_g(cfx_handle* h, const double* v, double* jac, uint32_t flags) {
+    if (!jac) return h ? fail(h, CFX_EINVAL, "cfx_eval_jac_g: jac is NULL") : CFX_EINVAL;
+    return cfx_eval_all(h, v, nullptr, jac, nullptr, nullptr, flags);
+}
+
+extern "C" int cfx_eval_f(cfx_handle* h, const double* v, double* f, uint32_t flags) {
+    if (!f) return h ? fail(h, CFX_EINVAL, "cfx_eval_f: f is NULL") : CFX_EINVAL;
+    return cfx_eval_all(h, v, nullptr, nullptr, f, nullptr, flags);
+}
+
+extern "C" int cfx_eval_grad_f(cfx_handle* h, const double* v, double* grad, uint32_t flags) {
+    if (!grad) return h ? fail(h, CFX_EINVAL, "cfx_eval_grad_f: grad is NULL") : CFX_EINVAL;
+    return cfx_eval_all(h, v, nullptr, nullptr, nullptr, grad, flags);
+}
+
+extern "C" int cfx_eval_h(cfx_handle* h, const double* v, const double* obj_factor, const double* lambda,
+                          double* hess, uint32_t flags) {
+    (void)v;
+    (void)obj_factor;
+    (void)lambda;
+    (void)hess;
+    (void)flags;
+    return h ? fail(h, CFX_EUNSUPPORTED, "cfx_eval_h: not built yet") : CFX_EINVAL;
+}
+
+extern "C" int cfx_integrate(cfx_handle* h, const double* x0, const double* u, double* traj, uint32_t flags) {
+    if (!h || !traj) return CFX_EINVAL;
+    if (h->sz.nu > 0 && !u) return fail(h, CFX_EINVAL, "cfx_integrate: this model needs per-interval controls");
+    CFX_HIP(h, hipSetDevice(h->device));
+    int rc = CFX_OK;
+    const int64_t nsamp = (int64_t)h->kp.N * h->kp.m + 1;
+    const double* X0 = x0 ? stage_in(h, S_A1, x0, h->sz.nx, flags, &rc) : nullptr;
+    if (x0 && !X0) return rc;
+    const double* U = h->sz.nu ? stage_in(h, S_A2, u, (int64_t)h->kp.N * h->sz.nu, flags, &rc) : nullptr;
+    if (h->sz.nu && !U) return rc;
+    double* TR = stage_out(h, S_OUT, traj, nsamp * h->sz.nx, flags, &rc);
+    if (!TR) return rc;
+    hipError_t e = is_int(h->model) ? launch_ivp_hmed(h->model, h->scheme, h->tmax, h->kp, X0, U, TR, h->stream)
+                                    : launch_ivp_ding(h->model, h->scheme, h->kp, X0, U, TR, h->stream);
+    CFX_HIP(h, e);
+    if ((rc = finish_out(h, S_OUT, TR, traj, nsamp * h->sz.nx, flags)) != CFX_OK) return rc;
+    return sync_if_host(h, flags);
+}

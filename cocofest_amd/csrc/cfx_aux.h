@@ -1,0 +1,133 @@
+// cfx_aux.h — small kernels around the shooting kernel: objective value/gradient, the Hmed
+// sliding-window rows, AoS <-> SoA transposes.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "cfx_kernels.h"
+
+namespace cfx {
+
+// One quadratic tracking term (fes_ocp.py:531-569): w_eff * (z_k - target_k)^2 for k in [k0, k1],
+// w_eff = weight * dt (Lagrange) or weight (Mayer).
+struct DevObjective {
+    int32_t var_kind;   // 0 state, 1 control
+    int32_t var_index;
+    int32_t node_first, node_last;
+    int32_t target_off; // offset into the targets array, -1: scalar target
+    int32_t pad_;
+    double w_eff;
+    double target_value;
+};
+
+// Objective value and gradient, one thread per instance.  GRAD must be zeroed beforehand.
+__global__ void __launch_bounds__(256) k_objective(const KParams P, int n_obj, const DevObjective* __restrict__ obj,
+                                                   const double* __restrict__ targets, const double* __restrict__ V,
+                                                   double* __restrict__ F, double* __restrict__ GRAD) {
+    const int64_t B = P.B;
+    const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= B) return;
+    double f = 0.0;
+    for (int t = 0; t < n_obj; ++t) {
+        const DevObjective o = obj[t];
+        for (int k = o.node_first; k <= o.node_last; ++k) {
+            const int64_t off = (int64_t)k * P.nz + (o.var_kind == 0 ? 0 : P.nx) + o.var_index;
+            const double z = V[off * B + b];
+            const double tgt = o.target_off >= 0 ? targets[o.target_off + k] : o.target_value;
+            const double d = z - tgt;
+            f += o.w_eff * d * d;
+            if (GRAD) GRAD[off * B + b] += 2.0 * o.w_eff * d;
+        }
+    }
+    if (F) F[b] = f;
+}
+
+// Objective Hessian diagonal contributions added into the Lagrangian Hessian values.
+__global__ void __launch_bounds__(256) k_objective_hess(const KParams P, int n_obj, const DevObjective* __restrict__ obj,
+                                                        const double* __restrict__ obj_factor,
+                                                        double* __restrict__ H) {
+    const int64_t B = P.B;
+    const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= B) return;
+    const double s = obj_factor[b];
+    for (int t = 0; t < n_obj; ++t) {
+        const DevObjective o = obj[t];
+        const int e = (o.var_kind == 0 ? 0 : P.nx) + o.var_index;  // position inside the node block
+        for (int k = o.node_first; k <= o.node_last; ++k) {
+            int64_t hoff;
+            if (k == P.N) {
+                hoff = (int64_t)P.N * P.nhk + e;  // x_N diagonal
+            } else {
+                hoff = (int64_t)k * P.nhk + e * (e + 1) / 2 + e;
+            }
+            H[hoff * B + b] += 2.0 * o.w_eff * s;
+        }
+    }
+}
+
+// Hmed sliding-window rows (custom_constraints.py:102-119): g = u_k[j] - window_k(p)[j], J = +1 / -1.
+// slot (k, j): param index or -1 for the intensity-floor padding; joff = J offset of its +1 entry.
+__global__ void __launch_bounds__(256) k_slide(const KParams P, const int32_t* __restrict__ sl_param,
+                                               const int32_t* __restrict__ sl_joff, double floor_value,
+                                               const double* __restrict__ V, double* __restrict__ G,
+                                               double* __restrict__ J) {
+    const int64_t B = P.B;
+    const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= B) return;
+    const int64_t p_off = (int64_t)P.N * P.nz + P.nx;
+    for (int k = 0; k < P.N; ++k) {
+        for (int j = 0; j < P.T; ++j) {
+            const int slot = k * P.T + j;
+            const int pi = sl_param[slot];
+            if (G) {
+                const double u = V[((int64_t)k * P.nz + P.nx + j) * B + b];
+                const double w = pi >= 0 ? V[(p_off + pi) * B + b] : floor_value;
+                G[((int64_t)k * P.ngk + P.nx + j) * B + b] = u - w;
+            }
+            if (J) {
+                const int64_t jo = sl_joff[slot];
+                J[jo * B + b] = 1.0;
+                if (pi >= 0) J[(jo + 1) * B + b] = -1.0;
+            }
+        }
+    }
+}
+
+// dst[e * B + b] = src[b * len + e]  (AoS -> SoA) through a 64x64 LDS tile; 256 threads.
+__global__ void __launch_bounds__(256) k_aos_to_soa(const double* __restrict__ src, double* __restrict__ dst,
+                                                    int64_t B, int64_t len) {
+    __shared__ double tile[64][65];
+    const int64_t b0 = (int64_t)blockIdx.x * 64;
+    const int64_t e0 = (int64_t)blockIdx.y * 64;
+    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+    for (int r = ty; r < 64; r += 4) {  // read rows b, columns e (coalesced in e)
+        const int64_t b = b0 + r, e = e0 + tx;
+        if (b < B && e < len) tile[r][tx] = src[b * len + e];
+    }
+    __syncthreads();
+    for (int r = ty; r < 64; r += 4) {  // write rows e, columns b (coalesced in b)
+        const int64_t e = e0 + r, b = b0 + tx;
+        if (b < B && e < len) dst[e * B + b] = tile[tx][r];
+    }
+}
+
+// dst[b * len + e] = src[e * B + b]  (SoA -> AoS)
+__global__ void __launch_bounds__(256) k_soa_to_aos(const double* __restrict__ src, double* __restrict__ dst,
+                                                    int64_t B, int64_t len) {
+    __shared__ double tile[64][65];
+    const int64_t b0 = (int64_t)blockIdx.x * 64;
+    const int64_t e0 = (int64_t)blockIdx.y * 64;
+    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+    for (int r = ty; r < 64; r += 4) {
+        const int64_t e = e0 + r, b = b0 + tx;
+        if (b < B && e < len) tile[r][tx] = src[e * B + b];
+    }
+    __syncthreads();
+    for (int r = ty; r < 64; r += 4) {
+        const int64_t b = b0 + r, e = e0 + tx;
+        if (b < B && e < len) dst[b * len + e] = tile[tx][r];
+    }
+}
+
+}  // namespace cfx

@@ -1,0 +1,47 @@
+// cfx_launch.h — host-side launchers of the templated kernels (instantiated per model family in
+// cfx_inst_ding.hip / cfx_inst_hmed.hip so the builds run in parallel).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "cfx_kernels.h"
+
+namespace cfx {
+
+// Jacobian directions carried per lane, per model (nz = nx + nu).  Hmed splits its nx + T directions
+// into chunks of 4 (nx = 2) or 5 (nx = 5); the others carry all directions in one lane.
+constexpr int dirs_of(int model) {
+    return model == M_D03 ? 2 : model == M_D03F ? 5 : model == M_D07 ? 3 : model == M_D07F ? 6 : model == M_H18 ? 4 : 5;
+}
+
+// Smallest supported register-resident truncation bucket >= T (Hmed only).
+inline int tmax_bucket(int T) { return T <= 4 ? 4 : T <= 8 ? 8 : T <= 16 ? 16 : 32; }
+
+hipError_t launch_shooting_ding(int model, int scheme, bool derivs, const KParams& P, const double* V, double* G,
+                                double* J, hipStream_t s);
+hipError_t launch_shooting_hmed(int model, int scheme, bool derivs, int tmax, const KParams& P, const double* V,
+                                double* G, double* J, hipStream_t s);
+hipError_t launch_ivp_ding(int model, int scheme, const KParams& P, const double* X0, const double* U, double* TR,
+                           hipStream_t s);
+hipError_t launch_ivp_hmed(int model, int scheme, int tmax, const KParams& P, const double* X0, const double* U,
+                           double* TR, hipStream_t s);
+
+constexpr int kBlock = 256;
+
+template <int MODEL, int SCHEME, int D, int TMAX>
+hipError_t launch_shooting_t(const KParams& P, const double* V, double* G, double* J, hipStream_t s) {
+    const int nz = P.nz;
+    const int nchunk = D > 0 ? (nz + D - 1) / D : 1;
+    dim3 grid((unsigned)((P.B + kBlock - 1) / kBlock), (unsigned)P.N, (unsigned)nchunk);
+    hipLaunchKernelGGL((k_shooting<MODEL, SCHEME, D, TMAX>), grid, dim3(kBlock), 0, s, P, V, G, J);
+    return hipGetLastError();
+}
+
+template <int MODEL, int SCHEME, int TMAX>
+hipError_t launch_ivp_t(const KParams& P, const double* X0, const double* U, double* TR, hipStream_t s) {
+    dim3 grid((unsigned)((P.B + kBlock - 1) / kBlock));
+    hipLaunchKernelGGL((k_ivp<MODEL, SCHEME, TMAX>), grid, dim3(kBlock), 0, s, P, X0, U, TR);
+    return hipGetLastError();
+}
+
+}  // namespace cfx

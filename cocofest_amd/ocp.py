@@ -1,0 +1,362 @@
+"""OcpFes: build the transcribed FES optimal-control problem (reference: cocofest/optimization/fes_ocp.py).
+
+``OcpFes.prepare_ocp`` keeps the reference's signature and validation messages.  Instead of a bioptim
+``OptimalControlProgram`` it returns a :class:`FesOcp`, which owns the NLP layout, bounds, initial
+guess and objective, and opens libcfx handles that evaluate g, J_g, f, grad f and the Lagrangian
+Hessian for batches of instances on the GPU (``FesOcp.nlp``), plus a host interior-point driver
+(``FesOcp.solve``).
+
+Transcription: bioptim multiple shooting with explicit RK sub-steps (``OdeSolver.RK1/RK2/RK4``);
+decision vector per instance [x_0, u_0, ..., x_{N-1}, u_{N-1}, x_N, p]; constraints per interval:
+Phi(x_k, u_k) - x_{k+1}, then (Hmed with intensity parameters) u_k - window_k(p).
+"""
+
+from __future__ import annotations
+
+from enum import Enum
+from fractions import Fraction
+from math import gcd
+
+import numpy as np
+
+from . import _cfx
+from .fes_models import (
+    DingModelPulseIntensityFrequency,
+    DingModelPulseWidthFrequency,
+    FesModel,
+)
+from .fourier import FourierSeries
+from .ode_solver import ControlType, OdeSolver
+
+
+class Node(Enum):
+    START = "start"
+    END = "end"
+    ALL = "all"
+    ALL_SHOOTING = "all_shooting"
+
+
+class ObjectiveFcn:
+    class Lagrange(Enum):
+        MINIMIZE_STATE = "minimize_state"
+        TRACK_STATE = "track_state"
+        MINIMIZE_CONTROL = "minimize_control"
+        TRACK_CONTROL = "track_control"
+
+    class Mayer(Enum):
+        MINIMIZE_STATE = "minimize_state"
+        TRACK_STATE = "track_state"
+
+
+class Objective:
+    """One quadratic objective term (the subset of bioptim ObjectiveFcn the reference's FES OCPs use)."""
+
+    def __init__(self, objective, key: str, weight: float = 1, target=None, node: Node = None, quadratic: bool = True):
+        if not quadratic:
+            raise NotImplementedError("only quadratic objective terms are supported")
+        self.objective = objective
+        self.key = key
+        self.weight = float(weight)
+        self.target = target
+        lagrange = isinstance(objective, ObjectiveFcn.Lagrange)
+        self.node = node if node is not None else (Node.ALL_SHOOTING if lagrange else Node.END)
+        self.lagrange = lagrange
+
+
+class ObjectiveList:
+    def __init__(self):
+        self._items = []
+
+    def add(self, objective, **kwargs):
+        self._items.append(objective if isinstance(objective, Objective) else Objective(objective, **kwargs))
+
+    def __getitem__(self, i):
+        # the reference indexes ObjectiveList as objective["custom"][0][i] (fes_ocp.py:331,537)
+        return self._items if i == 0 else self._items[i]
+
+    def __len__(self):
+        return len(self._items)
+
+    def __iter__(self):
+        return iter(self._items)
+
+
+class FesOcp:
+    """The transcribed OCP: layout, bounds, initial guess, objective and GPU callbacks."""
+
+    def __init__(self, model, n_shooting, final_time, ode_solver, rows, stim_idx_at_node_list, objectives,
+                 x_bounds, x_init, u_bounds, u_init, p_bounds, p_init, n_params, last_stim_idx, intensity_floor,
+                 n_threads=1, use_sx=True):
+        self.model = model
+        self.n_shooting = n_shooting
+        self.final_time = final_time
+        self.ode_solver = ode_solver
+        self.stim_rows = rows
+        self.stim_idx_at_node_list = stim_idx_at_node_list
+        self.objectives = objectives
+        self.x_bounds, self.x_init = x_bounds, x_init
+        self.u_bounds, self.u_init = u_bounds, u_init
+        self.p_bounds, self.p_init = p_bounds, p_init
+        self.n_params = n_params
+        self.last_stim_idx = last_stim_idx
+        self.intensity_floor = intensity_floor
+        self.n_threads, self.use_sx = n_threads, use_sx
+        self.nx = model.nb_state
+        self.nu = u_init.shape[0]
+        self.truncation = model._sum_stim_truncation
+
+    # ---- layout -------------------------------------------------------------------------------------
+    @property
+    def nv(self):
+        return self.n_shooting * (self.nx + self.nu) + self.nx + self.n_params
+
+    def pack(self, x, u=None, p=None):
+        """(nx, N+1) states, (nu, N) controls, (n_params,) parameters -> decision vector (nv,)."""
+        N, nx, nu = self.n_shooting, self.nx, self.nu
+        v = np.empty(self.nv)
+        body = v[: N * (nx + nu)].reshape(N, nx + nu)
+        body[:, :nx] = np.asarray(x)[:, :N].T
+        if nu:
+            body[:, nx:] = np.asarray(u).T
+        v[N * (nx + nu): N * (nx + nu) + nx] = np.asarray(x)[:, N]
+        if self.n_params:
+            v[N * (nx + nu) + nx:] = p
+        return v
+
+    def unpack(self, v):
+        N, nx, nu = self.n_shooting, self.nx, self.nu
+        v = np.asarray(v)
+        body = v[: N * (nx + nu)].reshape(N, nx + nu)
+        x = np.concatenate([body[:, :nx].T, v[N * (nx + nu): N * (nx + nu) + nx, None]], axis=1)
+        states = {name: x[i][np.newaxis, :] for i, name in enumerate(self.model.name_dof)}
+        controls = {}
+        if nu:
+            key = "last_pulse_width" if isinstance(self.model, DingModelPulseWidthFrequency) else "pulse_intensity"
+            controls[key] = body[:, nx:].T
+        params = {"pulse_intensity": v[N * (nx + nu) + nx:]} if self.n_params else {}
+        return states, controls, params
+
+    def bounds_vector(self):
+        lo = self.pack(self.x_bounds[0], self.u_bounds[0] if self.nu else None, self.p_bounds[0])
+        hi = self.pack(self.x_bounds[1], self.u_bounds[1] if self.nu else None, self.p_bounds[1])
+        return lo, hi
+
+    def initial_guess_vector(self):
+        return self.pack(self.x_init, self.u_init if self.nu else None, self.p_init)
+
+    # ---- GPU callbacks ------------------------------------------------------------------------------
+    def nlp(self, batch: int = 1, layout: str = "aos", device: int = 0) -> _cfx.Handle:
+        """Open a libcfx handle evaluating ``batch`` instances of this problem on GPU ``device``."""
+        if isinstance(self.ode_solver, OdeSolver.COLLOCATION):
+            raise NotImplementedError("COLLOCATION transcription is not available in libcfx yet")
+        return _cfx.Handle(
+            model_id=self.model.cfx_model_id, constants=self.model.cfx_constants(), scheme=self.ode_solver.scheme,
+            n_steps=self.ode_solver.n_integration_steps, n_shooting=self.n_shooting,
+            truncation=self.truncation, final_time=float(self.final_time), stim_rows=self.stim_rows, batch=batch,
+            layout=_cfx.LAYOUT_AOS if layout == "aos" else _cfx.LAYOUT_SOA, n_params=self.n_params,
+            last_stim_idx=self.last_stim_idx, intensity_floor=self.intensity_floor,
+            objectives=self.objectives, device=device)
+
+    def solve(self, solver=None, **kwargs):
+        from .solver import solve_ocp
+
+        return solve_ocp(self, solver=solver, **kwargs)
+
+
+class OcpFes:
+    """Prepares the FES OCP (reference: cocofest/optimization/fes_ocp.py:32-577)."""
+
+    @staticmethod
+    def prepare_ocp(model: FesModel = None, final_time: int | float = None, pulse_width: dict = None,
+                    pulse_intensity: dict = None, objective: dict = None, use_sx: bool = True,
+                    ode_solver=OdeSolver.RK1(n_integration_steps=10), control_type: ControlType = ControlType.CONSTANT,
+                    n_threads: int = 1, n_shooting: int | None = None) -> FesOcp:
+        """Same arguments as the reference (fes_ocp.py:112-190).  ``n_shooting`` (extension) overrides the
+        LCM node count of ``prepare_n_shooting``; the default keeps the reference's rule."""
+        n = OcpFes.prepare_n_shooting(model.stim_time, final_time) if n_shooting is None else n_shooting
+        pulse_width, pulse_intensity, objective = OcpFes._fill_dict(pulse_width, pulse_intensity, objective)
+        OcpFes._sanity_check(model=model, n_shooting=n, final_time=final_time, objective=objective, use_sx=use_sx,
+                             ode_solver=ode_solver, n_threads=n_threads)
+        n_params, p_bounds, p_init = OcpFes._build_parameters(model, pulse_intensity)
+        table, stim_idx_at_node_list = model.get_numerical_data_time_series(n, final_time)
+        rows = table["stim_time"][:, 0, :].T.copy()
+        x_bounds, x_init = OcpFes._set_bounds(model, n)
+        max_bound = (pulse_width["max"] if isinstance(model, DingModelPulseWidthFrequency)
+                     else pulse_intensity["max"] if isinstance(model, DingModelPulseIntensityFrequency) else None)
+        u_bounds, u_init = OcpFes._set_u_bounds(model, n, max_bound=max_bound)
+        objectives = OcpFes._set_objective(model, n, objective)
+        last_stim_idx, floor = None, 0.0
+        if isinstance(model, DingModelPulseIntensityFrequency):
+            floor = float(model.min_pulse_intensity())
+            if n_params:
+                last_stim_idx = OcpFes._build_constraints(model, n, stim_idx_at_node_list)
+        return FesOcp(model, n, final_time, ode_solver, rows, stim_idx_at_node_list, objectives, x_bounds, x_init,
+                      u_bounds, u_init, p_bounds, p_init, n_params, last_stim_idx, floor, n_threads, use_sx)
+
+    @staticmethod
+    def prepare_n_shooting(stim_time, final_time):
+        """Number of shooting nodes so that every stimulation falls on a node: the LCM of the reduced
+        denominators of t_i / final_time (fes_ocp.py:192-222)."""
+        t_final = Fraction(final_time).limit_denominator()
+        n_shooting = 1
+        for t in stim_time:
+            d = (Fraction(t).limit_denominator() / t_final).denominator
+            n_shooting = n_shooting * d // gcd(n_shooting, d)
+        if n_shooting >= 1000:
+            print(f"Warning: The number of shooting nodes is very high n = {n_shooting}.\n"
+                  "The optimization might be long, consider using stimulation time with even spacing (common frequency).")
+        return n_shooting
+
+    @staticmethod
+    def _fill_dict(pulse_width, pulse_intensity, objective):
+        default_pulse = {"fixed": None, "min": None, "max": None, "bimapping": False}
+        default_objective = {"force_tracking": None, "end_node_tracking": None, "cycling": None, "custom": None}
+        return ({**default_pulse, **(pulse_width or {})}, {**default_pulse, **(pulse_intensity or {})},
+                {**default_objective, **(objective or {})})
+
+    @staticmethod
+    def _sanity_check(model=None, n_shooting=None, final_time=None, objective=None, use_sx=None, ode_solver=None,
+                      n_threads=None):
+        """Input validation with the reference's messages (fes_ocp.py:279-344)."""
+        if not isinstance(model, FesModel):
+            raise TypeError(
+                f"The current model type used is {type(model)}, it must be a FesModel type."
+                f"Current available models are: DingModelFrequency, DingModelFrequencyWithFatigue,"
+                f"DingModelPulseWidthFrequency, DingModelPulseWidthFrequencyWithFatigue,"
+                f"DingModelPulseIntensityFrequency, DingModelPulseIntensityFrequencyWithFatigue")
+        if not isinstance(n_shooting, int) or n_shooting < 0:
+            raise TypeError("n_shooting must be a positive int type")
+        if not isinstance(final_time, int | float) or final_time < 0:
+            raise TypeError("final_time must be a positive int or float type")
+        ft = objective["force_tracking"]
+        if ft is not None:
+            if isinstance(ft, list):
+                if isinstance(ft[0], np.ndarray) and isinstance(ft[1], np.ndarray):
+                    if len(ft[0]) != len(ft[1]) or len(ft) != 2:
+                        raise ValueError("force_tracking time and force argument must be same length and force_tracking "
+                                         "list size 2")
+                else:
+                    raise TypeError("force_tracking argument must be np.ndarray type")
+            else:
+                raise TypeError("force_tracking must be list type")
+        if objective["end_node_tracking"] is not None:
+            if not isinstance(objective["end_node_tracking"], int | float):
+                raise TypeError("end_node_tracking must be int or float type")
+        if objective["custom"] is not None:
+            if not isinstance(objective["custom"], ObjectiveList):
+                raise TypeError("custom_objective must be a ObjectiveList type")
+            if not all(isinstance(x, Objective) for x in objective["custom"][0]):
+                raise TypeError("All elements in ObjectiveList must be an Objective type")
+        if not isinstance(ode_solver, (OdeSolver.RK1, OdeSolver.RK2, OdeSolver.RK4, OdeSolver.COLLOCATION)):
+            raise TypeError("ode_solver must be a OdeSolver type")
+        if not isinstance(use_sx, bool):
+            raise TypeError("use_sx must be a bool type")
+        if not isinstance(n_threads, int):
+            raise TypeError("n_thread must be a int type")
+
+    @staticmethod
+    def _build_parameters(model, pulse_intensity):
+        """Hmed pulse-intensity parameters (fes_ocp.py:350-411) -> (n_params, (lb, ub), init)."""
+        empty = (0, (np.zeros(0), np.zeros(0)), np.zeros(0))
+        if not isinstance(model, DingModelPulseIntensityFrequency):
+            return empty
+        n_stim = len(model.stim_time)
+        if pulse_intensity["bimapping"]:
+            raise NotImplementedError("bimapped pulse intensities are not supported (the reference's sliding-window "
+                                      "constraint indexes past a size-1 parameter)")
+        fixed = pulse_intensity["fixed"]
+        if fixed:
+            vals = np.array(fixed if isinstance(fixed, list) else [fixed] * n_stim, dtype=float)
+            return n_stim, (vals.copy(), vals.copy()), vals.copy()
+        if pulse_intensity["max"]:
+            lo = float(model.min_pulse_intensity())
+            hi = float(pulse_intensity["max"])
+            return n_stim, (np.full(n_stim, lo), np.full(n_stim, hi)), np.full(n_stim, (lo + hi) / 2)
+        return empty
+
+    @staticmethod
+    def _build_constraints(model, n_shooting, stim_idx_at_node_list):
+        """Sliding-window rows, one per node (fes_ocp.py:413-438): index of the last parameter of node k."""
+        return np.array([stim_idx_at_node_list[i][-1] for i in range(n_shooting)], dtype=np.int32)
+
+    @staticmethod
+    def _set_bounds(model, n_shooting):
+        """State bounds (fes_ocp.py:452-499): node 0 fixed at rest; after it Cn in [0, 2], F in [0, 1000],
+        A in [0, A_rest], Tau1 / Km in [rest, 1].  Returns ((lb, ub) each (nx, N+1), x_init (nx, N+1))."""
+        rest = model.standard_rest_values().astype(float)[:, 0]
+        lo, hi = rest.copy(), rest.copy()
+        for i, name in enumerate(model.name_dof):
+            if name == "Cn":
+                hi[i] = 2
+            if name == "F":
+                hi[i] = 1000
+            elif name in ("Tau1", "Km"):
+                hi[i] = 1
+            elif name == "A":
+                lo[i] = 0
+        lb = np.repeat(lo[:, None], n_shooting + 1, axis=1)
+        ub = np.repeat(hi[:, None], n_shooting + 1, axis=1)
+        lb[:, 0] = rest
+        ub[:, 0] = rest
+        x_init = np.repeat(rest[:, None], n_shooting + 1, axis=1)
+        return (lb, ub), x_init
+
+    @staticmethod
+    def _set_u_bounds(model, n_shooting, max_bound):
+        """Control bounds and initial guess (fes_ocp.py:501-529) -> ((lb, ub) each (nu, N), u_init (nu, N))."""
+        hi = np.inf if max_bound is None else float(max_bound)
+        if isinstance(model, DingModelPulseWidthFrequency):
+            lo = float(model.pd0)
+            return (np.full((1, n_shooting), lo), np.full((1, n_shooting), hi)), np.zeros((1, n_shooting))
+        if isinstance(model, DingModelPulseIntensityFrequency):
+            T = model._sum_stim_truncation
+            lo = float(model.min_pulse_intensity())
+            return (np.full((T, n_shooting), lo), np.full((T, n_shooting), hi)), np.zeros((T, n_shooting))
+        return (np.zeros((0, n_shooting)), np.zeros((0, n_shooting))), np.zeros((0, n_shooting))
+
+    @staticmethod
+    def _set_objective(model, n_shooting, objective):
+        """Objective terms (fes_ocp.py:531-569) as libcfx term descriptors."""
+        terms = []
+        if objective["custom"]:
+            for ob in objective["custom"][0]:
+                terms.append(OcpFes._term_from_objective(model, n_shooting, ob))
+        if objective["force_tracking"]:
+            coeffs = FourierSeries().compute_real_fourier_coeffs(objective["force_tracking"][0],
+                                                                 objective["force_tracking"][1], 50)
+            target = FourierSeries().fit_func_by_fourier_series_with_real_coeffs(np.linspace(0, 1, n_shooting + 1),
+                                                                                 coeffs)
+            terms.append(dict(kind=_cfx.OBJ_LAGRANGE, var_kind=_cfx.VAR_STATE, var_index=model.name_dof.index("F"),
+                              node_first=0, node_last=n_shooting, weight=100.0, target=np.asarray(target, float)))
+        if objective["end_node_tracking"]:
+            terms.append(dict(kind=_cfx.OBJ_MAYER, var_kind=_cfx.VAR_STATE, var_index=model.name_dof.index("F"),
+                              node_first=n_shooting, node_last=n_shooting, weight=1.0,
+                              target_value=float(objective["end_node_tracking"])))
+        return terms
+
+    @staticmethod
+    def _term_from_objective(model, n_shooting, ob: Objective):
+        state = ob.objective in (ObjectiveFcn.Lagrange.MINIMIZE_STATE, ObjectiveFcn.Lagrange.TRACK_STATE,
+                                 ObjectiveFcn.Mayer.MINIMIZE_STATE, ObjectiveFcn.Mayer.TRACK_STATE)
+        if state:
+            idx = model.name_dof.index(ob.key)
+        else:
+            if ob.key not in ("last_pulse_width", "pulse_intensity"):
+                raise ValueError(f"unknown control key {ob.key}")
+            idx = 0
+        last = n_shooting if state else n_shooting - 1
+        first, end = {Node.START: (0, 0), Node.END: (last, last), Node.ALL: (0, last),
+                      Node.ALL_SHOOTING: (0, n_shooting - 1)}[ob.node]
+        term = dict(kind=_cfx.OBJ_LAGRANGE if ob.lagrange else _cfx.OBJ_MAYER,
+                    var_kind=_cfx.VAR_STATE if state else _cfx.VAR_CONTROL, var_index=idx, node_first=first,
+                    node_last=end, weight=ob.weight)
+        if ob.target is None:
+            term["target_value"] = 0.0
+        elif np.ndim(ob.target) == 0:
+            term["target_value"] = float(ob.target)
+        else:
+            tgt = np.zeros(n_shooting + 1)
+            arr = np.asarray(ob.target, dtype=float).ravel()
+            tgt[first: first + arr.size] = arr
+            term["target"] = tgt
+        return term

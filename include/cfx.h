@@ -1,0 +1,168 @@
+/*
+ * cfx.h — C ABI of libcfx, the MI355X (gfx950) NLP-callback engine for cocofest's FES optimal-control
+ * problems (Ding2003 / Ding2007 / Hmed2018 calcium-force models, with or without fatigue).
+ *
+ * What it replaces (reference: Ipuch/cocofest @ 2025-02-24; transcription/evaluation live in the
+ * unvendored bioptim + CasADi + Ipopt stack):
+ *   - the bioptim dynamics plugin registered by every model's declare_ding_variables
+ *     (cocofest/models/ding2003.py:373-392, ding2007.py:288-308, hmed2018.py:281-301) and called
+ *     symbolically through `dynamics(time, states, controls, parameters, algebraic_states,
+ *     numerical_timeseries, nlp, ...)` (cocofest/models/fes_model.py:182-202);
+ *   - the CasADi-generated NLP callbacks that Ipopt invokes on the OptimalControlProgram built at
+ *     cocofest/optimization/fes_ocp.py:171-190 (Ipopt TNLP eval_f / eval_grad_f / eval_g /
+ *     eval_jac_g / eval_h: solver-owned contiguous double arrays, COO sparsity fixed up front);
+ *   - the single-shooting integration behind IvpFes.integrate (cocofest/integration/ivp_fes.py:282-297).
+ *
+ * Conventions
+ *   - Plain C types only.  Every buffer is caller-owned.  With CFX_DEVICE the pointers are HIP device
+ *     pointers and the call is asynchronous on the handle's stream; otherwise they are host pointers
+ *     and the call copies in, computes on the GPU and copies out before returning.
+ *   - All arithmetic is FP64.  Every evaluation runs on the GPU; there is no CPU fallback: creating a
+ *     handle without a usable HIP device fails with CFX_ENODEV.
+ *   - Batches: B independent instances of one problem (multi-start, parameter sweeps, NMPC scenarios).
+ *     CFX_LAYOUT_AOS: instance-major, element e of instance b at buf[b*len + e] (Ipopt's per-instance
+ *     contiguous arrays).  CFX_LAYOUT_SOA: element-major, buf[e*B + b] (coalesced; the native layout).
+ *   - Decision vector of one instance (node-major): [x_0, u_0, x_1, u_1, ..., x_{N-1}, u_{N-1}, x_N, p]
+ *     with x_k the nx states (Cn, F[, A, Tau1, Km]; state_configure.py:8-319), u_k the nu controls
+ *     (Ding2007: last_pulse_width; Hmed2018: the T pulse intensities aligned with the node's stim row),
+ *     p the Hmed intensity parameters (fes_ocp.py:350-411).
+ *   - Constraints of one instance: per interval k, the nx continuity rows Phi(x_k,u_k) - x_{k+1}
+ *     followed (Hmed with parameters) by the T sliding-window rows u_k - window_k(p)
+ *     (custom_constraints.py:102-119, fes_ocp.py:413-438).
+ *   - Integer error codes; cfx_last_error() gives the message.  A handle is bound to one device and one
+ *     stream and is not thread-safe; use one handle per GPU / per thread.
+ */
+#ifndef CFX_H
+#define CFX_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CFX_ABI_VERSION 1
+
+/* return codes */
+#define CFX_OK 0
+#define CFX_EINVAL (-1)
+#define CFX_EHIP (-2)
+#define CFX_ENOMEM (-3)
+#define CFX_EUNSUPPORTED (-4)
+#define CFX_ENODEV (-5)
+
+/* models (cocofest/models/model_maker.py:9-22) */
+#define CFX_DING2003 0
+#define CFX_DING2003_FATIGUE 1
+#define CFX_DING2007 2
+#define CFX_DING2007_FATIGUE 3
+#define CFX_HMED2018 4
+#define CFX_HMED2018_FATIGUE 5
+
+/* transcription (OdeSolver.RK1/RK2/RK4 with n_integration_steps; fes_ocp.py:120,334-338) */
+#define CFX_RK1 1
+#define CFX_RK2 2
+#define CFX_RK4 4
+
+/* layouts and call flags */
+#define CFX_LAYOUT_AOS 0
+#define CFX_LAYOUT_SOA 1
+#define CFX_DEVICE 1u /* pointers are device pointers; call is asynchronous on the handle stream */
+
+/* objective terms (fes_ocp.py:531-569) */
+#define CFX_OBJ_LAGRANGE 0 /* weight * dt * (z_k - target_k)^2 summed over the node range */
+#define CFX_OBJ_MAYER 1    /* weight * (z_k - target_k)^2 summed over the node range */
+#define CFX_VAR_STATE 0
+#define CFX_VAR_CONTROL 1
+
+typedef struct cfx_constants {
+    /* ding2003.py:51-66 */
+    double tauc, r0_km_relationship, a_rest, tau1_rest, tau2, km_rest;
+    /* ding2007.py:63-79 */
+    double a_scale, pd0, pdt;
+    /* hmed2018.py:53-63 */
+    double ar, bs, Is, cr;
+    /* ding2003_with_fatigue.py:50-59 */
+    double alpha_a, alpha_tau1, alpha_km, tau_fat;
+    /* force-length / force-velocity multipliers and passive force (ding2003.py:274-311) */
+    double fl, fv, fp;
+} cfx_constants;
+
+typedef struct cfx_objective {
+    int32_t kind;       /* CFX_OBJ_LAGRANGE | CFX_OBJ_MAYER */
+    int32_t var_kind;   /* CFX_VAR_STATE | CFX_VAR_CONTROL */
+    int32_t var_index;  /* state or control component */
+    int32_t node_first; /* inclusive node range; controls: 0..N-1, states: 0..N */
+    int32_t node_last;
+    double weight;
+    const double *target; /* per node (indexed by node, length N+1) or NULL -> target_value */
+    double target_value;
+} cfx_objective;
+
+typedef struct cfx_problem {
+    int32_t abi_version; /* CFX_ABI_VERSION */
+    int32_t model;       /* CFX_DING2003 ... CFX_HMED2018_FATIGUE */
+    int32_t scheme;      /* CFX_RK1 | CFX_RK2 | CFX_RK4 */
+    int32_t n_steps;     /* RK sub-steps per shooting interval (n_integration_steps) */
+    int32_t n_shooting;  /* N */
+    int32_t truncation;  /* sum_stim_truncation T (<= 32) */
+    int32_t n_params;    /* Hmed pulse-intensity parameters (0: no sliding-window constraints) */
+    int32_t layout;      /* CFX_LAYOUT_AOS | CFX_LAYOUT_SOA */
+    int64_t batch;       /* B >= 1 */
+    double final_time;
+    /* stim table, row k = the last T stim times <= k*final_time/N (history placeholders -1e7):
+       numerical_data_timeseries of ding2003.py:399-429, row-major [(N+1) * T] */
+    const double *stim_rows;
+    const int32_t *last_stim_idx; /* [N] index of the last parameter in node k's window (Hmed) */
+    double intensity_floor;       /* sliding-window left padding (min_pulse_intensity) */
+    cfx_constants constants;
+    int32_t n_objectives;
+    const cfx_objective *objectives;
+    int32_t device; /* HIP device ordinal */
+} cfx_problem;
+
+typedef struct cfx_handle cfx_handle;
+
+/* Problem sizes: decision variables, constraints, J_g non-zeros, Hessian (lower triangle) non-zeros,
+   per instance. */
+typedef struct cfx_sizes {
+    int64_t nv, ng, nnz_jac, nnz_hess;
+    int32_t nx, nu;
+} cfx_sizes;
+
+/* ---- lifetime ------------------------------------------------------------------------------------ */
+/* Ipopt: get_nlp_info (sizes fixed at creation) */
+int cfx_create(const cfx_problem *problem, cfx_handle **out);
+void cfx_destroy(cfx_handle *h);
+int cfx_get_sizes(const cfx_handle *h, cfx_sizes *out);
+int cfx_set_stream(cfx_handle *h, void *hip_stream); /* NULL: the handle's own stream */
+int cfx_synchronize(cfx_handle *h);
+const char *cfx_last_error(const cfx_handle *h); /* h == NULL: last cfx_create failure of this thread */
+int cfx_abi_version(void);
+int cfx_device_count(void);
+
+/* ---- sparsity (Ipopt eval_jac_g / eval_h with values == NULL) ---------------------------------- */
+int cfx_jac_structure(const cfx_handle *h, int32_t *row, int32_t *col);  /* nnz_jac entries */
+int cfx_hess_structure(const cfx_handle *h, int32_t *row, int32_t *col); /* nnz_hess, row >= col */
+
+/* ---- NLP callbacks over the whole batch -------------------------------------------------------- */
+int cfx_eval_g(cfx_handle *h, const double *v, double *g, uint32_t flags);         /* eval_g */
+int cfx_eval_jac_g(cfx_handle *h, const double *v, double *jac, uint32_t flags);   /* eval_jac_g values */
+int cfx_eval_f(cfx_handle *h, const double *v, double *f, uint32_t flags);         /* eval_f, f[B] */
+int cfx_eval_grad_f(cfx_handle *h, const double *v, double *grad, uint32_t flags); /* eval_grad_f */
+/* eval_h: values of obj_factor[b]*Hess(f) + sum_i lambda[b,i]*Hess(g_i), lower triangle */
+int cfx_eval_h(cfx_handle *h, const double *v, const double *obj_factor, const double *lambda, double *hess,
+               uint32_t flags);
+/* fused g + J_g (+ f, grad f when non-NULL) in one pass over the decision vectors */
+int cfx_eval_all(cfx_handle *h, const double *v, double *g, double *jac, double *f, double *grad,
+                 uint32_t flags);
+
+/* ---- IvpFes.integrate: single shooting from x0 (NULL: rest state) with per-interval controls
+   u [N*nu per instance], writing every sub-step state: traj [(N*n_steps+1)*nx per instance]. ---- */
+int cfx_integrate(cfx_handle *h, const double *x0, const double *u, double *traj, uint32_t flags);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* CFX_H */

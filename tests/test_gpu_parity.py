@@ -1,0 +1,213 @@
+"""Parity of the gfx950 kernels (through the libcfx C ABI) with the oracle and the reference goldens.
+
+Tolerances: FP64 everywhere.  IVP trajectories vs the reference's 8-decimal golden literals: 6e-9
+absolute.  Callback values vs the oracle (same inputs, complex-step derivatives): relative 1e-11 on
+g / J / f / grad (RK recursions of <= 40 stages; the kernels use reciprocal-multiply where the oracle
+divides, a few ulp per stage).
+"""
+
+import numpy as np
+import pytest
+
+from oracle import fes_oracle as O
+from tests import cases
+from tests.conftest import golden_stims
+
+pytestmark = pytest.mark.gpu
+
+RTOL = 1e-11
+
+
+def _close(actual, desired, rtol=RTOL, what=""):
+    desired = np.asarray(desired)
+    scale = np.maximum(np.abs(desired), np.max(np.abs(desired), axis=-1, keepdims=True) * 1e-6 + 1e-300)
+    err = np.max(np.abs(actual - desired) / scale) if desired.size else 0.0
+    assert err <= rtol, f"{what}: max scaled error {err:.3e} > {rtol:.1e}"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _require_gpu():
+    from cocofest_amd import _cfx
+
+    lib = _cfx.load_library()  # raises if libcfx.so is missing: no silent fallback
+    if lib.cfx_device_count() < 1:
+        pytest.fail("no HIP device visible to libcfx")
+
+
+def test_ivp_goldens_on_gpu(ivp_goldens):
+    """The 9 reference golden trajectories (tests/shard1/test_ivp.py) through IvpFes -> cfx_integrate."""
+    from cocofest_amd import IvpFes, ModelMaker, OdeSolver
+
+    shared = {}
+    for case in ivp_goldens:
+        name = case["model"]
+        if case["pulse_mode"] == "single" or name not in shared:
+            shared[name] = ModelMaker.create_model(name, stim_time=[0, 0.1, 0.2], sum_stim_truncation=3)
+        model = shared[name]  # the pulse-mode cases reuse (and mutate) one model, as the reference's test does
+        fes = {"model": model, "pulse_mode": case["pulse_mode"]}
+        if case["pulse_width"]:
+            fes["pulse_width"] = case["pulse_width"]
+        if case["pulse_intensity"]:
+            fes["pulse_intensity"] = case["pulse_intensity"]
+        ivp = IvpFes(fes, {"final_time": 0.3, "ode_solver": OdeSolver.RK4(n_integration_steps=10)})
+        result = ivp.integrate(return_time=False)
+        f = result["F"][0]
+        if case["slice"]:
+            f = f[case["slice"][0]: case["slice"][1]]
+        np.testing.assert_allclose(f, case["F"], rtol=0, atol=6e-9, err_msg=case["source"])
+        # and against the oracle on every state and sample
+        c = O.model_constants(name)
+        stims = golden_stims(case["pulse_mode"], case["stim_time"])
+        n = O.prepare_n_shooting(stims, 0.3)
+        tab = O.stim_table(stims, n, 0.3, 3)
+        u = O.ivp_controls(name, tab, n, 3, case["pulse_width"], case["pulse_intensity"])
+        ref = O.ivp_integrate(name, c, tab.rows, u, 0.3, "RK4", 10)
+        got = np.stack([result[k][0] for k in model.name_dof])
+        _close(got, ref, what=f"ivp {name} {case['pulse_mode']}")
+
+
+STIMS = [0.0, 0.05, 0.1, 0.15]
+
+
+@pytest.mark.parametrize("scheme", ["RK1", "RK2", "RK4"])
+@pytest.mark.parametrize("name", O.MODEL_NAMES)
+def test_shooting_g_and_jacobian_vs_oracle(name, scheme):
+    T = 3
+    ocp = cases.product_ocp(name, STIMS, 0.2, T, scheme=scheme, m=3)
+    pb = cases.oracle_problem(name, STIMS, 0.2, T, scheme=scheme, m=3)
+    assert ocp.nv == pb.nv and ocp.n_shooting == pb.n_shooting
+    B = 7
+    v = cases.random_decision(pb, B, seed=11)
+    h = ocp.nlp(batch=B, layout="aos")
+    assert (h.nv, h.ng) == (pb.nv, pb.ng)
+    rows, cols = h.jac_structure()
+    orows, ocols = O.jac_structure(pb)
+    np.testing.assert_array_equal(rows, orows)
+    np.testing.assert_array_equal(cols, ocols)
+    g = h.eval_g(v)
+    jac = h.eval_jac_g(v)
+    _close(g, O.eval_g(pb, v), what=f"g {name} {scheme}")
+    _close(jac, O.eval_jac_g(pb, v), what=f"J {name} {scheme}")
+    # fused call gives identical values
+    g2, j2 = np.empty_like(g), np.empty_like(jac)
+    h.eval_all(v, g=g2, jac=j2)
+    np.testing.assert_array_equal(g2, g)
+    np.testing.assert_array_equal(j2, jac)
+
+
+@pytest.mark.parametrize("T", [1, 5, 10, 17, 32])
+def test_hmed_truncation_buckets(T):
+    stims = [round(0.02 * i, 2) for i in range(12)]
+    for name in ("hmed2018", "hmed2018_with_fatigue"):
+        ocp = cases.product_ocp(name, stims, 0.24, T, scheme="RK2", m=2)
+        pb = cases.oracle_problem(name, stims, 0.24, T, scheme="RK2", m=2)
+        v = cases.random_decision(pb, 3, seed=T)
+        h = ocp.nlp(batch=3)
+        _close(h.eval_g(v), O.eval_g(pb, v), what=f"g {name} T={T}")
+        _close(h.eval_jac_g(v), O.eval_jac_g(pb, v), what=f"J {name} T={T}")
+
+
+def test_objective_value_and_gradient():
+    t = np.linspace(0, 1, 40)
+    force = 80 * np.sin(np.pi * t) ** 2
+    obj = {"force_tracking": [t, force], "end_node_tracking": 40}
+    for name in ("ding2003", "ding2007_with_fatigue"):
+        ocp = cases.product_ocp(name, cases.TEN_PULSES, 1.0, 5, scheme="RK1", m=4, objective=obj)
+        pb = cases.oracle_problem(name, cases.TEN_PULSES, 1.0, 5, scheme="RK1", m=4, objective=obj)
+        v = cases.random_decision(pb, 4, seed=3)
+        h = ocp.nlp(batch=4)
+        _close(h.eval_f(v), O.eval_f(pb, v), what=f"f {name}")
+        _close(h.eval_grad_f(v), O.eval_grad_f(pb, v), what=f"grad {name}")
+
+
+def test_layouts_and_device_pointers_are_bitwise_identical():
+    import torch
+
+    cfg = cases.cfg2()
+    ocp = cases.product_ocp(**cfg)
+    pb = cases.oracle_problem(**cfg)
+    B = 300  # not a multiple of the 256-thread block
+    v = cases.random_decision(pb, B, seed=5)
+    ha = ocp.nlp(batch=B, layout="aos")
+    hs = ocp.nlp(batch=B, layout="soa")
+    ga, ja = ha.eval_g(v), ha.eval_jac_g(v)
+    vs = np.ascontiguousarray(v.T)
+    gs, js = hs.eval_g(vs), hs.eval_jac_g(vs)
+    np.testing.assert_array_equal(gs.T, ga)
+    np.testing.assert_array_equal(js.T, ja)
+    # torch device buffers, SoA, in place on the current stream
+    dv = torch.from_numpy(vs).cuda()
+    dg = torch.empty((hs.ng, B), dtype=torch.float64, device="cuda")
+    dj = torch.empty((hs.nnz_jac, B), dtype=torch.float64, device="cuda")
+    hs.eval_all(dv, g=dg, jac=dj)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(dg.cpu().numpy(), gs)
+    np.testing.assert_array_equal(dj.cpu().numpy(), js)
+    # device AoS
+    dva = torch.from_numpy(v).cuda()
+    dga = torch.empty((B, ha.ng), dtype=torch.float64, device="cuda")
+    ha.eval_all(dva, g=dga)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(dga.cpu().numpy(), ga)
+    _close(ga, O.eval_g(pb, v), what="cfg2 g")
+
+
+def test_full_size_properties_cfg2():
+    """BASELINE config 2 at bench size: batch invariance (instance b gives the same bits alone and inside a
+    2^17 batch) and feasibility of the forward RK1 x 10 integration (the 0-DOF optimum): g == 0."""
+    import torch
+
+    cfg = cases.cfg2()
+    ocp = cases.product_ocp(**cfg)
+    pb = cases.oracle_problem(**cfg)
+    B = 1 << 17
+    v = cases.random_decision(pb, B, seed=9)
+    hs = ocp.nlp(batch=B, layout="soa")
+    dv = torch.from_numpy(np.ascontiguousarray(v.T)).cuda()
+    dg = torch.empty((hs.ng, B), dtype=torch.float64, device="cuda")
+    dj = torch.empty((hs.nnz_jac, B), dtype=torch.float64, device="cuda")
+    hs.eval_all(dv, g=dg, jac=dj)
+    torch.cuda.synchronize()
+    pick = np.array([0, 1, 63, 64, 255, 256, 4097, B - 1])
+    h1 = ocp.nlp(batch=len(pick), layout="aos")
+    np.testing.assert_array_equal(h1.eval_g(v[pick]), dg[:, pick].cpu().numpy().T)
+    np.testing.assert_array_equal(h1.eval_jac_g(v[pick]), dj[:, pick].cpu().numpy().T)
+    _close(dg[:, pick].cpu().numpy().T, O.eval_g(pb, v[pick]), what="cfg2 big-batch g")
+    # forward-integrated trajectory is feasible
+    from cocofest_amd import IvpFes, ModelMaker, OdeSolver
+
+    model = ModelMaker.create_model("ding2003", stim_time=cases.TEN_PULSES, sum_stim_truncation=20)
+    ivp = IvpFes({"model": model}, {"final_time": 1.0, "ode_solver": OdeSolver.RK1(n_integration_steps=10)})
+    res = ivp.integrate(return_time=False)
+    nodes = np.stack([res["Cn"][0][::10], res["F"][0][::10]])  # N = 10 (the reference's LCM rule)
+    ocp10 = cases.product_ocp(**cases.cfg2(n_shooting=None))
+    g = ocp10.nlp(batch=1).eval_g(ocp10.pack(nodes)[None, :])
+    assert np.max(np.abs(g)) < 1e-9
+
+
+def test_edge_sizes():
+    # N = 1, batch 1, truncation 1
+    for name in ("ding2003_with_fatigue", "ding2007", "hmed2018"):
+        ocp = cases.product_ocp(name, [0.0], 0.1, 1, scheme="RK4", m=1)
+        pb = cases.oracle_problem(name, [0.0], 0.1, 1, scheme="RK4", m=1)
+        assert pb.n_shooting == 1
+        v = cases.random_decision(pb, 1, seed=2)
+        h = ocp.nlp(batch=1)
+        _close(h.eval_g(v), O.eval_g(pb, v), what=f"edge g {name}")
+        _close(h.eval_jac_g(v), O.eval_jac_g(pb, v), what=f"edge J {name}")
+
+
+def test_errors_are_loud():
+    from cocofest_amd import CfxError
+    from cocofest_amd import _cfx
+
+    ocp = cases.product_ocp(**cases.cfg2())
+    with pytest.raises(CfxError):
+        _cfx.Handle(model_id=9, constants={}, scheme=1, n_steps=1, n_shooting=2, truncation=1, final_time=1.0,
+                    stim_rows=np.zeros(3), batch=1)
+    with pytest.raises(CfxError):
+        _cfx.Handle(model_id=0, constants={}, scheme=3, n_steps=1, n_shooting=2, truncation=1, final_time=1.0,
+                    stim_rows=np.zeros(3), batch=1)
+    h = ocp.nlp(batch=2)
+    with pytest.raises(CfxError):
+        h.eval_h(np.zeros((2, h.nv)), np.ones(2), np.zeros((2, h.ng)))

@@ -1,0 +1,206 @@
+"""Host-side logic of the product (no GPU needed): library load + exported symbols, stimulation tables,
+problem layout, bounds, objectives, validation messages of the reference API."""
+
+import re
+
+import numpy as np
+import pytest
+
+from oracle import fes_oracle as O
+from tests import cases
+from tests.conftest import ROOT
+
+
+def _declared_symbols():
+    text = (ROOT / "include" / "cfx.h").read_text()
+    return sorted(set(re.findall(r"^\s*(?:int|void|const char \*)\s*\*?\s*(cfx_\w+)\s*\(", text, re.M)))
+
+
+def test_library_loads_and_exports_every_declared_symbol():
+    from cocofest_amd import _cfx
+
+    lib = _cfx.load_library()
+    declared = _declared_symbols()
+    assert len(declared) >= 17
+    for name in declared:
+        assert hasattr(lib, name), name
+    assert set(declared) == set(_cfx.SIGNATURES)
+    assert lib.cfx_abi_version() == _cfx.ABI_VERSION
+
+
+def test_create_without_device_fails_loudly():
+    from cocofest_amd import CfxError
+    from cocofest_amd import _cfx
+
+    lib = _cfx.load_library()
+    if lib.cfx_device_count() > 0:
+        pytest.skip("a HIP device is visible")
+    ocp = cases.product_ocp(**cases.cfg2())
+    with pytest.raises(CfxError) as exc:
+        ocp.nlp(batch=4)
+    assert exc.value.code == _cfx.ENODEV
+
+
+def test_missing_library_is_an_error(tmp_path):
+    from cocofest_amd import CfxError
+    from cocofest_amd import _cfx
+
+    with pytest.raises(CfxError):
+        _cfx.load_library(tmp_path / "nope.so")
+
+
+def test_prepare_n_shooting_matches_reference(ref_formulas):
+    from cocofest_amd import OcpFes
+
+    for tb in ref_formulas["tables"]:
+        assert OcpFes.prepare_n_shooting(tb["stim_time"], tb["final_time"]) == tb["n_shooting"]
+    assert OcpFes.prepare_n_shooting(cases.cfg3()["stims"], 1.0) == 100
+
+
+def test_stim_table_matches_reference_and_oracle(ref_formulas):
+    from cocofest_amd import ModelMaker
+
+    for tb in ref_formulas["tables"]:
+        prev = {"time": list(tb["previous_stim"])} if tb["previous_stim"] else None
+        if prev and tb["model"].startswith("hmed"):
+            prev["pulse_intensity"] = [50] * len(prev["time"])
+        model = ModelMaker.create_model(tb["model"], stim_time=list(tb["stim_time"]),
+                                        sum_stim_truncation=tb["truncation"], previous_stim=prev)
+        table, idx = model.get_numerical_data_time_series(tb["n_shooting"], tb["final_time"])
+        rows = table["stim_time"][:, 0, :].T
+        assert table["stim_time"].shape == (tb["truncation"], 1, tb["n_shooting"] + 1)
+        oracle = O.stim_table(tb["stim_time"], tb["n_shooting"], tb["final_time"], tb["truncation"],
+                              previous_stim=tb["previous_stim"])
+        np.testing.assert_array_equal(rows, oracle.rows)
+        assert idx == oracle.stim_idx_at_node
+        if tb["final_time"] != 0.3:  # float-lookup discrepancy case
+            np.testing.assert_array_equal(rows, np.array(tb["rows"]))
+            assert idx == tb["stim_idx_at_node"]
+
+
+@pytest.mark.parametrize("name", O.MODEL_NAMES)
+def test_model_constants_match_oracle(name):
+    from cocofest_amd import ModelMaker
+
+    model = ModelMaker.create_model(name, sum_stim_truncation=10)
+    c = O.model_constants(name)
+    got = model.cfx_constants()
+    for k, v in c.items():
+        assert got[k] == pytest.approx(v, rel=1e-15), k
+    assert model.nb_state == O.n_states(name)
+    np.testing.assert_array_equal(model.standard_rest_values()[:, 0], O.rest_values(name, c))
+
+
+def test_unknown_model_type():
+    from cocofest_amd import ModelMaker
+
+    with pytest.raises(ValueError, match="Unknown model type: foo"):
+        ModelMaker.create_model("foo")
+
+
+def test_ocp_layout_bounds_and_objectives():
+    from cocofest_amd import _cfx
+
+    t = np.linspace(0, 1, 40)
+    force = 80 * np.sin(np.pi * t) ** 2
+    for name in O.MODEL_NAMES:
+        ocp = cases.product_ocp(name, cases.TEN_PULSES, 1.0, 5, scheme="RK1", m=4,
+                                objective={"force_tracking": [t, force], "end_node_tracking": 40})
+        pb = cases.oracle_problem(name, cases.TEN_PULSES, 1.0, 5, scheme="RK1", m=4,
+                                  objective={"force_tracking": [t, force], "end_node_tracking": 40})
+        assert ocp.nv == pb.nv
+        lo, hi = O.state_bounds(name, pb.c)
+        np.testing.assert_array_equal(ocp.x_bounds[0][:, 0], lo[:, 0])
+        np.testing.assert_array_equal(ocp.x_bounds[1][:, 5], hi[:, 1])
+        np.testing.assert_array_equal(ocp.x_bounds[1][:, -1], hi[:, 2])
+        lb, ub = ocp.bounds_vector()
+        assert lb.shape == ub.shape == (ocp.nv,) and np.all(lb <= ub)
+        tr = ocp.objectives[0]
+        assert tr["kind"] == _cfx.OBJ_LAGRANGE and tr["weight"] == 100.0
+        np.testing.assert_allclose(tr["target"], pb.objectives[0].target, rtol=1e-13, atol=1e-12)
+        assert ocp.objectives[1]["kind"] == _cfx.OBJ_MAYER and ocp.objectives[1]["node_first"] == pb.n_shooting
+
+
+def test_hmed_sliding_window_indices_match_oracle():
+    ocp = cases.product_ocp("hmed2018", cases.TEN_PULSES, 1.0, 4)
+    pb = cases.oracle_problem("hmed2018", cases.TEN_PULSES, 1.0, 4)
+    np.testing.assert_array_equal(ocp.last_stim_idx, pb.last_stim_idx)
+    assert ocp.n_params == pb.n_params == 10
+    assert ocp.intensity_floor == pytest.approx(17.02854931878943, rel=1e-15)
+
+
+def test_pack_unpack_roundtrip():
+    ocp = cases.product_ocp("ding2007_with_fatigue", cases.TEN_PULSES, 1.0, 5)
+    v = np.arange(ocp.nv, dtype=float)
+    states, controls, params = ocp.unpack(v)
+    x = np.concatenate([states[k] for k in ocp.model.name_dof])
+    np.testing.assert_array_equal(ocp.pack(x, controls["last_pulse_width"]), v)
+
+
+def test_ocp_sanity_messages():
+    from cocofest_amd import ModelMaker, OcpFes
+
+    model = ModelMaker.create_model("ding2003", stim_time=[0, 0.1])
+    with pytest.raises(TypeError, match="force_tracking must be list type"):
+        OcpFes.prepare_ocp(model=model, final_time=0.2, objective={"force_tracking": 3})
+    with pytest.raises(TypeError, match="end_node_tracking must be int or float type"):
+        OcpFes.prepare_ocp(model=model, final_time=0.2, objective={"end_node_tracking": "a"})
+    with pytest.raises(TypeError, match="ode_solver must be a OdeSolver type"):
+        OcpFes.prepare_ocp(model=model, final_time=0.2, ode_solver=None)
+    with pytest.raises(TypeError, match="use_sx must be a bool type"):
+        OcpFes.prepare_ocp(model=model, final_time=0.2, use_sx=None)
+    with pytest.raises(TypeError, match="n_thread must be a int type"):
+        OcpFes.prepare_ocp(model=model, final_time=0.2, n_threads=None)
+    with pytest.raises(TypeError, match="it must be a FesModel type"):
+        OcpFes._sanity_check(model=3, n_shooting=2, final_time=1.0, objective={})
+
+
+def test_ivp_validation_messages_match_reference():
+    """The input errors of tests/shard1/test_ivp.py:186-332 that the current reference code raises."""
+    import re as _re
+
+    from cocofest_amd import IvpFes, ModelMaker
+
+    d03 = ModelMaker.create_model("ding2003", stim_time=[0, 0.1, 0.2], sum_stim_truncation=3)
+    d07 = ModelMaker.create_model("ding2007", stim_time=[0, 0.1, 0.2], sum_stim_truncation=3)
+    h18 = ModelMaker.create_model("hmed2018", stim_time=[0, 0.1, 0.2], sum_stim_truncation=3)
+    with pytest.raises(ValueError, match=_re.escape("The number of stimulation needs to be integer within the final "
+                                                    "time t, set round down to True or set final_time * frequency "
+                                                    "to make the result an integer.")):
+        IvpFes.from_frequency_and_final_time({"model": d03, "frequency": 30, "round_down": False},
+                                             {"final_time": 1.25})
+    with pytest.raises(ValueError, match="Pulse mode not yet implemented"):
+        IvpFes({"model": d03, "stim_time": [0, 0.1, 0.2], "pulse_mode": "Quadruplet"}, {"final_time": 0.3})
+    with pytest.raises(ValueError, match=_re.escape("pulse width must be greater than minimum pulse width")):
+        IvpFes({"model": d07, "pulse_width": 0.00001}, {"final_time": 0.3})
+    with pytest.raises(ValueError, match=_re.escape("pulse width must be greater than minimum pulse width")):
+        IvpFes({"model": d07, "pulse_width": [0.001, 0.0001, 0.003]}, {"final_time": 0.3})
+    with pytest.raises(TypeError, match="pulse_width must be int, float or list type"):
+        IvpFes({"model": d07, "pulse_width": True}, {"final_time": 0.3})
+    with pytest.raises(ValueError, match=_re.escape("Pulse intensity must be greater than minimum pulse intensity")):
+        IvpFes({"model": h18, "pulse_intensity": 0.1}, {"final_time": 0.3})
+    with pytest.raises(ValueError, match=_re.escape("Pulse intensity must be greater than minimum pulse intensity")):
+        IvpFes({"model": h18, "pulse_intensity": [20, 30, 0.1]}, {"final_time": 0.3})
+    with pytest.raises(TypeError, match="pulse_intensity must be int, float or list type"):
+        IvpFes({"model": h18, "pulse_intensity": True}, {"final_time": 0.3})
+    with pytest.raises(ValueError, match="ode_solver must be a OdeSolver type"):
+        IvpFes({"model": d03}, {"final_time": 0.3, "ode_solver": None})
+    with pytest.raises(ValueError, match="n_thread must be a int type"):
+        IvpFes({"model": d03}, {"final_time": 0.3, "n_threads": None})
+
+
+def test_ivp_host_setup_matches_oracle():
+    """IvpFes host preparation (n_shooting, pulse modes, table, controls) equals the oracle's."""
+    from cocofest_amd import IvpFes, ModelMaker
+
+    h18 = ModelMaker.create_model("hmed2018", stim_time=[0, 0.1, 0.2], sum_stim_truncation=3)
+    ivp = IvpFes({"model": h18, "pulse_intensity": [50, 60, 70]}, {"final_time": 0.3})
+    tab = O.stim_table([0, 0.1, 0.2], 3, 0.3, 3)
+    np.testing.assert_array_equal(ivp.stim_rows, tab.rows)
+    np.testing.assert_array_equal(ivp.controls.T, O.ivp_controls("hmed2018", tab, 3, 3, None, [50, 60, 70]))
+    d03 = ModelMaker.create_model("ding2003_with_fatigue", stim_time=[0, 0.1, 0.2], sum_stim_truncation=3)
+    ivp = IvpFes({"model": d03, "pulse_mode": "doublet"}, {"final_time": 0.3})
+    assert ivp.n_shooting == 60 and d03.stim_time == [0, 0.005, 0.1, 0.105, 0.2, 0.205]
+    d07 = ModelMaker.create_model("ding2007", stim_time=[0, 0.1, 0.2], sum_stim_truncation=3)
+    ivp = IvpFes({"model": d07, "pulse_width": [0.0003, 0.0004, 0.0005]}, {"final_time": 0.3})
+    np.testing.assert_array_equal(ivp.controls[0], [0.0003, 0.0004, 0.0005])
