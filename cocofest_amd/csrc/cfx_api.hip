@@ -2,6 +2,7 @@
 // coefficient tables, sparsity, buffer staging, and the launches of the gfx950 kernels.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstring>
 #include <string>
@@ -98,6 +99,47 @@ static void build_tables(const cfx_handle* h, std::vector<double>& tab) {
             }
         }
     }
+}
+
+// Dependency bitmask (over z = (x_k, u_k)) of every state after one interval (bits 0..nx-1: states,
+// nx..nx+nu-1: controls).  RHS dependencies: cn_dot <- cn (+ every Hmed intensity through cn_sum);
+// F_dot <- cn, F (+ A, Tau1, Km with fatigue, + pulse width for Ding2007); A/Tau1/Km_dot <- itself, F.
+static void structure_pattern(int model, int scheme, int m, int nx, int nu, uint64_t* dep) {
+    const bool fat = is_fatigue(model), pw = is_pw(model), hm = is_int(model);
+    const uint64_t ubits = hm ? (((1ull << nu) - 1ull) << nx) : 0ull;
+    const uint64_t pwbit = pw ? (1ull << nx) : 0ull;
+    auto f = [&](const uint64_t* x, uint64_t* o) {
+        o[0] = x[0] | ubits;
+        o[1] = x[0] | x[1] | (fat ? (x[2] | x[3] | x[4]) : 0ull) | pwbit;
+        if (fat) {
+            o[2] = x[2] | x[1];
+            o[3] = x[3] | x[1];
+            o[4] = x[4] | x[1];
+        }
+    };
+    uint64_t x[5], k[5], xs[5], acc[5];
+    for (int r = 0; r < nx; ++r) x[r] = 1ull << r;
+    for (int j = 0; j < m; ++j) {
+        f(x, k);
+        if (scheme == 1) {
+            for (int r = 0; r < nx; ++r) x[r] |= k[r];
+            continue;
+        }
+        for (int r = 0; r < nx; ++r) {
+            acc[r] = k[r];
+            xs[r] = x[r] | k[r];
+        }
+        const int extra = scheme == 2 ? 1 : 3;
+        for (int st = 0; st < extra; ++st) {
+            f(xs, k);
+            for (int r = 0; r < nx; ++r) {
+                acc[r] |= k[r];
+                xs[r] = x[r] | k[r];
+            }
+        }
+        for (int r = 0; r < nx; ++r) x[r] |= acc[r];
+    }
+    for (int r = 0; r < nx; ++r) dep[r] = x[r];
 }
 
 static double* ensure(cfx_handle* h, DevBuf& b, size_t count, int* rc) {
@@ -274,11 +316,23 @@ extern "C" int cfx_create(const cfx_problem* p, cfx_handle** out) {
     h->sz.nu = nu;
     h->sz.nv = (int64_t)N * nz + nx + p->n_params;
     h->sz.ng = (int64_t)N * ngk;
-    const int nnzk = nx * (nz + 1);
     const int nhk = nz * (nz + 1) / 2;
+    // structural sparsity of dPhi/d(x_k, u_k), as CasADi derives it symbolically: dependency bitmasks
+    // pushed through the RHS and the RK stages (identical for every interval)
+    uint64_t dep[5];
+    structure_pattern(h->model, h->scheme, p->n_steps, nx, nu, dep);
+    KParams& kp = h->kp;
+    int nnzk = 0;
+    for (int r = 0; r < nx; ++r) {
+        for (int c = 0; c < kMaxNz; ++c) kp.jpos[r][c] = -1;
+        for (int c = 0; c < nz; ++c)
+            if (dep[r] >> c & 1ull) kp.jpos[r][c] = (int16_t)nnzk++;
+        kp.jneg[r] = (int16_t)nnzk++;
+    }
     for (int k = 0; k < N; ++k) {
         for (int r = 0; r < nx; ++r) {
             for (int c = 0; c < nz; ++c) {
+                if (!(dep[r] >> c & 1ull)) continue;
                 h->jrow.push_back(k * ngk + r);
                 h->jcol.push_back(k * nz + c);
             }
@@ -321,7 +375,6 @@ extern "C" int cfx_create(const cfx_problem* p, cfx_handle** out) {
 
     // kernel parameters
     const cfx_constants& c = p->constants;
-    KParams& kp = h->kp;
     kp.B = p->batch;
     kp.nx = nx;
     kp.N = N;
@@ -355,6 +408,13 @@ extern "C" int cfx_create(const cfx_problem* p, cfx_handle** out) {
     kp.inv_tau_fat = is_fatigue(h->model) ? 1.0 / c.tau_fat : 0.0;
     kp.a_fat_rest = is_pw(h->model) ? c.a_scale : c.a_rest;
     kp.mult = c.fl * c.fv + c.fp;
+    {
+        // intervals per thread: as many as possible (x read once) while keeping >= 2048 workgroups in flight
+        const int64_t bx = (p->batch + kBlock - 1) / kBlock;
+        const int64_t nch = nchunk_of(h->model, nz);
+        int64_t kpt = (int64_t)N * bx * nch / 2048;
+        kp.kpt = (int32_t)std::max<int64_t>(1, std::min<int64_t>(N, kpt));
+    }
 
     if (hipSetDevice(h->device) != hipSuccess) return create_fail(h, CFX_EHIP, "cfx_create: hipSetDevice failed");
     if (hipStreamCreateWithFlags(&h->own_stream, hipStreamNonBlocking) != hipSuccess)
@@ -410,7 +470,7 @@ extern "C" int cfx_get_sizes(const cfx_handle* h, cfx_sizes* out) {
 
 extern "C" int cfx_set_stream(cfx_handle* h, void* stream) {
     if (!h) return CFX_EINVAL;
-    h->stream = stream ? (hipStream_t)stream : h->own_stream;
+    h->stream = (hipStream_t)stream;
     return CFX_OK;
 }
 

@@ -2,15 +2,17 @@
 //
 // Data layout in HBM (SoA, "element-major, instance-minor"): element e of instance b lives at
 // buf[e * B + b], so the 64 lanes of a wave (64 consecutive instances) read/write 512 contiguous bytes
-// per access.  One thread owns one (instance, shooting interval, direction chunk); the interval index
-// and the chunk are blockIdx.y / blockIdx.z, hence wave-uniform, so every read of the per-interval
+// per access.  One thread owns one instance, a run of KPT consecutive shooting intervals (the end state
+// of interval k is the loaded start state of interval k+1, so x is read once) and one chunk of
+// Jacobian directions.  Interval index and chunk are wave-uniform, so every read of the per-interval
 // stimulation coefficient table is a scalar (SMEM) load shared by the whole wave.
 //
 // The stimulation sum of the reference (cn_sum_fun, cocofest/models/ding2003.py:230-252) depends only
 // on time and on the stim table row, never on a decision variable (Ding2003/Ding2007), or linearly on
 // lambda_i(u) (Hmed2018, hmed2018.py:97-98,169-180).  It is therefore evaluated once per problem on the
 // host, at every RK stage time of every interval, with the reference's own operation order
-// (r_i * exp(-(t - t_i)/tauc), summed over i), leaving 2 divisions and ~20 flops per RHS on the GPU.
+// (r_i * exp(-(t - t_i)/tauc), summed over i).  What remains per RHS on the GPU: two reciprocals and
+// ~15 FP64 ops, plus a handful of FMAs per Jacobian direction with hand-derived partial derivatives.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -28,6 +30,8 @@ constexpr bool is_pw(int m) { return m == M_D07 || m == M_D07F; }
 constexpr bool is_int(int m) { return m == M_H18 || m == M_H18F; }
 constexpr int stages_of(int scheme) { return scheme == 4 ? 4 : (scheme == 2 ? 2 : 1); }
 
+constexpr int kMaxNz = 5 + 32;  // nx + truncation
+
 // Everything a kernel needs, passed by value (kernel argument segment).
 struct KParams {
     int64_t B;       // batch = SoA leading dimension
@@ -39,10 +43,11 @@ struct KParams {
     int32_t T;       // truncation
     int32_t Q;       // RHS slots per interval (m * stages)
     int32_t ngk;     // constraint rows per interval (nx + n_slide)
-    int32_t nnzk;    // J_g entries per interval (nx * (nz + 1))
+    int32_t nnzk;    // J_g entries per interval (structural pattern + the -I)
     int32_t nhk;     // Hessian entries per interval (nz (nz+1) / 2)
     int32_t n_slide; // sliding-window rows per interval
     int32_t n_params;
+    int32_t kpt;     // shooting intervals per thread
     double dt, h;
     // model constants (reciprocals precomputed on the host)
     double inv_tauc, tau2, km_rest, tau1_rest, a_rest, a_scale, pd0, pdt;
@@ -50,222 +55,290 @@ struct KParams {
     double alpha_a, alpha_tau1, alpha_km, inv_tau_fat, a_fat_rest, mult;
     const double* tab;  // Ding: cs[N*Q]; Hmed: coef[N*Q*TMAX] (zero padded past T)
     const double* rest; // rest state [nx] (IVP default x0)
+    // J_g value offset, inside an interval block, of dPhi_r/dz_c (-1: structural zero) and of the -1 on x_{k+1}[r]
+    int16_t jpos[5][kMaxNz];
+    int16_t jneg[5];
+};
+
+// 1/x from v_rcp_f64 refined by two Newton steps (inputs here are positive and well scaled).
+CFX_HD double frcp(double x) {
+    double y = __builtin_amdgcn_rcp(x);
+    double e = fma(-x, y, 1.0);
+    y = fma(y, e, y);
+    e = fma(-x, y, 1.0);
+    return fma(y, e, y);
+}
+
+// Pulse-width amplitude factor of Ding2007 (ding2007.py:172-188) for one interval:
+// E = 1 - exp(-(pw - pd0)/pdt) and dE/dpw; pwdir = lane direction carrying d/dpw (-1: none).
+struct Amp {
+    double E, dE;
+    int pwdir;
 };
 
 // ---------------------------------------------------------------------------------------------------
-// Right-hand side, written once for double / Dual / Jet.
-//   cn_dot = (cs - cn) / tauc                                  (ding2003.py:254-266)
-//   F_dot  = (A * s - F / (tau1 + tau2 * s)) * (fl*fv + fp),  s = cn / (Km + cn)   (ding2003.py:274-311)
-//   A_dot  = -(A - A_rest)/tau_fat + alpha_A F, same for Tau1, Km  (ding2003_with_fatigue.py:197-240)
-// Ding2007: A is scaled by afac = 1 - exp(-(pw - pd0)/pdt)  (ding2007.py:172-188); for the model
-// without fatigue afac already contains a_scale.
+// Right-hand side and its directional derivatives.
+//   cn_dot = (cs - cn) / tauc                                              (ding2003.py:254-266)
+//   F_dot  = (A s - F / (tau1 + tau2 s)) (fl fv + fp),  s = cn / (Km + cn)     (ding2003.py:274-311)
+//   A_dot  = alpha_A F - (A - A_rest) / tau_fat, same for Tau1, Km          (ding2003_with_fatigue.py:197-240)
+// Ding2007 scales A by E(pw) (a_scale * E without fatigue).  xd[r][j] = d x_r / d z along lane
+// direction j, csd[j] = d cs / d z (Hmed only), fd likewise for the output.
 // ---------------------------------------------------------------------------------------------------
-template <int MODEL, class S, class CS>
-CFX_HD void rhs(const KParams& P, const S* x, const CS& cs, const S& afac, S* dx) {
-    const S& cn = x[0];
-    const S& F = x[1];
-    dx[0] = P.inv_tauc * (cs - cn);
-    if constexpr (is_fatigue(MODEL)) {
-        const S& A = x[2];
-        const S& tau1 = x[3];
-        const S& km = x[4];
-        const S s = cn / (km + cn);
-        if constexpr (is_pw(MODEL)) {
-            dx[1] = ((A * afac) * s - F / (tau1 + P.tau2 * s)) * P.mult;
-        } else {
-            dx[1] = (A * s - F / (tau1 + P.tau2 * s)) * P.mult;
-        }
-        dx[2] = P.alpha_a * F - (A - P.a_fat_rest) * P.inv_tau_fat;
-        dx[3] = P.alpha_tau1 * F - (tau1 - P.tau1_rest) * P.inv_tau_fat;
-        dx[4] = P.alpha_km * F - (km - P.km_rest) * P.inv_tau_fat;
-    } else {
-        const S s = cn / (P.km_rest + cn);
-        if constexpr (is_pw(MODEL)) {
-            dx[1] = (afac * s - F / (P.tau1_rest + P.tau2 * s)) * P.mult;
-        } else {
-            dx[1] = (P.a_rest * s - F / (P.tau1_rest + P.tau2 * s)) * P.mult;
+template <int MODEL, int D, bool CSD>
+CFX_HD void rhs_tan(const KParams& P, const double* x, const double (*xd)[D > 0 ? D : 1], double cs,
+                    const double* csd, const Amp& amp, double* f, double (*fd)[D > 0 ? D : 1]) {
+    constexpr bool FAT = is_fatigue(MODEL), PW = is_pw(MODEL);
+    const double cn = x[0], F = x[1];
+    f[0] = P.inv_tauc * (cs - cn);
+    const double km = FAT ? x[4] : P.km_rest;
+    const double tau1 = FAT ? x[3] : P.tau1_rest;
+    const double A = FAT ? x[2] : (PW ? P.a_scale : P.a_rest);
+    const double Aeff = PW ? A * amp.E : A;
+    const double r = frcp(km + cn);
+    const double s = cn * r;
+    const double iD = frcp(tau1 + P.tau2 * s);
+    f[1] = (Aeff * s - F * iD) * P.mult;
+    if (FAT) {
+        f[2] = P.alpha_a * F - (A - P.a_fat_rest) * P.inv_tau_fat;
+        f[3] = P.alpha_tau1 * F - (tau1 - P.tau1_rest) * P.inv_tau_fat;
+        f[4] = P.alpha_km * F - (km - P.km_rest) * P.inv_tau_fat;
+    }
+    if constexpr (D > 0) {
+        const double q = P.mult * (Aeff + F * P.tau2 * iD * iD) * r;  // mult (Aeff + F tau2 / D^2) / (Km + cn)
+        const double g_cn = q * km * r;                              // * ds/dcn = Km / (Km + cn)^2
+        const double g_F = -P.mult * iD;
+        const double g_A = P.mult * s * (PW ? amp.E : 1.0);
+        const double g_tau = P.mult * F * iD * iD;
+        const double g_km = -q * s;                                  // * ds/dKm = -cn / (Km + cn)^2
+        const double g_pw = PW ? P.mult * s * A * amp.dE : 0.0;
+#pragma unroll
+        for (int j = 0; j < D; ++j) {
+            fd[0][j] = P.inv_tauc * ((CSD ? csd[j] : 0.0) - xd[0][j]);
+            double t = g_cn * xd[0][j] + g_F * xd[1][j];
+            if (FAT) t += g_A * xd[2][j] + g_tau * xd[3][j] + g_km * xd[4][j];
+            if (PW && j == amp.pwdir) t += g_pw;
+            fd[1][j] = t;
+            if (FAT) {
+                fd[2][j] = P.alpha_a * xd[1][j] - P.inv_tau_fat * xd[2][j];
+                fd[3][j] = P.alpha_tau1 * xd[1][j] - P.inv_tau_fat * xd[3][j];
+                fd[4][j] = P.alpha_km * xd[1][j] - P.inv_tau_fat * xd[4][j];
+            }
         }
     }
 }
 
-// Stimulation-sum providers: slot q (= ((k*m + j) * stages + stage)) -> cs value (+ derivatives).
+// Stimulation-sum providers: slot q (= (k*m + j) * stages + stage) -> cs value (+ derivatives).
 struct CsTable {
+    static constexpr bool kDeriv = false;
     const double* tab;
-    CFX_HD double operator()(int q) const { return tab[q]; }
+    template <int D>
+    CFX_HD double eval(int q, double*) const { return tab[q]; }
 };
 
-// Hmed2018: cs = sum_i coef[q][i] * lambda_i(u_i); lambda values held in registers, the derivative
-// enters only along this lane's u-directions (uidx >= 0).
-template <int D, int TMAX>
+// Hmed2018: cs = sum_i coef[q][i] * lambda_i(u_i) with lambda_i held in registers; the derivative exists only
+// along this lane's u-directions (uidx >= 0): d cs / d u_i = coef[q][i] * lambda_i'(u_i).
+template <int DMAX, int TMAX>
 struct CsHmed {
+    static constexpr bool kDeriv = true;
     const double* coef;
     double lamv[TMAX];
-    double lamd[D > 0 ? D : 1];
-    int uidx[D > 0 ? D : 1];
-    CFX_HD Dual<D> operator()(int q) const {
+    double lamd[DMAX > 0 ? DMAX : 1];
+    int uidx[DMAX > 0 ? DMAX : 1];
+    template <int D>
+    CFX_HD double eval(int q, double* csd) const {
         const double* c = coef + (int64_t)q * TMAX;
         double s = 0.0;
 #pragma unroll
         for (int i = 0; i < TMAX; ++i) s += c[i] * lamv[i];
-        Dual<D> r;
-        r.v = s;
 #pragma unroll
-        for (int j = 0; j < D; ++j) r.d[j] = uidx[j] >= 0 ? c[uidx[j]] * lamd[j] : 0.0;
-        return r;
-    }
-};
-
-// value-only Hmed provider (g, IVP)
-template <int TMAX>
-struct CsHmedV {
-    const double* coef;
-    double lamv[TMAX];
-    CFX_HD double operator()(int q) const {
-        const double* c = coef + (int64_t)q * TMAX;
-        double s = 0.0;
-#pragma unroll
-        for (int i = 0; i < TMAX; ++i) s += c[i] * lamv[i];
+        for (int j = 0; j < D; ++j) csd[j] = uidx[j] >= 0 ? c[uidx[j]] * lamd[j] : 0.0;
         return s;
     }
 };
 
-// m sub-steps of RK-s over one interval (bioptim RK1 = Euler, RK2 = midpoint, RK4 = classic;
-// stage times t, t+h/2, t+h/2, t+h; control held constant).  q0 = first RHS slot of the interval.
-template <int MODEL, int SCHEME, class S, class CSP>
-CFX_HD void integrate_interval(const KParams& P, int q0, S* x, const S& afac, const CSP& csp) {
+// m sub-steps of RK-s over one interval (bioptim RK1 = Euler, RK2 = midpoint, RK4 = classic; stage
+// times t, t+h/2, t+h/2, t+h; control held constant), carrying D tangent directions.  q0 = first slot.
+template <int MODEL, int SCHEME, int D, class CSP>
+CFX_HD void integrate_tan(const KParams& P, int q0, int msteps, double* x, double (*xd)[D > 0 ? D : 1],
+                          const Amp& amp, const CSP& csp) {
     constexpr int NX = nx_of(MODEL);
-    const double h = P.h;
-    const double h2 = 0.5 * P.h;
-    const double h6 = P.h / 6.0;
+    constexpr int DD = D > 0 ? D : 1;
+    constexpr bool CSD = CSP::kDeriv;
+    const double h = P.h, h2 = 0.5 * P.h, h6 = P.h / 6.0;
     int q = q0;
-    for (int j = 0; j < P.m; ++j) {
-        S k1[NX];
-        rhs<MODEL>(P, x, csp(q), afac, k1);
+    for (int j = 0; j < msteps; ++j) {
+        double csd[DD];
+        double k[NX], kd[NX][DD];
+        double cs = csp.template eval<D>(q, csd);
+        rhs_tan<MODEL, D, CSD>(P, x, xd, cs, csd, amp, k, kd);
         if constexpr (SCHEME == 1) {
 #pragma unroll
-            for (int r = 0; r < NX; ++r) x[r] = x[r] + h * k1[r];
+            for (int r = 0; r < NX; ++r) {
+                x[r] = x[r] + h * k[r];
+#pragma unroll
+                for (int d = 0; d < D; ++d) xd[r][d] = xd[r][d] + h * kd[r][d];
+            }
             q += 1;
         } else if constexpr (SCHEME == 2) {
-            S xs[NX], k2[NX];
+            double xs[NX], xsd[NX][DD];
 #pragma unroll
-            for (int r = 0; r < NX; ++r) xs[r] = x[r] + h2 * k1[r];
-            rhs<MODEL>(P, xs, csp(q + 1), afac, k2);
+            for (int r = 0; r < NX; ++r) {
+                xs[r] = x[r] + h2 * k[r];
 #pragma unroll
-            for (int r = 0; r < NX; ++r) x[r] = x[r] + h * k2[r];
+                for (int d = 0; d < D; ++d) xsd[r][d] = xd[r][d] + h2 * kd[r][d];
+            }
+            cs = csp.template eval<D>(q + 1, csd);
+            rhs_tan<MODEL, D, CSD>(P, xs, xsd, cs, csd, amp, k, kd);
+#pragma unroll
+            for (int r = 0; r < NX; ++r) {
+                x[r] = x[r] + h * k[r];
+#pragma unroll
+                for (int d = 0; d < D; ++d) xd[r][d] = xd[r][d] + h * kd[r][d];
+            }
             q += 2;
         } else {
-            S xs[NX], acc[NX], kk[NX];
+            double xs[NX], xsd[NX][DD], acc[NX], accd[NX][DD];
 #pragma unroll
             for (int r = 0; r < NX; ++r) {
-                acc[r] = k1[r];
-                xs[r] = x[r] + h2 * k1[r];
+                acc[r] = k[r];
+                xs[r] = x[r] + h2 * k[r];
+#pragma unroll
+                for (int d = 0; d < D; ++d) {
+                    accd[r][d] = kd[r][d];
+                    xsd[r][d] = xd[r][d] + h2 * kd[r][d];
+                }
             }
-            rhs<MODEL>(P, xs, csp(q + 1), afac, kk);
+#pragma unroll
+            for (int st = 1; st < 4; ++st) {
+                cs = csp.template eval<D>(q + st, csd);
+                rhs_tan<MODEL, D, CSD>(P, xs, xsd, cs, csd, amp, k, kd);
+                if (st < 3) {
+                    const double c = st == 1 ? h2 : h;
+#pragma unroll
+                    for (int r = 0; r < NX; ++r) {
+                        acc[r] = acc[r] + 2.0 * k[r];
+                        xs[r] = x[r] + c * k[r];
+#pragma unroll
+                        for (int d = 0; d < D; ++d) {
+                            accd[r][d] = accd[r][d] + 2.0 * kd[r][d];
+                            xsd[r][d] = xd[r][d] + c * kd[r][d];
+                        }
+                    }
+                }
+            }
 #pragma unroll
             for (int r = 0; r < NX; ++r) {
-                acc[r] = acc[r] + 2.0 * kk[r];
-                xs[r] = x[r] + h2 * kk[r];
-            }
-            rhs<MODEL>(P, xs, csp(q + 2), afac, kk);
+                x[r] = x[r] + h6 * (acc[r] + k[r]);
 #pragma unroll
-            for (int r = 0; r < NX; ++r) {
-                acc[r] = acc[r] + 2.0 * kk[r];
-                xs[r] = x[r] + h * kk[r];
+                for (int d = 0; d < D; ++d) xd[r][d] = xd[r][d] + h6 * (accd[r][d] + kd[r][d]);
             }
-            rhs<MODEL>(P, xs, csp(q + 3), afac, kk);
-#pragma unroll
-            for (int r = 0; r < NX; ++r) x[r] = x[r] + h6 * (acc[r] + kk[r]);
             q += 4;
         }
     }
 }
 
+// Per-interval control set-up: Ding2007 amplitude factor, Hmed lambdas.  gdir(j) = global direction of
+// lane direction j (chunk * D + j); u directions start at NX.
+template <int MODEL, int D, int TMAX>
+CFX_HD void load_controls(const KParams& P, const double* Vb, int64_t B, int xo, int chunk, Amp& amp,
+                          CsHmed<D, TMAX>& csh) {
+    constexpr int NX = nx_of(MODEL);
+    amp.E = 1.0;
+    amp.dE = 0.0;
+    amp.pwdir = -1;
+    if constexpr (is_pw(MODEL)) {
+        const double pw = Vb[(int64_t)(xo + NX) * B];
+        const double ex = exp(-(pw - P.pd0) / P.pdt);
+        amp.E = 1.0 - ex;
+        amp.dE = ex / P.pdt;
+        const int j = NX - chunk * D;
+        amp.pwdir = (j >= 0 && j < D) ? j : -1;
+    }
+    if constexpr (is_int(MODEL)) {
+        csh.coef = P.tab;
+#pragma unroll
+        for (int i = 0; i < TMAX; ++i) {
+            const double ui = i < P.T ? Vb[(int64_t)(xo + NX + i) * B] : P.Is;
+            csh.lamv[i] = i < P.T ? P.ar * (tanh(P.bs * (ui - P.Is)) + P.cr) : 0.0;
+        }
+#pragma unroll
+        for (int j = 0; j < D; ++j) {
+            const int gd = chunk * D + j;
+            csh.uidx[j] = -1;
+            csh.lamd[j] = 0.0;
+            if (gd >= NX && gd < P.nz) {
+                const double th = tanh(P.bs * (Vb[(int64_t)(xo + gd) * B] - P.Is));
+                csh.lamd[j] = P.ar * P.bs * (1.0 - th * th);
+                csh.uidx[j] = gd - NX;
+            }
+        }
+    }
+}
+
 // ---------------------------------------------------------------------------------------------------
-// Kernel 1: continuity residuals g_k = Phi(x_k, u_k) - x_{k+1} and the dense Jacobian block
-// dPhi/d(x_k, u_k) (+ the -I on x_{k+1}).  Thread = (instance b, interval k = blockIdx.y,
-// direction chunk = blockIdx.z); D directions per lane (D = 0: g only).
+// Kernel 1: continuity residuals g_k = Phi(x_k, u_k) - x_{k+1} and the structurally non-zero entries of
+// dPhi/d(x_k, u_k) (+ the -1 on x_{k+1}).  Thread = (instance b, intervals [k0, k0+kpt), direction chunk);
+// D directions per lane (D = 0: g only).
 // ---------------------------------------------------------------------------------------------------
 template <int MODEL, int SCHEME, int D, int TMAX>
 __global__ void __launch_bounds__(256) k_shooting(const KParams P, const double* __restrict__ V,
                                                   double* __restrict__ G, double* __restrict__ J) {
     constexpr int NX = nx_of(MODEL);
-    using S = Dual<D>;
+    constexpr int DD = D > 0 ? D : 1;
     const int64_t B = P.B;
     const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= B) return;
-    const int k = blockIdx.y;
+    const int k0 = blockIdx.y * P.kpt;
+    const int k1 = min(P.N, k0 + P.kpt);
     const int chunk = blockIdx.z;
-    const int xo = k * P.nz;
     const double* Vb = V + b;
 
-    S x[NX];
+    double x[NX];
 #pragma unroll
-    for (int r = 0; r < NX; ++r) x[r] = dconst<D>(Vb[(int64_t)(xo + r) * B]);
-#pragma unroll
-    for (int j = 0; j < D; ++j) {
-        const int gd = chunk * D + j;
-        if (gd < NX) {
-#pragma unroll
-            for (int r = 0; r < NX; ++r)
-                if (r == gd) x[r].d[j] = 1.0;
-        }
-    }
+    for (int r = 0; r < NX; ++r) x[r] = Vb[(int64_t)(k0 * P.nz + r) * B];
 
-    S afac = dconst<D>(0.0);
-    if constexpr (is_pw(MODEL)) {
-        S pw = dconst<D>(Vb[(int64_t)(xo + NX) * B]);
-#pragma unroll
-        for (int j = 0; j < D; ++j)
-            if (chunk * D + j == NX) pw.d[j] = 1.0;
-        const S e = 1.0 - sexp((-1.0) * (pw - P.pd0) / P.pdt);
-        afac = is_fatigue(MODEL) ? e : P.a_scale * e;
-    }
-
-    if constexpr (is_int(MODEL)) {
-        CsHmed<D, TMAX> csp;
-        csp.coef = P.tab;
-#pragma unroll
-        for (int i = 0; i < TMAX; ++i) {
-            const double ui = i < P.T ? Vb[(int64_t)(xo + NX + i) * B] : P.Is;
-            csp.lamv[i] = i < P.T ? P.ar * (tanh(P.bs * (ui - P.Is)) + P.cr) : 0.0;
-        }
-#pragma unroll
-        for (int j = 0; j < D; ++j) {
-            const int gd = chunk * D + j;
-            if (gd >= NX && gd < P.nz) {
-                const double ui = Vb[(int64_t)(xo + gd) * B];
-                const double th = tanh(P.bs * (ui - P.Is));
-                csp.lamd[j] = P.ar * P.bs * (1.0 - th * th);
-                csp.uidx[j] = gd - NX;
-            } else {
-                csp.lamd[j] = 0.0;
-                csp.uidx[j] = -1;
-            }
-        }
-        integrate_interval<MODEL, SCHEME>(P, k * P.Q, x, afac, csp);
-    } else {
-        integrate_interval<MODEL, SCHEME>(P, k * P.Q, x, afac, CsTable{P.tab});
-    }
-
-    if (G != nullptr && chunk == 0) {
-        const int xn = (k + 1) * P.nz;
+    for (int k = k0; k < k1; ++k) {
+        const int xo = k * P.nz;
+        double xd[NX][DD];
 #pragma unroll
         for (int r = 0; r < NX; ++r)
-            G[(int64_t)(k * P.ngk + r) * B + b] = value(x[r]) - Vb[(int64_t)(xn + r) * B];
-    }
-    if constexpr (D > 0) {
-        if (J != nullptr) {
-            const int64_t jo = (int64_t)k * P.nnzk;
 #pragma unroll
-            for (int r = 0; r < NX; ++r) {
+            for (int j = 0; j < D; ++j) xd[r][j] = (chunk * D + j == r) ? 1.0 : 0.0;
+        Amp amp;
+        CsHmed<D, TMAX> csh;
+        load_controls<MODEL, D, TMAX>(P, Vb, B, xo, chunk, amp, csh);
+        if constexpr (is_int(MODEL)) {
+            integrate_tan<MODEL, SCHEME, D>(P, k * P.Q, P.m, x, xd, amp, csh);
+        } else {
+            integrate_tan<MODEL, SCHEME, D>(P, k * P.Q, P.m, x, xd, amp, CsTable{P.tab});
+        }
+        const int xn = (k + 1) * P.nz;
+        double xnext[NX];
 #pragma unroll
-                for (int j = 0; j < D; ++j) {
-                    const int gd = chunk * D + j;
-                    if (gd < P.nz) J[(jo + r * (P.nz + 1) + gd) * B + b] = x[r].d[j];
+        for (int r = 0; r < NX; ++r) xnext[r] = Vb[(int64_t)(xn + r) * B];
+        if (G != nullptr && chunk == 0) {
+#pragma unroll
+            for (int r = 0; r < NX; ++r) G[(int64_t)(k * P.ngk + r) * B + b] = x[r] - xnext[r];
+        }
+        if constexpr (D > 0) {
+            if (J != nullptr) {
+                const int64_t jo = (int64_t)k * P.nnzk;
+#pragma unroll
+                for (int r = 0; r < NX; ++r) {
+#pragma unroll
+                    for (int j = 0; j < D; ++j) {
+                        const int gd = chunk * D + j;
+                        if (gd < P.nz) {
+                            const int pos = P.jpos[r][gd];
+                            if (pos >= 0) J[(jo + pos) * B + b] = xd[r][j];
+                        }
+                    }
+                    if (chunk == 0) J[(jo + P.jneg[r]) * B + b] = -1.0;
                 }
-                if (chunk == 0) J[(jo + r * (P.nz + 1) + P.nz) * B + b] = -1.0;
             }
         }
+#pragma unroll
+        for (int r = 0; r < NX; ++r) x[r] = xnext[r];
     }
 }
 
@@ -281,37 +354,25 @@ __global__ void __launch_bounds__(256) k_ivp(const KParams P, const double* __re
     const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= B) return;
     double x[NX];
+    double xd[NX][1];
 #pragma unroll
     for (int r = 0; r < NX; ++r) {
         x[r] = X0 ? X0[(int64_t)r * B + b] : P.rest[r];
         TR[(int64_t)r * B + b] = x[r];
     }
     int64_t s = 1;
+    const double* Ub = U ? U + b : nullptr;
     for (int k = 0; k < P.N; ++k) {
-        double afac = 0.0;
-        if constexpr (is_pw(MODEL)) {
-            const double pw = U[(int64_t)(k * P.nu) * B + b];
-            const double e = 1.0 - exp(-(pw - P.pd0) / P.pdt);
-            afac = is_fatigue(MODEL) ? e : P.a_scale * e;
-        }
-        // integrate sub-step by sub-step so every sample is stored
-        KParams Pk = P;
-        Pk.m = 1;
-        CsHmedV<TMAX> csh;
-        if constexpr (is_int(MODEL)) {
-            csh.coef = P.tab;
-#pragma unroll
-            for (int i = 0; i < TMAX; ++i) {
-                const double ui = i < P.T ? U[(int64_t)(k * P.nu + i) * B + b] : P.Is;
-                csh.lamv[i] = i < P.T ? P.ar * (tanh(P.bs * (ui - P.Is)) + P.cr) : 0.0;
-            }
-        }
+        Amp amp;
+        CsHmed<0, TMAX> csh;
+        // controls of interval k live at U[(k*nu + i)*B + b]; load_controls reads Vb[(xo + NX + i)*B]
+        load_controls<MODEL, 0, TMAX>(P, Ub, B, k * P.nu - NX, 0, amp, csh);
         for (int j = 0; j < P.m; ++j) {
             const int q0 = (k * P.m + j) * stages_of(SCHEME);
             if constexpr (is_int(MODEL)) {
-                integrate_interval<MODEL, SCHEME>(Pk, q0, x, afac, csh);
+                integrate_tan<MODEL, SCHEME, 0>(P, q0, 1, x, xd, amp, csh);
             } else {
-                integrate_interval<MODEL, SCHEME>(Pk, q0, x, afac, CsTable{P.tab});
+                integrate_tan<MODEL, SCHEME, 0>(P, q0, 1, x, xd, amp, CsTable{P.tab});
             }
 #pragma unroll
             for (int r = 0; r < NX; ++r) TR[(s * NX + r) * B + b] = x[r];

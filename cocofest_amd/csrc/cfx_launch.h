@@ -14,6 +14,9 @@ constexpr int dirs_of(int model) {
     return model == M_D03 ? 2 : model == M_D03F ? 5 : model == M_D07 ? 3 : model == M_D07F ? 6 : model == M_H18 ? 4 : 5;
 }
 
+// Direction chunks per lane group for a problem with nz directions.
+inline int nchunk_of(int model, int nz) { return (nz + dirs_of(model) - 1) / dirs_of(model); }
+
 // Smallest supported register-resident truncation bucket >= T (Hmed only).
 inline int tmax_bucket(int T) { return T <= 4 ? 4 : T <= 8 ? 8 : T <= 16 ? 16 : 32; }
 
@@ -32,7 +35,7 @@ template <int MODEL, int SCHEME, int D, int TMAX>
 hipError_t launch_shooting_t(const KParams& P, const double* V, double* G, double* J, hipStream_t s) {
     const int nz = P.nz;
     const int nchunk = D > 0 ? (nz + D - 1) / D : 1;
-    dim3 grid((unsigned)((P.B + kBlock - 1) / kBlock), (unsigned)P.N, (unsigned)nchunk);
+    dim3 grid((unsigned)((P.B + kBlock - 1) / kBlock), (unsigned)((P.N + P.kpt - 1) / P.kpt), (unsigned)nchunk);
     hipLaunchKernelGGL((k_shooting<MODEL, SCHEME, D, TMAX>), grid, dim3(kBlock), 0, s, P, V, G, J);
     return hipGetLastError();
 }

@@ -135,7 +135,9 @@ typedef struct cfx_sizes {
 int cfx_create(const cfx_problem *problem, cfx_handle **out);
 void cfx_destroy(cfx_handle *h);
 int cfx_get_sizes(const cfx_handle *h, cfx_sizes *out);
-int cfx_set_stream(cfx_handle *h, void *hip_stream); /* NULL: the handle's own stream */
+/* Launch stream for CFX_DEVICE calls, used as given (NULL = the HIP null stream).  A new handle uses a
+   non-blocking stream of its own until this is called. */
+int cfx_set_stream(cfx_handle *h, void *hip_stream);
 int cfx_synchronize(cfx_handle *h);
 const char *cfx_last_error(const cfx_handle *h); /* h == NULL: last cfx_create failure of this thread */
 int cfx_abi_version(void);

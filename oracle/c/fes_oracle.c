@@ -158,11 +158,12 @@ static void interval(const ctx *c, const rhs_in *in, int scheme, int m, double t
 
 /*
  * Continuity residuals + Jacobian values (+ Hmed sliding rows) for B instances, AoS, in the include/cfx.h
- * ordering.  g / jac may be NULL.  Returns 0, or -1 on unsupported sizes.
+ * ordering.  jpos[r*nz + c] / jneg[r]: offsets inside an interval block of the structurally non-zero entries
+ * and of the -1 (nnzk per interval).  g / jac may be NULL.  Returns 0, or -1 on unsupported sizes.
  */
 int oracle_shooting(int model, int scheme, int m, int N, int T, double tf, const double *rows, const double *consts,
                     int n_params, const int32_t *last_idx, double floor_value, int64_t B, const double *v, double *g,
-                    double *jac, int nthreads) {
+                    double *jac, const int32_t *jpos, const int32_t *jneg, int nnzk, int nthreads) {
     const int nx = (model & 1) ? 5 : 2;
     const int nu = (model == 2 || model == 3) ? 1 : (model >= 4 ? T : 0);
     const int nz = nx + nu;
@@ -171,7 +172,6 @@ int oracle_shooting(int model, int scheme, int m, int N, int T, double tf, const
     const int ngk = nx + n_slide;
     const int64_t nv = (int64_t)N * nz + nx + n_params;
     const int64_t ng = (int64_t)N * ngk;
-    const int nnzk = nx * (nz + 1);
     int64_t nnz_slide = 0;
     if (n_slide)
         for (int k = 0; k < N; ++k)
@@ -216,8 +216,9 @@ int oracle_shooting(int model, int scheme, int m, int N, int T, double tf, const
             if (jac) {
                 double *jb = jac + b * nnz + (int64_t)k * nnzk;
                 for (int r = 0; r < nx; ++r) {
-                    for (int q = 0; q < nz; ++q) jb[r * (nz + 1) + q] = x[r].d[q];
-                    jb[r * (nz + 1) + nz] = -1.0;
+                    for (int q = 0; q < nz; ++q)
+                        if (jpos[r * nz + q] >= 0) jb[jpos[r * nz + q]] = x[r].d[q];
+                    jb[jneg[r]] = -1.0;
                 }
             }
         }

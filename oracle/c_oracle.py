@@ -30,7 +30,7 @@ def load():
         lib.oracle_shooting.restype = C.c_int
         lib.oracle_shooting.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_double, C.c_void_p,
                                         C.c_void_p, C.c_int, C.c_void_p, C.c_double, C.c_int64, C.c_void_p,
-                                        C.c_void_p, C.c_void_p, C.c_int]
+                                        C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int]
         _lib = lib
     return _lib
 
@@ -44,13 +44,25 @@ def shooting(pb: O.Problem, v, want_g=True, want_jac=True, threads=1):
     rows = np.ascontiguousarray(pb.rows, dtype=np.float64)
     last = np.ascontiguousarray(pb.last_stim_idx if pb.n_params else [0], dtype=np.int32)
     nnz = O.jac_structure(pb)[0].size
+    pattern = O.structural_pattern(pb)
+    nz = pb.nx + pb.nu
+    jpos = np.full((pb.nx, nz), -1, dtype=np.int32)
+    jneg = np.empty(pb.nx, dtype=np.int32)
+    off = 0
+    for r in range(pb.nx):
+        for c in sorted(pattern[r]):
+            jpos[r, c] = off
+            off += 1
+        jneg[r] = off
+        off += 1
     g = np.empty((B, pb.ng)) if want_g else None
     jac = np.empty((B, nnz)) if want_jac else None
     model = O.MODEL_NAMES.index(pb.name)
     rc = lib.oracle_shooting(model, SCHEME[pb.scheme], pb.n_steps, pb.n_shooting, pb.truncation, pb.final_time,
                              rows.ctypes.data, consts.ctypes.data, pb.n_params, last.ctypes.data,
                              pb.intensity_floor, B, v.ctypes.data, None if g is None else g.ctypes.data,
-                             None if jac is None else jac.ctypes.data, threads)
+                             None if jac is None else jac.ctypes.data, jpos.ctypes.data, jneg.ctypes.data, off,
+                             threads)
     if rc != 0:
         raise RuntimeError("oracle_shooting: unsupported size")
     return g, jac

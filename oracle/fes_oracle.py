@@ -389,16 +389,50 @@ def continuity_blocks(pb: Problem, v, h=1e-30):
     return out
 
 
+def structural_pattern(pb: Problem):
+    """Symbolic (CasADi-style) sparsity of dPhi/d(x_k, u_k): the set of z-indices each state of the interval
+    end depends on, propagated through the RHS dependencies of a3-a9 and the RK stages.  Returns a list of
+    sets, one per state.  Placeholder history terms keep their (numerically zero) structural entries, as a
+    symbolic evaluation of cn_sum_fun with the stim times as inputs would."""
+    nx, nu = pb.nx, pb.nu
+    kind = control_kind(pb.name)
+    fatigue = pb.name.endswith("with_fatigue")
+
+    def f(x):
+        out = [x[0] | (set(range(nx, nx + nu)) if kind == "pulse_intensity" else set())]
+        fdep = x[0] | x[1]
+        if fatigue:
+            fdep = fdep | x[2] | x[3] | x[4]
+        if kind == "pulse_width":
+            fdep = fdep | {nx}
+        out.append(fdep)
+        if fatigue:
+            out += [x[2] | x[1], x[3] | x[1], x[4] | x[1]]
+        return out
+
+    x = [{r} for r in range(nx)]
+    n_stage = {"RK1": 1, "RK2": 2, "RK4": 4}[pb.scheme]
+    for _ in range(pb.n_steps):
+        k = f(x)
+        acc = [set(a) for a in k]
+        for _ in range(n_stage - 1):
+            k = f([x[r] | k[r] for r in range(nx)])
+            acc = [acc[r] | k[r] for r in range(nx)]
+        x = [x[r] | acc[r] for r in range(nx)]
+    return x
+
+
 def jac_structure(pb: Problem):
     """Triplet structure (row, col) of J_g, in the build's value order: per interval k, for every
-    continuity row r the dense (x_k, u_k) entries then the -1 on x_{k+1}[r]; then, after all intervals,
-    the sliding-window entries (+1 on u_k[j], -1 on the parameter it equals)."""
+    continuity row r its structurally non-zero (x_k, u_k) entries (ascending) then the -1 on x_{k+1}[r];
+    then, after all intervals, the sliding-window entries (+1 on u_k[j], -1 on the parameter it equals)."""
     rows, cols = [], []
     nx, nu, ns = pb.nx, pb.nu, pb.n_slide
+    pattern = structural_pattern(pb)
     for k in range(pb.n_shooting):
         g0 = k * (nx + ns)
         for r in range(nx):
-            for c in range(nx + nu):
+            for c in sorted(pattern[r]):
                 rows.append(g0 + r)
                 cols.append(pb.x_off(k) + c)
             rows.append(g0 + r)
@@ -422,9 +456,13 @@ def eval_jac_g(pb: Problem, v):
     """J_g values in ``jac_structure`` order, shape (B, nnz)."""
     blocks = continuity_blocks(pb, v)
     B = v.shape[0]
-    nx, nz = pb.nx, pb.nx + pb.nu
-    per = np.concatenate([blocks, -np.ones((B, pb.n_shooting, nx, 1))], axis=3)  # (B,N,nx,nz+1)
-    vals = [per.reshape(B, -1)]
+    pattern = structural_pattern(pb)
+    cols = []
+    for k in range(pb.n_shooting):
+        for r in range(pb.nx):
+            cols += [blocks[:, k, r, c] for c in sorted(pattern[r])]
+            cols.append(-np.ones(B))
+    vals = [np.stack(cols, axis=1)]
     if pb.n_slide:
         sl = []
         for k in range(pb.n_shooting):

@@ -62,7 +62,7 @@ def random_decision(pb, B, seed=0):
         X[..., 3] = r.uniform(pb.c["tau1_rest"], 0.1, X.shape[:2])
         X[..., 4] = r.uniform(pb.c["km_rest"], 0.3, X.shape[:2])
     U = np.empty((B, pb.n_shooting, pb.nu))
-    if pb.nu == 1:
+    if O.control_kind(pb.name) == "pulse_width":
         U[...] = r.uniform(pb.c["pd0"], 6e-4, U.shape)
     elif pb.nu:
         U[...] = r.uniform(17.1, 130.0, U.shape)

@@ -143,3 +143,19 @@ def test_c_port_matches_numpy_oracle(name, scheme):
     g, jac = c_oracle.shooting(pb, v, threads=2)
     np.testing.assert_allclose(g, O.eval_g(pb, v), rtol=1e-12, atol=1e-10)
     np.testing.assert_allclose(jac, O.eval_jac_g(pb, v), rtol=1e-10, atol=1e-9)
+
+
+@pytest.mark.parametrize("scheme", ["RK1", "RK2", "RK4"])
+@pytest.mark.parametrize("name", O.MODEL_NAMES)
+def test_structural_pattern_covers_every_nonzero(name, scheme):
+    for m in (1, 2, 3):
+        pb, v = _small_problem(name, scheme=scheme, m=m)
+        blocks = O.continuity_blocks(pb, v)
+        pattern = O.structural_pattern(pb)
+        for r in range(pb.nx):
+            outside = [c for c in range(pb.nx + pb.nu) if c not in pattern[r]]
+            assert np.all(blocks[:, :, r, outside] == 0.0), (r, outside)
+        if not name.startswith("hmed"):  # Hmed placeholder entries are structural but numerically zero
+            for r in range(pb.nx):
+                inside = sorted(pattern[r])
+                assert np.all(np.any(blocks[:, :, r, inside] != 0.0, axis=(0, 1)))
