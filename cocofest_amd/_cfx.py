@@ -103,6 +103,12 @@ def load_library(path: str | os.PathLike | None = None):
     if _lib is not None and path is None:
         return _lib
     p = pathlib.Path(path) if path else LIB_PATH
+    # One HIP runtime per process: torch ships its own libamdhip64.so.7 (same soname as /opt/rocm's).  Load it
+    # first so libcfx binds to the already-loaded runtime instead of pulling in a second one.
+    try:
+        import torch  # noqa: F401
+    except Exception:
+        pass
     if not p.exists():
         raise CfxError(ENODEV, f"{p} not found: build it with `make -C cocofest_amd/csrc` (no CPU fallback)")
     lib = C.CDLL(str(p))

@@ -1,0 +1,50 @@
+"""Kernel probe: time the cfg2 shooting kernel variants in one process (interleaved rounds) so A/B
+differences are not cross-process noise.  Usage: python scripts/kprobe.py [--batch B] [--rounds R]"""
+
+import argparse
+import json
+import pathlib
+import sys
+
+import torch
+
+ROOT = pathlib.Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+
+import bench  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=1 << 20)
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--reps", type=int, default=50)
+    ap.add_argument("--n-shooting", type=int, default=20)
+    a = ap.parse_args()
+    ocp = bench.build_problem()
+    B = a.batch
+    h = ocp.nlp(batch=B, layout="soa")
+    v = bench.synthetic_soa(ocp, B, 1, "cuda:0")
+    g = torch.empty((h.ng, B), dtype=torch.float64, device="cuda")
+    j = torch.empty((h.nnz_jac, B), dtype=torch.float64, device="cuda")
+    variants = {"g+J": dict(g=g, jac=j), "g": dict(g=g), "J": dict(jac=j)}
+    res = {k: [] for k in variants}
+    for _ in range(a.rounds):
+        for name, kw in variants.items():
+            for _ in range(3):
+                h.eval_all(v, **kw)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(a.reps):
+                h.eval_all(v, **kw)
+            e1.record()
+            torch.cuda.synchronize()
+            res[name].append(e0.elapsed_time(e1) / a.reps)
+    out = {k: {"median_ms": sorted(x)[len(x) // 2], "min_ms": min(x)} for k, x in res.items()}
+    out["bytes_per_instance_gJ"] = 8 * (h.nv + h.ng + h.nnz_jac)
+    out["batch"] = B
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
