@@ -39,6 +39,7 @@ struct cfx_handle {
     hipStream_t own_stream = nullptr, stream = nullptr;
     double* d_tab = nullptr;
     double* d_rest = nullptr;
+    double* d_cna = nullptr;
     DevObjective* d_obj = nullptr;
     double* d_targets = nullptr;
     int32_t* d_sl_param = nullptr;
@@ -140,6 +141,64 @@ static void structure_pattern(int model, int scheme, int m, int nx, int nu, uint
         for (int r = 0; r < nx; ++r) x[r] |= acc[r];
     }
     for (int r = 0; r < nx; ++r) dep[r] = x[r];
+}
+
+// Ding families: the calcium state under explicit RK is affine in the interval start value,
+// cn(slot) = cna[slot] * cn0 + cnb[k][slot] (see cfx_kernels.h, integrate).  Derived from the stage-time
+// calcium sums cs[k*Q + slot] by running the scheme on (slope, offset) pairs.
+static void affine_calcium(const cfx_handle* h, const std::vector<double>& cs, std::vector<double>& cna,
+                           std::vector<double>& cnb) {
+    const int N = h->prob.n_shooting, m = h->prob.n_steps, S = h->stages, Q = m * S;
+    const double al = 1.0 / h->prob.constants.tauc;
+    const double hh = (h->prob.final_time / N) / m;
+    cna.assign(Q + 1, 0.0);
+    cnb.assign((size_t)N * (Q + 1), 0.0);
+    for (int k = 0; k < N; ++k) {
+        double a = 1.0, b = 0.0;
+        double* ob = &cnb[(size_t)k * (Q + 1)];
+        auto rate = [&](double sa, double sb, int q, double& ka, double& kb) {  // k = al (cs - cn)
+            ka = -al * sa;
+            kb = al * (cs[(size_t)k * Q + q] - sb);
+        };
+        for (int j = 0; j < m; ++j) {
+            const int q = j * S;
+            cna[q] = a;
+            ob[q] = b;
+            double k1a, k1b;
+            rate(a, b, q, k1a, k1b);
+            if (S == 1) {
+                a += hh * k1a;
+                b += hh * k1b;
+            } else if (S == 2) {
+                const double sa = a + hh / 2 * k1a, sb = b + hh / 2 * k1b;
+                cna[q + 1] = sa;
+                ob[q + 1] = sb;
+                double k2a, k2b;
+                rate(sa, sb, q + 1, k2a, k2b);
+                a += hh * k2a;
+                b += hh * k2b;
+            } else {
+                double sa = a + hh / 2 * k1a, sb = b + hh / 2 * k1b, k2a, k2b, k3a, k3b, k4a, k4b;
+                cna[q + 1] = sa;
+                ob[q + 1] = sb;
+                rate(sa, sb, q + 1, k2a, k2b);
+                sa = a + hh / 2 * k2a;
+                sb = b + hh / 2 * k2b;
+                cna[q + 2] = sa;
+                ob[q + 2] = sb;
+                rate(sa, sb, q + 2, k3a, k3b);
+                sa = a + hh * k3a;
+                sb = b + hh * k3b;
+                cna[q + 3] = sa;
+                ob[q + 3] = sb;
+                rate(sa, sb, q + 3, k4a, k4b);
+                a += hh / 6 * (k1a + 2 * k2a + 2 * k3a + k4a);
+                b += hh / 6 * (k1b + 2 * k2b + 2 * k3b + k4b);
+            }
+        }
+        cna[Q] = a;
+        ob[Q] = b;
+    }
 }
 
 static double* ensure(cfx_handle* h, DevBuf& b, size_t count, int* rc) {
@@ -408,6 +467,8 @@ extern "C" int cfx_create(const cfx_problem* p, cfx_handle** out) {
     kp.inv_tau_fat = is_fatigue(h->model) ? 1.0 / c.tau_fat : 0.0;
     kp.a_fat_rest = is_pw(h->model) ? c.a_scale : c.a_rest;
     kp.mult = c.fl * c.fv + c.fp;
+    kp.neg_mult = -kp.mult;
+    kp.mult_km = kp.mult * c.km_rest;
     {
         // intervals per thread: as many as possible (x read once) while keeping >= 2048 workgroups in flight
         const int64_t bx = (p->batch + kBlock - 1) / kBlock;
@@ -421,8 +482,16 @@ extern "C" int cfx_create(const cfx_problem* p, cfx_handle** out) {
         return create_fail(h, CFX_EHIP, "cfx_create: hipStreamCreate failed");
     h->stream = h->own_stream;
 
-    std::vector<double> tab;
+    std::vector<double> tab, cna;
     build_tables(h, tab);
+    if (!hmed) {
+        std::vector<double> cnb;
+        affine_calcium(h, tab, cna, cnb);
+        tab.swap(cnb);
+        kp.tstride = kp.Q + 1;
+    } else {
+        kp.tstride = kp.Q;
+    }
     std::vector<double> rest(nx, 0.0);
     if (nx == 5) {
         rest[2] = kp.a_fat_rest;
@@ -436,12 +505,14 @@ extern "C" int cfx_create(const cfx_problem* p, cfx_handle** out) {
     };
     if (!upload((void**)&h->d_tab, tab.data(), tab.size() * sizeof(double)) ||
         !upload((void**)&h->d_rest, rest.data(), rest.size() * sizeof(double)) ||
+        !upload((void**)&h->d_cna, cna.data(), cna.size() * sizeof(double)) ||
         !upload((void**)&h->d_obj, dobj.data(), dobj.size() * sizeof(DevObjective)) ||
         !upload((void**)&h->d_targets, targets.data(), targets.size() * sizeof(double)) ||
         !upload((void**)&h->d_sl_param, sl_param.data(), sl_param.size() * sizeof(int32_t)) ||
         !upload((void**)&h->d_sl_joff, sl_joff.data(), sl_joff.size() * sizeof(int32_t)))
         return create_fail(h, CFX_ENOMEM, "cfx_create: device allocation/upload failed");
     kp.tab = h->d_tab;
+    kp.cna = h->d_cna;
     kp.rest = h->d_rest;
     *out = h;
     return CFX_OK;
@@ -455,7 +526,7 @@ extern "C" void cfx_destroy(cfx_handle* h) {
         if (h->main[s].p) (void)hipFree(h->main[s].p);
         if (h->stage[s].p) (void)hipFree(h->stage[s].p);
     }
-    for (void* p : {(void*)h->d_tab, (void*)h->d_rest, (void*)h->d_obj, (void*)h->d_targets, (void*)h->d_sl_param,
+    for (void* p : {(void*)h->d_tab, (void*)h->d_rest, (void*)h->d_cna, (void*)h->d_obj, (void*)h->d_targets, (void*)h->d_sl_param,
                     (void*)h->d_sl_joff})
         if (p) (void)hipFree(p);
     if (h->own_stream) (void)hipStreamDestroy(h->own_stream);

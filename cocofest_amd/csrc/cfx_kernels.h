@@ -30,6 +30,7 @@ constexpr bool is_pw(int m) { return m == M_D07 || m == M_D07F; }
 constexpr bool is_int(int m) { return m == M_H18 || m == M_H18F; }
 constexpr int stages_of(int scheme) { return scheme == 4 ? 4 : (scheme == 2 ? 2 : 1); }
 
+
 constexpr int kMaxNz = 5 + 32;  // nx + truncation
 
 // Everything a kernel needs, passed by value (kernel argument segment).
@@ -53,7 +54,10 @@ struct KParams {
     double inv_tauc, tau2, km_rest, tau1_rest, a_rest, a_scale, pd0, pdt;
     double ar, bs, Is, cr;
     double alpha_a, alpha_tau1, alpha_km, inv_tau_fat, a_fat_rest, mult;
-    const double* tab;  // Ding: cs[N*Q]; Hmed: coef[N*Q*TMAX] (zero padded past T)
+    double neg_mult, mult_km;  // -mult, mult * km_rest
+    const double* tab;  // Ding: cnb[N*(Q+1)] affine calcium offsets; Hmed: coef[N*Q*TMAX] (zero padded past T)
+    const double* cna;  // Ding: affine calcium slopes per slot [Q+1] (identical for every interval)
+    int32_t tstride;    // per-interval stride of tab (Ding: Q+1)
     const double* rest; // rest state [nx] (IVP default x0)
     // J_g value offset, inside an interval block, of dPhi_r/dz_c (-1: structural zero) and of the -1 on x_{k+1}[r]
     int16_t jpos[5][kMaxNz];
@@ -77,44 +81,52 @@ struct Amp {
 };
 
 // ---------------------------------------------------------------------------------------------------
-// Right-hand side and its directional derivatives.
-//   cn_dot = (cs - cn) / tauc                                              (ding2003.py:254-266)
+// Force (and fatigue) right-hand side with its directional derivatives, for a given calcium value cn and
+// its tangent cnd (the calcium row itself is handled by the integrator).
 //   F_dot  = (A s - F / (tau1 + tau2 s)) (fl fv + fp),  s = cn / (Km + cn)     (ding2003.py:274-311)
 //   A_dot  = alpha_A F - (A - A_rest) / tau_fat, same for Tau1, Km          (ding2003_with_fatigue.py:197-240)
-// Ding2007 scales A by E(pw) (a_scale * E without fatigue).  xd[r][j] = d x_r / d z along lane
-// direction j, csd[j] = d cs / d z (Hmed only), fd likewise for the output.
+// Ding2007 scales A by E(pw) (ding2007.py:172-188).  With d1 = Km + cn and d2 = tau1 d1 + tau2 cn:
+// s = cn / d1 and 1 / (tau1 + tau2 s) = d1 / d2, so a single reciprocal R = 1 / (d1 d2) serves both
+// quotients (1/d1 = d2 R, 1/d2 = d1 R); the partial derivatives below are exact rearrangements:
+//   dF/dcn = Km W, dF/dKm = -cn W with W = fl fv (A / d1^2 + F tau2 / d2^2);  dF/dF = -d1/d2;
+//   dF/dTau1 = F (d1/d2)^2;  dF/dA = s (E);  dF/dpw = s A dE/dpw.
+// xd[r][j] = d x_r / d z along lane direction j; fd likewise for the output (rows 1..nx-1 written).
 // ---------------------------------------------------------------------------------------------------
-template <int MODEL, int D, bool CSD>
-CFX_HD void rhs_tan(const KParams& P, const double* x, const double (*xd)[D > 0 ? D : 1], double cs,
-                    const double* csd, const Amp& amp, double* f, double (*fd)[D > 0 ? D : 1]) {
+template <int MODEL, int D, bool CN_SPARSE>
+CFX_HD void rhs_force(const KParams& P, double cn, const double* cnd, const double* x,
+                      const double (*xd)[D > 0 ? D : 1], const Amp& amp, double* f, double (*fd)[D > 0 ? D : 1]) {
+    // CN_SPARSE: the calcium tangent is cnd[0] along lane direction 0 and exactly zero elsewhere
     constexpr bool FAT = is_fatigue(MODEL), PW = is_pw(MODEL);
-    const double cn = x[0], F = x[1];
-    f[0] = P.inv_tauc * (cs - cn);
+    const double F = x[1];
     const double km = FAT ? x[4] : P.km_rest;
     const double tau1 = FAT ? x[3] : P.tau1_rest;
     const double A = FAT ? x[2] : (PW ? P.a_scale : P.a_rest);
     const double Aeff = PW ? A * amp.E : A;
-    const double r = frcp(km + cn);
-    const double s = cn * r;
-    const double iD = frcp(tau1 + P.tau2 * s);
-    f[1] = (Aeff * s - F * iD) * P.mult;
+    const double d1 = km + cn;
+    const double d2 = fma(tau1, d1, P.tau2 * cn);
+    const double R = frcp(d1 * d2);
+    const double q1 = d2 * R;  // 1 / d1
+    const double q2 = d1 * R;  // 1 / d2
+    const double t1 = cn * q1; // s
+    const double t2 = d1 * q2; // 1 / (tau1 + tau2 s)
+    f[1] = P.mult * (Aeff * t1 - F * t2);
     if (FAT) {
         f[2] = P.alpha_a * F - (A - P.a_fat_rest) * P.inv_tau_fat;
         f[3] = P.alpha_tau1 * F - (tau1 - P.tau1_rest) * P.inv_tau_fat;
         f[4] = P.alpha_km * F - (km - P.km_rest) * P.inv_tau_fat;
     }
     if constexpr (D > 0) {
-        const double q = P.mult * (Aeff + F * P.tau2 * iD * iD) * r;  // mult (Aeff + F tau2 / D^2) / (Km + cn)
-        const double g_cn = q * km * r;                              // * ds/dcn = Km / (Km + cn)^2
-        const double g_F = -P.mult * iD;
-        const double g_A = P.mult * s * (PW ? amp.E : 1.0);
-        const double g_tau = P.mult * F * iD * iD;
-        const double g_km = -q * s;                                  // * ds/dKm = -cn / (Km + cn)^2
-        const double g_pw = PW ? P.mult * s * A * amp.dE : 0.0;
+        const double W0 = fma(Aeff, q1 * q1, (F * P.tau2) * (q2 * q2));
+        const double g_cn = (FAT ? P.mult * km : P.mult_km) * W0;
+        const double g_F = P.neg_mult * t2;
+        const double g_A = P.mult * t1 * (PW ? amp.E : 1.0);
+        const double g_tau = P.mult * F * (t2 * t2);
+        const double g_km = -cn * P.mult * W0;
+        const double g_pw = PW ? P.mult * t1 * A * amp.dE : 0.0;
 #pragma unroll
         for (int j = 0; j < D; ++j) {
-            fd[0][j] = P.inv_tauc * ((CSD ? csd[j] : 0.0) - xd[0][j]);
-            double t = g_cn * xd[0][j] + g_F * xd[1][j];
+            double t = g_F * xd[1][j];
+            if (!CN_SPARSE || j == 0) t = fma(g_cn, cnd[j], t);
             if (FAT) t += g_A * xd[2][j] + g_tau * xd[3][j] + g_km * xd[4][j];
             if (PW && j == amp.pwdir) t += g_pw;
             fd[1][j] = t;
@@ -127,19 +139,11 @@ CFX_HD void rhs_tan(const KParams& P, const double* x, const double (*xd)[D > 0 
     }
 }
 
-// Stimulation-sum providers: slot q (= (k*m + j) * stages + stage) -> cs value (+ derivatives).
-struct CsTable {
-    static constexpr bool kDeriv = false;
-    const double* tab;
-    template <int D>
-    CFX_HD double eval(int q, double*) const { return tab[q]; }
-};
-
-// Hmed2018: cs = sum_i coef[q][i] * lambda_i(u_i) with lambda_i held in registers; the derivative exists only
-// along this lane's u-directions (uidx >= 0): d cs / d u_i = coef[q][i] * lambda_i'(u_i).
+// Hmed2018 stimulation sum: cs = sum_i coef[q][i] * lambda_i(u_i) with lambda_i held in registers
+// (cn_sum_fun with lambda_i, ding2003.py:230-252 / hmed2018.py:97-98); its derivative exists only along
+// this lane's u-directions (uidx >= 0): d cs / d u_i = coef[q][i] * lambda_i'(u_i).
 template <int DMAX, int TMAX>
 struct CsHmed {
-    static constexpr bool kDeriv = true;
     const double* coef;
     double lamv[TMAX];
     double lamd[DMAX > 0 ? DMAX : 1];
@@ -156,89 +160,125 @@ struct CsHmed {
     }
 };
 
-// m sub-steps of RK-s over one interval (bioptim RK1 = Euler, RK2 = midpoint, RK4 = classic; stage
-// times t, t+h/2, t+h/2, t+h; control held constant), carrying D tangent directions.  q0 = first slot.
-template <int MODEL, int SCHEME, int D, class CSP>
-CFX_HD void integrate_tan(const KParams& P, int q0, int msteps, double* x, double (*xd)[D > 0 ? D : 1],
-                          const Amp& amp, const CSP& csp) {
+// ---------------------------------------------------------------------------------------------------
+// Sub-steps [j0, j0 + msteps) of RK-s over interval k (bioptim RK1 = Euler, RK2 = midpoint, RK4 = classic;
+// stage times t, t+h/2, t+h/2, t+h; control held constant), carrying D tangent directions.
+//
+// Ding2003 / Ding2007 (with or without fatigue): the calcium ODE cn_dot = (cs(t) - cn) / tauc is linear
+// with a decision-independent forcing, so under any explicit RK scheme every stage value is affine in the
+// interval's start value: cn = cna[slot] * cn0 + cnb[k][slot], precomputed on the host (slot = j*S + stage;
+// slot j*S is the start of sub-step j, slot m*S the interval end).  Its tangent is cna along the cn0
+// direction and zero elsewhere.  Hmed2018 (cs depends on the intensities) integrates cn like the others.
+// ---------------------------------------------------------------------------------------------------
+template <int MODEL, int SCHEME, int D, int TMAX>
+CFX_HD void integrate(const KParams& P, int k, int j0, int msteps, double cn0, int chunk, double* x,
+                      double (*xd)[D > 0 ? D : 1], const Amp& amp, const CsHmed<D, TMAX>& csh) {
     constexpr int NX = nx_of(MODEL);
     constexpr int DD = D > 0 ? D : 1;
-    constexpr bool CSD = CSP::kDeriv;
+    constexpr bool LIN = !is_int(MODEL);
+    constexpr int S = stages_of(SCHEME);
+    constexpr int R0 = LIN ? 1 : 0;  // first integrated state row
     const double h = P.h, h2 = 0.5 * P.h, h6 = P.h / 6.0;
-    int q = q0;
-    for (int j = 0; j < msteps; ++j) {
-        double csd[DD];
-        double k[NX], kd[NX][DD];
-        double cs = csp.template eval<D>(q, csd);
-        rhs_tan<MODEL, D, CSD>(P, x, xd, cs, csd, amp, k, kd);
+    const double* cnb = P.tab + (int64_t)k * P.tstride;
+    const bool dir0 = chunk == 0;  // lane direction 0 is d/dcn0 only in chunk 0
+
+    // one RHS evaluation at stage slot `slot` with stage-input state (xs, xsd)
+    auto stage = [&](const double* xs, const double (*xsd)[DD], int slot, double* kk, double (*kkd)[DD]) {
+        double cn, cnd[DD];
+        if constexpr (LIN) {
+            const double a = P.cna[slot];
+            cn = fma(a, cn0, cnb[slot]);
+#pragma unroll
+            for (int d = 0; d < D; ++d) cnd[d] = (dir0 && d == 0) ? a : 0.0;
+        } else {
+            double csd[DD];
+            const double cs = csh.template eval<D>(k * P.Q + slot, csd);
+            cn = xs[0];
+            kk[0] = P.inv_tauc * (cs - cn);
+#pragma unroll
+            for (int d = 0; d < D; ++d) {
+                cnd[d] = xsd[0][d];
+                kkd[0][d] = P.inv_tauc * (csd[d] - cnd[d]);
+            }
+        }
+        rhs_force<MODEL, D, LIN>(P, cn, cnd, xs, xsd, amp, kk, kkd);
+    };
+
+    for (int j = j0; j < j0 + msteps; ++j) {
+        const int slot = j * S;
+        double k1[NX], k1d[NX][DD];
+        stage(x, xd, slot, k1, k1d);
         if constexpr (SCHEME == 1) {
 #pragma unroll
-            for (int r = 0; r < NX; ++r) {
-                x[r] = x[r] + h * k[r];
+            for (int r = R0; r < NX; ++r) {
+                x[r] = x[r] + h * k1[r];
 #pragma unroll
-                for (int d = 0; d < D; ++d) xd[r][d] = xd[r][d] + h * kd[r][d];
+                for (int d = 0; d < D; ++d) xd[r][d] = xd[r][d] + h * k1d[r][d];
             }
-            q += 1;
         } else if constexpr (SCHEME == 2) {
-            double xs[NX], xsd[NX][DD];
+            double xs[NX], xsd[NX][DD], k2[NX], k2d[NX][DD];
 #pragma unroll
-            for (int r = 0; r < NX; ++r) {
-                xs[r] = x[r] + h2 * k[r];
+            for (int r = R0; r < NX; ++r) {
+                xs[r] = x[r] + h2 * k1[r];
 #pragma unroll
-                for (int d = 0; d < D; ++d) xsd[r][d] = xd[r][d] + h2 * kd[r][d];
+                for (int d = 0; d < D; ++d) xsd[r][d] = xd[r][d] + h2 * k1d[r][d];
             }
-            cs = csp.template eval<D>(q + 1, csd);
-            rhs_tan<MODEL, D, CSD>(P, xs, xsd, cs, csd, amp, k, kd);
+            stage(xs, xsd, slot + 1, k2, k2d);
 #pragma unroll
-            for (int r = 0; r < NX; ++r) {
-                x[r] = x[r] + h * k[r];
+            for (int r = R0; r < NX; ++r) {
+                x[r] = x[r] + h * k2[r];
 #pragma unroll
-                for (int d = 0; d < D; ++d) xd[r][d] = xd[r][d] + h * kd[r][d];
+                for (int d = 0; d < D; ++d) xd[r][d] = xd[r][d] + h * k2d[r][d];
             }
-            q += 2;
         } else {
-            double xs[NX], xsd[NX][DD], acc[NX], accd[NX][DD];
+            double xs[NX], xsd[NX][DD], acc[NX], accd[NX][DD], kk[NX], kkd[NX][DD];
 #pragma unroll
-            for (int r = 0; r < NX; ++r) {
-                acc[r] = k[r];
-                xs[r] = x[r] + h2 * k[r];
+            for (int r = R0; r < NX; ++r) {
+                acc[r] = k1[r];
+                xs[r] = x[r] + h2 * k1[r];
 #pragma unroll
                 for (int d = 0; d < D; ++d) {
-                    accd[r][d] = kd[r][d];
-                    xsd[r][d] = xd[r][d] + h2 * kd[r][d];
+                    accd[r][d] = k1d[r][d];
+                    xsd[r][d] = xd[r][d] + h2 * k1d[r][d];
                 }
             }
 #pragma unroll
             for (int st = 1; st < 4; ++st) {
-                cs = csp.template eval<D>(q + st, csd);
-                rhs_tan<MODEL, D, CSD>(P, xs, xsd, cs, csd, amp, k, kd);
+                stage(xs, xsd, slot + st, kk, kkd);
                 if (st < 3) {
                     const double c = st == 1 ? h2 : h;
 #pragma unroll
-                    for (int r = 0; r < NX; ++r) {
-                        acc[r] = acc[r] + 2.0 * k[r];
-                        xs[r] = x[r] + c * k[r];
+                    for (int r = R0; r < NX; ++r) {
+                        acc[r] = acc[r] + 2.0 * kk[r];
+                        xs[r] = x[r] + c * kk[r];
 #pragma unroll
                         for (int d = 0; d < D; ++d) {
-                            accd[r][d] = accd[r][d] + 2.0 * kd[r][d];
-                            xsd[r][d] = xd[r][d] + c * kd[r][d];
+                            accd[r][d] = accd[r][d] + 2.0 * kkd[r][d];
+                            xsd[r][d] = xd[r][d] + c * kkd[r][d];
                         }
                     }
                 }
             }
 #pragma unroll
-            for (int r = 0; r < NX; ++r) {
-                x[r] = x[r] + h6 * (acc[r] + k[r]);
+            for (int r = R0; r < NX; ++r) {
+                x[r] = x[r] + h6 * (acc[r] + kk[r]);
 #pragma unroll
-                for (int d = 0; d < D; ++d) xd[r][d] = xd[r][d] + h6 * (accd[r][d] + kd[r][d]);
+                for (int d = 0; d < D; ++d) xd[r][d] = xd[r][d] + h6 * (accd[r][d] + kkd[r][d]);
             }
-            q += 4;
         }
+    }
+    if constexpr (LIN) {
+        const int se = (j0 + msteps) * S;
+        const double a = P.cna[se];
+        x[0] = fma(a, cn0, cnb[se]);
+#pragma unroll
+        for (int d = 0; d < D; ++d) xd[0][d] = (dir0 && d == 0) ? a : 0.0;
     }
 }
 
-// Per-interval control set-up: Ding2007 amplitude factor, Hmed lambdas.  gdir(j) = global direction of
-// lane direction j (chunk * D + j); u directions start at NX.
+// Per-interval control set-up: Ding2007 amplitude factor, Hmed lambdas.  Lane direction j carries global
+// direction chunk * D + j; u directions start at NX.  Controls of the interval are read at
+// Vb[(xo + NX + i) * B].
 template <int MODEL, int D, int TMAX>
 CFX_HD void load_controls(const KParams& P, const double* Vb, int64_t B, int xo, int chunk, Amp& amp,
                           CsHmed<D, TMAX>& csh) {
@@ -290,7 +330,7 @@ __global__ void __launch_bounds__(256) k_shooting(const KParams P, const double*
     if (b >= B) return;
     const int k0 = blockIdx.y * P.kpt;
     const int k1 = min(P.N, k0 + P.kpt);
-    const int chunk = blockIdx.z;
+    const int chunk = is_int(MODEL) ? (int)blockIdx.z : 0;  // the other models carry every direction in one lane
     const double* Vb = V + b;
 
     double x[NX];
@@ -307,15 +347,11 @@ __global__ void __launch_bounds__(256) k_shooting(const KParams P, const double*
         Amp amp;
         CsHmed<D, TMAX> csh;
         load_controls<MODEL, D, TMAX>(P, Vb, B, xo, chunk, amp, csh);
-        if constexpr (is_int(MODEL)) {
-            integrate_tan<MODEL, SCHEME, D>(P, k * P.Q, P.m, x, xd, amp, csh);
-        } else {
-            integrate_tan<MODEL, SCHEME, D>(P, k * P.Q, P.m, x, xd, amp, CsTable{P.tab});
-        }
         const int xn = (k + 1) * P.nz;
-        double xnext[NX];
+        double xnext[NX];  // issued before the integration so its latency hides under it
 #pragma unroll
         for (int r = 0; r < NX; ++r) xnext[r] = Vb[(int64_t)(xn + r) * B];
+        integrate<MODEL, SCHEME, D, TMAX>(P, k, 0, P.m, x[0], chunk, x, xd, amp, csh);
         if (G != nullptr && chunk == 0) {
 #pragma unroll
             for (int r = 0; r < NX; ++r) G[(int64_t)(k * P.ngk + r) * B + b] = x[r] - xnext[r];
@@ -367,13 +403,9 @@ __global__ void __launch_bounds__(256) k_ivp(const KParams P, const double* __re
         CsHmed<0, TMAX> csh;
         // controls of interval k live at U[(k*nu + i)*B + b]; load_controls reads Vb[(xo + NX + i)*B]
         load_controls<MODEL, 0, TMAX>(P, Ub, B, k * P.nu - NX, 0, amp, csh);
+        const double cn0 = x[0];
         for (int j = 0; j < P.m; ++j) {
-            const int q0 = (k * P.m + j) * stages_of(SCHEME);
-            if constexpr (is_int(MODEL)) {
-                integrate_tan<MODEL, SCHEME, 0>(P, q0, 1, x, xd, amp, csh);
-            } else {
-                integrate_tan<MODEL, SCHEME, 0>(P, q0, 1, x, xd, amp, CsTable{P.tab});
-            }
+            integrate<MODEL, SCHEME, 0, TMAX>(P, k, j, 1, cn0, 0, x, xd, amp, csh);
 #pragma unroll
             for (int r = 0; r < NX; ++r) TR[(s * NX + r) * B + b] = x[r];
             ++s;
