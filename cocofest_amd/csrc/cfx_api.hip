@@ -4,6 +4,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -33,7 +34,7 @@ struct cfx_handle {
     std::vector<int32_t> last_idx;
     std::vector<cfx_objective> objs;
     cfx_sizes sz{};
-    int model = 0, scheme = 1, tmax = 1, stages = 1;
+    int model = 0, scheme = 1, tmax = 1, stages = 1, ni = 1;
     KParams kp{};
     int device = 0;
     hipStream_t own_stream = nullptr, stream = nullptr;
@@ -470,8 +471,15 @@ extern "C" int cfx_create(const cfx_problem* p, cfx_handle** out) {
     kp.neg_mult = -kp.mult;
     kp.mult_km = kp.mult * c.km_rest;
     {
+        // instances per thread (Ding families): 2 side by side once the batch fills the chip twice over;
+        // CFX_NI=1|2|4 overrides (tuning)
+        h->ni = (!hmed && p->batch >= (int64_t)2 * 256 * 2048) ? 2 : 1;
+        if (const char* e = std::getenv("CFX_NI")) {
+            const int v = std::atoi(e);
+            if (!hmed && (v == 1 || v == 2 || v == 4)) h->ni = v;
+        }
         // intervals per thread: as many as possible (x read once) while keeping >= 2048 workgroups in flight
-        const int64_t bx = (p->batch + kBlock - 1) / kBlock;
+        const int64_t bx = (p->batch + (int64_t)kBlock * h->ni - 1) / ((int64_t)kBlock * h->ni);
         const int64_t nch = nchunk_of(h->model, nz);
         int64_t kpt = (int64_t)N * bx * nch / 2048;
         kp.kpt = (int32_t)std::max<int64_t>(1, std::min<int64_t>(N, kpt));
@@ -572,7 +580,7 @@ extern "C" int cfx_hess_structure(const cfx_handle* h, int32_t* row, int32_t* co
 // ------------------------------------------------------------------------------------------------------
 static hipError_t launch_shooting(cfx_handle* h, bool derivs, const double* V, double* G, double* J) {
     if (is_int(h->model)) return launch_shooting_hmed(h->model, h->scheme, derivs, h->tmax, h->kp, V, G, J, h->stream);
-    return launch_shooting_ding(h->model, h->scheme, derivs, h->kp, V, G, J, h->stream);
+    return launch_shooting_ding(h->model, h->scheme, derivs, h->ni, h->kp, V, G, J, h->stream);
 }
 
 extern "C" int cfx_eval_all(cfx_handle* h, const double* v, double* g, double* jac, double* f, double* grad,

@@ -10,14 +10,14 @@ static hipError_t shooting_t(int scheme, bool derivs, const KParams& P, const do
     constexpr int D = dirs_of(MODEL);
     switch (scheme) {
         case 1:
-            return derivs ? launch_shooting_t<MODEL, 1, D, TMAX>(P, V, G, J, s)
-                          : launch_shooting_t<MODEL, 1, 0, TMAX>(P, V, G, J, s);
+            return derivs ? launch_shooting_t<MODEL, 1, D, TMAX, 1>(P, V, G, J, s)
+                          : launch_shooting_t<MODEL, 1, 0, TMAX, 1>(P, V, G, J, s);
         case 2:
-            return derivs ? launch_shooting_t<MODEL, 2, D, TMAX>(P, V, G, J, s)
-                          : launch_shooting_t<MODEL, 2, 0, TMAX>(P, V, G, J, s);
+            return derivs ? launch_shooting_t<MODEL, 2, D, TMAX, 1>(P, V, G, J, s)
+                          : launch_shooting_t<MODEL, 2, 0, TMAX, 1>(P, V, G, J, s);
         case 4:
-            return derivs ? launch_shooting_t<MODEL, 4, D, TMAX>(P, V, G, J, s)
-                          : launch_shooting_t<MODEL, 4, 0, TMAX>(P, V, G, J, s);
+            return derivs ? launch_shooting_t<MODEL, 4, D, TMAX, 1>(P, V, G, J, s)
+                          : launch_shooting_t<MODEL, 4, 0, TMAX, 1>(P, V, G, J, s);
         default:
             return hipErrorInvalidValue;
     }

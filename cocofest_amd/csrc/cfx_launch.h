@@ -20,8 +20,8 @@ inline int nchunk_of(int model, int nz) { return (nz + dirs_of(model) - 1) / dir
 // Smallest supported register-resident truncation bucket >= T (Hmed only).
 inline int tmax_bucket(int T) { return T <= 4 ? 4 : T <= 8 ? 8 : T <= 16 ? 16 : 32; }
 
-hipError_t launch_shooting_ding(int model, int scheme, bool derivs, const KParams& P, const double* V, double* G,
-                                double* J, hipStream_t s);
+hipError_t launch_shooting_ding(int model, int scheme, bool derivs, int ni, const KParams& P, const double* V,
+                                double* G, double* J, hipStream_t s);
 hipError_t launch_shooting_hmed(int model, int scheme, bool derivs, int tmax, const KParams& P, const double* V,
                                 double* G, double* J, hipStream_t s);
 hipError_t launch_ivp_ding(int model, int scheme, const KParams& P, const double* X0, const double* U, double* TR,
@@ -31,12 +31,13 @@ hipError_t launch_ivp_hmed(int model, int scheme, int tmax, const KParams& P, co
 
 constexpr int kBlock = 256;
 
-template <int MODEL, int SCHEME, int D, int TMAX>
+template <int MODEL, int SCHEME, int D, int TMAX, int NI>
 hipError_t launch_shooting_t(const KParams& P, const double* V, double* G, double* J, hipStream_t s) {
     const int nz = P.nz;
     const int nchunk = D > 0 ? (nz + D - 1) / D : 1;
-    dim3 grid((unsigned)((P.B + kBlock - 1) / kBlock), (unsigned)((P.N + P.kpt - 1) / P.kpt), (unsigned)nchunk);
-    hipLaunchKernelGGL((k_shooting<MODEL, SCHEME, D, TMAX>), grid, dim3(kBlock), 0, s, P, V, G, J);
+    const int64_t per_block = (int64_t)kBlock * NI;
+    dim3 grid((unsigned)((P.B + per_block - 1) / per_block), (unsigned)((P.N + P.kpt - 1) / P.kpt), (unsigned)nchunk);
+    hipLaunchKernelGGL((k_shooting<MODEL, SCHEME, D, TMAX, NI>), grid, dim3(kBlock), 0, s, P, V, G, J);
     return hipGetLastError();
 }
 

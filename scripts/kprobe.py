@@ -21,16 +21,26 @@ def main():
     ap.add_argument("--reps", type=int, default=50)
     ap.add_argument("--n-shooting", type=int, default=20)
     a = ap.parse_args()
+    import os
+
     ocp = bench.build_problem()
     B = a.batch
-    h = ocp.nlp(batch=B, layout="soa")
+    handles = {}
+    for ni in (1, 2, 4):
+        os.environ["CFX_NI"] = str(ni)
+        handles[ni] = ocp.nlp(batch=B, layout="soa")
+    os.environ.pop("CFX_NI")
+    h = handles[1]
     v = bench.synthetic_soa(ocp, B, 1, "cuda:0")
     g = torch.empty((h.ng, B), dtype=torch.float64, device="cuda")
     j = torch.empty((h.nnz_jac, B), dtype=torch.float64, device="cuda")
-    variants = {"g+J": dict(g=g, jac=j), "g": dict(g=g), "J": dict(jac=j)}
+    variants = {}
+    for ni, hh in handles.items():
+        variants[f"g+J ni={ni}"] = (hh, dict(g=g, jac=j))
+        variants[f"g ni={ni}"] = (hh, dict(g=g))
     res = {k: [] for k in variants}
     for _ in range(a.rounds):
-        for name, kw in variants.items():
+        for name, (h, kw) in variants.items():
             for _ in range(3):
                 h.eval_all(v, **kw)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
