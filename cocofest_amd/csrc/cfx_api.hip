@@ -473,10 +473,11 @@ extern "C" int cfx_create(const cfx_problem* p, cfx_handle** out) {
     {
         // instances per thread (Ding families): 2 side by side once the batch fills the chip twice over;
         // CFX_NI=1|2|4 overrides (tuning)
-        h->ni = (!hmed && p->batch >= (int64_t)2 * 256 * 2048) ? 2 : 1;
+        // NI adjacent instances per lane (16-byte accesses) need B % NI == 0; the launch also checks alignment
+        h->ni = (!hmed && p->batch % 2 == 0 && p->batch >= (int64_t)256 * 1024) ? 2 : 1;
         if (const char* e = std::getenv("CFX_NI")) {
             const int v = std::atoi(e);
-            if (!hmed && (v == 1 || v == 2 || v == 4)) h->ni = v;
+            if (!hmed && (v == 1 || v == 2 || v == 4) && p->batch % v == 0) h->ni = v;
         }
         // intervals per thread: as many as possible (x read once) while keeping >= 2048 workgroups in flight
         const int64_t bx = (p->batch + (int64_t)kBlock * h->ni - 1) / ((int64_t)kBlock * h->ni);
@@ -580,7 +581,10 @@ extern "C" int cfx_hess_structure(const cfx_handle* h, int32_t* row, int32_t* co
 // ------------------------------------------------------------------------------------------------------
 static hipError_t launch_shooting(cfx_handle* h, bool derivs, const double* V, double* G, double* J) {
     if (is_int(h->model)) return launch_shooting_hmed(h->model, h->scheme, derivs, h->tmax, h->kp, V, G, J, h->stream);
-    return launch_shooting_ding(h->model, h->scheme, derivs, h->ni, h->kp, V, G, J, h->stream);
+    // 16-byte lane accesses need 16-byte aligned buffers (B % NI == 0 keeps every row aligned)
+    auto aligned = [](const void* p) { return ((uintptr_t)p & 15u) == 0; };
+    const int ni = (aligned(V) && aligned(G) && aligned(J)) ? h->ni : 1;
+    return launch_shooting_ding(h->model, h->scheme, derivs, ni, h->kp, V, G, J, h->stream);
 }
 
 extern "C" int cfx_eval_all(cfx_handle* h, const double* v, double* g, double* jac, double* f, double* grad,

@@ -340,20 +340,46 @@ CFX_HD void load_controls(const KParams& P, const double* Vb, int64_t B, int xo,
 // dPhi/d(x_k, u_k) (+ the -1 on x_{k+1}).  Thread = (instance b, intervals [k0, k0+kpt), direction chunk);
 // D directions per lane (D = 0: g only).
 // ---------------------------------------------------------------------------------------------------
+// NI adjacent instances per lane: element e of instances b0 .. b0+NI-1 is NI contiguous doubles, moved as
+// NI/2 16-byte accesses per lane (1 KiB per wave instruction).  Requires B % NI == 0 and 16-byte aligned
+// buffers for NI > 1 (checked on the host).
+template <int NI>
+CFX_HD void ld_lane(const double* p, double (&o)[NI]) {
+    if constexpr (NI == 1) {
+        o[0] = p[0];
+    } else {
+#pragma unroll
+        for (int i = 0; i < NI; i += 2) {
+            const double2 t = *reinterpret_cast<const double2*>(p + i);
+            o[i] = t.x;
+            o[i + 1] = t.y;
+        }
+    }
+}
+template <int NI>
+CFX_HD void st_lane(double* p, const double (&v)[NI]) {
+    if constexpr (NI == 1) {
+        p[0] = v[0];
+    } else {
+#pragma unroll
+        for (int i = 0; i < NI; i += 2) *reinterpret_cast<double2*>(p + i) = make_double2(v[i], v[i + 1]);
+    }
+}
+template <int NI>
+CFX_HD void st_lane_const(double* p, double c) {
+    double v[NI];
+#pragma unroll
+    for (int i = 0; i < NI; ++i) v[i] = c;
+    st_lane<NI>(p, v);
+}
+
 template <int MODEL, int SCHEME, int D, int TMAX, int NI>
 __global__ void __launch_bounds__(256) k_shooting(const KParams P, const double* __restrict__ V,
                                                   double* __restrict__ G, double* __restrict__ J) {
     constexpr int NX = nx_of(MODEL);
     const int64_t B = P.B;
-    int64_t bi[NI];
-    bool ok[NI];
-#pragma unroll
-    for (int i = 0; i < NI; ++i) {
-        const int64_t b = ((int64_t)blockIdx.x * NI + i) * blockDim.x + threadIdx.x;
-        ok[i] = b < B;
-        bi[i] = ok[i] ? b : B - 1;  // out-of-range lanes recompute the last instance and store nothing
-    }
-    if (!ok[0]) return;
+    const int64_t b0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * NI;
+    if (b0 >= B) return;
     const int k0 = blockIdx.y * P.kpt;
     const int k1 = min(P.N, k0 + P.kpt);
     const int chunk = is_int(MODEL) ? (int)blockIdx.z : 0;  // the other models carry every direction in one lane
@@ -361,56 +387,64 @@ __global__ void __launch_bounds__(256) k_shooting(const KParams P, const double*
     IState<NX, D> st[NI];
     CsHmed<D, TMAX> csh[NI];
 #pragma unroll
-    for (int i = 0; i < NI; ++i)
+    for (int r = 0; r < NX; ++r) {
+        double t[NI];
+        ld_lane<NI>(V + (int64_t)(k0 * P.nz + r) * B + b0, t);
 #pragma unroll
-        for (int r = 0; r < NX; ++r) st[i].x[r] = V[(int64_t)(k0 * P.nz + r) * B + bi[i]];
+        for (int i = 0; i < NI; ++i) st[i].x[r] = t[i];
+    }
 
     for (int k = k0; k < k1; ++k) {
         const int xo = k * P.nz;
         const int xn = (k + 1) * P.nz;
-        double xnext[NI][NX];  // issued before the integration so its latency hides under it
+        double xnext[NX][NI];  // issued before the integration so its latency hides under it
+#pragma unroll
+        for (int r = 0; r < NX; ++r) ld_lane<NI>(V + (int64_t)(xn + r) * B + b0, xnext[r]);
 #pragma unroll
         for (int i = 0; i < NI; ++i) {
-#pragma unroll
-            for (int r = 0; r < NX; ++r) xnext[i][r] = V[(int64_t)(xn + r) * B + bi[i]];
 #pragma unroll
             for (int r = 0; r < NX; ++r)
 #pragma unroll
                 for (int j = 0; j < D; ++j) st[i].xd[r][j] = (chunk * D + j == r) ? 1.0 : 0.0;
             st[i].cn0 = st[i].x[0];
-            load_controls<MODEL, D, TMAX>(P, V + bi[i], B, xo, chunk, st[i].amp, csh[i]);
+            load_controls<MODEL, D, TMAX>(P, V + b0 + i, B, xo, chunk, st[i].amp, csh[i]);
         }
         integrate<MODEL, SCHEME, D, TMAX, NI>(P, k, 0, P.m, chunk, st, csh);
+        if (G != nullptr && chunk == 0) {
 #pragma unroll
-        for (int i = 0; i < NI; ++i) {
-            if (!ok[i]) continue;
-            const int64_t b = bi[i];
-            if (G != nullptr && chunk == 0) {
+            for (int r = 0; r < NX; ++r) {
+                double t[NI];
 #pragma unroll
-                for (int r = 0; r < NX; ++r) G[(int64_t)(k * P.ngk + r) * B + b] = st[i].x[r] - xnext[i][r];
+                for (int i = 0; i < NI; ++i) t[i] = st[i].x[r] - xnext[r][i];
+                st_lane<NI>(G + (int64_t)(k * P.ngk + r) * B + b0, t);
             }
-            if constexpr (D > 0) {
-                if (J != nullptr) {
-                    const int64_t jo = (int64_t)k * P.nnzk;
+        }
+        if constexpr (D > 0) {
+            if (J != nullptr) {
+                const int64_t jo = (int64_t)k * P.nnzk;
 #pragma unroll
-                    for (int r = 0; r < NX; ++r) {
+                for (int r = 0; r < NX; ++r) {
 #pragma unroll
-                        for (int j = 0; j < D; ++j) {
-                            const int gd = chunk * D + j;
-                            if (gd < P.nz) {
-                                const int pos = P.jpos[r][gd];
-                                if (pos >= 0) J[(jo + pos) * B + b] = st[i].xd[r][j];
+                    for (int j = 0; j < D; ++j) {
+                        const int gd = chunk * D + j;
+                        if (gd < P.nz) {
+                            const int pos = P.jpos[r][gd];
+                            if (pos >= 0) {
+                                double t[NI];
+#pragma unroll
+                                for (int i = 0; i < NI; ++i) t[i] = st[i].xd[r][j];
+                                st_lane<NI>(J + (jo + pos) * B + b0, t);
                             }
                         }
-                        if (chunk == 0) J[(jo + P.jneg[r]) * B + b] = -1.0;
                     }
+                    if (chunk == 0) st_lane_const<NI>(J + (jo + P.jneg[r]) * B + b0, -1.0);
                 }
             }
         }
 #pragma unroll
         for (int i = 0; i < NI; ++i)
 #pragma unroll
-            for (int r = 0; r < NX; ++r) st[i].x[r] = xnext[i][r];
+            for (int r = 0; r < NX; ++r) st[i].x[r] = xnext[r][i];
     }
 }
 

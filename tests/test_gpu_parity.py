@@ -211,3 +211,39 @@ def test_errors_are_loud():
     h = ocp.nlp(batch=2)
     with pytest.raises(CfxError):
         h.eval_h(np.zeros((2, h.nv)), np.ones(2), np.zeros((2, h.ng)))
+
+
+@pytest.mark.parametrize("name", ["ding2003", "ding2003_with_fatigue", "ding2007", "ding2007_with_fatigue"])
+def test_instances_per_lane_variants_are_identical(name, monkeypatch):
+    """NI adjacent instances per lane (16-byte accesses) must give the same bits as NI = 1, including a batch
+    that is not a multiple of the 256-thread block and a misaligned (offset) device buffer."""
+    import torch
+
+    ocp = cases.product_ocp(name, cases.TEN_PULSES, 1.0, 5, scheme="RK4", m=2)
+    pb = cases.oracle_problem(name, cases.TEN_PULSES, 1.0, 5, scheme="RK4", m=2)
+    B = 1028  # % 4 == 0, not a multiple of 256
+    v = cases.random_decision(pb, B, seed=21)
+    dv = torch.from_numpy(np.ascontiguousarray(v.T)).cuda()
+    out = {}
+    for ni in ("1", "2", "4"):
+        monkeypatch.setenv("CFX_NI", ni)
+        h = ocp.nlp(batch=B, layout="soa")
+        g = torch.empty((h.ng, B), dtype=torch.float64, device="cuda")
+        j = torch.empty((h.nnz_jac, B), dtype=torch.float64, device="cuda")
+        h.eval_all(dv, g=g, jac=j)
+        torch.cuda.synchronize()
+        out[ni] = (g.cpu().numpy(), j.cpu().numpy())
+        h.close()
+    for ni in ("2", "4"):
+        np.testing.assert_array_equal(out[ni][0], out["1"][0])
+        np.testing.assert_array_equal(out[ni][1], out["1"][1])
+    _close(out["1"][0].T, O.eval_g(pb, v), what=f"g {name}")
+    _close(out["1"][1].T, O.eval_jac_g(pb, v), what=f"J {name}")
+    # an 8-byte-offset output buffer forces the scalar path, same result
+    monkeypatch.setenv("CFX_NI", "2")
+    h = ocp.nlp(batch=B, layout="soa")
+    big = torch.empty((h.ng * B + 1,), dtype=torch.float64, device="cuda")
+    g_off = big[1:].view(h.ng, B)
+    h.eval_all(dv, g=g_off)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(g_off.cpu().numpy(), out["1"][0])
