@@ -34,7 +34,7 @@ struct cfx_handle {
     std::vector<int32_t> last_idx;
     std::vector<cfx_objective> objs;
     cfx_sizes sz{};
-    int model = 0, scheme = 1, tmax = 1, stages = 1, ni = 1;
+    int model = 0, scheme = 1, tmax = 1, stages = 1, ni = 1, ni_g = 1;
     KParams kp{};
     int device = 0;
     hipStream_t own_stream = nullptr, stream = nullptr;
@@ -474,10 +474,13 @@ extern "C" int cfx_create(const cfx_problem* p, cfx_handle** out) {
         // instances per thread (Ding families): 2 side by side once the batch fills the chip twice over;
         // CFX_NI=1|2|4 overrides (tuning)
         // NI adjacent instances per lane (16-byte accesses) need B % NI == 0; the launch also checks alignment
-        h->ni = (!hmed && p->batch % 2 == 0 && p->batch >= (int64_t)256 * 1024) ? 2 : 1;
+        // Measured on MI355X (cfg2, B = 2^20): g + J_g is store-bound and fastest at NI = 1; the g-only pass
+        // (fewer stores) gains ~7% from NI = 4.
+        h->ni = 1;
+        h->ni_g = (!hmed && p->batch % 4 == 0 && p->batch >= (int64_t)256 * 1024) ? 4 : 1;
         if (const char* e = std::getenv("CFX_NI")) {
             const int v = std::atoi(e);
-            if (!hmed && (v == 1 || v == 2 || v == 4) && p->batch % v == 0) h->ni = v;
+            if (!hmed && (v == 1 || v == 2 || v == 4) && p->batch % v == 0) h->ni = h->ni_g = v;
         }
         // intervals per thread: as many as possible (x read once) while keeping >= 2048 workgroups in flight
         const int64_t bx = (p->batch + (int64_t)kBlock * h->ni - 1) / ((int64_t)kBlock * h->ni);
@@ -583,7 +586,7 @@ static hipError_t launch_shooting(cfx_handle* h, bool derivs, const double* V, d
     if (is_int(h->model)) return launch_shooting_hmed(h->model, h->scheme, derivs, h->tmax, h->kp, V, G, J, h->stream);
     // 16-byte lane accesses need 16-byte aligned buffers (B % NI == 0 keeps every row aligned)
     auto aligned = [](const void* p) { return ((uintptr_t)p & 15u) == 0; };
-    const int ni = (aligned(V) && aligned(G) && aligned(J)) ? h->ni : 1;
+    const int ni = (aligned(V) && aligned(G) && aligned(J)) ? (derivs ? h->ni : h->ni_g) : 1;
     return launch_shooting_ding(h->model, h->scheme, derivs, ni, h->kp, V, G, J, h->stream);
 }
 

@@ -18,11 +18,26 @@ pytestmark = pytest.mark.gpu
 RTOL = 1e-11
 
 
-def _close(actual, desired, rtol=RTOL, what=""):
+def _close(actual, desired, rtol=RTOL, what="", scale=None):
+    """max |actual - desired| / scale <= rtol; scale defaults to |desired| floored at 1e-6 of its row max."""
     desired = np.asarray(desired)
-    scale = np.maximum(np.abs(desired), np.max(np.abs(desired), axis=-1, keepdims=True) * 1e-6 + 1e-300)
+    floor = np.max(np.abs(desired), axis=-1, keepdims=True) * 1e-6 + 1e-300
+    scale = np.maximum(np.abs(desired) if scale is None else scale, floor)
     err = np.max(np.abs(actual - desired) / scale) if desired.size else 0.0
     assert err <= rtol, f"{what}: max scaled error {err:.3e} > {rtol:.1e}"
+
+
+def _close_g(pb, v, actual, desired, rtol=RTOL, what=""):
+    """g is a difference (Phi(x_k, u_k) - x_{k+1}, u_k - window): scale each row by |g| + |x_{k+1}| (resp. |u_k|),
+    i.e. compare Phi itself to relative rtol."""
+    X, U, _ = pb.unpack(v)
+    parts = []
+    for k in range(pb.n_shooting):
+        parts.append(np.abs(X[:, k + 1, :]))
+        if pb.n_slide:
+            parts.append(np.abs(U[:, k, :]))
+    ref = np.concatenate(parts, axis=1)
+    _close(actual, desired, rtol=rtol, what=what, scale=np.abs(np.asarray(desired)) + ref)
 
 
 @pytest.fixture(scope="module", autouse=True)
@@ -86,7 +101,7 @@ def test_shooting_g_and_jacobian_vs_oracle(name, scheme):
     np.testing.assert_array_equal(cols, ocols)
     g = h.eval_g(v)
     jac = h.eval_jac_g(v)
-    _close(g, O.eval_g(pb, v), what=f"g {name} {scheme}")
+    _close_g(pb, v, g, O.eval_g(pb, v), what=f"g {name} {scheme}")
     _close(jac, O.eval_jac_g(pb, v), what=f"J {name} {scheme}")
     # fused call gives identical values
     g2, j2 = np.empty_like(g), np.empty_like(jac)
@@ -103,7 +118,7 @@ def test_hmed_truncation_buckets(T):
         pb = cases.oracle_problem(name, stims, 0.24, T, scheme="RK2", m=2)
         v = cases.random_decision(pb, 3, seed=T)
         h = ocp.nlp(batch=3)
-        _close(h.eval_g(v), O.eval_g(pb, v), what=f"g {name} T={T}")
+        _close_g(pb, v, h.eval_g(v), O.eval_g(pb, v), what=f"g {name} T={T}")
         _close(h.eval_jac_g(v), O.eval_jac_g(pb, v), what=f"J {name} T={T}")
 
 
@@ -149,7 +164,7 @@ def test_layouts_and_device_pointers_are_bitwise_identical():
     ha.eval_all(dva, g=dga)
     torch.cuda.synchronize()
     np.testing.assert_array_equal(dga.cpu().numpy(), ga)
-    _close(ga, O.eval_g(pb, v), what="cfg2 g")
+    _close_g(pb, v, ga, O.eval_g(pb, v), what="cfg2 g")
 
 
 def test_full_size_properties_cfg2():
@@ -172,7 +187,7 @@ def test_full_size_properties_cfg2():
     h1 = ocp.nlp(batch=len(pick), layout="aos")
     np.testing.assert_array_equal(h1.eval_g(v[pick]), dg[:, pick].cpu().numpy().T)
     np.testing.assert_array_equal(h1.eval_jac_g(v[pick]), dj[:, pick].cpu().numpy().T)
-    _close(dg[:, pick].cpu().numpy().T, O.eval_g(pb, v[pick]), what="cfg2 big-batch g")
+    _close_g(pb, v[pick], dg[:, pick].cpu().numpy().T, O.eval_g(pb, v[pick]), what="cfg2 big-batch g")
     # forward-integrated trajectory is feasible
     from cocofest_amd import IvpFes, ModelMaker, OdeSolver
 
@@ -193,7 +208,7 @@ def test_edge_sizes():
         assert pb.n_shooting == 1
         v = cases.random_decision(pb, 1, seed=2)
         h = ocp.nlp(batch=1)
-        _close(h.eval_g(v), O.eval_g(pb, v), what=f"edge g {name}")
+        _close_g(pb, v, h.eval_g(v), O.eval_g(pb, v), what=f"edge g {name}")
         _close(h.eval_jac_g(v), O.eval_jac_g(pb, v), what=f"edge J {name}")
 
 
@@ -237,7 +252,7 @@ def test_instances_per_lane_variants_are_identical(name, monkeypatch):
     for ni in ("2", "4"):
         np.testing.assert_array_equal(out[ni][0], out["1"][0])
         np.testing.assert_array_equal(out[ni][1], out["1"][1])
-    _close(out["1"][0].T, O.eval_g(pb, v), what=f"g {name}")
+    _close_g(pb, v, out["1"][0].T, O.eval_g(pb, v), what=f"g {name}")
     _close(out["1"][1].T, O.eval_jac_g(pb, v), what=f"J {name}")
     # an 8-byte-offset output buffer forces the scalar path, same result
     monkeypatch.setenv("CFX_NI", "2")
