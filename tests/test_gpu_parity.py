@@ -234,8 +234,10 @@ def test_instances_per_lane_variants_are_identical(name, monkeypatch):
     that is not a multiple of the 256-thread block and a misaligned (offset) device buffer."""
     import torch
 
-    ocp = cases.product_ocp(name, cases.TEN_PULSES, 1.0, 5, scheme="RK4", m=2)
-    pb = cases.oracle_problem(name, cases.TEN_PULSES, 1.0, 5, scheme="RK4", m=2)
+    # RK4 with h * (1/tauc) = 1: coarser steps drive the RK4 stage calcium negative on random inputs and the
+    # discretisation itself becomes ill-conditioned (1e-10-level rounding amplification in any implementation)
+    ocp = cases.product_ocp(name, cases.TEN_PULSES, 1.0, 5, scheme="RK4", m=5)
+    pb = cases.oracle_problem(name, cases.TEN_PULSES, 1.0, 5, scheme="RK4", m=5)
     B = 1028  # % 4 == 0, not a multiple of 256
     v = cases.random_decision(pb, B, seed=21)
     dv = torch.from_numpy(np.ascontiguousarray(v.T)).cuda()
