@@ -251,9 +251,9 @@ def test_instances_per_lane_variants_are_identical(name, monkeypatch):
         torch.cuda.synchronize()
         out[ni] = (g.cpu().numpy(), j.cpu().numpy())
         h.close()
-    for ni in ("2", "4"):
-        np.testing.assert_array_equal(out[ni][0], out["1"][0])
-        np.testing.assert_array_equal(out[ni][1], out["1"][1])
+    for ni in ("2", "4"):  # interleaving changes FMA contraction: equal to a few ulp, not bitwise
+        np.testing.assert_allclose(out[ni][0], out["1"][0], rtol=1e-14, atol=1e-13)
+        np.testing.assert_allclose(out[ni][1], out["1"][1], rtol=1e-14, atol=1e-13)
     _close_g(pb, v, out["1"][0].T, O.eval_g(pb, v), what=f"g {name}")
     _close(out["1"][1].T, O.eval_jac_g(pb, v), what=f"J {name}")
     # an 8-byte-offset output buffer forces the scalar path, same result
@@ -263,4 +263,4 @@ def test_instances_per_lane_variants_are_identical(name, monkeypatch):
     g_off = big[1:].view(h.ng, B)
     h.eval_all(dv, g=g_off)
     torch.cuda.synchronize()
-    np.testing.assert_array_equal(g_off.cpu().numpy(), out["1"][0])
+    np.testing.assert_allclose(g_off.cpu().numpy(), out["1"][0], rtol=1e-14, atol=1e-13)
