@@ -45,6 +45,8 @@ struct cfx_handle {
     double* d_targets = nullptr;
     int32_t* d_sl_param = nullptr;
     int32_t* d_sl_joff = nullptr;
+    HTask* d_htasks = nullptr;
+    int n_htasks = 1, hbs = 1;
     int n_obj = 0;
     std::vector<int32_t> jrow, jcol, hrow, hcol;
     DevBuf main[S_COUNT], stage[S_COUNT];
@@ -510,6 +512,19 @@ extern "C" int cfx_create(const cfx_problem* p, cfx_handle** out) {
         rest[3] = c.tau1_rest;
         rest[4] = c.km_rest;
     }
+    // Hessian tasks: blocks of bs directions, one task per block pair (I <= J); a single task when the
+    // lane's jet holds every direction
+    std::vector<HTask> htasks;
+    {
+        const int dj = hjet_of(h->model);
+        h->hbs = hsplit_of(h->model) ? dj / 2 : dj;
+        const int nb = (nz + h->hbs - 1) / h->hbs;
+        for (int I = 0; I < nb; ++I)
+            for (int J = I; J < nb; ++J) htasks.push_back(HTask{(int16_t)I, (int16_t)J});
+        h->n_htasks = (int)htasks.size();
+        if (!hsplit_of(h->model) && nb != 1)
+            return create_fail(h, CFX_EINVAL, "cfx_create: internal Hessian task layout error");
+    }
     auto upload = [&](void** dst, const void* src, size_t bytes) -> bool {
         if (bytes == 0) return true;
         if (hipMalloc(dst, bytes) != hipSuccess) return false;
@@ -521,7 +536,8 @@ extern "C" int cfx_create(const cfx_problem* p, cfx_handle** out) {
         !upload((void**)&h->d_obj, dobj.data(), dobj.size() * sizeof(DevObjective)) ||
         !upload((void**)&h->d_targets, targets.data(), targets.size() * sizeof(double)) ||
         !upload((void**)&h->d_sl_param, sl_param.data(), sl_param.size() * sizeof(int32_t)) ||
-        !upload((void**)&h->d_sl_joff, sl_joff.data(), sl_joff.size() * sizeof(int32_t)))
+        !upload((void**)&h->d_sl_joff, sl_joff.data(), sl_joff.size() * sizeof(int32_t)) ||
+        !upload((void**)&h->d_htasks, htasks.data(), htasks.size() * sizeof(HTask)))
         return create_fail(h, CFX_ENOMEM, "cfx_create: device allocation/upload failed");
     kp.tab = h->d_tab;
     kp.cna = h->d_cna;
@@ -538,7 +554,7 @@ extern "C" void cfx_destroy(cfx_handle* h) {
         if (h->main[s].p) (void)hipFree(h->main[s].p);
         if (h->stage[s].p) (void)hipFree(h->stage[s].p);
     }
-    for (void* p : {(void*)h->d_tab, (void*)h->d_rest, (void*)h->d_cna, (void*)h->d_obj, (void*)h->d_targets, (void*)h->d_sl_param,
+    for (void* p : {(void*)h->d_tab, (void*)h->d_rest, (void*)h->d_cna, (void*)h->d_htasks, (void*)h->d_obj, (void*)h->d_targets, (void*)h->d_sl_param,
                     (void*)h->d_sl_joff})
         if (p) (void)hipFree(p);
     if (h->own_stream) (void)hipStreamDestroy(h->own_stream);
@@ -644,12 +660,26 @@ extern "C" int cfx_eval_grad_f(cfx_handle* h, const double* v, double* grad, uin
 
 extern "C" int cfx_eval_h(cfx_handle* h, const double* v, const double* obj_factor, const double* lambda,
                           double* hess, uint32_t flags) {
-    (void)v;
-    (void)obj_factor;
-    (void)lambda;
-    (void)hess;
-    (void)flags;
-    return h ? fail(h, CFX_EUNSUPPORTED, "cfx_eval_h: not built yet") : CFX_EINVAL;
+    if (!h || !v || !obj_factor || !lambda || !hess) return h ? fail(h, CFX_EINVAL, "cfx_eval_h: NULL argument") : CFX_EINVAL;
+    CFX_HIP(h, hipSetDevice(h->device));
+    int rc = CFX_OK;
+    const int64_t B = h->prob.batch;
+    const double* V = stage_in(h, S_V, v, h->sz.nv, flags, &rc);
+    if (!V) return rc;
+    const double* OF = stage_in(h, S_A1, obj_factor, 1, flags, &rc);
+    if (!OF) return rc;
+    const double* LAM = stage_in(h, S_A2, lambda, h->sz.ng, flags, &rc);
+    if (!LAM) return rc;
+    double* H = stage_out(h, S_OUT, hess, h->sz.nnz_hess, flags, &rc);
+    if (!H) return rc;
+    CFX_HIP(h, launch_hessian(h->model, h->scheme, h->tmax, h->kp, h->d_htasks, h->n_htasks, h->hbs, V, LAM, H,
+                              h->stream));
+    if (h->n_obj)
+        hipLaunchKernelGGL(k_objective_hess, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, h->stream, h->kp,
+                           h->n_obj, h->d_obj, OF, H);
+    CFX_HIP(h, hipGetLastError());
+    if ((rc = finish_out(h, S_OUT, H, hess, h->sz.nnz_hess, flags)) != CFX_OK) return rc;
+    return sync_if_host(h, flags);
 }
 
 extern "C" int cfx_integrate(cfx_handle* h, const double* x0, const double* u, double* traj, uint32_t flags) {

@@ -4,6 +4,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include "cfx_hessian.h"
 #include "cfx_kernels.h"
 
 namespace cfx {
@@ -30,6 +31,24 @@ hipError_t launch_ivp_hmed(int model, int scheme, int tmax, const KParams& P, co
                            double* TR, hipStream_t s);
 
 constexpr int kBlock = 256;
+
+// Hessian jets: slots per lane (DJ), and whether the directions are split in block-pair tasks of DJ/2 each.
+// Chosen so the RK4 stage arrays of Jet<DJ> stay in VGPRs (5 states x 4 arrays x Jet<2> = 240 registers).
+constexpr int hjet_of(int model) {
+    return model == M_D03 ? 2 : model == M_D07 ? 3 : model == M_H18 ? 4 : 2;
+}
+constexpr bool hsplit_of(int model) { return model != M_D03 && model != M_D07; }
+
+hipError_t launch_hessian(int model, int scheme, int tmax, const KParams& P, const HTask* tasks, int ntasks, int bs,
+                          const double* V, const double* LAM, double* H, hipStream_t s);
+
+template <int MODEL, int SCHEME, int DJ, int TMAX>
+hipError_t launch_hessian_t(const KParams& P, const HTask* tasks, int ntasks, int bs, const double* V,
+                            const double* LAM, double* H, hipStream_t s) {
+    dim3 grid((unsigned)((P.B + kBlock - 1) / kBlock), (unsigned)P.N, (unsigned)ntasks);
+    hipLaunchKernelGGL((k_hessian<MODEL, SCHEME, DJ, TMAX>), grid, dim3(kBlock), 0, s, P, tasks, bs, V, LAM, H);
+    return hipGetLastError();
+}
 
 template <int MODEL, int SCHEME, int D, int TMAX, int NI>
 hipError_t launch_shooting_t(const KParams& P, const double* V, double* G, double* J, hipStream_t s) {

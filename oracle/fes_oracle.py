@@ -501,10 +501,43 @@ def eval_grad_f(pb: Problem, v):
     return g
 
 
-def lagrangian_hessian_blocks(pb: Problem, v, obj_factor, lam, delta=1e-6):
+def lagrangian_hessian_blocks(pb: Problem, v, obj_factor, lam, delta=1e-3):
     """Hessian of obj_factor*f + lam^T g restricted to the build's structure:
     per interval k the dense (x_k,u_k) block (B, N, nz, nz) and the x_N diagonal (B, nx).
-    The continuity part is a central difference of complex-step gradients of lam_k^T Phi_k."""
+    The continuity part is a central difference of complex-step gradients of lam_k^T Phi_k (the gradients
+    are exact to rounding), Richardson-extrapolated over steps delta and delta/2: O(delta^4) truncation."""
+    H1, HN = _lagrangian_hessian_fd(pb, v, obj_factor, lam, delta)
+    H2, _ = _lagrangian_hessian_fd(pb, v, obj_factor, lam, delta / 2)
+    return (4 * H2 - H1) / 3, HN
+
+
+def hess_structure(pb: Problem):
+    """(row, col) of the Hessian values in the build's packed order (row >= col)."""
+    nz = pb.nx + pb.nu
+    rows, cols = [], []
+    for k in range(pb.n_shooting):
+        for i in range(nz):
+            for j in range(i + 1):
+                rows.append(pb.x_off(k) + i)
+                cols.append(pb.x_off(k) + j)
+    for r in range(pb.nx):
+        rows.append(pb.x_off(pb.n_shooting) + r)
+        cols.append(pb.x_off(pb.n_shooting) + r)
+    return np.array(rows), np.array(cols)
+
+
+def hessian_values(pb: Problem, v, obj_factor, lam):
+    """Lagrangian Hessian in the build's packed order: per interval the lower triangle (i, j <= i) of the
+    (x_k, u_k) block row-major, then the x_N diagonal; shape (B, N*nz(nz+1)/2 + nx)."""
+    H, HN = lagrangian_hessian_blocks(pb, v, obj_factor, lam)
+    nz = pb.nx + pb.nu
+    il, jl = np.tril_indices(nz)
+    order = np.argsort(il * (il + 1) // 2 + jl)
+    blocks = H[:, :, il[order], jl[order]].reshape(v.shape[0], -1)
+    return np.concatenate([blocks, HN], axis=1)
+
+
+def _lagrangian_hessian_fd(pb: Problem, v, obj_factor, lam, delta):
     B = v.shape[0]
     nx, nu, nz, N = pb.nx, pb.nu, pb.nx + pb.nu, pb.n_shooting
     ng_k = nx + pb.n_slide
@@ -526,6 +559,7 @@ def lagrangian_hessian_blocks(pb: Problem, v, obj_factor, lam, delta=1e-6):
             vm[:, off] -= step[:, kk]
         H[:, :, :, j] = (grad_lphi(vp) - grad_lphi(vm)) / (2 * step[:, :, None])
     H = 0.5 * (H + H.transpose(0, 1, 3, 2))
+    obj_factor = np.broadcast_to(np.asarray(obj_factor, dtype=float), (B,))
     HN = np.zeros((B, nx))
     for w, _, _, off in _obj_terms(pb, v):
         k, r = divmod(off, nx + nu)

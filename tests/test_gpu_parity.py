@@ -225,7 +225,7 @@ def test_errors_are_loud():
                     stim_rows=np.zeros(3), batch=1)
     h = ocp.nlp(batch=2)
     with pytest.raises(CfxError):
-        h.eval_h(np.zeros((2, h.nv)), np.ones(2), np.zeros((2, h.ng)))
+        h.eval_h(np.zeros((2, h.nv)), None, np.zeros((2, h.ng)))
 
 
 @pytest.mark.parametrize("name", ["ding2003", "ding2003_with_fatigue", "ding2007", "ding2007_with_fatigue"])
@@ -264,3 +264,29 @@ def test_instances_per_lane_variants_are_identical(name, monkeypatch):
     h.eval_all(dv, g=g_off)
     torch.cuda.synchronize()
     np.testing.assert_allclose(g_off.cpu().numpy(), out["1"][0], rtol=1e-14, atol=1e-13)
+
+
+@pytest.mark.parametrize("scheme", ["RK1", "RK2", "RK4"])
+@pytest.mark.parametrize("name", O.MODEL_NAMES)
+def test_lagrangian_hessian_vs_oracle(name, scheme):
+    """cfx_eval_h vs central differences of complex-step gradients (Richardson, ~1e-10 accurate)."""
+    t = np.linspace(0, 1, 30)
+    obj = {"force_tracking": [t, 60 * np.sin(np.pi * t) ** 2], "end_node_tracking": 50}
+    stims = [0.0, 0.02, 0.04, 0.06]
+    ocp = cases.product_ocp(name, stims, 0.08, 3, scheme=scheme, m=2, objective=obj)
+    pb = cases.oracle_problem(name, stims, 0.08, 3, scheme=scheme, m=2, objective=obj)
+    B = 3
+    v = cases.random_decision(pb, B, seed=4)
+    rng = np.random.default_rng(5)
+    lam = rng.normal(size=(B, pb.ng))
+    of = rng.uniform(0.5, 2.0, B)
+    h = ocp.nlp(batch=B)
+    r, c = h.hess_structure()
+    orr, occ = O.hess_structure(pb)
+    np.testing.assert_array_equal(r, orr)
+    np.testing.assert_array_equal(c, occ)
+    got = h.eval_h(v, of, lam)
+    ref = O.hessian_values(pb, v, of, lam)
+    scale = np.maximum(np.abs(ref), 1e-4 * np.max(np.abs(ref), axis=1, keepdims=True))
+    err = np.max(np.abs(got - ref) / scale)
+    assert err < 1e-7, f"H {name} {scheme}: {err:.3e}"
