@@ -254,8 +254,9 @@ def test_instances_per_lane_variants_are_identical(name, monkeypatch):
     for ni in ("2", "4"):  # interleaving changes FMA contraction: equal to a few ulp, not bitwise
         np.testing.assert_allclose(out[ni][0], out["1"][0], rtol=1e-14, atol=1e-13)
         np.testing.assert_allclose(out[ni][1], out["1"][1], rtol=1e-14, atol=1e-13)
-    _close_g(pb, v, out["1"][0].T, O.eval_g(pb, v), what=f"g {name}")
-    _close(out["1"][1].T, O.eval_jac_g(pb, v), what=f"J {name}")
+    # 50 RK4 stages per interval: a little more rounding accumulation than the short cases above
+    _close_g(pb, v, out["1"][0].T, O.eval_g(pb, v), rtol=1e-10, what=f"g {name}")
+    _close(out["1"][1].T, O.eval_jac_g(pb, v), rtol=1e-10, what=f"J {name}")
     # an 8-byte-offset output buffer forces the scalar path, same result
     monkeypatch.setenv("CFX_NI", "2")
     h = ocp.nlp(batch=B, layout="soa")
