@@ -552,7 +552,7 @@ def _lagrangian_hessian_fd(pb: Problem, v, obj_factor, lam, delta):
     for j in range(nz):
         vp, vm = v.copy(), v.copy()
         offs = [(pb.x_off(k) + j) if j < nx else (pb.u_off(k) + j - nx) for k in range(N)]
-        scale = np.maximum(1.0, np.abs(v[:, offs]))
+        scale = np.maximum(1e-4, np.abs(v[:, offs]))  # relative steps (pulse widths are ~1e-4 s)
         step = delta * scale  # (B, N)
         for kk, off in enumerate(offs):
             vp[:, off] += step[:, kk]
