@@ -1,0 +1,49 @@
+"""A CPU stand-in for a libcfx handle, backed by the oracle, used to test host-side drivers (the IPM) on the
+CPU.  Test infrastructure only — it is never used by the product."""
+
+import numpy as np
+
+from oracle import fes_oracle as O
+
+
+class OracleHandle:
+    def __init__(self, pb: O.Problem, batch: int):
+        self.pb, self.batch = pb, batch
+        self.nv, self.ng = pb.nv, pb.ng
+        r, c = O.jac_structure(pb)
+        self._jr, self._jc = r.astype(np.int32), c.astype(np.int32)
+        hr, hc = O.hess_structure(pb)
+        self._hr, self._hc = hr.astype(np.int32), hc.astype(np.int32)
+        self.nnz_jac, self.nnz_hess = r.size, hr.size
+
+    def jac_structure(self):
+        return self._jr, self._jc
+
+    def hess_structure(self):
+        return self._hr, self._hc
+
+    @staticmethod
+    def _np(t):
+        return t.detach().cpu().numpy()
+
+    def eval_all(self, v, g=None, jac=None, f=None, grad=None):
+        import torch
+
+        vv = self._np(v)
+        if g is not None:
+            g.copy_(torch.from_numpy(O.eval_g(self.pb, vv)))
+        if jac is not None:
+            jac.copy_(torch.from_numpy(O.eval_jac_g(self.pb, vv)))
+        if f is not None:
+            f.copy_(torch.from_numpy(O.eval_f(self.pb, vv)))
+        if grad is not None:
+            grad.copy_(torch.from_numpy(O.eval_grad_f(self.pb, vv)))
+
+    def eval_h(self, v, of, lam, hess):
+        import torch
+
+        hess.copy_(torch.from_numpy(O.hessian_values(self.pb, self._np(v), self._np(of), self._np(lam))))
+        return hess
+
+    def close(self):
+        pass
