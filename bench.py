@@ -40,6 +40,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--batch", type=int, default=1 << 20, help="instances per GPU")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline sample budget (0: skip)")
+    ap.add_argument("--no-solve", action="store_true", help="skip the wall-clock-to-convergence section")
     return ap.parse_args()
 
 
@@ -96,6 +97,41 @@ def cpu_baseline(ocp, budget_s):
     return {"value": done / el, "unit": "instance-evals/s", "cores": threads, "kind": "port",
             "sample": f"{done} instances of cfg2 (g + J_g, as-written calcium sum: 2T-1 exp per RK stage), "
                       f"oracle/c/fes_oracle.c, OpenMP {threads} threads, {el:.1f} s"}
+
+
+def convergence(device):
+    """Second half of the BASELINE metric: wall-clock to an Ipopt-equivalent KKT point (tol 1e-6) of the batched
+    interior-point driver over libcfx (cocofest_amd/solver.py), single instance and multi-start batch."""
+    from cocofest_amd import ModelMaker, OcpFes, OdeSolver
+    from cocofest_amd.solver import BatchedIpm, IpmOptions
+
+    out = {}
+    # cfg 3: Ding2007 pulse width, 30 pulses, N = 100, force tracking (reference force curve), RK1 x 10
+    ft = json.loads((ROOT / "tests" / "golden" / "ref_formulas.json").read_text())["misc"]["force_tracking"]
+    model = ModelMaker.create_model("ding2007", stim_time=[float(v) for v in np.round(np.linspace(0, 1, 31)[:-1], 2)],
+                                    sum_stim_truncation=10)
+    ocp3 = OcpFes.prepare_ocp(model=model, final_time=1, pulse_width={"min": model.pd0, "max": 0.0006},
+                              objective={"force_tracking": [np.array(ft["time"]), np.array(ft["force"])]},
+                              ode_solver=OdeSolver.RK1(n_integration_steps=10))
+    cases = {"cfg3_single": (ocp3, 1), "cfg3_multistart_256": (ocp3, 256), "cfg2_single": (build_problem(), 1)}
+    for name, (ocp, B) in cases.items():
+        rng = np.random.default_rng(0)
+        v0 = np.tile(ocp.initial_guess_vector(), (B, 1))
+        if B > 1:
+            lb, ub = ocp.bounds_vector()
+            free = lb != ub
+            v0[:, free] = np.clip(v0[:, free] + rng.uniform(0, 1, (B, free.sum())) * np.minimum(ub[free] - lb[free], 10),
+                                  lb[free], ub[free])
+        ipm = BatchedIpm(ocp, batch=B, device=device, options=IpmOptions(tol=1e-6, max_iter=300))
+        ipm.solve(v0[:, :] if B > 1 else None)  # warm-up (kernel loading, allocator)
+        ipm.calls = {k: 0 for k in ipm.calls}
+        res = ipm.solve(v0 if B > 1 else None)
+        ipm.close()
+        out[name] = {"batch": B, "wall_s": res.wall_time, "converged": int(res.converged.sum()),
+                     "iterations_max": int(res.iterations.max()), "iterations_median": float(np.median(res.iterations)),
+                     "solves_per_s": float(res.converged.sum() / res.wall_time), "callbacks": res.n_callbacks,
+                     "nv": ipm.n, "ng": ipm.m}
+    return out
 
 
 def main():
@@ -155,6 +191,7 @@ def main():
     out = None
     if rank == 0:
         cpu = cpu_baseline(ocp, args.cpu_seconds) if (world == 1 and args.cpu_seconds > 0) else None
+        conv = convergence(local) if (world == 1 and not args.no_solve) else None
         out = {
             "metric": METRIC,
             "value": value,
@@ -188,6 +225,7 @@ def main():
                 "kernel_ms": kern_ms,
             },
             "cpu_baseline": cpu,
+            "convergence": conv,
         }
     h.close()
     if dist:
