@@ -92,6 +92,8 @@ SIGNATURES = {
     "cfx_eval_h": (C.c_int, [_P, _P, _P, _P, _P, C.c_uint32]),
     "cfx_eval_all": (C.c_int, [_P, _P, _P, _P, _P, _P, C.c_uint32]),
     "cfx_integrate": (C.c_int, [_P, _P, _P, _P, C.c_uint32]),
+    "cfx_band_lu": (C.c_int, [C.c_int64, C.c_int32, C.c_int32, C.c_int64, _P, _P, _P, C.c_int32, _P, _P]),
+    "cfx_band_lu_solve": (C.c_int, [C.c_int64, C.c_int32, C.c_int32, C.c_int64, _P, _P, C.c_int32, _P, _P]),
 }
 
 _lib = None
@@ -130,6 +132,50 @@ def _ptr(a):
     if isinstance(a, np.ndarray):
         return a.ctypes.data
     return a.data_ptr()
+
+
+def _band_check(ab, ipiv, rhs, kl, ku):
+    import torch
+
+    if not (ab.is_cuda and ab.dtype == torch.float64 and ab.is_contiguous() and ab.dim() == 3):
+        raise CfxError(EINVAL, "band: ab must be a contiguous (B, n, 2kl+ku+1) float64 device tensor")
+    B, n, ldab = ab.shape
+    if ldab != 2 * kl + ku + 1:
+        raise CfxError(EINVAL, f"band: ab.shape[2] = {ldab} != 2*kl+ku+1 = {2 * kl + ku + 1}")
+    if not (ipiv.is_cuda and ipiv.dtype == torch.int32 and ipiv.is_contiguous() and tuple(ipiv.shape) == (B, n)):
+        raise CfxError(EINVAL, "band: ipiv must be a contiguous (B, n) int32 device tensor")
+    if rhs is not None and not (rhs.is_cuda and rhs.dtype == torch.float64 and rhs.is_contiguous()
+                                and rhs.shape[0] == B and rhs.shape[-1] == n and rhs.dim() in (2, 3)):
+        raise CfxError(EINVAL, "band: rhs must be a contiguous (B, n) or (B, nrhs, n) float64 device tensor")
+    nrhs = 0 if rhs is None else (1 if rhs.dim() == 2 else rhs.shape[1])
+    return B, n, nrhs
+
+
+def band_lu(ab, ipiv, info, kl: int, ku: int, rhs=None):
+    """Factor B banded systems in place (cfx_band_lu) on torch's current stream and, with ``rhs``, solve in
+    place.  ab: (B, n, 2kl+ku+1) float64 LAPACK band storage per instance, ipiv: (B, n) int32, info: (B,) int32."""
+    import torch
+
+    lib = load_library()
+    B, n, nrhs = _band_check(ab, ipiv, rhs, kl, ku)
+    if not (info.is_cuda and info.dtype == torch.int32 and info.numel() == B):
+        raise CfxError(EINVAL, "band: info must be a (B,) int32 device tensor")
+    rc = lib.cfx_band_lu(n, kl, ku, B, _ptr(ab), _ptr(ipiv), _ptr(info), nrhs, _ptr(rhs),
+                         torch.cuda.current_stream().cuda_stream)
+    if rc != OK:
+        raise CfxError(rc, lib.cfx_last_error(None).decode())
+
+
+def band_lu_solve(ab, ipiv, kl: int, ku: int, rhs):
+    """Solve in place with factors from band_lu (cfx_band_lu_solve)."""
+    import torch
+
+    lib = load_library()
+    B, n, nrhs = _band_check(ab, ipiv, rhs, kl, ku)
+    rc = lib.cfx_band_lu_solve(n, kl, ku, B, _ptr(ab), _ptr(ipiv), nrhs, _ptr(rhs),
+                               torch.cuda.current_stream().cuda_stream)
+    if rc != OK:
+        raise CfxError(rc, lib.cfx_last_error(None).decode())
 
 
 class Handle:

@@ -15,9 +15,10 @@
 
 using namespace cfx;
 
-namespace {
-
+// last failure of a handle-free call (cfx_create, cfx_band_lu*) on this thread; cfx_last_error(NULL)
 thread_local std::string g_create_error;
+
+namespace {
 
 enum Slot { S_V = 0, S_A1, S_A2, S_G, S_J, S_F, S_GRAD, S_OUT, S_COUNT };
 

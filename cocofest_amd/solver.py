@@ -2,15 +2,17 @@
 `ocp.solve(Solver.IPOPT(...))`, SURVEY.md section 3 stack B).
 
 All B instances of one transcribed problem iterate in lockstep on the GPU: the callbacks (g, J_g, f, grad f,
-Lagrangian Hessian) come from libcfx in one launch each for the whole batch, the Newton/KKT systems are
-assembled densely per instance and solved with batched FP64 LU (torch.linalg on ROCm), and every scalar
-decision (step length, barrier update, convergence) is taken per instance with masks.  Dense KKT is the
-right shape here: the transcribed FES problems have 40-600 free variables per instance.
+Lagrangian Hessian) come from libcfx in one launch each for the whole batch, everything else is kept in the
+callbacks' sparse (triplet) form, and the Newton/KKT system of every instance is assembled directly in
+band storage and factored by libcfx's batched band LU (cfx_band_lu: one wave per instance, band in LDS).
+The band comes from ordering the KKT unknowns stage by stage — each constraint row sits between the
+variables it couples (x_k, u_k | g_k | x_{k+1}) — which makes the half-bandwidth a few times nx + nu
+instead of n.  This plays the part of the sparse LDL^T (MUMPS) Ipopt factors the same matrix with.
 
-Algorithm (Ipopt's, simplified — monotone Fiacco-McCormick barrier, l1-merit backtracking instead of the
-filter, curvature-based inertia correction): minimise f(v) - mu sum ln(v - lb) - mu sum ln(ub - v) s.t.
-g(v) = 0; fixed variables (lb == ub, e.g. the initial state) are removed; default tol 1e-6 on the scaled
-KKT error as Ipopt's `tol`.
+Algorithm (Ipopt's, simplified — monotone Fiacco-McCormick barrier, filter line search with one
+second-order correction, curvature-based inertia correction, gradient-based problem scaling): minimise
+f(v) - mu sum ln(v - lb) - mu sum ln(ub - v) s.t. g(v) = 0; fixed variables (lb == ub, e.g. the initial
+state) are removed; default tol 1e-6 on the scaled KKT error as Ipopt's `tol`.
 """
 
 from __future__ import annotations
@@ -35,6 +37,7 @@ class IpmOptions:
     armijo: float = 1e-4
     max_backtrack: int = 30
     delta_c: float = 1e-9
+    curv_min: float = 1e-8  # inertia-free test: dx^T (W + Sigma + dw) dx >= curv_min |dx|^2 (scaled space)
     verbose: bool = False
 
 
@@ -54,9 +57,10 @@ class BatchedIpm:
     """Interior-point solver for B instances of one FesOcp on one GPU."""
 
     def __init__(self, ocp, batch: int = 1, device: int = 0, options: IpmOptions | None = None, handle=None,
-                 torch_device=None):
-        """``handle`` / ``torch_device`` let tests drive the same algorithm with another evaluator on the CPU;
-        the product path always opens a libcfx handle on GPU ``device``."""
+                 torch_device=None, band=None):
+        """``handle`` / ``torch_device`` / ``band`` let tests drive the same algorithm with another evaluator and
+        linear solver on the CPU; the product path always opens a libcfx handle and uses libcfx's band LU on
+        GPU ``device``."""
         import torch
 
         self.torch = torch
@@ -84,34 +88,101 @@ class BatchedIpm:
         # gradient-based function scaling (Ipopt nlp_scaling_method): set at the starting point
         self.sf = torch.ones((batch,), dtype=torch.float64, device=self.dev)
         self.sg = torch.ones((batch, h.ng), dtype=torch.float64, device=self.dev)
-        jr, jc = h.jac_structure()
-        hr, hc = h.hess_structure()
-        self.jr, self.jc = torch.as_tensor(jr, device=self.dev).long(), torch.as_tensor(jc, device=self.dev).long()
-        self.hr, self.hc = torch.as_tensor(hr, device=self.dev).long(), torch.as_tensor(hc, device=self.dev).long()
-        self.calls = {"eval_all": 0, "eval_h": 0, "eval_g_f": 0}
+        self._build_kkt_maps(*h.jac_structure(), *h.hess_structure())
+        self.band = band if band is not None else GpuBandSolver()
+        self.calls = {"eval_all": 0, "eval_h": 0, "eval_g_f": 0, "kkt_factor": 0}
+
+    def _build_kkt_maps(self, jr, jc, hr, hc):
+        """Triplet maps of J_g and the Hessian restricted to the free variables, the stage-wise ordering of the
+        KKT unknowns (free variables, then the multipliers of g) and the band-storage position of every
+        KKT entry."""
+        torch = self.torch
+        nf, m = len(self.free), self.m
+        posF = np.full(self.n, -1, dtype=np.int64)
+        posF[self.free] = np.arange(nf)
+        jr, jc, hr, hc = (np.asarray(a, dtype=np.int64) for a in (jr, jc, hr, hc))
+        jsel = np.where(posF[jc] >= 0)[0]
+        hsel = np.where((posF[hr] >= 0) & (posF[hc] >= 0))[0]
+        jrF, jcF = jr[jsel], posF[jc[jsel]]
+        hrF, hcF = posF[hr[hsel]], posF[hc[hsel]]
+        # unknown u: variable j -> key j; constraint row i -> midpoint of the free columns it couples
+        cmin = np.full(m, np.inf)
+        cmax = np.full(m, -np.inf)
+        np.minimum.at(cmin, jrF, jcF)
+        np.maximum.at(cmax, jrF, jcF)
+        ckey = np.where(np.isfinite(cmin), 0.5 * (cmin + cmax) + 0.25, nf)
+        key = np.concatenate([np.arange(nf, dtype=np.float64), ckey])
+        order = np.argsort(key, kind="stable")
+        pos = np.empty(nf + m, dtype=np.int64)
+        pos[order] = np.arange(nf + m)
+        # KKT entries (row, col) in band order: H (both triangles), J, J^T, the two diagonals
+        off = hrF != hcF
+        rows = np.concatenate([pos[hrF], pos[hcF[off]], pos[nf + jrF], pos[jcF], pos[:nf], pos[nf:]])
+        cols = np.concatenate([pos[hcF], pos[hrF[off]], pos[jcF], pos[nf + jrF], pos[:nf], pos[nf:]])
+        kl = int(max(0, (rows - cols).max()))
+        ku = int(max(0, (cols - rows).max()))
+        ldab = 2 * kl + ku + 1
+        flat = cols * ldab + kl + ku + rows - cols
+        nh, nho, nj = len(hsel), int(off.sum()), len(jsel)
+        sl = np.cumsum([0, nh, nho, nj, nj, nf, m])
+        L = lambda a: torch.as_tensor(a, device=self.dev, dtype=torch.long)  # noqa: E731
+        self.nK, self.kl, self.ku, self.ldab = nf + m, kl, ku, ldab
+        self.jselT, self.jrF, self.jcF = L(jsel), L(jrF), L(jcF)
+        self.hselT, self.hrF, self.hcF, self.hoff = L(hsel), L(hrF), L(hcF), torch.as_tensor(off, device=self.dev)
+        self.posT = L(pos)
+        self.idx_h, self.idx_ht = L(flat[sl[0]:sl[1]]), L(flat[sl[1]:sl[2]])
+        self.idx_j, self.idx_jt = L(flat[sl[2]:sl[3]]), L(flat[sl[3]:sl[4]])
+        self.idx_dx, self.idx_dy = L(flat[sl[4]:sl[5]]), L(flat[sl[5]:sl[6]])
 
     # ---- callbacks (device, AoS); _scaled_* return the scaled problem in x~ ---------------------------------
     def _scaled_all(self, v):
+        """g, J_g values over the free columns (triplets jrF, jcF), f, grad f of the scaled problem."""
         g, jac, f, grad = self._eval_all(v)
         gF = grad[:, self.freeT] * self.d * self.sf[:, None]
-        JF = self._dense_jac(jac) * self.d[None, None, :] * self.sg[:, :, None]
-        return g * self.sg, JF, f * self.sf, gF
+        jv = jac[:, self.jselT] * self.d[self.jcF] * self.sg[:, self.jrF]
+        return g * self.sg, jv, f * self.sf, gF
 
     def _scaled_gf(self, v):
         g, f = self._eval_gf(v)
         return g * self.sg, f * self.sf
 
     def _scaled_hess(self, v, y):
+        """Lagrangian Hessian values over the free variables (triplets hrF >= hcF) of the scaled problem."""
         hv = self._eval_h(v, y * self.sg, self.sf)
-        return self._dense_hess(hv) * self.d[None, :, None] * self.d[None, None, :]
+        return hv[:, self.hselT] * self.d[self.hrF] * self.d[self.hcF]
+
+    def _jt_mul(self, jv, y):
+        """J^T y over the free variables."""
+        out = self.torch.zeros((self.B, len(self.free)), dtype=self.torch.float64, device=self.dev)
+        return out.index_add_(1, self.jcF, jv * y[:, self.jrF])
+
+    def _quad_w(self, hv, dx):
+        """dx^T W dx from the lower-triangle triplets."""
+        t = hv * dx[:, self.hrF] * dx[:, self.hcF]
+        return (t * (1.0 + self.hoff.to(t.dtype))).sum(1)
 
     def _set_function_scaling(self, v):
+        torch = self.torch
         g, jac, f, grad = self._eval_all(v)
         gF = grad[:, self.freeT] * self.d
-        JF = self._dense_jac(jac) * self.d[None, None, :]
-        torch = self.torch
+        ja = (jac[:, self.jselT] * self.d[self.jcF]).abs()
+        rmax = torch.zeros((self.B, self.m), dtype=torch.float64, device=self.dev)
+        rmax.scatter_reduce_(1, self.jrF.expand(self.B, -1), ja, reduce="amax")
         self.sf = torch.clamp(100.0 / torch.clamp(gF.abs().amax(1), min=1e-300), max=1.0)
-        self.sg = torch.clamp(100.0 / torch.clamp(JF.abs().amax(2), min=1e-300), max=1.0)
+        self.sg = torch.clamp(100.0 / torch.clamp(rmax, min=1e-300), max=1.0)
+
+    def _kkt_band(self, hv, diag_x, jv):
+        """Band storage (B, nK, ldab) of [[W + diag_x, J^T], [J, -delta_c I]] in the stage-wise order."""
+        torch = self.torch
+        ab = torch.zeros((self.B, self.nK * self.ldab), dtype=torch.float64, device=self.dev)
+        ab.index_add_(1, self.idx_h, hv)
+        ab.index_add_(1, self.idx_ht, hv[:, self.hoff])
+        ab.index_add_(1, self.idx_j, jv)
+        ab.index_add_(1, self.idx_jt, jv)
+        ab.index_add_(1, self.idx_dx, diag_x)
+        ab[:, self.idx_dy] -= self.opt.delta_c
+        self.calls["kkt_factor"] += 1
+        return ab.view(self.B, self.nK, self.ldab)
 
     def _eval_all(self, v):
         torch = self.torch
@@ -138,22 +209,6 @@ class BatchedIpm:
         self.h.eval_h(v, of.contiguous(), y.contiguous(), hv)
         self.calls["eval_h"] += 1
         return hv
-
-    # ---- dense assembly ---------------------------------------------------------------------------------
-    def _dense_jac(self, jac):
-        J = self.torch.zeros((self.B, self.m, self.n), dtype=self.torch.float64, device=self.dev)
-        J[:, self.jr, self.jc] = jac
-        return J[:, :, self.freeT]
-
-    def _dense_hess(self, hv):
-        torch = self.torch
-        H = torch.zeros((self.B, self.n, self.n), dtype=torch.float64, device=self.dev)
-        H.index_put_((torch.arange(self.B, device=self.dev)[:, None], self.hr[None, :], self.hc[None, :]), hv,
-                     accumulate=True)
-        off = self.hr != self.hc
-        H.index_put_((torch.arange(self.B, device=self.dev)[:, None], self.hc[off][None, :], self.hr[off][None, :]),
-                     hv[:, off], accumulate=True)
-        return H[:, self.freeT][:, :, self.freeT]
 
     # ---- main loop --------------------------------------------------------------------------------------
     def solve(self, v0=None):
@@ -183,27 +238,32 @@ class BatchedIpm:
         zl = torch.where(hasL, mu[:, None] / sl, torch.zeros_like(x))
         zu = torch.where(hasU, mu[:, None] / su, torch.zeros_like(x))
         y = torch.zeros((B, m), dtype=torch.float64, device=self.dev)
+        reinit_y = torch.ones((B,), dtype=torch.bool, device=self.dev) if m else torch.zeros((B,), dtype=torch.bool,
+                                                                                          device=self.dev)
         delta_w_last = torch.zeros((B,), dtype=torch.float64, device=self.dev)
         done = torch.zeros((B,), dtype=torch.bool, device=self.dev)
         iters = torch.zeros((B,), dtype=torch.int64, device=self.dev)
         err0 = torch.full((B,), np.inf, dtype=torch.float64, device=self.dev)
-        I_n = torch.eye(nf, dtype=torch.float64, device=self.dev)
         filt = torch.full((B, 64, 2), np.inf, dtype=torch.float64, device=self.dev)  # (theta, phi) pairs
         filt[:, :, 1] = -np.inf
         fpos = torch.zeros((B,), dtype=torch.int64, device=self.dev)
 
+        self._v_template = v
+
         def full(xf):  # scaled free variables -> full decision vector
-            vv = v.clone()
-            vv[:, self.freeT] = xf * self.d
-            return vv
+            return self._full(xf)
 
         for it in range(opt.max_iter):
             vfull = full(x)
-            g, JF, f, gF = self._scaled_all(vfull)
+            g, jv, f, gF = self._scaled_all(vfull)
             sl = torch.where(hasL, x - lbF, torch.ones_like(x))
             su = torch.where(hasU, ubF - x, torch.ones_like(x))
+            if bool(reinit_y.any()):  # least-squares multipliers (Ipopt's constr_mult_init), start and restoration
+                y = torch.where(reinit_y[:, None], self._ls_multipliers(jv, gF - zl + zu), y)
+                reinit_y = torch.zeros_like(reinit_y)
             # KKT error (Ipopt scaling s_d, s_c)
-            rd = gF + torch.einsum("bmn,bm->bn", JF, y) - zl + zu
+            jty = self._jt_mul(jv, y)
+            rd = gF + jty - zl + zu
             zsum = zl.abs().sum(1) + zu.abs().sum(1) + y.abs().sum(1)
             sd = torch.clamp(zsum / (2 * nf + m), min=opt.s_max) / opt.s_max
             sc = torch.clamp((zl.abs().sum(1) + zu.abs().sum(1)) / (2 * nf), min=opt.s_max) / opt.s_max
@@ -233,20 +293,17 @@ class BatchedIpm:
             sig = torch.where(hasL, zl / sl, torch.zeros_like(x)) + torch.where(hasU, zu / su, torch.zeros_like(x))
             bar = torch.where(hasL, mu[:, None] / sl, torch.zeros_like(x)) - torch.where(hasU, mu[:, None] / su,
                                                                                          torch.zeros_like(x))
-            rhs_x = -(gF + torch.einsum("bmn,bm->bn", JF, y) - bar)
+            rhs_x = -(gF + jty - bar)
             rhs = torch.cat([rhs_x, -g], dim=1)
             # inertia correction by curvature test: increase delta_w until dx^T (W + Sigma + dw) dx > 0
             dw = torch.zeros((B,), dtype=torch.float64, device=self.dev)
             for attempt in range(12):
-                Kxx = W + torch.diag_embed(sig) + dw[:, None, None] * I_n
-                top = torch.cat([Kxx, JF.transpose(1, 2)], dim=2)
-                bot = torch.cat([JF, -opt.delta_c * torch.eye(m, dtype=torch.float64, device=self.dev).expand(B, m, m)],
-                                dim=2)
-                K = torch.cat([top, bot], dim=1)
-                sol = torch.linalg.solve(K, rhs)
+                dxx = sig + dw[:, None]
+                K = self.band.factor(self._kkt_band(W, dxx, jv), self.kl, self.ku)
+                sol = self._kkt_solve(K, rhs)
                 dx, dy = sol[:, :nf], sol[:, nf:]
-                curv = torch.einsum("bi,bij,bj->b", dx, Kxx, dx)
-                bad = (~done) & ((curv <= 1e-12 * (dx * dx).sum(1)) | ~torch.isfinite(curv))
+                curv = self._quad_w(W, dx) + (dxx * dx * dx).sum(1)
+                bad = (~done) & ((curv <= opt.curv_min * (dx * dx).sum(1)) | ~torch.isfinite(curv))
                 if not bool(bad.any()):
                     break
                 first = dw == 0
@@ -281,7 +338,7 @@ class BatchedIpm:
                     soc_try = (~accepted) & (~ok) & (gt.abs().sum(1) >= theta)
                     if bool(soc_try.any()):
                         c_soc = alpha[:, None] * g + gt
-                        sol_c = torch.linalg.solve(K, torch.cat([rhs_x * alpha[:, None], -c_soc], dim=1))
+                        sol_c = self._kkt_solve(K, torch.cat([rhs_x * alpha[:, None], -c_soc], dim=1))
                         dxc = sol_c[:, :nf]
                         a_c = torch.minimum(self._max_step(sl, dxc, hasL, tau), self._max_step(su, -dxc, hasU, tau))
                         xc = x + a_c[:, None] * dxc
@@ -306,8 +363,17 @@ class BatchedIpm:
                                                       (fpos % filt.shape[1])[:, None])[:, :, None],
                                torch.stack([(1 - 1e-5) * theta, phi - 1e-5 * theta], dim=1)[:, None, :], filt)
             fpos = fpos + grow.long()
-            # a failed search takes the shortest step anyway (restoration-free fallback)
-            x_new = torch.where(failed[:, None], x + alpha[:, None] * dx, x_acc)
+            # a failed search: a feasibility-restoration step (minimum-norm Newton step on g = 0 in the metric
+            # Sigma + I, backtracking on ||g||_1 only), then a fresh filter and least-squares multipliers
+            x_new = x_acc
+            failed = failed & ~done
+            if bool(failed.any()) and m:
+                xr = self._restoration_step(x, g, jv, sig, tau)
+                x_new = torch.where(failed[:, None], xr, x_acc)
+                filt = torch.where(failed[:, None, None], torch.tensor([np.inf, -np.inf], dtype=torch.float64,
+                                                                       device=self.dev), filt)
+                reinit_y = reinit_y | failed
+                alpha = torch.where(failed, torch.zeros_like(alpha), alpha)  # y and z stay put this iteration
             alpha_eff = torch.where(failed, alpha, torch.where(accepted, alpha, alpha))
             step = (~done)
             alpha = torch.where(step, alpha_eff, torch.zeros_like(alpha_eff))
@@ -317,7 +383,7 @@ class BatchedIpm:
                       f"a_p {float(a_p[0]):.2e} dw {float(dw[0]):.1e}")
             x = torch.where(step[:, None], x_new, x)
             y = y + alpha[:, None] * dy
-            az = torch.where(step, a_z, torch.zeros_like(a_z))
+            az = torch.where(step & ~failed, a_z, torch.zeros_like(a_z))
             zl = zl + az[:, None] * dzl
             zu = zu + az[:, None] * dzu
             # keep z within [mu / (kappa s), kappa mu / s] (Ipopt kappa_Sigma = 1e10)
@@ -334,6 +400,55 @@ class BatchedIpm:
         return IpmResult(v=vfinal.cpu().numpy(), y=y.cpu().numpy(), f=f.cpu().numpy(), converged=done.cpu().numpy(),
                          iterations=iters.cpu().numpy(), kkt_error=err0.cpu().numpy(),
                          wall_time=time.perf_counter() - t0, n_callbacks=dict(self.calls))
+
+    def _full(self, xf):
+        vv = self._v_template.clone()
+        vv[:, self.freeT] = xf * self.d
+        return vv
+
+    def _ls_multipliers(self, jv, r):
+        """y minimising ||r + J^T y||: [[I, J^T], [J, 0]] [w; y] = [-r; 0]; dropped when |y| > 1e3 (Ipopt)."""
+        torch = self.torch
+        B, nf = self.B, len(self.free)
+        K = self.band.factor(self._kkt_band(torch.zeros((B, self.hrF.numel()), dtype=torch.float64, device=self.dev),
+                                            torch.ones((B, nf), dtype=torch.float64, device=self.dev), jv),
+                             self.kl, self.ku)
+        sol = self._kkt_solve(K, torch.cat([-r, torch.zeros((B, self.m), dtype=torch.float64, device=self.dev)], 1))
+        y = sol[:, nf:]
+        ok = torch.isfinite(y).all(1) & (y.abs().amax(1) <= 1e3)
+        return torch.where(ok[:, None], y, torch.zeros_like(y))
+
+    def _restoration_step(self, x, g, jv, sig, tau):
+        """Minimum-norm step towards g = 0 ([[Sigma + I, J^T], [J, 0]]), kept inside the bounds by the fraction
+        to the boundary and halved until ||g||_1 decreases."""
+        torch = self.torch
+        B, nf = self.B, len(self.free)
+        K = self.band.factor(self._kkt_band(torch.zeros((B, self.hrF.numel()), dtype=torch.float64, device=self.dev),
+                                            sig + 1.0, jv), self.kl, self.ku)
+        dx = self._kkt_solve(K, torch.cat([torch.zeros((B, nf), dtype=torch.float64, device=self.dev), -g], 1))[:, :nf]
+        sl = torch.where(self.hasL, x - self.lbF, torch.ones_like(x))
+        su = torch.where(self.hasU, self.ubF - x, torch.ones_like(x))
+        a = torch.minimum(self._max_step(sl, dx, self.hasL, tau), self._max_step(su, -dx, self.hasU, tau))
+        theta = g.abs().sum(1)
+        out = x.clone()
+        todo = torch.ones((B,), dtype=torch.bool, device=self.dev)
+        for _ in range(20):
+            xt = x + a[:, None] * dx
+            gt, _ = self._scaled_gf(self._full(xt))
+            ok = todo & torch.isfinite(gt).all(1) & (gt.abs().sum(1) < theta)
+            out = torch.where(ok[:, None], xt, out)
+            todo = todo & ~ok
+            if not bool(todo.any()):
+                break
+            a = a * 0.5
+        return out
+
+    def _kkt_solve(self, K, rhs):
+        """Solve with factored KKT K for a natural-order right-hand side (free variables, then g rows)."""
+        rb = self.torch.empty_like(rhs)
+        rb[:, self.posT] = rhs
+        xb = self.band.solve(K, rb)
+        return xb[:, self.posT]
 
     def _max_step(self, s, ds, has, tau):
         torch = self.torch
@@ -364,18 +479,32 @@ class BatchedIpm:
         ok = finite & (tt <= theta_max) & ~in_filter & torch.where(switching, armijo_ok, suff)
         return ok, switching & armijo_ok
 
-    def _merit(self, f, g, x, mu, nu):
-        torch = self.torch
-        sl = torch.where(self.hasL, x - self.lbF, torch.ones_like(x))
-        su = torch.where(self.hasU, self.ubF - x, torch.ones_like(x))
-        bad = ((sl <= 0) & self.hasL).any(1) | ((su <= 0) & self.hasU).any(1)
-        barrier = torch.where(self.hasL, torch.log(torch.clamp(sl, min=1e-300)), torch.zeros_like(x)).sum(1) + \
-            torch.where(self.hasU, torch.log(torch.clamp(su, min=1e-300)), torch.zeros_like(x)).sum(1)
-        phi = f - mu * barrier + nu * g.abs().sum(1)
-        return torch.where(bad, torch.full_like(phi, np.inf), phi)
-
     def close(self):
         self.h.close()
+
+
+class GpuBandSolver:
+    """Batched band LU of libcfx (cfx_band_lu / cfx_band_lu_solve) on torch's current stream."""
+
+    def factor(self, ab, kl, ku):
+        import torch
+
+        from . import _cfx
+
+        ab = ab.contiguous()
+        B, n, _ = ab.shape
+        ipiv = torch.empty((B, n), dtype=torch.int32, device=ab.device)
+        info = torch.empty((B,), dtype=torch.int32, device=ab.device)
+        _cfx.band_lu(ab, ipiv, info, kl, ku)
+        return (ab, ipiv, info, kl, ku)
+
+    def solve(self, fac, rhs):
+        from . import _cfx
+
+        ab, ipiv, _info, kl, ku = fac
+        x = rhs.contiguous().clone()
+        _cfx.band_lu_solve(ab, ipiv, kl, ku, x)
+        return x
 
 
 def solve_ocp(ocp, solver=None, batch: int = 1, device: int = 0, v0=None, **kwargs):

@@ -139,7 +139,8 @@ int cfx_get_sizes(const cfx_handle *h, cfx_sizes *out);
    non-blocking stream of its own until this is called. */
 int cfx_set_stream(cfx_handle *h, void *hip_stream);
 int cfx_synchronize(cfx_handle *h);
-const char *cfx_last_error(const cfx_handle *h); /* h == NULL: last cfx_create failure of this thread */
+const char *cfx_last_error(const cfx_handle *h); /* h == NULL: last handle-free failure (cfx_create,
+                                                     cfx_band_lu*) of this thread */
 int cfx_abi_version(void);
 int cfx_device_count(void);
 
@@ -162,6 +163,21 @@ int cfx_eval_all(cfx_handle *h, const double *v, double *g, double *jac, double 
 /* ---- IvpFes.integrate: single shooting from x0 (NULL: rest state) with per-interval controls
    u [N*nu per instance], writing every sub-step state: traj [(N*n_steps+1)*nx per instance]. ---- */
 int cfx_integrate(cfx_handle *h, const double *x0, const double *u, double *traj, uint32_t flags);
+
+/* ---- Newton / KKT linear algebra of the batched interior-point driver ----------------------------
+   Replaces the sparse symmetric-indefinite factorisation Ipopt runs every iteration on the KKT matrix
+   (MUMPS by default; `Solver.IPOPT` as built at cocofest/optimization/fes_ocp.py:171-190 and
+   cocofest/examples, bioptim's linear_solver option).  B independent n x n banded systems, LAPACK
+   dgbtrf/dgbtrs semantics (partial pivoting), device pointers, instance-major:
+     ab   [B][n][2 kl + ku + 1]  column j of instance b at ab + (b n + j)(2 kl + ku + 1); A(i, j) at row
+                                 kl + ku + i - j; rows < kl are fill-in (zeroed by cfx_band_lu)
+     ipiv [B][n]  0-based pivot rows;   info [B]  0 or j + 1 for the first zero pivot;   rhs [B][nrhs][n]
+   cfx_band_lu factors in place and, when nrhs > 0, solves; cfx_band_lu_solve re-uses the factors.
+   Launched on `hip_stream` (NULL = the HIP null stream); errors via cfx_last_error(NULL). */
+int cfx_band_lu(int64_t n, int32_t kl, int32_t ku, int64_t batch, double *ab, int32_t *ipiv, int32_t *info,
+                int32_t nrhs, double *rhs, void *hip_stream);
+int cfx_band_lu_solve(int64_t n, int32_t kl, int32_t ku, int64_t batch, const double *ab, const int32_t *ipiv,
+                      int32_t nrhs, double *rhs, void *hip_stream);
 
 #ifdef __cplusplus
 }

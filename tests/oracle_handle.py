@@ -47,3 +47,27 @@ class OracleHandle:
 
     def close(self):
         pass
+
+
+class DenseBandSolver:
+    """CPU stand-in for libcfx's batched band LU (GpuBandSolver): expands the band storage to dense matrices
+    and solves with torch.linalg.  Test infrastructure only."""
+
+    def factor(self, ab, kl, ku):
+        import torch
+
+        B, n, ldab = ab.shape
+        kv = kl + ku
+        i = torch.arange(n)[:, None]
+        j = torch.arange(n)[None, :]
+        r = kv + i - j
+        inband = (r >= kl) & (r < ldab)
+        A = torch.zeros((B, n, n), dtype=ab.dtype)
+        jj = j.expand(n, n)[inband]
+        A[:, inband] = ab[:, jj, r[inband]]
+        return A
+
+    def solve(self, A, rhs):
+        import torch
+
+        return torch.linalg.solve(A, rhs)

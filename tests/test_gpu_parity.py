@@ -6,6 +6,9 @@ g / J / f / grad (RK recursions of <= 40 stages; the kernels use reciprocal-mult
 divides, a few ulp per stage).
 """
 
+import json
+import pathlib
+
 import numpy as np
 import pytest
 
@@ -319,11 +322,9 @@ def test_interior_point_pulse_width_force_tracking():
     respects the bounds, for a small multi-start batch."""
     from cocofest_amd.solver import BatchedIpm
 
-    force = np.array(__import__("json").loads((__import__("pathlib").Path(__file__).parent / "golden" /
-                                               "ref_formulas.json").read_text())["misc"]["force_tracking"]["force"])
-    time = np.array(__import__("json").loads((__import__("pathlib").Path(__file__).parent / "golden" /
-                                              "ref_formulas.json").read_text())["misc"]["force_tracking"]["time"])
-    cfg = dict(cases.cfg3(), objective={"force_tracking": [time, force]})
+    ft = json.loads((pathlib.Path(__file__).parent / "golden" / "ref_formulas.json").read_text())
+    ft = ft["misc"]["force_tracking"]
+    cfg = dict(cases.cfg3(), objective={"force_tracking": [np.array(ft["time"]), np.array(ft["force"])]})
     ocp = cases.product_ocp(**cfg)
     pb = cases.oracle_problem(**cfg)
     ipm = BatchedIpm(ocp, batch=4)
@@ -338,3 +339,95 @@ def test_interior_point_pulse_width_force_tracking():
     assert res.converged.all(), (res.kkt_error, res.iterations)
     assert np.max(np.abs(O.eval_g(pb, res.v))) < 1e-5
     assert np.all(res.v >= lb - 1e-8) and np.all(res.v <= ub + 1e-8)
+
+
+def _band_system(rng, B, n, kl, ku, zero_diag=False):
+    """Random banded matrices (B, n, n), their LAPACK band storage (B, n, 2kl+ku+1) and right-hand sides."""
+    A = np.zeros((B, n, n))
+    for d in range(-kl, ku + 1):
+        idx = np.arange(max(0, -d), min(n, n - d))
+        A[:, idx, idx + d] = rng.standard_normal((B, idx.size))
+    if zero_diag:
+        A[:, np.arange(n), np.arange(n)] = 0.0  # KKT-like: forces row interchanges
+    ldab = 2 * kl + ku + 1
+    ab = np.full((B, n, ldab), np.nan)  # fill-in rows must be ignored (zeroed by the factorisation)
+    for j in range(n):
+        for i in range(max(0, j - ku), min(n, j + kl + 1)):
+            ab[:, j, kl + ku + i - j] = A[:, i, j]
+    ab[:, :, kl:] = np.nan_to_num(ab[:, :, kl:])
+    return A, ab
+
+
+@pytest.mark.parametrize("n,kl,ku,zero_diag", [(1, 0, 0, False), (7, 3, 1, False), (80, 5, 5, True),
+                                               (500, 6, 6, True), (300, 40, 40, False), (64, 63, 63, False),
+                                               (200, 70, 2, True)])
+def test_band_lu_matches_dense_solve(n, kl, ku, zero_diag):
+    """cfx_band_lu / cfx_band_lu_solve vs numpy's dense LU on random band matrices: LDS-resident bands and the
+    global-memory variant (300 x 161 band > 160 KiB), bandwidths beyond one wave (kl = 70), zero diagonals."""
+    import torch
+
+    from cocofest_amd import _cfx
+
+    rng = np.random.default_rng(n + kl)
+    B = 5
+    A, ab = _band_system(rng, B, n, kl, ku, zero_diag)
+    rhs = rng.standard_normal((B, 2, n))
+    ref = np.linalg.solve(A, rhs.transpose(0, 2, 1)).transpose(0, 2, 1)
+    abt = torch.tensor(ab, device="cuda")
+    ipiv = torch.empty((B, n), dtype=torch.int32, device="cuda")
+    info = torch.empty((B,), dtype=torch.int32, device="cuda")
+    x = torch.tensor(rhs, device="cuda")
+    _cfx.band_lu(abt, ipiv, info, kl, ku, rhs=x)
+    torch.cuda.synchronize()
+    assert (info.cpu().numpy() == 0).all()
+    cond = np.linalg.cond(A).max()
+    tol = 1e-13 * cond * n
+    assert np.max(np.abs(x.cpu().numpy() - ref)) <= tol * max(1.0, np.abs(ref).max())
+    x2 = torch.tensor(rhs[:, :1], device="cuda")  # re-use of the factors
+    _cfx.band_lu_solve(abt, ipiv, kl, ku, x2)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(x2.cpu().numpy(), x.cpu().numpy()[:, :1])
+
+
+def test_band_lu_reports_singular_and_bad_arguments():
+    import torch
+
+    from cocofest_amd import _cfx
+
+    n, kl, ku = 10, 2, 2
+    rng = np.random.default_rng(1)
+    A, ab = _band_system(rng, 2, n, kl, ku)
+    ab[1, 4, :] = 0.0  # column 4 of instance 1 is zero: first zero pivot at j = 4 (info 5)
+    abt = torch.tensor(ab, device="cuda")
+    ipiv = torch.empty((2, n), dtype=torch.int32, device="cuda")
+    info = torch.empty((2,), dtype=torch.int32, device="cuda")
+    _cfx.band_lu(abt, ipiv, info, kl, ku)
+    torch.cuda.synchronize()
+    assert info.cpu().tolist() == [0, 5]
+    with pytest.raises(_cfx.CfxError):
+        _cfx.band_lu(abt, ipiv, info, kl + 1, ku)  # storage does not match the bandwidths
+    lib = _cfx.load_library()
+    assert lib.cfx_band_lu(0, 0, 0, 1, abt.data_ptr(), ipiv.data_ptr(), info.data_ptr(), 0, None, None) == _cfx.EINVAL
+
+
+def test_interior_point_hmed_intensity():
+    """Hmed2018 intensity optimisation (sliding-window rows make the widest KKT band of the families): the
+    batched interior point reaches a feasible KKT point within the intensity bounds."""
+    from cocofest_amd.solver import BatchedIpm
+
+    cfg = dict(name="hmed2018", stims=[0.0, 0.1, 0.2, 0.3, 0.4], final_time=0.5, truncation=5, scheme="RK1", m=5,
+               objective={"end_node_tracking": 60}, n_shooting=None)
+    ocp = cases.product_ocp(**cfg)
+    pb = cases.oracle_problem(**cfg)
+    ipm = BatchedIpm(ocp, batch=8)
+    rng = np.random.default_rng(5)
+    v0 = np.tile(ocp.initial_guess_vector(), (8, 1))
+    lb, ub = ocp.bounds_vector()
+    free = lb != ub
+    v0[:, free] = np.clip(v0[:, free] + rng.uniform(0, 10, (8, free.sum())), lb[free], ub[free])
+    res = ipm.solve(v0)
+    ipm.close()
+    assert res.converged.all(), (res.kkt_error, res.iterations)
+    assert np.max(np.abs(O.eval_g(pb, res.v))) < 1e-5
+    assert np.all(res.v >= lb - 1e-8) and np.all(res.v <= ub + 1e-8)
+    assert abs(pb.unpack(res.v)[0][:, -1, 1] - 60).max() < 1e-3  # reachable target is met

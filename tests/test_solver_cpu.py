@@ -4,7 +4,7 @@ import numpy as np
 
 from oracle import fes_oracle as O
 from tests import cases
-from tests.oracle_handle import OracleHandle
+from tests.oracle_handle import DenseBandSolver, OracleHandle
 
 
 def _ipm(cfg, batch, **opts):
@@ -12,7 +12,8 @@ def _ipm(cfg, batch, **opts):
 
     ocp = cases.product_ocp(**cfg)
     pb = cases.oracle_problem(**cfg)
-    ipm = BatchedIpm(ocp, batch=batch, options=IpmOptions(**opts), handle=OracleHandle(pb, batch), torch_device="cpu")
+    ipm = BatchedIpm(ocp, batch=batch, options=IpmOptions(**opts), handle=OracleHandle(pb, batch), torch_device="cpu",
+                     band=DenseBandSolver())
     return ocp, pb, ipm
 
 
@@ -44,3 +45,16 @@ def test_pulse_width_problem_reaches_a_kkt_point():
     assert np.all(res.v >= lb - 1e-9) and np.all(res.v <= ub + 1e-9)
     X, U, _ = pb.unpack(res.v)
     assert abs(X[0, -1, 1] - 30) < 1.0  # reachable target: the end force is driven to it
+
+
+def test_zero_initial_guess_needs_multiplier_init_and_restoration():
+    """cfg 2 from the reference's default initial guess (all states 0, on their lower bounds): converges to the
+    forward integration (least-squares multipliers + restoration steps when the filter search fails)."""
+    cfg = cases.cfg2()
+    ocp, pb, ipm = _ipm(cfg, batch=1)
+    res = ipm.solve()
+    assert res.converged.all(), (res.kkt_error, res.iterations)
+    c = O.model_constants("ding2003")
+    traj = O.ivp_integrate("ding2003", c, pb.rows, np.zeros((pb.n_shooting, 0)), 1.0, "RK1", 10)
+    X, _, _ = pb.unpack(res.v)
+    np.testing.assert_allclose(X[0].T, traj[:, ::10], rtol=1e-6, atol=1e-6)
