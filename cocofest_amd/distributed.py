@@ -1,0 +1,173 @@
+"""Multi-GPU paths: one process per GPU, torch.distributed (RCCL on ROCm, gloo in the
+CPU tests).
+
+Two ways the callbacks shard:
+
+* ``shard_instances`` — independent instances (multi-start, parameter sweeps, independent NMPC scenarios):
+  rank r owns a contiguous block of the batch and evaluates / solves it with its own libcfx handle.  No
+  data-path collective; ``gather_instances`` collects results at the end.
+
+* ``IntervalShardedNlp`` — ONE large OCP split by interval ranges.  Block k of g / J_g / H depends only on
+  x_k, u_k, x_{k+1} (a one-node halo) and the parameters, so rank r evaluates intervals [k0, k1) through
+  ``FesOcp.interval_slice`` and the exchange step is one all-gather per callback of the value slices (fixed
+  sparsity, so every rank knows where each gathered value lands).  Overlapping contributions (the objective
+  at shared nodes, parameter gradients, Hessian entries of the halo node) are summed by the index-add that
+  places the gathered slices.  Every rank ends with the full callback values, so the host driver can run
+  replicated on every rank (or on rank 0 only) on identical data.
+"""
+
+from __future__ import annotations
+
+import numpy as np
+
+
+def shard_range(total: int, rank: int, world: int):
+    """Contiguous block [lo, hi) of ``total`` items owned by ``rank`` (sizes differ by at most one)."""
+    if world < 1 or not 0 <= rank < world:
+        raise ValueError(f"rank {rank} outside world of size {world}")
+    base, extra = divmod(total, world)
+    lo = rank * base + min(rank, extra)
+    return lo, lo + base + (1 if rank < extra else 0)
+
+
+def shard_instances(v0, rank: int, world: int):
+    """The block of instance rows (B, nv) this rank owns."""
+    lo, hi = shard_range(len(v0), rank, world)
+    return v0[lo:hi]
+
+
+def gather_instances(local, group=None):
+    """All-gather per-rank blocks of rows (sizes may differ by one) into the full (B, ...) tensor on every
+    rank, in rank order."""
+    import torch
+    import torch.distributed as dist
+
+    world = dist.get_world_size(group)
+    n = torch.tensor([local.shape[0]], dtype=torch.int64, device=local.device)
+    sizes = [torch.zeros_like(n) for _ in range(world)]
+    dist.all_gather(sizes, n, group=group)
+    sizes = [int(s.item()) for s in sizes]
+    pad = max(sizes)
+    buf = torch.zeros((pad,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
+    buf[: local.shape[0]] = local
+    out = [torch.empty_like(buf) for _ in range(world)]
+    dist.all_gather(out, buf, group=group)
+    return torch.cat([o[:s] for o, s in zip(out, sizes)], dim=0)
+
+
+class IntervalShardedNlp:
+    """The callbacks of one OCP with its intervals split over the ranks of ``group``.
+
+    ``evaluator(sub_ocp, batch)`` opens the per-rank evaluator of an interval slice; by default a libcfx
+    handle (AoS, batch-major) on this rank's GPU.  The interface mirrors ``_cfx.Handle`` for the calls the
+    host driver makes (``eval_all``, ``eval_h``, structures), on (B, nv) torch tensors of the FULL problem.
+    """
+
+    def __init__(self, ocp, batch: int = 1, group=None, device=None, evaluator=None):
+        import torch
+        import torch.distributed as dist
+
+        self.torch, self.dist, self.group = torch, dist, group
+        self.ocp, self.B = ocp, batch
+        self.rank, self.world = dist.get_rank(group), dist.get_world_size(group)
+        if self.world > ocp.n_shooting:
+            raise ValueError(f"{self.world} ranks for {ocp.n_shooting} intervals")
+        self.k0, self.k1 = shard_range(ocp.n_shooting, self.rank, self.world)
+        self.sub = ocp.interval_slice(self.k0, self.k1)
+        if evaluator is None:
+            local = torch.cuda.current_device() if device is None else device
+            self.h = self.sub.nlp(batch=batch, layout="aos", device=local)
+            self.dev = torch.device("cuda", local)
+        else:
+            self.h = evaluator(self.sub, batch)
+            self.dev = torch.device("cpu") if device is None else torch.device(device)
+        o = ocp
+        self.nz = o.nx + o.nu
+        self.ngk = o.nx + (o.nu if (o.n_params and o.last_stim_idx is not None) else 0)
+        self._exchange_structures()
+
+    # ---- global structure and the local -> global maps ------------------------------------------------
+    def _exchange_structures(self):
+        """Map this slice's structures to global indices and all-gather them (host objects, once)."""
+        torch, o = self.torch, self.ocp
+        body = (self.k1 - self.k0) * self.nz + o.nx
+        cols = np.empty(self.sub.nv, dtype=np.int64)
+        cols[:body] = self.k0 * self.nz + np.arange(body)
+        cols[body:] = o.nv - o.n_params + np.arange(self.sub.nv - body)
+        jr, jc = (np.asarray(a, np.int64) for a in self.h.jac_structure())
+        hr, hc = (np.asarray(a, np.int64) for a in self.h.hess_structure())
+        g0 = self.k0 * self.ngk
+        mine = dict(jr=jr + g0, jc=cols[jc], hr=cols[hr], hc=cols[hc], cols=cols,
+                    grows=g0 + np.arange(self.sub.n_shooting * self.ngk))
+        parts = [None] * self.world
+        self.dist.all_gather_object(parts, mine, group=self.group)
+        self._jr = np.concatenate([p["jr"] for p in parts])
+        self._jc = np.concatenate([p["jc"] for p in parts])
+        hp = np.unique(np.stack([np.concatenate([p["hr"] for p in parts]), np.concatenate([p["hc"] for p in parts])],
+                                1), axis=0)
+        self._hr, self._hc = hp[:, 0], hp[:, 1]
+        hindex = {(int(r), int(c)): i for i, (r, c) in enumerate(zip(self._hr, self._hc))}
+        L = lambda a: torch.as_tensor(np.asarray(a), dtype=torch.long, device=self.dev)  # noqa: E731
+        offs = np.cumsum([0] + [len(p["jr"]) for p in parts])
+        self.map_j = [L(np.arange(offs[i], offs[i + 1])) for i in range(self.world)]
+        self.map_g = [L(p["grows"]) for p in parts]
+        self.map_v = [L(p["cols"]) for p in parts]
+        self.map_h = [L([hindex[(int(r), int(c))] for r, c in zip(p["hr"], p["hc"])]) for p in parts]
+        self.cols_local = self.map_v[self.rank]
+        self.nv, self.ng = o.nv, o.n_shooting * self.ngk
+        self.nnz_jac, self.nnz_hess = len(self._jr), len(self._hr)
+
+    def jac_structure(self):
+        return self._jr.astype(np.int32), self._jc.astype(np.int32)
+
+    def hess_structure(self):
+        return self._hr.astype(np.int32), self._hc.astype(np.int32)
+
+    # ---- exchange -------------------------------------------------------------------------------------
+    def _allgather_place(self, local, maps, width):
+        """All-gather every rank's (B, L_r) slice and index-add it into a (B, width) global array."""
+        torch, dist = self.torch, self.dist
+        pad = max(m.numel() for m in maps)
+        buf = torch.zeros((self.B, pad), dtype=torch.float64, device=self.dev)
+        buf[:, : local.shape[1]] = local
+        out = [torch.empty_like(buf) for _ in range(self.world)]
+        dist.all_gather(out, buf, group=self.group)
+        full = torch.zeros((self.B, width), dtype=torch.float64, device=self.dev)
+        for o, m in zip(out, maps):
+            full.index_add_(1, m, o[:, : m.numel()])
+        return full
+
+    # ---- callbacks (same signatures as _cfx.Handle, AoS (B, ...) tensors) ------------------------------
+    def eval_all(self, v, g=None, jac=None, f=None, grad=None):
+        torch = self.torch
+        vl = v[:, self.cols_local].contiguous()
+        sub = self.sub
+        gl = torch.empty((self.B, sub.n_shooting * self.ngk), dtype=torch.float64, device=self.dev) \
+            if (g is not None or jac is not None) else None
+        jl = torch.empty((self.B, self.h.nnz_jac), dtype=torch.float64, device=self.dev) if jac is not None else None
+        fl = torch.empty((self.B,), dtype=torch.float64, device=self.dev) if f is not None else None
+        dl = torch.empty((self.B, sub.nv), dtype=torch.float64, device=self.dev) if grad is not None else None
+        self.h.eval_all(vl, g=gl, jac=jl, f=fl, grad=dl)
+        if g is not None:
+            g.copy_(self._allgather_place(gl, self.map_g, self.ng))
+        if jac is not None:
+            jac.copy_(self._allgather_place(jl, self.map_j, self.nnz_jac))
+        if f is not None:
+            fs = fl.clone()
+            self.dist.all_reduce(fs, group=self.group)
+            f.copy_(fs)
+        if grad is not None:
+            grad.copy_(self._allgather_place(dl, self.map_v, self.nv))
+
+    def eval_h(self, v, of, lam, hess):
+        torch = self.torch
+        vl = v[:, self.cols_local].contiguous()
+        g0 = self.k0 * self.ngk
+        laml = lam[:, g0: g0 + self.sub.n_shooting * self.ngk].contiguous()
+        hl = torch.empty((self.B, self.h.nnz_hess), dtype=torch.float64, device=self.dev)
+        self.h.eval_h(vl, of.contiguous(), laml, hl)
+        hess.copy_(self._allgather_place(hl, self.map_h, self.nnz_hess))
+        return hess
+
+    def close(self):
+        self.h.close()

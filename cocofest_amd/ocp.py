@@ -157,6 +157,42 @@ class FesOcp:
             last_stim_idx=self.last_stim_idx, intensity_floor=self.intensity_floor,
             objectives=self.objectives, device=device)
 
+    def interval_slice(self, k0: int, k1: int) -> "FesOcp":
+        """The callbacks of intervals [k0, k1) as a problem of their own (multi-GPU interval sharding).
+
+        Its decision vector is ``[x_k0, u_k0, ..., x_k1, p]`` — the global slice ``v[k0 nz : k1 nz + nx]`` plus
+        every parameter — and its constraints are the global rows of those intervals.  Stim times are shifted
+        by k0 dt (only the differences t - t_i enter the model).  Objective terms keep the nodes this slice
+        owns: k0 .. k1 - 1, and node N on the slice that ends at N, so summing the slices' f gives f."""
+        N = self.n_shooting
+        if not (0 <= k0 < k1 <= N):
+            raise ValueError(f"interval slice [{k0}, {k1}) outside [0, {N})")
+        dt = self.final_time / N
+        shift = k0 * dt
+        rows = np.where(self.stim_rows > -1e6, self.stim_rows - shift, self.stim_rows)[k0: k1 + 1].copy()
+        own_last = k1 if k1 == N else k1 - 1
+        terms = []
+        for t in self.objectives:
+            last = min(t["node_last"], own_last if t["var_kind"] == _cfx.VAR_STATE else k1 - 1)
+            first = max(t["node_first"], k0)
+            if first > last:
+                continue
+            nt = dict(t, node_first=first - k0, node_last=last - k0)
+            if t.get("target") is not None:
+                nt["target"] = np.asarray(t["target"], dtype=float)[k0: k1 + 1].copy()
+            terms.append(nt)
+        sl = lambda a: None if a is None else np.asarray(a)[..., k0: k1 + 1]  # noqa: E731
+        su = lambda a: None if a is None else np.asarray(a)[..., k0: k1]  # noqa: E731
+        x_bounds = (sl(self.x_bounds[0]), sl(self.x_bounds[1]))
+        u_bounds = (su(self.u_bounds[0]), su(self.u_bounds[1])) if self.nu else self.u_bounds
+        last_idx = None if self.last_stim_idx is None else np.asarray(self.last_stim_idx)[k0:k1].copy()
+        sub = FesOcp(self.model, k1 - k0, (k1 - k0) * dt, self.ode_solver, rows,
+                     self.stim_idx_at_node_list[k0: k1 + 1], terms, x_bounds, sl(self.x_init), u_bounds,
+                     su(self.u_init) if self.nu else self.u_init, self.p_bounds, self.p_init, self.n_params, last_idx,
+                     self.intensity_floor, self.n_threads, self.use_sx)
+        sub.global_slice = (k0, k1)
+        return sub
+
     def solve(self, solver=None, **kwargs):
         from .solver import solve_ocp
 
