@@ -134,6 +134,53 @@ def convergence(device):
     return out
 
 
+def ivp_section(device):
+    """IvpFes.integrate on the configuration of the reference's own timings
+    (examples/sensitivity/truncation/sensitivity_analysis.py: DingModelFrequencyWithFatigue, 10 single pulses,
+    truncation 10, final time 1 s, default RK4 x 10; 106.9 ms per integrate() in the authors' pickle,
+    truncation_single.pkl, unknown hardware): per-call latency at batch 1 (host arrays in / out, as
+    integrate() is called), and the batched kernel throughput over device-resident initial states."""
+    import torch
+
+    from cocofest_amd import DingModelFrequencyWithFatigue, IvpFes
+
+    ivp = IvpFes(fes_parameters={"model": DingModelFrequencyWithFatigue(stim_time=[round(0.1 * i, 1) for i in range(10)],
+                                                                        sum_stim_truncation=10)},
+                 ivp_parameters={"final_time": 1})
+    for _ in range(5):
+        ivp.integrate(return_time=False)
+    reps = 200
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        ivp.integrate(return_time=False)
+    ms_b1 = (time.perf_counter() - t0) / reps * 1e3
+    ivp.close()
+    B = 1 << 16
+    h = ivp.handle(batch=B, layout="soa", device=device)
+    rest = torch.tensor([0.0, 0.0, 3009.0, 0.050957, 0.103], dtype=torch.float64, device=f"cuda:{device}")
+    gen = torch.Generator(device=f"cuda:{device}")
+    gen.manual_seed(5)
+    x0 = (rest[:, None] * (0.8 + 0.2 * torch.rand((5, B), generator=gen, dtype=torch.float64,
+                                                  device=f"cuda:{device}"))).contiguous()
+    traj = torch.empty((h.n_shooting * h.n_steps + 1) * h.nx, B, dtype=torch.float64, device=f"cuda:{device}")
+    for _ in range(3):
+        h.integrate(x0=x0, traj=traj)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(10):
+        h.integrate(x0=x0, traj=traj)
+    e1.record()
+    torch.cuda.synchronize()
+    ms_batch = e0.elapsed_time(e1) / 10
+    h.close()
+    return {"config": "IvpFes DingModelFrequencyWithFatigue, 10 pulses @10 Hz, truncation 10, final_time 1 s, "
+                      "RK4 x 10 (N = 10, 101 samples per state)",
+            "ms_per_integrate_b1": ms_b1, "reference_ms_per_integrate": 106.9,
+            "reference_source": "truncation_single.pkl (authors' data, older API, unknown hardware)",
+            "batch": B, "ms_per_batched_launch": ms_batch, "integrations_per_s": B / (ms_batch * 1e-3)}
+
+
 def main():
     args = parse()
     import torch
@@ -192,6 +239,7 @@ def main():
     if rank == 0:
         cpu = cpu_baseline(ocp, args.cpu_seconds) if (world == 1 and args.cpu_seconds > 0) else None
         conv = convergence(local) if (world == 1 and not args.no_solve) else None
+        ivp = ivp_section(local) if (world == 1 and not args.no_solve) else None
         out = {
             "metric": METRIC,
             "value": value,
@@ -226,6 +274,7 @@ def main():
             },
             "cpu_baseline": cpu,
             "convergence": conv,
+            "ivp": ivp,
         }
     h.close()
     if dist:

@@ -163,12 +163,10 @@ class IvpFes:
     def integrate(self, shooting_type=None, integrator=None, to_merge=None, return_time=True,
                   duplicated_times=False):
         """Single-shooting integration from the rest state; returns {state: (1, N*m+1)} (and the time)."""
-        h = self.handle(batch=1)
-        try:
-            u = self.controls.T.reshape(1, -1).copy() if self.controls.shape[0] else None
-            traj = h.integrate(u=u)
-        finally:
-            h.close()
+        if getattr(self, "_h1", None) is None:  # the handle (tables, buffers) is built once per IvpFes
+            self._h1 = self.handle(batch=1)
+            self._u1 = self.controls.T.reshape(1, -1).copy() if self.controls.shape[0] else None
+        traj = self._h1.integrate(u=self._u1)
         m = self.ode_solver.n_integration_steps
         nx = self.model.nb_state
         traj = traj.reshape(self.n_shooting * m + 1, nx)
@@ -179,6 +177,17 @@ class IvpFes:
         time = np.array([k * (self.final_time / self.n_shooting) + j * hstep for k in range(self.n_shooting)
                          for j in range(m)] + [float(self.final_time)])
         return result, time
+
+    def close(self):
+        if getattr(self, "_h1", None) is not None:
+            self._h1.close()
+            self._h1 = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
     @classmethod
     def from_frequency_and_final_time(cls, fes_parameters: dict = None, ivp_parameters: dict = None):
