@@ -26,6 +26,7 @@ MODEL_IDS = {
     "hmed2018_with_fatigue": 5,
 }
 RK1, RK2, RK4 = 1, 2, 4
+COLLOCATION_LEGENDRE, COLLOCATION_RADAU = 16, 17
 LAYOUT_AOS, LAYOUT_SOA = 0, 1
 DEVICE = 1
 OBJ_LAGRANGE, OBJ_MAYER = 0, 1

@@ -11,6 +11,7 @@
 
 #include "../../include/cfx.h"
 #include "cfx_aux.h"
+#include "cfx_colloc.h"
 #include "cfx_launch.h"
 
 using namespace cfx;
@@ -36,6 +37,9 @@ struct cfx_handle {
     std::vector<cfx_objective> objs;
     cfx_sizes sz{};
     int model = 0, scheme = 1, tmax = 1, stages = 1, ni = 1, ni_g = 1;
+    bool colloc = false;  // direct collocation (n_steps = polynomial degree)
+    double tau[kMaxDeg + 1] = {};
+    int32_t* d_hdiag = nullptr;
     KParams kp{};
     int device = 0;
     hipStream_t own_stream = nullptr, stream = nullptr;
@@ -71,6 +75,105 @@ static int fail(cfx_handle* h, int code, const std::string& msg) {
 // ------------------------------------------------------------------------------------------------------
 // stimulation coefficients (cocofest/models/ding2003.py:200-252; hmed2018.py:97-98)
 // ------------------------------------------------------------------------------------------------------
+static double legendre_p(int n, double x) {
+    if (n == 0) return 1.0;
+    double p0 = 1.0, p1 = x;
+    for (int k = 2; k <= n; ++k) {
+        const double p2 = ((2.0 * k - 1.0) * x * p1 - (k - 1.0) * p0) / k;
+        p0 = p1;
+        p1 = p2;
+    }
+    return p1;
+}
+
+// Collocation points on (0, 1]: Gauss-Legendre (roots of P_d) or Radau IIA (roots of P_d - P_{d-1}, x = 1
+// included), mapped from [-1, 1]; sign-change scan + bisection to machine precision.  Then the Lagrange basis
+// through tau_0 = 0 and the points: C[i][j] = l_i'(tau_j), D[i] = l_i(1).
+static void collocation_coefficients(int d, bool radau, double* tau, double (*C)[kMaxDeg + 1], double* D) {
+    auto f = [&](double x) { return radau ? legendre_p(d, x) - legendre_p(d - 1, x) : legendre_p(d, x); };
+    int found = 0;
+    const int M = 40000;
+    double xa = -1.0, fa = f(xa);
+    for (int i = 1; i <= M && found < d; ++i) {
+        const double xb = -1.0 + 2.0 * i / M;
+        if (radau && i == M) break;  // the root x = 1 is added below
+        const double fb = f(xb);
+        if (fb == 0.0) {
+            tau[1 + found++] = xb;
+        } else if (fa * fb < 0.0) {
+            double lo = xa, hi = xb, flo = fa;
+            for (int it = 0; it < 200 && hi - lo > 0.0; ++it) {
+                const double mid = 0.5 * (lo + hi);
+                if (mid == lo || mid == hi) break;
+                const double fm = f(mid);
+                if ((fm < 0.0) == (flo < 0.0)) {
+                    lo = mid;
+                    flo = fm;
+                } else {
+                    hi = mid;
+                }
+            }
+            tau[1 + found++] = 0.5 * (lo + hi);
+        }
+        xa = xb;
+        fa = fb;
+    }
+    if (radau) tau[1 + found++] = 1.0;
+    tau[0] = 0.0;
+    for (int j = 1; j <= d; ++j) tau[j] = (tau[j] + 1.0) / 2.0;
+    for (int i = 0; i <= d; ++i) {
+        double den = 1.0, num1 = 1.0;
+        for (int r = 0; r <= d; ++r)
+            if (r != i) {
+                den *= tau[i] - tau[r];
+                num1 *= 1.0 - tau[r];
+            }
+        D[i] = num1 / den;
+        for (int j = 0; j <= d; ++j) {
+            double v;
+            if (j == i) {
+                v = 0.0;
+                for (int r = 0; r <= d; ++r)
+                    if (r != i) v += 1.0 / (tau[i] - tau[r]);
+            } else {
+                v = 1.0 / (tau[i] - tau[j]);
+                for (int r = 0; r <= d; ++r)
+                    if (r != i && r != j) v *= (tau[j] - tau[r]) / (tau[i] - tau[r]);
+            }
+            C[i][j] = v;
+        }
+    }
+}
+
+// Calcium sums (Ding) / per-stimulus coefficients (Hmed) at the collocation points t_k + tau_j dt,
+// slot k*d + j - 1 — the same expression and operation order as the RK stage tables.
+static void build_colloc_tables(const cfx_handle* h, std::vector<double>& tab) {
+    const cfx_problem& p = h->prob;
+    const cfx_constants& c = p.constants;
+    const int N = p.n_shooting, d = p.n_steps, T = p.truncation;
+    const double dt = p.final_time / N;
+    const double r0 = c.km_rest + c.r0_km_relationship;
+    const bool hmed = is_int(h->model);
+    const int w = hmed ? h->tmax : 1;
+    tab.assign((size_t)N * d * w, 0.0);
+    std::vector<double> ri(T);
+    for (int k = 0; k < N; ++k) {
+        const double* row = &h->rows[(size_t)k * T];
+        for (int i = 0; i < T; ++i) ri[i] = i == 0 ? 1.0 : 1.0 + (r0 - 1.0) * std::exp(-(row[i] - row[i - 1]) / c.tauc);
+        for (int j = 1; j <= d; ++j) {
+            const double t = k * dt + h->tau[j] * dt;
+            const size_t q = (size_t)k * d + j - 1;
+            if (hmed) {
+                for (int i = 0; i < T; ++i) tab[q * w + i] = ri[i] * std::exp(-(t - row[i]) / c.tauc);
+            } else {
+                double sum = 0.0;
+                for (int i = 0; i < T; ++i) sum = sum + ri[i] * std::exp(-(t - row[i]) / c.tauc);
+                tab[q] = sum;
+            }
+        }
+    }
+}
+
 static void build_tables(const cfx_handle* h, std::vector<double>& tab) {
     const cfx_problem& p = h->prob;
     const cfx_constants& c = p.constants;
@@ -304,8 +407,12 @@ extern "C" int cfx_create(const cfx_problem* p, cfx_handle** out) {
     if (p->abi_version != CFX_ABI_VERSION) return create_fail(nullptr, CFX_EINVAL, "cfx_create: ABI version mismatch");
     if (p->model < CFX_DING2003 || p->model > CFX_HMED2018_FATIGUE)
         return create_fail(nullptr, CFX_EINVAL, "cfx_create: unknown model");
-    if (p->scheme != CFX_RK1 && p->scheme != CFX_RK2 && p->scheme != CFX_RK4)
-        return create_fail(nullptr, CFX_EUNSUPPORTED, "cfx_create: scheme must be CFX_RK1, CFX_RK2 or CFX_RK4");
+    const bool colloc = p->scheme == CFX_COLLOCATION_LEGENDRE || p->scheme == CFX_COLLOCATION_RADAU;
+    if (p->scheme != CFX_RK1 && p->scheme != CFX_RK2 && p->scheme != CFX_RK4 && !colloc)
+        return create_fail(nullptr, CFX_EUNSUPPORTED,
+                           "cfx_create: scheme must be CFX_RK1, CFX_RK2, CFX_RK4 or CFX_COLLOCATION_LEGENDRE/RADAU");
+    if (colloc && (p->n_steps < 1 || p->n_steps > kMaxDeg))
+        return create_fail(nullptr, CFX_EUNSUPPORTED, "cfx_create: collocation degree (n_steps) must be in [1, 9]");
     if (p->n_steps < 1 || p->n_shooting < 1 || p->batch < 1 || !(p->final_time > 0.0))
         return create_fail(nullptr, CFX_EINVAL, "cfx_create: n_steps, n_shooting, batch and final_time must be positive");
     if (p->truncation < 1 || p->truncation > 32)
@@ -326,7 +433,8 @@ extern "C" int cfx_create(const cfx_problem* p, cfx_handle** out) {
     h->prob = *p;
     h->model = p->model;
     h->scheme = p->scheme;
-    h->stages = stages_of(p->scheme);
+    h->stages = colloc ? 1 : stages_of(p->scheme);
+    h->colloc = colloc;
     h->device = p->device;
     const int N = p->n_shooting, T = p->truncation;
     h->rows.assign(p->stim_rows, p->stim_rows + (size_t)(N + 1) * T);
@@ -342,9 +450,11 @@ extern "C" int cfx_create(const cfx_problem* p, cfx_handle** out) {
 
     const int nx = is_fatigue(h->model) ? 5 : 2;
     const int nu = is_pw(h->model) ? 1 : (hmed ? T : 0);
-    const int nz = nx + nu;
+    const int deg = colloc ? p->n_steps : 0;
+    const int uoff = colloc ? (deg + 1) * nx : nx;
+    const int nz = uoff + nu;  // decision block of one interval
     const int n_slide = (hmed && p->n_params > 0) ? T : 0;
-    const int ngk = nx + n_slide;
+    const int ngk = (colloc ? (deg + 1) * nx : nx) + n_slide;
 
     // objectives
     std::vector<DevObjective> dobj;
@@ -379,28 +489,55 @@ extern "C" int cfx_create(const cfx_problem* p, cfx_handle** out) {
     h->sz.nu = nu;
     h->sz.nv = (int64_t)N * nz + nx + p->n_params;
     h->sz.ng = (int64_t)N * ngk;
-    const int nhk = nz * (nz + 1) / 2;
-    // structural sparsity of dPhi/d(x_k, u_k), as CasADi derives it symbolically: dependency bitmasks
-    // pushed through the RHS and the RK stages (identical for every interval)
-    uint64_t dep[5];
-    structure_pattern(h->model, h->scheme, p->n_steps, nx, nu, dep);
+    const int per_point = nx * (nx + 1) / 2 + nu * nx;  // collocation Hessian entries of one point
+    const int nhk = colloc ? nx + deg * per_point + nu * (nu + 1) / 2 : nz * (nz + 1) / 2;
     KParams& kp = h->kp;
     int nnzk = 0;
-    for (int r = 0; r < nx; ++r) {
-        for (int c = 0; c < kMaxNz; ++c) kp.jpos[r][c] = -1;
-        for (int c = 0; c < nz; ++c)
-            if (dep[r] >> c & 1ull) kp.jpos[r][c] = (int16_t)nnzk++;
-        kp.jneg[r] = (int16_t)nnzk++;
-    }
-    for (int k = 0; k < N; ++k) {
+    if (!colloc) {
+        // structural sparsity of dPhi/d(x_k, u_k), as CasADi derives it symbolically: dependency bitmasks
+        // pushed through the RHS and the RK stages (identical for every interval)
+        uint64_t dep[5];
+        structure_pattern(h->model, h->scheme, p->n_steps, nx, nu, dep);
         for (int r = 0; r < nx; ++r) {
-            for (int c = 0; c < nz; ++c) {
-                if (!(dep[r] >> c & 1ull)) continue;
+            for (int c = 0; c < kMaxNz; ++c) kp.jpos[r][c] = -1;
+            for (int c = 0; c < nz; ++c)
+                if (dep[r] >> c & 1ull) kp.jpos[r][c] = (int16_t)nnzk++;
+            kp.jneg[r] = (int16_t)nnzk++;
+        }
+        for (int k = 0; k < N; ++k) {
+            for (int r = 0; r < nx; ++r) {
+                for (int c = 0; c < nz; ++c) {
+                    if (!(dep[r] >> c & 1ull)) continue;
+                    h->jrow.push_back(k * ngk + r);
+                    h->jcol.push_back(k * nz + c);
+                }
                 h->jrow.push_back(k * ngk + r);
-                h->jcol.push_back(k * nz + c);
+                h->jcol.push_back((k + 1) * nz + r);
             }
-            h->jrow.push_back(k * ngk + r);
-            h->jcol.push_back((k + 1) * nz + r);
+        }
+    } else {
+        // collocation (cfx_colloc.h): defect rows [x^0_r..x^d_r, other states of point j, controls], then
+        // continuity rows [x^0_r..x^d_r, -1 on x_{k+1}^0_r]
+        for (int k = 0; k < N; ++k) {
+            const size_t before = h->jrow.size();
+            auto put = [&](int row, int col) {
+                h->jrow.push_back(row);
+                h->jcol.push_back(col);
+            };
+            for (int j = 1; j <= deg; ++j)
+                for (int r = 0; r < nx; ++r) {
+                    const int row = k * ngk + (j - 1) * nx + r;
+                    for (int i = 0; i <= deg; ++i) put(row, k * nz + i * nx + r);
+                    for (int c = 0; c < nx; ++c)
+                        if (c != r && (col_xdeps(h->model, r) >> c & 1u)) put(row, k * nz + j * nx + c);
+                    for (int c = 0; c < col_udeps(h->model, r, nu); ++c) put(row, k * nz + uoff + c);
+                }
+            for (int r = 0; r < nx; ++r) {
+                const int row = k * ngk + deg * nx + r;
+                for (int i = 0; i <= deg; ++i) put(row, k * nz + i * nx + r);
+                put(row, (k + 1) * nz + r);
+            }
+            nnzk = (int)(h->jrow.size() - before);
         }
     }
     std::vector<int32_t> sl_param, sl_joff;
@@ -414,25 +551,47 @@ extern "C" int cfx_create(const cfx_problem* p, cfx_handle** out) {
                 const bool valid = pi >= 0 && pi <= idx;
                 sl_param.push_back(valid ? pi : -1);
                 sl_joff.push_back((int32_t)h->jrow.size());
-                h->jrow.push_back(k * ngk + nx + j);
-                h->jcol.push_back(k * nz + nx + j);
+                h->jrow.push_back(k * ngk + (ngk - n_slide) + j);
+                h->jcol.push_back(k * nz + uoff + j);
                 if (valid) {
-                    h->jrow.push_back(k * ngk + nx + j);
+                    h->jrow.push_back(k * ngk + (ngk - n_slide) + j);
                     h->jcol.push_back(p_off + pi);
                 }
             }
         }
     }
     h->sz.nnz_jac = (int64_t)h->jrow.size();
-    for (int k = 0; k < N; ++k)
-        for (int i = 0; i < nz; ++i)
-            for (int j = 0; j <= i; ++j) {
-                h->hrow.push_back(k * nz + i);
-                h->hcol.push_back(k * nz + j);
+    auto hput = [&](int r, int c) {
+        h->hrow.push_back(r);
+        h->hcol.push_back(c);
+    };
+    std::vector<int32_t> hdiag((size_t)(N + 1) * (nx + nu), -1);  // objective-term diagonal positions
+    for (int k = 0; k < N; ++k) {
+        if (!colloc) {
+            for (int i = 0; i < nz; ++i) {
+                hdiag[(size_t)k * (nx + nu) + i] = (int32_t)(k * nhk + i * (i + 1) / 2 + i);
+                for (int j = 0; j <= i; ++j) hput(k * nz + i, k * nz + j);
             }
+        } else {
+            for (int r = 0; r < nx; ++r) {
+                hdiag[(size_t)k * (nx + nu) + r] = (int32_t)(k * nhk + r);
+                hput(k * nz + r, k * nz + r);
+            }
+            for (int j = 1; j <= deg; ++j) {
+                for (int a = 0; a < nx; ++a)
+                    for (int b = 0; b <= a; ++b) hput(k * nz + j * nx + a, k * nz + j * nx + b);
+                for (int a = 0; a < nu; ++a)
+                    for (int b = 0; b < nx; ++b) hput(k * nz + uoff + a, k * nz + j * nx + b);
+            }
+            for (int a = 0; a < nu; ++a) {
+                hdiag[(size_t)k * (nx + nu) + nx + a] = (int32_t)(k * nhk + nx + deg * per_point + a * (a + 1) / 2 + a);
+                for (int b = 0; b <= a; ++b) hput(k * nz + uoff + a, k * nz + uoff + b);
+            }
+        }
+    }
     for (int r = 0; r < nx; ++r) {
-        h->hrow.push_back(N * nz + r);
-        h->hcol.push_back(N * nz + r);
+        hdiag[(size_t)N * (nx + nu) + r] = (int32_t)(N * nhk + r);
+        hput(N * nz + r, N * nz + r);
     }
     h->sz.nnz_hess = (int64_t)h->hrow.size();
 
@@ -445,7 +604,10 @@ extern "C" int cfx_create(const cfx_problem* p, cfx_handle** out) {
     kp.nu = nu;
     kp.nz = nz;
     kp.T = T;
-    kp.Q = p->n_steps * h->stages;
+    kp.Q = colloc ? deg : p->n_steps * h->stages;
+    kp.uoff = uoff;
+    kp.deg = deg;
+    if (colloc) collocation_coefficients(deg, p->scheme == CFX_COLLOCATION_RADAU, h->tau, kp.colC, kp.colD);
     kp.ngk = ngk;
     kp.nnzk = nnzk;
     kp.nhk = nhk;
@@ -498,8 +660,14 @@ extern "C" int cfx_create(const cfx_problem* p, cfx_handle** out) {
     h->stream = h->own_stream;
 
     std::vector<double> tab, cna;
-    build_tables(h, tab);
-    if (!hmed) {
+    if (colloc) {
+        build_colloc_tables(h, tab);
+        kp.tstride = deg;
+    } else {
+        build_tables(h, tab);
+    }
+    if (colloc) {
+    } else if (!hmed) {
         std::vector<double> cnb;
         affine_calcium(h, tab, cna, cnb);
         tab.swap(cnb);
@@ -519,7 +687,8 @@ extern "C" int cfx_create(const cfx_problem* p, cfx_handle** out) {
     {
         const int dj = hjet_of(h->model);
         h->hbs = hsplit_of(h->model) ? dj / 2 : dj;
-        const int nb = (nz + h->hbs - 1) / h->hbs;
+        const int ndir = colloc ? nx + nu : nz;  // collocation: directions of one point (x^j, u)
+        const int nb = (ndir + h->hbs - 1) / h->hbs;
         for (int I = 0; I < nb; ++I)
             for (int J = I; J < nb; ++J) htasks.push_back(HTask{(int16_t)I, (int16_t)J});
         h->n_htasks = (int)htasks.size();
@@ -538,11 +707,13 @@ extern "C" int cfx_create(const cfx_problem* p, cfx_handle** out) {
         !upload((void**)&h->d_targets, targets.data(), targets.size() * sizeof(double)) ||
         !upload((void**)&h->d_sl_param, sl_param.data(), sl_param.size() * sizeof(int32_t)) ||
         !upload((void**)&h->d_sl_joff, sl_joff.data(), sl_joff.size() * sizeof(int32_t)) ||
-        !upload((void**)&h->d_htasks, htasks.data(), htasks.size() * sizeof(HTask)))
+        !upload((void**)&h->d_htasks, htasks.data(), htasks.size() * sizeof(HTask)) ||
+        !upload((void**)&h->d_hdiag, hdiag.data(), hdiag.size() * sizeof(int32_t)))
         return create_fail(h, CFX_ENOMEM, "cfx_create: device allocation/upload failed");
     kp.tab = h->d_tab;
     kp.cna = h->d_cna;
     kp.rest = h->d_rest;
+    kp.hdiag = h->d_hdiag;
     *out = h;
     return CFX_OK;
 }
@@ -555,8 +726,8 @@ extern "C" void cfx_destroy(cfx_handle* h) {
         if (h->main[s].p) (void)hipFree(h->main[s].p);
         if (h->stage[s].p) (void)hipFree(h->stage[s].p);
     }
-    for (void* p : {(void*)h->d_tab, (void*)h->d_rest, (void*)h->d_cna, (void*)h->d_htasks, (void*)h->d_obj, (void*)h->d_targets, (void*)h->d_sl_param,
-                    (void*)h->d_sl_joff})
+    for (void* p : {(void*)h->d_tab, (void*)h->d_rest, (void*)h->d_cna, (void*)h->d_htasks, (void*)h->d_obj,
+                    (void*)h->d_targets, (void*)h->d_sl_param, (void*)h->d_sl_joff, (void*)h->d_hdiag})
         if (p) (void)hipFree(p);
     if (h->own_stream) (void)hipStreamDestroy(h->own_stream);
     delete h;
@@ -600,6 +771,7 @@ extern "C" int cfx_hess_structure(const cfx_handle* h, int32_t* row, int32_t* co
 // evaluation
 // ------------------------------------------------------------------------------------------------------
 static hipError_t launch_shooting(cfx_handle* h, bool derivs, const double* V, double* G, double* J) {
+    if (h->colloc) return launch_colloc(h->model, h->tmax, h->kp, V, G, derivs ? J : nullptr, h->stream);
     if (is_int(h->model)) return launch_shooting_hmed(h->model, h->scheme, derivs, h->tmax, h->kp, V, G, J, h->stream);
     // 16-byte lane accesses need 16-byte aligned buffers (B % NI == 0 keeps every row aligned)
     auto aligned = [](const void* p) { return ((uintptr_t)p & 15u) == 0; };
@@ -673,8 +845,12 @@ extern "C" int cfx_eval_h(cfx_handle* h, const double* v, const double* obj_fact
     if (!LAM) return rc;
     double* H = stage_out(h, S_OUT, hess, h->sz.nnz_hess, flags, &rc);
     if (!H) return rc;
-    CFX_HIP(h, launch_hessian(h->model, h->scheme, h->tmax, h->kp, h->d_htasks, h->n_htasks, h->hbs, V, LAM, H,
-                              h->stream));
+    if (h->colloc)
+        CFX_HIP(h, launch_colloc_hess(h->model, h->tmax, h->kp, h->d_htasks, h->n_htasks, h->hbs, V, LAM, H,
+                                      h->stream));
+    else
+        CFX_HIP(h, launch_hessian(h->model, h->scheme, h->tmax, h->kp, h->d_htasks, h->n_htasks, h->hbs, V, LAM, H,
+                                  h->stream));
     if (h->n_obj)
         hipLaunchKernelGGL(k_objective_hess, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, h->stream, h->kp,
                            h->n_obj, h->d_obj, OF, H);
@@ -685,6 +861,7 @@ extern "C" int cfx_eval_h(cfx_handle* h, const double* v, const double* obj_fact
 
 extern "C" int cfx_integrate(cfx_handle* h, const double* x0, const double* u, double* traj, uint32_t flags) {
     if (!h || !traj) return CFX_EINVAL;
+    if (h->colloc) return fail(h, CFX_EUNSUPPORTED, "cfx_integrate: not available for a collocation transcription");
     if (h->sz.nu > 0 && !u) return fail(h, CFX_EINVAL, "cfx_integrate: this model needs per-interval controls");
     CFX_HIP(h, hipSetDevice(h->device));
     int rc = CFX_OK;

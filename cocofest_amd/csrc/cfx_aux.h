@@ -32,7 +32,7 @@ __global__ void __launch_bounds__(256) k_objective(const KParams P, int n_obj, c
     for (int t = 0; t < n_obj; ++t) {
         const DevObjective o = obj[t];
         for (int k = o.node_first; k <= o.node_last; ++k) {
-            const int64_t off = (int64_t)k * P.nz + (o.var_kind == 0 ? 0 : P.nx) + o.var_index;
+            const int64_t off = (int64_t)k * P.nz + (o.var_kind == 0 ? 0 : P.uoff) + o.var_index;
             const double z = V[off * B + b];
             const double tgt = o.target_off >= 0 ? targets[o.target_off + k] : o.target_value;
             const double d = z - tgt;
@@ -53,14 +53,9 @@ __global__ void __launch_bounds__(256) k_objective_hess(const KParams P, int n_o
     const double s = obj_factor[b];
     for (int t = 0; t < n_obj; ++t) {
         const DevObjective o = obj[t];
-        const int e = (o.var_kind == 0 ? 0 : P.nx) + o.var_index;  // position inside the node block
+        const int e = (o.var_kind == 0 ? 0 : P.nx) + o.var_index;  // element of (x_k, u_k)
         for (int k = o.node_first; k <= o.node_last; ++k) {
-            int64_t hoff;
-            if (k == P.N) {
-                hoff = (int64_t)P.N * P.nhk + e;  // x_N diagonal
-            } else {
-                hoff = (int64_t)k * P.nhk + e * (e + 1) / 2 + e;
-            }
+            const int64_t hoff = P.hdiag[k * (P.nx + P.nu) + e];
             H[hoff * B + b] += 2.0 * o.w_eff * s;
         }
     }
@@ -76,14 +71,15 @@ __global__ void __launch_bounds__(256) k_slide(const KParams P, const int32_t* _
     const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= B) return;
     const int64_t p_off = (int64_t)P.N * P.nz + P.nx;
+    const int g_off = P.ngk - P.n_slide;  // the window rows follow the interval's dynamics rows
     for (int k = 0; k < P.N; ++k) {
         for (int j = 0; j < P.T; ++j) {
             const int slot = k * P.T + j;
             const int pi = sl_param[slot];
             if (G) {
-                const double u = V[((int64_t)k * P.nz + P.nx + j) * B + b];
+                const double u = V[((int64_t)k * P.nz + P.uoff + j) * B + b];
                 const double w = pi >= 0 ? V[(p_off + pi) * B + b] : floor_value;
-                G[((int64_t)k * P.ngk + P.nx + j) * B + b] = u - w;
+                G[((int64_t)k * P.ngk + g_off + j) * B + b] = u - w;
             }
             if (J) {
                 const int64_t jo = sl_joff[slot];

@@ -32,6 +32,7 @@ constexpr int stages_of(int scheme) { return scheme == 4 ? 4 : (scheme == 2 ? 2 
 
 
 constexpr int kMaxNz = 5 + 32;  // nx + truncation
+constexpr int kMaxDeg = 9;      // collocation polynomial degree
 
 // Everything a kernel needs, passed by value (kernel argument segment).
 struct KParams {
@@ -62,6 +63,14 @@ struct KParams {
     // J_g value offset, inside an interval block, of dPhi_r/dz_c (-1: structural zero) and of the -1 on x_{k+1}[r]
     int16_t jpos[5][kMaxNz];
     int16_t jneg[5];
+    // offset of u_k inside an interval's decision block (nx for shooting, (deg+1) nx for collocation)
+    int32_t uoff;
+    // direct collocation (cfx_colloc.h): polynomial degree, C[i][j] = l_i'(tau_j), D[i] = l_i(1)
+    int32_t deg;
+    double colC[kMaxDeg + 1][kMaxDeg + 1];
+    double colD[kMaxDeg + 1];
+    // Hessian value index of the diagonal entry of (node k, element e), e < nx + nu, k <= N (objective terms)
+    const int32_t* hdiag;
 };
 
 // 1/x from v_rcp_f64 (relative error <= 4.6e-8 measured on MI355X) and one cubic correction

@@ -42,6 +42,12 @@ constexpr bool hsplit_of(int model) { return model != M_D03 && model != M_D07; }
 hipError_t launch_hessian(int model, int scheme, int tmax, const KParams& P, const HTask* tasks, int ntasks, int bs,
                           const double* V, const double* LAM, double* H, hipStream_t s);
 
+// direct collocation (cfx_colloc.h, instantiated in cfx_inst_colloc.hip)
+hipError_t launch_colloc(int model, int tmax, const KParams& P, const double* V, double* G, double* J,
+                         hipStream_t s);
+hipError_t launch_colloc_hess(int model, int tmax, const KParams& P, const HTask* tasks, int ntasks, int bs,
+                              const double* V, const double* LAM, double* H, hipStream_t s);
+
 template <int MODEL, int SCHEME, int DJ, int TMAX>
 hipError_t launch_hessian_t(const KParams& P, const HTask* tasks, int ntasks, int bs, const double* V,
                             const double* LAM, double* H, hipStream_t s) {

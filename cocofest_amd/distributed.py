@@ -81,9 +81,8 @@ class IntervalShardedNlp:
         else:
             self.h = evaluator(self.sub, batch)
             self.dev = torch.device("cpu") if device is None else torch.device(device)
-        o = ocp
-        self.nz = o.nx + o.nu
-        self.ngk = o.nx + (o.nu if (o.n_params and o.last_stim_idx is not None) else 0)
+        self.nz = ocp.nzb   # decision block of one interval (shooting or collocation)
+        self.ngk = ocp.ngk  # constraint rows of one interval
         self._exchange_structures()
 
     # ---- global structure and the local -> global maps ------------------------------------------------

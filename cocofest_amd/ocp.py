@@ -106,39 +106,73 @@ class FesOcp:
         self.truncation = model._sum_stim_truncation
 
     # ---- layout -------------------------------------------------------------------------------------
+    # Decision vector per instance: per interval k the block [x_k, u_k] (multiple shooting) or
+    # [x_k^0, x_k^1..x_k^d, u_k] (direct collocation, degree d), then x_N, then the parameters.
+    @property
+    def degree(self):
+        return self.ode_solver.polynomial_degree if isinstance(self.ode_solver, OdeSolver.COLLOCATION) else 0
+
+    @property
+    def uoff(self):
+        return (self.degree + 1) * self.nx if self.degree else self.nx
+
+    @property
+    def nzb(self):
+        """Size of one interval's decision block."""
+        return self.uoff + self.nu
+
+    @property
+    def ngk(self):
+        """Constraint rows per interval (dynamics rows, then the Hmed sliding-window rows)."""
+        n_slide = self.nu if (self.n_params and self.last_stim_idx is not None) else 0
+        return (self.degree + 1) * self.nx + n_slide if self.degree else self.nx + n_slide
+
     @property
     def nv(self):
-        return self.n_shooting * (self.nx + self.nu) + self.nx + self.n_params
+        return self.n_shooting * self.nzb + self.nx + self.n_params
 
-    def pack(self, x, u=None, p=None):
-        """(nx, N+1) states, (nu, N) controls, (n_params,) parameters -> decision vector (nv,)."""
-        N, nx, nu = self.n_shooting, self.nx, self.nu
+    def pack(self, x, u=None, p=None, x_points=None):
+        """(nx, N+1) node states, (nu, N) controls, (n_params,) parameters -> decision vector (nv,).
+        Collocation states: ``x_points`` (nx, N, d), by default each interval's start node state."""
+        N, nx, nu, d, nzb = self.n_shooting, self.nx, self.nu, self.degree, self.nzb
+        x = np.asarray(x, dtype=float)
         v = np.empty(self.nv)
-        body = v[: N * (nx + nu)].reshape(N, nx + nu)
-        body[:, :nx] = np.asarray(x)[:, :N].T
+        body = v[: N * nzb].reshape(N, nzb)
+        body[:, :nx] = x[:, :N].T
+        if d:
+            xp = np.repeat(x[:, :N, None], d, axis=2) if x_points is None else np.asarray(x_points, dtype=float)
+            body[:, nx: (d + 1) * nx] = xp.transpose(1, 2, 0).reshape(N, d * nx)
         if nu:
-            body[:, nx:] = np.asarray(u).T
-        v[N * (nx + nu): N * (nx + nu) + nx] = np.asarray(x)[:, N]
+            body[:, self.uoff:] = np.asarray(u).T
+        v[N * nzb: N * nzb + nx] = x[:, N]
         if self.n_params:
-            v[N * (nx + nu) + nx:] = p
+            v[N * nzb + nx:] = p
         return v
 
     def unpack(self, v):
-        N, nx, nu = self.n_shooting, self.nx, self.nu
+        N, nx, nu, nzb = self.n_shooting, self.nx, self.nu, self.nzb
         v = np.asarray(v)
-        body = v[: N * (nx + nu)].reshape(N, nx + nu)
-        x = np.concatenate([body[:, :nx].T, v[N * (nx + nu): N * (nx + nu) + nx, None]], axis=1)
+        body = v[: N * nzb].reshape(N, nzb)
+        x = np.concatenate([body[:, :nx].T, v[N * nzb: N * nzb + nx, None]], axis=1)
         states = {name: x[i][np.newaxis, :] for i, name in enumerate(self.model.name_dof)}
         controls = {}
         if nu:
             key = "last_pulse_width" if isinstance(self.model, DingModelPulseWidthFrequency) else "pulse_intensity"
-            controls[key] = body[:, nx:].T
-        params = {"pulse_intensity": v[N * (nx + nu) + nx:]} if self.n_params else {}
+            controls[key] = body[:, self.uoff:].T
+        params = {"pulse_intensity": v[N * nzb + nx:]} if self.n_params else {}
         return states, controls, params
 
     def bounds_vector(self):
-        lo = self.pack(self.x_bounds[0], self.u_bounds[0] if self.nu else None, self.p_bounds[0])
-        hi = self.pack(self.x_bounds[1], self.u_bounds[1] if self.nu else None, self.p_bounds[1])
+        """Collocation points of interval k take the bounds of the intermediate nodes (column max(k, 1)), so the
+        fixed initial node does not pin the first interval's interior states."""
+        pts = None
+        if self.degree:
+            cols = np.minimum(np.maximum(np.arange(self.n_shooting), 1), self.n_shooting)
+            pts = [np.repeat(np.asarray(b, dtype=float)[:, cols, None], self.degree, axis=2) for b in self.x_bounds]
+        lo = self.pack(self.x_bounds[0], self.u_bounds[0] if self.nu else None, self.p_bounds[0],
+                       x_points=None if pts is None else pts[0])
+        hi = self.pack(self.x_bounds[1], self.u_bounds[1] if self.nu else None, self.p_bounds[1],
+                       x_points=None if pts is None else pts[1])
         return lo, hi
 
     def initial_guess_vector(self):
@@ -147,8 +181,6 @@ class FesOcp:
     # ---- GPU callbacks ------------------------------------------------------------------------------
     def nlp(self, batch: int = 1, layout: str = "aos", device: int = 0) -> _cfx.Handle:
         """Open a libcfx handle evaluating ``batch`` instances of this problem on GPU ``device``."""
-        if isinstance(self.ode_solver, OdeSolver.COLLOCATION):
-            raise NotImplementedError("COLLOCATION transcription is not available in libcfx yet")
         return _cfx.Handle(
             model_id=self.model.cfx_model_id, constants=self.model.cfx_constants(), scheme=self.ode_solver.scheme,
             n_steps=self.ode_solver.n_integration_steps, n_shooting=self.n_shooting,

@@ -35,14 +35,22 @@ class OdeSolver:
         scheme = _cfx.RK4
 
     class COLLOCATION:
-        """Direct collocation (accepted by the reference's sanity check, fes_ocp.py:334-338)."""
-
-        scheme = None
+        """Direct collocation (accepted by the reference's sanity check, fes_ocp.py:334-338; bioptim's
+        defaults: degree 4, Legendre points): one Lagrange polynomial per shooting interval through the node
+        state and ``polynomial_degree`` collocation points (Legendre or Radau IIA), controls held constant."""
 
         def __init__(self, polynomial_degree: int = 4, method: str = "legendre"):
+            if not isinstance(polynomial_degree, int) or not 1 <= polynomial_degree <= 9:
+                raise ValueError("polynomial_degree must be an int in [1, 9]")
+            if method not in ("legendre", "radau"):
+                raise ValueError("method must be 'legendre' or 'radau'")
             self.polynomial_degree = polynomial_degree
             self.method = method
             self.n_integration_steps = polynomial_degree
+            self.scheme = _cfx.COLLOCATION_LEGENDRE if method == "legendre" else _cfx.COLLOCATION_RADAU
+
+        def __repr__(self):
+            return f"COLLOCATION(polynomial_degree={self.polynomial_degree}, method={self.method!r})"
 
 
 class ControlType(Enum):

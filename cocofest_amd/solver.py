@@ -105,13 +105,32 @@ class BatchedIpm:
         hsel = np.where((posF[hr] >= 0) & (posF[hc] >= 0))[0]
         jrF, jcF = jr[jsel], posF[jc[jsel]]
         hrF, hcF = posF[hr[hsel]], posF[hc[hsel]]
-        # unknown u: variable j -> key j; constraint row i -> midpoint of the free columns it couples
-        cmin = np.full(m, np.inf)
-        cmax = np.full(m, -np.inf)
-        np.minimum.at(cmin, jrF, jcF)
-        np.maximum.at(cmax, jrF, jcF)
-        ckey = np.where(np.isfinite(cmin), 0.5 * (cmin + cmax) + 0.25, nf)
-        key = np.concatenate([np.arange(nf, dtype=np.float64), ckey])
+        # unknown u: variable j -> key j; constraint row i -> midpoint of the keys of the free columns it couples.
+        # Parameters sit at the end of the decision vector but each is used by a few neighbouring rows only
+        # (the Hmed sliding windows): they take the mean key of the rows that use them.
+        vkey = np.arange(nf, dtype=np.float64)
+        n_par = int(getattr(self.ocp, "n_params", 0) or 0)
+        par = np.zeros(nf, dtype=bool)
+        if n_par:
+            par = self.free >= self.n - n_par
+
+        def row_keys(vk, skip):
+            sel = ~skip[jcF]
+            cmin = np.full(m, np.inf)
+            cmax = np.full(m, -np.inf)
+            np.minimum.at(cmin, jrF[sel], vk[jcF[sel]])
+            np.maximum.at(cmax, jrF[sel], vk[jcF[sel]])
+            return np.where(np.isfinite(cmin), 0.5 * (cmin + cmax) + 0.25, nf)
+
+        ckey = row_keys(vkey, par)
+        if par.any():
+            ssum = np.zeros(nf)
+            cnt = np.zeros(nf)
+            np.add.at(ssum, jcF, ckey[jrF])
+            np.add.at(cnt, jcF, 1.0)
+            vkey = np.where(par & (cnt > 0), ssum / np.maximum(cnt, 1.0) + 0.1, vkey)
+            ckey = row_keys(vkey, np.zeros(nf, dtype=bool))
+        key = np.concatenate([vkey, ckey])
         order = np.argsort(key, kind="stable")
         pos = np.empty(nf + m, dtype=np.int64)
         pos[order] = np.arange(nf + m)

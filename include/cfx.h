@@ -63,6 +63,12 @@ extern "C" {
 #define CFX_RK1 1
 #define CFX_RK2 2
 #define CFX_RK4 4
+/* direct collocation (OdeSolver.COLLOCATION(polynomial_degree, method)): one Lagrange polynomial per shooting
+   interval through the node state and `n_steps` (= the degree d, 1..9) Legendre or Radau IIA points.
+   Decision block per interval [x_k^0, x_k^1..x_k^d, u_k]; rows per interval: d defect blocks of nx, the
+   continuity block of nx, then the sliding-window rows.  cfx_integrate is not available for it. */
+#define CFX_COLLOCATION_LEGENDRE 16
+#define CFX_COLLOCATION_RADAU 17
 
 /* layouts and call flags */
 #define CFX_LAYOUT_AOS 0
@@ -102,8 +108,8 @@ typedef struct cfx_objective {
 typedef struct cfx_problem {
     int32_t abi_version; /* CFX_ABI_VERSION */
     int32_t model;       /* CFX_DING2003 ... CFX_HMED2018_FATIGUE */
-    int32_t scheme;      /* CFX_RK1 | CFX_RK2 | CFX_RK4 */
-    int32_t n_steps;     /* RK sub-steps per shooting interval (n_integration_steps) */
+    int32_t scheme;      /* CFX_RK1 | CFX_RK2 | CFX_RK4 | CFX_COLLOCATION_LEGENDRE | CFX_COLLOCATION_RADAU */
+    int32_t n_steps;     /* RK sub-steps per shooting interval (n_integration_steps); collocation degree */
     int32_t n_shooting;  /* N */
     int32_t truncation;  /* sum_stim_truncation T (<= 32) */
     int32_t n_params;    /* Hmed pulse-intensity parameters (0: no sliding-window constraints) */

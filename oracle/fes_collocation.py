@@ -44,6 +44,9 @@ def collocation_points(d: int, method: str = "legendre") -> np.ndarray:
         c[d] = 1.0
         c[d - 1] = -1.0
         x = np.sort(np.real(np.polynomial.legendre.legroots(c)))
+        dc = np.polynomial.legendre.legder(c)
+        for _ in range(4):  # Newton polish: companion-matrix roots are only good to ~1e-14
+            x[:-1] -= np.polynomial.legendre.legval(x[:-1], c) / np.polynomial.legendre.legval(x[:-1], dc)
         x[-1] = 1.0
     else:
         raise ValueError(f"unknown collocation method {method}")
@@ -55,14 +58,15 @@ def coefficients(d: int, method: str = "legendre"):
     tau = np.concatenate([[0.0], collocation_points(d, method)])
     C = np.zeros((d + 1, d + 1))
     D = np.zeros(d + 1)
-    for i in range(d + 1):
-        others = [tau[r] for r in range(d + 1) if r != i]
-        den = np.prod([tau[i] - t for t in others])
-        poly = np.poly1d(others, r=True) / den
-        D[i] = poly(1.0)
-        dp = poly.deriv()
-        for j in range(d + 1):
-            C[i, j] = dp(tau[j])
+    idx = range(d + 1)
+    for i in idx:
+        D[i] = np.prod([(1.0 - tau[r]) / (tau[i] - tau[r]) for r in idx if r != i])
+        for j in idx:
+            if j == i:  # l_i'(tau_i) = sum_{r != i} 1 / (tau_i - tau_r)
+                C[i, j] = sum(1.0 / (tau[i] - tau[r]) for r in idx if r != i)
+            else:  # l_i'(tau_j) = prod_{r != i, j} (tau_j - tau_r) / (tau_i - tau_r) / (tau_i - tau_j)
+                C[i, j] = np.prod([(tau[j] - tau[r]) / (tau[i] - tau[r]) for r in idx if r not in (i, j)]) / (
+                    tau[i] - tau[j])
     return tau, C, D
 
 

@@ -86,3 +86,31 @@ def cfg3(fatigue=False):
     stims = [float(v) for v in np.round(np.linspace(0, 1, 31)[:-1], 2)]
     return dict(name="ding2007_with_fatigue" if fatigue else "ding2007", stims=stims, final_time=1.0, truncation=10,
                 scheme="RK1", m=10, objective=None, n_shooting=None)
+
+
+def random_collocation_decision(pb, B, seed=0):
+    """Decision vectors (B, nv) of a collocation problem (oracle ColProblem): node states / controls / parameters
+    as random_decision, collocation states within +-20 % of their interval's start state."""
+    from oracle import fes_oracle as O
+
+    base_pb = O.Problem(**{f: getattr(pb, f) for f in O.Problem.__dataclass_fields__})
+    base = random_decision(base_pb, B, seed)
+    X, U, P = base_pb.unpack(base)
+    rng = np.random.default_rng(seed + 1)
+    XC = np.repeat(X[:, :-1, None, :], pb.degree + 1, axis=2)
+    XC[:, :, 1:, :] *= rng.uniform(0.8, 1.2, (B, pb.n_shooting, pb.degree, pb.nx))
+    return pb.pack(XC, X[:, -1], U if pb.nu else None, P if pb.n_params else None)
+
+
+def product_collocation_ocp(name, stims, final_time, truncation, degree=3, method="legendre", objective=None,
+                            n_shooting=None, intensity_params=True):
+    from cocofest_amd import ModelMaker, OcpFes, OdeSolver
+
+    model = ModelMaker.create_model(name, stim_time=list(stims), sum_stim_truncation=truncation)
+    kw = {}
+    if name.startswith("ding2007"):
+        kw["pulse_width"] = {"min": model.pd0, "max": 0.0006}
+    if name.startswith("hmed2018") and intensity_params:
+        kw["pulse_intensity"] = {"max": 130}
+    return OcpFes.prepare_ocp(model=model, final_time=final_time, objective=objective or {},
+                              ode_solver=OdeSolver.COLLOCATION(degree, method), n_shooting=n_shooting, **kw)

