@@ -134,6 +134,45 @@ def convergence(device):
     return out
 
 
+def collocation_section(device, steps=50):
+    """The same cfg-2 problem transcribed by direct collocation (OdeSolver.COLLOCATION(4, "legendre"), bioptim's
+    default degree): g + J_g throughput of k_colloc over a device-resident SoA batch, and its algorithmic HBM
+    bandwidth (read v, write g and J_g values)."""
+    import torch
+
+    from cocofest_amd import ModelMaker, OcpFes, OdeSolver
+
+    model = ModelMaker.create_model("ding2003", stim_time=[round(0.1 * i, 1) for i in range(10)],
+                                    sum_stim_truncation=20)
+    ocp = OcpFes.prepare_ocp(model=model, final_time=1, objective={"end_node_tracking": 100},
+                             ode_solver=OdeSolver.COLLOCATION(4, "legendre"), n_shooting=20)
+    B = 1 << 18
+    h = ocp.nlp(batch=B, layout="soa", device=device)
+    dev = f"cuda:{device}"
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(7)
+    v = torch.rand((h.nv, B), generator=gen, dtype=torch.float64, device=dev)
+    v *= torch.tensor([1.5, 250.0] * (h.nv // 2), dtype=torch.float64, device=dev)[:, None]
+    g = torch.empty((h.ng, B), dtype=torch.float64, device=dev)
+    jac = torch.empty((h.nnz_jac, B), dtype=torch.float64, device=dev)
+    for _ in range(5):
+        h.eval_all(v, g=g, jac=jac)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(steps):
+        h.eval_all(v, g=g, jac=jac)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / steps
+    nbytes = 8 * (h.nv + h.ng + h.nnz_jac)
+    h.close()
+    return {"workload": "cfg2 by direct collocation, Legendre degree 4 (nv = 202, ng = 200)", "batch": B,
+            "nv": ocp.nv, "ng": int(ocp.n_shooting * ocp.ngk), "nnz_jac": nbytes // 8 - ocp.nv - ocp.n_shooting * ocp.ngk,
+            "ms_per_launch": ms, "instance_evals_per_s": B / (ms * 1e-3),
+            "achieved_GBps": nbytes * B / (ms * 1e-3) / 1e9, "bytes_per_instance": nbytes}
+
+
 def ivp_section(device):
     """IvpFes.integrate on the configuration of the reference's own timings
     (examples/sensitivity/truncation/sensitivity_analysis.py: DingModelFrequencyWithFatigue, 10 single pulses,
@@ -240,6 +279,7 @@ def main():
         cpu = cpu_baseline(ocp, args.cpu_seconds) if (world == 1 and args.cpu_seconds > 0) else None
         conv = convergence(local) if (world == 1 and not args.no_solve) else None
         ivp = ivp_section(local) if (world == 1 and not args.no_solve) else None
+        col = collocation_section(local) if (world == 1 and not args.no_solve) else None
         out = {
             "metric": METRIC,
             "value": value,
@@ -275,6 +315,7 @@ def main():
             "cpu_baseline": cpu,
             "convergence": conv,
             "ivp": ivp,
+            "collocation": col,
         }
     h.close()
     if dist:
