@@ -27,6 +27,8 @@ import numpy as np
 class IpmOptions:
     tol: float = 1e-6
     max_iter: int = 200
+    acceptable_tol: float = 1e-6  # Ipopt "solved to acceptable level": err <= acceptable_tol for
+    acceptable_iter: int = 15     # acceptable_iter consecutive iterations
     mu_init: float = 0.1
     bound_push: float = 1e-2
     tau_min: float = 0.99
@@ -230,7 +232,10 @@ class BatchedIpm:
         return hv
 
     # ---- main loop --------------------------------------------------------------------------------------
-    def solve(self, v0=None):
+    def solve(self, v0=None, fixed_values=None):
+        """Solve from ``v0`` (B, nv) (default: the problem's initial guess).  ``fixed_values`` (B, n_fixed)
+        overrides, per instance, the variables whose bounds coincide (e.g. each NMPC scenario's own initial
+        state); by default they take their bound."""
         torch = self.torch
         opt = self.opt
         B, nf, m = self.B, len(self.free), self.m
@@ -238,7 +243,10 @@ class BatchedIpm:
         if v0 is None:
             v0 = np.tile(self.ocp.initial_guess_vector(), (B, 1))
         v = torch.as_tensor(np.asarray(v0, dtype=np.float64), device=self.dev).clone()
-        v[:, self.fixed] = self.lb_full[self.fixed]
+        if fixed_values is None:
+            v[:, self.fixed] = self.lb_full[self.fixed]
+        else:
+            v[:, self.fixed] = torch.as_tensor(np.asarray(fixed_values, dtype=np.float64), device=self.dev)
         self._set_function_scaling(v)
         x = v[:, self.freeT] / self.d
         # push the start strictly inside the bounds (Ipopt bound_push / bound_frac)
@@ -262,6 +270,7 @@ class BatchedIpm:
         delta_w_last = torch.zeros((B,), dtype=torch.float64, device=self.dev)
         done = torch.zeros((B,), dtype=torch.bool, device=self.dev)
         iters = torch.zeros((B,), dtype=torch.int64, device=self.dev)
+        acc_count = torch.zeros((B,), dtype=torch.int64, device=self.dev)
         err0 = torch.full((B,), np.inf, dtype=torch.float64, device=self.dev)
         filt = torch.full((B, 64, 2), np.inf, dtype=torch.float64, device=self.dev)  # (theta, phi) pairs
         filt[:, :, 1] = -np.inf
@@ -292,7 +301,8 @@ class BatchedIpm:
             e_p = g.abs().amax(1) if m else torch.zeros_like(mu)
             e_c0 = torch.maximum(compl_l.abs().amax(1), compl_u.abs().amax(1)) / sc
             err0 = torch.maximum(torch.maximum(e_d, e_p), e_c0)
-            newly = (~done) & (err0 <= opt.tol)
+            acc_count = torch.where(err0 <= opt.acceptable_tol, acc_count + 1, torch.zeros_like(acc_count))
+            newly = (~done) & ((err0 <= opt.tol) | (acc_count >= opt.acceptable_iter))
             done = done | newly
             if bool(done.all()):
                 break

@@ -527,3 +527,40 @@ def test_interior_point_collocation_pulse_width():
     assert np.max(np.abs(CO.eval_g(pb, res.v))) < 1e-5
     lb, ub = ocp.bounds_vector()
     assert np.all(res.v >= lb - 1e-8) and np.all(res.v <= ub + 1e-8)
+
+
+def _gpu_nmpc(model, **kw):
+    from cocofest_amd import OdeSolver
+    from cocofest_amd.nmpc import FesNmpc
+    from cocofest_amd.solver import IpmOptions
+
+    return FesNmpc(model, cycle_duration=0.5, n_cycles_simultaneous=2, n_cycles_to_advance=1,
+                   ode_solver=OdeSolver.RK4(n_integration_steps=5), options=IpmOptions(tol=1e-9), **kw)
+
+
+@pytest.mark.parametrize("fatigue", [False, True])
+def test_nmpc_hmed_on_gpu_is_self_consistent(fatigue):
+    """Receding horizon over libcfx (Hmed2018 intensities, 3 cycles, 4 scenarios): see test_nmpc_cpu.py."""
+    from tests.test_nmpc_cpu import test_hmed_free_intensities_are_self_consistent
+
+    test_hmed_free_intensities_are_self_consistent(fatigue, batch=4, nmpc_factory=_gpu_nmpc)
+
+
+def test_nmpc_pulse_width_with_fatigue_on_gpu():
+    """The reference's own NMPC model (Ding2007 with fatigue, pulse widths): every window converges and the
+    committed pulse widths reproduce the committed states by forward integration."""
+    from cocofest_amd import DingModelPulseWidthFrequencyWithFatigue
+
+    from tests.test_nmpc_cpu import CYCLE, _forward
+
+    model = DingModelPulseWidthFrequencyWithFatigue(stim_time=CYCLE, sum_stim_truncation=4)
+    res = _gpu_nmpc(model, pulse_width={"min": model.pd0, "max": 0.0006}, objective={"end_node_tracking": 60.0},
+                    batch=3).solve(n_cycles=3)
+    assert all(c.all() for c in res.converged), res.iterations
+    pw = res.controls["last_pulse_width"]
+    stims = [t + 0.5 * c for c in range(3) for t in CYCLE]
+    for b in range(3):
+        ref = _forward("ding2007_with_fatigue", stims, 3, 4, controls=lambda tab, N, b=b: pw[b].T.reshape(N, 1),
+                       x0=None)
+        got = np.stack([res.states[k][b] for k in model.name_dof])
+        np.testing.assert_allclose(got, ref, rtol=1e-6, atol=1e-6)

@@ -1,0 +1,95 @@
+"""Receding-horizon control (cocofest_amd/nmpc.py) on the CPU with the oracle as evaluator: window shifting,
+stimulation history and the Hmed history intensities are checked against single forward integrations of the
+whole committed horizon."""
+
+import numpy as np
+import pytest
+
+from oracle import fes_oracle as O
+from tests.oracle_handle import DenseBandSolver, OracleHandle, oracle_problem_from_ocp
+
+CYCLE = [0.0, 0.1, 0.2]  # three pulses per 0.5 s cycle
+
+
+def _nmpc(model, **kw):
+    from cocofest_amd import OdeSolver
+    from cocofest_amd.nmpc import FesNmpc
+    from cocofest_amd.solver import IpmOptions
+
+    return FesNmpc(model, cycle_duration=0.5, n_cycles_simultaneous=2, n_cycles_to_advance=1,
+                   ode_solver=OdeSolver.RK4(n_integration_steps=5), options=IpmOptions(tol=1e-9),
+                   evaluator=lambda ocp, B: OracleHandle(oracle_problem_from_ocp(ocp), B), band=DenseBandSolver(),
+                   torch_device="cpu", **kw)
+
+
+def _forward(name, stims, n_cycles, T, controls=None, x0=None):
+    c = O.model_constants(name)
+    N = 10 * n_cycles // 2
+    tab = O.stim_table(stims, N, 0.5 * n_cycles, T)
+    u = np.zeros((N, 0)) if controls is None else controls(tab, N)
+    return O.ivp_integrate(name, c, tab.rows, u, 0.5 * n_cycles, "RK4", 5, x0=x0)[:, ::5]
+
+
+def test_zero_dof_nmpc_equals_one_long_integration():
+    """Ding2003 (no controls): every window's optimum is the forward integration from its start state with its
+    stimulation history, so the committed horizon is one long integration with every pulse."""
+    from cocofest_amd import DingModelFrequency
+
+    model = DingModelFrequency(stim_time=CYCLE, sum_stim_truncation=4)
+    res = _nmpc(model, objective={"end_node_tracking": 50.0}, batch=1).solve(n_cycles=3)
+    assert all(c.all() for c in res.converged)
+    stims = [t + 0.5 * c for c in range(3) for t in CYCLE]
+    np.testing.assert_allclose(res.stim_time, stims)
+    ref = _forward("ding2003", stims, 3, 4)
+    got = np.stack([res.states["Cn"][0], res.states["F"][0]])
+    np.testing.assert_allclose(res.time, np.linspace(0, 1.5, 16), atol=1e-12)
+    np.testing.assert_allclose(got, ref, rtol=1e-7, atol=1e-7)
+
+
+def test_hmed_fixed_intensities_with_history_equal_one_long_integration():
+    """Hmed2018 with every intensity fixed (0 DOF): the history intensities carried from window to window must
+    reproduce the long integration in which every pulse has that intensity."""
+    from cocofest_amd import DingModelPulseIntensityFrequency
+
+    model = DingModelPulseIntensityFrequency(stim_time=CYCLE, sum_stim_truncation=4)
+    res = _nmpc(model, pulse_intensity={"fixed": 80.0}, objective={"end_node_tracking": 50.0}, batch=2).solve(
+        n_cycles=3)
+    assert all(c.all() for c in res.converged)
+    stims = [t + 0.5 * c for c in range(3) for t in CYCLE]
+    ref = _forward("hmed2018", stims, 3, 4, controls=lambda tab, N: np.full((N, 4), 80.0))
+    for b in range(2):
+        got = np.stack([res.states["Cn"][b], res.states["F"][b]])
+        np.testing.assert_allclose(got, ref, rtol=1e-7, atol=1e-7)
+    np.testing.assert_allclose(res.pulse_intensity, 80.0)
+
+
+@pytest.mark.parametrize("fatigue", [False])  # the fatigue variant runs on the GPU (test_gpu_parity.py)
+def test_hmed_free_intensities_are_self_consistent(fatigue, batch=1, nmpc_factory=None):
+    """Hmed2018 intensities optimised per window (end-force tracking): every window converges, intensities stay
+    in their bounds, and integrating the committed intensities from rest reproduces the committed states."""
+    from cocofest_amd import DingModelPulseIntensityFrequency, DingModelPulseIntensityFrequencyWithFatigue
+
+    cls = DingModelPulseIntensityFrequencyWithFatigue if fatigue else DingModelPulseIntensityFrequency
+    name = "hmed2018_with_fatigue" if fatigue else "hmed2018"
+    model = cls(stim_time=CYCLE, sum_stim_truncation=4)
+    res = (nmpc_factory or _nmpc)(model, pulse_intensity={"max": 130}, objective={"end_node_tracking": 40.0},
+                                  batch=batch).solve(n_cycles=3)
+    assert all(c.all() for c in res.converged), res.iterations
+    imin = O.min_pulse_intensity(O.model_constants(name))
+    assert res.pulse_intensity.min() >= imin - 1e-8 and res.pulse_intensity.max() <= 130 + 1e-8
+    stims = [t + 0.5 * c for c in range(3) for t in CYCLE]
+    for b in range(batch):
+        I = res.pulse_intensity[b]
+
+        def controls(tab, N, I=I):
+            # row k holds the last T pulses <= t_k; placeholder slots contribute nothing (any value)
+            out = np.empty((N, 4))
+            for k in range(N):
+                idx = [i for i, t in enumerate(stims) if t <= k * 0.1 + 1e-12][-4:]
+                vals = [I[i] for i in idx]
+                out[k] = [50.0] * (4 - len(vals)) + vals
+            return out
+
+        ref = _forward(name, stims, 3, 4, controls=controls)
+        got = np.stack([res.states[k][b] for k in model.name_dof])
+        np.testing.assert_allclose(got, ref, rtol=1e-6, atol=1e-6)
