@@ -41,6 +41,7 @@ def parse():
     ap.add_argument("--batch", type=int, default=1 << 20, help="instances per GPU")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline sample budget (0: skip)")
     ap.add_argument("--no-solve", action="store_true", help="skip the wall-clock-to-convergence section")
+    ap.add_argument("--nmpc-horizons", type=int, default=200, help="cfg-4 NMPC horizons (0: skip)")
     return ap.parse_args()
 
 
@@ -173,6 +174,34 @@ def collocation_section(device, steps=50):
             "achieved_GBps": nbytes * B / (ms * 1e-3) / 1e9, "bytes_per_instance": nbytes}
 
 
+def nmpc_section(device, n_windows, batch=64):
+    """cfg 4 (BASELINE.json configs[3]): Hmed2018 pulse-intensity NMPC, receding 1 s horizons of 10 pulses
+    (N = 10, truncation 10, RK1 x 10, the reference force curve tracked in every horizon), ``batch`` independent
+    scenarios (random initial states) advancing in lockstep on one GPU.  Horizons of one trajectory are
+    sequential; scenarios are what shards across GPUs."""
+    from cocofest_amd import DingModelPulseIntensityFrequency, OdeSolver
+    from cocofest_amd.nmpc import FesNmpc
+
+    ft = json.loads((ROOT / "tests" / "golden" / "ref_formulas.json").read_text())["misc"]["force_tracking"]
+    model = DingModelPulseIntensityFrequency(stim_time=[round(0.1 * i, 1) for i in range(10)], sum_stim_truncation=10)
+    nmpc = FesNmpc(model, cycle_duration=1.0, n_cycles_simultaneous=1, n_cycles_to_advance=1,
+                   objective={"force_tracking": [np.array(ft["time"]), np.array(ft["force"])]},
+                   pulse_intensity={"max": 130}, ode_solver=OdeSolver.RK1(n_integration_steps=10), batch=batch,
+                   device=device)
+    rng = np.random.default_rng(0)
+    x0 = np.stack([rng.uniform(0, 0.5, batch), rng.uniform(0, 50, batch)], axis=1)
+    t0 = time.perf_counter()
+    res = nmpc.solve(n_cycles=n_windows, x0=x0)
+    wall = time.perf_counter() - t0
+    its = np.stack(res.iterations)
+    conv = np.stack(res.converged)
+    return {"workload": "Hmed2018 pulse-intensity NMPC, 1 s horizons x 10 pulses, N = 10, truncation 10, RK1 x 10, "
+                        "force tracking per horizon", "horizons": n_windows, "scenarios": batch,
+            "wall_s": wall, "ms_per_horizon": wall / n_windows * 1e3,
+            "scenario_horizons_per_s": batch * n_windows / wall, "converged_frac": float(conv.mean()),
+            "iterations_median": float(np.median(its)), "iterations_max": int(its.max())}
+
+
 def ivp_section(device):
     """IvpFes.integrate on the configuration of the reference's own timings
     (examples/sensitivity/truncation/sensitivity_analysis.py: DingModelFrequencyWithFatigue, 10 single pulses,
@@ -280,6 +309,7 @@ def main():
         conv = convergence(local) if (world == 1 and not args.no_solve) else None
         ivp = ivp_section(local) if (world == 1 and not args.no_solve) else None
         col = collocation_section(local) if (world == 1 and not args.no_solve) else None
+        nm = nmpc_section(local, args.nmpc_horizons) if (world == 1 and not args.no_solve and args.nmpc_horizons) else None
         out = {
             "metric": METRIC,
             "value": value,
@@ -316,6 +346,7 @@ def main():
             "convergence": conv,
             "ivp": ivp,
             "collocation": col,
+            "nmpc": nm,
         }
     h.close()
     if dist:

@@ -137,16 +137,21 @@ class FesNmpc:
         warm = None
         n_windows = int(np.ceil(n_cycles / self.n_adv))
         t_off = 0.0
+        # windows whose stimulation history has the same times share one transcription (stim table, handle,
+        # KKT maps): with identical cycles that is every window after the first T pulses
+        cache = {}
         for w in range(n_windows):
             t0 = time.perf_counter()
-            ocp = self._window_ocp(hist_t, hist_i[0] if self.hmed else None)
-            if self.hmed:  # per-scenario history intensities: fixed leading parameters
-                pass
-            if self.evaluator is not None:
-                ipm = BatchedIpm(ocp, batch=B, options=self.options, handle=self.evaluator(ocp, B),
-                                 torch_device=self.torch_device, band=self.band)
-            else:
-                ipm = BatchedIpm(ocp, batch=B, device=self.device, options=self.options)
+            key = tuple(np.round(hist_t, 9))
+            if key not in cache:
+                ocp = self._window_ocp(hist_t, hist_i[0] if self.hmed else None)
+                if self.evaluator is not None:
+                    ipm = BatchedIpm(ocp, batch=B, options=self.options, handle=self.evaluator(ocp, B),
+                                     torch_device=self.torch_device, band=self.band)
+                else:
+                    ipm = BatchedIpm(ocp, batch=B, device=self.device, options=self.options)
+                cache[key] = (ocp, ipm)
+            ocp, ipm = cache[key]
             v0 = np.tile(ocp.initial_guess_vector(), (B, 1)) if warm is None else warm
             fixed = np.tile(ocp.bounds_vector()[0][ipm.fixed], (B, 1))
             # node-0 states are this window's start state per scenario; Hmed history intensities per scenario
@@ -163,7 +168,6 @@ class FesNmpc:
             v0 = v0.copy()
             v0[:, ipm.fixed] = fixed
             res = ipm.solve(v0, fixed_values=fixed)
-            ipm.close()
             result.iterations.append(res.iterations)
             result.converged.append(res.converged)
             # commit the first n_adv cycles
@@ -195,6 +199,8 @@ class FesNmpc:
             # warm start: shift by the committed nodes, repeat the last cycle
             warm = self._shift(ocp, V, adv_nodes)
             result.window_wall.append(time.perf_counter() - t0)
+        for _, ipm in cache.values():
+            ipm.close()
         X = np.concatenate(states, axis=2)
         n_keep = n_cycles * self.cycle_len
         result.time = np.asarray(t_nodes[: n_keep + 1])
