@@ -2,7 +2,8 @@
 
 The public names mirror the reference package (Ipuch/cocofest) for the accelerated path: the six FES
 models, ``ModelMaker``, ``OcpFes``, ``IvpFes``, ``FourierSeries`` and the bioptim-style ``OdeSolver`` /
-``ObjectiveFcn`` / ``ObjectiveList`` / ``Node`` the reference's call sites use.  All NLP callbacks and
+``ObjectiveFcn`` / ``ObjectiveList`` / ``Node`` the reference's call sites use, ``FesNmpc`` (receding
+horizon, every model family) and the batched interior-point driver standing in for Ipopt.  All NLP callbacks and
 integrations execute in libcfx (hand-written HIP for gfx950) — there is no CPU evaluation path.
 """
 
@@ -19,13 +20,15 @@ from .fes_models import (
 )
 from .fourier import FourierSeries
 from .ivp import IvpFes
+from .nmpc import FesNmpc, NmpcResult
 from .ocp import FesOcp, Node, Objective, ObjectiveFcn, ObjectiveList, OcpFes
 from .ode_solver import ControlType, OdeSolver
+from .solver import BatchedIpm, IpmOptions, IpmResult
 
 __all__ = [
     "CfxError", "Handle", "load_library", "DingModelFrequency", "DingModelFrequencyWithFatigue",
     "DingModelPulseIntensityFrequency", "DingModelPulseIntensityFrequencyWithFatigue",
     "DingModelPulseWidthFrequency", "DingModelPulseWidthFrequencyWithFatigue", "FesModel", "ModelMaker",
     "FourierSeries", "IvpFes", "FesOcp", "Node", "Objective", "ObjectiveFcn", "ObjectiveList", "OcpFes",
-    "ControlType", "OdeSolver",
+    "ControlType", "OdeSolver", "FesNmpc", "NmpcResult", "BatchedIpm", "IpmOptions", "IpmResult",
 ]
