@@ -5,7 +5,7 @@ Workload (BASELINE.json configs[1], SURVEY.md section 8(d) cfg 2): OcpFes DingMo
 10 Hz, final time 1 s, n_shooting 20, end-force 100 N objective, bioptim default transcription RK1 x 10
 multiple shooting.  One "instance-evaluation" = g (40 continuity rows) + J_g (120 values) of one OCP
 instance.  Each GPU evaluates a resident batch of B instances (synthetic decision vectors, seeded) per
-step with ONE libcfx call (cfx_eval_all, device pointers, SoA layout) = one kernel launch.
+step with ONE libcfx call (cfx_eval_all, device pointers, 64-instance tiled layout) = one kernel launch.
 
 Multi-GPU (torchrun): instances are independent, so each rank owns its own batch (weak scaling, no
 data-path collective); only the timing max-reduction crosses ranks.
@@ -63,6 +63,12 @@ def synthetic_soa(ocp, B, seed, device):
     v = torch.rand((ocp.nv, B), generator=gen, dtype=torch.float64, device=device)
     scale = torch.tensor([1.5, 250.0] * (ocp.nv // 2), dtype=torch.float64, device=device)[:, None]
     return v * scale
+
+
+def to_tiled(a):
+    """(len, B) SoA -> CFX_LAYOUT_TILED64 (B / 64, len, 64): element e of instance b at ((b/64) len + e) 64 + b%64."""
+    n, B = a.shape
+    return a.T.reshape(B // 64, 64, n).transpose(1, 2).contiguous()
 
 
 def pmc_traffic():
@@ -267,10 +273,10 @@ def main():
 
     ocp = build_problem()
     B = args.batch
-    h = ocp.nlp(batch=B, layout="soa", device=local)
-    v = synthetic_soa(ocp, B, seed=1234 + rank, device=f"cuda:{local}")
-    g = torch.empty((h.ng, B), dtype=torch.float64, device=f"cuda:{local}")
-    jac = torch.empty((h.nnz_jac, B), dtype=torch.float64, device=f"cuda:{local}")
+    h = ocp.nlp(batch=B, layout="tiled64", device=local)
+    v = to_tiled(synthetic_soa(ocp, B, seed=1234 + rank, device=f"cuda:{local}"))
+    g = torch.empty((B // 64, h.ng, 64), dtype=torch.float64, device=f"cuda:{local}")
+    jac = torch.empty((B // 64, h.nnz_jac, 64), dtype=torch.float64, device=f"cuda:{local}")
 
     for _ in range(args.warmup):
         h.eval_all(v, g=g, jac=jac)
@@ -328,12 +334,12 @@ def main():
                             "end_node_tracking=100N, RK1 x 10 multiple shooting; one step = g + J_g of every instance",
                 "batch_per_gpu": B,
                 "nv": h.nv, "ng": h.ng, "nnz_jac": h.nnz_jac,
-                "layout": "SoA (element-major, instance-minor), device-resident",
+                "layout": "CFX_LAYOUT_TILED64 (64-instance tiles, element-major inside a tile), device-resident",
                 "parallelism": f"instances sharded over {world} GPU(s), no data-path collective",
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": "cfx::k_shooting<DING2003, RK1, D=2>",
+                "kernel": "cfx::k_shooting<DING2003, RK1, D=2, NI=2>",
                 "achieved": achieved,
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",

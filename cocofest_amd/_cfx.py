@@ -27,7 +27,7 @@ MODEL_IDS = {
 }
 RK1, RK2, RK4 = 1, 2, 4
 COLLOCATION_LEGENDRE, COLLOCATION_RADAU = 16, 17
-LAYOUT_AOS, LAYOUT_SOA = 0, 1
+LAYOUT_AOS, LAYOUT_SOA, LAYOUT_TILED64 = 0, 1, 2
 DEVICE = 1
 OBJ_LAGRANGE, OBJ_MAYER = 0, 1
 VAR_STATE, VAR_CONTROL = 0, 1
@@ -294,7 +294,11 @@ class Handle:
             self._check(self.lib.cfx_set_stream(self.h, torch.cuda.current_stream().cuda_stream))
 
     def _shape(self, n):
-        return (self.batch, n) if self.layout == LAYOUT_AOS else (n, self.batch)
+        if self.layout == LAYOUT_AOS:
+            return (self.batch, n)
+        if self.layout == LAYOUT_TILED64:  # (tile, element, instance in tile)
+            return (self.batch // 64, n, 64) if n > 1 else (self.batch,)
+        return (n, self.batch)
 
     def eval_all(self, v, g=None, jac=None, f=None, grad=None):
         fl = self._flags(v, g, jac, f, grad)

@@ -417,8 +417,11 @@ extern "C" int cfx_create(const cfx_problem* p, cfx_handle** out) {
         return create_fail(nullptr, CFX_EINVAL, "cfx_create: n_steps, n_shooting, batch and final_time must be positive");
     if (p->truncation < 1 || p->truncation > 32)
         return create_fail(nullptr, CFX_EUNSUPPORTED, "cfx_create: truncation must be in [1, 32]");
-    if (p->layout != CFX_LAYOUT_AOS && p->layout != CFX_LAYOUT_SOA)
+    if (p->layout != CFX_LAYOUT_AOS && p->layout != CFX_LAYOUT_SOA && p->layout != CFX_LAYOUT_TILED64)
         return create_fail(nullptr, CFX_EINVAL, "cfx_create: unknown layout");
+    if (p->layout == CFX_LAYOUT_TILED64 && (p->batch % 64 != 0 || colloc))
+        return create_fail(nullptr, CFX_EUNSUPPORTED,
+                           "cfx_create: CFX_LAYOUT_TILED64 needs batch % 64 == 0 and a shooting transcription");
     if (!p->stim_rows) return create_fail(nullptr, CFX_EINVAL, "cfx_create: stim_rows is NULL");
     const bool hmed = p->model >= CFX_HMED2018;
     if (p->n_params < 0 || (p->n_params > 0 && (!hmed || !p->last_stim_idx)))
@@ -598,6 +601,10 @@ extern "C" int cfx_create(const cfx_problem* p, cfx_handle** out) {
     // kernel parameters
     const cfx_constants& c = p->constants;
     kp.B = p->batch;
+    kp.tiled = p->layout == CFX_LAYOUT_TILED64;
+    kp.nv_tot = h->sz.nv;
+    kp.ng_tot = h->sz.ng;
+    kp.nnz_tot = h->sz.nnz_jac;
     kp.nx = nx;
     kp.N = N;
     kp.m = p->n_steps;
@@ -641,7 +648,9 @@ extern "C" int cfx_create(const cfx_problem* p, cfx_handle** out) {
         // NI adjacent instances per lane (16-byte accesses) need B % NI == 0; the launch also checks alignment
         // Measured on MI355X (cfg2, B = 2^20): g + J_g is store-bound and fastest at NI = 1; the g-only pass
         // (fewer stores) gains ~7% from NI = 4.
-        h->ni = 1;
+        // With 64-instance tiles the g + J_g pass is fastest at NI = 2 (0.29 vs 0.30 ms at NI = 1, SoA NI = 1:
+        // 0.32 ms; scripts/kprobe.py).
+        h->ni = (!hmed && p->layout == CFX_LAYOUT_TILED64) ? 2 : 1;
         h->ni_g = (!hmed && p->batch % 4 == 0 && p->batch >= (int64_t)256 * 1024) ? 4 : 1;
         if (const char* e = std::getenv("CFX_NI")) {
             const int v = std::atoi(e);
@@ -834,6 +843,7 @@ extern "C" int cfx_eval_grad_f(cfx_handle* h, const double* v, double* grad, uin
 extern "C" int cfx_eval_h(cfx_handle* h, const double* v, const double* obj_factor, const double* lambda,
                           double* hess, uint32_t flags) {
     if (!h || !v || !obj_factor || !lambda || !hess) return h ? fail(h, CFX_EINVAL, "cfx_eval_h: NULL argument") : CFX_EINVAL;
+    if (h->kp.tiled) return fail(h, CFX_EUNSUPPORTED, "cfx_eval_h: not available with CFX_LAYOUT_TILED64");
     CFX_HIP(h, hipSetDevice(h->device));
     int rc = CFX_OK;
     const int64_t B = h->prob.batch;
@@ -862,6 +872,7 @@ extern "C" int cfx_eval_h(cfx_handle* h, const double* v, const double* obj_fact
 extern "C" int cfx_integrate(cfx_handle* h, const double* x0, const double* u, double* traj, uint32_t flags) {
     if (!h || !traj) return CFX_EINVAL;
     if (h->colloc) return fail(h, CFX_EUNSUPPORTED, "cfx_integrate: not available for a collocation transcription");
+    if (h->kp.tiled) return fail(h, CFX_EUNSUPPORTED, "cfx_integrate: not available with CFX_LAYOUT_TILED64");
     if (h->sz.nu > 0 && !u) return fail(h, CFX_EINVAL, "cfx_integrate: this model needs per-interval controls");
     CFX_HIP(h, hipSetDevice(h->device));
     int rc = CFX_OK;

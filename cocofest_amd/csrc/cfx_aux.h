@@ -28,16 +28,17 @@ __global__ void __launch_bounds__(256) k_objective(const KParams P, int n_obj, c
     const int64_t B = P.B;
     const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= B) return;
+    const int64_t ES = lay_stride(P), vb = lay_base(P, P.nv_tot, b);  // V and GRAD share the layout
     double f = 0.0;
     for (int t = 0; t < n_obj; ++t) {
         const DevObjective o = obj[t];
         for (int k = o.node_first; k <= o.node_last; ++k) {
             const int64_t off = (int64_t)k * P.nz + (o.var_kind == 0 ? 0 : P.uoff) + o.var_index;
-            const double z = V[off * B + b];
+            const double z = V[vb + off * ES];
             const double tgt = o.target_off >= 0 ? targets[o.target_off + k] : o.target_value;
             const double d = z - tgt;
             f += o.w_eff * d * d;
-            if (GRAD) GRAD[off * B + b] += 2.0 * o.w_eff * d;
+            if (GRAD) GRAD[vb + off * ES] += 2.0 * o.w_eff * d;
         }
     }
     if (F) F[b] = f;
@@ -72,19 +73,21 @@ __global__ void __launch_bounds__(256) k_slide(const KParams P, const int32_t* _
     if (b >= B) return;
     const int64_t p_off = (int64_t)P.N * P.nz + P.nx;
     const int g_off = P.ngk - P.n_slide;  // the window rows follow the interval's dynamics rows
+    const int64_t ES = lay_stride(P), vb = lay_base(P, P.nv_tot, b), gb = lay_base(P, P.ng_tot, b),
+                  jb = lay_base(P, P.nnz_tot, b);
     for (int k = 0; k < P.N; ++k) {
         for (int j = 0; j < P.T; ++j) {
             const int slot = k * P.T + j;
             const int pi = sl_param[slot];
             if (G) {
-                const double u = V[((int64_t)k * P.nz + P.uoff + j) * B + b];
-                const double w = pi >= 0 ? V[(p_off + pi) * B + b] : floor_value;
-                G[((int64_t)k * P.ngk + g_off + j) * B + b] = u - w;
+                const double u = V[vb + ((int64_t)k * P.nz + P.uoff + j) * ES];
+                const double w = pi >= 0 ? V[vb + (p_off + pi) * ES] : floor_value;
+                G[gb + ((int64_t)k * P.ngk + g_off + j) * ES] = u - w;
             }
             if (J) {
                 const int64_t jo = sl_joff[slot];
-                J[jo * B + b] = 1.0;
-                if (pi >= 0) J[(jo + 1) * B + b] = -1.0;
+                J[jb + jo * ES] = 1.0;
+                if (pi >= 0) J[jb + (jo + 1) * ES] = -1.0;
             }
         }
     }

@@ -71,7 +71,17 @@ struct KParams {
     double colD[kMaxDeg + 1];
     // Hessian value index of the diagonal entry of (node k, element e), e < nx + nu, k <= N (objective terms)
     const int32_t* hdiag;
+    // CFX_LAYOUT_TILED64: element e of instance b at ((b / 64) * len + e) * 64 + b % 64 (len = nv, ng or
+    // nnz_jac per instance); otherwise SoA e * B + b
+    int32_t tiled;
+    int64_t nv_tot, ng_tot, nnz_tot;
 };
+
+// Element stride and the offset of instance b's element 0 in a buffer of `len` doubles per instance.
+CFX_HD int64_t lay_stride(const KParams& P) { return P.tiled ? 64 : P.B; }
+CFX_HD int64_t lay_base(const KParams& P, int64_t len, int64_t b) {
+    return P.tiled ? ((b >> 6) * len) * 64 + (b & 63) : b;
+}
 
 // 1/x from v_rcp_f64 (relative error <= 4.6e-8 measured on MI355X) and one cubic correction
 // y (1 + e + e^2), e = 1 - x y: residual O(e^3) ~ 1e-22, i.e. the FP64 rounding of the last FMAs.
@@ -393,12 +403,18 @@ __global__ void __launch_bounds__(256) k_shooting(const KParams P, const double*
     const int k1 = min(P.N, k0 + P.kpt);
     const int chunk = is_int(MODEL) ? (int)blockIdx.z : 0;  // the other models carry every direction in one lane
 
+    // layout: element stride ES, per-buffer instance offsets (SoA: b0; 64-instance tiles: see KParams).  The
+    // accesses stay expressed on the __restrict__ arguments (a derived `G ? G + off : nullptr` pointer loses
+    // the no-alias fact, and the table reads then turn into vector loads behind every store).
+    const int64_t ES = lay_stride(P);
+    const int64_t vb = lay_base(P, P.nv_tot, b0), gb = lay_base(P, P.ng_tot, b0), jb = lay_base(P, P.nnz_tot, b0);
+
     IState<NX, D> st[NI];
     CsHmed<D, TMAX> csh[NI];
 #pragma unroll
     for (int r = 0; r < NX; ++r) {
         double t[NI];
-        ld_lane<NI>(V + (int64_t)(k0 * P.nz + r) * B + b0, t);
+        ld_lane<NI>(V + vb + (int64_t)(k0 * P.nz + r) * ES, t);
 #pragma unroll
         for (int i = 0; i < NI; ++i) st[i].x[r] = t[i];
     }
@@ -408,7 +424,7 @@ __global__ void __launch_bounds__(256) k_shooting(const KParams P, const double*
         const int xn = (k + 1) * P.nz;
         double xnext[NX][NI];  // issued before the integration so its latency hides under it
 #pragma unroll
-        for (int r = 0; r < NX; ++r) ld_lane<NI>(V + (int64_t)(xn + r) * B + b0, xnext[r]);
+        for (int r = 0; r < NX; ++r) ld_lane<NI>(V + vb + (int64_t)(xn + r) * ES, xnext[r]);
 #pragma unroll
         for (int i = 0; i < NI; ++i) {
 #pragma unroll
@@ -416,7 +432,7 @@ __global__ void __launch_bounds__(256) k_shooting(const KParams P, const double*
 #pragma unroll
                 for (int j = 0; j < D; ++j) st[i].xd[r][j] = (chunk * D + j == r) ? 1.0 : 0.0;
             st[i].cn0 = st[i].x[0];
-            load_controls<MODEL, D, TMAX>(P, V + b0 + i, B, xo, chunk, st[i].amp, csh[i]);
+            load_controls<MODEL, D, TMAX>(P, V + vb + i, ES, xo, chunk, st[i].amp, csh[i]);
         }
         integrate<MODEL, SCHEME, D, TMAX, NI>(P, k, 0, P.m, chunk, st, csh);
         if (G != nullptr && chunk == 0) {
@@ -425,7 +441,7 @@ __global__ void __launch_bounds__(256) k_shooting(const KParams P, const double*
                 double t[NI];
 #pragma unroll
                 for (int i = 0; i < NI; ++i) t[i] = st[i].x[r] - xnext[r][i];
-                st_lane<NI>(G + (int64_t)(k * P.ngk + r) * B + b0, t);
+                st_lane<NI>(G + gb + (int64_t)(k * P.ngk + r) * ES, t);
             }
         }
         if constexpr (D > 0) {
@@ -442,11 +458,11 @@ __global__ void __launch_bounds__(256) k_shooting(const KParams P, const double*
                                 double t[NI];
 #pragma unroll
                                 for (int i = 0; i < NI; ++i) t[i] = st[i].xd[r][j];
-                                st_lane<NI>(J + (jo + pos) * B + b0, t);
+                                st_lane<NI>(J + jb + (jo + pos) * ES, t);
                             }
                         }
                     }
-                    if (chunk == 0) st_lane_const<NI>(J + (jo + P.jneg[r]) * B + b0, -1.0);
+                    if (chunk == 0) st_lane_const<NI>(J + jb + (jo + P.jneg[r]) * ES, -1.0);
                 }
             }
         }

@@ -185,7 +185,8 @@ class FesOcp:
             model_id=self.model.cfx_model_id, constants=self.model.cfx_constants(), scheme=self.ode_solver.scheme,
             n_steps=self.ode_solver.n_integration_steps, n_shooting=self.n_shooting,
             truncation=self.truncation, final_time=float(self.final_time), stim_rows=self.stim_rows, batch=batch,
-            layout=_cfx.LAYOUT_AOS if layout == "aos" else _cfx.LAYOUT_SOA, n_params=self.n_params,
+            layout={"aos": _cfx.LAYOUT_AOS, "soa": _cfx.LAYOUT_SOA, "tiled64": _cfx.LAYOUT_TILED64}[layout],
+            n_params=self.n_params,
             last_stim_idx=self.last_stim_idx, intensity_floor=self.intensity_floor,
             objectives=self.objectives, device=device)
 

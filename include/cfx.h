@@ -73,6 +73,11 @@ extern "C" {
 /* layouts and call flags */
 #define CFX_LAYOUT_AOS 0
 #define CFX_LAYOUT_SOA 1
+/* 64-instance tiles: element e of instance b at ((b / 64) * len + e) * 64 + b % 64, len = the per-instance
+   length of the buffer (nv, ng, nnz_jac, nv for grad, 1 for f).  batch % 64 == 0.  Keeps each wave's stores
+   inside one contiguous tile instead of spreading them over len rows B apart (+6 % on the store-bound
+   g + J_g pass).  Shooting transcriptions, eval_g / eval_jac_g / eval_f / eval_grad_f / eval_all only. */
+#define CFX_LAYOUT_TILED64 2
 #define CFX_DEVICE 1u /* pointers are device pointers; call is asynchronous on the handle stream */
 
 /* objective terms (fes_ocp.py:531-569) */
@@ -113,7 +118,7 @@ typedef struct cfx_problem {
     int32_t n_shooting;  /* N */
     int32_t truncation;  /* sum_stim_truncation T (<= 32) */
     int32_t n_params;    /* Hmed pulse-intensity parameters (0: no sliding-window constraints) */
-    int32_t layout;      /* CFX_LAYOUT_AOS | CFX_LAYOUT_SOA */
+    int32_t layout;      /* CFX_LAYOUT_AOS | CFX_LAYOUT_SOA | CFX_LAYOUT_TILED64 */
     int64_t batch;       /* B >= 1 */
     double final_time;
     /* stim table, row k = the last T stim times <= k*final_time/N (history placeholders -1e7):

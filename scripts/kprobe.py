@@ -29,24 +29,31 @@ def main():
     for ni in (1, 2, 4):
         os.environ["CFX_NI"] = str(ni)
         handles[ni] = ocp.nlp(batch=B, layout="soa")
+        handles[f"t{ni}"] = ocp.nlp(batch=B, layout="tiled64")
     os.environ.pop("CFX_NI")
     h = handles[1]
     v = bench.synthetic_soa(ocp, B, 1, "cuda:0")
     g = torch.empty((h.ng, B), dtype=torch.float64, device="cuda")
     j = torch.empty((h.nnz_jac, B), dtype=torch.float64, device="cuda")
+    vt = v.T.reshape(B // 64, 64, -1).transpose(1, 2).contiguous()
+    gt = torch.empty((B // 64, h.ng, 64), dtype=torch.float64, device="cuda")
+    jt = torch.empty((B // 64, h.nnz_jac, 64), dtype=torch.float64, device="cuda")
     variants = {}
     for ni, hh in handles.items():
-        variants[f"g+J ni={ni}"] = (hh, dict(g=g, jac=j))
-        variants[f"g ni={ni}"] = (hh, dict(g=g))
+        if isinstance(ni, str):
+            variants[f"g+J tiled ni={ni[1:]}"] = (hh, dict(v=vt, g=gt, jac=jt))
+            continue
+        variants[f"g+J ni={ni}"] = (hh, dict(v=v, g=g, jac=j))
+        variants[f"g ni={ni}"] = (hh, dict(v=v, g=g))
     res = {k: [] for k in variants}
     for _ in range(a.rounds):
         for name, (h, kw) in variants.items():
             for _ in range(3):
-                h.eval_all(v, **kw)
+                h.eval_all(**kw)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             for _ in range(a.reps):
-                h.eval_all(v, **kw)
+                h.eval_all(**kw)
             e1.record()
             torch.cuda.synchronize()
             res[name].append(e0.elapsed_time(e1) / a.reps)

@@ -170,6 +170,49 @@ def test_layouts_and_device_pointers_are_bitwise_identical():
     _close_g(pb, v, ga, O.eval_g(pb, v), what="cfg2 g")
 
 
+@pytest.mark.parametrize("name", ["ding2003", "ding2007_with_fatigue", "hmed2018"])
+def test_tiled_layout_is_bitwise_identical(name):
+    """CFX_LAYOUT_TILED64 (64-instance tiles) gives the same g, J_g, f, grad f bits as SoA; Hmed's sliding
+    rows and the objective kernels included; unsupported entry points fail loudly."""
+    import torch
+
+    from cocofest_amd import _cfx
+
+    cfg = dict(name=name, stims=[0.0, 0.1, 0.2, 0.3], final_time=0.4, truncation=4, scheme="RK2", m=5,
+               objective={"end_node_tracking": 40.0}, n_shooting=None)
+    ocp = cases.product_ocp(**cfg)
+    pb = cases.oracle_problem(**cfg)
+    B = 320
+    v = cases.random_decision(pb, B, seed=9)
+    hs, ht = ocp.nlp(batch=B, layout="soa"), ocp.nlp(batch=B, layout="tiled64")
+
+    def run(h, vin, shape):
+        g = torch.empty(shape(h.ng), dtype=torch.float64, device="cuda")
+        j = torch.empty(shape(h.nnz_jac), dtype=torch.float64, device="cuda")
+        f = torch.empty((B,), dtype=torch.float64, device="cuda")
+        gr = torch.empty(shape(h.nv), dtype=torch.float64, device="cuda")
+        h.eval_all(vin, g=g, jac=j, f=f, grad=gr)
+        torch.cuda.synchronize()
+        return g.cpu().numpy(), j.cpu().numpy(), f.cpu().numpy(), gr.cpu().numpy()
+
+    soa = run(hs, torch.tensor(np.ascontiguousarray(v.T), device="cuda"), lambda n: (n, B))
+    vt = np.ascontiguousarray(v.reshape(B // 64, 64, -1).transpose(0, 2, 1))
+    til = run(ht, torch.tensor(vt, device="cuda"), lambda n: (B // 64, n, 64))
+    untile = lambda a: a.transpose(0, 2, 1).reshape(B, -1).T  # noqa: E731
+    np.testing.assert_array_equal(untile(til[0]), soa[0])
+    np.testing.assert_array_equal(untile(til[1]), soa[1])
+    np.testing.assert_array_equal(til[2], soa[2])
+    np.testing.assert_array_equal(untile(til[3]), soa[3])
+    with pytest.raises(_cfx.CfxError):
+        ht.eval_h(torch.tensor(vt, device="cuda"), torch.ones(B, dtype=torch.float64, device="cuda"),
+                  torch.zeros((B // 64, ht.ng, 64), dtype=torch.float64, device="cuda"),
+                  torch.empty((B // 64, ht.nnz_hess, 64), dtype=torch.float64, device="cuda"))
+    with pytest.raises(_cfx.CfxError):
+        ocp.nlp(batch=100, layout="tiled64")
+    hs.close()
+    ht.close()
+
+
 def test_full_size_properties_cfg2():
     """BASELINE config 2 at bench size: batch invariance (instance b gives the same bits alone and inside a
     2^17 batch) and feasibility of the forward RK1 x 10 integration (the 0-DOF optimum): g == 0."""
