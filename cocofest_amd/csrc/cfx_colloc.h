@@ -36,20 +36,36 @@ constexpr int col_rowlen(int model, int r, int deg, int nu) {
     return deg + 1 + __builtin_popcount(col_xdeps(model, r) & ~(1u << r)) + col_udeps(model, r, nu);
 }
 
-template <int MODEL, int TMAX>
+// DEG > 0: the degree is a compile-time constant and every input of the interval (x^0..x^d, x_{k+1}, the
+// controls) is loaded into registers before the first store — on CDNA vmcnt counts stores too, so a load
+// issued after stores waits for them; DEG == 0: any degree, states re-read from memory per point.
+template <int MODEL, int TMAX, int DEG>
 __global__ void __launch_bounds__(256) k_colloc(const KParams P, const double* __restrict__ V, double* __restrict__ G,
                                                 double* __restrict__ J) {
     constexpr int NX = nx_of(MODEL);
     constexpr bool PW = is_pw(MODEL), HM = is_int(MODEL);
     constexpr int DD = NX + (PW ? 1 : 0);  // directions of the RHS partials: the point's states (+ pulse width)
+    constexpr int XS = DEG > 0 ? DEG + 1 : 1;
+    constexpr int UN = DEG > 0 ? DEG + 1 : 1;  // unroll factor of the point / basis loops
     const int64_t B = P.B;
     const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= B) return;
     const int k = blockIdx.y;
-    const int d = P.deg;
+    const int d = DEG > 0 ? DEG : P.deg;
     const double* Vb = V + b;
     const int64_t xo = (int64_t)k * P.nz;
     auto ld = [&](int64_t e) { return Vb[(xo + e) * B]; };
+
+    double xs[XS][NX], xn[NX];
+    if constexpr (DEG > 0) {
+#pragma unroll
+        for (int i = 0; i <= DEG; ++i)
+#pragma unroll
+            for (int r = 0; r < NX; ++r) xs[i][r] = ld(i * NX + r);
+    }
+#pragma unroll
+    for (int r = 0; r < NX; ++r) xn[r] = Vb[((int64_t)(k + 1) * P.nz + r) * B];
+    auto X = [&](int i, int r) { return DEG > 0 ? xs[i][r] : ld(i * NX + r); };
 
     Amp amp{1.0, 0.0, -1};
     double lam[TMAX], lamd[TMAX];
@@ -73,10 +89,11 @@ __global__ void __launch_bounds__(256) k_colloc(const KParams P, const double* _
     const int64_t jo = (int64_t)k * P.nnzk;
     const int64_t go = (int64_t)k * P.ngk;
 
+#pragma unroll UN
     for (int j = 1; j <= d; ++j) {
         double x[NX];
 #pragma unroll
-        for (int r = 0; r < NX; ++r) x[r] = ld(j * NX + r);
+        for (int r = 0; r < NX; ++r) x[r] = X(j, r);
         const int q = k * d + j - 1;
         double cs;
         const double* coef = P.tab + (int64_t)q * (HM ? TMAX : 1);
@@ -100,7 +117,8 @@ __global__ void __launch_bounds__(256) k_colloc(const KParams P, const double* _
 #pragma unroll
             for (int r = 0; r < NX; ++r) {
                 double poly = 0.0;
-                for (int i = 0; i <= d; ++i) poly = fma(P.colC[i][j], i == j ? x[r] : ld(i * NX + r), poly);
+#pragma unroll UN
+                for (int i = 0; i <= d; ++i) poly = fma(P.colC[i][j], X(i, r), poly);
                 G[(go + (j - 1) * NX + r) * B + b] = fma(-P.dt, f[r], poly);
             }
         }
@@ -109,14 +127,20 @@ __global__ void __launch_bounds__(256) k_colloc(const KParams P, const double* _
 #pragma unroll
             for (int r = 0; r < NX; ++r) {
                 const double diag = r == 0 ? -P.inv_tauc : fd[r][r];
-                for (int i = 0; i <= d; ++i) J[(o + i) * B + b] = i == j ? fma(-P.dt, diag, P.colC[i][j]) : P.colC[i][j];
+#pragma unroll UN
+                for (int i = 0; i <= d; ++i)
+                    J[(o + i) * B + b] = i == j ? fma(-P.dt, diag, P.colC[i][j]) : P.colC[i][j];
                 o += d + 1;
 #pragma unroll
                 for (int c = 0; c < NX; ++c)
                     if (c != r && (col_xdeps(MODEL, r) >> c & 1u)) J[(o++) * B + b] = -P.dt * fd[r][c];
                 if constexpr (HM) {
-                    if (r == 0)
-                        for (int i = 0; i < P.T; ++i) J[(o++) * B + b] = -P.dt * P.inv_tauc * coef[i] * lamd[i];
+                    if (r == 0) {
+#pragma unroll
+                        for (int i = 0; i < TMAX; ++i)  // register-resident lamd: no dynamic indexing
+                            if (i < P.T) J[(o + i) * B + b] = -P.dt * P.inv_tauc * coef[i] * lamd[i];
+                        o += P.T;
+                    }
                 }
                 if constexpr (PW) {
                     if (r == 1) J[(o++) * B + b] = -P.dt * fd[1][NX];
@@ -125,16 +149,17 @@ __global__ void __launch_bounds__(256) k_colloc(const KParams P, const double* _
         }
     }
     // continuity
-    const int64_t xn = (int64_t)(k + 1) * P.nz;
 #pragma unroll
     for (int r = 0; r < NX; ++r) {
         if (G) {
             double e = 0.0;
-            for (int i = 0; i <= d; ++i) e = fma(P.colD[i], ld(i * NX + r), e);
-            G[(go + d * NX + r) * B + b] = e - Vb[(xn + r) * B];
+#pragma unroll UN
+            for (int i = 0; i <= d; ++i) e = fma(P.colD[i], X(i, r), e);
+            G[(go + d * NX + r) * B + b] = e - xn[r];
         }
         if (J) {
             const int64_t o = jo + (int64_t)d * sumrow + (int64_t)r * (d + 2);
+#pragma unroll UN
             for (int i = 0; i <= d; ++i) J[(o + i) * B + b] = P.colD[i];
             J[(o + d + 1) * B + b] = -1.0;
         }

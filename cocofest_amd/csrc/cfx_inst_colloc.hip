@@ -4,11 +4,24 @@
 
 namespace cfx {
 
+template <int MODEL, int TMAX, int DEG>
+static hipError_t colloc_deg(const KParams& P, const double* V, double* G, double* J, hipStream_t s) {
+    dim3 grid((unsigned)((P.B + kBlock - 1) / kBlock), (unsigned)P.N);
+    hipLaunchKernelGGL((k_colloc<MODEL, TMAX, DEG>), grid, dim3(kBlock), 0, s, P, V, G, J);
+    return hipGetLastError();
+}
+
+// degrees 1..5 (bioptim's default is 4) with register-resident states; any other degree runs the generic kernel
 template <int MODEL, int TMAX>
 static hipError_t colloc_t(const KParams& P, const double* V, double* G, double* J, hipStream_t s) {
-    dim3 grid((unsigned)((P.B + kBlock - 1) / kBlock), (unsigned)P.N);
-    hipLaunchKernelGGL((k_colloc<MODEL, TMAX>), grid, dim3(kBlock), 0, s, P, V, G, J);
-    return hipGetLastError();
+    switch (P.deg) {
+        case 1: return colloc_deg<MODEL, TMAX, 1>(P, V, G, J, s);
+        case 2: return colloc_deg<MODEL, TMAX, 2>(P, V, G, J, s);
+        case 3: return colloc_deg<MODEL, TMAX, 3>(P, V, G, J, s);
+        case 4: return colloc_deg<MODEL, TMAX, 4>(P, V, G, J, s);
+        case 5: return colloc_deg<MODEL, TMAX, 5>(P, V, G, J, s);
+        default: return colloc_deg<MODEL, TMAX, 0>(P, V, G, J, s);
+    }
 }
 
 template <int MODEL, int TMAX>
