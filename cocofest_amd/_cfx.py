@@ -105,7 +105,7 @@ def load_library(path: str | os.PathLike | None = None):
     global _lib
     if _lib is not None and path is None:
         return _lib
-    p = pathlib.Path(path) if path else LIB_PATH
+    p = pathlib.Path(path) if path else pathlib.Path(os.environ.get("CFX_LIB", LIB_PATH))
     # One HIP runtime per process: torch ships its own libamdhip64.so.7 (same soname as /opt/rocm's).  Load it
     # first so libcfx binds to the already-loaded runtime instead of pulling in a second one.
     try:

@@ -658,7 +658,7 @@ extern "C" int cfx_create(const cfx_problem* p, cfx_handle** out) {
         }
         // intervals per thread: as many as possible (x read once) while keeping >= 2048 workgroups in flight
         const int64_t bx = (p->batch + (int64_t)kBlock * h->ni - 1) / ((int64_t)kBlock * h->ni);
-        const int64_t nch = nchunk_of(h->model, nz);
+        const int64_t nch = nchunk_of(h->model, h->scheme, h->tmax, nz);
         int64_t kpt = (int64_t)N * bx * nch / 2048;
         kp.kpt = (int32_t)std::max<int64_t>(1, std::min<int64_t>(N, kpt));
     }
@@ -804,7 +804,8 @@ extern "C" int cfx_eval_all(cfx_handle* h, const double* v, double* g, double* j
     if (G || J) {
         CFX_HIP(h, launch_shooting(h, J != nullptr, V, G, J));
         if (h->kp.n_slide)
-            hipLaunchKernelGGL(k_slide, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, h->stream, h->kp, h->d_sl_param,
+            hipLaunchKernelGGL(k_slide, dim3((unsigned)((B + 255) / 256), (unsigned)(h->kp.N * h->kp.T)), dim3(256), 0,
+                               h->stream, h->kp, h->d_sl_param,
                                h->d_sl_joff, h->prob.intensity_floor, V, G, J);
     }
     if (F || GR) {

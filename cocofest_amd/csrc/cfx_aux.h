@@ -64,6 +64,8 @@ __global__ void __launch_bounds__(256) k_objective_hess(const KParams P, int n_o
 
 // Hmed sliding-window rows (custom_constraints.py:102-119): g = u_k[j] - window_k(p)[j], J = +1 / -1.
 // slot (k, j): param index or -1 for the intensity-floor padding; joff = J offset of its +1 entry.
+// Thread = (instance, slot): its two loads precede its stores (a per-instance loop over the slots would issue
+// every load behind the previous slot's stores, which vmcnt serialises).
 __global__ void __launch_bounds__(256) k_slide(const KParams P, const int32_t* __restrict__ sl_param,
                                                const int32_t* __restrict__ sl_joff, double floor_value,
                                                const double* __restrict__ V, double* __restrict__ G,
@@ -71,25 +73,22 @@ __global__ void __launch_bounds__(256) k_slide(const KParams P, const int32_t* _
     const int64_t B = P.B;
     const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= B) return;
+    const int slot = blockIdx.y;  // k * T + j
+    const int k = slot / P.T, j = slot - k * P.T;
     const int64_t p_off = (int64_t)P.N * P.nz + P.nx;
     const int g_off = P.ngk - P.n_slide;  // the window rows follow the interval's dynamics rows
     const int64_t ES = lay_stride(P), vb = lay_base(P, P.nv_tot, b), gb = lay_base(P, P.ng_tot, b),
                   jb = lay_base(P, P.nnz_tot, b);
-    for (int k = 0; k < P.N; ++k) {
-        for (int j = 0; j < P.T; ++j) {
-            const int slot = k * P.T + j;
-            const int pi = sl_param[slot];
-            if (G) {
-                const double u = V[vb + ((int64_t)k * P.nz + P.uoff + j) * ES];
-                const double w = pi >= 0 ? V[vb + (p_off + pi) * ES] : floor_value;
-                G[gb + ((int64_t)k * P.ngk + g_off + j) * ES] = u - w;
-            }
-            if (J) {
-                const int64_t jo = sl_joff[slot];
-                J[jb + jo * ES] = 1.0;
-                if (pi >= 0) J[jb + (jo + 1) * ES] = -1.0;
-            }
-        }
+    const int pi = sl_param[slot];
+    if (G) {
+        const double u = V[vb + ((int64_t)k * P.nz + P.uoff + j) * ES];
+        const double w = pi >= 0 ? V[vb + (p_off + pi) * ES] : floor_value;
+        G[gb + ((int64_t)k * P.ngk + g_off + j) * ES] = u - w;
+    }
+    if (J) {
+        const int64_t jo = sl_joff[slot];
+        J[jb + jo * ES] = 1.0;
+        if (pi >= 0) J[jb + (jo + 1) * ES] = -1.0;
     }
 }
 

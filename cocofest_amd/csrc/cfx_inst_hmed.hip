@@ -7,16 +7,15 @@ namespace cfx {
 template <int MODEL, int TMAX>
 static hipError_t shooting_t(int scheme, bool derivs, const KParams& P, const double* V, double* G, double* J,
                              hipStream_t s) {
-    constexpr int D = dirs_of(MODEL);
     switch (scheme) {
         case 1:
-            return derivs ? launch_shooting_t<MODEL, 1, D, TMAX, 1>(P, V, G, J, s)
+            return derivs ? launch_shooting_t<MODEL, 1, dirs_of(MODEL, 1, TMAX), TMAX, 1>(P, V, G, J, s)
                           : launch_shooting_t<MODEL, 1, 0, TMAX, 1>(P, V, G, J, s);
         case 2:
-            return derivs ? launch_shooting_t<MODEL, 2, D, TMAX, 1>(P, V, G, J, s)
+            return derivs ? launch_shooting_t<MODEL, 2, dirs_of(MODEL, 2, TMAX), TMAX, 1>(P, V, G, J, s)
                           : launch_shooting_t<MODEL, 2, 0, TMAX, 1>(P, V, G, J, s);
         case 4:
-            return derivs ? launch_shooting_t<MODEL, 4, D, TMAX, 1>(P, V, G, J, s)
+            return derivs ? launch_shooting_t<MODEL, 4, dirs_of(MODEL, 4, TMAX), TMAX, 1>(P, V, G, J, s)
                           : launch_shooting_t<MODEL, 4, 0, TMAX, 1>(P, V, G, J, s);
         default:
             return hipErrorInvalidValue;

@@ -161,12 +161,14 @@ CFX_HD void rhs_force(const KParams& P, double cn, const double* cnd, const doub
 // Hmed2018 stimulation sum: cs = sum_i coef[q][i] * lambda_i(u_i) with lambda_i held in registers
 // (cn_sum_fun with lambda_i, ding2003.py:230-252 / hmed2018.py:97-98); its derivative exists only along
 // this lane's u-directions (uidx >= 0): d cs / d u_i = coef[q][i] * lambda_i'(u_i).
+// Lane direction j carries intensity ubase + j (ubase = chunk * D - nx, wave-uniform, so the coefficient
+// c[ubase + j] is a scalar load); lamd[j] = 0 for directions that are not intensities.
 template <int DMAX, int TMAX>
 struct CsHmed {
     const double* coef;
     double lamv[TMAX];
     double lamd[DMAX > 0 ? DMAX : 1];
-    int uidx[DMAX > 0 ? DMAX : 1];
+    int ubase;
     template <int D>
     CFX_HD double eval(int q, double* csd) const {
         const double* c = coef + (int64_t)q * TMAX;
@@ -174,7 +176,10 @@ struct CsHmed {
 #pragma unroll
         for (int i = 0; i < TMAX; ++i) s += c[i] * lamv[i];
 #pragma unroll
-        for (int j = 0; j < D; ++j) csd[j] = uidx[j] >= 0 ? c[uidx[j]] * lamd[j] : 0.0;
+        for (int j = 0; j < D; ++j) {
+            const int ui = ubase + j;
+            csd[j] = (ui >= 0 && ui < TMAX) ? c[ui] * lamd[j] : 0.0;
+        }
         return s;
     }
 };
@@ -203,7 +208,7 @@ struct IState {
 // ---------------------------------------------------------------------------------------------------
 template <int MODEL, int SCHEME, int D, int TMAX, int NI>
 CFX_HD void integrate(const KParams& P, int k, int j0, int msteps, int chunk, IState<nx_of(MODEL), D> (&st)[NI],
-                      const CsHmed<D, TMAX> (&csh)[NI]) {
+                      CsHmed<D, TMAX> (&csh)[NI]) {
     constexpr int NX = nx_of(MODEL);
     constexpr int DD = D > 0 ? D : 1;
     constexpr bool LIN = !is_int(MODEL);
@@ -340,15 +345,14 @@ CFX_HD void load_controls(const KParams& P, const double* Vb, int64_t B, int xo,
             const double ui = i < P.T ? Vb[(int64_t)(xo + NX + i) * B] : P.Is;
             csh.lamv[i] = i < P.T ? P.ar * (tanh(P.bs * (ui - P.Is)) + P.cr) : 0.0;
         }
+        csh.ubase = chunk * D - NX;
 #pragma unroll
         for (int j = 0; j < D; ++j) {
             const int gd = chunk * D + j;
-            csh.uidx[j] = -1;
             csh.lamd[j] = 0.0;
             if (gd >= NX && gd < P.nz) {
                 const double th = tanh(P.bs * (Vb[(int64_t)(xo + gd) * B] - P.Is));
                 csh.lamd[j] = P.ar * P.bs * (1.0 - th * th);
-                csh.uidx[j] = gd - NX;
             }
         }
     }

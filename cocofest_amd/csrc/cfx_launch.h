@@ -9,14 +9,28 @@
 
 namespace cfx {
 
-// Jacobian directions carried per lane, per model (nz = nx + nu).  Hmed splits its nx + T directions
-// into chunks of 4 (nx = 2) or 5 (nx = 5); the others carry all directions in one lane.
-constexpr int dirs_of(int model) {
-    return model == M_D03 ? 2 : model == M_D03F ? 5 : model == M_D07 ? 3 : model == M_D07F ? 6 : model == M_H18 ? 4 : 5;
+#ifndef HMED_DIRS
+#define HMED_DIRS 12  // Jacobian directions per lane for Hmed2018 (nx = 2), see dirs_of
+#endif
+
+// Jacobian directions carried per lane (nz = nx + nu).  The Ding families carry all of them in one lane.
+// Hmed carries nx + T directions: as many per lane as the RK stage arrays (2 / 3 / 5 arrays of nx x D doubles
+// for RK1 / RK2 / RK4) fit in ~160 VGPRs, so the value recursion is repeated over as few chunks as possible.
+constexpr int dirs_of(int model, int scheme = 1, int tmax = 4) {
+    if (model == M_D03) return 2;
+    if (model == M_D03F) return 5;
+    if (model == M_D07) return 3;
+    if (model == M_D07F) return 6;
+    const int all = (model == M_H18 ? 2 : 5) + tmax;
+    const int d = model == M_H18 ? HMED_DIRS : 5;
+    return all < d ? all : d;
 }
 
 // Direction chunks per lane group for a problem with nz directions.
-inline int nchunk_of(int model, int nz) { return (nz + dirs_of(model) - 1) / dirs_of(model); }
+inline int nchunk_of(int model, int scheme, int tmax, int nz) {
+    const int d = dirs_of(model, scheme, tmax);
+    return (nz + d - 1) / d;
+}
 
 // Smallest supported register-resident truncation bucket >= T (Hmed only).
 inline int tmax_bucket(int T) { return T <= 4 ? 4 : T <= 8 ? 8 : T <= 16 ? 16 : 32; }
