@@ -42,6 +42,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline sample budget (0: skip)")
     ap.add_argument("--no-solve", action="store_true", help="skip the wall-clock-to-convergence section")
     ap.add_argument("--nmpc-horizons", type=int, default=200, help="cfg-4 NMPC horizons (0: skip)")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="process-group backend; gloo (ranks may share a GPU) rehearses the N > 1 path on one card")
     return ap.parse_args()
 
 
@@ -264,12 +266,17 @@ def main():
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
     local = int(os.environ.get("LOCAL_RANK", 0))
+    if args.backend == "gloo":  # rehearsal: ranks share the visible GPUs
+        local %= max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dist = None
     if world > 1:
         import torch.distributed as dist
 
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.backend == "nccl":  # RCCL on ROCm
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
 
     ocp = build_problem()
     B = args.batch
@@ -298,7 +305,7 @@ def main():
     wall = time.perf_counter() - t0
     kern_ms = ev0.elapsed_time(ev1) / args.steps  # one kernel launch per step, on this stream
 
-    t = torch.tensor([wall], dtype=torch.float64, device=f"cuda:{local}")
+    t = torch.tensor([wall], dtype=torch.float64, device=f"cuda:{local}" if args.backend == "nccl" else "cpu")
     if dist:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     wall_max = float(t.item())
