@@ -607,3 +607,29 @@ def test_nmpc_pulse_width_with_fatigue_on_gpu():
                        x0=None)
         got = np.stack([res.states[k][b] for k in model.name_dof])
         np.testing.assert_allclose(got, ref, rtol=1e-6, atol=1e-6)
+
+
+@pytest.mark.parametrize("name", ["ding2007", "hmed2018", "ding2007_with_fatigue"])
+def test_interior_point_on_gpu_matches_the_oracle_driven_run(name):
+    """The same interior point driven by libcfx (GPU callbacks + band LU) and by the oracle on the CPU
+    (dense solves) lands on the same KKT point; with test_solver_cpu.py's scipy cross-check this ties the GPU
+    optimum to an independent NLP solver."""
+    from cocofest_amd.solver import BatchedIpm, IpmOptions
+    from tests.oracle_handle import DenseBandSolver, OracleHandle, oracle_problem_from_ocp
+
+    t = np.linspace(0, 1, 11)
+    cfg = dict(name=name, stims=[0.0, 0.05, 0.1, 0.15], final_time=0.2, truncation=4, scheme="RK1", m=5,
+               objective={"force_tracking": [t, 40 * t]}, n_shooting=None)
+    ocp = cases.product_ocp(**cfg)
+    pb = oracle_problem_from_ocp(ocp)
+    gpu = BatchedIpm(ocp, batch=2, options=IpmOptions(tol=1e-10))
+    rg = gpu.solve()
+    gpu.close()
+    cpu = BatchedIpm(ocp, batch=1, options=IpmOptions(tol=1e-10), handle=OracleHandle(pb, 1), torch_device="cpu",
+                     band=DenseBandSolver())
+    rc = cpu.solve()
+    assert rg.converged.all() and rc.converged.all()
+    np.testing.assert_allclose(rg.f, rc.f[0], rtol=1e-9)
+    ref = rc.v[0]
+    scale = np.where(np.abs(ref) < 1e-2, np.abs(ref) + 1e-6, np.maximum(np.abs(ref), 1e-3 * np.abs(ref).max()))
+    assert np.max(np.abs(rg.v - ref) / scale) < 1e-6

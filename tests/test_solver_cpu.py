@@ -1,6 +1,7 @@
 """The batched interior-point driver (cocofest_amd/solver.py) on the CPU, with the oracle as evaluator."""
 
 import numpy as np
+import pytest
 
 from oracle import fes_oracle as O
 from tests import cases
@@ -58,3 +59,52 @@ def test_zero_initial_guess_needs_multiplier_init_and_restoration():
     traj = O.ivp_integrate("ding2003", c, pb.rows, np.zeros((pb.n_shooting, 0)), 1.0, "RK1", 10)
     X, _, _ = pb.unpack(res.v)
     np.testing.assert_allclose(X[0].T, traj[:, ::10], rtol=1e-6, atol=1e-6)
+
+
+def _scipy_reference(ocp, pb):
+    """The same NLP solved by an independent solver (scipy trust-constr, exact g / J_g / f / grad f from the
+    oracle): the Ipopt stand-in for 'Ipopt-equivalent' optima (Ipopt / CasADi are not installable here)."""
+    from scipy.optimize import Bounds, NonlinearConstraint, minimize
+
+    lb, ub = ocp.bounds_vector()
+    free = lb != ub
+    sc = np.where(ub[free] - lb[free] < 1, ub[free] - lb[free], 1.0)
+    jr, jc = O.jac_structure(pb)
+
+    def full(y):
+        v = lb.copy()
+        v[free] = y * sc
+        return v[None]
+
+    def dG(y):
+        J = np.zeros((pb.ng, pb.nv))
+        J[jr, jc] = O.eval_jac_g(pb, full(y))[0]
+        return J[:, free] * sc
+
+    x0 = np.clip(ocp.initial_guess_vector()[free], lb[free], ub[free]) / sc
+    r = minimize(lambda y: O.eval_f(pb, full(y))[0], x0, jac=lambda y: O.eval_grad_f(pb, full(y))[0][free] * sc,
+                 method="trust-constr", constraints=[NonlinearConstraint(lambda y: O.eval_g(pb, full(y))[0], 0, 0,
+                                                                         jac=dG)],
+                 bounds=Bounds(lb[free] / sc, ub[free] / sc), options=dict(gtol=1e-12, xtol=1e-14, maxiter=5000))
+    return full(r.x)[0], r
+
+
+@pytest.mark.parametrize("name", ["ding2007", "hmed2018"])
+def test_interior_point_matches_an_independent_nlp_solver(name):
+    """Force tracking with 4 pulses (pulse widths / intensities free): the batched interior point and scipy's
+    trust-constr reach the same KKT point (decision vectors within 1e-8 relative, same objective)."""
+    import warnings
+
+    t = np.linspace(0, 1, 11)
+    cfg = dict(name=name, stims=[0.0, 0.05, 0.1, 0.15], final_time=0.2, truncation=4, scheme="RK1", m=5,
+               objective={"force_tracking": [t, 40 * t]}, n_shooting=None)
+    ocp, pb, ipm = _ipm(cfg, batch=1, tol=1e-10)
+    res = ipm.solve()
+    assert res.converged.all()
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        ref, r = _scipy_reference(ocp, pb)
+    np.testing.assert_allclose(res.f[0], r.fun, rtol=1e-9)
+    scale = np.maximum(np.abs(ref), 1e-3 * np.abs(ref).max())
+    scale = np.where(np.abs(ref) < 1e-2, np.abs(ref) + 1e-6, scale)  # pulse widths ~1e-4 s
+    assert np.max(np.abs(res.v[0] - ref) / scale) < 1e-6
