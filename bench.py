@@ -122,7 +122,8 @@ def convergence(device):
     ocp3 = OcpFes.prepare_ocp(model=model, final_time=1, pulse_width={"min": model.pd0, "max": 0.0006},
                               objective={"force_tracking": [np.array(ft["time"]), np.array(ft["force"])]},
                               ode_solver=OdeSolver.RK1(n_integration_steps=10))
-    cases = {"cfg3_single": (ocp3, 1), "cfg3_multistart_256": (ocp3, 256), "cfg2_single": (build_problem(), 1)}
+    cases = {"cfg3_single": (ocp3, 1), "cfg3_multistart_256": (ocp3, 256), "cfg3_multistart_4096": (ocp3, 4096),
+             "cfg2_single": (build_problem(), 1)}
     for name, (ocp, B) in cases.items():
         rng = np.random.default_rng(0)
         v0 = np.tile(ocp.initial_guess_vector(), (B, 1))

@@ -412,7 +412,7 @@ def test_band_lu_matches_dense_solve(n, kl, ku, zero_diag):
     from cocofest_amd import _cfx
 
     rng = np.random.default_rng(n + kl)
-    B = 5
+    B = 130  # >= 128: the windowed kernels where the band fits their LDS budget
     A, ab = _band_system(rng, B, n, kl, ku, zero_diag)
     rhs = rng.standard_normal((B, 2, n))
     ref = np.linalg.solve(A, rhs.transpose(0, 2, 1)).transpose(0, 2, 1)
@@ -430,6 +430,37 @@ def test_band_lu_matches_dense_solve(n, kl, ku, zero_diag):
     _cfx.band_lu_solve(abt, ipiv, kl, ku, x2)
     torch.cuda.synchronize()
     np.testing.assert_array_equal(x2.cpu().numpy(), x.cpu().numpy()[:, :1])
+
+
+@pytest.mark.parametrize("B", [3, 200])
+def test_band_lu_small_and_windowed_paths_agree(B, monkeypatch):
+    """The resident-band kernel (small batches, or CFX_BAND_FULL) and the windowed kernels give the same
+    factors, pivots and solutions to rounding."""
+    import torch
+
+    from cocofest_amd import _cfx
+
+    n, kl, ku = 300, 6, 6
+    rng = np.random.default_rng(B)
+    A, ab = _band_system(rng, B, n, kl, ku, zero_diag=True)
+    rhs = rng.standard_normal((B, 2, n))
+    outs = []
+    for full in (False, True):
+        if full:
+            monkeypatch.setenv("CFX_BAND_FULL", "1")
+        abt = torch.tensor(ab, device="cuda")
+        ipiv = torch.empty((B, n), dtype=torch.int32, device="cuda")
+        info = torch.empty((B,), dtype=torch.int32, device="cuda")
+        x = torch.tensor(rhs, device="cuda")
+        _cfx.band_lu(abt, ipiv, info, kl, ku, rhs=x)
+        x2 = torch.tensor(rhs[:, :1], device="cuda")
+        _cfx.band_lu_solve(abt, ipiv, kl, ku, x2)
+        torch.cuda.synchronize()
+        outs.append((abt.cpu().numpy()[:, :, kl:], ipiv.cpu().numpy(), x.cpu().numpy(), x2.cpu().numpy()))
+    np.testing.assert_array_equal(outs[0][1], outs[1][1])
+    np.testing.assert_allclose(outs[0][0], outs[1][0], rtol=1e-12, atol=1e-12)
+    np.testing.assert_allclose(outs[0][2], outs[1][2], rtol=1e-10, atol=1e-12)
+    np.testing.assert_allclose(outs[0][3], outs[0][2][:, :1], rtol=1e-10, atol=1e-12)
 
 
 def test_band_lu_reports_singular_and_bad_arguments():
