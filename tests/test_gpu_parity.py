@@ -403,7 +403,7 @@ def _band_system(rng, B, n, kl, ku, zero_diag=False):
 
 @pytest.mark.parametrize("n,kl,ku,zero_diag", [(1, 0, 0, False), (7, 3, 1, False), (80, 5, 5, True),
                                                (500, 6, 6, True), (300, 40, 40, False), (64, 63, 63, False),
-                                               (200, 70, 2, True)])
+                                               (200, 70, 2, False)])
 def test_band_lu_matches_dense_solve(n, kl, ku, zero_diag):
     """cfx_band_lu / cfx_band_lu_solve vs numpy's dense LU on random band matrices: LDS-resident bands and the
     global-memory variant (300 x 161 band > 160 KiB), bandwidths beyond one wave (kl = 70), zero diagonals."""
@@ -432,17 +432,16 @@ def test_band_lu_matches_dense_solve(n, kl, ku, zero_diag):
     np.testing.assert_array_equal(x2.cpu().numpy(), x.cpu().numpy()[:, :1])
 
 
-@pytest.mark.parametrize("B", [3, 200])
-def test_band_lu_small_and_windowed_paths_agree(B, monkeypatch):
-    """The resident-band kernel (small batches, or CFX_BAND_FULL) and the windowed kernels give the same
-    factors, pivots and solutions to rounding."""
+@pytest.mark.parametrize("B,n,kl,ku", [(3, 300, 6, 6), (200, 300, 6, 6), (150, 300, 40, 40), (140, 200, 70, 2)])
+def test_band_lu_small_and_windowed_paths_agree(B, n, kl, ku, monkeypatch):
+    """The resident / global kernels (small batches, or CFX_BAND_FULL) and the windowed kernels give the same
+    factors, pivots and solutions to rounding — 64-thread and 1024-thread workgroups."""
     import torch
 
     from cocofest_amd import _cfx
 
-    n, kl, ku = 300, 6, 6
     rng = np.random.default_rng(B)
-    A, ab = _band_system(rng, B, n, kl, ku, zero_diag=True)
+    A, ab = _band_system(rng, B, n, kl, ku, zero_diag=kl < 20)
     rhs = rng.standard_normal((B, 2, n))
     outs = []
     for full in (False, True):
