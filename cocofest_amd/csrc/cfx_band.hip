@@ -8,7 +8,7 @@
 // step is a pivot search (argmax), a row swap, a scale and a rank-1 update of the km x (ju - j) trailing
 // block, spread over the workgroup's NT threads (64 for narrow bands, 256 / 1024 for wide ones).
 //
-// Three placements of the band:
+// Four placements of the band (the register one is described with its kernels below):
 //  * windowed (batches >= 128, or whenever the whole band does not fit LDS): the step at column j only
 //    touches columns j .. j + kl + ku, so LDS holds a circular window of kl + ku + 2 columns; column j is
 //    stored to HBM with one coalesced write as it leaves and column j + kl + ku + 1 is loaded; pivots and
@@ -27,10 +27,21 @@
 #include <algorithm>
 #include <cstdlib>
 #include <string>
+#include <type_traits>
 
 #include "../../include/cfx.h"
 
 extern thread_local std::string g_create_error;
+
+#define CFX_INLINE __attribute__((always_inline))  // lambdas over register arrays: never outlined
+
+template <int A, int B, class F>
+__device__ __forceinline__ void static_for(F&& f) {  // f(integral_constant<A>), ..., f(integral_constant<B - 1>)
+    if constexpr (A < B) {
+        f(std::integral_constant<int, A>{});
+        static_for<A + 1, B>(f);
+    }
+}
 
 namespace cfx {
 
@@ -334,6 +345,340 @@ __global__ void __launch_bounds__(NT) k_band_solve_win(int n, int kl, int ku, in
 }
 
 // ---------------------------------------------------------------------------------------------------
+// register placement: one wavefront per instance, the active window in VGPRs
+// ---------------------------------------------------------------------------------------------------
+// The step at column j touches rows j .. j + kl and columns j .. j + kv.  Lane c holds columns j + c + 64 k
+// (k < KC) of that window, its rows in registers r[k][0 .. kl].  A step is: pivot search down lane 0's
+// registers, a register swap in every lane (the pivot row index is wave-uniform), the multipliers
+// broadcast with v_readlane and one FMA per row in every lane, the U row stored by the lanes that hold it,
+// then the window slides: rows move up one register and columns one lane left (DPP wave_shl), and the next
+// row of the original band, prefetched during the step, enters at the bottom.  No LDS and no barriers:
+// the per-column latency of the shared-memory kernels above (LDS round trips + __syncthreads) is the whole
+// cost of a single solve, and this is what removes it.  Bands with kl <= 63 and kv < 64 KC.
+__device__ __forceinline__ double lane_read(double v, int l) {  // v on lane l (wave-uniform l)
+    const unsigned long long u = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)(unsigned)u, l);
+    const int hi = __builtin_amdgcn_readlane((int)(unsigned)(u >> 32), l);
+    return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+}
+__device__ __forceinline__ double from_next_lane(double v) {  // v on lane + 1, 0.0 on lane 63
+    const unsigned long long u = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_mov_dpp((int)(unsigned)u, 0x130, 0xf, 0xf, true);  // wave_shl:1
+    const int hi = __builtin_amdgcn_mov_dpp((int)(unsigned)(u >> 32), 0x130, 0xf, 0xf, true);
+    return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+}
+// lanes i <- i + 1 across the KC registers of a 64 KC-long vector (the last lane of register k takes the
+// first lane of register k + 1)
+template <int KC>
+__device__ __forceinline__ void slide(double (&v)[KC]) {
+    const int lane = threadIdx.x;
+    static_for<0, KC>([&](auto K_) CFX_INLINE {
+        constexpr int k = decltype(K_)::value;
+        double s = from_next_lane(v[k]);
+        if (k + 1 < KC) {
+            const double head = lane_read(v[k + 1], 0);
+            s = lane == 63 ? head : s;
+        }
+        v[k] = s;
+    });
+}
+
+// Loads run D steps ahead of their use (a D-deep software pipeline, unrolled so that every prefetch keeps
+// its own registers): the waitcnt before a use then only covers loads issued D steps earlier, never the
+// stores of the steps in between.  Every prefetched element is one no earlier step writes.
+
+// The window is padded to KLM = 8 NCH - 1 >= kl rows: rows j + kl + 1 .. j + KLM hold zeros in column j
+// (outside the band, and no earlier step reaches them), so they are never chosen as pivots and take zero
+// multipliers — the factors are exactly those of the kl-row window, and every register loop has a
+// compile-time trip count (static_for: constant register indices from the front end on, so the window
+// never leaves registers).  Rows past n are zeros as well.  The pivot row (a wave-uniform index) is
+// swapped in by a chain of uniform branches, one taken.
+// Write target of lanes with nothing to store (shared by every wave; its contents are meaningless).
+__device__ double g_band_sink[64 * 4];
+
+
+// rows 0 and p of the window (p wave-uniform): one uniform branch per row, kept apart by the volatile asm
+// (neither if-converted to KLM selects per register nor merged)
+template <int KLM, int KC>
+__device__ __forceinline__ void swap_rows(double (&r)[KC][KLM + 1], int p) {
+    static_for<1, KLM + 1>([&](auto I) CFX_INLINE {
+        constexpr int i = decltype(I)::value;
+        if (p == i) {
+#pragma unroll
+            for (int k = 0; k < KC; ++k) {
+                const double t = r[k][0];
+                r[k][0] = r[k][i];
+                r[k][i] = t;
+            }
+            asm volatile("; swap row %0" ::"i"(i));  // distinct tail per branch: the branches are neither
+                                                     // if-converted nor sunk into one swap via a pointer
+        }
+    });
+}
+template <int L>
+__device__ __forceinline__ int write_lane(int x, int old) {  // old with lane L replaced by the uniform x
+    asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(old) : "s"(x), "i"(L));
+    return old;
+}
+__device__ __forceinline__ int lo32(double v) { return (int)(unsigned)__double_as_longlong(v); }
+__device__ __forceinline__ int hi32(double v) { return (int)(unsigned)((unsigned long long)__double_as_longlong(v) >> 32); }
+__device__ __forceinline__ double from32(int lo, int hi) {
+    return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+}
+
+// x <- U^-1 L^-1 P x for nrhs right-hand sides x[c * n + i] with the factors of k_band_lu*: forward pass
+// with lane i holding x[j + i] (i <= kl), backward pass with lane i + 64 k holding x[j - i - 64 k] (<= kv).
+// Same pipeline discipline as the factorisation: prefetches D steps ahead, consumed (and pinned) before the
+// step's store, every lane storing (to the sink when it has nothing to store).
+template <int KC, int D>
+__device__ __forceinline__ void reg_solve(int n, int kl, int ku, int nrhs, const double* ab, const int32_t* piv,
+                                          double* xs) {
+    const int lane = threadIdx.x;
+    const int ldab = 2 * kl + ku + 1, kv = kl + ku;
+    double* dsink = g_band_sink + lane;
+    for (int c = 0; c < nrhs; ++c) {
+        double* x = xs + (int64_t)c * n;
+        if (kl > 0) {
+            // prefetches load unconditionally from clamped addresses and are masked at their use
+            auto mult_ok = [&](int j) { return j < n && lane >= 1 && lane <= min(kl, n - 1 - j); };
+            auto mult = [&](int j) { return ab[mult_ok(j) ? j * ldab + kv + lane : 0]; };  // L(j + lane, j)
+            auto enter_ok = [&](int j) { return lane == kl && j + 1 + kl < n; };
+            auto enter = [&](int j) { return x[enter_ok(j) ? j + 1 + kl : 0]; };
+            auto pivot = [&](int j) { return piv[min(j, n - 1)]; };
+            double xw = (lane <= kl && lane < n) ? x[lane] : 0.0;
+            double lc[D], nx[D];
+            int pj[D];
+            static_for<0, D>([&](auto S_) CFX_INLINE {
+                constexpr int s = decltype(S_)::value;
+                lc[s] = mult(s);
+                nx[s] = enter(s);
+                pj[s] = pivot(s);
+            });
+            auto step = [&](int j, double& lcs, double& nxs, int& pjs, int jpre) CFX_INLINE {
+                double lcv = mult_ok(j) ? lcs : 0.0, nxv = enter_ok(j) ? nxs : 0.0;
+                int pjv = pjs;
+                asm volatile("" : "+v"(lcv), "+v"(nxv), "+v"(pjv)::"memory");
+                lcs = mult(jpre);
+                nxs = enter(jpre);
+                pjs = pivot(jpre);
+                const int p = __builtin_amdgcn_readfirstlane(pjv) - j;
+                if (p != 0) {
+                    const double a = lane_read(xw, 0), b = lane_read(xw, p);
+                    xw = lane == 0 ? b : (lane == p ? a : xw);
+                }
+                const double xj = lane_read(xw, 0);
+                xw -= lcv * xj;
+                *(lane == 0 ? x + j : dsink) = xj;
+                xw = from_next_lane(xw);
+                if (lane == kl) xw = nxv;
+            };
+            int j0 = 0;
+            for (; j0 + D <= n - 1; j0 += D) {
+                static_for<0, D>([&](auto S_) CFX_INLINE {
+                    constexpr int s = decltype(S_)::value;
+                    step(j0 + s, lc[s], nx[s], pj[s], j0 + s + D);
+                });
+            }
+            static_for<0, D>([&](auto S_) CFX_INLINE {
+                constexpr int s = decltype(S_)::value;
+                if (j0 + s < n - 1) step(j0 + s, lc[s], nx[s], pj[s], n);
+            });
+            if (lane == 0) x[n - 1] = xw;
+            __threadfence();  // the backward pass re-reads what this one stored
+        }
+        // U(j - i, j) on lane i = lane + 64 k <= min(kv, j) (i = 0: the diagonal)
+        auto ucol_ok = [&](int j, int k) { return j >= 0 && lane + 64 * k <= min(kv, j); };
+        auto ucol = [&](int j, int k) { return ab[ucol_ok(j, k) ? j * ldab + kv - lane - 64 * k : 0]; };
+        auto enter_ok = [&](int j, int k) { return lane + 64 * k == kv && j - 1 - kv >= 0; };
+        auto enter = [&](int j, int k) { return x[enter_ok(j, k) ? j - 1 - kv : 0]; };
+        double xw[KC], uc[D][KC], nx[D][KC];
+        static_for<0, KC>([&](auto K_) CFX_INLINE {
+            constexpr int k = decltype(K_)::value;
+            const int i = lane + 64 * k;
+            xw[k] = (i <= kv && n - 1 - i >= 0) ? x[n - 1 - i] : 0.0;
+#pragma unroll
+            for (int s = 0; s < D; ++s) {
+                uc[s][k] = ucol(n - 1 - s, k);
+                nx[s][k] = enter(n - 1 - s, k);
+            }
+        });
+        auto step = [&](int j, double (&ucs)[KC], double (&nxs)[KC], int jpre) CFX_INLINE {
+            double ucv[KC], nxv[KC];
+            static_for<0, KC>([&](auto K_) CFX_INLINE {
+                constexpr int k = decltype(K_)::value;
+                ucv[k] = ucol_ok(j, k) ? ucs[k] : 0.0;
+                nxv[k] = enter_ok(j, k) ? nxs[k] : 0.0;
+                asm volatile("" : "+v"(ucv[k]), "+v"(nxv[k])::"memory");
+                ucs[k] = ucol(jpre, k);
+                nxs[k] = enter(jpre, k);
+            });
+            const double xj = lane_read(xw[0], 0) / lane_read(ucv[0], 0);
+            *(lane == 0 ? x + j : dsink) = xj;
+            static_for<0, KC>([&](auto K_) CFX_INLINE {
+                constexpr int k = decltype(K_)::value;
+                xw[k] -= (k == 0 && lane == 0) ? 0.0 : ucv[k] * xj;
+            });
+            slide<KC>(xw);
+            static_for<0, KC>([&](auto K_) CFX_INLINE {
+                constexpr int k = decltype(K_)::value;
+                if (lane + 64 * k == kv) xw[k] = nxv[k];
+            });
+        };
+        int j0 = n - 1;
+        for (; j0 - D + 1 >= 0; j0 -= D) {
+            static_for<0, D>([&](auto S_) CFX_INLINE {
+                constexpr int s = decltype(S_)::value;
+                step(j0 - s, uc[s], nx[s], j0 - s - D);
+            });
+        }
+        static_for<0, D>([&](auto S_) CFX_INLINE {
+            constexpr int s = decltype(S_)::value;
+            if (j0 - s >= 0) step(j0 - s, uc[s], nx[s], -1);
+        });
+    }
+}
+
+template <int NCH, int KC, int D>
+__global__ void __launch_bounds__(64) k_band_lu_reg(int n, int kl, int ku, int nrhs, double* __restrict__ AB,
+                                                    int32_t* __restrict__ IPIV, double* __restrict__ RHS,
+                                                    int32_t* __restrict__ INFO) {
+    constexpr int KLM = 8 * NCH - 1;
+    const int lane = threadIdx.x;
+    const int64_t b = blockIdx.x;
+    const int ldab = 2 * kl + ku + 1, kv = kl + ku;  // n * ldab < 2^31 (checked at dispatch)
+    double* ab = AB + b * (int64_t)n * ldab;
+    int32_t* piv = IPIV + b * n;
+    // lane constants: U(j, j + c) is ab[j ldab + cofs]; the entering row's element is ab[(j + 1) ldab + cofs
+    // + KLM], inside the band for KLM - kl <= c <= KLM + ku
+    int cofs[KC];
+    bool uok[KC], eok[KC];
+    static_for<0, KC>([&](auto K_) CFX_INLINE {
+        constexpr int k = decltype(K_)::value;
+        const int c = lane + 64 * k;
+        cofs[k] = c * (ldab - 1) + kv;
+        uok[k] = c <= kv;
+        eok[k] = c >= KLM - kl && c <= KLM + ku;
+    });
+    auto entering_ok = [&](int j, int k) { return eok[k] && j + 1 + KLM < n && j + 1 + lane + 64 * k < n; };
+    // prefetches load unconditionally (element 0 stands in outside the band) and are masked at their use
+    auto fetch = [&](int j, int k) { return ab[entering_ok(j, k) ? (j + 1) * ldab + cofs[k] + KLM : 0]; };
+    // every lane stores every step (lanes with nothing to store write the sink): no store sits under a
+    // branch, so the compiler's vmcnt waits for a prefetch count the stores issued after it exactly
+    double* dsink = g_band_sink + lane;
+    int32_t* isink = reinterpret_cast<int32_t*>(g_band_sink + 64 * KC) + lane;
+
+    double r[KC][KLM + 1];  // r[k][i]: row j + i of the window, column j + lane + 64 k
+    static_for<0, KC>([&](auto K_) CFX_INLINE {
+        constexpr int k = decltype(K_)::value;
+        const int c = lane + 64 * k;
+        static_for<0, KLM + 1>([&](auto I) CFX_INLINE {
+            constexpr int i = decltype(I)::value;
+            r[k][i] = (i < n && c < n && i - c <= kl && c - i <= ku) ? ab[c * ldab + kv + i - c] : 0.0;
+        });
+        // fill-in positions above the matrix, which no U row reaches (LAPACK zeroes them too)
+        if (c < min(kv, n))
+            for (int q = 0; q < min(kl, kv - c); ++q) ab[c * ldab + q] = 0.0;
+    });
+    double nxt[D][KC];  // row j + 1 + KLM enters the window after step j; fetched D steps ahead
+    static_for<0, D>([&](auto S_) CFX_INLINE {
+        constexpr int s = decltype(S_)::value;
+        static_for<0, KC>([&](auto K_) CFX_INLINE { nxt[s][decltype(K_)::value] = fetch(s, decltype(K_)::value); });
+    });
+    int info = 0;
+
+    auto step = [&](int j, double (&pre)[KC], int jpre) CFX_INLINE {
+        // take the row that enters after this step and refill its slot (row of step jpre) before this
+        // step's stores, so that the wait for a prefetch never covers stores just issued
+        double ent[KC];
+        static_for<0, KC>([&](auto K_) CFX_INLINE {
+            constexpr int k = decltype(K_)::value;
+            ent[k] = entering_ok(j, k) ? pre[k] : 0.0;
+            asm volatile("" : "+v"(ent[k])::"memory");  // pinned here: not sunk past the stores below
+            pre[k] = fetch(jpre, k);
+        });
+        // pivot: first largest |A(j + i, j)| on lane 0 (column j is its first register)
+        double best = fabs(r[0][0]);
+        int p = 0;
+        static_for<1, KLM + 1>([&](auto I) CFX_INLINE {
+            constexpr int i = decltype(I)::value;
+            const double a = fabs(r[0][i]);
+            p = a > best ? i : p;
+            best = fmax(best, a);
+        });
+        p = __builtin_amdgcn_readfirstlane(p);
+        *(lane == 0 ? piv + j : isink) = j + p;
+        // u: the pivot row (row j of U); row p takes row j
+        swap_rows<KLM, KC>(r, p);
+        double u[KC];
+        static_for<0, KC>([&](auto K_) CFX_INLINE {
+            constexpr int k = decltype(K_)::value;
+            u[k] = r[k][0];
+            *(uok[k] && j + lane + 64 * k < n ? ab + j * ldab + cofs[k] : dsink + 64 * k) = u[k];
+        });
+        const double pivot = lane_read(u[0], 0);
+        // multipliers (all zero for a zero pivot, whose column is zero: the stored column is unchanged)
+        const double inv = pivot != 0.0 ? 1.0 / pivot : 0.0;
+        if (pivot == 0.0 && info == 0) info = j + 1;
+        int llo = 0, lhi = 0;  // lane i gathers L(j + i, j)
+        static_for<1, KLM + 1>([&](auto I) CFX_INLINE {
+            constexpr int i = decltype(I)::value;
+            const double t = r[0][i] * inv;  // lane 0's value is L(j + i, j)
+            const int tlo = __builtin_amdgcn_readlane(lo32(t), 0), thi = __builtin_amdgcn_readlane(hi32(t), 0);
+            llo = write_lane<i>(tlo, llo);
+            lhi = write_lane<i>(thi, lhi);
+            const double l = from32(tlo, thi);
+            static_for<0, KC>([&](auto K_) CFX_INLINE {
+                constexpr int k = decltype(K_)::value;
+                r[k][i] -= l * u[k];
+            });
+        });
+        *(lane >= 1 && lane <= min(kl, n - 1 - j) ? ab + j * ldab + kv + lane : dsink + 64 * KC) = from32(llo, lhi);
+        // slide the window down-right by one; the prefetched row enters at the bottom
+        static_for<0, KLM>([&](auto I) CFX_INLINE {
+            constexpr int i = decltype(I)::value;
+            double row[KC];
+            static_for<0, KC>([&](auto K_) CFX_INLINE {
+                constexpr int k = decltype(K_)::value;
+                row[k] = r[k][i + 1];
+            });
+            slide<KC>(row);
+            static_for<0, KC>([&](auto K_) CFX_INLINE {
+                constexpr int k = decltype(K_)::value;
+                r[k][i] = row[k];
+            });
+        });
+        static_for<0, KC>([&](auto K_) CFX_INLINE {
+            constexpr int k = decltype(K_)::value;
+            r[k][KLM] = ent[k];
+        });
+    };
+    int j0 = 0;
+    for (; j0 + D <= n; j0 += D) {
+        static_for<0, D>([&](auto S_) CFX_INLINE {
+            constexpr int s = decltype(S_)::value;
+            step(j0 + s, nxt[s], j0 + s + D);
+        });
+    }
+    static_for<0, D>([&](auto S_) CFX_INLINE {  // the last steps prefetch nothing (their rows are past n)
+        constexpr int s = decltype(S_)::value;
+        if (j0 + s < n) step(j0 + s, nxt[s], n);
+    });
+    if (lane == 0) INFO[b] = info;
+    if (nrhs > 0) {
+        __threadfence();  // the solve reads the factors stored above
+        reg_solve<KC, D>(n, kl, ku, nrhs, ab, piv, RHS + b * (int64_t)n * nrhs);
+    }
+}
+
+template <int KC, int D>
+__global__ void __launch_bounds__(64) k_band_solve_reg(int n, int kl, int ku, int nrhs, const double* __restrict__ AB,
+                                                       const int32_t* __restrict__ IPIV, double* __restrict__ RHS) {
+    const int64_t b = blockIdx.x;
+    reg_solve<KC, D>(n, kl, ku, nrhs, AB + b * (int64_t)n * (2 * kl + ku + 1), IPIV + b * n,
+                     RHS + b * (int64_t)n * nrhs);
+}
+
+// ---------------------------------------------------------------------------------------------------
 // dispatch
 // ---------------------------------------------------------------------------------------------------
 template <class K>
@@ -369,6 +714,53 @@ static hipError_t launch_nt(int placement, int64_t n, int32_t kl, int32_t ku, in
     return hipGetLastError();
 }
 
+template <int NCH, int KC, int D = (NCH <= 2 && KC == 1) ? 8 : 2>
+static hipError_t launch_reg(int64_t n, int32_t kl, int32_t ku, int64_t batch, double* ab, int32_t* ipiv,
+                             int32_t* info, int32_t nrhs, double* rhs, hipStream_t s, int factor) {
+    if (factor)
+        hipLaunchKernelGGL((k_band_lu_reg<NCH, KC, D>), dim3((unsigned)batch), dim3(64), 0, s, (int)n, kl, ku, nrhs,
+                           ab, ipiv, rhs, info);
+    else
+        hipLaunchKernelGGL((k_band_solve_reg<KC, D>), dim3((unsigned)batch), dim3(64), 0, s, (int)n, kl, ku, nrhs,
+                           (const double*)ab, (const int32_t*)ipiv, rhs);
+    return hipGetLastError();
+}
+
+// Register placement when the window fits: the padded rows (8 NCH - 1 >= kl) plus the ku + 1 columns of
+// the pivot row within 64 KC lanes, and 32-bit offsets within an instance.
+static int reg_chunks(int64_t n, int32_t kl, int32_t ku) {
+    const int64_t ldab = 2 * (int64_t)kl + ku + 1;
+    if (n * ldab >= (int64_t)1 << 31) return -1;
+    const int nch = kl / 8 + 1;  // 8 nch - 1 >= kl
+    if (nch > 6 || 8 * nch + ku > 128) return -1;
+    return nch;
+}
+
+static hipError_t reg_dispatch(int64_t n, int32_t kl, int32_t ku, int64_t batch, double* ab, int32_t* ipiv,
+                               int32_t* info, int32_t nrhs, double* rhs, hipStream_t s, int factor) {
+#define CFX_REG(M, C) launch_reg<M, C>(n, kl, ku, batch, ab, ipiv, info, nrhs, rhs, s, factor)
+    const int nch = reg_chunks(n, kl, ku);
+    if (8 * nch + ku <= 64) {
+        switch (nch) {
+            case 1: return CFX_REG(1, 1);
+            case 2: return CFX_REG(2, 1);
+            case 3: return CFX_REG(3, 1);
+            case 4: return CFX_REG(4, 1);
+            case 5: return CFX_REG(5, 1);
+            default: return CFX_REG(6, 1);
+        }
+    }
+    switch (nch) {
+        case 1: return CFX_REG(1, 2);
+        case 2: return CFX_REG(2, 2);
+        case 3: return CFX_REG(3, 2);
+        case 4: return CFX_REG(4, 2);
+        case 5: return CFX_REG(5, 2);
+        default: return CFX_REG(6, 2);
+    }
+#undef CFX_REG
+}
+
 static int band_launch(int64_t n, int32_t kl, int32_t ku, int64_t batch, double* ab, int32_t* ipiv, int32_t* info,
                        int32_t nrhs, double* rhs, void* stream, int factor) {
     if (n < 1 || n > (1 << 24) || kl < 0 || ku < 0 || kl >= n || ku >= n || batch < 1 || batch > 0x7fffffff ||
@@ -383,11 +775,25 @@ static int band_launch(int64_t n, int32_t kl, int32_t ku, int64_t batch, double*
     const int chunk = (int)std::max<int64_t>(1, std::min<int64_t>(kChunk, (kBandLds - fixed_win) / (ldab * 8)));
     const size_t lds_win = (size_t)(fixed_win + (int64_t)chunk * ldab * 8);
     const size_t lds_full = (size_t)(n * ldab + n * nrhs) * sizeof(double) + (size_t)n * sizeof(int32_t);
-    // placement: small batches keep the whole band resident when it fits (latency-bound); otherwise the
-    // window; bands too wide for both run on the global copy.  CFX_BAND_FULL forces resident / global.
+    // placement: the register kernels whenever the window fits a wavefront's registers; otherwise small
+    // batches keep the whole band resident when it fits LDS (latency-bound), larger ones use the window,
+    // and bands too wide for both run on the global copy.  CFX_BAND_PLACEMENT=0..3 forces one (where it
+    // fits); CFX_BAND_FULL forces resident / global.
     int placement;
     const bool force_full = std::getenv("CFX_BAND_FULL") != nullptr;
-    if (!force_full && !(batch < 128 && lds_full <= (size_t)kBandLds) && lds_win <= (size_t)kBandLds && chunk >= 4)
+    const char* forced = std::getenv("CFX_BAND_PLACEMENT");
+    const bool win_ok = lds_win <= (size_t)kBandLds && chunk >= 4;
+    // the register solve (one wave per instance) loses to the windowed one once the batch fills the chip
+    const bool reg_ok = reg_chunks(n, kl, ku) > 0 && (factor || batch < 2048 || !win_ok);
+    if (forced && *forced == '3' && reg_chunks(n, kl, ku) > 0)
+        placement = 3;
+    else if (forced && *forced == '0' && win_ok)
+        placement = 0;
+    else if (forced && (*forced == '1' || *forced == '2'))
+        placement = lds_full <= (size_t)kBandLds ? 1 : 2;
+    else if (!force_full && !forced && reg_ok)
+        placement = 3;
+    else if (!force_full && !(batch < 128 && lds_full <= (size_t)kBandLds) && win_ok)
         placement = 0;
     else
         placement = lds_full <= (size_t)kBandLds ? 1 : 2;
@@ -396,7 +802,9 @@ static int band_launch(int64_t n, int32_t kl, int32_t ku, int64_t batch, double*
     const int64_t work = (int64_t)kl * (kl + ku);
     const hipStream_t s = (hipStream_t)stream;
     hipError_t e;
-    if (work <= 192)
+    if (placement == 3)
+        e = reg_dispatch(n, kl, ku, batch, ab, ipiv, info, nrhs, rhs, s, factor);
+    else if (work <= 192)
         e = launch_nt<64>(placement, n, kl, ku, batch, ab, ipiv, info, nrhs, rhs, s, factor, lds, chunk);
     else if (work <= 2048)
         e = launch_nt<256>(placement, n, kl, ku, batch, ab, ipiv, info, nrhs, rhs, s, factor, lds, chunk);
