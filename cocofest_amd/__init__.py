@@ -2,7 +2,8 @@
 
 The public names mirror the reference package (Ipuch/cocofest) for the accelerated path: the six FES
 models, ``ModelMaker``, ``OcpFes``, ``IvpFes``, ``FourierSeries`` and the bioptim-style ``OdeSolver`` /
-``ObjectiveFcn`` / ``ObjectiveList`` / ``Node`` the reference's call sites use, ``FesNmpc`` (receding
+``ObjectiveFcn`` / ``ObjectiveList`` / ``Node`` the reference's call sites use, ``FesMskModel`` / ``OcpFesMsk``
+(FES muscles driving a bioMod skeleton), ``FesNmpc`` (receding
 horizon, every model family) and the batched interior-point driver standing in for Ipopt.  All NLP callbacks and
 integrations execute in libcfx (hand-written HIP for gfx950) — there is no CPU evaluation path.
 """
@@ -20,6 +21,7 @@ from .fes_models import (
 )
 from .fourier import FourierSeries
 from .ivp import IvpFes
+from .msk import FesMskModel, FesMskOcp, OcpFesMsk
 from .nmpc import FesNmpc, NmpcResult
 from .ocp import FesOcp, Node, Objective, ObjectiveFcn, ObjectiveList, OcpFes
 from .ode_solver import ControlType, OdeSolver
@@ -30,5 +32,5 @@ __all__ = [
     "DingModelPulseIntensityFrequency", "DingModelPulseIntensityFrequencyWithFatigue",
     "DingModelPulseWidthFrequency", "DingModelPulseWidthFrequencyWithFatigue", "FesModel", "ModelMaker",
     "FourierSeries", "IvpFes", "FesOcp", "Node", "Objective", "ObjectiveFcn", "ObjectiveList", "OcpFes",
-    "ControlType", "OdeSolver", "FesNmpc", "NmpcResult", "BatchedIpm", "IpmOptions", "IpmResult",
+    "ControlType", "OdeSolver", "FesMskModel", "FesMskOcp", "OcpFesMsk", "FesNmpc", "NmpcResult", "BatchedIpm", "IpmOptions", "IpmResult",
 ]

@@ -29,7 +29,8 @@ RK1, RK2, RK4 = 1, 2, 4
 COLLOCATION_LEGENDRE, COLLOCATION_RADAU = 16, 17
 LAYOUT_AOS, LAYOUT_SOA, LAYOUT_TILED64 = 0, 1, 2
 DEVICE = 1
-OBJ_LAGRANGE, OBJ_MAYER = 0, 1
+OBJ_LAGRANGE, OBJ_MAYER, OBJ_MAYER_INV = 0, 1, 2
+MSK_FORCE_LENGTH, MSK_FORCE_VELOCITY, MSK_PASSIVE_FORCE, MSK_RESIDUAL_TORQUE = 1, 2, 4, 8
 VAR_STATE, VAR_CONTROL = 0, 1
 
 
@@ -67,6 +68,24 @@ class Problem(C.Structure):
     ]
 
 
+class MskMuscle(C.Structure):
+    _fields_ = [("model", C.c_int32), ("constants", Constants), ("n_points", C.c_int32),
+                ("point_frame", C.POINTER(C.c_int32)), ("point_pos", C.POINTER(C.c_double)),
+                ("optimal_length", C.c_double), ("tendon_slack_length", C.c_double), ("pennation_angle", C.c_double)]
+
+
+class MskProblem(C.Structure):
+    _fields_ = [
+        ("abi_version", C.c_int32), ("scheme", C.c_int32), ("n_steps", C.c_int32), ("n_shooting", C.c_int32),
+        ("truncation", C.c_int32), ("layout", C.c_int32), ("batch", C.c_int64), ("final_time", C.c_double),
+        ("stim_rows", C.POINTER(C.c_double)), ("n_dof", C.c_int32), ("dof_axis", C.POINTER(C.c_int32)),
+        ("dof_frame", C.POINTER(C.c_double)), ("gravity", C.c_double * 3), ("body_mass", C.POINTER(C.c_double)),
+        ("body_com", C.POINTER(C.c_double)), ("body_inertia", C.POINTER(C.c_double)), ("n_muscles", C.c_int32),
+        ("muscles", C.POINTER(MskMuscle)), ("flags", C.c_uint32), ("n_objectives", C.c_int32),
+        ("objectives", C.POINTER(Objective)), ("device", C.c_int32),
+    ]
+
+
 class Sizes(C.Structure):
     _fields_ = [("nv", C.c_int64), ("ng", C.c_int64), ("nnz_jac", C.c_int64), ("nnz_hess", C.c_int64),
                 ("nx", C.c_int32), ("nu", C.c_int32)]
@@ -93,6 +112,7 @@ SIGNATURES = {
     "cfx_eval_h": (C.c_int, [_P, _P, _P, _P, _P, C.c_uint32]),
     "cfx_eval_all": (C.c_int, [_P, _P, _P, _P, _P, _P, C.c_uint32]),
     "cfx_integrate": (C.c_int, [_P, _P, _P, _P, C.c_uint32]),
+    "cfx_msk_create": (C.c_int, [C.POINTER(MskProblem), C.POINTER(_P)]),
     "cfx_band_lu": (C.c_int, [C.c_int64, C.c_int32, C.c_int32, C.c_int64, _P, _P, _P, C.c_int32, _P, _P]),
     "cfx_band_lu_solve": (C.c_int, [C.c_int64, C.c_int32, C.c_int32, C.c_int64, _P, _P, C.c_int32, _P, _P]),
 }
@@ -179,6 +199,24 @@ def band_lu_solve(ab, ipiv, kl: int, ku: int, rhs):
         raise CfxError(rc, lib.cfx_last_error(None).decode())
 
 
+def _objective_array(objectives, keep):
+    objs = (Objective * max(1, len(objectives)))()
+    for i, o in enumerate(objectives):
+        objs[i].kind = o["kind"]
+        objs[i].var_kind = o["var_kind"]
+        objs[i].var_index = o["var_index"]
+        objs[i].node_first = o["node_first"]
+        objs[i].node_last = o["node_last"]
+        objs[i].weight = o["weight"]
+        if o.get("target") is not None:
+            t = np.ascontiguousarray(o["target"], dtype=np.float64)
+            keep.append(t)
+            objs[i].target = t.ctypes.data_as(_D)
+        objs[i].target_value = float(o.get("target_value", 0.0))
+    keep.append(objs)
+    return objs
+
+
 class Handle:
     """One libcfx handle: a batch of B instances of one transcribed FES problem on one GPU.
 
@@ -214,25 +252,15 @@ class Handle:
         for name, _ in Constants._fields_:
             setattr(cst, name, float(constants.get(name, 0.0)))
         pb.constants = cst
-        objs = (Objective * max(1, len(objectives)))()
-        for i, o in enumerate(objectives):
-            objs[i].kind = o["kind"]
-            objs[i].var_kind = o["var_kind"]
-            objs[i].var_index = o["var_index"]
-            objs[i].node_first = o["node_first"]
-            objs[i].node_last = o["node_last"]
-            objs[i].weight = o["weight"]
-            if o.get("target") is not None:
-                t = np.ascontiguousarray(o["target"], dtype=np.float64)
-                self._keep.append(t)
-                objs[i].target = t.ctypes.data_as(_D)
-            objs[i].target_value = float(o.get("target_value", 0.0))
-        self._keep.append(objs)
+        objs = _objective_array(objectives, self._keep)
         pb.n_objectives = len(objectives)
         pb.objectives = objs
         pb.device = device
         h = C.c_void_p()
         rc = self.lib.cfx_create(C.byref(pb), C.byref(h))
+        self._attach(rc, h, batch, layout, n_shooting, n_steps, device)
+
+    def _attach(self, rc, h, batch, layout, n_shooting, n_steps, device):
         if rc != OK:
             raise CfxError(rc, self.lib.cfx_last_error(None).decode())
         self.h = h
@@ -342,3 +370,57 @@ class Handle:
 
     def synchronize(self):
         self._check(self.lib.cfx_synchronize(self.h))
+
+
+class MskHandle(Handle):
+    """A libcfx handle for a musculoskeletal problem (cfx_msk_create): FES muscles driving a serial chain of
+    revolute dofs.  Same evaluation interface as :class:`Handle`.
+
+    ``chain``: dict with ``axis`` (nq,), ``frame`` (nq, 12), ``gravity`` (3,), ``mass`` (nq,), ``com`` (nq, 3),
+    ``inertia`` (nq, 9); ``muscles``: list of dicts with ``model_id``, ``constants``, ``point_frame``,
+    ``point_pos`` (n, 3), ``optimal_length``, ``tendon_slack_length``, ``pennation_angle``."""
+
+    def __init__(self, *, chain, muscles, scheme, n_steps, n_shooting, truncation, final_time, stim_rows, batch,
+                 flags=0, layout=LAYOUT_SOA, objectives=(), device=0):
+        self.lib = load_library()
+        self._keep = []
+
+        def arr(a, dt=np.float64):
+            a = np.ascontiguousarray(a, dtype=dt).reshape(-1)
+            self._keep.append(a)
+            return a.ctypes.data_as(C.POINTER(C.c_int32 if dt == np.int32 else C.c_double))
+
+        pb = MskProblem()
+        pb.abi_version = ABI_VERSION
+        pb.scheme, pb.n_steps, pb.n_shooting, pb.truncation = scheme, n_steps, n_shooting, truncation
+        pb.layout, pb.batch, pb.final_time = layout, batch, final_time
+        pb.stim_rows = arr(stim_rows)
+        pb.n_dof = len(chain["axis"])
+        pb.dof_axis = arr(chain["axis"], np.int32)
+        pb.dof_frame = arr(chain["frame"])
+        for i in range(3):
+            pb.gravity[i] = float(chain["gravity"][i])
+        pb.body_mass, pb.body_com, pb.body_inertia = arr(chain["mass"]), arr(chain["com"]), arr(chain["inertia"])
+        mus = (MskMuscle * len(muscles))()
+        for i, m in enumerate(muscles):
+            mus[i].model = m["model_id"]
+            cst = Constants()
+            for name, _ in Constants._fields_:
+                setattr(cst, name, float(m["constants"].get(name, 0.0)))
+            mus[i].constants = cst
+            mus[i].n_points = len(m["point_frame"])
+            mus[i].point_frame = arr(m["point_frame"], np.int32)
+            mus[i].point_pos = arr(m["point_pos"])
+            mus[i].optimal_length = m["optimal_length"]
+            mus[i].tendon_slack_length = m["tendon_slack_length"]
+            mus[i].pennation_angle = m["pennation_angle"]
+        self._keep.append(mus)
+        pb.n_muscles = len(muscles)
+        pb.muscles = mus
+        pb.flags = flags
+        pb.objectives = _objective_array(objectives, self._keep)
+        pb.n_objectives = len(objectives)
+        pb.device = device
+        h = C.c_void_p()
+        rc = self.lib.cfx_msk_create(C.byref(pb), C.byref(h))
+        self._attach(rc, h, batch, layout, n_shooting, n_steps, device)

@@ -13,6 +13,7 @@
 #include "cfx_aux.h"
 #include "cfx_colloc.h"
 #include "cfx_launch.h"
+#include "cfx_msk_launch.h"
 
 using namespace cfx;
 
@@ -54,6 +55,12 @@ struct cfx_handle {
     int n_htasks = 1, hbs = 1;
     int n_obj = 0;
     std::vector<int32_t> jrow, jcol, hrow, hcol;
+    // musculoskeletal problems (cfx_msk_create)
+    bool msk = false;
+    int msk_nq = 0, msk_nm = 0, msk_fam = 0;
+    MskParams mp{};
+    MskGeom* d_geom = nullptr;
+    MskObjective* d_mobj = nullptr;
     DevBuf main[S_COUNT], stage[S_COUNT];
     std::string err;
 };
@@ -736,7 +743,8 @@ extern "C" void cfx_destroy(cfx_handle* h) {
         if (h->stage[s].p) (void)hipFree(h->stage[s].p);
     }
     for (void* p : {(void*)h->d_tab, (void*)h->d_rest, (void*)h->d_cna, (void*)h->d_htasks, (void*)h->d_obj,
-                    (void*)h->d_targets, (void*)h->d_sl_param, (void*)h->d_sl_joff, (void*)h->d_hdiag})
+                    (void*)h->d_targets, (void*)h->d_sl_param, (void*)h->d_sl_joff, (void*)h->d_hdiag,
+                    (void*)h->d_geom, (void*)h->d_mobj})
         if (p) (void)hipFree(p);
     if (h->own_stream) (void)hipStreamDestroy(h->own_stream);
     delete h;
@@ -788,9 +796,16 @@ static hipError_t launch_shooting(cfx_handle* h, bool derivs, const double* V, d
     return launch_shooting_ding(h->model, h->scheme, derivs, ni, h->kp, V, G, J, h->stream);
 }
 
+static int msk_eval_all(cfx_handle* h, const double* v, double* g, double* jac, double* f, double* grad,
+                        uint32_t flags);
+static int msk_eval_h(cfx_handle* h, const double* v, const double* obj_factor, const double* lambda, double* hess,
+                      uint32_t flags);
+static int msk_integrate(cfx_handle* h, const double* x0, const double* u, double* traj, uint32_t flags);
+
 extern "C" int cfx_eval_all(cfx_handle* h, const double* v, double* g, double* jac, double* f, double* grad,
                             uint32_t flags) {
     if (!h || !v) return CFX_EINVAL;
+    if (h->msk) return msk_eval_all(h, v, g, jac, f, grad, flags);
     CFX_HIP(h, hipSetDevice(h->device));
     int rc = CFX_OK;
     const int64_t B = h->prob.batch;
@@ -844,6 +859,7 @@ extern "C" int cfx_eval_grad_f(cfx_handle* h, const double* v, double* grad, uin
 extern "C" int cfx_eval_h(cfx_handle* h, const double* v, const double* obj_factor, const double* lambda,
                           double* hess, uint32_t flags) {
     if (!h || !v || !obj_factor || !lambda || !hess) return h ? fail(h, CFX_EINVAL, "cfx_eval_h: NULL argument") : CFX_EINVAL;
+    if (h->msk) return msk_eval_h(h, v, obj_factor, lambda, hess, flags);
     if (h->kp.tiled) return fail(h, CFX_EUNSUPPORTED, "cfx_eval_h: not available with CFX_LAYOUT_TILED64");
     CFX_HIP(h, hipSetDevice(h->device));
     int rc = CFX_OK;
@@ -872,6 +888,7 @@ extern "C" int cfx_eval_h(cfx_handle* h, const double* v, const double* obj_fact
 
 extern "C" int cfx_integrate(cfx_handle* h, const double* x0, const double* u, double* traj, uint32_t flags) {
     if (!h || !traj) return CFX_EINVAL;
+    if (h->msk) return msk_integrate(h, x0, u, traj, flags);
     if (h->colloc) return fail(h, CFX_EUNSUPPORTED, "cfx_integrate: not available for a collocation transcription");
     if (h->kp.tiled) return fail(h, CFX_EUNSUPPORTED, "cfx_integrate: not available with CFX_LAYOUT_TILED64");
     if (h->sz.nu > 0 && !u) return fail(h, CFX_EINVAL, "cfx_integrate: this model needs per-interval controls");
@@ -887,6 +904,315 @@ extern "C" int cfx_integrate(cfx_handle* h, const double* x0, const double* u, d
     hipError_t e = is_int(h->model) ? launch_ivp_hmed(h->model, h->scheme, h->tmax, h->kp, X0, U, TR, h->stream)
                                     : launch_ivp_ding(h->model, h->scheme, h->kp, X0, U, TR, h->stream);
     CFX_HIP(h, e);
+    if ((rc = finish_out(h, S_OUT, TR, traj, nsamp * h->sz.nx, flags)) != CFX_OK) return rc;
+    return sync_if_host(h, flags);
+}
+
+// ------------------------------------------------------------------------------------------------------
+// musculoskeletal problems (FesMskModel + OcpFesMsk; cfx_msk.h)
+// ------------------------------------------------------------------------------------------------------
+extern "C" int cfx_msk_create(const cfx_msk_problem* p, cfx_handle** out) {
+    if (!p || !out) return create_fail(nullptr, CFX_EINVAL, "cfx_msk_create: NULL argument");
+    *out = nullptr;
+    auto bad = [](const std::string& m) { return create_fail(nullptr, CFX_EINVAL, "cfx_msk_create: " + m); };
+    if (p->abi_version != CFX_ABI_VERSION) return bad("ABI version mismatch");
+    if (p->scheme != CFX_RK1 && p->scheme != CFX_RK2 && p->scheme != CFX_RK4)
+        return create_fail(nullptr, CFX_EUNSUPPORTED, "cfx_msk_create: scheme must be CFX_RK1, CFX_RK2 or CFX_RK4");
+    if (p->n_steps < 1 || p->n_shooting < 1 || p->batch < 1 || !(p->final_time > 0.0))
+        return bad("n_steps, n_shooting, batch and final_time must be positive");
+    if (p->truncation < 1 || p->truncation > 64) return bad("truncation must be in [1, 64]");
+    if (p->layout != CFX_LAYOUT_AOS && p->layout != CFX_LAYOUT_SOA)
+        return create_fail(nullptr, CFX_EUNSUPPORTED, "cfx_msk_create: layout must be CFX_LAYOUT_AOS or CFX_LAYOUT_SOA");
+    if (!p->stim_rows || !p->dof_axis || !p->dof_frame || !p->body_mass || !p->body_com || !p->body_inertia ||
+        !p->muscles)
+        return bad("NULL array");
+    const int nq = p->n_dof, nm = p->n_muscles;
+    if (nq < 1 || nq > CFX_MSK_MAX_DOF) return bad("n_dof must be in [1, 4]");
+    if (nm < 1 || nm > CFX_MSK_MAX_MUSCLES) return bad("n_muscles must be in [1, 8]");
+    const int fam = p->muscles[0].model;
+    if (fam < CFX_DING2003 || fam > CFX_DING2007_FATIGUE)
+        return create_fail(nullptr, CFX_EUNSUPPORTED, "cfx_msk_create: muscle models must be Ding2003 / Ding2007 families");
+    for (int m = 0; m < nm; ++m) {
+        const cfx_msk_muscle& mu = p->muscles[m];
+        if (mu.model != fam) return bad("every muscle must use the same model family");
+        if (mu.n_points < 2 || mu.n_points > CFX_MSK_MAX_POINTS || !mu.point_frame || !mu.point_pos)
+            return bad("muscle " + std::to_string(m) + ": 2..16 path points with frames and positions");
+        for (int i = 0; i < mu.n_points; ++i)
+            if (mu.point_frame[i] < -1 || mu.point_frame[i] >= nq) return bad("muscle point frame out of range");
+        if (!(mu.optimal_length > 0.0) || !(std::cos(mu.pennation_angle) > 0.0))
+            return bad("muscle optimal length must be positive and |pennation| < pi/2");
+    }
+    for (int j = 0; j < nq; ++j)
+        if (p->dof_axis[j] < 0 || p->dof_axis[j] > 2) return bad("dof_axis must be 0, 1 or 2");
+    if (!msk_supported(nq, nm, fam, p->scheme))
+        return create_fail(nullptr, CFX_EUNSUPPORTED,
+                           "cfx_msk_create: shape (n_dof " + std::to_string(nq) + ", muscles " + std::to_string(nm) +
+                               ", model " + std::to_string(fam) + ", scheme " + std::to_string(p->scheme) +
+                               ") is not compiled into this libcfx (cfx_inst_msk_*.hip)");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1)
+        return create_fail(nullptr, CFX_ENODEV, "cfx_msk_create: no HIP device available (libcfx has no CPU path)");
+    if (p->device < 0 || p->device >= ndev) return create_fail(nullptr, CFX_ENODEV, "cfx_msk_create: bad device ordinal");
+
+    const bool fat = fam & 1, pw = fam == CFX_DING2007 || fam == CFX_DING2007_FATIGUE;
+    const bool residual = p->flags & CFX_MSK_RESIDUAL_TORQUE;
+    const int N = p->n_shooting, T = p->truncation, m = p->n_steps, S = stages_of(p->scheme);
+    const int nxm = fat ? 5 : 2, nx = nm * nxm + 2 * nq, npw = pw ? nm : 0, nu = npw + (residual ? nq : 0);
+    const int nz = nx + nu;
+    if (nz > 64) return bad("more than 64 decision variables per interval");
+
+    cfx_handle* h = new cfx_handle();
+    h->msk = true;
+    h->msk_nq = nq, h->msk_nm = nm, h->msk_fam = fam;
+    h->prob.abi_version = p->abi_version;
+    h->prob.scheme = p->scheme, h->prob.n_steps = m, h->prob.n_shooting = N, h->prob.truncation = T;
+    h->prob.layout = p->layout, h->prob.batch = p->batch, h->prob.final_time = p->final_time;
+    h->prob.device = p->device;
+    h->scheme = p->scheme, h->stages = S, h->device = p->device;
+
+    // ---- constants
+    MskGeom G;
+    std::memset(&G, 0, sizeof(G));
+    for (int j = 0; j < nq; ++j) {
+        G.axis[j] = p->dof_axis[j];
+        for (int e = 0; e < 9; ++e) G.A[j][e] = p->dof_frame[j * 12 + e];
+        for (int e = 0; e < 3; ++e) G.t[j][e] = p->dof_frame[j * 12 + 9 + e];
+        G.mass[j] = p->body_mass[j];
+        for (int e = 0; e < 3; ++e) G.com[j][e] = p->body_com[j * 3 + e];
+        for (int e = 0; e < 9; ++e) G.inertia[j][e] = p->body_inertia[j * 9 + e];
+    }
+    for (int e = 0; e < 3; ++e) G.grav[e] = p->gravity[e];
+    std::vector<double> rest(nx, 0.0);
+    for (int mi = 0; mi < nm; ++mi) {
+        const cfx_msk_muscle& mu = p->muscles[mi];
+        const cfx_constants& c = mu.constants;
+        G.npts[mi] = mu.n_points;
+        for (int i = 0; i < mu.n_points; ++i) {
+            G.pt_frame[mi][i] = mu.point_frame[i];
+            for (int e = 0; e < 3; ++e) G.pt_pos[mi][i][e] = mu.point_pos[i * 3 + e];
+        }
+        MskMuscleConst& C = G.mc[mi];
+        C.inv_tauc = 1.0 / c.tauc, C.tau2 = c.tau2, C.km_rest = c.km_rest, C.tau1_rest = c.tau1_rest;
+        C.a_force = pw ? c.a_scale : c.a_rest;
+        C.pd0 = c.pd0, C.inv_pdt = pw ? 1.0 / c.pdt : 0.0;
+        C.alpha_a = c.alpha_a, C.alpha_tau1 = c.alpha_tau1, C.alpha_km = c.alpha_km;
+        C.inv_tau_fat = fat ? 1.0 / c.tau_fat : 0.0;
+        C.a_fat_rest = pw ? c.a_scale : c.a_rest;  // ding2007_with_fatigue.py:198-241: A relaxes to a_scale
+        C.inv_lopt = 1.0 / mu.optimal_length, C.slack = mu.tendon_slack_length;
+        C.inv_cos_penn = 1.0 / std::cos(mu.pennation_angle);
+        if (fat) {
+            rest[mi * nxm + 2] = C.a_fat_rest;
+            rest[mi * nxm + 3] = c.tau1_rest;
+            rest[mi * nxm + 4] = c.km_rest;
+        }
+    }
+    G.fl_on = (p->flags & CFX_MSK_FORCE_LENGTH) ? 1 : 0;
+    G.fv_on = (p->flags & CFX_MSK_FORCE_VELOCITY) ? 1 : 0;
+    G.fp_on = (p->flags & CFX_MSK_PASSIVE_FORCE) ? 1 : 0;
+
+    // ---- calcium sums at every RK stage time, per muscle (ding2003.py:230-252, reference operation order)
+    const double dt = p->final_time / N, hh = dt / m;
+    const int Q = m * S;
+    std::vector<double> cs((size_t)N * Q * nm);
+    for (int k = 0; k < N; ++k) {
+        const double* row = p->stim_rows + (size_t)k * T;
+        for (int mi = 0; mi < nm; ++mi) {
+            const cfx_constants& c = p->muscles[mi].constants;
+            const double r0 = c.km_rest + c.r0_km_relationship;
+            std::vector<double> ri(T);
+            for (int i = 0; i < T; ++i)
+                ri[i] = i == 0 ? 1.0 : 1.0 + (r0 - 1.0) * std::exp(-(row[i] - row[i - 1]) / c.tauc);
+            for (int j = 0; j < m; ++j)
+                for (int st = 0; st < S; ++st) {
+                    double t = k * dt + j * hh;
+                    if (S == 2 && st == 1) t += hh / 2;
+                    if (S == 4 && (st == 1 || st == 2)) t += hh / 2;
+                    if (S == 4 && st == 3) t += hh;
+                    double sum = 0.0;
+                    for (int i = 0; i < T; ++i) sum = sum + ri[i] * std::exp(-(t - row[i]) / c.tauc);
+                    cs[((size_t)k * Q + (size_t)j * S + st) * nm + mi] = sum;
+                }
+        }
+    }
+    MskParams& P = h->mp;
+    P.B = p->batch, P.N = N, P.m = m, P.nx = nx, P.nu = nu, P.nz = nz, P.Q = Q;
+    P.residual = residual ? 1 : 0, P.npw = npw, P.dt = dt, P.h = hh;
+
+    // ---- structural Jacobian pattern (Dep pass on the host through the same RHS code)
+    std::vector<uint64_t> dep(nx);
+    {
+        MskParams Ph = P;
+        Ph.cs = cs.data();
+        msk_dep_pattern(nq, nm, fam, p->scheme, Ph, G, dep.data());
+    }
+    for (int e = 0; e < kMskMaxX * kMskMaxZ; ++e) G.jpos[e] = -1;
+    int16_t pos = 0;
+    for (int r = 0; r < nx; ++r) {
+        for (int c = 0; c < nz; ++c)
+            if (dep[r] >> c & 1ull) G.jpos[r * kMskMaxZ + c] = pos++;
+        G.jneg[r] = pos++;
+    }
+    const int nnzk = pos;
+    P.nnzk = nnzk;
+    for (int k = 0; k < N; ++k)
+        for (int r = 0; r < nx; ++r) {
+            for (int c = 0; c < nz; ++c)
+                if (dep[r] >> c & 1ull) {
+                    h->jrow.push_back(k * nx + r);
+                    h->jcol.push_back(k * nz + c);
+                }
+            h->jrow.push_back(k * nx + r);
+            h->jcol.push_back((k + 1) * nz + r);
+        }
+    // ---- Hessian: dense lower triangle of every interval block, then the diagonal of x_N
+    const int nhk = nz * (nz + 1) / 2;
+    P.nhk = nhk;
+    for (int k = 0; k < N; ++k)
+        for (int i = 0; i < nz; ++i)
+            for (int j = 0; j <= i; ++j) {
+                h->hrow.push_back(k * nz + i);
+                h->hcol.push_back(k * nz + j);
+            }
+    for (int r = 0; r < nx; ++r) {
+        h->hrow.push_back(N * nz + r);
+        h->hcol.push_back(N * nz + r);
+    }
+    std::vector<int32_t> hdiag((size_t)(N + 1) * nz, -1);
+    for (int k = 0; k < N; ++k)
+        for (int e = 0; e < nz; ++e) hdiag[(size_t)k * nz + e] = k * nhk + e * (e + 1) / 2 + e;
+    for (int r = 0; r < nx; ++r) hdiag[(size_t)N * nz + r] = N * nhk + r;
+    std::vector<int16_t> tasks;
+    for (int I = 0; I < nz; ++I)
+        for (int J = I; J < nz; ++J) {
+            tasks.push_back((int16_t)I);
+            tasks.push_back((int16_t)J);
+        }
+    h->n_htasks = nz * (nz + 1) / 2;
+
+    // ---- objective terms
+    std::vector<MskObjective> mobj;
+    std::vector<double> targets;
+    for (int t = 0; t < p->n_objectives; ++t) {
+        const cfx_objective& o = p->objectives[t];
+        const bool st = o.var_kind == CFX_VAR_STATE;
+        const int lim = st ? N : N - 1;
+        if ((o.var_kind != CFX_VAR_STATE && o.var_kind != CFX_VAR_CONTROL) || o.var_index < 0 ||
+            o.var_index >= (st ? nx : nu) || o.node_first < 0 || o.node_last > lim || o.node_first > o.node_last ||
+            (o.kind != CFX_OBJ_LAGRANGE && o.kind != CFX_OBJ_MAYER && o.kind != CFX_OBJ_MAYER_INV) ||
+            (o.kind == CFX_OBJ_MAYER_INV && !st))
+            return create_fail(h, CFX_EINVAL, "cfx_msk_create: invalid objective term " + std::to_string(t));
+        MskObjective d{};
+        d.kind = o.kind;
+        d.var_kind = st ? 0 : 1;
+        d.var_index = o.var_index;
+        d.node_first = o.node_first;
+        d.node_last = o.node_last;
+        d.w_eff = o.weight * (o.kind == CFX_OBJ_LAGRANGE ? dt : 1.0);
+        d.target_value = o.target_value;
+        d.target_off = -1;
+        if (o.target && o.kind != CFX_OBJ_MAYER_INV) {
+            d.target_off = (int32_t)targets.size();
+            targets.insert(targets.end(), o.target, o.target + N + 1);
+        }
+        mobj.push_back(d);
+    }
+    h->n_obj = (int)mobj.size();
+    h->sz.nv = (int64_t)N * nz + nx;
+    h->sz.ng = (int64_t)N * nx;
+    h->sz.nnz_jac = (int64_t)h->jrow.size();
+    h->sz.nnz_hess = (int64_t)h->hrow.size();
+    h->sz.nx = nx;
+    h->sz.nu = nu;
+
+    if (hipSetDevice(h->device) != hipSuccess) return create_fail(h, CFX_EHIP, "cfx_msk_create: hipSetDevice failed");
+    if (hipStreamCreateWithFlags(&h->own_stream, hipStreamNonBlocking) != hipSuccess)
+        return create_fail(h, CFX_EHIP, "cfx_msk_create: hipStreamCreate failed");
+    h->stream = h->own_stream;
+    auto upload = [&](void** dst, const void* src, size_t bytes) -> bool {
+        if (bytes == 0) return true;
+        if (hipMalloc(dst, bytes) != hipSuccess) return false;
+        return hipMemcpy(*dst, src, bytes, hipMemcpyHostToDevice) == hipSuccess;
+    };
+    if (!upload((void**)&h->d_geom, &G, sizeof(G)) ||
+        !upload((void**)&h->d_tab, cs.data(), cs.size() * sizeof(double)) ||
+        !upload((void**)&h->d_rest, rest.data(), rest.size() * sizeof(double)) ||
+        !upload((void**)&h->d_mobj, mobj.data(), mobj.size() * sizeof(MskObjective)) ||
+        !upload((void**)&h->d_targets, targets.data(), targets.size() * sizeof(double)) ||
+        !upload((void**)&h->d_htasks, tasks.data(), tasks.size() * sizeof(int16_t)) ||
+        !upload((void**)&h->d_hdiag, hdiag.data(), hdiag.size() * sizeof(int32_t)))
+        return create_fail(h, CFX_ENOMEM, "cfx_msk_create: device allocation/upload failed");
+    P.cs = h->d_tab;
+    P.rest = h->d_rest;
+    *out = h;
+    return CFX_OK;
+}
+
+static int msk_eval_all(cfx_handle* h, const double* v, double* g, double* jac, double* f, double* grad,
+                        uint32_t flags) {
+    CFX_HIP(h, hipSetDevice(h->device));
+    int rc = CFX_OK;
+    const int64_t B = h->prob.batch;
+    const double* V = stage_in(h, S_V, v, h->sz.nv, flags, &rc);
+    if (!V) return rc;
+    double* G = g ? stage_out(h, S_G, g, h->sz.ng, flags, &rc) : nullptr;
+    double* J = jac ? stage_out(h, S_J, jac, h->sz.nnz_jac, flags, &rc) : nullptr;
+    double* F = f ? stage_out(h, S_F, f, 1, flags, &rc) : nullptr;
+    double* GR = grad ? stage_out(h, S_GRAD, grad, h->sz.nv, flags, &rc) : nullptr;
+    if (rc != CFX_OK) return rc;
+    if (G || J)
+        CFX_HIP(h, launch_msk_shooting(h->msk_nq, h->msk_nm, h->msk_fam, h->scheme, h->mp, h->d_geom, V, G, J,
+                                       h->stream));
+    if (F || GR) {
+        if (GR) CFX_HIP(h, hipMemsetAsync(GR, 0, (size_t)B * h->sz.nv * sizeof(double), h->stream));
+        hipLaunchKernelGGL(k_msk_objective, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, h->stream, h->mp,
+                           h->n_obj, h->d_mobj, h->d_targets, V, F, GR, (const double*)nullptr, (double*)nullptr,
+                           (const int32_t*)nullptr);
+    }
+    CFX_HIP(h, hipGetLastError());
+    if (G && (rc = finish_out(h, S_G, G, g, h->sz.ng, flags)) != CFX_OK) return rc;
+    if (J && (rc = finish_out(h, S_J, J, jac, h->sz.nnz_jac, flags)) != CFX_OK) return rc;
+    if (F && (rc = finish_out(h, S_F, F, f, 1, flags)) != CFX_OK) return rc;
+    if (GR && (rc = finish_out(h, S_GRAD, GR, grad, h->sz.nv, flags)) != CFX_OK) return rc;
+    return sync_if_host(h, flags);
+}
+
+static int msk_eval_h(cfx_handle* h, const double* v, const double* obj_factor, const double* lambda, double* hess,
+                      uint32_t flags) {
+    CFX_HIP(h, hipSetDevice(h->device));
+    int rc = CFX_OK;
+    const int64_t B = h->prob.batch;
+    const double* V = stage_in(h, S_V, v, h->sz.nv, flags, &rc);
+    if (!V) return rc;
+    const double* OF = stage_in(h, S_A1, obj_factor, 1, flags, &rc);
+    if (!OF) return rc;
+    const double* LAM = stage_in(h, S_A2, lambda, h->sz.ng, flags, &rc);
+    if (!LAM) return rc;
+    double* H = stage_out(h, S_OUT, hess, h->sz.nnz_hess, flags, &rc);
+    if (!H) return rc;
+    CFX_HIP(h, hipMemsetAsync(H, 0, (size_t)B * h->sz.nnz_hess * sizeof(double), h->stream));
+    CFX_HIP(h, launch_msk_hessian(h->msk_nq, h->msk_nm, h->msk_fam, h->scheme, h->mp, h->d_geom,
+                                  (const int16_t*)h->d_htasks, h->n_htasks, V, LAM, H, h->stream));
+    if (h->n_obj)
+        hipLaunchKernelGGL(k_msk_objective, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, h->stream, h->mp,
+                           h->n_obj, h->d_mobj, h->d_targets, V, (double*)nullptr, (double*)nullptr, OF, H,
+                           (const int32_t*)h->d_hdiag);
+    CFX_HIP(h, hipGetLastError());
+    if ((rc = finish_out(h, S_OUT, H, hess, h->sz.nnz_hess, flags)) != CFX_OK) return rc;
+    return sync_if_host(h, flags);
+}
+
+static int msk_integrate(cfx_handle* h, const double* x0, const double* u, double* traj, uint32_t flags) {
+    if (h->sz.nu > 0 && !u) return fail(h, CFX_EINVAL, "cfx_integrate: this model needs per-interval controls");
+    CFX_HIP(h, hipSetDevice(h->device));
+    int rc = CFX_OK;
+    const int64_t nsamp = (int64_t)h->mp.N * h->mp.m + 1;
+    const double* X0 = x0 ? stage_in(h, S_A1, x0, h->sz.nx, flags, &rc) : nullptr;
+    if (x0 && !X0) return rc;
+    const double* U = h->sz.nu ? stage_in(h, S_A2, u, (int64_t)h->mp.N * h->sz.nu, flags, &rc) : nullptr;
+    if (h->sz.nu && !U) return rc;
+    double* TR = stage_out(h, S_OUT, traj, nsamp * h->sz.nx, flags, &rc);
+    if (!TR) return rc;
+    CFX_HIP(h, launch_msk_ivp(h->msk_nq, h->msk_nm, h->msk_fam, h->scheme, h->mp, h->d_geom, X0, U, TR, h->stream));
     if ((rc = finish_out(h, S_OUT, TR, traj, nsamp * h->sz.nx, flags)) != CFX_OK) return rc;
     return sync_if_host(h, flags);
 }

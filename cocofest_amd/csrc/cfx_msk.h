@@ -1,0 +1,748 @@
+// cfx_msk.h — gfx950 kernels of the musculoskeletal FES path (FesMskModel, cocofest/models/dynamical_model.py).
+//
+// One right-hand side couples NM FES muscles (the Ding calcium/force[/fatigue] ODEs) to a serial chain of NQ
+// revolute dofs (biorbd model reduced on the host, see cfx_api.hip:msk_reduce):
+//   frames    R_j = R_{j-1} A_j Rot_axis(q_j), o_j = o_{j-1} + R_{j-1} t_j            (constant [A_j | t_j])
+//   muscles   points fixed in a frame; muscle-tendon length L = sum |P_{i+1} - P_i|, length Jacobian
+//             J_L[k] = sum u_i . (z_k x (P_{i+1} - o_k) - z_k x (P_i - o_k)) over the dofs above each point;
+//             fibre length (L - slack) / cos(pennation); velocity J_L qdot; De Groote FL / FV / FP
+//             (cocofest/models/hill_coefficients.py:11-126) scale dF/dt (ding2003.py:274-311)
+//   torque    tau = -J_L^T F (+ residual torque)                         (dynamical_model.py:206-334)
+//   dynamics  qddot = M(q)^-1 (tau - h(q, qdot)); M from body Jacobians, h by recursive Newton-Euler with
+//             qddot = 0 (gravity as a base acceleration), one composite rigid body per dof frame.
+// Everything is written once over a generic scalar S: double (values), Dual<D> (Jacobian directions), Jet<D>
+// (Lagrangian Hessian blocks) and Dep (structural dependency bitmasks, run on the host to get CasADi-style
+// sparsity).  Constants come from an MskGeom block in device memory; every index into it is wave-uniform, so
+// the reads are scalar loads.  No MFMA: a 2-dof arm has no dense contraction worth a matrix core.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "cfx_dual.h"
+
+namespace cfx {
+
+#define MSK_HD __host__ __device__ __forceinline__
+
+constexpr int kMskMaxQ = 4;      // dofs of the serial chain
+constexpr int kMskMaxMus = 8;    // muscles
+constexpr int kMskMaxPts = 16;   // path points per muscle (origin, via points, insertion)
+constexpr int kMskMaxX = kMskMaxMus * 5 + 2 * kMskMaxQ;
+constexpr int kMskMaxZ = kMskMaxX + kMskMaxMus + kMskMaxQ;
+
+// ---- structural dependency bitmask (host sparsity pass) ------------------------------------------------------
+struct Dep {
+    uint64_t m;
+};
+MSK_HD Dep operator+(Dep a, Dep b) { return Dep{a.m | b.m}; }
+MSK_HD Dep operator-(Dep a, Dep b) { return Dep{a.m | b.m}; }
+MSK_HD Dep operator*(Dep a, Dep b) { return Dep{a.m | b.m}; }
+MSK_HD Dep operator/(Dep a, Dep b) { return Dep{a.m | b.m}; }
+MSK_HD Dep operator+(Dep a, double) { return a; }
+MSK_HD Dep operator+(double, Dep a) { return a; }
+MSK_HD Dep operator-(Dep a, double) { return a; }
+MSK_HD Dep operator-(double, Dep a) { return a; }
+MSK_HD Dep operator*(Dep a, double) { return a; }
+MSK_HD Dep operator*(double, Dep a) { return a; }
+MSK_HD Dep operator/(Dep a, double) { return a; }
+MSK_HD Dep operator/(double, Dep a) { return a; }
+MSK_HD Dep operator-(Dep a) { return a; }
+MSK_HD double value(Dep) { return 1.0; }
+
+template <int D>
+CFX_HD Dual<D> operator-(const Dual<D>& a) {
+    return 0.0 - a;
+}
+template <int D>
+CFX_HD Jet<D> operator-(const Jet<D>& a) {
+    return 0.0 - a;
+}
+
+// constants of each scalar type
+template <class S>
+struct Num;
+template <>
+struct Num<double> {
+    static MSK_HD double c(double v) { return v; }
+};
+template <>
+struct Num<Dep> {
+    static MSK_HD Dep c(double) { return Dep{0}; }
+};
+template <int D>
+struct Num<Dual<D>> {
+    static CFX_HD Dual<D> c(double v) { return dconst<D>(v); }
+};
+template <int D>
+struct Num<Jet<D>> {
+    static CFX_HD Jet<D> c(double v) { return jconst<D>(v); }
+};
+
+// ---- elementary functions (value, first and second derivative through the generic chain rule) -----------
+MSK_HD double mexp(double x) { return exp(x); }
+MSK_HD double mlog(double x) { return log(x); }
+MSK_HD double msqrt(double x) { return sqrt(x); }
+MSK_HD double msin(double x) { return sin(x); }
+MSK_HD double mcos(double x) { return cos(x); }
+MSK_HD Dep mexp(Dep a) { return a; }
+MSK_HD Dep mlog(Dep a) { return a; }
+MSK_HD Dep msqrt(Dep a) { return a; }
+MSK_HD Dep msin(Dep a) { return a; }
+MSK_HD Dep mcos(Dep a) { return a; }
+
+template <int D>
+CFX_HD Dual<D> dchain(const Dual<D>& a, double f0, double f1) {
+    Dual<D> r;
+    r.v = f0;
+#pragma unroll
+    for (int i = 0; i < D; ++i) r.d[i] = f1 * a.d[i];
+    return r;
+}
+template <int D>
+CFX_HD Dual<D> mexp(const Dual<D>& a) {
+    const double e = exp(a.v);
+    return dchain(a, e, e);
+}
+template <int D>
+CFX_HD Dual<D> mlog(const Dual<D>& a) {
+    return dchain(a, log(a.v), 1.0 / a.v);
+}
+template <int D>
+CFX_HD Dual<D> msqrt(const Dual<D>& a) {
+    const double s = sqrt(a.v);
+    return dchain(a, s, 0.5 / s);
+}
+template <int D>
+CFX_HD Dual<D> msin(const Dual<D>& a) {
+    return dchain(a, sin(a.v), cos(a.v));
+}
+template <int D>
+CFX_HD Dual<D> mcos(const Dual<D>& a) {
+    return dchain(a, cos(a.v), -sin(a.v));
+}
+template <int D>
+CFX_HD Jet<D> mexp(const Jet<D>& a) {
+    const double e = exp(a.v);
+    return jchain(a, e, e, e);
+}
+template <int D>
+CFX_HD Jet<D> mlog(const Jet<D>& a) {
+    const double i = 1.0 / a.v;
+    return jchain(a, log(a.v), i, -i * i);
+}
+template <int D>
+CFX_HD Jet<D> msqrt(const Jet<D>& a) {
+    const double s = sqrt(a.v);
+    return jchain(a, s, 0.5 / s, -0.25 / (s * a.v));
+}
+template <int D>
+CFX_HD Jet<D> msin(const Jet<D>& a) {
+    const double s = sin(a.v), c = cos(a.v);
+    return jchain(a, s, c, -s);
+}
+template <int D>
+CFX_HD Jet<D> mcos(const Jet<D>& a) {
+    const double s = sin(a.v), c = cos(a.v);
+    return jchain(a, c, -s, -c);
+}
+
+// ---- problem constants ----------------------------------------------------------------------------------------
+struct MskMuscleConst {
+    double inv_tauc, tau2, km_rest, tau1_rest, a_force;  // a_force: A_rest (Ding2003) or a_scale (Ding2007)
+    double pd0, inv_pdt;
+    double alpha_a, alpha_tau1, alpha_km, inv_tau_fat, a_fat_rest;
+    double inv_lopt, slack, inv_cos_penn;
+};
+
+struct MskGeom {
+    int32_t axis[kMskMaxQ];        // 0 / 1 / 2: rotation about the frame's x / y / z
+    double A[kMskMaxQ][9];         // constant rotation from frame j-1 (ground for j = 0) to dof j's joint frame
+    double t[kMskMaxQ][3];         // its translation, in frame j-1
+    double grav[3];
+    double mass[kMskMaxQ];         // composite body moving with frame j (mass, com and inertia about the com, in frame j)
+    double com[kMskMaxQ][3];
+    double inertia[kMskMaxQ][9];
+    int32_t npts[kMskMaxMus];
+    int32_t pt_frame[kMskMaxMus][kMskMaxPts];  // -1: ground
+    double pt_pos[kMskMaxMus][kMskMaxPts][3];
+    MskMuscleConst mc[kMskMaxMus];
+    int32_t fl_on, fv_on, fp_on;
+    int16_t jpos[kMskMaxX * kMskMaxZ];  // J_g value offset of dPhi_r/dz_c inside an interval block (-1: zero)
+    int16_t jneg[kMskMaxX];            // offset of the -1 on x_{k+1}[r]
+};
+
+struct MskParams {
+    int64_t B;
+    int32_t N, m, nx, nu, nz, Q, nnzk, nhk, residual, npw;
+    double dt, h;
+    const double* cs;    // calcium sums [N][Q][NM] at every RK stage time (host, reference operation order)
+    const double* rest;  // rest state [nx] (IVP default x0)
+};
+
+template <int FAM>
+constexpr int msk_nxm() {
+    return (FAM & 1) ? 5 : 2;
+}
+template <int FAM>
+constexpr bool msk_pw() {
+    return FAM == 2 || FAM == 3;
+}
+
+// ---- small vector helpers ---------------------------------------------------------------------------------------
+template <class S>
+MSK_HD void cross3(const S* a, const S* b, S* r) {
+    r[0] = a[1] * b[2] - a[2] * b[1];
+    r[1] = a[2] * b[0] - a[0] * b[2];
+    r[2] = a[0] * b[1] - a[1] * b[0];
+}
+template <class S>
+MSK_HD S dot3(const S* a, const S* b) {
+    return a[0] * b[0] + a[1] * b[1] + a[2] * b[2];
+}
+
+// Frames of the chain: R[j] (row-major 3x3), o[j], joint axis z[j] (world).
+template <int NQ, class S>
+MSK_HD void msk_frames(const MskGeom& G, const S* q, S (*R)[9], S (*o)[3], S (*z)[3]) {
+#pragma unroll
+    for (int j = 0; j < NQ; ++j) {
+        S Rb[9];
+        if (j == 0) {
+#pragma unroll
+            for (int e = 0; e < 9; ++e) Rb[e] = Num<S>::c(G.A[0][e]);
+#pragma unroll
+            for (int e = 0; e < 3; ++e) o[0][e] = Num<S>::c(G.t[0][e]);
+        } else {
+#pragma unroll
+            for (int r = 0; r < 3; ++r) {
+#pragma unroll
+                for (int c = 0; c < 3; ++c)
+                    Rb[r * 3 + c] = R[j - 1][r * 3] * G.A[j][c] + R[j - 1][r * 3 + 1] * G.A[j][3 + c] +
+                                    R[j - 1][r * 3 + 2] * G.A[j][6 + c];
+                o[j][r] = o[j - 1][r] + R[j - 1][r * 3] * G.t[j][0] + R[j - 1][r * 3 + 1] * G.t[j][1] +
+                          R[j - 1][r * 3 + 2] * G.t[j][2];
+            }
+        }
+        const S c = mcos(q[j]), s = msin(q[j]);
+        // R_j = Rb Rot(q): columns (a, b) of the rotation plane mix, the axis column is kept
+        const int ax = G.axis[j];
+#pragma unroll
+        for (int r = 0; r < 3; ++r) {
+            // uniform branches keep every register index compile-time
+            S ca, cb, cz;
+            if (ax == 2) {
+                ca = Rb[r * 3 + 0], cb = Rb[r * 3 + 1], cz = Rb[r * 3 + 2];
+            } else if (ax == 0) {
+                ca = Rb[r * 3 + 1], cb = Rb[r * 3 + 2], cz = Rb[r * 3 + 0];
+            } else {
+                ca = Rb[r * 3 + 2], cb = Rb[r * 3 + 0], cz = Rb[r * 3 + 1];
+            }
+            const S na = ca * c + cb * s, nb = cb * c - ca * s;
+            z[j][r] = cz;
+            if (ax == 2) {
+                R[j][r * 3 + 0] = na, R[j][r * 3 + 1] = nb, R[j][r * 3 + 2] = cz;
+            } else if (ax == 0) {
+                R[j][r * 3 + 1] = na, R[j][r * 3 + 2] = nb, R[j][r * 3 + 0] = cz;
+            } else {
+                R[j][r * 3 + 2] = na, R[j][r * 3 + 0] = nb, R[j][r * 3 + 1] = cz;
+            }
+        }
+    }
+}
+
+// World position of a point fixed in frame f (-1: ground) and its Jacobian columns z_k x (P - o_k), k <= f.
+template <int NQ, class S>
+MSK_HD void msk_point(const S (*R)[9], const S (*o)[3], const S (*z)[3], int f, const double* p, S* P, S (*dP)[3]) {
+#pragma unroll
+    for (int e = 0; e < 3; ++e) P[e] = Num<S>::c(p[e]);
+#pragma unroll
+    for (int k = 0; k < NQ; ++k)
+#pragma unroll
+        for (int e = 0; e < 3; ++e) dP[k][e] = Num<S>::c(0.0);
+#pragma unroll
+    for (int j = 0; j < NQ; ++j) {
+        if (f == j) {
+#pragma unroll
+            for (int e = 0; e < 3; ++e) P[e] = o[j][e] + R[j][e * 3] * p[0] + R[j][e * 3 + 1] * p[1] + R[j][e * 3 + 2] * p[2];
+#pragma unroll
+            for (int k = 0; k <= j; ++k) {
+                S r[3] = {P[0] - o[k][0], P[1] - o[k][1], P[2] - o[k][2]};
+                cross3(z[k], r, dP[k]);
+            }
+        }
+    }
+}
+
+// De Groote force-length (hill_coefficients.py:11-63), force-velocity (66-96), passive force (99-126).
+template <class S>
+MSK_HD S hill_fl(const S& nl) {
+    const double b1[3] = {0.815, 0.433, 0.100}, b2[3] = {1.055, 0.717, 1.000}, b3[3] = {0.162, -0.030, 0.354},
+                 b4[3] = {0.063, 0.200, 0.0};
+    S r = Num<S>::c(0.0);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const S d = nl - b2[i];
+        const S w = b3[i] + b4[i] * nl;
+        r = r + b1[i] * mexp((-0.5 * (d * d)) / (w * w));
+    }
+    return r;
+}
+template <class S>
+MSK_HD S hill_fv(const S& vel) {
+    const S w = (-8.149 * (vel / 10.0)) + (-0.374);
+    return -0.318 * mlog(w + msqrt(w * w + 1.0)) + 0.886;
+}
+template <class S>
+MSK_HD S hill_fp(const S& nl) {
+    const S fp = (mexp(4.0 * (nl - 1.0) / 0.6) - 1.0) / (exp(4.0) - 1.0);
+    return value(fp) > 0.0 ? fp : Num<S>::c(0.0);
+}
+
+// FesMskModel.muscle_dynamic for one state: f = dx/dt.  cs[m]: calcium sum of muscle m at this stage time.
+template <int NQ, int NM, int FAM, class S>
+MSK_HD void msk_rhs(const MskGeom& G, int residual, const double* cs, const S* x, const S* u, S* f) {
+    constexpr int NXM = msk_nxm<FAM>();
+    constexpr bool FAT = (FAM & 1) != 0, PW = msk_pw<FAM>();
+    constexpr int XQ = NM * NXM, XQD = XQ + NQ;
+    constexpr int NPW = PW ? NM : 0;
+    S R[NQ][9], o[NQ][3], z[NQ][3];
+    msk_frames<NQ>(G, x + XQ, R, o, z);
+    S tau[NQ];
+#pragma unroll
+    for (int k = 0; k < NQ; ++k) tau[k] = residual ? u[NPW + k] : Num<S>::c(0.0);
+#pragma unroll
+    for (int mu = 0; mu < NM; ++mu) {
+        const MskMuscleConst& C = G.mc[mu];
+        // ---- geometry: muscle-tendon length and its Jacobian
+        S L = Num<S>::c(0.0), JL[NQ];
+#pragma unroll
+        for (int k = 0; k < NQ; ++k) JL[k] = Num<S>::c(0.0);
+        S P0[3], dP0[NQ][3];
+        msk_point<NQ>(R, o, z, G.pt_frame[mu][0], G.pt_pos[mu][0], P0, dP0);
+        const int np = G.npts[mu];
+        for (int i = 1; i < np; ++i) {
+            S P1[3], dP1[NQ][3];
+            msk_point<NQ>(R, o, z, G.pt_frame[mu][i], G.pt_pos[mu][i], P1, dP1);
+            const S d[3] = {P1[0] - P0[0], P1[1] - P0[1], P1[2] - P0[2]};
+            const S n = msqrt(dot3(d, d));
+            const S inv = 1.0 / n;
+            L = L + n;
+#pragma unroll
+            for (int k = 0; k < NQ; ++k) {
+                const S dd[3] = {dP1[k][0] - dP0[k][0], dP1[k][1] - dP0[k][1], dP1[k][2] - dP0[k][2]};
+                JL[k] = JL[k] + dot3(d, dd) * inv;
+            }
+#pragma unroll
+            for (int e = 0; e < 3; ++e) {
+                P0[e] = P1[e];
+#pragma unroll
+                for (int k = 0; k < NQ; ++k) dP0[k][e] = dP1[k][e];
+            }
+        }
+        // ---- Hill coefficients
+        const S nl = ((L - C.slack) * C.inv_cos_penn) * C.inv_lopt;
+        S vel = Num<S>::c(0.0);
+#pragma unroll
+        for (int k = 0; k < NQ; ++k) vel = vel + JL[k] * x[XQD + k];
+        const S fl = G.fl_on ? hill_fl(nl) : Num<S>::c(1.0);
+        const S fv = G.fv_on ? hill_fv(vel) : Num<S>::c(1.0);
+        const S mult = G.fp_on ? fl * fv + hill_fp(nl) : fl * fv;
+        // ---- FES muscle ODE (ding2003.py:254-311, ding2003_with_fatigue.py:197-240, ding2007.py:172-188)
+        const S& cn = x[mu * NXM];
+        const S& F = x[mu * NXM + 1];
+        f[mu * NXM] = (cs[mu] - cn) * C.inv_tauc;
+        S km = Num<S>::c(C.km_rest), tau1 = Num<S>::c(C.tau1_rest), A = Num<S>::c(C.a_force);
+        if constexpr (FAT) {
+            A = x[mu * NXM + 2];
+            tau1 = x[mu * NXM + 3];
+            km = x[mu * NXM + 4];
+        }
+        S Aeff = A;
+        if constexpr (PW) Aeff = A * (1.0 - mexp(-(u[mu] - C.pd0) * C.inv_pdt));
+        const S s = cn / (km + cn);
+        f[mu * NXM + 1] = (Aeff * s - F / (tau1 + C.tau2 * s)) * mult;
+        if constexpr (FAT) {
+            f[mu * NXM + 2] = C.alpha_a * F - (A - C.a_fat_rest) * C.inv_tau_fat;
+            f[mu * NXM + 3] = C.alpha_tau1 * F - (tau1 - C.tau1_rest) * C.inv_tau_fat;
+            f[mu * NXM + 4] = C.alpha_km * F - (km - C.km_rest) * C.inv_tau_fat;
+        }
+        // ---- joint torque -J_L^T F (dynamical_model.py:331-332)
+#pragma unroll
+        for (int k = 0; k < NQ; ++k) tau[k] = tau[k] - JL[k] * F;
+    }
+    // ---- rigid-body dynamics: h by Newton-Euler (qddot = 0), M from the body Jacobians
+    S w[3] = {Num<S>::c(0.0), Num<S>::c(0.0), Num<S>::c(0.0)};
+    S al[3] = {Num<S>::c(0.0), Num<S>::c(0.0), Num<S>::c(0.0)};
+    S acc[3] = {Num<S>::c(-G.grav[0]), Num<S>::c(-G.grav[1]), Num<S>::c(-G.grav[2])};
+    S h[NQ], M[NQ][NQ];
+#pragma unroll
+    for (int i = 0; i < NQ; ++i) {
+        h[i] = Num<S>::c(0.0);
+#pragma unroll
+        for (int k = 0; k < NQ; ++k) M[i][k] = Num<S>::c(0.0);
+    }
+#pragma unroll
+    for (int j = 0; j < NQ; ++j) {
+        const S* qd = x + XQD;
+        if (j > 0) {
+            const S r[3] = {o[j][0] - o[j - 1][0], o[j][1] - o[j - 1][1], o[j][2] - o[j - 1][2]};
+            S t1[3], t2[3], t3[3];
+            cross3(al, r, t1);
+            cross3(w, r, t2);
+            cross3(w, t2, t3);
+#pragma unroll
+            for (int e = 0; e < 3; ++e) acc[e] = acc[e] + t1[e] + t3[e];
+            const S zq[3] = {z[j][0] * qd[j], z[j][1] * qd[j], z[j][2] * qd[j]};
+            S t4[3];
+            cross3(w, zq, t4);
+#pragma unroll
+            for (int e = 0; e < 3; ++e) {
+                al[e] = al[e] + t4[e];
+                w[e] = w[e] + zq[e];
+            }
+        } else {
+#pragma unroll
+            for (int e = 0; e < 3; ++e) w[e] = z[0][e] * qd[0];
+        }
+        if (G.mass[j] == 0.0) continue;
+        // composite body of frame j
+        S rc[3], c[3];
+#pragma unroll
+        for (int e = 0; e < 3; ++e) {
+            rc[e] = R[j][e * 3] * G.com[j][0] + R[j][e * 3 + 1] * G.com[j][1] + R[j][e * 3 + 2] * G.com[j][2];
+            c[e] = o[j][e] + rc[e];
+        }
+        S RI[9], Iw[9];  // Iw = R I R^T
+#pragma unroll
+        for (int r = 0; r < 3; ++r)
+#pragma unroll
+            for (int cc = 0; cc < 3; ++cc)
+                RI[r * 3 + cc] = R[j][r * 3] * G.inertia[j][cc] + R[j][r * 3 + 1] * G.inertia[j][3 + cc] +
+                                 R[j][r * 3 + 2] * G.inertia[j][6 + cc];
+#pragma unroll
+        for (int r = 0; r < 3; ++r)
+#pragma unroll
+            for (int cc = 0; cc < 3; ++cc)
+                Iw[r * 3 + cc] = RI[r * 3] * R[j][cc * 3] + RI[r * 3 + 1] * R[j][cc * 3 + 1] + RI[r * 3 + 2] * R[j][cc * 3 + 2];
+        S t1[3], t2[3], t3[3], ac[3];
+        cross3(al, rc, t1);
+        cross3(w, rc, t2);
+        cross3(w, t2, t3);
+        const double mj = G.mass[j];
+        S Fb[3];
+#pragma unroll
+        for (int e = 0; e < 3; ++e) {
+            ac[e] = acc[e] + t1[e] + t3[e];
+            Fb[e] = mj * ac[e];
+        }
+        S Iwa[3], Iww[3], t5[3], Nb[3];
+#pragma unroll
+        for (int e = 0; e < 3; ++e) {
+            Iwa[e] = Iw[e * 3] * al[0] + Iw[e * 3 + 1] * al[1] + Iw[e * 3 + 2] * al[2];
+            Iww[e] = Iw[e * 3] * w[0] + Iw[e * 3 + 1] * w[1] + Iw[e * 3 + 2] * w[2];
+        }
+        cross3(w, Iww, t5);
+#pragma unroll
+        for (int e = 0; e < 3; ++e) Nb[e] = Iwa[e] + t5[e];
+        S Jv[NQ][3], IJ[NQ][3];
+#pragma unroll
+        for (int i = 0; i <= j; ++i) {
+            const S r[3] = {c[0] - o[i][0], c[1] - o[i][1], c[2] - o[i][2]};
+            S m1[3];
+            cross3(r, Fb, m1);
+            const S mm[3] = {m1[0] + Nb[0], m1[1] + Nb[1], m1[2] + Nb[2]};
+            h[i] = h[i] + dot3(z[i], mm);
+            cross3(z[i], r, Jv[i]);
+#pragma unroll
+            for (int e = 0; e < 3; ++e) IJ[i][e] = Iw[e * 3] * z[i][0] + Iw[e * 3 + 1] * z[i][1] + Iw[e * 3 + 2] * z[i][2];
+        }
+#pragma unroll
+        for (int i = 0; i <= j; ++i)
+#pragma unroll
+            for (int k = 0; k <= i; ++k) M[i][k] = M[i][k] + mj * dot3(Jv[i], Jv[k]) + dot3(z[i], IJ[k]);
+    }
+    // ---- solve M qddot = tau - h (symmetric positive definite, unrolled Cholesky)
+    S rhs[NQ];
+#pragma unroll
+    for (int i = 0; i < NQ; ++i) rhs[i] = tau[i] - h[i];
+    if constexpr (NQ == 1) {
+        f[XQD] = rhs[0] / M[0][0];
+    } else if constexpr (NQ == 2) {
+        const S det = M[0][0] * M[1][1] - M[1][0] * M[1][0];
+        f[XQD] = (M[1][1] * rhs[0] - M[1][0] * rhs[1]) / det;
+        f[XQD + 1] = (M[0][0] * rhs[1] - M[1][0] * rhs[0]) / det;
+    } else {
+        S Lc[NQ][NQ];
+#pragma unroll
+        for (int i = 0; i < NQ; ++i)
+#pragma unroll
+            for (int k = 0; k <= i; ++k) {
+                S sum = M[i][k];
+#pragma unroll
+                for (int p = 0; p < k; ++p) sum = sum - Lc[i][p] * Lc[k][p];
+                Lc[i][k] = i == k ? msqrt(sum) : sum / Lc[k][k];
+            }
+        S y[NQ];
+#pragma unroll
+        for (int i = 0; i < NQ; ++i) {
+            S sum = rhs[i];
+#pragma unroll
+            for (int p = 0; p < i; ++p) sum = sum - Lc[i][p] * y[p];
+            y[i] = sum / Lc[i][i];
+        }
+#pragma unroll
+        for (int i = NQ - 1; i >= 0; --i) {
+            S sum = y[i];
+#pragma unroll
+            for (int p = i + 1; p < NQ; ++p) sum = sum - Lc[p][i] * f[XQD + p];
+            f[XQD + i] = sum / Lc[i][i];
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < NQ; ++k) f[XQ + k] = x[XQD + k];
+}
+
+// Phi_m(x, u) over interval k: m RK sub-steps (bioptim convention: constant control, RK4 stage times
+// t, t + h/2, t + h/2, t + h).  x is overwritten with the end state.
+template <int NQ, int NM, int FAM, int SCHEME, class S>
+MSK_HD void msk_interval(const MskParams& P, const MskGeom& G, int k, S* x, const S* u) {
+    constexpr int NX = NM * msk_nxm<FAM>() + 2 * NQ;
+    constexpr int ST = SCHEME == 4 ? 4 : (SCHEME == 2 ? 2 : 1);
+    constexpr int NMC = NM;
+    const double h = P.h;
+    for (int j = 0; j < P.m; ++j) {
+        const double* cs = P.cs + ((int64_t)k * P.Q + j * ST) * NMC;
+        if constexpr (SCHEME == 1) {
+            S f[NX];
+            msk_rhs<NQ, NM, FAM>(G, P.residual, cs, x, u, f);
+#pragma unroll
+            for (int r = 0; r < NX; ++r) x[r] = x[r] + h * f[r];
+        } else if constexpr (SCHEME == 2) {
+            S f[NX], xs[NX];
+            msk_rhs<NQ, NM, FAM>(G, P.residual, cs, x, u, f);
+#pragma unroll
+            for (int r = 0; r < NX; ++r) xs[r] = x[r] + (0.5 * h) * f[r];
+            msk_rhs<NQ, NM, FAM>(G, P.residual, cs + NMC, xs, u, f);
+#pragma unroll
+            for (int r = 0; r < NX; ++r) x[r] = x[r] + h * f[r];
+        } else {
+            S acc[NX], xs[NX], f[NX];
+            msk_rhs<NQ, NM, FAM>(G, P.residual, cs, x, u, f);
+#pragma unroll
+            for (int r = 0; r < NX; ++r) {
+                acc[r] = f[r];
+                xs[r] = x[r] + (0.5 * h) * f[r];
+            }
+            msk_rhs<NQ, NM, FAM>(G, P.residual, cs + NMC, xs, u, f);
+#pragma unroll
+            for (int r = 0; r < NX; ++r) {
+                acc[r] = acc[r] + 2.0 * f[r];
+                xs[r] = x[r] + (0.5 * h) * f[r];
+            }
+            msk_rhs<NQ, NM, FAM>(G, P.residual, cs + 2 * NMC, xs, u, f);
+#pragma unroll
+            for (int r = 0; r < NX; ++r) {
+                acc[r] = acc[r] + 2.0 * f[r];
+                xs[r] = x[r] + h * f[r];
+            }
+            msk_rhs<NQ, NM, FAM>(G, P.residual, cs + 3 * NMC, xs, u, f);
+#pragma unroll
+            for (int r = 0; r < NX; ++r) x[r] = x[r] + (h / 6.0) * (acc[r] + f[r]);
+        }
+    }
+}
+
+// ---- g + J_g: thread = (instance, interval, chunk of D Jacobian directions) ---------------------------------
+template <int NQ, int NM, int FAM, int SCHEME, int D>
+__global__ void __launch_bounds__(256) k_msk_shooting(const MskParams P, const MskGeom* __restrict__ GG,
+                                                      const double* __restrict__ V, double* __restrict__ Gout,
+                                                      double* __restrict__ J) {
+    constexpr int NX = NM * msk_nxm<FAM>() + 2 * NQ;
+    constexpr int NUMAX = (msk_pw<FAM>() ? NM : 0) + NQ;
+    const int64_t B = P.B;
+    const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= B) return;
+    const int k = blockIdx.y;
+    const int c0 = blockIdx.z * D;
+    const MskGeom& G = *GG;
+    const int nz = P.nz, nu = P.nu;
+    const int64_t zb = (int64_t)k * nz;
+    using S = Dual<D>;
+    S x[NX], u[NUMAX > 0 ? NUMAX : 1];
+#pragma unroll
+    for (int r = 0; r < NX; ++r) {
+        x[r] = dconst<D>(V[(zb + r) * B + b]);
+#pragma unroll
+        for (int d = 0; d < D; ++d) x[r].d[d] = (r == c0 + d) ? 1.0 : 0.0;
+    }
+#pragma unroll
+    for (int i = 0; i < NUMAX; ++i) {
+        u[i] = dconst<D>(i < nu ? V[(zb + NX + i) * B + b] : 0.0);
+#pragma unroll
+        for (int d = 0; d < D; ++d) u[i].d[d] = (NX + i == c0 + d) ? 1.0 : 0.0;
+    }
+    double xn[NX];
+    if (Gout && blockIdx.z == 0) {
+#pragma unroll
+        for (int r = 0; r < NX; ++r) xn[r] = V[(zb + nz + r) * B + b];
+    }
+    msk_interval<NQ, NM, FAM, SCHEME>(P, G, k, x, u);
+    if (Gout && blockIdx.z == 0) {
+#pragma unroll
+        for (int r = 0; r < NX; ++r) Gout[((int64_t)k * NX + r) * B + b] = x[r].v - xn[r];
+    }
+    if (J) {
+        const int64_t jb = (int64_t)k * P.nnzk;
+#pragma unroll
+        for (int r = 0; r < NX; ++r)
+#pragma unroll
+            for (int d = 0; d < D; ++d) {
+                const int col = c0 + d;
+                if (col < nz) {
+                    const int pos = G.jpos[r * kMskMaxZ + col];
+                    if (pos >= 0) J[(jb + pos) * B + b] = x[r].d[d];
+                }
+            }
+        if (blockIdx.z == 0) {
+#pragma unroll
+            for (int r = 0; r < NX; ++r) J[(jb + G.jneg[r]) * B + b] = -1.0;
+        }
+    }
+}
+
+// ---- Lagrangian Hessian blocks: thread = (instance, interval, direction-block pair task) ------------------
+// Task (I, J), I <= J, seeds blocks I and J (BS directions each) in Jet<2 BS> slots and writes
+// sum_r lambda_{k,r} d^2 Phi_r / dz_a dz_b for a in block J, b in block I (a >= b), packed lower triangle.
+template <int NQ, int NM, int FAM, int SCHEME, int BS>
+__global__ void __launch_bounds__(256) k_msk_hessian(const MskParams P, const MskGeom* __restrict__ GG,
+                                                     const int16_t* __restrict__ tasks, const double* __restrict__ V,
+                                                     const double* __restrict__ LAM, double* __restrict__ H) {
+    constexpr int NX = NM * msk_nxm<FAM>() + 2 * NQ;
+    constexpr int NUMAX = (msk_pw<FAM>() ? NM : 0) + NQ;
+    constexpr int DJ = 2 * BS;
+    const int64_t B = P.B;
+    const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= B) return;
+    const int k = blockIdx.y;
+    const int I = tasks[2 * blockIdx.z], Jb = tasks[2 * blockIdx.z + 1];
+    const MskGeom& G = *GG;
+    const int nz = P.nz, nu = P.nu;
+    const int64_t zb = (int64_t)k * nz;
+    using S = Jet<DJ>;
+    // slot s -> global direction (block I for s < BS, block J for s >= BS; unused when I == J)
+    auto dir_of = [&](int s) { return s < BS ? I * BS + s : (I == Jb ? -1 : Jb * BS + (s - BS)); };
+    S x[NX], u[NUMAX > 0 ? NUMAX : 1];
+#pragma unroll
+    for (int r = 0; r < NX; ++r) {
+        x[r] = jconst<DJ>(V[(zb + r) * B + b]);
+#pragma unroll
+        for (int s = 0; s < DJ; ++s) x[r].g[s] = (dir_of(s) == r) ? 1.0 : 0.0;
+    }
+#pragma unroll
+    for (int i = 0; i < NUMAX; ++i) {
+        u[i] = jconst<DJ>(i < nu ? V[(zb + NX + i) * B + b] : 0.0);
+#pragma unroll
+        for (int s = 0; s < DJ; ++s) u[i].g[s] = (dir_of(s) == NX + i) ? 1.0 : 0.0;
+    }
+    msk_interval<NQ, NM, FAM, SCHEME>(P, G, k, x, u);
+    double acc[S::H];
+#pragma unroll
+    for (int p = 0; p < S::H; ++p) acc[p] = 0.0;
+#pragma unroll
+    for (int r = 0; r < NX; ++r) {
+        const double lam = LAM[((int64_t)k * NX + r) * B + b];
+#pragma unroll
+        for (int p = 0; p < S::H; ++p) acc[p] += lam * x[r].h[p];
+    }
+    const int64_t hb = (int64_t)k * P.nhk;
+#pragma unroll
+    for (int s = 0; s < DJ; ++s)
+#pragma unroll
+        for (int t = 0; t <= s; ++t) {
+            const int a = dir_of(s), c = dir_of(t);
+            if (a < 0 || c < 0 || a >= nz || c >= nz) continue;
+            const bool same = I == Jb;
+            if (!same && !(s >= BS && t < BS)) continue;  // cross task: only (block J, block I) pairs
+            const int hi = a > c ? a : c, lo = a > c ? c : a;
+            H[(hb + hi * (hi + 1) / 2 + lo) * B + b] = acc[s * (s + 1) / 2 + t];
+        }
+}
+
+// ---- single shooting (IVP): thread = instance, every sub-step written -------------------------------------
+template <int NQ, int NM, int FAM, int SCHEME>
+__global__ void __launch_bounds__(256) k_msk_ivp(const MskParams P, const MskGeom* __restrict__ GG,
+                                                 const double* __restrict__ X0, const double* __restrict__ U,
+                                                 double* __restrict__ TR) {
+    constexpr int NX = NM * msk_nxm<FAM>() + 2 * NQ;
+    constexpr int NUMAX = (msk_pw<FAM>() ? NM : 0) + NQ;
+    const int64_t B = P.B;
+    const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= B) return;
+    const MskGeom& G = *GG;
+    double x[NX], u[NUMAX > 0 ? NUMAX : 1];
+#pragma unroll
+    for (int r = 0; r < NX; ++r) x[r] = X0 ? X0[(int64_t)r * B + b] : P.rest[r];
+    int64_t row = 0;
+#pragma unroll
+    for (int r = 0; r < NX; ++r) TR[(row * NX + r) * B + b] = x[r];
+    MskParams P1 = P;
+    P1.m = 1;
+    for (int k = 0; k < P.N; ++k) {
+#pragma unroll
+        for (int i = 0; i < NUMAX; ++i) u[i] = i < P.nu ? U[((int64_t)k * P.nu + i) * B + b] : 0.0;
+        for (int j = 0; j < P.m; ++j) {
+            MskParams Pj = P1;
+            Pj.cs = P.cs + (int64_t)j * (P.Q / P.m) * NM;  // sub-step j's stage sums inside interval k
+            msk_interval<NQ, NM, FAM, SCHEME>(Pj, G, k, x, u);
+            ++row;
+#pragma unroll
+            for (int r = 0; r < NX; ++r) TR[(row * NX + r) * B + b] = x[r];
+        }
+    }
+}
+
+// ---- objective: quadratic tracking terms and the fatigue ratio term; thread = instance ---------------------
+struct MskObjective {
+    int32_t kind;  // 0 Lagrange quadratic, 1 Mayer quadratic, 2 Mayer inverse square  w (c / z)^2
+    int32_t var_kind, var_index, node_first, node_last, target_off;
+    double w_eff, target_value;
+};
+
+static __global__ void __launch_bounds__(256) k_msk_objective(const MskParams P, int n_obj, const MskObjective* __restrict__ obj,
+                                                       const double* __restrict__ targets, const double* __restrict__ V,
+                                                       double* __restrict__ F, double* __restrict__ GRAD,
+                                                       const double* __restrict__ obj_factor, double* __restrict__ H,
+                                                       const int32_t* __restrict__ hdiag) {
+    const int64_t B = P.B;
+    const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= B) return;
+    double f = 0.0;
+    const double s = H ? obj_factor[b] : 0.0;
+    for (int t = 0; t < n_obj; ++t) {
+        const MskObjective o = obj[t];
+        for (int k = o.node_first; k <= o.node_last; ++k) {
+            const int e = (o.var_kind == 0 ? 0 : P.nx) + o.var_index;
+            const int64_t off = (int64_t)k * P.nz + e;
+            const double z = V[off * B + b];
+            double val, g1, g2;
+            if (o.kind == 2) {
+                const double r = o.target_value / z;
+                val = o.w_eff * r * r;
+                g1 = -2.0 * val / z;
+                g2 = 6.0 * val / (z * z);
+            } else {
+                const double tgt = o.target_off >= 0 ? targets[o.target_off + k] : o.target_value;
+                const double d = z - tgt;
+                val = o.w_eff * d * d;
+                g1 = 2.0 * o.w_eff * d;
+                g2 = 2.0 * o.w_eff;
+            }
+            f += val;
+            if (GRAD) GRAD[off * B + b] += g1;
+            if (H) H[(int64_t)hdiag[k * P.nz + e] * B + b] += s * g2;
+        }
+    }
+    if (F) F[b] = f;
+}
+
+}  // namespace cfx

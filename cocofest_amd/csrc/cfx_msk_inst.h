@@ -1,0 +1,85 @@
+// cfx_msk_inst.h — kernel instantiation helpers shared by the cfx_inst_msk_*.hip translation units (one per
+// model family pair, so the builds run in parallel).
+#pragma once
+
+#include "cfx_msk_launch.h"
+
+namespace cfx {
+
+
+constexpr int kMskBlk = 256;
+
+// Jacobian directions carried per lane: enough to keep the RK stage arrays in VGPRs.
+constexpr int msk_dirs_for(int nq, int nm, int fam) {
+    return (nm * ((fam & 1) ? 5 : 2) + 2 * nq) > 16 ? 2 : 4;
+}
+
+template <int NQ, int NM, int FAM, int SCHEME>
+void dep_t(const MskParams& P, const MskGeom& G, uint64_t* dep) {
+    constexpr int NX = NM * msk_nxm<FAM>() + 2 * NQ;
+    constexpr int NUMAX = (msk_pw<FAM>() ? NM : 0) + NQ;
+    Dep x[NX], u[NUMAX];
+    for (int r = 0; r < NX; ++r) x[r].m = 1ull << r;
+    for (int i = 0; i < NUMAX; ++i) u[i].m = i < P.nu ? 1ull << (NX + i) : 0ull;
+    msk_interval<NQ, NM, FAM, SCHEME>(P, G, 0, x, u);
+    for (int r = 0; r < NX; ++r) dep[r] = x[r].m;
+}
+
+template <int NQ, int NM, int FAM, int SCHEME>
+hipError_t shoot_t(const MskParams& P, const MskGeom* G, const double* V, double* Gout, double* J, hipStream_t s) {
+    constexpr int D = msk_dirs_for(NQ, NM, FAM);
+    const int nchunk = J ? (P.nz + D - 1) / D : 1;
+    dim3 grid((unsigned)((P.B + kMskBlk - 1) / kMskBlk), (unsigned)P.N, (unsigned)nchunk);
+    hipLaunchKernelGGL((k_msk_shooting<NQ, NM, FAM, SCHEME, D>), grid, dim3(kMskBlk), 0, s, P, G, V, Gout, J);
+    return hipGetLastError();
+}
+
+template <int NQ, int NM, int FAM, int SCHEME>
+hipError_t hess_t(const MskParams& P, const MskGeom* G, const int16_t* tasks, int ntasks, const double* V,
+                  const double* LAM, double* H, hipStream_t s) {
+    dim3 grid((unsigned)((P.B + kMskBlk - 1) / kMskBlk), (unsigned)P.N, (unsigned)ntasks);
+    hipLaunchKernelGGL((k_msk_hessian<NQ, NM, FAM, SCHEME, 1>), grid, dim3(kMskBlk), 0, s, P, G, tasks, V, LAM, H);
+    return hipGetLastError();
+}
+
+template <int NQ, int NM, int FAM, int SCHEME>
+hipError_t ivp_t(const MskParams& P, const MskGeom* G, const double* X0, const double* U, double* TR, hipStream_t s) {
+    dim3 grid((unsigned)((P.B + kMskBlk - 1) / kMskBlk));
+    hipLaunchKernelGGL((k_msk_ivp<NQ, NM, FAM, SCHEME>), grid, dim3(kMskBlk), 0, s, P, G, X0, U, TR);
+    return hipGetLastError();
+}
+
+// One dispatched call: op 0 = dependency pattern (host), 1 = g + J_g, 2 = Hessian, 3 = IVP, 4 = "is it compiled".
+struct MskCall {
+    int op, nq, nm, fam, scheme;
+    const MskParams* P;
+    const MskGeom* G;      // device copy (kernels) or host copy (op 0)
+    uint64_t* dep;
+    const double *V, *LAM, *X0, *U;
+    double *Gout, *J, *H, *TR;
+    const int16_t* tasks;
+    int ntasks;
+    hipStream_t s;
+    hipError_t err;
+};
+
+template <int NQ, int NM, int FAM, int SC>
+bool msk_try(MskCall& c) {
+    if (c.nq != NQ || c.nm != NM || c.fam != FAM || c.scheme != SC) return false;
+    switch (c.op) {
+        case 0: dep_t<NQ, NM, FAM, SC>(*c.P, *c.G, c.dep); break;
+        case 1: c.err = shoot_t<NQ, NM, FAM, SC>(*c.P, c.G, c.V, c.Gout, c.J, c.s); break;
+        case 2: c.err = hess_t<NQ, NM, FAM, SC>(*c.P, c.G, c.tasks, c.ntasks, c.V, c.LAM, c.H, c.s); break;
+        case 3: c.err = ivp_t<NQ, NM, FAM, SC>(*c.P, c.G, c.X0, c.U, c.TR, c.s); break;
+        default: break;
+    }
+    return true;
+}
+
+#define CFX_MSK_SCHEMES(NQ, NM, FAM) msk_try<NQ, NM, FAM, 1>(c) || msk_try<NQ, NM, FAM, 4>(c)
+
+// per-unit dispatchers (cfx_inst_msk_d03.hip, cfx_inst_msk_d07.hip)
+bool msk_dispatch_d03(MskCall& c);
+bool msk_dispatch_d07(MskCall& c);
+
+}  // namespace cfx

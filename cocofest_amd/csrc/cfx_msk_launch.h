@@ -1,0 +1,27 @@
+// cfx_msk_launch.h — host-side entry points of the musculoskeletal kernels (instantiated in cfx_inst_msk.hip).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "cfx_msk.h"
+
+namespace cfx {
+
+// Supported shapes: is (n_dof, n_muscles, family, scheme) compiled in?
+bool msk_supported(int nq, int nm, int fam, int scheme);
+
+// Structural dependency masks of the nx end states of one interval over z = (x_k, u_k) (host, Dep arithmetic).
+void msk_dep_pattern(int nq, int nm, int fam, int scheme, const MskParams& P, const MskGeom& G, uint64_t* dep);
+
+// Jacobian directions per lane of k_msk_shooting for a shape.
+int msk_dirs(int nq, int nm, int fam);
+
+hipError_t launch_msk_shooting(int nq, int nm, int fam, int scheme, const MskParams& P, const MskGeom* G,
+                               const double* V, double* Gout, double* J, hipStream_t s);
+hipError_t launch_msk_hessian(int nq, int nm, int fam, int scheme, const MskParams& P, const MskGeom* G,
+                              const int16_t* tasks, int ntasks, const double* V, const double* LAM, double* H,
+                              hipStream_t s);
+hipError_t launch_msk_ivp(int nq, int nm, int fam, int scheme, const MskParams& P, const MskGeom* G,
+                          const double* X0, const double* U, double* TR, hipStream_t s);
+
+}  // namespace cfx

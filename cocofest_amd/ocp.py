@@ -51,11 +51,15 @@ class ObjectiveFcn:
 class Objective:
     """One quadratic objective term (the subset of bioptim ObjectiveFcn the reference's FES OCPs use)."""
 
-    def __init__(self, objective, key: str, weight: float = 1, target=None, node: Node = None, quadratic: bool = True):
+    def __init__(self, objective, key: str, weight: float = 1, target=None, node: Node = None, quadratic: bool = True,
+                 index=None, phase: int = 0):
         if not quadratic:
             raise NotImplementedError("only quadratic objective terms are supported")
+        if phase != 0:
+            raise NotImplementedError("single-phase problems only")
         self.objective = objective
         self.key = key
+        self.index = index
         self.weight = float(weight)
         self.target = target
         lagrange = isinstance(objective, ObjectiveFcn.Lagrange)
@@ -286,8 +290,9 @@ class OcpFes:
     @staticmethod
     def _sanity_check(model=None, n_shooting=None, final_time=None, objective=None, use_sx=None, ode_solver=None,
                       n_threads=None):
-        """Input validation with the reference's messages (fes_ocp.py:279-344)."""
-        if not isinstance(model, FesModel):
+        """Input validation with the reference's messages (fes_ocp.py:279-344).  A FesMskModel passes the model
+        check (fes_ocp.py:289-291); every other check applies to it unchanged."""
+        if not isinstance(model, FesModel) and not hasattr(model, "muscles_dynamics_model"):
             raise TypeError(
                 f"The current model type used is {type(model)}, it must be a FesModel type."
                 f"Current available models are: DingModelFrequency, DingModelFrequencyWithFatigue,"

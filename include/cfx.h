@@ -175,6 +175,66 @@ int cfx_eval_all(cfx_handle *h, const double *v, double *g, double *jac, double 
    u [N*nu per instance], writing every sub-step state: traj [(N*n_steps+1)*nx per instance]. ---- */
 int cfx_integrate(cfx_handle *h, const double *x0, const double *u, double *traj, uint32_t flags);
 
+/* ---- musculoskeletal problems (FesMskModel + OcpFesMsk) --------------------------------------------
+   Replaces the bioptim dynamics plugin FesMskModel registers (cocofest/models/dynamical_model.py:133-203,
+   406-451: every muscle's FES ODE scaled by the De Groote force-length / force-velocity / passive-force
+   coefficients of hill_coefficients.py:11-126, joint torque -J_L(q)^T F, biorbd forward dynamics) and the NLP
+   callbacks of the OCP built by OcpFesMsk.prepare_ocp (cocofest/optimization/fes_ocp_dynamics.py:158-251).
+   The skeleton is a serial chain of revolute dofs (the host reduces a bioMod: constant segment transforms
+   between dofs are composed, the segments moving with a dof are merged into one composite body).
+   Per node the states are [muscle 0 (Cn, F[, A, Tau1, Km]), muscle 1, ..., q (n_dof), qdot (n_dof)]; the
+   controls [last_pulse_width of every muscle (Ding2007 families)] then [tau (n_dof)] with
+   CFX_MSK_RESIDUAL_TORQUE; the decision vector, constraint rows and layouts are those of cfx_problem's
+   shooting transcription (CFX_RK1/2/4, CFX_LAYOUT_AOS or CFX_LAYOUT_SOA).  The handle works with every
+   cfx_* call above (sizes, structures, eval_*, eval_h, integrate, destroy). */
+#define CFX_MSK_MAX_DOF 4
+#define CFX_MSK_MAX_MUSCLES 8
+#define CFX_MSK_MAX_POINTS 16
+#define CFX_MSK_FORCE_LENGTH 1u   /* hill_coefficients.py:11-63 (the reference gates it with the FV flag) */
+#define CFX_MSK_FORCE_VELOCITY 2u /* hill_coefficients.py:66-96 */
+#define CFX_MSK_PASSIVE_FORCE 4u  /* hill_coefficients.py:99-126 */
+#define CFX_MSK_RESIDUAL_TORQUE 8u
+/* objective kind for MSK problems: weight * (target_value / z_k)^2 at the nodes of the range
+   (CustomObjective.minimize_overall_muscle_fatigue, cocofest/custom_objectives.py:80-101: a_rest / A) */
+#define CFX_OBJ_MAYER_INV 2
+
+typedef struct cfx_msk_muscle {
+    int32_t model; /* CFX_DING2003 .. CFX_DING2007_FATIGUE; all muscles of a problem share the model family */
+    cfx_constants constants;
+    int32_t n_points;           /* origin, via points, insertion (<= CFX_MSK_MAX_POINTS) */
+    const int32_t *point_frame; /* [n_points] dof frame the point is fixed in (moves with q_0..q_j), -1: ground */
+    const double *point_pos;    /* [n_points * 3] position in that frame */
+    double optimal_length, tendon_slack_length, pennation_angle;
+} cfx_msk_muscle;
+
+typedef struct cfx_msk_problem {
+    int32_t abi_version; /* CFX_ABI_VERSION */
+    int32_t scheme;      /* CFX_RK1 | CFX_RK2 | CFX_RK4 */
+    int32_t n_steps;
+    int32_t n_shooting;
+    int32_t truncation;
+    int32_t layout; /* CFX_LAYOUT_AOS | CFX_LAYOUT_SOA */
+    int64_t batch;
+    double final_time;
+    const double *stim_rows; /* [(N+1) * T], shared by every muscle (fes_ocp_dynamics.py:86-90) */
+    int32_t n_dof;
+    const int32_t *dof_axis;  /* [n_dof] 0 / 1 / 2: rotation about x / y / z of the dof's joint frame */
+    const double *dof_frame;  /* [n_dof * 12] joint frame j relative to frame j-1 (ground for j = 0): row-major
+                                 3x3 rotation, then the translation (in frame j-1) */
+    double gravity[3];
+    const double *body_mass;    /* [n_dof] composite body moving with frame j */
+    const double *body_com;     /* [n_dof * 3] its centre of mass, frame j */
+    const double *body_inertia; /* [n_dof * 9] its inertia about the com, frame j axes, row-major */
+    int32_t n_muscles;
+    const cfx_msk_muscle *muscles;
+    uint32_t flags; /* CFX_MSK_* */
+    int32_t n_objectives;
+    const cfx_objective *objectives; /* var_index over the state / control layout above */
+    int32_t device;
+} cfx_msk_problem;
+
+int cfx_msk_create(const cfx_msk_problem *problem, cfx_handle **out);
+
 /* ---- Newton / KKT linear algebra of the batched interior-point driver ----------------------------
    Replaces the sparse symmetric-indefinite factorisation Ipopt runs every iteration on the KKT matrix
    (MUMPS by default; `Solver.IPOPT` as built at cocofest/optimization/fes_ocp.py:171-190 and

@@ -1,0 +1,172 @@
+"""GPU parity of the musculoskeletal path (FesMskModel / OcpFesMsk) against the CPU oracle (oracle/fes_msk.py).
+
+Tolerances (FP64): g relative 1e-10 of |Phi|; J_g entries relative 1e-9 (the kernel's dual numbers against the
+oracle's complex step through a different rigid-body formulation: M from body Jacobians vs Newton-Euler unit
+accelerations); Hessian blocks 1e-5 relative to the block scale (oracle by central differences of complex-step
+gradients); f / grad f 1e-12; IVP trajectories 1e-10 relative.  The oracle is pinned by self-consistency only
+(parity with biorbd + bioptim unpinned, see oracle/fes_msk.py).
+"""
+
+import numpy as np
+import pytest
+
+from oracle import fes_msk as M
+from tests import msk_cases as MC
+
+pytestmark = pytest.mark.gpu
+
+CASES = {
+    "cfg5_d07f_rk4": MC.cfg5(),
+    "d07_rk1_residual": MC.cfg5(model="ding2007", scheme="RK1", m=5, residual=True, fatigue=False),
+    "d03f_rk4_nofv": MC.cfg5(model="ding2003_with_fatigue", fv=False),
+    "d03_rk4_residual": MC.cfg5(model="ding2003", residual=True, fatigue=False, m=2),
+}
+
+
+def _dense_blocks(pb, jr, jc, jv, k):
+    """Interval k's dPhi/dz block (nx x nz) and its -1 block from the product's triplets."""
+    nx, nz = pb.nx, pb.nz
+    D = np.zeros((nx, nz))
+    neg = np.zeros((nx, nx))
+    for r, c, v in zip(jr, jc, jv):
+        if k * nx <= r < (k + 1) * nx:
+            if k * nz <= c < (k + 1) * nz:
+                D[r - k * nx, c - k * nz] = v
+            else:
+                neg[r - k * nx, c - (k + 1) * nz] = v
+    return D, neg
+
+
+@pytest.mark.parametrize("case", list(CASES))
+def test_msk_g_and_jacobian_match_oracle(case):
+    cfg = CASES[case]
+    ocp = MC.product_ocp(**cfg)
+    pb = MC.oracle_problem(**cfg)
+    assert (ocp.nx, ocp.nu, ocp.nv) == (pb.nx, pb.nu, pb.nv)
+    B = 3
+    V = MC.random_decision(pb, B, seed=11)
+    h = ocp.nlp(batch=B, layout="aos")
+    g = h.eval_g(V)
+    jac = h.eval_jac_g(V)
+    jr, jc = h.jac_structure()
+    h.close()
+    for b in range(B):
+        ref_g = M.eval_g(pb, V[b])
+        phi = np.abs(ref_g) + np.abs(np.concatenate([V[b][(k + 1) * pb.nz:(k + 1) * pb.nz + pb.nx]
+                                                     for k in range(pb.n_shooting)]))
+        assert np.max(np.abs(g[b] - ref_g) / (phi + 1e-12)) < 1e-10
+        for k in (0, 4, pb.n_shooting - 1) if b == 0 else (b + 2,):
+            ref = M.continuity_jacobian(pb, V[b], k)
+            D, neg = _dense_blocks(pb, jr, jc, jac[b], k)
+            np.testing.assert_array_equal(neg, -np.eye(pb.nx))
+            scale = np.abs(ref) + 1e-9 * np.max(np.abs(ref), axis=1, keepdims=True)
+            assert np.max(np.abs(D - ref) / scale) < 1e-9, (case, b, k)
+
+
+@pytest.mark.parametrize("case", ["cfg5_d07f_rk4", "d07_rk1_residual"])
+def test_msk_objective_matches_oracle(case):
+    cfg = CASES[case]
+    ocp = MC.product_ocp(**cfg)
+    pb = MC.oracle_problem(**cfg)
+    B = 2
+    V = MC.random_decision(pb, B, seed=5)
+    h = ocp.nlp(batch=B, layout="aos")
+    f = h.eval_f(V)
+    gr = h.eval_grad_f(V)
+    h.close()
+    for b in range(B):
+        np.testing.assert_allclose(f[b], M.eval_f(pb, V[b]), rtol=1e-12)
+        np.testing.assert_allclose(gr[b], M.eval_grad_f(pb, V[b]), rtol=1e-12, atol=1e-14 * np.abs(gr[b]).max())
+
+
+def _lagrangian_block_fd(pb, v, lam_k, k, rel=1e-4):
+    """d^2 (lam_k . Phi_k) / dz^2 by central differences of complex-step gradients (oracle)."""
+    X, U = M.unpack(pb, v)
+    z0 = np.concatenate([X[k], U[k]])
+
+    def grad(z):
+        out = np.empty(pb.nz)
+        for j in range(pb.nz):
+            zz = z.astype(complex)
+            zz[j] += 1e-30j
+            out[j] = np.imag(lam_k @ M.integrate_interval(pb, k, zz[: pb.nx], zz[pb.nx:])) / 1e-30
+        return out
+
+    H = np.empty((pb.nz, pb.nz))
+    for j in range(pb.nz):
+        d = rel * max(abs(z0[j]), 1e-3)
+        e = np.zeros(pb.nz)
+        e[j] = d
+        H[:, j] = (grad(z0 + e) - grad(z0 - e)) / (2 * d)
+    return 0.5 * (H + H.T)
+
+
+@pytest.mark.parametrize("case", ["cfg5_d07f_rk4", "d07_rk1_residual"])
+def test_msk_hessian_matches_oracle(case):
+    cfg = CASES[case]
+    ocp = MC.product_ocp(**cfg)
+    pb = MC.oracle_problem(**cfg)
+    B = 1
+    V = MC.random_decision(pb, B, seed=3)
+    lam = np.random.default_rng(4).normal(size=(B, pb.ng))
+    of = np.array([0.7])
+    h = ocp.nlp(batch=B, layout="aos")
+    hv = h.eval_h(V, of, lam)
+    hr, hc = h.hess_structure()
+    h0 = h.eval_h(V, np.zeros(1), np.zeros_like(lam))  # objective-only part (obj_factor 0 -> zero)
+    h.close()
+    assert np.all(h0 == 0.0)
+    nz, nx = pb.nz, pb.nx
+    for k in (1, pb.n_shooting - 1):
+        ref = _lagrangian_block_fd(pb, V[0], lam[0, k * nx:(k + 1) * nx], k)
+        got = np.zeros((nz, nz))
+        for r, c, val in zip(hr, hc, hv[0]):
+            if k * nz <= r < (k + 1) * nz and k * nz <= c < (k + 1) * nz:
+                got[r - k * nz, c - k * nz] += val
+                if r != c:
+                    got[c - k * nz, r - k * nz] += val
+        # objective diagonal terms at node k (qdot Mayer / fatigue live at node N only; residual torque Lagrange)
+        for o in pb.objectives:
+            if o["node_first"] <= k <= o["node_last"]:
+                e = o["var_index"] + (0 if o["var_kind"] == 0 else nx)
+                w = o["weight"] * (pb.dt if o["kind"] == 0 else 1.0)
+                ref[e, e] += of[0] * 2 * w
+        scale = np.max(np.abs(ref))
+        assert np.max(np.abs(got - ref)) < 2e-5 * scale, (case, k, np.max(np.abs(got - ref)) / scale)
+
+
+def test_msk_ivp_matches_oracle():
+    cfg = MC.cfg5(m=4)
+    ocp = MC.product_ocp(**cfg)
+    pb = MC.oracle_problem(**cfg)
+    B = 2
+    r = np.random.default_rng(9)
+    U = r.uniform(2e-4, 5e-4, size=(B, pb.n_shooting, pb.nu))
+    x0 = np.tile(ocp.initial_guess_vector()[: pb.nx], (B, 1))
+    x0[:, pb.nxm + pb.nq - 1] = 0.3  # elbow start angle
+    h = ocp.nlp(batch=B, layout="aos")
+    tr = h.integrate(x0=x0, u=U.reshape(B, -1))
+    h.close()
+    for b in range(B):
+        ref = M.ivp(pb, x0[b], U[b])
+        got = tr[b].reshape(-1, pb.nx)
+        scale = np.abs(ref) + 1e-8 * np.abs(ref).max(axis=0)
+        err = np.abs(got - ref) / scale
+        assert err.max() < 1e-9, (b, err.max(), np.unravel_index(err.argmax(), err.shape))
+
+
+def test_msk_cfg5_interior_point_converges():
+    """BASELINE config 5 from the reference's initial guess: the batched interior point over the MSK callbacks
+    reaches the KKT tolerance, the elbow ends at 90 deg (3.14 / 2, the reference's conversion) at rest.
+
+    RK4 x 5 instead of OcpFesMsk's default RK4 x 1: with Ding2007's tau_c = 11 ms a single RK4 step of 0.1 s
+    amplifies the calcium state by |R(-h / tau_c)| = 192 per interval, so from Cn_0 = 0 the continuity row
+    already forces Cn_1 = -234 < 0 and the default transcription is infeasible under the reference's bounds."""
+    ocp = MC.product_ocp(**MC.cfg5(m=5))
+    res = ocp.solve(tol=1e-6, max_iter=1000)
+    print("iterations", res.iterations, "kkt", res.kkt_error, "f", res.f, "wall", res.wall_time)
+    assert bool(res.converged[0])
+    states, controls, _ = ocp.unpack(res.v[0])
+    q_elbow = states[f"q_{ocp.model.name_dof[1]}"][0]
+    assert abs(q_elbow[0] - 3.14 / 36) < 1e-9 and abs(q_elbow[-1] - 1.57) < 1e-9
+    assert np.all(controls["last_pulse_width_BIClong"] >= ocp.model.muscles_dynamics_model[0].pd0 - 1e-12)
