@@ -22,7 +22,7 @@ thread_local std::string g_create_error;
 
 namespace {
 
-enum Slot { S_V = 0, S_A1, S_A2, S_G, S_J, S_F, S_GRAD, S_OUT, S_COUNT };
+enum Slot { S_V = 0, S_A1, S_A2, S_G, S_J, S_F, S_GRAD, S_OUT, S_WORK, S_COUNT };
 
 struct DevBuf {
     double* p = nullptr;
@@ -986,11 +986,29 @@ extern "C" int cfx_msk_create(const cfx_msk_problem* p, cfx_handle** out) {
     for (int mi = 0; mi < nm; ++mi) {
         const cfx_msk_muscle& mu = p->muscles[mi];
         const cfx_constants& c = mu.constants;
-        G.npts[mi] = mu.n_points;
-        for (int i = 0; i < mu.n_points; ++i) {
-            G.pt_frame[mi][i] = mu.point_frame[i];
-            for (int e = 0; e < 3; ++e) G.pt_pos[mi][i][e] = mu.point_pos[i * 3 + e];
+        // A path segment whose two ends are fixed in the same frame keeps its length and adds nothing to the
+        // length Jacobian (d . (z x d) = 0): its length is summed once here; the kernels visit only the segments
+        // that cross frames (2 of the 8 of BIClong, 2 of the 4 of TRIlong in arm26).
+        int ns = 0;
+        double cl = 0.0;
+        for (int i = 0; i + 1 < mu.n_points; ++i) {
+            const double* a = mu.point_pos + i * 3;
+            const double* e3 = mu.point_pos + (i + 1) * 3;
+            if (mu.point_frame[i] == mu.point_frame[i + 1]) {
+                cl += std::sqrt((e3[0] - a[0]) * (e3[0] - a[0]) + (e3[1] - a[1]) * (e3[1] - a[1]) +
+                                (e3[2] - a[2]) * (e3[2] - a[2]));
+                continue;
+            }
+            G.seg_frame[mi][ns][0] = mu.point_frame[i];
+            G.seg_frame[mi][ns][1] = mu.point_frame[i + 1];
+            for (int e = 0; e < 3; ++e) {
+                G.seg_pos[mi][ns][0][e] = a[e];
+                G.seg_pos[mi][ns][1][e] = e3[e];
+            }
+            ++ns;
         }
+        G.nseg[mi] = ns;
+        G.const_len[mi] = cl;
         MskMuscleConst& C = G.mc[mi];
         C.inv_tauc = 1.0 / c.tauc, C.tau2 = c.tau2, C.km_rest = c.km_rest, C.tau1_rest = c.tau1_rest;
         C.a_force = pw ? c.a_scale : c.a_rest;
@@ -1159,9 +1177,16 @@ static int msk_eval_all(cfx_handle* h, const double* v, double* g, double* jac, 
     double* F = f ? stage_out(h, S_F, f, 1, flags, &rc) : nullptr;
     double* GR = grad ? stage_out(h, S_GRAD, grad, h->sz.nv, flags, &rc) : nullptr;
     if (rc != CFX_OK) return rc;
-    if (G || J)
-        CFX_HIP(h, launch_msk_shooting(h->msk_nq, h->msk_nm, h->msk_fam, h->scheme, h->mp, h->d_geom, V, G, J,
+    if (G || J) {
+        MskParams P = h->mp;
+        if (J) {  // per-stage Jacobian coefficients between the two g + J_g launches
+            const size_t nw = (size_t)B * P.N * P.Q * msk_ncoef_host(h->msk_nq, h->msk_nm);
+            P.scratch = ensure(h, h->main[S_WORK], nw, &rc);
+            if (!P.scratch) return rc;
+        }
+        CFX_HIP(h, launch_msk_shooting(h->msk_nq, h->msk_nm, h->msk_fam, h->scheme, P, h->d_geom, V, G, J,
                                        h->stream));
+    }
     if (F || GR) {
         if (GR) CFX_HIP(h, hipMemsetAsync(GR, 0, (size_t)B * h->sz.nv * sizeof(double), h->stream));
         hipLaunchKernelGGL(k_msk_objective, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, h->stream, h->mp,

@@ -26,8 +26,6 @@ bool msk_supported(int nq, int nm, int fam, int scheme) {
     return dispatch(c);
 }
 
-int msk_dirs(int nq, int nm, int fam) { return msk_dirs_for(nq, nm, fam); }
-
 void msk_dep_pattern(int nq, int nm, int fam, int scheme, const MskParams& P, const MskGeom& G, uint64_t* dep) {
     MskCall c = make(0, nq, nm, fam, scheme);
     c.P = &P, c.G = &G, c.dep = dep;

@@ -163,9 +163,12 @@ struct MskGeom {
     double mass[kMskMaxQ];         // composite body moving with frame j (mass, com and inertia about the com, in frame j)
     double com[kMskMaxQ][3];
     double inertia[kMskMaxQ][9];
-    int32_t npts[kMskMaxMus];
-    int32_t pt_frame[kMskMaxMus][kMskMaxPts];  // -1: ground
-    double pt_pos[kMskMaxMus][kMskMaxPts][3];
+    // muscle paths: only the segments whose ends move with different frames (-1: ground) vary with q; the
+    // segments inside one rigid frame contribute a constant length and nothing to the length Jacobian
+    int32_t nseg[kMskMaxMus];
+    int32_t seg_frame[kMskMaxMus][kMskMaxPts][2];
+    double seg_pos[kMskMaxMus][kMskMaxPts][2][3];
+    double const_len[kMskMaxMus];
     MskMuscleConst mc[kMskMaxMus];
     int32_t fl_on, fv_on, fp_on;
     int16_t jpos[kMskMaxX * kMskMaxZ];  // J_g value offset of dPhi_r/dz_c inside an interval block (-1: zero)
@@ -178,6 +181,7 @@ struct MskParams {
     double dt, h;
     const double* cs;    // calcium sums [N][Q][NM] at every RK stage time (host, reference operation order)
     const double* rest;  // rest state [nx] (IVP default x0)
+    double* scratch;     // k_msk_stagecoef -> k_msk_tangents: per-stage Jacobian coefficients [N][Q][NC][B]
 };
 
 template <int FAM>
@@ -298,31 +302,30 @@ MSK_HD S hill_fp(const S& nl) {
     return value(fp) > 0.0 ? fp : Num<S>::c(0.0);
 }
 
-// FesMskModel.muscle_dynamic for one state: f = dx/dt.  cs[m]: calcium sum of muscle m at this stage time.
-template <int NQ, int NM, int FAM, class S>
-MSK_HD void msk_rhs(const MskGeom& G, int residual, const double* cs, const S* x, const S* u, S* f) {
-    constexpr int NXM = msk_nxm<FAM>();
-    constexpr bool FAT = (FAM & 1) != 0, PW = msk_pw<FAM>();
-    constexpr int XQ = NM * NXM, XQD = XQ + NQ;
-    constexpr int NPW = PW ? NM : 0;
+// The skeleton of FesMskModel.muscle_dynamic (dynamical_model.py:133-334) for given muscle forces F: frames,
+// every muscle's length / length Jacobian / velocity and its Hill multiplier mult = FL FV (+ FP), the joint
+// torques -J_L^T F (+ residual taur, nullable) and the forward dynamics qdd.  Mv / JLv (nullable) receive the
+// values of M and J_L.
+template <int NQ, int NM, class S>
+MSK_HD void msk_skeleton(const MskGeom& G, const S* q, const S* qd, const S* F, const S* taur, S* mult, S* qdd,
+                         double (*Mv)[NQ], double (*JLv)[NQ]) {
     S R[NQ][9], o[NQ][3], z[NQ][3];
-    msk_frames<NQ>(G, x + XQ, R, o, z);
+    msk_frames<NQ>(G, q, R, o, z);
     S tau[NQ];
 #pragma unroll
-    for (int k = 0; k < NQ; ++k) tau[k] = residual ? u[NPW + k] : Num<S>::c(0.0);
+    for (int k = 0; k < NQ; ++k) tau[k] = taur ? taur[k] : Num<S>::c(0.0);
 #pragma unroll
     for (int mu = 0; mu < NM; ++mu) {
         const MskMuscleConst& C = G.mc[mu];
-        // ---- geometry: muscle-tendon length and its Jacobian
-        S L = Num<S>::c(0.0), JL[NQ];
+        // ---- geometry: muscle-tendon length and its Jacobian over the frame-crossing segments
+        S L = Num<S>::c(G.const_len[mu]), JL[NQ];
 #pragma unroll
         for (int k = 0; k < NQ; ++k) JL[k] = Num<S>::c(0.0);
-        S P0[3], dP0[NQ][3];
-        msk_point<NQ>(R, o, z, G.pt_frame[mu][0], G.pt_pos[mu][0], P0, dP0);
-        const int np = G.npts[mu];
-        for (int i = 1; i < np; ++i) {
-            S P1[3], dP1[NQ][3];
-            msk_point<NQ>(R, o, z, G.pt_frame[mu][i], G.pt_pos[mu][i], P1, dP1);
+        const int ns = G.nseg[mu];
+        for (int i = 0; i < ns; ++i) {
+            S P0[3], dP0[NQ][3], P1[3], dP1[NQ][3];
+            msk_point<NQ>(R, o, z, G.seg_frame[mu][i][0], G.seg_pos[mu][i][0], P0, dP0);
+            msk_point<NQ>(R, o, z, G.seg_frame[mu][i][1], G.seg_pos[mu][i][1], P1, dP1);
             const S d[3] = {P1[0] - P0[0], P1[1] - P0[1], P1[2] - P0[2]};
             const S n = msqrt(dot3(d, d));
             const S inv = 1.0 / n;
@@ -332,43 +335,21 @@ MSK_HD void msk_rhs(const MskGeom& G, int residual, const double* cs, const S* x
                 const S dd[3] = {dP1[k][0] - dP0[k][0], dP1[k][1] - dP0[k][1], dP1[k][2] - dP0[k][2]};
                 JL[k] = JL[k] + dot3(d, dd) * inv;
             }
-#pragma unroll
-            for (int e = 0; e < 3; ++e) {
-                P0[e] = P1[e];
-#pragma unroll
-                for (int k = 0; k < NQ; ++k) dP0[k][e] = dP1[k][e];
-            }
         }
         // ---- Hill coefficients
         const S nl = ((L - C.slack) * C.inv_cos_penn) * C.inv_lopt;
         S vel = Num<S>::c(0.0);
 #pragma unroll
-        for (int k = 0; k < NQ; ++k) vel = vel + JL[k] * x[XQD + k];
+        for (int k = 0; k < NQ; ++k) vel = vel + JL[k] * qd[k];
         const S fl = G.fl_on ? hill_fl(nl) : Num<S>::c(1.0);
         const S fv = G.fv_on ? hill_fv(vel) : Num<S>::c(1.0);
-        const S mult = G.fp_on ? fl * fv + hill_fp(nl) : fl * fv;
-        // ---- FES muscle ODE (ding2003.py:254-311, ding2003_with_fatigue.py:197-240, ding2007.py:172-188)
-        const S& cn = x[mu * NXM];
-        const S& F = x[mu * NXM + 1];
-        f[mu * NXM] = (cs[mu] - cn) * C.inv_tauc;
-        S km = Num<S>::c(C.km_rest), tau1 = Num<S>::c(C.tau1_rest), A = Num<S>::c(C.a_force);
-        if constexpr (FAT) {
-            A = x[mu * NXM + 2];
-            tau1 = x[mu * NXM + 3];
-            km = x[mu * NXM + 4];
-        }
-        S Aeff = A;
-        if constexpr (PW) Aeff = A * (1.0 - mexp(-(u[mu] - C.pd0) * C.inv_pdt));
-        const S s = cn / (km + cn);
-        f[mu * NXM + 1] = (Aeff * s - F / (tau1 + C.tau2 * s)) * mult;
-        if constexpr (FAT) {
-            f[mu * NXM + 2] = C.alpha_a * F - (A - C.a_fat_rest) * C.inv_tau_fat;
-            f[mu * NXM + 3] = C.alpha_tau1 * F - (tau1 - C.tau1_rest) * C.inv_tau_fat;
-            f[mu * NXM + 4] = C.alpha_km * F - (km - C.km_rest) * C.inv_tau_fat;
-        }
+        mult[mu] = G.fp_on ? fl * fv + hill_fp(nl) : fl * fv;
         // ---- joint torque -J_L^T F (dynamical_model.py:331-332)
 #pragma unroll
-        for (int k = 0; k < NQ; ++k) tau[k] = tau[k] - JL[k] * F;
+        for (int k = 0; k < NQ; ++k) {
+            tau[k] = tau[k] - JL[k] * F[mu];
+            if (JLv) JLv[mu][k] = value(JL[k]);
+        }
     }
     // ---- rigid-body dynamics: h by Newton-Euler (qddot = 0), M from the body Jacobians
     S w[3] = {Num<S>::c(0.0), Num<S>::c(0.0), Num<S>::c(0.0)};
@@ -383,7 +364,6 @@ MSK_HD void msk_rhs(const MskGeom& G, int residual, const double* cs, const S* x
     }
 #pragma unroll
     for (int j = 0; j < NQ; ++j) {
-        const S* qd = x + XQD;
         if (j > 0) {
             const S r[3] = {o[j][0] - o[j - 1][0], o[j][1] - o[j - 1][1], o[j][2] - o[j - 1][2]};
             S t1[3], t2[3], t3[3];
@@ -461,16 +441,22 @@ MSK_HD void msk_rhs(const MskGeom& G, int residual, const double* cs, const S* x
 #pragma unroll
             for (int k = 0; k <= i; ++k) M[i][k] = M[i][k] + mj * dot3(Jv[i], Jv[k]) + dot3(z[i], IJ[k]);
     }
+    if (Mv) {
+#pragma unroll
+        for (int i = 0; i < NQ; ++i)
+#pragma unroll
+            for (int k = 0; k <= i; ++k) Mv[i][k] = Mv[k][i] = value(M[i][k]);
+    }
     // ---- solve M qddot = tau - h (symmetric positive definite, unrolled Cholesky)
     S rhs[NQ];
 #pragma unroll
     for (int i = 0; i < NQ; ++i) rhs[i] = tau[i] - h[i];
     if constexpr (NQ == 1) {
-        f[XQD] = rhs[0] / M[0][0];
+        qdd[0] = rhs[0] / M[0][0];
     } else if constexpr (NQ == 2) {
         const S det = M[0][0] * M[1][1] - M[1][0] * M[1][0];
-        f[XQD] = (M[1][1] * rhs[0] - M[1][0] * rhs[1]) / det;
-        f[XQD + 1] = (M[0][0] * rhs[1] - M[1][0] * rhs[0]) / det;
+        qdd[0] = (M[1][1] * rhs[0] - M[1][0] * rhs[1]) / det;
+        qdd[1] = (M[0][0] * rhs[1] - M[1][0] * rhs[0]) / det;
     } else {
         S Lc[NQ][NQ];
 #pragma unroll
@@ -494,12 +480,52 @@ MSK_HD void msk_rhs(const MskGeom& G, int residual, const double* cs, const S* x
         for (int i = NQ - 1; i >= 0; --i) {
             S sum = y[i];
 #pragma unroll
-            for (int p = i + 1; p < NQ; ++p) sum = sum - Lc[p][i] * f[XQD + p];
-            f[XQD + i] = sum / Lc[i][i];
+            for (int p = i + 1; p < NQ; ++p) sum = sum - Lc[p][i] * qdd[p];
+            qdd[i] = sum / Lc[i][i];
+        }
+    }
+}
+
+// FesMskModel.muscle_dynamic for one state: f = dx/dt.  cs[m]: calcium sum of muscle m at this stage time.
+template <int NQ, int NM, int FAM, class S>
+MSK_HD void msk_rhs(const MskGeom& G, int residual, const double* cs, const S* x, const S* u, S* f) {
+    constexpr int NXM = msk_nxm<FAM>();
+    constexpr bool FAT = (FAM & 1) != 0, PW = msk_pw<FAM>();
+    constexpr int XQ = NM * NXM, XQD = XQ + NQ;
+    constexpr int NPW = PW ? NM : 0;
+    S F[NM], mult[NM], qdd[NQ], taur[NQ];
+#pragma unroll
+    for (int mu = 0; mu < NM; ++mu) F[mu] = x[mu * NXM + 1];
+#pragma unroll
+    for (int k = 0; k < NQ; ++k) taur[k] = residual ? u[NPW + k] : Num<S>::c(0.0);
+    msk_skeleton<NQ, NM>(G, x + XQ, x + XQD, F, residual ? taur : nullptr, mult, qdd, nullptr, nullptr);
+#pragma unroll
+    for (int mu = 0; mu < NM; ++mu) {
+        const MskMuscleConst& C = G.mc[mu];
+        // FES muscle ODE (ding2003.py:254-311, ding2003_with_fatigue.py:197-240, ding2007.py:172-188)
+        const S& cn = x[mu * NXM];
+        f[mu * NXM] = (cs[mu] - cn) * C.inv_tauc;
+        S km = Num<S>::c(C.km_rest), tau1 = Num<S>::c(C.tau1_rest), A = Num<S>::c(C.a_force);
+        if constexpr (FAT) {
+            A = x[mu * NXM + 2];
+            tau1 = x[mu * NXM + 3];
+            km = x[mu * NXM + 4];
+        }
+        S Aeff = A;
+        if constexpr (PW) Aeff = A * (1.0 - mexp(-(u[mu] - C.pd0) * C.inv_pdt));
+        const S s = cn / (km + cn);
+        f[mu * NXM + 1] = (Aeff * s - F[mu] / (tau1 + C.tau2 * s)) * mult[mu];
+        if constexpr (FAT) {
+            f[mu * NXM + 2] = C.alpha_a * F[mu] - (A - C.a_fat_rest) * C.inv_tau_fat;
+            f[mu * NXM + 3] = C.alpha_tau1 * F[mu] - (tau1 - C.tau1_rest) * C.inv_tau_fat;
+            f[mu * NXM + 4] = C.alpha_km * F[mu] - (km - C.km_rest) * C.inv_tau_fat;
         }
     }
 #pragma unroll
-    for (int k = 0; k < NQ; ++k) f[XQ + k] = x[XQD + k];
+    for (int k = 0; k < NQ; ++k) {
+        f[XQ + k] = x[XQD + k];
+        f[XQD + k] = qdd[k];
+    }
 }
 
 // Phi_m(x, u) over interval k: m RK sub-steps (bioptim convention: constant control, RK4 stage times
@@ -607,6 +633,286 @@ __global__ void __launch_bounds__(256) k_msk_shooting(const MskParams P, const M
 #pragma unroll
             for (int r = 0; r < NX; ++r) J[(jb + G.jneg[r]) * B + b] = -1.0;
         }
+    }
+}
+
+// ---- g + J_g, structured (two launches) ---------------------------------------------------------------------
+// The muscle ODEs touch the skeleton only through mult_m(q, qdot) (Hill multiplier) and the forces F_m, and the
+// skeleton is linear in F and in the residual torque: qdd = a(q, qdot) + sum_m B_m(q) F_m + M^-1 tau.  So every
+// RK stage's RHS Jacobian is assembled from one Dual<2 nq> pass of the skeleton over (q, qdot) — independent of
+// how many Jacobian columns are wanted — the values of B_m = -M^-1 J_L[m]^T and M^-1, and the analytic partials
+// of the muscle ODEs (ding2003.py:254-311, ding2003_with_fatigue.py:197-240, ding2007.py:172-188).
+//   k_msk_stagecoef  thread = (instance, interval): the value recursion (g) and, per RK stage, those NC
+//                    coefficients, stored element-major over the batch in a scratch buffer;
+//   k_msk_tangents   thread = (instance, interval, Jacobian column): the RK recursion of one tangent column
+//                    through the stored stage Jacobians (~100 FMAs per stage); the lanes of one instance read
+//                    the same coefficient (one broadcast load), consecutive instances are contiguous.
+
+template <int NQ, int NM>
+constexpr int msk_ncoef() {
+    return NM * (6 + 2 * NQ) + 3 * NQ * NQ + NQ * NM;
+}
+
+// dF'/d(cn, F, A, Tau1, Km, pw) (times the Hill multiplier) and base = A_eff s - F / (tau1 + tau2 s).
+template <int FAM>
+__device__ __forceinline__ void msk_muscle_coef(const MskMuscleConst& C, const double* xm, double pw, double mult,
+                                                double* c, double& base) {
+    constexpr bool FAT = (FAM & 1) != 0, PW = msk_pw<FAM>();
+    const double cn = xm[0], F = xm[1];
+    double A = C.a_force, tau1 = C.tau1_rest, km = C.km_rest;
+    if constexpr (FAT) {
+        A = xm[2];
+        tau1 = xm[3];
+        km = xm[4];
+    }
+    double E = 1.0, dE = 0.0;
+    if constexpr (PW) {
+        const double e = exp(-(pw - C.pd0) * C.inv_pdt);
+        E = 1.0 - e;
+        dE = e * C.inv_pdt;
+    }
+    const double Aeff = A * E;
+    const double d1 = km + cn, s = cn / d1, den = tau1 + C.tau2 * s, iden = 1.0 / den;
+    base = Aeff * s - F * iden;
+    const double dbs = Aeff + F * C.tau2 * iden * iden;  // d base / d s
+    const double id1 = 1.0 / (d1 * d1);
+    c[0] = mult * dbs * km * id1;
+    c[1] = -mult * iden;
+    c[2] = FAT ? mult * s * E : 0.0;
+    c[3] = FAT ? mult * F * iden * iden : 0.0;
+    c[4] = FAT ? -mult * dbs * cn * id1 : 0.0;
+    c[5] = PW ? mult * s * A * dE : 0.0;
+}
+
+// One RK stage: the RHS value f(xs, u) and the stage coefficients written to Ws[c * B].
+template <int NQ, int NM, int FAM>
+__device__ __forceinline__ void msk_stage(const MskGeom& G, int residual, const double* cs, const double* xs,
+                                          const double* u, double* f, double* __restrict__ Ws, int64_t B) {
+    constexpr int NXM = msk_nxm<FAM>(), XQ = NM * NXM, XQD = XQ + NQ, ND = 2 * NQ;
+    constexpr bool FAT = (FAM & 1) != 0, PW = msk_pw<FAM>();
+    constexpr int NPW = PW ? NM : 0, OM = 6 + ND, ODQ = NM * OM, OB = ODQ + NQ * ND, OMI = OB + NQ * NM;
+    using S = Dual<ND>;
+    S q[NQ], qd[NQ], F[NM], taur[NQ], mult[NM], qdd[NQ];
+#pragma unroll
+    for (int k = 0; k < NQ; ++k) {
+        q[k] = dconst<ND>(xs[XQ + k]);
+        qd[k] = dconst<ND>(xs[XQD + k]);
+        q[k].d[k] = 1.0;
+        qd[k].d[NQ + k] = 1.0;
+        taur[k] = dconst<ND>(residual ? u[NPW + k] : 0.0);
+    }
+#pragma unroll
+    for (int mu = 0; mu < NM; ++mu) F[mu] = dconst<ND>(xs[mu * NXM + 1]);
+    double Mv[NQ][NQ], JLv[NM][NQ];
+    msk_skeleton<NQ, NM>(G, q, qd, F, residual ? taur : nullptr, mult, qdd, Mv, JLv);
+#pragma unroll
+    for (int mu = 0; mu < NM; ++mu) {
+        const MskMuscleConst& C = G.mc[mu];
+        const double* xm = xs + mu * NXM;
+        double c[6], base;
+        msk_muscle_coef<FAM>(C, xm, PW ? u[mu] : 0.0, mult[mu].v, c, base);
+        f[mu * NXM] = (cs[mu] - xm[0]) * C.inv_tauc;
+        f[mu * NXM + 1] = base * mult[mu].v;
+        if constexpr (FAT) {
+            f[mu * NXM + 2] = C.alpha_a * xm[1] - (xm[2] - C.a_fat_rest) * C.inv_tau_fat;
+            f[mu * NXM + 3] = C.alpha_tau1 * xm[1] - (xm[3] - C.tau1_rest) * C.inv_tau_fat;
+            f[mu * NXM + 4] = C.alpha_km * xm[1] - (xm[4] - C.km_rest) * C.inv_tau_fat;
+        }
+#pragma unroll
+        for (int e = 0; e < 6; ++e) Ws[(mu * OM + e) * B] = c[e];
+#pragma unroll
+        for (int d = 0; d < ND; ++d) Ws[(mu * OM + 6 + d) * B] = base * mult[mu].d[d];
+    }
+    // M^-1 (symmetric positive definite, NQ <= 4: Gauss-Jordan without pivoting)
+    double Mi[NQ][NQ];
+    if constexpr (NQ == 1) {
+        Mi[0][0] = 1.0 / Mv[0][0];
+    } else if constexpr (NQ == 2) {
+        const double id = 1.0 / (Mv[0][0] * Mv[1][1] - Mv[1][0] * Mv[1][0]);
+        Mi[0][0] = Mv[1][1] * id, Mi[1][1] = Mv[0][0] * id, Mi[0][1] = Mi[1][0] = -Mv[1][0] * id;
+    } else {
+        double a[NQ][NQ];
+#pragma unroll
+        for (int i = 0; i < NQ; ++i)
+#pragma unroll
+            for (int k = 0; k < NQ; ++k) a[i][k] = Mv[i][k], Mi[i][k] = i == k ? 1.0 : 0.0;
+#pragma unroll
+        for (int p = 0; p < NQ; ++p) {
+            const double ip = 1.0 / a[p][p];
+#pragma unroll
+            for (int k = 0; k < NQ; ++k) a[p][k] *= ip, Mi[p][k] *= ip;
+#pragma unroll
+            for (int i = 0; i < NQ; ++i)
+                if (i != p) {
+                    const double fi = a[i][p];
+#pragma unroll
+                    for (int k = 0; k < NQ; ++k) a[i][k] -= fi * a[p][k], Mi[i][k] -= fi * Mi[p][k];
+                }
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < NQ; ++i) {
+        f[XQ + i] = xs[XQD + i];
+        f[XQD + i] = qdd[i].v;
+#pragma unroll
+        for (int d = 0; d < ND; ++d) Ws[(ODQ + i * ND + d) * B] = qdd[i].d[d];
+#pragma unroll
+        for (int mu = 0; mu < NM; ++mu) {
+            double bsum = 0.0;
+#pragma unroll
+            for (int k = 0; k < NQ; ++k) bsum += Mi[i][k] * JLv[mu][k];
+            Ws[(OB + i * NM + mu) * B] = -bsum;
+        }
+#pragma unroll
+        for (int k = 0; k < NQ; ++k) Ws[(OMI + i * NQ + k) * B] = Mi[i][k];
+    }
+}
+
+template <int NQ, int NM, int FAM, int SCHEME>
+__global__ void __launch_bounds__(256) k_msk_stagecoef(const MskParams P, const MskGeom* __restrict__ GG,
+                                                       const double* __restrict__ V, double* __restrict__ Gout) {
+    constexpr int NXM = msk_nxm<FAM>(), NX = NM * NXM + 2 * NQ;
+    constexpr int NUMAX = (msk_pw<FAM>() ? NM : 0) + NQ;
+    constexpr int NC = msk_ncoef<NQ, NM>();
+    constexpr int ST = SCHEME == 4 ? 4 : (SCHEME == 2 ? 2 : 1);
+    const int64_t B = P.B;
+    const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= B) return;
+    const int k = blockIdx.y;
+    const MskGeom& G = *GG;
+    const int nz = P.nz, nu = P.nu, Q = P.Q, residual = P.residual;
+    const int64_t zb = (int64_t)k * nz;
+    const double h = P.h;
+    double* __restrict__ Wk = P.scratch + (int64_t)k * Q * NC * B + b;
+    double x[NX], u[NUMAX];
+#pragma unroll
+    for (int r = 0; r < NX; ++r) x[r] = V[(zb + r) * B + b];
+#pragma unroll
+    for (int i = 0; i < NUMAX; ++i) u[i] = i < nu ? V[(zb + NX + i) * B + b] : 0.0;
+    for (int j = 0; j < P.m; ++j) {
+        double acc[NX], xs[NX];
+#pragma unroll
+        for (int r = 0; r < NX; ++r) xs[r] = x[r];
+#pragma unroll
+        for (int st = 0; st < ST; ++st) {
+            const int slot = j * ST + st;
+            double f[NX];
+            msk_stage<NQ, NM, FAM>(G, residual, P.cs + ((int64_t)k * Q + slot) * NM, xs, u, f,
+                                   Wk + (int64_t)slot * NC * B, B);
+            const double cst = (ST == 4 && st == 2) ? h : 0.5 * h;
+#pragma unroll
+            for (int r = 0; r < NX; ++r) {
+                if (ST == 4) {
+                    if (st == 0) acc[r] = f[r];
+                    else if (st < 3) acc[r] = acc[r] + 2.0 * f[r];
+                }
+                if (st + 1 < ST) xs[r] = x[r] + cst * f[r];
+            }
+            if (st + 1 == ST) {
+#pragma unroll
+                for (int r = 0; r < NX; ++r) x[r] = ST == 4 ? x[r] + (h / 6.0) * (acc[r] + f[r]) : x[r] + h * f[r];
+            }
+        }
+    }
+    if (Gout) {
+#pragma unroll
+        for (int r = 0; r < NX; ++r) Gout[((int64_t)k * NX + r) * B + b] = x[r] - V[(zb + nz + r) * B + b];
+    }
+}
+
+// tk = (df/dx, df/du)(stage) . (t, tu) for one tangent column, from the stored stage coefficients.
+template <int NQ, int NM, int FAM>
+__device__ __forceinline__ void msk_tangent(const MskGeom& G, int residual, const double* __restrict__ Ws, int64_t B,
+                                            const double* t, const double* tu, double* tk) {
+    constexpr int NXM = msk_nxm<FAM>(), XQ = NM * NXM, XQD = XQ + NQ, ND = 2 * NQ;
+    constexpr bool FAT = (FAM & 1) != 0, PW = msk_pw<FAM>();
+    constexpr int NPW = PW ? NM : 0, OM = 6 + ND, ODQ = NM * OM, OB = ODQ + NQ * ND, OMI = OB + NQ * NM;
+#pragma unroll
+    for (int mu = 0; mu < NM; ++mu) {
+        const MskMuscleConst& C = G.mc[mu];
+        const int o = mu * NXM;
+        const double* c = Ws + (int64_t)mu * OM * B;
+        tk[o] = -C.inv_tauc * t[o];
+        double s = c[0] * t[o] + c[B] * t[o + 1];
+        if constexpr (FAT) s += c[2 * B] * t[o + 2] + c[3 * B] * t[o + 3] + c[4 * B] * t[o + 4];
+        if constexpr (PW) s += c[5 * B] * tu[mu];
+#pragma unroll
+        for (int e = 0; e < ND; ++e) s += c[(6 + e) * B] * t[XQ + e];
+        tk[o + 1] = s;
+        if constexpr (FAT) {
+            tk[o + 2] = C.alpha_a * t[o + 1] - C.inv_tau_fat * t[o + 2];
+            tk[o + 3] = C.alpha_tau1 * t[o + 1] - C.inv_tau_fat * t[o + 3];
+            tk[o + 4] = C.alpha_km * t[o + 1] - C.inv_tau_fat * t[o + 4];
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < NQ; ++i) {
+        tk[XQ + i] = t[XQD + i];
+        double s = 0.0;
+#pragma unroll
+        for (int e = 0; e < ND; ++e) s += Ws[(ODQ + i * ND + e) * B] * t[XQ + e];
+#pragma unroll
+        for (int mu = 0; mu < NM; ++mu) s += Ws[(OB + i * NM + mu) * B] * t[mu * NXM + 1];
+        if (residual) {
+#pragma unroll
+            for (int k = 0; k < NQ; ++k) s += Ws[(OMI + i * NQ + k) * B] * tu[NPW + k];
+        }
+        tk[XQD + i] = s;
+    }
+}
+
+template <int NQ, int NM, int FAM, int SCHEME>
+__global__ void __launch_bounds__(256) k_msk_tangents(const MskParams P, const MskGeom* __restrict__ GG,
+                                                      double* __restrict__ J) {
+    constexpr int NXM = msk_nxm<FAM>(), NX = NM * NXM + 2 * NQ;
+    constexpr int NUMAX = (msk_pw<FAM>() ? NM : 0) + NQ;
+    constexpr int NC = msk_ncoef<NQ, NM>();
+    constexpr int ST = SCHEME == 4 ? 4 : (SCHEME == 2 ? 2 : 1);
+    const int64_t B = P.B;
+    const int nz = P.nz;
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t b = t / nz;
+    const int col = (int)(t - b * nz);
+    if (b >= B) return;
+    const int k = blockIdx.y;
+    const MskGeom& G = *GG;
+    const int residual = P.residual;
+    const double h = P.h;
+    const double* __restrict__ Wk = P.scratch + (int64_t)k * P.Q * NC * B + b;
+    double tx[NX], tu[NUMAX];
+#pragma unroll
+    for (int r = 0; r < NX; ++r) tx[r] = r == col ? 1.0 : 0.0;
+#pragma unroll
+    for (int i = 0; i < NUMAX; ++i) tu[i] = NX + i == col ? 1.0 : 0.0;
+    for (int j = 0; j < P.m; ++j) {
+        double tacc[NX], txs[NX];
+#pragma unroll
+        for (int r = 0; r < NX; ++r) txs[r] = tx[r];
+#pragma unroll
+        for (int st = 0; st < ST; ++st) {
+            double tk[NX];
+            msk_tangent<NQ, NM, FAM>(G, residual, Wk + (int64_t)(j * ST + st) * NC * B, B, txs, tu, tk);
+            const double cst = (ST == 4 && st == 2) ? h : 0.5 * h;
+#pragma unroll
+            for (int r = 0; r < NX; ++r) {
+                if (ST == 4) {
+                    if (st == 0) tacc[r] = tk[r];
+                    else if (st < 3) tacc[r] = tacc[r] + 2.0 * tk[r];
+                }
+                if (st + 1 < ST) txs[r] = tx[r] + cst * tk[r];
+                else tx[r] = ST == 4 ? tx[r] + (h / 6.0) * (tacc[r] + tk[r]) : tx[r] + h * tk[r];
+            }
+        }
+    }
+    const int64_t jb = (int64_t)k * P.nnzk;
+#pragma unroll
+    for (int r = 0; r < NX; ++r) {
+        const int pos = G.jpos[r * kMskMaxZ + col];
+        if (pos >= 0) J[(jb + pos) * B + b] = tx[r];
+    }
+    if (col == 0) {
+#pragma unroll
+        for (int r = 0; r < NX; ++r) J[(jb + G.jneg[r]) * B + b] = -1.0;
     }
 }
 

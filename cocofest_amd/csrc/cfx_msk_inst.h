@@ -9,11 +9,6 @@ namespace cfx {
 
 constexpr int kMskBlk = 256;
 
-// Jacobian directions carried per lane: enough to keep the RK stage arrays in VGPRs.
-constexpr int msk_dirs_for(int nq, int nm, int fam) {
-    return (nm * ((fam & 1) ? 5 : 2) + 2 * nq) > 16 ? 2 : 4;
-}
-
 template <int NQ, int NM, int FAM, int SCHEME>
 void dep_t(const MskParams& P, const MskGeom& G, uint64_t* dep) {
     constexpr int NX = NM * msk_nxm<FAM>() + 2 * NQ;
@@ -27,10 +22,17 @@ void dep_t(const MskParams& P, const MskGeom& G, uint64_t* dep) {
 
 template <int NQ, int NM, int FAM, int SCHEME>
 hipError_t shoot_t(const MskParams& P, const MskGeom* G, const double* V, double* Gout, double* J, hipStream_t s) {
-    constexpr int D = msk_dirs_for(NQ, NM, FAM);
-    const int nchunk = J ? (P.nz + D - 1) / D : 1;
-    dim3 grid((unsigned)((P.B + kMskBlk - 1) / kMskBlk), (unsigned)P.N, (unsigned)nchunk);
-    hipLaunchKernelGGL((k_msk_shooting<NQ, NM, FAM, SCHEME, D>), grid, dim3(kMskBlk), 0, s, P, G, V, Gout, J);
+    const unsigned gx = (unsigned)((P.B + kMskBlk - 1) / kMskBlk);
+    if (!J) {  // g only: the value recursion without derivative directions
+        hipLaunchKernelGGL((k_msk_shooting<NQ, NM, FAM, SCHEME, 0>), dim3(gx, (unsigned)P.N), dim3(kMskBlk), 0, s, P, G,
+                           V, Gout, J);
+        return hipGetLastError();
+    }
+    // g + J_g: stage coefficients (one thread per instance and interval), then one thread per Jacobian column
+    hipLaunchKernelGGL((k_msk_stagecoef<NQ, NM, FAM, SCHEME>), dim3(gx, (unsigned)P.N), dim3(kMskBlk), 0, s, P, G, V,
+                       Gout);
+    const unsigned gt = (unsigned)((P.B * P.nz + kMskBlk - 1) / kMskBlk);
+    hipLaunchKernelGGL((k_msk_tangents<NQ, NM, FAM, SCHEME>), dim3(gt, (unsigned)P.N), dim3(kMskBlk), 0, s, P, G, J);
     return hipGetLastError();
 }
 

@@ -13,8 +13,8 @@ bool msk_supported(int nq, int nm, int fam, int scheme);
 // Structural dependency masks of the nx end states of one interval over z = (x_k, u_k) (host, Dep arithmetic).
 void msk_dep_pattern(int nq, int nm, int fam, int scheme, const MskParams& P, const MskGeom& G, uint64_t* dep);
 
-// Jacobian directions per lane of k_msk_shooting for a shape.
-int msk_dirs(int nq, int nm, int fam);
+// Per-stage Jacobian coefficients of k_msk_stagecoef (msk_ncoef in cfx_msk.h).
+inline int msk_ncoef_host(int nq, int nm) { return nm * (6 + 2 * nq) + 3 * nq * nq + nq * nm; }
 
 hipError_t launch_msk_shooting(int nq, int nm, int fam, int scheme, const MskParams& P, const MskGeom* G,
                                const double* V, double* Gout, double* J, hipStream_t s);
