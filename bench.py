@@ -258,6 +258,70 @@ def ivp_section(device):
             "batch": B, "ms_per_batched_launch": ms_batch, "integrations_per_s": B / (ms_batch * 1e-3)}
 
 
+def msk_section(device, steps=10):
+    """BASELINE.json configs[4]: arm26 biceps / triceps + Ding2007 with fatigue, 10 pulses
+    @ 10 Hz, 1 s, elbow 5 -> 90 deg, force-length / force-velocity on, qdot(end) = 0 and minimize_muscle_fatigue
+    (examples/dynamics/minimize_fatigue/pulse_duration_optimization_minimize_fatigue.py:15-55).  g + J_g
+    throughput of the MSK kernels (k_msk_stagecoef + k_msk_tangents) over a device-resident SoA batch at
+    OcpFesMsk's default transcription (RK4 x 1), and the batched interior point's wall-clock to convergence at
+    RK4 x 5 (the default is infeasible for Ding2007's tau_c)."""
+    import torch
+
+    import cocofest_amd as C
+    from cocofest_amd.solver import BatchedIpm, IpmOptions
+
+    def build(m):
+        mm = C.FesMskModel(biorbd_path=str(ROOT / "tests" / "golden" / "biomod_arm26_biceps_triceps.json"),
+                           muscles_model=[C.DingModelPulseWidthFrequencyWithFatigue(muscle_name=n, sum_stim_truncation=10)
+                                          for n in ("BIClong", "TRIlong")],
+                           stim_time=[round(0.1 * i, 1) for i in range(10)], activate_force_length_relationship=True,
+                           activate_force_velocity_relationship=True)
+        ol = C.ObjectiveList()
+        ol.add(C.ObjectiveFcn.Mayer.MINIMIZE_STATE, key="qdot", index=[0, 1], node=C.Node.END,
+               target=np.zeros((2, 1)), weight=100)
+        return C.OcpFesMsk.prepare_ocp(model=mm, final_time=1, objective={"custom": ol, "minimize_muscle_fatigue": True},
+                                       msk_info={"bound_type": "start_end", "bound_data": [[0, 5], [0, 90]]},
+                                       ode_solver=C.OdeSolver.RK4(n_integration_steps=m))
+
+    ocp = build(1)
+    B = 1 << 16
+    dev = f"cuda:{device}"
+    h = ocp.nlp(batch=B, layout="soa", device=device)
+    lo, hi = ocp.bounds_vector()
+    lo = np.where(np.isfinite(lo), lo, -2.0)
+    hi = np.minimum(np.where(np.isfinite(hi), hi, 2.0), lo + 100.0)  # forces up to 100 N, |qdot| <= 2 rad/s
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(11)
+    r = 0.2 + 0.6 * torch.rand((h.nv, B), generator=gen, dtype=torch.float64, device=dev)
+    v = (torch.as_tensor(lo, device=dev)[:, None] + torch.as_tensor(hi - lo, device=dev)[:, None] * r).contiguous()
+    g = torch.empty((h.ng, B), dtype=torch.float64, device=dev)
+    jac = torch.empty((h.nnz_jac, B), dtype=torch.float64, device=dev)
+    for _ in range(3):
+        h.eval_all(v, g=g, jac=jac)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(steps):
+        h.eval_all(v, g=g, jac=jac)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / steps
+    nbytes = 8 * (h.nv + h.ng + h.nnz_jac)
+    nv, ng, nnz = h.nv, h.ng, h.nnz_jac
+    h.close()
+    ocp5 = build(5)
+    ipm = BatchedIpm(ocp5, batch=1, device=device, options=IpmOptions(tol=1e-6, max_iter=1000))
+    res = ipm.solve()
+    ipm.close()
+    return {"workload": "cfg5: arm26 biceps/triceps + Ding2007 with fatigue, 10 pulses @ 10 Hz, 1 s, 5 -> 90 deg, "
+                        "FL/FV on, RK4 x 1 (OcpFesMsk default); one step = g + J_g of every instance",
+            "batch": B, "nv": nv, "ng": ng, "nnz_jac": nnz, "ms_per_step": ms, "instance_evals_per_s": B / (ms * 1e-3),
+            "algorithmic_GBps": nbytes * B / (ms * 1e-3) / 1e9, "bytes_per_instance": nbytes,
+            "kernels": "k_msk_stagecoef + k_msk_tangents (compute-bound: FP64 VALU, see profiles/)",
+            "convergence_rk4x5": {"wall_s": res.wall_time, "converged": int(res.converged.sum()),
+                                  "iterations": int(res.iterations.max()), "f": float(res.f[0])}}
+
+
 def main():
     args = parse()
     import torch
@@ -324,6 +388,7 @@ def main():
         ivp = ivp_section(local) if (world == 1 and not args.no_solve) else None
         col = collocation_section(local) if (world == 1 and not args.no_solve) else None
         nm = nmpc_section(local, args.nmpc_horizons) if (world == 1 and not args.no_solve and args.nmpc_horizons) else None
+        msk = msk_section(local) if (world == 1 and not args.no_solve) else None
         out = {
             "metric": METRIC,
             "value": value,
@@ -361,6 +426,7 @@ def main():
             "ivp": ivp,
             "collocation": col,
             "nmpc": nm,
+            "msk": msk,
         }
     h.close()
     if dist:

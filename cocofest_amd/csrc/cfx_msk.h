@@ -645,8 +645,8 @@ __global__ void __launch_bounds__(256) k_msk_shooting(const MskParams P, const M
 //   k_msk_stagecoef  thread = (instance, interval): the value recursion (g) and, per RK stage, those NC
 //                    coefficients, stored element-major over the batch in a scratch buffer;
 //   k_msk_tangents   thread = (instance, interval, Jacobian column): the RK recursion of one tangent column
-//                    through the stored stage Jacobians (~100 FMAs per stage); the lanes of one instance read
-//                    the same coefficient (one broadcast load), consecutive instances are contiguous.
+//                    through the stored stage Jacobians (~100 FMAs per stage); a block holds 256 consecutive
+//                    instances of one column, so coefficient loads and J stores are coalesced.
 
 template <int NQ, int NM>
 constexpr int msk_ncoef() {
@@ -870,9 +870,10 @@ __global__ void __launch_bounds__(256) k_msk_tangents(const MskParams P, const M
     constexpr int ST = SCHEME == 4 ? 4 : (SCHEME == 2 ? 2 : 1);
     const int64_t B = P.B;
     const int nz = P.nz;
-    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t b = t / nz;
-    const int col = (int)(t - b * nz);
+    // block = 256 consecutive instances x one column; the nz column blocks of an instance range are adjacent in
+    // the grid, so they run together and share the range's coefficients in L2; loads and stores are coalesced
+    const int col = (int)(blockIdx.x % (unsigned)nz);
+    const int64_t b = (int64_t)(blockIdx.x / (unsigned)nz) * blockDim.x + threadIdx.x;
     if (b >= B) return;
     const int k = blockIdx.y;
     const MskGeom& G = *GG;

@@ -31,7 +31,7 @@ hipError_t shoot_t(const MskParams& P, const MskGeom* G, const double* V, double
     // g + J_g: stage coefficients (one thread per instance and interval), then one thread per Jacobian column
     hipLaunchKernelGGL((k_msk_stagecoef<NQ, NM, FAM, SCHEME>), dim3(gx, (unsigned)P.N), dim3(kMskBlk), 0, s, P, G, V,
                        Gout);
-    const unsigned gt = (unsigned)((P.B * P.nz + kMskBlk - 1) / kMskBlk);
+    const unsigned gt = (unsigned)(((P.B + kMskBlk - 1) / kMskBlk) * P.nz);
     hipLaunchKernelGGL((k_msk_tangents<NQ, NM, FAM, SCHEME>), dim3(gt, (unsigned)P.N), dim3(kMskBlk), 0, s, P, G, J);
     return hipGetLastError();
 }
