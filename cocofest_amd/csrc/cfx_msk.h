@@ -19,6 +19,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "cfx_dual.h"
 
 namespace cfx {
@@ -302,78 +304,117 @@ MSK_HD S hill_fp(const S& nl) {
     return value(fp) > 0.0 ? fp : Num<S>::c(0.0);
 }
 
+// Promotion of a q-only quantity (SQ) to the (q, qdot) scalar (SV): identity when both are the same type, else
+// Dual<nq> -> Dual<2 nq> with zero qdot directions.
+template <class T>
+struct DualN;
+template <int D>
+struct DualN<Dual<D>> {
+    static constexpr int n = D;
+};
+template <int B, int A>
+CFX_HD Dual<B> dual_up(const Dual<A>& a) {
+    Dual<B> r = dconst<B>(a.v);
+#pragma unroll
+    for (int i = 0; i < A; ++i) r.d[i] = a.d[i];
+    return r;
+}
+template <class SV, class SQ>
+MSK_HD SV up(const SQ& a) {
+    if constexpr (std::is_same<SV, SQ>::value) {
+        return a;
+    } else {
+        return dual_up<DualN<SV>::n>(a);
+    }
+}
+template <class SV, class SQ>
+MSK_HD void up3(const SQ* a, SV* r) {
+#pragma unroll
+    for (int e = 0; e < 3; ++e) r[e] = up<SV>(a[e]);
+}
+
 // The skeleton of FesMskModel.muscle_dynamic (dynamical_model.py:133-334) for given muscle forces F: frames,
 // every muscle's length / length Jacobian / velocity and its Hill multiplier mult = FL FV (+ FP), the joint
 // torques -J_L^T F (+ residual taur, nullable) and the forward dynamics qdd.  Mv / JLv (nullable) receive the
-// values of M and J_L.
-template <int NQ, int NM, class S>
-MSK_HD void msk_skeleton(const MskGeom& G, const S* q, const S* qd, const S* F, const S* taur, S* mult, S* qdd,
+// values of M and J_L.  Quantities that depend on q only (frames, muscle geometry, the body Jacobians, M) are
+// computed in SQ, those that also depend on qdot (velocities, Hill FV, Newton-Euler, qdd) in SV: with
+// SQ = Dual<nq>, SV = Dual<2 nq> the q-only half of the work carries half the derivative directions.
+template <int NQ, int NM, class SV, class SQ>
+MSK_HD void msk_skeleton(const MskGeom& G, const SQ* q, const SV* qd, const SV* F, const SV* taur, SV* mult, SV* qdd,
                          double (*Mv)[NQ], double (*JLv)[NQ]) {
-    S R[NQ][9], o[NQ][3], z[NQ][3];
+    SQ R[NQ][9], o[NQ][3], z[NQ][3];
     msk_frames<NQ>(G, q, R, o, z);
-    S tau[NQ];
+    SV tau[NQ];
 #pragma unroll
-    for (int k = 0; k < NQ; ++k) tau[k] = taur ? taur[k] : Num<S>::c(0.0);
+    for (int k = 0; k < NQ; ++k) tau[k] = taur ? taur[k] : Num<SV>::c(0.0);
 #pragma unroll
     for (int mu = 0; mu < NM; ++mu) {
         const MskMuscleConst& C = G.mc[mu];
         // ---- geometry: muscle-tendon length and its Jacobian over the frame-crossing segments
-        S L = Num<S>::c(G.const_len[mu]), JL[NQ];
+        SQ L = Num<SQ>::c(G.const_len[mu]), JL[NQ];
 #pragma unroll
-        for (int k = 0; k < NQ; ++k) JL[k] = Num<S>::c(0.0);
+        for (int k = 0; k < NQ; ++k) JL[k] = Num<SQ>::c(0.0);
         const int ns = G.nseg[mu];
         for (int i = 0; i < ns; ++i) {
-            S P0[3], dP0[NQ][3], P1[3], dP1[NQ][3];
+            SQ P0[3], dP0[NQ][3], P1[3], dP1[NQ][3];
             msk_point<NQ>(R, o, z, G.seg_frame[mu][i][0], G.seg_pos[mu][i][0], P0, dP0);
             msk_point<NQ>(R, o, z, G.seg_frame[mu][i][1], G.seg_pos[mu][i][1], P1, dP1);
-            const S d[3] = {P1[0] - P0[0], P1[1] - P0[1], P1[2] - P0[2]};
-            const S n = msqrt(dot3(d, d));
-            const S inv = 1.0 / n;
+            const SQ d[3] = {P1[0] - P0[0], P1[1] - P0[1], P1[2] - P0[2]};
+            const SQ n = msqrt(dot3(d, d));
+            const SQ inv = 1.0 / n;
             L = L + n;
 #pragma unroll
             for (int k = 0; k < NQ; ++k) {
-                const S dd[3] = {dP1[k][0] - dP0[k][0], dP1[k][1] - dP0[k][1], dP1[k][2] - dP0[k][2]};
+                const SQ dd[3] = {dP1[k][0] - dP0[k][0], dP1[k][1] - dP0[k][1], dP1[k][2] - dP0[k][2]};
                 JL[k] = JL[k] + dot3(d, dd) * inv;
             }
         }
         // ---- Hill coefficients
-        const S nl = ((L - C.slack) * C.inv_cos_penn) * C.inv_lopt;
-        S vel = Num<S>::c(0.0);
+        const SQ nl = ((L - C.slack) * C.inv_cos_penn) * C.inv_lopt;
+        SV JLu[NQ];
+        SV vel = Num<SV>::c(0.0);
 #pragma unroll
-        for (int k = 0; k < NQ; ++k) vel = vel + JL[k] * qd[k];
-        const S fl = G.fl_on ? hill_fl(nl) : Num<S>::c(1.0);
-        const S fv = G.fv_on ? hill_fv(vel) : Num<S>::c(1.0);
-        mult[mu] = G.fp_on ? fl * fv + hill_fp(nl) : fl * fv;
+        for (int k = 0; k < NQ; ++k) {
+            JLu[k] = up<SV>(JL[k]);
+            vel = vel + JLu[k] * qd[k];
+        }
+        const SV fl = G.fl_on ? up<SV>(hill_fl(nl)) : Num<SV>::c(1.0);
+        const SV fv = G.fv_on ? hill_fv(vel) : Num<SV>::c(1.0);
+        mult[mu] = G.fp_on ? fl * fv + up<SV>(hill_fp(nl)) : fl * fv;
         // ---- joint torque -J_L^T F (dynamical_model.py:331-332)
 #pragma unroll
         for (int k = 0; k < NQ; ++k) {
-            tau[k] = tau[k] - JL[k] * F[mu];
+            tau[k] = tau[k] - JLu[k] * F[mu];
             if (JLv) JLv[mu][k] = value(JL[k]);
         }
     }
     // ---- rigid-body dynamics: h by Newton-Euler (qddot = 0), M from the body Jacobians
-    S w[3] = {Num<S>::c(0.0), Num<S>::c(0.0), Num<S>::c(0.0)};
-    S al[3] = {Num<S>::c(0.0), Num<S>::c(0.0), Num<S>::c(0.0)};
-    S acc[3] = {Num<S>::c(-G.grav[0]), Num<S>::c(-G.grav[1]), Num<S>::c(-G.grav[2])};
-    S h[NQ], M[NQ][NQ];
+    SV w[3] = {Num<SV>::c(0.0), Num<SV>::c(0.0), Num<SV>::c(0.0)};
+    SV al[3] = {Num<SV>::c(0.0), Num<SV>::c(0.0), Num<SV>::c(0.0)};
+    SV acc[3] = {Num<SV>::c(-G.grav[0]), Num<SV>::c(-G.grav[1]), Num<SV>::c(-G.grav[2])};
+    SV h[NQ];
+    SQ M[NQ][NQ];
 #pragma unroll
     for (int i = 0; i < NQ; ++i) {
-        h[i] = Num<S>::c(0.0);
+        h[i] = Num<SV>::c(0.0);
 #pragma unroll
-        for (int k = 0; k < NQ; ++k) M[i][k] = Num<S>::c(0.0);
+        for (int k = 0; k < NQ; ++k) M[i][k] = Num<SQ>::c(0.0);
     }
 #pragma unroll
     for (int j = 0; j < NQ; ++j) {
+        SV zj[3];
+        up3(z[j], zj);
         if (j > 0) {
-            const S r[3] = {o[j][0] - o[j - 1][0], o[j][1] - o[j - 1][1], o[j][2] - o[j - 1][2]};
-            S t1[3], t2[3], t3[3];
+            const SQ rq[3] = {o[j][0] - o[j - 1][0], o[j][1] - o[j - 1][1], o[j][2] - o[j - 1][2]};
+            SV r[3], t1[3], t2[3], t3[3];
+            up3(rq, r);
             cross3(al, r, t1);
             cross3(w, r, t2);
             cross3(w, t2, t3);
 #pragma unroll
             for (int e = 0; e < 3; ++e) acc[e] = acc[e] + t1[e] + t3[e];
-            const S zq[3] = {z[j][0] * qd[j], z[j][1] * qd[j], z[j][2] * qd[j]};
-            S t4[3];
+            const SV zq[3] = {zj[0] * qd[j], zj[1] * qd[j], zj[2] * qd[j]};
+            SV t4[3];
             cross3(w, zq, t4);
 #pragma unroll
             for (int e = 0; e < 3; ++e) {
@@ -382,17 +423,17 @@ MSK_HD void msk_skeleton(const MskGeom& G, const S* q, const S* qd, const S* F, 
             }
         } else {
 #pragma unroll
-            for (int e = 0; e < 3; ++e) w[e] = z[0][e] * qd[0];
+            for (int e = 0; e < 3; ++e) w[e] = zj[e] * qd[0];
         }
         if (G.mass[j] == 0.0) continue;
         // composite body of frame j
-        S rc[3], c[3];
+        SQ rc[3], c[3];
 #pragma unroll
         for (int e = 0; e < 3; ++e) {
             rc[e] = R[j][e * 3] * G.com[j][0] + R[j][e * 3 + 1] * G.com[j][1] + R[j][e * 3 + 2] * G.com[j][2];
             c[e] = o[j][e] + rc[e];
         }
-        S RI[9], Iw[9];  // Iw = R I R^T
+        SQ RI[9], Iw[9];  // Iw = R I R^T
 #pragma unroll
         for (int r = 0; r < 3; ++r)
 #pragma unroll
@@ -404,35 +445,36 @@ MSK_HD void msk_skeleton(const MskGeom& G, const S* q, const S* qd, const S* F, 
 #pragma unroll
             for (int cc = 0; cc < 3; ++cc)
                 Iw[r * 3 + cc] = RI[r * 3] * R[j][cc * 3] + RI[r * 3 + 1] * R[j][cc * 3 + 1] + RI[r * 3 + 2] * R[j][cc * 3 + 2];
-        S t1[3], t2[3], t3[3], ac[3];
-        cross3(al, rc, t1);
-        cross3(w, rc, t2);
+        SV rcu[3], t1[3], t2[3], t3[3], Fb[3], Iwu[9];
+        up3(rc, rcu);
+#pragma unroll
+        for (int e = 0; e < 9; ++e) Iwu[e] = up<SV>(Iw[e]);
+        cross3(al, rcu, t1);
+        cross3(w, rcu, t2);
         cross3(w, t2, t3);
         const double mj = G.mass[j];
-        S Fb[3];
+#pragma unroll
+        for (int e = 0; e < 3; ++e) Fb[e] = mj * (acc[e] + t1[e] + t3[e]);
+        SV Iwa[3], Iww[3], t5[3], Nb[3];
 #pragma unroll
         for (int e = 0; e < 3; ++e) {
-            ac[e] = acc[e] + t1[e] + t3[e];
-            Fb[e] = mj * ac[e];
-        }
-        S Iwa[3], Iww[3], t5[3], Nb[3];
-#pragma unroll
-        for (int e = 0; e < 3; ++e) {
-            Iwa[e] = Iw[e * 3] * al[0] + Iw[e * 3 + 1] * al[1] + Iw[e * 3 + 2] * al[2];
-            Iww[e] = Iw[e * 3] * w[0] + Iw[e * 3 + 1] * w[1] + Iw[e * 3 + 2] * w[2];
+            Iwa[e] = Iwu[e * 3] * al[0] + Iwu[e * 3 + 1] * al[1] + Iwu[e * 3 + 2] * al[2];
+            Iww[e] = Iwu[e * 3] * w[0] + Iwu[e * 3 + 1] * w[1] + Iwu[e * 3 + 2] * w[2];
         }
         cross3(w, Iww, t5);
 #pragma unroll
         for (int e = 0; e < 3; ++e) Nb[e] = Iwa[e] + t5[e];
-        S Jv[NQ][3], IJ[NQ][3];
+        SQ Jv[NQ][3], IJ[NQ][3];
 #pragma unroll
         for (int i = 0; i <= j; ++i) {
-            const S r[3] = {c[0] - o[i][0], c[1] - o[i][1], c[2] - o[i][2]};
-            S m1[3];
+            const SQ rq[3] = {c[0] - o[i][0], c[1] - o[i][1], c[2] - o[i][2]};
+            SV r[3], zi[3], m1[3];
+            up3(rq, r);
+            up3(z[i], zi);
             cross3(r, Fb, m1);
-            const S mm[3] = {m1[0] + Nb[0], m1[1] + Nb[1], m1[2] + Nb[2]};
-            h[i] = h[i] + dot3(z[i], mm);
-            cross3(z[i], r, Jv[i]);
+            const SV mm[3] = {m1[0] + Nb[0], m1[1] + Nb[1], m1[2] + Nb[2]};
+            h[i] = h[i] + dot3(zi, mm);
+            cross3(z[i], rq, Jv[i]);
 #pragma unroll
             for (int e = 0; e < 3; ++e) IJ[i][e] = Iw[e * 3] * z[i][0] + Iw[e * 3 + 1] * z[i][1] + Iw[e * 3 + 2] * z[i][2];
         }
@@ -448,37 +490,41 @@ MSK_HD void msk_skeleton(const MskGeom& G, const S* q, const S* qd, const S* F, 
             for (int k = 0; k <= i; ++k) Mv[i][k] = Mv[k][i] = value(M[i][k]);
     }
     // ---- solve M qddot = tau - h (symmetric positive definite, unrolled Cholesky)
-    S rhs[NQ];
+    SV rhs[NQ], Mu[NQ][NQ];
 #pragma unroll
-    for (int i = 0; i < NQ; ++i) rhs[i] = tau[i] - h[i];
+    for (int i = 0; i < NQ; ++i) {
+        rhs[i] = tau[i] - h[i];
+#pragma unroll
+        for (int k = 0; k <= i; ++k) Mu[i][k] = up<SV>(M[i][k]);
+    }
     if constexpr (NQ == 1) {
-        qdd[0] = rhs[0] / M[0][0];
+        qdd[0] = rhs[0] / Mu[0][0];
     } else if constexpr (NQ == 2) {
-        const S det = M[0][0] * M[1][1] - M[1][0] * M[1][0];
-        qdd[0] = (M[1][1] * rhs[0] - M[1][0] * rhs[1]) / det;
-        qdd[1] = (M[0][0] * rhs[1] - M[1][0] * rhs[0]) / det;
+        const SV det = Mu[0][0] * Mu[1][1] - Mu[1][0] * Mu[1][0];
+        qdd[0] = (Mu[1][1] * rhs[0] - Mu[1][0] * rhs[1]) / det;
+        qdd[1] = (Mu[0][0] * rhs[1] - Mu[1][0] * rhs[0]) / det;
     } else {
-        S Lc[NQ][NQ];
+        SV Lc[NQ][NQ];
 #pragma unroll
         for (int i = 0; i < NQ; ++i)
 #pragma unroll
             for (int k = 0; k <= i; ++k) {
-                S sum = M[i][k];
+                SV sum = Mu[i][k];
 #pragma unroll
                 for (int p = 0; p < k; ++p) sum = sum - Lc[i][p] * Lc[k][p];
                 Lc[i][k] = i == k ? msqrt(sum) : sum / Lc[k][k];
             }
-        S y[NQ];
+        SV y[NQ];
 #pragma unroll
         for (int i = 0; i < NQ; ++i) {
-            S sum = rhs[i];
+            SV sum = rhs[i];
 #pragma unroll
             for (int p = 0; p < i; ++p) sum = sum - Lc[i][p] * y[p];
             y[i] = sum / Lc[i][i];
         }
 #pragma unroll
         for (int i = NQ - 1; i >= 0; --i) {
-            S sum = y[i];
+            SV sum = y[i];
 #pragma unroll
             for (int p = i + 1; p < NQ; ++p) sum = sum - Lc[p][i] * qdd[p];
             qdd[i] = sum / Lc[i][i];
@@ -642,11 +688,12 @@ __global__ void __launch_bounds__(256) k_msk_shooting(const MskParams P, const M
 // RK stage's RHS Jacobian is assembled from one Dual<2 nq> pass of the skeleton over (q, qdot) — independent of
 // how many Jacobian columns are wanted — the values of B_m = -M^-1 J_L[m]^T and M^-1, and the analytic partials
 // of the muscle ODEs (ding2003.py:254-311, ding2003_with_fatigue.py:197-240, ding2007.py:172-188).
-//   k_msk_stagecoef  thread = (instance, interval): the value recursion (g) and, per RK stage, those NC
+//   k_msk_stagecoef  thread = (instance, interval): the value recursion (g) and, per RK stage (skeleton in
+//                    Dual<nq> for the q-only part, Dual<2 nq> for the velocity-dependent part), those NC
 //                    coefficients, stored element-major over the batch in a scratch buffer;
 //   k_msk_tangents   thread = (instance, interval, Jacobian column): the RK recursion of one tangent column
 //                    through the stored stage Jacobians (~100 FMAs per stage); a block holds 256 consecutive
-//                    instances of one column, so coefficient loads and J stores are coalesced.
+//                    instances of one column (coalesced loads and J stores), XCD-aware block numbering.
 
 template <int NQ, int NM>
 constexpr int msk_ncoef() {
@@ -692,10 +739,11 @@ __device__ __forceinline__ void msk_stage(const MskGeom& G, int residual, const 
     constexpr bool FAT = (FAM & 1) != 0, PW = msk_pw<FAM>();
     constexpr int NPW = PW ? NM : 0, OM = 6 + ND, ODQ = NM * OM, OB = ODQ + NQ * ND, OMI = OB + NQ * NM;
     using S = Dual<ND>;
-    S q[NQ], qd[NQ], F[NM], taur[NQ], mult[NM], qdd[NQ];
+    Dual<NQ> q[NQ];  // q-only quantities carry the nq q-directions, the rest all 2 nq (msk_skeleton)
+    S qd[NQ], F[NM], taur[NQ], mult[NM], qdd[NQ];
 #pragma unroll
     for (int k = 0; k < NQ; ++k) {
-        q[k] = dconst<ND>(xs[XQ + k]);
+        q[k] = dconst<NQ>(xs[XQ + k]);
         qd[k] = dconst<ND>(xs[XQD + k]);
         q[k].d[k] = 1.0;
         qd[k].d[NQ + k] = 1.0;
@@ -870,10 +918,13 @@ __global__ void __launch_bounds__(256) k_msk_tangents(const MskParams P, const M
     constexpr int ST = SCHEME == 4 ? 4 : (SCHEME == 2 ? 2 : 1);
     const int64_t B = P.B;
     const int nz = P.nz;
-    // block = 256 consecutive instances x one column; the nz column blocks of an instance range are adjacent in
-    // the grid, so they run together and share the range's coefficients in L2; loads and stores are coalesced
-    const int col = (int)(blockIdx.x % (unsigned)nz);
-    const int64_t b = (int64_t)(blockIdx.x / (unsigned)nz) * blockDim.x + threadIdx.x;
+    // block = 256 consecutive instances x one column.  Workgroups are dispatched round-robin over the 8 XCDs
+    // (blockIdx % 8), each with its own L2: the nz column blocks of one instance range are given ids of the same
+    // residue, so they run on one XCD, together, and read the range's coefficients from that XCD's L2.
+    const unsigned L = blockIdx.x, slot = L >> 3;
+    const int col = (int)(slot % (unsigned)nz);
+    const int64_t range = (int64_t)(slot / (unsigned)nz) * 8 + (L & 7);
+    const int64_t b = range * blockDim.x + threadIdx.x;
     if (b >= B) return;
     const int k = blockIdx.y;
     const MskGeom& G = *GG;
@@ -905,6 +956,73 @@ __global__ void __launch_bounds__(256) k_msk_tangents(const MskParams P, const M
             }
         }
     }
+    const int64_t jb = (int64_t)k * P.nnzk;
+#pragma unroll
+    for (int r = 0; r < NX; ++r) {
+        const int pos = G.jpos[r * kMskMaxZ + col];
+        if (pos >= 0) J[(jb + pos) * B + b] = tx[r];
+    }
+    if (col == 0) {
+#pragma unroll
+        for (int r = 0; r < NX; ++r) J[(jb + G.jneg[r]) * B + b] = -1.0;
+    }
+}
+
+// k_msk_tangents with the stage coefficients staged in LDS: block = 32 instances x nz columns (a wave holds two
+// columns of 32 instances, nz <= 16, <= 512 threads so the 200-odd VGPRs of a column fit), so each coefficient
+// is read from L2 once per block instead of once per column.  Per RK sub-step the block loads the ST stages'
+// coefficients of its 32 instances (ST * NC * 256 B), then every thread carries its column through them.
+constexpr int kMskLdsCols = 16;
+
+template <int NQ, int NM, int FAM, int SCHEME>
+__global__ void __launch_bounds__(32 * kMskLdsCols) k_msk_tangents_lds(const MskParams P, const MskGeom* __restrict__ GG,
+                                                                     double* __restrict__ J) {
+    constexpr int NXM = msk_nxm<FAM>(), NX = NM * NXM + 2 * NQ;
+    constexpr int NUMAX = (msk_pw<FAM>() ? NM : 0) + NQ;
+    constexpr int NC = msk_ncoef<NQ, NM>();
+    constexpr int ST = SCHEME == 4 ? 4 : (SCHEME == 2 ? 2 : 1);
+    extern __shared__ double sW[];  // [ST][NC][32]
+    const int64_t B = P.B;
+    const int nz = P.nz, lane = threadIdx.x & 31, col = threadIdx.x >> 5, nthr = 32 * nz;
+    const int64_t b0 = (int64_t)blockIdx.x * 32, b = b0 + lane;
+    const int k = blockIdx.y;
+    const MskGeom& G = *GG;
+    const int residual = P.residual;
+    const double h = P.h;
+    const double* __restrict__ Wk = P.scratch + (int64_t)k * P.Q * NC * B;
+    double tx[NX], tu[NUMAX];
+#pragma unroll
+    for (int r = 0; r < NX; ++r) tx[r] = r == col ? 1.0 : 0.0;
+#pragma unroll
+    for (int i = 0; i < NUMAX; ++i) tu[i] = NX + i == col ? 1.0 : 0.0;
+    for (int j = 0; j < P.m; ++j) {
+        __syncthreads();  // the previous sub-step's coefficients are consumed
+        for (int e = threadIdx.x; e < ST * NC * 32; e += nthr) {
+            const int l = e & 31, sc = e >> 5;  // sc = st * NC + c
+            const int64_t bb = b0 + l;
+            sW[e] = bb < B ? Wk[((int64_t)j * ST * NC + sc) * B + bb] : 0.0;
+        }
+        __syncthreads();
+        double tacc[NX], txs[NX];
+#pragma unroll
+        for (int r = 0; r < NX; ++r) txs[r] = tx[r];
+#pragma unroll
+        for (int st = 0; st < ST; ++st) {
+            double tk[NX];
+            msk_tangent<NQ, NM, FAM>(G, residual, sW + st * NC * 32 + lane, 32, txs, tu, tk);
+            const double cst = (ST == 4 && st == 2) ? h : 0.5 * h;
+#pragma unroll
+            for (int r = 0; r < NX; ++r) {
+                if (ST == 4) {
+                    if (st == 0) tacc[r] = tk[r];
+                    else if (st < 3) tacc[r] = tacc[r] + 2.0 * tk[r];
+                }
+                if (st + 1 < ST) txs[r] = tx[r] + cst * tk[r];
+                else tx[r] = ST == 4 ? tx[r] + (h / 6.0) * (tacc[r] + tk[r]) : tx[r] + h * tk[r];
+            }
+        }
+    }
+    if (b >= B) return;
     const int64_t jb = (int64_t)k * P.nnzk;
 #pragma unroll
     for (int r = 0; r < NX; ++r) {

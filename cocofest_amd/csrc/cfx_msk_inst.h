@@ -31,7 +31,14 @@ hipError_t shoot_t(const MskParams& P, const MskGeom* G, const double* V, double
     // g + J_g: stage coefficients (one thread per instance and interval), then one thread per Jacobian column
     hipLaunchKernelGGL((k_msk_stagecoef<NQ, NM, FAM, SCHEME>), dim3(gx, (unsigned)P.N), dim3(kMskBlk), 0, s, P, G, V,
                        Gout);
-    const unsigned gt = (unsigned)(((P.B + kMskBlk - 1) / kMskBlk) * P.nz);
+    if (P.nz <= kMskLdsCols) {  // coefficients through LDS, one block per 32 instances
+        constexpr int NC = msk_ncoef<NQ, NM>(), ST = SCHEME == 4 ? 4 : (SCHEME == 2 ? 2 : 1);
+        hipLaunchKernelGGL((k_msk_tangents_lds<NQ, NM, FAM, SCHEME>), dim3((unsigned)((P.B + 31) / 32), (unsigned)P.N),
+                           dim3(32 * P.nz), ST * NC * 32 * sizeof(double), s, P, G, J);
+        return hipGetLastError();
+    }
+    const int64_t ranges8 = ((P.B + kMskBlk - 1) / kMskBlk + 7) / 8 * 8;  // instance ranges, padded to 8 XCDs
+    const unsigned gt = (unsigned)(ranges8 * P.nz);
     hipLaunchKernelGGL((k_msk_tangents<NQ, NM, FAM, SCHEME>), dim3(gt, (unsigned)P.N), dim3(kMskBlk), 0, s, P, G, J);
     return hipGetLastError();
 }
