@@ -317,7 +317,7 @@ def msk_section(device, steps=10):
                         "FL/FV on, RK4 x 1 (OcpFesMsk default); one step = g + J_g of every instance",
             "batch": B, "nv": nv, "ng": ng, "nnz_jac": nnz, "ms_per_step": ms, "instance_evals_per_s": B / (ms * 1e-3),
             "algorithmic_GBps": nbytes * B / (ms * 1e-3) / 1e9, "bytes_per_instance": nbytes,
-            "kernels": "k_msk_stagecoef + k_msk_tangents (compute-bound: FP64 VALU, see profiles/)",
+            "kernels": "k_msk_stagecoef + k_msk_tangents_lds (compute-bound: FP64 VALU, see profiles/)",
             "convergence_rk4x5": {"wall_s": res.wall_time, "converged": int(res.converged.sum()),
                                   "iterations": int(res.iterations.max()), "f": float(res.f[0])}}
 
