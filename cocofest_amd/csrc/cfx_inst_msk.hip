@@ -1,8 +1,9 @@
 // cfx_inst_msk.hip — dispatch of the musculoskeletal kernels over the shapes compiled in by the
-// cfx_inst_msk_*.hip units (cfx_msk_inst.h).
+// cfx_inst_msk_s<nq><nm>.hip units (cfx_msk_inst.h).
 //
 // Shapes (n_dof, n_muscles): the reference's arm26 models (examples/msk_models/*.bioMod) reduced to serial
-// chains; arm26_biceps_triceps (2, 2) is BASELINE config 5.  Families: Ding2003 / Ding2007, with and without
+// chains — arm26_biceps_1dof (1, 1), arm26_biceps (2, 1), arm26_biceps_triceps (2, 2, BASELINE config 5),
+// arm26 (2, 6).  Families: Ding2003 / Ding2007, with and without
 // fatigue; schemes RK1 and RK4 (OcpFesMsk's default is RK4 x 1, fes_ocp_dynamics.py:168).
 #include "cfx_msk_inst.h"
 
@@ -10,7 +11,9 @@ namespace cfx {
 
 namespace {
 
-bool dispatch(MskCall& c) { return msk_dispatch_d03(c) || msk_dispatch_d07(c); }
+bool dispatch(MskCall& c) {
+    return msk_dispatch_s22(c) || msk_dispatch_s21(c) || msk_dispatch_s11(c) || msk_dispatch_s26(c);
+}
 
 MskCall make(int op, int nq, int nm, int fam, int scheme) {
     MskCall c{};

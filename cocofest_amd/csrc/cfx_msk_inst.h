@@ -87,8 +87,10 @@ bool msk_try(MskCall& c) {
 
 #define CFX_MSK_SCHEMES(NQ, NM, FAM) msk_try<NQ, NM, FAM, 1>(c) || msk_try<NQ, NM, FAM, 4>(c)
 
-// per-unit dispatchers (cfx_inst_msk_d03.hip, cfx_inst_msk_d07.hip)
-bool msk_dispatch_d03(MskCall& c);
-bool msk_dispatch_d07(MskCall& c);
+// per-shape dispatchers (cfx_inst_msk_s<nq><nm>.hip)
+bool msk_dispatch_s11(MskCall& c);
+bool msk_dispatch_s21(MskCall& c);
+bool msk_dispatch_s22(MskCall& c);
+bool msk_dispatch_s26(MskCall& c);
 
 }  // namespace cfx

@@ -20,6 +20,12 @@ CASES = {
     "d07_rk1_residual": MC.cfg5(model="ding2007", scheme="RK1", m=5, residual=True, fatigue=False),
     "d03f_rk4_nofv": MC.cfg5(model="ding2003_with_fatigue", fv=False),
     "d03_rk4_residual": MC.cfg5(model="ding2003", residual=True, fatigue=False, m=2),
+    # the other arm26 shapes of the reference's examples/msk_models
+    "biceps_1dof_d07f": MC.cfg5(biomod="arm26_biceps_1dof", muscles=("BIClong",)),
+    "biceps_2dof_d07_residual": MC.cfg5(biomod="arm26_biceps", muscles=("BIClong",), model="ding2007", fatigue=False,
+                                        residual=True),
+    "arm26_6muscles_d03_rk1": MC.cfg5(biomod="arm26", model="ding2003", fatigue=False, scheme="RK1", m=3,
+                                      muscles=("BIClong", "BICshort", "BRA", "TRIlong", "TRIlat", "TRImed")),
 }
 
 
