@@ -258,7 +258,37 @@ def ivp_section(device):
             "batch": B, "ms_per_batched_launch": ms_batch, "integrations_per_s": B / (ms_batch * 1e-3)}
 
 
-def msk_section(device, steps=10):
+def msk_cpu_baseline(ocp, budget_s):
+    """cfg-5 CPU baseline: the plain-C port of the musculoskeletal oracle (oracle/c/fes_msk.c: full segment tree,
+    Newton-Euler forward dynamics with unit accelerations, as-written calcium sum, complex-step Jacobian columns),
+    all usable host cores, on a bounded sample of the same workload (g + J_g of cfg-5 instances at RK4 x 1)."""
+    from oracle import c_msk, fes_msk as M, fes_oracle as O
+
+    threads = min(16, len(os.sched_getaffinity(0)))
+    bm = json.loads((ROOT / "tests" / "golden" / "biomod_arm26_biceps_triceps.json").read_text())
+    mus = [M.MskMuscle(model="ding2007_with_fatigue", name=n, c=O.model_constants("ding2007_with_fatigue"))
+           for n in ("BIClong", "TRIlong")]
+    pb = M.MskProblem(bm=bm, muscles=mus, rows=np.asarray(ocp.stim_rows, dtype=np.float64),
+                      n_shooting=ocp.n_shooting, final_time=1.0, scheme="RK4", m=1, fv_on=True)
+    lo, hi = ocp.bounds_vector()
+    lo = np.where(np.isfinite(lo), lo, -2.0)
+    hi = np.minimum(np.where(np.isfinite(hi), hi, 2.0), lo + 100.0)
+    chunk = 16 * threads
+    v = lo + (hi - lo) * (0.2 + 0.6 * np.random.default_rng(11).random((chunk, pb.nv)))
+    c_msk.shooting(pb, v[:threads], threads=threads)  # load
+    done, t0 = 0, time.perf_counter()
+    while True:
+        c_msk.shooting(pb, v, threads=threads)
+        done += chunk
+        el = time.perf_counter() - t0
+        if el >= budget_s:
+            break
+    return {"value": done / el, "unit": "instance-evals/s", "cores": threads, "kind": "port",
+            "sample": f"{done} cfg-5 instances (g + J_g, RK4 x 1), oracle/c/fes_msk.c, OpenMP {threads} threads, "
+                      f"{el:.1f} s"}
+
+
+def msk_section(device, steps=10, cpu_seconds=0.0):
     """BASELINE.json configs[4]: arm26 biceps / triceps + Ding2007 with fatigue, 10 pulses
     @ 10 Hz, 1 s, elbow 5 -> 90 deg, force-length / force-velocity on, qdot(end) = 0 and minimize_muscle_fatigue
     (examples/dynamics/minimize_fatigue/pulse_duration_optimization_minimize_fatigue.py:15-55).  g + J_g
@@ -284,6 +314,7 @@ def msk_section(device, steps=10):
                                        ode_solver=C.OdeSolver.RK4(n_integration_steps=m))
 
     ocp = build(1)
+    cpu = msk_cpu_baseline(ocp, cpu_seconds) if cpu_seconds > 0 else None
     B = 1 << 16
     dev = f"cuda:{device}"
     h = ocp.nlp(batch=B, layout="soa", device=device)
@@ -318,6 +349,7 @@ def msk_section(device, steps=10):
             "batch": B, "nv": nv, "ng": ng, "nnz_jac": nnz, "ms_per_step": ms, "instance_evals_per_s": B / (ms * 1e-3),
             "algorithmic_GBps": nbytes * B / (ms * 1e-3) / 1e9, "bytes_per_instance": nbytes,
             "kernels": "k_msk_stagecoef + k_msk_tangents_lds (compute-bound: FP64 VALU, see profiles/)",
+            "cpu_baseline": cpu,
             "convergence_rk4x5": {"wall_s": res.wall_time, "converged": int(res.converged.sum()),
                                   "iterations": int(res.iterations.max()), "f": float(res.f[0])}}
 
@@ -388,7 +420,7 @@ def main():
         ivp = ivp_section(local) if (world == 1 and not args.no_solve) else None
         col = collocation_section(local) if (world == 1 and not args.no_solve) else None
         nm = nmpc_section(local, args.nmpc_horizons) if (world == 1 and not args.no_solve and args.nmpc_horizons) else None
-        msk = msk_section(local) if (world == 1 and not args.no_solve) else None
+        msk = msk_section(local, cpu_seconds=args.cpu_seconds / 2) if (world == 1 and not args.no_solve) else None
         out = {
             "metric": METRIC,
             "value": value,

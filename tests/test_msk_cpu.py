@@ -212,3 +212,23 @@ def test_msk_handle_fails_loudly_without_a_gpu():
     ocp = MC.product_ocp(**MC.cfg5())
     with pytest.raises(CfxError):
         ocp.nlp(batch=4)
+
+
+@pytest.mark.parametrize("kw", [MC.cfg5(), MC.cfg5(model="ding2007", scheme="RK1", residual=True, fatigue=False),
+                                MC.cfg5(model="ding2003", biomod="arm26",
+                                        muscles=("BIClong", "BICshort", "BRA", "TRIlong", "TRIlat", "TRImed"),
+                                        fatigue=False)],
+                         ids=["cfg5", "d07_rk1_residual", "arm26_6muscles"])
+def test_c_port_matches_numpy_oracle(kw):
+    """The C port (bench.py's cfg-5 CPU baseline) reproduces the numpy oracle's g and interval Jacobians."""
+    from oracle import c_msk
+
+    pb = MC.oracle_problem(**kw)
+    v = MC.random_decision(pb, 2, seed=5)
+    g, J = c_msk.shooting(pb, v, threads=2)
+    for b in range(2):
+        gr = M.eval_g(pb, v[b])
+        np.testing.assert_allclose(g[b], gr, rtol=1e-12, atol=1e-12 * np.abs(gr).max())
+        k = pb.n_shooting - 1
+        Jr = M.continuity_jacobian(pb, v[b], k)
+        np.testing.assert_allclose(J[b, k], Jr, rtol=1e-11, atol=1e-12 * np.abs(Jr).max())
