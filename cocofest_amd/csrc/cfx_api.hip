@@ -1214,9 +1214,12 @@ static int msk_eval_h(cfx_handle* h, const double* v, const double* obj_factor, 
     if (!LAM) return rc;
     double* H = stage_out(h, S_OUT, hess, h->sz.nnz_hess, flags, &rc);
     if (!H) return rc;
+    const size_t nw = msk_hess_work_host(h->msk_nq, h->msk_nm, h->mp.nx, h->mp.nz, h->n_htasks, B, h->mp.N, h->mp.Q);
+    double* W = ensure(h, h->main[S_WORK], nw, &rc);
+    if (!W) return rc;
     CFX_HIP(h, hipMemsetAsync(H, 0, (size_t)B * h->sz.nnz_hess * sizeof(double), h->stream));
     CFX_HIP(h, launch_msk_hessian(h->msk_nq, h->msk_nm, h->msk_fam, h->scheme, h->mp, h->d_geom,
-                                  (const int16_t*)h->d_htasks, h->n_htasks, V, LAM, H, h->stream));
+                                  (const int16_t*)h->d_htasks, h->n_htasks, V, LAM, H, W, h->stream));
     if (h->n_obj)
         hipLaunchKernelGGL(k_msk_objective, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, h->stream, h->mp,
                            h->n_obj, h->d_mobj, h->d_targets, V, (double*)nullptr, (double*)nullptr, OF, H,

@@ -44,9 +44,9 @@ hipError_t launch_msk_shooting(int nq, int nm, int fam, int scheme, const MskPar
 
 hipError_t launch_msk_hessian(int nq, int nm, int fam, int scheme, const MskParams& P, const MskGeom* G,
                               const int16_t* tasks, int ntasks, const double* V, const double* LAM, double* H,
-                              hipStream_t s) {
+                              double* work, hipStream_t s) {
     MskCall c = make(2, nq, nm, fam, scheme);
-    c.P = &P, c.G = G, c.tasks = tasks, c.ntasks = ntasks, c.V = V, c.LAM = LAM, c.H = H, c.s = s;
+    c.P = &P, c.G = G, c.tasks = tasks, c.ntasks = ntasks, c.V = V, c.LAM = LAM, c.H = H, c.work = work, c.s = s;
     return dispatch(c) ? c.err : hipErrorInvalidValue;
 }
 

@@ -818,7 +818,8 @@ __device__ __forceinline__ void msk_stage(const MskGeom& G, int residual, const 
 
 template <int NQ, int NM, int FAM, int SCHEME>
 __global__ void __launch_bounds__(256) k_msk_stagecoef(const MskParams P, const MskGeom* __restrict__ GG,
-                                                       const double* __restrict__ V, double* __restrict__ Gout) {
+                                                       const double* __restrict__ V, double* __restrict__ Gout,
+                                                       double* __restrict__ XS) {
     constexpr int NXM = msk_nxm<FAM>(), NX = NM * NXM + 2 * NQ;
     constexpr int NUMAX = (msk_pw<FAM>() ? NM : 0) + NQ;
     constexpr int NC = msk_ncoef<NQ, NM>();
@@ -844,6 +845,10 @@ __global__ void __launch_bounds__(256) k_msk_stagecoef(const MskParams P, const 
 #pragma unroll
         for (int st = 0; st < ST; ++st) {
             const int slot = j * ST + st;
+            if (XS) {  // stage values for the stage-wise Hessian (k_msk_hpair)
+#pragma unroll
+                for (int r = 0; r < NX; ++r) XS[(((int64_t)k * Q + slot) * NX + r) * B + b] = xs[r];
+            }
             double f[NX];
             msk_stage<NQ, NM, FAM>(G, residual, P.cs + ((int64_t)k * Q + slot) * NM, xs, u, f,
                                    Wk + (int64_t)slot * NC * B, B);
@@ -968,23 +973,25 @@ __global__ void __launch_bounds__(256) k_msk_tangents(const MskParams P, const M
     }
 }
 
-// k_msk_tangents with the stage coefficients staged in LDS: block = 32 instances x nz columns (a wave holds two
-// columns of 32 instances, nz <= 16, <= 512 threads so the 200-odd VGPRs of a column fit), so each coefficient
-// is read from L2 once per block instead of once per column.  Per RK sub-step the block loads the ST stages'
-// coefficients of its 32 instances (ST * NC * 256 B), then every thread carries its column through them.
+// k_msk_tangents with the stage coefficients staged in LDS: block = TW instances x nz columns (nz <= 16, a wave
+// holds 64 / TW columns of TW instances), so each coefficient is read from L2 once per block instead of once per
+// column.  Per RK sub-step the block loads the ST stages' coefficients of its TW instances (ST * NC * TW * 8 B),
+// then every thread carries its column through them.  A column takes ~200 VGPRs (2 waves per SIMD).  cfg 5 at
+// B = 65536: TW = 32 0.66 ms, TW = 16 0.70 ms; 0.96 ms before the staging loads were issued all at once.
 constexpr int kMskLdsCols = 16;
+constexpr int kMskLdsLoads = 16;  // coefficient loads in flight per thread while staging
 
-template <int NQ, int NM, int FAM, int SCHEME>
+template <int NQ, int NM, int FAM, int SCHEME, int TW>
 __global__ void __launch_bounds__(32 * kMskLdsCols) k_msk_tangents_lds(const MskParams P, const MskGeom* __restrict__ GG,
                                                                      double* __restrict__ J) {
     constexpr int NXM = msk_nxm<FAM>(), NX = NM * NXM + 2 * NQ;
     constexpr int NUMAX = (msk_pw<FAM>() ? NM : 0) + NQ;
     constexpr int NC = msk_ncoef<NQ, NM>();
     constexpr int ST = SCHEME == 4 ? 4 : (SCHEME == 2 ? 2 : 1);
-    extern __shared__ double sW[];  // [ST][NC][32]
+    extern __shared__ double sW[];  // [ST][NC][TW]
     const int64_t B = P.B;
-    const int nz = P.nz, lane = threadIdx.x & 31, col = threadIdx.x >> 5, nthr = 32 * nz;
-    const int64_t b0 = (int64_t)blockIdx.x * 32, b = b0 + lane;
+    const int nz = P.nz, lane = threadIdx.x % TW, col = threadIdx.x / TW, nthr = TW * nz;
+    const int64_t b0 = (int64_t)blockIdx.x * TW, b = b0 + lane;
     const int k = blockIdx.y;
     const MskGeom& G = *GG;
     const int residual = P.residual;
@@ -997,10 +1004,19 @@ __global__ void __launch_bounds__(32 * kMskLdsCols) k_msk_tangents_lds(const Msk
     for (int i = 0; i < NUMAX; ++i) tu[i] = NX + i == col ? 1.0 : 0.0;
     for (int j = 0; j < P.m; ++j) {
         __syncthreads();  // the previous sub-step's coefficients are consumed
-        for (int e = threadIdx.x; e < ST * NC * 32; e += nthr) {
-            const int l = e & 31, sc = e >> 5;  // sc = st * NC + c
-            const int64_t bb = b0 + l;
-            sW[e] = bb < B ? Wk[((int64_t)j * ST * NC + sc) * B + bb] : 0.0;
+        // all of a thread's loads are issued before the first LDS store, so the block waits for one HBM round
+        // trip per sub-step rather than one per element (ST * NC / nz of them, 9 for cfg 5)
+        for (int e0 = threadIdx.x; e0 < ST * NC * TW; e0 += kMskLdsLoads * nthr) {
+            double tmp[kMskLdsLoads];
+#pragma unroll
+            for (int i = 0; i < kMskLdsLoads; ++i) {
+                const int e = e0 + i * nthr, l = e % TW, sc = e / TW;  // sc = st * NC + c
+                const int64_t bb = b0 + l;
+                tmp[i] = (e < ST * NC * TW && bb < B) ? Wk[((int64_t)j * ST * NC + sc) * B + bb] : 0.0;
+            }
+#pragma unroll
+            for (int i = 0; i < kMskLdsLoads; ++i)
+                if (e0 + i * nthr < ST * NC * TW) sW[e0 + i * nthr] = tmp[i];
         }
         __syncthreads();
         double tacc[NX], txs[NX];
@@ -1009,7 +1025,7 @@ __global__ void __launch_bounds__(32 * kMskLdsCols) k_msk_tangents_lds(const Msk
 #pragma unroll
         for (int st = 0; st < ST; ++st) {
             double tk[NX];
-            msk_tangent<NQ, NM, FAM>(G, residual, sW + st * NC * 32 + lane, 32, txs, tu, tk);
+            msk_tangent<NQ, NM, FAM>(G, residual, sW + st * NC * TW + lane, TW, txs, tu, tk);
             const double cst = (ST == 4 && st == 2) ? h : 0.5 * h;
 #pragma unroll
             for (int r = 0; r < NX; ++r) {
@@ -1035,62 +1051,230 @@ __global__ void __launch_bounds__(32 * kMskLdsCols) k_msk_tangents_lds(const Msk
     }
 }
 
-// ---- Lagrangian Hessian blocks: thread = (instance, interval, direction-block pair task) ------------------
-// Task (I, J), I <= J, seeds blocks I and J (BS directions each) in Jet<2 BS> slots and writes
-// sum_r lambda_{k,r} d^2 Phi_r / dz_a dz_b for a in block J, b in block I (a >= b), packed lower triangle.
-template <int NQ, int NM, int FAM, int SCHEME, int BS>
-__global__ void __launch_bounds__(256) k_msk_hessian(const MskParams P, const MskGeom* __restrict__ GG,
-                                                     const int16_t* __restrict__ tasks, const double* __restrict__ V,
-                                                     const double* __restrict__ LAM, double* __restrict__ H) {
+// ---- Lagrangian Hessian by stages ------------------------------------------------------------------------------
+// lambda^T Phi_m(z) is a composition whose only nonlinear nodes are the RK stage evaluations k_s = f(Y_s, u); every
+// other operation is linear in (z, k).  Its Hessian is therefore  sum_s mu_s^T f''(Y_s, u)[dY_s/dz, dY_s/dz],
+// mu_s = d(lambda^T Phi)/dk_s.  Five launches: stage values and coefficients (k_msk_stagecoef with XS), stage
+// tangents T_s = dY_s/dz (k_msk_htan, thread per column), stage adjoints mu_s (k_msk_hadj, backward sweep), the
+// Y-space Hessians G_s = d^2(mu_s^T f)/dY^2 (k_msk_hpair, thread per stage and coordinate pair, Jet<2>) and the
+// projection H = sum_s T_s^T G_s T_s (k_msk_hproj, thread per Hessian entry).  Every stage is its own thread, so
+// at batch 1 the latency is one Jet<2> RHS rather than m * ST of them in sequence.
+
+// explicit Butcher tableaux of RK1 / RK2 (midpoint) / RK4: weights b_s and sub-diagonal a_{s,s-1}
+template <int ST>
+__device__ __forceinline__ double rk_b(int s) {
+    return ST == 1 ? 1.0 : (ST == 2 ? (s == 1 ? 1.0 : 0.0) : ((s == 0 || s == 3) ? 1.0 / 6.0 : 1.0 / 3.0));
+}
+template <int ST>
+__device__ __forceinline__ double rk_a(int s) {
+    return (ST == 4 && s == 3) ? 1.0 : 0.5;
+}
+
+// a = (df/dx)^T w at the stage whose coefficients are Ws (the transpose of msk_tangent's state part)
+template <int NQ, int NM, int FAM>
+__device__ __forceinline__ void msk_tangent_T(const MskGeom& G, const double* __restrict__ Ws, int64_t B,
+                                              const double* w, double* a) {
+    constexpr int NXM = msk_nxm<FAM>(), XQ = NM * NXM, XQD = XQ + NQ, ND = 2 * NQ, NX = XQ + 2 * NQ;
+    constexpr bool FAT = (FAM & 1) != 0;
+    constexpr int OM = 6 + ND, ODQ = NM * OM, OB = ODQ + NQ * ND;
+#pragma unroll
+    for (int r = 0; r < NX; ++r) a[r] = 0.0;
+#pragma unroll
+    for (int mu = 0; mu < NM; ++mu) {
+        const MskMuscleConst& C = G.mc[mu];
+        const int o = mu * NXM;
+        const double* c = Ws + (int64_t)mu * OM * B;
+        const double w1 = w[o + 1];
+        a[o] += c[0] * w1 - C.inv_tauc * w[o];
+        a[o + 1] += c[B] * w1;
+        if constexpr (FAT) {
+            a[o + 1] += C.alpha_a * w[o + 2] + C.alpha_tau1 * w[o + 3] + C.alpha_km * w[o + 4];
+            a[o + 2] += c[2 * B] * w1 - C.inv_tau_fat * w[o + 2];
+            a[o + 3] += c[3 * B] * w1 - C.inv_tau_fat * w[o + 3];
+            a[o + 4] += c[4 * B] * w1 - C.inv_tau_fat * w[o + 4];
+        }
+#pragma unroll
+        for (int e = 0; e < ND; ++e) a[XQ + e] += c[(6 + e) * B] * w1;
+    }
+#pragma unroll
+    for (int i = 0; i < NQ; ++i) {
+        a[XQD + i] += w[XQ + i];
+        const double wi = w[XQD + i];
+#pragma unroll
+        for (int e = 0; e < ND; ++e) a[XQ + e] += Ws[(ODQ + i * ND + e) * B] * wi;
+#pragma unroll
+        for (int mu = 0; mu < NM; ++mu) a[mu * NXM + 1] += Ws[(OB + i * NM + mu) * B] * wi;
+    }
+}
+
+// stage input tangents TS[k][q][r][col][b] = dY_q[r]/dz[col] (thread = instance, interval, column)
+template <int NQ, int NM, int FAM, int SCHEME>
+__global__ void __launch_bounds__(256) k_msk_htan(const MskParams P, const MskGeom* __restrict__ GG,
+                                                  double* __restrict__ TS) {
+    constexpr int NXM = msk_nxm<FAM>(), NX = NM * NXM + 2 * NQ;
+    constexpr int NUMAX = (msk_pw<FAM>() ? NM : 0) + NQ;
+    constexpr int NC = msk_ncoef<NQ, NM>();
+    constexpr int ST = SCHEME == 4 ? 4 : (SCHEME == 2 ? 2 : 1);
+    const int64_t B = P.B;
+    const int nz = P.nz, Q = P.Q;
+    // flat item index, instance fastest (coalesced for large B; at batch 1 the items of a wave are distinct
+    // columns and intervals, so the launch is a few waves rather than N * nz single-lane ones)
+    const int64_t item = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (item >= B * P.N * nz) return;
+    const int64_t b = item % B, rest = item / B;
+    const int col = (int)(rest % nz), k = (int)(rest / nz);
+    const MskGeom& G = *GG;
+    const double h = P.h;
+    const double* __restrict__ Wk = P.scratch + (int64_t)k * Q * NC * B + b;
+    double tx[NX], tu[NUMAX];
+#pragma unroll
+    for (int r = 0; r < NX; ++r) tx[r] = r == col ? 1.0 : 0.0;
+#pragma unroll
+    for (int i = 0; i < NUMAX; ++i) tu[i] = NX + i == col ? 1.0 : 0.0;
+    for (int j = 0; j < P.m; ++j) {
+        double tacc[NX], txs[NX];
+#pragma unroll
+        for (int r = 0; r < NX; ++r) txs[r] = tx[r];
+#pragma unroll
+        for (int st = 0; st < ST; ++st) {
+            const int slot = j * ST + st;
+            double* __restrict__ ts = TS + (((int64_t)k * Q + slot) * NX * nz + col) * B + b;
+#pragma unroll
+            for (int r = 0; r < NX; ++r) ts[(int64_t)r * nz * B] = txs[r];
+            double tk[NX];
+            msk_tangent<NQ, NM, FAM>(G, P.residual, Wk + (int64_t)slot * NC * B, B, txs, tu, tk);
+            const double cst = (ST == 4 && st == 2) ? h : 0.5 * h;
+#pragma unroll
+            for (int r = 0; r < NX; ++r) {
+                if (ST == 4) {
+                    if (st == 0) tacc[r] = tk[r];
+                    else if (st < 3) tacc[r] = tacc[r] + 2.0 * tk[r];
+                }
+                if (st + 1 < ST) txs[r] = tx[r] + cst * tk[r];
+                else tx[r] = ST == 4 ? tx[r] + (h / 6.0) * (tacc[r] + tk[r]) : tx[r] + h * tk[r];
+            }
+        }
+    }
+}
+
+// stage adjoints MU[k][q][r][b] = d(lambda_k^T Phi)/dk_q[r] by the reverse sweep of the RK sub-steps
+template <int NQ, int NM, int FAM, int SCHEME>
+__global__ void __launch_bounds__(256) k_msk_hadj(const MskParams P, const MskGeom* __restrict__ GG,
+                                                  const double* __restrict__ LAM, double* __restrict__ MU) {
+    constexpr int NXM = msk_nxm<FAM>(), NX = NM * NXM + 2 * NQ;
+    constexpr int NC = msk_ncoef<NQ, NM>();
+    constexpr int ST = SCHEME == 4 ? 4 : (SCHEME == 2 ? 2 : 1);
+    const int64_t B = P.B;
+    const int64_t item = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (item >= B * P.N) return;
+    const int64_t b = item % B;
+    const int k = (int)(item / B), Q = P.Q;
+    const MskGeom& G = *GG;
+    const double h = P.h;
+    const double* __restrict__ Wk = P.scratch + (int64_t)k * Q * NC * B + b;
+    double xb[NX];
+#pragma unroll
+    for (int r = 0; r < NX; ++r) xb[r] = LAM[((int64_t)k * NX + r) * B + b];
+    for (int j = P.m - 1; j >= 0; --j) {
+        double xn[NX], yb[NX];
+#pragma unroll
+        for (int r = 0; r < NX; ++r) xn[r] = xb[r], yb[r] = 0.0;
+#pragma unroll
+        for (int st = ST - 1; st >= 0; --st) {
+            const int slot = j * ST + st;
+            const double wb = h * rk_b<ST>(st), wa = st + 1 < ST ? h * rk_a<ST>(st + 1) : 0.0;
+            double mu[NX];
+#pragma unroll
+            for (int r = 0; r < NX; ++r) {
+                mu[r] = wb * xb[r] + wa * yb[r];
+                MU[(((int64_t)k * Q + slot) * NX + r) * B + b] = mu[r];
+            }
+            msk_tangent_T<NQ, NM, FAM>(G, Wk + (int64_t)slot * NC * B, B, mu, yb);
+#pragma unroll
+            for (int r = 0; r < NX; ++r) xn[r] += yb[r];
+        }
+#pragma unroll
+        for (int r = 0; r < NX; ++r) xb[r] = xn[r];
+    }
+}
+
+// GQ[k][q][t][b] = d^2(mu_q^T f)/dY_I dY_J at stage q for coordinate pair t = (I, J) of (x, u)
+template <int NQ, int NM, int FAM>
+__global__ void __launch_bounds__(256) k_msk_hpair(const MskParams P, const MskGeom* __restrict__ GG,
+                                                   const int16_t* __restrict__ tasks, int ntasks,
+                                                   const double* __restrict__ V, const double* __restrict__ XS,
+                                                   const double* __restrict__ MU, double* __restrict__ GQ) {
     constexpr int NX = NM * msk_nxm<FAM>() + 2 * NQ;
     constexpr int NUMAX = (msk_pw<FAM>() ? NM : 0) + NQ;
-    constexpr int DJ = 2 * BS;
+    using S = Jet<2>;
     const int64_t B = P.B;
-    const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (b >= B) return;
-    const int k = blockIdx.y;
-    const int I = tasks[2 * blockIdx.z], Jb = tasks[2 * blockIdx.z + 1];
+    const int64_t item = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (item >= B * P.N * P.Q * ntasks) return;
+    const int64_t b = item % B, rest = item / B;
+    const int t = (int)(rest % ntasks), kq = (int)(rest / ntasks), k = kq / P.Q;
+    const int I = tasks[2 * t], J = tasks[2 * t + 1];
     const MskGeom& G = *GG;
-    const int nz = P.nz, nu = P.nu;
-    const int64_t zb = (int64_t)k * nz;
-    using S = Jet<DJ>;
-    // slot s -> global direction (block I for s < BS, block J for s >= BS; unused when I == J)
-    auto dir_of = [&](int s) { return s < BS ? I * BS + s : (I == Jb ? -1 : Jb * BS + (s - BS)); };
-    S x[NX], u[NUMAX > 0 ? NUMAX : 1];
+    const int nu = P.nu;
+    const int64_t zb = (int64_t)k * P.nz;
+    S x[NX], u[NUMAX];
 #pragma unroll
     for (int r = 0; r < NX; ++r) {
-        x[r] = jconst<DJ>(V[(zb + r) * B + b]);
-#pragma unroll
-        for (int s = 0; s < DJ; ++s) x[r].g[s] = (dir_of(s) == r) ? 1.0 : 0.0;
+        x[r] = jconst<2>(XS[((int64_t)kq * NX + r) * B + b]);
+        x[r].g[0] = r == I ? 1.0 : 0.0;
+        x[r].g[1] = (I != J && r == J) ? 1.0 : 0.0;
     }
 #pragma unroll
     for (int i = 0; i < NUMAX; ++i) {
-        u[i] = jconst<DJ>(i < nu ? V[(zb + NX + i) * B + b] : 0.0);
-#pragma unroll
-        for (int s = 0; s < DJ; ++s) u[i].g[s] = (dir_of(s) == NX + i) ? 1.0 : 0.0;
+        u[i] = jconst<2>(i < nu ? V[(zb + NX + i) * B + b] : 0.0);
+        u[i].g[0] = NX + i == I ? 1.0 : 0.0;
+        u[i].g[1] = (I != J && NX + i == J) ? 1.0 : 0.0;
     }
-    msk_interval<NQ, NM, FAM, SCHEME>(P, G, k, x, u);
-    double acc[S::H];
+    S f[NX];
+    msk_rhs<NQ, NM, FAM>(G, P.residual, P.cs + (int64_t)kq * NM, x, u, f);
+    const int hi = I == J ? 0 : 1;  // Jet<2> second-order slots: (0,0), (1,0), (1,1)
+    double acc = 0.0;
 #pragma unroll
-    for (int p = 0; p < S::H; ++p) acc[p] = 0.0;
+    for (int r = 0; r < NX; ++r) acc += MU[((int64_t)kq * NX + r) * B + b] * f[r].h[hi];
+    GQ[((int64_t)kq * ntasks + t) * B + b] = acc;
+}
+
+// H[k][(a, c)] = sum_q T_q[:, a]^T G_q T_q[:, c], (a >= c) = the pair of task p; T_q's control rows are the identity
+template <int NQ, int NM, int FAM>
+__global__ void __launch_bounds__(256) k_msk_hproj(const MskParams P, const int16_t* __restrict__ tasks, int ntasks,
+                                                   const double* __restrict__ TS, const double* __restrict__ GQ,
+                                                   double* __restrict__ H) {
+    constexpr int NX = NM * msk_nxm<FAM>() + 2 * NQ;
+    constexpr int NZ = NX + (msk_pw<FAM>() ? NM : 0) + NQ;  // upper bound of nz
+    const int64_t B = P.B;
+    const int nz = P.nz, Q = P.Q;
+    const int64_t item = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (item >= B * P.N * ntasks) return;
+    const int64_t b = item % B, rest = item / B;
+    const int p = (int)(rest % ntasks), k = (int)(rest / ntasks);
+    const int c = tasks[2 * p], a = tasks[2 * p + 1];  // tasks hold I <= J
+    double s = 0.0;
+    for (int q = 0; q < Q; ++q) {
+        const int64_t kq = (int64_t)k * Q + q;
+        double ta[NZ], tc[NZ];
 #pragma unroll
-    for (int r = 0; r < NX; ++r) {
-        const double lam = LAM[((int64_t)k * NX + r) * B + b];
-#pragma unroll
-        for (int p = 0; p < S::H; ++p) acc[p] += lam * x[r].h[p];
-    }
-    const int64_t hb = (int64_t)k * P.nhk;
-#pragma unroll
-    for (int s = 0; s < DJ; ++s)
-#pragma unroll
-        for (int t = 0; t <= s; ++t) {
-            const int a = dir_of(s), c = dir_of(t);
-            if (a < 0 || c < 0 || a >= nz || c >= nz) continue;
-            const bool same = I == Jb;
-            if (!same && !(s >= BS && t < BS)) continue;  // cross task: only (block J, block I) pairs
-            const int hi = a > c ? a : c, lo = a > c ? c : a;
-            H[(hb + hi * (hi + 1) / 2 + lo) * B + b] = acc[s * (s + 1) / 2 + t];
+        for (int I = 0; I < NX; ++I) {
+            ta[I] = TS[((kq * NX + I) * nz + a) * B + b];
+            tc[I] = TS[((kq * NX + I) * nz + c) * B + b];
         }
+#pragma unroll
+        for (int I = NX; I < NZ; ++I) ta[I] = I == a ? 1.0 : 0.0, tc[I] = I == c ? 1.0 : 0.0;
+        const double* __restrict__ gq = GQ + kq * ntasks * B + b;
+#pragma unroll
+        for (int I = 0; I < NZ; ++I)
+#pragma unroll
+            for (int J = I; J < NZ; ++J) {
+                if (J >= nz) continue;
+                const int t = I * nz - I * (I - 1) / 2 + (J - I);  // lexicographic (I <= J) task order
+                const double g = gq[(int64_t)t * B];
+                s += I == J ? g * ta[I] * tc[I] : g * (ta[I] * tc[J] + ta[J] * tc[I]);
+            }
+    }
+    H[((int64_t)k * P.nhk + a * (a + 1) / 2 + c) * B + b] = s;
 }
 
 // ---- single shooting (IVP): thread = instance, every sub-step written -------------------------------------

@@ -30,11 +30,11 @@ hipError_t shoot_t(const MskParams& P, const MskGeom* G, const double* V, double
     }
     // g + J_g: stage coefficients (one thread per instance and interval), then one thread per Jacobian column
     hipLaunchKernelGGL((k_msk_stagecoef<NQ, NM, FAM, SCHEME>), dim3(gx, (unsigned)P.N), dim3(kMskBlk), 0, s, P, G, V,
-                       Gout);
+                       Gout, (double*)nullptr);
     if (P.nz <= kMskLdsCols) {  // coefficients through LDS, one block per 32 instances
-        constexpr int NC = msk_ncoef<NQ, NM>(), ST = SCHEME == 4 ? 4 : (SCHEME == 2 ? 2 : 1);
-        hipLaunchKernelGGL((k_msk_tangents_lds<NQ, NM, FAM, SCHEME>), dim3((unsigned)((P.B + 31) / 32), (unsigned)P.N),
-                           dim3(32 * P.nz), ST * NC * 32 * sizeof(double), s, P, G, J);
+        constexpr int NC = msk_ncoef<NQ, NM>(), ST = SCHEME == 4 ? 4 : (SCHEME == 2 ? 2 : 1), TW = 32;
+        hipLaunchKernelGGL((k_msk_tangents_lds<NQ, NM, FAM, SCHEME, TW>), dim3((unsigned)((P.B + TW - 1) / TW), (unsigned)P.N),
+                           dim3(TW * P.nz), ST * NC * TW * sizeof(double), s, P, G, J);
         return hipGetLastError();
     }
     const int64_t ranges8 = ((P.B + kMskBlk - 1) / kMskBlk + 7) / 8 * 8;  // instance ranges, padded to 8 XCDs
@@ -45,9 +45,26 @@ hipError_t shoot_t(const MskParams& P, const MskGeom* G, const double* V, double
 
 template <int NQ, int NM, int FAM, int SCHEME>
 hipError_t hess_t(const MskParams& P, const MskGeom* G, const int16_t* tasks, int ntasks, const double* V,
-                  const double* LAM, double* H, hipStream_t s) {
-    dim3 grid((unsigned)((P.B + kMskBlk - 1) / kMskBlk), (unsigned)P.N, (unsigned)ntasks);
-    hipLaunchKernelGGL((k_msk_hessian<NQ, NM, FAM, SCHEME, 1>), grid, dim3(kMskBlk), 0, s, P, G, tasks, V, LAM, H);
+                  const double* LAM, double* H, double* work, hipStream_t s) {
+    // work (msk_hess_work_host doubles): stage coefficients | XS | TS | MU | GQ
+    constexpr int NX = NM * msk_nxm<FAM>() + 2 * NQ, NC = msk_ncoef<NQ, NM>();
+    const int64_t BNQ = P.B * P.N * P.Q;
+    MskParams Pw = P;
+    Pw.scratch = work;
+    double* XS = work + BNQ * NC;
+    double* TS = XS + BNQ * NX;
+    double* MU = TS + BNQ * NX * P.nz;
+    double* GQ = MU + BNQ * NX;
+    const unsigned gx = (unsigned)((P.B + kMskBlk - 1) / kMskBlk);
+    auto flat = [](int64_t items) { return dim3((unsigned)((items + kMskBlk - 1) / kMskBlk)); };
+    hipLaunchKernelGGL((k_msk_stagecoef<NQ, NM, FAM, SCHEME>), dim3(gx, (unsigned)P.N), dim3(kMskBlk), 0, s, Pw, G, V,
+                       (double*)nullptr, XS);
+    hipLaunchKernelGGL((k_msk_htan<NQ, NM, FAM, SCHEME>), flat(P.B * P.N * P.nz), dim3(kMskBlk), 0, s, Pw, G, TS);
+    hipLaunchKernelGGL((k_msk_hadj<NQ, NM, FAM, SCHEME>), flat(P.B * P.N), dim3(kMskBlk), 0, s, Pw, G, LAM, MU);
+    hipLaunchKernelGGL((k_msk_hpair<NQ, NM, FAM>), flat(P.B * P.N * P.Q * ntasks), dim3(kMskBlk), 0, s, Pw, G, tasks,
+                       ntasks, V, (const double*)XS, (const double*)MU, GQ);
+    hipLaunchKernelGGL((k_msk_hproj<NQ, NM, FAM>), flat(P.B * P.N * ntasks), dim3(kMskBlk), 0, s, Pw, tasks, ntasks,
+                       (const double*)TS, (const double*)GQ, H);
     return hipGetLastError();
 }
 
@@ -65,7 +82,7 @@ struct MskCall {
     const MskGeom* G;      // device copy (kernels) or host copy (op 0)
     uint64_t* dep;
     const double *V, *LAM, *X0, *U;
-    double *Gout, *J, *H, *TR;
+    double *Gout, *J, *H, *TR, *work;
     const int16_t* tasks;
     int ntasks;
     hipStream_t s;
@@ -78,7 +95,7 @@ bool msk_try(MskCall& c) {
     switch (c.op) {
         case 0: dep_t<NQ, NM, FAM, SC>(*c.P, *c.G, c.dep); break;
         case 1: c.err = shoot_t<NQ, NM, FAM, SC>(*c.P, c.G, c.V, c.Gout, c.J, c.s); break;
-        case 2: c.err = hess_t<NQ, NM, FAM, SC>(*c.P, c.G, c.tasks, c.ntasks, c.V, c.LAM, c.H, c.s); break;
+        case 2: c.err = hess_t<NQ, NM, FAM, SC>(*c.P, c.G, c.tasks, c.ntasks, c.V, c.LAM, c.H, c.work, c.s); break;
         case 3: c.err = ivp_t<NQ, NM, FAM, SC>(*c.P, c.G, c.X0, c.U, c.TR, c.s); break;
         default: break;
     }

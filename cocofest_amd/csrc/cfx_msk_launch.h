@@ -16,11 +16,17 @@ void msk_dep_pattern(int nq, int nm, int fam, int scheme, const MskParams& P, co
 // Per-stage Jacobian coefficients of k_msk_stagecoef (msk_ncoef in cfx_msk.h).
 inline int msk_ncoef_host(int nq, int nm) { return nm * (6 + 2 * nq) + 3 * nq * nq + nq * nm; }
 
+// Work buffer of launch_msk_hessian (doubles): stage coefficients, stage values XS, stage tangents TS, stage
+// adjoints MU and the Y-space pair Hessians GQ of every (instance, interval, stage).
+inline size_t msk_hess_work_host(int nq, int nm, int nx, int nz, int ntasks, int64_t B, int N, int Q) {
+    return (size_t)B * N * Q * ((size_t)msk_ncoef_host(nq, nm) + nx + (size_t)nx * nz + nx + ntasks);
+}
+
 hipError_t launch_msk_shooting(int nq, int nm, int fam, int scheme, const MskParams& P, const MskGeom* G,
                                const double* V, double* Gout, double* J, hipStream_t s);
 hipError_t launch_msk_hessian(int nq, int nm, int fam, int scheme, const MskParams& P, const MskGeom* G,
                               const int16_t* tasks, int ntasks, const double* V, const double* LAM, double* H,
-                              hipStream_t s);
+                              double* work, hipStream_t s);
 hipError_t launch_msk_ivp(int nq, int nm, int fam, int scheme, const MskParams& P, const MskGeom* G,
                           const double* X0, const double* U, double* TR, hipStream_t s);
 
