@@ -107,26 +107,29 @@ def _lagrangian_block_fd(pb, v, lam_k, k, rel=1e-4):
     return 0.5 * (H + H.T)
 
 
-@pytest.mark.parametrize("case", ["cfg5_d07f_rk4", "d07_rk1_residual"])
+@pytest.mark.parametrize("case", ["cfg5_d07f_rk4", "d07_rk1_residual", "d03_rk4_residual", "biceps_1dof_d07f",
+                                  "arm26_6muscles_d03_rk1"])
 def test_msk_hessian_matches_oracle(case):
+    """Stage-wise Hessian (stage tangents, adjoints swept back through m sub-steps, per-stage pair Hessians) against
+    finite differences of the oracle's complex-step gradients, on two instances of a batch of three."""
     cfg = CASES[case]
     ocp = MC.product_ocp(**cfg)
     pb = MC.oracle_problem(**cfg)
-    B = 1
+    B = 3
     V = MC.random_decision(pb, B, seed=3)
     lam = np.random.default_rng(4).normal(size=(B, pb.ng))
-    of = np.array([0.7])
+    of = np.array([0.7, 0.3, 1.1])
     h = ocp.nlp(batch=B, layout="aos")
     hv = h.eval_h(V, of, lam)
     hr, hc = h.hess_structure()
-    h0 = h.eval_h(V, np.zeros(1), np.zeros_like(lam))  # objective-only part (obj_factor 0 -> zero)
+    h0 = h.eval_h(V, np.zeros(B), np.zeros_like(lam))  # objective-only part (obj_factor 0 -> zero)
     h.close()
     assert np.all(h0 == 0.0)
     nz, nx = pb.nz, pb.nx
-    for k in (1, pb.n_shooting - 1):
-        ref = _lagrangian_block_fd(pb, V[0], lam[0, k * nx:(k + 1) * nx], k)
+    for b, k in ((0, 1), (B - 1, pb.n_shooting - 1)):
+        ref = _lagrangian_block_fd(pb, V[b], lam[b, k * nx:(k + 1) * nx], k)
         got = np.zeros((nz, nz))
-        for r, c, val in zip(hr, hc, hv[0]):
+        for r, c, val in zip(hr, hc, hv[b]):
             if k * nz <= r < (k + 1) * nz and k * nz <= c < (k + 1) * nz:
                 got[r - k * nz, c - k * nz] += val
                 if r != c:
@@ -136,7 +139,7 @@ def test_msk_hessian_matches_oracle(case):
             if o["node_first"] <= k <= o["node_last"]:
                 e = o["var_index"] + (0 if o["var_kind"] == 0 else nx)
                 w = o["weight"] * (pb.dt if o["kind"] == 0 else 1.0)
-                ref[e, e] += of[0] * 2 * w
+                ref[e, e] += of[b] * 2 * w
         scale = np.max(np.abs(ref))
         assert np.max(np.abs(got - ref)) < 2e-5 * scale, (case, k, np.max(np.abs(got - ref)) / scale)
 
