@@ -41,6 +41,7 @@ def parse():
     ap.add_argument("--batch", type=int, default=1 << 20, help="instances per GPU")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline sample budget (0: skip)")
     ap.add_argument("--no-solve", action="store_true", help="skip the wall-clock-to-convergence section")
+    ap.add_argument("--no-msk", action="store_true", help="skip the cfg-5 musculoskeletal section")
     ap.add_argument("--nmpc-horizons", type=int, default=200, help="cfg-4 NMPC horizons (0: skip)")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="process-group backend; gloo (ranks may share a GPU) rehearses the N > 1 path on one card")
@@ -288,41 +289,39 @@ def msk_cpu_baseline(ocp, budget_s):
                       f"{el:.1f} s"}
 
 
-def msk_section(device, steps=10, cpu_seconds=0.0):
+def msk_build(m):
     """BASELINE.json configs[4]: arm26 biceps / triceps + Ding2007 with fatigue, 10 pulses
     @ 10 Hz, 1 s, elbow 5 -> 90 deg, force-length / force-velocity on, qdot(end) = 0 and minimize_muscle_fatigue
-    (examples/dynamics/minimize_fatigue/pulse_duration_optimization_minimize_fatigue.py:15-55).  g + J_g
-    throughput of the MSK kernels (k_msk_stagecoef + k_msk_tangents) over a device-resident SoA batch at
-    OcpFesMsk's default transcription (RK4 x 1), and the batched interior point's wall-clock to convergence at
-    RK4 x 5 (the default is infeasible for Ding2007's tau_c)."""
+    (examples/dynamics/minimize_fatigue/pulse_duration_optimization_minimize_fatigue.py:15-55), RK4 x m."""
+    import cocofest_amd as C
+
+    mm = C.FesMskModel(biorbd_path=str(ROOT / "tests" / "golden" / "biomod_arm26_biceps_triceps.json"),
+                       muscles_model=[C.DingModelPulseWidthFrequencyWithFatigue(muscle_name=n, sum_stim_truncation=10)
+                                      for n in ("BIClong", "TRIlong")],
+                       stim_time=[round(0.1 * i, 1) for i in range(10)], activate_force_length_relationship=True,
+                       activate_force_velocity_relationship=True)
+    ol = C.ObjectiveList()
+    ol.add(C.ObjectiveFcn.Mayer.MINIMIZE_STATE, key="qdot", index=[0, 1], node=C.Node.END,
+           target=np.zeros((2, 1)), weight=100)
+    return C.OcpFesMsk.prepare_ocp(model=mm, final_time=1, objective={"custom": ol, "minimize_muscle_fatigue": True},
+                                   msk_info={"bound_type": "start_end", "bound_data": [[0, 5], [0, 90]]},
+                                   ode_solver=C.OdeSolver.RK4(n_integration_steps=m))
+
+
+def msk_throughput(local, dist, world, rank, backend, steps=10, B=1 << 16):
+    """cfg-5 g + J_g throughput at OcpFesMsk's default transcription (RK4 x 1) over a device-resident SoA batch of
+    B instances per GPU (the "multi-muscle batched Jacobian on 1 -> 8 GPUs" of configs[4]): every rank evaluates
+    its own instances (no data-path collective), timed between barriers, max over ranks."""
     import torch
 
-    import cocofest_amd as C
-    from cocofest_amd.solver import BatchedIpm, IpmOptions
-
-    def build(m):
-        mm = C.FesMskModel(biorbd_path=str(ROOT / "tests" / "golden" / "biomod_arm26_biceps_triceps.json"),
-                           muscles_model=[C.DingModelPulseWidthFrequencyWithFatigue(muscle_name=n, sum_stim_truncation=10)
-                                          for n in ("BIClong", "TRIlong")],
-                           stim_time=[round(0.1 * i, 1) for i in range(10)], activate_force_length_relationship=True,
-                           activate_force_velocity_relationship=True)
-        ol = C.ObjectiveList()
-        ol.add(C.ObjectiveFcn.Mayer.MINIMIZE_STATE, key="qdot", index=[0, 1], node=C.Node.END,
-               target=np.zeros((2, 1)), weight=100)
-        return C.OcpFesMsk.prepare_ocp(model=mm, final_time=1, objective={"custom": ol, "minimize_muscle_fatigue": True},
-                                       msk_info={"bound_type": "start_end", "bound_data": [[0, 5], [0, 90]]},
-                                       ode_solver=C.OdeSolver.RK4(n_integration_steps=m))
-
-    ocp = build(1)
-    cpu = msk_cpu_baseline(ocp, cpu_seconds) if cpu_seconds > 0 else None
-    B = 1 << 16
-    dev = f"cuda:{device}"
-    h = ocp.nlp(batch=B, layout="soa", device=device)
+    ocp = msk_build(1)
+    dev = f"cuda:{local}"
+    h = ocp.nlp(batch=B, layout="soa", device=local)
     lo, hi = ocp.bounds_vector()
     lo = np.where(np.isfinite(lo), lo, -2.0)
     hi = np.minimum(np.where(np.isfinite(hi), hi, 2.0), lo + 100.0)  # forces up to 100 N, |qdot| <= 2 rad/s
     gen = torch.Generator(device=dev)
-    gen.manual_seed(11)
+    gen.manual_seed(11 + rank)
     r = 0.2 + 0.6 * torch.rand((h.nv, B), generator=gen, dtype=torch.float64, device=dev)
     v = (torch.as_tensor(lo, device=dev)[:, None] + torch.as_tensor(hi - lo, device=dev)[:, None] * r).contiguous()
     g = torch.empty((h.ng, B), dtype=torch.float64, device=dev)
@@ -330,28 +329,51 @@ def msk_section(device, steps=10, cpu_seconds=0.0):
     for _ in range(3):
         h.eval_all(v, g=g, jac=jac)
     torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
     e0.record()
     for _ in range(steps):
         h.eval_all(v, g=g, jac=jac)
     e1.record()
     torch.cuda.synchronize()
-    ms = e0.elapsed_time(e1) / steps
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    t = torch.tensor([wall], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
+    if dist:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    wall_max = float(t.item())
     nbytes = 8 * (h.nv + h.ng + h.nnz_jac)
-    nv, ng, nnz = h.nv, h.ng, h.nnz_jac
+    out = {"workload": "cfg5: arm26 biceps/triceps + Ding2007 with fatigue, 10 pulses @ 10 Hz, 1 s, 5 -> 90 deg, "
+                       "FL/FV on, RK4 x 1 (OcpFesMsk default); one step = g + J_g of every instance",
+           "n_gpus": world, "batch_per_gpu": B, "nv": h.nv, "ng": h.ng, "nnz_jac": h.nnz_jac,
+           "ms_per_step": wall_max / steps * 1e3, "kernel_ms_per_step": e0.elapsed_time(e1) / steps,
+           "instance_evals_per_s": world * B / (wall_max / steps),
+           "algorithmic_GBps": nbytes * world * B / (wall_max / steps) / 1e9, "bytes_per_instance": nbytes,
+           "scaling": "weak", "parallelism": f"instances sharded over {world} GPU(s), no data-path collective",
+           "kernels": "k_msk_stagecoef + k_msk_tangents_lds (compute-bound: FP64 VALU, see profiles/)"}
     h.close()
-    ocp5 = build(5)
-    ipm = BatchedIpm(ocp5, batch=1, device=device, options=IpmOptions(tol=1e-6, max_iter=1000))
+    return out, ocp
+
+
+def msk_section(device, tp, ocp1, cpu_seconds=0.0):
+    """The N = 1 extras of the cfg-5 section: the C port's CPU baseline on a bounded sample of the same workload,
+    and the batched interior point's wall-clock to convergence at RK4 x 5 (the default RK4 x 1 is infeasible for
+    Ding2007's tau_c)."""
+    from cocofest_amd.solver import BatchedIpm, IpmOptions
+
+    out = dict(tp)
+    out["cpu_baseline"] = msk_cpu_baseline(ocp1, cpu_seconds) if cpu_seconds > 0 else None
+    ipm = BatchedIpm(msk_build(5), batch=1, device=device, options=IpmOptions(tol=1e-6, max_iter=1000))
     res = ipm.solve()
     ipm.close()
-    return {"workload": "cfg5: arm26 biceps/triceps + Ding2007 with fatigue, 10 pulses @ 10 Hz, 1 s, 5 -> 90 deg, "
-                        "FL/FV on, RK4 x 1 (OcpFesMsk default); one step = g + J_g of every instance",
-            "batch": B, "nv": nv, "ng": ng, "nnz_jac": nnz, "ms_per_step": ms, "instance_evals_per_s": B / (ms * 1e-3),
-            "algorithmic_GBps": nbytes * B / (ms * 1e-3) / 1e9, "bytes_per_instance": nbytes,
-            "kernels": "k_msk_stagecoef + k_msk_tangents_lds (compute-bound: FP64 VALU, see profiles/)",
-            "cpu_baseline": cpu,
-            "convergence_rk4x5": {"wall_s": res.wall_time, "converged": int(res.converged.sum()),
-                                  "iterations": int(res.iterations.max()), "f": float(res.f[0])}}
+    out["convergence_rk4x5"] = {"wall_s": res.wall_time, "converged": int(res.converged.sum()),
+                                "iterations": int(res.iterations.max()), "f": float(res.f[0])}
+    return out
 
 
 def main():
@@ -413,6 +435,8 @@ def main():
     achieved = bytes_per_instance * B / (kern_ms * 1e-3) / 1e9
     traffic = pmc_traffic()
 
+    msk_tp, msk_ocp = msk_throughput(local, dist, world, rank, args.backend) if not args.no_msk else (None, None)
+
     out = None
     if rank == 0:
         cpu = cpu_baseline(ocp, args.cpu_seconds) if (world == 1 and args.cpu_seconds > 0) else None
@@ -420,7 +444,9 @@ def main():
         ivp = ivp_section(local) if (world == 1 and not args.no_solve) else None
         col = collocation_section(local) if (world == 1 and not args.no_solve) else None
         nm = nmpc_section(local, args.nmpc_horizons) if (world == 1 and not args.no_solve and args.nmpc_horizons) else None
-        msk = msk_section(local, cpu_seconds=args.cpu_seconds / 2) if (world == 1 and not args.no_solve) else None
+        msk = msk_tp
+        if msk_tp is not None and world == 1 and not args.no_solve:
+            msk = msk_section(local, msk_tp, msk_ocp, cpu_seconds=args.cpu_seconds / 2)
         out = {
             "metric": METRIC,
             "value": value,
