@@ -102,7 +102,8 @@ bool msk_try(MskCall& c) {
     return true;
 }
 
-#define CFX_MSK_SCHEMES(NQ, NM, FAM) msk_try<NQ, NM, FAM, 1>(c) || msk_try<NQ, NM, FAM, 4>(c)
+#define CFX_MSK_SCHEMES(NQ, NM, FAM) \
+    msk_try<NQ, NM, FAM, 1>(c) || msk_try<NQ, NM, FAM, 2>(c) || msk_try<NQ, NM, FAM, 4>(c)
 
 // per-shape dispatchers (cfx_inst_msk_s<nq><nm>.hip)
 bool msk_dispatch_s11(MskCall& c);
