@@ -1238,31 +1238,33 @@ __global__ void __launch_bounds__(256) k_msk_hpair(const MskParams P, const MskG
     GQ[((int64_t)kq * ntasks + t) * B + b] = acc;
 }
 
-// H[k][(a, c)] = sum_q T_q[:, a]^T G_q T_q[:, c], (a >= c) = the pair of task p; T_q's control rows are the identity
+// H[k][:, a] = sum_q T_q^T (G_q T_q[:, a]) for the rows >= a (thread = instance, interval, column a): each thread
+// reads the stage's pair Hessians once and the tangent columns it needs, instead of one thread per entry
+// re-reading both (3.5x fewer loads).  T_q's control rows are the identity.
 template <int NQ, int NM, int FAM>
-__global__ void __launch_bounds__(256) k_msk_hproj(const MskParams P, const int16_t* __restrict__ tasks, int ntasks,
-                                                   const double* __restrict__ TS, const double* __restrict__ GQ,
-                                                   double* __restrict__ H) {
+__global__ void __launch_bounds__(256) k_msk_hproj(const MskParams P, const double* __restrict__ TS,
+                                                   const double* __restrict__ GQ, int ntasks, double* __restrict__ H) {
     constexpr int NX = NM * msk_nxm<FAM>() + 2 * NQ;
     constexpr int NZ = NX + (msk_pw<FAM>() ? NM : 0) + NQ;  // upper bound of nz
     const int64_t B = P.B;
     const int nz = P.nz, Q = P.Q;
     const int64_t item = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (item >= B * P.N * ntasks) return;
+    if (item >= B * P.N * nz) return;
     const int64_t b = item % B, rest = item / B;
-    const int p = (int)(rest % ntasks), k = (int)(rest / ntasks);
-    const int c = tasks[2 * p], a = tasks[2 * p + 1];  // tasks hold I <= J
-    double s = 0.0;
+    const int a = (int)(rest % nz), k = (int)(rest / nz);
+    double out[NZ];
+#pragma unroll
+    for (int i = 0; i < NZ; ++i) out[i] = 0.0;
     for (int q = 0; q < Q; ++q) {
         const int64_t kq = (int64_t)k * Q + q;
-        double ta[NZ], tc[NZ];
+        const double* __restrict__ ts = TS + kq * NX * nz * B + b;  // [r][col][b]
+        double ta[NZ], w[NZ];
 #pragma unroll
-        for (int I = 0; I < NX; ++I) {
-            ta[I] = TS[((kq * NX + I) * nz + a) * B + b];
-            tc[I] = TS[((kq * NX + I) * nz + c) * B + b];
-        }
+        for (int I = 0; I < NX; ++I) ta[I] = ts[((int64_t)I * nz + a) * B];
 #pragma unroll
-        for (int I = NX; I < NZ; ++I) ta[I] = I == a ? 1.0 : 0.0, tc[I] = I == c ? 1.0 : 0.0;
+        for (int I = NX; I < NZ; ++I) ta[I] = I == a ? 1.0 : 0.0;
+#pragma unroll
+        for (int I = 0; I < NZ; ++I) w[I] = 0.0;
         const double* __restrict__ gq = GQ + kq * ntasks * B + b;
 #pragma unroll
         for (int I = 0; I < NZ; ++I)
@@ -1271,10 +1273,22 @@ __global__ void __launch_bounds__(256) k_msk_hproj(const MskParams P, const int1
                 if (J >= nz) continue;
                 const int t = I * nz - I * (I - 1) / 2 + (J - I);  // lexicographic (I <= J) task order
                 const double g = gq[(int64_t)t * B];
-                s += I == J ? g * ta[I] * tc[I] : g * (ta[I] * tc[J] + ta[J] * tc[I]);
+                w[I] += g * ta[J];
+                if (J != I) w[J] += g * ta[I];
             }
+#pragma unroll
+        for (int c = 0; c < NZ; ++c) {
+            if (c < a || c >= nz) continue;
+            double sacc = c >= NX ? w[c] : 0.0;
+#pragma unroll
+            for (int I = 0; I < NX; ++I) sacc += ts[((int64_t)I * nz + c) * B] * w[I];
+            out[c] += sacc;
+        }
     }
-    H[((int64_t)k * P.nhk + a * (a + 1) / 2 + c) * B + b] = s;
+    const int64_t hb = (int64_t)k * P.nhk;
+#pragma unroll
+    for (int c = 0; c < NZ; ++c)
+        if (c >= a && c < nz) H[(hb + c * (c + 1) / 2 + a) * B + b] = out[c];
 }
 
 // ---- single shooting (IVP): thread = instance, every sub-step written -------------------------------------

@@ -63,8 +63,8 @@ hipError_t hess_t(const MskParams& P, const MskGeom* G, const int16_t* tasks, in
     hipLaunchKernelGGL((k_msk_hadj<NQ, NM, FAM, SCHEME>), flat(P.B * P.N), dim3(kMskBlk), 0, s, Pw, G, LAM, MU);
     hipLaunchKernelGGL((k_msk_hpair<NQ, NM, FAM>), flat(P.B * P.N * P.Q * ntasks), dim3(kMskBlk), 0, s, Pw, G, tasks,
                        ntasks, V, (const double*)XS, (const double*)MU, GQ);
-    hipLaunchKernelGGL((k_msk_hproj<NQ, NM, FAM>), flat(P.B * P.N * ntasks), dim3(kMskBlk), 0, s, Pw, tasks, ntasks,
-                       (const double*)TS, (const double*)GQ, H);
+    hipLaunchKernelGGL((k_msk_hproj<NQ, NM, FAM>), flat(P.B * P.N * P.nz), dim3(kMskBlk), 0, s, Pw, (const double*)TS,
+                       (const double*)GQ, ntasks, H);
     return hipGetLastError();
 }
 
