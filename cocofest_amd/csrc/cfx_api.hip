@@ -1099,13 +1099,29 @@ extern "C" int cfx_msk_create(const cfx_msk_problem* p, cfx_handle** out) {
     for (int k = 0; k < N; ++k)
         for (int e = 0; e < nz; ++e) hdiag[(size_t)k * nz + e] = k * nhk + e * (e + 1) / 2 + e;
     for (int r = 0; r < nx; ++r) hdiag[(size_t)N * nz + r] = N * nhk + r;
+    // Y-space pairs (I <= J) of the stage-wise Hessian with a structurally non-zero second derivative, as
+    // (I, J, lexicographic pair index) triples: a muscle's ODE reads only its own states, its own pulse width and
+    // (q, qdot), and q'' is linear in the muscle forces and the residual torques, so pairs of two muscles'
+    // variables vanish, and so do the residual torques' pairs with anything but q.
     std::vector<int16_t> tasks;
-    for (int I = 0; I < nz; ++I)
-        for (int J = I; J < nz; ++J) {
-            tasks.push_back((int16_t)I);
-            tasks.push_back((int16_t)J);
-        }
-    h->n_htasks = nz * (nz + 1) / 2;
+    {
+        std::vector<int> owner(nz, -1);  // muscle index, -1 skeleton, -2 residual torque
+        for (int r = 0; r < nm * nxm; ++r) owner[r] = r / nxm;
+        for (int i = 0; i < npw; ++i) owner[nx + i] = i;
+        for (int i = npw; i < nu; ++i) owner[nx + i] = -2;
+        auto is_q = [&](int e) { return e >= nm * nxm && e < nm * nxm + nq; };
+        int t = 0;
+        for (int I = 0; I < nz; ++I)
+            for (int J = I; J < nz; ++J, ++t) {
+                const int a = owner[I], c = owner[J];
+                if (a >= 0 && c >= 0 && a != c) continue;
+                if ((a == -2 && !is_q(J)) || (c == -2 && !is_q(I))) continue;
+                tasks.push_back((int16_t)I);
+                tasks.push_back((int16_t)J);
+                tasks.push_back((int16_t)t);
+            }
+    }
+    h->n_htasks = (int)(tasks.size() / 3);
 
     // ---- objective terms
     std::vector<MskObjective> mobj;
@@ -1214,7 +1230,8 @@ static int msk_eval_h(cfx_handle* h, const double* v, const double* obj_factor, 
     if (!LAM) return rc;
     double* H = stage_out(h, S_OUT, hess, h->sz.nnz_hess, flags, &rc);
     if (!H) return rc;
-    const size_t nw = msk_hess_work_host(h->msk_nq, h->msk_nm, h->mp.nx, h->mp.nz, h->n_htasks, B, h->mp.N, h->mp.Q);
+    const size_t nw = msk_hess_work_host(h->msk_nq, h->msk_nm, h->mp.nx, h->mp.nz, h->mp.nz * (h->mp.nz + 1) / 2, B,
+                                         h->mp.N, h->mp.Q);
     double* W = ensure(h, h->main[S_WORK], nw, &rc);
     if (!W) return rc;
     CFX_HIP(h, hipMemsetAsync(H, 0, (size_t)B * h->sz.nnz_hess * sizeof(double), h->stream));

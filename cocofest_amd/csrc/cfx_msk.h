@@ -1198,10 +1198,11 @@ __global__ void __launch_bounds__(256) k_msk_hadj(const MskParams P, const MskGe
     }
 }
 
-// GQ[k][q][t][b] = d^2(mu_q^T f)/dY_I dY_J at stage q for coordinate pair t = (I, J) of (x, u)
+// GQ[k][q][t][b] = d^2(mu_q^T f)/dY_I dY_J at stage q for coordinate pair t = (I, J) of (x, u); tasks holds
+// (I, J, t) triples of the structurally non-zero pairs (cfx_msk_create)
 template <int NQ, int NM, int FAM>
 __global__ void __launch_bounds__(256) k_msk_hpair(const MskParams P, const MskGeom* __restrict__ GG,
-                                                   const int16_t* __restrict__ tasks, int ntasks,
+                                                   const int16_t* __restrict__ tasks, int ntasks, int npair,
                                                    const double* __restrict__ V, const double* __restrict__ XS,
                                                    const double* __restrict__ MU, double* __restrict__ GQ) {
     constexpr int NX = NM * msk_nxm<FAM>() + 2 * NQ;
@@ -1211,8 +1212,8 @@ __global__ void __launch_bounds__(256) k_msk_hpair(const MskParams P, const MskG
     const int64_t item = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (item >= B * P.N * P.Q * ntasks) return;
     const int64_t b = item % B, rest = item / B;
-    const int t = (int)(rest % ntasks), kq = (int)(rest / ntasks), k = kq / P.Q;
-    const int I = tasks[2 * t], J = tasks[2 * t + 1];
+    const int p = (int)(rest % ntasks), kq = (int)(rest / ntasks), k = kq / P.Q;
+    const int I = tasks[3 * p], J = tasks[3 * p + 1], t = tasks[3 * p + 2];
     const MskGeom& G = *GG;
     const int nu = P.nu;
     const int64_t zb = (int64_t)k * P.nz;
@@ -1235,7 +1236,7 @@ __global__ void __launch_bounds__(256) k_msk_hpair(const MskParams P, const MskG
     double acc = 0.0;
 #pragma unroll
     for (int r = 0; r < NX; ++r) acc += MU[((int64_t)kq * NX + r) * B + b] * f[r].h[hi];
-    GQ[((int64_t)kq * ntasks + t) * B + b] = acc;
+    GQ[((int64_t)kq * npair + t) * B + b] = acc;
 }
 
 // H[k][:, a] = sum_q T_q^T (G_q T_q[:, a]) for the rows >= a (thread = instance, interval, column a): each thread

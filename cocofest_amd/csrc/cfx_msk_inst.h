@@ -55,6 +55,11 @@ hipError_t hess_t(const MskParams& P, const MskGeom* G, const int16_t* tasks, in
     double* TS = XS + BNQ * NX;
     double* MU = TS + BNQ * NX * P.nz;
     double* GQ = MU + BNQ * NX;
+    const int npair = P.nz * (P.nz + 1) / 2;  // GQ holds every pair; the structurally zero ones stay 0
+    if (ntasks < npair) {
+        const hipError_t e = hipMemsetAsync(GQ, 0, (size_t)BNQ * npair * sizeof(double), s);
+        if (e != hipSuccess) return e;
+    }
     const unsigned gx = (unsigned)((P.B + kMskBlk - 1) / kMskBlk);
     auto flat = [](int64_t items) { return dim3((unsigned)((items + kMskBlk - 1) / kMskBlk)); };
     hipLaunchKernelGGL((k_msk_stagecoef<NQ, NM, FAM, SCHEME>), dim3(gx, (unsigned)P.N), dim3(kMskBlk), 0, s, Pw, G, V,
@@ -62,9 +67,9 @@ hipError_t hess_t(const MskParams& P, const MskGeom* G, const int16_t* tasks, in
     hipLaunchKernelGGL((k_msk_htan<NQ, NM, FAM, SCHEME>), flat(P.B * P.N * P.nz), dim3(kMskBlk), 0, s, Pw, G, TS);
     hipLaunchKernelGGL((k_msk_hadj<NQ, NM, FAM, SCHEME>), flat(P.B * P.N), dim3(kMskBlk), 0, s, Pw, G, LAM, MU);
     hipLaunchKernelGGL((k_msk_hpair<NQ, NM, FAM>), flat(P.B * P.N * P.Q * ntasks), dim3(kMskBlk), 0, s, Pw, G, tasks,
-                       ntasks, V, (const double*)XS, (const double*)MU, GQ);
+                       ntasks, npair, V, (const double*)XS, (const double*)MU, GQ);
     hipLaunchKernelGGL((k_msk_hproj<NQ, NM, FAM>), flat(P.B * P.N * P.nz), dim3(kMskBlk), 0, s, Pw, (const double*)TS,
-                       (const double*)GQ, ntasks, H);
+                       (const double*)GQ, npair, H);
     return hipGetLastError();
 }
 
