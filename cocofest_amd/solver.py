@@ -40,6 +40,9 @@ class IpmOptions:
     max_backtrack: int = 30
     delta_c: float = 1e-9
     curv_min: float = 1e-8  # inertia-free test: dx^T (W + Sigma + dw) dx >= curv_min |dx|^2 (scaled space)
+    # iterative-refinement steps on each Newton solve (as Ipopt refines its KKT solves); off by default: on cfg 5 /
+    # cfg 3 it leaves the iteration counts unchanged and costs a band solve per step (scripts/ipm_refine_probe.py)
+    refine: int = 0
     verbose: bool = False
 
 
@@ -192,6 +195,17 @@ class BatchedIpm:
         self.sf = torch.clamp(100.0 / torch.clamp(gF.abs().amax(1), min=1e-300), max=1.0)
         self.sg = torch.clamp(100.0 / torch.clamp(rmax, min=1e-300), max=1.0)
 
+    def _kkt_matvec(self, hv, diag_x, jv, dx, dy):
+        """[[W + diag_x, J^T], [J, -delta_c I]] [dx; dy] from the triplets (the residual of iterative refinement)."""
+        torch = self.torch
+        wx = diag_x * dx
+        wx = wx.index_add(1, self.hrF, hv * dx[:, self.hcF])
+        wx = wx.index_add(1, self.hcF[self.hoff], (hv * dx[:, self.hrF])[:, self.hoff])
+        top = wx + self._jt_mul(jv, dy)
+        jd = torch.zeros((self.B, self.m), dtype=torch.float64, device=self.dev)
+        jd.index_add_(1, self.jrF, jv * dx[:, self.jcF])
+        return torch.cat([top, jd - self.opt.delta_c * dy], dim=1)
+
     def _kkt_band(self, hv, diag_x, jv):
         """Band storage (B, nK, ldab) of [[W + diag_x, J^T], [J, -delta_c I]] in the stage-wise order."""
         torch = self.torch
@@ -330,6 +344,8 @@ class BatchedIpm:
                 dxx = sig + dw[:, None]
                 K = self.band.factor(self._kkt_band(W, dxx, jv), self.kl, self.ku)
                 sol = self._kkt_solve(K, rhs)
+                for _ in range(opt.refine):
+                    sol = sol + self._kkt_solve(K, rhs - self._kkt_matvec(W, dxx, jv, sol[:, :nf], sol[:, nf:]))
                 dx, dy = sol[:, :nf], sol[:, nf:]
                 curv = self._quad_w(W, dx) + (dxx * dx * dx).sum(1)
                 bad = (~done) & ((curv <= opt.curv_min * (dx * dx).sum(1)) | ~torch.isfinite(curv))
