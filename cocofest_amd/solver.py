@@ -43,6 +43,8 @@ class IpmOptions:
     # iterative-refinement steps on each Newton solve (as Ipopt refines its KKT solves); off by default: on cfg 5 /
     # cfg 3 it leaves the iteration counts unchanged and costs a band solve per step (scripts/ipm_refine_probe.py)
     refine: int = 0
+    max_soc: int = 4        # second-order corrections per iteration (Ipopt max_soc)
+    kappa_soc: float = 0.99  # required infeasibility decrease between corrections (Ipopt kappa_soc)
     verbose: bool = False
 
 
@@ -379,10 +381,14 @@ class BatchedIpm:
                 ok, arm = self._filter_accept(gt, ft, xt, theta, phi, dphi, alpha, mu, theta_max, theta_min, filt)
                 ok = ok & ~accepted
                 if ls == 0:
-                    # second-order correction for rejected full steps that increased the infeasibility
+                    # second-order corrections for rejected full steps that increased the infeasibility: up to
+                    # max_soc of them while each cuts the infeasibility by kappa_soc (Ipopt's defaults 4 / 0.99)
                     soc_try = (~accepted) & (~ok) & (gt.abs().sum(1) >= theta)
-                    if bool(soc_try.any()):
-                        c_soc = alpha[:, None] * g + gt
+                    c_soc = alpha[:, None] * g + gt
+                    theta_soc = gt.abs().sum(1)
+                    for _ in range(opt.max_soc):
+                        if not bool(soc_try.any()):
+                            break
                         sol_c = self._kkt_solve(K, torch.cat([rhs_x * alpha[:, None], -c_soc], dim=1))
                         dxc = sol_c[:, :nf]
                         a_c = torch.minimum(self._max_step(sl, dxc, hasL, tau), self._max_step(su, -dxc, hasU, tau))
@@ -395,6 +401,10 @@ class BatchedIpm:
                         dx_acc = torch.where(okc[:, None], (xc - x) / alpha.clamp(min=1e-300)[:, None], dx_acc)
                         armijo_step = torch.where(okc, armc, armijo_step)
                         accepted = accepted | okc
+                        theta_c = gc.abs().sum(1)
+                        soc_try = soc_try & ~okc & (a_c >= 0.99) & (theta_c <= opt.kappa_soc * theta_soc)
+                        theta_soc = theta_c
+                        c_soc = a_c[:, None] * c_soc + gc
                 x_acc = torch.where(ok[:, None], xt, x_acc)
                 armijo_step = torch.where(ok, arm, armijo_step)
                 accepted = accepted | ok
