@@ -34,14 +34,14 @@ def starts(ocp, B, amp, cap):
     return v0
 
 
-for refine, max_soc in ((0, 1), (0, 4)):
+for refine, max_soc, relax in ((0, 4, 0.0), (0, 4, 1e-8)):
     for name, ocp, B, amp, cap in (("cfg5", ocp5, 1, 0, 10), ("cfg5_ms64", ocp5, 64, 0.1, 10),
                                    ("cfg3", ocp3, 1, 0, 10), ("cfg3_ms256", ocp3, 256, 1, 10)):
-        ipm = BatchedIpm(ocp, batch=B, options=IpmOptions(tol=1e-6, max_iter=1000, refine=refine, max_soc=max_soc))
+        ipm = BatchedIpm(ocp, batch=B, options=IpmOptions(tol=1e-6, max_iter=1000, refine=refine, max_soc=max_soc, bound_relax_factor=relax))
         v0 = starts(ocp, B, amp, cap)
         ipm.solve(v0) if name.startswith("cfg3") else None  # warm-up
         res = ipm.solve(v0)
         ipm.close()
-        print(f"refine={refine} max_soc={max_soc} {name}: wall {res.wall_time:.2f} s, converged {int(res.converged.sum())}/{B}, "
+        print(f"refine={refine} max_soc={max_soc} relax={relax} {name}: wall {res.wall_time:.2f} s, converged {int(res.converged.sum())}/{B}, "
               f"iterations median {np.median(res.iterations):.0f} max {res.iterations.max()}, "
               f"f median {np.median(res.f):.6g}", flush=True)
