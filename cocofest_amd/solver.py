@@ -63,6 +63,31 @@ class IpmResult:
     n_callbacks: dict = field(default_factory=dict)
 
 
+class _SegmentSum:
+    """Deterministic `out.index_add_(1, idx, src)` for a fixed index: the sources of each output position are
+    gathered in a fixed order from a padded (n_out_used, k_max) table and summed, so the KKT assembly (and with it
+    the iteration path) is the same on every run, which GPU atomics do not guarantee."""
+
+    def __init__(self, torch, idx, device):
+        idx = np.asarray(idx, dtype=np.int64)
+        order = np.argsort(idx, kind="stable")
+        uniq, counts = np.unique(idx, return_counts=True)
+        kmax = int(counts.max()) if counts.size else 1
+        table = np.full((uniq.size, kmax), idx.size, dtype=np.int64)  # padding points at a zero column
+        starts = np.concatenate([[0], np.cumsum(counts)[:-1]]).astype(np.int64)
+        for k in range(kmax):
+            has = counts > k
+            table[has, k] = order[starts[has] + k]
+        self.torch = torch
+        self.uniq = torch.as_tensor(uniq, device=device)
+        self.table = torch.as_tensor(table, device=device)
+
+    def add_(self, out, src):
+        srcp = self.torch.cat([src, src.new_zeros((src.shape[0], 1))], dim=1)
+        out[:, self.uniq] += srcp[:, self.table].sum(-1)
+        return out
+
+
 class BatchedIpm:
     """Interior-point solver for B instances of one FesOcp on one GPU."""
 
@@ -169,6 +194,10 @@ class BatchedIpm:
         self.idx_h, self.idx_ht = L(flat[sl[0]:sl[1]]), L(flat[sl[1]:sl[2]])
         self.idx_j, self.idx_jt = L(flat[sl[2]:sl[3]]), L(flat[sl[3]:sl[4]])
         self.idx_dx, self.idx_dy = L(flat[sl[4]:sl[5]]), L(flat[sl[5]:sl[6]])
+        self.seg_kkt = _SegmentSum(torch, flat[sl[0]:sl[5]], self.dev)  # H, H^T, J, J^T, diag_x entries
+        self.seg_jt = _SegmentSum(torch, jcF, self.dev)  # J^T y
+        self.seg_j = _SegmentSum(torch, jrF, self.dev)  # J dx
+        self.seg_h = _SegmentSum(torch, np.concatenate([hrF, hcF[off]]), self.dev)  # W dx
 
     # ---- callbacks (device, AoS); _scaled_* return the scaled problem in x~ ---------------------------------
     def _scaled_all(self, v):
@@ -190,7 +219,7 @@ class BatchedIpm:
     def _jt_mul(self, jv, y):
         """J^T y over the free variables."""
         out = self.torch.zeros((self.B, len(self.free)), dtype=self.torch.float64, device=self.dev)
-        return out.index_add_(1, self.jcF, jv * y[:, self.jrF])
+        return self.seg_jt.add_(out, jv * y[:, self.jrF])
 
     def _quad_w(self, hv, dx):
         """dx^T W dx from the lower-triangle triplets."""
@@ -210,23 +239,17 @@ class BatchedIpm:
     def _kkt_matvec(self, hv, diag_x, jv, dx, dy):
         """[[W + diag_x, J^T], [J, -delta_c I]] [dx; dy] from the triplets (the residual of iterative refinement)."""
         torch = self.torch
-        wx = diag_x * dx
-        wx = wx.index_add(1, self.hrF, hv * dx[:, self.hcF])
-        wx = wx.index_add(1, self.hcF[self.hoff], (hv * dx[:, self.hrF])[:, self.hoff])
+        wx = self.seg_h.add_(diag_x * dx, torch.cat([hv * dx[:, self.hcF], (hv * dx[:, self.hrF])[:, self.hoff]], 1))
         top = wx + self._jt_mul(jv, dy)
-        jd = torch.zeros((self.B, self.m), dtype=torch.float64, device=self.dev)
-        jd.index_add_(1, self.jrF, jv * dx[:, self.jcF])
+        jd = self.seg_j.add_(torch.zeros((self.B, self.m), dtype=torch.float64, device=self.dev),
+                             jv * dx[:, self.jcF])
         return torch.cat([top, jd - self.opt.delta_c * dy], dim=1)
 
     def _kkt_band(self, hv, diag_x, jv):
         """Band storage (B, nK, ldab) of [[W + diag_x, J^T], [J, -delta_c I]] in the stage-wise order."""
         torch = self.torch
         ab = torch.zeros((self.B, self.nK * self.ldab), dtype=torch.float64, device=self.dev)
-        ab.index_add_(1, self.idx_h, hv)
-        ab.index_add_(1, self.idx_ht, hv[:, self.hoff])
-        ab.index_add_(1, self.idx_j, jv)
-        ab.index_add_(1, self.idx_jt, jv)
-        ab.index_add_(1, self.idx_dx, diag_x)
+        self.seg_kkt.add_(ab, torch.cat([hv, hv[:, self.hoff], jv, jv, diag_x], dim=1))
         ab[:, self.idx_dy] -= self.opt.delta_c
         self.calls["kkt_factor"] += 1
         return ab.view(self.B, self.nK, self.ldab)

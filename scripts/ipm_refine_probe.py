@@ -34,7 +34,7 @@ def starts(ocp, B, amp, cap):
     return v0
 
 
-for refine, max_soc, relax in ((0, 4, 0.0), (0, 4, 1e-8)):
+for refine, max_soc, relax in ((0, 4, 0.0), (0, 4, 0.0)):  # twice: the solve is deterministic
     for name, ocp, B, amp, cap in (("cfg5", ocp5, 1, 0, 10), ("cfg5_ms64", ocp5, 64, 0.1, 10),
                                    ("cfg3", ocp3, 1, 0, 10), ("cfg3_ms256", ocp3, 256, 1, 10)):
         ipm = BatchedIpm(ocp, batch=B, options=IpmOptions(tol=1e-6, max_iter=1000, refine=refine, max_soc=max_soc, bound_relax_factor=relax))
