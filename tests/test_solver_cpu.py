@@ -108,3 +108,21 @@ def test_interior_point_matches_an_independent_nlp_solver(name):
     scale = np.maximum(np.abs(ref), 1e-3 * np.abs(ref).max())
     scale = np.where(np.abs(ref) < 1e-2, np.abs(ref) + 1e-6, scale)  # pulse widths ~1e-4 s
     assert np.max(np.abs(res.v[0] - ref) / scale) < 1e-6
+
+
+def test_segment_sum_matches_index_add():
+    """The KKT assembly's fixed gather-sum (no atomics) adds every source into its position like index_add_,
+    duplicates included, and is bitwise reproducible."""
+    import torch
+
+    from cocofest_amd.solver import _SegmentSum
+
+    rng = np.random.default_rng(0)
+    idx = rng.integers(0, 40, 300)
+    src = torch.as_tensor(rng.standard_normal((5, 300)))
+    seg = _SegmentSum(torch, idx, torch.device("cpu"))
+    got = seg.add_(torch.ones((5, 50), dtype=torch.float64), src)
+    ref = torch.ones((5, 50), dtype=torch.float64).index_add_(1, torch.as_tensor(idx), src)
+    torch.testing.assert_close(got, ref, rtol=1e-13, atol=1e-13)
+    again = seg.add_(torch.ones((5, 50), dtype=torch.float64), src)
+    assert torch.equal(got, again)
