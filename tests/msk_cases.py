@@ -36,7 +36,8 @@ def cfg5(**kw):
     return d
 
 
-def product_ocp(model, biomod, muscles, scheme, m, fv, residual, fatigue, qdot_end, truncation, bound=(5, 90)):
+def product_ocp(model, biomod, muscles, scheme, m, fv, residual, fatigue, qdot_end, truncation, bound=(5, 90),
+                passive=False):
     import cocofest_amd as C
 
     cls = getattr(C, FAMILY[model])
@@ -58,16 +59,20 @@ def product_ocp(model, biomod, muscles, scheme, m, fv, residual, fatigue, qdot_e
     nq = mm.nb_q
     info = {"bound_type": "start_end", "bound_data": [[0] * (nq - 1) + [bound[0]], [0] * (nq - 1) + [bound[1]]],
             "with_residual_torque": residual}
-    return C.OcpFesMsk.prepare_ocp(model=mm, final_time=1, objective=obj, msk_info=info, ode_solver=solver)
+    ocp = C.OcpFesMsk.prepare_ocp(model=mm, final_time=1, objective=obj, msk_info=info, ode_solver=solver)
+    if passive:  # OcpFesMsk drops the flag as the reference does; set it back to exercise the kernels' FP term
+        ocp.model.activate_passive_force_relationship = True
+    return ocp
 
 
-def oracle_problem(model, biomod, muscles, scheme, m, fv, residual, fatigue, qdot_end, truncation, bound=(5, 90)):
+def oracle_problem(model, biomod, muscles, scheme, m, fv, residual, fatigue, qdot_end, truncation, bound=(5, 90),
+                   passive=False):
     bm = json.loads(pathlib.Path(biomod_path(biomod)).read_text())
     n = O.prepare_n_shooting(STIMS, 1)
     tab = O.stim_table(STIMS, n, 1, truncation)
     mus = [M.MskMuscle(model=model, name=nm, c=O.model_constants(model)) for nm in muscles]
     pb = M.MskProblem(bm=bm, muscles=mus, rows=tab.rows, n_shooting=n, final_time=1.0, scheme=scheme, m=m, fv_on=fv,
-                      fp_on=False, residual=residual)
+                      fp_on=passive, residual=residual)
     nq, nxm = pb.nq, pb.nxm
     if qdot_end:
         for j in range(nq):

@@ -21,6 +21,7 @@ CASES = {
     "d03f_rk4_nofv": MC.cfg5(model="ding2003_with_fatigue", fv=False),
     "d03_rk4_residual": MC.cfg5(model="ding2003", residual=True, fatigue=False, m=2),
     "d07f_rk2": MC.cfg5(scheme="RK2", m=3),
+    "d07f_passive": MC.cfg5(passive=True),
     # the other arm26 shapes of the reference's examples/msk_models
     "biceps_1dof_d07f": MC.cfg5(biomod="arm26_biceps_1dof", muscles=("BIClong",)),
     "biceps_2dof_d07_residual": MC.cfg5(biomod="arm26_biceps", muscles=("BIClong",), model="ding2007", fatigue=False,
@@ -108,7 +109,7 @@ def _lagrangian_block_fd(pb, v, lam_k, k, rel=1e-4):
     return 0.5 * (H + H.T)
 
 
-@pytest.mark.parametrize("case", ["cfg5_d07f_rk4", "d07_rk1_residual", "d03_rk4_residual", "d07f_rk2",
+@pytest.mark.parametrize("case", ["cfg5_d07f_rk4", "d07_rk1_residual", "d03_rk4_residual", "d07f_rk2", "d07f_passive",
                                   "biceps_1dof_d07f", "arm26_6muscles_d03_rk1"])
 def test_msk_hessian_matches_oracle(case):
     """Stage-wise Hessian (stage tangents, adjoints swept back through m sub-steps, per-stage pair Hessians) against
