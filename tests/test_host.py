@@ -41,6 +41,72 @@ def test_create_without_device_fails_loudly():
     assert exc.value.code == _cfx.ENODEV
 
 
+@pytest.mark.parametrize("field, value, code, msg", [
+    ("abi_version", 99, "EINVAL", "ABI version mismatch"),
+    ("model", 6, "EINVAL", "unknown model"),
+    ("model", -1, "EINVAL", "unknown model"),
+    ("scheme", 3, "EUNSUPPORTED", "scheme must be"),
+    ("n_steps", 0, "EINVAL", "must be positive"),
+    ("n_shooting", 0, "EINVAL", "must be positive"),
+    ("batch", 0, "EINVAL", "must be positive"),
+    ("final_time", 0.0, "EINVAL", "must be positive"),
+    ("truncation", 0, "EUNSUPPORTED", "truncation must be in [1, 32]"),
+    ("truncation", 33, "EUNSUPPORTED", "truncation must be in [1, 32]"),
+    ("layout", 7, "EINVAL", "unknown layout"),
+    ("stim_rows", None, "EINVAL", "stim_rows is NULL"),
+    ("n_params", 2, "EINVAL", "intensity parameters need a Hmed2018 model"),
+])
+def test_create_rejects_bad_problem_before_touching_the_device(field, value, code, msg):
+    """cfx_create validates the problem before any HIP call (cfx_api.hip:411-434), so every rejection is
+    reachable without a GPU; the message is reported through cfx_last_error(NULL)."""
+    import ctypes as C
+
+    from cocofest_amd import _cfx
+
+    lib = _cfx.load_library()
+    rows = np.zeros(3)
+    pb = _cfx.Problem()
+    pb.abi_version, pb.model, pb.scheme, pb.n_steps = _cfx.ABI_VERSION, 0, 1, 1
+    pb.n_shooting, pb.truncation, pb.layout, pb.batch, pb.final_time = 2, 1, _cfx.LAYOUT_SOA, 1, 1.0
+    pb.stim_rows = rows.ctypes.data_as(C.POINTER(C.c_double))
+    setattr(pb, field, value)
+    h = C.c_void_p()
+    assert lib.cfx_create(C.byref(pb), C.byref(h)) == getattr(_cfx, code)
+    assert not h.value
+    assert msg in lib.cfx_last_error(None).decode()
+
+
+def test_tiled_layout_and_collocation_limits_are_rejected():
+    import ctypes as C
+
+    from cocofest_amd import _cfx
+
+    lib = _cfx.load_library()
+    rows = np.zeros(3)
+
+    def create(**kw):
+        pb = _cfx.Problem()
+        pb.abi_version, pb.model, pb.scheme, pb.n_steps = _cfx.ABI_VERSION, 0, 1, 1
+        pb.n_shooting, pb.truncation, pb.layout, pb.batch, pb.final_time = 2, 1, _cfx.LAYOUT_SOA, 64, 1.0
+        pb.stim_rows = rows.ctypes.data_as(C.POINTER(C.c_double))
+        for k, v in kw.items():
+            setattr(pb, k, v)
+        return lib.cfx_create(C.byref(pb), C.byref(C.c_void_p())), lib.cfx_last_error(None).decode()
+
+    rc, msg = create(layout=_cfx.LAYOUT_TILED64, batch=65)
+    assert rc == _cfx.EUNSUPPORTED and "batch % 64 == 0" in msg
+    rc, msg = create(layout=_cfx.LAYOUT_TILED64, scheme=16, n_steps=4)  # CFX_COLLOCATION_LEGENDRE
+    assert rc == _cfx.EUNSUPPORTED and "shooting transcription" in msg
+    rc, msg = create(scheme=17, n_steps=10)  # CFX_COLLOCATION_RADAU, degree above 9
+    assert rc == _cfx.EUNSUPPORTED and "degree" in msg
+    # NULL arguments: no handle and no problem are plain EINVAL, not a crash
+    assert lib.cfx_create(None, C.byref(C.c_void_p())) == _cfx.EINVAL
+    assert lib.cfx_get_sizes(None, C.byref(_cfx.Sizes())) == _cfx.EINVAL
+    assert lib.cfx_set_stream(None, None) == _cfx.EINVAL
+    assert lib.cfx_band_lu_solve(4, 1, 1, 1, None, None, 0, None, None) == _cfx.EINVAL
+    assert "nrhs" in lib.cfx_last_error(None).decode()
+
+
 def test_missing_library_is_an_error(tmp_path):
     from cocofest_amd import CfxError
     from cocofest_amd import _cfx
