@@ -107,6 +107,34 @@ def test_tiled_layout_and_collocation_limits_are_rejected():
     assert "nrhs" in lib.cfx_last_error(None).decode()
 
 
+@pytest.mark.parametrize("field, value, code, msg", [
+    ("abi_version", 99, "EINVAL", "ABI version mismatch"),
+    ("scheme", 16, "EUNSUPPORTED", "scheme must be CFX_RK1, CFX_RK2 or CFX_RK4"),
+    ("n_shooting", 0, "EINVAL", "must be positive"),
+    ("final_time", -1.0, "EINVAL", "must be positive"),
+    ("truncation", 65, "EINVAL", "truncation must be in [1, 64]"),
+    ("layout", 2, "EUNSUPPORTED", "layout must be CFX_LAYOUT_AOS or CFX_LAYOUT_SOA"),
+    (None, None, "EINVAL", "NULL array"),  # a valid header whose geometry arrays are missing
+])
+def test_msk_create_rejects_bad_problem_before_touching_the_device(field, value, code, msg):
+    """cfx_msk_create's header checks (cfx_api.hip:915-928) run before any HIP call."""
+    import ctypes as C
+
+    from cocofest_amd import _cfx
+
+    lib = _cfx.load_library()
+    pb = _cfx.MskProblem()
+    pb.abi_version, pb.scheme, pb.n_steps, pb.n_shooting = _cfx.ABI_VERSION, 4, 1, 2
+    pb.truncation, pb.layout, pb.batch, pb.final_time = 10, _cfx.LAYOUT_SOA, 1, 1.0
+    if field is not None:
+        setattr(pb, field, value)
+    h = C.c_void_p()
+    assert lib.cfx_msk_create(C.byref(pb), C.byref(h)) == getattr(_cfx, code)
+    assert not h.value
+    assert msg in lib.cfx_last_error(None).decode()
+    assert lib.cfx_msk_create(None, C.byref(h)) == _cfx.EINVAL
+
+
 def test_missing_library_is_an_error(tmp_path):
     from cocofest_amd import CfxError
     from cocofest_amd import _cfx
