@@ -146,6 +146,15 @@ def load_library(path: str | os.PathLike | None = None):
     return lib
 
 
+def _is_tensor(a):
+    """True for a torch.Tensor (torch imported lazily: host-only callers never load it)."""
+    if type(a).__module__.split(".")[0] != "torch":
+        return False
+    import torch
+
+    return isinstance(a, torch.Tensor)
+
+
 def _ptr(a):
     """Address of a numpy array / torch tensor (None -> NULL)."""
     if a is None:
@@ -199,7 +208,9 @@ def band_lu_solve(ab, ipiv, kl: int, ku: int, rhs):
         raise CfxError(rc, lib.cfx_last_error(None).decode())
 
 
-def _objective_array(objectives, keep):
+def _objective_array(objectives, keep, n_shooting):
+    """ctypes array of objective terms; a term's target array must hold one value per node (n_shooting + 1):
+    libcfx reads exactly that many."""
     objs = (Objective * max(1, len(objectives)))()
     for i, o in enumerate(objectives):
         objs[i].kind = o["kind"]
@@ -209,7 +220,10 @@ def _objective_array(objectives, keep):
         objs[i].node_last = o["node_last"]
         objs[i].weight = o["weight"]
         if o.get("target") is not None:
-            t = np.ascontiguousarray(o["target"], dtype=np.float64)
+            t = np.ascontiguousarray(o["target"], dtype=np.float64).reshape(-1)
+            if t.size != n_shooting + 1:
+                raise CfxError(EINVAL, f"objective term {i}: target has {t.size} values, expected n_shooting + 1 = "
+                                       f"{n_shooting + 1}")
             keep.append(t)
             objs[i].target = t.ctypes.data_as(_D)
         objs[i].target_value = float(o.get("target_value", 0.0))
@@ -252,7 +266,7 @@ class Handle:
         for name, _ in Constants._fields_:
             setattr(cst, name, float(constants.get(name, 0.0)))
         pb.constants = cst
-        objs = _objective_array(objectives, self._keep)
+        objs = _objective_array(objectives, self._keep, n_shooting)
         pb.n_objectives = len(objectives)
         pb.objectives = objs
         pb.device = device
@@ -302,15 +316,44 @@ class Handle:
         return r, c
 
     # ---- evaluation ----
-    @staticmethod
-    def _flags(*arrays):
-        dev = [a for a in arrays if a is not None and not isinstance(a, np.ndarray)]
-        if dev and len(dev) != len([a for a in arrays if a is not None]):
+    def _buffers(self, *slots):
+        """Check every buffer of one call against its slot before libcfx sees it; return (buffers, flags).
+
+        ``slots``: (name, buffer or None, per-instance length, is_output).  libcfx reads / writes exactly
+        batch * length doubles per buffer, so a wrong size, dtype or stride would be an out-of-bounds host
+        access, and a CPU tensor sent as a device pointer a GPU fault: all of these raise ``CfxError``.
+        Host inputs may be any array-like (converted to C-contiguous float64); host outputs must already be
+        C-contiguous float64 numpy arrays (results are written in place).  Device buffers must be contiguous
+        float64 CUDA tensors on the handle's device."""
+        out, kinds = [], []
+        for name, a, n, is_out in slots:
+            if a is None:
+                out.append(None)
+                continue
+            want = self.batch * n
+            if _is_tensor(a):
+                if not a.is_cuda:
+                    raise CfxError(EINVAL, f"{name}: CPU tensor; pass a numpy array (host) or a CUDA tensor (device)")
+                if a.device.index != self.device:
+                    raise CfxError(EINVAL, f"{name}: tensor on cuda:{a.device.index}, handle on cuda:{self.device}")
+                if str(a.dtype) != "torch.float64" or not a.is_contiguous():
+                    raise CfxError(EINVAL, f"{name}: device buffers must be contiguous float64 tensors")
+                if a.numel() != want:
+                    raise CfxError(EINVAL, f"{name}: {a.numel()} elements, expected batch * {n} = {want}")
+                kinds.append(True)
+            else:
+                if is_out:
+                    if not (isinstance(a, np.ndarray) and a.dtype == np.float64 and a.flags.c_contiguous):
+                        raise CfxError(EINVAL, f"{name}: host outputs must be C-contiguous float64 numpy arrays")
+                else:
+                    a = np.ascontiguousarray(a, dtype=np.float64)
+                if a.size != want:
+                    raise CfxError(EINVAL, f"{name}: {a.size} elements, expected batch * {n} = {want}")
+                kinds.append(False)
+            out.append(a)
+        if kinds and any(kinds) != all(kinds):
             raise CfxError(EINVAL, "mix of host and device buffers in one call")
-        for a in dev:
-            if not a.is_contiguous() or str(a.dtype) != "torch.float64":
-                raise CfxError(EINVAL, "device buffers must be contiguous float64 tensors")
-        return DEVICE if dev else 0
+        return out, (DEVICE if kinds and kinds[0] else 0)
 
     def set_stream(self, stream_ptr):
         self._check(self.lib.cfx_set_stream(self.h, stream_ptr))
@@ -329,7 +372,9 @@ class Handle:
         return (n, self.batch)
 
     def eval_all(self, v, g=None, jac=None, f=None, grad=None):
-        fl = self._flags(v, g, jac, f, grad)
+        (v, g, jac, f, grad), fl = self._buffers(("v", v, self.nv, False), ("g", g, self.ng, True),
+                                                  ("jac", jac, self.nnz_jac, True), ("f", f, 1, True),
+                                                  ("grad", grad, self.nv, True))
         self._torch_stream(fl)
         self._check(self.lib.cfx_eval_all(self.h, _ptr(v), _ptr(g), _ptr(jac), _ptr(f), _ptr(grad), fl))
 
@@ -355,7 +400,8 @@ class Handle:
 
     def eval_h(self, v, obj_factor, lam, hess=None):
         hess = np.empty(self._shape(self.nnz_hess)) if hess is None else hess
-        fl = self._flags(v, obj_factor, lam, hess)
+        (v, obj_factor, lam, hess), fl = self._buffers(("v", v, self.nv, False), ("obj_factor", obj_factor, 1, False),
+                                                       ("lam", lam, self.ng, False), ("hess", hess, self.nnz_hess, True))
         self._torch_stream(fl)
         self._check(self.lib.cfx_eval_h(self.h, _ptr(v), _ptr(obj_factor), _ptr(lam), _ptr(hess), fl))
         return hess
@@ -363,7 +409,8 @@ class Handle:
     def integrate(self, x0=None, u=None, traj=None):
         n = (self.n_shooting * self.n_steps + 1) * self.nx
         traj = np.empty(self._shape(n)) if traj is None else traj
-        fl = self._flags(x0, u, traj)
+        (x0, u, traj), fl = self._buffers(("x0", x0, self.nx, False), ("u", u, self.n_shooting * self.nu, False),
+                                          ("traj", traj, n, True))
         self._torch_stream(fl)
         self._check(self.lib.cfx_integrate(self.h, _ptr(x0), _ptr(u), _ptr(traj), fl))
         return traj
@@ -418,7 +465,7 @@ class MskHandle(Handle):
         pb.n_muscles = len(muscles)
         pb.muscles = mus
         pb.flags = flags
-        pb.objectives = _objective_array(objectives, self._keep)
+        pb.objectives = _objective_array(objectives, self._keep, n_shooting)
         pb.n_objectives = len(objectives)
         pb.device = device
         h = C.c_void_p()

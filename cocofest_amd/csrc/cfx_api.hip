@@ -331,7 +331,10 @@ static double* ensure(cfx_handle* h, DevBuf& b, size_t count, int* rc) {
     return b.p;
 }
 
-static dim3 tgrid(int64_t B, int64_t len) { return dim3((unsigned)((B + 63) / 64), (unsigned)((len + 63) / 64)); }
+// transposes: 64 x 64 tiles, the element tiles strided over grid.y (a per-instance length past 64 * 65535 loops)
+static dim3 tgrid(int64_t B, int64_t len) {
+    return dim3((unsigned)((B + 63) / 64), (unsigned)std::min<int64_t>((len + 63) / 64, kMaxGridY));
+}
 
 // Device SoA view of an input buffer of `len` doubles per instance.
 static const double* stage_in(cfx_handle* h, int slot, const double* ptr, int64_t len, uint32_t flags, int* rc) {
@@ -430,6 +433,10 @@ extern "C" int cfx_create(const cfx_problem* p, cfx_handle** out) {
         return create_fail(nullptr, CFX_EUNSUPPORTED,
                            "cfx_create: CFX_LAYOUT_TILED64 needs batch % 64 == 0 and a shooting transcription");
     if (!p->stim_rows) return create_fail(nullptr, CFX_EINVAL, "cfx_create: stim_rows is NULL");
+    if (p->n_objectives < 0 || (p->n_objectives > 0 && !p->objectives))
+        return create_fail(nullptr, CFX_EINVAL, "cfx_create: n_objectives < 0, or objectives is NULL");
+    if (p->n_shooting > kMaxGridY)  // grid.y = intervals in the shooting / Hessian / collocation launches
+        return create_fail(nullptr, CFX_EUNSUPPORTED, "cfx_create: n_shooting must be <= 65535");
     const bool hmed = p->model >= CFX_HMED2018;
     if (p->n_params < 0 || (p->n_params > 0 && (!hmed || !p->last_stim_idx)))
         return create_fail(nullptr, CFX_EINVAL,
@@ -819,7 +826,10 @@ extern "C" int cfx_eval_all(cfx_handle* h, const double* v, double* g, double* j
     if (G || J) {
         CFX_HIP(h, launch_shooting(h, J != nullptr, V, G, J));
         if (h->kp.n_slide)
-            hipLaunchKernelGGL(k_slide, dim3((unsigned)((B + 255) / 256), (unsigned)(h->kp.N * h->kp.T)), dim3(256), 0,
+            hipLaunchKernelGGL(k_slide,
+                               dim3((unsigned)((B + 255) / 256),
+                                    (unsigned)std::min<int64_t>((int64_t)h->kp.N * h->kp.T, kMaxGridY)),
+                               dim3(256), 0,
                                h->stream, h->kp, h->d_sl_param,
                                h->d_sl_joff, h->prob.intensity_floor, V, G, J);
     }
@@ -921,6 +931,10 @@ extern "C" int cfx_msk_create(const cfx_msk_problem* p, cfx_handle** out) {
     if (p->n_steps < 1 || p->n_shooting < 1 || p->batch < 1 || !(p->final_time > 0.0))
         return bad("n_steps, n_shooting, batch and final_time must be positive");
     if (p->truncation < 1 || p->truncation > 64) return bad("truncation must be in [1, 64]");
+    if (p->n_shooting > kMaxGridY)
+        return create_fail(nullptr, CFX_EUNSUPPORTED, "cfx_msk_create: n_shooting must be <= 65535");
+    if (p->n_objectives < 0 || (p->n_objectives > 0 && !p->objectives))
+        return bad("n_objectives < 0, or objectives is NULL");
     if (p->layout != CFX_LAYOUT_AOS && p->layout != CFX_LAYOUT_SOA)
         return create_fail(nullptr, CFX_EUNSUPPORTED, "cfx_msk_create: layout must be CFX_LAYOUT_AOS or CFX_LAYOUT_SOA");
     if (!p->stim_rows || !p->dof_axis || !p->dof_frame || !p->body_mass || !p->body_com || !p->body_inertia ||
@@ -1230,6 +1244,9 @@ static int msk_eval_h(cfx_handle* h, const double* v, const double* obj_factor, 
     if (!LAM) return rc;
     double* H = stage_out(h, S_OUT, hess, h->sz.nnz_hess, flags, &rc);
     if (!H) return rc;
+    // the pair kernel runs one thread per (instance, interval, stage, pair task) on a flat grid
+    if ((int64_t)B * h->mp.N * h->mp.Q * h->n_htasks > (int64_t)INT32_MAX)
+        return fail(h, CFX_EUNSUPPORTED, "cfx_eval_h: batch too large for one Hessian launch; split the batch");
     const size_t nw = msk_hess_work_host(h->msk_nq, h->msk_nm, h->mp.nx, h->mp.nz, h->mp.nz * (h->mp.nz + 1) / 2, B,
                                          h->mp.N, h->mp.Q);
     double* W = ensure(h, h->main[S_WORK], nw, &rc);

@@ -73,22 +73,24 @@ __global__ void __launch_bounds__(256) k_slide(const KParams P, const int32_t* _
     const int64_t B = P.B;
     const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= B) return;
-    const int slot = blockIdx.y;  // k * T + j
-    const int k = slot / P.T, j = slot - k * P.T;
     const int64_t p_off = (int64_t)P.N * P.nz + P.nx;
     const int g_off = P.ngk - P.n_slide;  // the window rows follow the interval's dynamics rows
     const int64_t ES = lay_stride(P), vb = lay_base(P, P.nv_tot, b), gb = lay_base(P, P.ng_tot, b),
                   jb = lay_base(P, P.nnz_tot, b);
-    const int pi = sl_param[slot];
-    if (G) {
-        const double u = V[vb + ((int64_t)k * P.nz + P.uoff + j) * ES];
-        const double w = pi >= 0 ? V[vb + (p_off + pi) * ES] : floor_value;
-        G[gb + ((int64_t)k * P.ngk + g_off + j) * ES] = u - w;
-    }
-    if (J) {
-        const int64_t jo = sl_joff[slot];
-        J[jb + jo * ES] = 1.0;
-        if (pi >= 0) J[jb + (jo + 1) * ES] = -1.0;
+    // slot = k * T + j; grid.y is capped at 65535, so the slots are strided over it
+    for (int slot = blockIdx.y; slot < P.N * P.T; slot += gridDim.y) {
+        const int k = slot / P.T, j = slot - k * P.T;
+        const int pi = sl_param[slot];
+        if (G) {
+            const double u = V[vb + ((int64_t)k * P.nz + P.uoff + j) * ES];
+            const double w = pi >= 0 ? V[vb + (p_off + pi) * ES] : floor_value;
+            G[gb + ((int64_t)k * P.ngk + g_off + j) * ES] = u - w;
+        }
+        if (J) {
+            const int64_t jo = sl_joff[slot];
+            J[jb + jo * ES] = 1.0;
+            if (pi >= 0) J[jb + (jo + 1) * ES] = -1.0;
+        }
     }
 }
 
@@ -97,16 +99,18 @@ __global__ void __launch_bounds__(256) k_aos_to_soa(const double* __restrict__ s
                                                     int64_t B, int64_t len) {
     __shared__ double tile[64][65];
     const int64_t b0 = (int64_t)blockIdx.x * 64;
-    const int64_t e0 = (int64_t)blockIdx.y * 64;
     const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
-    for (int r = ty; r < 64; r += 4) {  // read rows b, columns e (coalesced in e)
-        const int64_t b = b0 + r, e = e0 + tx;
-        if (b < B && e < len) tile[r][tx] = src[b * len + e];
-    }
-    __syncthreads();
-    for (int r = ty; r < 64; r += 4) {  // write rows e, columns b (coalesced in b)
-        const int64_t e = e0 + r, b = b0 + tx;
-        if (b < B && e < len) dst[e * B + b] = tile[tx][r];
+    for (int64_t e0 = (int64_t)blockIdx.y * 64; e0 < len; e0 += (int64_t)gridDim.y * 64) {
+        for (int r = ty; r < 64; r += 4) {  // read rows b, columns e (coalesced in e)
+            const int64_t b = b0 + r, e = e0 + tx;
+            if (b < B && e < len) tile[r][tx] = src[b * len + e];
+        }
+        __syncthreads();
+        for (int r = ty; r < 64; r += 4) {  // write rows e, columns b (coalesced in b)
+            const int64_t e = e0 + r, b = b0 + tx;
+            if (b < B && e < len) dst[e * B + b] = tile[tx][r];
+        }
+        __syncthreads();
     }
 }
 
@@ -115,16 +119,18 @@ __global__ void __launch_bounds__(256) k_soa_to_aos(const double* __restrict__ s
                                                     int64_t B, int64_t len) {
     __shared__ double tile[64][65];
     const int64_t b0 = (int64_t)blockIdx.x * 64;
-    const int64_t e0 = (int64_t)blockIdx.y * 64;
     const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
-    for (int r = ty; r < 64; r += 4) {
-        const int64_t e = e0 + r, b = b0 + tx;
-        if (b < B && e < len) tile[r][tx] = src[e * B + b];
-    }
-    __syncthreads();
-    for (int r = ty; r < 64; r += 4) {
-        const int64_t b = b0 + r, e = e0 + tx;
-        if (b < B && e < len) dst[b * len + e] = tile[tx][r];
+    for (int64_t e0 = (int64_t)blockIdx.y * 64; e0 < len; e0 += (int64_t)gridDim.y * 64) {
+        for (int r = ty; r < 64; r += 4) {
+            const int64_t e = e0 + r, b = b0 + tx;
+            if (b < B && e < len) tile[r][tx] = src[e * B + b];
+        }
+        __syncthreads();
+        for (int r = ty; r < 64; r += 4) {
+            const int64_t b = b0 + r, e = e0 + tx;
+            if (b < B && e < len) dst[b * len + e] = tile[tx][r];
+        }
+        __syncthreads();
     }
 }
 

@@ -33,6 +33,7 @@ constexpr int stages_of(int scheme) { return scheme == 4 ? 4 : (scheme == 2 ? 2 
 
 constexpr int kMaxNz = 5 + 32;  // nx + truncation
 constexpr int kMaxDeg = 9;      // collocation polynomial degree
+constexpr int kMaxGridY = 65535;  // launch grid y / z limit
 
 // Everything a kernel needs, passed by value (kernel argument segment).
 struct KParams {
@@ -396,23 +397,17 @@ CFX_HD void st_lane_const(double* p, double c) {
     st_lane<NI>(p, v);
 }
 
-template <int MODEL, int SCHEME, int D, int TMAX, int NI>
-__global__ void __launch_bounds__(256) k_shooting(const KParams P, const double* __restrict__ V,
-                                                  double* __restrict__ G, double* __restrict__ J) {
+// The interval loop of one thread.  WG: g is written (G != nullptr, direction chunk 0); J != nullptr whenever
+// D > 0 (the launcher picks D = 0 for g-only calls).  WG is a template parameter so that each loop body is
+// branch-free around its loads: on CDNA vmcnt counts stores as well as loads, and with a runtime "is G present"
+// branch the compiler had to place the wait for x_{k+1} at the merge point after the interval's stores, where it
+// waited for all of them to complete before the next interval could start.  With WG the g rows consume x_{k+1}
+// before any store of the interval is issued.
+template <int MODEL, int SCHEME, int D, int TMAX, int NI, bool WG>
+__device__ __forceinline__ void shoot_run(const KParams& P, const double* __restrict__ V, double* __restrict__ G,
+                                          double* __restrict__ J, int k0, int k1, int chunk, int64_t ES, int64_t vb,
+                                          int64_t gb, int64_t jb) {
     constexpr int NX = nx_of(MODEL);
-    const int64_t B = P.B;
-    const int64_t b0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * NI;
-    if (b0 >= B) return;
-    const int k0 = blockIdx.y * P.kpt;
-    const int k1 = min(P.N, k0 + P.kpt);
-    const int chunk = is_int(MODEL) ? (int)blockIdx.z : 0;  // the other models carry every direction in one lane
-
-    // layout: element stride ES, per-buffer instance offsets (SoA: b0; 64-instance tiles: see KParams).  The
-    // accesses stay expressed on the __restrict__ arguments (a derived `G ? G + off : nullptr` pointer loses
-    // the no-alias fact, and the table reads then turn into vector loads behind every store).
-    const int64_t ES = lay_stride(P);
-    const int64_t vb = lay_base(P, P.nv_tot, b0), gb = lay_base(P, P.ng_tot, b0), jb = lay_base(P, P.nnz_tot, b0);
-
     IState<NX, D> st[NI];
     CsHmed<D, TMAX> csh[NI];
 #pragma unroll
@@ -422,6 +417,14 @@ __global__ void __launch_bounds__(256) k_shooting(const KParams P, const double*
 #pragma unroll
         for (int i = 0; i < NI; ++i) st[i].x[r] = t[i];
     }
+    // Consume the start state here, before the loop: the wait the compiler places for these loads would otherwise
+    // sit at the loop header (its pending state merges the preheader's loads with the back edge) and run every
+    // interval, where vmcnt then also waits for the previous interval's stores.  Not volatile and no memory
+    // clobber: the table reads stay scalar loads.
+#pragma unroll
+    for (int i = 0; i < NI; ++i)
+#pragma unroll
+        for (int r = 0; r < NX; ++r) asm("" : "+v"(st[i].x[r]));
 
     for (int k = k0; k < k1; ++k) {
         const int xo = k * P.nz;
@@ -439,7 +442,7 @@ __global__ void __launch_bounds__(256) k_shooting(const KParams P, const double*
             load_controls<MODEL, D, TMAX>(P, V + vb + i, ES, xo, chunk, st[i].amp, csh[i]);
         }
         integrate<MODEL, SCHEME, D, TMAX, NI>(P, k, 0, P.m, chunk, st, csh);
-        if (G != nullptr && chunk == 0) {
+        if constexpr (WG) {
 #pragma unroll
             for (int r = 0; r < NX; ++r) {
                 double t[NI];
@@ -447,33 +450,62 @@ __global__ void __launch_bounds__(256) k_shooting(const KParams P, const double*
                 for (int i = 0; i < NI; ++i) t[i] = st[i].x[r] - xnext[r][i];
                 st_lane<NI>(G + gb + (int64_t)(k * P.ngk + r) * ES, t);
             }
+        } else {
+            // no g rows: consume x_{k+1} explicitly before the stores (see above)
+#pragma unroll
+            for (int r = 0; r < NX; ++r)
+#pragma unroll
+                for (int i = 0; i < NI; ++i) asm("" : "+v"(xnext[r][i]));
         }
         if constexpr (D > 0) {
-            if (J != nullptr) {
-                const int64_t jo = (int64_t)k * P.nnzk;
+            const int64_t jo = (int64_t)k * P.nnzk;
 #pragma unroll
-                for (int r = 0; r < NX; ++r) {
+            for (int r = 0; r < NX; ++r) {
 #pragma unroll
-                    for (int j = 0; j < D; ++j) {
-                        const int gd = chunk * D + j;
-                        if (gd < P.nz) {
-                            const int pos = P.jpos[r][gd];
-                            if (pos >= 0) {
-                                double t[NI];
+                for (int j = 0; j < D; ++j) {
+                    const int gd = chunk * D + j;
+                    if (gd < P.nz) {
+                        const int pos = P.jpos[r][gd];
+                        if (pos >= 0) {
+                            double t[NI];
 #pragma unroll
-                                for (int i = 0; i < NI; ++i) t[i] = st[i].xd[r][j];
-                                st_lane<NI>(J + jb + (jo + pos) * ES, t);
-                            }
+                            for (int i = 0; i < NI; ++i) t[i] = st[i].xd[r][j];
+                            st_lane<NI>(J + jb + (jo + pos) * ES, t);
                         }
                     }
-                    if (chunk == 0) st_lane_const<NI>(J + jb + (jo + P.jneg[r]) * ES, -1.0);
                 }
+                if (chunk == 0) st_lane_const<NI>(J + jb + (jo + P.jneg[r]) * ES, -1.0);
             }
         }
 #pragma unroll
         for (int i = 0; i < NI; ++i)
 #pragma unroll
             for (int r = 0; r < NX; ++r) st[i].x[r] = xnext[r][i];
+    }
+}
+
+template <int MODEL, int SCHEME, int D, int TMAX, int NI>
+__global__ void __launch_bounds__(256) k_shooting(const KParams P, const double* __restrict__ V,
+                                                  double* __restrict__ G, double* __restrict__ J) {
+    const int64_t B = P.B;
+    const int64_t b0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * NI;
+    if (b0 >= B) return;
+    const int k0 = blockIdx.y * P.kpt;
+    const int k1 = min(P.N, k0 + P.kpt);
+    const int chunk = is_int(MODEL) ? (int)blockIdx.z : 0;  // the other models carry every direction in one lane
+
+    // layout: element stride ES, per-buffer instance offsets (SoA: b0; 64-instance tiles: see KParams).  The
+    // accesses stay expressed on the __restrict__ arguments (a derived `G ? G + off : nullptr` pointer loses
+    // the no-alias fact, and the table reads then turn into vector loads behind every store).
+    const int64_t ES = lay_stride(P);
+    const int64_t vb = lay_base(P, P.nv_tot, b0), gb = lay_base(P, P.ng_tot, b0), jb = lay_base(P, P.nnz_tot, b0);
+    if constexpr (D == 0) {
+        shoot_run<MODEL, SCHEME, 0, TMAX, NI, true>(P, V, G, J, k0, k1, chunk, ES, vb, gb, jb);
+    } else {
+        if (G != nullptr && chunk == 0)
+            shoot_run<MODEL, SCHEME, D, TMAX, NI, true>(P, V, G, J, k0, k1, chunk, ES, vb, gb, jb);
+        else
+            shoot_run<MODEL, SCHEME, D, TMAX, NI, false>(P, V, G, J, k0, k1, chunk, ES, vb, gb, jb);
     }
 }
 

@@ -383,7 +383,9 @@ class BatchedIpm:
                     sol = sol + self._kkt_solve(K, rhs - self._kkt_matvec(W, dxx, jv, sol[:, :nf], sol[:, nf:]))
                 dx, dy = sol[:, :nf], sol[:, nf:]
                 curv = self._quad_w(W, dx) + (dxx * dx * dx).sum(1)
-                bad = (~done) & ((curv <= opt.curv_min * (dx * dx).sum(1)) | ~torch.isfinite(curv))
+                # a zero pivot (LAPACK info != 0) or a non-finite solution counts as wrong inertia: more delta_w
+                bad = (~done) & ((curv <= opt.curv_min * (dx * dx).sum(1)) | ~torch.isfinite(curv) |
+                                 self.band.singular(K) | ~torch.isfinite(sol).all(1))
                 if not bool(bad.any()):
                     break
                 first = dw == 0
@@ -471,10 +473,13 @@ class BatchedIpm:
                       f"a_p {float(a_p[0]):.2e} dw {float(dw[0]):.1e} "
                       f"argmax|rd| v[{int(self.free[int(rd[0].abs().argmax())])}]")
             x = torch.where(step[:, None], x_new, x)
-            y = y + alpha[:, None] * dy
+            # updates only where a step is taken and finite (0 * NaN would poison a finished instance for good)
+            mv = (alpha > 0) & torch.isfinite(dy).all(1)
+            y = torch.where(mv[:, None], y + alpha[:, None] * dy, y)
             az = torch.where(step & ~failed, a_z, torch.zeros_like(a_z))
-            zl = zl + az[:, None] * dzl
-            zu = zu + az[:, None] * dzu
+            mz = (az > 0) & torch.isfinite(dzl).all(1) & torch.isfinite(dzu).all(1)
+            zl = torch.where(mz[:, None], zl + az[:, None] * dzl, zl)
+            zu = torch.where(mz[:, None], zu + az[:, None] * dzu, zu)
             # keep z within [mu / (kappa s), kappa mu / s] (Ipopt kappa_Sigma = 1e10)
             sl = torch.where(hasL, x - lbF, torch.ones_like(x))
             su = torch.where(hasU, ubF - x, torch.ones_like(x))
@@ -587,6 +592,11 @@ class GpuBandSolver:
         info = torch.empty((B,), dtype=torch.int32, device=ab.device)
         _cfx.band_lu(ab, ipiv, info, kl, ku)
         return (ab, ipiv, info, kl, ku)
+
+    @staticmethod
+    def singular(fac):
+        """(B,) bool: instances whose factorisation hit an exactly zero pivot (LAPACK info != 0)."""
+        return fac[2] != 0
 
     def solve(self, fac, rhs):
         from . import _cfx

@@ -74,6 +74,12 @@ class DenseBandSolver:
         A[:, inband] = ab[:, jj, r[inband]]
         return A
 
+    @staticmethod
+    def singular(A):
+        import torch
+
+        return torch.zeros(A.shape[0], dtype=torch.bool)
+
     def solve(self, A, rhs):
         import torch
 

@@ -106,11 +106,12 @@ def test_shooting_g_and_jacobian_vs_oracle(name, scheme):
     jac = h.eval_jac_g(v)
     _close_g(pb, v, g, O.eval_g(pb, v), what=f"g {name} {scheme}")
     _close(jac, O.eval_jac_g(pb, v), what=f"J {name} {scheme}")
-    # fused call gives identical values
+    # fused call gives the same values: g bit for bit; J runs a separately compiled loop body (with / without the
+    # g rows), whose FMA contraction may differ by an ulp
     g2, j2 = np.empty_like(g), np.empty_like(jac)
     h.eval_all(v, g=g2, jac=j2)
     np.testing.assert_array_equal(g2, g)
-    np.testing.assert_array_equal(j2, jac)
+    np.testing.assert_allclose(j2, jac, rtol=1e-14, atol=1e-300)
 
 
 @pytest.mark.parametrize("T", [1, 5, 10, 17, 32])
@@ -460,6 +461,36 @@ def test_band_lu_small_and_windowed_paths_agree(B, n, kl, ku, monkeypatch):
     np.testing.assert_allclose(outs[0][0], outs[1][0], rtol=1e-12, atol=1e-12)
     np.testing.assert_allclose(outs[0][2], outs[1][2], rtol=1e-10, atol=1e-12)
     np.testing.assert_allclose(outs[0][3], outs[0][2][:, :1], rtol=1e-10, atol=1e-12)
+
+
+@pytest.mark.parametrize("n", [60, 502])
+def test_band_lu_large_batch_factor_then_solve(n):
+    """From 2048 instances on, cfx_band_lu factors with the register kernel while cfx_band_lu_solve may pick the
+    windowed one (the multi-start IPM reuses factors this way at 4096 starts): the reused factors must solve like
+    the factorisation's own solve and like numpy's dense solve."""
+    import torch
+
+    from cocofest_amd import _cfx
+
+    B, kl, ku = 2112, 6, 6
+    rng = np.random.default_rng(n)
+    A, ab = _band_system(rng, B, n, kl, ku, zero_diag=True)
+    rhs = rng.standard_normal((B, n))
+    abt = torch.tensor(ab, device="cuda")
+    ipiv = torch.empty((B, n), dtype=torch.int32, device="cuda")
+    info = torch.empty((B,), dtype=torch.int32, device="cuda")
+    x = torch.tensor(rhs, device="cuda")
+    _cfx.band_lu(abt, ipiv, info, kl, ku, rhs=x)
+    x2 = torch.tensor(rhs, device="cuda")
+    _cfx.band_lu_solve(abt, ipiv, kl, ku, x2)
+    torch.cuda.synchronize()
+    assert (info.cpu().numpy() == 0).all()
+    xs, x2s = x.cpu().numpy(), x2.cpu().numpy()
+    np.testing.assert_allclose(x2s, xs, rtol=1e-10, atol=1e-12 * np.abs(xs).max())
+    pick = rng.choice(B, 64, replace=False)  # dense reference on a sample of the batch
+    ref = np.linalg.solve(A[pick], rhs[pick][:, :, None])[:, :, 0]
+    cond = np.linalg.cond(A[pick]).max()
+    assert np.max(np.abs(x2s[pick] - ref)) <= 1e-13 * cond * n * max(1.0, np.abs(ref).max())
 
 
 def test_band_lu_reports_singular_and_bad_arguments():

@@ -55,6 +55,9 @@ def test_create_without_device_fails_loudly():
     ("layout", 7, "EINVAL", "unknown layout"),
     ("stim_rows", None, "EINVAL", "stim_rows is NULL"),
     ("n_params", 2, "EINVAL", "intensity parameters need a Hmed2018 model"),
+    ("n_objectives", -1, "EINVAL", "n_objectives < 0, or objectives is NULL"),
+    ("n_objectives", 2, "EINVAL", "n_objectives < 0, or objectives is NULL"),  # objectives left NULL
+    ("n_shooting", 65536, "EUNSUPPORTED", "n_shooting must be <= 65535"),
 ])
 def test_create_rejects_bad_problem_before_touching_the_device(field, value, code, msg):
     """cfx_create validates the problem before any HIP call (cfx_api.hip:411-434), so every rejection is
@@ -114,6 +117,9 @@ def test_tiled_layout_and_collocation_limits_are_rejected():
     ("final_time", -1.0, "EINVAL", "must be positive"),
     ("truncation", 65, "EINVAL", "truncation must be in [1, 64]"),
     ("layout", 2, "EUNSUPPORTED", "layout must be CFX_LAYOUT_AOS or CFX_LAYOUT_SOA"),
+    ("n_shooting", 70000, "EUNSUPPORTED", "n_shooting must be <= 65535"),
+    ("n_objectives", -3, "EINVAL", "n_objectives < 0, or objectives is NULL"),
+    ("n_objectives", 1, "EINVAL", "n_objectives < 0, or objectives is NULL"),
     (None, None, "EINVAL", "NULL array"),  # a valid header whose geometry arrays are missing
 ])
 def test_msk_create_rejects_bad_problem_before_touching_the_device(field, value, code, msg):
@@ -133,6 +139,78 @@ def test_msk_create_rejects_bad_problem_before_touching_the_device(field, value,
     assert not h.value
     assert msg in lib.cfx_last_error(None).decode()
     assert lib.cfx_msk_create(None, C.byref(h)) == _cfx.EINVAL
+
+
+def _bare_handle(batch=4, device=0, layout=None):
+    """A Handle whose sizes are set by hand (no cfx_create, so no GPU): exercises the Python-side buffer checks
+    that run before any libcfx call."""
+    from cocofest_amd import _cfx
+
+    h = _cfx.Handle.__new__(_cfx.Handle)
+    h.lib, h.h = None, None
+    h.batch, h.device, h.layout = batch, device, _cfx.LAYOUT_SOA if layout is None else layout
+    h.nv, h.ng, h.nnz_jac, h.nnz_hess, h.nx, h.nu, h.n_shooting, h.n_steps = 6, 4, 10, 9, 2, 0, 2, 1
+    return h
+
+
+def test_buffer_checks_reject_bad_host_arrays():
+    """Every host buffer is checked against its slot before the call: libcfx reads / writes exactly batch * len
+    doubles, so a wrong dtype, stride or size would be an out-of-bounds host access (_cfx.py)."""
+    from cocofest_amd import CfxError
+
+    h = _bare_handle()
+    v = np.zeros((4, 6))
+    cases_bad = [
+        dict(v=np.zeros((4, 5))),                                    # short input
+        dict(v=v, g=np.zeros((4, 4), dtype=np.float32)),             # float32 output
+        dict(v=v, g=np.zeros((4, 8))[:, ::2]),                       # non-contiguous output
+        dict(v=v, g=np.zeros((4, 3))),                               # short output
+        dict(v=v, jac=np.zeros((4, 11))),                            # long output
+        dict(v=v, f=np.zeros(3)),                                    # f is one value per instance
+        dict(v=v, grad=[0.0] * 24),                                  # outputs must be numpy arrays
+    ]
+    for kw in cases_bad:
+        with pytest.raises(CfxError) as exc:
+            h.eval_all(**kw)
+        assert exc.value.code == -1, kw
+    with pytest.raises(CfxError):
+        h.eval_h(v, np.ones(4), np.zeros((4, 5)), np.zeros((4, 9)))  # lambda of the wrong size
+    with pytest.raises(CfxError):
+        h.integrate(x0=np.zeros((4, 3)), traj=np.zeros((4, 6)))      # x0 of the wrong size
+    # well-formed inputs are converted (non-contiguous float32 view -> contiguous float64 copy) and accepted
+    (vv, g), fl = h._buffers(("v", np.zeros((4, 12), dtype=np.float32)[:, ::2], 6, False),
+                             ("g", np.zeros((4, 4)), 4, True))
+    assert fl == 0 and vv.dtype == np.float64 and vv.flags.c_contiguous and g.shape == (4, 4)
+
+
+def test_buffer_checks_reject_bad_tensors():
+    """A CPU tensor must never be sent as a device pointer (GPU fault), and device tensors must match the handle's
+    device and the slot's size."""
+    import torch
+
+    from cocofest_amd import CfxError
+
+    h = _bare_handle()
+    with pytest.raises(CfxError) as exc:
+        h.eval_all(torch.zeros((4, 6), dtype=torch.float64))
+    assert "CPU tensor" in str(exc.value)
+    with pytest.raises(CfxError) as exc:
+        h.eval_all(torch.zeros((4, 6), dtype=torch.float64), g=np.zeros((4, 4)))
+    assert "CPU tensor" in str(exc.value)
+
+
+def test_objective_target_length_is_checked():
+    from cocofest_amd import CfxError
+    from cocofest_amd import _cfx
+
+    keep = []
+    ok = _cfx._objective_array([dict(kind=0, var_kind=0, var_index=1, node_first=0, node_last=2, weight=1.0,
+                                     target=np.zeros(3))], keep, 2)
+    assert ok[0].weight == 1.0
+    with pytest.raises(CfxError) as exc:
+        _cfx._objective_array([dict(kind=0, var_kind=0, var_index=1, node_first=0, node_last=2, weight=1.0,
+                                    target=np.zeros(2))], keep, 2)
+    assert "expected n_shooting + 1 = 3" in str(exc.value)
 
 
 def test_missing_library_is_an_error(tmp_path):
