@@ -91,6 +91,20 @@ class Sizes(C.Structure):
                 ("nx", C.c_int32), ("nu", C.c_int32)]
 
 
+class IpmOptions(C.Structure):
+    _fields_ = [("tol", C.c_double), ("max_iter", C.c_int32), ("acceptable_tol", C.c_double),
+                ("acceptable_iter", C.c_int32), ("mu_init", C.c_double), ("bound_relax_factor", C.c_double),
+                ("bound_push", C.c_double), ("tau_min", C.c_double), ("kappa_eps", C.c_double),
+                ("kappa_mu", C.c_double), ("theta_mu", C.c_double), ("s_max", C.c_double), ("armijo", C.c_double),
+                ("max_backtrack", C.c_int32), ("delta_c", C.c_double), ("curv_min", C.c_double),
+                ("max_soc", C.c_int32), ("kappa_soc", C.c_double)]
+
+
+class IpmStats(C.Structure):
+    _fields_ = [("eval_all", C.c_int64), ("eval_g_f", C.c_int64), ("eval_h", C.c_int64), ("kkt_factor", C.c_int64),
+                ("iterations", C.c_int64), ("host_syncs", C.c_int64), ("wall_s", C.c_double)]
+
+
 # exported symbols and their signatures (must match include/cfx.h)
 _P = C.c_void_p
 _D = C.POINTER(C.c_double)
@@ -115,6 +129,13 @@ SIGNATURES = {
     "cfx_msk_create": (C.c_int, [C.POINTER(MskProblem), C.POINTER(_P)]),
     "cfx_band_lu": (C.c_int, [C.c_int64, C.c_int32, C.c_int32, C.c_int64, _P, _P, _P, C.c_int32, _P, _P]),
     "cfx_band_lu_solve": (C.c_int, [C.c_int64, C.c_int32, C.c_int32, C.c_int64, _P, _P, C.c_int32, _P, _P]),
+    "cfx_ipm_default_options": (None, [C.POINTER(IpmOptions)]),
+    "cfx_ipm_create": (C.c_int, [_P, _P, _P, C.c_int32, C.POINTER(IpmOptions), C.POINTER(_P)]),
+    "cfx_ipm_solve": (C.c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _P, C.c_uint32]),
+    "cfx_ipm_get_stats": (C.c_int, [_P, C.POINTER(IpmStats)]),
+    "cfx_ipm_n_fixed": (C.c_int, [_P]),
+    "cfx_ipm_last_error": (C.c_char_p, [_P]),
+    "cfx_ipm_destroy": (None, [_P]),
 }
 
 _lib = None
@@ -471,3 +492,74 @@ class MskHandle(Handle):
         h = C.c_void_p()
         rc = self.lib.cfx_msk_create(C.byref(pb), C.byref(h))
         self._attach(rc, h, batch, layout, n_shooting, n_steps, device)
+
+
+class Ipm:
+    """A libcfx interior-point solver (cfx_ipm_*) bound to a handle (CFX_LAYOUT_AOS, or batch 1): the whole
+    iteration runs on the handle's GPU.  ``options``: a dict of cfx_ipm_options fields (libcfx defaults for the
+    rest).  Host (numpy) inputs and outputs; the call returns when the solve is done."""
+
+    def __init__(self, handle: Handle, lb, ub, n_params: int = 0, options: dict | None = None):
+        self.lib = handle.lib
+        self.handle = handle  # keeps the handle alive
+        self.batch, self.nv, self.ng = handle.batch, handle.nv, handle.ng
+        if handle.batch > 1 and handle.layout != LAYOUT_AOS:
+            raise CfxError(EINVAL, "Ipm: the handle must use the AoS layout (or batch 1)")
+        lb = np.ascontiguousarray(lb, dtype=np.float64).reshape(-1)
+        ub = np.ascontiguousarray(ub, dtype=np.float64).reshape(-1)
+        if lb.size != self.nv or ub.size != self.nv:
+            raise CfxError(EINVAL, f"Ipm: bounds must hold nv = {self.nv} values")
+        opt = IpmOptions()
+        self.lib.cfx_ipm_default_options(C.byref(opt))
+        for k, v in (options or {}).items():
+            if k not in dict(IpmOptions._fields_):
+                raise CfxError(EINVAL, f"Ipm: unknown option {k!r}")
+            setattr(opt, k, v)
+        s = C.c_void_p()
+        rc = self.lib.cfx_ipm_create(handle.h, lb.ctypes.data, ub.ctypes.data, int(n_params), C.byref(opt), C.byref(s))
+        if rc != OK:
+            raise CfxError(rc, self.lib.cfx_last_error(None).decode())
+        self.s = s
+        self.n_fixed = self.lib.cfx_ipm_n_fixed(self.s)
+
+    def solve(self, v0, fixed_values=None):
+        """Returns (v, y, f, converged, iterations, kkt_error) as numpy arrays."""
+        B = self.batch
+        v0 = np.ascontiguousarray(v0, dtype=np.float64)
+        if v0.size != B * self.nv:
+            raise CfxError(EINVAL, f"Ipm.solve: v0 has {v0.size} values, expected batch * nv = {B * self.nv}")
+        fv = None
+        if fixed_values is not None:
+            fv = np.ascontiguousarray(fixed_values, dtype=np.float64)
+            if fv.size != B * self.n_fixed:
+                raise CfxError(EINVAL, f"Ipm.solve: fixed_values has {fv.size} values, expected batch * n_fixed = "
+                                       f"{B * self.n_fixed}")
+        v = np.empty((B, self.nv))
+        y = np.empty((B, self.ng))
+        f = np.empty(B)
+        conv = np.empty(B, dtype=np.int32)
+        its = np.empty(B, dtype=np.int32)
+        kkt = np.empty(B)
+        rc = self.lib.cfx_ipm_solve(self.s, v0.ctypes.data, None if fv is None else fv.ctypes.data, v.ctypes.data,
+                                    y.ctypes.data, f.ctypes.data, conv.ctypes.data, its.ctypes.data, kkt.ctypes.data, 0)
+        if rc != OK:
+            raise CfxError(rc, self.lib.cfx_ipm_last_error(self.s).decode())
+        return v, y, f, conv.astype(bool), its.astype(np.int64), kkt
+
+    def stats(self):
+        st = IpmStats()
+        rc = self.lib.cfx_ipm_get_stats(self.s, C.byref(st))
+        if rc != OK:
+            raise CfxError(rc, "cfx_ipm_get_stats")
+        return {k: getattr(st, k) for k, _ in IpmStats._fields_}
+
+    def close(self):
+        if getattr(self, "s", None):
+            self.lib.cfx_ipm_destroy(self.s)
+            self.s = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

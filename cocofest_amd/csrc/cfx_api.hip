@@ -12,6 +12,7 @@
 #include "../../include/cfx.h"
 #include "cfx_aux.h"
 #include "cfx_colloc.h"
+#include "cfx_internal.h"
 #include "cfx_launch.h"
 #include "cfx_msk_launch.h"
 
@@ -336,11 +337,17 @@ static dim3 tgrid(int64_t B, int64_t len) {
     return dim3((unsigned)((B + 63) / 64), (unsigned)std::min<int64_t>((len + 63) / 64, kMaxGridY));
 }
 
+// AoS buffers go through a transpose unless they are SoA already: one element per instance, or one instance
+// (a batch of 1 has the same memory image in both layouts).
+static bool is_aos(const cfx_handle* h, int64_t len) {
+    return h->prob.layout == CFX_LAYOUT_AOS && len > 1 && h->prob.batch > 1;
+}
+
 // Device SoA view of an input buffer of `len` doubles per instance.
 static const double* stage_in(cfx_handle* h, int slot, const double* ptr, int64_t len, uint32_t flags, int* rc) {
     const int64_t B = h->prob.batch;
     const bool dev = flags & CFX_DEVICE;
-    const bool aos = h->prob.layout == CFX_LAYOUT_AOS && len > 1;
+    const bool aos = is_aos(h, len);
     if (dev && !aos) return ptr;
     const size_t n = (size_t)B * len;
     double* m = ensure(h, h->main[slot], n, rc);
@@ -364,7 +371,7 @@ static const double* stage_in(cfx_handle* h, int slot, const double* ptr, int64_
 // Device SoA buffer an output is written to.
 static double* stage_out(cfx_handle* h, int slot, double* ptr, int64_t len, uint32_t flags, int* rc) {
     const bool dev = flags & CFX_DEVICE;
-    const bool aos = h->prob.layout == CFX_LAYOUT_AOS && len > 1;
+    const bool aos = is_aos(h, len);
     if (dev && !aos) return ptr;
     return ensure(h, h->main[slot], (size_t)h->prob.batch * len, rc);
 }
@@ -372,7 +379,7 @@ static double* stage_out(cfx_handle* h, int slot, double* ptr, int64_t len, uint
 static int finish_out(cfx_handle* h, int slot, double* soa, double* ptr, int64_t len, uint32_t flags) {
     const int64_t B = h->prob.batch;
     const bool dev = flags & CFX_DEVICE;
-    const bool aos = h->prob.layout == CFX_LAYOUT_AOS && len > 1;
+    const bool aos = is_aos(h, len);
     const size_t n = (size_t)B * len;
     if (dev && !aos) return CFX_OK;
     double* src = soa;
@@ -760,6 +767,16 @@ extern "C" void cfx_destroy(cfx_handle* h) {
 extern "C" int cfx_get_sizes(const cfx_handle* h, cfx_sizes* out) {
     if (!h || !out) return CFX_EINVAL;
     *out = h->sz;
+    return CFX_OK;
+}
+
+// internal (cfx_internal.h): what the interior-point driver needs to know about a handle
+int cfx_internal_info(const cfx_handle* h, int64_t* batch, int* layout, int* device, hipStream_t* stream) {
+    if (!h) return CFX_EINVAL;
+    *batch = h->prob.batch;
+    *layout = h->prob.layout;
+    *device = h->device;
+    *stream = h->stream;
     return CFX_OK;
 }
 

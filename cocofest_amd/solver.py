@@ -607,6 +607,50 @@ class GpuBandSolver:
         return x
 
 
+_NATIVE_OPTIONS = ("tol", "max_iter", "acceptable_tol", "acceptable_iter", "mu_init", "bound_relax_factor",
+                   "bound_push", "tau_min", "kappa_eps", "kappa_mu", "theta_mu", "s_max", "armijo", "max_backtrack",
+                   "delta_c", "curv_min", "max_soc", "kappa_soc")
+
+
+class NativeIpm:
+    """The interior point of :class:`BatchedIpm`, run by libcfx itself (``cfx_ipm_*``, csrc/cfx_ipm.hip): the whole
+    iteration stays on the GPU — callbacks, fused barrier-algebra kernels, band assembly, band LU — and the host
+    reads a 16-byte counter twice per iteration instead of issuing ~1,500 tensor operations.  Same constructor,
+    ``solve`` and result as :class:`BatchedIpm`, which remains the algorithm's executable specification (CPU-testable
+    with the oracle, cross-checked against scipy).  Iterative refinement (``refine``) is BatchedIpm-only."""
+
+    def __init__(self, ocp, batch: int = 1, device: int = 0, options: IpmOptions | None = None):
+        from . import _cfx
+
+        self.ocp = ocp
+        self.B = batch
+        self.opt = options or IpmOptions()
+        if self.opt.refine:
+            raise ValueError("NativeIpm: iterative refinement (refine > 0) is only available in BatchedIpm")
+        self.h = ocp.nlp(batch=batch, layout="aos", device=device)
+        self.n, self.m = self.h.nv, self.h.ng
+        lb, ub = ocp.bounds_vector()
+        self.ipm = _cfx.Ipm(self.h, lb, ub, int(getattr(ocp, "n_params", 0) or 0),
+                            {k: getattr(self.opt, k) for k in _NATIVE_OPTIONS})
+        self.calls = {"eval_all": 0, "eval_h": 0, "eval_g_f": 0, "kkt_factor": 0}
+
+    def solve(self, v0=None, fixed_values=None):
+        t0 = time.perf_counter()
+        if v0 is None:
+            v0 = np.tile(self.ocp.initial_guess_vector(), (self.B, 1))
+        v, y, f, conv, its, kkt = self.ipm.solve(v0, fixed_values)
+        wall = time.perf_counter() - t0
+        st = self.ipm.stats()
+        self.calls = {k: int(st[k]) for k in ("eval_all", "eval_h", "eval_g_f", "kkt_factor")}
+        self.last_stats = st
+        return IpmResult(v=v, y=y, f=f, converged=conv, iterations=its, kkt_error=kkt, wall_time=wall,
+                         n_callbacks=dict(self.calls))
+
+    def close(self):
+        self.ipm.close()
+        self.h.close()
+
+
 def solve_ocp(ocp, solver=None, batch: int = 1, device: int = 0, v0=None, **kwargs):
     """`FesOcp.solve`: interior-point solve of `batch` instances (multi-start when v0 differs per row)."""
     opts = IpmOptions(**{k: v for k, v in kwargs.items() if hasattr(IpmOptions, k)})

@@ -250,6 +250,57 @@ int cfx_band_lu(int64_t n, int32_t kl, int32_t ku, int64_t batch, double *ab, in
 int cfx_band_lu_solve(int64_t n, int32_t kl, int32_t ku, int64_t batch, const double *ab, const int32_t *ipiv,
                       int32_t nrhs, double *rhs, void *hip_stream);
 
+/* ---- batched interior-point solver ---------------------------------------------------------------
+   Replaces the solver role of `ocp.solve(Solver.IPOPT(...))` (bioptim's Ipopt interface; called e.g. at
+   examples/getting_started/frequency_optimization.py:22 and examples/getting_started/pulse_duration_optimization.py:41
+   with `_max_iter` / `_tol`): Ipopt's primal-dual barrier method (monotone Fiacco-McCormick mu update, filter line
+   search with second-order corrections, inertia correction by a curvature test, gradient-based problem scaling,
+   least-squares multiplier initialisation, a feasibility-restoration step) for the B instances of one handle in
+   lockstep.  Every iteration stays on the handle's GPU: the callbacks above, fused vector kernels for the barrier
+   algebra, the KKT matrix assembled in band storage (unknowns ordered stage by stage) and factored by the batched
+   band LU below; the host only reads a few counters per iteration (all done? wrong inertia? every trial point
+   accepted?).  The handle must use CFX_LAYOUT_AOS (or have batch 1).  Fixed variables (lb == ub) are removed. */
+typedef struct cfx_ipm_options {
+    double tol;                /* Ipopt tol on the scaled KKT error (default 1e-6) */
+    int32_t max_iter;          /* default 200 */
+    double acceptable_tol;     /* acceptable level (1e-6) held for acceptable_iter (15) iterations */
+    int32_t acceptable_iter;
+    double mu_init;            /* 0.1 */
+    double bound_relax_factor; /* 0 (off) */
+    double bound_push;         /* 1e-2 */
+    double tau_min;            /* 0.99 */
+    double kappa_eps, kappa_mu, theta_mu; /* 10, 0.2, 1.5 */
+    double s_max;              /* 100 */
+    double armijo;             /* 1e-4 */
+    int32_t max_backtrack;     /* 30 */
+    double delta_c;            /* 1e-9 */
+    double curv_min;           /* 1e-8: dx^T (W + Sigma + dw) dx >= curv_min |dx|^2 */
+    int32_t max_soc;           /* 4 */
+    double kappa_soc;          /* 0.99 */
+} cfx_ipm_options;
+
+typedef struct cfx_ipm_stats {
+    int64_t eval_all, eval_g_f, eval_h, kkt_factor, iterations, host_syncs;
+    double wall_s; /* last cfx_ipm_solve */
+} cfx_ipm_stats;
+
+typedef struct cfx_ipm cfx_ipm;
+
+void cfx_ipm_default_options(cfx_ipm_options *opt);
+/* lb, ub: [nv] host arrays (+-inf allowed); n_params: trailing parameters of the decision vector (Hmed) */
+int cfx_ipm_create(cfx_handle *h, const double *lb, const double *ub, int32_t n_params, const cfx_ipm_options *opt,
+                   cfx_ipm **out);
+/* v0 [B][nv] starting points; fixed_values [B][n_fixed] values of the fixed variables in index order (NULL: their
+   bound); outputs (any may be NULL): v [B][nv], y [B][ng] multipliers of the unscaled problem, f [B],
+   converged [B], iterations [B], kkt_error [B] (scaled).  CFX_DEVICE: every pointer is a device pointer and the
+   outputs are written asynchronously on the handle's stream; otherwise host pointers. */
+int cfx_ipm_solve(cfx_ipm *s, const double *v0, const double *fixed_values, double *v, double *y, double *f,
+                  int32_t *converged, int32_t *iterations, double *kkt_error, uint32_t flags);
+int cfx_ipm_get_stats(const cfx_ipm *s, cfx_ipm_stats *out);
+int cfx_ipm_n_fixed(const cfx_ipm *s);
+const char *cfx_ipm_last_error(const cfx_ipm *s);
+void cfx_ipm_destroy(cfx_ipm *s);
+
 #ifdef __cplusplus
 }
 #endif

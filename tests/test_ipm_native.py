@@ -1,0 +1,154 @@
+"""libcfx's native interior point (cfx_ipm_*, csrc/cfx_ipm.hip) against BatchedIpm, the algorithm's executable
+specification (solver.py; cross-checked against scipy's trust-constr in test_solver_cpu.py and against the
+oracle-driven run in test_gpu_parity.py): the same problems from the same starts reach the same KKT points.
+
+The two run the same arithmetic with different reduction orders (block reductions vs torch kernels), so
+iterates agree to rounding and the iteration counts may differ by a few near the tolerance; the solutions are
+compared at the solver tolerance."""
+
+import json
+import pathlib
+
+import numpy as np
+import pytest
+
+from tests import cases
+
+pytestmark = pytest.mark.gpu
+
+FT = json.loads((pathlib.Path(__file__).parent / "golden" / "ref_formulas.json").read_text())["misc"]["force_tracking"]
+TRACK = {"force_tracking": [np.array(FT["time"]), np.array(FT["force"])]}
+
+
+def _starts(ocp, B, seed, spread=10.0):
+    v0 = np.tile(ocp.initial_guess_vector(), (B, 1))
+    if B > 1:
+        rng = np.random.default_rng(seed)
+        lb, ub = ocp.bounds_vector()
+        free = lb != ub
+        v0[:, free] = np.clip(v0[:, free] + rng.uniform(0, 1, (B, free.sum())) * np.minimum(ub[free] - lb[free], spread),
+                              lb[free], ub[free])
+    return v0
+
+
+def _both(ocp, B, v0, tol=1e-8, fixed_values=None, max_iter=300):
+    from cocofest_amd.solver import BatchedIpm, IpmOptions, NativeIpm
+
+    opts = IpmOptions(tol=tol, max_iter=max_iter)
+    ref = BatchedIpm(ocp, batch=B, options=opts)
+    r_ref = ref.solve(v0, fixed_values=fixed_values)
+    ref.close()
+    nat = NativeIpm(ocp, batch=B, options=opts)
+    r_nat = nat.solve(v0, fixed_values=fixed_values)
+    nat.close()
+    return r_ref, r_nat
+
+
+def _compare(ocp, r_ref, r_nat, vtol=1e-5, ftol=1e-7, it_slack=3):
+    assert r_nat.converged.all(), (r_nat.kkt_error, r_nat.iterations)
+    np.testing.assert_array_equal(r_nat.converged, r_ref.converged)
+    assert np.all(np.abs(r_nat.iterations - r_ref.iterations) <= it_slack), (r_nat.iterations, r_ref.iterations)
+    np.testing.assert_allclose(r_nat.f, r_ref.f, rtol=ftol, atol=1e-10)
+    lb, ub = ocp.bounds_vector()
+    span = np.where(np.isfinite(ub - lb), ub - lb, np.maximum(np.abs(r_ref.v).max(0), 1.0))
+    err = np.max(np.abs(r_nat.v - r_ref.v) / np.maximum(span, 1e-12))
+    assert err < vtol, err
+    free = lb != ub  # fixed entries take the caller's values
+    assert np.all(r_nat.v[:, free] >= lb[free] - 1e-8) and np.all(r_nat.v[:, free] <= ub[free] + 1e-8)
+
+
+@pytest.mark.parametrize("B", [1, 8])
+def test_native_ipm_cfg3_pulse_width_tracking(B):
+    """cfg 3 (Ding2007 pulse widths, 30 pulses, N = 100, Fourier force tracking): single start and random starts."""
+    cfg = dict(cases.cfg3(), objective=TRACK)
+    ocp = cases.product_ocp(**cfg)
+    r_ref, r_nat = _both(ocp, B, _starts(ocp, B, 0))
+    _compare(ocp, r_ref, r_nat)
+
+
+def test_native_ipm_cfg2_is_the_forward_integration():
+    """cfg 2 (0 DOF) from the reference's zero initial guess: the optimum is the RK1 x 10 forward integration."""
+    from oracle import fes_oracle as O
+
+    cfg = cases.cfg2()
+    ocp = cases.product_ocp(**cfg)
+    pb = cases.oracle_problem(**cfg)
+    r_ref, r_nat = _both(ocp, 1, _starts(ocp, 1, 0))
+    _compare(ocp, r_ref, r_nat)
+    traj = O.ivp_integrate("ding2003", O.model_constants("ding2003"), pb.rows, np.zeros((pb.n_shooting, 0)), 1.0,
+                           "RK1", 10)
+    X, _, _ = pb.unpack(r_nat.v)
+    np.testing.assert_allclose(X[0], traj[:, ::10].T, rtol=1e-7, atol=1e-8)
+
+
+def test_native_ipm_hmed_sliding_window():
+    """Hmed2018 intensities with sliding-window constraints and intensity parameters (the parameter ordering)."""
+    cfg = dict(name="hmed2018", stims=[0.0, 0.1, 0.2, 0.3, 0.4], final_time=0.5, truncation=5, scheme="RK1", m=5,
+               objective={"end_node_tracking": 60}, n_shooting=None)
+    ocp = cases.product_ocp(**cfg)
+    rng = np.random.default_rng(5)
+    v0 = np.tile(ocp.initial_guess_vector(), (8, 1))
+    lb, ub = ocp.bounds_vector()
+    free = lb != ub
+    v0[:, free] = np.clip(v0[:, free] + rng.uniform(0, 10, (8, free.sum())), lb[free], ub[free])
+    r_ref, r_nat = _both(ocp, 8, v0)
+    _compare(ocp, r_ref, r_nat)
+
+
+@pytest.mark.parametrize("name", ["ding2003_with_fatigue", "ding2007_with_fatigue", "hmed2018_with_fatigue"])
+def test_native_ipm_fatigue_families_rk4(name):
+    t = np.linspace(0, 1, 11)
+    cfg = dict(name=name, stims=[0.0, 0.05, 0.1, 0.15], final_time=0.2, truncation=4, scheme="RK4", m=3,
+               objective={"force_tracking": [t, 40 * t]}, n_shooting=None)
+    ocp = cases.product_ocp(**cfg)
+    r_ref, r_nat = _both(ocp, 2, _starts(ocp, 2, 1))
+    _compare(ocp, r_ref, r_nat)
+
+
+def test_native_ipm_collocation():
+    """Direct collocation (Legendre degree 4) of the cfg 3 shape."""
+    stims = [float(t) for t in np.round(np.linspace(0, 1, 31)[:-1], 2)]
+    ocp = cases.product_collocation_ocp("ding2007", stims, 1.0, 10, degree=4, objective=TRACK)
+    r_ref, r_nat = _both(ocp, 2, _starts(ocp, 2, 0), tol=1e-6)
+    _compare(ocp, r_ref, r_nat)
+
+
+def test_native_ipm_fixed_values_per_instance():
+    """Per-instance values of the fixed variables (each NMPC scenario's own initial state)."""
+    cfg = dict(cases.cfg3(), objective=TRACK)
+    ocp = cases.product_ocp(**cfg)
+    lb, ub = ocp.bounds_vector()
+    nfix = int((lb == ub).sum())
+    fixed = np.stack([np.linspace(0.0, 0.3, nfix), np.linspace(0.0, 20.0, nfix)])
+    r_ref, r_nat = _both(ocp, 2, _starts(ocp, 2, 3), fixed_values=fixed)
+    _compare(ocp, r_ref, r_nat)
+    np.testing.assert_array_equal(r_nat.v[:, lb == ub], fixed)
+
+
+def test_native_ipm_msk_rk4x5():
+    """BASELINE config 5 (arm26 biceps / triceps + Ding2007 with fatigue) at RK4 x 5, batch 1."""
+    import bench
+
+    ocp = bench.msk_build(5)
+    r_ref, r_nat = _both(ocp, 1, _starts(ocp, 1, 0), tol=1e-6, max_iter=1000)
+    _compare(ocp, r_ref, r_nat, vtol=1e-4, ftol=1e-6, it_slack=40)
+
+
+def test_native_ipm_rejects_bad_input():
+    from cocofest_amd import _cfx
+    from cocofest_amd.solver import NativeIpm
+
+    ocp = cases.product_ocp(**cases.cfg2())
+    nat = NativeIpm(ocp, batch=2)
+    with pytest.raises(_cfx.CfxError):
+        nat.ipm.solve(np.zeros((3, nat.n)))
+    with pytest.raises(_cfx.CfxError):
+        nat.ipm.solve(np.zeros((2, nat.n)), fixed_values=np.zeros(7))
+    nat.close()
+    h = ocp.nlp(batch=4, layout="soa")
+    lb, ub = ocp.bounds_vector()
+    with pytest.raises(_cfx.CfxError):
+        _cfx.Ipm(h, lb, ub)  # batched solves need the AoS layout
+    with pytest.raises(_cfx.CfxError):
+        _cfx.Ipm(ocp.nlp(batch=1), lb, ub, options={"max_backtrack": 0})
+    h.close()
