@@ -115,7 +115,7 @@ def convergence(device):
     """Second half of the BASELINE metric: wall-clock to an Ipopt-equivalent KKT point (tol 1e-6) of the batched
     interior-point driver over libcfx (cocofest_amd/solver.py), single instance and multi-start batch."""
     from cocofest_amd import ModelMaker, OcpFes, OdeSolver
-    from cocofest_amd.solver import BatchedIpm, IpmOptions
+    from cocofest_amd.solver import IpmOptions, NativeIpm
 
     out = {}
     # cfg 3: Ding2007 pulse width, 30 pulses, N = 100, force tracking (reference force curve), RK1 x 10
@@ -135,7 +135,7 @@ def convergence(device):
             free = lb != ub
             v0[:, free] = np.clip(v0[:, free] + rng.uniform(0, 1, (B, free.sum())) * np.minimum(ub[free] - lb[free], 10),
                                   lb[free], ub[free])
-        ipm = BatchedIpm(ocp, batch=B, device=device, options=IpmOptions(tol=1e-6, max_iter=300))
+        ipm = NativeIpm(ocp, batch=B, device=device, options=IpmOptions(tol=1e-6, max_iter=300))
         ipm.solve(v0[:, :] if B > 1 else None)  # warm-up (kernel loading, allocator)
         ipm.calls = {k: 0 for k in ipm.calls}
         res = ipm.solve(v0 if B > 1 else None)
@@ -366,11 +366,11 @@ def msk_section(device, tp, ocp1, cpu_seconds=0.0):
     """The N = 1 extras of the cfg-5 section: the C port's CPU baseline on a bounded sample of the same workload,
     and the batched interior point's wall-clock to convergence at RK4 x 5 (the default RK4 x 1 is infeasible for
     Ding2007's tau_c)."""
-    from cocofest_amd.solver import BatchedIpm, IpmOptions
+    from cocofest_amd.solver import IpmOptions, NativeIpm
 
     out = dict(tp)
     out["cpu_baseline"] = msk_cpu_baseline(ocp1, cpu_seconds) if cpu_seconds > 0 else None
-    ipm = BatchedIpm(msk_build(5), batch=1, device=device, options=IpmOptions(tol=1e-6, max_iter=1000))
+    ipm = NativeIpm(msk_build(5), batch=1, device=device, options=IpmOptions(tol=1e-6, max_iter=1000))
     res = ipm.solve()
     ipm.close()
     out["convergence_rk4x5"] = {"wall_s": res.wall_time, "converged": int(res.converged.sum()),

@@ -121,7 +121,7 @@ class FesNmpc:
     def solve(self, n_cycles: int, x0=None, hist=None):
         """Advance until ``n_cycles`` cycles are committed.  x0: (B, nx) initial states (default rest).
         Returns an NmpcResult with the committed trajectory of every scenario."""
-        from .solver import BatchedIpm
+        from .solver import BatchedIpm, NativeIpm
 
         B, T = self.B, self.T
         nx = self.model.nb_state
@@ -149,7 +149,7 @@ class FesNmpc:
                     ipm = BatchedIpm(ocp, batch=B, options=self.options, handle=self.evaluator(ocp, B),
                                      torch_device=self.torch_device, band=self.band)
                 else:
-                    ipm = BatchedIpm(ocp, batch=B, device=self.device, options=self.options)
+                    ipm = NativeIpm(ocp, batch=B, device=self.device, options=self.options)
                 cache[key] = (ocp, ipm)
             ocp, ipm = cache[key]
             v0 = np.tile(ocp.initial_guess_vector(), (B, 1)) if warm is None else warm

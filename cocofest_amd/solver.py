@@ -630,6 +630,8 @@ class NativeIpm:
         self.h = ocp.nlp(batch=batch, layout="aos", device=device)
         self.n, self.m = self.h.nv, self.h.ng
         lb, ub = ocp.bounds_vector()
+        self.fixed = np.where(lb == ub)[0]
+        self.free = np.where(lb != ub)[0]
         self.ipm = _cfx.Ipm(self.h, lb, ub, int(getattr(ocp, "n_params", 0) or 0),
                             {k: getattr(self.opt, k) for k in _NATIVE_OPTIONS})
         self.calls = {"eval_all": 0, "eval_h": 0, "eval_g_f": 0, "kkt_factor": 0}
@@ -658,7 +660,8 @@ def solve_ocp(ocp, solver=None, batch: int = 1, device: int = 0, v0=None, **kwar
         for k in ("tol", "max_iter"):
             if hasattr(solver, k):
                 setattr(opts, k, getattr(solver, k))
-    ipm = BatchedIpm(ocp, batch=batch, device=device, options=opts)
+    # the product path is libcfx's own solver; BatchedIpm only for what it alone offers (iterative refinement)
+    ipm = (BatchedIpm if opts.refine else NativeIpm)(ocp, batch=batch, device=device, options=opts)
     try:
         return ipm.solve(v0)
     finally:
