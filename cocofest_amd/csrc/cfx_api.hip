@@ -682,6 +682,8 @@ extern "C" int cfx_create(const cfx_problem* p, cfx_handle** out) {
         const int64_t nch = nchunk_of(h->model, h->scheme, h->tmax, nz);
         int64_t kpt = (int64_t)N * bx * nch / 2048;
         kp.kpt = (int32_t)std::max<int64_t>(1, std::min<int64_t>(N, kpt));
+        if (const char* e = std::getenv("CFX_KPT"))  // tuning override
+            kp.kpt = (int32_t)std::max<int64_t>(1, std::min<int64_t>(N, std::atoi(e)));
     }
 
     if (hipSetDevice(h->device) != hipSuccess) return create_fail(h, CFX_EHIP, "cfx_create: hipSetDevice failed");
@@ -850,7 +852,10 @@ extern "C" int cfx_eval_all(cfx_handle* h, const double* v, double* g, double* j
                                h->stream, h->kp, h->d_sl_param,
                                h->d_sl_joff, h->prob.intensity_floor, V, G, J);
     }
-    if (F || GR) {
+    if ((F || GR) && B < kObjBlockMaxB) {  // latency-bound: a block per instance, a thread per node
+        hipLaunchKernelGGL(k_objective_blk, dim3((unsigned)B), dim3(256), 0, h->stream, h->kp, h->n_obj, h->d_obj,
+                           h->d_targets, V, F, GR);
+    } else if (F || GR) {
         if (GR) CFX_HIP(h, hipMemsetAsync(GR, 0, (size_t)B * h->sz.nv * sizeof(double), h->stream));
         hipLaunchKernelGGL(k_objective, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, h->stream, h->kp, h->n_obj,
                            h->d_obj, h->d_targets, V, F, GR);
@@ -905,7 +910,10 @@ extern "C" int cfx_eval_h(cfx_handle* h, const double* v, const double* obj_fact
     else
         CFX_HIP(h, launch_hessian(h->model, h->scheme, h->tmax, h->kp, h->d_htasks, h->n_htasks, h->hbs, V, LAM, H,
                                   h->stream));
-    if (h->n_obj)
+    if (h->n_obj && B < kObjBlockMaxB)
+        hipLaunchKernelGGL(k_objective_hess_blk, dim3((unsigned)B), dim3(256), 0, h->stream, h->kp, h->n_obj,
+                           h->d_obj, OF, H);
+    else if (h->n_obj)
         hipLaunchKernelGGL(k_objective_hess, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, h->stream, h->kp,
                            h->n_obj, h->d_obj, OF, H);
     CFX_HIP(h, hipGetLastError());

@@ -62,6 +62,59 @@ __global__ void __launch_bounds__(256) k_objective_hess(const KParams P, int n_o
     }
 }
 
+// Small batches (latency-bound: the interior point at batch 1): one block per instance, a thread per node.
+// Every term of a node is handled by that node's thread, so no two threads touch one gradient or Hessian entry;
+// the block zeroes its own gradient first (no separate memset), f is a block sum in a fixed order.
+constexpr int64_t kObjBlockMaxB = 2048;
+
+__device__ inline double block_sum256(double v, double* sh) {
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
+    __syncthreads();
+    return sh[0] + sh[1] + sh[2] + sh[3];
+}
+
+__global__ void __launch_bounds__(256) k_objective_blk(const KParams P, int n_obj, const DevObjective* __restrict__ obj,
+                                                       const double* __restrict__ targets,
+                                                       const double* __restrict__ V, double* __restrict__ F,
+                                                       double* __restrict__ GRAD) {
+    __shared__ double sh[4];
+    const int64_t b = blockIdx.x;
+    const int64_t ES = lay_stride(P), vb = lay_base(P, P.nv_tot, b);
+    if (GRAD) {
+        for (int64_t e = threadIdx.x; e < P.nv_tot; e += 256) GRAD[vb + e * ES] = 0.0;
+        __syncthreads();
+    }
+    double f = 0.0;
+    for (int k = threadIdx.x; k <= P.N; k += 256)
+        for (int t = 0; t < n_obj; ++t) {
+            const DevObjective o = obj[t];
+            if (k < o.node_first || k > o.node_last) continue;
+            const int64_t off = (int64_t)k * P.nz + (o.var_kind == 0 ? 0 : P.uoff) + o.var_index;
+            const double d = V[vb + off * ES] - (o.target_off >= 0 ? targets[o.target_off + k] : o.target_value);
+            f += o.w_eff * d * d;
+            if (GRAD) GRAD[vb + off * ES] += 2.0 * o.w_eff * d;
+        }
+    f = block_sum256(f, sh);
+    if (F && threadIdx.x == 0) F[b] = f;
+}
+
+__global__ void __launch_bounds__(256) k_objective_hess_blk(const KParams P, int n_obj,
+                                                            const DevObjective* __restrict__ obj,
+                                                            const double* __restrict__ obj_factor,
+                                                            double* __restrict__ H) {
+    const int64_t B = P.B;
+    const int64_t b = blockIdx.x;
+    const double s = obj_factor[b];
+    for (int k = threadIdx.x; k <= P.N; k += 256)
+        for (int t = 0; t < n_obj; ++t) {
+            const DevObjective o = obj[t];
+            if (k < o.node_first || k > o.node_last) continue;
+            const int e = (o.var_kind == 0 ? 0 : P.nx) + o.var_index;
+            H[(int64_t)P.hdiag[k * (P.nx + P.nu) + e] * B + b] += 2.0 * o.w_eff * s;
+        }
+}
+
 // Hmed sliding-window rows (custom_constraints.py:102-119): g = u_k[j] - window_k(p)[j], J = +1 / -1.
 // slot (k, j): param index or -1 for the intensity-floor padding; joff = J offset of its +1 entry.
 // Thread = (instance, slot): its two loads precede its stores (a per-instance loop over the slots would issue
