@@ -31,8 +31,12 @@ def main(src, dst, algorithmic_bytes):
     stats = next(src.rglob("*kernel_stats.csv"), None)
     kern = {}
     if stats:
+        # the headline launch: the k_shooting instantiation with the most GPU time (the bench command also runs
+        # small k_shooting launches inside its convergence sections)
+        best = 0.0
         for row in csv.DictReader(open(stats)):
-            if "k_shooting" in row["Name"]:
+            if "k_shooting" in row["Name"] and float(row["TotalDurationNs"]) > best:
+                best = float(row["TotalDurationNs"])
                 kern = {"name": row["Name"], "calls": int(row["Calls"]), "avg_ns": float(row["AverageNs"]),
                         "min_ns": float(row["MinNs"]), "max_ns": float(row["MaxNs"])}
         (dst / "kernel_stats.csv").write_text(stats.read_text())
