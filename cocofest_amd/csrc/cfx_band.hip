@@ -30,6 +30,7 @@
 #include <type_traits>
 
 #include "../../include/cfx.h"
+#include "cfx_internal.h"
 
 extern thread_local std::string g_create_error;
 
@@ -678,6 +679,20 @@ __global__ void __launch_bounds__(64) k_band_solve_reg(int n, int kl, int ku, in
                      RHS + b * (int64_t)n * nrhs);
 }
 
+// Right-hand sides solved in parallel, one wavefront each (grid (batch, nx + (Y ? 1 : 0))): column c < nx of
+// instance b at X + b x_inst + c x_rhs, the extra one at Y + b y_inst.  For the bordered KKT solves of the
+// interior point (cfx_ipm.hip), where the border's columns are as many right-hand sides as the band is wide.
+template <int KC, int D>
+__global__ void __launch_bounds__(64) k_band_solve_reg_multi(int n, int kl, int ku, const double* __restrict__ AB,
+                                                             const int32_t* __restrict__ IPIV, double* X,
+                                                             int64_t x_inst, int64_t x_rhs, int nx, double* Y,
+                                                             int64_t y_inst) {
+    const int64_t b = blockIdx.x;
+    const int c = blockIdx.y;
+    double* xs = c < nx ? X + b * x_inst + (int64_t)c * x_rhs : Y + b * y_inst;
+    reg_solve<KC, D>(n, kl, ku, 1, AB + b * (int64_t)n * (2 * kl + ku + 1), IPIV + b * n, xs);
+}
+
 // ---------------------------------------------------------------------------------------------------
 // dispatch
 // ---------------------------------------------------------------------------------------------------
@@ -818,6 +833,35 @@ static int band_launch(int64_t n, int32_t kl, int32_t ku, int64_t batch, double*
 }
 
 }  // namespace cfx
+
+// internal (cfx_internal.h): does the register placement apply to (n, kl, ku)
+int cfx_band_reg_ok(int64_t n, int32_t kl, int32_t ku) { return cfx::reg_chunks(n, kl, ku) > 0; }
+
+// internal (cfx_internal.h): parallel right-hand sides with the factors of cfx_band_lu (register placement only)
+int cfx_band_solve_multi(int64_t n, int32_t kl, int32_t ku, int64_t batch, const double* ab, const int32_t* ipiv,
+                         double* X, int64_t x_inst, int64_t x_rhs, int32_t nx, double* Y, int64_t y_inst,
+                         void* stream) {
+    const int nch = cfx::reg_chunks(n, kl, ku);
+    const int ny = Y ? 1 : 0;
+    if (nch <= 0 || batch < 1 || batch > 0x7fffffff || nx < 0 || nx + ny < 1 || nx + ny > 65535 || (nx && !X)) {
+        g_create_error = "cfx_band_solve_multi: invalid argument";
+        return CFX_EINVAL;
+    }
+    const dim3 grid((unsigned)batch, (unsigned)(nx + ny));
+    const hipStream_t s = (hipStream_t)stream;
+    if (8 * nch + ku <= 64)
+        hipLaunchKernelGGL((cfx::k_band_solve_reg_multi<1, 8>), grid, dim3(64), 0, s, (int)n, kl, ku, ab, ipiv, X,
+                           x_inst, x_rhs, nx, Y, y_inst);
+    else
+        hipLaunchKernelGGL((cfx::k_band_solve_reg_multi<2, 2>), grid, dim3(64), 0, s, (int)n, kl, ku, ab, ipiv, X,
+                           x_inst, x_rhs, nx, Y, y_inst);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        g_create_error = std::string("cfx_band_solve_multi: ") + hipGetErrorString(e);
+        return CFX_EHIP;
+    }
+    return CFX_OK;
+}
 
 extern "C" int cfx_band_lu(int64_t n, int32_t kl, int32_t ku, int64_t batch, double* ab, int32_t* ipiv, int32_t* info,
                            int32_t nrhs, double* rhs, void* stream) {

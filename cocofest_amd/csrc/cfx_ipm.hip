@@ -39,6 +39,7 @@ constexpr int kIB = 256;    // threads per instance block
 constexpr int kFilt = 64;   // filter entries per instance (a ring, as solver.py)
 constexpr int kSlots = 64;  // counter ring: one 4-int slot per host read
 constexpr int kMaxY = 65535;
+constexpr int kMaxBorder = 32;  // free parameters handled as a dense border
 
 // per-instance scalars of the iteration
 struct Scal {
@@ -62,6 +63,11 @@ struct IpmK {
     const int32_t *jrw_ptr, *jrw_idx;  // triplets of each constraint row (row scaling)
     const int32_t *kkt_ptr, *kkt_src;  // sources of each band-storage entry
     const int32_t* pos;                // KKT unknown (free variables, then rows) -> band order
+    // bordered KKT (Hmed intensity parameters, whose sliding windows couple most stages): the band holds the nA
+    // unknowns other than the np free parameters, which form a dense border [[A, Cr], [Cc, D]] solved by a
+    // Schur complement (np <= kMaxBorder); np = 0: the whole KKT matrix is one band
+    int nA, np;
+    int64_t NE_A, NE_tot;  // band-storage entries of A; all assembled entries (band, Cr, Cc, D)
     // per instance
     double *x, *zl, *zu, *dx, *dzl, *dzu, *xt, *xacc, *xr, *dxr, *sig, *gF;  // [B][nf]
     double *rhs, *rb;                                                       // [B][nK]
@@ -69,7 +75,9 @@ struct IpmK {
     double *vx, *vt, *grad;                                                 // [B][n]
     double *jac, *jv, *hv;                                                  // [B][nnzj], [B][nj], [B][nnzh]
     double *fraw, *ft, *of;                                                 // [B]
-    double* ab;                                                             // [B][nK][ldab]
+    double* ab;                                                             // [B][nA][ldab]
+    double *Xb, *Ccb, *Db, *Sf;  // [B][np][nA] Cr -> A^-1 Cr, [B][np][nA] Cc, [B][np][np] D, LU of the Schur complement
+    int32_t* Sp;                 // [B][np] its pivots
     int32_t *ipiv, *info;                                                   // [B][nK], [B]
     double* filt;                                                           // [B][kFilt][2]
     Scal* sc;                                                               // [B]
@@ -356,7 +364,7 @@ __global__ void __launch_bounds__(kIB) k_ipm_begin(const IpmK K, int mode, int s
 __global__ void __launch_bounds__(kIB) k_ipm_kkt(const IpmK K, int mode) {
     const int64_t b = blockIdx.x;
     const int64_t p = (int64_t)blockIdx.y * kIB + threadIdx.x;
-    const int64_t NE = (int64_t)K.nK * K.ldab;
+    const int64_t NE = K.NE_tot;
     if (p < NE) {
         double v = 0.0;
         const double* hv = K.hv + b * K.nnzh;
@@ -375,7 +383,18 @@ __global__ void __launch_bounds__(kIB) k_ipm_kkt(const IpmK K, int mode) {
                 default: v -= K.o.delta_c; break;
             }
         }
-        K.ab[b * NE + p] = v;
+        if (p < K.NE_A) {
+            K.ab[b * K.NE_A + p] = v;
+        } else {  // the border: Cr (column-major, as right-hand sides of A), Cc (row-major), D
+            const int64_t nb = (int64_t)K.np * K.nA;
+            int64_t q = p - K.NE_A;
+            if (q < nb)
+                K.Xb[b * nb + q] = v;
+            else if ((q -= nb) < nb)
+                K.Ccb[b * nb + q] = v;
+            else
+                K.Db[b * K.np * K.np + (q - nb)] = v;
+        }
     }
     if (p < K.nK) {
         const int nf = K.nf;
@@ -388,6 +407,105 @@ __global__ void __launch_bounds__(kIB) k_ipm_kkt(const IpmK K, int mode) {
             r = p < nf ? 0.0 : -K.gS[b * K.m + (p - nf)];
         K.rb[b * K.nK + K.pos[p]] = r;
     }
+}
+
+// Bordered KKT: after the band factorisation of A and the solves A^-1 [Cr | r_A] (X and the band part of rb),
+// the Schur complement S = D - Cc A^-1 Cr (np x np, LU with partial pivoting in LDS, kept for the second-order
+// corrections: factor = 0 re-uses it), x_p = S^-1 (r_p - Cc y) and x_A = y - (A^-1 Cr) x_p, written back into rb.
+// A zero pivot of S is reported in info (nA + k + 1, LAPACK style) like one of A.
+__global__ void __launch_bounds__(kIB) k_ipm_schur(const IpmK K, int factor) {
+    __shared__ double S[kMaxBorder][kMaxBorder + 1];
+    __shared__ double sv[kMaxBorder];
+    __shared__ int piv[kMaxBorder];
+    __shared__ int sing;
+    const int64_t b = blockIdx.x;
+    const int nA = K.nA, np = K.np, t = threadIdx.x;
+    const double* X = K.Xb + b * np * nA;
+    const double* Cc = K.Ccb + b * np * nA;
+    double* rb = K.rb + b * K.nK;
+    double* Sf = K.Sf + b * np * np;
+    int32_t* Sp = K.Sp + b * np;
+    if (factor) {
+        for (int e = t; e < np * np; e += kIB) {
+            const int i = e / np, j = e - (e / np) * np;
+            double acc = K.Db[b * np * np + e];
+            for (int a = 0; a < nA; ++a) acc -= Cc[i * nA + a] * X[j * nA + a];
+            S[i][j] = acc;
+        }
+        if (t == 0) sing = 0;
+        __syncthreads();
+        for (int k = 0; k < np; ++k) {
+            if (t < 64) {  // first largest |S(i, k)|, i >= k
+                double a = (t >= k && t < np) ? fabs(S[t][k]) : -1.0;
+                int idx = t;
+                for (int o = 32; o > 0; o >>= 1) {
+                    const double a2 = __shfl_xor(a, o, 64);
+                    const int i2 = __shfl_xor(idx, o, 64);
+                    if (a2 > a || (a2 == a && i2 < idx)) {
+                        a = a2;
+                        idx = i2;
+                    }
+                }
+                if (t == 0) piv[k] = idx;
+            }
+            __syncthreads();
+            const int p = piv[k];
+            if (p != k && t < np) {
+                const double tmp = S[k][t];
+                S[k][t] = S[p][t];
+                S[p][t] = tmp;
+            }
+            __syncthreads();
+            const double pv = S[k][k];
+            const double inv = pv != 0.0 ? 1.0 / pv : 0.0;
+            if (t == 0 && pv == 0.0 && !sing) sing = nA + k + 1;
+            if (t > k && t < np) S[t][k] *= inv;
+            __syncthreads();
+            const int w = np - k - 1;
+            for (int e = t; e < w * w; e += kIB) {
+                const int i = k + 1 + e / w, j = k + 1 + e - (e / w) * w;
+                S[i][j] -= S[i][k] * S[k][j];
+            }
+            __syncthreads();
+        }
+        for (int e = t; e < np * np; e += kIB) Sf[e] = S[e / np][e - (e / np) * np];
+        if (t < np) Sp[t] = piv[t];
+        if (t == 0 && sing && K.info[b] == 0) K.info[b] = sing;
+    } else {
+        for (int e = t; e < np * np; e += kIB) S[e / np][e - (e / np) * np] = Sf[e];
+        if (t < np) piv[t] = Sp[t];
+    }
+    // s = r_p - Cc y
+    for (int i = t; i < np; i += kIB) {
+        double acc = rb[nA + i];
+        for (int a = 0; a < nA; ++a) acc -= Cc[i * nA + a] * rb[a];
+        sv[i] = acc;
+    }
+    __syncthreads();
+    if (t == 0) {  // x_p = S^-1 s (getrs: interchanges, unit-lower, upper)
+        for (int k = 0; k < np; ++k) {
+            const int p = piv[k];
+            if (p != k) {
+                const double tmp = sv[k];
+                sv[k] = sv[p];
+                sv[p] = tmp;
+            }
+        }
+        for (int k = 0; k < np; ++k)
+            for (int i = k + 1; i < np; ++i) sv[i] -= S[i][k] * sv[k];
+        for (int k = np - 1; k >= 0; --k) {
+            double acc = sv[k];
+            for (int j = k + 1; j < np; ++j) acc -= S[k][j] * sv[j];
+            sv[k] = acc / S[k][k];
+        }
+    }
+    __syncthreads();
+    for (int a = t; a < nA; a += kIB) {
+        double acc = rb[a];
+        for (int c = 0; c < np; ++c) acc -= X[c * nA + a] * sv[c];
+        rb[a] = acc;
+    }
+    for (int c = t; c < np; c += kIB) rb[nA + c] = sv[c];
 }
 
 // Newton step in natural order and the curvature test (solver.py inertia loop); bumps dw where it fails.
@@ -1052,53 +1170,88 @@ extern "C" int cfx_ipm_create(cfx_handle* h, const double* lb, const double* ub,
         for (int r = 0; r < m; ++r) key[r] = std::isfinite(cmin[r]) ? 0.5 * (cmin[r] + cmax[r]) + 0.25 : nf;
         return key;
     };
-    std::vector<double> ckey = row_keys(vkey, true);
-    if (anypar) {
-        std::vector<double> ssum(nf, 0.0), cnt(nf, 0.0);
-        for (int s2 = 0; s2 < nj; ++s2) {
-            ssum[jcF[s2]] += ckey[jrF[s2]];
-            cnt[jcF[s2]] += 1.0;
-        }
-        for (int i = 0; i < nf; ++i)
-            if (par[i] && cnt[i] > 0) vkey[i] = ssum[i] / std::max(cnt[i], 1.0) + 0.1;
-        ckey = row_keys(vkey, false);
-    }
     const int nK = nf + m;
-    std::vector<double> key(vkey);
-    key.insert(key.end(), ckey.begin(), ckey.end());
-    std::vector<int32_t> order(nK);
-    std::iota(order.begin(), order.end(), 0);
-    std::stable_sort(order.begin(), order.end(), [&](int32_t a, int32_t c) { return key[a] < key[c]; });
-    std::vector<int32_t> pos(nK);
-    for (int k = 0; k < nK; ++k) pos[order[k]] = k;
-    // KKT entries in band order: H (both triangles), J, J^T, diag_x, diag_y
-    std::vector<int64_t> rows, cols;
-    std::vector<int32_t> src;
-    auto add = [&](int64_t r, int64_t c, int32_t code) {
-        rows.push_back(r);
-        cols.push_back(c);
-        src.push_back(code);
-    };
-    for (int s2 = 0; s2 < nh; ++s2) add(pos[hrF[s2]], pos[hcF[s2]], (SRC_W << kSrcShift) | s2);
+    int np_free = 0;
+    for (int i = 0; i < nf; ++i) np_free += par[i];
+    // KKT entries: H (both triangles), J, J^T, diag_x, diag_y, as (unknown, unknown, source)
+    std::vector<int32_t> er, ec, src;
+    for (int s2 = 0; s2 < nh; ++s2) er.push_back(hrF[s2]), ec.push_back(hcF[s2]), src.push_back((SRC_W << kSrcShift) | s2);
     for (int s2 = 0; s2 < nh; ++s2)
-        if (hoff[s2]) add(pos[hcF[s2]], pos[hrF[s2]], (SRC_W << kSrcShift) | s2);
-    for (int s2 = 0; s2 < nj; ++s2) add(pos[nf + jrF[s2]], pos[jcF[s2]], (SRC_JV << kSrcShift) | s2);
-    for (int s2 = 0; s2 < nj; ++s2) add(pos[jcF[s2]], pos[nf + jrF[s2]], (SRC_JV << kSrcShift) | s2);
-    for (int i = 0; i < nf; ++i) add(pos[i], pos[i], (SRC_DIAG << kSrcShift) | i);
-    for (int j = 0; j < m; ++j) add(pos[nf + j], pos[nf + j], SRC_DC << kSrcShift);
-    int64_t kl = 0, ku = 0;
-    for (size_t e = 0; e < rows.size(); ++e) {
-        kl = std::max(kl, rows[e] - cols[e]);
-        ku = std::max(ku, cols[e] - rows[e]);
+        if (hoff[s2]) er.push_back(hcF[s2]), ec.push_back(hrF[s2]), src.push_back((SRC_W << kSrcShift) | s2);
+    for (int s2 = 0; s2 < nj; ++s2) er.push_back(nf + jrF[s2]), ec.push_back(jcF[s2]), src.push_back((SRC_JV << kSrcShift) | s2);
+    for (int s2 = 0; s2 < nj; ++s2) er.push_back(jcF[s2]), ec.push_back(nf + jrF[s2]), src.push_back((SRC_JV << kSrcShift) | s2);
+    for (int i = 0; i < nf; ++i) er.push_back(i), ec.push_back(i), src.push_back((SRC_DIAG << kSrcShift) | i);
+    for (int j = 0; j < m; ++j) er.push_back(nf + j), ec.push_back(nf + j), src.push_back(SRC_DC << kSrcShift);
+    // one ordering: border = true places the free parameters last (keys of the rows computed without them)
+    struct Order {
+        std::vector<int32_t> pos;
+        int64_t kl = 0, ku = 0;
+        int nA = 0;
+    };
+    auto make_order = [&](bool border) {
+        std::vector<double> vk(vkey);
+        std::vector<double> ck = row_keys(vk, true);
+        if (anypar) {
+            if (border) {
+                for (int i = 0; i < nf; ++i)
+                    if (par[i]) vk[i] = INFINITY;
+            } else {
+                std::vector<double> ssum(nf, 0.0), cnt(nf, 0.0);
+                for (int s2 = 0; s2 < nj; ++s2) {
+                    ssum[jcF[s2]] += ck[jrF[s2]];
+                    cnt[jcF[s2]] += 1.0;
+                }
+                for (int i = 0; i < nf; ++i)
+                    if (par[i] && cnt[i] > 0) vk[i] = ssum[i] / std::max(cnt[i], 1.0) + 0.1;
+                ck = row_keys(vk, false);
+            }
+        }
+        std::vector<double> key(vk);
+        key.insert(key.end(), ck.begin(), ck.end());
+        std::vector<int32_t> order(nK);
+        std::iota(order.begin(), order.end(), 0);
+        std::stable_sort(order.begin(), order.end(), [&](int32_t a, int32_t c) { return key[a] < key[c]; });
+        Order o;
+        o.pos.resize(nK);
+        for (int k = 0; k < nK; ++k) o.pos[order[k]] = k;
+        o.nA = border ? nK - np_free : nK;
+        for (size_t e = 0; e < er.size(); ++e) {
+            const int64_t r = o.pos[er[e]], c = o.pos[ec[e]];
+            if (r < o.nA && c < o.nA) {
+                o.kl = std::max(o.kl, r - c);
+                o.ku = std::max(o.ku, c - r);
+            }
+        }
+        return o;
+    };
+    Order ord = make_order(false);
+    // a dense border pays when the parameters widen the band past the one-wavefront factorisation and the rest
+    // is narrow enough for it (Hmed windows spanning most of the horizon: NMPC windows with T = N)
+    if (np_free >= 1 && np_free <= kMaxBorder && !cfx_band_reg_ok(nK, (int32_t)ord.kl, (int32_t)ord.ku)) {
+        Order ob = make_order(true);
+        if (cfx_band_reg_ok(ob.nA, (int32_t)ob.kl, (int32_t)ob.ku)) ord = ob;
     }
+    const std::vector<int32_t>& pos = ord.pos;
+    const int64_t kl = ord.kl, ku = ord.ku, nA = ord.nA, npb = nK - nA;
     const int64_t ldab = 2 * kl + ku + 1;
-    const int64_t NE = (int64_t)nK * ldab;
+    const int64_t NE_A = nA * ldab, NE = NE_A + 2 * npb * nA + npb * npb;
     if (nh >= (1 << kSrcShift) || nj >= (1 << kSrcShift) || NE >= INT32_MAX || (NE + kIB - 1) / kIB > kMaxY) {
         s->err = "cfx_ipm_create: KKT band too large";
         return create_fail(s, CFX_EUNSUPPORTED);
     }
-    std::vector<int64_t> flat(rows.size());
-    for (size_t e = 0; e < rows.size(); ++e) flat[e] = cols[e] * ldab + kl + ku + rows[e] - cols[e];
+    // assembled entry -> slot: band storage of A, then (border) Cr column-major, Cc row-major, D row-major
+    std::vector<int64_t> flat(er.size());
+    for (size_t e = 0; e < er.size(); ++e) {
+        const int64_t r = pos[er[e]], c = pos[ec[e]];
+        if (r < nA && c < nA)
+            flat[e] = c * ldab + kl + ku + r - c;
+        else if (r < nA)
+            flat[e] = NE_A + (c - nA) * nA + r;
+        else if (c < nA)
+            flat[e] = NE_A + npb * nA + (r - nA) * nA + c;
+        else
+            flat[e] = NE_A + 2 * npb * nA + (r - nA) * npb + (c - nA);
+    }
     std::vector<int32_t> kptr, kidx, kcode;
     csr(flat, NE, kptr, kidx);
     kcode.resize(kidx.size());
@@ -1114,6 +1267,10 @@ extern "C" int cfx_ipm_create(cfx_handle* h, const double* lb, const double* ub,
     K.kl = (int)kl;
     K.ku = (int)ku;
     K.ldab = (int)ldab;
+    K.nA = (int)nA;
+    K.np = (int)npb;
+    K.NE_A = NE_A;
+    K.NE_tot = NE;
     K.nfix = (int)fixedv.size();
     K.free = dupload(s, freev, &rc);
     K.fixed = dupload(s, fixedv, &rc);
@@ -1155,7 +1312,12 @@ extern "C" int cfx_ipm_create(cfx_handle* h, const double* lb, const double* ub,
     K.fraw = dalloc<double>(s, B, &rc);
     K.ft = dalloc<double>(s, B, &rc);
     K.of = dalloc<double>(s, B, &rc);
-    K.ab = dalloc<double>(s, B * NE, &rc);
+    K.ab = dalloc<double>(s, B * NE_A, &rc);
+    K.Xb = dalloc<double>(s, B * npb * nA, &rc);
+    K.Ccb = dalloc<double>(s, B * npb * nA, &rc);
+    K.Db = dalloc<double>(s, B * npb * npb, &rc);
+    K.Sf = dalloc<double>(s, B * npb * npb, &rc);
+    K.Sp = dalloc<int32_t>(s, B * npb, &rc);
     K.ipiv = dalloc<int32_t>(s, B * nK, &rc);
     K.info = dalloc<int32_t>(s, B, &rc);
     K.filt = dalloc<double>(s, B * kFilt * 2, &rc);
@@ -1171,6 +1333,11 @@ extern "C" int cfx_ipm_create(cfx_handle* h, const double* lb, const double* ub,
         s->err = "hipHostMalloc failed";
     }
     if (rc != CFX_OK) return create_fail(s, rc);
+    s->st.kkt_n = nK;
+    s->st.kkt_kl = kl;
+    s->st.kkt_ku = ku;
+    s->st.kkt_band_n = nA;
+    s->st.kkt_border = npb;
     *out = s;
     return CFX_OK;
 }
@@ -1205,11 +1372,31 @@ struct Run {
     }
     int kkt_factor(int mode) {
         const IpmK& K = s->K;
-        const int64_t NE = (int64_t)K.nK * K.ldab;
-        hipLaunchKernelGGL(k_ipm_kkt, dim3((unsigned)K.B, (unsigned)((NE + kIB - 1) / kIB)), dim3(kIB), 0, st, K, mode);
+        hipLaunchKernelGGL(k_ipm_kkt, dim3((unsigned)K.B, (unsigned)((K.NE_tot + kIB - 1) / kIB)), dim3(kIB), 0, st,
+                           K, mode);
         IPM_HIP(s, hipGetLastError());
-        IPM_BAND(s, cfx_band_lu(K.nK, K.kl, K.ku, K.B, K.ab, K.ipiv, K.info, 1, K.rb, st));
+        if (K.np) {  // bordered: factor A, solve A^-1 [Cr | r_A] (parallel right-hand sides), Schur complement
+            IPM_BAND(s, cfx_band_lu(K.nA, K.kl, K.ku, K.B, K.ab, K.ipiv, K.info, 0, nullptr, st));
+            IPM_BAND(s, cfx_band_solve_multi(K.nA, K.kl, K.ku, K.B, K.ab, K.ipiv, K.Xb, (int64_t)K.np * K.nA, K.nA,
+                                             K.np, K.rb, K.nK, st));
+            hipLaunchKernelGGL(k_ipm_schur, g, dim3(kIB), 0, st, K, 1);
+            IPM_HIP(s, hipGetLastError());
+        } else {
+            IPM_BAND(s, cfx_band_lu(K.nK, K.kl, K.ku, K.B, K.ab, K.ipiv, K.info, 1, K.rb, st));
+        }
         s->st.kkt_factor++;
+        return CFX_OK;
+    }
+    // another right-hand side (in rb, band order) with the factors of the last kkt_factor
+    int resolve() {
+        const IpmK& K = s->K;
+        if (K.np) {
+            IPM_BAND(s, cfx_band_solve_multi(K.nA, K.kl, K.ku, K.B, K.ab, K.ipiv, nullptr, 0, 0, 0, K.rb, K.nK, st));
+            hipLaunchKernelGGL(k_ipm_schur, g, dim3(kIB), 0, st, K, 0);
+            IPM_HIP(s, hipGetLastError());
+        } else {
+            IPM_BAND(s, cfx_band_lu_solve(K.nK, K.kl, K.ku, K.B, K.ab, K.ipiv, 1, K.rb, st));
+        }
         return CFX_OK;
     }
 };
@@ -1293,7 +1480,7 @@ static int ipm_solve(cfx_ipm* s, const double* v0, const double* fixed_values, d
             if (ls == 0)
                 for (int q = 0; q < K.o.max_soc && c[1] > 0; ++q) {
                     hipLaunchKernelGGL(k_ipm_soc_rhs, R.g, blk, 0, st, K);
-                    IPM_BAND(s, cfx_band_lu_solve(K.nK, K.kl, K.ku, K.B, K.ab, K.ipiv, 1, K.rb, st));
+                    IPM_RUN(R.resolve());
                     hipLaunchKernelGGL(k_ipm_soc_trial, R.g, blk, 0, st, K);
                     IPM_RUN(R.eval_gf(true));
                     sl = R.next_slot();

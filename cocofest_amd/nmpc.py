@@ -42,6 +42,7 @@ class NmpcResult:
     iterations: list = field(default_factory=list)   # per window: (B,) IPM iterations
     converged: list = field(default_factory=list)    # per window: (B,) bool
     window_wall: list = field(default_factory=list)  # per window: seconds
+    solve_wall: list = field(default_factory=list)   # per window: seconds inside the interior point
 
 
 class FesNmpc:
@@ -167,7 +168,9 @@ class FesNmpc:
                         fixed[:, fidx[p0 + j]] = hist_i[:, j]
             v0 = v0.copy()
             v0[:, ipm.fixed] = fixed
+            ts = time.perf_counter()
             res = ipm.solve(v0, fixed_values=fixed)
+            result.solve_wall.append(time.perf_counter() - ts)
             result.iterations.append(res.iterations)
             result.converged.append(res.converged)
             # commit the first n_adv cycles

@@ -282,6 +282,9 @@ typedef struct cfx_ipm_options {
 typedef struct cfx_ipm_stats {
     int64_t eval_all, eval_g_f, eval_h, kkt_factor, iterations, host_syncs;
     double wall_s; /* last cfx_ipm_solve */
+    /* KKT layout: unknowns, the band's half-bandwidths and unknowns, free parameters in a dense border (Schur
+       complement; 0: one band) */
+    int64_t kkt_n, kkt_kl, kkt_ku, kkt_band_n, kkt_border;
 } cfx_ipm_stats;
 
 typedef struct cfx_ipm cfx_ipm;

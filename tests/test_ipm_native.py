@@ -134,6 +134,33 @@ def test_native_ipm_msk_rk4x5():
     _compare(ocp, r_ref, r_nat, vtol=1e-4, ftol=1e-6, it_slack=40)
 
 
+@pytest.mark.parametrize("T", [5, 10])
+def test_native_ipm_nmpc_window_bordered_kkt(T):
+    """A cfg-4 NMPC window (Hmed2018 intensities, 10 pulses, history intensities as fixed leading parameters): with
+    T = 10 the parameters' sliding windows span the horizon, so the native solver factors the KKT matrix as a band
+    plus a dense parameter border (Schur complement) while BatchedIpm factors one wide band; both reach the same
+    point."""
+    from cocofest_amd import DingModelPulseIntensityFrequency, OdeSolver
+    from cocofest_amd.nmpc import FesNmpc
+    from cocofest_amd.solver import NativeIpm
+
+    model = DingModelPulseIntensityFrequency(stim_time=[round(0.1 * i, 1) for i in range(10)], sum_stim_truncation=T)
+    nm = FesNmpc(model, cycle_duration=1.0, n_cycles_simultaneous=1, n_cycles_to_advance=1, objective=TRACK,
+                 pulse_intensity={"max": 130}, ode_solver=OdeSolver.RK1(n_integration_steps=10), batch=1)
+    ocp = nm._window_ocp([-1e7] * T, np.full(T, float(model.min_pulse_intensity())))
+    lb, ub = ocp.bounds_vector()
+    fixed = np.tile(lb[lb == ub], (2, 1))
+    fixed[1, :2] = [0.2, 30.0]  # a second scenario starting from another state (as FesNmpc's x0 per scenario)
+    r_ref, r_nat = _both(ocp, 2, np.tile(ocp.initial_guess_vector(), (2, 1)), fixed_values=fixed)
+    assert r_ref.converged.all(), (r_ref.kkt_error, r_ref.iterations)
+    _compare(ocp, r_ref, r_nat)
+    nat = NativeIpm(ocp, batch=1)
+    st = nat.ipm.stats()
+    nat.close()
+    assert st["kkt_border"] == (10 if T == 10 else 0), st
+    assert st["kkt_band_n"] + st["kkt_border"] == st["kkt_n"]
+
+
 def test_native_ipm_rejects_bad_input():
     from cocofest_amd import _cfx
     from cocofest_amd.solver import NativeIpm
