@@ -684,6 +684,9 @@ extern "C" int cfx_create(const cfx_problem* p, cfx_handle** out) {
         kp.kpt = (int32_t)std::max<int64_t>(1, std::min<int64_t>(N, kpt));
         if (const char* e = std::getenv("CFX_KPT"))  // tuning override
             kp.kpt = (int32_t)std::max<int64_t>(1, std::min<int64_t>(N, std::atoi(e)));
+        // interval chunks as the fast grid index (tuning override; the instance blocks must fit grid.y)
+        if (const char* e = std::getenv("CFX_IFAST"))
+            kp.ifast = std::atoi(e) != 0 && bx <= kMaxGridY;
     }
 
     if (hipSetDevice(h->device) != hipSuccess) return create_fail(h, CFX_EHIP, "cfx_create: hipSetDevice failed");

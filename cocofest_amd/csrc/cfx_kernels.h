@@ -51,6 +51,7 @@ struct KParams {
     int32_t n_slide; // sliding-window rows per interval
     int32_t n_params;
     int32_t kpt;     // shooting intervals per thread
+    int32_t ifast;   // shooting launch: interval chunks on grid.x (fast), instance blocks on grid.y
     double dt, h;
     // model constants (reciprocals precomputed on the host)
     double inv_tauc, tau2, km_rest, tau1_rest, a_rest, a_scale, pd0, pdt;
@@ -488,9 +489,10 @@ template <int MODEL, int SCHEME, int D, int TMAX, int NI>
 __global__ void __launch_bounds__(256) k_shooting(const KParams P, const double* __restrict__ V,
                                                   double* __restrict__ G, double* __restrict__ J) {
     const int64_t B = P.B;
-    const int64_t b0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * NI;
+    const unsigned bi = P.ifast ? blockIdx.y : blockIdx.x, bk = P.ifast ? blockIdx.x : blockIdx.y;
+    const int64_t b0 = ((int64_t)bi * blockDim.x + threadIdx.x) * NI;
     if (b0 >= B) return;
-    const int k0 = blockIdx.y * P.kpt;
+    const int k0 = bk * P.kpt;
     const int k1 = min(P.N, k0 + P.kpt);
     const int chunk = is_int(MODEL) ? (int)blockIdx.z : 0;  // the other models carry every direction in one lane
 

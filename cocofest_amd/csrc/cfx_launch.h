@@ -75,7 +75,8 @@ hipError_t launch_shooting_t(const KParams& P, const double* V, double* G, doubl
     const int nz = P.nz;
     const int nchunk = D > 0 ? (nz + D - 1) / D : 1;
     const int64_t per_block = (int64_t)kBlock * NI;  // NI adjacent instances per lane
-    dim3 grid((unsigned)((P.B + per_block - 1) / per_block), (unsigned)((P.N + P.kpt - 1) / P.kpt), (unsigned)nchunk);
+    const unsigned nbi = (unsigned)((P.B + per_block - 1) / per_block), nbk = (unsigned)((P.N + P.kpt - 1) / P.kpt);
+    dim3 grid(P.ifast ? nbk : nbi, P.ifast ? nbi : nbk, (unsigned)nchunk);
     hipLaunchKernelGGL((k_shooting<MODEL, SCHEME, D, TMAX, NI>), grid, dim3(kBlock), 0, s, P, V, G, J);
     return hipGetLastError();
 }
