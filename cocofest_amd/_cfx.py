@@ -104,7 +104,7 @@ class IpmStats(C.Structure):
     _fields_ = [("eval_all", C.c_int64), ("eval_g_f", C.c_int64), ("eval_h", C.c_int64), ("kkt_factor", C.c_int64),
                 ("iterations", C.c_int64), ("host_syncs", C.c_int64), ("wall_s", C.c_double),
                 ("kkt_n", C.c_int64), ("kkt_kl", C.c_int64), ("kkt_ku", C.c_int64), ("kkt_band_n", C.c_int64),
-                ("kkt_border", C.c_int64)]
+                ("kkt_border", C.c_int64), ("kkt_blocks", C.c_int64)]
 
 
 # exported symbols and their signatures (must match include/cfx.h)

@@ -679,18 +679,20 @@ __global__ void __launch_bounds__(64) k_band_solve_reg(int n, int kl, int ku, in
                      RHS + b * (int64_t)n * nrhs);
 }
 
-// Right-hand sides solved in parallel, one wavefront each (grid (batch, nx + (Y ? 1 : 0))): column c < nx of
-// instance b at X + b x_inst + c x_rhs, the extra one at Y + b y_inst.  For the bordered KKT solves of the
-// interior point (cfx_ipm.hip), where the border's columns are as many right-hand sides as the band is wide.
+// Right-hand sides solved in parallel, one wavefront each (grid (batch, nx + (Y ? 1 : 0))).  The batch index
+// bb = b parts + q addresses system q of instance b (factors at bb); its column c < nx is at X + b x_inst +
+// q x_part + c x_rhs, the extra one at Y + b y_inst + q y_part.  For the bordered / dissected KKT solves of the
+// interior point (cfx_ipm.hip), where the border's columns are as many right-hand sides.
 template <int KC, int D>
 __global__ void __launch_bounds__(64) k_band_solve_reg_multi(int n, int kl, int ku, const double* __restrict__ AB,
-                                                             const int32_t* __restrict__ IPIV, double* X,
-                                                             int64_t x_inst, int64_t x_rhs, int nx, double* Y,
-                                                             int64_t y_inst) {
-    const int64_t b = blockIdx.x;
+                                                             const int32_t* __restrict__ IPIV, int parts, double* X,
+                                                             int64_t x_inst, int64_t x_part, int64_t x_rhs, int nx,
+                                                             double* Y, int64_t y_inst, int64_t y_part) {
+    const int64_t bb = blockIdx.x;
+    const int64_t b = bb / parts, q = bb - (bb / parts) * parts;
     const int c = blockIdx.y;
-    double* xs = c < nx ? X + b * x_inst + (int64_t)c * x_rhs : Y + b * y_inst;
-    reg_solve<KC, D>(n, kl, ku, 1, AB + b * (int64_t)n * (2 * kl + ku + 1), IPIV + b * n, xs);
+    double* xs = c < nx ? X + b * x_inst + q * x_part + (int64_t)c * x_rhs : Y + b * y_inst + q * y_part;
+    reg_solve<KC, D>(n, kl, ku, 1, AB + bb * (int64_t)n * (2 * kl + ku + 1), IPIV + bb * n, xs);
 }
 
 // ---------------------------------------------------------------------------------------------------
@@ -838,23 +840,24 @@ static int band_launch(int64_t n, int32_t kl, int32_t ku, int64_t batch, double*
 int cfx_band_reg_ok(int64_t n, int32_t kl, int32_t ku) { return cfx::reg_chunks(n, kl, ku) > 0; }
 
 // internal (cfx_internal.h): parallel right-hand sides with the factors of cfx_band_lu (register placement only)
-int cfx_band_solve_multi(int64_t n, int32_t kl, int32_t ku, int64_t batch, const double* ab, const int32_t* ipiv,
-                         double* X, int64_t x_inst, int64_t x_rhs, int32_t nx, double* Y, int64_t y_inst,
-                         void* stream) {
+int cfx_band_solve_multi(int64_t n, int32_t kl, int32_t ku, int64_t batch, int32_t parts, const double* ab,
+                         const int32_t* ipiv, double* X, int64_t x_inst, int64_t x_part, int64_t x_rhs, int32_t nx,
+                         double* Y, int64_t y_inst, int64_t y_part, void* stream) {
     const int nch = cfx::reg_chunks(n, kl, ku);
     const int ny = Y ? 1 : 0;
-    if (nch <= 0 || batch < 1 || batch > 0x7fffffff || nx < 0 || nx + ny < 1 || nx + ny > 65535 || (nx && !X)) {
+    if (nch <= 0 || batch < 1 || batch > 0x7fffffff || parts < 1 || batch % parts || nx < 0 || nx + ny < 1 ||
+        nx + ny > 65535 || (nx && !X)) {
         g_create_error = "cfx_band_solve_multi: invalid argument";
         return CFX_EINVAL;
     }
     const dim3 grid((unsigned)batch, (unsigned)(nx + ny));
     const hipStream_t s = (hipStream_t)stream;
     if (8 * nch + ku <= 64)
-        hipLaunchKernelGGL((cfx::k_band_solve_reg_multi<1, 8>), grid, dim3(64), 0, s, (int)n, kl, ku, ab, ipiv, X,
-                           x_inst, x_rhs, nx, Y, y_inst);
+        hipLaunchKernelGGL((cfx::k_band_solve_reg_multi<1, 8>), grid, dim3(64), 0, s, (int)n, kl, ku, ab, ipiv,
+                           parts, X, x_inst, x_part, x_rhs, nx, Y, y_inst, y_part);
     else
-        hipLaunchKernelGGL((cfx::k_band_solve_reg_multi<2, 2>), grid, dim3(64), 0, s, (int)n, kl, ku, ab, ipiv, X,
-                           x_inst, x_rhs, nx, Y, y_inst);
+        hipLaunchKernelGGL((cfx::k_band_solve_reg_multi<2, 2>), grid, dim3(64), 0, s, (int)n, kl, ku, ab, ipiv,
+                           parts, X, x_inst, x_part, x_rhs, nx, Y, y_inst, y_part);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         g_create_error = std::string("cfx_band_solve_multi: ") + hipGetErrorString(e);

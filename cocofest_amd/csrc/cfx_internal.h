@@ -15,9 +15,10 @@ extern thread_local std::string g_create_error;
 int cfx_internal_info(const cfx_handle* h, int64_t* batch, int* layout, int* device, hipStream_t* stream);
 
 // batched band LU helpers (cfx_band.hip): does the one-wavefront register placement apply; parallel right-hand
-// sides (one wavefront each) with the factors of cfx_band_lu: column c < nx of instance b at X + b x_inst +
-// c x_rhs, plus (Y != NULL) one at Y + b y_inst
+// sides (one wavefront each) with the factors of cfx_band_lu over batch = instances x parts systems: system q
+// of instance b has its column c < nx at X + b x_inst + q x_part + c x_rhs, plus (Y != NULL) one at
+// Y + b y_inst + q y_part
 int cfx_band_reg_ok(int64_t n, int32_t kl, int32_t ku);
-int cfx_band_solve_multi(int64_t n, int32_t kl, int32_t ku, int64_t batch, const double* ab, const int32_t* ipiv,
-                         double* X, int64_t x_inst, int64_t x_rhs, int32_t nx, double* Y, int64_t y_inst,
-                         void* stream);
+int cfx_band_solve_multi(int64_t n, int32_t kl, int32_t ku, int64_t batch, int32_t parts, const double* ab,
+                         const int32_t* ipiv, double* X, int64_t x_inst, int64_t x_part, int64_t x_rhs, int32_t nx,
+                         double* Y, int64_t y_inst, int64_t y_part, void* stream);

@@ -63,11 +63,19 @@ struct IpmK {
     const int32_t *jrw_ptr, *jrw_idx;  // triplets of each constraint row (row scaling)
     const int32_t *kkt_ptr, *kkt_src;  // sources of each band-storage entry
     const int32_t* pos;                // KKT unknown (free variables, then rows) -> band order
-    // bordered KKT (Hmed intensity parameters, whose sliding windows couple most stages): the band holds the nA
-    // unknowns other than the np free parameters, which form a dense border [[A, Cr], [Cc, D]] solved by a
-    // Schur complement (np <= kMaxBorder); np = 0: the whole KKT matrix is one band
-    int nA, np;
-    int64_t NE_A, NE_tot;  // band-storage entries of A; all assembled entries (band, Cr, Cc, D)
+    // KKT layout.  P = 1, np = 0: one band of nA = nK unknowns (factor + solve in one launch).  Otherwise the
+    // unknowns split into P diagonal band blocks of nA rows each (padded with unit rows) and a dense border of np
+    // unknowns — Hmed intensity parameters, whose sliding windows couple most stages, and the separators between
+    // the blocks (nested dissection of the stage chain, so that the P blocks factor side by side) — solved by a
+    // Schur complement on the border (np <= kMaxBorder).  rb (right-hand side / solution, per instance nKp =
+    // P nA + np): block q at q nA, the border at P nA.
+    int P, nA, np, nKp;
+    int64_t NE_A, NE_tot;  // band-storage entries of the P blocks; all assembled entries (bands, Cr, Cc, D)
+    // the border is sparse in the blocks: block q couples to na_q <= na border unknowns act[q][.] (its "active"
+    // columns: Cr_q and A_q^-1 Cr_q are stored for those only, slot sl[q][k] of border unknown k, -1: none), and
+    // Cc is a list of non-zeros grouped by border row (ccr_ptr; block ccr_q, block row ccr_a)
+    int na, ncc;
+    const int32_t *act, *sl, *ccr_ptr, *ccr_q, *ccr_a;
     // per instance
     double *x, *zl, *zu, *dx, *dzl, *dzu, *xt, *xacc, *xr, *dxr, *sig, *gF;  // [B][nf]
     double *rhs, *rb;                                                       // [B][nK]
@@ -75,10 +83,11 @@ struct IpmK {
     double *vx, *vt, *grad;                                                 // [B][n]
     double *jac, *jv, *hv;                                                  // [B][nnzj], [B][nj], [B][nnzh]
     double *fraw, *ft, *of;                                                 // [B]
-    double* ab;                                                             // [B][nA][ldab]
-    double *Xb, *Ccb, *Db, *Sf;  // [B][np][nA] Cr -> A^-1 Cr, [B][np][nA] Cc, [B][np][np] D, LU of the Schur complement
-    int32_t* Sp;                 // [B][np] its pivots
-    int32_t *ipiv, *info;                                                   // [B][nK], [B]
+    double* ab;                                                             // [B][P][nA][ldab]
+    // [B][P][na][nA] Cr -> A^-1 Cr (active columns), [B][ncc] Cc non-zeros, [B][np][np] D, LU of the Schur complement
+    double *Xb, *Ccb, *Db, *Sf;
+    int32_t* Sp;  // [B][np] its pivots
+    int32_t *ipiv, *info;                                                   // [B][P][nA], [B][P]
     double* filt;                                                           // [B][kFilt][2]
     Scal* sc;                                                               // [B]
     int32_t* cnt;                                                           // [kSlots][4]
@@ -380,20 +389,20 @@ __global__ void __launch_bounds__(kIB) k_ipm_kkt(const IpmK K, int mode) {
                     break;
                 case SRC_JV: v += jv[idx]; break;
                 case SRC_DIAG: v += mode == KKT_NEWTON ? sig[idx] + dw : (mode == KKT_LSMULT ? 1.0 : sig[idx] + 1.0); break;
-                default: v -= K.o.delta_c; break;
+                default: v += idx ? 1.0 : -K.o.delta_c; break;  // unit diagonal of a padding row / -delta_c
             }
         }
         if (p < K.NE_A) {
             K.ab[b * K.NE_A + p] = v;
-        } else {  // the border: Cr (column-major, as right-hand sides of A), Cc (row-major), D
-            const int64_t nb = (int64_t)K.np * K.nA;
+        } else {  // the border: Cr (active columns per block, as right-hand sides), Cc non-zeros, D
+            const int64_t nb = (int64_t)K.P * K.na * K.nA;
             int64_t q = p - K.NE_A;
             if (q < nb)
                 K.Xb[b * nb + q] = v;
-            else if ((q -= nb) < nb)
-                K.Ccb[b * nb + q] = v;
+            else if ((q -= nb) < K.ncc)
+                K.Ccb[b * K.ncc + q] = v;
             else
-                K.Db[b * K.np * K.np + (q - nb)] = v;
+                K.Db[b * K.np * K.np + (q - K.ncc)] = v;
         }
     }
     if (p < K.nK) {
@@ -405,31 +414,37 @@ __global__ void __launch_bounds__(kIB) k_ipm_kkt(const IpmK K, int mode) {
             r = p < nf ? -(K.gF[b * nf + p] - K.zl[b * nf + p] + K.zu[b * nf + p]) : 0.0;
         else
             r = p < nf ? 0.0 : -K.gS[b * K.m + (p - nf)];
-        K.rb[b * K.nK + K.pos[p]] = r;
+        K.rb[b * K.nKp + K.pos[p]] = r;
     }
 }
 
-// Bordered KKT: after the band factorisation of A and the solves A^-1 [Cr | r_A] (X and the band part of rb),
-// the Schur complement S = D - Cc A^-1 Cr (np x np, LU with partial pivoting in LDS, kept for the second-order
-// corrections: factor = 0 re-uses it), x_p = S^-1 (r_p - Cc y) and x_A = y - (A^-1 Cr) x_p, written back into rb.
-// A zero pivot of S is reported in info (nA + k + 1, LAPACK style) like one of A.
+// Bordered / dissected KKT: after the band factorisations of the P blocks A_q and the solves A_q^-1 [Cr_q | r_q]
+// (X and the block parts of rb), the Schur complement S = D - sum_q Cc_q A_q^-1 Cr_q (np x np, LU with partial
+// pivoting in LDS, kept for the second-order corrections: factor = 0 re-uses it), the border x_p =
+// S^-1 (r_p - sum_q Cc_q y_q) and the blocks x_q = y_q - (A_q^-1 Cr_q) x_p, written back into rb.  A zero pivot
+// of S is reported in info like one of a block (P nA + k + 1).
 __global__ void __launch_bounds__(kIB) k_ipm_schur(const IpmK K, int factor) {
     __shared__ double S[kMaxBorder][kMaxBorder + 1];
     __shared__ double sv[kMaxBorder];
     __shared__ int piv[kMaxBorder];
     __shared__ int sing;
     const int64_t b = blockIdx.x;
-    const int nA = K.nA, np = K.np, t = threadIdx.x;
-    const double* X = K.Xb + b * np * nA;
-    const double* Cc = K.Ccb + b * np * nA;
-    double* rb = K.rb + b * K.nK;
+    const int nA = K.nA, np = K.np, P = K.P, na = K.na, t = threadIdx.x;
+    const int64_t nb = (int64_t)na * nA;  // per block
+    const double* X = K.Xb + b * P * nb;
+    const double* Cc = K.Ccb + b * K.ncc;
+    double* rb = K.rb + b * K.nKp;
     double* Sf = K.Sf + b * np * np;
     int32_t* Sp = K.Sp + b * np;
+    const int PA = P * nA;
     if (factor) {
-        for (int e = t; e < np * np; e += kIB) {
+        for (int e = t; e < np * np; e += kIB) {  // S(i, j) = D(i, j) - sum over row i's Cc non-zeros
             const int i = e / np, j = e - (e / np) * np;
             double acc = K.Db[b * np * np + e];
-            for (int a = 0; a < nA; ++a) acc -= Cc[i * nA + a] * X[j * nA + a];
+            for (int z = K.ccr_ptr[i]; z < K.ccr_ptr[i + 1]; ++z) {
+                const int q = K.ccr_q[z], c = K.sl[q * np + j];
+                if (c >= 0) acc -= Cc[z] * X[q * nb + (int64_t)c * nA + K.ccr_a[z]];
+            }
             S[i][j] = acc;
         }
         if (t == 0) sing = 0;
@@ -458,7 +473,7 @@ __global__ void __launch_bounds__(kIB) k_ipm_schur(const IpmK K, int factor) {
             __syncthreads();
             const double pv = S[k][k];
             const double inv = pv != 0.0 ? 1.0 / pv : 0.0;
-            if (t == 0 && pv == 0.0 && !sing) sing = nA + k + 1;
+            if (t == 0 && pv == 0.0 && !sing) sing = PA + k + 1;
             if (t > k && t < np) S[t][k] *= inv;
             __syncthreads();
             const int w = np - k - 1;
@@ -470,15 +485,15 @@ __global__ void __launch_bounds__(kIB) k_ipm_schur(const IpmK K, int factor) {
         }
         for (int e = t; e < np * np; e += kIB) Sf[e] = S[e / np][e - (e / np) * np];
         if (t < np) Sp[t] = piv[t];
-        if (t == 0 && sing && K.info[b] == 0) K.info[b] = sing;
+        if (t == 0 && sing && K.info[b * P] == 0) K.info[b * P] = sing;
     } else {
         for (int e = t; e < np * np; e += kIB) S[e / np][e - (e / np) * np] = Sf[e];
         if (t < np) piv[t] = Sp[t];
     }
-    // s = r_p - Cc y
+    // s = r_p - sum_q Cc_q y_q
     for (int i = t; i < np; i += kIB) {
-        double acc = rb[nA + i];
-        for (int a = 0; a < nA; ++a) acc -= Cc[i * nA + a] * rb[a];
+        double acc = rb[PA + i];
+        for (int z = K.ccr_ptr[i]; z < K.ccr_ptr[i + 1]; ++z) acc -= Cc[z] * rb[K.ccr_q[z] * nA + K.ccr_a[z]];
         sv[i] = acc;
     }
     __syncthreads();
@@ -500,12 +515,16 @@ __global__ void __launch_bounds__(kIB) k_ipm_schur(const IpmK K, int factor) {
         }
     }
     __syncthreads();
-    for (int a = t; a < nA; a += kIB) {
-        double acc = rb[a];
-        for (int c = 0; c < np; ++c) acc -= X[c * nA + a] * sv[c];
-        rb[a] = acc;
+    for (int e = t; e < PA; e += kIB) {
+        const int q = e / nA, a = e - (e / nA) * nA;
+        double acc = rb[e];
+        for (int c = 0; c < na; ++c) {
+            const int k = K.act[q * na + c];
+            if (k >= 0) acc -= X[q * nb + (int64_t)c * nA + a] * sv[k];
+        }
+        rb[e] = acc;
     }
-    for (int c = t; c < np; c += kIB) rb[nA + c] = sv[c];
+    for (int c = t; c < np; c += kIB) rb[PA + c] = sv[c];
 }
 
 // Newton step in natural order and the curvature test (solver.py inertia loop); bumps dw where it fails.
@@ -515,7 +534,7 @@ __global__ void __launch_bounds__(kIB) k_ipm_curv(const IpmK K, int slot) {
     const int64_t b = blockIdx.x;
     const int nf = K.nf;
     load_scal(K, b, S);
-    const double* rb = K.rb + b * K.nK;
+    const double* rb = K.rb + b * K.nKp;
     double* dx = K.dx + b * nf;
     double* dy = K.dy + b * K.m;
     double nonfin = 0.0;
@@ -546,7 +565,9 @@ __global__ void __launch_bounds__(kIB) k_ipm_curv(const IpmK K, int slot) {
     nrm = breduce(nrm, OpSum(), sh);
     nonfin = breduce(nonfin, OpMax(), sh);
     const double curv = quad + dd;
-    const bool bad = !S.done && ((curv <= K.o.curv_min * nrm) || !isfinite(curv) || K.info[b] != 0 || nonfin > 0);
+    bool sing = false;
+    for (int q = 0; q < K.P; ++q) sing = sing || K.info[b * K.P + q] != 0;
+    const bool bad = !S.done && ((curv <= K.o.curv_min * nrm) || !isfinite(curv) || sing || nonfin > 0);
     if (threadIdx.x == 0 && bad) {
         if (S.dw == 0.0)
             S.dw = S.dwl > 0 ? clamp_lo(S.dwl / 3, 1e-20) : 1e-4;
@@ -695,7 +716,7 @@ __global__ void __launch_bounds__(kIB) k_ipm_soc_rhs(const IpmK K) {
     const double a = K.sc[b].alpha;
     const int nf = K.nf;
     for (int i = threadIdx.x; i < K.nK; i += kIB)
-        K.rb[b * K.nK + K.pos[i]] = i < nf ? K.rhs[b * K.nK + i] * a : -K.csoc[b * K.m + (i - nf)];
+        K.rb[b * K.nKp + K.pos[i]] = i < nf ? K.rhs[b * K.nK + i] * a : -K.csoc[b * K.m + (i - nf)];
 }
 
 // corrected trial x + a_c dx_c (into xr)
@@ -704,7 +725,7 @@ __global__ void __launch_bounds__(kIB) k_ipm_soc_trial(const IpmK K) {
     const int64_t b = blockIdx.x;
     const int nf = K.nf;
     const double* x = K.x + b * nf;
-    const double* rb = K.rb + b * K.nK;
+    const double* rb = K.rb + b * K.nKp;
     const double tau = K.sc[b].tau;
     double apl = INFINITY, apu = INFINITY;
     for (int i = threadIdx.x; i < nf; i += kIB) {
@@ -769,7 +790,7 @@ __global__ void __launch_bounds__(kIB) k_ipm_resto_init(const IpmK K, int slot) 
     const int nf = K.nf, m = K.m;
     load_scal(K, b, S);
     const double* x = K.x + b * nf;
-    const double* rb = K.rb + b * K.nK;
+    const double* rb = K.rb + b * K.nKp;
     double* dxr = K.dxr + b * nf;
     double apl = INFINITY, apu = INFINITY, th = 0.0;
     for (int i = threadIdx.x; i < nf; i += kIB) {
@@ -846,7 +867,7 @@ __global__ void __launch_bounds__(kIB) k_ipm_lsmult(const IpmK K) {
     load_scal(K, b, S);
     if (!S.reinit) return;  // block-uniform
     const int nf = K.nf, m = K.m;
-    const double* rb = K.rb + b * K.nK;
+    const double* rb = K.rb + b * K.nKp;
     double big = 0.0, nonfin = 0.0;
     for (int j = threadIdx.x; j < m; j += kIB) {
         const double v = rb[K.pos[nf + j]];
@@ -1231,27 +1252,167 @@ extern "C" int cfx_ipm_create(cfx_handle* h, const double* lb, const double* ub,
         Order ob = make_order(true);
         if (cfx_band_reg_ok(ob.nA, (int32_t)ob.kl, (int32_t)ob.ku)) ord = ob;
     }
-    const std::vector<int32_t>& pos = ord.pos;
-    const int64_t kl = ord.kl, ku = ord.ku, nA = ord.nA, npb = nK - nA;
+    // Nested dissection of the band (small batches, where one wavefront per instance leaves the chip idle and
+    // the band LU is a chain of nK pivot steps): cut the band order at P - 1 places where few unknowns couple across
+    // — the boundary B_c = {v >= c : v has a neighbour < c} separates [0, c) from [c, nA) \ B_c; at a stage
+    // boundary it is the next node's states — and move the separators into the dense border.  The P blocks then
+    // factor side by side (a batch of B P systems), the border by its Schur complement.
+    const int nAb = ord.nA, nparb = nK - ord.nA;  // band unknowns, parameters already in the border
+    std::vector<int32_t> minadj(nAb);
+    std::vector<std::vector<int32_t>> nbr(nAb);
+    for (int v = 0; v < nAb; ++v) minadj[v] = v;
+    for (size_t e = 0; e < er.size(); ++e) {
+        const int r = ord.pos[er[e]], c = ord.pos[ec[e]];
+        if (r < nAb && c < nAb && r != c) minadj[std::max(r, c)] = std::min(minadj[std::max(r, c)], std::min(r, c));
+    }
+    const int w = (int)std::max(ord.kl, ord.ku);
+    auto boundary = [&](int c) {  // B_c
+        std::vector<int32_t> bnd;
+        for (int v = c; v < std::min(nAb, c + w + 1); ++v)
+            if (minadj[v] < c) bnd.push_back(v);
+        return bnd;
+    };
+    struct Cut {
+        int P = 1;
+        std::vector<int32_t> slot;  // band position -> slot (block q: q nA + local; border: P nA + k), per band unknown
+        int nA = 0, nsep = 0;
+        int64_t kl = 0, ku = 0;
+    };
+    auto dissect = [&](int P) {
+        Cut d;
+        d.P = P;
+        std::vector<int32_t> cuts{0};
+        std::vector<uint8_t> sep(nAb, 0);
+        const double t = (double)nAb / P;
+        for (int k = 1; k < P; ++k) {
+            int best = -1;
+            size_t bsz = SIZE_MAX;
+            const int lo = std::max(cuts.back() + w + 2, (int)(k * t - t / 4)), hi = std::min(nAb - w - 2, (int)(k * t + t / 4));
+            for (int c = lo; c <= hi; ++c) {
+                const size_t z = boundary(c).size();
+                if (z < bsz || (z == bsz && std::abs(c - k * t) < std::abs(best - k * t))) {
+                    bsz = z;
+                    best = c;
+                }
+            }
+            if (best < 0) return Cut{};
+            cuts.push_back(best);
+            for (int v : boundary(best)) sep[v] = 1;
+        }
+        cuts.push_back(nAb);
+        std::vector<int32_t> part(nAb), local(nAb);
+        int nA = 0;
+        for (int q = 0; q < P; ++q) {
+            int l = 0;
+            for (int v = cuts[q]; v < cuts[q + 1]; ++v)
+                if (!sep[v]) part[v] = q, local[v] = l++;
+            nA = std::max(nA, l);
+        }
+        d.nA = nA;
+        d.slot.assign(nAb, -1);
+        int k = 0;
+        for (int v = 0; v < nAb; ++v) d.slot[v] = sep[v] ? P * nA + k++ : part[v] * nA + local[v];
+        d.nsep = k;
+        for (size_t e = 0; e < er.size(); ++e) {
+            const int r = ord.pos[er[e]], c = ord.pos[ec[e]];
+            if (r >= nAb || c >= nAb || sep[r] || sep[c]) continue;
+            if (part[r] != part[c]) return Cut{};  // not a separator (cannot happen for a boundary set)
+            d.kl = std::max<int64_t>(d.kl, local[r] - local[c]);
+            d.ku = std::max<int64_t>(d.ku, local[c] - local[r]);
+        }
+        return d;
+    };
+    Cut cut;
+    if (s->B <= 8 && nAb >= 96) {
+        for (int P = std::min(16, nAb / 24); P >= 2 && cut.P == 1; --P) {
+            Cut d = dissect(P);
+            if (d.P > 1 && d.nsep + nparb <= kMaxBorder && (int64_t)s->B * P <= 1024 &&
+                cfx_band_reg_ok(d.nA, (int32_t)d.kl, (int32_t)d.ku))
+                cut = d;
+        }
+    }
+    const int P = cut.P;
+    const int64_t kl = P > 1 ? cut.kl : ord.kl, ku = P > 1 ? cut.ku : ord.ku;
+    const int64_t nA = P > 1 ? cut.nA : nAb, npb = (P > 1 ? cut.nsep : 0) + nparb;
+    const int64_t nKp = P * nA + npb;
+    // natural unknown -> slot in rb
+    std::vector<int32_t> pos(nK);
+    for (int i = 0; i < nK; ++i) {
+        const int v = ord.pos[i];
+        pos[i] = v < nAb ? (P > 1 ? cut.slot[v] : v) : (int32_t)(P * nA + (P > 1 ? cut.nsep : 0) + (v - nAb));
+    }
     const int64_t ldab = 2 * kl + ku + 1;
-    const int64_t NE_A = nA * ldab, NE = NE_A + 2 * npb * nA + npb * npb;
+    const int64_t PA = P * nA;
+    // border structure: active columns of each block, Cc non-zeros by border row
+    std::vector<std::vector<uint8_t>> isact(P, std::vector<uint8_t>(npb, 0));
+    std::vector<std::vector<int64_t>> ccrow(npb);  // border row k -> (q, a) keys q * nA + a
+    for (size_t e = 0; e < er.size(); ++e) {
+        const int64_t r = pos[er[e]], c = pos[ec[e]];
+        if (r < PA && c >= PA) isact[r / nA][c - PA] = 1;
+        if (r >= PA && c < PA) {
+            isact[c / nA][r - PA] = 1;
+            ccrow[r - PA].push_back(c);
+        }
+    }
+    int na = 0;
+    std::vector<int32_t> slv((size_t)P * npb, -1);
+    for (int q = 0; q < P; ++q) {
+        int cnt = 0;
+        for (int k = 0; k < npb; ++k)
+            if (isact[q][k]) slv[(size_t)q * npb + k] = cnt++;
+        na = std::max(na, cnt);
+    }
+    std::vector<int32_t> actv((size_t)P * std::max(na, 1), -1);
+    for (int q = 0; q < P; ++q)
+        for (int k = 0; k < npb; ++k)
+            if (slv[(size_t)q * npb + k] >= 0) actv[(size_t)q * na + slv[(size_t)q * npb + k]] = k;
+    std::vector<int32_t> ccptr(npb + 1, 0), ccq, cca;
+    std::vector<std::vector<int64_t>> ccsorted(npb);
+    for (int k = 0; k < npb; ++k) {
+        std::vector<int64_t> v = ccrow[k];
+        std::sort(v.begin(), v.end());
+        v.erase(std::unique(v.begin(), v.end()), v.end());
+        ccsorted[k] = v;
+        ccptr[k + 1] = ccptr[k] + (int32_t)v.size();
+        for (int64_t key : v) {
+            ccq.push_back((int32_t)(key / nA));
+            cca.push_back((int32_t)(key - (key / nA) * nA));
+        }
+    }
+    const int64_t ncc = ccq.size();
+    const int64_t NE_A = P * nA * ldab, NE = NE_A + P * na * nA + ncc + npb * npb;
     if (nh >= (1 << kSrcShift) || nj >= (1 << kSrcShift) || NE >= INT32_MAX || (NE + kIB - 1) / kIB > kMaxY) {
         s->err = "cfx_ipm_create: KKT band too large";
         return create_fail(s, CFX_EUNSUPPORTED);
     }
-    // assembled entry -> slot: band storage of A, then (border) Cr column-major, Cc row-major, D row-major
+    // assembled entry -> slot: the blocks' band storage, then (border) Cr active columns per block, the Cc
+    // non-zeros, D row-major; padding rows of the blocks get a unit diagonal
     std::vector<int64_t> flat(er.size());
     for (size_t e = 0; e < er.size(); ++e) {
         const int64_t r = pos[er[e]], c = pos[ec[e]];
-        if (r < nA && c < nA)
-            flat[e] = c * ldab + kl + ku + r - c;
-        else if (r < nA)
-            flat[e] = NE_A + (c - nA) * nA + r;
-        else if (c < nA)
-            flat[e] = NE_A + npb * nA + (r - nA) * nA + c;
-        else
-            flat[e] = NE_A + 2 * npb * nA + (r - nA) * npb + (c - nA);
+        if (r < PA && c < PA) {  // same block (dissection guarantees it)
+            const int64_t q = r / nA, lr = r - q * nA, lc = c - q * nA;
+            flat[e] = q * nA * ldab + lc * ldab + kl + ku + lr - lc;
+        } else if (r < PA) {
+            const int64_t q = r / nA;
+            flat[e] = NE_A + (q * na + slv[(size_t)q * npb + (c - PA)]) * nA + (r - q * nA);
+        } else if (c < PA) {
+            const int64_t k = r - PA;
+            const auto& v = ccsorted[k];
+            flat[e] = NE_A + P * na * nA + ccptr[k] + (std::lower_bound(v.begin(), v.end(), c) - v.begin());
+        } else {
+            flat[e] = NE_A + P * na * nA + ncc + (r - PA) * npb + (c - PA);
+        }
     }
+    std::vector<bool> used(PA, false);
+    for (int i = 0; i < nK; ++i)
+        if (pos[i] < PA) used[pos[i]] = true;
+    for (int64_t sl = 0; sl < PA; ++sl)
+        if (!used[sl]) {
+            const int64_t q = sl / nA, l = sl - q * nA;
+            flat.push_back(q * nA * ldab + l * ldab + kl + ku);
+            src.push_back((SRC_DC << kSrcShift) | 1);
+        }
     std::vector<int32_t> kptr, kidx, kcode;
     csr(flat, NE, kptr, kidx);
     kcode.resize(kidx.size());
@@ -1267,8 +1428,17 @@ extern "C" int cfx_ipm_create(cfx_handle* h, const double* lb, const double* ub,
     K.kl = (int)kl;
     K.ku = (int)ku;
     K.ldab = (int)ldab;
+    K.P = P;
+    K.na = na;
+    K.ncc = (int)ncc;
+    K.act = dupload(s, actv, &rc);
+    K.sl = dupload(s, slv, &rc);
+    K.ccr_ptr = dupload(s, ccptr, &rc);
+    K.ccr_q = dupload(s, ccq, &rc);
+    K.ccr_a = dupload(s, cca, &rc);
     K.nA = (int)nA;
     K.np = (int)npb;
+    K.nKp = (int)nKp;
     K.NE_A = NE_A;
     K.NE_tot = NE;
     K.nfix = (int)fixedv.size();
@@ -1300,7 +1470,7 @@ extern "C" int cfx_ipm_create(cfx_handle* h, const double* lb, const double* ub,
     double** fbufs[] = {&K.x, &K.zl, &K.zu, &K.dx, &K.dzl, &K.dzu, &K.xt, &K.xacc, &K.xr, &K.dxr, &K.sig, &K.gF};
     for (double** p : fbufs) *p = dalloc<double>(s, B * nf, &rc);
     K.rhs = dalloc<double>(s, B * nK, &rc);
-    K.rb = dalloc<double>(s, B * nK, &rc);
+    K.rb = dalloc<double>(s, B * nKp, &rc);
     double** mbufs[] = {&K.y, &K.dy, &K.gS, &K.csoc, &K.sg, &K.ysc, &K.graw, &K.gt};
     for (double** p : mbufs) *p = dalloc<double>(s, B * m, &rc);
     K.vx = dalloc<double>(s, B * n, &rc);
@@ -1313,13 +1483,13 @@ extern "C" int cfx_ipm_create(cfx_handle* h, const double* lb, const double* ub,
     K.ft = dalloc<double>(s, B, &rc);
     K.of = dalloc<double>(s, B, &rc);
     K.ab = dalloc<double>(s, B * NE_A, &rc);
-    K.Xb = dalloc<double>(s, B * npb * nA, &rc);
-    K.Ccb = dalloc<double>(s, B * npb * nA, &rc);
+    K.Xb = dalloc<double>(s, B * P * na * nA, &rc);
+    K.Ccb = dalloc<double>(s, B * ncc, &rc);
     K.Db = dalloc<double>(s, B * npb * npb, &rc);
     K.Sf = dalloc<double>(s, B * npb * npb, &rc);
     K.Sp = dalloc<int32_t>(s, B * npb, &rc);
-    K.ipiv = dalloc<int32_t>(s, B * nK, &rc);
-    K.info = dalloc<int32_t>(s, B, &rc);
+    K.ipiv = dalloc<int32_t>(s, B * nKp, &rc);
+    K.info = dalloc<int32_t>(s, B * P, &rc);
     K.filt = dalloc<double>(s, B * kFilt * 2, &rc);
     K.sc = dalloc<Scal>(s, B, &rc);
     K.cnt = dalloc<int32_t>(s, 4 * kSlots, &rc);
@@ -1338,6 +1508,7 @@ extern "C" int cfx_ipm_create(cfx_handle* h, const double* lb, const double* ub,
     s->st.kkt_ku = ku;
     s->st.kkt_band_n = nA;
     s->st.kkt_border = npb;
+    s->st.kkt_blocks = P;
     *out = s;
     return CFX_OK;
 }
@@ -1375,10 +1546,11 @@ struct Run {
         hipLaunchKernelGGL(k_ipm_kkt, dim3((unsigned)K.B, (unsigned)((K.NE_tot + kIB - 1) / kIB)), dim3(kIB), 0, st,
                            K, mode);
         IPM_HIP(s, hipGetLastError());
-        if (K.np) {  // bordered: factor A, solve A^-1 [Cr | r_A] (parallel right-hand sides), Schur complement
-            IPM_BAND(s, cfx_band_lu(K.nA, K.kl, K.ku, K.B, K.ab, K.ipiv, K.info, 0, nullptr, st));
-            IPM_BAND(s, cfx_band_solve_multi(K.nA, K.kl, K.ku, K.B, K.ab, K.ipiv, K.Xb, (int64_t)K.np * K.nA, K.nA,
-                                             K.np, K.rb, K.nK, st));
+        if (K.np) {  // blocks + border: factor the blocks, A_q^-1 [Cr_q | r_q] (parallel right-hand sides), Schur
+            const int64_t BP = K.B * K.P, nb = (int64_t)K.na * K.nA;
+            IPM_BAND(s, cfx_band_lu(K.nA, K.kl, K.ku, BP, K.ab, K.ipiv, K.info, 0, nullptr, st));
+            IPM_BAND(s, cfx_band_solve_multi(K.nA, K.kl, K.ku, BP, K.P, K.ab, K.ipiv, K.Xb, K.P * nb, nb, K.nA, K.na,
+                                             K.rb, K.nKp, K.nA, st));
             hipLaunchKernelGGL(k_ipm_schur, g, dim3(kIB), 0, st, K, 1);
             IPM_HIP(s, hipGetLastError());
         } else {
@@ -1391,7 +1563,8 @@ struct Run {
     int resolve() {
         const IpmK& K = s->K;
         if (K.np) {
-            IPM_BAND(s, cfx_band_solve_multi(K.nA, K.kl, K.ku, K.B, K.ab, K.ipiv, nullptr, 0, 0, 0, K.rb, K.nK, st));
+            IPM_BAND(s, cfx_band_solve_multi(K.nA, K.kl, K.ku, K.B * K.P, K.P, K.ab, K.ipiv, nullptr, 0, 0, 0, 0,
+                                             K.rb, K.nKp, K.nA, st));
             hipLaunchKernelGGL(k_ipm_schur, g, dim3(kIB), 0, st, K, 0);
             IPM_HIP(s, hipGetLastError());
         } else {
@@ -1428,6 +1601,7 @@ static int ipm_solve(cfx_ipm* s, const double* v0, const double* fixed_values, d
     s->st.eval_all = s->st.eval_g_f = s->st.eval_h = s->st.kkt_factor = s->st.iterations = s->st.host_syncs = 0;
     s->slot = 0;
     IPM_HIP(s, hipMemsetAsync(K.cnt, 0, 4 * kSlots * sizeof(int32_t), st));
+    IPM_HIP(s, hipMemsetAsync(K.rb, 0, B * K.nKp * sizeof(double), st));  // padding rows of the blocks stay 0
     IPM_HIP(s, hipMemcpyAsync(K.vx, v0, B * K.n * sizeof(double), kin, st));
     if (fixed_values && K.nfix)
         IPM_HIP(s, hipMemcpyAsync(s->d_fv, fixed_values, B * K.nfix * sizeof(double), kin, st));

@@ -285,6 +285,7 @@ typedef struct cfx_ipm_stats {
     /* KKT layout: unknowns, the band's half-bandwidths and unknowns, free parameters in a dense border (Schur
        complement; 0: one band) */
     int64_t kkt_n, kkt_kl, kkt_ku, kkt_band_n, kkt_border;
+    int64_t kkt_blocks; /* band blocks factored side by side (nested dissection of the stage chain; 1: none) */
 } cfx_ipm_stats;
 
 typedef struct cfx_ipm cfx_ipm;

@@ -60,10 +60,17 @@ def _compare(ocp, r_ref, r_nat, vtol=1e-5, ftol=1e-7, it_slack=3):
 @pytest.mark.parametrize("B", [1, 8])
 def test_native_ipm_cfg3_pulse_width_tracking(B):
     """cfg 3 (Ding2007 pulse widths, 30 pulses, N = 100, Fourier force tracking): single start and random starts."""
+    from cocofest_amd.solver import NativeIpm
+
     cfg = dict(cases.cfg3(), objective=TRACK)
     ocp = cases.product_ocp(**cfg)
     r_ref, r_nat = _both(ocp, B, _starts(ocp, B, 0))
     _compare(ocp, r_ref, r_nat)
+    nat = NativeIpm(ocp, batch=B)
+    st = nat.ipm.stats()
+    nat.close()
+    # small batches: the 500-unknown band is cut at stage boundaries into blocks factored side by side
+    assert st["kkt_blocks"] > 1 and st["kkt_border"] <= 32, st
 
 
 def test_native_ipm_cfg2_is_the_forward_integration():
@@ -157,8 +164,8 @@ def test_native_ipm_nmpc_window_bordered_kkt(T):
     nat = NativeIpm(ocp, batch=1)
     st = nat.ipm.stats()
     nat.close()
-    assert st["kkt_border"] == (10 if T == 10 else 0), st
-    assert st["kkt_band_n"] + st["kkt_border"] == st["kkt_n"]
+    assert st["kkt_border"] >= (10 if T == 10 else 0), st  # T = 10: the 10 free intensities are in the border
+    assert st["kkt_blocks"] * st["kkt_band_n"] + st["kkt_border"] >= st["kkt_n"]
 
 
 def test_native_ipm_rejects_bad_input():
