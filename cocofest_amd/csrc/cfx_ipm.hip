@@ -979,6 +979,16 @@ __global__ void __launch_bounds__(kIB) k_ipm_out(const IpmK K, double* __restric
     }
 }
 
+// Publish one counter slot to host-mapped memory: the four counts, then (release, system scope) the sequence
+// number the host spins on.  Replaces a device-to-host copy + stream synchronisation (~25 us of host wake-up
+// and relaunch latency per read on the batch-1 path) by a poll of pinned memory.
+__global__ void k_ipm_publish(const int32_t* __restrict__ cnt, int32_t* pub, int32_t seq) {
+    if (threadIdx.x == 0) {
+        for (int i = 0; i < 4; ++i) __hip_atomic_store(pub + 1 + i, cnt[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(pub, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------------------------------------------------------
@@ -991,6 +1001,9 @@ struct cfx_ipm {
     IpmK K{};
     std::vector<void*> allocs;
     int32_t* h_cnt = nullptr;
+    int32_t *h_pub = nullptr, *d_pub = nullptr;  // host-mapped counter mailbox [seq, 4 counts]
+    int32_t seq = 0;
+    bool poll = true;  // CFX_IPM_SYNC=stream: copy + hipStreamSynchronize instead
     int slot = 0;
     cfx_ipm_stats st{};
     std::string err;
@@ -1323,7 +1336,7 @@ extern "C" int cfx_ipm_create(cfx_handle* h, const double* lb, const double* ub,
         return d;
     };
     Cut cut;
-    if (s->B <= 8 && nAb >= 96) {
+    if (s->B <= 8 && nAb >= 48) {
         for (int P = std::min(16, nAb / 24); P >= 2 && cut.P == 1; --P) {
             Cut d = dissect(P);
             if (d.P > 1 && d.nsep + nparb <= kMaxBorder && (int64_t)s->B * P <= 1024 &&
@@ -1498,6 +1511,13 @@ extern "C" int cfx_ipm_create(cfx_handle* h, const double* lb, const double* ub,
     s->d_kkt = dalloc<double>(s, B, &rc);
     s->d_conv = dalloc<int32_t>(s, B, &rc);
     s->d_its = dalloc<int32_t>(s, B, &rc);
+    if (rc == CFX_OK && (hipHostMalloc((void**)&s->h_pub, 16 * sizeof(int32_t), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+                         hipHostGetDevicePointer((void**)&s->d_pub, s->h_pub, 0) != hipSuccess)) {
+        rc = CFX_ENOMEM;
+        s->err = "hipHostMalloc (mapped) failed";
+    }
+    if (s->h_pub) std::memset(s->h_pub, 0, 16 * sizeof(int32_t));
+    if (const char* e = std::getenv("CFX_IPM_SYNC")) s->poll = std::strcmp(e, "stream") != 0;
     if (rc == CFX_OK && hipHostMalloc((void**)&s->h_cnt, 4 * sizeof(int32_t), hipHostMallocDefault) != hipSuccess) {
         rc = CFX_ENOMEM;
         s->err = "hipHostMalloc failed";
@@ -1525,10 +1545,29 @@ struct Run {
         return k;
     }
     int read(int slot, int32_t* c) {
+        s->st.host_syncs++;
+        if (s->poll) {
+            const int32_t seq = ++s->seq;
+            hipLaunchKernelGGL(k_ipm_publish, dim3(1), dim3(64), 0, st, (const int32_t*)(s->K.cnt + 4 * slot), s->d_pub,
+                               seq);
+            IPM_HIP(s, hipGetLastError());
+            const auto t0 = std::chrono::steady_clock::now();
+            for (long spin = 0;; ++spin) {
+                if (__atomic_load_n(s->h_pub, __ATOMIC_ACQUIRE) == seq) {
+                    for (int i = 0; i < 4; ++i) c[i] = __atomic_load_n(s->h_pub + 1 + i, __ATOMIC_RELAXED);
+                    return CFX_OK;
+                }
+                // a launch failure never publishes: after a while, let the stream report it
+                if ((spin & 1023) == 1023 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(200)) {
+                    IPM_HIP(s, hipStreamSynchronize(st));
+                    if (__atomic_load_n(s->h_pub, __ATOMIC_ACQUIRE) == seq) continue;
+                    return ipm_fail(s, CFX_EHIP, "cfx_ipm_solve: counter mailbox not written");
+                }
+            }
+        }
         IPM_HIP(s, hipMemcpyAsync(s->h_cnt, s->K.cnt + 4 * slot, 4 * sizeof(int32_t), hipMemcpyDeviceToHost, st));
         IPM_HIP(s, hipStreamSynchronize(st));
         std::memcpy(c, s->h_cnt, 4 * sizeof(int32_t));
-        s->st.host_syncs++;
         return CFX_OK;
     }
     int eval_full(double* v) {
@@ -1729,5 +1768,6 @@ extern "C" void cfx_ipm_destroy(cfx_ipm* s) {
     if (s->stream) (void)hipStreamSynchronize(s->stream);
     for (void* p : s->allocs) (void)hipFree(p);
     if (s->h_cnt) (void)hipHostFree(s->h_cnt);
+    if (s->h_pub) (void)hipHostFree(s->h_pub);
     delete s;
 }

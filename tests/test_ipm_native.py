@@ -99,7 +99,9 @@ def test_native_ipm_hmed_sliding_window():
     free = lb != ub
     v0[:, free] = np.clip(v0[:, free] + rng.uniform(0, 10, (8, free.sum())), lb[free], ub[free])
     r_ref, r_nat = _both(ocp, 8, v0)
-    _compare(ocp, r_ref, r_nat)
+    # only the end force is tracked, so the optimal intensity profile is degenerate (a flat valley of equal f):
+    # same f to 1e-7, intensities within 1e-4 of their range
+    _compare(ocp, r_ref, r_nat, vtol=1e-4)
 
 
 @pytest.mark.parametrize("name", ["ding2003_with_fatigue", "ding2007_with_fatigue", "hmed2018_with_fatigue"])
