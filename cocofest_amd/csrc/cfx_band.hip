@@ -395,7 +395,15 @@ __device__ __forceinline__ void slide(double (&v)[KC]) {
 // never leaves registers).  Rows past n are zeros as well.  The pivot row (a wave-uniform index) is
 // swapped in by a chain of uniform branches, one taken.
 // Write target of lanes with nothing to store (shared by every wave; its contents are meaningless).
-__device__ double g_band_sink[64 * 4];
+// Store sinks of the register kernels (lanes with nothing to store write here, so no store sits under a branch):
+// one slot per workgroup modulo kSinkSlots.  A single shared sink made every wavefront of a large batch store
+// into the same few cache lines: at 4,096 instances the factorisation ran 15x slower per instance than alone.
+constexpr int kSinkSlots = 2048;
+constexpr int kSinkSlot = 64 * 5;  // doubles per slot: up to 3 x 64 doubles and 64 ints
+__device__ double g_band_sink[kSinkSlots * kSinkSlot];
+__device__ __forceinline__ double* block_sink() {
+    return g_band_sink + (size_t)((blockIdx.x + (size_t)blockIdx.y * gridDim.x) % kSinkSlots) * kSinkSlot;
+}
 
 
 // rows 0 and p of the window (p wave-uniform): one uniform branch per row, kept apart by the volatile asm
@@ -436,7 +444,7 @@ __device__ __forceinline__ void reg_solve(int n, int kl, int ku, int nrhs, const
                                           double* xs) {
     const int lane = threadIdx.x;
     const int ldab = 2 * kl + ku + 1, kv = kl + ku;
-    double* dsink = g_band_sink + lane;
+    double* dsink = block_sink() + lane;
     for (int c = 0; c < nrhs; ++c) {
         double* x = xs + (int64_t)c * n;
         if (kl > 0) {
@@ -565,8 +573,9 @@ __global__ void __launch_bounds__(64) k_band_lu_reg(int n, int kl, int ku, int n
     auto fetch = [&](int j, int k) { return ab[entering_ok(j, k) ? (j + 1) * ldab + cofs[k] + KLM : 0]; };
     // every lane stores every step (lanes with nothing to store write the sink): no store sits under a
     // branch, so the compiler's vmcnt waits for a prefetch count the stores issued after it exactly
-    double* dsink = g_band_sink + lane;
-    int32_t* isink = reinterpret_cast<int32_t*>(g_band_sink + 64 * KC) + lane;
+    double* const sinkb = block_sink();
+    double* dsink = sinkb + lane;
+    int32_t* isink = reinterpret_cast<int32_t*>(sinkb + 64 * (KC + 1)) + lane;
 
     double r[KC][KLM + 1];  // r[k][i]: row j + i of the window, column j + lane + 64 k
     static_for<0, KC>([&](auto K_) CFX_INLINE {
