@@ -186,11 +186,15 @@ def collocation_section(device, steps=50):
             "achieved_GBps": nbytes * B / (ms * 1e-3) / 1e9, "bytes_per_instance": nbytes}
 
 
-def nmpc_section(device, n_windows, batch=64):
+def nmpc_section(device, n_windows, dist=None, world=1, rank=0, backend="nccl", batch=64):
     """cfg 4 (BASELINE.json configs[3]): Hmed2018 pulse-intensity NMPC, receding 1 s horizons of 10 pulses
     (N = 10, truncation 10, RK1 x 10, the reference force curve tracked in every horizon), ``batch`` independent
-    scenarios (random initial states) advancing in lockstep on one GPU.  Horizons of one trajectory are
-    sequential; scenarios are what shards across GPUs."""
+    scenarios (random initial states) advancing in lockstep per GPU.  Horizons of one trajectory are sequential;
+    scenarios are what shards: every rank runs its own ``batch`` scenarios (weak scaling), timed between
+    barriers (max over ranks), and the committed force trajectories of all ranks are all-gathered at the end
+    (RCCL over xGMI with the nccl backend) — the only exchange the path has."""
+    import torch
+
     from cocofest_amd import DingModelPulseIntensityFrequency, OdeSolver
     from cocofest_amd.nmpc import FesNmpc
 
@@ -200,18 +204,33 @@ def nmpc_section(device, n_windows, batch=64):
                    objective={"force_tracking": [np.array(ft["time"]), np.array(ft["force"])]},
                    pulse_intensity={"max": 130}, ode_solver=OdeSolver.RK1(n_integration_steps=10), batch=batch,
                    device=device)
-    rng = np.random.default_rng(0)
+    rng = np.random.default_rng(rank)
     x0 = np.stack([rng.uniform(0, 0.5, batch), rng.uniform(0, 50, batch)], axis=1)
+    if dist:
+        dist.barrier()
     t0 = time.perf_counter()
     res = nmpc.solve(n_cycles=n_windows, x0=x0)
     wall = time.perf_counter() - t0
     its = np.stack(res.iterations)
     conv = np.stack(res.converged)
-    return {"workload": "Hmed2018 pulse-intensity NMPC, 1 s horizons x 10 pulses, N = 10, truncation 10, RK1 x 10, "
-                        "force tracking per horizon", "horizons": n_windows, "scenarios": batch,
-            "wall_s": wall, "ms_per_horizon": wall / n_windows * 1e3,
-            "scenario_horizons_per_s": batch * n_windows / wall, "converged_frac": float(conv.mean()),
-            "iterations_median": float(np.median(its)), "iterations_max": int(its.max())}
+    out = {"workload": "Hmed2018 pulse-intensity NMPC, 1 s horizons x 10 pulses, N = 10, truncation 10, RK1 x 10, "
+                       "force tracking per horizon", "horizons": n_windows, "scenarios_per_gpu": batch, "n_gpus": world,
+           "scaling": "weak", "parallelism": f"scenarios sharded over {world} GPU(s); committed trajectories "
+                                             "all-gathered at the end"}
+    conv_frac = float(conv.mean())
+    if dist:
+        dev = f"cuda:{device}" if backend == "nccl" else "cpu"
+        t = torch.tensor([wall, 1.0 - conv_frac], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        wall, conv_frac = float(t[0]), 1.0 - float(t[1])
+        F = torch.as_tensor(np.ascontiguousarray(res.states["F"]), dtype=torch.float64, device=dev)
+        parts = [torch.empty_like(F) for _ in range(world)]
+        dist.all_gather(parts, F)
+        out["gathered_force_shape"] = [world] + list(F.shape)
+    out.update({"wall_s": wall, "ms_per_horizon": wall / n_windows * 1e3,
+                "scenario_horizons_per_s": world * batch * n_windows / wall, "converged_frac": conv_frac,
+                "iterations_median": float(np.median(its)), "iterations_max": int(its.max())})
+    return out
 
 
 def ivp_section(device):
@@ -447,6 +466,9 @@ def main():
     traffic = pmc_traffic()
 
     msk_tp, msk_ocp = msk_throughput(local, dist, world, rank, args.backend) if not args.no_msk else (None, None)
+    # cfg 4 on every rank (scenarios shard; weak scaling)
+    nm = nmpc_section(local, args.nmpc_horizons, dist, world, rank, args.backend) \
+        if (not args.no_solve and args.nmpc_horizons) else None
 
     out = None
     if rank == 0:
@@ -454,7 +476,6 @@ def main():
         conv = convergence(local) if (world == 1 and not args.no_solve) else None
         ivp = ivp_section(local) if (world == 1 and not args.no_solve) else None
         col = collocation_section(local) if (world == 1 and not args.no_solve) else None
-        nm = nmpc_section(local, args.nmpc_horizons) if (world == 1 and not args.no_solve and args.nmpc_horizons) else None
         msk = msk_tp
         if msk_tp is not None and world == 1 and not args.no_solve:
             msk = msk_section(local, msk_tp, msk_ocp, cpu_seconds=args.cpu_seconds / 2)
