@@ -423,11 +423,20 @@ __global__ void __launch_bounds__(kIB) k_ipm_kkt(const IpmK K, int mode) {
 // pivoting in LDS, kept for the second-order corrections: factor = 0 re-uses it), the border x_p =
 // S^-1 (r_p - sum_q Cc_q y_q) and the blocks x_q = y_q - (A_q^-1 Cr_q) x_p, written back into rb.  A zero pivot
 // of S is reported in info like one of a block (P nA + k + 1).
+// ordering point for the single-wavefront phases below: LDS traffic of the wave completed, no compiler motion
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
+constexpr int kSchurStage = 2048;  // Cc non-zeros / active-slot entries staged in LDS (else read from global)
+
 __global__ void __launch_bounds__(kIB) k_ipm_schur(const IpmK K, int factor) {
     __shared__ double S[kMaxBorder][kMaxBorder + 1];
     __shared__ double sv[kMaxBorder];
     __shared__ int piv[kMaxBorder];
-    __shared__ int sing;
+    __shared__ double ccv[kSchurStage];
+    __shared__ int ccq[kSchurStage], cca[kSchurStage], slt[kSchurStage];
     const int64_t b = blockIdx.x;
     const int nA = K.nA, np = K.np, P = K.P, na = K.na, t = threadIdx.x;
     const int64_t nb = (int64_t)na * nA;  // per block
@@ -437,20 +446,31 @@ __global__ void __launch_bounds__(kIB) k_ipm_schur(const IpmK K, int factor) {
     double* Sf = K.Sf + b * np * np;
     int32_t* Sp = K.Sp + b * np;
     const int PA = P * nA;
+    // the sparse coupling of the border rows, staged once (every S entry and s_i walks its row)
+    const bool staged = K.ncc <= kSchurStage && P * np <= kSchurStage;
+    if (staged) {
+        for (int z = t; z < K.ncc; z += kIB) ccv[z] = Cc[z], ccq[z] = K.ccr_q[z], cca[z] = K.ccr_a[z];
+        for (int e = t; e < P * np; e += kIB) slt[e] = K.sl[e];
+        __syncthreads();
+    }
+    auto cval = [&](int z) { return staged ? ccv[z] : Cc[z]; };
+    auto cq = [&](int z) { return staged ? ccq[z] : K.ccr_q[z]; };
+    auto ca = [&](int z) { return staged ? cca[z] : K.ccr_a[z]; };
+    auto slot = [&](int q, int j) { return staged ? slt[q * np + j] : K.sl[q * np + j]; };
     if (factor) {
         for (int e = t; e < np * np; e += kIB) {  // S(i, j) = D(i, j) - sum over row i's Cc non-zeros
             const int i = e / np, j = e - (e / np) * np;
             double acc = K.Db[b * np * np + e];
             for (int z = K.ccr_ptr[i]; z < K.ccr_ptr[i + 1]; ++z) {
-                const int q = K.ccr_q[z], c = K.sl[q * np + j];
-                if (c >= 0) acc -= Cc[z] * X[q * nb + (int64_t)c * nA + K.ccr_a[z]];
+                const int q = cq(z), c = slot(q, j);
+                if (c >= 0) acc -= cval(z) * X[q * nb + (int64_t)c * nA + ca(z)];
             }
             S[i][j] = acc;
         }
-        if (t == 0) sing = 0;
         __syncthreads();
-        for (int k = 0; k < np; ++k) {
-            if (t < 64) {  // first largest |S(i, k)|, i >= k
+        if (t < 64) {  // LU with partial pivoting (first largest |S(i, k)|, i >= k) in one wavefront
+            int sing = 0;
+            for (int k = 0; k < np; ++k) {
                 double a = (t >= k && t < np) ? fabs(S[t][k]) : -1.0;
                 int idx = t;
                 for (int o = 32; o > 0; o >>= 1) {
@@ -461,58 +481,59 @@ __global__ void __launch_bounds__(kIB) k_ipm_schur(const IpmK K, int factor) {
                         idx = i2;
                     }
                 }
-                if (t == 0) piv[k] = idx;
+                const int p = idx;  // the same in every lane
+                if (t == 0) piv[k] = p;
+                if (p != k && t < np) {  // lanes over columns
+                    const double tmp = S[k][t];
+                    S[k][t] = S[p][t];
+                    S[p][t] = tmp;
+                }
+                wave_sync();
+                const double pv = S[k][k];
+                const double inv = pv != 0.0 ? 1.0 / pv : 0.0;
+                if (pv == 0.0 && !sing) sing = PA + k + 1;
+                if (t > k && t < np) S[t][k] *= inv;
+                wave_sync();
+                if (t > k && t < np) {  // lane t updates column t of the trailing rows
+                    const double ukt = S[k][t];
+                    for (int i = k + 1; i < np; ++i) S[i][t] -= S[i][k] * ukt;
+                }
+                wave_sync();
             }
-            __syncthreads();
-            const int p = piv[k];
-            if (p != k && t < np) {
-                const double tmp = S[k][t];
-                S[k][t] = S[p][t];
-                S[p][t] = tmp;
-            }
-            __syncthreads();
-            const double pv = S[k][k];
-            const double inv = pv != 0.0 ? 1.0 / pv : 0.0;
-            if (t == 0 && pv == 0.0 && !sing) sing = PA + k + 1;
-            if (t > k && t < np) S[t][k] *= inv;
-            __syncthreads();
-            const int w = np - k - 1;
-            for (int e = t; e < w * w; e += kIB) {
-                const int i = k + 1 + e / w, j = k + 1 + e - (e / w) * w;
-                S[i][j] -= S[i][k] * S[k][j];
-            }
-            __syncthreads();
+            if (t == 0 && sing && K.info[b * P] == 0) K.info[b * P] = sing;
         }
+        __syncthreads();
         for (int e = t; e < np * np; e += kIB) Sf[e] = S[e / np][e - (e / np) * np];
         if (t < np) Sp[t] = piv[t];
-        if (t == 0 && sing && K.info[b * P] == 0) K.info[b * P] = sing;
     } else {
         for (int e = t; e < np * np; e += kIB) S[e / np][e - (e / np) * np] = Sf[e];
         if (t < np) piv[t] = Sp[t];
+        __syncthreads();
     }
-    // s = r_p - sum_q Cc_q y_q
-    for (int i = t; i < np; i += kIB) {
-        double acc = rb[PA + i];
-        for (int z = K.ccr_ptr[i]; z < K.ccr_ptr[i + 1]; ++z) acc -= Cc[z] * rb[K.ccr_q[z] * nA + K.ccr_a[z]];
-        sv[i] = acc;
-    }
-    __syncthreads();
-    if (t == 0) {  // x_p = S^-1 s (getrs: interchanges, unit-lower, upper)
-        for (int k = 0; k < np; ++k) {
+    if (t < 64) {  // x_p = S^-1 (r_p - sum_q Cc_q y_q), lane i holding component i (getrs)
+        double x = 0.0;
+        if (t < np) {
+            x = rb[PA + t];
+            for (int z = K.ccr_ptr[t]; z < K.ccr_ptr[t + 1]; ++z) x -= cval(z) * rb[cq(z) * nA + ca(z)];
+        }
+        for (int k = 0; k < np; ++k) {  // row interchanges in order
             const int p = piv[k];
             if (p != k) {
-                const double tmp = sv[k];
-                sv[k] = sv[p];
-                sv[p] = tmp;
+                const double xk = __shfl(x, k, 64), xp = __shfl(x, p, 64);
+                if (t == k) x = xp;
+                if (t == p) x = xk;
             }
         }
-        for (int k = 0; k < np; ++k)
-            for (int i = k + 1; i < np; ++i) sv[i] -= S[i][k] * sv[k];
-        for (int k = np - 1; k >= 0; --k) {
-            double acc = sv[k];
-            for (int j = k + 1; j < np; ++j) acc -= S[k][j] * sv[j];
-            sv[k] = acc / S[k][k];
+        for (int k = 0; k < np; ++k) {  // unit lower
+            const double xk = __shfl(x, k, 64);
+            if (t > k && t < np) x -= S[t][k] * xk;
         }
+        for (int k = np - 1; k >= 0; --k) {  // upper
+            if (t == k) x = x / S[k][k];
+            const double xk = __shfl(x, k, 64);
+            if (t < k) x -= S[t][k] * xk;
+        }
+        if (t < np) sv[t] = x;
     }
     __syncthreads();
     for (int e = t; e < PA; e += kIB) {
