@@ -376,3 +376,46 @@ def test_ivp_host_setup_matches_oracle():
     d07 = ModelMaker.create_model("ding2007", stim_time=[0, 0.1, 0.2], sum_stim_truncation=3)
     ivp = IvpFes({"model": d07, "pulse_width": [0.0003, 0.0004, 0.0005]}, {"final_time": 0.3})
     np.testing.assert_array_equal(ivp.controls[0], [0.0003, 0.0004, 0.0005])
+
+
+def test_ipm_abi_null_and_default_options():
+    """cfx_ipm_*: NULL arguments are rejected without touching a device; the default options are Ipopt's (and
+    those of solver.IpmOptions, the algorithm's executable specification)."""
+    import ctypes as C
+
+    from cocofest_amd import _cfx
+    from cocofest_amd.solver import _NATIVE_OPTIONS, IpmOptions
+
+    lib = _cfx.load_library()
+    opt = _cfx.IpmOptions()
+    lib.cfx_ipm_default_options(C.byref(opt))
+    ref = IpmOptions()
+    for k in _NATIVE_OPTIONS:
+        assert getattr(opt, k) == getattr(ref, k), k
+    lib.cfx_ipm_default_options(None)  # tolerated
+    s = C.c_void_p()
+    lb = np.zeros(4)
+    assert lib.cfx_ipm_create(None, lb.ctypes.data, lb.ctypes.data, 0, C.byref(opt), C.byref(s)) == _cfx.EINVAL
+    assert lib.cfx_ipm_solve(None, None, None, None, None, None, None, None, None, 0) == _cfx.EINVAL
+    st = _cfx.IpmStats()
+    assert lib.cfx_ipm_get_stats(None, C.byref(st)) == _cfx.EINVAL
+    assert lib.cfx_ipm_n_fixed(None) == -1
+    assert lib.cfx_ipm_last_error(None) == b""
+    lib.cfx_ipm_destroy(None)
+
+
+def test_ipm_option_structs_match_the_header():
+    """The ctypes mirrors of cfx_ipm_options / cfx_ipm_stats list the header's fields in order."""
+    from cocofest_amd import _cfx
+
+    text = (ROOT / "include" / "cfx.h").read_text()
+    for struct, cls in (("cfx_ipm_options", _cfx.IpmOptions), ("cfx_ipm_stats", _cfx.IpmStats)):
+        body = re.search(r"typedef struct %s \{(.*?)\} %s;" % (struct, struct), text, re.S).group(1)
+        body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)
+        names = []
+        for decl in body.split(";"):
+            decl = decl.strip()
+            if not decl:
+                continue
+            names += [n.strip() for n in decl.split(None, 1)[1].split(",")]
+        assert names == [f for f, _ in cls._fields_], struct
