@@ -816,8 +816,11 @@ __device__ __forceinline__ void msk_stage(const MskGeom& G, int residual, const 
     }
 }
 
+#ifndef CFX_MSK_SC_ATTR
+#define CFX_MSK_SC_ATTR  // tuning hook (occupancy attributes of k_msk_stagecoef)
+#endif
 template <int NQ, int NM, int FAM, int SCHEME>
-__global__ void __launch_bounds__(256) k_msk_stagecoef(const MskParams P, const MskGeom* __restrict__ GG,
+__global__ void __launch_bounds__(256) CFX_MSK_SC_ATTR k_msk_stagecoef(const MskParams P, const MskGeom* __restrict__ GG,
                                                        const double* __restrict__ V, double* __restrict__ Gout,
                                                        double* __restrict__ XS) {
     constexpr int NXM = msk_nxm<FAM>(), NX = NM * NXM + 2 * NQ;
