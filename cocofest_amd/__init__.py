@@ -22,7 +22,7 @@ from .fes_models import (
 from .fourier import FourierSeries
 from .ivp import IvpFes
 from .msk import FesMskModel, FesMskOcp, OcpFesMsk
-from .nmpc import FesNmpc, NmpcResult
+from .nmpc import FesNmpc, NmpcFesMsk, NmpcResult
 from .ocp import FesOcp, Node, Objective, ObjectiveFcn, ObjectiveList, OcpFes
 from .ode_solver import ControlType, OdeSolver
 from .solver import BatchedIpm, IpmOptions, IpmResult
@@ -32,5 +32,5 @@ __all__ = [
     "DingModelPulseIntensityFrequency", "DingModelPulseIntensityFrequencyWithFatigue",
     "DingModelPulseWidthFrequency", "DingModelPulseWidthFrequencyWithFatigue", "FesModel", "ModelMaker",
     "FourierSeries", "IvpFes", "FesOcp", "Node", "Objective", "ObjectiveFcn", "ObjectiveList", "OcpFes",
-    "ControlType", "OdeSolver", "FesMskModel", "FesMskOcp", "OcpFesMsk", "FesNmpc", "NmpcResult", "BatchedIpm", "IpmOptions", "IpmResult",
+    "ControlType", "OdeSolver", "FesMskModel", "FesMskOcp", "OcpFesMsk", "FesNmpc", "NmpcFesMsk", "NmpcResult", "BatchedIpm", "IpmOptions", "IpmResult",
 ]

@@ -21,6 +21,7 @@ one trajectory are sequential.
 
 from __future__ import annotations
 
+import copy
 import time
 from dataclasses import dataclass, field
 
@@ -235,3 +236,174 @@ class FesNmpc:
             n_new = int(round(self.n_adv * len(self.cycle_stims)))
             out[:, N * nzb + nx + T:] = np.concatenate([w[:, n_new:], w[:, w.shape[1] - n_new:]], axis=1)
         return out
+
+
+class NmpcFesMsk:
+    """Receding horizon over musculoskeletal windows (reference: ``NmpcFesMsk``,
+    cocofest/optimization/fes_ocp_dynamics_nmpc_cyclic.py:16-102, a bioptim
+    ``MultiCyclicNonlinearModelPredictiveControl`` over ``OcpFesMsk._prepare_optimization_problem``).
+
+    A window is ``n_cycles_simultaneous`` cycles of the muscles' ``stim_time`` (one cycle's pulses), transcribed
+    by :class:`OcpFesMsk` with the window's stimulation history (the last T pulses, ``update_stim``,
+    fes_ocp_dynamics_nmpc_cyclic.py:34-46) as ``previous_stim`` of every muscle.  After each window the first
+    ``n_cycles_to_advance`` cycles are committed; the next window starts from the committed state (every state of
+    its node 0 fixed to it, per scenario: bioptim's advance_window_bounds_states) and the shifted solution is its
+    warm start (advance_window_initial_guess_states).  B scenarios advance in lockstep in one native interior-point
+    solve per window.  The cycling-specific parts (wheel angle, ``prepare_nmpc_for_cycling``, which calls a
+    method the reference does not define) and external forces are not covered."""
+
+    def __init__(self, model, cycle_duration: float, n_cycles_simultaneous: int = 3, n_cycles_to_advance: int = 1,
+                 pulse_width: dict | None = None, objective: dict | None = None, msk_info: dict | None = None,
+                 ode_solver=OdeSolver.RK4(n_integration_steps=1), n_shooting_per_cycle: int | None = None,
+                 n_total_cycles: int | None = None, batch: int = 1, device: int = 0, options=None):
+        from .msk import FesMskModel
+
+        if not isinstance(model, FesMskModel):
+            raise TypeError("model must be a FesMskModel")
+        if n_cycles_to_advance < 1 or n_cycles_simultaneous < n_cycles_to_advance:
+            raise ValueError("need 1 <= n_cycles_to_advance <= n_cycles_simultaneous")
+        muscles = model.muscles_dynamics_model
+        st = list(muscles[0].stim_time)
+        if not st or min(st) < 0 or max(st) >= cycle_duration:
+            raise ValueError("the muscles' stim_time must hold one cycle's pulses in [0, cycle_duration)")
+        self.model, self.cycle_duration = model, float(cycle_duration)
+        self.n_sim, self.n_adv, self.n_total = n_cycles_simultaneous, n_cycles_to_advance, n_total_cycles
+        self.cycle_stims = st
+        self.pulse_width, self.objective, self.msk_info = pulse_width, dict(objective or {}), dict(msk_info or {})
+        self.ode_solver = ode_solver
+        self.B, self.device, self.options = batch, device, options
+        self.T = muscles[0]._sum_stim_truncation
+        n = OcpFes.prepare_n_shooting(self._window_stims(), self.cycle_duration * self.n_sim)
+        if n_shooting_per_cycle is not None:
+            n = n_shooting_per_cycle * self.n_sim
+        if n % self.n_sim:
+            raise ValueError("the window's node count must split evenly into cycles")
+        self.n_shooting, self.cycle_len = n, n // self.n_sim
+
+    @staticmethod
+    def prepare_nmpc(model=None, cycle_duration=None, n_cycles_simultaneous: int = None, n_cycles_to_advance: int = None,
+                     n_total_cycles: int = None, pulse_width: dict = None, pulse_intensity: dict = None,
+                     objective: dict = None, msk_info: dict = None, external_forces: dict = None,
+                     initial_guess_warm_start: bool = False, use_sx: bool = True,
+                     ode_solver=OdeSolver.RK4(n_integration_steps=1), n_threads: int = 1, control_type=None,
+                     n_shooting_per_cycle: int | None = None, batch: int = 1, device: int = 0, options=None):
+        """Same arguments as the reference's ``NmpcFesMsk.prepare_nmpc`` (fes_ocp_dynamics_nmpc_cyclic.py:49-102),
+        plus the batch / device of the native solver."""
+        if external_forces:
+            raise NotImplementedError("NmpcFesMsk: external forces are not supported")
+        if pulse_intensity:
+            raise NotImplementedError("NmpcFesMsk: Hmed2018 pulse-intensity muscles are not supported")
+        return NmpcFesMsk(model, cycle_duration, n_cycles_simultaneous, n_cycles_to_advance, pulse_width=pulse_width,
+                          objective=objective, msk_info=msk_info, ode_solver=ode_solver,
+                          n_shooting_per_cycle=n_shooting_per_cycle, n_total_cycles=n_total_cycles, batch=batch,
+                          device=device, options=options)
+
+    def _window_stims(self):
+        return [round(t + c * self.cycle_duration, 10) for c in range(self.n_sim) for t in self.cycle_stims]
+
+    def _window_ocp(self, hist_times):
+        from .msk import FesMskModel, OcpFesMsk
+
+        base = self.model
+        muscles = []
+        for m in base.muscles_dynamics_model:  # copies keep any constants the caller set on the muscles
+            c = copy.deepcopy(m)
+            c.stim_time, c.previous_stim = self._window_stims(), {"time": list(hist_times)}
+            c._last_table_src = None
+            muscles.append(c)
+        model = FesMskModel(name=base.name, biorbd_path=base.biorbd_path, muscles_model=muscles,
+                            activate_force_length_relationship=base.activate_force_length_relationship,
+                            activate_force_velocity_relationship=base.activate_force_velocity_relationship,
+                            activate_passive_force_relationship=base.activate_passive_force_relationship,
+                            activate_residual_torque=base.activate_residual_torque)
+        ocp = OcpFesMsk.prepare_ocp(model=model, final_time=self.cycle_duration * self.n_sim,
+                                    pulse_width=self.pulse_width, objective=self.objective, msk_info=self.msk_info,
+                                    ode_solver=self.ode_solver, n_shooting=self.n_shooting)
+        # node 0 of every state is the window's start state (the values are set per scenario at each solve)
+        lo, hi = ocp.x_bounds
+        start = np.where(lo[:, 0] == hi[:, 0], lo[:, 0], ocp.x_init[:, 0])
+        lo[:, 0] = hi[:, 0] = start
+        return ocp
+
+    def solve(self, update_functions=None, solver=None, n_cycles: int | None = None, x0=None):
+        """Advance until ``n_cycles`` cycles are committed (default ``n_total_cycles``), or — bioptim style — while
+        ``update_functions(self, cycle_idx, result)`` returns True.  x0: (B, nx) start states (default: the first
+        window's node-0 bounds / initial guess).  Returns an NmpcResult."""
+        from .solver import IpmOptions, NativeIpm
+
+        if n_cycles is None:
+            n_cycles = self.n_total
+        if n_cycles is None and update_functions is None:
+            raise ValueError("give n_cycles (or n_total_cycles) or update_functions")
+        opts = self.options or IpmOptions()
+        if solver is not None:
+            for k in ("tol", "max_iter"):
+                if hasattr(solver, k):
+                    setattr(opts, k, getattr(solver, k))
+        B, T = self.B, self.T
+        hist_t = [PLACEHOLDER_TIME] * T
+        cache = {}
+        result = NmpcResult(time=None, states={}, controls={}, pulse_intensity=None, stim_time=[])
+        states, ctrl_parts, committed = [], [], []
+        t_nodes, t_off, warm, x_start = [0.0], 0.0, None, None
+        adv_nodes, adv_time = self.n_adv * self.cycle_len, self.n_adv * self.cycle_duration
+        ocp = None
+        w = 0
+        while True:
+            if n_cycles is not None and w * self.n_adv >= n_cycles:
+                break
+            t0 = time.perf_counter()
+            key = tuple(np.round(hist_t, 9))
+            if key not in cache:
+                o = self._window_ocp(hist_t)
+                cache[key] = (o, NativeIpm(o, batch=B, device=self.device, options=opts))
+            ocp, ipm = cache[key]
+            nx = ocp.nx
+            if x_start is None:
+                x_start = np.tile(ocp.x_bounds[0][:, 0], (B, 1)) if x0 is None else \
+                    np.asarray(x0, dtype=float).reshape(B, nx)
+                states.append(x_start[:, :, None])
+            lb, _ = ocp.bounds_vector()
+            fixed = np.tile(lb[ipm.fixed], (B, 1))
+            fidx = {int(j): i for i, j in enumerate(ipm.fixed)}
+            for r in range(nx):
+                fixed[:, fidx[r]] = x_start[:, r]
+            v0 = np.tile(ocp.initial_guess_vector(), (B, 1)) if warm is None else warm.copy()
+            v0[:, ipm.fixed] = fixed
+            ts = time.perf_counter()
+            res = ipm.solve(v0, fixed_values=fixed)
+            result.solve_wall.append(time.perf_counter() - ts)
+            result.iterations.append(res.iterations)
+            result.converged.append(res.converged)
+            N, nzb = ocp.n_shooting, ocp.nzb
+            body = res.v[:, : N * nzb].reshape(B, N, nzb)
+            xs = np.concatenate([body[:, :, :nx], res.v[:, None, N * nzb: N * nzb + nx]], 1)
+            states.append(np.transpose(xs[:, 1: adv_nodes + 1, :], (0, 2, 1)))
+            dt = ocp.final_time / N
+            t_nodes += [t_off + (k + 1) * dt for k in range(adv_nodes)]
+            if ocp.nu:
+                ctrl_parts.append(np.transpose(body[:, :adv_nodes, nx:], (0, 2, 1)))
+            x_start = xs[:, adv_nodes, :]
+            new = [t for t in self._window_stims() if t < adv_time - 1e-12]
+            committed += [t + t_off for t in new]
+            hist_t = [t - adv_time for t in (list(hist_t) + new)[-T:]]
+            hist_t = [PLACEHOLDER_TIME if t < PLACEHOLDER_TIME / 2 else t for t in hist_t]
+            t_off += adv_time
+            blocks = np.concatenate([body[:, adv_nodes:], body[:, N - adv_nodes:]], axis=1)
+            warm = res.v.copy()
+            warm[:, : N * nzb] = blocks.reshape(B, -1)
+            result.window_wall.append(time.perf_counter() - t0)
+            w += 1
+            if update_functions is not None and not update_functions(self, w, result):
+                break
+        for _, ipm in cache.values():
+            ipm.close()
+        X = np.concatenate(states, axis=2)
+        n_keep = (w * self.n_adv if n_cycles is None else n_cycles) * self.cycle_len
+        result.time = np.asarray(t_nodes[: n_keep + 1])
+        result.states = {name: X[:, i, : n_keep + 1] for i, name in enumerate(ocp.state_names)}
+        if ctrl_parts:
+            C = np.concatenate(ctrl_parts, axis=2)[:, :, :n_keep]
+            result.controls = {name: C[:, i] for i, name in enumerate(ocp.control_names)}
+        result.stim_time = committed[: (n_keep // self.cycle_len) * len(self.cycle_stims)]
+        return result

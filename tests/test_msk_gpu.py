@@ -181,3 +181,62 @@ def test_msk_cfg5_interior_point_converges():
     q_elbow = states[f"q_{ocp.model.name_dof[1]}"][0]
     assert abs(q_elbow[0] - 3.14 / 36) < 1e-9 and abs(q_elbow[-1] - 1.57) < 1e-9
     assert np.all(controls["last_pulse_width_BIClong"] >= ocp.model.muscles_dynamics_model[0].pd0 - 1e-12)
+
+
+def _msk_nmpc(batch=1, n_sim=2):
+    import cocofest_amd as C
+
+    mm = C.FesMskModel(biorbd_path=MC.biomod_path("arm26_biceps_triceps"),
+                       muscles_model=[C.DingModelPulseWidthFrequencyWithFatigue(muscle_name=n, sum_stim_truncation=10)
+                                      for n in ("BIClong", "TRIlong")],
+                       stim_time=[0.0, 0.1, 0.2, 0.3, 0.4], activate_force_length_relationship=True,
+                       activate_force_velocity_relationship=True)
+    ol = C.ObjectiveList()
+    ol.add(C.ObjectiveFcn.Lagrange.MINIMIZE_STATE, key="q", index=[1], node=C.Node.ALL, target=np.array([[1.0]]),
+           weight=10, quadratic=True)
+    return C.NmpcFesMsk.prepare_nmpc(model=mm, cycle_duration=0.5, n_cycles_simultaneous=n_sim, n_cycles_to_advance=1,
+                                     n_total_cycles=3, objective={"custom": ol, "minimize_muscle_fatigue": True},
+                                     msk_info={"bound_type": "start", "bound_data": [0, 5]},
+                                     ode_solver=C.OdeSolver.RK4(n_integration_steps=5), batch=batch)
+
+
+def test_nmpc_fes_msk_commits_a_forward_consistent_trajectory():
+    """NmpcFesMsk (fes_ocp_dynamics_nmpc_cyclic.py:16-102): 3 cycles of 0.5 s, windows of 2 cycles, 2 scenarios
+    starting at 5 and 20 deg.  Every window converges, and the committed pulse widths integrated forward over the
+    whole 1.5 s (one long OcpFesMsk transcription, stimulation history included) reproduce the committed states:
+    the windows' stimulation histories and start states are carried over exactly."""
+    import cocofest_amd as C
+
+    nm = _msk_nmpc(batch=2)
+    w0 = nm._window_ocp([-1e7] * nm.T)
+    x0 = np.tile(w0.x_bounds[0][:, 0], (2, 1))
+    x0[1, w0.state_names.index(f"q_{w0.model.name_dof[1]}")] = 3.14 / 9
+    res = nm.solve(x0=x0)
+    assert len(res.converged) == 3 and all(bool(np.all(c)) for c in res.converged), res.iterations
+    assert len(res.stim_time) == 15 and abs(res.stim_time[-1] - 1.4) < 1e-12
+    names = w0.state_names
+    X = np.stack([res.states[n] for n in names], axis=1)  # (B, nx, 3 * 5 + 1)
+    assert X.shape == (2, len(names), 16) and abs(res.time[-1] - 1.5) < 1e-12
+    # one long transcription of the committed pulses
+    model = nm.model
+    mm = C.FesMskModel(biorbd_path=model.biorbd_path,
+                       muscles_model=[C.DingModelPulseWidthFrequencyWithFatigue(muscle_name=m.muscle_name,
+                                                                                 sum_stim_truncation=10)
+                                      for m in model.muscles_dynamics_model],
+                       stim_time=list(res.stim_time), activate_force_length_relationship=True,
+                       activate_force_velocity_relationship=True)
+    long = C.OcpFesMsk.prepare_ocp(model=mm, final_time=1.5, objective={"minimize_muscle_fatigue": True},
+                                   msk_info={"bound_type": "start", "bound_data": [0, 5]},
+                                   ode_solver=C.OdeSolver.RK4(n_integration_steps=5), n_shooting=15)
+    U = np.stack([res.controls[n] for n in long.control_names], axis=2)  # (B, 15, nu)
+    h = long.nlp(batch=2, layout="aos")
+    tr = h.integrate(x0=X[:, :, 0].copy(), u=U.reshape(2, -1).copy())
+    h.close()
+    for b in range(2):
+        got = tr[b].reshape(-1, long.nx)[::5].T
+        scale = np.abs(X[b]).max(axis=1, keepdims=True) + 1e-3
+        err = np.abs(got - X[b]) / scale
+        assert err.max() < 1e-5, (b, err.max(), np.unravel_index(err.argmax(), err.shape))
+    # the elbow moves toward the 1 rad target in both scenarios
+    qe = res.states[f"q_{model.name_dof[1]}"]
+    assert np.all(np.abs(qe[:, -1] - 1.0) < np.abs(qe[:, 0] - 1.0))

@@ -93,3 +93,45 @@ def test_hmed_free_intensities_are_self_consistent(fatigue, batch=1, nmpc_factor
         ref = _forward(name, stims, 3, 4, controls=controls)
         got = np.stack([res.states[k][b] for k in model.name_dof])
         np.testing.assert_allclose(got, ref, rtol=1e-6, atol=1e-6)
+
+
+def test_msk_nmpc_window_history_matches_one_long_transcription():
+    """NmpcFesMsk's window stimulation tables (update_stim, fes_ocp_dynamics_nmpc_cyclic.py:34-46): a window that
+    starts after k committed cycles sees, interval for interval, the stim rows of one long transcription shifted by k
+    cycles, and every state of its node 0 is fixed (the per-scenario start values go in at solve time)."""
+    import cocofest_amd as C
+    from tests import msk_cases as MC
+
+    mm = C.FesMskModel(biorbd_path=MC.biomod_path("arm26_biceps_triceps"),
+                       muscles_model=[C.DingModelPulseWidthFrequencyWithFatigue(muscle_name=n, sum_stim_truncation=4)
+                                      for n in ("BIClong", "TRIlong")],
+                       stim_time=[0.0, 0.1, 0.2, 0.3, 0.4], activate_force_length_relationship=True,
+                       activate_force_velocity_relationship=True)
+    nm = C.NmpcFesMsk.prepare_nmpc(model=mm, cycle_duration=0.5, n_cycles_simultaneous=2, n_cycles_to_advance=1,
+                                   msk_info={"bound_type": "start", "bound_data": [0, 5]},
+                                   objective={"minimize_muscle_fatigue": True})
+    assert nm.n_shooting == 10 and nm.cycle_len == 5
+    long_m = C.FesMskModel(biorbd_path=MC.biomod_path("arm26_biceps_triceps"),
+                           muscles_model=[C.DingModelPulseWidthFrequencyWithFatigue(muscle_name=n,
+                                                                                     sum_stim_truncation=4)
+                                          for n in ("BIClong", "TRIlong")],
+                           stim_time=[round(0.1 * i, 1) for i in range(20)])
+    long = C.OcpFesMsk.prepare_ocp(model=long_m, final_time=2.0, n_shooting=20,
+                                   msk_info={"bound_type": "start", "bound_data": [0, 5]})
+    for k in range(3):  # history after k committed cycles (relative to the window start)
+        past = [round(0.1 * i - 0.5 * k, 10) for i in range(5 * k)][-4:]
+        hist = [-1e7] * (4 - len(past)) + past
+        w = nm._window_ocp(hist)
+        rows = np.asarray(w.stim_rows)[:10]  # the intervals' rows (node N's row drives no interval)
+        ref = np.asarray(long.stim_rows)[5 * k: 5 * k + 10] - 0.5 * k
+        pad = ref < -1e6
+        assert np.allclose(rows[~pad], ref[~pad], atol=1e-12, rtol=0), k
+        assert np.all(rows[pad] < -1e6)
+        lo, hi = w.x_bounds
+        assert np.array_equal(lo[:, 0], hi[:, 0])
+    assert nm.model.muscles_dynamics_model[0].stim_time == [0.0, 0.1, 0.2, 0.3, 0.4]  # the caller's model untouched
+    with pytest.raises(NotImplementedError):
+        C.NmpcFesMsk.prepare_nmpc(model=mm, cycle_duration=0.5, n_cycles_simultaneous=2, n_cycles_to_advance=1,
+                                  pulse_intensity={"min": 20})
+    with pytest.raises(ValueError):
+        C.NmpcFesMsk(mm, cycle_duration=0.3)
