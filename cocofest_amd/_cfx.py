@@ -97,7 +97,8 @@ class IpmOptions(C.Structure):
                 ("bound_push", C.c_double), ("tau_min", C.c_double), ("kappa_eps", C.c_double),
                 ("kappa_mu", C.c_double), ("theta_mu", C.c_double), ("s_max", C.c_double), ("armijo", C.c_double),
                 ("max_backtrack", C.c_int32), ("delta_c", C.c_double), ("curv_min", C.c_double),
-                ("max_soc", C.c_int32), ("kappa_soc", C.c_double)]
+                ("max_soc", C.c_int32), ("kappa_soc", C.c_double), ("watchdog_shortened_iter_trigger", C.c_int32),
+                ("watchdog_trial_iter_max", C.c_int32)]
 
 
 class IpmStats(C.Structure):

@@ -45,7 +45,9 @@ constexpr int kMaxBorder = 32;  // free parameters handled as a dense border
 struct Scal {
     double mu, tau, sf, fS, theta, phi, dphi, alpha, a_p, a_z, theta_max, theta_min, dw, dwl, err0, theta_soc, a_c,
         theta_r, a_r;
-    int32_t done, acc, iters, fpos, accepted, armijo, soc, reinit, todo, pad;
+    double wd_theta, wd_phi, wd_dphi, wd_ap, wd_mu;  // watchdog reference: the iterate where it started
+    int32_t done, acc, iters, fpos, accepted, armijo, soc, reinit, todo;
+    int32_t wd_short, wd_on, wd_trial, skip_first, forced, pad[2];
 };
 
 struct IpmK {
@@ -78,6 +80,8 @@ struct IpmK {
     const int32_t *act, *sl, *ccr_ptr, *ccr_q, *ccr_a;
     // per instance
     double *x, *zl, *zu, *dx, *dzl, *dzu, *xt, *xacc, *xr, *dxr, *sig, *gF;  // [B][nf]
+    double *lbI, *ubI;                                                      // [B][nf] bounds (moved per instance)
+    double *wx, *wzl, *wzu, *wy;                                            // watchdog iterate [B][nf] / [B][m]
     double *rhs, *rb;                                                       // [B][nK]
     double *y, *dy, *gS, *csoc, *sg, *ysc, *graw, *gt;                      // [B][m]
     double *vx, *vt, *grad;                                                 // [B][n]
@@ -153,17 +157,35 @@ __device__ inline double step_term(bool has, double s, double ds, double tau) {
     return (has && ds < 0) ? (-tau * s) / ds : INFINITY;
 }
 
+// Ipopt's safe slacks (solver.py _safe_slacks): a slack in [0, eps min(1, mu)) — a point that landed on its bound in
+// floating point — is measured to the bound moved outwards by slack_move max(1, |bound|); k_ipm_update makes the move
+// of an accepted point permanent
+constexpr double kEps = 2.220446049250313e-16;
+constexpr double kSlackMove = 1.8189894035458565e-12;  // eps^(3/4), Ipopt slack_move
+__device__ inline double slack_min(double mu) { return kEps * clamp_hi(mu, 1.0); }
+__device__ inline double moved_lb(double lb, double s, double smin) {
+    return (s < smin && s >= 0) ? lb - kSlackMove * clamp_lo(fabs(lb), 1.0) : lb;
+}
+__device__ inline double moved_ub(double ub, double s, double smin) {
+    return (s < smin && s >= 0) ? ub + kSlackMove * clamp_lo(fabs(ub), 1.0) : ub;
+}
+
 // solver.py _barrier_obj: f - mu (sum ln sl + sum ln su), +inf outside the bounds
-__device__ double barrier_obj(const IpmK& K, const double* x, double f, double mu, double* sh) {
+__device__ double barrier_obj(const IpmK& K, int64_t b, const double* x, double f, double mu, double* sh) {
     double sL = 0.0, sU = 0.0, bad = 0.0;
+    const double* lbI = K.lbI + b * K.nf;
+    const double* ubI = K.ubI + b * K.nf;
+    const double smin = slack_min(mu);
     for (int i = threadIdx.x; i < K.nf; i += kIB) {
         if (K.hasL[i]) {
-            const double sl = x[i] - K.lbF[i];
+            double sl = x[i] - lbI[i];
+            sl = x[i] - moved_lb(lbI[i], sl, smin);
             if (sl <= 0) bad = 1.0;
             sL += log(clamp_lo(sl, 1e-300));
         }
         if (K.hasU[i]) {
-            const double su = K.ubF[i] - x[i];
+            double su = ubI[i] - x[i];
+            su = moved_ub(ubI[i], su, smin) - x[i];
             if (su <= 0) bad = 1.0;
             sU += log(clamp_lo(su, 1e-300));
         }
@@ -182,10 +204,16 @@ __device__ void filter_accept(const IpmK& K, const Scal& S, const double* filt, 
         if (tt >= filt[2 * k] && pt >= filt[2 * k + 1]) inf_ = 1.0;
     inf_ = breduce(inf_, OpMax(), sh);
     const bool finite = isfinite(pt) && isfinite(tt);
-    const bool switching = (S.dphi < 0) && (alpha * pow(clamp_lo(-S.dphi, 0.0), 2.3) > 1.0 * pow(S.theta, 1.1)) &&
-                           (S.theta <= S.theta_min);
-    const bool armijo_ok = pt <= S.phi + K.o.armijo * alpha * S.dphi;
-    const bool suff = (tt <= (1 - 1e-5) * S.theta) || (pt <= S.phi - 1e-5 * S.theta);
+    // in the watchdog, trial points are judged against the iterate where it started (with its full step length)
+    const double theta = S.wd_on ? S.wd_theta : S.theta, phi = S.wd_on ? S.wd_phi : S.phi;
+    const double dphi = S.wd_on ? S.wd_dphi : S.dphi;
+    if (S.wd_on) alpha = S.wd_ap;
+    const bool switching = (dphi < 0) && (alpha * pow(clamp_lo(-dphi, 0.0), 2.3) > 1.0 * pow(theta, 1.1)) &&
+                           (theta <= S.theta_min);
+    // Ipopt's Compare_le(lhs, rhs, base): lhs - rhs <= 10 eps |base| (round-off in phi near an optimum)
+    const double tol_phi = 10 * kEps * fabs(phi);
+    const bool armijo_ok = (pt - phi) - K.o.armijo * alpha * dphi <= tol_phi;
+    const bool suff = (tt - (1 - 1e-5) * theta <= 10 * kEps * theta) || ((pt - phi) + 1e-5 * theta <= tol_phi);
     ok = finite && (tt <= S.theta_max) && !(inf_ > 0) && (switching ? armijo_ok : suff);
     arm = switching && armijo_ok;
 }
@@ -231,6 +259,8 @@ __global__ void __launch_bounds__(kIB) k_ipm_init(const IpmK K) {
         double xi = K.vx[b * K.n + K.free[i]] / K.d[i];
         const bool hL = K.hasL[i], hU = K.hasU[i];
         const double lb = K.lbF[i], ub = K.ubF[i];
+        K.lbI[b * K.nf + i] = lb;
+        K.ubI[b * K.nf + i] = ub;
         double pl = K.o.bound_push * clamp_lo(hL ? fabs(lb) : 1.0, 1.0);
         double pu = K.o.bound_push * clamp_lo(hU ? fabs(ub) : 1.0, 1.0);
         const double width = (hL && hU) ? ub - lb : INFINITY;
@@ -286,6 +316,8 @@ __global__ void __launch_bounds__(kIB) k_ipm_begin(const IpmK K, int mode, int s
     const double* zl = K.zl + b * nf;
     const double* zu = K.zu + b * nf;
     const double* y = K.y + b * m;
+    const double* lbI = K.lbI + b * nf;
+    const double* ubI = K.ubI + b * nf;
     double* rhs = K.rhs + b * K.nK;
     double szl = 0, szu = 0, sy = 0, ed = 0, ep = 0, ecl = 0, ecu = 0;
     for (int i = threadIdx.x; i < nf; i += kIB) {
@@ -299,8 +331,8 @@ __global__ void __launch_bounds__(kIB) k_ipm_begin(const IpmK K, int mode, int s
         const double rd = gj - zl[i] + zu[i];
         szl += fabs(zl[i]);
         szu += fabs(zu[i]);
-        const double cl = K.hasL[i] ? (x[i] - K.lbF[i]) * zl[i] : 0.0;
-        const double cu = K.hasU[i] ? (K.ubF[i] - x[i]) * zu[i] : 0.0;
+        const double cl = K.hasL[i] ? (x[i] - lbI[i]) * zl[i] : 0.0;
+        const double cu = K.hasU[i] ? (ubI[i] - x[i]) * zu[i] : 0.0;
         ed = max_n(ed, fabs(rd));
         ecl = max_n(ecl, fabs(cl));
         ecu = max_n(ecu, fabs(cu));
@@ -332,8 +364,8 @@ __global__ void __launch_bounds__(kIB) k_ipm_begin(const IpmK K, int mode, int s
         const double mu = S.mu;
         double ecm = 0.0;
         for (int i = threadIdx.x; i < nf; i += kIB) {
-            const double cl = K.hasL[i] ? (x[i] - K.lbF[i]) * zl[i] - mu : 0.0;
-            const double cu = K.hasU[i] ? (K.ubF[i] - x[i]) * zu[i] - mu : 0.0;
+            const double cl = K.hasL[i] ? (x[i] - lbI[i]) * zl[i] - mu : 0.0;
+            const double cu = K.hasU[i] ? (ubI[i] - x[i]) * zu[i] - mu : 0.0;
             ecm = max_n(ecm, max_n(fabs(cl), fabs(cu)));
         }
         ecm = breduce(ecm, OpMax(), sh) / sc;
@@ -348,7 +380,7 @@ __global__ void __launch_bounds__(kIB) k_ipm_begin(const IpmK K, int mode, int s
     double* sig = K.sig + b * nf;
     for (int i = threadIdx.x; i < nf; i += kIB) {
         const bool hL = K.hasL[i], hU = K.hasU[i];
-        const double sl = hL ? x[i] - K.lbF[i] : 1.0, su = hU ? K.ubF[i] - x[i] : 1.0;
+        const double sl = hL ? x[i] - lbI[i] : 1.0, su = hU ? ubI[i] - x[i] : 1.0;
         sig[i] = (hL ? zl[i] / sl : 0.0) + (hU ? zu[i] / su : 0.0);
         const double bar = (hL ? mu / sl : 0.0) - (hU ? mu / su : 0.0);
         rhs[i] = -(rhs[i] - bar);
@@ -617,10 +649,12 @@ __global__ void __launch_bounds__(kIB) k_ipm_dir(const IpmK K, int it) {
     double* dzl = K.dzl + b * nf;
     double* dzu = K.dzu + b * nf;
     const double mu = S.mu, tau = S.tau;
+    const double* lbI = K.lbI + b * nf;
+    const double* ubI = K.ubI + b * nf;
     double apl = INFINITY, apu = INFINITY, azl = INFINITY, azu = INFINITY, dphi = 0.0, theta = 0.0;
     for (int i = threadIdx.x; i < nf; i += kIB) {
         const bool hL = K.hasL[i], hU = K.hasU[i];
-        const double sl = hL ? x[i] - K.lbF[i] : 1.0, su = hU ? K.ubF[i] - x[i] : 1.0;
+        const double sl = hL ? x[i] - lbI[i] : 1.0, su = hU ? ubI[i] - x[i] : 1.0;
         const double vzl = hL ? mu / sl - zl[i] - zl[i] / sl * dx[i] : 0.0;
         const double vzu = hU ? mu / su - zu[i] + zu[i] / su * dx[i] : 0.0;
         dzl[i] = vzl;
@@ -639,8 +673,21 @@ __global__ void __launch_bounds__(kIB) k_ipm_dir(const IpmK K, int it) {
     azu = breduce(azu, OpMin(), sh);
     dphi = breduce(dphi, OpSum(), sh);
     theta = breduce(theta, OpSum(), sh);
-    const double phi = barrier_obj(K, x, S.fS, mu, sh);
+    const double phi = barrier_obj(K, b, x, S.fS, mu, sh);
     const double a_p = min_n(clamp_hi(apl, 1.0), clamp_hi(apu, 1.0));
+    // watchdog start (Ipopt StartWatchDog): remember this iterate and its line-search reference values
+    const int trig = K.o.watchdog_shortened_iter_trigger;
+    const bool wd_start = !S.done && !S.wd_on && trig > 0 && S.wd_short >= trig;
+    if (wd_start) {
+        for (int i = threadIdx.x; i < nf; i += kIB) {
+            K.wx[b * nf + i] = x[i];
+            K.wzl[b * nf + i] = zl[i];
+            K.wzu[b * nf + i] = zu[i];
+        }
+        for (int j = threadIdx.x; j < m; j += kIB) K.wy[b * m + j] = K.y[b * m + j];
+    }
+    const double alpha0 = S.skip_first ? 0.5 * a_p : a_p;
+    __syncthreads();
     if (threadIdx.x == 0) {
         S.dwl = S.dw;
         S.a_p = a_p;
@@ -652,16 +699,26 @@ __global__ void __launch_bounds__(kIB) k_ipm_dir(const IpmK K, int it) {
             S.theta_max = 1e4 * clamp_lo(theta, 1.0);
             S.theta_min = 1e-4 * clamp_lo(theta, 1.0);
         }
-        S.alpha = a_p;
+        if (wd_start) {
+            S.wd_on = 1;
+            S.wd_trial = 0;
+            S.wd_theta = theta;
+            S.wd_phi = phi;
+            S.wd_dphi = dphi;
+            S.wd_ap = a_p;
+            S.wd_mu = mu;
+        }
+        S.alpha = alpha0;
         S.accepted = S.done;
         S.armijo = 0;
         S.soc = 0;
+        S.forced = 0;
     }
     double* xacc = K.xacc + b * nf;
     double* xt = K.xt + b * nf;
     for (int i = threadIdx.x; i < nf; i += kIB) {
         xacc[i] = x[i];
-        xt[i] = x[i] + a_p * dx[i];
+        xt[i] = x[i] + alpha0 * dx[i];
     }
     __syncthreads();
     write_full(K, b, xt, K.vt);
@@ -682,17 +739,19 @@ __global__ void __launch_bounds__(kIB) k_ipm_accept(const IpmK K, int ls, int sl
     for (int j = threadIdx.x; j < m; j += kIB) tt += fabs(gt[j] * sg[j]);
     tt = breduce(tt, OpSum(), sh);
     const double* xt = K.xt + b * nf;
-    const double pt = barrier_obj(K, xt, K.ft[b] * S.sf, S.mu, sh);
+    const double pt = barrier_obj(K, b, xt, K.ft[b] * S.sf, S.mu, sh);
     bool ok, arm;
     filter_accept(K, S, K.filt + b * kFilt * 2, tt, pt, S.alpha, sh, ok, arm);
     ok = ok && !S.accepted;
+    // a watchdog iteration takes its full step whether or not it is acceptable (no corrections, no backtracking)
+    const bool forced = ls == 0 && S.wd_on && !ok && !S.accepted;
     bool soc = false;
     if (ls == 0) {
-        soc = !S.accepted && !ok && (tt >= S.theta);
+        soc = !S.accepted && !ok && !forced && (tt >= S.theta) && !S.skip_first;
         double* cs = K.csoc + b * m;
         for (int j = threadIdx.x; j < m; j += kIB) cs[j] = S.alpha * K.gS[b * m + j] + gt[j] * sg[j];
     }
-    if (ok) {
+    if (ok || forced) {
         double* xacc = K.xacc + b * nf;
         for (int i = threadIdx.x; i < nf; i += kIB) xacc[i] = xt[i];
     }
@@ -704,6 +763,10 @@ __global__ void __launch_bounds__(kIB) k_ipm_accept(const IpmK K, int ls, int sl
         }
         if (ok) {
             S.armijo = arm;
+            S.accepted = 1;
+        }
+        if (forced) {
+            S.forced = 1;
             S.accepted = 1;
         }
     }
@@ -748,11 +811,13 @@ __global__ void __launch_bounds__(kIB) k_ipm_soc_trial(const IpmK K) {
     const double* x = K.x + b * nf;
     const double* rb = K.rb + b * K.nKp;
     const double tau = K.sc[b].tau;
+    const double* lbI = K.lbI + b * nf;
+    const double* ubI = K.ubI + b * nf;
     double apl = INFINITY, apu = INFINITY;
     for (int i = threadIdx.x; i < nf; i += kIB) {
         const double d = rb[K.pos[i]];
-        if (K.hasL[i]) apl = min_n(apl, step_term(true, x[i] - K.lbF[i], d, tau));
-        if (K.hasU[i]) apu = min_n(apu, step_term(true, K.ubF[i] - x[i], -d, tau));
+        if (K.hasL[i]) apl = min_n(apl, step_term(true, x[i] - lbI[i], d, tau));
+        if (K.hasU[i]) apu = min_n(apu, step_term(true, ubI[i] - x[i], -d, tau));
     }
     apl = breduce(apl, OpMin(), sh);
     apu = breduce(apu, OpMin(), sh);
@@ -776,7 +841,7 @@ __global__ void __launch_bounds__(kIB) k_ipm_soc_accept(const IpmK K, int slot) 
     for (int j = threadIdx.x; j < m; j += kIB) tt += fabs(gt[j] * sg[j]);
     tt = breduce(tt, OpSum(), sh);
     const double* xr = K.xr + b * nf;
-    const double pt = barrier_obj(K, xr, K.ft[b] * S.sf, S.mu, sh);
+    const double pt = barrier_obj(K, b, xr, K.ft[b] * S.sf, S.mu, sh);
     bool okc, armc;
     filter_accept(K, S, K.filt + b * kFilt * 2, tt, pt, S.alpha, sh, okc, armc);
     okc = okc && S.soc && (S.a_c >= 0.99);
@@ -813,12 +878,14 @@ __global__ void __launch_bounds__(kIB) k_ipm_resto_init(const IpmK K, int slot) 
     const double* x = K.x + b * nf;
     const double* rb = K.rb + b * K.nKp;
     double* dxr = K.dxr + b * nf;
+    const double* lbI = K.lbI + b * nf;
+    const double* ubI = K.ubI + b * nf;
     double apl = INFINITY, apu = INFINITY, th = 0.0;
     for (int i = threadIdx.x; i < nf; i += kIB) {
         const double d = rb[K.pos[i]];
         dxr[i] = d;
-        if (K.hasL[i]) apl = min_n(apl, step_term(true, x[i] - K.lbF[i], d, S.tau));
-        if (K.hasU[i]) apu = min_n(apu, step_term(true, K.ubF[i] - x[i], -d, S.tau));
+        if (K.hasL[i]) apl = min_n(apl, step_term(true, x[i] - lbI[i], d, S.tau));
+        if (K.hasU[i]) apu = min_n(apu, step_term(true, ubI[i] - x[i], -d, S.tau));
     }
     for (int j = threadIdx.x; j < m; j += kIB) th += fabs(K.gS[b * m + j]);
     apl = breduce(apl, OpMin(), sh);
@@ -910,8 +977,15 @@ __global__ void __launch_bounds__(kIB) k_ipm_update(const IpmK K, int resto) {
     const int nf = K.nf, m = K.m;
     load_scal(K, b, S);
     const bool failed = !S.accepted && !S.done;
-    const bool grow = !S.done && S.accepted && !S.armijo;
+    const bool forced = S.forced;
+    const bool grow = !S.done && S.accepted && !S.armijo && !forced;
     const bool reset = failed && resto && m > 0;
+    // watchdog bookkeeping (solver.py): an acceptable point ends it; after watchdog_trial_iter_max unacceptable full
+    // steps the iterate returns to where it started, and the next line search starts at half its step
+    const bool wd_ok = S.wd_on && S.accepted && !forced;
+    const int wd_trial = S.wd_trial + (forced ? 1 : 0);
+    const bool wd_back = forced && wd_trial > K.o.watchdog_trial_iter_max;
+    const bool shortened = S.accepted && !forced && S.alpha < S.a_p;
     double* filt = K.filt + b * kFilt * 2;
     if (threadIdx.x == 0 && grow) {
         const int k = S.fpos % kFilt;
@@ -944,7 +1018,9 @@ __global__ void __launch_bounds__(kIB) k_ipm_update(const IpmK K, int resto) {
     const double az = (step && !failed) ? S.a_z : 0.0;
     const bool mz = az > 0 && !(nfz > 0);
     const double* xnew = reset ? K.xr + b * nf : K.xacc + b * nf;
-    const double mu = S.mu;
+    const double mu = S.mu, smin = slack_min(mu);
+    double* lbI = K.lbI + b * nf;
+    double* ubI = K.ubI + b * nf;
     for (int i = threadIdx.x; i < nf; i += kIB) {
         double xi = step ? xnew[i] : x[i];
         x[i] = xi;
@@ -954,17 +1030,28 @@ __global__ void __launch_bounds__(kIB) k_ipm_update(const IpmK K, int resto) {
             u = u + az * dzu[i];
         }
         if (K.hasL[i]) {
-            const double sl = xi - K.lbF[i];
+            const double lbv = moved_lb(lbI[i], xi - lbI[i], smin);
+            lbI[i] = lbv;
+            const double sl = xi - lbv;
             l = clamp_hi(clamp_lo(l, mu / (1e10 * sl)), 1e10 * mu / sl);
         }
         if (K.hasU[i]) {
-            const double su = K.ubF[i] - xi;
+            const double ubv = moved_ub(ubI[i], ubI[i] - xi, smin);
+            ubI[i] = ubv;
+            const double su = ubv - xi;
             u = clamp_hi(clamp_lo(u, mu / (1e10 * su)), 1e10 * mu / su);
         }
         zl[i] = l;
         zu[i] = u;
+        if (wd_back) {  // back to the watchdog iterate
+            x[i] = K.wx[b * nf + i];
+            zl[i] = K.wzl[b * nf + i];
+            zu[i] = K.wzu[b * nf + i];
+        }
     }
-    if (mv)
+    if (wd_back)
+        for (int j = threadIdx.x; j < m; j += kIB) K.y[b * m + j] = K.wy[b * m + j];
+    else if (mv)
         for (int j = threadIdx.x; j < m; j += kIB) K.y[b * m + j] = K.y[b * m + j] + alpha * dy[j];
     __syncthreads();
     write_full(K, b, x, K.vx);
@@ -973,6 +1060,11 @@ __global__ void __launch_bounds__(kIB) k_ipm_update(const IpmK K, int resto) {
         if (reset) S.reinit = 1;
         S.alpha = alpha;
         S.iters += step;
+        S.wd_trial = wd_trial;
+        S.wd_on = S.wd_on && !wd_ok && !wd_back;
+        S.wd_short = (wd_ok || wd_back || failed || !shortened) ? 0 : S.wd_short + 1;
+        S.skip_first = wd_back;
+        if (wd_back) S.mu = S.wd_mu;
     }
     store_scal(K, b, S);
 }
@@ -1102,6 +1194,8 @@ extern "C" void cfx_ipm_default_options(cfx_ipm_options* o) {
     o->curv_min = 1e-8;
     o->max_soc = 4;
     o->kappa_soc = 0.99;
+    o->watchdog_shortened_iter_trigger = 10;
+    o->watchdog_trial_iter_max = 3;
 }
 
 // CSR of `key` (values in [0, nkeys)) with the sources of each key in increasing source order
@@ -1147,6 +1241,7 @@ extern "C" int cfx_ipm_create(cfx_handle* h, const double* lb, const double* ub,
     cfx_sizes sz{};
     if (cfx_get_sizes(h, &sz) != CFX_OK || (s->B > 1 && layout != CFX_LAYOUT_AOS) || layout == CFX_LAYOUT_TILED64 ||
         n_params < 0 || n_params > sz.nv || K.o.max_iter < 0 || K.o.max_backtrack < 1 || K.o.max_soc < 0 ||
+        K.o.watchdog_shortened_iter_trigger < 0 || K.o.watchdog_trial_iter_max < 0 ||
         s->B > 0x7fffffff) {
         s->err = "cfx_ipm_create: the handle must use CFX_LAYOUT_AOS (or batch 1) and the options must be valid";
         return create_fail(s, CFX_EINVAL);
@@ -1503,11 +1598,12 @@ extern "C" int cfx_ipm_create(cfx_handle* h, const double* lb, const double* ub,
     K.kkt_src = dupload(s, kcode, &rc);
     K.pos = dupload(s, pos, &rc);
     const size_t B = (size_t)s->B;
-    double** fbufs[] = {&K.x, &K.zl, &K.zu, &K.dx, &K.dzl, &K.dzu, &K.xt, &K.xacc, &K.xr, &K.dxr, &K.sig, &K.gF};
+    double** fbufs[] = {&K.x,   &K.zl,  &K.zu, &K.dx,  &K.dzl, &K.dzu, &K.xt, &K.xacc, &K.xr,
+                        &K.dxr, &K.sig, &K.gF, &K.lbI, &K.ubI, &K.wx,  &K.wzl, &K.wzu};
     for (double** p : fbufs) *p = dalloc<double>(s, B * nf, &rc);
     K.rhs = dalloc<double>(s, B * nK, &rc);
     K.rb = dalloc<double>(s, B * nKp, &rc);
-    double** mbufs[] = {&K.y, &K.dy, &K.gS, &K.csoc, &K.sg, &K.ysc, &K.graw, &K.gt};
+    double** mbufs[] = {&K.y, &K.dy, &K.gS, &K.csoc, &K.sg, &K.ysc, &K.graw, &K.gt, &K.wy};
     for (double** p : mbufs) *p = dalloc<double>(s, B * m, &rc);
     K.vx = dalloc<double>(s, B * n, &rc);
     K.vt = dalloc<double>(s, B * n, &rc);

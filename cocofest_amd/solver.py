@@ -48,6 +48,11 @@ class IpmOptions:
     refine: int = 0
     max_soc: int = 4        # second-order corrections per iteration (Ipopt max_soc)
     kappa_soc: float = 0.99  # required infeasibility decrease between corrections (Ipopt kappa_soc)
+    # Ipopt's watchdog (on by default there): after this many consecutive shortened line searches the full step is
+    # taken for up to watchdog_trial_iter_max iterations, judged against the iterate where the watchdog started;
+    # if none is acceptable the solver returns there and backtracks.  0 disables it
+    watchdog_shortened_iter_trigger: int = 10
+    watchdog_trial_iter_max: int = 3
     verbose: bool = False
 
 
@@ -299,7 +304,9 @@ class BatchedIpm:
         self._set_function_scaling(v)
         x = v[:, self.freeT] / self.d
         # push the start strictly inside the bounds (Ipopt bound_push / bound_frac)
-        lbF, ubF, hasL, hasU = self.lbF, self.ubF, self.hasL, self.hasU
+        # per-instance bounds: Ipopt moves a bound by slack_move when a slack falls below machine precision
+        lbF, ubF, hasL, hasU = self.lbF.expand(B, -1).clone(), self.ubF.expand(B, -1).clone(), self.hasL, self.hasU
+        self._lbI, self._ubI = lbF, ubF
         pl = opt.bound_push * torch.clamp(torch.where(hasL, lbF.abs(), torch.ones_like(lbF)), min=1.0)
         pu = opt.bound_push * torch.clamp(torch.where(hasU, ubF.abs(), torch.ones_like(ubF)), min=1.0)
         both = hasL & hasU
@@ -324,6 +331,12 @@ class BatchedIpm:
         filt = torch.full((B, 64, 2), np.inf, dtype=torch.float64, device=self.dev)  # (theta, phi) pairs
         filt[:, :, 1] = -np.inf
         fpos = torch.zeros((B,), dtype=torch.int64, device=self.dev)
+        # watchdog state (Ipopt IpBacktrackingLineSearch: StartWatchDog / StopWatchDog)
+        wd_short = torch.zeros((B,), dtype=torch.int64, device=self.dev)
+        wd_on = torch.zeros((B,), dtype=torch.bool, device=self.dev)
+        wd_trial = torch.zeros((B,), dtype=torch.int64, device=self.dev)
+        skip_first = torch.zeros((B,), dtype=torch.bool, device=self.dev)
+        wd = None
 
         self._v_template = v
 
@@ -405,20 +418,45 @@ class BatchedIpm:
             if it == 0:
                 theta_max = 1e4 * torch.clamp(theta, min=1.0)
                 theta_min = 1e-4 * torch.clamp(theta, min=1.0)
-            alpha = a_p.clone()
+            # watchdog start: remember this iterate, its direction and its line-search reference values
+            wd_start = (~done) & (~wd_on) & (wd_short >= opt.watchdog_shortened_iter_trigger) & \
+                (opt.watchdog_shortened_iter_trigger > 0)
+            if bool(wd_start.any()):
+                cur = dict(x=x, y=y, zl=zl, zu=zu, mu=mu, theta=theta, phi=phi, dphi=dphi, a_p=a_p)
+                if wd is None:
+                    wd = {k: t.clone() for k, t in cur.items()}
+                for k, t in cur.items():
+                    c = wd_start.view(-1, *([1] * (t.dim() - 1)))
+                    wd[k] = torch.where(c, t, wd[k])
+                wd_on = wd_on | wd_start
+                wd_trial = torch.where(wd_start, torch.zeros_like(wd_trial), wd_trial)
+            if wd is not None:  # in the watchdog, trial points are judged against the watchdog iterate
+                r_theta = torch.where(wd_on, wd["theta"], theta)
+                r_phi = torch.where(wd_on, wd["phi"], phi)
+                r_dphi = torch.where(wd_on, wd["dphi"], dphi)
+            else:
+                r_theta, r_phi, r_dphi = theta, phi, dphi
+            alpha = torch.where(skip_first, 0.5 * a_p, a_p)
             accepted = done.clone()
+            forced = torch.zeros_like(done)
             armijo_step = torch.zeros_like(done)
             x_acc = x.clone()
             dx_acc = dx.clone()
             for ls in range(opt.max_backtrack):
                 xt = x + alpha[:, None] * dx
                 gt, ft = self._scaled_gf(full(xt))
-                ok, arm = self._filter_accept(gt, ft, xt, theta, phi, dphi, alpha, mu, theta_max, theta_min, filt)
+                a_test = torch.where(wd_on, wd["a_p"], alpha) if wd is not None else alpha
+                ok, arm = self._filter_accept(gt, ft, xt, r_theta, r_phi, r_dphi, a_test, mu, theta_max, theta_min,
+                                              filt)
                 ok = ok & ~accepted
                 if ls == 0:
+                    # watchdog iterations take the full step whether or not it is acceptable (no corrections)
+                    forced = wd_on & ~ok & ~accepted
+                    x_acc = torch.where(forced[:, None], xt, x_acc)
+                    accepted = accepted | forced
                     # second-order corrections for rejected full steps that increased the infeasibility: up to
                     # max_soc of them while each cuts the infeasibility by kappa_soc (Ipopt's defaults 4 / 0.99)
-                    soc_try = (~accepted) & (~ok) & (gt.abs().sum(1) >= theta)
+                    soc_try = (~accepted) & (~ok) & (gt.abs().sum(1) >= theta) & ~skip_first
                     c_soc = alpha[:, None] * g + gt
                     theta_soc = gt.abs().sum(1)
                     for _ in range(opt.max_soc):
@@ -447,8 +485,17 @@ class BatchedIpm:
                     break
                 alpha = torch.where(accepted, alpha, alpha * 0.5)
             failed = ~accepted
+            # watchdog bookkeeping: an acceptable point ends it; after watchdog_trial_iter_max unacceptable full
+            # steps the solver returns to the watchdog iterate, and the next line search starts at half its step
+            wd_ok = wd_on & accepted & ~forced
+            wd_trial = torch.where(forced, wd_trial + 1, wd_trial)
+            wd_back = forced & (wd_trial > opt.watchdog_trial_iter_max)
+            wd_on = wd_on & ~wd_ok & ~wd_back
+            shortened = accepted & ~forced & (alpha < a_p)
+            wd_short = torch.where(wd_ok | wd_back | failed | ~shortened, torch.zeros_like(wd_short), wd_short + 1)
+            skip_first = wd_back.clone()
             # filter augmentation for h-type (non-Armijo) steps
-            grow = (~done) & accepted & ~armijo_step
+            grow = (~done) & accepted & ~armijo_step & ~forced
             filt = torch.where(grow[:, None, None] & (torch.arange(filt.shape[1], device=self.dev) ==
                                                       (fpos % filt.shape[1])[:, None])[:, :, None],
                                torch.stack([(1 - 1e-5) * theta, phi - 1e-5 * theta], dim=1)[:, None, :], filt)
@@ -480,11 +527,17 @@ class BatchedIpm:
             mz = (az > 0) & torch.isfinite(dzl).all(1) & torch.isfinite(dzu).all(1)
             zl = torch.where(mz[:, None], zl + az[:, None] * dzl, zl)
             zu = torch.where(mz[:, None], zu + az[:, None] * dzu, zu)
+            self._adjust_bounds(x, mu)
             # keep z within [mu / (kappa s), kappa mu / s] (Ipopt kappa_Sigma = 1e10)
             sl = torch.where(hasL, x - lbF, torch.ones_like(x))
             su = torch.where(hasU, ubF - x, torch.ones_like(x))
             zl = torch.where(hasL, torch.clamp(zl, min=mu[:, None] / (1e10 * sl), max=1e10 * mu[:, None] / sl), zl)
             zu = torch.where(hasU, torch.clamp(zu, min=mu[:, None] / (1e10 * su), max=1e10 * mu[:, None] / su), zu)
+            if wd is not None and bool(wd_back.any()):  # back to the watchdog iterate
+                c = wd_back[:, None]
+                x, y = torch.where(c, wd["x"], x), torch.where(c, wd["y"], y)
+                zl, zu = torch.where(c, wd["zl"], zl), torch.where(c, wd["zu"], zu)
+                mu = torch.where(wd_back, wd["mu"], mu)
             iters = iters + step.long()
         x = torch.minimum(torch.maximum(x, self.lbF0), self.ubF0)  # inf bounds leave x as is
         vfinal = full(x)
@@ -521,8 +574,8 @@ class BatchedIpm:
         K = self.band.factor(self._kkt_band(torch.zeros((B, self.hrF.numel()), dtype=torch.float64, device=self.dev),
                                             sig + 1.0, jv), self.kl, self.ku)
         dx = self._kkt_solve(K, torch.cat([torch.zeros((B, nf), dtype=torch.float64, device=self.dev), -g], 1))[:, :nf]
-        sl = torch.where(self.hasL, x - self.lbF, torch.ones_like(x))
-        su = torch.where(self.hasU, self.ubF - x, torch.ones_like(x))
+        sl = torch.where(self.hasL, x - self._lbI, torch.ones_like(x))
+        su = torch.where(self.hasU, self._ubI - x, torch.ones_like(x))
         a = torch.minimum(self._max_step(sl, dx, self.hasL, tau), self._max_step(su, -dx, self.hasU, tau))
         theta = g.abs().sum(1)
         out = x.clone()
@@ -550,10 +603,35 @@ class BatchedIpm:
         ratio = torch.where(has & (ds < 0), -tau[:, None] * s / ds, torch.full_like(s, np.inf))
         return torch.clamp(ratio.amin(1), max=1.0)
 
+    SLACK_MOVE = np.finfo(np.float64).eps ** 0.75  # Ipopt slack_move
+
+    def _safe_slacks(self, x, mu):
+        """Slacks to the current bounds, and for those below eps min(1, mu) (a trial point that lands on a bound
+        in floating point) the bound moved outwards by slack_move max(1, |bound|) (Ipopt's CalculateSafeSlack /
+        AdjustVariableBounds).  Returns (sl, su, lb, ub) with the moved bounds."""
+        torch = self.torch
+        s_min = np.finfo(np.float64).eps * torch.clamp(mu, max=1.0)[:, None]
+        lb, ub = self._lbI, self._ubI
+        sl = torch.where(self.hasL, x - lb, torch.ones_like(x))
+        su = torch.where(self.hasU, ub - x, torch.ones_like(x))
+        ml = self.hasL & (sl < s_min) & (sl >= 0)
+        mu_ = self.hasU & (su < s_min) & (su >= 0)
+        if bool(ml.any()) or bool(mu_.any()):
+            lb = torch.where(ml, lb - self.SLACK_MOVE * torch.clamp(lb.abs(), min=1.0), lb)
+            ub = torch.where(mu_, ub + self.SLACK_MOVE * torch.clamp(ub.abs(), min=1.0), ub)
+            sl = torch.where(self.hasL, x - lb, sl)
+            su = torch.where(self.hasU, ub - x, su)
+        return sl, su, lb, ub
+
+    def _adjust_bounds(self, x, mu):
+        """Make the bound moves of an accepted point permanent (per instance)."""
+        _, _, lb, ub = self._safe_slacks(x, mu)
+        self._lbI.copy_(lb)
+        self._ubI.copy_(ub)
+
     def _barrier_obj(self, f, x, mu):
         torch = self.torch
-        sl = torch.where(self.hasL, x - self.lbF, torch.ones_like(x))
-        su = torch.where(self.hasU, self.ubF - x, torch.ones_like(x))
+        sl, su, _, _ = self._safe_slacks(x, mu)
         bad = ((sl <= 0) & self.hasL).any(1) | ((su <= 0) & self.hasU).any(1)
         barrier = torch.where(self.hasL, torch.log(torch.clamp(sl, min=1e-300)), torch.zeros_like(x)).sum(1) + \
             torch.where(self.hasU, torch.log(torch.clamp(su, min=1e-300)), torch.zeros_like(x)).sum(1)
@@ -568,8 +646,12 @@ class BatchedIpm:
         finite = torch.isfinite(pt) & torch.isfinite(tt)
         s_phi, s_theta, delta = 2.3, 1.1, 1.0
         switching = (dphi < 0) & (alpha * (-dphi).clamp(min=0) ** s_phi > delta * theta ** s_theta) & (theta <= theta_min)
-        armijo_ok = pt <= phi + opt.armijo * alpha * dphi
-        suff = (tt <= (1 - 1e-5) * theta) | (pt <= phi - 1e-5 * theta)
+        # Ipopt's Compare_le(lhs, rhs, base): lhs - rhs <= 10 eps |base|, so that round-off in phi near an optimum
+        # does not reject a step
+        tol_phi = 10 * np.finfo(np.float64).eps * phi.abs()
+        armijo_ok = (pt - phi) - opt.armijo * alpha * dphi <= tol_phi
+        suff = (tt - (1 - 1e-5) * theta <= 10 * np.finfo(np.float64).eps * theta) | \
+            ((pt - phi) + 1e-5 * theta <= tol_phi)
         in_filter = ((tt[:, None] >= filt[:, :, 0]) & (pt[:, None] >= filt[:, :, 1])).any(1)
         ok = finite & (tt <= theta_max) & ~in_filter & torch.where(switching, armijo_ok, suff)
         return ok, switching & armijo_ok
@@ -609,7 +691,8 @@ class GpuBandSolver:
 
 _NATIVE_OPTIONS = ("tol", "max_iter", "acceptable_tol", "acceptable_iter", "mu_init", "bound_relax_factor",
                    "bound_push", "tau_min", "kappa_eps", "kappa_mu", "theta_mu", "s_max", "armijo", "max_backtrack",
-                   "delta_c", "curv_min", "max_soc", "kappa_soc")
+                   "delta_c", "curv_min", "max_soc", "kappa_soc", "watchdog_shortened_iter_trigger",
+                   "watchdog_trial_iter_max")
 
 
 class NativeIpm:

@@ -277,6 +277,11 @@ typedef struct cfx_ipm_options {
     double curv_min;           /* 1e-8: dx^T (W + Sigma + dw) dx >= curv_min |dx|^2 */
     int32_t max_soc;           /* 4 */
     double kappa_soc;          /* 0.99 */
+    /* Ipopt's watchdog: after this many consecutive shortened line searches (10; 0: off) full steps are taken for
+       up to watchdog_trial_iter_max (3) iterations, judged against the iterate where it started; none acceptable:
+       back there, backtracking from half the step */
+    int32_t watchdog_shortened_iter_trigger;
+    int32_t watchdog_trial_iter_max;
 } cfx_ipm_options;
 
 typedef struct cfx_ipm_stats {
