@@ -126,3 +126,18 @@ def test_segment_sum_matches_index_add():
     torch.testing.assert_close(got, ref, rtol=1e-13, atol=1e-13)
     again = seg.add_(torch.ones((5, 50), dtype=torch.float64), src)
     assert torch.equal(got, again)
+
+
+def test_safe_slacks_and_watchdog_keep_the_end_game_short():
+    """Near the optimum of the Hmed force-tracking case (tol 1e-10, mu -> 1e-11) the fraction-to-the-boundary step
+    lands intensities exactly on I_min in floating point: without Ipopt's safe slacks (slack_move bound moves) the
+    barrier is +inf there and every iteration halves its step (159 iterations); with them, and the watchdog for
+    the shortened-step streaks that remain, the solve ends in a few dozen."""
+    t = np.linspace(0, 1, 11)
+    cfg = dict(name="hmed2018", stims=[0.0, 0.05, 0.1, 0.15], final_time=0.2, truncation=4, scheme="RK1", m=5,
+               objective={"force_tracking": [t, 40 * t]}, n_shooting=None)
+    ocp, pb, ipm = _ipm(cfg, batch=1, tol=1e-10)
+    res = ipm.solve()
+    assert res.converged.all() and res.iterations[0] <= 60, res.iterations
+    lb, ub = ocp.bounds_vector()
+    assert np.all(res.v[0] >= lb - 1e-12) and np.all(res.v[0] <= ub + 1e-12)  # final point on the original bounds
