@@ -59,6 +59,10 @@ struct cfx_handle {
     // musculoskeletal problems (cfx_msk_create)
     bool msk = false;
     int msk_nq = 0, msk_nm = 0, msk_fam = 0;
+    // stage-data reuse between cfx_eval_all (with J_g) and the next cfx_eval_h at the same caller pointer, while the
+    // interior point (the only caller that guarantees the point is unchanged in between) has it switched on
+    bool msk_stash = false, stash_valid = false;
+    const double* stash_v = nullptr;
     MskParams mp{};
     MskGeom* d_geom = nullptr;
     MskObjective* d_mobj = nullptr;
@@ -949,6 +953,13 @@ extern "C" int cfx_integrate(cfx_handle* h, const double* x0, const double* u, d
 // ------------------------------------------------------------------------------------------------------
 // musculoskeletal problems (FesMskModel + OcpFesMsk; cfx_msk.h)
 // ------------------------------------------------------------------------------------------------------
+int cfx_internal_msk_stash(cfx_handle* h, int on) {
+    if (!h) return CFX_EINVAL;
+    h->msk_stash = h->msk && on;
+    h->stash_valid = false;
+    return CFX_OK;
+}
+
 extern "C" int cfx_msk_create(const cfx_msk_problem* p, cfx_handle** out) {
     if (!p || !out) return create_fail(nullptr, CFX_EINVAL, "cfx_msk_create: NULL argument");
     *out = nullptr;
@@ -1237,13 +1248,19 @@ static int msk_eval_all(cfx_handle* h, const double* v, double* g, double* jac, 
     if (rc != CFX_OK) return rc;
     if (G || J) {
         MskParams P = h->mp;
-        if (J) {  // per-stage Jacobian coefficients between the two g + J_g launches
-            const size_t nw = (size_t)B * P.N * P.Q * msk_ncoef_host(h->msk_nq, h->msk_nm);
+        if (J) {  // per-stage Jacobian coefficients (and stage values) between the g + J_g launches
+            const size_t nw = h->msk_stash ? msk_hess_work_host(h->msk_nq, h->msk_nm, P.nx, P.nz, P.nz * (P.nz + 1) / 2,
+                                                                B, P.N, P.Q)
+                                           : msk_shoot_work_host(h->msk_nq, h->msk_nm, P.nx, B, P.N, P.Q);
             P.scratch = ensure(h, h->main[S_WORK], nw, &rc);
             if (!P.scratch) return rc;
         }
         CFX_HIP(h, launch_msk_shooting(h->msk_nq, h->msk_nm, h->msk_fam, h->scheme, P, h->d_geom, V, G, J,
-                                       h->stream));
+                                       h->msk_stash, h->stream));
+        if (J) {
+            h->stash_valid = h->msk_stash;
+            h->stash_v = v;
+        }
     }
     if (F || GR) {
         if (GR) CFX_HIP(h, hipMemsetAsync(GR, 0, (size_t)B * h->sz.nv * sizeof(double), h->stream));
@@ -1280,8 +1297,10 @@ static int msk_eval_h(cfx_handle* h, const double* v, const double* obj_factor, 
     double* W = ensure(h, h->main[S_WORK], nw, &rc);
     if (!W) return rc;
     CFX_HIP(h, hipMemsetAsync(H, 0, (size_t)B * h->sz.nnz_hess * sizeof(double), h->stream));
+    const bool reuse = h->msk_stash && h->stash_valid && h->stash_v == v;
+    h->stash_valid = false;
     CFX_HIP(h, launch_msk_hessian(h->msk_nq, h->msk_nm, h->msk_fam, h->scheme, h->mp, h->d_geom,
-                                  (const int16_t*)h->d_htasks, h->n_htasks, V, LAM, H, W, h->stream));
+                                  (const int16_t*)h->d_htasks, h->n_htasks, V, LAM, H, W, reuse, h->stream));
     if (h->n_obj)
         hipLaunchKernelGGL(k_msk_objective, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, h->stream, h->mp,
                            h->n_obj, h->d_mobj, h->d_targets, V, (double*)nullptr, (double*)nullptr, OF, H,

@@ -36,17 +36,18 @@ void msk_dep_pattern(int nq, int nm, int fam, int scheme, const MskParams& P, co
 }
 
 hipError_t launch_msk_shooting(int nq, int nm, int fam, int scheme, const MskParams& P, const MskGeom* G,
-                               const double* V, double* Gout, double* J, hipStream_t s) {
+                               const double* V, double* Gout, double* J, bool keep_xs, hipStream_t s) {
     MskCall c = make(1, nq, nm, fam, scheme);
-    c.P = &P, c.G = G, c.V = V, c.Gout = Gout, c.J = J, c.s = s;
+    c.P = &P, c.G = G, c.V = V, c.Gout = Gout, c.J = J, c.flag = keep_xs, c.s = s;
     return dispatch(c) ? c.err : hipErrorInvalidValue;
 }
 
 hipError_t launch_msk_hessian(int nq, int nm, int fam, int scheme, const MskParams& P, const MskGeom* G,
                               const int16_t* tasks, int ntasks, const double* V, const double* LAM, double* H,
-                              double* work, hipStream_t s) {
+                              double* work, bool reuse, hipStream_t s) {
     MskCall c = make(2, nq, nm, fam, scheme);
-    c.P = &P, c.G = G, c.tasks = tasks, c.ntasks = ntasks, c.V = V, c.LAM = LAM, c.H = H, c.work = work, c.s = s;
+    c.P = &P, c.G = G, c.tasks = tasks, c.ntasks = ntasks, c.V = V, c.LAM = LAM, c.H = H, c.work = work;
+    c.flag = reuse, c.s = s;
     return dispatch(c) ? c.err : hipErrorInvalidValue;
 }
 

@@ -1749,6 +1749,13 @@ static int ipm_solve(cfx_ipm* s, const double* v0, const double* fixed_values, d
     if (cfx_internal_info(s->h, &Bq, &layout, &dev, &st) != CFX_OK) return ipm_fail(s, CFX_EINVAL, "bad handle");
     IPM_HIP(s, hipSetDevice(s->device));
     s->stream = st;
+    // MSK handles: eval_h re-uses the stage data of the eval_all just before it at the same point (switched off
+    // again on every exit path)
+    struct StashGuard {
+        cfx_handle* h;
+        ~StashGuard() { cfx_internal_msk_stash(h, 0); }
+    } stash_guard{s->h};
+    cfx_internal_msk_stash(s->h, 1);
     IpmK& K = s->K;
     const bool devp = flags & CFX_DEVICE;
     const size_t B = (size_t)K.B;

@@ -1334,6 +1334,143 @@ __global__ void __launch_bounds__(256) k_msk_hproj(const MskParams P, const doub
         if (c >= a && c < nz) H[(hb + c * (c + 1) / 2 + a) * B + b] = out[c];
 }
 
+// ---- small batches: every stage in its own thread ------------------------------------------------------------
+// k_msk_stagecoef runs m * ST dependent stage evaluations (Dual skeleton) per thread; at batch 1 that chain is the
+// whole launch (~0.5 ms for cfg 5 at RK4 x 5).  Split: k_msk_values runs the plain-double recursion (the g values)
+// and stores every stage input XS, then k_msk_stagecoef_par evaluates each stage's coefficients in its own thread,
+// so the latency is one double recursion plus one Dual stage.  Same for the Hessian projection: k_msk_hproj_stage
+// gives every (stage, column) its own thread and k_msk_hproj_sum adds the stages up in the order k_msk_hproj does.
+template <int NQ, int NM, int FAM, int SCHEME>
+__global__ void __launch_bounds__(256) k_msk_values(const MskParams P, const MskGeom* __restrict__ GG,
+                                                    const double* __restrict__ V, double* __restrict__ Gout,
+                                                    double* __restrict__ XS) {
+    constexpr int NXM = msk_nxm<FAM>(), NX = NM * NXM + 2 * NQ;
+    constexpr int NUMAX = (msk_pw<FAM>() ? NM : 0) + NQ;
+    constexpr int ST = SCHEME == 4 ? 4 : (SCHEME == 2 ? 2 : 1);
+    const int64_t B = P.B;
+    const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= B) return;
+    const int k = blockIdx.y;
+    const MskGeom& G = *GG;
+    const int nz = P.nz, nu = P.nu, Q = P.Q, residual = P.residual;
+    const int64_t zb = (int64_t)k * nz;
+    const double h = P.h;
+    double x[NX], u[NUMAX];
+#pragma unroll
+    for (int r = 0; r < NX; ++r) x[r] = V[(zb + r) * B + b];
+#pragma unroll
+    for (int i = 0; i < NUMAX; ++i) u[i] = i < nu ? V[(zb + NX + i) * B + b] : 0.0;
+    for (int j = 0; j < P.m; ++j) {
+        double acc[NX], xs[NX];
+#pragma unroll
+        for (int r = 0; r < NX; ++r) xs[r] = x[r];
+#pragma unroll
+        for (int st = 0; st < ST; ++st) {
+            const int64_t kq = (int64_t)k * Q + j * ST + st;
+#pragma unroll
+            for (int r = 0; r < NX; ++r) XS[(kq * NX + r) * B + b] = xs[r];
+            double f[NX];
+            msk_rhs<NQ, NM, FAM>(G, residual, P.cs + kq * NM, xs, u, f);
+            const double cst = (ST == 4 && st == 2) ? h : 0.5 * h;
+#pragma unroll
+            for (int r = 0; r < NX; ++r) {
+                if (ST == 4) {
+                    if (st == 0) acc[r] = f[r];
+                    else if (st < 3) acc[r] = acc[r] + 2.0 * f[r];
+                }
+                if (st + 1 < ST) xs[r] = x[r] + cst * f[r];
+                else x[r] = ST == 4 ? x[r] + (h / 6.0) * (acc[r] + f[r]) : x[r] + h * f[r];
+            }
+        }
+    }
+    if (Gout) {
+#pragma unroll
+        for (int r = 0; r < NX; ++r) Gout[((int64_t)k * NX + r) * B + b] = x[r] - V[(zb + nz + r) * B + b];
+    }
+}
+
+// stage coefficients of k_msk_stagecoef from the stored stage inputs (thread = instance, interval, stage)
+template <int NQ, int NM, int FAM>
+__global__ void __launch_bounds__(256) k_msk_stagecoef_par(const MskParams P, const MskGeom* __restrict__ GG,
+                                                           const double* __restrict__ V, const double* __restrict__ XS) {
+    constexpr int NXM = msk_nxm<FAM>(), NX = NM * NXM + 2 * NQ;
+    constexpr int NUMAX = (msk_pw<FAM>() ? NM : 0) + NQ;
+    constexpr int NC = msk_ncoef<NQ, NM>();
+    const int64_t B = P.B;
+    const int64_t item = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (item >= B * P.N * P.Q) return;
+    const int64_t b = item % B, kq = item / B;
+    const int k = (int)(kq / P.Q);
+    const MskGeom& G = *GG;
+    const int nu = P.nu;
+    const int64_t zb = (int64_t)k * P.nz;
+    double xs[NX], u[NUMAX], f[NX];
+#pragma unroll
+    for (int r = 0; r < NX; ++r) xs[r] = XS[(kq * NX + r) * B + b];
+#pragma unroll
+    for (int i = 0; i < NUMAX; ++i) u[i] = i < nu ? V[(zb + NX + i) * B + b] : 0.0;
+    msk_stage<NQ, NM, FAM>(G, P.residual, P.cs + kq * NM, xs, u, f, P.scratch + kq * NC * B + b, B);
+}
+
+// one stage's term T_q^T (G_q T_q[:, a]) of k_msk_hproj (thread = instance, column a, interval-stage kq)
+template <int NQ, int NM, int FAM>
+__global__ void __launch_bounds__(256) k_msk_hproj_stage(const MskParams P, const double* __restrict__ TS,
+                                                         const double* __restrict__ GQ, int ntasks,
+                                                         double* __restrict__ HQ) {
+    constexpr int NX = NM * msk_nxm<FAM>() + 2 * NQ;
+    constexpr int NZ = NX + (msk_pw<FAM>() ? NM : 0) + NQ;
+    const int64_t B = P.B;
+    const int nz = P.nz;
+    const int64_t item = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (item >= B * P.N * P.Q * nz) return;
+    const int64_t b = item % B, rest = item / B;
+    const int a = (int)(rest % nz);
+    const int64_t kq = rest / nz;
+    const double* __restrict__ ts = TS + kq * NX * nz * B + b;
+    double ta[NZ], w[NZ];
+#pragma unroll
+    for (int I = 0; I < NX; ++I) ta[I] = ts[((int64_t)I * nz + a) * B];
+#pragma unroll
+    for (int I = NX; I < NZ; ++I) ta[I] = I == a ? 1.0 : 0.0;
+#pragma unroll
+    for (int I = 0; I < NZ; ++I) w[I] = 0.0;
+    const double* __restrict__ gq = GQ + kq * ntasks * B + b;
+#pragma unroll
+    for (int I = 0; I < NZ; ++I)
+#pragma unroll
+        for (int J = I; J < NZ; ++J) {
+            if (J >= nz) continue;
+            const int t = I * nz - I * (I - 1) / 2 + (J - I);
+            const double g = gq[(int64_t)t * B];
+            w[I] += g * ta[J];
+            if (J != I) w[J] += g * ta[I];
+        }
+    double* __restrict__ hq = HQ + kq * P.nhk * B + b;
+#pragma unroll
+    for (int c = 0; c < NZ; ++c) {
+        if (c < a || c >= nz) continue;
+        double sacc = c >= NX ? w[c] : 0.0;
+#pragma unroll
+        for (int I = 0; I < NX; ++I) sacc += ts[((int64_t)I * nz + c) * B] * w[I];
+        hq[(int64_t)(c * (c + 1) / 2 + a) * B] = sacc;
+    }
+}
+
+// H[k][e] = sum over the interval's stages of HQ, in stage order (thread = instance, entry, interval)
+static __global__ void __launch_bounds__(256) k_msk_hproj_sum(const MskParams P, const double* __restrict__ HQ,
+                                                       double* __restrict__ H) {
+    const int64_t B = P.B;
+    const int nhk = P.nhk, Q = P.Q;
+    const int64_t item = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (item >= B * P.N * nhk) return;
+    const int64_t b = item % B, rest = item / B;
+    const int e = (int)(rest % nhk);
+    const int64_t k = rest / nhk;
+    double s = 0.0;
+    for (int q = 0; q < Q; ++q) s += HQ[(((k * Q + q) * nhk) + e) * B + b];
+    H[(k * nhk + e) * B + b] = s;
+}
+
 // ---- single shooting (IVP): thread = instance, every sub-step written -------------------------------------
 template <int NQ, int NM, int FAM, int SCHEME>
 __global__ void __launch_bounds__(256) k_msk_ivp(const MskParams P, const MskGeom* __restrict__ GG,

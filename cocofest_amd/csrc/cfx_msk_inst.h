@@ -21,18 +21,30 @@ void dep_t(const MskParams& P, const MskGeom& G, uint64_t* dep) {
 }
 
 template <int NQ, int NM, int FAM, int SCHEME>
-hipError_t shoot_t(const MskParams& P, const MskGeom* G, const double* V, double* Gout, double* J, hipStream_t s) {
+hipError_t shoot_t(const MskParams& P, const MskGeom* G, const double* V, double* Gout, double* J, bool keep_xs,
+                   hipStream_t s) {
     const unsigned gx = (unsigned)((P.B + kMskBlk - 1) / kMskBlk);
     if (!J) {  // g only: the value recursion without derivative directions
         hipLaunchKernelGGL((k_msk_shooting<NQ, NM, FAM, SCHEME, 0>), dim3(gx, (unsigned)P.N), dim3(kMskBlk), 0, s, P, G,
                            V, Gout, J);
         return hipGetLastError();
     }
-    // g + J_g: stage coefficients (one thread per instance and interval), then one thread per Jacobian column
-    hipLaunchKernelGGL((k_msk_stagecoef<NQ, NM, FAM, SCHEME>), dim3(gx, (unsigned)P.N), dim3(kMskBlk), 0, s, P, G, V,
-                       Gout, (double*)nullptr);
+    // g + J_g: stage coefficients, then one thread per Jacobian column
+    constexpr int NX = NM * msk_nxm<FAM>() + 2 * NQ, NC = msk_ncoef<NQ, NM>();
+    double* XS = P.scratch + P.B * P.N * P.Q * NC;
+    if (P.B <= kMskSmallBatch) {  // value recursion, then every stage's coefficients in its own thread
+        hipLaunchKernelGGL((k_msk_values<NQ, NM, FAM, SCHEME>), dim3(gx, (unsigned)P.N), dim3(kMskBlk), 0, s, P, G, V,
+                           Gout, XS);
+        hipLaunchKernelGGL((k_msk_stagecoef_par<NQ, NM, FAM>),
+                           dim3((unsigned)((P.B * P.N * P.Q + kMskBlk - 1) / kMskBlk)), dim3(kMskBlk), 0, s, P, G, V,
+                           (const double*)XS);
+    } else {
+        hipLaunchKernelGGL((k_msk_stagecoef<NQ, NM, FAM, SCHEME>), dim3(gx, (unsigned)P.N), dim3(kMskBlk), 0, s, P, G,
+                           V, Gout, keep_xs ? XS : (double*)nullptr);
+    }
+    (void)NX;
     if (P.nz <= kMskLdsCols) {  // coefficients through LDS, one block per 32 instances
-        constexpr int NC = msk_ncoef<NQ, NM>(), ST = SCHEME == 4 ? 4 : (SCHEME == 2 ? 2 : 1), TW = 32;
+        constexpr int ST = SCHEME == 4 ? 4 : (SCHEME == 2 ? 2 : 1), TW = 32;
         hipLaunchKernelGGL((k_msk_tangents_lds<NQ, NM, FAM, SCHEME, TW>), dim3((unsigned)((P.B + TW - 1) / TW), (unsigned)P.N),
                            dim3(TW * P.nz), ST * NC * TW * sizeof(double), s, P, G, J);
         return hipGetLastError();
@@ -45,8 +57,8 @@ hipError_t shoot_t(const MskParams& P, const MskGeom* G, const double* V, double
 
 template <int NQ, int NM, int FAM, int SCHEME>
 hipError_t hess_t(const MskParams& P, const MskGeom* G, const int16_t* tasks, int ntasks, const double* V,
-                  const double* LAM, double* H, double* work, hipStream_t s) {
-    // work (msk_hess_work_host doubles): stage coefficients | XS | TS | MU | GQ
+                  const double* LAM, double* H, double* work, bool reuse, hipStream_t s) {
+    // work (msk_hess_work_host doubles): stage coefficients | XS | TS | MU | GQ [| HQ]
     constexpr int NX = NM * msk_nxm<FAM>() + 2 * NQ, NC = msk_ncoef<NQ, NM>();
     const int64_t BNQ = P.B * P.N * P.Q;
     MskParams Pw = P;
@@ -62,14 +74,31 @@ hipError_t hess_t(const MskParams& P, const MskGeom* G, const int16_t* tasks, in
     }
     const unsigned gx = (unsigned)((P.B + kMskBlk - 1) / kMskBlk);
     auto flat = [](int64_t items) { return dim3((unsigned)((items + kMskBlk - 1) / kMskBlk)); };
-    hipLaunchKernelGGL((k_msk_stagecoef<NQ, NM, FAM, SCHEME>), dim3(gx, (unsigned)P.N), dim3(kMskBlk), 0, s, Pw, G, V,
-                       (double*)nullptr, XS);
+    const bool small = P.B <= kMskSmallBatch;
+    if (!reuse) {  // stage values and coefficients (reuse: left by the g + J_g launch at this point)
+        if (small) {
+            hipLaunchKernelGGL((k_msk_values<NQ, NM, FAM, SCHEME>), dim3(gx, (unsigned)P.N), dim3(kMskBlk), 0, s, Pw, G,
+                               V, (double*)nullptr, XS);
+            hipLaunchKernelGGL((k_msk_stagecoef_par<NQ, NM, FAM>), flat(BNQ), dim3(kMskBlk), 0, s, Pw, G, V,
+                               (const double*)XS);
+        } else {
+            hipLaunchKernelGGL((k_msk_stagecoef<NQ, NM, FAM, SCHEME>), dim3(gx, (unsigned)P.N), dim3(kMskBlk), 0, s, Pw,
+                               G, V, (double*)nullptr, XS);
+        }
+    }
     hipLaunchKernelGGL((k_msk_htan<NQ, NM, FAM, SCHEME>), flat(P.B * P.N * P.nz), dim3(kMskBlk), 0, s, Pw, G, TS);
     hipLaunchKernelGGL((k_msk_hadj<NQ, NM, FAM, SCHEME>), flat(P.B * P.N), dim3(kMskBlk), 0, s, Pw, G, LAM, MU);
-    hipLaunchKernelGGL((k_msk_hpair<NQ, NM, FAM>), flat(P.B * P.N * P.Q * ntasks), dim3(kMskBlk), 0, s, Pw, G, tasks,
+    hipLaunchKernelGGL((k_msk_hpair<NQ, NM, FAM>), flat(BNQ * ntasks), dim3(kMskBlk), 0, s, Pw, G, tasks,
                        ntasks, npair, V, (const double*)XS, (const double*)MU, GQ);
-    hipLaunchKernelGGL((k_msk_hproj<NQ, NM, FAM>), flat(P.B * P.N * P.nz), dim3(kMskBlk), 0, s, Pw, (const double*)TS,
-                       (const double*)GQ, npair, H);
+    if (small) {
+        double* HQ = GQ + BNQ * npair;
+        hipLaunchKernelGGL((k_msk_hproj_stage<NQ, NM, FAM>), flat(BNQ * P.nz), dim3(kMskBlk), 0, s, Pw,
+                           (const double*)TS, (const double*)GQ, npair, HQ);
+        hipLaunchKernelGGL(k_msk_hproj_sum, flat(P.B * P.N * P.nhk), dim3(kMskBlk), 0, s, Pw, (const double*)HQ, H);
+    } else {
+        hipLaunchKernelGGL((k_msk_hproj<NQ, NM, FAM>), flat(P.B * P.N * P.nz), dim3(kMskBlk), 0, s, Pw,
+                           (const double*)TS, (const double*)GQ, npair, H);
+    }
     return hipGetLastError();
 }
 
@@ -90,6 +119,7 @@ struct MskCall {
     double *Gout, *J, *H, *TR, *work;
     const int16_t* tasks;
     int ntasks;
+    bool flag;  // op 1: keep the stage values; op 2: reuse the stage values and coefficients
     hipStream_t s;
     hipError_t err;
 };
@@ -99,8 +129,8 @@ bool msk_try(MskCall& c) {
     if (c.nq != NQ || c.nm != NM || c.fam != FAM || c.scheme != SC) return false;
     switch (c.op) {
         case 0: dep_t<NQ, NM, FAM, SC>(*c.P, *c.G, c.dep); break;
-        case 1: c.err = shoot_t<NQ, NM, FAM, SC>(*c.P, c.G, c.V, c.Gout, c.J, c.s); break;
-        case 2: c.err = hess_t<NQ, NM, FAM, SC>(*c.P, c.G, c.tasks, c.ntasks, c.V, c.LAM, c.H, c.work, c.s); break;
+        case 1: c.err = shoot_t<NQ, NM, FAM, SC>(*c.P, c.G, c.V, c.Gout, c.J, c.flag, c.s); break;
+        case 2: c.err = hess_t<NQ, NM, FAM, SC>(*c.P, c.G, c.tasks, c.ntasks, c.V, c.LAM, c.H, c.work, c.flag, c.s); break;
         case 3: c.err = ivp_t<NQ, NM, FAM, SC>(*c.P, c.G, c.X0, c.U, c.TR, c.s); break;
         default: break;
     }

@@ -16,17 +16,28 @@ void msk_dep_pattern(int nq, int nm, int fam, int scheme, const MskParams& P, co
 // Per-stage Jacobian coefficients of k_msk_stagecoef (msk_ncoef in cfx_msk.h).
 inline int msk_ncoef_host(int nq, int nm) { return nm * (6 + 2 * nq) + 3 * nq * nq + nq * nm; }
 
-// Work buffer of launch_msk_hessian (doubles): stage coefficients, stage values XS, stage tangents TS, stage
-// adjoints MU and the Y-space pair Hessians GQ of every (instance, interval, stage).
+// Batches up to this size run the stage-parallel kernels (k_msk_values + k_msk_stagecoef_par, k_msk_hproj_stage +
+// k_msk_hproj_sum): at a few instances the launches are latency-bound, and a thread per stage cuts the chain.
+constexpr int64_t kMskSmallBatch = 256;
+
+// Work buffer of launch_msk_shooting / launch_msk_hessian (doubles): stage coefficients, stage values XS (their
+// first two regions are what g + J_g needs), stage tangents TS, stage adjoints MU, the Y-space pair Hessians GQ
+// and, for small batches, the per-stage Hessian terms HQ of every (instance, interval, stage).
+inline size_t msk_shoot_work_host(int nq, int nm, int nx, int64_t B, int N, int Q) {
+    return (size_t)B * N * Q * ((size_t)msk_ncoef_host(nq, nm) + nx);
+}
 inline size_t msk_hess_work_host(int nq, int nm, int nx, int nz, int ntasks, int64_t B, int N, int Q) {
-    return (size_t)B * N * Q * ((size_t)msk_ncoef_host(nq, nm) + nx + (size_t)nx * nz + nx + ntasks);
+    const size_t hq = B <= kMskSmallBatch ? (size_t)nz * (nz + 1) / 2 : 0;
+    return (size_t)B * N * Q * ((size_t)msk_ncoef_host(nq, nm) + nx + (size_t)nx * nz + nx + ntasks + hq);
 }
 
+// g (+ J_g when J != nullptr; P.scratch then points at a msk_shoot_work_host buffer).  keep_xs: also leave the stage
+// values in the buffer's XS region, so that a launch_msk_hessian at the same point can skip the recursion (reuse).
 hipError_t launch_msk_shooting(int nq, int nm, int fam, int scheme, const MskParams& P, const MskGeom* G,
-                               const double* V, double* Gout, double* J, hipStream_t s);
+                               const double* V, double* Gout, double* J, bool keep_xs, hipStream_t s);
 hipError_t launch_msk_hessian(int nq, int nm, int fam, int scheme, const MskParams& P, const MskGeom* G,
                               const int16_t* tasks, int ntasks, const double* V, const double* LAM, double* H,
-                              double* work, hipStream_t s);
+                              double* work, bool reuse, hipStream_t s);
 hipError_t launch_msk_ivp(int nq, int nm, int fam, int scheme, const MskParams& P, const MskGeom* G,
                           const double* X0, const double* U, double* TR, hipStream_t s);
 

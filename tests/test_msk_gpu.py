@@ -240,3 +240,28 @@ def test_nmpc_fes_msk_commits_a_forward_consistent_trajectory():
     # the elbow moves toward the 1 rad target in both scenarios
     qe = res.states[f"q_{model.name_dof[1]}"]
     assert np.all(np.abs(qe[:, -1] - 1.0) < np.abs(qe[:, 0] - 1.0))
+
+
+@pytest.mark.parametrize("case", ["cfg5_d07f_rk4", "arm26_6muscles_d03_rk1", "d07_rk1_residual"])
+def test_msk_small_and_large_batch_paths_agree(case):
+    """Batches up to cfx's kMskSmallBatch (256) run the stage-parallel kernels (k_msk_values + k_msk_stagecoef_par,
+    k_msk_hproj_stage + k_msk_hproj_sum), larger ones the fused per-interval kernels: the same instances give the same
+    g, J_g and Lagrangian Hessian either way (the oracle tests above run the small path)."""
+    cfg = CASES[case]
+    ocp = MC.product_ocp(**cfg)
+    pb = MC.oracle_problem(**cfg)
+    Bl = 300
+    V = MC.random_decision(pb, Bl, seed=5)
+    lam = np.random.default_rng(6).normal(size=(Bl, pb.ng))
+    of = np.linspace(0.2, 1.5, Bl)
+    out = {}
+    for B in (2, Bl):
+        h = ocp.nlp(batch=B, layout="aos")
+        g, jac = np.empty((B, h.ng)), np.empty((B, h.nnz_jac))
+        h.eval_all(V[:B].copy(), g=g, jac=jac)
+        hv = h.eval_h(V[:B].copy(), of[:B].copy(), lam[:B].copy())
+        h.close()
+        out[B] = (g[:2], jac[:2], hv[:2])
+    for a, b_ in zip(out[2], out[Bl]):
+        scale = np.abs(a) + 1e-9 * np.abs(a).max()
+        assert np.max(np.abs(a - b_) / scale) < 1e-12
