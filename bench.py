@@ -376,7 +376,7 @@ def msk_throughput(local, dist, world, rank, backend, steps=10, B=1 << 16):
            "instance_evals_per_s": world * B / (wall_max / steps),
            "algorithmic_GBps": nbytes * world * B / (wall_max / steps) / 1e9, "bytes_per_instance": nbytes,
            "scaling": "weak", "parallelism": f"instances sharded over {world} GPU(s), no data-path collective",
-           "kernels": "k_msk_stagecoef + k_msk_tangents_lds (compute-bound: FP64 VALU, see profiles/)"}
+           "kernels": "k_msk_values + k_msk_stagecoef_par + k_msk_tangents_lds (compute-bound: FP64 VALU, see profiles/)"}
     h.close()
     return out, ocp
 

@@ -15,7 +15,7 @@ import numpy as np
 
 LIB_PATH = pathlib.Path(__file__).with_name("libcfx.so")
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 OK, EINVAL, EHIP, ENOMEM, EUNSUPPORTED, ENODEV = 0, -1, -2, -3, -4, -5
 MODEL_IDS = {
     "ding2003": 0,
@@ -82,7 +82,8 @@ class MskProblem(C.Structure):
         ("dof_frame", C.POINTER(C.c_double)), ("gravity", C.c_double * 3), ("body_mass", C.POINTER(C.c_double)),
         ("body_com", C.POINTER(C.c_double)), ("body_inertia", C.POINTER(C.c_double)), ("n_muscles", C.c_int32),
         ("muscles", C.POINTER(MskMuscle)), ("flags", C.c_uint32), ("n_objectives", C.c_int32),
-        ("objectives", C.POINTER(Objective)), ("device", C.c_int32),
+        ("objectives", C.POINTER(Objective)), ("device", C.c_int32), ("n_params", C.c_int32),
+        ("last_stim_idx", C.POINTER(C.c_int32)), ("param_offset", C.POINTER(C.c_int32)),
     ]
 
 
@@ -452,7 +453,8 @@ class MskHandle(Handle):
     ``point_pos`` (n, 3), ``optimal_length``, ``tendon_slack_length``, ``pennation_angle``."""
 
     def __init__(self, *, chain, muscles, scheme, n_steps, n_shooting, truncation, final_time, stim_rows, batch,
-                 flags=0, layout=LAYOUT_SOA, objectives=(), device=0):
+                 flags=0, layout=LAYOUT_SOA, objectives=(), device=0, n_params=0, last_stim_idx=None,
+                 param_offset=None):
         self.lib = load_library()
         self._keep = []
 
@@ -492,6 +494,10 @@ class MskHandle(Handle):
         pb.objectives = _objective_array(objectives, self._keep, n_shooting)
         pb.n_objectives = len(objectives)
         pb.device = device
+        pb.n_params = int(n_params)
+        if n_params:
+            pb.last_stim_idx = arr(last_stim_idx, np.int32)
+            pb.param_offset = arr(param_offset, np.int32)
         h = C.c_void_p()
         rc = self.lib.cfx_msk_create(C.byref(pb), C.byref(h))
         self._attach(rc, h, batch, layout, n_shooting, n_steps, device)

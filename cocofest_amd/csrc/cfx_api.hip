@@ -66,6 +66,8 @@ struct cfx_handle {
     MskParams mp{};
     MskGeom* d_geom = nullptr;
     MskObjective* d_mobj = nullptr;
+    double* d_msk_imin = nullptr;  // Hmed: I_min per muscle (sliding-window padding)
+    int msk_ns = 0;                // Hmed: sliding-window rows per interval (0: none)
     DevBuf main[S_COUNT], stage[S_COUNT];
     std::string err;
 };
@@ -767,7 +769,7 @@ extern "C" void cfx_destroy(cfx_handle* h) {
     }
     for (void* p : {(void*)h->d_tab, (void*)h->d_rest, (void*)h->d_cna, (void*)h->d_htasks, (void*)h->d_obj,
                     (void*)h->d_targets, (void*)h->d_sl_param, (void*)h->d_sl_joff, (void*)h->d_hdiag,
-                    (void*)h->d_geom, (void*)h->d_mobj})
+                    (void*)h->d_geom, (void*)h->d_mobj, (void*)h->d_msk_imin})
         if (p) (void)hipFree(p);
     if (h->own_stream) (void)hipStreamDestroy(h->own_stream);
     delete h;
@@ -982,12 +984,19 @@ extern "C" int cfx_msk_create(const cfx_msk_problem* p, cfx_handle** out) {
     const int nq = p->n_dof, nm = p->n_muscles;
     if (nq < 1 || nq > CFX_MSK_MAX_DOF) return bad("n_dof must be in [1, 4]");
     if (nm < 1 || nm > CFX_MSK_MAX_MUSCLES) return bad("n_muscles must be in [1, 8]");
-    const int fam = p->muscles[0].model;
-    if (fam < CFX_DING2003 || fam > CFX_DING2007_FATIGUE)
-        return create_fail(nullptr, CFX_EUNSUPPORTED, "cfx_msk_create: muscle models must be Ding2003 / Ding2007 families");
+    const int model = p->muscles[0].model;
+    if (model < CFX_DING2003 || model > CFX_HMED2018_FATIGUE)
+        return create_fail(nullptr, CFX_EUNSUPPORTED, "cfx_msk_create: unknown muscle model");
+    const bool hmed = model >= CFX_HMED2018;
+    if (hmed && p->truncation > 20)
+        return create_fail(nullptr, CFX_EUNSUPPORTED, "cfx_msk_create: Hmed2018 muscles need truncation <= 20");
+    // kernel family: Ding 0..3 as the model ids; Hmed2018 4 / 5 (T <= 10) and 6 / 7 (T <= 20), bit 0 fatigue
+    const int fam = hmed ? 4 + (model - CFX_HMED2018) + (p->truncation > 10 ? 2 : 0) : model;
+    if (p->n_params < 0 || (p->n_params > 0 && (!hmed || !p->last_stim_idx || !p->param_offset)))
+        return bad("intensity parameters need Hmed2018 muscles, last_stim_idx and param_offset");
     for (int m = 0; m < nm; ++m) {
         const cfx_msk_muscle& mu = p->muscles[m];
-        if (mu.model != fam) return bad("every muscle must use the same model family");
+        if (mu.model != model) return bad("every muscle must use the same model family");
         if (mu.n_points < 2 || mu.n_points > CFX_MSK_MAX_POINTS || !mu.point_frame || !mu.point_pos)
             return bad("muscle " + std::to_string(m) + ": 2..16 path points with frames and positions");
         for (int i = 0; i < mu.n_points; ++i)
@@ -1007,12 +1016,23 @@ extern "C" int cfx_msk_create(const cfx_msk_problem* p, cfx_handle** out) {
         return create_fail(nullptr, CFX_ENODEV, "cfx_msk_create: no HIP device available (libcfx has no CPU path)");
     if (p->device < 0 || p->device >= ndev) return create_fail(nullptr, CFX_ENODEV, "cfx_msk_create: bad device ordinal");
 
-    const bool fat = fam & 1, pw = fam == CFX_DING2007 || fam == CFX_DING2007_FATIGUE;
+    const bool fat = model & 1, pw = model == CFX_DING2007 || model == CFX_DING2007_FATIGUE;
     const bool residual = p->flags & CFX_MSK_RESIDUAL_TORQUE;
     const int N = p->n_shooting, T = p->truncation, m = p->n_steps, S = stages_of(p->scheme);
-    const int nxm = fat ? 5 : 2, nx = nm * nxm + 2 * nq, npw = pw ? nm : 0, nu = npw + (residual ? nq : 0);
+    const int nxm = fat ? 5 : 2, nx = nm * nxm + 2 * nq, npw = pw ? nm : 0, nint = hmed ? nm * T : 0;
+    const int nu = npw + nint + (residual ? nq : 0);
     const int nz = nx + nu;
     if (nz > 64) return bad("more than 64 decision variables per interval");
+    const int ns = p->n_params > 0 ? nint : 0;  // sliding-window rows per interval
+    const int ngk = nx + ns;
+    if (p->n_params > 0) {
+        for (int k = 0; k < N; ++k)
+            if (p->last_stim_idx[k] < -1) return bad("last_stim_idx out of range");
+        for (int mi = 0; mi < nm; ++mi) {
+            const int64_t hi = (int64_t)p->param_offset[mi] + p->last_stim_idx[N - 1];
+            if (p->param_offset[mi] < 0 || hi >= p->n_params) return bad("param_offset / last_stim_idx out of range");
+        }
+    }
 
     cfx_handle* h = new cfx_handle();
     h->msk = true;
@@ -1071,6 +1091,7 @@ extern "C" int cfx_msk_create(const cfx_msk_problem* p, cfx_handle** out) {
         C.a_fat_rest = pw ? c.a_scale : c.a_rest;  // ding2007_with_fatigue.py:198-241: A relaxes to a_scale
         C.inv_lopt = 1.0 / mu.optimal_length, C.slack = mu.tendon_slack_length;
         C.inv_cos_penn = 1.0 / std::cos(mu.pennation_angle);
+        C.ar = c.ar, C.bs = c.bs, C.Is = c.Is, C.cr = c.cr;
         if (fat) {
             rest[mi * nxm + 2] = C.a_fat_rest;
             rest[mi * nxm + 3] = c.tau1_rest;
@@ -1084,7 +1105,8 @@ extern "C" int cfx_msk_create(const cfx_msk_problem* p, cfx_handle** out) {
     // ---- calcium sums at every RK stage time, per muscle (ding2003.py:230-252, reference operation order)
     const double dt = p->final_time / N, hh = dt / m;
     const int Q = m * S;
-    std::vector<double> cs((size_t)N * Q * nm);
+    const int TM = hmed ? (T > 10 ? 20 : 10) : 1;  // Hmed: per-pulse coefficients, padded to the kernel's TMAX
+    std::vector<double> cs((size_t)N * Q * nm * TM, 0.0);
     for (int k = 0; k < N; ++k) {
         const double* row = p->stim_rows + (size_t)k * T;
         for (int mi = 0; mi < nm; ++mi) {
@@ -1099,15 +1121,22 @@ extern "C" int cfx_msk_create(const cfx_msk_problem* p, cfx_handle** out) {
                     if (S == 2 && st == 1) t += hh / 2;
                     if (S == 4 && (st == 1 || st == 2)) t += hh / 2;
                     if (S == 4 && st == 3) t += hh;
+                    const size_t kq = (size_t)k * Q + (size_t)j * S + st;
+                    if (hmed) {  // cs = sum_i coef_i lambda(I_i), formed in the kernels (hmed2018.py:97-98)
+                        for (int i = 0; i < T; ++i) cs[(kq * nm + mi) * TM + i] = ri[i] * std::exp(-(t - row[i]) / c.tauc);
+                        continue;
+                    }
                     double sum = 0.0;
                     for (int i = 0; i < T; ++i) sum = sum + ri[i] * std::exp(-(t - row[i]) / c.tauc);
-                    cs[((size_t)k * Q + (size_t)j * S + st) * nm + mi] = sum;
+                    cs[kq * nm + mi] = sum;
                 }
         }
     }
     MskParams& P = h->mp;
     P.B = p->batch, P.N = N, P.m = m, P.nx = nx, P.nu = nu, P.nz = nz, P.Q = Q;
     P.residual = residual ? 1 : 0, P.npw = npw, P.dt = dt, P.h = hh;
+    P.T = T, P.ngk = ngk;
+    h->msk_ns = ns;
 
     // ---- structural Jacobian pattern (Dep pass on the host through the same RHS code)
     std::vector<uint64_t> dep(nx);
@@ -1129,12 +1158,36 @@ extern "C" int cfx_msk_create(const cfx_msk_problem* p, cfx_handle** out) {
         for (int r = 0; r < nx; ++r) {
             for (int c = 0; c < nz; ++c)
                 if (dep[r] >> c & 1ull) {
-                    h->jrow.push_back(k * nx + r);
+                    h->jrow.push_back(k * ngk + r);
                     h->jcol.push_back(k * nz + c);
                 }
-            h->jrow.push_back(k * nx + r);
+            h->jrow.push_back(k * ngk + r);
             h->jcol.push_back((k + 1) * nz + r);
         }
+    // sliding-window rows: +1 on the intensity control, -1 on its parameter (custom_constraints.py:102-119)
+    std::vector<int32_t> sl_param, sl_joff;
+    std::vector<double> imin(nm, 0.0);
+    const int64_t p_off = (int64_t)N * nz + nx;
+    if (ns) {
+        for (int mi = 0; mi < nm; ++mi) {  // hmed2018.py:303-310
+            const cfx_constants& c = p->muscles[mi].constants;
+            imin[mi] = std::atanh(-c.cr) / c.bs + c.Is;
+        }
+        for (int k = 0; k < N; ++k)
+            for (int sidx = 0; sidx < ns; ++sidx) {
+                const int mi = sidx / T, j = sidx - mi * T;
+                const int rel = p->last_stim_idx[k] + 1 - T + j;
+                const int pi = rel >= 0 ? p->param_offset[mi] + rel : -1;
+                sl_param.push_back(pi);
+                sl_joff.push_back((int32_t)h->jrow.size());
+                h->jrow.push_back(k * ngk + nx + sidx);
+                h->jcol.push_back(k * nz + nx + npw + sidx);
+                if (pi >= 0) {
+                    h->jrow.push_back(k * ngk + nx + sidx);
+                    h->jcol.push_back((int32_t)(p_off + pi));
+                }
+            }
+    }
     // ---- Hessian: dense lower triangle of every interval block, then the diagonal of x_N
     const int nhk = nz * (nz + 1) / 2;
     P.nhk = nhk;
@@ -1158,15 +1211,18 @@ extern "C" int cfx_msk_create(const cfx_msk_problem* p, cfx_handle** out) {
     // variables vanish, and so do the residual torques' pairs with anything but q.
     std::vector<int16_t> tasks;
     {
-        std::vector<int> owner(nz, -1);  // muscle index, -1 skeleton, -2 residual torque
+        std::vector<int> owner(nz, -1);  // muscle index, -1 skeleton, -2 residual torque, -3 Hmed intensity
         for (int r = 0; r < nm * nxm; ++r) owner[r] = r / nxm;
         for (int i = 0; i < npw; ++i) owner[nx + i] = i;
-        for (int i = npw; i < nu; ++i) owner[nx + i] = -2;
+        for (int i = npw; i < npw + nint; ++i) owner[nx + i] = -3;
+        for (int i = npw + nint; i < nu; ++i) owner[nx + i] = -2;
         auto is_q = [&](int e) { return e >= nm * nxm && e < nm * nxm + nq; };
         int t = 0;
         for (int I = 0; I < nz; ++I)
             for (int J = I; J < nz; ++J, ++t) {
                 const int a = owner[I], c = owner[J];
+                // an intensity enters only its own lambda (linearly weighted in cn_dot): diagonal pairs only
+                if ((a == -3 || c == -3) && !(a == -3 && I == J)) continue;
                 if (a >= 0 && c >= 0 && a != c) continue;
                 if ((a == -2 && !is_q(J)) || (c == -2 && !is_q(I))) continue;
                 tasks.push_back((int16_t)I);
@@ -1204,8 +1260,8 @@ extern "C" int cfx_msk_create(const cfx_msk_problem* p, cfx_handle** out) {
         mobj.push_back(d);
     }
     h->n_obj = (int)mobj.size();
-    h->sz.nv = (int64_t)N * nz + nx;
-    h->sz.ng = (int64_t)N * nx;
+    h->sz.nv = (int64_t)N * nz + nx + (ns ? p->n_params : 0);
+    h->sz.ng = (int64_t)N * ngk;
     h->sz.nnz_jac = (int64_t)h->jrow.size();
     h->sz.nnz_hess = (int64_t)h->hrow.size();
     h->sz.nx = nx;
@@ -1226,7 +1282,10 @@ extern "C" int cfx_msk_create(const cfx_msk_problem* p, cfx_handle** out) {
         !upload((void**)&h->d_mobj, mobj.data(), mobj.size() * sizeof(MskObjective)) ||
         !upload((void**)&h->d_targets, targets.data(), targets.size() * sizeof(double)) ||
         !upload((void**)&h->d_htasks, tasks.data(), tasks.size() * sizeof(int16_t)) ||
-        !upload((void**)&h->d_hdiag, hdiag.data(), hdiag.size() * sizeof(int32_t)))
+        !upload((void**)&h->d_hdiag, hdiag.data(), hdiag.size() * sizeof(int32_t)) ||
+        !upload((void**)&h->d_sl_param, sl_param.data(), sl_param.size() * sizeof(int32_t)) ||
+        !upload((void**)&h->d_sl_joff, sl_joff.data(), sl_joff.size() * sizeof(int32_t)) ||
+        !upload((void**)&h->d_msk_imin, imin.data(), imin.size() * sizeof(double)))
         return create_fail(h, CFX_ENOMEM, "cfx_msk_create: device allocation/upload failed");
     P.cs = h->d_tab;
     P.rest = h->d_rest;
@@ -1257,6 +1316,12 @@ static int msk_eval_all(cfx_handle* h, const double* v, double* g, double* jac, 
         }
         CFX_HIP(h, launch_msk_shooting(h->msk_nq, h->msk_nm, h->msk_fam, h->scheme, P, h->d_geom, V, G, J,
                                        h->msk_stash, h->stream));
+        if (h->msk_ns) {
+            const int64_t items = B * P.N * h->msk_ns;
+            hipLaunchKernelGGL(k_msk_slide, dim3((unsigned)((items + 255) / 256)), dim3(256), 0, h->stream, P,
+                               h->msk_ns, (const int32_t*)h->d_sl_param, (const int32_t*)h->d_sl_joff,
+                               (const double*)h->d_msk_imin, (int64_t)P.N * P.nz + P.nx, V, G, J);
+        }
         if (J) {
             h->stash_valid = h->msk_stash;
             h->stash_v = v;

@@ -376,7 +376,7 @@ __device__ __forceinline__ void slide(double (&v)[KC]) {
     static_for<0, KC>([&](auto K_) CFX_INLINE {
         constexpr int k = decltype(K_)::value;
         double s = from_next_lane(v[k]);
-        if (k + 1 < KC) {
+        if constexpr (k + 1 < KC) {
             const double head = lane_read(v[k + 1], 0);
             s = lane == 63 ? head : s;
         }

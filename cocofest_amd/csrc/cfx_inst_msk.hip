@@ -12,7 +12,8 @@ namespace cfx {
 namespace {
 
 bool dispatch(MskCall& c) {
-    return msk_dispatch_s22(c) || msk_dispatch_s21(c) || msk_dispatch_s11(c) || msk_dispatch_s26(c);
+    return msk_dispatch_s22(c) || msk_dispatch_s21(c) || msk_dispatch_s11(c) || msk_dispatch_s26(c) ||
+           msk_dispatch_hmed(c);
 }
 
 MskCall make(int op, int nq, int nm, int fam, int scheme) {

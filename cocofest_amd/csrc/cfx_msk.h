@@ -31,7 +31,7 @@ constexpr int kMskMaxQ = 4;      // dofs of the serial chain
 constexpr int kMskMaxMus = 8;    // muscles
 constexpr int kMskMaxPts = 16;   // path points per muscle (origin, via points, insertion)
 constexpr int kMskMaxX = kMskMaxMus * 5 + 2 * kMskMaxQ;
-constexpr int kMskMaxZ = kMskMaxX + kMskMaxMus + kMskMaxQ;
+constexpr int kMskMaxZ = 64;  // decision variables of one interval (the dependency masks are 64-bit)
 
 // ---- structural dependency bitmask (host sparsity pass) ------------------------------------------------------
 struct Dep {
@@ -155,6 +155,7 @@ struct MskMuscleConst {
     double pd0, inv_pdt;
     double alpha_a, alpha_tau1, alpha_km, inv_tau_fat, a_fat_rest;
     double inv_lopt, slack, inv_cos_penn;
+    double ar, bs, Is, cr;  // Hmed2018 recruitment curve lambda(I) (hmed2018.py:169-180)
 };
 
 struct MskGeom {
@@ -180,10 +181,13 @@ struct MskGeom {
 struct MskParams {
     int64_t B;
     int32_t N, m, nx, nu, nz, Q, nnzk, nhk, residual, npw;
+    int32_t T, ngk;      // truncation; rows per interval (nx continuity rows, then the Hmed sliding-window rows)
     double dt, h;
-    const double* cs;    // calcium sums [N][Q][NM] at every RK stage time (host, reference operation order)
+    // calcium sums [N][Q][NM] at every RK stage time (host, reference operation order); Hmed2018: the per-pulse
+    // coefficients r_i exp(-(t - t_i) / tau_c) [N][Q][NM][TMAX] of cs = sum_i coef_i lambda(I_i)
+    const double* cs;
     const double* rest;  // rest state [nx] (IVP default x0)
-    double* scratch;     // k_msk_stagecoef -> k_msk_tangents: per-stage Jacobian coefficients [N][Q][NC][B]
+    double* scratch;     // k_msk_stagecoef_par -> k_msk_tangents: per-stage Jacobian coefficients [N][Q][NC][B]
 };
 
 template <int FAM>
@@ -193,6 +197,87 @@ constexpr int msk_nxm() {
 template <int FAM>
 constexpr bool msk_pw() {
     return FAM == 2 || FAM == 3;
+}
+// Hmed2018 families: 4 / 5 (T <= 10), 6 / 7 (T <= 20); bit 0 is fatigue as for the Ding families
+template <int FAM>
+constexpr bool msk_hmed() {
+    return FAM >= 4;
+}
+template <int FAM>
+constexpr int msk_tmax() {
+    return FAM < 4 ? 0 : (FAM < 6 ? 10 : 20);
+}
+// Controls in the kernels' canonical slots: [pulse widths (Ding2007) | TMAX intensities per muscle (Hmed2018) |
+// residual torques]; msk_udec maps a slot to its control index in the decision vector (-1: a padding intensity
+// past the truncation, or a residual torque the problem does not have).
+template <int NM, int FAM>
+constexpr int msk_nui() {
+    return (msk_pw<FAM>() ? NM : 0) + NM * msk_tmax<FAM>();
+}
+template <int NQ, int NM, int FAM>
+constexpr int msk_numax() {
+    return msk_nui<NM, FAM>() + NQ;
+}
+template <int NM, int FAM>
+MSK_HD int msk_udec(int c, int T, int nu) {
+    if constexpr (msk_hmed<FAM>()) {
+        constexpr int TM = msk_tmax<FAM>();
+        if (c < NM * TM) {
+            const int m = c / TM, j = c - m * TM;
+            return j < T ? m * T + j : -1;
+        }
+        const int d = NM * T + (c - NM * TM);
+        return d < nu ? d : -1;
+    } else {
+        return c < nu ? c : -1;
+    }
+}
+// stride of the stage table P.cs per (interval, stage)
+template <int NM, int FAM>
+constexpr int msk_cs_stride() {
+    return msk_hmed<FAM>() ? NM * msk_tmax<FAM>() : NM;
+}
+// Hmed2018 recruitment lambda(I) = ar (tanh(bs (I - Is)) + cr) and its first two derivatives (hmed2018.py:169-180)
+MSK_HD void msk_lambda(const MskMuscleConst& L, double I, double& l0, double& l1, double& l2) {
+    const double t = tanh(L.bs * (I - L.Is)), s = 1.0 - t * t;
+    l0 = L.ar * (t + L.cr);
+    l1 = L.ar * L.bs * s;
+    l2 = -2.0 * L.ar * L.bs * L.bs * t * s;
+}
+// the lambdas of one interval's intensities (canonical slots u[mu TMAX + i])
+template <int NM, int FAM, class SU>
+MSK_HD void msk_interval_lam(const MskGeom& G, const SU* u, double* lam) {
+    if constexpr (msk_hmed<FAM>()) {
+        constexpr int TM = msk_tmax<FAM>();
+#pragma unroll
+        for (int mu = 0; mu < NM; ++mu)
+#pragma unroll
+            for (int i = 0; i < TM; ++i) {
+                double l1, l2;
+                msk_lambda(G.mc[mu], value(u[mu * TM + i]), lam[mu * TM + i], l1, l2);
+            }
+    }
+}
+// the NM calcium sums of stage kq: the table (Ding) or sum_i coef_i lambda_i (Hmed; lam: the NM * TMAX lambdas of
+// the interval's intensities, nullptr on the host dependency pass, where only the structure matters)
+template <int NM, int FAM>
+MSK_HD void msk_stage_cs(const double* __restrict__ tab, int64_t kq, const double* lam, double* cs) {
+    if constexpr (msk_hmed<FAM>()) {
+        constexpr int TM = msk_tmax<FAM>();
+        const double* c = tab + kq * NM * TM;
+#pragma unroll
+        for (int mu = 0; mu < NM; ++mu) {
+            double sum = 0.0;
+            if (lam) {
+#pragma unroll
+                for (int i = 0; i < TM; ++i) sum = sum + c[mu * TM + i] * lam[mu * TM + i];
+            }
+            cs[mu] = sum;
+        }
+    } else {
+#pragma unroll
+        for (int mu = 0; mu < NM; ++mu) cs[mu] = tab[kq * NM + mu];
+    }
 }
 
 // ---- small vector helpers ---------------------------------------------------------------------------------------
@@ -538,12 +623,12 @@ MSK_HD void msk_rhs(const MskGeom& G, int residual, const double* cs, const S* x
     constexpr int NXM = msk_nxm<FAM>();
     constexpr bool FAT = (FAM & 1) != 0, PW = msk_pw<FAM>();
     constexpr int XQ = NM * NXM, XQD = XQ + NQ;
-    constexpr int NPW = PW ? NM : 0;
+    constexpr int NUI = msk_nui<NM, FAM>();
     S F[NM], mult[NM], qdd[NQ], taur[NQ];
 #pragma unroll
     for (int mu = 0; mu < NM; ++mu) F[mu] = x[mu * NXM + 1];
 #pragma unroll
-    for (int k = 0; k < NQ; ++k) taur[k] = residual ? u[NPW + k] : Num<S>::c(0.0);
+    for (int k = 0; k < NQ; ++k) taur[k] = residual ? u[NUI + k] : Num<S>::c(0.0);
     msk_skeleton<NQ, NM>(G, x + XQ, x + XQD, F, residual ? taur : nullptr, mult, qdd, nullptr, nullptr);
 #pragma unroll
     for (int mu = 0; mu < NM; ++mu) {
@@ -551,6 +636,11 @@ MSK_HD void msk_rhs(const MskGeom& G, int residual, const double* cs, const S* x
         // FES muscle ODE (ding2003.py:254-311, ding2003_with_fatigue.py:197-240, ding2007.py:172-188)
         const S& cn = x[mu * NXM];
         f[mu * NXM] = (cs[mu] - cn) * C.inv_tauc;
+        if constexpr (msk_hmed<FAM>() && std::is_same<S, Dep>::value) {
+            // structure pass: cn_dot reads the muscle's intensities through cs (hmed2018.py:97-98)
+#pragma unroll
+            for (int i = 0; i < msk_tmax<FAM>(); ++i) f[mu * NXM] = f[mu * NXM] + u[mu * msk_tmax<FAM>() + i];
+        }
         S km = Num<S>::c(C.km_rest), tau1 = Num<S>::c(C.tau1_rest), A = Num<S>::c(C.a_force);
         if constexpr (FAT) {
             A = x[mu * NXM + 2];
@@ -577,13 +667,16 @@ MSK_HD void msk_rhs(const MskGeom& G, int residual, const double* cs, const S* x
 // Phi_m(x, u) over interval k: m RK sub-steps (bioptim convention: constant control, RK4 stage times
 // t, t + h/2, t + h/2, t + h).  x is overwritten with the end state.
 template <int NQ, int NM, int FAM, int SCHEME, class S>
-MSK_HD void msk_interval(const MskParams& P, const MskGeom& G, int k, S* x, const S* u) {
+MSK_HD void msk_interval(const MskParams& P, const MskGeom& G, int k, S* x, const S* u, const double* lam) {
     constexpr int NX = NM * msk_nxm<FAM>() + 2 * NQ;
     constexpr int ST = SCHEME == 4 ? 4 : (SCHEME == 2 ? 2 : 1);
     constexpr int NMC = NM;
     const double h = P.h;
     for (int j = 0; j < P.m; ++j) {
-        const double* cs = P.cs + ((int64_t)k * P.Q + j * ST) * NMC;
+        double csv[ST * NMC];  // the stage sums of this sub-step
+#pragma unroll
+        for (int st = 0; st < ST; ++st) msk_stage_cs<NM, FAM>(P.cs, (int64_t)k * P.Q + j * ST + st, lam, csv + st * NMC);
+        const double* cs = csv;
         if constexpr (SCHEME == 1) {
             S f[NX];
             msk_rhs<NQ, NM, FAM>(G, P.residual, cs, x, u, f);
@@ -630,7 +723,7 @@ __global__ void __launch_bounds__(256) k_msk_shooting(const MskParams P, const M
                                                       const double* __restrict__ V, double* __restrict__ Gout,
                                                       double* __restrict__ J) {
     constexpr int NX = NM * msk_nxm<FAM>() + 2 * NQ;
-    constexpr int NUMAX = (msk_pw<FAM>() ? NM : 0) + NQ;
+    constexpr int NUMAX = msk_numax<NQ, NM, FAM>();
     const int64_t B = P.B;
     const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= B) return;
@@ -649,19 +742,22 @@ __global__ void __launch_bounds__(256) k_msk_shooting(const MskParams P, const M
     }
 #pragma unroll
     for (int i = 0; i < NUMAX; ++i) {
-        u[i] = dconst<D>(i < nu ? V[(zb + NX + i) * B + b] : 0.0);
+        const int dc = msk_udec<NM, FAM>(i, P.T, nu);
+        u[i] = dconst<D>(dc >= 0 ? V[(zb + NX + dc) * B + b] : 0.0);
 #pragma unroll
-        for (int d = 0; d < D; ++d) u[i].d[d] = (NX + i == c0 + d) ? 1.0 : 0.0;
+        for (int d = 0; d < D; ++d) u[i].d[d] = (dc >= 0 && NX + dc == c0 + d) ? 1.0 : 0.0;
     }
     double xn[NX];
     if (Gout && blockIdx.z == 0) {
 #pragma unroll
         for (int r = 0; r < NX; ++r) xn[r] = V[(zb + nz + r) * B + b];
     }
-    msk_interval<NQ, NM, FAM, SCHEME>(P, G, k, x, u);
+    double lam[msk_hmed<FAM>() ? NM * msk_tmax<FAM>() : 1];
+    msk_interval_lam<NM, FAM>(G, u, lam);
+    msk_interval<NQ, NM, FAM, SCHEME>(P, G, k, x, u, lam);
     if (Gout && blockIdx.z == 0) {
 #pragma unroll
-        for (int r = 0; r < NX; ++r) Gout[((int64_t)k * NX + r) * B + b] = x[r].v - xn[r];
+        for (int r = 0; r < NX; ++r) Gout[((int64_t)k * P.ngk + r) * B + b] = x[r].v - xn[r];
     }
     if (J) {
         const int64_t jb = (int64_t)k * P.nnzk;
@@ -682,15 +778,16 @@ __global__ void __launch_bounds__(256) k_msk_shooting(const MskParams P, const M
     }
 }
 
-// ---- g + J_g, structured (two launches) ---------------------------------------------------------------------
+// ---- g + J_g, structured (three launches) -------------------------------------------------------------------
 // The muscle ODEs touch the skeleton only through mult_m(q, qdot) (Hill multiplier) and the forces F_m, and the
 // skeleton is linear in F and in the residual torque: qdd = a(q, qdot) + sum_m B_m(q) F_m + M^-1 tau.  So every
 // RK stage's RHS Jacobian is assembled from one Dual<2 nq> pass of the skeleton over (q, qdot) — independent of
 // how many Jacobian columns are wanted — the values of B_m = -M^-1 J_L[m]^T and M^-1, and the analytic partials
 // of the muscle ODEs (ding2003.py:254-311, ding2003_with_fatigue.py:197-240, ding2007.py:172-188).
-//   k_msk_stagecoef  thread = (instance, interval): the value recursion (g) and, per RK stage (skeleton in
-//                    Dual<nq> for the q-only part, Dual<2 nq> for the velocity-dependent part), those NC
-//                    coefficients, stored element-major over the batch in a scratch buffer;
+//   k_msk_values     thread = (instance, interval): the value recursion (g), every stage input stored (XS);
+//   k_msk_stagecoef_par  thread = (instance, interval, stage): per RK stage (skeleton in Dual<nq> for the q-only
+//                    part, Dual<2 nq> for the velocity-dependent part), those NC coefficients, stored
+//                    element-major over the batch in a scratch buffer;
 //   k_msk_tangents   thread = (instance, interval, Jacobian column): the RK recursion of one tangent column
 //                    through the stored stage Jacobians (~100 FMAs per stage); a block holds 256 consecutive
 //                    instances of one column (coalesced loads and J stores), XCD-aware block numbering.
@@ -737,7 +834,7 @@ __device__ __forceinline__ void msk_stage(const MskGeom& G, int residual, const 
                                           const double* u, double* f, double* __restrict__ Ws, int64_t B) {
     constexpr int NXM = msk_nxm<FAM>(), XQ = NM * NXM, XQD = XQ + NQ, ND = 2 * NQ;
     constexpr bool FAT = (FAM & 1) != 0, PW = msk_pw<FAM>();
-    constexpr int NPW = PW ? NM : 0, OM = 6 + ND, ODQ = NM * OM, OB = ODQ + NQ * ND, OMI = OB + NQ * NM;
+    constexpr int NUI = msk_nui<NM, FAM>(), OM = 6 + ND, ODQ = NM * OM, OB = ODQ + NQ * ND, OMI = OB + NQ * NM;
     using S = Dual<ND>;
     Dual<NQ> q[NQ];  // q-only quantities carry the nq q-directions, the rest all 2 nq (msk_skeleton)
     S qd[NQ], F[NM], taur[NQ], mult[NM], qdd[NQ];
@@ -747,7 +844,7 @@ __device__ __forceinline__ void msk_stage(const MskGeom& G, int residual, const 
         qd[k] = dconst<ND>(xs[XQD + k]);
         q[k].d[k] = 1.0;
         qd[k].d[NQ + k] = 1.0;
-        taur[k] = dconst<ND>(residual ? u[NPW + k] : 0.0);
+        taur[k] = dconst<ND>(residual ? u[NUI + k] : 0.0);
     }
 #pragma unroll
     for (int mu = 0; mu < NM; ++mu) F[mu] = dconst<ND>(xs[mu * NXM + 1]);
@@ -757,8 +854,9 @@ __device__ __forceinline__ void msk_stage(const MskGeom& G, int residual, const 
     for (int mu = 0; mu < NM; ++mu) {
         const MskMuscleConst& C = G.mc[mu];
         const double* xm = xs + mu * NXM;
-        double c[6], base;
-        msk_muscle_coef<FAM>(C, xm, PW ? u[mu] : 0.0, mult[mu].v, c, base);
+        double c[6], base, pw = 0.0;
+        if constexpr (PW) pw = u[mu];  // (a plain ternary would still index u out of range for NM > NQ)
+        msk_muscle_coef<FAM>(C, xm, pw, mult[mu].v, c, base);
         f[mu * NXM] = (cs[mu] - xm[0]) * C.inv_tauc;
         f[mu * NXM + 1] = base * mult[mu].v;
         if constexpr (FAT) {
@@ -816,79 +914,21 @@ __device__ __forceinline__ void msk_stage(const MskGeom& G, int residual, const 
     }
 }
 
-#ifndef CFX_MSK_SC_ATTR
-#define CFX_MSK_SC_ATTR  // tuning hook (occupancy attributes of k_msk_stagecoef)
-#endif
-template <int NQ, int NM, int FAM, int SCHEME>
-__global__ void __launch_bounds__(256) CFX_MSK_SC_ATTR k_msk_stagecoef(const MskParams P, const MskGeom* __restrict__ GG,
-                                                       const double* __restrict__ V, double* __restrict__ Gout,
-                                                       double* __restrict__ XS) {
-    constexpr int NXM = msk_nxm<FAM>(), NX = NM * NXM + 2 * NQ;
-    constexpr int NUMAX = (msk_pw<FAM>() ? NM : 0) + NQ;
-    constexpr int NC = msk_ncoef<NQ, NM>();
-    constexpr int ST = SCHEME == 4 ? 4 : (SCHEME == 2 ? 2 : 1);
-    const int64_t B = P.B;
-    const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (b >= B) return;
-    const int k = blockIdx.y;
-    const MskGeom& G = *GG;
-    const int nz = P.nz, nu = P.nu, Q = P.Q, residual = P.residual;
-    const int64_t zb = (int64_t)k * nz;
-    const double h = P.h;
-    double* __restrict__ Wk = P.scratch + (int64_t)k * Q * NC * B + b;
-    double x[NX], u[NUMAX];
-#pragma unroll
-    for (int r = 0; r < NX; ++r) x[r] = V[(zb + r) * B + b];
-#pragma unroll
-    for (int i = 0; i < NUMAX; ++i) u[i] = i < nu ? V[(zb + NX + i) * B + b] : 0.0;
-    for (int j = 0; j < P.m; ++j) {
-        double acc[NX], xs[NX];
-#pragma unroll
-        for (int r = 0; r < NX; ++r) xs[r] = x[r];
-#pragma unroll 1  // one copy of the ~5k-instruction stage body: 1.16 ms vs 1.30 ms unrolled (cfg 5, B = 65536)
-        for (int st = 0; st < ST; ++st) {
-            const int slot = j * ST + st;
-            if (XS) {  // stage values for the stage-wise Hessian (k_msk_hpair)
-#pragma unroll
-                for (int r = 0; r < NX; ++r) XS[(((int64_t)k * Q + slot) * NX + r) * B + b] = xs[r];
-            }
-            double f[NX];
-            msk_stage<NQ, NM, FAM>(G, residual, P.cs + ((int64_t)k * Q + slot) * NM, xs, u, f,
-                                   Wk + (int64_t)slot * NC * B, B);
-            const double cst = (ST == 4 && st == 2) ? h : 0.5 * h;
-#pragma unroll
-            for (int r = 0; r < NX; ++r) {
-                if (ST == 4) {
-                    if (st == 0) acc[r] = f[r];
-                    else if (st < 3) acc[r] = acc[r] + 2.0 * f[r];
-                }
-                if (st + 1 < ST) xs[r] = x[r] + cst * f[r];
-            }
-            if (st + 1 == ST) {
-#pragma unroll
-                for (int r = 0; r < NX; ++r) x[r] = ST == 4 ? x[r] + (h / 6.0) * (acc[r] + f[r]) : x[r] + h * f[r];
-            }
-        }
-    }
-    if (Gout) {
-#pragma unroll
-        for (int r = 0; r < NX; ++r) Gout[((int64_t)k * NX + r) * B + b] = x[r] - V[(zb + nz + r) * B + b];
-    }
-}
-
 // tk = (df/dx, df/du)(stage) . (t, tu) for one tangent column, from the stored stage coefficients.
+// dcs: Hmed, the stage's d cs_mu / d(column) (zero unless the column is one of the muscle's intensities).
 template <int NQ, int NM, int FAM>
 __device__ __forceinline__ void msk_tangent(const MskGeom& G, int residual, const double* __restrict__ Ws, int64_t B,
-                                            const double* t, const double* tu, double* tk) {
+                                            const double* t, const double* tu, const double* dcs, double* tk) {
     constexpr int NXM = msk_nxm<FAM>(), XQ = NM * NXM, XQD = XQ + NQ, ND = 2 * NQ;
     constexpr bool FAT = (FAM & 1) != 0, PW = msk_pw<FAM>();
-    constexpr int NPW = PW ? NM : 0, OM = 6 + ND, ODQ = NM * OM, OB = ODQ + NQ * ND, OMI = OB + NQ * NM;
+    constexpr int NUI = msk_nui<NM, FAM>(), OM = 6 + ND, ODQ = NM * OM, OB = ODQ + NQ * ND, OMI = OB + NQ * NM;
 #pragma unroll
     for (int mu = 0; mu < NM; ++mu) {
         const MskMuscleConst& C = G.mc[mu];
         const int o = mu * NXM;
         const double* c = Ws + (int64_t)mu * OM * B;
         tk[o] = -C.inv_tauc * t[o];
+        if constexpr (msk_hmed<FAM>()) tk[o] += C.inv_tauc * dcs[mu];
         double s = c[0] * t[o] + c[B] * t[o + 1];
         if constexpr (FAT) s += c[2 * B] * t[o + 2] + c[3 * B] * t[o + 3] + c[4 * B] * t[o + 4];
         if constexpr (PW) s += c[5 * B] * tu[mu];
@@ -911,17 +951,47 @@ __device__ __forceinline__ void msk_tangent(const MskGeom& G, int residual, cons
         for (int mu = 0; mu < NM; ++mu) s += Ws[(OB + i * NM + mu) * B] * t[mu * NXM + 1];
         if (residual) {
 #pragma unroll
-            for (int k = 0; k < NQ; ++k) s += Ws[(OMI + i * NQ + k) * B] * tu[NPW + k];
+            for (int k = 0; k < NQ; ++k) s += Ws[(OMI + i * NQ + k) * B] * tu[NUI + k];
         }
         tk[XQD + i] = s;
     }
 }
 
+// Hmed: is z-column col one of muscle m's intensities (its slot i), and lambda'(I) there; the stage's d cs / d col
+// is then coef[kq][m][i] lambda'(I) (cn_sum is linear in the lambdas, hmed2018.py:97-98)
+struct MskICol {
+    int m, i;
+    double dlam;
+};
+template <int NM, int FAM>
+__device__ __forceinline__ MskICol msk_icol(const MskParams& P, const MskGeom& G, const double* __restrict__ V,
+                                            int64_t zb, int64_t b, bool valid, int col) {
+    MskICol r{-1, 0, 0.0};
+    if constexpr (msk_hmed<FAM>()) {
+        const int d = col - P.nx;
+        if (d >= 0 && d < NM * P.T) {
+            r.m = d / P.T;
+            r.i = d - r.m * P.T;
+            double l0, l2;
+            msk_lambda(G.mc[r.m], valid ? V[(zb + col) * P.B + b] : 0.0, l0, r.dlam, l2);
+        }
+    }
+    return r;
+}
+template <int NM, int FAM>
+__device__ __forceinline__ void msk_icol_dcs(const MskParams& P, const MskICol& ic, int64_t kq, double* dcs) {
+    if constexpr (msk_hmed<FAM>()) {
+        constexpr int TM = msk_tmax<FAM>();
+#pragma unroll
+        for (int mu = 0; mu < NM; ++mu) dcs[mu] = mu == ic.m ? P.cs[(kq * NM + mu) * TM + ic.i] * ic.dlam : 0.0;
+    }
+}
+
 template <int NQ, int NM, int FAM, int SCHEME>
 __global__ void __launch_bounds__(256) k_msk_tangents(const MskParams P, const MskGeom* __restrict__ GG,
-                                                      double* __restrict__ J) {
+                                                      const double* __restrict__ V, double* __restrict__ J) {
     constexpr int NXM = msk_nxm<FAM>(), NX = NM * NXM + 2 * NQ;
-    constexpr int NUMAX = (msk_pw<FAM>() ? NM : 0) + NQ;
+    constexpr int NUMAX = msk_numax<NQ, NM, FAM>();
     constexpr int NC = msk_ncoef<NQ, NM>();
     constexpr int ST = SCHEME == 4 ? 4 : (SCHEME == 2 ? 2 : 1);
     const int64_t B = P.B;
@@ -943,15 +1013,20 @@ __global__ void __launch_bounds__(256) k_msk_tangents(const MskParams P, const M
 #pragma unroll
     for (int r = 0; r < NX; ++r) tx[r] = r == col ? 1.0 : 0.0;
 #pragma unroll
-    for (int i = 0; i < NUMAX; ++i) tu[i] = NX + i == col ? 1.0 : 0.0;
+    for (int i = 0; i < NUMAX; ++i) {
+        const int dc = msk_udec<NM, FAM>(i, P.T, P.nu);
+        tu[i] = dc >= 0 && NX + dc == col ? 1.0 : 0.0;
+    }
+    const MskICol ic = msk_icol<NM, FAM>(P, G, V, (int64_t)k * nz, b, true, col);
     for (int j = 0; j < P.m; ++j) {
         double tacc[NX], txs[NX];
 #pragma unroll
         for (int r = 0; r < NX; ++r) txs[r] = tx[r];
 #pragma unroll
         for (int st = 0; st < ST; ++st) {
-            double tk[NX];
-            msk_tangent<NQ, NM, FAM>(G, residual, Wk + (int64_t)(j * ST + st) * NC * B, B, txs, tu, tk);
+            double tk[NX], dcs[NM];
+            msk_icol_dcs<NM, FAM>(P, ic, (int64_t)k * P.Q + j * ST + st, dcs);
+            msk_tangent<NQ, NM, FAM>(G, residual, Wk + (int64_t)(j * ST + st) * NC * B, B, txs, tu, dcs, tk);
             const double cst = (ST == 4 && st == 2) ? h : 0.5 * h;
 #pragma unroll
             for (int r = 0; r < NX; ++r) {
@@ -986,9 +1061,10 @@ constexpr int kMskLdsLoads = 16;  // coefficient loads in flight per thread whil
 
 template <int NQ, int NM, int FAM, int SCHEME, int TW>
 __global__ void __launch_bounds__(32 * kMskLdsCols) k_msk_tangents_lds(const MskParams P, const MskGeom* __restrict__ GG,
+                                                                     const double* __restrict__ V,
                                                                      double* __restrict__ J) {
     constexpr int NXM = msk_nxm<FAM>(), NX = NM * NXM + 2 * NQ;
-    constexpr int NUMAX = (msk_pw<FAM>() ? NM : 0) + NQ;
+    constexpr int NUMAX = msk_numax<NQ, NM, FAM>();
     constexpr int NC = msk_ncoef<NQ, NM>();
     constexpr int ST = SCHEME == 4 ? 4 : (SCHEME == 2 ? 2 : 1);
     extern __shared__ double sW[];  // [ST][NC][TW]
@@ -1004,7 +1080,11 @@ __global__ void __launch_bounds__(32 * kMskLdsCols) k_msk_tangents_lds(const Msk
 #pragma unroll
     for (int r = 0; r < NX; ++r) tx[r] = r == col ? 1.0 : 0.0;
 #pragma unroll
-    for (int i = 0; i < NUMAX; ++i) tu[i] = NX + i == col ? 1.0 : 0.0;
+    for (int i = 0; i < NUMAX; ++i) {
+        const int dc = msk_udec<NM, FAM>(i, P.T, P.nu);
+        tu[i] = dc >= 0 && NX + dc == col ? 1.0 : 0.0;
+    }
+    const MskICol ic = msk_icol<NM, FAM>(P, G, V, (int64_t)k * nz, b, b < B, col);
     for (int j = 0; j < P.m; ++j) {
         __syncthreads();  // the previous sub-step's coefficients are consumed
         // all of a thread's loads are issued before the first LDS store, so the block waits for one HBM round
@@ -1027,8 +1107,9 @@ __global__ void __launch_bounds__(32 * kMskLdsCols) k_msk_tangents_lds(const Msk
         for (int r = 0; r < NX; ++r) txs[r] = tx[r];
 #pragma unroll
         for (int st = 0; st < ST; ++st) {
-            double tk[NX];
-            msk_tangent<NQ, NM, FAM>(G, residual, sW + st * NC * TW + lane, TW, txs, tu, tk);
+            double tk[NX], dcs[NM];
+            msk_icol_dcs<NM, FAM>(P, ic, (int64_t)k * P.Q + j * ST + st, dcs);
+            msk_tangent<NQ, NM, FAM>(G, residual, sW + st * NC * TW + lane, TW, txs, tu, dcs, tk);
             const double cst = (ST == 4 && st == 2) ? h : 0.5 * h;
 #pragma unroll
             for (int r = 0; r < NX; ++r) {
@@ -1057,7 +1138,7 @@ __global__ void __launch_bounds__(32 * kMskLdsCols) k_msk_tangents_lds(const Msk
 // ---- Lagrangian Hessian by stages ------------------------------------------------------------------------------
 // lambda^T Phi_m(z) is a composition whose only nonlinear nodes are the RK stage evaluations k_s = f(Y_s, u); every
 // other operation is linear in (z, k).  Its Hessian is therefore  sum_s mu_s^T f''(Y_s, u)[dY_s/dz, dY_s/dz],
-// mu_s = d(lambda^T Phi)/dk_s.  Five launches: stage values and coefficients (k_msk_stagecoef with XS), stage
+// mu_s = d(lambda^T Phi)/dk_s.  Five launches: stage values and coefficients (as for g + J_g, or re-used), stage
 // tangents T_s = dY_s/dz (k_msk_htan, thread per column), stage adjoints mu_s (k_msk_hadj, backward sweep), the
 // Y-space Hessians G_s = d^2(mu_s^T f)/dY^2 (k_msk_hpair, thread per stage and coordinate pair, Jet<2>) and the
 // projection H = sum_s T_s^T G_s T_s (k_msk_hproj, thread per Hessian entry).  Every stage is its own thread, so
@@ -1113,9 +1194,9 @@ __device__ __forceinline__ void msk_tangent_T(const MskGeom& G, const double* __
 // stage input tangents TS[k][q][r][col][b] = dY_q[r]/dz[col] (thread = instance, interval, column)
 template <int NQ, int NM, int FAM, int SCHEME>
 __global__ void __launch_bounds__(256) k_msk_htan(const MskParams P, const MskGeom* __restrict__ GG,
-                                                  double* __restrict__ TS) {
+                                                  const double* __restrict__ V, double* __restrict__ TS) {
     constexpr int NXM = msk_nxm<FAM>(), NX = NM * NXM + 2 * NQ;
-    constexpr int NUMAX = (msk_pw<FAM>() ? NM : 0) + NQ;
+    constexpr int NUMAX = msk_numax<NQ, NM, FAM>();
     constexpr int NC = msk_ncoef<NQ, NM>();
     constexpr int ST = SCHEME == 4 ? 4 : (SCHEME == 2 ? 2 : 1);
     const int64_t B = P.B;
@@ -1133,7 +1214,11 @@ __global__ void __launch_bounds__(256) k_msk_htan(const MskParams P, const MskGe
 #pragma unroll
     for (int r = 0; r < NX; ++r) tx[r] = r == col ? 1.0 : 0.0;
 #pragma unroll
-    for (int i = 0; i < NUMAX; ++i) tu[i] = NX + i == col ? 1.0 : 0.0;
+    for (int i = 0; i < NUMAX; ++i) {
+        const int dc = msk_udec<NM, FAM>(i, P.T, P.nu);
+        tu[i] = dc >= 0 && NX + dc == col ? 1.0 : 0.0;
+    }
+    const MskICol ic = msk_icol<NM, FAM>(P, G, V, (int64_t)k * nz, b, true, col);
     for (int j = 0; j < P.m; ++j) {
         double tacc[NX], txs[NX];
 #pragma unroll
@@ -1144,8 +1229,9 @@ __global__ void __launch_bounds__(256) k_msk_htan(const MskParams P, const MskGe
             double* __restrict__ ts = TS + (((int64_t)k * Q + slot) * NX * nz + col) * B + b;
 #pragma unroll
             for (int r = 0; r < NX; ++r) ts[(int64_t)r * nz * B] = txs[r];
-            double tk[NX];
-            msk_tangent<NQ, NM, FAM>(G, P.residual, Wk + (int64_t)slot * NC * B, B, txs, tu, tk);
+            double tk[NX], dcs[NM];
+            msk_icol_dcs<NM, FAM>(P, ic, (int64_t)k * Q + slot, dcs);
+            msk_tangent<NQ, NM, FAM>(G, P.residual, Wk + (int64_t)slot * NC * B, B, txs, tu, dcs, tk);
             const double cst = (ST == 4 && st == 2) ? h : 0.5 * h;
 #pragma unroll
             for (int r = 0; r < NX; ++r) {
@@ -1177,7 +1263,7 @@ __global__ void __launch_bounds__(256) k_msk_hadj(const MskParams P, const MskGe
     const double* __restrict__ Wk = P.scratch + (int64_t)k * Q * NC * B + b;
     double xb[NX];
 #pragma unroll
-    for (int r = 0; r < NX; ++r) xb[r] = LAM[((int64_t)k * NX + r) * B + b];
+    for (int r = 0; r < NX; ++r) xb[r] = LAM[((int64_t)k * P.ngk + r) * B + b];
     for (int j = P.m - 1; j >= 0; --j) {
         double xn[NX], yb[NX];
 #pragma unroll
@@ -1209,7 +1295,7 @@ __global__ void __launch_bounds__(256) k_msk_hpair(const MskParams P, const MskG
                                                    const double* __restrict__ V, const double* __restrict__ XS,
                                                    const double* __restrict__ MU, double* __restrict__ GQ) {
     constexpr int NX = NM * msk_nxm<FAM>() + 2 * NQ;
-    constexpr int NUMAX = (msk_pw<FAM>() ? NM : 0) + NQ;
+    constexpr int NUMAX = msk_numax<NQ, NM, FAM>();
     using S = Jet<2>;
     const int64_t B = P.B;
     const int64_t item = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1225,6 +1311,23 @@ __global__ void __launch_bounds__(256) k_msk_hpair(const MskParams P, const MskG
     // from the stage coefficients, so no skeleton is evaluated (42 of cfg 5's 100 pairs)
     constexpr int NXM = msk_nxm<FAM>(), NPW = msk_pw<FAM>() ? NM : 0, NC = msk_ncoef<NQ, NM>();
     constexpr bool FAT = (FAM & 1) != 0;
+    if constexpr (msk_hmed<FAM>()) {
+        // intensity pairs: cs is a sum of separate lambda(I_i), entering cn_dot linearly, so the only second
+        // derivative is d2/dI_i^2 = coef_i lambda''(I_i) / tau_c on the muscle's Cn row (the host lists no other)
+        const int dI = I - NX, dJ = J - NX;
+        if (dI >= 0 && dI < NM * P.T) {
+            double val = 0.0;
+            if (dJ == dI) {
+                const int m = dI / P.T, i = dI - m * P.T;
+                double l0, l1, l2;
+                msk_lambda(G.mc[m], V[(zb + I) * B + b], l0, l1, l2);
+                const double muc = MU[((int64_t)kq * NX + m * NXM) * B + b];
+                val = muc * G.mc[m].inv_tauc * P.cs[((int64_t)kq * NM + m) * msk_tmax<FAM>() + i] * l2;
+            }
+            GQ[((int64_t)kq * npair + t) * B + b] = val;
+            return;
+        }
+    }
     auto owner = [](int e) { return e < NM * NXM ? e / NXM : ((e >= NX && e < NX + NPW) ? e - NX : -1); };
     const int mI = owner(I), mJ = owner(J);
     if (mI >= 0 && mI == mJ) {
@@ -1268,12 +1371,20 @@ __global__ void __launch_bounds__(256) k_msk_hpair(const MskParams P, const MskG
     }
 #pragma unroll
     for (int i = 0; i < NUMAX; ++i) {
-        u[i] = jconst<2>(i < nu ? V[(zb + NX + i) * B + b] : 0.0);
-        u[i].g[0] = NX + i == I ? 1.0 : 0.0;
-        u[i].g[1] = (I != J && NX + i == J) ? 1.0 : 0.0;
+        const int dc = msk_udec<NM, FAM>(i, P.T, nu);
+        u[i] = jconst<2>(dc >= 0 ? V[(zb + NX + dc) * B + b] : 0.0);
+        u[i].g[0] = dc >= 0 && NX + dc == I ? 1.0 : 0.0;
+        u[i].g[1] = (I != J && dc >= 0 && NX + dc == J) ? 1.0 : 0.0;
     }
     S f[NX];
-    msk_rhs<NQ, NM, FAM>(G, P.residual, P.cs + (int64_t)kq * NM, x, u, f);
+    double csl[NM];  // cs enters cn_dot linearly: its value does not reach a second derivative
+    if constexpr (msk_hmed<FAM>()) {
+#pragma unroll
+        for (int mu = 0; mu < NM; ++mu) csl[mu] = 0.0;
+    } else {
+        msk_stage_cs<NM, FAM>(P.cs, kq, nullptr, csl);
+    }
+    msk_rhs<NQ, NM, FAM>(G, P.residual, csl, x, u, f);
     const int hi = I == J ? 0 : 1;  // Jet<2> second-order slots: (0,0), (1,0), (1,1)
     double acc = 0.0;
 #pragma unroll
@@ -1334,18 +1445,19 @@ __global__ void __launch_bounds__(256) k_msk_hproj(const MskParams P, const doub
         if (c >= a && c < nz) H[(hb + c * (c + 1) / 2 + a) * B + b] = out[c];
 }
 
-// ---- small batches: every stage in its own thread ------------------------------------------------------------
-// k_msk_stagecoef runs m * ST dependent stage evaluations (Dual skeleton) per thread; at batch 1 that chain is the
-// whole launch (~0.5 ms for cfg 5 at RK4 x 5).  Split: k_msk_values runs the plain-double recursion (the g values)
-// and stores every stage input XS, then k_msk_stagecoef_par evaluates each stage's coefficients in its own thread,
-// so the latency is one double recursion plus one Dual stage.  Same for the Hessian projection: k_msk_hproj_stage
-// gives every (stage, column) its own thread and k_msk_hproj_sum adds the stages up in the order k_msk_hproj does.
+// ---- every stage in its own thread ----------------------------------------------------------------------------
+// A fused kernel running the m * ST dependent stage evaluations (Dual skeleton) of an interval in one thread was
+// latency-bound at batch 1 (~0.5 ms for cfg 5 at RK4 x 5).  Split: k_msk_values runs the plain-double recursion (the
+// g values) and stores every stage input XS, then k_msk_stagecoef_par evaluates each stage's coefficients in its own
+// thread, so the latency is one double recursion plus one Dual stage.  Small batches also split the Hessian
+// projection: k_msk_hproj_stage gives every (stage, column) its own thread and k_msk_hproj_sum adds the stages up in
+// the order k_msk_hproj does.
 template <int NQ, int NM, int FAM, int SCHEME>
 __global__ void __launch_bounds__(256) k_msk_values(const MskParams P, const MskGeom* __restrict__ GG,
                                                     const double* __restrict__ V, double* __restrict__ Gout,
                                                     double* __restrict__ XS) {
     constexpr int NXM = msk_nxm<FAM>(), NX = NM * NXM + 2 * NQ;
-    constexpr int NUMAX = (msk_pw<FAM>() ? NM : 0) + NQ;
+    constexpr int NUMAX = msk_numax<NQ, NM, FAM>();
     constexpr int ST = SCHEME == 4 ? 4 : (SCHEME == 2 ? 2 : 1);
     const int64_t B = P.B;
     const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1359,7 +1471,12 @@ __global__ void __launch_bounds__(256) k_msk_values(const MskParams P, const Msk
 #pragma unroll
     for (int r = 0; r < NX; ++r) x[r] = V[(zb + r) * B + b];
 #pragma unroll
-    for (int i = 0; i < NUMAX; ++i) u[i] = i < nu ? V[(zb + NX + i) * B + b] : 0.0;
+    for (int i = 0; i < NUMAX; ++i) {
+        const int dc = msk_udec<NM, FAM>(i, P.T, nu);
+        u[i] = dc >= 0 ? V[(zb + NX + dc) * B + b] : 0.0;
+    }
+    double lam[msk_hmed<FAM>() ? NM * msk_tmax<FAM>() : 1];
+    msk_interval_lam<NM, FAM>(G, u, lam);
     for (int j = 0; j < P.m; ++j) {
         double acc[NX], xs[NX];
 #pragma unroll
@@ -1369,8 +1486,9 @@ __global__ void __launch_bounds__(256) k_msk_values(const MskParams P, const Msk
             const int64_t kq = (int64_t)k * Q + j * ST + st;
 #pragma unroll
             for (int r = 0; r < NX; ++r) XS[(kq * NX + r) * B + b] = xs[r];
-            double f[NX];
-            msk_rhs<NQ, NM, FAM>(G, residual, P.cs + kq * NM, xs, u, f);
+            double f[NX], csl[NM];
+            msk_stage_cs<NM, FAM>(P.cs, kq, lam, csl);
+            msk_rhs<NQ, NM, FAM>(G, residual, csl, xs, u, f);
             const double cst = (ST == 4 && st == 2) ? h : 0.5 * h;
 #pragma unroll
             for (int r = 0; r < NX; ++r) {
@@ -1385,16 +1503,16 @@ __global__ void __launch_bounds__(256) k_msk_values(const MskParams P, const Msk
     }
     if (Gout) {
 #pragma unroll
-        for (int r = 0; r < NX; ++r) Gout[((int64_t)k * NX + r) * B + b] = x[r] - V[(zb + nz + r) * B + b];
+        for (int r = 0; r < NX; ++r) Gout[((int64_t)k * P.ngk + r) * B + b] = x[r] - V[(zb + nz + r) * B + b];
     }
 }
 
-// stage coefficients of k_msk_stagecoef from the stored stage inputs (thread = instance, interval, stage)
+// stage coefficients from the stored stage inputs (thread = instance, interval, stage)
 template <int NQ, int NM, int FAM>
 __global__ void __launch_bounds__(256) k_msk_stagecoef_par(const MskParams P, const MskGeom* __restrict__ GG,
                                                            const double* __restrict__ V, const double* __restrict__ XS) {
     constexpr int NXM = msk_nxm<FAM>(), NX = NM * NXM + 2 * NQ;
-    constexpr int NUMAX = (msk_pw<FAM>() ? NM : 0) + NQ;
+    constexpr int NUMAX = msk_numax<NQ, NM, FAM>();
     constexpr int NC = msk_ncoef<NQ, NM>();
     const int64_t B = P.B;
     const int64_t item = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1404,12 +1522,22 @@ __global__ void __launch_bounds__(256) k_msk_stagecoef_par(const MskParams P, co
     const MskGeom& G = *GG;
     const int nu = P.nu;
     const int64_t zb = (int64_t)k * P.nz;
-    double xs[NX], u[NUMAX], f[NX];
+    double xs[NX], u[NUMAX], f[NX], csl[NM];
 #pragma unroll
     for (int r = 0; r < NX; ++r) xs[r] = XS[(kq * NX + r) * B + b];
 #pragma unroll
-    for (int i = 0; i < NUMAX; ++i) u[i] = i < nu ? V[(zb + NX + i) * B + b] : 0.0;
-    msk_stage<NQ, NM, FAM>(G, P.residual, P.cs + kq * NM, xs, u, f, P.scratch + kq * NC * B + b, B);
+    for (int i = 0; i < NUMAX; ++i) {
+        const int dc = msk_udec<NM, FAM>(i, P.T, nu);
+        u[i] = dc >= 0 ? V[(zb + NX + dc) * B + b] : 0.0;
+    }
+    // f is not used here, and cs enters only f: the Hmed sums are not formed
+    if constexpr (msk_hmed<FAM>()) {
+#pragma unroll
+        for (int mu = 0; mu < NM; ++mu) csl[mu] = 0.0;
+    } else {
+        msk_stage_cs<NM, FAM>(P.cs, kq, nullptr, csl);
+    }
+    msk_stage<NQ, NM, FAM>(G, P.residual, csl, xs, u, f, P.scratch + kq * NC * B + b, B);
 }
 
 // one stage's term T_q^T (G_q T_q[:, a]) of k_msk_hproj (thread = instance, column a, interval-stage kq)
@@ -1477,12 +1605,13 @@ __global__ void __launch_bounds__(256) k_msk_ivp(const MskParams P, const MskGeo
                                                  const double* __restrict__ X0, const double* __restrict__ U,
                                                  double* __restrict__ TR) {
     constexpr int NX = NM * msk_nxm<FAM>() + 2 * NQ;
-    constexpr int NUMAX = (msk_pw<FAM>() ? NM : 0) + NQ;
+    constexpr int NUMAX = msk_numax<NQ, NM, FAM>();
     const int64_t B = P.B;
     const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= B) return;
     const MskGeom& G = *GG;
     double x[NX], u[NUMAX > 0 ? NUMAX : 1];
+    double lam[msk_hmed<FAM>() ? NM * msk_tmax<FAM>() : 1];
 #pragma unroll
     for (int r = 0; r < NX; ++r) x[r] = X0 ? X0[(int64_t)r * B + b] : P.rest[r];
     int64_t row = 0;
@@ -1492,15 +1621,45 @@ __global__ void __launch_bounds__(256) k_msk_ivp(const MskParams P, const MskGeo
     P1.m = 1;
     for (int k = 0; k < P.N; ++k) {
 #pragma unroll
-        for (int i = 0; i < NUMAX; ++i) u[i] = i < P.nu ? U[((int64_t)k * P.nu + i) * B + b] : 0.0;
+        for (int i = 0; i < NUMAX; ++i) {
+            const int dc = msk_udec<NM, FAM>(i, P.T, P.nu);
+            u[i] = dc >= 0 ? U[((int64_t)k * P.nu + dc) * B + b] : 0.0;
+        }
+        msk_interval_lam<NM, FAM>(G, u, lam);
         for (int j = 0; j < P.m; ++j) {
             MskParams Pj = P1;
-            Pj.cs = P.cs + (int64_t)j * (P.Q / P.m) * NM;  // sub-step j's stage sums inside interval k
-            msk_interval<NQ, NM, FAM, SCHEME>(Pj, G, k, x, u);
+            Pj.cs = P.cs + (int64_t)j * (P.Q / P.m) * msk_cs_stride<NM, FAM>();  // sub-step j's stages inside interval k
+            msk_interval<NQ, NM, FAM, SCHEME>(Pj, G, k, x, u, lam);
             ++row;
 #pragma unroll
             for (int r = 0; r < NX; ++r) TR[(row * NX + r) * B + b] = x[r];
         }
+    }
+}
+
+// ---- Hmed sliding-window rows (CustomConstraint.pulse_intensity_sliding_window_constraint, custom_constraints.py:
+// 102-119): row (k, s) = u_k[s] - (parameter sl_param[k][s], or I_min where the window reaches before the first
+// pulse); J entries +1 (and -1 on the parameter) at sl_joff.  thread = (instance, row)
+static __global__ void __launch_bounds__(256) k_msk_slide(const MskParams P, int ns, const int32_t* __restrict__ sl_param,
+                                                   const int32_t* __restrict__ sl_joff, const double* __restrict__ imin,
+                                                   int64_t p_off, const double* __restrict__ V,
+                                                   double* __restrict__ Gout, double* __restrict__ J) {
+    const int64_t B = P.B;
+    const int64_t item = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (item >= B * P.N * ns) return;
+    const int64_t b = item % B, rest = item / B;
+    const int s = (int)(rest % ns);
+    const int64_t k = rest / ns;
+    const int64_t r = k * ns + s;
+    const int pi = sl_param[r];
+    if (Gout) {
+        const double u = V[(k * P.nz + P.nx + s) * B + b];
+        const double w = pi >= 0 ? V[(p_off + pi) * B + b] : imin[s / P.T];
+        Gout[(k * P.ngk + P.nx + s) * B + b] = u - w;
+    }
+    if (J) {
+        J[(int64_t)sl_joff[r] * B + b] = 1.0;
+        if (pi >= 0) J[((int64_t)sl_joff[r] + 1) * B + b] = -1.0;
     }
 }
 

@@ -12,11 +12,14 @@ constexpr int kMskBlk = 256;
 template <int NQ, int NM, int FAM, int SCHEME>
 void dep_t(const MskParams& P, const MskGeom& G, uint64_t* dep) {
     constexpr int NX = NM * msk_nxm<FAM>() + 2 * NQ;
-    constexpr int NUMAX = (msk_pw<FAM>() ? NM : 0) + NQ;
+    constexpr int NUMAX = msk_numax<NQ, NM, FAM>();
     Dep x[NX], u[NUMAX];
     for (int r = 0; r < NX; ++r) x[r].m = 1ull << r;
-    for (int i = 0; i < NUMAX; ++i) u[i].m = i < P.nu ? 1ull << (NX + i) : 0ull;
-    msk_interval<NQ, NM, FAM, SCHEME>(P, G, 0, x, u);
+    for (int i = 0; i < NUMAX; ++i) {
+        const int dc = msk_udec<NM, FAM>(i, P.T, P.nu);
+        u[i].m = dc >= 0 ? 1ull << (NX + dc) : 0ull;
+    }
+    msk_interval<NQ, NM, FAM, SCHEME>(P, G, 0, x, u, (const double*)nullptr);
     for (int r = 0; r < NX; ++r) dep[r] = x[r].m;
 }
 
@@ -29,29 +32,24 @@ hipError_t shoot_t(const MskParams& P, const MskGeom* G, const double* V, double
                            V, Gout, J);
         return hipGetLastError();
     }
-    // g + J_g: stage coefficients, then one thread per Jacobian column
-    constexpr int NX = NM * msk_nxm<FAM>() + 2 * NQ, NC = msk_ncoef<NQ, NM>();
+    // g + J_g: the value recursion (stage inputs XS), every stage's coefficients in its own thread, then one
+    // thread per Jacobian column
+    constexpr int NC = msk_ncoef<NQ, NM>();
     double* XS = P.scratch + P.B * P.N * P.Q * NC;
-    if (P.B <= kMskSmallBatch) {  // value recursion, then every stage's coefficients in its own thread
-        hipLaunchKernelGGL((k_msk_values<NQ, NM, FAM, SCHEME>), dim3(gx, (unsigned)P.N), dim3(kMskBlk), 0, s, P, G, V,
-                           Gout, XS);
-        hipLaunchKernelGGL((k_msk_stagecoef_par<NQ, NM, FAM>),
-                           dim3((unsigned)((P.B * P.N * P.Q + kMskBlk - 1) / kMskBlk)), dim3(kMskBlk), 0, s, P, G, V,
-                           (const double*)XS);
-    } else {
-        hipLaunchKernelGGL((k_msk_stagecoef<NQ, NM, FAM, SCHEME>), dim3(gx, (unsigned)P.N), dim3(kMskBlk), 0, s, P, G,
-                           V, Gout, keep_xs ? XS : (double*)nullptr);
-    }
-    (void)NX;
+    (void)keep_xs;  // the stage values are always left in XS
+    hipLaunchKernelGGL((k_msk_values<NQ, NM, FAM, SCHEME>), dim3(gx, (unsigned)P.N), dim3(kMskBlk), 0, s, P, G, V, Gout,
+                       XS);
+    hipLaunchKernelGGL((k_msk_stagecoef_par<NQ, NM, FAM>), dim3((unsigned)((P.B * P.N * P.Q + kMskBlk - 1) / kMskBlk)),
+                       dim3(kMskBlk), 0, s, P, G, V, (const double*)XS);
     if (P.nz <= kMskLdsCols) {  // coefficients through LDS, one block per 32 instances
         constexpr int ST = SCHEME == 4 ? 4 : (SCHEME == 2 ? 2 : 1), TW = 32;
         hipLaunchKernelGGL((k_msk_tangents_lds<NQ, NM, FAM, SCHEME, TW>), dim3((unsigned)((P.B + TW - 1) / TW), (unsigned)P.N),
-                           dim3(TW * P.nz), ST * NC * TW * sizeof(double), s, P, G, J);
+                           dim3(TW * P.nz), ST * NC * TW * sizeof(double), s, P, G, V, J);
         return hipGetLastError();
     }
     const int64_t ranges8 = ((P.B + kMskBlk - 1) / kMskBlk + 7) / 8 * 8;  // instance ranges, padded to 8 XCDs
     const unsigned gt = (unsigned)(ranges8 * P.nz);
-    hipLaunchKernelGGL((k_msk_tangents<NQ, NM, FAM, SCHEME>), dim3(gt, (unsigned)P.N), dim3(kMskBlk), 0, s, P, G, J);
+    hipLaunchKernelGGL((k_msk_tangents<NQ, NM, FAM, SCHEME>), dim3(gt, (unsigned)P.N), dim3(kMskBlk), 0, s, P, G, V, J);
     return hipGetLastError();
 }
 
@@ -76,17 +74,12 @@ hipError_t hess_t(const MskParams& P, const MskGeom* G, const int16_t* tasks, in
     auto flat = [](int64_t items) { return dim3((unsigned)((items + kMskBlk - 1) / kMskBlk)); };
     const bool small = P.B <= kMskSmallBatch;
     if (!reuse) {  // stage values and coefficients (reuse: left by the g + J_g launch at this point)
-        if (small) {
-            hipLaunchKernelGGL((k_msk_values<NQ, NM, FAM, SCHEME>), dim3(gx, (unsigned)P.N), dim3(kMskBlk), 0, s, Pw, G,
-                               V, (double*)nullptr, XS);
-            hipLaunchKernelGGL((k_msk_stagecoef_par<NQ, NM, FAM>), flat(BNQ), dim3(kMskBlk), 0, s, Pw, G, V,
-                               (const double*)XS);
-        } else {
-            hipLaunchKernelGGL((k_msk_stagecoef<NQ, NM, FAM, SCHEME>), dim3(gx, (unsigned)P.N), dim3(kMskBlk), 0, s, Pw,
-                               G, V, (double*)nullptr, XS);
-        }
+        hipLaunchKernelGGL((k_msk_values<NQ, NM, FAM, SCHEME>), dim3(gx, (unsigned)P.N), dim3(kMskBlk), 0, s, Pw, G, V,
+                           (double*)nullptr, XS);
+        hipLaunchKernelGGL((k_msk_stagecoef_par<NQ, NM, FAM>), flat(BNQ), dim3(kMskBlk), 0, s, Pw, G, V,
+                           (const double*)XS);
     }
-    hipLaunchKernelGGL((k_msk_htan<NQ, NM, FAM, SCHEME>), flat(P.B * P.N * P.nz), dim3(kMskBlk), 0, s, Pw, G, TS);
+    hipLaunchKernelGGL((k_msk_htan<NQ, NM, FAM, SCHEME>), flat(P.B * P.N * P.nz), dim3(kMskBlk), 0, s, Pw, G, V, TS);
     hipLaunchKernelGGL((k_msk_hadj<NQ, NM, FAM, SCHEME>), flat(P.B * P.N), dim3(kMskBlk), 0, s, Pw, G, LAM, MU);
     hipLaunchKernelGGL((k_msk_hpair<NQ, NM, FAM>), flat(BNQ * ntasks), dim3(kMskBlk), 0, s, Pw, G, tasks,
                        ntasks, npair, V, (const double*)XS, (const double*)MU, GQ);
@@ -145,5 +138,6 @@ bool msk_dispatch_s11(MskCall& c);
 bool msk_dispatch_s21(MskCall& c);
 bool msk_dispatch_s22(MskCall& c);
 bool msk_dispatch_s26(MskCall& c);
+bool msk_dispatch_hmed(MskCall& c);
 
 }  // namespace cfx

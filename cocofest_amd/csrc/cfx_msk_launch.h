@@ -13,11 +13,11 @@ bool msk_supported(int nq, int nm, int fam, int scheme);
 // Structural dependency masks of the nx end states of one interval over z = (x_k, u_k) (host, Dep arithmetic).
 void msk_dep_pattern(int nq, int nm, int fam, int scheme, const MskParams& P, const MskGeom& G, uint64_t* dep);
 
-// Per-stage Jacobian coefficients of k_msk_stagecoef (msk_ncoef in cfx_msk.h).
+// Per-stage Jacobian coefficients of k_msk_stagecoef_par (msk_ncoef in cfx_msk.h).
 inline int msk_ncoef_host(int nq, int nm) { return nm * (6 + 2 * nq) + 3 * nq * nq + nq * nm; }
 
-// Batches up to this size run the stage-parallel kernels (k_msk_values + k_msk_stagecoef_par, k_msk_hproj_stage +
-// k_msk_hproj_sum): at a few instances the launches are latency-bound, and a thread per stage cuts the chain.
+// Batches up to this size split the Hessian projection by stage (k_msk_hproj_stage + k_msk_hproj_sum): at a few
+// instances the launch is latency-bound, and a thread per stage cuts the chain.
 constexpr int64_t kMskSmallBatch = 256;
 
 // Work buffer of launch_msk_shooting / launch_msk_hessian (doubles): stage coefficients, stage values XS (their
@@ -31,8 +31,8 @@ inline size_t msk_hess_work_host(int nq, int nm, int nx, int nz, int ntasks, int
     return (size_t)B * N * Q * ((size_t)msk_ncoef_host(nq, nm) + nx + (size_t)nx * nz + nx + ntasks + hq);
 }
 
-// g (+ J_g when J != nullptr; P.scratch then points at a msk_shoot_work_host buffer).  keep_xs: also leave the stage
-// values in the buffer's XS region, so that a launch_msk_hessian at the same point can skip the recursion (reuse).
+// g (+ J_g when J != nullptr; P.scratch then points at a msk_shoot_work_host buffer, whose XS region keeps the stage
+// values, so that a launch_msk_hessian at the same point can skip the recursion: reuse).  keep_xs: unused.
 hipError_t launch_msk_shooting(int nq, int nm, int fam, int scheme, const MskParams& P, const MskGeom* G,
                                const double* V, double* Gout, double* J, bool keep_xs, hipStream_t s);
 hipError_t launch_msk_hessian(int nq, int nm, int fam, int scheme, const MskParams& P, const MskGeom* G,

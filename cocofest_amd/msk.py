@@ -344,13 +344,14 @@ class FesMskModel:
 class FesMskOcp:
     """Transcribed musculoskeletal FES OCP: layout, bounds, initial guess, objective and GPU callbacks.
 
-    Decision vector per instance [x_0, u_0, ..., x_{N-1}, u_{N-1}, x_N]; states [muscle blocks, q, qdot],
-    controls [pulse width per muscle (Ding2007)] then [tau] (residual torque)."""
-
-    n_params = 0
+    Decision vector per instance [x_0, u_0, ..., x_{N-1}, u_{N-1}, x_N (, p)]; states [muscle blocks, q, qdot],
+    controls [pulse width per muscle (Ding2007) | T pulse intensities per muscle (Hmed2018)] then [tau] (residual
+    torque); Hmed2018: the trailing parameters p are the pulses' intensities (per muscle, or shared), tied to the
+    intensity controls by the sliding-window rows (fes_ocp_dynamics.py:343-438)."""
 
     def __init__(self, model: FesMskModel, n_shooting, final_time, ode_solver, rows, objectives, x_bounds, x_init,
-                 u_bounds, u_init, state_names, control_names, n_threads=1, use_sx=True):
+                 u_bounds, u_init, state_names, control_names, n_threads=1, use_sx=True, n_params=0, p_bounds=None,
+                 p_init=None, param_names=(), last_stim_idx=None, param_offset=None):
         self.model = model
         self.n_shooting = n_shooting
         self.final_time = final_time
@@ -363,6 +364,12 @@ class FesMskOcp:
         self.nx, self.nu = len(state_names), len(control_names)
         self.n_threads, self.use_sx = n_threads, use_sx
         self.truncation = model.muscles_dynamics_model[0]._sum_stim_truncation
+        self.n_params = int(n_params)
+        self.p_bounds = p_bounds if p_bounds is not None else (np.zeros(0), np.zeros(0))
+        self.p_init = p_init if p_init is not None else np.zeros(0)
+        self.param_names = list(param_names)  # one name per parameter block, e.g. pulse_intensity_BIClong
+        self.last_stim_idx = last_stim_idx
+        self.param_offset = param_offset
 
     @property
     def nzb(self):
@@ -370,32 +377,45 @@ class FesMskOcp:
 
     @property
     def nv(self):
-        return self.n_shooting * self.nzb + self.nx
+        return self.n_shooting * self.nzb + self.nx + self.n_params
 
-    def pack(self, x, u=None):
+    def pack(self, x, u=None, p=None):
         N, nx = self.n_shooting, self.nx
         v = np.empty(self.nv)
         body = v[: N * self.nzb].reshape(N, self.nzb)
         body[:, :nx] = np.asarray(x, dtype=float)[:, :N].T
         if self.nu:
             body[:, nx:] = np.asarray(u, dtype=float).T
-        v[N * self.nzb:] = np.asarray(x, dtype=float)[:, N]
+        v[N * self.nzb: N * self.nzb + nx] = np.asarray(x, dtype=float)[:, N]
+        if self.n_params:
+            v[N * self.nzb + nx:] = np.asarray(p, dtype=float)
         return v
 
     def unpack(self, v):
+        """(states, controls, parameters) dicts, each value (1, n) — parameters by block name."""
         N, nx = self.n_shooting, self.nx
         v = np.asarray(v)
         body = v[: N * self.nzb].reshape(N, self.nzb)
-        x = np.concatenate([body[:, :nx].T, v[N * self.nzb:, None]], axis=1)
+        x = np.concatenate([body[:, :nx].T, v[N * self.nzb: N * self.nzb + nx, None]], axis=1)
         states = {n: x[i][None, :] for i, n in enumerate(self.state_names)}
         controls = {n: body[:, nx + i][None, :] for i, n in enumerate(self.control_names)}
-        return states, controls, {}
+        params = {}
+        if self.n_params:
+            p = v[N * self.nzb + nx:]
+            bounds = list(self.param_offset_blocks()) + [self.n_params]
+            for i, name in enumerate(self.param_names):
+                params[name] = p[bounds[i]: bounds[i + 1]][None, :]
+        return states, controls, params
+
+    def param_offset_blocks(self):
+        return sorted(set(int(o) for o in self.param_offset)) if self.n_params else []
 
     def bounds_vector(self):
-        return (self.pack(self.x_bounds[0], self.u_bounds[0]), self.pack(self.x_bounds[1], self.u_bounds[1]))
+        return (self.pack(self.x_bounds[0], self.u_bounds[0], self.p_bounds[0]),
+                self.pack(self.x_bounds[1], self.u_bounds[1], self.p_bounds[1]))
 
     def initial_guess_vector(self):
-        return self.pack(self.x_init, self.u_init)
+        return self.pack(self.x_init, self.u_init, self.p_init)
 
     def nlp(self, batch: int = 1, layout: str = "aos", device: int = 0) -> _cfx.MskHandle:
         """Open a libcfx handle evaluating ``batch`` instances of this problem on GPU ``device``."""
@@ -404,7 +424,7 @@ class FesMskOcp:
             n_steps=self.ode_solver.n_integration_steps, n_shooting=self.n_shooting, truncation=self.truncation,
             final_time=float(self.final_time), stim_rows=self.stim_rows, batch=batch, flags=self.model.cfx_flags(),
             layout={"aos": _cfx.LAYOUT_AOS, "soa": _cfx.LAYOUT_SOA}[layout], objectives=self.objectives,
-            device=device)
+            device=device, n_params=self.n_params, last_stim_idx=self.last_stim_idx, param_offset=self.param_offset)
 
     def solve(self, solver=None, **kwargs):
         from .solver import solve_ocp
@@ -437,25 +457,64 @@ class OcpFesMsk:
         OcpFesMsk._sanity_check_msk_inputs(model, msk_info, objective)
         if isinstance(ode_solver, OdeSolver.COLLOCATION):
             raise NotImplementedError("OcpFesMsk: direct collocation is not available for musculoskeletal models")
-        if any(isinstance(m, DingModelPulseIntensityFrequency) for m in muscles):
-            raise NotImplementedError("OcpFesMsk: Hmed2018 pulse-intensity muscles are not supported yet")
         if len({type(m) for m in muscles}) != 1 or len({m._sum_stim_truncation for m in muscles}) != 1:
             raise ValueError("OcpFesMsk: every muscle must use the same model class and truncation")
         if bool(msk_info["with_residual_torque"]) != bool(model.activate_residual_torque):
             raise ValueError("msk_info['with_residual_torque'] must match the model's activate_residual_torque")
         # the OCP's model is rebuilt without the passive-force flag (fes_ocp_dynamics.py:120-131)
         model.activate_passive_force_relationship = False
-        table, _ = muscles[0].get_numerical_data_time_series(n, final_time)
+        table, stim_idx_at_node_list = muscles[0].get_numerical_data_time_series(n, final_time)
         rows = table["stim_time"][:, 0, :].T.copy()
         state_names = model.state_names()
-        control_names = ([f"last_pulse_width_{m.muscle_name}" for m in muscles]
-                         if isinstance(muscles[0], DingModelPulseWidthFrequency) else [])
+        hmed = isinstance(muscles[0], DingModelPulseIntensityFrequency)
+        T = muscles[0]._sum_stim_truncation
+        if isinstance(muscles[0], DingModelPulseWidthFrequency):
+            control_names = [f"last_pulse_width_{m.muscle_name}" for m in muscles]
+        elif hmed:  # configure_pulse_intensity: T intensities per muscle (dynamical_model.py:437-440)
+            control_names = [f"pulse_intensity_{m.muscle_name}_{j}" for m in muscles for j in range(T)]
+        else:
+            control_names = []
         control_names += [f"tau_{q}" for q in model.name_dof] if model.activate_residual_torque else []
         x_bounds, x_init = OcpFesMsk._set_bounds(model, n, msk_info)
         u_bounds, u_init = OcpFesMsk._set_u_bounds(model, n)
         terms = OcpFesMsk._set_objective(model, n, objective, state_names, control_names)
+        par = {}
+        if hmed:
+            n_params, p_bounds, p_init, names, offsets = OcpFesMsk._build_parameters(model, pulse_intensity)
+            # _build_constraints (fes_ocp_dynamics.py:413-438): the window of node k ends at its last pulse
+            last = np.array([stim_idx_at_node_list[k][-1] for k in range(n)], dtype=np.int32)
+            par = dict(n_params=n_params, p_bounds=p_bounds, p_init=p_init, param_names=names, last_stim_idx=last,
+                       param_offset=offsets)
         return FesMskOcp(model, n, final_time, ode_solver, rows, terms, x_bounds, x_init, u_bounds, u_init,
-                         state_names, control_names, n_threads, use_sx)
+                         state_names, control_names, n_threads, use_sx, **par)
+
+    @staticmethod
+    def _build_parameters(model, pulse_intensity):
+        """Hmed2018 pulse-intensity parameters (fes_ocp_dynamics.py:343-411): one block of n_stim intensities per
+        muscle (one shared block with same_for_all_muscles), fixed or bounded by [min, max] with the mid-point as
+        initial guess.  Returns (n_params, (lb, ub), init, block names, per-muscle block offsets)."""
+        muscles = model.muscles_dynamics_model
+        n_stim = len(muscles[0].stim_time)
+        if pulse_intensity["bimapping"]:
+            raise NotImplementedError("bimapped pulse intensities are not supported (the reference's sliding-window "
+                                      "constraint indexes past a size-1 parameter)")
+        fixed, lo, hi = pulse_intensity["fixed"], pulse_intensity["min"], pulse_intensity["max"]
+        if fixed:
+            vals = np.array(fixed if isinstance(fixed, list) else [fixed] * n_stim, dtype=float)
+            if vals.size != n_stim:
+                raise ValueError("pulse_intensity['fixed'] must hold one value per pulse")
+            blo, bhi, binit = vals, vals, vals
+        elif lo and hi:
+            blo, bhi = np.full(n_stim, float(lo)), np.full(n_stim, float(hi))
+            binit = np.full(n_stim, (float(lo) + float(hi)) / 2)
+        else:
+            raise ValueError("Hmed2018 muscles need pulse_intensity 'fixed', or 'min' and 'max'")
+        shared = bool(pulse_intensity["same_for_all_muscles"])
+        nblocks = 1 if shared else len(muscles)
+        names = (["pulse_intensity"] if shared else [f"pulse_intensity_{m.muscle_name}" for m in muscles])
+        offsets = np.array([0 if shared else i * n_stim for i in range(len(muscles))], dtype=np.int32)
+        return (nblocks * n_stim, (np.tile(blo, nblocks), np.tile(bhi, nblocks)), np.tile(binit, nblocks), names,
+                offsets)
 
     @staticmethod
     def _fill_msk_dict(pulse_width, pulse_intensity, objective, msk_info):
@@ -582,13 +641,17 @@ class OcpFesMsk:
 
     @staticmethod
     def _set_u_bounds(model, n):
-        """_set_u_bounds_fes / _set_u_bounds_msk (fes_ocp_dynamics.py:542-589): pulse width in [pd0, 0.0006]
-        (initial guess 0), residual torque in [-200, 200] (initial guess 0)."""
+        """_set_u_bounds_fes / _set_u_bounds_msk (fes_ocp_dynamics.py:542-589): pulse width in [pd0, 0.0006],
+        pulse intensities in [I_min, 130] (initial guess 0), residual torque in [-200, 200] (initial guess 0)."""
         lo, hi = [], []
         if isinstance(model.muscles_dynamics_model[0], DingModelPulseWidthFrequency):
             for m in model.muscles_dynamics_model:
                 lo.append(m.pd0)
                 hi.append(0.0006)
+        if isinstance(model.muscles_dynamics_model[0], DingModelPulseIntensityFrequency):
+            for m in model.muscles_dynamics_model:
+                lo += [float(m.min_pulse_intensity())] * m._sum_stim_truncation
+                hi += [130.0] * m._sum_stim_truncation
         if model.activate_residual_torque:
             lo += [-200.0] * model.nb_q
             hi += [200.0] * model.nb_q

@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define CFX_ABI_VERSION 1
+#define CFX_ABI_VERSION 2
 
 /* return codes */
 #define CFX_OK 0
@@ -199,7 +199,7 @@ int cfx_integrate(cfx_handle *h, const double *x0, const double *u, double *traj
 #define CFX_OBJ_MAYER_INV 2
 
 typedef struct cfx_msk_muscle {
-    int32_t model; /* CFX_DING2003 .. CFX_DING2007_FATIGUE; all muscles of a problem share the model family */
+    int32_t model; /* CFX_DING2003 .. CFX_HMED2018_FATIGUE; all muscles of a problem share the model family */
     cfx_constants constants;
     int32_t n_points;           /* origin, via points, insertion (<= CFX_MSK_MAX_POINTS) */
     const int32_t *point_frame; /* [n_points] dof frame the point is fixed in (moves with q_0..q_j), -1: ground */
@@ -231,6 +231,15 @@ typedef struct cfx_msk_problem {
     int32_t n_objectives;
     const cfx_objective *objectives; /* var_index over the state / control layout above */
     int32_t device;
+    /* Hmed2018 muscles (truncation <= 20): the controls of a node are T pulse intensities per muscle (then the
+       residual torques), as OcpFesMsk configures them (dynamical_model.py:437-440).  n_params > 0: the pulse
+       intensities are trailing parameters of the decision vector and each interval k gets n_muscles * T rows
+       u_k[m T + s] - p[param_offset[m] + last_stim_idx[k] - T + 1 + s] (I_min where that index is negative),
+       after its continuity rows (CustomConstraint.pulse_intensity_sliding_window_constraint,
+       custom_constraints.py:102-119; fes_ocp_dynamics.py:413-438) */
+    int32_t n_params;
+    const int32_t *last_stim_idx; /* [n_shooting] parameter index of the last pulse <= t_k (muscle-relative) */
+    const int32_t *param_offset;  /* [n_muscles] first parameter of each muscle's intensities (equal: shared) */
 } cfx_msk_problem;
 
 int cfx_msk_create(const cfx_msk_problem *problem, cfx_handle **out);

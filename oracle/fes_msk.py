@@ -433,6 +433,11 @@ class MskProblem:
     residual: bool = False
     objectives: list = field(default_factory=list)  # O.Objective-like: kind, var_kind, index, nodes, weight, target
     fatigue_weight: float = 0.0  # minimize_muscle_fatigue Mayer at node N: w * sum_m (a_rest_m / A_m)^2
+    # Hmed2018 muscles: T intensity controls each; with n_params > 0 the trailing parameters are the pulses'
+    # intensities (muscle m's block at param_offset[m]) tied to the controls by sliding-window rows
+    n_params: int = 0
+    last_stim_idx: list = None
+    param_offset: list = None
 
     @property
     def nq(self):
@@ -451,8 +456,20 @@ class MskProblem:
         return sum(1 for m in self.muscles if O.control_kind(m.model) == "pulse_width")
 
     @property
+    def T(self):
+        return self.rows.shape[1]
+
+    @property
+    def n_int(self):
+        return sum(self.T for m in self.muscles if O.control_kind(m.model) == "pulse_intensity")
+
+    @property
+    def n_slide(self):
+        return self.n_int if self.n_params else 0
+
+    @property
     def nu(self):
-        return self.n_pw + (self.nq if self.residual else 0)
+        return self.n_pw + self.n_int + (self.nq if self.residual else 0)
 
     @property
     def nz(self):
@@ -460,11 +477,11 @@ class MskProblem:
 
     @property
     def nv(self):
-        return self.n_shooting * self.nz + self.nx
+        return self.n_shooting * self.nz + self.nx + self.n_params
 
     @property
     def ng(self):
-        return self.n_shooting * self.nx
+        return self.n_shooting * (self.nx + self.n_slide)
 
     @property
     def dt(self):
@@ -498,6 +515,9 @@ def msk_rhs(pb: MskProblem, t, x, u, row):
         if O.control_kind(mus.model) == "pulse_width":
             um = np.array([u[pw]])
             pw += 1
+        elif O.control_kind(mus.model) == "pulse_intensity":  # the muscle's T intensities (dynamical_model.py:253-255)
+            um = u[pw: pw + pb.T]
+            pw += pb.T
         dxm = O.rhs(mus.model, mus.c, t, xm, um, row, fl=fl, fv=fv, fp=fp)
         dx.extend(list(dxm))
         JL_rows.append(JL)
@@ -506,7 +526,7 @@ def msk_rhs(pb: MskProblem, t, x, u, row):
     JLm = np.stack(JL_rows)  # (n_muscles, nq): musclesLengthJacobian rows in muscle order
     tau = -JLm.T @ np.array(F)  # dynamical_model.py:331-332
     if pb.residual:
-        tau = tau + u[pb.n_pw: pb.n_pw + nq]
+        tau = tau + u[pb.n_pw + pb.n_int: pb.n_pw + pb.n_int + nq]
     qddot = forward_dynamics(pb.bm, q, qdot, tau)
     return np.concatenate([np.array(dx), qdot, qddot])
 
@@ -526,15 +546,37 @@ def integrate_interval(pb: MskProblem, k, x, u, keep_substeps=False):
 def unpack(pb: MskProblem, v):
     N, nx, nz = pb.n_shooting, pb.nx, pb.nz
     body = v[: N * nz].reshape(N, nz)
-    X = np.concatenate([body[:, :nx], v[None, N * nz:]], axis=0)  # (N+1, nx)
+    X = np.concatenate([body[:, :nx], v[None, N * nz: N * nz + nx]], axis=0)  # (N+1, nx)
     U = body[:, nx:]
     return X, U
 
 
-def eval_g(pb: MskProblem, v):
-    """Continuity rows Phi(x_k, u_k) - x_{k+1}, interval-major."""
+def sliding_rows(pb: MskProblem, v, k):
+    """custom_constraints.py:102-119 per Hmed muscle: u_k's T intensities minus the last T parameters up to the
+    node's last pulse, left-padded with the muscle's I_min."""
     X, U = unpack(pb, v)
-    return np.concatenate([integrate_interval(pb, k, X[k], U[k]) - X[k + 1] for k in range(pb.n_shooting)])
+    P = v[pb.n_shooting * pb.nz + pb.nx:]
+    out, off = [], pb.n_pw
+    for mi, mus in enumerate(pb.muscles):
+        idx = pb.last_stim_idx[k]
+        cols = [P[pb.param_offset[mi] + i] for i in range(idx + 1)]
+        while len(cols) < pb.T:
+            cols.insert(0, O.min_pulse_intensity(mus.c))
+        cols = cols[len(cols) - pb.T:]
+        out.append(U[k, off: off + pb.T] - np.array(cols))
+        off += pb.T
+    return np.concatenate(out)
+
+
+def eval_g(pb: MskProblem, v):
+    """Per interval: continuity rows Phi(x_k, u_k) - x_{k+1}, then (Hmed with parameters) the sliding rows."""
+    X, U = unpack(pb, v)
+    parts = []
+    for k in range(pb.n_shooting):
+        parts.append(integrate_interval(pb, k, X[k], U[k]) - X[k + 1])
+        if pb.n_slide:
+            parts.append(sliding_rows(pb, v, k))
+    return np.concatenate(parts)
 
 
 def continuity_jacobian(pb: MskProblem, v, k):

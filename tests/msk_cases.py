@@ -19,7 +19,14 @@ from oracle import fes_oracle as O
 GOLDEN = pathlib.Path(__file__).with_name("golden")
 STIMS = [round(0.1 * i, 10) for i in range(10)]  # 10 pulses @ 10 Hz (BASELINE config 5)
 FAMILY = {"ding2003": "DingModelFrequency", "ding2003_with_fatigue": "DingModelFrequencyWithFatigue",
-          "ding2007": "DingModelPulseWidthFrequency", "ding2007_with_fatigue": "DingModelPulseWidthFrequencyWithFatigue"}
+          "ding2007": "DingModelPulseWidthFrequency", "ding2007_with_fatigue": "DingModelPulseWidthFrequencyWithFatigue",
+          "hmed2018": "DingModelPulseIntensityFrequency",
+          "hmed2018_with_fatigue": "DingModelPulseIntensityFrequencyWithFatigue"}
+I_MAX = 130.0  # the reference's Hmed MSK intensity bounds (tests/shard2/test_fes_dynamics.py:120-125)
+
+
+def _hmed(model):
+    return model.startswith("hmed2018")
 
 
 def biomod_path(name="arm26_biceps_triceps") -> str:
@@ -40,6 +47,9 @@ def product_ocp(model, biomod, muscles, scheme, m, fv, residual, fatigue, qdot_e
                 passive=False):
     import cocofest_amd as C
 
+    pint = None
+    if _hmed(model):  # intensities bounded by [I_min, 130] (the reference's Hmed MSK test)
+        pint = {"min": float(O.min_pulse_intensity(O.model_constants(model))), "max": I_MAX}
     cls = getattr(C, FAMILY[model])
     mm = C.FesMskModel(biorbd_path=biomod_path(biomod),
                        muscles_model=[cls(muscle_name=n, sum_stim_truncation=truncation) for n in muscles],
@@ -59,7 +69,8 @@ def product_ocp(model, biomod, muscles, scheme, m, fv, residual, fatigue, qdot_e
     nq = mm.nb_q
     info = {"bound_type": "start_end", "bound_data": [[0] * (nq - 1) + [bound[0]], [0] * (nq - 1) + [bound[1]]],
             "with_residual_torque": residual}
-    ocp = C.OcpFesMsk.prepare_ocp(model=mm, final_time=1, objective=obj, msk_info=info, ode_solver=solver)
+    ocp = C.OcpFesMsk.prepare_ocp(model=mm, final_time=1, objective=obj, msk_info=info, ode_solver=solver,
+                                  pulse_intensity=pint)
     if passive:  # OcpFesMsk drops the flag as the reference does; set it back to exercise the kernels' FP term
         ocp.model.activate_passive_force_relationship = True
     return ocp
@@ -73,6 +84,11 @@ def oracle_problem(model, biomod, muscles, scheme, m, fv, residual, fatigue, qdo
     mus = [M.MskMuscle(model=model, name=nm, c=O.model_constants(model)) for nm in muscles]
     pb = M.MskProblem(bm=bm, muscles=mus, rows=tab.rows, n_shooting=n, final_time=1.0, scheme=scheme, m=m, fv_on=fv,
                       fp_on=passive, residual=residual)
+    if _hmed(model):  # one block of n_stim intensity parameters per muscle; node k's window ends at its last pulse
+        pb.n_params = len(STIMS) * len(muscles)
+        pb.param_offset = [i * len(STIMS) for i in range(len(muscles))]
+        dt = 1.0 / n
+        pb.last_stim_idx = [sum(1 for t in STIMS if t <= k * dt + 1e-12) - 1 for k in range(n)]
     nq, nxm = pb.nq, pb.nxm
     if qdot_end:
         for j in range(nq):
@@ -80,8 +96,8 @@ def oracle_problem(model, biomod, muscles, scheme, m, fv, residual, fatigue, qdo
                                       weight=100.0, target_value=0.0))
     if residual:
         for j in range(nq):
-            pb.objectives.append(dict(kind=0, var_kind=1, var_index=pb.n_pw + j, node_first=0, node_last=n - 1,
-                                      weight=10000.0, target_value=0.0))
+            pb.objectives.append(dict(kind=0, var_kind=1, var_index=pb.n_pw + pb.n_int + j, node_first=0,
+                                      node_last=n - 1, weight=10000.0, target_value=0.0))
     if fatigue:
         pb.fatigue_weight = 1.0
     return pb
@@ -112,11 +128,16 @@ def random_decision(pb, B, seed=0):
     U = np.empty((B, N, pb.nu))
     for i in range(pb.n_pw):
         U[..., i] = r.uniform(1.4e-4, 6e-4, U.shape[:2])
+    imin = [O.min_pulse_intensity(m.c) for m in pb.muscles if O.control_kind(m.model) == "pulse_intensity"]
+    for i in range(pb.n_int):  # intensities in [I_min, 130]
+        U[..., pb.n_pw + i] = r.uniform(imin[i // pb.T], I_MAX, U.shape[:2])
     for j in range(nq if pb.residual else 0):
-        U[..., pb.n_pw + j] = r.uniform(-5.0, 5.0, U.shape[:2])
+        U[..., pb.n_pw + pb.n_int + j] = r.uniform(-5.0, 5.0, U.shape[:2])
     V = np.empty((B, pb.nv))
     body = V[:, : N * pb.nz].reshape(B, N, pb.nz)
     body[..., :nx] = X[:, :N]
     body[..., nx:] = U
-    V[:, N * pb.nz:] = X[:, N]
+    V[:, N * pb.nz: N * pb.nz + nx] = X[:, N]
+    if pb.n_params:
+        V[:, N * pb.nz + nx:] = r.uniform(imin[0], I_MAX, (B, pb.n_params))
     return V

@@ -28,15 +28,26 @@ CASES = {
                                         residual=True),
     "arm26_6muscles_d03_rk1": MC.cfg5(biomod="arm26", model="ding2003", fatigue=False, scheme="RK1", m=3,
                                       muscles=("BIClong", "BICshort", "BRA", "TRIlong", "TRIlat", "TRImed")),
+    # Hmed2018 muscles: T pulse-intensity controls per muscle, intensity parameters and sliding-window rows (the
+    # reference's tests/shard2/test_fes_dynamics.py:104-183 shape; truncation 10 and 20 kernel families)
+    "hmed_f_rk4_residual": MC.cfg5(model="hmed2018_with_fatigue", residual=True, m=2),
+    "hmed_rk1_t20": MC.cfg5(model="hmed2018", fatigue=False, scheme="RK1", m=3, truncation=20),
+    "hmed_biceps_1dof_rk2": MC.cfg5(biomod="arm26_biceps_1dof", muscles=("BIClong",), model="hmed2018_with_fatigue",
+                                    scheme="RK2", m=2),
 }
+
+
+def _ngk(pb):
+    return pb.ng // pb.n_shooting
 
 
 def _dense_blocks(pb, jr, jc, jv, k):
     """Interval k's dPhi/dz block (nx x nz) and its -1 block from the product's triplets."""
-    nx, nz = pb.nx, pb.nz
+    nx, nz, ngk = pb.nx, pb.nz, _ngk(pb)
     D = np.zeros((nx, nz))
     neg = np.zeros((nx, nx))
     for r, c, v in zip(jr, jc, jv):
+        r = r - k * ngk + k * nx  # continuity rows of interval k -> k nx .. k nx + nx - 1
         if k * nx <= r < (k + 1) * nx:
             if k * nz <= c < (k + 1) * nz:
                 D[r - k * nx, c - k * nz] = v
@@ -58,10 +69,12 @@ def test_msk_g_and_jacobian_match_oracle(case):
     jac = h.eval_jac_g(V)
     jr, jc = h.jac_structure()
     h.close()
+    ngk = _ngk(pb)
     for b in range(B):
         ref_g = M.eval_g(pb, V[b])
-        phi = np.abs(ref_g) + np.abs(np.concatenate([V[b][(k + 1) * pb.nz:(k + 1) * pb.nz + pb.nx]
-                                                     for k in range(pb.n_shooting)]))
+        nxt = np.concatenate([np.concatenate([V[b][(k + 1) * pb.nz:(k + 1) * pb.nz + pb.nx], np.full(ngk - pb.nx, 130.0)])
+                              for k in range(pb.n_shooting)])
+        phi = np.abs(ref_g) + np.abs(nxt)
         assert np.max(np.abs(g[b] - ref_g) / (phi + 1e-12)) < 1e-10
         for k in (0, 4, pb.n_shooting - 1) if b == 0 else (b + 2,):
             ref = M.continuity_jacobian(pb, V[b], k)
@@ -69,6 +82,19 @@ def test_msk_g_and_jacobian_match_oracle(case):
             np.testing.assert_array_equal(neg, -np.eye(pb.nx))
             scale = np.abs(ref) + 1e-9 * np.max(np.abs(ref), axis=1, keepdims=True)
             assert np.max(np.abs(D - ref) / scale) < 1e-9, (case, b, k)
+    if pb.n_slide:  # sliding-window rows are linear: their Jacobian is the difference quotient, exactly
+        ngk, k = _ngk(pb), 3
+        dense = np.zeros((pb.n_slide, pb.nv))
+        for r, c, val in zip(jr, jc, jac[0]):
+            if k * ngk + pb.nx <= r < (k + 1) * ngk:
+                dense[r - k * ngk - pb.nx, c] += val
+        ref = np.zeros_like(dense)
+        base = M.sliding_rows(pb, V[0], k)
+        for c in range(pb.nv):
+            vv = V[0].copy()
+            vv[c] += 1.0
+            ref[:, c] = M.sliding_rows(pb, vv, k) - base
+        np.testing.assert_allclose(dense, ref, atol=1e-12)
 
 
 @pytest.mark.parametrize("case", ["cfg5_d07f_rk4", "d07_rk1_residual"])
@@ -129,7 +155,7 @@ def test_msk_hessian_matches_oracle(case):
     assert np.all(h0 == 0.0)
     nz, nx = pb.nz, pb.nx
     for b, k in ((0, 1), (B - 1, pb.n_shooting - 1)):
-        ref = _lagrangian_block_fd(pb, V[b], lam[b, k * nx:(k + 1) * nx], k)
+        ref = _lagrangian_block_fd(pb, V[b], lam[b, k * _ngk(pb):k * _ngk(pb) + nx], k)
         got = np.zeros((nz, nz))
         for r, c, val in zip(hr, hc, hv[b]):
             if k * nz <= r < (k + 1) * nz and k * nz <= c < (k + 1) * nz:
@@ -265,3 +291,32 @@ def test_msk_small_and_large_batch_paths_agree(case):
     for a, b_ in zip(out[2], out[Bl]):
         scale = np.abs(a) + 1e-9 * np.abs(a).max()
         assert np.max(np.abs(a - b_) / scale) < 1e-12
+
+
+def test_msk_hmed_interior_point_converges():
+    """The reference's Hmed MSK case (tests/shard2/test_fes_dynamics.py:104-183: arm26 biceps / triceps, Hmed2018 with
+    fatigue, residual torque minimised, elbow 5 -> 120 deg, intensities in [I_min, 130]) at RK4 x 5 (RK4 x 1 is unstable
+    for the calcium ODE at 0.1 s, see the cfg-5 test above), solved by the native interior point: converged, and the
+    optimum is feasible for the oracle (continuity and sliding-window rows ~ 0), intensities within their bounds.
+    The reference's golden values were produced by a pre-refactor API (pulse intensities as parameters only) and do
+    not apply (parity unpinned)."""
+    from cocofest_amd.solver import IpmOptions, NativeIpm
+
+    cfg = MC.cfg5(model="hmed2018_with_fatigue", residual=True, m=5, qdot_end=False, fatigue=False, bound=(5, 120))
+    ocp = MC.product_ocp(**cfg)
+    pb = MC.oracle_problem(**cfg)
+    nat = NativeIpm(ocp, batch=1, options=IpmOptions(tol=1e-6, max_iter=1500))
+    res = nat.solve()
+    nat.close()
+    print("iterations", res.iterations, "f", res.f, "stats", nat.last_stats)
+    assert bool(res.converged[0])
+    v = res.v[0]
+    g = M.eval_g(pb, v)
+    assert np.max(np.abs(g)) < 1e-5, np.max(np.abs(g))
+    states, controls, params = ocp.unpack(v)
+    q_elbow = states[f"q_{ocp.model.name_dof[1]}"][0]
+    assert abs(q_elbow[0] - 3.14 / 36) < 1e-9 and abs(q_elbow[-1] - 3.14 / 1.5) < 1e-9
+    imin = ocp.model.muscles_dynamics_model[0].min_pulse_intensity()
+    for name in ("pulse_intensity_BIClong", "pulse_intensity_TRIlong"):
+        p = params[name][0]
+        assert p.shape == (10,) and np.all(p >= imin - 1e-9) and np.all(p <= 130 + 1e-9)
