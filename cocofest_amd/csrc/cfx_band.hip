@@ -707,11 +707,16 @@ __global__ void __launch_bounds__(64) k_band_solve_reg_multi(int n, int kl, int 
 // ---------------------------------------------------------------------------------------------------
 // dispatch
 // ---------------------------------------------------------------------------------------------------
+// Raise a kernel's dynamic-LDS limit above 64 KiB only when a launch needs more than it was last raised to (one
+// attribute call per kernel and size, not one per launch).
 template <class K>
 static hipError_t allow_lds(K kernel, size_t bytes) {
-    if (bytes <= 65536) return hipSuccess;
-    return hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
-                               (int)bytes);
+    static size_t raised = 65536;  // one per kernel instantiation (K is the kernel's type; one address per type here)
+    if (bytes <= raised) return hipSuccess;
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kernel),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+    if (e == hipSuccess) raised = bytes;
+    return e;
 }
 
 template <int NT>

@@ -433,10 +433,11 @@ def test_band_lu_matches_dense_solve(n, kl, ku, zero_diag):
     np.testing.assert_array_equal(x2.cpu().numpy(), x.cpu().numpy()[:, :1])
 
 
-@pytest.mark.parametrize("B,n,kl,ku", [(3, 300, 6, 6), (200, 300, 6, 6), (150, 300, 40, 40), (140, 200, 70, 2)])
+@pytest.mark.parametrize("B,n,kl,ku", [(3, 300, 6, 6), (200, 300, 6, 6), (150, 300, 40, 40), (140, 200, 70, 2),
+                                      (3, 106, 42, 42), (1, 298, 42, 42), (5, 70, 30, 10)])
 def test_band_lu_small_and_windowed_paths_agree(B, n, kl, ku, monkeypatch):
-    """The resident / global kernels (small batches, or CFX_BAND_FULL) and the windowed kernels give the same
-    factors, pivots and solutions to rounding — 64-thread and 1024-thread workgroups."""
+    """The resident / global kernels (small batches, or CFX_BAND_FULL) and the register / windowed kernels give the
+    same factors, pivots and solutions to rounding (the MSK KKT shapes kl = ku = 42 included)."""
     import torch
 
     from cocofest_amd import _cfx
