@@ -11,7 +11,7 @@ ROOT = pathlib.Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT))
 
 import bench  # noqa: E402
-from cocofest_amd.solver import BatchedIpm, IpmOptions  # noqa: E402
+from cocofest_amd.solver import BatchedIpm, IpmOptions, NativeIpm  # noqa: E402
 
 ocp = bench.msk_build(5)
 for B, amp in (() if "--hess-only" in sys.argv else ((64, 0.1), (64, 0.3), (512, 0.1))):
@@ -21,10 +21,11 @@ for B, amp in (() if "--hess-only" in sys.argv else ((64, 0.1), (64, 0.3), (512,
     free = lb != ub
     span = np.minimum(np.where(np.isfinite(ub - lb), ub - lb, 10.0), 10.0)[free]
     v0[:, free] = np.clip(v0[:, free] + amp * rng.uniform(-1, 1, (B, free.sum())) * span, lb[free], ub[free])
-    ipm = BatchedIpm(ocp, batch=B, options=IpmOptions(tol=1e-6, max_iter=1000))
+    cls = NativeIpm if "--native" in sys.argv else BatchedIpm
+    ipm = cls(ocp, batch=B, options=IpmOptions(tol=1e-6, max_iter=1000))
     res = ipm.solve(v0)
     ipm.close()
-    print(f"B={B} amp={amp}: wall {res.wall_time:.2f} s, converged {int(res.converged.sum())}/{B}, iterations "
+    print(f"{cls.__name__} B={B} amp={amp}: wall {res.wall_time:.2f} s, converged {int(res.converged.sum())}/{B}, iterations "
           f"median {np.median(res.iterations):.0f} max {res.iterations.max()}, f median {np.median(res.f):.4f} "
           f"min {res.f.min():.4f}", flush=True)
 
