@@ -119,7 +119,7 @@ __global__ void __launch_bounds__(256) k_colloc(const KParams P, const double* _
                 double poly = 0.0;
 #pragma unroll UN
                 for (int i = 0; i <= d; ++i) poly = fma(P.colC[i][j], X(i, r), poly);
-                G[(go + (j - 1) * NX + r) * B + b] = fma(-P.dt, f[r], poly);
+                st_nt(G + (go + (j - 1) * NX + r) * B + b, fma(-P.dt, f[r], poly));
             }
         }
         if (J) {
@@ -129,21 +129,21 @@ __global__ void __launch_bounds__(256) k_colloc(const KParams P, const double* _
                 const double diag = r == 0 ? -P.inv_tauc : fd[r][r];
 #pragma unroll UN
                 for (int i = 0; i <= d; ++i)
-                    J[(o + i) * B + b] = i == j ? fma(-P.dt, diag, P.colC[i][j]) : P.colC[i][j];
+                    st_nt(J + (o + i) * B + b, i == j ? fma(-P.dt, diag, P.colC[i][j]) : P.colC[i][j]);
                 o += d + 1;
 #pragma unroll
                 for (int c = 0; c < NX; ++c)
-                    if (c != r && (col_xdeps(MODEL, r) >> c & 1u)) J[(o++) * B + b] = -P.dt * fd[r][c];
+                    if (c != r && (col_xdeps(MODEL, r) >> c & 1u)) st_nt(J + (o++) * B + b, -P.dt * fd[r][c]);
                 if constexpr (HM) {
                     if (r == 0) {
 #pragma unroll
                         for (int i = 0; i < TMAX; ++i)  // register-resident lamd: no dynamic indexing
-                            if (i < P.T) J[(o + i) * B + b] = -P.dt * P.inv_tauc * coef[i] * lamd[i];
+                            if (i < P.T) st_nt(J + (o + i) * B + b, -P.dt * P.inv_tauc * coef[i] * lamd[i]);
                         o += P.T;
                     }
                 }
                 if constexpr (PW) {
-                    if (r == 1) J[(o++) * B + b] = -P.dt * fd[1][NX];
+                    if (r == 1) st_nt(J + (o++) * B + b, -P.dt * fd[1][NX]);
                 }
             }
         }
@@ -155,13 +155,13 @@ __global__ void __launch_bounds__(256) k_colloc(const KParams P, const double* _
             double e = 0.0;
 #pragma unroll UN
             for (int i = 0; i <= d; ++i) e = fma(P.colD[i], X(i, r), e);
-            G[(go + d * NX + r) * B + b] = e - xn[r];
+            st_nt(G + (go + d * NX + r) * B + b, e - xn[r]);
         }
         if (J) {
             const int64_t o = jo + (int64_t)d * sumrow + (int64_t)r * (d + 2);
 #pragma unroll UN
-            for (int i = 0; i <= d; ++i) J[(o + i) * B + b] = P.colD[i];
-            J[(o + d + 1) * B + b] = -1.0;
+            for (int i = 0; i <= d; ++i) st_nt(J + (o + i) * B + b, P.colD[i]);
+            st_nt(J + (o + d + 1) * B + b, -1.0);
         }
     }
 }

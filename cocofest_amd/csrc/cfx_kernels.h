@@ -381,13 +381,30 @@ CFX_HD void ld_lane(const double* p, double (&o)[NI]) {
         }
     }
 }
+// Output stores are non-temporal (`global_store … nt`): the callback outputs are a write stream far larger than the
+// 256 MiB Infinity Cache.  cfg 2, B = 2^20: 0.315 -> 0.287 ms together with the shorter interval chunks of
+// cfx_create (scripts/store_probe.py, profiles/round2/store_probe.jsonl).  The lines stay in the XCD's L2 (a
+// consumer launched next still hits there).
+CFX_HD void st_nt(double* p, double v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    __builtin_nontemporal_store(v, p);
+#else
+    *p = v;
+#endif
+}
 template <int NI>
 CFX_HD void st_lane(double* p, const double (&v)[NI]) {
     if constexpr (NI == 1) {
-        p[0] = v[0];
+        st_nt(p, v[0]);
     } else {
+#if defined(__HIP_DEVICE_COMPILE__)
+        typedef double nt2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+        for (int i = 0; i < NI; i += 2) __builtin_nontemporal_store(nt2{v[i], v[i + 1]}, reinterpret_cast<nt2*>(p + i));
+#else
 #pragma unroll
         for (int i = 0; i < NI; i += 2) *reinterpret_cast<double2*>(p + i) = make_double2(v[i], v[i + 1]);
+#endif
     }
 }
 template <int NI>

@@ -4,7 +4,10 @@
 //   tiled  : 64-instance tiles ((b/64)*E + e)*64 + b%64, 8 B per lane
 //   soa2   : SoA, 2 adjacent instances per lane (16 B per lane)
 //   soa2nt : soa2 with nontemporal stores
-//   wstream/rstream: pure write / read streaming of the same byte count (reference ceilings)
+//   tiled2nt<KPT>: 64-instance tiles, 2 adjacent instances per lane, nontemporal stores, KPT intervals per thread
+//            with the interval chunks as the fast grid index (the round-2 launch shape of k_shooting)
+//   wstream/rstream: pure write / read streaming of the same byte count (reference ceilings); wstreamnt: 16-B
+//            nontemporal stores
 #include <hip/hip_runtime.h>
 #include <cstdio>
 
@@ -61,9 +64,37 @@ __global__ void __launch_bounds__(256) k2(const double* __restrict__ V, double* 
     }
 }
 
+template <int KPT>
+__global__ void __launch_bounds__(256) k3(const double* __restrict__ V, double* __restrict__ G, double* __restrict__ J,
+                                          int64_t B) {
+    const int64_t b = ((int64_t)blockIdx.y * 256 + threadIdx.x) * 2;
+    if (b >= B) return;
+    const int k0 = blockIdx.x * KPT;
+    typedef double nt2 __attribute__((ext_vector_type(2)));
+    auto ld = [&](int E, int e) { return *reinterpret_cast<const nt2*>(V + idx<true>(B, E, e, b)); };
+    auto st = [&](double* P, int E, int e, nt2 v) {
+        __builtin_nontemporal_store(v, reinterpret_cast<nt2*>(P + idx<true>(B, E, e, b)));
+    };
+    nt2 x0 = ld(EV, k0 * NZ), x1 = ld(EV, k0 * NZ + 1);
+    for (int kk = k0; kk < k0 + KPT; ++kk) {
+        const nt2 n0 = ld(EV, (kk + 1) * NZ), n1 = ld(EV, (kk + 1) * NZ + 1);
+        st(G, EG, kk * 2, x0 - n0);
+        st(G, EG, kk * 2 + 1, x1 - n1);
+#pragma unroll
+        for (int q = 0; q < 5; ++q) st(J, EJ, kk * 5 + q, x0 * (double)q + x1);
+        x0 = n0;
+        x1 = n1;
+    }
+}
+
 __global__ void kw(double4* __restrict__ out, int64_t n) {
     for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
         out[i] = make_double4(1.0, 2.0, 3.0, (double)i);
+}
+__global__ void kwnt(double* __restrict__ out, int64_t n) {
+    typedef double nt2 __attribute__((ext_vector_type(2)));
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+        __builtin_nontemporal_store(nt2{1.0, (double)i}, reinterpret_cast<nt2*>(out) + i);
 }
 __global__ void kr(const double2* __restrict__ in, double* out, int64_t n) {
     double s = 0;
@@ -79,7 +110,7 @@ void timeit(const char* name, double bytes, F launch) {
     (void)hipEventCreate(&e0);
     (void)hipEventCreate(&e1);
     (void)hipEventRecord(e0);
-    const int reps = 40;
+    const int reps = 200;
     for (int r = 0; r < reps; ++r) launch();
     (void)hipEventRecord(e1);
     (void)hipEventSynchronize(e1);
@@ -105,6 +136,9 @@ int main() {
         timeit("tiled", bytes, [&] { hipLaunchKernelGGL((k1<true>), dim3(B / 256), dim3(256), 0, 0, V, G, J, B); });
         timeit("soa2", bytes, [&] { hipLaunchKernelGGL((k2<false>), dim3(B / 512), dim3(256), 0, 0, V, G, J, B); });
         timeit("soa2nt", bytes, [&] { hipLaunchKernelGGL((k2<true>), dim3(B / 512), dim3(256), 0, 0, V, G, J, B); });
+        timeit("t2nt k4", bytes, [&] { hipLaunchKernelGGL((k3<4>), dim3(N / 4, B / 512), dim3(256), 0, 0, V, G, J, B); });
+        timeit("t2nt k20", bytes, [&] { hipLaunchKernelGGL((k3<20>), dim3(1, B / 512), dim3(256), 0, 0, V, G, J, B); });
+        timeit("wstrnt", sbytes, [&] { hipLaunchKernelGGL(kwnt, dim3(8192), dim3(256), 0, 0, S, (int64_t)(sbytes / 16)); });
         timeit("wstream", sbytes, [&] { hipLaunchKernelGGL(kw, dim3(8192), dim3(256), 0, 0, (double4*)S, (int64_t)(sbytes / 32)); });
         timeit("rstream", sbytes, [&] { hipLaunchKernelGGL(kr, dim3(8192), dim3(256), 0, 0, (const double2*)S, G, (int64_t)(sbytes / 16)); });
     }
