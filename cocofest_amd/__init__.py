@@ -23,7 +23,7 @@ from .fourier import FourierSeries
 from .ivp import IvpFes
 from .msk import FesMskModel, FesMskOcp, OcpFesMsk
 from .nmpc import FesNmpc, NmpcFesMsk, NmpcResult
-from .ocp import FesOcp, Node, Objective, ObjectiveFcn, ObjectiveList, OcpFes
+from .ocp import Axis, Constraint, ConstraintFcn, ConstraintList, FesOcp, Node, Objective, ObjectiveFcn, ObjectiveList, OcpFes
 from .ode_solver import ControlType, OdeSolver
 from .solver import BatchedIpm, IpmOptions, IpmResult
 
@@ -31,6 +31,6 @@ __all__ = [
     "CfxError", "Handle", "load_library", "DingModelFrequency", "DingModelFrequencyWithFatigue",
     "DingModelPulseIntensityFrequency", "DingModelPulseIntensityFrequencyWithFatigue",
     "DingModelPulseWidthFrequency", "DingModelPulseWidthFrequencyWithFatigue", "FesModel", "ModelMaker",
-    "FourierSeries", "IvpFes", "FesOcp", "Node", "Objective", "ObjectiveFcn", "ObjectiveList", "OcpFes",
+    "FourierSeries", "IvpFes", "FesOcp", "Axis", "Constraint", "ConstraintFcn", "ConstraintList", "Node", "Objective", "ObjectiveFcn", "ObjectiveList", "OcpFes",
     "ControlType", "OdeSolver", "FesMskModel", "FesMskOcp", "OcpFesMsk", "FesNmpc", "NmpcFesMsk", "NmpcResult", "BatchedIpm", "IpmOptions", "IpmResult",
 ]

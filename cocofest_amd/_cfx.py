@@ -15,7 +15,7 @@ import numpy as np
 
 LIB_PATH = pathlib.Path(__file__).with_name("libcfx.so")
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 OK, EINVAL, EHIP, ENOMEM, EUNSUPPORTED, ENODEV = 0, -1, -2, -3, -4, -5
 MODEL_IDS = {
     "ding2003": 0,
@@ -74,6 +74,10 @@ class MskMuscle(C.Structure):
                 ("optimal_length", C.c_double), ("tendon_slack_length", C.c_double), ("pennation_angle", C.c_double)]
 
 
+class MskMarkerPair(C.Structure):
+    _fields_ = [("node", C.c_int32), ("axes", C.c_int32), ("frame", C.c_int32 * 2), ("pos", (C.c_double * 3) * 2)]
+
+
 class MskProblem(C.Structure):
     _fields_ = [
         ("abi_version", C.c_int32), ("scheme", C.c_int32), ("n_steps", C.c_int32), ("n_shooting", C.c_int32),
@@ -84,6 +88,7 @@ class MskProblem(C.Structure):
         ("muscles", C.POINTER(MskMuscle)), ("flags", C.c_uint32), ("n_objectives", C.c_int32),
         ("objectives", C.POINTER(Objective)), ("device", C.c_int32), ("n_params", C.c_int32),
         ("last_stim_idx", C.POINTER(C.c_int32)), ("param_offset", C.POINTER(C.c_int32)),
+        ("n_marker_pairs", C.c_int32), ("marker_pairs", C.POINTER(MskMarkerPair)),
     ]
 
 
@@ -450,11 +455,12 @@ class MskHandle(Handle):
 
     ``chain``: dict with ``axis`` (nq,), ``frame`` (nq, 12), ``gravity`` (3,), ``mass`` (nq,), ``com`` (nq, 3),
     ``inertia`` (nq, 9); ``muscles``: list of dicts with ``model_id``, ``constants``, ``point_frame``,
-    ``point_pos`` (n, 3), ``optimal_length``, ``tendon_slack_length``, ``pennation_angle``."""
+    ``point_pos`` (n, 3), ``optimal_length``, ``tendon_slack_length``, ``pennation_angle``; ``marker_pairs``: dicts
+    ``node``, ``axes`` (bit mask), ``frame`` (2,), ``pos`` (2, 3) (cfx_msk_marker_pair)."""
 
     def __init__(self, *, chain, muscles, scheme, n_steps, n_shooting, truncation, final_time, stim_rows, batch,
                  flags=0, layout=LAYOUT_SOA, objectives=(), device=0, n_params=0, last_stim_idx=None,
-                 param_offset=None):
+                 param_offset=None, marker_pairs=()):
         self.lib = load_library()
         self._keep = []
 
@@ -498,6 +504,16 @@ class MskHandle(Handle):
         if n_params:
             pb.last_stim_idx = arr(last_stim_idx, np.int32)
             pb.param_offset = arr(param_offset, np.int32)
+        if marker_pairs:
+            mk = (MskMarkerPair * len(marker_pairs))()
+            for i, c in enumerate(marker_pairs):
+                mk[i].node, mk[i].axes = int(c["node"]), int(c["axes"])
+                for j in range(2):
+                    mk[i].frame[j] = int(c["frame"][j])
+                    for e in range(3):
+                        mk[i].pos[j][e] = float(c["pos"][j][e])
+            self._keep.append(mk)
+            pb.n_marker_pairs, pb.marker_pairs = len(marker_pairs), mk
         h = C.c_void_p()
         rc = self.lib.cfx_msk_create(C.byref(pb), C.byref(h))
         self._attach(rc, h, batch, layout, n_shooting, n_steps, device)

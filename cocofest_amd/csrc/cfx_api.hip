@@ -68,6 +68,8 @@ struct cfx_handle {
     MskObjective* d_mobj = nullptr;
     double* d_msk_imin = nullptr;  // Hmed: I_min per muscle (sliding-window padding)
     int msk_ns = 0;                // Hmed: sliding-window rows per interval (0: none)
+    MskMarker* d_mk = nullptr;     // marker superimpositions (cfx_msk_marker_pair)
+    int n_mk = 0;
     DevBuf main[S_COUNT], stage[S_COUNT];
     std::string err;
 };
@@ -775,7 +777,7 @@ extern "C" void cfx_destroy(cfx_handle* h) {
     }
     for (void* p : {(void*)h->d_tab, (void*)h->d_rest, (void*)h->d_cna, (void*)h->d_htasks, (void*)h->d_obj,
                     (void*)h->d_targets, (void*)h->d_sl_param, (void*)h->d_sl_joff, (void*)h->d_hdiag,
-                    (void*)h->d_geom, (void*)h->d_mobj, (void*)h->d_msk_imin})
+                    (void*)h->d_geom, (void*)h->d_mobj, (void*)h->d_msk_imin, (void*)h->d_mk})
         if (p) (void)hipFree(p);
     if (h->own_stream) (void)hipStreamDestroy(h->own_stream);
     delete h;
@@ -1012,6 +1014,16 @@ extern "C" int cfx_msk_create(const cfx_msk_problem* p, cfx_handle** out) {
     }
     for (int j = 0; j < nq; ++j)
         if (p->dof_axis[j] < 0 || p->dof_axis[j] > 2) return bad("dof_axis must be 0, 1 or 2");
+    if (p->n_marker_pairs < 0 || (p->n_marker_pairs > 0 && !p->marker_pairs))
+        return bad("n_marker_pairs < 0, or marker_pairs is NULL");
+    for (int i = 0; i < p->n_marker_pairs; ++i) {
+        const cfx_msk_marker_pair& c = p->marker_pairs[i];
+        if (c.node < 0 || c.node > p->n_shooting) return bad("marker pair node out of [0, n_shooting]");
+        if (c.axes < 1 || c.axes > 7) return bad("marker pair axes must select X, Y and / or Z (bits 1, 2, 4)");
+        for (int e = 0; e < 2; ++e)
+            if (c.frame[e] < -1 || c.frame[e] >= nq) return bad("marker frame out of range");
+        if (c.frame[0] < 0 && c.frame[1] < 0) return bad("marker pair: both markers are fixed to the ground");
+    }
     if (!msk_supported(nq, nm, fam, p->scheme))
         return create_fail(nullptr, CFX_EUNSUPPORTED,
                            "cfx_msk_create: shape (n_dof " + std::to_string(nq) + ", muscles " + std::to_string(nm) +
@@ -1194,7 +1206,33 @@ extern "C" int cfx_msk_create(const cfx_msk_problem* p, cfx_handle** out) {
                 }
             }
     }
-    // ---- Hessian: dense lower triangle of every interval block, then the diagonal of x_N
+    // marker superimposition rows after every interval's rows: nd J_g entries per row on q_node (dof order)
+    const int qoff = nm * nxm;
+    std::vector<MskMarker> mks(p->n_marker_pairs);
+    int64_t mrow = (int64_t)N * ngk;
+    for (int i = 0; i < p->n_marker_pairs; ++i) {
+        const cfx_msk_marker_pair& c = p->marker_pairs[i];
+        MskMarker& d = mks[i];
+        std::memset(&d, 0, sizeof(d));
+        d.node = c.node;
+        for (int a = 0; a < 3; ++a)
+            if (c.axes >> a & 1) d.axis[d.nrow++] = a;
+        d.nd = std::max(c.frame[0], c.frame[1]) + 1;
+        d.row0 = (int32_t)mrow;
+        d.jo = (int32_t)h->jrow.size();
+        for (int e = 0; e < 2; ++e) {
+            d.frame[e] = c.frame[e];
+            for (int a = 0; a < 3; ++a) d.pos[e][a] = c.pos[e][a];
+        }
+        for (int r = 0; r < d.nrow; ++r)
+            for (int j = 0; j < d.nd; ++j) {
+                h->jrow.push_back((int32_t)(mrow + r));
+                h->jcol.push_back(c.node * nz + qoff + j);
+            }
+        mrow += d.nrow;
+    }
+    // ---- Hessian: dense lower triangle of every interval block, then the diagonal of x_N (and, for marker pairs at
+    // node N, the q_N pairs off the diagonal)
     const int nhk = nz * (nz + 1) / 2;
     P.nhk = nhk;
     for (int k = 0; k < N; ++k)
@@ -1206,6 +1244,29 @@ extern "C" int cfx_msk_create(const cfx_msk_problem* p, cfx_handle** out) {
     for (int r = 0; r < nx; ++r) {
         h->hrow.push_back(N * nz + r);
         h->hcol.push_back(N * nz + r);
+    }
+    {
+        int ndN = 0;  // q_N pairs (i > j) needed by pairs at node N
+        for (const MskMarker& d : mks)
+            if (d.node == N) ndN = std::max(ndN, d.nd);
+        std::vector<int32_t> offN((size_t)kMskMaxQ * kMskMaxQ, -1);
+        for (int i = 0; i < ndN; ++i)
+            for (int j = 0; j < i; ++j) {
+                offN[i * kMskMaxQ + j] = (int32_t)h->hrow.size();
+                h->hrow.push_back(N * nz + qoff + i);
+                h->hcol.push_back(N * nz + qoff + j);
+            }
+        for (MskMarker& d : mks)
+            for (int i = 0; i < kMskMaxQ; ++i)
+                for (int j = 0; j <= i; ++j) {
+                    int32_t& o = d.hoff[i * (i + 1) / 2 + j];
+                    o = -1;
+                    if (i >= d.nd) continue;
+                    if (d.node < N)
+                        o = d.node * nhk + (qoff + i) * (qoff + i + 1) / 2 + qoff + j;
+                    else
+                        o = i == j ? N * nhk + qoff + i : offN[i * kMskMaxQ + j];
+                }
     }
     std::vector<int32_t> hdiag((size_t)(N + 1) * nz, -1);
     for (int k = 0; k < N; ++k)
@@ -1267,11 +1328,12 @@ extern "C" int cfx_msk_create(const cfx_msk_problem* p, cfx_handle** out) {
     }
     h->n_obj = (int)mobj.size();
     h->sz.nv = (int64_t)N * nz + nx + (ns ? p->n_params : 0);
-    h->sz.ng = (int64_t)N * ngk;
+    h->sz.ng = mrow;
     h->sz.nnz_jac = (int64_t)h->jrow.size();
     h->sz.nnz_hess = (int64_t)h->hrow.size();
     h->sz.nx = nx;
     h->sz.nu = nu;
+    h->n_mk = (int)mks.size();
 
     if (hipSetDevice(h->device) != hipSuccess) return create_fail(h, CFX_EHIP, "cfx_msk_create: hipSetDevice failed");
     if (hipStreamCreateWithFlags(&h->own_stream, hipStreamNonBlocking) != hipSuccess)
@@ -1291,12 +1353,29 @@ extern "C" int cfx_msk_create(const cfx_msk_problem* p, cfx_handle** out) {
         !upload((void**)&h->d_hdiag, hdiag.data(), hdiag.size() * sizeof(int32_t)) ||
         !upload((void**)&h->d_sl_param, sl_param.data(), sl_param.size() * sizeof(int32_t)) ||
         !upload((void**)&h->d_sl_joff, sl_joff.data(), sl_joff.size() * sizeof(int32_t)) ||
-        !upload((void**)&h->d_msk_imin, imin.data(), imin.size() * sizeof(double)))
+        !upload((void**)&h->d_msk_imin, imin.data(), imin.size() * sizeof(double)) ||
+        !upload((void**)&h->d_mk, mks.data(), mks.size() * sizeof(MskMarker)))
         return create_fail(h, CFX_ENOMEM, "cfx_msk_create: device allocation/upload failed");
     P.cs = h->d_tab;
     P.rest = h->d_rest;
     *out = h;
     return CFX_OK;
+}
+
+// marker superimposition rows / their Hessian terms (k_msk_markers, one thread per instance)
+static hipError_t launch_msk_markers(cfx_handle* h, const double* V, double* G, double* J, const double* LAM,
+                                     double* H) {
+    if (!h->n_mk) return hipSuccess;
+    const MskParams& P = h->mp;
+    const dim3 grid((unsigned)((P.B + 255) / 256)), blk(256);
+    const int qoff = P.nx - 2 * h->msk_nq;  // q follows the muscle blocks
+    switch (h->msk_nq) {
+        case 1: hipLaunchKernelGGL(k_msk_markers<1>, grid, blk, 0, h->stream, P, h->d_geom, h->n_mk, h->d_mk, qoff, V, G, J, LAM, H); break;
+        case 2: hipLaunchKernelGGL(k_msk_markers<2>, grid, blk, 0, h->stream, P, h->d_geom, h->n_mk, h->d_mk, qoff, V, G, J, LAM, H); break;
+        case 3: hipLaunchKernelGGL(k_msk_markers<3>, grid, blk, 0, h->stream, P, h->d_geom, h->n_mk, h->d_mk, qoff, V, G, J, LAM, H); break;
+        default: hipLaunchKernelGGL(k_msk_markers<4>, grid, blk, 0, h->stream, P, h->d_geom, h->n_mk, h->d_mk, qoff, V, G, J, LAM, H); break;
+    }
+    return hipGetLastError();
 }
 
 static int msk_eval_all(cfx_handle* h, const double* v, double* g, double* jac, double* f, double* grad,
@@ -1328,6 +1407,7 @@ static int msk_eval_all(cfx_handle* h, const double* v, double* g, double* jac, 
                                h->msk_ns, (const int32_t*)h->d_sl_param, (const int32_t*)h->d_sl_joff,
                                (const double*)h->d_msk_imin, (int64_t)P.N * P.nz + P.nx, V, G, J);
         }
+        CFX_HIP(h, launch_msk_markers(h, V, G, J, nullptr, nullptr));
         if (J) {
             h->stash_valid = h->msk_stash;
             h->stash_v = v;
@@ -1376,6 +1456,7 @@ static int msk_eval_h(cfx_handle* h, const double* v, const double* obj_factor, 
         hipLaunchKernelGGL(k_msk_objective, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, h->stream, h->mp,
                            h->n_obj, h->d_mobj, h->d_targets, V, (double*)nullptr, (double*)nullptr, OF, H,
                            (const int32_t*)h->d_hdiag);
+    CFX_HIP(h, launch_msk_markers(h, V, nullptr, nullptr, LAM, H));
     CFX_HIP(h, hipGetLastError());
     if ((rc = finish_out(h, S_OUT, H, hess, h->sz.nnz_hess, flags)) != CFX_OK) return rc;
     return sync_if_host(h, flags);

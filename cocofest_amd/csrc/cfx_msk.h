@@ -1663,6 +1663,89 @@ static __global__ void __launch_bounds__(256) k_msk_slide(const MskParams P, int
     }
 }
 
+// ---- marker superimposition rows (bioptim ConstraintFcn.SUPERIMPOSE_MARKERS, cfx_msk_marker_pair) ------------
+// Row r of a pair: world axis axis[r] of marker(second) - marker(first) at q_node.  A marker fixed in dof frame f
+// moves with q_0 .. q_f, so a pair depends on its first nd = max(frame) + 1 dofs: nd J_g entries per row (dof order,
+// from jo), and the Hessian entries of the q_node pairs (i, j <= i < nd) at hoff (packed as Jet<NQ>::h).
+struct MskMarker {
+    int32_t node, nrow, nd, row0, jo;
+    int32_t axis[3];
+    int32_t frame[2];
+    int32_t hoff[kMskMaxQ * (kMskMaxQ + 1) / 2];
+    double pos[2][3];
+};
+
+template <int NQ, class S>
+MSK_HD void msk_marker_diff(const MskGeom& G, const MskMarker& c, const S* q, S* d) {
+    S R[NQ][9], o[NQ][3], z[NQ][3];
+    msk_frames<NQ>(G, q, R, o, z);
+    S P0[3], P1[3], dP[NQ][3];
+    msk_point<NQ>(R, o, z, c.frame[0], c.pos[0], P0, dP);
+    msk_point<NQ>(R, o, z, c.frame[1], c.pos[1], P1, dP);
+#pragma unroll
+    for (int a = 0; a < 3; ++a) d[a] = P1[a] - P0[a];
+}
+template <class S>
+MSK_HD const S& msk_axis(const S* d, int a) {  // wave-uniform a: a select, not a dynamically indexed array
+    return a == 0 ? d[0] : a == 1 ? d[1] : d[2];
+}
+
+// thread = instance, every pair in order (a few rows each; one thread per instance keeps the += of pairs that share
+// a node race-free).  LAM == nullptr: the rows into Gout (nullable) and their J_g values into J (nullable);
+// otherwise sum_r lambda_r d^2 row_r / dq^2 is added to H (after the dynamics' Hessian launch, same stream).
+template <int NQ>
+__global__ void __launch_bounds__(256) k_msk_markers(const MskParams P, const MskGeom* __restrict__ GG, int n,
+                                                     const MskMarker* __restrict__ mk, int qoff,
+                                                     const double* __restrict__ V, double* __restrict__ Gout,
+                                                     double* __restrict__ J, const double* __restrict__ LAM,
+                                                     double* __restrict__ H) {
+    const int64_t B = P.B;
+    const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= B) return;
+    const MskGeom& G = *GG;
+    for (int i = 0; i < n; ++i) {
+        const MskMarker& c = mk[i];
+        const int64_t qb = (int64_t)c.node * P.nz + qoff;
+        if (LAM) {
+            Jet<NQ> q[NQ], d[3];
+#pragma unroll
+            for (int j = 0; j < NQ; ++j) {
+                q[j] = jconst<NQ>(V[(qb + j) * B + b]);
+                q[j].g[j] = 1.0;
+            }
+            msk_marker_diff<NQ>(G, c, q, d);
+            for (int r = 0; r < c.nrow; ++r) {
+                const double lam = LAM[(int64_t)(c.row0 + r) * B + b];
+                const Jet<NQ>& e = msk_axis(d, c.axis[r]);
+#pragma unroll
+                for (int t = 0; t < Jet<NQ>::H; ++t)
+                    if (c.hoff[t] >= 0) H[(int64_t)c.hoff[t] * B + b] += lam * e.h[t];
+            }
+        } else if (J) {
+            Dual<NQ> q[NQ], d[3];
+#pragma unroll
+            for (int j = 0; j < NQ; ++j) {
+                q[j] = dconst<NQ>(V[(qb + j) * B + b]);
+                q[j].d[j] = 1.0;
+            }
+            msk_marker_diff<NQ>(G, c, q, d);
+            for (int r = 0; r < c.nrow; ++r) {
+                const Dual<NQ>& e = msk_axis(d, c.axis[r]);
+                if (Gout) Gout[(int64_t)(c.row0 + r) * B + b] = e.v;
+#pragma unroll
+                for (int j = 0; j < NQ; ++j)
+                    if (j < c.nd) J[(int64_t)(c.jo + r * c.nd + j) * B + b] = e.d[j];
+            }
+        } else if (Gout) {
+            double q[NQ], d[3];
+#pragma unroll
+            for (int j = 0; j < NQ; ++j) q[j] = V[(qb + j) * B + b];
+            msk_marker_diff<NQ>(G, c, q, d);
+            for (int r = 0; r < c.nrow; ++r) Gout[(int64_t)(c.row0 + r) * B + b] = msk_axis(d, c.axis[r]);
+        }
+    }
+}
+
 // ---- objective: quadratic tracking terms and the fatigue ratio term; thread = instance ---------------------
 struct MskObjective {
     int32_t kind;  // 0 Lagrange quadratic, 1 Mayer quadratic, 2 Mayer inverse square  w (c / z)^2

@@ -17,13 +17,14 @@ import json
 import math
 import pathlib
 import re
+import warnings
 
 import numpy as np
 
 from . import _cfx
 from .fes_models import DingModelPulseIntensityFrequency, DingModelPulseWidthFrequency, FesModel
 from .fourier import FourierSeries
-from .ocp import Node, Objective, ObjectiveFcn, ObjectiveList, OcpFes
+from .ocp import Constraint, ConstraintFcn, Node, Objective, ObjectiveFcn, ObjectiveList, OcpFes
 from .ode_solver import ControlType, OdeSolver
 
 # ---------------------------------------------------------------------------------------------------------------
@@ -53,11 +54,12 @@ _SKIP = {"meshfile": 1, "meshscale": 3, "meshcolor": 3, "mesh": 3}
 
 
 def parse_biomod(text: str) -> dict:
-    """bioMod text -> {"gravity", "segments", "muscles"} (segments in file order, each with parent, 4x4 RT,
-    rotation axes, mass, com, inertia, q ranges; muscles with their path and characteristics)."""
+    """bioMod text -> {"gravity", "segments", "markers", "muscles"} (segments in file order, each with parent, 4x4
+    RT, rotation axes, mass, com, inertia, q ranges; markers with their parent segment and position; muscles with
+    their path and characteristics)."""
     words = " ".join(line.split("//", 1)[0] for line in text.splitlines()).split()
     it = iter(words)
-    model = {"gravity": [0.0, 0.0, -9.81], "segments": [], "muscles": []}
+    model = {"gravity": [0.0, 0.0, -9.81], "segments": [], "markers": [], "muscles": []}
     groups, vias = {}, []
 
     def take(n):
@@ -103,10 +105,21 @@ def parse_biomod(text: str) -> dict:
                 else:
                     raise NotImplementedError(f"bioMod: segment keyword {w!r} is not supported")
             model["segments"].append(seg)
-        elif key == "marker":
+        elif key == "marker":  # a point fixed in its parent segment: parent, position
+            mk = {"name": next(it), "parent": None, "position": [0.0, 0.0, 0.0]}
             for w in it:
-                if w.lower() == "endmarker":
+                k = w.lower()
+                if k == "endmarker":
                     break
+                if k == "parent":
+                    mk["parent"] = next(it)
+                elif k == "position":
+                    mk["position"] = take(3)
+                elif k in ("technical", "anatomical", "axestoremove"):
+                    next(it)
+                else:
+                    raise NotImplementedError(f"bioMod: marker keyword {w!r} is not supported")
+            model["markers"].append(mk)
         elif key == "musclegroup":
             name, grp = next(it), {}
             for w in it:
@@ -160,7 +173,7 @@ _AXIS = {"x": 0, "y": 1, "z": 2}
 
 def reduce_to_chain(bm: dict) -> dict:
     """Serial chain of revolute dofs: per dof the constant joint frame relative to the previous dof's frame, one
-    composite body per dof frame, and every muscle path point in the frame of the dof it moves with."""
+    composite body per dof frame, and every muscle path point and marker in the frame of the dof it moves with."""
     frame_of, K_of = {}, {}  # segment -> (dof frame index or -1, constant 4x4 from that frame to the segment)
     axes, frames, names, ranges = [], [], [], []
     for seg in bm["segments"]:
@@ -210,10 +223,15 @@ def reduce_to_chain(bm: dict) -> dict:
                                 "optimal_length": float(mus["optimallength"]),
                                 "tendon_slack_length": float(mus["tendonslacklength"]),
                                 "pennation_angle": float(mus.get("pennationangle", 0.0))}
+    markers = {}
+    for mk in bm.get("markers", []):
+        K = K_of[mk["parent"]]
+        markers[mk["name"]] = {"frame": int(frame_of[mk["parent"]]),
+                               "pos": K[:3, :3] @ np.asarray(mk["position"], dtype=float) + K[:3, 3]}
     return {"axis": np.array(axes, dtype=np.int32), "frame": np.array(frames), "gravity": np.array(bm["gravity"]),
             "mass": mass, "com": com, "inertia": inertia.reshape(nq, 9), "q_names": names,
             "q_ranges": np.array(ranges, dtype=float), "muscles": muscles,
-            "muscle_order": [m["name"] for m in bm["muscles"]]}
+            "muscle_order": [m["name"] for m in bm["muscles"]], "markers": markers}
 
 
 # ---------------------------------------------------------------------------------------------------------------
@@ -351,7 +369,7 @@ class FesMskOcp:
 
     def __init__(self, model: FesMskModel, n_shooting, final_time, ode_solver, rows, objectives, x_bounds, x_init,
                  u_bounds, u_init, state_names, control_names, n_threads=1, use_sx=True, n_params=0, p_bounds=None,
-                 p_init=None, param_names=(), last_stim_idx=None, param_offset=None):
+                 p_init=None, param_names=(), last_stim_idx=None, param_offset=None, marker_pairs=()):
         self.model = model
         self.n_shooting = n_shooting
         self.final_time = final_time
@@ -370,6 +388,12 @@ class FesMskOcp:
         self.param_names = list(param_names)  # one name per parameter block, e.g. pulse_intensity_BIClong
         self.last_stim_idx = last_stim_idx
         self.param_offset = param_offset
+        # SUPERIMPOSE_MARKERS rows after every interval's rows (cfx_msk_marker_pair dicts + marker names)
+        self.marker_pairs = list(marker_pairs)
+
+    @property
+    def n_marker_rows(self) -> int:
+        return sum(bin(c["axes"]).count("1") for c in self.marker_pairs)
 
     @property
     def nzb(self):
@@ -424,7 +448,8 @@ class FesMskOcp:
             n_steps=self.ode_solver.n_integration_steps, n_shooting=self.n_shooting, truncation=self.truncation,
             final_time=float(self.final_time), stim_rows=self.stim_rows, batch=batch, flags=self.model.cfx_flags(),
             layout={"aos": _cfx.LAYOUT_AOS, "soa": _cfx.LAYOUT_SOA}[layout], objectives=self.objectives,
-            device=device, n_params=self.n_params, last_stim_idx=self.last_stim_idx, param_offset=self.param_offset)
+            device=device, n_params=self.n_params, last_stim_idx=self.last_stim_idx, param_offset=self.param_offset,
+            marker_pairs=self.marker_pairs)
 
     def solve(self, solver=None, **kwargs):
         from .solver import solve_ocp
@@ -440,9 +465,12 @@ class OcpFesMsk:
                     pulse_intensity: dict = None, objective: dict = None, msk_info: dict = None, use_sx: bool = True,
                     initial_guess_warm_start: bool = False, ode_solver=OdeSolver.RK4(n_integration_steps=1),
                     control_type: ControlType = ControlType.CONSTANT, n_threads: int = 1, external_forces: dict = None,
-                    n_shooting: int | None = None) -> FesMskOcp:
-        """Same arguments as the reference (fes_ocp_dynamics.py:158-251).  ``n_shooting`` (extension) overrides
-        the LCM node count of ``OcpFes.prepare_n_shooting``."""
+                    n_shooting: int | None = None, apply_custom_constraint: bool = False) -> FesMskOcp:
+        """Same arguments as the reference (fes_ocp_dynamics.py:158-251).  Extensions: ``n_shooting`` overrides the
+        LCM node count of ``OcpFes.prepare_n_shooting``; ``apply_custom_constraint`` enforces
+        ``msk_info["custom_constraint"]``.  The reference accepts that constraint list but never applies it: its
+        ``_prepare_optimization_problem`` calls ``_build_constraints`` without it (fes_ocp_dynamics.py:107; the
+        parameter is read at 424-450), so by default it is ignored here too, with a warning."""
         if external_forces:
             raise NotImplementedError("OcpFesMsk: external forces are not supported")
         if initial_guess_warm_start:
@@ -485,8 +513,42 @@ class OcpFesMsk:
             last = np.array([stim_idx_at_node_list[k][-1] for k in range(n)], dtype=np.int32)
             par = dict(n_params=n_params, p_bounds=p_bounds, p_init=p_init, param_names=names, last_stim_idx=last,
                        param_offset=offsets)
+        pairs = []
+        if msk_info["custom_constraint"]:
+            if apply_custom_constraint:
+                pairs = OcpFesMsk._build_constraints(model, n, msk_info["custom_constraint"])
+            else:
+                warnings.warn("msk_info['custom_constraint'] is not applied, as in the reference "
+                              "(fes_ocp_dynamics.py:107 builds the constraints without it); pass "
+                              "apply_custom_constraint=True to enforce it", stacklevel=2)
         return FesMskOcp(model, n, final_time, ode_solver, rows, terms, x_bounds, x_init, u_bounds, u_init,
-                         state_names, control_names, n_threads, use_sx, **par)
+                         state_names, control_names, n_threads, use_sx, marker_pairs=pairs, **par)
+
+    @staticmethod
+    def _build_constraints(model, n, custom_constraint) -> list:
+        """The custom constraints of ``_build_constraints`` (fes_ocp_dynamics.py:444-448) as marker pairs: every
+        ``ConstraintFcn.SUPERIMPOSE_MARKERS`` of phase 0, one pair per node, markers re-expressed in the frame of
+        the dof they move with (``reduce_to_chain``)."""
+        markers = model.chain["markers"]
+        pairs = []
+        for i in range(len(custom_constraint)):
+            if not custom_constraint[i]:
+                continue
+            for c in custom_constraint[i]:
+                if not isinstance(c, Constraint) or c.constraint is not ConstraintFcn.SUPERIMPOSE_MARKERS:
+                    raise NotImplementedError("custom_constraint: only ConstraintFcn.SUPERIMPOSE_MARKERS is supported")
+                for name in (c.first_marker, c.second_marker):
+                    if name not in markers:
+                        raise ValueError(f"marker {name!r} is not in {model.biorbd_path}")
+                m1, m2 = markers[c.first_marker], markers[c.second_marker]
+                if m1["frame"] < 0 and m2["frame"] < 0:
+                    raise ValueError("SUPERIMPOSE_MARKERS: both markers are fixed to the ground")
+                axes = sum(1 << int(a) for a in set(c.axes))
+                for k in c.nodes(n):
+                    pairs.append({"node": k, "axes": axes, "frame": [m1["frame"], m2["frame"]],
+                                  "pos": [list(m1["pos"]), list(m2["pos"])], "first": c.first_marker,
+                                  "second": c.second_marker})
+        return pairs
 
     @staticmethod
     def _build_parameters(model, pulse_intensity):

@@ -13,7 +13,7 @@ Phi(x_k, u_k) - x_{k+1}, then (Hmed with intensity parameters) u_k - window_k(p)
 
 from __future__ import annotations
 
-from enum import Enum
+from enum import Enum, IntEnum
 from fractions import Fraction
 from math import gcd
 
@@ -34,6 +34,74 @@ class Node(Enum):
     END = "end"
     ALL = "all"
     ALL_SHOOTING = "all_shooting"
+
+
+class Axis(IntEnum):
+    """bioptim ``Axis`` (world axes of marker constraints)."""
+    X = 0
+    Y = 1
+    Z = 2
+
+
+class ConstraintFcn(Enum):
+    """The bioptim constraint the reference's OcpFesMsk examples pass as ``msk_info["custom_constraint"]``
+    (examples/dynamics/reaching_task/*.py)."""
+    SUPERIMPOSE_MARKERS = "superimpose_markers"
+
+
+class Constraint:
+    """One ``ConstraintFcn.SUPERIMPOSE_MARKERS`` equality: marker(second) - marker(first) = 0 on ``axes`` (all three
+    by default) at ``node`` (an int, ``Node.START`` / ``Node.END`` / ``Node.ALL`` / ``Node.ALL_SHOOTING``)."""
+
+    def __init__(self, constraint, node=None, first_marker: str = None, second_marker: str = None, axes=None,
+                 phase: int = 0, **extra):
+        if not isinstance(constraint, ConstraintFcn):
+            raise NotImplementedError(f"constraint {constraint!r} is not supported (SUPERIMPOSE_MARKERS only)")
+        if extra:
+            raise NotImplementedError(f"SUPERIMPOSE_MARKERS: unsupported arguments {sorted(extra)}")
+        if phase != 0:
+            raise NotImplementedError("single-phase problems only")
+        if node is None:
+            raise ValueError("SUPERIMPOSE_MARKERS: give the node (an int or a Node)")
+        if not first_marker or not second_marker:
+            raise ValueError("SUPERIMPOSE_MARKERS needs first_marker and second_marker")
+        self.constraint = constraint
+        self.node = node
+        self.first_marker, self.second_marker = first_marker, second_marker
+        self.axes = [Axis(a) for a in (axes if axes is not None else (Axis.X, Axis.Y, Axis.Z))]
+        self.phase = phase
+
+    def nodes(self, n_shooting: int) -> list:
+        if isinstance(self.node, Node):
+            return {Node.START: [0], Node.END: [n_shooting], Node.ALL: list(range(n_shooting + 1)),
+                    Node.ALL_SHOOTING: list(range(n_shooting))}[self.node]
+        nodes = [int(k) for k in (self.node if isinstance(self.node, (list, tuple, range)) else [self.node])]
+        for k in nodes:
+            if not 0 <= k <= n_shooting:
+                raise ValueError(f"SUPERIMPOSE_MARKERS: node {k} is outside [0, {n_shooting}]")
+        return nodes
+
+
+class ConstraintList:
+    """bioptim ``ConstraintList`` for one phase: ``custom_constraint[0]`` is the phase's list (the reference walks
+    it as ``custom_constraint[i][j]``, fes_ocp_dynamics.py:444-448)."""
+
+    def __init__(self):
+        self._items = []
+
+    def add(self, constraint, **kwargs):
+        self._items.append(constraint if isinstance(constraint, Constraint) else Constraint(constraint, **kwargs))
+
+    def __getitem__(self, i):
+        if i != 0:
+            raise IndexError("single-phase ConstraintList")
+        return self._items
+
+    def __len__(self):
+        return 1 if self._items else 0
+
+    def __iter__(self):
+        return iter(self._items)
 
 
 class ObjectiveFcn:

@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define CFX_ABI_VERSION 2
+#define CFX_ABI_VERSION 3
 
 /* return codes */
 #define CFX_OK 0
@@ -207,6 +207,18 @@ typedef struct cfx_msk_muscle {
     double optimal_length, tendon_slack_length, pennation_angle;
 } cfx_msk_muscle;
 
+/* A marker superimposition (bioptim ConstraintFcn.SUPERIMPOSE_MARKERS as OcpFesMsk passes msk_info
+   ["custom_constraint"] through, cocofest/optimization/fes_ocp_dynamics.py:424-450; used by
+   examples/dynamics/reaching_task/ examples): at node `node`, for each selected world axis, one equality row
+   marker(second) - marker(first) = 0 over q_node (bioptim's superimpose_markers penalty).  A marker is a point
+   fixed in a dof frame (-1: ground), as the muscle path points. */
+typedef struct cfx_msk_marker_pair {
+    int32_t node;     /* 0 .. n_shooting */
+    int32_t axes;     /* bit a set: a row for world axis a (X = 1, Y = 2, Z = 4), rows in axis order */
+    int32_t frame[2]; /* dof frame of the first / second marker (-1: ground) */
+    double pos[2][3]; /* their positions in those frames */
+} cfx_msk_marker_pair;
+
 typedef struct cfx_msk_problem {
     int32_t abi_version; /* CFX_ABI_VERSION */
     int32_t scheme;      /* CFX_RK1 | CFX_RK2 | CFX_RK4 */
@@ -240,6 +252,10 @@ typedef struct cfx_msk_problem {
     int32_t n_params;
     const int32_t *last_stim_idx; /* [n_shooting] parameter index of the last pulse <= t_k (muscle-relative) */
     const int32_t *param_offset;  /* [n_muscles] first parameter of each muscle's intensities (equal: shared) */
+    /* marker superimpositions: their rows follow every interval's rows (in pair order, axes ascending); J_g
+       entries on q_node of the dofs that move either marker; the Hessian gains the (q_node, q_node) pairs */
+    int32_t n_marker_pairs;
+    const cfx_msk_marker_pair *marker_pairs;
 } cfx_msk_problem;
 
 int cfx_msk_create(const cfx_msk_problem *problem, cfx_handle **out);

@@ -77,8 +77,9 @@ def _num(tok: str) -> float:
 
 
 def parse_biomod(text: str) -> dict:
-    """Segments (parent, RT, rotation dofs, mass, com, inertia, q ranges), gravity and muscles (origin,
-    via points, insertion, optimal length, maximal force, tendon slack length, pennation angle)."""
+    """Segments (parent, RT, rotation dofs, mass, com, inertia, q ranges), gravity, markers (parent segment,
+    position) and muscles (origin, via points, insertion, optimal length, maximal force, tendon slack length,
+    pennation angle)."""
     toks = []
     for line in text.splitlines():
         line = line.split("//")[0]
@@ -93,7 +94,7 @@ def parse_biomod(text: str) -> dict:
     def nums(n):
         return [_num(nxt()) for _ in range(n)]
 
-    out = {"gravity": [0.0, 0.0, -9.81], "segments": [], "muscles": [], "groups": {}}
+    out = {"gravity": [0.0, 0.0, -9.81], "segments": [], "markers": [], "muscles": [], "groups": {}}
     vias = []
     while pos < len(toks):
         t = nxt()
@@ -138,9 +139,22 @@ def parse_biomod(text: str) -> dict:
                 else:
                     raise NotImplementedError(f"bioMod: unsupported segment keyword {k!r}")
             out["segments"].append(seg)
-        elif tl == "marker":
-            while nxt().lower() != "endmarker":
-                pass
+        elif tl == "marker":  # a point fixed in its parent segment (biorbd Marker): parent, position
+            mk = {"name": nxt(), "parent": None, "position": [0.0, 0.0, 0.0]}
+            while True:
+                k = nxt()
+                kl = k.lower()
+                if kl == "endmarker":
+                    break
+                if kl == "parent":
+                    mk["parent"] = nxt()
+                elif kl == "position":
+                    mk["position"] = nums(3)
+                elif kl in ("technical", "anatomical", "axestoremove"):
+                    nxt()
+                else:
+                    raise NotImplementedError(f"bioMod: unsupported marker keyword {k!r}")
+            out["markers"].append(mk)
         elif tl == "musclegroup":
             name = nxt()
             grp = {}
@@ -255,6 +269,15 @@ def _point_jacobian(bm, dofs, seg, P):
         if d["segment"] in anc:
             J[:, k] = np.cross(d["axis"], P - d["origin"])
     return J
+
+
+def marker_position(bm: dict, name: str, q):
+    """World position of a bioMod marker (a point fixed in its parent segment) at q (biorbd ``markers(q)``)."""
+    for mk in bm.get("markers", []):
+        if mk["name"] == name:
+            frames, _ = forward_kinematics(bm, q)
+            return _point_world(frames, mk["parent"], mk["position"])
+    raise ValueError(f"marker {name!r} is not in the bioMod")
 
 
 def muscle_path(mus: dict):
@@ -438,6 +461,10 @@ class MskProblem:
     n_params: int = 0
     last_stim_idx: list = None
     param_offset: list = None
+    # bioptim ConstraintFcn.SUPERIMPOSE_MARKERS as OcpFesMsk's msk_info["custom_constraint"] passes it
+    # (fes_ocp_dynamics.py:424-450): dicts node, first, second (marker names), axes (world axis indices); rows
+    # marker(second) - marker(first) at q_node, after every interval's rows
+    marker_pairs: list = field(default_factory=list)
 
     @property
     def nq(self):
@@ -480,8 +507,12 @@ class MskProblem:
         return self.n_shooting * self.nz + self.nx + self.n_params
 
     @property
+    def n_marker_rows(self):
+        return sum(len(c["axes"]) for c in self.marker_pairs)
+
+    @property
     def ng(self):
-        return self.n_shooting * (self.nx + self.n_slide)
+        return self.n_shooting * (self.nx + self.n_slide) + self.n_marker_rows
 
     @property
     def dt(self):
@@ -568,14 +599,29 @@ def sliding_rows(pb: MskProblem, v, k):
     return np.concatenate(out)
 
 
+def marker_rows(pb: MskProblem, v):
+    """SUPERIMPOSE_MARKERS rows (bioptim penalty ``superimpose_markers``: marker(second) - marker(first), the
+    selected axes), in the order of ``pb.marker_pairs``."""
+    X, _ = unpack(pb, v)
+    out = []
+    for c in pb.marker_pairs:
+        q = X[c["node"], pb.nxm: pb.nxm + pb.nq]
+        d = marker_position(pb.bm, c["second"], q) - marker_position(pb.bm, c["first"], q)
+        out.extend(d[a] for a in c["axes"])
+    return np.array(out, dtype=np.result_type(v.dtype, float))
+
+
 def eval_g(pb: MskProblem, v):
-    """Per interval: continuity rows Phi(x_k, u_k) - x_{k+1}, then (Hmed with parameters) the sliding rows."""
+    """Per interval: continuity rows Phi(x_k, u_k) - x_{k+1}, then (Hmed with parameters) the sliding rows; then
+    the marker rows."""
     X, U = unpack(pb, v)
     parts = []
     for k in range(pb.n_shooting):
         parts.append(integrate_interval(pb, k, X[k], U[k]) - X[k + 1])
         if pb.n_slide:
             parts.append(sliding_rows(pb, v, k))
+    if pb.marker_pairs:
+        parts.append(marker_rows(pb, v))
     return np.concatenate(parts)
 
 

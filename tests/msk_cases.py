@@ -30,7 +30,8 @@ def _hmed(model):
 
 
 def biomod_path(name="arm26_biceps_triceps") -> str:
-    return str(GOLDEN / f"biomod_{name}.json")
+    """A fixture name, or the path of a parsed bioMod written by a test (ends in .json)."""
+    return name if name.endswith(".json") else str(GOLDEN / f"biomod_{name}.json")
 
 
 def cfg5(**kw):
@@ -44,7 +45,9 @@ def cfg5(**kw):
 
 
 def product_ocp(model, biomod, muscles, scheme, m, fv, residual, fatigue, qdot_end, truncation, bound=(5, 90),
-                passive=False):
+                passive=False, markers=(), bound_type="start_end"):
+    """``markers``: SUPERIMPOSE_MARKERS constraints as dicts first, second, node (int or "end"), axes (indices),
+    passed through msk_info["custom_constraint"] with apply_custom_constraint=True."""
     import cocofest_amd as C
 
     pint = None
@@ -67,17 +70,25 @@ def product_ocp(model, biomod, muscles, scheme, m, fv, residual, fatigue, qdot_e
         obj["minimize_residual_torque"] = True
     solver = {"RK1": C.OdeSolver.RK1, "RK2": C.OdeSolver.RK2, "RK4": C.OdeSolver.RK4}[scheme](n_integration_steps=m)
     nq = mm.nb_q
-    info = {"bound_type": "start_end", "bound_data": [[0] * (nq - 1) + [bound[0]], [0] * (nq - 1) + [bound[1]]],
+    start, end = [0] * (nq - 1) + [bound[0]], [0] * (nq - 1) + [bound[1]]
+    info = {"bound_type": bound_type, "bound_data": {"start_end": [start, end], "start": start, "end": end}[bound_type],
             "with_residual_torque": residual}
+    if markers:
+        cl = C.ConstraintList()
+        for mk in markers:
+            cl.add(C.ConstraintFcn.SUPERIMPOSE_MARKERS, first_marker=mk["first"], second_marker=mk["second"],
+                   node=C.Node.END if mk["node"] == "end" else mk["node"], axes=[C.Axis(a) for a in mk["axes"]],
+                   phase=0)
+        info["custom_constraint"] = cl
     ocp = C.OcpFesMsk.prepare_ocp(model=mm, final_time=1, objective=obj, msk_info=info, ode_solver=solver,
-                                  pulse_intensity=pint)
+                                  pulse_intensity=pint, apply_custom_constraint=bool(markers))
     if passive:  # OcpFesMsk drops the flag as the reference does; set it back to exercise the kernels' FP term
         ocp.model.activate_passive_force_relationship = True
     return ocp
 
 
 def oracle_problem(model, biomod, muscles, scheme, m, fv, residual, fatigue, qdot_end, truncation, bound=(5, 90),
-                   passive=False):
+                   passive=False, markers=(), bound_type="start_end"):
     bm = json.loads(pathlib.Path(biomod_path(biomod)).read_text())
     n = O.prepare_n_shooting(STIMS, 1)
     tab = O.stim_table(STIMS, n, 1, truncation)
@@ -100,6 +111,9 @@ def oracle_problem(model, biomod, muscles, scheme, m, fv, residual, fatigue, qdo
                                       node_last=n - 1, weight=10000.0, target_value=0.0))
     if fatigue:
         pb.fatigue_weight = 1.0
+    for mk in markers:
+        pb.marker_pairs.append(dict(node=n if mk["node"] == "end" else mk["node"], first=mk["first"],
+                                    second=mk["second"], axes=sorted(set(mk["axes"]))))
     return pb
 
 

@@ -147,6 +147,95 @@ def test_chain_reduction_reproduces_tree_kinematics_and_inertia(name):
     np.testing.assert_allclose(Mc, M.mass_matrix(bm, q), rtol=1e-12, atol=1e-14)
 
 
+@pytest.mark.parametrize("name", FIXTURES)
+def test_chain_reduction_reproduces_tree_marker_positions(name):
+    """Markers re-expressed in the frame of the dof they move with land where the full tree puts them."""
+    from cocofest_amd.msk import reduce_to_chain
+
+    bm = _bm(name)
+    ch = reduce_to_chain(bm)
+    assert set(ch["markers"]) == {m["name"] for m in bm["markers"]}
+    for q in (np.linspace(-0.3, 1.2, M.nb_q(bm)), np.linspace(0.9, -0.4, M.nb_q(bm))):
+        R, o = _chain_frames(ch, q)
+        for mk in bm["markers"]:
+            g = ch["markers"][mk["name"]]
+            got = g["pos"] if g["frame"] < 0 else R[g["frame"]] @ g["pos"] + o[g["frame"]]
+            np.testing.assert_allclose(got, M.marker_position(bm, mk["name"], q), atol=1e-14)
+
+
+REACH = [dict(first="COM_hand", second="target", node="end", axes=(0, 1))]
+
+
+def test_custom_constraint_is_ignored_as_in_the_reference_unless_applied():
+    """The reference drops msk_info["custom_constraint"] (fes_ocp_dynamics.py:107 calls _build_constraints without
+    it): by default the OCP has no marker rows (and says so); apply_custom_constraint=True adds them."""
+    import cocofest_amd as C
+
+    cfg = MC.cfg5()
+    cl = C.ConstraintList()
+    cl.add(C.ConstraintFcn.SUPERIMPOSE_MARKERS, first_marker="COM_hand", second_marker="target", node=C.Node.END,
+           axes=[C.Axis.X, C.Axis.Y], phase=0)
+    assert len(cl) == 1 and len(cl[0]) == 1
+    base = MC.product_ocp(**cfg)
+    mm = base.model
+    info = {"bound_type": "start_end", "bound_data": [[0, 5], [0, 90]], "custom_constraint": cl}
+    with pytest.warns(UserWarning, match="not applied, as in the reference"):
+        ign = C.OcpFesMsk.prepare_ocp(model=mm, final_time=1, msk_info=info)
+    assert ign.marker_pairs == []
+    app = C.OcpFesMsk.prepare_ocp(model=mm, final_time=1, msk_info=info, apply_custom_constraint=True)
+    assert len(app.marker_pairs) == 1 and app.n_marker_rows == 2
+    c = app.marker_pairs[0]
+    assert c["node"] == app.n_shooting and c["axes"] == 3 and c["frame"] == [1, -1]
+    # the product's pair and the oracle's rows agree at a random point (same layout, chain vs tree kinematics)
+    pb = MC.oracle_problem(**cfg, markers=REACH)
+    v = MC.random_decision(pb, 1, seed=2)[0]
+    X, _ = M.unpack(pb, v)
+    q = X[-1, pb.nxm: pb.nxm + pb.nq]
+    R, o = _chain_frames(mm.chain, q)
+    p1 = R[1] @ np.asarray(c["pos"][0]) + o[1]
+    np.testing.assert_allclose((np.asarray(c["pos"][1]) - p1)[:2], M.marker_rows(pb, v), atol=1e-14)
+    assert pb.ng == pb.n_shooting * pb.nx + 2
+
+
+def test_custom_constraint_validation():
+    import cocofest_amd as C
+
+    with pytest.raises(NotImplementedError, match="SUPERIMPOSE_MARKERS only"):
+        C.ConstraintList().add("track_state", node=1)
+    with pytest.raises(NotImplementedError, match="unsupported arguments"):
+        C.ConstraintList().add(C.ConstraintFcn.SUPERIMPOSE_MARKERS, first_marker="a", second_marker="b", node=1,
+                               min_bound=0)
+    with pytest.raises(ValueError, match="give the node"):
+        C.ConstraintList().add(C.ConstraintFcn.SUPERIMPOSE_MARKERS, first_marker="a", second_marker="b")
+    mm = MC.product_ocp(**MC.cfg5()).model
+    for kw, err, msg in ((dict(first_marker="COM_hand", second_marker="nowhere", node=3), ValueError, "not in"),
+                         (dict(first_marker="COM_hand", second_marker="target", node=11), ValueError, "outside"),
+                         (dict(first_marker="target", second_marker="target", node=2), ValueError, "ground")):
+        cl = C.ConstraintList()
+        cl.add(C.ConstraintFcn.SUPERIMPOSE_MARKERS, **kw)
+        with pytest.raises(err, match=msg):
+            C.OcpFesMsk.prepare_ocp(model=mm, final_time=1, msk_info={"custom_constraint": cl},
+                                    apply_custom_constraint=True)
+
+
+@pytest.mark.parametrize("pair, msg", [
+    (dict(node=11, axes=1, frame=[1, -1]), "marker pair node out of"),
+    (dict(node=2, axes=0, frame=[1, -1]), "axes must select"),
+    (dict(node=2, axes=8, frame=[1, -1]), "axes must select"),
+    (dict(node=2, axes=3, frame=[2, -1]), "marker frame out of range"),
+    (dict(node=2, axes=3, frame=[-1, -1]), "fixed to the ground"),
+])
+def test_msk_create_rejects_bad_marker_pairs(pair, msg):
+    """cfx_msk_create validates the marker pairs before any HIP call (EINVAL and the reason)."""
+    from cocofest_amd import CfxError, _cfx
+
+    ocp = MC.product_ocp(**MC.cfg5())
+    ocp.marker_pairs = [dict(pos=[[0.0] * 3, [0.0] * 3], **pair)]
+    with pytest.raises(CfxError, match=msg) as e:
+        ocp.nlp(batch=1)
+    assert e.value.code == _cfx.EINVAL
+
+
 # ---- OcpFesMsk facade -----------------------------------------------------------------------------------------
 
 def test_ocp_fes_msk_layout_bounds_and_objective():

@@ -7,6 +7,9 @@ gradients); f / grad f 1e-12; IVP trajectories 1e-10 relative.  The oracle is pi
 (parity with biorbd + bioptim unpinned, see oracle/fes_msk.py).
 """
 
+import json
+import pathlib
+
 import numpy as np
 import pytest
 
@@ -170,6 +173,102 @@ def test_msk_hessian_matches_oracle(case):
                 ref[e, e] += of[b] * 2 * w
         scale = np.max(np.abs(ref))
         assert np.max(np.abs(got - ref)) < 2e-5 * scale, (case, k, np.max(np.abs(got - ref)) / scale)
+
+
+# ---- SUPERIMPOSE_MARKERS rows (msk_info["custom_constraint"] with apply_custom_constraint=True) -----------------
+SIX = ("BIClong", "BICshort", "BRA", "TRIlong", "TRIlat", "TRImed")
+MARKER_CASES = {
+    "cfg5_end_xy": (MC.cfg5(), [dict(first="COM_hand", second="target", node="end", axes=(0, 1))]),
+    "d07_rk1_mid_xyz_end_y": (MC.cfg5(model="ding2007", scheme="RK1", m=2, residual=True, fatigue=False),
+                              [dict(first="COM_hand", second="target", node=3, axes=(0, 1, 2)),
+                               dict(first="target", second="COM_hand", node="end", axes=(1,)),
+                               dict(first="COM_hand", second="target", node=3, axes=(2,))]),
+    "arm26_6muscles_reach": (MC.cfg5(biomod="arm26", model="ding2003", fatigue=False, scheme="RK1", m=2, muscles=SIX),
+                             [dict(first="COM_hand", second="reaching_target", node="end", axes=(0, 1)),
+                              dict(first="COM_hand", second="target", node=0, axes=(0,))]),
+    "biceps_1dof_xy": (MC.cfg5(biomod="arm26_biceps_1dof", muscles=("BIClong",)),
+                       [dict(first="COM_hand", second="target", node=5, axes=(0, 1))]),
+}
+
+
+@pytest.mark.parametrize("case", list(MARKER_CASES))
+def test_msk_marker_rows_match_oracle(case):
+    """Marker rows after the interval rows: values, J_g (complex step of the oracle's tree kinematics) and the
+    Lagrangian Hessian terms (central differences of complex-step gradients); the dynamics rows are unchanged."""
+    cfg, markers = MARKER_CASES[case]
+    ocp = MC.product_ocp(**cfg, markers=markers)
+    pb = MC.oracle_problem(**cfg, markers=markers)
+    nmr = pb.n_marker_rows
+    r0 = pb.ng - nmr
+    B = 3
+    V = MC.random_decision(pb, B, seed=5)
+    h = ocp.nlp(batch=B, layout="aos")
+    assert (h.ng, ocp.n_marker_rows) == (pb.ng, nmr)
+    g = h.eval_g(V)
+    jac = h.eval_jac_g(V)
+    jr, jc = h.jac_structure()
+    lam = np.zeros((B, pb.ng))
+    lam[:, r0:] = np.random.default_rng(6).normal(size=(B, nmr))
+    hv = h.eval_h(V, np.zeros(B), lam)
+    hr, hc = h.hess_structure()
+    ref_plain = MC.product_ocp(**cfg).nlp(batch=B, layout="aos")
+    g0 = ref_plain.eval_g(V)
+    ref_plain.close()
+    h.close()
+    np.testing.assert_array_equal(g[:, :r0], g0)  # the interval rows do not see the marker rows
+    qcols = sorted({pb.nz * c["node"] + pb.nxm + j for c in pb.marker_pairs for j in range(pb.nq)})
+    for b in range(B):
+        np.testing.assert_allclose(g[b, r0:], M.marker_rows(pb, V[b]), rtol=0, atol=1e-14)
+        got = np.zeros((nmr, pb.nv))
+        for r, c, val in zip(jr, jc, jac[b]):
+            if r >= r0:
+                got[r - r0, c] += val
+
+        def jac_ref(v):
+            out = np.zeros((nmr, pb.nv))
+            for c in qcols:
+                vv = v.astype(complex)
+                vv[c] += 1e-30j
+                out[:, c] = np.imag(M.marker_rows(pb, vv)) / 1e-30
+            return out
+
+        np.testing.assert_allclose(got, jac_ref(V[b]), rtol=0, atol=1e-14)
+        Hgot = np.zeros((pb.nv, pb.nv))
+        for r, c, val in zip(hr, hc, hv[b]):
+            Hgot[r, c] += val
+            if r != c:
+                Hgot[c, r] += val
+        Href = np.zeros_like(Hgot)
+        eps = 1e-6
+        for c in qcols:
+            vp, vm = V[b].copy(), V[b].copy()
+            vp[c] += eps
+            vm[c] -= eps
+            Href[:, c] = (lam[b, r0:] @ jac_ref(vp) - lam[b, r0:] @ jac_ref(vm)) / (2 * eps)
+        scale = np.max(np.abs(Href))
+        assert np.max(np.abs(Hgot - Href)) < 1e-7 * scale, (case, b, np.max(np.abs(Hgot - Href)) / scale)
+
+
+def test_msk_reaching_marker_constraint_reproduces_the_bounded_optimum(tmp_path):
+    """cfg 5 with its end posture given by a SUPERIMPOSE_MARKERS constraint instead of the end bounds: the hand
+    (COM_hand) at node N on a ground marker placed where the cfg-5 end posture (shoulder 0, elbow 3.14 / 2) puts it.
+    Same optimum as test_msk_cfg5_interior_point_converges, reached through the marker rows (their J_g entries and
+    Hessian terms, the rows in the KKT band) in the native interior point."""
+    bm = json.loads(pathlib.Path(MC.biomod_path("arm26_biceps_triceps")).read_text())
+    goal = M.marker_position(bm, "COM_hand", [0.0, 3.14 / 2])
+    bm["markers"].append({"name": "goal", "parent": "base", "position": [float(x) for x in goal]})
+    path = tmp_path / "biomod_goal.json"
+    path.write_text(json.dumps(bm))
+    ref = MC.product_ocp(**MC.cfg5(m=5)).solve(tol=1e-6, max_iter=1000)
+    ocp = MC.product_ocp(**MC.cfg5(m=5, biomod=str(path)), bound_type="start",
+                         markers=[dict(first="COM_hand", second="goal", node="end", axes=(0, 1))])
+    res = ocp.solve(tol=1e-6, max_iter=1000)
+    print("iterations", res.iterations, ref.iterations, "f", res.f, ref.f, "wall", res.wall_time)
+    assert bool(res.converged[0]) and bool(ref.converged[0])
+    states, _, _ = ocp.unpack(res.v[0])
+    q = [states[f"q_{n}"][0] for n in ocp.model.name_dof]
+    assert abs(q[0][-1]) < 1e-5 and abs(q[1][-1] - 1.57) < 1e-5
+    assert abs(res.f[0] - ref.f[0]) < 1e-5 * abs(ref.f[0])
 
 
 def test_msk_ivp_matches_oracle():
