@@ -419,3 +419,35 @@ def test_ipm_option_structs_match_the_header():
                 continue
             names += [n.strip() for n in decl.split(None, 1)[1].split(",")]
         assert names == [f for f, _ in cls._fields_], struct
+
+
+def test_ctypes_mirrors_match_the_c_header_layout(tmp_path):
+    """Every ctypes structure of _cfx.py has the size and field offsets gcc gives the include/cfx.h struct of the
+    same name (a drifted field would shift every later argument across the C ABI)."""
+    import ctypes
+    import pathlib
+    import shutil
+    import subprocess
+
+    from cocofest_amd import _cfx
+
+    if shutil.which("gcc") is None:
+        pytest.skip("gcc not available")
+    pairs = [(_cfx.Constants, "cfx_constants"), (_cfx.Objective, "cfx_objective"), (_cfx.Problem, "cfx_problem"),
+             (_cfx.Sizes, "cfx_sizes"), (_cfx.MskMuscle, "cfx_msk_muscle"), (_cfx.MskMarkerPair, "cfx_msk_marker_pair"),
+             (_cfx.MskProblem, "cfx_msk_problem"), (_cfx.IpmOptions, "cfx_ipm_options"), (_cfx.IpmStats, "cfx_ipm_stats")]
+    lines, want = [], []
+    for cls, cname in pairs:
+        lines.append(f'printf("%zu\\n", sizeof({cname}));')
+        want.append(ctypes.sizeof(cls))
+        for name, _ in cls._fields_:
+            lines.append(f'printf("%zu\\n", offsetof({cname}, {name}));')
+            want.append(getattr(cls, name).offset)
+    src = tmp_path / "layout.c"
+    inc = pathlib.Path(__file__).resolve().parents[1] / "include"
+    src.write_text('#include <stddef.h>\n#include <stdio.h>\n#include "cfx.h"\nint main(void) {\n' + "\n".join(lines)
+                   + "\nreturn 0;\n}\n")
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-std=c11", "-I", str(inc), str(src), "-o", str(exe)], check=True)
+    got = [int(x) for x in subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split()]
+    assert got == want
