@@ -1,0 +1,33 @@
+"""cfg 3 (Ding2007 pulse width, N = 100, force tracking) native interior point at batch 1, solved `reps` times after
+a warm-up, for a rocprofv3 kernel trace: python scripts/profile_cfg3_native.py [reps]"""
+import json
+import pathlib
+import sys
+import time
+
+import numpy as np
+
+ROOT = pathlib.Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+
+from cocofest_amd import ModelMaker, OcpFes, OdeSolver  # noqa: E402
+from cocofest_amd.solver import IpmOptions, NativeIpm  # noqa: E402
+
+reps = int(sys.argv[1]) if len(sys.argv) > 1 else 10
+ft = json.loads((ROOT / "tests" / "golden" / "ref_formulas.json").read_text())["misc"]["force_tracking"]
+model = ModelMaker.create_model("ding2007", stim_time=[float(v) for v in np.round(np.linspace(0, 1, 31)[:-1], 2)],
+                                sum_stim_truncation=10)
+ocp = OcpFes.prepare_ocp(model=model, final_time=1, pulse_width={"min": model.pd0, "max": 0.0006},
+                         objective={"force_tracking": [np.array(ft["time"]), np.array(ft["force"])]},
+                         ode_solver=OdeSolver.RK1(n_integration_steps=10))
+ipm = NativeIpm(ocp, batch=1, options=IpmOptions(tol=1e-6, max_iter=300))
+ipm.solve()
+walls = []
+for _ in range(reps):
+    t = time.perf_counter()
+    r = ipm.solve()
+    walls.append(time.perf_counter() - t)
+print(json.dumps({"wall_s_median": float(np.median(walls)), "wall_s_min": min(walls), "iterations": int(r.iterations[0]),
+                  "callbacks": r.n_callbacks, "stats": {k: (float(v) if not isinstance(v, int) else v)
+                                                       for k, v in ipm.last_stats.items()}}))
+ipm.close()
