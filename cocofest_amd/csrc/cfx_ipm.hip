@@ -1451,9 +1451,14 @@ extern "C" int cfx_ipm_create(cfx_handle* h, const double* lb, const double* ub,
         }
         return d;
     };
+    // Blocks per instance: up to 8 at batch 1 (cfg 3: 9.6 ms vs 10.3 with 16 / 11.4 with 4), about 128 / B above
+    // (cfg 4 NMPC, 64 scenarios: 4.04 / 4.19 / 5.12 ms per horizon with 2 / 4 / 8 blocks, 4.60 undissected;
+    // scripts/gpu_nmpc_nd.sh); batches above 64 keep one band per instance.
     Cut cut;
-    if (s->B <= 8 && nAb >= 48) {
-        int pmax = std::min(8, nAb / 24);  // 8: cfg 3 at batch 1 9.6 ms vs 10.3 (16) / 11.4 (4)
+    int64_t nd_batch = 64;
+    if (const char* e = std::getenv("CFX_IPM_ND_BATCH")) nd_batch = std::atoll(e);  // tuning override
+    if (s->B <= nd_batch && nAb >= 48) {
+        int pmax = (int)std::min<int64_t>(std::min(8, nAb / 24), std::max<int64_t>(2, 128 / s->B));
         if (const char* e = std::getenv("CFX_IPM_PARTS")) pmax = std::min(pmax, std::atoi(e));  // tuning override
         for (int P = pmax; P >= 2 && cut.P == 1; --P) {
             Cut d = dissect(P);
