@@ -1453,9 +1453,10 @@ extern "C" int cfx_ipm_create(cfx_handle* h, const double* lb, const double* ub,
     };
     // Blocks per instance: up to 8 at batch 1 (cfg 3: 9.6 ms vs 10.3 with 16 / 11.4 with 4), about 128 / B above
     // (cfg 4 NMPC, 64 scenarios: 4.04 / 4.19 / 5.12 ms per horizon with 2 / 4 / 8 blocks, 4.60 undissected;
-    // scripts/gpu_nmpc_nd.sh); batches above 64 keep one band per instance.
+    // scripts/gpu_nmpc_nd.sh), 2 blocks up to batch 512 (cfg 3, 256 starts: 22.9 vs 27.5 ms; scripts/gpu_cfg3_nd.sh);
+    // larger batches fill the chip with one band per instance.
     Cut cut;
-    int64_t nd_batch = 64;
+    int64_t nd_batch = 512;
     if (const char* e = std::getenv("CFX_IPM_ND_BATCH")) nd_batch = std::atoll(e);  // tuning override
     if (s->B <= nd_batch && nAb >= 48) {
         int pmax = (int)std::min<int64_t>(std::min(8, nAb / 24), std::max<int64_t>(2, 128 / s->B));
