@@ -8,7 +8,7 @@
 // step is a pivot search (argmax), a row swap, a scale and a rank-1 update of the km x (ju - j) trailing
 // block, spread over the workgroup's NT threads (64 for narrow bands, 256 / 1024 for wide ones).
 //
-// Four placements of the band (the register one is described with its kernels below):
+// Five placements of the band (the register and lane ones are described with their kernels below):
 //  * windowed (batches >= 128, or whenever the whole band does not fit LDS): the step at column j only
 //    touches columns j .. j + kl + ku, so LDS holds a circular window of kl + ku + 2 columns; column j is
 //    stored to HBM with one coalesced write as it leaves and column j + kl + ku + 1 is loaded; pivots and
@@ -26,6 +26,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <mutex>
 #include <string>
 #include <type_traits>
 
@@ -705,6 +706,262 @@ __global__ void __launch_bounds__(64) k_band_solve_reg_multi(int n, int kl, int 
 }
 
 // ---------------------------------------------------------------------------------------------------
+// lane placement: one lane per instance (large batches of narrow bands)
+// ---------------------------------------------------------------------------------------------------
+// Once the batch alone fills the chip, a wavefront per instance spends every column step on cross-lane
+// operations for one instance while thousands of such waves queue for the CUs.  Here a lane owns an instance
+// and runs dgbtf2's column loop on its own register window — rows j .. j + K, columns j .. j + 2K, K = max(kl,
+// ku) <= 8 a compile-time bound — so a step is plain FP64 arithmetic: the pivot row (lane-varying) is exchanged
+// by selects, the window slides by register moves, and the next row of the band enters from a D-step-deep
+// prefetch.  Same storage, pivots and zero-pivot convention as the other placements (the factors are
+// interchangeable).  Every lane stores every step (to its sink slot when it has nothing to store), so no store
+// sits under a branch and the waits for the prefetches count exactly.
+constexpr int kLaneD = 2;  // prefetch depth (steps)
+
+// Element strides: band entry e (LAPACK column-major index within the instance) at ab[e ae], pivot j at
+// piv[j pe], right-hand-side entry i at x[i xe] — 1 for the caller's instance-major arrays, the batch for the
+// instance-minor copies of the coalesced path.
+template <int K>
+__device__ __forceinline__ void lane_solve(int n, int kl, int ku, const double* ab, int64_t ae, const int32_t* piv,
+                                           int64_t pe, double* x, int64_t xe) {
+    constexpr int KV = 2 * K, D = kLaneD;
+    const int ldab = 2 * kl + ku + 1, kv = kl + ku;
+    if (kl > 0) {  // x <- L^-1 P x: the window holds x[j .. j + K]
+        auto lok = [&](int j, int i) { return i <= kl && j + i < n; };
+        auto lget = [&](int j, int i) { return ab[(lok(j, i) ? (int64_t)j * ldab + kv + i : 0) * ae]; };
+        auto eok = [&](int j) { return j + 1 + K < n; };
+        auto eget = [&](int j) { return x[(eok(j) ? j + 1 + K : 0) * xe]; };
+        double xw[K + 1];
+        static_for<0, K + 1>([&](auto I) CFX_INLINE {
+            constexpr int i = decltype(I)::value;
+            xw[i] = i < n ? x[i * xe] : 0.0;
+        });
+        double lp[D][K + 1], ep[D];
+        int pp[D];
+        static_for<0, D>([&](auto S_) CFX_INLINE {
+            constexpr int s = decltype(S_)::value;
+            static_for<1, K + 1>([&](auto I) CFX_INLINE { lp[s][decltype(I)::value] = lget(s, decltype(I)::value); });
+            ep[s] = eget(s);
+            pp[s] = piv[min(s, n - 1) * pe];
+        });
+        auto step = [&](int j, double (&lps)[K + 1], double& eps, int& pps, int jpre) CFX_INLINE {
+            double lv[K + 1], ev = eok(j) ? eps : 0.0;
+            int p = pps - j;
+            static_for<1, K + 1>([&](auto I) CFX_INLINE {
+                constexpr int i = decltype(I)::value;
+                lv[i] = lok(j, i) ? lps[i] : 0.0;
+                asm volatile("" : "+v"(lv[i])::"memory");
+                lps[i] = lget(jpre, i);
+            });
+            asm volatile("" : "+v"(ev), "+v"(p)::"memory");
+            eps = eget(jpre);
+            pps = piv[min(jpre, n - 1) * pe];
+            double x0 = xw[0];
+            static_for<1, K + 1>([&](auto I) CFX_INLINE {
+                constexpr int i = decltype(I)::value;
+                const double t = xw[i];
+                xw[i] = p == i ? xw[0] : t;
+                x0 = p == i ? t : x0;
+            });
+            x[j * xe] = x0;
+            static_for<1, K + 1>([&](auto I) CFX_INLINE {
+                constexpr int i = decltype(I)::value;
+                xw[i - 1] = xw[i] - lv[i] * x0;
+            });
+            xw[K] = ev;
+        };
+        int j0 = 0;
+        for (; j0 + D <= n - 1; j0 += D)
+            static_for<0, D>([&](auto S_) CFX_INLINE {
+                constexpr int s = decltype(S_)::value;
+                step(j0 + s, lp[s], ep[s], pp[s], j0 + s + D);
+            });
+        static_for<0, D>([&](auto S_) CFX_INLINE {
+            constexpr int s = decltype(S_)::value;
+            if (j0 + s < n - 1) step(j0 + s, lp[s], ep[s], pp[s], n);
+        });
+        x[(n - 1) * xe] = xw[0];
+        __threadfence();  // the backward pass re-reads what this one stored
+    }
+    // x <- U^-1 x: the window holds x[j - KV .. j] reversed (xw[t] = x[j - t])
+    auto uok = [&](int j, int t) { return j >= 0 && t <= kv && j - t >= 0; };
+    auto uget = [&](int j, int t) { return ab[(uok(j, t) ? (int64_t)j * ldab + kv - t : 0) * ae]; };
+    auto eok = [&](int j) { return j - 1 - KV >= 0; };
+    auto eget = [&](int j) { return x[(eok(j) ? j - 1 - KV : 0) * xe]; };
+    double xw[KV + 1];
+    static_for<0, KV + 1>([&](auto T) CFX_INLINE {
+        constexpr int t = decltype(T)::value;
+        xw[t] = n - 1 - t >= 0 ? x[(n - 1 - t) * xe] : 0.0;
+    });
+    double up[D][KV + 1], ep[D];
+    static_for<0, D>([&](auto S_) CFX_INLINE {
+        constexpr int s = decltype(S_)::value;
+        static_for<0, KV + 1>([&](auto T) CFX_INLINE { up[s][decltype(T)::value] = uget(n - 1 - s, decltype(T)::value); });
+        ep[s] = eget(n - 1 - s);
+    });
+    auto step = [&](int j, double (&ups)[KV + 1], double& eps, int jpre) CFX_INLINE {
+        double uv[KV + 1], ev = eok(j) ? eps : 0.0;
+        static_for<0, KV + 1>([&](auto T) CFX_INLINE {
+            constexpr int t = decltype(T)::value;
+            uv[t] = uok(j, t) ? ups[t] : 0.0;
+            asm volatile("" : "+v"(uv[t])::"memory");
+            ups[t] = uget(jpre, t);
+        });
+        asm volatile("" : "+v"(ev)::"memory");
+        eps = eget(jpre);
+        const double xj = xw[0] / uv[0];
+        x[j * xe] = xj;
+        static_for<1, KV + 1>([&](auto T) CFX_INLINE {
+            constexpr int t = decltype(T)::value;
+            xw[t - 1] = xw[t] - uv[t] * xj;
+        });
+        xw[KV] = ev;
+    };
+    int j0 = n - 1;
+    for (; j0 - D + 1 >= 0; j0 -= D)
+        static_for<0, D>([&](auto S_) CFX_INLINE {
+            constexpr int s = decltype(S_)::value;
+            step(j0 - s, up[s], ep[s], j0 - s - D);
+        });
+    static_for<0, D>([&](auto S_) CFX_INLINE {
+        constexpr int s = decltype(S_)::value;
+        if (j0 - s >= 0) step(j0 - s, up[s], ep[s], -1);
+    });
+}
+
+// instance b's arrays start at b * *_inst; element strides as lane_solve (x_rhs: between right-hand sides)
+struct LaneLayout {
+    int64_t ab_inst, ab_el, pv_inst, pv_el, x_inst, x_el, x_rhs;
+};
+
+template <int K>
+__global__ void __launch_bounds__(64) k_band_lu_lane(int64_t batch, int n, int kl, int ku, int nrhs,
+                                                     double* __restrict__ AB, int32_t* __restrict__ IPIV,
+                                                     double* __restrict__ RHS, int32_t* __restrict__ INFO,
+                                                     LaneLayout L) {
+    constexpr int KW = 2 * K + 1, D = kLaneD;
+    const int64_t b = (int64_t)blockIdx.x * 64 + threadIdx.x;
+    if (b >= batch) return;
+    const int ldab = 2 * kl + ku + 1, kv = kl + ku;  // n * ldab < 2^31 (checked at dispatch)
+    const int64_t ae = L.ab_el, pe = L.pv_el;
+    double* ab = AB + b * L.ab_inst;
+    int32_t* piv = IPIV + b * L.pv_inst;
+    double* const sink = block_sink() + threadIdx.x;  // stores with nothing to store land here
+    int32_t* const isink = reinterpret_cast<int32_t*>(block_sink() + 64 * 4) + threadIdx.x;
+    // A(i, c) of the original band: i - c <= kl, c - i <= ku, inside the matrix
+    auto bok = [&](int i, int c) { return i < n && c < n && i - c <= kl && c - i <= ku; };
+    auto bget = [&](int i, int c) { return ab[(bok(i, c) ? (int64_t)c * ldab + kv + i - c : 0) * ae]; };
+    double W[K + 1][KW];  // W[i][c] = A(j + i, j + c) of the current step
+    static_for<0, K + 1>([&](auto I) CFX_INLINE {
+        constexpr int i = decltype(I)::value;
+        static_for<0, KW>([&](auto C_) CFX_INLINE {
+            constexpr int c = decltype(C_)::value;
+            W[i][c] = bok(i, c) ? bget(i, c) : 0.0;
+        });
+    });
+    for (int c = 0; c < min(kv, n); ++c)  // fill-in positions above the matrix, which no U row reaches
+        for (int q = 0; q < min(kl, kv - c); ++q) ab[((int64_t)c * ldab + q) * ae] = 0.0;
+    double nxt[D][KW];  // row j + 1 + K (columns j + 1 ..) enters after step j; fetched D steps ahead
+    static_for<0, D>([&](auto S_) CFX_INLINE {
+        constexpr int s = decltype(S_)::value;
+        static_for<0, KW>([&](auto C_) CFX_INLINE {
+            constexpr int c = decltype(C_)::value;
+            nxt[s][c] = bget(s + 1 + K, s + 1 + c);
+        });
+    });
+    int info = 0;
+    auto step = [&](int j, double (&pre)[KW], int jpre) CFX_INLINE {
+        double ent[KW];
+        static_for<0, KW>([&](auto C_) CFX_INLINE {
+            constexpr int c = decltype(C_)::value;
+            ent[c] = bok(j + 1 + K, j + 1 + c) ? pre[c] : 0.0;
+            asm volatile("" : "+v"(ent[c])::"memory");  // taken before this step's stores
+            pre[c] = bget(jpre + 1 + K, jpre + 1 + c);
+        });
+        // pivot: first largest |A(j + i, j)|
+        double best = fabs(W[0][0]);
+        int p = 0;
+        static_for<1, K + 1>([&](auto I) CFX_INLINE {
+            constexpr int i = decltype(I)::value;
+            const double a = fabs(W[i][0]);
+            p = a > best ? i : p;
+            best = fmax(best, a);
+        });
+        *(j < n ? piv + j * pe : isink) = j + p;
+        // U: row p; row p takes row 0
+        double U[KW];
+        static_for<0, KW>([&](auto C_) CFX_INLINE { U[decltype(C_)::value] = W[0][decltype(C_)::value]; });
+        static_for<1, K + 1>([&](auto I) CFX_INLINE {
+            constexpr int i = decltype(I)::value;
+            static_for<0, KW>([&](auto C_) CFX_INLINE {
+                constexpr int c = decltype(C_)::value;
+                const double t = W[i][c];
+                W[i][c] = p == i ? W[0][c] : t;
+                U[c] = p == i ? t : U[c];
+            });
+        });
+        static_for<0, KW>([&](auto C_) CFX_INLINE {  // U(j, j + c) at band row kv - c of column j + c
+            constexpr int c = decltype(C_)::value;
+            *(c <= kv && j + c < n ? ab + ((int64_t)(j + c) * ldab + kv - c) * ae : sink) = U[c];
+        });
+        const double inv = U[0] != 0.0 ? 1.0 / U[0] : 0.0;  // zero pivot: zero column, zero multipliers
+        if (U[0] == 0.0 && info == 0) info = j + 1;
+        static_for<1, K + 1>([&](auto I) CFX_INLINE {
+            constexpr int i = decltype(I)::value;
+            const double l = W[i][0] * inv;
+            *(i <= kl && j + i < n ? ab + ((int64_t)j * ldab + kv + i) * ae : sink) = l;
+            static_for<1, KW>([&](auto C_) CFX_INLINE {
+                constexpr int c = decltype(C_)::value;
+                W[i - 1][c - 1] = W[i][c] - l * U[c];  // update and slide up-left in one move
+            });
+            W[i - 1][KW - 1] = 0.0;
+        });
+        static_for<0, KW>([&](auto C_) CFX_INLINE { W[K][decltype(C_)::value] = ent[decltype(C_)::value]; });
+    };
+    int j0 = 0;
+    for (; j0 + D <= n; j0 += D)
+        static_for<0, D>([&](auto S_) CFX_INLINE {
+            constexpr int s = decltype(S_)::value;
+            step(j0 + s, nxt[s], j0 + s + D);
+        });
+    static_for<0, D>([&](auto S_) CFX_INLINE {  // the last steps prefetch nothing (their rows are past n)
+        constexpr int s = decltype(S_)::value;
+        if (j0 + s < n) step(j0 + s, nxt[s], n);
+    });
+    INFO[b] = info;
+    if (nrhs > 0) __threadfence();  // the solve reads the factors stored above
+    for (int c = 0; c < nrhs; ++c) lane_solve<K>(n, kl, ku, ab, ae, piv, pe, RHS + b * L.x_inst + c * L.x_rhs, L.x_el);
+}
+
+template <int K>
+__global__ void __launch_bounds__(64) k_band_solve_lane(int64_t batch, int n, int kl, int ku, int nrhs,
+                                                        const double* __restrict__ AB, const int32_t* __restrict__ IPIV,
+                                                        double* __restrict__ RHS) {
+    const int64_t b = (int64_t)blockIdx.x * 64 + threadIdx.x;
+    if (b >= batch) return;
+    const int64_t ldab = 2 * kl + ku + 1;
+    for (int c = 0; c < nrhs; ++c)
+        lane_solve<K>(n, kl, ku, AB + b * n * ldab, 1, IPIV + b * n, 1, RHS + (b * nrhs + c) * (int64_t)n, 1);
+}
+
+// [rows][cols] -> [cols][rows] through 64 x 64 LDS tiles (the coalesced lane path's instance-minor copies)
+template <class T>
+__global__ void __launch_bounds__(256) k_band_transpose(const T* __restrict__ src, T* __restrict__ dst, int64_t rows,
+                                                        int64_t cols) {
+    __shared__ T tile[64][65];
+    const int64_t r0 = (int64_t)blockIdx.x * 64;
+    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+    for (int64_t c0 = (int64_t)blockIdx.y * 64; c0 < cols; c0 += (int64_t)gridDim.y * 64) {
+        for (int r = ty; r < 64; r += 4)
+            if (r0 + r < rows && c0 + tx < cols) tile[r][tx] = src[(r0 + r) * cols + c0 + tx];
+        __syncthreads();
+        for (int r = ty; r < 64; r += 4)
+            if (c0 + r < cols && r0 + tx < rows) dst[(c0 + r) * rows + r0 + tx] = tile[tx][r];
+        __syncthreads();
+    }
+}
+
+// ---------------------------------------------------------------------------------------------------
 // dispatch
 // ---------------------------------------------------------------------------------------------------
 // Raise a kernel's dynamic-LDS limit above 64 KiB only when a launch needs more than it was last raised to (one
@@ -792,6 +1049,84 @@ static hipError_t reg_dispatch(int64_t n, int32_t kl, int32_t ku, int64_t batch,
 #undef CFX_REG
 }
 
+// Lane placement: batches of at least kLaneBatch instances with max(kl, ku) <= kLaneMaxK.  Each lane runs its
+// instance's ~30-instruction-deep dependent chain per column alone (one wave per SIMD, nothing to hide the
+// latency: ~4.4 us per column against the register kernel's ~0.3 us), so it only wins once the register kernel's
+// waves queue for the CUs — cfg-3 KKT (n = 502, kl = ku = 6), factor + solve: 0.51 / 2.29 ms (register / lane) at
+// 1,024 instances, 1.74 / 2.56 at 4,096, 7.75 / 3.66 at 16,384; solve alone 2.54 / 0.79 ms at 16,384
+// (scripts/band_lane_probe.py, profiles/round2/band_lane_probe.jsonl).
+constexpr int64_t kLaneBatch = 8192;
+constexpr int kLaneMaxK = 8;
+static bool lane_ok(int64_t n, int32_t kl, int32_t ku) {
+    return std::max(kl, ku) <= kLaneMaxK && n * (2 * (int64_t)kl + ku + 1) < ((int64_t)1 << 31);
+}
+// Device workspace of the coalesced lane path (instance-minor copies of the band, pivots and right-hand sides):
+// grown on demand, one per device, kept for the process.
+static std::mutex g_lane_ws_mutex;
+static void* g_lane_ws[64];
+static size_t g_lane_ws_bytes[64];
+static void* lane_workspace(size_t bytes) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+    std::lock_guard<std::mutex> lock(g_lane_ws_mutex);
+    if (g_lane_ws_bytes[dev] < bytes) {
+        if (g_lane_ws[dev]) (void)hipFree(g_lane_ws[dev]);
+        g_lane_ws[dev] = nullptr;
+        g_lane_ws_bytes[dev] = 0;
+        if (hipMalloc(&g_lane_ws[dev], bytes) != hipSuccess) return nullptr;
+        g_lane_ws_bytes[dev] = bytes;
+    }
+    return g_lane_ws[dev];
+}
+template <class T>
+static void transpose(const T* src, T* dst, int64_t rows, int64_t cols, hipStream_t s) {
+    const dim3 grid((unsigned)((rows + 63) / 64), (unsigned)std::min<int64_t>((cols + 63) / 64, 65535));
+    hipLaunchKernelGGL(k_band_transpose<T>, grid, dim3(256), 0, s, src, dst, rows, cols);
+}
+
+template <int K>
+static hipError_t launch_lane_k(int64_t n, int32_t kl, int32_t ku, int64_t batch, double* ab, int32_t* ipiv,
+                                int32_t* info, int32_t nrhs, double* rhs, hipStream_t s, int factor) {
+    const dim3 grid((unsigned)((batch + 63) / 64));
+    const int64_t ldab = 2 * (int64_t)kl + ku + 1, len = n * ldab, xl = (int64_t)nrhs * n;
+    if (factor && !std::getenv("CFX_BAND_LANE_DIRECT")) {
+        // coalesced: every lane access of a wave is one contiguous 512-byte run in the instance-minor copies
+        const size_t bytes = (size_t)batch * ((len + xl) * sizeof(double) + n * sizeof(int32_t));
+        double* wab = static_cast<double*>(lane_workspace(bytes));
+        if (!wab) return hipErrorOutOfMemory;
+        double* wx = wab + batch * len;
+        int32_t* wp = reinterpret_cast<int32_t*>(wx + batch * xl);
+        transpose<double>(ab, wab, batch, len, s);
+        if (nrhs) transpose<double>(rhs, wx, batch, xl, s);
+        const LaneLayout L{1, batch, 1, batch, 1, batch, n * batch};
+        hipLaunchKernelGGL(k_band_lu_lane<K>, grid, dim3(64), 0, s, batch, (int)n, kl, ku, nrhs, wab, wp, wx, info, L);
+        transpose<double>(wab, ab, len, batch, s);
+        transpose<int32_t>(wp, ipiv, n, batch, s);
+        if (nrhs) transpose<double>(wx, rhs, xl, batch, s);
+    } else if (factor) {
+        const LaneLayout L{len, 1, n, 1, xl, 1, n};
+        hipLaunchKernelGGL(k_band_lu_lane<K>, grid, dim3(64), 0, s, batch, (int)n, kl, ku, nrhs, ab, ipiv, rhs, info, L);
+    } else
+        hipLaunchKernelGGL(k_band_solve_lane<K>, grid, dim3(64), 0, s, batch, (int)n, kl, ku, nrhs,
+                           (const double*)ab, (const int32_t*)ipiv, rhs);
+    return hipGetLastError();
+}
+static hipError_t lane_dispatch(int64_t n, int32_t kl, int32_t ku, int64_t batch, double* ab, int32_t* ipiv,
+                                int32_t* info, int32_t nrhs, double* rhs, hipStream_t s, int factor) {
+#define CFX_LANE(K) launch_lane_k<K>(n, kl, ku, batch, ab, ipiv, info, nrhs, rhs, s, factor)
+    switch (std::max(std::max(kl, ku), 1)) {
+        case 1: return CFX_LANE(1);
+        case 2: return CFX_LANE(2);
+        case 3: return CFX_LANE(3);
+        case 4: return CFX_LANE(4);
+        case 5: return CFX_LANE(5);
+        case 6: return CFX_LANE(6);
+        case 7: return CFX_LANE(7);
+        default: return CFX_LANE(8);
+    }
+#undef CFX_LANE
+}
+
 static int band_launch(int64_t n, int32_t kl, int32_t ku, int64_t batch, double* ab, int32_t* ipiv, int32_t* info,
                        int32_t nrhs, double* rhs, void* stream, int factor) {
     if (n < 1 || n > (1 << 24) || kl < 0 || ku < 0 || kl >= n || ku >= n || batch < 1 || batch > 0x7fffffff ||
@@ -809,15 +1144,20 @@ static int band_launch(int64_t n, int32_t kl, int32_t ku, int64_t batch, double*
     // placement: the register kernels whenever the window fits a wavefront's registers; otherwise small
     // batches keep the whole band resident when it fits LDS (latency-bound), larger ones use the window,
     // and bands too wide for both run on the global copy.  CFX_BAND_PLACEMENT=0..3 forces one (where it
-    // fits); CFX_BAND_FULL forces resident / global.
+    // fits; 4: the lane placement); CFX_BAND_FULL forces resident / global.  Batches of >= kLaneBatch narrow
+    // bands take the lane placement.
     int placement;
     const bool force_full = std::getenv("CFX_BAND_FULL") != nullptr;
     const char* forced = std::getenv("CFX_BAND_PLACEMENT");
     const bool win_ok = lds_win <= (size_t)kBandLds && chunk >= 4;
     // the register solve (one wave per instance) loses to the windowed one once the batch fills the chip
     const bool reg_ok = reg_chunks(n, kl, ku) > 0 && (factor || batch < 2048 || !win_ok);
-    if (forced && *forced == '3' && reg_chunks(n, kl, ku) > 0)
+    if (forced && *forced == '4' && lane_ok(n, kl, ku))
+        placement = 4;
+    else if (forced && *forced == '3' && reg_chunks(n, kl, ku) > 0)
         placement = 3;
+    else if (!force_full && !forced && batch >= kLaneBatch && lane_ok(n, kl, ku))
+        placement = 4;
     else if (forced && *forced == '0' && win_ok)
         placement = 0;
     else if (forced && (*forced == '1' || *forced == '2'))
@@ -833,7 +1173,9 @@ static int band_launch(int64_t n, int32_t kl, int32_t ku, int64_t batch, double*
     const int64_t work = (int64_t)kl * (kl + ku);
     const hipStream_t s = (hipStream_t)stream;
     hipError_t e;
-    if (placement == 3)
+    if (placement == 4)
+        e = lane_dispatch(n, kl, ku, batch, ab, ipiv, info, nrhs, rhs, s, factor);
+    else if (placement == 3)
         e = reg_dispatch(n, kl, ku, batch, ab, ipiv, info, nrhs, rhs, s, factor);
     else if (work <= 192)
         e = launch_nt<64>(placement, n, kl, ku, batch, ab, ipiv, info, nrhs, rhs, s, factor, lds, chunk);

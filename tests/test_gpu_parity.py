@@ -494,6 +494,47 @@ def test_band_lu_large_batch_factor_then_solve(n):
     assert np.max(np.abs(x2s[pick] - ref)) <= 1e-13 * cond * n * max(1.0, np.abs(ref).max())
 
 
+@pytest.mark.parametrize("B,n,kl,ku,zero_diag", [(1100, 502, 6, 6, True), (64, 60, 6, 6, True), (70, 37, 3, 1, False),
+                                                 (65, 100, 8, 8, True), (64, 50, 0, 2, False), (64, 80, 5, 2, True),
+                                                 (64, 9, 8, 8, False), (3, 1, 0, 0, False)])
+def test_band_lu_lane_placement(B, n, kl, ku, zero_diag, monkeypatch):
+    """The lane placement (one lane per instance, large batches of bands with max(kl, ku) <= 8; forced here with
+    CFX_BAND_PLACEMENT=4) against the register placement (same factors, pivots and solutions) and numpy's dense
+    solve; factors of one placement solve with the other's kernels."""
+    import torch
+
+    from cocofest_amd import _cfx
+
+    rng = np.random.default_rng(B + n + kl)
+    A, ab = _band_system(rng, B, n, kl, ku, zero_diag=zero_diag)
+    rhs = rng.standard_normal((B, 2, n))
+    outs = {}
+    for pl in ("4", "3"):
+        monkeypatch.setenv("CFX_BAND_PLACEMENT", pl)
+        abt = torch.tensor(ab, device="cuda")
+        ipiv = torch.empty((B, n), dtype=torch.int32, device="cuda")
+        info = torch.empty((B,), dtype=torch.int32, device="cuda")
+        x = torch.tensor(rhs, device="cuda")
+        _cfx.band_lu(abt, ipiv, info, kl, ku, rhs=x)
+        monkeypatch.setenv("CFX_BAND_PLACEMENT", "3" if pl == "4" else "4")  # solve with the other placement
+        x2 = torch.tensor(rhs[:, 1:], device="cuda")
+        _cfx.band_lu_solve(abt, ipiv, kl, ku, x2)
+        torch.cuda.synchronize()
+        outs[pl] = (abt.cpu().numpy()[:, :, kl:], ipiv.cpu().numpy(), info.cpu().numpy(), x.cpu().numpy(),
+                    x2.cpu().numpy())
+    lane, reg = outs["4"], outs["3"]
+    np.testing.assert_array_equal(lane[1], reg[1])
+    np.testing.assert_array_equal(lane[2], 0)
+    np.testing.assert_allclose(lane[0], reg[0], rtol=1e-12, atol=1e-12)
+    scale = np.abs(reg[3]).max()  # solutions: the two placements round in a different order
+    np.testing.assert_allclose(lane[3], reg[3], rtol=1e-9, atol=1e-11 * scale)
+    np.testing.assert_allclose(lane[4], lane[3][:, 1:], rtol=1e-9, atol=1e-11 * scale)
+    pick = rng.choice(B, min(B, 32), replace=False)
+    ref = np.linalg.solve(A[pick], rhs[pick].transpose(0, 2, 1)).transpose(0, 2, 1)
+    cond = np.linalg.cond(A[pick]).max()
+    assert np.max(np.abs(lane[3][pick] - ref)) <= 1e-13 * cond * n * max(1.0, np.abs(ref).max())
+
+
 def test_band_lu_reports_singular_and_bad_arguments():
     import torch
 
