@@ -132,6 +132,29 @@ __device__ double breduce(double v, Op op, double* sh) {
     return r;
 }
 
+// Several block-wide reductions with one pair of barriers: v[i] reduced with op[i] (0 sum, 1 max, 2 min), each in
+// breduce's order, so every value is bit-identical to its own breduce.
+template <int N>
+__device__ void breduce_n(double (&v)[N], const int (&op)[N]) {
+    __shared__ double shn[kIB / 64][N];
+    auto apply = [&](int i, double a, double c) { return op[i] == 0 ? a + c : (op[i] == 1 ? max_n(a, c) : min_n(a, c)); };
+    for (int o = 32; o > 0; o >>= 1)
+#pragma unroll
+        for (int i = 0; i < N; ++i) v[i] = apply(i, v[i], __shfl_xor(v[i], o, 64));
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0)
+#pragma unroll
+        for (int i = 0; i < N; ++i) shn[threadIdx.x >> 6][i] = v[i];
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        double r = shn[0][i];
+#pragma unroll
+        for (int w = 1; w < kIB / 64; ++w) r = apply(i, r, shn[w][i]);
+        v[i] = r;
+    }
+}
+
 // counter slot: thread 0 of block 0 clears the next slot (the next counting kernel runs after this one)
 __device__ inline void count_add(const IpmK& K, int slot, int which, int v) {
     if (threadIdx.x == 0) {
@@ -190,9 +213,14 @@ __device__ double barrier_obj(const IpmK& K, int64_t b, const double* x, double 
             sU += log(clamp_lo(su, 1e-300));
         }
     }
-    sL = breduce(sL, OpSum(), sh);
-    sU = breduce(sU, OpSum(), sh);
-    bad = breduce(bad, OpMax(), sh);
+    {
+        double rv[3] = {sL, sU, bad};
+        const int ro[3] = {0, 0, 1};
+        breduce_n(rv, ro);
+        sL = rv[0];
+        sU = rv[1];
+        bad = rv[2];
+    }
     return bad > 0 ? INFINITY : f - mu * (sL + sU);
 }
 
@@ -341,13 +369,18 @@ __global__ void __launch_bounds__(kIB) k_ipm_begin(const IpmK K, int mode, int s
         sy += fabs(y[j]);
         ep = max_n(ep, fabs(gS[j]));
     }
-    szl = breduce(szl, OpSum(), sh);
-    szu = breduce(szu, OpSum(), sh);
-    sy = breduce(sy, OpSum(), sh);
-    ed = breduce(ed, OpMax(), sh);
-    ep = breduce(ep, OpMax(), sh);
-    ecl = breduce(ecl, OpMax(), sh);
-    ecu = breduce(ecu, OpMax(), sh);
+    {
+        double rv[7] = {szl, szu, sy, ed, ep, ecl, ecu};
+        const int ro[7] = {0, 0, 0, 1, 1, 1, 1};
+        breduce_n(rv, ro);
+        szl = rv[0];
+        szu = rv[1];
+        sy = rv[2];
+        ed = rv[3];
+        ep = rv[4];
+        ecl = rv[5];
+        ecu = rv[6];
+    }
     const double smax = K.o.s_max;
     const double sd = clamp_lo((szl + szu + sy) / (2.0 * nf + m), smax) / smax;
     const double sc = clamp_lo((szl + szu) / (2.0 * nf), smax) / smax;
@@ -613,10 +646,15 @@ __global__ void __launch_bounds__(kIB) k_ipm_curv(const IpmK K, int slot) {
         dd += (sig[i] + S.dw) * dx[i] * dx[i];
         nrm += dx[i] * dx[i];
     }
-    quad = breduce(quad, OpSum(), sh);
-    dd = breduce(dd, OpSum(), sh);
-    nrm = breduce(nrm, OpSum(), sh);
-    nonfin = breduce(nonfin, OpMax(), sh);
+    {
+        double rv[4] = {quad, dd, nrm, nonfin};
+        const int ro[4] = {0, 0, 0, 1};
+        breduce_n(rv, ro);
+        quad = rv[0];
+        dd = rv[1];
+        nrm = rv[2];
+        nonfin = rv[3];
+    }
     const double curv = quad + dd;
     bool sing = false;
     for (int q = 0; q < K.P; ++q) sing = sing || K.info[b * K.P + q] != 0;
@@ -667,12 +705,17 @@ __global__ void __launch_bounds__(kIB) k_ipm_dir(const IpmK K, int it) {
         dphi += (gF[i] - bar) * dx[i];
     }
     for (int j = threadIdx.x; j < m; j += kIB) theta += fabs(K.gS[b * m + j]);
-    apl = breduce(apl, OpMin(), sh);
-    apu = breduce(apu, OpMin(), sh);
-    azl = breduce(azl, OpMin(), sh);
-    azu = breduce(azu, OpMin(), sh);
-    dphi = breduce(dphi, OpSum(), sh);
-    theta = breduce(theta, OpSum(), sh);
+    {
+        double rv[6] = {apl, apu, azl, azu, dphi, theta};
+        const int ro[6] = {2, 2, 2, 2, 0, 0};
+        breduce_n(rv, ro);
+        apl = rv[0];
+        apu = rv[1];
+        azl = rv[2];
+        azu = rv[3];
+        dphi = rv[4];
+        theta = rv[5];
+    }
     const double phi = barrier_obj(K, b, x, S.fS, mu, sh);
     const double a_p = min_n(clamp_hi(apl, 1.0), clamp_hi(apu, 1.0));
     // watchdog start (Ipopt StartWatchDog): remember this iterate and its line-search reference values
@@ -819,8 +862,13 @@ __global__ void __launch_bounds__(kIB) k_ipm_soc_trial(const IpmK K) {
         if (K.hasL[i]) apl = min_n(apl, step_term(true, x[i] - lbI[i], d, tau));
         if (K.hasU[i]) apu = min_n(apu, step_term(true, ubI[i] - x[i], -d, tau));
     }
-    apl = breduce(apl, OpMin(), sh);
-    apu = breduce(apu, OpMin(), sh);
+    {
+        double rv[2] = {apl, apu};
+        const int ro[2] = {2, 2};
+        breduce_n(rv, ro);
+        apl = rv[0];
+        apu = rv[1];
+    }
     const double a_c = min_n(clamp_hi(apl, 1.0), clamp_hi(apu, 1.0));
     double* xr = K.xr + b * nf;
     for (int i = threadIdx.x; i < nf; i += kIB) xr[i] = x[i] + a_c * rb[K.pos[i]];
@@ -888,9 +936,14 @@ __global__ void __launch_bounds__(kIB) k_ipm_resto_init(const IpmK K, int slot) 
         if (K.hasU[i]) apu = min_n(apu, step_term(true, ubI[i] - x[i], -d, S.tau));
     }
     for (int j = threadIdx.x; j < m; j += kIB) th += fabs(K.gS[b * m + j]);
-    apl = breduce(apl, OpMin(), sh);
-    apu = breduce(apu, OpMin(), sh);
-    th = breduce(th, OpSum(), sh);
+    {
+        double rv[3] = {apl, apu, th};
+        const int ro[3] = {2, 2, 0};
+        breduce_n(rv, ro);
+        apl = rv[0];
+        apu = rv[1];
+        th = rv[2];
+    }
     const double a = min_n(clamp_hi(apl, 1.0), clamp_hi(apu, 1.0));
     const bool failed = !S.accepted && !S.done;
     double* xr = K.xr + b * nf;
@@ -924,8 +977,13 @@ __global__ void __launch_bounds__(kIB) k_ipm_resto_accept(const IpmK K, int slot
         if (!isfinite(v)) nonfin = 1.0;
         tt += fabs(v);
     }
-    tt = breduce(tt, OpSum(), sh);
-    nonfin = breduce(nonfin, OpMax(), sh);
+    {
+        double rv[2] = {tt, nonfin};
+        const int ro[2] = {0, 1};
+        breduce_n(rv, ro);
+        tt = rv[0];
+        nonfin = rv[1];
+    }
     const bool ok = S.todo && !(nonfin > 0) && (tt < S.theta_r);
     const double* x = K.x + b * nf;
     const double* dxr = K.dxr + b * nf;
@@ -962,8 +1020,13 @@ __global__ void __launch_bounds__(kIB) k_ipm_lsmult(const IpmK K) {
         if (!isfinite(v)) nonfin = 1.0;
         big = max_n(big, fabs(v));
     }
-    big = breduce(big, OpMax(), sh);
-    nonfin = breduce(nonfin, OpMax(), sh);
+    {
+        double rv[2] = {big, nonfin};
+        const int ro[2] = {1, 1};
+        breduce_n(rv, ro);
+        big = rv[0];
+        nonfin = rv[1];
+    }
     const bool ok = !(nonfin > 0) && big <= 1e3;
     for (int j = threadIdx.x; j < m; j += kIB) K.y[b * m + j] = ok ? rb[K.pos[nf + j]] : 0.0;
     if (threadIdx.x == 0) K.sc[b].reinit = 0;
@@ -1012,8 +1075,13 @@ __global__ void __launch_bounds__(kIB) k_ipm_update(const IpmK K, int resto) {
         if (!isfinite(dy[j])) nfy = 1.0;
     for (int i = threadIdx.x; i < nf; i += kIB)
         if (!isfinite(dzl[i]) || !isfinite(dzu[i])) nfz = 1.0;
-    nfy = breduce(nfy, OpMax(), sh);
-    nfz = breduce(nfz, OpMax(), sh);
+    {
+        double rv[2] = {nfy, nfz};
+        const int ro[2] = {1, 1};
+        breduce_n(rv, ro);
+        nfy = rv[0];
+        nfz = rv[1];
+    }
     const bool mv = alpha > 0 && !(nfy > 0);
     const double az = (step && !failed) ? S.a_z : 0.0;
     const bool mz = az > 0 && !(nfz > 0);
