@@ -671,6 +671,11 @@ extern "C" int cfx_create(const cfx_problem* p, cfx_handle** out) {
     kp.mult = c.fl * c.fv + c.fp;
     kp.neg_mult = -kp.mult;
     kp.mult_km = kp.mult * c.km_rest;
+    kp.tau12 = c.tau1_rest + c.tau2;
+    kp.tau1km = c.tau1_rest * c.km_rest;
+    kp.hm = kp.h * kp.mult;
+    kp.hmkm = kp.hm * c.km_rest;
+    kp.hmkmt2 = kp.hmkm * c.tau2;
     {
         // instances per thread (Ding families): 2 side by side once the batch fills the chip twice over;
         // CFX_NI=1|2|4 overrides (tuning)
