@@ -111,20 +111,90 @@ def cpu_baseline(ocp, budget_s):
                       f"oracle/c/fes_oracle.c, OpenMP {threads} threads, {el:.1f} s"}
 
 
+def build_cfg3():
+    """BASELINE.json configs[2]: Ding2007 pulse width, 30 pulses (round(linspace(0, 1, 31)[:-1], 2)), N = 100,
+    truncation 10, force tracking of the reference force curve (Fourier 50), RK1 x 10."""
+    from cocofest_amd import ModelMaker, OcpFes, OdeSolver
+
+    ft = json.loads((ROOT / "tests" / "golden" / "ref_formulas.json").read_text())["misc"]["force_tracking"]
+    model = ModelMaker.create_model("ding2007", stim_time=[float(v) for v in np.round(np.linspace(0, 1, 31)[:-1], 2)],
+                                    sum_stim_truncation=10)
+    return OcpFes.prepare_ocp(model=model, final_time=1, pulse_width={"min": model.pd0, "max": 0.0006},
+                              objective={"force_tracking": [np.array(ft["time"]), np.array(ft["force"])]},
+                              ode_solver=OdeSolver.RK1(n_integration_steps=10))
+
+
+def cfg3_synthetic(ocp, B, seed):
+    """Instance-major decision vectors (B, nv) of cfg 3: Cn ~ U(0, 1.5), F ~ U(0, 250), pw ~ U(pd0, 6e-4)."""
+    rng = np.random.default_rng(seed)
+    nz = 3
+    per = np.array([1.5, 250.0, 0.0])
+    v = rng.uniform(0.0, 1.0, (B, ocp.nv))
+    for k in range(ocp.nv):
+        e = k % nz
+        v[:, k] = v[:, k] * per[e] if e < 2 else ocp.model.pd0 + v[:, k] * (6e-4 - ocp.model.pd0)
+    return v
+
+
+def cfg3_section(device, cpu_seconds, steps=50, B=1 << 18):
+    """BASELINE.json configs[2] callback throughput: g + J_g of cfg 3 (the fused Euler step of Ding2007, one pulse
+    width per interval) over a device-resident CFX_LAYOUT_TILED64 batch, HIP events on the launch stream; its
+    algorithmic HBM rate (read v, write g and J_g values) and the C port on the host cores on a bounded sample."""
+    import torch
+
+    from oracle import c_oracle, fes_oracle as O
+
+    ocp = build_cfg3()
+    dev = f"cuda:{device}"
+    h = ocp.nlp(batch=B, layout="tiled64", device=device)
+    va = cfg3_synthetic(ocp, B, seed=0)
+    v = to_tiled(torch.from_numpy(np.ascontiguousarray(va.T)).to(dev))
+    g = torch.empty((B // 64, h.ng, 64), dtype=torch.float64, device=dev)
+    jac = torch.empty((B // 64, h.nnz_jac, 64), dtype=torch.float64, device=dev)
+    for _ in range(5):
+        h.eval_all(v, g=g, jac=jac)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(steps):
+        h.eval_all(v, g=g, jac=jac)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / steps
+    nbytes = 8 * (h.nv + h.ng + h.nnz_jac)
+    out = {"workload": "cfg3: OcpFes DingModelPulseWidthFrequency, 30 pulses, n_shooting=100, truncation 10, force "
+                       "tracking, RK1 x 10; one launch = g + J_g of every instance",
+           "batch": B, "nv": h.nv, "ng": h.ng, "nnz_jac": h.nnz_jac, "layout": "CFX_LAYOUT_TILED64",
+           "ms_per_launch": ms, "instance_evals_per_s": B / (ms * 1e-3),
+           "achieved_GBps": nbytes * B / (ms * 1e-3) / 1e9, "bytes_per_instance": nbytes, "cpu_baseline": None}
+    h.close()
+    if cpu_seconds > 0:
+        threads = min(16, len(os.sched_getaffinity(0)))
+        pb = O.Problem(name="ding2007", c=O.model_constants("ding2007"), n_shooting=ocp.n_shooting, final_time=1.0,
+                       truncation=10, rows=ocp.stim_rows, scheme="RK1", n_steps=10)
+        chunk = 1024
+        c_oracle.shooting(pb, va[:64], threads=threads)
+        done, t0 = 0, time.perf_counter()
+        while True:
+            c_oracle.shooting(pb, va[:chunk], threads=threads)
+            done += chunk
+            el = time.perf_counter() - t0
+            if el >= cpu_seconds:
+                break
+        out["cpu_baseline"] = {"value": done / el, "unit": "instance-evals/s", "cores": threads, "kind": "port",
+                               "sample": f"{done} cfg-3 instances (g + J_g, as-written calcium sum), "
+                                         f"oracle/c/fes_oracle.c, OpenMP {threads} threads, {el:.1f} s"}
+    return out
+
+
 def convergence(device):
     """Second half of the BASELINE metric: wall-clock to an Ipopt-equivalent KKT point (tol 1e-6) of the batched
     interior-point driver over libcfx (cocofest_amd/solver.py), single instance and multi-start batch."""
-    from cocofest_amd import ModelMaker, OcpFes, OdeSolver
     from cocofest_amd.solver import IpmOptions, NativeIpm
 
     out = {}
     # cfg 3: Ding2007 pulse width, 30 pulses, N = 100, force tracking (reference force curve), RK1 x 10
-    ft = json.loads((ROOT / "tests" / "golden" / "ref_formulas.json").read_text())["misc"]["force_tracking"]
-    model = ModelMaker.create_model("ding2007", stim_time=[float(v) for v in np.round(np.linspace(0, 1, 31)[:-1], 2)],
-                                    sum_stim_truncation=10)
-    ocp3 = OcpFes.prepare_ocp(model=model, final_time=1, pulse_width={"min": model.pd0, "max": 0.0006},
-                              objective={"force_tracking": [np.array(ft["time"]), np.array(ft["force"])]},
-                              ode_solver=OdeSolver.RK1(n_integration_steps=10))
+    ocp3 = build_cfg3()
     cases = {"cfg3_single": (ocp3, 1), "cfg3_multistart_256": (ocp3, 256), "cfg3_multistart_4096": (ocp3, 4096),
              "cfg2_single": (build_problem(), 1)}
     for name, (ocp, B) in cases.items():
@@ -476,6 +546,7 @@ def main():
         conv = convergence(local) if (world == 1 and not args.no_solve) else None
         ivp = ivp_section(local) if (world == 1 and not args.no_solve) else None
         col = collocation_section(local) if (world == 1 and not args.no_solve) else None
+        c3 = cfg3_section(local, args.cpu_seconds / 4) if (world == 1 and not args.no_solve) else None
         msk = msk_tp
         if msk_tp is not None and world == 1 and not args.no_solve:
             msk = msk_section(local, msk_tp, msk_ocp, cpu_seconds=args.cpu_seconds / 2)
@@ -515,6 +586,7 @@ def main():
             "convergence": conv,
             "ivp": ivp,
             "collocation": col,
+            "cfg3_callbacks": c3,
             "nmpc": nm,
             "msk": msk,
         }
