@@ -1,5 +1,6 @@
 """Batch-1 native interior point wall-clock (cfg 3 and cfg 2 single solves, best of 5) for the counter-read mode in
-the environment (CFX_IPM_PUB=launch: a separate k_ipm_publish launch per read; default: in-kernel publish)."""
+the environment (CFX_IPM_PUB=launch: a separate k_ipm_publish launch per read; default: in-kernel publish).  The
+in-kernel mode was measured (profiles/round2/ipm_pub/) and not kept; the probe now times the shipped mode either way."""
 import json
 import os
 import sys
