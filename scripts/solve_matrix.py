@@ -39,21 +39,26 @@ def cases():
 
 
 def main():
-    from cocofest_amd.solver import BatchedIpm, IpmOptions
+    """usage: solve_matrix.py [--native] [name filters...]; --native: the native interior point (cfx_ipm, the product
+    path of OcpFes.solve) instead of the torch-orchestrated BatchedIpm of round 1."""
+    from cocofest_amd.solver import BatchedIpm, IpmOptions, NativeIpm
 
     res = {}
-    only = sys.argv[1:]
+    native = "--native" in sys.argv[1:]
+    only = [a for a in sys.argv[1:] if a != "--native"]
     for name, ocp in cases().items():
         if only and not any(o in name for o in only):
             continue
         t0 = time.perf_counter()
         try:
-            ipm = BatchedIpm(ocp, batch=1, options=IpmOptions(tol=1e-6, max_iter=300))
+            opts = IpmOptions(tol=1e-6, max_iter=300)
+            ipm = NativeIpm(ocp, batch=1, device=0, options=opts) if native else BatchedIpm(ocp, batch=1, options=opts)
             r = ipm.solve()
             ipm.close()
             res[name] = {"converged": bool(r.converged[0]), "iters": int(r.iterations[0]), "f": float(r.f[0]),
-                         "kkt": float(r.kkt_error[0]), "wall": round(time.perf_counter() - t0, 3),
-                         "nK": ipm.nK, "kl": ipm.kl}
+                         "kkt": float(r.kkt_error[0]), "wall": round(time.perf_counter() - t0, 3)}
+            if not native:
+                res[name].update(nK=ipm.nK, kl=ipm.kl)
         except Exception as e:  # report, keep going
             res[name] = {"error": repr(e)[:200]}
         print(name, res[name], flush=True, file=sys.stderr)
