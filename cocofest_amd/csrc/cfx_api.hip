@@ -1067,15 +1067,31 @@ extern "C" int cfx_msk_create(const cfx_msk_problem* p, cfx_handle** out) {
     h->scheme = p->scheme, h->stages = S, h->device = p->device;
 
     // ---- constants
+    // Every joint turned into a rotation about its frame's z axis, so the kernels carry no per-joint axis selects:
+    // frame j is replaced by R'_j = R_j P_j, whose columns are R_j's columns perm_j = (a, b, axis) — (1, 2, 0) for x,
+    // (2, 0, 1) for y, (0, 1, 2) for z — and R_j Rot_axis(q) P_j = R_j P_j Rot_z(q).  Quantities given in frame j
+    // follow: p' = P_j^T p (com, via points, markers), I' = P_j^T I P_j, and the constant joint transform becomes
+    // A'_j = P_{j-1}^T A_j P_j, t'_j = P_{j-1}^T t_j (P_{-1} = I, the ground).  World positions, axes, the mass
+    // matrix and every callback value are unchanged.
+    int perm[kMskMaxQ + 1][3];  // perm[j + 1]: frame j (perm[0]: the ground)
+    for (int e = 0; e < 3; ++e) perm[0][e] = e;
+    for (int j = 0; j < nq; ++j) {
+        const int ax = p->dof_axis[j];
+        for (int e = 0; e < 3; ++e) perm[j + 1][e] = (ax + 1 + e) % 3;
+    }
+    auto pf = [&](int frame) { return perm[frame + 1]; };  // frame -1: the ground
     MskGeom G;
     std::memset(&G, 0, sizeof(G));
     for (int j = 0; j < nq; ++j) {
-        G.axis[j] = p->dof_axis[j];
-        for (int e = 0; e < 9; ++e) G.A[j][e] = p->dof_frame[j * 12 + e];
-        for (int e = 0; e < 3; ++e) G.t[j][e] = p->dof_frame[j * 12 + 9 + e];
+        const int *pp = pf(j - 1), *pj = pf(j);
+        G.axis[j] = 2;
+        for (int r = 0; r < 3; ++r)
+            for (int c2 = 0; c2 < 3; ++c2) G.A[j][r * 3 + c2] = p->dof_frame[j * 12 + pp[r] * 3 + pj[c2]];
+        for (int e = 0; e < 3; ++e) G.t[j][e] = p->dof_frame[j * 12 + 9 + pp[e]];
         G.mass[j] = p->body_mass[j];
-        for (int e = 0; e < 3; ++e) G.com[j][e] = p->body_com[j * 3 + e];
-        for (int e = 0; e < 9; ++e) G.inertia[j][e] = p->body_inertia[j * 9 + e];
+        for (int e = 0; e < 3; ++e) G.com[j][e] = p->body_com[j * 3 + pj[e]];
+        for (int r = 0; r < 3; ++r)
+            for (int c2 = 0; c2 < 3; ++c2) G.inertia[j][r * 3 + c2] = p->body_inertia[j * 9 + pj[r] * 3 + pj[c2]];
     }
     for (int e = 0; e < 3; ++e) G.grav[e] = p->gravity[e];
     std::vector<double> rest(nx, 0.0);
@@ -1097,9 +1113,10 @@ extern "C" int cfx_msk_create(const cfx_msk_problem* p, cfx_handle** out) {
             }
             G.seg_frame[mi][ns][0] = mu.point_frame[i];
             G.seg_frame[mi][ns][1] = mu.point_frame[i + 1];
+            const int *p0 = pf(mu.point_frame[i]), *p1 = pf(mu.point_frame[i + 1]);
             for (int e = 0; e < 3; ++e) {
-                G.seg_pos[mi][ns][0][e] = a[e];
-                G.seg_pos[mi][ns][1][e] = e3[e];
+                G.seg_pos[mi][ns][0][e] = a[p0[e]];
+                G.seg_pos[mi][ns][1][e] = e3[p1[e]];
             }
             ++ns;
         }
@@ -1227,7 +1244,7 @@ extern "C" int cfx_msk_create(const cfx_msk_problem* p, cfx_handle** out) {
         d.jo = (int32_t)h->jrow.size();
         for (int e = 0; e < 2; ++e) {
             d.frame[e] = c.frame[e];
-            for (int a = 0; a < 3; ++a) d.pos[e][a] = c.pos[e][a];
+            for (int a = 0; a < 3; ++a) d.pos[e][a] = c.pos[e][pf(c.frame[e])[a]];  // in the z-axis frame (above)
         }
         for (int r = 0; r < d.nrow; ++r)
             for (int j = 0; j < d.nd; ++j) {

@@ -159,7 +159,7 @@ struct MskMuscleConst {
 };
 
 struct MskGeom {
-    int32_t axis[kMskMaxQ];        // 0 / 1 / 2: rotation about the frame's x / y / z
+    int32_t axis[kMskMaxQ];        // always 2: cfx_msk_create turns every joint into a rotation about its frame's z
     double A[kMskMaxQ][9];         // constant rotation from frame j-1 (ground for j = 0) to dof j's joint frame
     double t[kMskMaxQ][3];         // its translation, in frame j-1
     double grav[3];
@@ -315,28 +315,15 @@ MSK_HD void msk_frames(const MskGeom& G, const S* q, S (*R)[9], S (*o)[3], S (*z
             }
         }
         const S c = mcos(q[j]), s = msin(q[j]);
-        // R_j = Rb Rot(q): columns (a, b) of the rotation plane mix, the axis column is kept
-        const int ax = G.axis[j];
+        // R_j = Rb Rot_z(q): columns 0 and 1 mix, the axis column 2 is kept (cfx_msk_create expresses every joint
+        // as a rotation about its frame's z axis, G.axis[j] == 2)
 #pragma unroll
         for (int r = 0; r < 3; ++r) {
-            // uniform branches keep every register index compile-time
-            S ca, cb, cz;
-            if (ax == 2) {
-                ca = Rb[r * 3 + 0], cb = Rb[r * 3 + 1], cz = Rb[r * 3 + 2];
-            } else if (ax == 0) {
-                ca = Rb[r * 3 + 1], cb = Rb[r * 3 + 2], cz = Rb[r * 3 + 0];
-            } else {
-                ca = Rb[r * 3 + 2], cb = Rb[r * 3 + 0], cz = Rb[r * 3 + 1];
-            }
-            const S na = ca * c + cb * s, nb = cb * c - ca * s;
+            const S ca = Rb[r * 3 + 0], cb = Rb[r * 3 + 1], cz = Rb[r * 3 + 2];
+            R[j][r * 3 + 0] = ca * c + cb * s;
+            R[j][r * 3 + 1] = cb * c - ca * s;
+            R[j][r * 3 + 2] = cz;
             z[j][r] = cz;
-            if (ax == 2) {
-                R[j][r * 3 + 0] = na, R[j][r * 3 + 1] = nb, R[j][r * 3 + 2] = cz;
-            } else if (ax == 0) {
-                R[j][r * 3 + 1] = na, R[j][r * 3 + 2] = nb, R[j][r * 3 + 0] = cz;
-            } else {
-                R[j][r * 3 + 2] = na, R[j][r * 3 + 0] = nb, R[j][r * 3 + 1] = cz;
-            }
         }
     }
 }

@@ -34,6 +34,28 @@ def biomod_path(name="arm26_biceps_triceps") -> str:
     return name if name.endswith(".json") else str(GOLDEN / f"biomod_{name}.json")
 
 
+_ROTATED = {}
+
+
+def rotated_biomod(axes=("x", "y"), base="arm26_biceps_triceps") -> str:
+    """The arm26 fixture with its two joints turned to rotate about other axes (shoulder ``axes[0]``, elbow
+    ``axes[1]``; the reference model has z for both), written once to a temporary .json: exercises the kernels'
+    z-axis canonical frames (cfx_msk_create) against the oracle, which walks the tree with the axes as given."""
+    key = (tuple(axes), base)
+    if key not in _ROTATED:
+        import tempfile
+
+        d = json.loads((GOLDEN / f"biomod_{base}.json").read_text())
+        it = iter(axes)
+        for seg in d["segments"]:
+            if seg.get("rotations") == "z":
+                seg["rotations"] = next(it)
+        path = pathlib.Path(tempfile.mkdtemp(prefix="cfx_biomod_")) / f"biomod_{base}_{''.join(axes)}.json"
+        path.write_text(json.dumps(d))
+        _ROTATED[key] = str(path)
+    return _ROTATED[key]
+
+
 def cfg5(**kw):
     """BASELINE config 5: arm26 biceps/triceps + Ding2007 with fatigue, 10 pulses @ 10 Hz, 1 s, elbow 5 -> 90 deg,
     FL/FV on, no residual torque, qdot(end) = 0 (weight 100) and minimize_muscle_fatigue, RK4 x 1

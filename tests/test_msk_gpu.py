@@ -37,6 +37,10 @@ CASES = {
     "hmed_rk1_t20": MC.cfg5(model="hmed2018", fatigue=False, scheme="RK1", m=3, truncation=20),
     "hmed_biceps_1dof_rk2": MC.cfg5(biomod="arm26_biceps_1dof", muscles=("BIClong",), model="hmed2018_with_fatigue",
                                     scheme="RK2", m=2),
+    # joints about x / y (and y / x): the kernels' frames are re-expressed so every joint turns about its z axis
+    "rotated_xy_d07f": MC.cfg5(biomod=MC.rotated_biomod(("x", "y"))),
+    "rotated_yx_d03_residual": MC.cfg5(biomod=MC.rotated_biomod(("y", "x")), model="ding2003", fatigue=False,
+                                       residual=True, m=2),
 }
 
 
@@ -188,6 +192,8 @@ MARKER_CASES = {
                               dict(first="COM_hand", second="target", node=0, axes=(0,))]),
     "biceps_1dof_xy": (MC.cfg5(biomod="arm26_biceps_1dof", muscles=("BIClong",)),
                        [dict(first="COM_hand", second="target", node=5, axes=(0, 1))]),
+    "rotated_xy_reach": (MC.cfg5(biomod=MC.rotated_biomod(("x", "y"))),
+                         [dict(first="COM_hand", second="target", node="end", axes=(0, 1, 2))]),
 }
 
 
