@@ -1042,83 +1042,118 @@ __global__ void __launch_bounds__(256) k_msk_tangents(const MskParams P, const M
 // holds 64 / TW columns of TW instances), so each coefficient is read from L2 once per block instead of once per
 // column.  Per RK sub-step the block loads the ST stages' coefficients of its TW instances (ST * NC * TW * 8 B),
 // then every thread carries its column through them.  A column takes ~200 VGPRs (2 waves per SIMD).  cfg 5 at
-// B = 65536: TW = 32 0.66 ms, TW = 16 0.70 ms; 0.96 ms before the staging loads were issued all at once.
+// B = 65536: TW = 32 0.66 ms, TW = 16 0.70 ms; 0.96 ms before the staging loads were issued all at once.  A block
+// runs kpb consecutive intervals with the next sub-step's coefficients prefetched during the current one (below).
 constexpr int kMskLdsCols = 16;
 constexpr int kMskLdsLoads = 16;  // coefficient loads in flight per thread while staging
 
 template <int NQ, int NM, int FAM, int SCHEME, int TW>
 __global__ void __launch_bounds__(32 * kMskLdsCols) k_msk_tangents_lds(const MskParams P, const MskGeom* __restrict__ GG,
                                                                      const double* __restrict__ V,
-                                                                     double* __restrict__ J) {
+                                                                     double* __restrict__ J, int kpb) {
     constexpr int NXM = msk_nxm<FAM>(), NX = NM * NXM + 2 * NQ;
     constexpr int NUMAX = msk_numax<NQ, NM, FAM>();
     constexpr int NC = msk_ncoef<NQ, NM>();
     constexpr int ST = SCHEME == 4 ? 4 : (SCHEME == 2 ? 2 : 1);
-    extern __shared__ double sW[];  // [ST][NC][TW]
+    constexpr int NE = ST * NC * TW;  // coefficients of one sub-step of the block's TW instances
+    extern __shared__ double sW[];    // [2][ST][NC][TW] (two buffers when B is even)
     const int64_t B = P.B;
     const int nz = P.nz, lane = threadIdx.x % TW, col = threadIdx.x / TW, nthr = TW * nz;
     const int64_t b0 = (int64_t)blockIdx.x * TW, b = b0 + lane;
-    const int k = blockIdx.y;
+    const int k0 = blockIdx.y * kpb, k1 = min(P.N, k0 + kpb);
     const MskGeom& G = *GG;
     const int residual = P.residual;
     const double h = P.h;
-    const double* __restrict__ Wk = P.scratch + (int64_t)k * P.Q * NC * B;
-    double tx[NX], tu[NUMAX];
-#pragma unroll
-    for (int r = 0; r < NX; ++r) tx[r] = r == col ? 1.0 : 0.0;
-#pragma unroll
-    for (int i = 0; i < NUMAX; ++i) {
-        const int dc = msk_udec<NM, FAM>(i, P.T, P.nu);
-        tu[i] = dc >= 0 && NX + dc == col ? 1.0 : 0.0;
-    }
-    const MskICol ic = msk_icol<NM, FAM>(P, G, V, (int64_t)k * nz, b, b < B, col);
-    for (int j = 0; j < P.m; ++j) {
-        __syncthreads();  // the previous sub-step's coefficients are consumed
-        // all of a thread's loads are issued before the first LDS store, so the block waits for one HBM round
-        // trip per sub-step rather than one per element (ST * NC / nz of them, 9 for cfg 5)
-        for (int e0 = threadIdx.x; e0 < ST * NC * TW; e0 += kMskLdsLoads * nthr) {
-            double tmp[kMskLdsLoads];
-#pragma unroll
-            for (int i = 0; i < kMskLdsLoads; ++i) {
-                const int e = e0 + i * nthr, l = e % TW, sc = e / TW;  // sc = st * NC + c
-                const int64_t bb = b0 + l;
-                tmp[i] = (e < ST * NC * TW && bb < B) ? Wk[((int64_t)j * ST * NC + sc) * B + bb] : 0.0;
-            }
-#pragma unroll
-            for (int i = 0; i < kMskLdsLoads; ++i)
-                if (e0 + i * nthr < ST * NC * TW) sW[e0 + i * nthr] = tmp[i];
+    // Several intervals per block (kpb) with the coefficients double-buffered in LDS: while a sub-step computes from
+    // one buffer, the next (interval, sub-step)'s coefficients stream into the other by direct-to-LDS loads
+    // (global_load_lds_dwordx4: lane L of a wave moves 16 B to M0 + 16 L, so one wave instruction fills four
+    // TW-double rows), so only the block's first staging waits for HBM and no registers hold the prefetch.  Needs
+    // 16-byte rows (B even); otherwise the sub-steps stage through registers one at a time.
+    static_assert(TW == 32, "a 16-lane quarter of a wave moves one TW-double row");
+    const bool async = (B % 2) == 0;
+    const int wave = threadIdx.x / 64, nwave = nthr / 64, L = threadIdx.x % 64;  // full waves only (nz odd: one half)
+    auto issue = [&](int kk, int j, int buf) {
+        const double* __restrict__ Wk = P.scratch + (int64_t)kk * P.Q * NC * B + (int64_t)j * ST * NC * B;
+        double* base = sW + buf * NE;
+        for (int c = wave; wave < nwave && c * 4 * TW < NE; c += nwave) {  // chunk c: rows 4c .. 4c + 3 (st * NC + c)
+            const int row = 4 * c + L / 16, l = (L % 16) * 2;
+            if (row * TW < NE && b0 + l < B)
+                __builtin_amdgcn_global_load_lds(Wk + (int64_t)row * B + b0 + l,
+                                                 (__attribute__((address_space(3))) void*)(base + c * 4 * TW), 16, 0, 0);
         }
-        __syncthreads();
-        double tacc[NX], txs[NX];
+    };
+    int buf = 0;
+    if (async && k0 < k1) issue(k0, 0, 0);
+    for (int k = k0; k < k1; ++k) {
+        const double* __restrict__ Wk = P.scratch + (int64_t)k * P.Q * NC * B;
+        double tx[NX], tu[NUMAX];
 #pragma unroll
-        for (int r = 0; r < NX; ++r) txs[r] = tx[r];
+        for (int r = 0; r < NX; ++r) tx[r] = r == col ? 1.0 : 0.0;
 #pragma unroll
-        for (int st = 0; st < ST; ++st) {
-            double tk[NX], dcs[NM];
-            msk_icol_dcs<NM, FAM>(P, ic, (int64_t)k * P.Q + j * ST + st, dcs);
-            msk_tangent<NQ, NM, FAM>(G, residual, sW + st * NC * TW + lane, TW, txs, tu, dcs, tk);
-            const double cst = (ST == 4 && st == 2) ? h : 0.5 * h;
+        for (int i = 0; i < NUMAX; ++i) {
+            const int dc = msk_udec<NM, FAM>(i, P.T, P.nu);
+            tu[i] = dc >= 0 && NX + dc == col ? 1.0 : 0.0;
+        }
+        const MskICol ic = msk_icol<NM, FAM>(P, G, V, (int64_t)k * nz, b, b < B, col);
+        for (int j = 0; j < P.m; ++j) {
+            const double* sWb = sW;
+            if (async) {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's direct-to-LDS loads have landed
+                __syncthreads();  // every wave's have, and the other buffer's readers are done
+                const bool last = j + 1 == P.m;
+                if (!last || k + 1 < k1) issue(last ? k + 1 : k, last ? 0 : j + 1, buf ^ 1);
+                sWb = sW + buf * NE;
+                buf ^= 1;
+            } else {
+                __syncthreads();  // the previous sub-step's coefficients are consumed
+                // all of a thread's loads are issued before the first LDS store, so the block waits for one HBM round
+                // trip per sub-step rather than one per element
+                for (int e0 = threadIdx.x; e0 < NE; e0 += kMskLdsLoads * nthr) {
+                    double tmp[kMskLdsLoads];
+#pragma unroll
+                    for (int i = 0; i < kMskLdsLoads; ++i) {
+                        const int e = e0 + i * nthr, l = e % TW, sc = e / TW;  // sc = st * NC + c
+                        const int64_t bb = b0 + l;
+                        tmp[i] = (e < NE && bb < B) ? Wk[((int64_t)j * ST * NC + sc) * B + bb] : 0.0;
+                    }
+#pragma unroll
+                    for (int i = 0; i < kMskLdsLoads; ++i)
+                        if (e0 + i * nthr < NE) sW[e0 + i * nthr] = tmp[i];
+                }
+                __syncthreads();
+            }
+            double tacc[NX], txs[NX];
+#pragma unroll
+            for (int r = 0; r < NX; ++r) txs[r] = tx[r];
+#pragma unroll
+            for (int st = 0; st < ST; ++st) {
+                double tk[NX], dcs[NM];
+                msk_icol_dcs<NM, FAM>(P, ic, (int64_t)k * P.Q + j * ST + st, dcs);
+                msk_tangent<NQ, NM, FAM>(G, residual, sWb + st * NC * TW + lane, TW, txs, tu, dcs, tk);
+                const double cst = (ST == 4 && st == 2) ? h : 0.5 * h;
+#pragma unroll
+                for (int r = 0; r < NX; ++r) {
+                    if (ST == 4) {
+                        if (st == 0) tacc[r] = tk[r];
+                        else if (st < 3) tacc[r] = tacc[r] + 2.0 * tk[r];
+                    }
+                    if (st + 1 < ST) txs[r] = tx[r] + cst * tk[r];
+                    else tx[r] = ST == 4 ? tx[r] + (h / 6.0) * (tacc[r] + tk[r]) : tx[r] + h * tk[r];
+                }
+            }
+        }
+        if (b < B) {
+            const int64_t jb = (int64_t)k * P.nnzk;
 #pragma unroll
             for (int r = 0; r < NX; ++r) {
-                if (ST == 4) {
-                    if (st == 0) tacc[r] = tk[r];
-                    else if (st < 3) tacc[r] = tacc[r] + 2.0 * tk[r];
-                }
-                if (st + 1 < ST) txs[r] = tx[r] + cst * tk[r];
-                else tx[r] = ST == 4 ? tx[r] + (h / 6.0) * (tacc[r] + tk[r]) : tx[r] + h * tk[r];
+                const int pos = G.jpos[r * kMskMaxZ + col];
+                if (pos >= 0) J[(jb + pos) * B + b] = tx[r];
+            }
+            if (col == 0) {
+#pragma unroll
+                for (int r = 0; r < NX; ++r) J[(jb + G.jneg[r]) * B + b] = -1.0;
             }
         }
-    }
-    if (b >= B) return;
-    const int64_t jb = (int64_t)k * P.nnzk;
-#pragma unroll
-    for (int r = 0; r < NX; ++r) {
-        const int pos = G.jpos[r * kMskMaxZ + col];
-        if (pos >= 0) J[(jb + pos) * B + b] = tx[r];
-    }
-    if (col == 0) {
-#pragma unroll
-        for (int r = 0; r < NX; ++r) J[(jb + G.jneg[r]) * B + b] = -1.0;
     }
 }
 

@@ -2,6 +2,9 @@
 // model family pair, so the builds run in parallel).
 #pragma once
 
+#include <algorithm>
+#include <cstdlib>
+
 #include "cfx_msk_launch.h"
 
 namespace cfx {
@@ -43,8 +46,21 @@ hipError_t shoot_t(const MskParams& P, const MskGeom* G, const double* V, double
                        dim3(kMskBlk), 0, s, P, G, V, (const double*)XS);
     if (P.nz <= kMskLdsCols) {  // coefficients through LDS, one block per 32 instances
         constexpr int ST = SCHEME == 4 ? 4 : (SCHEME == 2 ? 2 : 1), TW = 32;
-        hipLaunchKernelGGL((k_msk_tangents_lds<NQ, NM, FAM, SCHEME, TW>), dim3((unsigned)((P.B + TW - 1) / TW), (unsigned)P.N),
-                           dim3(TW * P.nz), ST * NC * TW * sizeof(double), s, P, G, V, J);
+        // intervals per block: as many as keep >= 4,096 blocks (16 per CU); CFX_MSK_KPB overrides (tuning)
+        const int64_t nbx = (P.B + TW - 1) / TW;
+        int kpb = (int)std::max<int64_t>(1, std::min<int64_t>(P.N, nbx * P.N / 4096));
+        if (const char* e = std::getenv("CFX_MSK_KPB")) kpb = std::max(1, std::min(P.N, std::atoi(e)));
+        // two coefficient buffers when B is even (k_msk_tangents_lds): above the default 64 KiB of dynamic LDS for cfg 5
+        const size_t lds = (P.B % 2 == 0 ? 2 : 1) * ST * NC * TW * sizeof(double);
+        static size_t raised = 65536;  // one per instantiation
+        if (lds > raised) {
+            const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_msk_tangents_lds<NQ, NM, FAM, SCHEME, TW>),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+            if (e != hipSuccess) return e;
+            raised = lds;
+        }
+        hipLaunchKernelGGL((k_msk_tangents_lds<NQ, NM, FAM, SCHEME, TW>), dim3((unsigned)nbx, (unsigned)((P.N + kpb - 1) / kpb)),
+                           dim3(TW * P.nz), lds, s, P, G, V, J, kpb);
         return hipGetLastError();
     }
     const int64_t ranges8 = ((P.B + kMskBlk - 1) / kMskBlk + 7) / 8 * 8;  // instance ranges, padded to 8 XCDs
