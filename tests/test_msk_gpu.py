@@ -63,13 +63,16 @@ def _dense_blocks(pb, jr, jc, jv, k):
     return D, neg
 
 
-@pytest.mark.parametrize("case", list(CASES))
+@pytest.mark.parametrize("case", list(CASES) + ["cfg5_d07f_rk4@odd", "rotated_xy_d07f@odd"])
 def test_msk_g_and_jacobian_match_oracle(case):
-    cfg = CASES[case]
+    """An even batch stages the tangent kernel's coefficients by direct-to-LDS loads (k_msk_tangents_lds), an odd one
+    through registers: both against the oracle."""
+    name, _, odd = case.partition("@")
+    cfg = CASES[name]
     ocp = MC.product_ocp(**cfg)
     pb = MC.oracle_problem(**cfg)
     assert (ocp.nx, ocp.nu, ocp.nv) == (pb.nx, pb.nu, pb.nv)
-    B = 3
+    B = 3 if odd else 4
     V = MC.random_decision(pb, B, seed=11)
     h = ocp.nlp(batch=B, layout="aos")
     g = h.eval_g(V)
