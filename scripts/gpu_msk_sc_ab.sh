@@ -1,3 +1,4 @@
+# (The CFX_MSK_SC_BLOCKS switch and the grid-stride kernel were removed after this measurement, profiles/round2/msk_sc_ab/.)
 # Grid-stride prefetching k_msk_stagecoef_par: A/B of blocks (512 = ~40 items per thread, 10240 = one item per thread),
 # alternating kernel traces of the MSK probe, then the MSK GPU tests.
 set -o pipefail
