@@ -465,6 +465,9 @@ class MskProblem:
     # (fes_ocp_dynamics.py:424-450): dicts node, first, second (marker names), axes (world axis indices); rows
     # marker(second) - marker(first) at q_node, after every interval's rows
     marker_pairs: list = field(default_factory=list)
+    # muscle-model conventions of the revision that wrote the reference's stored reaching-task solutions
+    # (fes_oracle.rhs ``legacy``); test infrastructure for tests/test_reference_solution.py
+    legacy: bool = False
 
     @property
     def nq(self):
@@ -549,7 +552,7 @@ def msk_rhs(pb: MskProblem, t, x, u, row):
         elif O.control_kind(mus.model) == "pulse_intensity":  # the muscle's T intensities (dynamical_model.py:253-255)
             um = u[pw: pw + pb.T]
             pw += pb.T
-        dxm = O.rhs(mus.model, mus.c, t, xm, um, row, fl=fl, fv=fv, fp=fp)
+        dxm = O.rhs(mus.model, mus.c, t, xm, um, row, fl=fl, fv=fv, fp=fp, legacy=pb.legacy)
         dx.extend(list(dxm))
         JL_rows.append(JL)
         F.append(xm[1])

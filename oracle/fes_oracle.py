@@ -160,15 +160,22 @@ def stim_table(stim_time, n_shooting, final_time, truncation, previous_stim=None
 # --------------------------------------------------------------------------------------
 
 
-def cn_sum(c, t, row, lam=None):
+def cn_sum(c, t, row, lam=None, legacy_skip_first=False):
     """ding2003.py:200-252 (ri_fun, exp_time_fun, cn_sum_fun); r0 = km_rest + 1.04 (268-272).
 
     ``row`` has shape (T, ...) broadcastable against ``t``; ``lam`` likewise or None (lambda_i = 1,
-    ding2003.py:148-150).
+    ding2003.py:148-150).  ``legacy_skip_first``: the convention of the revision that wrote the reference's stored
+    reaching-task solutions (examples/dynamics/reaching_task/result_file/*.pkl), measured from their calcium
+    trajectories (tests/test_reference_solution.py): once a window holds more than one real pulse its first term is
+    left out of the sum (the later terms keep their r_i).  Test infrastructure only; the product follows the current
+    cn_sum_fun.
     """
     r0 = c["km_rest"] + c["r0_km_relationship"]
     total = 0
+    n_real = np.sum(np.asarray(row) > -1e6, axis=0) if legacy_skip_first else None
     for i in range(row.shape[0]):
+        if legacy_skip_first and i == row.shape[0] - n_real and n_real > 1:
+            continue
         ri = 1 if i == 0 else 1 + (r0 - 1) * np.exp(-(row[i] - row[i - 1]) / c["tauc"])
         term = ri * np.exp(-(t - row[i]) / c["tauc"])
         total = total + (term if lam is None else term * lam[i])
@@ -185,19 +192,23 @@ def a_calculation(c, a_scale, pulse_width):
     return a_scale * (1 - np.exp(-(pulse_width - c["pd0"]) / c["pdt"]))
 
 
-def rhs(name, c, t, x, u, row, fl=1.0, fv=1.0, fp=0.0):
+def rhs(name, c, t, x, u, row, fl=1.0, fv=1.0, fp=0.0, legacy=False):
     """system_dynamics of the six models.
 
     ding2003.py:153-198, ding2003_with_fatigue.py:138-240, ding2007.py:121-170,
     ding2007_with_fatigue.py:133-241, hmed2018.py:119-167, hmed2018_with_fatigue.py:124-229.
     x: (nx, ...); u: (nu, ...) or None; row: (T, ...).
+    ``legacy``: the conventions of the revision that wrote the reference's stored reaching-task solutions (measured
+    from their trajectories, tests/test_reference_solution.py): the calcium sum skips a window's first pulse once it
+    holds several (cn_sum), and the fatigue models take r0 from the Km state instead of km_rest.  Test infrastructure
+    only; the product follows the current reference.
     """
     fatigue = name.endswith("with_fatigue")
     cn, f = x[0], x[1]
     lam = None
     if name.startswith("hmed2018"):
         lam = [lambda_i(c, u[i]) for i in range(row.shape[0])]
-    cs = cn_sum(c, t, row, lam)
+    cs = cn_sum(dict(c, km_rest=x[4]) if (legacy and fatigue) else c, t, row, lam, legacy)
     cn_dot = (1 / c["tauc"]) * cs - (cn / c["tauc"])  # ding2003.py:254-266
     if fatigue:
         a, tau1, km = x[2], x[3], x[4]

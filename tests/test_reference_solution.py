@@ -1,0 +1,191 @@
+"""The musculoskeletal path against a solution the reference itself computed.
+
+Fixture: the two solutions of the reference's reaching task (examples/dynamics/reaching_task/
+reaching_task_pulse_duration_optimization.py:80-118, stored in result_file/pulse_duration_minimize_muscle_*.pkl by an
+older revision of that script; bioptim + Ipopt + biorbd), extracted as numbers by tests/golden/
+extract_reaching_solution.py: arm26 with six Ding2007-with-fatigue muscles (alpha_a and a_scale scaled per muscle as
+the script does), 60 pulses at 40 Hz over 1.5 s, 1,500 shooting intervals (1 ms), the hand on `reaching_target` (x, y)
+at node 1000 (the current script says 650; the stored hand meets the target at node 1000 to 2e-16), the elbow back
+to 5 deg at the end; per-pulse durations (OCP parameters in that revision; here the
+per-interval `last_pulse_width` control of the pulse the interval follows), residual torque tau (0 throughout).
+
+What the stored trajectory says about that revision, measured here:
+  * RK4 with one step per interval (OcpFesMsk's default): RK4 x 2 leaves 1e-3 N force residuals, RK4 x 1 1e-13;
+  * fatigue rates ten times the current defaults: alpha_a = -4.0 (x the script's fibre-type proportion),
+    alpha_tau1 = 2.1e-4, alpha_km = 1.9e-4 (least squares on the stored A / Tau1 / Km increments);
+  * the calcium sum leaves out a window's first pulse once the window holds several, and the fatigue models take r0
+    from the Km state (the current cn_sum_fun, ding2003.py:230-252, sums every pulse with r0 = km_rest + 1.04): with
+    the current convention the Cn rows miss by 8.6e-3 right after the second pulse.
+With those conventions the oracle's restatement of the whole right-hand side — the biorbd chain, muscle paths and
+length Jacobians, De Groote force-length / force-velocity, the Ding ODEs — reproduces every continuity row of the
+stored solution to 2e-12 on the muscle states and 1e-9 on the joint velocities (Ipopt's converged constraint
+violation), and the marker constraint to its tolerance.  The GPU kernels are then compared with the oracle at the
+same trajectory under the current convention (tests marked gpu).
+"""
+
+import json
+import pathlib
+
+import numpy as np
+import pytest
+
+from oracle import fes_msk as M
+from oracle import fes_oracle as O
+
+GOLDEN = pathlib.Path(__file__).with_name("golden")
+MUSCLES = ["BIClong", "BICshort", "TRIlong", "TRIlat", "TRImed", "BRA"]
+# reaching_task_pulse_duration_optimization.py:27-50: fibre-type-2 proportions scale alpha_a, PCSA ratios a_scale
+ALPHA_A_PROP = [0.607, 0.607, 0.465, 0.465, 0.465, 0.457]
+A_SCALE_PROP = [12.7 / 28.3, 12.7 / 28.3, 1.0, 1.0, 1.0, 11.6 / 28.3]
+STIMS = [float(s) for s in np.round(np.linspace(0, 1.5, 61), 3)[:-1]]
+N, FINAL_TIME, T = 1500, 1.5, 60
+LEGACY_FATIGUE_RATE = 10.0  # the stored revision's alpha_a / alpha_tau1 / alpha_km over the current defaults
+SAMPLE = [0, 1, 2, 12, 24, 25, 26, 49, 50, 51, 100, 101, 400, 649, 650, 651, 900, 999, 1000, 1200, 1498, 1499]
+MARKER_NODE = 1000
+
+
+def load(objective="fatigue"):
+    return dict(np.load(GOLDEN / f"reaching_pulse_duration_{objective}.npz"))
+
+
+def muscle_constants(legacy_rates=True):
+    out = []
+    for i in range(len(MUSCLES)):
+        c = dict(O.model_constants("ding2007_with_fatigue"))
+        c["alpha_a"] *= ALPHA_A_PROP[i]
+        c["a_scale"] *= A_SCALE_PROP[i]
+        if legacy_rates:
+            for k in ("alpha_a", "alpha_tau1", "alpha_km"):
+                c[k] *= LEGACY_FATIGUE_RATE
+        out.append(c)
+    return out
+
+
+def oracle_problem(legacy=True):
+    bm = json.loads((GOLDEN / "biomod_arm26.json").read_text())
+    tab = O.stim_table(STIMS, N, FINAL_TIME, T)
+    mus = [M.MskMuscle(model="ding2007_with_fatigue", name=n, c=c) for n, c in zip(MUSCLES, muscle_constants())]
+    pb = M.MskProblem(bm=bm, muscles=mus, rows=tab.rows, n_shooting=N, final_time=FINAL_TIME, scheme="RK4", m=1,
+                      fv_on=True, fp_on=False, residual=True, legacy=legacy)
+    pb.marker_pairs.append(dict(node=MARKER_NODE, first="COM_hand", second="reaching_target", axes=[0, 1]))
+    return pb
+
+
+def pulse_index():
+    """Index of the pulse each interval follows (the last stim time <= t_k, exact rational comparison)."""
+    return np.array([sum(1 for s in STIMS if round(s * 1000) <= k) - 1 for k in range(N)])
+
+
+def trajectory(d):
+    """States (nx, N+1) in the oracle / product order and controls (nu, N): pulse widths then tau."""
+    X = np.stack([d[f"{s}_{n}"] for n in MUSCLES for s in ("Cn", "F", "A", "Tau1", "Km")]
+                 + [d["q"][0], d["q"][1], d["qdot"][0], d["qdot"][1]])
+    idx = pulse_index()
+    U = np.stack([d[f"pulse_duration_{n}"][idx] for n in MUSCLES] + [d["tau"][0], d["tau"][1]])
+    return X, U
+
+
+def decision_vector(X, U, nz):
+    v = np.empty(N * nz + X.shape[0])
+    body = v[: N * nz].reshape(N, nz)
+    body[:, : X.shape[0]] = X[:, :N].T
+    body[:, X.shape[0]:] = U.T
+    v[N * nz:] = X[:, N]
+    return v
+
+
+def _residuals(pb, X, U, ks):
+    return np.array([M.integrate_interval(pb, k, X[:, k].astype(complex), U[:, k].astype(complex)).real - X[:, k + 1]
+                     for k in ks])
+
+
+@pytest.mark.parametrize("objective", ["fatigue", "force"])
+def test_oracle_reproduces_the_reference_solution(objective):
+    d = load(objective)
+    pb = oracle_problem(legacy=True)
+    X, U = trajectory(d)
+    assert X.shape == (pb.nx, N + 1) and U.shape == (pb.nu, N)
+    assert np.allclose(d["time"], np.arange(N + 1) * FINAL_TIME / N, atol=1e-12)
+    R = _residuals(pb, X, U, SAMPLE)
+    nxm = pb.nxm
+    scale = np.maximum(1.0, np.abs(X[:, [k + 1 for k in SAMPLE]].T))
+    # muscle states: every continuity row to 2e-12 relative (Ipopt met them to machine precision)
+    assert np.max(np.abs(R[:, :nxm]) / scale[:, :nxm]) < 1e-11, np.max(np.abs(R[:, :nxm]) / scale[:, :nxm])
+    # q, qdot: biorbd's forward dynamics against the oracle's chain: 1e-9 (Ipopt's constraint violation)
+    assert np.max(np.abs(R[:, nxm:])) < 1e-8, np.max(np.abs(R[:, nxm:]))
+    # the stored optimum satisfies the reaching constraint and the start / end postures of the script
+    v = decision_vector(X, U, pb.nz)
+    assert np.max(np.abs(M.marker_rows(pb, v))) < 1e-8
+    np.testing.assert_allclose(X[nxm: nxm + 2, 0], [0.0, 5 * 3.14 / 180], atol=1e-12)
+    np.testing.assert_allclose(X[nxm: nxm + 2, N], [0.0, 5 * 3.14 / 180], atol=1e-8)
+    # the per-pulse durations within the script's bounds [pd0, 0.6 ms], up to Ipopt's bound_relax_factor (1e-8)
+    pw = U[: len(MUSCLES)]
+    assert np.all(pw >= O.model_constants("ding2007")["pd0"] - 1e-8) and np.all(pw <= 6e-4 + 1e-8)
+
+
+def test_current_conventions_differ_exactly_where_documented():
+    """Without the stored revision's conventions the rows miss by the documented amounts: the first pulse's calcium
+    term after the second pulse (Cn rows, 8.6e-3 at interval 25, decaying as exp(-t / tau_c)), and the fatigue rates
+    (A rows)."""
+    d = load("fatigue")
+    X, U = trajectory(d)
+    cur = oracle_problem(legacy=False)
+    R = _residuals(cur, X, U, [24, 25, 26])
+    cn_rows = [5 * i for i in range(len(MUSCLES))]
+    assert np.max(np.abs(R[0, cn_rows])) < 1e-9  # one pulse in the window: both conventions agree
+    tauc, h = 0.011, 0.001
+    first_pulse = (1 - np.exp(-h / tauc)) * np.exp(-0.025 / tauc)  # integral of the skipped term over interval 25
+    np.testing.assert_allclose(R[1, cn_rows], first_pulse, rtol=0.05)
+    np.testing.assert_allclose(R[2, cn_rows], first_pulse * np.exp(-h / tauc), rtol=0.05)
+    # current fatigue rates (ten times smaller) leave the A rows off by ~alpha_a F h
+    rates = oracle_problem(legacy=True)
+    for m in rates.muscles:
+        for k in ("alpha_a", "alpha_tau1", "alpha_km"):
+            m.c[k] /= LEGACY_FATIGUE_RATE
+    Ra = _residuals(rates, X, U, [400])
+    assert np.max(np.abs(Ra[0, [5 * i + 2 for i in range(len(MUSCLES))]])) > 1e-2
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("objective", ["fatigue", "force"])
+def test_gpu_matches_the_oracle_at_the_reference_solution(objective):
+    """The product (OcpFesMsk with the script's six muscles, RK4 x 1, N = 1,500, all 60 pulses in the window, the
+    marker constraint at node 1000) evaluated by libcfx at the reference's stored trajectory: every continuity row of
+    the sample against the oracle under the current convention (relative 1e-10), and the marker rows ~ 0."""
+    import cocofest_amd as C
+
+    d = load(objective)
+    X, U = trajectory(d)
+    consts = muscle_constants()
+    models = []
+    for n, c in zip(MUSCLES, consts):
+        mm = C.DingModelPulseWidthFrequencyWithFatigue(muscle_name=n, sum_stim_truncation=T)
+        for k in ("alpha_a", "alpha_tau1", "alpha_km", "a_scale"):
+            setattr(mm, k, c[k])
+        models.append(mm)
+    model = C.FesMskModel(biorbd_path=str(GOLDEN / "biomod_arm26.json"), muscles_model=models, stim_time=STIMS,
+                          activate_force_length_relationship=True, activate_force_velocity_relationship=True,
+                          activate_residual_torque=True)
+    cl = C.ConstraintList()
+    cl.add(C.ConstraintFcn.SUPERIMPOSE_MARKERS, first_marker="COM_hand", second_marker="reaching_target", phase=0,
+           node=MARKER_NODE, axes=[C.Axis.X, C.Axis.Y])
+    ocp = C.OcpFesMsk.prepare_ocp(model=model, final_time=FINAL_TIME, n_shooting=N,
+                                  pulse_width={"min": O.model_constants("ding2007")["pd0"], "max": 0.0006},
+                                  objective={"minimize_muscle_fatigue": True},
+                                  msk_info={"with_residual_torque": True, "bound_type": "start_end",
+                                            "bound_data": [[0, 5], [0, 5]], "custom_constraint": cl},
+                                  ode_solver=C.OdeSolver.RK4(n_integration_steps=1), apply_custom_constraint=True)
+    pb = oracle_problem(legacy=False)
+    assert (ocp.nx, ocp.nu, ocp.nv) == (pb.nx, pb.nu, pb.nv)
+    assert ocp.state_names[:5] == ["Cn_BIClong", "F_BIClong", "A_BIClong", "Tau1_BIClong", "Km_BIClong"]
+    v = decision_vector(X, U, pb.nz)
+    h = ocp.nlp(batch=1, layout="aos")
+    g = h.eval_g(v[None, :])[0]
+    h.close()
+    nx = pb.nx
+    gk = g[: N * nx].reshape(N, nx)
+    R = _residuals(pb, X, U, SAMPLE)
+    ref_scale = np.abs(R) + np.abs(X[:, [k + 1 for k in SAMPLE]].T) + 1e-12
+    assert np.max(np.abs(gk[SAMPLE] - R) / ref_scale) < 1e-10
+    np.testing.assert_allclose(g[N * nx:], M.marker_rows(pb, v), atol=1e-13)
+    assert np.max(np.abs(g[N * nx:])) < 1e-8
