@@ -87,28 +87,66 @@ def pmc_traffic():
         return None
 
 
-def cpu_baseline(ocp, budget_s):
-    """The plain-C port of the reference's as-written evaluation (oracle/c), all usable host cores, on a
-    bounded sample of the same workload."""
-    from oracle import c_oracle, fes_oracle as O
-
-    threads = min(16, len(os.sched_getaffinity(0)))
-    pb = O.Problem(name="ding2003", c=O.model_constants("ding2003"), n_shooting=ocp.n_shooting, final_time=1.0,
-                   truncation=20, rows=ocp.stim_rows, scheme="RK1", n_steps=10)
-    rng = np.random.default_rng(0)
-    chunk = 4096
-    v = rng.uniform(0.0, 1.0, (chunk, pb.nv)) * np.tile([1.5, 250.0], pb.nv // 2)
-    c_oracle.shooting(pb, v[:64], threads=threads)  # warm-up / load
+def _timed(fn, budget_s, per_call):
+    """Calls fn() until budget_s has elapsed (one untimed call first); returns (units per second, units, seconds)."""
+    fn()
     done, t0 = 0, time.perf_counter()
     while True:
-        c_oracle.shooting(pb, v, threads=threads)
-        done += chunk
+        fn()
+        done += per_call
         el = time.perf_counter() - t0
         if el >= budget_s:
-            break
-    return {"value": done / el, "unit": "instance-evals/s", "cores": threads, "kind": "port",
-            "sample": f"{done} instances of cfg2 (g + J_g, as-written calcium sum: 2T-1 exp per RK stage), "
-                      f"oracle/c/fes_oracle.c, OpenMP {threads} threads, {el:.1f} s"}
+            return done / el, done, el
+
+
+def casadi_probe():
+    """the reference's CPU callback is CasADi's; record whether this host can import it (no install)."""
+    try:
+        import casadi  # noqa: F401
+
+        return {"importable": True, "version": getattr(casadi, "__version__", "?")}
+    except Exception as e:  # noqa: BLE001
+        return {"importable": False, "error": f"{type(e).__name__}: {e}"}
+
+
+def cpu_baseline(ocp, budget_s, name="ding2003", truncation=20, label="cfg2"):
+    """CPU legs on a bounded sample of the same workload, on this host's cores and on one core:
+
+    * as written (``kind: port``, the headline value): the plain-C port of the reference's evaluation as CasADi
+      would run its expression graph — 2T-1 exponentials per RK stage, dual-number derivatives (oracle/c/fes_oracle.c);
+    * same formulation: the GPU kernel's own algorithm on the CPU — affine calcium tables, the fused Euler step with
+      hand-derived tangents, 64-instance tiles, vectorised over the tile (oracle/c/fes_affine.c) — so that the GPU /
+      CPU ratio of this leg is hardware only."""
+    from oracle import c_affine, c_oracle, fes_oracle as O
+
+    threads = min(16, len(os.sched_getaffinity(0)))
+    pb = O.Problem(name=name, c=O.model_constants(name), n_shooting=ocp.n_shooting, final_time=1.0,
+                   truncation=truncation, rows=ocp.stim_rows, scheme="RK1", n_steps=ocp.ode_solver.n_integration_steps)
+    rng = np.random.default_rng(0)
+    chunk = 4096 if name == "ding2003" else 1024
+    v = rng.uniform(0.0, 1.0, (chunk, pb.nv))
+    per = np.array([1.5, 250.0] + ([5e-4] if pb.nu else []))
+    v *= np.tile(per, pb.nv // len(per) + 1)[: pb.nv]
+    if pb.nu:
+        v[:, 2::3] = np.maximum(v[:, 2::3], pb.c["pd0"])
+    legs = {}
+    rate, done, el = _timed(lambda: c_oracle.shooting(pb, v, threads=threads), budget_s * 0.5, chunk)
+    legs["as_written"] = {"value": rate, "threads": threads, "instances": done, "seconds": el}
+    rate, done, el = _timed(lambda: c_oracle.shooting(pb, v[: chunk // 8], threads=1), budget_s * 0.2, chunk // 8)
+    legs["as_written_1core"] = {"value": rate, "threads": 1, "instances": done, "seconds": el}
+    ev = c_affine.Evaluator(pb)
+    Bt = 1 << 15
+    vt = np.ascontiguousarray(np.tile(v, (Bt // chunk + 1, 1))[:Bt].reshape(Bt // 64, 64, pb.nv).transpose(0, 2, 1))
+    g, jac = np.empty((Bt // 64, ev.ng, 64)), np.empty((Bt // 64, ev.nnz, 64))
+    rate, done, el = _timed(lambda: ev(vt, threads=threads, g=g, jac=jac), budget_s * 0.15, Bt)
+    legs["same_formulation"] = {"value": rate, "threads": threads, "instances": done, "seconds": el}
+    rate, done, el = _timed(lambda: ev(vt, threads=1, g=g, jac=jac), budget_s * 0.15, Bt)
+    legs["same_formulation_1core"] = {"value": rate, "threads": 1, "instances": done, "seconds": el}
+    a = legs["as_written"]
+    return {"value": a["value"], "unit": "instance-evals/s", "cores": threads, "kind": "port",
+            "sample": f"{a['instances']} instances of {label} (g + J_g, as-written calcium sum: 2T-1 exp per RK stage), "
+                      f"oracle/c/fes_oracle.c, OpenMP {threads} threads, {a['seconds']:.1f} s; the other legs in `legs`",
+            "legs": legs, "casadi": casadi_probe()}
 
 
 def build_cfg3():
@@ -142,8 +180,6 @@ def cfg3_section(device, cpu_seconds, steps=50, B=1 << 18):
     algorithmic HBM rate (read v, write g and J_g values) and the C port on the host cores on a bounded sample."""
     import torch
 
-    from oracle import c_oracle, fes_oracle as O
-
     ocp = build_cfg3()
     dev = f"cuda:{device}"
     h = ocp.nlp(batch=B, layout="tiled64", device=device)
@@ -169,21 +205,7 @@ def cfg3_section(device, cpu_seconds, steps=50, B=1 << 18):
            "achieved_GBps": nbytes * B / (ms * 1e-3) / 1e9, "bytes_per_instance": nbytes, "cpu_baseline": None}
     h.close()
     if cpu_seconds > 0:
-        threads = min(16, len(os.sched_getaffinity(0)))
-        pb = O.Problem(name="ding2007", c=O.model_constants("ding2007"), n_shooting=ocp.n_shooting, final_time=1.0,
-                       truncation=10, rows=ocp.stim_rows, scheme="RK1", n_steps=10)
-        chunk = 1024
-        c_oracle.shooting(pb, va[:64], threads=threads)
-        done, t0 = 0, time.perf_counter()
-        while True:
-            c_oracle.shooting(pb, va[:chunk], threads=threads)
-            done += chunk
-            el = time.perf_counter() - t0
-            if el >= cpu_seconds:
-                break
-        out["cpu_baseline"] = {"value": done / el, "unit": "instance-evals/s", "cores": threads, "kind": "port",
-                               "sample": f"{done} cfg-3 instances (g + J_g, as-written calcium sum), "
-                                         f"oracle/c/fes_oracle.c, OpenMP {threads} threads, {el:.1f} s"}
+        out["cpu_baseline"] = cpu_baseline(ocp, cpu_seconds, name="ding2007", truncation=10, label="cfg3")
     return out
 
 

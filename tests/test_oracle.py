@@ -159,3 +159,23 @@ def test_structural_pattern_covers_every_nonzero(name, scheme):
             for r in range(pb.nx):
                 inside = sorted(pattern[r])
                 assert np.all(np.any(blocks[:, :, r, inside] != 0.0, axis=(0, 1)))
+
+
+@pytest.mark.parametrize("cfg", ["cfg2", "cfg3"])
+def test_same_formulation_cpu_baseline_matches_the_oracle(cfg):
+    """oracle/c/fes_affine.c — bench.py's same-formulation CPU leg (affine calcium tables, fused Euler step, 64-instance
+    tiles) — gives the oracle's g and J_g (complex step) to 1e-12 on BASELINE configs[1] and [2]."""
+    from oracle import c_affine
+    from tests import cases
+
+    pb = cases.oracle_problem(**getattr(cases, cfg)())
+    B = 128
+    v = cases.random_decision(pb, B, seed=4)
+    vt = np.ascontiguousarray(v.reshape(B // 64, 64, -1).transpose(0, 2, 1))
+    g, j = c_affine.Evaluator(pb)(vt, threads=2)
+    g = g.transpose(0, 2, 1).reshape(B, -1)
+    j = j.transpose(0, 2, 1).reshape(B, -1)
+    X, _, _ = pb.unpack(v)
+    ref_g, ref_j = O.eval_g(pb, v), O.eval_jac_g(pb, v)
+    assert np.max(np.abs(g - ref_g) / (np.abs(ref_g) + np.abs(X[:, 1:, :].reshape(B, -1)))) < 1e-12
+    assert np.max(np.abs(j - ref_j) / (np.abs(ref_j) + 1e-300)) < 1e-12
