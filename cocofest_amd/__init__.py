@@ -25,12 +25,12 @@ from .msk import FesMskModel, FesMskOcp, OcpFesMsk
 from .nmpc import FesNmpc, NmpcFesMsk, NmpcResult
 from .ocp import Axis, Constraint, ConstraintFcn, ConstraintList, FesOcp, Node, Objective, ObjectiveFcn, ObjectiveList, OcpFes
 from .ode_solver import ControlType, OdeSolver
-from .solver import BatchedIpm, IpmOptions, IpmResult
+from .solver import BatchedIpm, IpmOptions, IpmResult, Solver
 
 __all__ = [
     "CfxError", "Handle", "load_library", "DingModelFrequency", "DingModelFrequencyWithFatigue",
     "DingModelPulseIntensityFrequency", "DingModelPulseIntensityFrequencyWithFatigue",
     "DingModelPulseWidthFrequency", "DingModelPulseWidthFrequencyWithFatigue", "FesModel", "ModelMaker",
     "FourierSeries", "IvpFes", "FesOcp", "Axis", "Constraint", "ConstraintFcn", "ConstraintList", "Node", "Objective", "ObjectiveFcn", "ObjectiveList", "OcpFes",
-    "ControlType", "OdeSolver", "FesMskModel", "FesMskOcp", "OcpFesMsk", "FesNmpc", "NmpcFesMsk", "NmpcResult", "BatchedIpm", "IpmOptions", "IpmResult",
+    "ControlType", "OdeSolver", "FesMskModel", "FesMskOcp", "OcpFesMsk", "FesNmpc", "NmpcFesMsk", "NmpcResult", "BatchedIpm", "IpmOptions", "IpmResult", "Solver",
 ]

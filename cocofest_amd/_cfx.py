@@ -97,6 +97,11 @@ class Sizes(C.Structure):
                 ("nx", C.c_int32), ("nu", C.c_int32)]
 
 
+class LaunchShape(C.Structure):
+    _fields_ = [("intervals_per_thread", C.c_int32), ("intervals_fast", C.c_int32), ("instances_per_lane", C.c_int32),
+                ("instances_per_lane_g", C.c_int32), ("msk_intervals_per_block", C.c_int32)]
+
+
 class IpmOptions(C.Structure):
     _fields_ = [("tol", C.c_double), ("max_iter", C.c_int32), ("acceptable_tol", C.c_double),
                 ("acceptable_iter", C.c_int32), ("mu_init", C.c_double), ("bound_relax_factor", C.c_double),
@@ -121,6 +126,7 @@ SIGNATURES = {
     "cfx_create": (C.c_int, [C.POINTER(Problem), C.POINTER(_P)]),
     "cfx_destroy": (None, [_P]),
     "cfx_get_sizes": (C.c_int, [_P, C.POINTER(Sizes)]),
+    "cfx_get_launch_shape": (C.c_int, [_P, C.POINTER(LaunchShape)]),
     "cfx_set_stream": (C.c_int, [_P, _P]),
     "cfx_synchronize": (C.c_int, [_P]),
     "cfx_last_error": (C.c_char_p, [_P]),
@@ -329,6 +335,12 @@ class Handle:
             self.close()
         except Exception:
             pass
+
+    def launch_shape(self) -> dict:
+        """The g + J_g kernels' launch shape fixed at creation (cfx_get_launch_shape)."""
+        ls = LaunchShape()
+        self._check(self.lib.cfx_get_launch_shape(self.h, C.byref(ls)))
+        return {name: int(getattr(ls, name)) for name, _ in LaunchShape._fields_}
 
     # ---- structure ----
     def jac_structure(self):

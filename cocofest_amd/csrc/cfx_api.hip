@@ -61,8 +61,7 @@ struct cfx_handle {
     int msk_nq = 0, msk_nm = 0, msk_fam = 0;
     // stage-data reuse between cfx_eval_all (with J_g) and the next cfx_eval_h at the same caller pointer, while the
     // interior point (the only caller that guarantees the point is unchanged in between) has it switched on
-    bool msk_stash = false, stash_valid = false;
-    const double* stash_v = nullptr;
+    bool msk_stash = false, stash_valid = false, stash_same_point = false;
     MskParams mp{};
     MskGeom* d_geom = nullptr;
     MskObjective* d_mobj = nullptr;
@@ -794,6 +793,20 @@ extern "C" int cfx_get_sizes(const cfx_handle* h, cfx_sizes* out) {
     return CFX_OK;
 }
 
+extern "C" int cfx_get_launch_shape(const cfx_handle* h, cfx_launch_shape* out) {
+    if (!h || !out) return CFX_EINVAL;
+    std::memset(out, 0, sizeof(*out));
+    if (h->msk) {
+        out->msk_intervals_per_block = h->mp.kpb;
+    } else {
+        out->intervals_per_thread = h->kp.kpt;
+        out->intervals_fast = h->kp.ifast;
+        out->instances_per_lane = h->ni;
+        out->instances_per_lane_g = h->ni_g;
+    }
+    return CFX_OK;
+}
+
 // internal (cfx_internal.h): what the interior-point driver needs to know about a handle
 int cfx_internal_info(const cfx_handle* h, int64_t* batch, int* layout, int* device, hipStream_t* stream) {
     if (!h) return CFX_EINVAL;
@@ -970,8 +983,12 @@ extern "C" int cfx_integrate(cfx_handle* h, const double* x0, const double* u, d
 // ------------------------------------------------------------------------------------------------------
 int cfx_internal_msk_stash(cfx_handle* h, int on) {
     if (!h) return CFX_EINVAL;
+    if (on == 2) {  // the caller vouches that the next eval_h is at the point of the last eval_all with J_g
+        h->stash_same_point = h->msk_stash && h->stash_valid;
+        return CFX_OK;
+    }
     h->msk_stash = h->msk && on;
-    h->stash_valid = false;
+    h->stash_valid = h->stash_same_point = false;
     return CFX_OK;
 }
 
@@ -1176,6 +1193,9 @@ extern "C" int cfx_msk_create(const cfx_msk_problem* p, cfx_handle** out) {
     P.B = p->batch, P.N = N, P.m = m, P.nx = nx, P.nu = nu, P.nz = nz, P.Q = Q;
     P.residual = residual ? 1 : 0, P.npw = npw, P.dt = dt, P.h = hh;
     P.T = T, P.ngk = ngk;
+    P.kpb = msk_default_kpb(P.B, N);
+    if (const char* e = std::getenv("CFX_MSK_KPB"))  // tuning / test override of the tangent kernel's launch shape
+        P.kpb = std::max(1, std::min(N, std::atoi(e)));
     h->msk_ns = ns;
 
     // ---- structural Jacobian pattern (Dep pass on the host through the same RHS code)
@@ -1209,10 +1229,10 @@ extern "C" int cfx_msk_create(const cfx_msk_problem* p, cfx_handle** out) {
     std::vector<double> imin(nm, 0.0);
     const int64_t p_off = (int64_t)N * nz + nx;
     if (ns) {
-        for (int mi = 0; mi < nm; ++mi) {  // hmed2018.py:303-310
-            const cfx_constants& c = p->muscles[mi].constants;
-            imin[mi] = std::atanh(-c.cr) / c.bs + c.Is;
-        }
+        // every muscle's window is padded with muscles_dynamics_model[0].min_pulse_intensity()
+        // (custom_constraints.py:107-114; hmed2018.py:303-310), whatever the muscle's own recruitment constants
+        const cfx_constants& c0 = p->muscles[0].constants;
+        for (int mi = 0; mi < nm; ++mi) imin[mi] = std::atanh(-c0.cr) / c0.bs + c0.Is;
         for (int k = 0; k < N; ++k)
             for (int sidx = 0; sidx < ns; ++sidx) {
                 const int mi = sidx / T, j = sidx - mi * T;
@@ -1432,7 +1452,7 @@ static int msk_eval_all(cfx_handle* h, const double* v, double* g, double* jac, 
         CFX_HIP(h, launch_msk_markers(h, V, G, J, nullptr, nullptr));
         if (J) {
             h->stash_valid = h->msk_stash;
-            h->stash_v = v;
+            h->stash_same_point = false;
         }
     }
     if (F || GR) {
@@ -1470,8 +1490,8 @@ static int msk_eval_h(cfx_handle* h, const double* v, const double* obj_factor, 
     double* W = ensure(h, h->main[S_WORK], nw, &rc);
     if (!W) return rc;
     CFX_HIP(h, hipMemsetAsync(H, 0, (size_t)B * h->sz.nnz_hess * sizeof(double), h->stream));
-    const bool reuse = h->msk_stash && h->stash_valid && h->stash_v == v;
-    h->stash_valid = false;
+    const bool reuse = h->msk_stash && h->stash_valid && h->stash_same_point;
+    h->stash_valid = h->stash_same_point = false;
     CFX_HIP(h, launch_msk_hessian(h->msk_nq, h->msk_nm, h->msk_fam, h->scheme, h->mp, h->d_geom,
                                   (const int16_t*)h->d_htasks, h->n_htasks, V, LAM, H, W, reuse, h->stream));
     if (h->n_obj)

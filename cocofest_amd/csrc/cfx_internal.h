@@ -23,6 +23,7 @@ int cfx_band_solve_multi(int64_t n, int32_t kl, int32_t ku, int64_t batch, int32
                          const int32_t* ipiv, double* X, int64_t x_inst, int64_t x_part, int64_t x_rhs, int32_t nx,
                          double* Y, int64_t y_inst, int64_t y_part, void* stream);
 
-// MSK handles: keep the stage values / coefficients of a cfx_eval_all with J_g for the next cfx_eval_h at the same
-// caller pointer (on = 1).  Only for callers that leave the point unchanged in between (cfx_ipm_solve).
+// MSK handles: keep the stage values / coefficients of every cfx_eval_all with J_g (on = 1; 0 switches it off); a
+// following cfx_eval_h re-uses them only when the caller has declared, with on = 2 right before it, that the point
+// is the one of that eval_all (cfx_ipm_solve, which does not move K.vx in between).  Any other eval_h recomputes.
 int cfx_internal_msk_stash(cfx_handle* h, int on);

@@ -1863,6 +1863,7 @@ static int ipm_solve(cfx_ipm* s, const double* v0, const double* fixed_values, d
         }
         reinit = false;
         IPM_HIP(s, hipGetLastError());
+        cfx_internal_msk_stash(s->h, 2);  // K.vx is the point of eval_full above: the MSK stage data may be re-used
         IPM_CFX(s, cfx_eval_h(s->h, K.vx, K.of, K.ysc, K.hv, CFX_DEVICE));
         s->st.eval_h++;
         // inertia correction by the curvature test: grow dw until dx^T (W + Sigma + dw) dx > 0

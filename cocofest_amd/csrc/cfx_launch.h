@@ -76,8 +76,17 @@ hipError_t launch_shooting_t(const KParams& P, const double* V, double* G, doubl
     const int nchunk = D > 0 ? (nz + D - 1) / D : 1;
     const int64_t per_block = (int64_t)kBlock * NI;  // NI adjacent instances per lane
     const unsigned nbi = (unsigned)((P.B + per_block - 1) / per_block), nbk = (unsigned)((P.N + P.kpt - 1) / P.kpt);
-    dim3 grid(P.ifast ? nbk : nbi, P.ifast ? nbi : nbk, (unsigned)nchunk);
-    hipLaunchKernelGGL((k_shooting<MODEL, SCHEME, D, TMAX, NI>), grid, dim3(kBlock), 0, s, P, V, G, J);
+    if (!P.ifast || nbi <= (unsigned)kMaxGridY) {
+        dim3 grid(P.ifast ? nbk : nbi, P.ifast ? nbi : nbk, (unsigned)nchunk);
+        hipLaunchKernelGGL((k_shooting<MODEL, SCHEME, D, TMAX, NI>), grid, dim3(kBlock), 0, s, P, V, G, J);
+    } else {
+        // the intervals-fast order was chosen for the handle's instances per lane; this launch runs fewer (an
+        // unaligned buffer) and its instance blocks no longer fit grid.y: instance blocks on grid.x instead
+        KParams Q = P;
+        Q.ifast = 0;
+        hipLaunchKernelGGL((k_shooting<MODEL, SCHEME, D, TMAX, NI>), dim3(nbi, nbk, (unsigned)nchunk), dim3(kBlock), 0,
+                           s, Q, V, G, J);
+    }
     return hipGetLastError();
 }
 

@@ -182,6 +182,7 @@ struct MskParams {
     int64_t B;
     int32_t N, m, nx, nu, nz, Q, nnzk, nhk, residual, npw;
     int32_t T, ngk;      // truncation; rows per interval (nx continuity rows, then the Hmed sliding-window rows)
+    int32_t kpb;         // k_msk_tangents_lds: consecutive intervals per block (fixed by cfx_msk_create)
     double dt, h;
     // calcium sums [N][Q][NM] at every RK stage time (host, reference operation order); Hmed2018: the per-pulse
     // coefficients r_i exp(-(t - t_i) / tau_c) [N][Q][NM][TMAX] of cs = sum_i coef_i lambda(I_i)
@@ -1046,6 +1047,14 @@ __global__ void __launch_bounds__(256) k_msk_tangents(const MskParams P, const M
 // runs kpb consecutive intervals with the next sub-step's coefficients prefetched during the current one (below).
 constexpr int kMskLdsCols = 16;
 constexpr int kMskLdsLoads = 16;  // coefficient loads in flight per thread while staging
+constexpr int kMskTangentInstances = 32;  // TW: instances per k_msk_tangents_lds block
+
+// Default intervals per k_msk_tangents_lds block: as many as keep >= 4,096 blocks (16 per CU) in flight.
+inline int msk_default_kpb(int64_t B, int N) {
+    const int64_t nbx = (B + kMskTangentInstances - 1) / kMskTangentInstances;
+    const int64_t kpb = nbx * N / 4096;
+    return (int)(kpb < 1 ? 1 : (kpb > N ? N : kpb));
+}
 
 template <int NQ, int NM, int FAM, int SCHEME, int TW>
 __global__ void __launch_bounds__(32 * kMskLdsCols) k_msk_tangents_lds(const MskParams P, const MskGeom* __restrict__ GG,

@@ -46,10 +46,9 @@ hipError_t shoot_t(const MskParams& P, const MskGeom* G, const double* V, double
                        dim3(kMskBlk), 0, s, P, G, V, (const double*)XS);
     if (P.nz <= kMskLdsCols) {  // coefficients through LDS, one block per 32 instances
         constexpr int ST = SCHEME == 4 ? 4 : (SCHEME == 2 ? 2 : 1), TW = 32;
-        // intervals per block: as many as keep >= 4,096 blocks (16 per CU); CFX_MSK_KPB overrides (tuning)
+        static_assert(TW == kMskTangentInstances, "cfx_msk_create sizes kpb for this block width");
         const int64_t nbx = (P.B + TW - 1) / TW;
-        int kpb = (int)std::max<int64_t>(1, std::min<int64_t>(P.N, nbx * P.N / 4096));
-        if (const char* e = std::getenv("CFX_MSK_KPB")) kpb = std::max(1, std::min(P.N, std::atoi(e)));
+        const int kpb = std::max(1, std::min(P.N, P.kpb));  // intervals per block (cfx_msk_create)
         // two coefficient buffers when B is even (k_msk_tangents_lds): above the default 64 KiB of dynamic LDS for cfg 5
         const size_t lds = (P.B % 2 == 0 ? 2 : 1) * ST * NC * TW * sizeof(double);
         static size_t raised = 65536;  // one per instantiation

@@ -34,7 +34,10 @@ class IvpFes:
         self.pulse_width = self.fes_parameters["pulse_width"]
         self.pulse_intensity = self.fes_parameters["pulse_intensity"]
         self.final_time = self.ivp_parameters["final_time"]
-        self.n_shooting = OcpFes.prepare_n_shooting(self.stim_time, self.final_time)
+        # extension: ivp_parameters["n_shooting"] sets the node count (the reference always takes the LCM rule of
+        # OcpFes.prepare_n_shooting, ivp_fes.py:73), e.g. BASELINE configs[0]'s n_shooting = 20 for 10 pulses
+        self._n_shooting_given = self.ivp_parameters["n_shooting"]
+        self.n_shooting = self._n_shooting_given or OcpFes.prepare_n_shooting(self.stim_time, self.final_time)
         self.pulse_mode = self.fes_parameters["pulse_mode"]
         self._pulse_mode_settings()
         self.dt = np.array([self.final_time / self.n_shooting])
@@ -63,7 +66,8 @@ class IvpFes:
         self.fes_parameters = fes_parameters
 
     def _fill_ivp_dict(self, ivp_parameters):
-        default = {"final_time": None, "ode_solver": OdeSolver.RK4(n_integration_steps=10), "n_threads": 1}
+        default = {"final_time": None, "ode_solver": OdeSolver.RK4(n_integration_steps=10), "n_threads": 1,
+                   "n_shooting": None}
         ivp_parameters = {} if ivp_parameters is None else ivp_parameters
         for key in default:
             if key not in ivp_parameters:
@@ -102,6 +106,9 @@ class IvpFes:
             raise ValueError("ode_solver must be a OdeSolver type")
         if not isinstance(ivp["n_threads"], int):
             raise ValueError("n_thread must be a int type")
+        ns = ivp["n_shooting"]
+        if ns is not None and (isinstance(ns, bool) or not isinstance(ns, int) or ns < 1):
+            raise ValueError("n_shooting must be a positive int (or None for the stimulation-time LCM rule)")
 
     def _pulse_mode_settings(self):
         """Doublets / triplets add pulses 5 and 10 ms after each one and write the list back into the model
@@ -118,7 +125,8 @@ class IvpFes:
         self.stim_time.sort()
         self.model.stim_time = self.stim_time
         self.n_stim = len(self.stim_time)
-        self.n_shooting = OcpFes.prepare_n_shooting(self.stim_time, self.final_time)
+        if self._n_shooting_given is None:
+            self.n_shooting = OcpFes.prepare_n_shooting(self.stim_time, self.final_time)
 
     def _build_controls(self):
         """Per-interval controls, (nu, N).  Ding2007: width of the last pulse at or before the node

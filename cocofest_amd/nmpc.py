@@ -44,6 +44,35 @@ class NmpcResult:
     converged: list = field(default_factory=list)    # per window: (B,) bool
     window_wall: list = field(default_factory=list)  # per window: seconds
     solve_wall: list = field(default_factory=list)   # per window: seconds inside the interior point
+    # max_consecutive_failing: per scenario, the window whose failure made it the limit-th in a row (-1: never); that
+    # window and everything after it are not committed (NaN), as bioptim's loop stops before storing it
+    stopped_at: np.ndarray | None = None
+
+
+class _Failing:
+    """bioptim's ``max_consecutive_failing`` (MultiCyclicNonlinearModelPredictiveControl.solve, passed by
+    fes_nmpc.py:158,168) per scenario of a lockstep batch: a scenario stops after that many consecutive windows whose
+    interior point did not converge; the loop ends when every scenario has stopped (or the cycles / the update
+    function say so)."""
+
+    def __init__(self, B: int, limit: int | None):
+        self.limit = int(limit) if limit else 0
+        self.count = np.zeros(B, dtype=int)
+        self.stopped_at = np.full(B, -1, dtype=int)
+
+    def update(self, converged, w: int):
+        converged = np.asarray(converged, dtype=bool)
+        self.count = np.where(converged, 0, self.count + 1)
+        if self.limit:
+            newly = (self.stopped_at < 0) & (self.count >= self.limit)
+            self.stopped_at[newly] = w
+
+    def mask(self):
+        """Scenarios whose commits from the current window on are void."""
+        return self.stopped_at >= 0
+
+    def all_stopped(self) -> bool:
+        return bool(self.limit) and bool(np.all(self.stopped_at >= 0))
 
 
 class FesNmpc:
@@ -120,10 +149,18 @@ class FesNmpc:
         return ocp
 
     # ---- the receding-horizon loop --------------------------------------------------------------------
-    def solve(self, n_cycles: int, x0=None, hist=None):
-        """Advance until ``n_cycles`` cycles are committed.  x0: (B, nx) initial states (default rest).
-        Returns an NmpcResult with the committed trajectory of every scenario."""
-        from .solver import BatchedIpm, NativeIpm
+    def solve(self, n_cycles: int | None = None, x0=None, hist=None, update_functions=None, solver=None,
+              max_consecutive_failing: int | None = None):
+        """Advance until ``n_cycles`` cycles are committed, or — bioptim style — while
+        ``update_functions(self, cycle_idx, result)`` returns True (cycle_idx = windows solved so far).  x0: (B, nx)
+        initial states (default rest); solver: a Solver.IPOPT (options of every window's interior point);
+        max_consecutive_failing: stop a scenario after that many consecutive non-converged windows (NmpcResult.
+        stopped_at).  Returns an NmpcResult with the committed trajectory of every scenario."""
+        from .solver import BatchedIpm, IpmOptions, NativeIpm, apply_solver
+
+        if n_cycles is None and update_functions is None:
+            raise ValueError("give n_cycles or update_functions")
+        options = self.options if solver is None else apply_solver(copy.copy(self.options or IpmOptions()), solver)
 
         B, T = self.B, self.T
         nx = self.model.nb_state
@@ -137,21 +174,23 @@ class FesNmpc:
         ctrl_parts = []
         result = NmpcResult(time=None, states={}, controls={}, pulse_intensity=None, stim_time=[])
         warm = None
-        n_windows = int(np.ceil(n_cycles / self.n_adv))
+        n_windows = int(np.ceil(n_cycles / self.n_adv)) if n_cycles is not None else None
         t_off = 0.0
+        failing = _Failing(B, max_consecutive_failing)
         # windows whose stimulation history has the same times share one transcription (stim table, handle,
         # KKT maps): with identical cycles that is every window after the first T pulses
         cache = {}
-        for w in range(n_windows):
+        w = 0
+        while n_windows is None or w < n_windows:
             t0 = time.perf_counter()
             key = tuple(np.round(hist_t, 9))
             if key not in cache:
                 ocp = self._window_ocp(hist_t, hist_i[0] if self.hmed else None)
                 if self.evaluator is not None:
-                    ipm = BatchedIpm(ocp, batch=B, options=self.options, handle=self.evaluator(ocp, B),
+                    ipm = BatchedIpm(ocp, batch=B, options=options, handle=self.evaluator(ocp, B),
                                      torch_device=self.torch_device, band=self.band)
                 else:
-                    ipm = NativeIpm(ocp, batch=B, device=self.device, options=self.options)
+                    ipm = NativeIpm(ocp, batch=B, device=self.device, options=options)
                 cache[key] = (ocp, ipm)
             ocp, ipm = cache[key]
             v0 = np.tile(ocp.initial_guess_vector(), (B, 1)) if warm is None else warm
@@ -174,16 +213,19 @@ class FesNmpc:
             result.solve_wall.append(time.perf_counter() - ts)
             result.iterations.append(res.iterations)
             result.converged.append(res.converged)
+            failing.update(res.converged, w)
+            void = failing.mask()
             # commit the first n_adv cycles
             adv_nodes = self.n_adv * self.cycle_len
             V = res.v
             body = V[:, : ocp.n_shooting * nzb].reshape(B, ocp.n_shooting, nzb)
             xs = np.concatenate([body[:, :, :nx], V[:, None, ocp.n_shooting * nzb: ocp.n_shooting * nzb + nx]], 1)
             dt = ocp.final_time / ocp.n_shooting
-            states.append(np.transpose(xs[:, 1: adv_nodes + 1, :], (0, 2, 1)))
+            states.append(np.where(void[:, None, None], np.nan, np.transpose(xs[:, 1: adv_nodes + 1, :], (0, 2, 1))))
             t_nodes += [t_off + (k + 1) * dt for k in range(adv_nodes)]
             if ocp.nu:
-                ctrl_parts.append(np.transpose(body[:, :adv_nodes, ocp.uoff:], (0, 2, 1)))
+                ctrl_parts.append(np.where(void[:, None, None], np.nan,
+                                           np.transpose(body[:, :adv_nodes, ocp.uoff:], (0, 2, 1))))
             x_start = xs[:, adv_nodes, :]
             # pulses of the committed cycles and the new history (relative to the next window's start)
             adv_time = self.n_adv * self.cycle_duration
@@ -194,7 +236,7 @@ class FesNmpc:
             if self.hmed:
                 P = V[:, ocp.nv - ocp.n_params:]
                 new_int = P[:, T: T + len(new)]
-                committed_int.append(new_int)
+                committed_int.append(np.where(void[:, None], np.nan, new_int))
                 all_int = np.concatenate([hist_i, new_int], axis=1)
                 hist_i = all_int[:, -T:]
             hist_t = [t - adv_time for t in all_hist[-T:]]
@@ -203,8 +245,14 @@ class FesNmpc:
             # warm start: shift by the committed nodes, repeat the last cycle
             warm = self._shift(ocp, V, adv_nodes)
             result.window_wall.append(time.perf_counter() - t0)
+            w += 1
+            if failing.all_stopped() or (update_functions is not None and not update_functions(self, w, result)):
+                break
         for _, ipm in cache.values():
             ipm.close()
+        result.stopped_at = failing.stopped_at
+        if n_cycles is None or w * self.n_adv < n_cycles:
+            n_cycles = w * self.n_adv
         X = np.concatenate(states, axis=2)
         n_keep = n_cycles * self.cycle_len
         result.time = np.asarray(t_nodes[: n_keep + 1])
@@ -217,6 +265,18 @@ class FesNmpc:
         if self.hmed:
             result.pulse_intensity = np.concatenate(committed_int, axis=1)[:, :n_pulses]
         return result
+
+    def solve_fes_nmpc(self, update_functions, solver=None, total_cycles: int | None = None, cycle_solutions=None,
+                       get_all_iterations: bool = True, cyclic_options: dict | None = None,
+                       max_consecutive_failing: int = 3, x0=None):
+        """The reference's driver entry (fes_nmpc.py:150-192): run the receding horizon while ``update_functions``
+        allows it (at most ``total_cycles`` cycles), each window solved with ``solver``'s options, stopping a scenario
+        after ``max_consecutive_failing`` consecutive non-converged windows.  ``cycle_solutions`` /
+        ``get_all_iterations`` / ``cyclic_options`` select which bioptim Solution objects are built; every window's
+        convergence, iterations and the committed trajectory are always in the returned NmpcResult."""
+        del cycle_solutions, get_all_iterations, cyclic_options
+        return self.solve(n_cycles=total_cycles, x0=x0, update_functions=update_functions, solver=solver,
+                          max_consecutive_failing=max_consecutive_failing)
 
     def _shift(self, ocp, V, adv_nodes):
         """Warm start of the next window: the solution shifted by ``adv_nodes`` intervals, the freed tail filled
@@ -325,21 +385,20 @@ class NmpcFesMsk:
         lo[:, 0] = hi[:, 0] = start
         return ocp
 
-    def solve(self, update_functions=None, solver=None, n_cycles: int | None = None, x0=None):
+    def solve(self, update_functions=None, solver=None, n_cycles: int | None = None, x0=None,
+              max_consecutive_failing: int | None = None):
         """Advance until ``n_cycles`` cycles are committed (default ``n_total_cycles``), or — bioptim style — while
         ``update_functions(self, cycle_idx, result)`` returns True.  x0: (B, nx) start states (default: the first
-        window's node-0 bounds / initial guess).  Returns an NmpcResult."""
-        from .solver import IpmOptions, NativeIpm
+        window's node-0 bounds / initial guess); solver: a Solver.IPOPT; max_consecutive_failing: stop a scenario
+        after that many consecutive non-converged windows (NmpcResult.stopped_at).  Returns an NmpcResult."""
+        from .solver import IpmOptions, NativeIpm, apply_solver
 
         if n_cycles is None:
             n_cycles = self.n_total
         if n_cycles is None and update_functions is None:
             raise ValueError("give n_cycles (or n_total_cycles) or update_functions")
-        opts = self.options or IpmOptions()
-        if solver is not None:
-            for k in ("tol", "max_iter"):
-                if hasattr(solver, k):
-                    setattr(opts, k, getattr(solver, k))
+        opts = apply_solver(copy.copy(self.options or IpmOptions()), solver)
+        failing = _Failing(self.B, max_consecutive_failing)
         B, T = self.B, self.T
         hist_t = [PLACEHOLDER_TIME] * T
         cache = {}
@@ -375,14 +434,16 @@ class NmpcFesMsk:
             result.solve_wall.append(time.perf_counter() - ts)
             result.iterations.append(res.iterations)
             result.converged.append(res.converged)
+            failing.update(res.converged, w)
+            void = failing.mask()
             N, nzb = ocp.n_shooting, ocp.nzb
             body = res.v[:, : N * nzb].reshape(B, N, nzb)
             xs = np.concatenate([body[:, :, :nx], res.v[:, None, N * nzb: N * nzb + nx]], 1)
-            states.append(np.transpose(xs[:, 1: adv_nodes + 1, :], (0, 2, 1)))
+            states.append(np.where(void[:, None, None], np.nan, np.transpose(xs[:, 1: adv_nodes + 1, :], (0, 2, 1))))
             dt = ocp.final_time / N
             t_nodes += [t_off + (k + 1) * dt for k in range(adv_nodes)]
             if ocp.nu:
-                ctrl_parts.append(np.transpose(body[:, :adv_nodes, nx:], (0, 2, 1)))
+                ctrl_parts.append(np.where(void[:, None, None], np.nan, np.transpose(body[:, :adv_nodes, nx:], (0, 2, 1))))
             x_start = xs[:, adv_nodes, :]
             new = [t for t in self._window_stims() if t < adv_time - 1e-12]
             committed += [t + t_off for t in new]
@@ -394,12 +455,13 @@ class NmpcFesMsk:
             warm[:, : N * nzb] = blocks.reshape(B, -1)
             result.window_wall.append(time.perf_counter() - t0)
             w += 1
-            if update_functions is not None and not update_functions(self, w, result):
+            if failing.all_stopped() or (update_functions is not None and not update_functions(self, w, result)):
                 break
         for _, ipm in cache.values():
             ipm.close()
+        result.stopped_at = failing.stopped_at
         X = np.concatenate(states, axis=2)
-        n_keep = (w * self.n_adv if n_cycles is None else n_cycles) * self.cycle_len
+        n_keep = min(w * self.n_adv, n_cycles if n_cycles is not None else w * self.n_adv) * self.cycle_len
         result.time = np.asarray(t_nodes[: n_keep + 1])
         result.states = {name: X[:, i, : n_keep + 1] for i, name in enumerate(ocp.state_names)}
         if ctrl_parts:

@@ -53,7 +53,92 @@ class IpmOptions:
     # if none is acceptable the solver returns there and backtracks.  0 disables it
     watchdog_shortened_iter_trigger: int = 10
     watchdog_trial_iter_max: int = 3
+    # Ipopt's hessian_approximation: "exact" (the callbacks' Lagrangian Hessian) or "limited-memory" (L-BFGS of
+    # limited_memory_max_history pairs, Ipopt's defaults)
+    hessian_approximation: str = "exact"
+    limited_memory_max_history: int = 6
     verbose: bool = False
+
+
+class Solver:
+    """bioptim's solver namespace as cocofest uses it: ``ocp.solve(Solver.IPOPT(_max_iter=..., _tol=...,
+    _hessian_approximation="limited-memory"))`` (examples/getting_started/frequency_optimization.py:22,
+    pulse_duration_optimization.py:41).  The options map onto the native interior point's (IpmOptions); the
+    ones that only steer Ipopt's own output or its external linear solver are accepted and ignored."""
+
+    class IPOPT:
+        _OPTIONS = {"_tol": "tol", "_max_iter": "max_iter", "_acceptable_tol": "acceptable_tol",
+                    "_acceptable_iter": "acceptable_iter", "_mu_init": "mu_init",
+                    "_bound_relax_factor": "bound_relax_factor", "_bound_push": "bound_push",
+                    "_hessian_approximation": "hessian_approximation",
+                    "_limited_memory_max_history": "limited_memory_max_history", "_max_soc": "max_soc",
+                    "_watchdog_shortened_iter_trigger": "watchdog_shortened_iter_trigger",
+                    "_watchdog_trial_iter_max": "watchdog_trial_iter_max"}
+        _IGNORED = {"show_online_optim", "show_options", "_print_level", "_linear_solver", "_nlp_scaling_method",
+                    "_check_derivatives_for_naninf", "_c_compile", "_print_timing_statistics", "_output_file",
+                    "_constr_viol_tol", "_dual_inf_tol", "_compl_inf_tol"}
+
+        def __init__(self, show_online_optim: bool = False, show_options: dict | None = None, **kwargs):
+            self._tol = 1e-6
+            self._max_iter = 1000
+            self._hessian_approximation = "exact"
+            self._limited_memory_max_history = 6
+            self._print_level = 5
+            self._linear_solver = "mumps"
+            for k, v in kwargs.items():
+                if k not in self._OPTIONS and k not in self._IGNORED:
+                    raise TypeError(f"Solver.IPOPT: unknown option {k!r}")
+                setattr(self, k, v)
+            if self._hessian_approximation not in ("exact", "limited-memory"):
+                raise ValueError("hessian_approximation must be 'exact' or 'limited-memory'")
+
+        # bioptim's setters
+        def set_maximum_iterations(self, n: int):
+            self._max_iter = int(n)
+
+        def set_tol(self, tol: float):
+            self._tol = float(tol)
+
+        def set_hessian_approximation(self, value: str):
+            if value not in ("exact", "limited-memory"):
+                raise ValueError("hessian_approximation must be 'exact' or 'limited-memory'")
+            self._hessian_approximation = value
+
+        def set_limited_memory_max_history(self, n: int):
+            self._limited_memory_max_history = int(n)
+
+        def set_print_level(self, n: int):
+            self._print_level = int(n)
+
+        def set_linear_solver(self, name: str):
+            self._linear_solver = name
+
+        # the plain names the round-1 facade read
+        @property
+        def tol(self):
+            return self._tol
+
+        @property
+        def max_iter(self):
+            return self._max_iter
+
+        def apply(self, opts: "IpmOptions") -> "IpmOptions":
+            for k, name in self._OPTIONS.items():
+                if hasattr(self, k):
+                    setattr(opts, name, getattr(self, k))
+            return opts
+
+
+def apply_solver(opts: "IpmOptions", solver) -> "IpmOptions":
+    """Options of a Solver.IPOPT (or any object with tol / max_iter attributes) onto IpmOptions."""
+    if solver is None:
+        return opts
+    if isinstance(solver, Solver.IPOPT):
+        return solver.apply(opts)
+    for k in ("tol", "max_iter"):
+        if hasattr(solver, k):
+            setattr(opts, k, getattr(solver, k))
+    return opts
 
 
 @dataclass
@@ -738,11 +823,7 @@ class NativeIpm:
 
 def solve_ocp(ocp, solver=None, batch: int = 1, device: int = 0, v0=None, **kwargs):
     """`FesOcp.solve`: interior-point solve of `batch` instances (multi-start when v0 differs per row)."""
-    opts = IpmOptions(**{k: v for k, v in kwargs.items() if hasattr(IpmOptions, k)})
-    if solver is not None:
-        for k in ("tol", "max_iter"):
-            if hasattr(solver, k):
-                setattr(opts, k, getattr(solver, k))
+    opts = apply_solver(IpmOptions(**{k: v for k, v in kwargs.items() if hasattr(IpmOptions, k)}), solver)
     # the product path is libcfx's own solver; BatchedIpm only for what it alone offers (iterative refinement)
     ipm = (BatchedIpm if opts.refine else NativeIpm)(ocp, batch=batch, device=device, options=opts)
     try:

@@ -155,6 +155,18 @@ const char *cfx_last_error(const cfx_handle *h); /* h == NULL: last handle-free 
 int cfx_abi_version(void);
 int cfx_device_count(void);
 
+/* Launch shape of the handle's g + J_g kernels, fixed at creation from the batch size (tuning; the environment
+   variables CFX_KPT, CFX_IFAST, CFX_NI and CFX_MSK_KPB, read by cfx_create / cfx_msk_create, override it).  Every
+   shape gives the same bits; the parity tests pin that at the shapes the benchmark times. */
+typedef struct cfx_launch_shape {
+    int32_t intervals_per_thread;    /* shooting: consecutive intervals one thread integrates, x_{k+1} carried */
+    int32_t intervals_fast;          /* shooting: interval chunks on grid.x, instance blocks on grid.y */
+    int32_t instances_per_lane;      /* shooting g + J_g: adjacent instances per lane (16-byte accesses) */
+    int32_t instances_per_lane_g;    /* shooting g only */
+    int32_t msk_intervals_per_block; /* musculoskeletal tangent kernel: intervals per block (LDS double buffer) */
+} cfx_launch_shape;
+int cfx_get_launch_shape(const cfx_handle *h, cfx_launch_shape *out);
+
 /* ---- sparsity (Ipopt eval_jac_g / eval_h with values == NULL) ---------------------------------- */
 int cfx_jac_structure(const cfx_handle *h, int32_t *row, int32_t *col);  /* nnz_jac entries */
 int cfx_hess_structure(const cfx_handle *h, int32_t *row, int32_t *col); /* nnz_hess, row >= col */

@@ -742,3 +742,29 @@ def test_interior_point_on_gpu_matches_the_oracle_driven_run(name):
     ref = rc.v[0]
     scale = np.where(np.abs(ref) < 1e-2, np.abs(ref) + 1e-6, np.maximum(np.abs(ref), 1e-3 * np.abs(ref).max()))
     assert np.max(np.abs(rg.v - ref) / scale) < 1e-6
+
+
+@pytest.mark.parametrize("name", ["ding2003_with_fatigue", "ding2007_with_fatigue", "hmed2018_with_fatigue"])
+def test_cfg1_ivp_at_its_stated_size(name):
+    """BASELINE configs[0]: IvpFes DingModelFrequencyWithFatigue, 10 pulses @ 10 Hz, final time 1 s, n_shooting = 20
+    (the IvpFes n_shooting extension; the reference's LCM rule would give 10), RK4 x 10 — every sub-step sample
+    against the oracle's sequential integration (and the other fatigue families in the same shape)."""
+    from cocofest_amd import IvpFes, ModelMaker, OdeSolver
+
+    stims = cases.TEN_PULSES
+    model = ModelMaker.create_model(name, stim_time=list(stims), sum_stim_truncation=10)
+    fes = {"model": model}
+    if name.startswith("ding2007"):
+        fes["pulse_width"] = [2e-4 + 3e-5 * i for i in range(10)]
+    if name.startswith("hmed2018"):
+        fes["pulse_intensity"] = [40.0 + 5 * i for i in range(10)]
+    ivp = IvpFes(fes, {"final_time": 1.0, "ode_solver": OdeSolver.RK4(n_integration_steps=10), "n_shooting": 20})
+    assert ivp.n_shooting == 20
+    res = ivp.integrate(return_time=False)
+    got = np.stack([res[k][0] for k in model.name_dof])
+    assert got.shape == (len(model.name_dof), 20 * 10 + 1)
+    c = O.model_constants(name)
+    tab = O.stim_table(stims, 20, 1.0, 10)
+    u = O.ivp_controls(name, tab, 20, 10, fes.get("pulse_width"), fes.get("pulse_intensity"))
+    ref = O.ivp_integrate(name, c, tab.rows, u, 1.0, "RK4", 10)
+    _close(got, ref, what=f"cfg1 {name} N=20")

@@ -105,6 +105,7 @@ def test_tiled_layout_and_collocation_limits_are_rejected():
     # NULL arguments: no handle and no problem are plain EINVAL, not a crash
     assert lib.cfx_create(None, C.byref(C.c_void_p())) == _cfx.EINVAL
     assert lib.cfx_get_sizes(None, C.byref(_cfx.Sizes())) == _cfx.EINVAL
+    assert lib.cfx_get_launch_shape(None, C.byref(_cfx.LaunchShape())) == _cfx.EINVAL
     assert lib.cfx_set_stream(None, None) == _cfx.EINVAL
     assert lib.cfx_band_lu_solve(4, 1, 1, 1, None, None, 0, None, None) == _cfx.EINVAL
     assert "nrhs" in lib.cfx_last_error(None).decode()
@@ -435,7 +436,8 @@ def test_ctypes_mirrors_match_the_c_header_layout(tmp_path):
         pytest.skip("gcc not available")
     pairs = [(_cfx.Constants, "cfx_constants"), (_cfx.Objective, "cfx_objective"), (_cfx.Problem, "cfx_problem"),
              (_cfx.Sizes, "cfx_sizes"), (_cfx.MskMuscle, "cfx_msk_muscle"), (_cfx.MskMarkerPair, "cfx_msk_marker_pair"),
-             (_cfx.MskProblem, "cfx_msk_problem"), (_cfx.IpmOptions, "cfx_ipm_options"), (_cfx.IpmStats, "cfx_ipm_stats")]
+             (_cfx.MskProblem, "cfx_msk_problem"), (_cfx.IpmOptions, "cfx_ipm_options"), (_cfx.IpmStats, "cfx_ipm_stats"),
+             (_cfx.LaunchShape, "cfx_launch_shape")]
     lines, want = [], []
     for cls, cname in pairs:
         lines.append(f'printf("%zu\\n", sizeof({cname}));')
@@ -451,3 +453,22 @@ def test_ctypes_mirrors_match_the_c_header_layout(tmp_path):
     subprocess.run(["gcc", "-std=c11", "-I", str(inc), str(src), "-o", str(exe)], check=True)
     got = [int(x) for x in subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split()]
     assert got == want
+
+
+def test_ivp_n_shooting_extension():
+    """IvpFes(ivp_parameters={"n_shooting": N}) overrides the LCM node count (BASELINE configs[0] asks for 20 nodes
+    for 10 pulses); doublets keep the given count; invalid counts are refused."""
+    from cocofest_amd import IvpFes, ModelMaker
+
+    stims = [round(0.1 * i, 1) for i in range(10)]
+    m = ModelMaker.create_model("ding2003_with_fatigue", stim_time=list(stims), sum_stim_truncation=10)
+    assert IvpFes({"model": m}, {"final_time": 1.0}).n_shooting == 10
+    ivp = IvpFes({"model": m}, {"final_time": 1.0, "n_shooting": 20})
+    assert ivp.n_shooting == 20 and ivp.stim_rows.shape == (21, 10)
+    # node 1 (t = 0.05) sees only the first pulse, node 2 (t = 0.1) the first two
+    assert np.sum(ivp.stim_rows[1] > -1e6) == 1 and np.sum(ivp.stim_rows[2] > -1e6) == 2
+    m2 = ModelMaker.create_model("ding2003", stim_time=[0.0, 0.1], sum_stim_truncation=6)
+    assert IvpFes({"model": m2, "pulse_mode": "doublet"}, {"final_time": 0.2, "n_shooting": 8}).n_shooting == 8
+    for bad in (0, -3, 2.5, True):
+        with pytest.raises(ValueError):
+            IvpFes({"model": m}, {"final_time": 1.0, "n_shooting": bad})

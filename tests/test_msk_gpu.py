@@ -428,3 +428,25 @@ def test_msk_hmed_interior_point_converges():
     for name in ("pulse_intensity_BIClong", "pulse_intensity_TRIlong"):
         p = params[name][0]
         assert p.shape == (10,) and np.all(p >= imin - 1e-9) and np.all(p <= 130 + 1e-9)
+
+
+def test_msk_hmed_window_padding_uses_the_first_muscles_floor():
+    """custom_constraints.py:107-114 pads every muscle's sliding window with muscles_dynamics_model[0]'s
+    min_pulse_intensity(): with a second muscle whose recruitment constants (hence I_min) differ, its padded rows
+    still use the first muscle's floor."""
+    cfg = MC.cfg5(model="hmed2018", fatigue=False, scheme="RK1", m=2)
+    ocp = MC.product_ocp(**cfg)
+    pb = MC.oracle_problem(**cfg)
+    ocp.model.muscles_dynamics_model[1].Is = 70.0
+    ocp.model.muscles_dynamics_model[1].cr = 0.8
+    pb.muscles[1].c.update(Is=70.0, cr=0.8)
+    assert abs(M.O.min_pulse_intensity(pb.muscles[1].c) - M.O.min_pulse_intensity(pb.muscles[0].c)) > 1.0
+    V = MC.random_decision(pb, 2, seed=8)
+    h = ocp.nlp(batch=2, layout="aos")
+    g = h.eval_g(V)
+    h.close()
+    ngk = _ngk(pb)
+    for b in range(2):
+        for k in (0, 1, 3):  # windows that start before the first pulse
+            rows = g[b, k * ngk + pb.nx:(k + 1) * ngk]
+            np.testing.assert_allclose(rows, M.sliding_rows(pb, V[b], k), rtol=0, atol=1e-12)

@@ -135,3 +135,61 @@ def test_msk_nmpc_window_history_matches_one_long_transcription():
                                   pulse_intensity={"min": 20})
     with pytest.raises(ValueError):
         C.NmpcFesMsk(mm, cycle_duration=0.3)
+
+
+def test_solve_fes_nmpc_driver_entry_and_update_functions():
+    """FesNmpc.solve_fes_nmpc (fes_nmpc.py:150-192): the update function decides when to stop (bioptim's
+    `update_functions(nmpc, cycle_idx, sol)`), the Solver.IPOPT options reach every window's interior point."""
+    from cocofest_amd import DingModelFrequency, Solver
+
+    model = DingModelFrequency(stim_time=CYCLE, sum_stim_truncation=4)
+    calls = []
+
+    def update_functions(nmpc, cycle_idx, sol):
+        calls.append(cycle_idx)
+        return cycle_idx < 2
+
+    res = _nmpc(model, objective={"end_node_tracking": 50.0}, batch=1).solve_fes_nmpc(
+        update_functions, solver=Solver.IPOPT(_max_iter=40, _tol=1e-9), total_cycles=10)
+    assert calls == [1, 2] and len(res.converged) == 2 and all(c.all() for c in res.converged)
+    assert max(int(i.max()) for i in res.iterations) <= 40
+    assert res.states["F"].shape == (1, 2 * 5 + 1) and not np.isnan(res.states["F"]).any()
+    assert list(res.stopped_at) == [-1]
+    ref = _forward("ding2003", [t + 0.5 * c for c in range(2) for t in CYCLE], 2, 4)
+    np.testing.assert_allclose(res.states["F"][0], ref[1], rtol=1e-7, atol=1e-7)
+
+
+def test_max_consecutive_failing_stops_each_scenario():
+    """max_consecutive_failing = 3 (the reference's default, fes_nmpc.py:158): with an interior point capped at one
+    iteration every window fails, so each scenario stops at its third window, which is not committed (NaN), and
+    the loop ends there instead of running the 6 requested cycles."""
+    from cocofest_amd import DingModelPulseIntensityFrequency, Solver
+
+    model = DingModelPulseIntensityFrequency(stim_time=CYCLE, sum_stim_truncation=4)
+    res = _nmpc(model, pulse_intensity={"max": 130}, objective={"end_node_tracking": 40.0}, batch=2).solve_fes_nmpc(
+        lambda nmpc, k, sol: True, solver=Solver.IPOPT(_max_iter=1), total_cycles=6, max_consecutive_failing=3)
+    assert len(res.converged) == 3 and not any(c.any() for c in res.converged)
+    assert list(res.stopped_at) == [2, 2]
+    F = res.states["F"]
+    assert F.shape == (2, 3 * 5 + 1)
+    assert not np.isnan(F[:, : 2 * 5 + 1]).any() and np.isnan(F[:, 2 * 5 + 1:]).all()
+    assert np.isnan(res.pulse_intensity[:, 2 * len(CYCLE):]).all()
+
+
+def test_solver_ipopt_facade():
+    """Solver.IPOPT keeps bioptim's private option names and setters; unknown options are refused."""
+    from cocofest_amd import IpmOptions, Solver
+    from cocofest_amd.solver import apply_solver
+
+    s = Solver.IPOPT(show_online_optim=False, _max_iter=77, _tol=1e-8, _hessian_approximation="limited-memory",
+                     _print_level=0, _linear_solver="ma57")
+    s.set_limited_memory_max_history(9)
+    o = apply_solver(IpmOptions(), s)
+    assert (o.max_iter, o.tol, o.hessian_approximation, o.limited_memory_max_history) == (77, 1e-8, "limited-memory", 9)
+    s.set_maximum_iterations(5)
+    s.set_tol(1e-4)
+    assert (s.max_iter, s.tol) == (5, 1e-4)
+    with pytest.raises(TypeError):
+        Solver.IPOPT(_max_itr=3)
+    with pytest.raises(ValueError):
+        Solver.IPOPT(_hessian_approximation="bfgs")
