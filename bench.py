@@ -109,6 +109,21 @@ def casadi_probe():
         return {"importable": False, "error": f"{type(e).__name__}: {e}"}
 
 
+FP64_FMA_ISSUE_PEAK = 5.18e11  # wave-instr/s, measured (profiles/round1/micro_fp64_rate.txt: 8 chains, 8192 blocks)
+
+
+def msk_pmc():
+    """VALU wave-instructions per cfg-5 g + J_g step (k_msk_values + k_msk_stagecoef_par + k_msk_tangents_lds,
+    B = 65,536) from the committed rocprofv3 SQ pass (profiles/msk_pmc.json, scripts/r3/gpu_msk_prof.sh), if any."""
+    f = ROOT / "profiles" / "msk_pmc.json"
+    if not f.exists():
+        return None
+    try:
+        return json.loads(f.read_text())
+    except Exception:
+        return None
+
+
 def cpu_baseline(ocp, budget_s, name="ding2003", truncation=20, label="cfg2"):
     """CPU legs on a bounded sample of the same workload, on this host's cores and on one core:
 
@@ -469,6 +484,15 @@ def msk_throughput(local, dist, world, rank, backend, steps=10, B=1 << 16):
            "algorithmic_GBps": nbytes * world * B / (wall_max / steps) / 1e9, "bytes_per_instance": nbytes,
            "scaling": "weak", "parallelism": f"instances sharded over {world} GPU(s), no data-path collective",
            "kernels": "k_msk_values + k_msk_stagecoef_par + k_msk_tangents_lds (compute-bound: FP64 VALU, see profiles/)"}
+    pmc = msk_pmc()
+    if pmc and pmc.get("batch") == B:
+        # compute-bound: the VALU issue rate of the step's three kernels (committed SQ_INSTS_VALU per step over the
+        # step's kernel time measured here) against the measured FP64 FMA issue peak
+        achieved = pmc["valu_wave_instr_per_step"] / (out["kernel_ms_per_step"] * 1e-3)
+        out["roofline"] = {"bound": "fp64_valu", "achieved": achieved, "peak": FP64_FMA_ISSUE_PEAK,
+                           "unit": "VALU wave-instr/s", "frac": achieved / FP64_FMA_ISSUE_PEAK,
+                           "traffic": pmc.get("hbm_bytes_per_step"), "per_kernel": pmc.get("kernels"),
+                           "source": pmc.get("source")}
     h.close()
     return out, ocp
 

@@ -15,7 +15,7 @@ import numpy as np
 
 LIB_PATH = pathlib.Path(__file__).with_name("libcfx.so")
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 OK, EINVAL, EHIP, ENOMEM, EUNSUPPORTED, ENODEV = 0, -1, -2, -3, -4, -5
 MODEL_IDS = {
     "ding2003": 0,
@@ -109,7 +109,8 @@ class IpmOptions(C.Structure):
                 ("kappa_mu", C.c_double), ("theta_mu", C.c_double), ("s_max", C.c_double), ("armijo", C.c_double),
                 ("max_backtrack", C.c_int32), ("delta_c", C.c_double), ("curv_min", C.c_double),
                 ("max_soc", C.c_int32), ("kappa_soc", C.c_double), ("watchdog_shortened_iter_trigger", C.c_int32),
-                ("watchdog_trial_iter_max", C.c_int32)]
+                ("watchdog_trial_iter_max", C.c_int32), ("hessian_approximation", C.c_int32),
+                ("limited_memory_max_history", C.c_int32)]
 
 
 class IpmStats(C.Structure):

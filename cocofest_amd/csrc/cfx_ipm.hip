@@ -48,6 +48,9 @@ struct Scal {
     double wd_theta, wd_phi, wd_dphi, wd_ap, wd_mu;  // watchdog reference: the iterate where it started
     int32_t done, acc, iters, fpos, accepted, armijo, soc, reinit, todo;
     int32_t wd_short, wd_on, wd_trial, skip_first, forced, pad[2];
+    // limited-memory Hessian (L-BFGS): sigma, pairs held, next ring slot, previous iterate saved
+    double lsig;
+    int32_t lcount, lhead, lprev, lpad;
 };
 
 struct IpmK {
@@ -95,6 +98,16 @@ struct IpmK {
     double* filt;                                                           // [B][kFilt][2]
     Scal* sc;                                                               // [B]
     int32_t* cnt;                                                           // [kSlots][4]
+    // limited-memory Hessian (o.hessian_approximation == CFX_HESSIAN_LIMITED_MEMORY): hmax pairs (s, y) per instance
+    // in a ring, the previous iterate, the compact form's middle matrix M, the Woodbury columns P = K0^-1 Z in band
+    // order ([2 hmax][B][nKp], one rb-shaped array per column) and the LU of C = M - Z^T P
+    int lbfgs, hmax;
+    double *Sh, *Yh;           // [B][hmax][nf]
+    double *xprev, *gprev;     // [B][nf]
+    double* jvprev;            // [B][nj]
+    double *Mm, *Cl;           // [B][2 hmax][2 hmax]
+    int32_t* Cp;               // [B][2 hmax]
+    double* Zb;                // [2 hmax][B][nKp]
 };
 
 enum { KKT_NEWTON = 0, KKT_LSMULT = 1, KKT_RESTO = 2 };
@@ -310,6 +323,7 @@ __global__ void __launch_bounds__(kIB) k_ipm_init(const IpmK K) {
         Scal S{};
         S.mu = mu;
         S.sf = sf;
+        S.lsig = 1.0;  // Ipopt limited_memory_init_val
         S.err0 = INFINITY;
         S.reinit = K.m > 0;
         K.sc[b] = S;
@@ -444,7 +458,7 @@ __global__ void __launch_bounds__(kIB) k_ipm_kkt(const IpmK K, int mode) {
         const double* hv = K.hv + b * K.nnzh;
         const double* jv = K.jv + b * K.nj;
         const double* sig = K.sig + b * K.nf;
-        const double dw = K.sc[b].dw;
+        const double dw = K.sc[b].dw + (K.lbfgs ? K.sc[b].lsig : 0.0);  // L-BFGS: W = sigma I - low rank (Woodbury)
         for (int k = K.kkt_ptr[p]; k < K.kkt_ptr[p + 1]; ++k) {
             const int32_t code = K.kkt_src[k];
             const int idx = code & kSrcMask;
@@ -615,7 +629,6 @@ __global__ void __launch_bounds__(kIB) k_ipm_schur(const IpmK K, int factor) {
 
 // Newton step in natural order and the curvature test (solver.py inertia loop); bumps dw where it fails.
 __global__ void __launch_bounds__(kIB) k_ipm_curv(const IpmK K, int slot) {
-    __shared__ double sh[kIB / 64];
     __shared__ Scal S;
     const int64_t b = blockIdx.x;
     const int nf = K.nf;
@@ -658,7 +671,10 @@ __global__ void __launch_bounds__(kIB) k_ipm_curv(const IpmK K, int slot) {
     const double curv = quad + dd;
     bool sing = false;
     for (int q = 0; q < K.P; ++q) sing = sing || K.info[b * K.P + q] != 0;
-    const bool bad = !S.done && ((curv <= K.o.curv_min * nrm) || !isfinite(curv) || sing || nonfin > 0);
+    // L-BFGS: the approximation is positive definite by construction (pairs with s^T y <= 0 are skipped), so only a
+    // singular or non-finite factorisation asks for more regularisation
+    const bool weak = K.lbfgs ? false : ((curv <= K.o.curv_min * nrm) || !isfinite(curv));
+    const bool bad = !S.done && (weak || sing || nonfin > 0);
     if (threadIdx.x == 0 && bad) {
         if (S.dw == 0.0)
             S.dw = S.dwl > 0 ? clamp_lo(S.dwl / 3, 1e-20) : 1e-4;
@@ -848,7 +864,6 @@ __global__ void __launch_bounds__(kIB) k_ipm_soc_rhs(const IpmK K) {
 
 // corrected trial x + a_c dx_c (into xr)
 __global__ void __launch_bounds__(kIB) k_ipm_soc_trial(const IpmK K) {
-    __shared__ double sh[kIB / 64];
     const int64_t b = blockIdx.x;
     const int nf = K.nf;
     const double* x = K.x + b * nf;
@@ -918,7 +933,6 @@ __global__ void __launch_bounds__(kIB) k_ipm_soc_accept(const IpmK K, int slot) 
 // restoration (solver.py _restoration_step), for the instances whose line search failed: step from the band
 // solve of [[Sigma + I, J^T], [J, 0]] [dx; .] = [0; -g], fraction to the boundary, first trial
 __global__ void __launch_bounds__(kIB) k_ipm_resto_init(const IpmK K, int slot) {
-    __shared__ double sh[kIB / 64];
     __shared__ Scal S;
     const int64_t b = blockIdx.x;
     const int nf = K.nf, m = K.m;
@@ -964,7 +978,6 @@ __global__ void __launch_bounds__(kIB) k_ipm_resto_init(const IpmK K, int slot) 
 }
 
 __global__ void __launch_bounds__(kIB) k_ipm_resto_accept(const IpmK K, int slot) {
-    __shared__ double sh[kIB / 64];
     __shared__ Scal S;
     const int64_t b = blockIdx.x;
     const int nf = K.nf, m = K.m;
@@ -1007,7 +1020,6 @@ __global__ void __launch_bounds__(kIB) k_ipm_resto_accept(const IpmK K, int slot
 
 // least-squares multipliers (Ipopt's constr_mult_init), for the instances flagged reinit
 __global__ void __launch_bounds__(kIB) k_ipm_lsmult(const IpmK K) {
-    __shared__ double sh[kIB / 64];
     __shared__ Scal S;
     const int64_t b = blockIdx.x;
     load_scal(K, b, S);
@@ -1034,7 +1046,6 @@ __global__ void __launch_bounds__(kIB) k_ipm_lsmult(const IpmK K) {
 
 // end of an iteration: filter augmentation, restoration outcome, primal-dual steps, z safeguard
 __global__ void __launch_bounds__(kIB) k_ipm_update(const IpmK K, int resto) {
-    __shared__ double sh[kIB / 64];
     __shared__ Scal S;
     const int64_t b = blockIdx.x;
     const int nf = K.nf, m = K.m;
@@ -1125,7 +1136,11 @@ __global__ void __launch_bounds__(kIB) k_ipm_update(const IpmK K, int resto) {
     write_full(K, b, x, K.vx);
     if (threadIdx.x == 0) {
         if (grow) S.fpos += 1;
-        if (reset) S.reinit = 1;
+        if (reset) {
+            S.reinit = 1;
+            S.lcount = S.lhead = S.lprev = 0;  // the quasi-Newton pairs describe the abandoned region
+            S.lsig = 1.0;
+        }
         S.alpha = alpha;
         S.iters += step;
         S.wd_trial = wd_trial;
@@ -1167,6 +1182,233 @@ __global__ void k_ipm_publish(const int32_t* __restrict__ cnt, int32_t* pub, int
     if (threadIdx.x == 0) {
         for (int i = 0; i < 4; ++i) __hip_atomic_store(pub + 1 + i, cnt[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         __hip_atomic_store(pub, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
+// ---- limited-memory Hessian (Ipopt hessian_approximation = limited-memory, BFGS update, scalar1 initialisation) --
+// W ~ B = sigma I - Z M^-1 Z^T with Z = [sigma S, Y] (the last c <= hmax steps s = x+ - x and gradient-of-the-
+// Lagrangian changes y = grad L(x+, y+) - grad L(x, y+), oldest first) and M = [[sigma S^T S, L], [L^T, -D]]
+// (S^T Y = L + D + U).  The band factors are those of K0 = K with W replaced by sigma I; the Newton / correction
+// solves use  K^-1 r = K0^-1 r + P C^-1 Z^T K0^-1 r,  P = K0^-1 Z,  C = M - Z^T P  (Sherman-Morrison-Woodbury; Z is
+// zero on the constraint rows).  Unused slots of the 2 hmax columns are zero with an identity block in M and C.
+
+// pair slot of the r-th stored pair (oldest first)
+__device__ inline int lb_slot(const Scal& S, int H, int r) { return (S.lhead - S.lcount + r + 2 * H) % H; }
+
+// column q of Z at free variable i (q < H: sigma s_q, else y_{q-H}; zero past the stored pairs)
+__device__ inline double lb_z(const IpmK& K, const Scal& S, int64_t b, int q, int i) {
+    const int H = K.hmax;
+    const int r = q < H ? q : q - H;
+    if (r >= S.lcount) return 0.0;
+    const int64_t o = ((int64_t)b * H + lb_slot(S, H, r)) * K.nf + i;
+    return q < H ? S.lsig * K.Sh[o] : K.Yh[o];
+}
+
+// after k_ipm_begin: the pair of the last step (skipped unless s^T y > 1e-8 |s| |y|), sigma = s^T y / s^T s, the
+// current iterate saved, and M
+__global__ void __launch_bounds__(kIB) k_lbfgs_update(const IpmK K) {
+    __shared__ Scal S;
+    const int64_t b = blockIdx.x;
+    const int nf = K.nf, H = K.hmax, H2 = 2 * H;
+    load_scal(K, b, S);
+    const double* x = K.x + b * nf;
+    const double* gF = K.gF + b * nf;
+    const double* jv = K.jv + b * K.nj;
+    const double* y = K.y + b * K.m;
+    double* xp = K.xprev + b * nf;
+    double* gp = K.gprev + b * nf;
+    double* jp = K.jvprev + b * K.nj;
+    if (!S.done && S.lprev) {
+        double sy = 0.0, ss = 0.0, yy = 0.0;
+        for (int i = threadIdx.x; i < nf; i += kIB) {
+            double jty = 0.0, jtyp = 0.0;
+            for (int k = K.jt_ptr[i]; k < K.jt_ptr[i + 1]; ++k) {
+                const int t = K.jt_idx[k];
+                const double yk = y[K.jr[t]];
+                jty += jv[t] * yk;
+                jtyp += jp[t] * yk;
+            }
+            const double si = x[i] - xp[i], yi = (gF[i] - gp[i]) + (jty - jtyp);
+            xp[i] = si;  // the previous iterate is no longer needed: its arrays hold the candidate pair
+            gp[i] = yi;
+            sy += si * yi;
+            ss += si * si;
+            yy += yi * yi;
+        }
+        {
+            double rv[3] = {sy, ss, yy};
+            const int ro[3] = {0, 0, 0};
+            breduce_n(rv, ro);
+            sy = rv[0];
+            ss = rv[1];
+            yy = rv[2];
+        }
+        const bool take = isfinite(sy) && isfinite(yy) && ss > 0.0 && sy > 1e-8 * sqrt(ss * yy);
+        if (take) {
+            double* sn = K.Sh + ((int64_t)b * H + S.lhead) * nf;
+            double* yn = K.Yh + ((int64_t)b * H + S.lhead) * nf;
+            for (int i = threadIdx.x; i < nf; i += kIB) {
+                sn[i] = xp[i];
+                yn[i] = gp[i];
+            }
+        }
+        __syncthreads();
+        if (threadIdx.x == 0 && take) {
+            S.lhead = (S.lhead + 1) % H;
+            S.lcount = S.lcount < H ? S.lcount + 1 : H;
+            S.lsig = clamp_hi(clamp_lo(sy / ss, 1e-8), 1e8);
+        }
+        __syncthreads();
+    }
+    for (int i = threadIdx.x; i < nf; i += kIB) {
+        xp[i] = x[i];
+        gp[i] = gF[i];
+    }
+    for (int t = threadIdx.x; t < K.nj; t += kIB) jp[t] = jv[t];
+    if (threadIdx.x == 0) S.lprev = 1;
+    __syncthreads();
+    // M over the stored pairs (S rows / columns at 0.., Y at H..), identity elsewhere
+    double* Mb = K.Mm + b * H2 * H2;
+    for (int e = threadIdx.x; e < H2 * H2; e += kIB) {
+        const int r = e / H2, c = e - (e / H2) * H2;
+        const bool used = (r % H) < S.lcount && (c % H) < S.lcount;
+        Mb[e] = used ? 0.0 : (r == c ? 1.0 : 0.0);
+    }
+    __syncthreads();
+    const int c = S.lcount;
+    for (int i = 0; i < c; ++i)
+        for (int j = 0; j < c; ++j) {
+            const double* si = K.Sh + ((int64_t)b * H + lb_slot(S, H, i)) * nf;
+            const double* sj = K.Sh + ((int64_t)b * H + lb_slot(S, H, j)) * nf;
+            const double* yj = K.Yh + ((int64_t)b * H + lb_slot(S, H, j)) * nf;
+            double dss = 0.0, dsy = 0.0;
+            for (int t = threadIdx.x; t < nf; t += kIB) {
+                dss += si[t] * sj[t];
+                dsy += si[t] * yj[t];
+            }
+            double rv[2] = {dss, dsy};
+            const int ro[2] = {0, 0};
+            breduce_n(rv, ro);
+            if (threadIdx.x == 0) {
+                Mb[i * H2 + j] = S.lsig * rv[0];              // sigma S^T S
+                if (i > j) Mb[i * H2 + H + j] = rv[1];        // L
+                if (i > j) Mb[(H + j) * H2 + i] = rv[1];      // L^T
+                if (i == j) Mb[(H + i) * H2 + H + i] = -rv[1];  // -D
+            }
+        }
+    store_scal(K, b, S);
+}
+
+// the 2 H columns of Z in band order, one rb-shaped array per column (then solved in place: P = K0^-1 Z)
+__global__ void __launch_bounds__(kIB) k_lbfgs_zcols(const IpmK K) {
+    __shared__ Scal S;
+    const int64_t b = blockIdx.x;
+    load_scal(K, b, S);
+    const int H2 = 2 * K.hmax;
+    for (int q = 0; q < H2; ++q) {
+        double* z = K.Zb + ((int64_t)q * K.B + b) * K.nKp;
+        for (int i = threadIdx.x; i < K.nKp; i += kIB) z[i] = 0.0;
+        __syncthreads();
+        for (int i = threadIdx.x; i < K.nf; i += kIB) z[K.pos[i]] = lb_z(K, S, b, q, i);
+        __syncthreads();
+    }
+}
+
+// C = M - Z^T P and its LU (partial pivoting, one wavefront, lanes over columns)
+__global__ void __launch_bounds__(kIB) k_lbfgs_factor(const IpmK K) {
+    constexpr int HM2 = 32;
+    __shared__ Scal S;
+    __shared__ double C[HM2][HM2 + 1];
+    __shared__ int piv[HM2];
+    const int64_t b = blockIdx.x;
+    load_scal(K, b, S);
+    const int H2 = 2 * K.hmax, t = threadIdx.x;
+    const double* Mb = K.Mm + b * H2 * H2;
+    for (int e = t; e < H2 * H2; e += kIB) {
+        const int r = e / H2, c = e - (e / H2) * H2;
+        const double* P = K.Zb + ((int64_t)c * K.B + b) * K.nKp;
+        double acc = 0.0;
+        if ((r % K.hmax) < S.lcount && (c % K.hmax) < S.lcount)
+            for (int i = 0; i < K.nf; ++i) acc += lb_z(K, S, b, r, i) * P[K.pos[i]];
+        C[r][c] = Mb[e] - acc;
+    }
+    __syncthreads();
+    if (t < 64) {
+        for (int k = 0; k < H2; ++k) {
+            double a = (t >= k && t < H2) ? fabs(C[t][k]) : -1.0;
+            int idx = t;
+            for (int o = 32; o > 0; o >>= 1) {
+                const double a2 = __shfl_xor(a, o, 64);
+                const int i2 = __shfl_xor(idx, o, 64);
+                if (a2 > a || (a2 == a && i2 < idx)) {
+                    a = a2;
+                    idx = i2;
+                }
+            }
+            const int p = idx;
+            if (t == 0) piv[k] = p;
+            if (p != k && t < H2) {
+                const double tmp = C[k][t];
+                C[k][t] = C[p][t];
+                C[p][t] = tmp;
+            }
+            wave_sync();
+            const double pv = C[k][k];
+            const double inv = pv != 0.0 ? 1.0 / pv : 0.0;
+            if (t > k && t < H2) C[t][k] *= inv;
+            wave_sync();
+            if (t > k && t < H2) {
+                const double ukt = C[k][t];
+                for (int i = k + 1; i < H2; ++i) C[i][t] -= C[i][k] * ukt;
+            }
+            wave_sync();
+        }
+    }
+    __syncthreads();
+    for (int e = t; e < H2 * H2; e += kIB) K.Cl[b * H2 * H2 + e] = C[e / H2][e - (e / H2) * H2];
+    if (t < H2) K.Cp[b * H2 + t] = piv[t];
+}
+
+// rb (= K0^-1 r, band order) += P C^-1 Z^T rb
+__global__ void __launch_bounds__(kIB) k_lbfgs_apply(const IpmK K) {
+    constexpr int HM2 = 32;
+    __shared__ Scal S;
+    __shared__ double w[HM2];
+    const int64_t b = blockIdx.x;
+    load_scal(K, b, S);
+    const int H2 = 2 * K.hmax, t = threadIdx.x;
+    double* rb = K.rb + b * K.nKp;
+    if (t < 64) {
+        double v = 0.0;  // lane r: (Z^T u)_r
+        if (t < H2 && (t % K.hmax) < S.lcount)
+            for (int i = 0; i < K.nf; ++i) v += lb_z(K, S, b, t, i) * rb[K.pos[i]];
+        const double* L = K.Cl + b * H2 * H2;
+        const int32_t* pv = K.Cp + b * H2;
+        for (int k = 0; k < H2; ++k) {  // row interchanges, unit lower, upper (getrs)
+            const int p = pv[k];
+            if (p != k) {
+                const double vk = __shfl(v, k, 64), vp = __shfl(v, p, 64);
+                if (t == k) v = vp;
+                if (t == p) v = vk;
+            }
+        }
+        for (int k = 0; k < H2; ++k) {
+            const double vk = __shfl(v, k, 64);
+            if (t > k && t < H2) v -= L[t * H2 + k] * vk;
+        }
+        for (int k = H2 - 1; k >= 0; --k) {
+            if (t == k) v = v / L[k * H2 + k];
+            const double vk = __shfl(v, k, 64);
+            if (t < k) v -= L[t * H2 + k] * vk;
+        }
+        if (t < H2) w[t] = v;
+    }
+    __syncthreads();
+    for (int e = t; e < K.nKp; e += kIB) {
+        double acc = 0.0;
+        for (int q = 0; q < H2; ++q)
+            if ((q % K.hmax) < S.lcount) acc += K.Zb[((int64_t)q * K.B + b) * K.nKp + e] * w[q];
+        rb[e] += acc;
     }
 }
 
@@ -1264,6 +1506,8 @@ extern "C" void cfx_ipm_default_options(cfx_ipm_options* o) {
     o->kappa_soc = 0.99;
     o->watchdog_shortened_iter_trigger = 10;
     o->watchdog_trial_iter_max = 3;
+    o->hessian_approximation = CFX_HESSIAN_EXACT;
+    o->limited_memory_max_history = 6;
 }
 
 // CSR of `key` (values in [0, nkeys)) with the sources of each key in increasing source order
@@ -1310,6 +1554,9 @@ extern "C" int cfx_ipm_create(cfx_handle* h, const double* lb, const double* ub,
     if (cfx_get_sizes(h, &sz) != CFX_OK || (s->B > 1 && layout != CFX_LAYOUT_AOS) || layout == CFX_LAYOUT_TILED64 ||
         n_params < 0 || n_params > sz.nv || K.o.max_iter < 0 || K.o.max_backtrack < 1 || K.o.max_soc < 0 ||
         K.o.watchdog_shortened_iter_trigger < 0 || K.o.watchdog_trial_iter_max < 0 ||
+        (K.o.hessian_approximation != CFX_HESSIAN_EXACT && K.o.hessian_approximation != CFX_HESSIAN_LIMITED_MEMORY) ||
+        (K.o.hessian_approximation == CFX_HESSIAN_LIMITED_MEMORY &&
+         (K.o.limited_memory_max_history < 1 || K.o.limited_memory_max_history > 16)) ||
         s->B > 0x7fffffff) {
         s->err = "cfx_ipm_create: the handle must use CFX_LAYOUT_AOS (or batch 1) and the options must be valid";
         return create_fail(s, CFX_EINVAL);
@@ -1698,6 +1945,20 @@ extern "C" int cfx_ipm_create(cfx_handle* h, const double* lb, const double* ub,
     K.info = dalloc<int32_t>(s, B * P, &rc);
     K.filt = dalloc<double>(s, B * kFilt * 2, &rc);
     K.sc = dalloc<Scal>(s, B, &rc);
+    K.lbfgs = K.o.hessian_approximation == CFX_HESSIAN_LIMITED_MEMORY;
+    K.hmax = K.lbfgs ? K.o.limited_memory_max_history : 0;
+    if (K.lbfgs) {
+        const size_t H = (size_t)K.hmax, H2 = 2 * H;
+        K.Sh = dalloc<double>(s, B * H * nf, &rc);
+        K.Yh = dalloc<double>(s, B * H * nf, &rc);
+        K.xprev = dalloc<double>(s, B * nf, &rc);
+        K.gprev = dalloc<double>(s, B * nf, &rc);
+        K.jvprev = dalloc<double>(s, B * nj, &rc);
+        K.Mm = dalloc<double>(s, B * H2 * H2, &rc);
+        K.Cl = dalloc<double>(s, B * H2 * H2, &rc);
+        K.Cp = dalloc<int32_t>(s, B * H2, &rc);
+        K.Zb = dalloc<double>(s, H2 * B * nKp, &rc);
+    }
     K.cnt = dalloc<int32_t>(s, 4 * kSlots, &rc);
     s->d_fv = dalloc<double>(s, B * K.nfix, &rc);
     s->d_yo = dalloc<double>(s, B * m, &rc);
@@ -1727,6 +1988,12 @@ extern "C" int cfx_ipm_create(cfx_handle* h, const double* lb, const double* ub,
 }
 
 namespace {
+
+#define IPM_RUN(call)                  \
+    do {                               \
+        int r2_ = (call);              \
+        if (r2_ != CFX_OK) return r2_; \
+    } while (0)
 
 struct Run {
     cfx_ipm* s;
@@ -1791,9 +2058,11 @@ struct Run {
         s->st.kkt_factor++;
         return CFX_OK;
     }
-    // another right-hand side (in rb, band order) with the factors of the last kkt_factor
-    int resolve() {
-        const IpmK& K = s->K;
+    // another right-hand side (in rb, band order — or in the rb-shaped array `into`) with the factors of the last
+    // kkt_factor
+    int resolve(double* into = nullptr) {
+        IpmK K = s->K;
+        if (into) K.rb = into;
         if (K.np) {
             IPM_BAND(s, cfx_band_solve_multi(K.nA, K.kl, K.ku, K.B * K.P, K.P, K.ab, K.ipiv, nullptr, 0, 0, 0, 0,
                                              K.rb, K.nKp, K.nA, st));
@@ -1804,15 +2073,22 @@ struct Run {
         }
         return CFX_OK;
     }
+    // L-BFGS: after a Newton factorisation of K0, P = K0^-1 Z column by column, C = M - Z^T P, and the Newton
+    // solution corrected (rb += P C^-1 Z^T rb)
+    int lbfgs_newton() {
+        const IpmK& K = s->K;
+        hipLaunchKernelGGL(k_lbfgs_zcols, g, dim3(kIB), 0, st, K);
+        IPM_HIP(s, hipGetLastError());
+        for (int q = 0; q < 2 * K.hmax; ++q) IPM_RUN(resolve(K.Zb + (size_t)q * K.B * K.nKp));
+        hipLaunchKernelGGL(k_lbfgs_factor, g, dim3(kIB), 0, st, K);
+        hipLaunchKernelGGL(k_lbfgs_apply, g, dim3(kIB), 0, st, K);
+        IPM_HIP(s, hipGetLastError());
+        return CFX_OK;
+    }
 };
 
 }  // namespace
 
-#define IPM_RUN(call)                  \
-    do {                               \
-        int r2_ = (call);              \
-        if (r2_ != CFX_OK) return r2_; \
-    } while (0)
 
 static int ipm_solve(cfx_ipm* s, const double* v0, const double* fixed_values, double* v_out, double* y_out,
                      double* f_out, int32_t* conv_out, int32_t* its_out, double* kkt_out, uint32_t flags) {
@@ -1841,6 +2117,7 @@ static int ipm_solve(cfx_ipm* s, const double* v0, const double* fixed_values, d
     s->slot = 0;
     IPM_HIP(s, hipMemsetAsync(K.cnt, 0, 4 * kSlots * sizeof(int32_t), st));
     IPM_HIP(s, hipMemsetAsync(K.rb, 0, B * K.nKp * sizeof(double), st));  // padding rows of the blocks stay 0
+    if (K.lbfgs) IPM_HIP(s, hipMemsetAsync(K.hv, 0, B * K.nnzh * sizeof(double), st));  // W enters as sigma I
     IPM_HIP(s, hipMemcpyAsync(K.vx, v0, B * K.n * sizeof(double), kin, st));
     if (fixed_values && K.nfix)
         IPM_HIP(s, hipMemcpyAsync(s->d_fv, fixed_values, B * K.nfix * sizeof(double), kin, st));
@@ -1863,13 +2140,19 @@ static int ipm_solve(cfx_ipm* s, const double* v0, const double* fixed_values, d
         }
         reinit = false;
         IPM_HIP(s, hipGetLastError());
-        cfx_internal_msk_stash(s->h, 2);  // K.vx is the point of eval_full above: the MSK stage data may be re-used
-        IPM_CFX(s, cfx_eval_h(s->h, K.vx, K.of, K.ysc, K.hv, CFX_DEVICE));
-        s->st.eval_h++;
+        if (K.lbfgs) {  // quasi-Newton pair of the last step, M (no eval_h: hv stays zero)
+            hipLaunchKernelGGL(k_lbfgs_update, R.g, blk, 0, st, K);
+            IPM_HIP(s, hipGetLastError());
+        } else {
+            cfx_internal_msk_stash(s->h, 2);  // K.vx is the point of eval_full above: the MSK stage data may be re-used
+            IPM_CFX(s, cfx_eval_h(s->h, K.vx, K.of, K.ysc, K.hv, CFX_DEVICE));
+            s->st.eval_h++;
+        }
         // inertia correction by the curvature test: grow dw until dx^T (W + Sigma + dw) dx > 0
         bool all_done = false;
         for (int attempt = 0; attempt < 12; ++attempt) {
             IPM_RUN(R.kkt_factor(KKT_NEWTON));
+            if (K.lbfgs) IPM_RUN(R.lbfgs_newton());
             const int sl = R.next_slot();
             hipLaunchKernelGGL(k_ipm_curv, R.g, blk, 0, st, K, sl);
             IPM_HIP(s, hipGetLastError());
@@ -1895,6 +2178,7 @@ static int ipm_solve(cfx_ipm* s, const double* v0, const double* fixed_values, d
                 for (int q = 0; q < K.o.max_soc && c[1] > 0; ++q) {
                     hipLaunchKernelGGL(k_ipm_soc_rhs, R.g, blk, 0, st, K);
                     IPM_RUN(R.resolve());
+                    if (K.lbfgs) hipLaunchKernelGGL(k_lbfgs_apply, R.g, blk, 0, st, K);
                     hipLaunchKernelGGL(k_ipm_soc_trial, R.g, blk, 0, st, K);
                     IPM_RUN(R.eval_gf(true));
                     sl = R.next_slot();

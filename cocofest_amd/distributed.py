@@ -127,10 +127,14 @@ class IntervalShardedNlp:
         """All-gather every rank's (B, L_r) slice and index-add it into a (B, width) global array."""
         torch, dist = self.torch, self.dist
         pad = max(m.numel() for m in maps)
-        buf = torch.zeros((self.B, pad), dtype=torch.float64, device=self.dev)
-        buf[:, : local.shape[1]] = local
+        # gloo moves host memory only: a rank with device tensors stages the exchange through the host (the
+        # nccl / RCCL backend gathers the device buffers directly over xGMI)
+        cdev = torch.device("cpu") if (self.dev.type == "cuda" and dist.get_backend(self.group) == "gloo") else self.dev
+        buf = torch.zeros((self.B, pad), dtype=torch.float64, device=cdev)
+        buf[:, : local.shape[1]] = local.to(cdev)
         out = [torch.empty_like(buf) for _ in range(self.world)]
         dist.all_gather(out, buf, group=self.group)
+        out = [o.to(self.dev) for o in out]
         full = torch.zeros((self.B, width), dtype=torch.float64, device=self.dev)
         for o, m in zip(out, maps):
             full.index_add_(1, m, o[:, : m.numel()])
@@ -152,9 +156,9 @@ class IntervalShardedNlp:
         if jac is not None:
             jac.copy_(self._allgather_place(jl, self.map_j, self.nnz_jac))
         if f is not None:
-            fs = fl.clone()
+            fs = fl.cpu() if (self.dev.type == "cuda" and self.dist.get_backend(self.group) == "gloo") else fl.clone()
             self.dist.all_reduce(fs, group=self.group)
-            f.copy_(fs)
+            f.copy_(fs.to(self.dev))
         if grad is not None:
             grad.copy_(self._allgather_place(dl, self.map_v, self.nv))
 

@@ -192,6 +192,9 @@ class BatchedIpm:
         self.ocp = ocp
         self.B = batch
         self.opt = options or IpmOptions()
+        if self.opt.hessian_approximation != "exact":
+            raise ValueError("BatchedIpm: hessian_approximation='limited-memory' is implemented by the native interior "
+                             "point (NativeIpm / cfx_ipm) only")
         self.dev = torch.device(torch_device) if torch_device is not None else torch.device("cuda", device)
         self.h = handle if handle is not None else ocp.nlp(batch=batch, layout="aos", device=device)
         h = self.h
@@ -777,7 +780,8 @@ class GpuBandSolver:
 _NATIVE_OPTIONS = ("tol", "max_iter", "acceptable_tol", "acceptable_iter", "mu_init", "bound_relax_factor",
                    "bound_push", "tau_min", "kappa_eps", "kappa_mu", "theta_mu", "s_max", "armijo", "max_backtrack",
                    "delta_c", "curv_min", "max_soc", "kappa_soc", "watchdog_shortened_iter_trigger",
-                   "watchdog_trial_iter_max")
+                   "watchdog_trial_iter_max", "limited_memory_max_history")
+_HESSIAN_APPROXIMATION = {"exact": 0, "limited-memory": 1}
 
 
 class NativeIpm:
@@ -801,7 +805,8 @@ class NativeIpm:
         self.fixed = np.where(lb == ub)[0]
         self.free = np.where(lb != ub)[0]
         self.ipm = _cfx.Ipm(self.h, lb, ub, int(getattr(ocp, "n_params", 0) or 0),
-                            {k: getattr(self.opt, k) for k in _NATIVE_OPTIONS})
+                            {**{k: getattr(self.opt, k) for k in _NATIVE_OPTIONS},
+                             "hessian_approximation": _HESSIAN_APPROXIMATION[self.opt.hessian_approximation]})
         self.calls = {"eval_all": 0, "eval_h": 0, "eval_g_f": 0, "kkt_factor": 0}
 
     def solve(self, v0=None, fixed_values=None):

@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define CFX_ABI_VERSION 3
+#define CFX_ABI_VERSION 4
 
 /* return codes */
 #define CFX_OK 0
@@ -319,7 +319,15 @@ typedef struct cfx_ipm_options {
        back there, backtracking from half the step */
     int32_t watchdog_shortened_iter_trigger;
     int32_t watchdog_trial_iter_max;
+    /* Ipopt's hessian_approximation: CFX_HESSIAN_EXACT (the callbacks' eval_h) or CFX_HESSIAN_LIMITED_MEMORY (no
+       eval_h: an L-BFGS approximation of the Lagrangian Hessian from the last limited_memory_max_history (6, at
+       most 16) steps, compact form sigma I - low rank, sigma = s^T y / s^T s; the low-rank part enters every Newton
+       solve through the Sherman-Morrison-Woodbury identity on the band factors) */
+    int32_t hessian_approximation;
+    int32_t limited_memory_max_history;
 } cfx_ipm_options;
+#define CFX_HESSIAN_EXACT 0
+#define CFX_HESSIAN_LIMITED_MEMORY 1
 
 typedef struct cfx_ipm_stats {
     int64_t eval_all, eval_g_f, eval_h, kkt_factor, iterations, host_syncs;

@@ -1,0 +1,130 @@
+"""The interval-sharded callbacks (cocofest_amd/distributed.py IntervalShardedNlp) over libcfx GPU handles: a
+world-2 run on one card (gloo, the ranks share cuda:0 — the driver's 8-GPU node runs the same code over RCCL)
+reassembles the single-process libcfx callbacks, and the batched interior point converges on them in lockstep.
+SURVEY.md section 8(e); the reference's analogue is CasADi's `map` over intervals with n_threads
+(cocofest/optimization/fes_ocp.py:122,189)."""
+
+import os
+import socket
+
+import numpy as np
+import pytest
+
+from tests import cases
+from tests.test_distributed import CFGS, _dense
+
+pytestmark = pytest.mark.gpu
+WORLD = 2
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, port, out_dir):
+    import torch
+    import torch.distributed as dist
+
+    from cocofest_amd.distributed import IntervalShardedNlp
+    from cocofest_amd.solver import BatchedIpm, IpmOptions
+    from tests.oracle_handle import oracle_problem_from_ocp
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    try:
+        B = 3
+        for ci, cfg in enumerate(CFGS):
+            ocp = cases.product_ocp(**cfg)
+            nlp = IntervalShardedNlp(ocp, batch=B, device=0)  # libcfx handle of this rank's interval slice
+            v = cases.random_decision(oracle_problem_from_ocp(ocp), B, seed=7)
+            vt = torch.tensor(v, device="cuda")
+            g = torch.empty((B, nlp.ng), dtype=torch.float64, device="cuda")
+            jac = torch.empty((B, nlp.nnz_jac), dtype=torch.float64, device="cuda")
+            f = torch.empty((B,), dtype=torch.float64, device="cuda")
+            grad = torch.empty((B, nlp.nv), dtype=torch.float64, device="cuda")
+            nlp.eval_all(vt, g=g, jac=jac, f=f, grad=grad)
+            rng = np.random.default_rng(ci)
+            lam = rng.standard_normal((B, nlp.ng))
+            of = rng.uniform(0.5, 2.0, B)
+            hv = torch.empty((B, nlp.nnz_hess), dtype=torch.float64, device="cuda")
+            nlp.eval_h(vt, torch.tensor(of, device="cuda"), torch.tensor(lam, device="cuda"), hv)
+            torch.cuda.synchronize()
+            jr, jc = nlp.jac_structure()
+            hr, hc = nlp.hess_structure()
+            np.savez(os.path.join(out_dir, f"cfg{ci}_r{rank}.npz"), v=v, g=g.cpu().numpy(), f=f.cpu().numpy(),
+                     grad=grad.cpu().numpy(), lam=lam, of=of,
+                     J=_dense(B, (nlp.ng, nlp.nv), jr, jc, jac.cpu().numpy()),
+                     H=_dense(B, (nlp.nv, nlp.nv), hr, hc, hv.cpu().numpy(), sym=True))
+            nlp.close()
+        ocp = cases.product_ocp(**CFGS[1])
+        nlp = IntervalShardedNlp(ocp, batch=2, device=0)
+        ipm = BatchedIpm(ocp, batch=2, options=IpmOptions(tol=1e-8, max_iter=300), handle=nlp, torch_device="cuda")
+        v0 = np.tile(ocp.initial_guess_vector(), (2, 1))
+        lb, ub = ocp.bounds_vector()
+        free = lb != ub
+        v0[:, free] = np.clip(v0[:, free] + np.random.default_rng(1).uniform(0, 1, (2, free.sum())) * 0.5, lb[free],
+                              ub[free])
+        res = ipm.solve(v0)
+        np.savez(os.path.join(out_dir, f"ipm_r{rank}.npz"), v=res.v, converged=res.converged, f=res.f, v0=v0)
+        ipm.close()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.fixture(scope="module")
+def sharded_gpu_run(tmp_path_factory):
+    import torch.multiprocessing as mp
+
+    out = tmp_path_factory.mktemp("dist_gpu")
+    mp.spawn(_worker, args=(_free_port(), str(out)), nprocs=WORLD, join=True)
+    return out
+
+
+def _single_process(ocp, v, lam, of):
+    h = ocp.nlp(batch=v.shape[0], layout="aos")
+    g, jac = h.eval_g(v), h.eval_jac_g(v)
+    f, grad = h.eval_f(v), h.eval_grad_f(v)
+    hv = h.eval_h(v, of, lam)
+    jr, jc = h.jac_structure()
+    hr, hc = h.hess_structure()
+    h.close()
+    B = v.shape[0]
+    return dict(g=g, f=f, grad=grad, J=_dense(B, (h.ng, h.nv), jr, jc, jac),
+                H=_dense(B, (h.nv, h.nv), hr, hc, hv, sym=True))
+
+
+@pytest.mark.parametrize("ci", range(len(CFGS)))
+def test_interval_sharded_libcfx_matches_single_process(sharded_gpu_run, ci):
+    r0 = np.load(sharded_gpu_run / f"cfg{ci}_r0.npz")
+    r1 = np.load(sharded_gpu_run / f"cfg{ci}_r1.npz")
+    for k in ("g", "f", "grad", "J", "H"):  # every rank holds the same full values
+        np.testing.assert_array_equal(r0[k], r1[k])
+    ref = _single_process(cases.product_ocp(**CFGS[ci]), r0["v"], r0["lam"], r0["of"])
+    scale = lambda a: np.abs(a).max() + 1e-300  # noqa: E731
+    # the slices' stim times are shifted by k0 dt: rounding-level differences in the calcium tables only
+    for k in ("g", "J", "grad", "H"):
+        assert np.abs(r0[k] - ref[k]).max() <= 1e-12 * scale(ref[k]), k
+    np.testing.assert_allclose(r0["f"], ref["f"], rtol=1e-12)
+
+
+def test_batched_interior_point_on_interval_sharded_libcfx(sharded_gpu_run):
+    """BatchedIpm over the 2-rank interval-sharded libcfx callbacks converges in lockstep on both ranks, to the point
+    the single-process native interior point reaches from the same starts (Ding2007 with fatigue, force tracking)."""
+    from cocofest_amd.solver import IpmOptions, NativeIpm
+
+    r0 = np.load(sharded_gpu_run / "ipm_r0.npz")
+    r1 = np.load(sharded_gpu_run / "ipm_r1.npz")
+    assert r0["converged"].all()
+    np.testing.assert_array_equal(r0["v"], r1["v"])
+    ocp = cases.product_ocp(**CFGS[1])
+    nat = NativeIpm(ocp, batch=2, options=IpmOptions(tol=1e-8, max_iter=300))
+    res = nat.solve(r0["v0"])
+    nat.close()
+    assert res.converged.all()
+    lb, ub = ocp.bounds_vector()
+    rng = np.where(np.isfinite(ub - lb), ub - lb, np.maximum(1.0, np.abs(res.v).max(axis=0)))
+    assert np.max(np.abs(r0["v"] - res.v) / rng) < 1e-5
+    np.testing.assert_allclose(r0["f"], res.f, rtol=1e-7)

@@ -188,3 +188,37 @@ def test_native_ipm_rejects_bad_input():
     with pytest.raises(_cfx.CfxError):
         _cfx.Ipm(ocp.nlp(batch=1), lb, ub, options={"max_backtrack": 0})
     h.close()
+
+
+@pytest.mark.parametrize("B", [1, 16])
+def test_limited_memory_hessian_cfg3(B):
+    """Ipopt's hessian_approximation="limited-memory" — the option the reference's cfg-3-shaped example passes
+    (examples/getting_started/pulse_duration_optimization.py:41, Solver.IPOPT(_hessian_approximation=...)) — in the
+    native interior point: no eval_h, an L-BFGS Hessian (6 pairs) through the Woodbury identity on the band factors.
+    It reaches the exact-Hessian KKT point (the problem's optimum does not depend on the Hessian approximation) on
+    cfg 3 (Ding2007 pulse widths, N = 100, force tracking), from the reference's initial guess and random starts,
+    on both KKT layouts (batch 1: dissected blocks + border; batch 16: one band)."""
+    from cocofest_amd import Solver
+    from cocofest_amd.solver import IpmOptions, NativeIpm
+
+    cfg = dict(cases.cfg3(), objective=TRACK)
+    ocp = cases.product_ocp(**cfg)
+    v0 = _starts(ocp, B, 3, spread=1.0)
+    exact = NativeIpm(ocp, batch=B, options=IpmOptions(tol=1e-8, max_iter=300))
+    r_ex = exact.solve(v0)
+    exact.close()
+    lm = NativeIpm(ocp, batch=B, options=IpmOptions(tol=1e-8, max_iter=1000, hessian_approximation="limited-memory"))
+    r_lm = lm.solve(v0)
+    st = lm.ipm.stats()
+    lm.close()
+    print("iterations exact", r_ex.iterations, "limited-memory", r_lm.iterations, "wall", r_ex.wall_time, r_lm.wall_time)
+    assert r_ex.converged.all() and r_lm.converged.all(), (r_lm.iterations, r_lm.kkt_error)
+    assert st["eval_h"] == 0
+    np.testing.assert_allclose(r_lm.f, r_ex.f, rtol=1e-6, atol=1e-9)
+    lb, ub = ocp.bounds_vector()
+    span = np.where(np.isfinite(ub - lb), ub - lb, np.maximum(np.abs(r_ex.v).max(0), 1.0))
+    assert np.max(np.abs(r_lm.v - r_ex.v) / np.maximum(span, 1e-12)) < 1e-4
+    if B == 1:  # the bioptim-style entry: ocp.solve(Solver.IPOPT(...))
+        res = ocp.solve(Solver.IPOPT(_hessian_approximation="limited-memory", _max_iter=1000, _tol=1e-8))
+        assert bool(res.converged[0])
+        np.testing.assert_allclose(res.f, r_ex.f, rtol=1e-6, atol=1e-9)
