@@ -587,7 +587,8 @@ def unpack(pb: MskProblem, v):
 
 def sliding_rows(pb: MskProblem, v, k):
     """custom_constraints.py:102-119 per Hmed muscle: u_k's T intensities minus the last T parameters up to the
-    node's last pulse, left-padded with the muscle's I_min."""
+    node's last pulse, left-padded with muscles_dynamics_model[0]'s I_min (custom_constraints.py:107-114 pads every
+    muscle's window with the first muscle model's min_pulse_intensity())."""
     X, U = unpack(pb, v)
     P = v[pb.n_shooting * pb.nz + pb.nx:]
     out, off = [], pb.n_pw
@@ -595,7 +596,7 @@ def sliding_rows(pb: MskProblem, v, k):
         idx = pb.last_stim_idx[k]
         cols = [P[pb.param_offset[mi] + i] for i in range(idx + 1)]
         while len(cols) < pb.T:
-            cols.insert(0, O.min_pulse_intensity(mus.c))
+            cols.insert(0, O.min_pulse_intensity(pb.muscles[0].c))
         cols = cols[len(cols) - pb.T:]
         out.append(U[k, off: off + pb.T] - np.array(cols))
         off += pb.T

@@ -336,7 +336,7 @@ def test_bench_shape_cfg5_msk():
     h.close()
     small = ocp.nlp(batch=len(pick), layout="aos")
     assert small.launch_shape()["msk_intervals_per_block"] == 1
-    gs, js = np.empty_like(gp), np.empty_like(jp)
+    gs, js = np.empty(gp.shape), np.empty(jp.shape)
     small.eval_all(vp, g=gs, jac=js)
     small.close()
     np.testing.assert_array_equal(gp, gs)
