@@ -141,6 +141,7 @@ SIGNATURES = {
     "cfx_eval_grad_f": (C.c_int, [_P, _P, _P, C.c_uint32]),
     "cfx_eval_h": (C.c_int, [_P, _P, _P, _P, _P, C.c_uint32]),
     "cfx_eval_all": (C.c_int, [_P, _P, _P, _P, _P, _P, C.c_uint32]),
+    "cfx_eval_all_h": (C.c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _P, C.c_uint32]),
     "cfx_integrate": (C.c_int, [_P, _P, _P, _P, C.c_uint32]),
     "cfx_msk_create": (C.c_int, [C.POINTER(MskProblem), C.POINTER(_P)]),
     "cfx_band_lu": (C.c_int, [C.c_int64, C.c_int32, C.c_int32, C.c_int64, _P, _P, _P, C.c_int32, _P, _P]),
@@ -448,6 +449,27 @@ class Handle:
         self._torch_stream(fl)
         self._check(self.lib.cfx_eval_h(self.h, _ptr(v), _ptr(obj_factor), _ptr(lam), _ptr(hess), fl))
         return hess
+
+    def eval_all_h(self, v, obj_factor, lam, g=None, jac=None, f=None, grad=None, hess=None):
+        """g, J_g, (f, grad f) and the Lagrangian Hessian at one point (cfx_eval_all_h: one launch on the shooting
+        transcriptions).  Returns (g, jac, hess)."""
+        if _is_tensor(v):  # device call: the missing outputs on the handle's device
+            import torch
+
+            new = lambda n: torch.empty(self._shape(n), dtype=torch.float64, device=v.device)  # noqa: E731
+        else:
+            new = lambda n: np.empty(self._shape(n))  # noqa: E731
+        g = new(self.ng) if g is None else g
+        jac = new(self.nnz_jac) if jac is None else jac
+        hess = new(self.nnz_hess) if hess is None else hess
+        (v, obj_factor, lam, g, jac, f, grad, hess), fl = self._buffers(
+            ("v", v, self.nv, False), ("obj_factor", obj_factor, 1, False), ("lam", lam, self.ng, False),
+            ("g", g, self.ng, True), ("jac", jac, self.nnz_jac, True), ("f", f, 1, True),
+            ("grad", grad, self.nv, True), ("hess", hess, self.nnz_hess, True))
+        self._torch_stream(fl)
+        self._check(self.lib.cfx_eval_all_h(self.h, _ptr(v), _ptr(obj_factor), _ptr(lam), _ptr(g), _ptr(jac),
+                                            _ptr(f), _ptr(grad), _ptr(hess), fl))
+        return g, jac, hess
 
     def integrate(self, x0=None, u=None, traj=None):
         n = (self.n_shooting * self.n_steps + 1) * self.nx

@@ -633,6 +633,7 @@ extern "C" int cfx_create(const cfx_problem* p, cfx_handle** out) {
     kp.nv_tot = h->sz.nv;
     kp.ng_tot = h->sz.ng;
     kp.nnz_tot = h->sz.nnz_jac;
+    kp.nh_tot = h->sz.nnz_hess;
     kp.nx = nx;
     kp.N = N;
     kp.m = p->n_steps;
@@ -857,6 +858,45 @@ static hipError_t launch_shooting(cfx_handle* h, bool derivs, const double* V, d
     return launch_shooting_ding(h->model, h->scheme, derivs, ni, h->kp, V, G, J, h->stream);
 }
 
+// Hmed sliding-window rows of g / J_g (k_slide; nothing for the other families)
+static void launch_slide(cfx_handle* h, const double* V, double* G, double* J) {
+    if (!h->kp.n_slide) return;
+    const int64_t B = h->prob.batch;
+    hipLaunchKernelGGL(k_slide,
+                       dim3((unsigned)((B + 255) / 256),
+                            (unsigned)std::min<int64_t>((int64_t)h->kp.N * h->kp.T, kMaxGridY)),
+                       dim3(256), 0, h->stream, h->kp, h->d_sl_param, h->d_sl_joff, h->prob.intensity_floor, V, G, J);
+}
+
+// f and grad f (either may be NULL)
+static hipError_t launch_objective(cfx_handle* h, const double* V, double* F, double* GR) {
+    const int64_t B = h->prob.batch;
+    if ((F || GR) && B < kObjBlockMaxB) {  // latency-bound: a block per instance, a thread per node
+        hipLaunchKernelGGL(k_objective_blk, dim3((unsigned)B), dim3(256), 0, h->stream, h->kp, h->n_obj, h->d_obj,
+                           h->d_targets, V, F, GR);
+    } else if (F || GR) {
+        if (GR) {
+            hipError_t e = hipMemsetAsync(GR, 0, (size_t)B * h->sz.nv * sizeof(double), h->stream);
+            if (e != hipSuccess) return e;
+        }
+        hipLaunchKernelGGL(k_objective, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, h->stream, h->kp, h->n_obj,
+                           h->d_obj, h->d_targets, V, F, GR);
+    }
+    return hipGetLastError();
+}
+
+// obj_factor * Hess(f) added onto the constraint Hessian H
+static hipError_t launch_objective_hess(cfx_handle* h, const double* OF, double* H) {
+    const int64_t B = h->prob.batch;
+    if (h->n_obj && B < kObjBlockMaxB)
+        hipLaunchKernelGGL(k_objective_hess_blk, dim3((unsigned)B), dim3(256), 0, h->stream, h->kp, h->n_obj,
+                           h->d_obj, OF, H);
+    else if (h->n_obj)
+        hipLaunchKernelGGL(k_objective_hess, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, h->stream, h->kp,
+                           h->n_obj, h->d_obj, OF, H);
+    return hipGetLastError();
+}
+
 static int msk_eval_all(cfx_handle* h, const double* v, double* g, double* jac, double* f, double* grad,
                         uint32_t flags);
 static int msk_eval_h(cfx_handle* h, const double* v, const double* obj_factor, const double* lambda, double* hess,
@@ -869,7 +909,6 @@ extern "C" int cfx_eval_all(cfx_handle* h, const double* v, double* g, double* j
     if (h->msk) return msk_eval_all(h, v, g, jac, f, grad, flags);
     CFX_HIP(h, hipSetDevice(h->device));
     int rc = CFX_OK;
-    const int64_t B = h->prob.batch;
     const double* V = stage_in(h, S_V, v, h->sz.nv, flags, &rc);
     if (!V) return rc;
     double* G = g ? stage_out(h, S_G, g, h->sz.ng, flags, &rc) : nullptr;
@@ -879,23 +918,9 @@ extern "C" int cfx_eval_all(cfx_handle* h, const double* v, double* g, double* j
     if (rc != CFX_OK) return rc;
     if (G || J) {
         CFX_HIP(h, launch_shooting(h, J != nullptr, V, G, J));
-        if (h->kp.n_slide)
-            hipLaunchKernelGGL(k_slide,
-                               dim3((unsigned)((B + 255) / 256),
-                                    (unsigned)std::min<int64_t>((int64_t)h->kp.N * h->kp.T, kMaxGridY)),
-                               dim3(256), 0,
-                               h->stream, h->kp, h->d_sl_param,
-                               h->d_sl_joff, h->prob.intensity_floor, V, G, J);
+        launch_slide(h, V, G, J);
     }
-    if ((F || GR) && B < kObjBlockMaxB) {  // latency-bound: a block per instance, a thread per node
-        hipLaunchKernelGGL(k_objective_blk, dim3((unsigned)B), dim3(256), 0, h->stream, h->kp, h->n_obj, h->d_obj,
-                           h->d_targets, V, F, GR);
-    } else if (F || GR) {
-        if (GR) CFX_HIP(h, hipMemsetAsync(GR, 0, (size_t)B * h->sz.nv * sizeof(double), h->stream));
-        hipLaunchKernelGGL(k_objective, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, h->stream, h->kp, h->n_obj,
-                           h->d_obj, h->d_targets, V, F, GR);
-    }
-    CFX_HIP(h, hipGetLastError());
+    CFX_HIP(h, launch_objective(h, V, F, GR));
     if (G && (rc = finish_out(h, S_G, G, g, h->sz.ng, flags)) != CFX_OK) return rc;
     if (J && (rc = finish_out(h, S_J, J, jac, h->sz.nnz_jac, flags)) != CFX_OK) return rc;
     if (F && (rc = finish_out(h, S_F, F, f, 1, flags)) != CFX_OK) return rc;
@@ -927,10 +952,8 @@ extern "C" int cfx_eval_h(cfx_handle* h, const double* v, const double* obj_fact
                           double* hess, uint32_t flags) {
     if (!h || !v || !obj_factor || !lambda || !hess) return h ? fail(h, CFX_EINVAL, "cfx_eval_h: NULL argument") : CFX_EINVAL;
     if (h->msk) return msk_eval_h(h, v, obj_factor, lambda, hess, flags);
-    if (h->kp.tiled) return fail(h, CFX_EUNSUPPORTED, "cfx_eval_h: not available with CFX_LAYOUT_TILED64");
     CFX_HIP(h, hipSetDevice(h->device));
     int rc = CFX_OK;
-    const int64_t B = h->prob.batch;
     const double* V = stage_in(h, S_V, v, h->sz.nv, flags, &rc);
     if (!V) return rc;
     const double* OF = stage_in(h, S_A1, obj_factor, 1, flags, &rc);
@@ -944,14 +967,46 @@ extern "C" int cfx_eval_h(cfx_handle* h, const double* v, const double* obj_fact
                                       h->stream));
     else
         CFX_HIP(h, launch_hessian(h->model, h->scheme, h->tmax, h->kp, h->d_htasks, h->n_htasks, h->hbs, V, LAM, H,
-                                  h->stream));
-    if (h->n_obj && B < kObjBlockMaxB)
-        hipLaunchKernelGGL(k_objective_hess_blk, dim3((unsigned)B), dim3(256), 0, h->stream, h->kp, h->n_obj,
-                           h->d_obj, OF, H);
-    else if (h->n_obj)
-        hipLaunchKernelGGL(k_objective_hess, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, h->stream, h->kp,
-                           h->n_obj, h->d_obj, OF, H);
-    CFX_HIP(h, hipGetLastError());
+                                  nullptr, nullptr, h->stream));
+    CFX_HIP(h, launch_objective_hess(h, OF, H));
+    if ((rc = finish_out(h, S_OUT, H, hess, h->sz.nnz_hess, flags)) != CFX_OK) return rc;
+    return sync_if_host(h, flags);
+}
+
+extern "C" int cfx_eval_all_h(cfx_handle* h, const double* v, const double* obj_factor, const double* lambda,
+                              double* g, double* jac, double* f, double* grad, double* hess, uint32_t flags) {
+    if (!h || !v || !obj_factor || !lambda || !g || !jac || !hess)
+        return h ? fail(h, CFX_EINVAL, "cfx_eval_all_h: NULL argument") : CFX_EINVAL;
+    if (h->msk || h->colloc) {  // the callbacks, then the Hessian at the same point
+        int rc = cfx_eval_all(h, v, g, jac, f, grad, flags);
+        if (rc != CFX_OK) return rc;
+        if (h->msk) h->stash_same_point = h->msk_stash && h->stash_valid;
+        return cfx_eval_h(h, v, obj_factor, lambda, hess, flags);
+    }
+    CFX_HIP(h, hipSetDevice(h->device));
+    int rc = CFX_OK;
+    const double* V = stage_in(h, S_V, v, h->sz.nv, flags, &rc);
+    if (!V) return rc;
+    const double* OF = stage_in(h, S_A1, obj_factor, 1, flags, &rc);
+    if (!OF) return rc;
+    const double* LAM = stage_in(h, S_A2, lambda, h->sz.ng, flags, &rc);
+    if (!LAM) return rc;
+    double* G = stage_out(h, S_G, g, h->sz.ng, flags, &rc);
+    double* J = stage_out(h, S_J, jac, h->sz.nnz_jac, flags, &rc);
+    double* F = f ? stage_out(h, S_F, f, 1, flags, &rc) : nullptr;
+    double* GR = grad ? stage_out(h, S_GRAD, grad, h->sz.nv, flags, &rc) : nullptr;
+    double* H = stage_out(h, S_OUT, hess, h->sz.nnz_hess, flags, &rc);
+    if (rc != CFX_OK || !G || !J || !H) return rc != CFX_OK ? rc : fail(h, CFX_EINVAL, "cfx_eval_all_h: staging");
+    // one launch: the interval's second-order jets carry the g rows and the J_g columns too
+    CFX_HIP(h, launch_hessian(h->model, h->scheme, h->tmax, h->kp, h->d_htasks, h->n_htasks, h->hbs, V, LAM, H, G, J,
+                              h->stream));
+    launch_slide(h, V, G, J);
+    CFX_HIP(h, launch_objective(h, V, F, GR));
+    CFX_HIP(h, launch_objective_hess(h, OF, H));
+    if ((rc = finish_out(h, S_G, G, g, h->sz.ng, flags)) != CFX_OK) return rc;
+    if ((rc = finish_out(h, S_J, J, jac, h->sz.nnz_jac, flags)) != CFX_OK) return rc;
+    if (F && (rc = finish_out(h, S_F, F, f, 1, flags)) != CFX_OK) return rc;
+    if (GR && (rc = finish_out(h, S_GRAD, GR, grad, h->sz.nv, flags)) != CFX_OK) return rc;
     if ((rc = finish_out(h, S_OUT, H, hess, h->sz.nnz_hess, flags)) != CFX_OK) return rc;
     return sync_if_host(h, flags);
 }

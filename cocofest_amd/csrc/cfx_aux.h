@@ -52,12 +52,13 @@ __global__ void __launch_bounds__(256) k_objective_hess(const KParams P, int n_o
     const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= B) return;
     const double s = obj_factor[b];
+    const int64_t ES = lay_stride(P), hb = lay_base(P, P.nh_tot, b);
     for (int t = 0; t < n_obj; ++t) {
         const DevObjective o = obj[t];
         const int e = (o.var_kind == 0 ? 0 : P.nx) + o.var_index;  // element of (x_k, u_k)
         for (int k = o.node_first; k <= o.node_last; ++k) {
             const int64_t hoff = P.hdiag[k * (P.nx + P.nu) + e];
-            H[hoff * B + b] += 2.0 * o.w_eff * s;
+            H[hb + hoff * ES] += 2.0 * o.w_eff * s;
         }
     }
 }
@@ -103,15 +104,15 @@ __global__ void __launch_bounds__(256) k_objective_hess_blk(const KParams P, int
                                                             const DevObjective* __restrict__ obj,
                                                             const double* __restrict__ obj_factor,
                                                             double* __restrict__ H) {
-    const int64_t B = P.B;
     const int64_t b = blockIdx.x;
     const double s = obj_factor[b];
+    const int64_t ES = lay_stride(P), hb = lay_base(P, P.nh_tot, b);
     for (int k = threadIdx.x; k <= P.N; k += 256)
         for (int t = 0; t < n_obj; ++t) {
             const DevObjective o = obj[t];
             if (k < o.node_first || k > o.node_last) continue;
             const int e = (o.var_kind == 0 ? 0 : P.nx) + o.var_index;
-            H[(int64_t)P.hdiag[k * (P.nx + P.nu) + e] * B + b] += 2.0 * o.w_eff * s;
+            H[hb + (int64_t)P.hdiag[k * (P.nx + P.nu) + e] * ES] += 2.0 * o.w_eff * s;
         }
 }
 

@@ -67,10 +67,15 @@ struct CsHmedJet {
     }
 };
 
-template <int MODEL, int SCHEME, int DJ, int TMAX>
+// GJ: the same launch also writes the continuity rows g and every J_g value of the interval (cfx_eval_all_h, the
+// north star's residuals + Jacobian + Hessian in one launch): the jets' first-order parts are the Jacobian columns of
+// the task's own block (diagonal tasks, each block's columns written by exactly one thread), task (0, 0) writes the
+// g rows and the -1 on x_{k+1}; the calcium row of the Ding families is the affine recursion (cfx_kernels.h).
+template <int MODEL, int SCHEME, int DJ, int TMAX, bool GJ>
 __global__ void __launch_bounds__(256) k_hessian(const KParams P, const HTask* __restrict__ tasks, int bs,
                                                  const double* __restrict__ V, const double* __restrict__ LAM,
-                                                 double* __restrict__ H) {
+                                                 double* __restrict__ H, double* __restrict__ G,
+                                                 double* __restrict__ J) {
     constexpr int NX = nx_of(MODEL);
     constexpr bool LIN = !is_int(MODEL);
     constexpr int S = stages_of(SCHEME);
@@ -80,7 +85,10 @@ __global__ void __launch_bounds__(256) k_hessian(const KParams P, const HTask* _
     if (b >= B) return;
     const int k = blockIdx.y;
     const HTask task = tasks[blockIdx.z];
-    const double* Vb = V + b;
+    // layout (SoA or 64-instance tiles): element stride ES, per-buffer instance bases
+    const int64_t ES = lay_stride(P), vb = lay_base(P, P.nv_tot, b), lb = lay_base(P, P.ng_tot, b),
+                  hb = lay_base(P, P.nh_tot, b), jb = lay_base(P, P.nnz_tot, b);
+    auto Vat = [&](int64_t e) { return V[vb + e * ES]; };
     const int xo = k * P.nz;
 
     int gd[DJ];
@@ -100,12 +108,12 @@ __global__ void __launch_bounds__(256) k_hessian(const KParams P, const HTask* _
 
     J_t x[NX];
 #pragma unroll
-    for (int r = 0; r < NX; ++r) x[r] = seed(Vb[(int64_t)(xo + r) * B], r);
+    for (int r = 0; r < NX; ++r) x[r] = seed(Vat(xo + r), r);
     const J_t cn0 = x[0];
 
     J_t afac = jconst<DJ>(1.0);
     if constexpr (is_pw(MODEL)) {
-        const double pw = Vb[(int64_t)(xo + NX) * B];
+        const double pw = Vat(xo + NX);
         const double ex = exp(-(pw - P.pd0) / P.pdt);
         // E = 1 - exp(-(pw - pd0)/pdt): E' = ex/pdt, E'' = -ex/pdt^2
         afac = jchain(seed(pw, NX), 1.0 - ex, ex / P.pdt, -ex / (P.pdt * P.pdt));
@@ -115,7 +123,7 @@ __global__ void __launch_bounds__(256) k_hessian(const KParams P, const HTask* _
         csh.coef = P.tab;
 #pragma unroll
         for (int i = 0; i < TMAX; ++i) {
-            const double ui = i < P.T ? Vb[(int64_t)(xo + NX + i) * B] : P.Is;
+            const double ui = i < P.T ? Vat(xo + NX + i) : P.Is;
             csh.lamv[i] = i < P.T ? P.ar * (tanh(P.bs * (ui - P.Is)) + P.cr) : 0.0;
         }
 #pragma unroll
@@ -123,7 +131,7 @@ __global__ void __launch_bounds__(256) k_hessian(const KParams P, const HTask* _
             csh.uidx[s] = -1;
             csh.l1[s] = csh.l2[s] = 0.0;
             if (gd[s] >= NX) {
-                const double th = tanh(P.bs * (Vb[(int64_t)(xo + gd[s]) * B] - P.Is));
+                const double th = tanh(P.bs * (Vat(xo + gd[s]) - P.Is));
                 const double d1 = P.bs * (1.0 - th * th);
                 csh.l1[s] = P.ar * d1;
                 csh.l2[s] = -2.0 * P.ar * P.bs * th * d1;
@@ -183,9 +191,38 @@ __global__ void __launch_bounds__(256) k_hessian(const KParams P, const HTask* _
     }
     // the calcium row of the Ding families is affine in cn0: no second-order term
 
+    if constexpr (GJ) {
+        const int end = P.m * S;  // the interval end's calcium slot (LIN)
+        const int64_t jo = (int64_t)k * P.nnzk;
+        if (task.I == task.J) {  // this block's Jacobian columns
+#pragma unroll
+            for (int sl = 0; sl < DJ; ++sl) {
+                const int g = sl < bs ? gd[sl] : -1;
+                if (g < 0) continue;
+                if constexpr (LIN) {
+                    if (g == 0 && P.jpos[0][0] >= 0) J[jb + (jo + P.jpos[0][0]) * ES] = P.cna[end];
+                }
+#pragma unroll
+                for (int r = R0; r < NX; ++r) {
+                    const int pos = P.jpos[r][g];
+                    if (pos >= 0) J[jb + (jo + pos) * ES] = x[r].g[sl];
+                }
+            }
+        }
+        if (blockIdx.z == 0) {  // g rows and the -1 on x_{k+1}
+            const int xn = (k + 1) * P.nz;
+#pragma unroll
+            for (int r = 0; r < NX; ++r) {
+                const double phi = (LIN && r == 0) ? fma(P.cna[end], cn0.v, cnb[end]) : x[r].v;
+                G[lb + (int64_t)(k * P.ngk + r) * ES] = phi - Vat(xn + r);
+                J[jb + (jo + P.jneg[r]) * ES] = -1.0;
+            }
+        }
+    }
+
     double lam[NX];
 #pragma unroll
-    for (int r = 0; r < NX; ++r) lam[r] = LAM[(int64_t)(k * P.ngk + r) * B + b];
+    for (int r = 0; r < NX; ++r) lam[r] = LAM[lb + (int64_t)(k * P.ngk + r) * ES];
     const int64_t ho = (int64_t)k * P.nhk;
 #pragma unroll
     for (int s1 = 0; s1 < DJ; ++s1) {
@@ -199,13 +236,13 @@ __global__ void __launch_bounds__(256) k_hessian(const KParams P, const HTask* _
 #pragma unroll
             for (int r = R0; r < NX; ++r) acc += lam[r] * x[r].h[s1 * (s1 + 1) / 2 + s2];
             const int i = g1 > g2 ? g1 : g2, jj = g1 > g2 ? g2 : g1;
-            H[(ho + i * (i + 1) / 2 + jj) * B + b] = acc;
+            H[hb + (ho + i * (i + 1) / 2 + jj) * ES] = acc;
         }
     }
     // x_N has no interval block: its (objective-only) diagonal starts from zero
     if (k == P.N - 1 && blockIdx.z == 0) {
 #pragma unroll
-        for (int r = 0; r < NX; ++r) H[((int64_t)P.N * P.nhk + r) * B + b] = 0.0;
+        for (int r = 0; r < NX; ++r) H[hb + ((int64_t)P.N * P.nhk + r) * ES] = 0.0;
     }
 }
 

@@ -8,8 +8,9 @@
 // cross-checked there against scipy's trust-constr on the CPU; this file restates it as a handful of fused HIP
 // kernels around the libcfx callbacks and the batched band LU, so that one iteration is ~10 launches and two host
 // reads of a 16-byte counter instead of ~1,500 small tensor operations:
-//   eval_all(x) -> k_ipm_begin (scaling, KKT error, convergence, barrier update, Sigma, Newton rhs)
-//   eval_h -> k_ipm_kkt (band assembly + rhs permutation) -> band LU + solve -> k_ipm_curv (inertia test)  [read]
+//   eval_all_h(x) (g, J_g, f, grad f and the Hessian in one call: cfx_eval_all_h; eval_all then eval_h at the
+//   start and after least-squares multipliers) -> k_ipm_begin (scaling, KKT error, convergence, barrier update, Sigma,
+//   Newton rhs) -> k_ipm_kkt (band assembly + rhs permutation) -> band LU + solve -> k_ipm_curv (inertia)   [read]
 //   k_ipm_dir (dz, fraction to the boundary, filter quantities, first trial point)
 //   eval g, f (trial) -> k_ipm_accept (filter acceptance, second-order correction set-up)               [read]
 //   k_ipm_update (filter augmentation, primal / dual steps, z safeguard)
@@ -1132,6 +1133,9 @@ __global__ void __launch_bounds__(kIB) k_ipm_update(const IpmK K, int resto) {
         for (int j = threadIdx.x; j < m; j += kIB) K.y[b * m + j] = K.wy[b * m + j];
     else if (mv)
         for (int j = threadIdx.x; j < m; j += kIB) K.y[b * m + j] = K.y[b * m + j] + alpha * dy[j];
+    // the Hessian's multipliers at the new iterate, as k_ipm_begin will form them: the next iteration evaluates
+    // g, J_g and the Hessian in one call (cfx_eval_all_h) before k_ipm_begin runs
+    for (int j = threadIdx.x; j < m; j += kIB) K.ysc[b * m + j] = K.y[b * m + j] * K.sg[b * m + j];
     __syncthreads();
     write_full(K, b, x, K.vx);
     if (threadIdx.x == 0) {
@@ -2129,7 +2133,16 @@ static int ipm_solve(cfx_ipm* s, const double* v0, const double* fixed_values, d
     bool reinit = K.m > 0;
     int32_t c[4];
     for (int it = 0; it < K.o.max_iter; ++it) {
-        IPM_RUN(R.eval_full(K.vx));
+        // after an ordinary iteration the multipliers of the Hessian are known before k_ipm_begin (k_ipm_update
+        // formed them): g, J_g, f, grad f and the Hessian of the new iterate from one call
+        const bool fused = it > 0 && !reinit && !K.lbfgs && K.m > 0;
+        if (fused) {
+            IPM_CFX(s, cfx_eval_all_h(s->h, K.vx, K.of, K.ysc, K.graw, K.jac, K.fraw, K.grad, K.hv, CFX_DEVICE));
+            s->st.eval_all++;
+            s->st.eval_h++;
+        } else {
+            IPM_RUN(R.eval_full(K.vx));
+        }
         if (reinit) {  // least-squares multipliers for the flagged instances (start, after a restoration)
             hipLaunchKernelGGL(k_ipm_begin, R.g, blk, 0, st, K, 3, 0);
             IPM_RUN(R.kkt_factor(KKT_LSMULT));
@@ -2143,7 +2156,7 @@ static int ipm_solve(cfx_ipm* s, const double* v0, const double* fixed_values, d
         if (K.lbfgs) {  // quasi-Newton pair of the last step, M (no eval_h: hv stays zero)
             hipLaunchKernelGGL(k_lbfgs_update, R.g, blk, 0, st, K);
             IPM_HIP(s, hipGetLastError());
-        } else {
+        } else if (!fused) {
             cfx_internal_msk_stash(s->h, 2);  // K.vx is the point of eval_full above: the MSK stage data may be re-used
             IPM_CFX(s, cfx_eval_h(s->h, K.vx, K.of, K.ysc, K.hv, CFX_DEVICE));
             s->st.eval_h++;

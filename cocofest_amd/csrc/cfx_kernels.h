@@ -79,7 +79,7 @@ struct KParams {
     // CFX_LAYOUT_TILED64: element e of instance b at ((b / 64) * len + e) * 64 + b % 64 (len = nv, ng or
     // nnz_jac per instance); otherwise SoA e * B + b
     int32_t tiled;
-    int64_t nv_tot, ng_tot, nnz_tot;
+    int64_t nv_tot, ng_tot, nnz_tot, nh_tot;  // per-instance lengths of v, g, J_g and Hessian buffers (layout bases)
 };
 
 // Element stride and the offset of instance b's element 0 in a buffer of `len` doubles per instance.

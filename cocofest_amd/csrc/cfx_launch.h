@@ -53,8 +53,9 @@ constexpr int hjet_of(int model) {
 }
 constexpr bool hsplit_of(int model) { return model != M_D03 && model != M_D07; }
 
+// G, J (both or neither): the same launch writes g and J_g too (cfx_eval_all_h)
 hipError_t launch_hessian(int model, int scheme, int tmax, const KParams& P, const HTask* tasks, int ntasks, int bs,
-                          const double* V, const double* LAM, double* H, hipStream_t s);
+                          const double* V, const double* LAM, double* H, double* G, double* J, hipStream_t s);
 
 // direct collocation (cfx_colloc.h, instantiated in cfx_inst_colloc.hip)
 hipError_t launch_colloc(int model, int tmax, const KParams& P, const double* V, double* G, double* J,
@@ -64,9 +65,14 @@ hipError_t launch_colloc_hess(int model, int tmax, const KParams& P, const HTask
 
 template <int MODEL, int SCHEME, int DJ, int TMAX>
 hipError_t launch_hessian_t(const KParams& P, const HTask* tasks, int ntasks, int bs, const double* V,
-                            const double* LAM, double* H, hipStream_t s) {
+                            const double* LAM, double* H, double* G, double* J, hipStream_t s) {
     dim3 grid((unsigned)((P.B + kBlock - 1) / kBlock), (unsigned)P.N, (unsigned)ntasks);
-    hipLaunchKernelGGL((k_hessian<MODEL, SCHEME, DJ, TMAX>), grid, dim3(kBlock), 0, s, P, tasks, bs, V, LAM, H);
+    if (G && J)
+        hipLaunchKernelGGL((k_hessian<MODEL, SCHEME, DJ, TMAX, true>), grid, dim3(kBlock), 0, s, P, tasks, bs, V, LAM, H,
+                           G, J);
+    else
+        hipLaunchKernelGGL((k_hessian<MODEL, SCHEME, DJ, TMAX, false>), grid, dim3(kBlock), 0, s, P, tasks, bs, V, LAM,
+                           H, (double*)nullptr, (double*)nullptr);
     return hipGetLastError();
 }
 

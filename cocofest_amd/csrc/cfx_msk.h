@@ -1538,7 +1538,9 @@ __global__ void __launch_bounds__(256) k_msk_values(const MskParams P, const Msk
     }
 }
 
-// stage coefficients from the stored stage inputs (thread = instance, interval, stage)
+// stage coefficients from the stored stage inputs (thread = instance, interval, stage).  Occupancy is what the
+// 334-register allocation gives (one wave per SIMD); forcing two (amdgpu_waves_per_eu(2, 2), <= 256 registers) ran
+// 0.70 -> 0.81 ms at cfg 5 (profiles/round3/msk_w2).
 template <int NQ, int NM, int FAM>
 __global__ void __launch_bounds__(256) k_msk_stagecoef_par(const MskParams P, const MskGeom* __restrict__ GG,
                                                            const double* __restrict__ V, const double* __restrict__ XS) {

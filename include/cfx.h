@@ -182,6 +182,12 @@ int cfx_eval_h(cfx_handle *h, const double *v, const double *obj_factor, const d
 /* fused g + J_g (+ f, grad f when non-NULL) in one pass over the decision vectors */
 int cfx_eval_all(cfx_handle *h, const double *v, double *g, double *jac, double *f, double *grad,
                  uint32_t flags);
+/* g + J_g + eval_h (+ f, grad f when non-NULL) at one point: Ipopt's eval_g / eval_jac_g / eval_h of an
+   accepted iterate (IpoptAlgorithm's new point, then the Hessian with the new multipliers).  On the shooting
+   transcriptions ONE launch integrates every interval on second-order jets and writes the three outputs; the
+   collocation and musculoskeletal problems run eval_all then eval_h.  g, jac, hess must be non-NULL. */
+int cfx_eval_all_h(cfx_handle *h, const double *v, const double *obj_factor, const double *lambda, double *g,
+                   double *jac, double *f, double *grad, double *hess, uint32_t flags);
 
 /* ---- IvpFes.integrate: single shooting from x0 (NULL: rest state) with per-interval controls
    u [N*nu per instance], writing every sub-step state: traj [(N*n_steps+1)*nx per instance]. ---- */

@@ -4,7 +4,9 @@ reassembles the single-process libcfx callbacks, and the batched interior point 
 SURVEY.md section 8(e); the reference's analogue is CasADi's `map` over intervals with n_threads
 (cocofest/optimization/fes_ocp.py:122,189)."""
 
+import json
 import os
+import pathlib
 import socket
 
 import numpy as np
@@ -15,6 +17,9 @@ from tests.test_distributed import CFGS, _dense
 
 pytestmark = pytest.mark.gpu
 WORLD = 2
+_FT = json.loads((pathlib.Path(__file__).parent / "golden" / "ref_formulas.json").read_text())["misc"]["force_tracking"]
+# BASELINE configs[2] (cfg 3: Ding2007 pulse widths, 30 pulses, N = 100, force tracking) for the interior point
+IPM_CFG = dict(cases.cfg3(), objective={"force_tracking": [np.array(_FT["time"]), np.array(_FT["force"])]})
 
 
 def _free_port():
@@ -59,7 +64,7 @@ def _worker(rank, port, out_dir):
                      J=_dense(B, (nlp.ng, nlp.nv), jr, jc, jac.cpu().numpy()),
                      H=_dense(B, (nlp.nv, nlp.nv), hr, hc, hv.cpu().numpy(), sym=True))
             nlp.close()
-        ocp = cases.product_ocp(**CFGS[1])
+        ocp = cases.product_ocp(**IPM_CFG)
         nlp = IntervalShardedNlp(ocp, batch=2, device=0)
         ipm = BatchedIpm(ocp, batch=2, options=IpmOptions(tol=1e-6, max_iter=500), handle=nlp, torch_device="cuda")
         v0 = np.tile(ocp.initial_guess_vector(), (2, 1))  # the reference's initial guess, and a perturbed one
@@ -118,7 +123,7 @@ def test_interval_sharded_libcfx_matches_single_process(sharded_gpu_run, ci):
 
 
 def test_batched_interior_point_on_interval_sharded_libcfx(sharded_gpu_run):
-    """BatchedIpm over the 2-rank interval-sharded libcfx callbacks (Ding2007 with fatigue, force tracking, from the
+    """BatchedIpm over the 2-rank interval-sharded libcfx callbacks (cfg 3, 50 intervals per rank, from the
     reference's initial guess and a perturbed start) converges in lockstep on both ranks, to the point — and in the
     iterations — of the same algorithm on one process-local handle of the whole problem."""
     r0 = np.load(sharded_gpu_run / "ipm_r0.npz")
@@ -128,8 +133,10 @@ def test_batched_interior_point_on_interval_sharded_libcfx(sharded_gpu_run):
     assert r0["converged"].all(), (r0["iterations"], r0["kkt"])
     np.testing.assert_array_equal(r0["v"], r1["v"])
     assert np.all(np.abs(r0["iterations"] - one["iterations"]) <= 2), (r0["iterations"], one["iterations"])
-    ocp = cases.product_ocp(**CFGS[1])
+    ocp = cases.product_ocp(**IPM_CFG)
     lb, ub = ocp.bounds_vector()
-    span = np.where(np.isfinite(ub - lb), ub - lb, np.maximum(1.0, np.abs(one["v"]).max(axis=0)))
+    # fixed variables (lb == ub) have zero span: floor it with the variable's own magnitude
+    span = np.where(np.isfinite(ub - lb), ub - lb, 0.0)
+    span = np.maximum(span, np.maximum(1e-12, np.abs(one["v"]).max(axis=0)))
     assert np.max(np.abs(r0["v"] - one["v"]) / span) < 1e-6
     np.testing.assert_allclose(r0["f"], one["f"], rtol=1e-7)

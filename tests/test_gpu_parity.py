@@ -176,7 +176,8 @@ def test_layouts_and_device_pointers_are_bitwise_identical():
 def test_tiled_layout_is_bitwise_identical(name, scheme):
     """CFX_LAYOUT_TILED64 (64-instance tiles, two instances per lane) gives the same g, J_g, f, grad f bits as SoA
     (one per lane), and matches the oracle; Hmed's sliding rows and the objective kernels included; RK1 of the
-    two-state Ding families runs the fused Euler step; unsupported entry points fail loudly."""
+    two-state Ding families runs the fused Euler step; so does the Hessian (bitwise), and the fused g + J_g + Hessian
+    launch to rounding; a batch the tiles do not divide fails loudly."""
     import torch
 
     from cocofest_amd import _cfx
@@ -210,10 +211,20 @@ def test_tiled_layout_is_bitwise_identical(name, scheme):
     np.testing.assert_array_equal(untile(til[3]), soa[3])
     _close_g(pb, v, untile(til[0]).T, O.eval_g(pb, v), what=f"tiled g {name} {scheme}")
     _close(untile(til[1]).T, O.eval_jac_g(pb, v), what=f"tiled J {name} {scheme}")
-    with pytest.raises(_cfx.CfxError):
-        ht.eval_h(torch.tensor(vt, device="cuda"), torch.ones(B, dtype=torch.float64, device="cuda"),
-                  torch.zeros((B // 64, ht.ng, 64), dtype=torch.float64, device="cuda"),
-                  torch.empty((B // 64, ht.nnz_hess, 64), dtype=torch.float64, device="cuda"))
+    # the Lagrangian Hessian (and the fused g + J_g + H launch) on tiles: the same bits as SoA
+    rng = np.random.default_rng(3)
+    lam, of = rng.standard_normal((B, hs.ng)), rng.uniform(0.5, 2.0, B)
+    ofd = torch.tensor(of, device="cuda")
+    hh_s = hs.eval_h(torch.tensor(np.ascontiguousarray(v.T), device="cuda"), ofd,
+                     torch.tensor(np.ascontiguousarray(lam.T), device="cuda"),
+                     torch.empty((hs.nnz_hess, B), dtype=torch.float64, device="cuda"))
+    lt = torch.tensor(np.ascontiguousarray(lam.reshape(B // 64, 64, -1).transpose(0, 2, 1)), device="cuda")
+    hh_t = ht.eval_h(torch.tensor(vt, device="cuda"), ofd, lt,
+                     torch.empty((B // 64, ht.nnz_hess, 64), dtype=torch.float64, device="cuda"))
+    np.testing.assert_array_equal(untile(hh_t.cpu().numpy()), hh_s.cpu().numpy())
+    fg, fj, fh = ht.eval_all_h(torch.tensor(vt, device="cuda"), ofd, lt)
+    for got, want in ((fg, soa[0]), (fj, soa[1]), (fh, hh_s.cpu().numpy())):
+        assert np.abs(untile(got.cpu().numpy()) - want).max() <= 1e-13 * (np.abs(want).max() + 1.0)
     with pytest.raises(_cfx.CfxError):
         ocp.nlp(batch=100, layout="tiled64")
     hs.close()
@@ -344,6 +355,58 @@ def test_lagrangian_hessian_vs_oracle(name, scheme):
     scale = np.maximum(np.abs(ref), 1e-4 * np.max(np.abs(ref), axis=1, keepdims=True))
     err = np.max(np.abs(got - ref) / scale)
     assert err < 1e-7, f"H {name} {scheme}: {err:.3e}"
+
+
+@pytest.mark.parametrize("scheme", ["RK1", "RK2", "RK4"])
+@pytest.mark.parametrize("name", O.MODEL_NAMES)
+def test_fused_g_jacobian_hessian(name, scheme):
+    """cfx_eval_all_h — g, J_g, f, grad f and the Lagrangian Hessian from ONE shooting launch on second-order jets
+    (Hmed's sliding rows and the objective kernels beside it) — against the separate callbacks: f and grad f bit for
+    bit (the same kernels), g, J_g and the Hessian to rounding, 1e-13 of the largest entry (the jets' value and
+    first-order parts are the shooting kernel's recursion in another evaluation order; the Hessian instantiation that
+    also stores g and J_g is scheduled differently, a few ulp on Hmed), and g / J_g against the oracle."""
+    t = np.linspace(0, 1, 30)
+    obj = {"force_tracking": [t, 60 * np.sin(np.pi * t) ** 2], "end_node_tracking": 50}
+    stims = [0.0, 0.02, 0.04, 0.06]
+    ocp = cases.product_ocp(name, stims, 0.08, 3, scheme=scheme, m=2, objective=obj)
+    pb = cases.oracle_problem(name, stims, 0.08, 3, scheme=scheme, m=2, objective=obj)
+    B = 5
+    v = cases.random_decision(pb, B, seed=4)
+    rng = np.random.default_rng(5)
+    lam, of = rng.normal(size=(B, pb.ng)), rng.uniform(0.5, 2.0, B)
+    h = ocp.nlp(batch=B)
+    g, jac, grad = (np.empty((B, n)) for n in (h.ng, h.nnz_jac, h.nv))
+    f = np.empty(B)
+    h.eval_all(v, g=g, jac=jac, f=f, grad=grad)
+    hs = h.eval_h(v, of, lam)
+    fg, fj, ff, fgr = np.empty_like(g), np.empty_like(jac), np.empty_like(f), np.empty_like(grad)
+    _, _, fh = h.eval_all_h(v, of, lam, g=fg, jac=fj, f=ff, grad=fgr)
+    h.close()
+    np.testing.assert_array_equal(ff, f)
+    np.testing.assert_array_equal(fgr, grad)
+    for got, want in ((fg, g), (fj, jac), (fh, hs)):
+        assert np.abs(got - want).max() <= 1e-13 * (np.abs(want).max() + 1.0)
+    _close_g(pb, v, fg, O.eval_g(pb, v), what=f"fused g {name} {scheme}")
+    _close(fj, O.eval_jac_g(pb, v), what=f"fused J {name} {scheme}")
+
+
+def test_fused_callbacks_on_collocation_run_both_passes():
+    """cfx_eval_all_h on a collocation handle (eval_all, then eval_h): the separate callbacks' bits."""
+    ocp = cases.product_collocation_ocp("ding2007", COL_STIMS, 0.5, 4, degree=3, method="legendre",
+                                        objective={"end_node_tracking": 40.0}, n_shooting=5)
+    from tests.oracle_handle import oracle_problem_from_ocp
+
+    pb = oracle_problem_from_ocp(ocp)
+    B = 4
+    v = cases.random_collocation_decision(pb, B, seed=11)
+    rng = np.random.default_rng(3)
+    lam, of = rng.standard_normal((B, pb.ng)), rng.uniform(0.5, 2.0, B)
+    h = ocp.nlp(batch=B, layout="aos")
+    g, jac, hs = h.eval_g(v), h.eval_jac_g(v), h.eval_h(v, of, lam)
+    fg, fj, fh = h.eval_all_h(v, of, lam)
+    h.close()
+    for a, b in ((fg, g), (fj, jac), (fh, hs)):
+        np.testing.assert_array_equal(a, b)
 
 
 def test_interior_point_on_gpu_matches_forward_integration():

@@ -159,6 +159,12 @@ def test_msk_hessian_matches_oracle(case):
     of = np.array([0.7, 0.3, 1.1])
     h = ocp.nlp(batch=B, layout="aos")
     hv = h.eval_h(V, of, lam)
+    fg, fj, fh = h.eval_all_h(V, of, lam)  # cfx_eval_all_h: eval_all then eval_h on a musculoskeletal handle
+    np.testing.assert_array_equal(fh, hv)
+    g2, j2 = np.empty_like(fg), np.empty_like(fj)
+    h.eval_all(V, g=g2, jac=j2)  # g with J_g comes from the stage kernels (g alone: the value recursion, a few ulp off)
+    np.testing.assert_array_equal(fg, g2)
+    np.testing.assert_array_equal(fj, j2)
     hr, hc = h.hess_structure()
     h0 = h.eval_h(V, np.zeros(B), np.zeros_like(lam))  # objective-only part (obj_factor 0 -> zero)
     h.close()
