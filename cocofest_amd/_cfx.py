@@ -110,14 +110,17 @@ class IpmOptions(C.Structure):
                 ("max_backtrack", C.c_int32), ("delta_c", C.c_double), ("curv_min", C.c_double),
                 ("max_soc", C.c_int32), ("kappa_soc", C.c_double), ("watchdog_shortened_iter_trigger", C.c_int32),
                 ("watchdog_trial_iter_max", C.c_int32), ("hessian_approximation", C.c_int32),
-                ("limited_memory_max_history", C.c_int32)]
+                ("limited_memory_max_history", C.c_int32), ("restoration", C.c_int32),
+                ("max_resto_iter", C.c_int32), ("resto_penalty", C.c_double),
+                ("required_infeasibility_reduction", C.c_double)]
 
 
 class IpmStats(C.Structure):
     _fields_ = [("eval_all", C.c_int64), ("eval_g_f", C.c_int64), ("eval_h", C.c_int64), ("kkt_factor", C.c_int64),
                 ("iterations", C.c_int64), ("host_syncs", C.c_int64), ("wall_s", C.c_double),
                 ("kkt_n", C.c_int64), ("kkt_kl", C.c_int64), ("kkt_ku", C.c_int64), ("kkt_band_n", C.c_int64),
-                ("kkt_border", C.c_int64), ("kkt_blocks", C.c_int64)]
+                ("kkt_border", C.c_int64), ("kkt_blocks", C.c_int64), ("resto_phases", C.c_int64),
+                ("resto_iterations", C.c_int64)]
 
 
 # exported symbols and their signatures (must match include/cfx.h)

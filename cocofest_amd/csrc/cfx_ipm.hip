@@ -52,6 +52,11 @@ struct Scal {
     // limited-memory Hessian (L-BFGS): sigma, pairs held, next ring slot, previous iterate saved
     double lsig;
     int32_t lcount, lhead, lprev, lpad;
+    // restoration phase (CFX_RESTORATION_PHASE): its barrier, the original infeasibility where it started, its own
+    // regularisation, line-search and filter quantities; rs_on: in the phase, rs_ok: left it successfully
+    double rs_mu, rs_tau, rs_th0, rs_dw, rs_dwl, rs_theta, rs_phi, rs_dphi, rs_alpha, rs_ap, rs_az, rs_tmax, rs_tmin;
+    int32_t rs_on, rs_ok, rs_acc, rs_arm, rs_it;
+    int32_t stop;  // out of iterations (restoration-phase ones included): done, not converged
 };
 
 struct IpmK {
@@ -109,9 +114,16 @@ struct IpmK {
     double *Mm, *Cl;           // [B][2 hmax][2 hmax]
     int32_t* Cp;               // [B][2 hmax]
     double* Zb;                // [2 hmax][B][nKp]
+    // restoration phase: p, n (the constraint relaxation c(x) - p + n = 0), their multipliers, steps and trial values,
+    // the phase's constraint multipliers, the eliminated (2,2) block -(p / zp + n / zn) of its KKT matrix ([B][m]);
+    // the phase's multipliers of the x bounds ([B][nf]); its filter; a zero objective factor for its Hessian ([B])
+    int rsphase;
+    double *rp, *rn, *rzp, *rzn, *rdp, *rdn, *rdzp, *rdzn, *rpt, *rnt, *ry, *rdc;
+    double *rzl, *rzu;
+    double *rfilt, *ofz;
 };
 
-enum { KKT_NEWTON = 0, KKT_LSMULT = 1, KKT_RESTO = 2 };
+enum { KKT_NEWTON = 0, KKT_LSMULT = 1, KKT_RESTO = 2, KKT_RSNLP = 3 };
 enum { SRC_W = 0, SRC_JV = 1, SRC_DIAG = 2, SRC_DC = 3 };
 constexpr int kSrcShift = 29;
 constexpr int32_t kSrcMask = (1 << kSrcShift) - 1;
@@ -238,31 +250,53 @@ __device__ double barrier_obj(const IpmK& K, int64_t b, const double* x, double 
     return bad > 0 ? INFINITY : f - mu * (sL + sU);
 }
 
-// solver.py _filter_accept: (accepted, by the Armijo / f-type rule) for a trial with tt = ||g||_1, pt = barrier
-__device__ void filter_accept(const IpmK& K, const Scal& S, const double* filt, double tt, double pt, double alpha,
-                              double* sh, bool& ok, bool& arm) {
+// (tt, pt) dominated by an entry of the filter (block-wide, same in every thread)
+__device__ bool filter_dominated(const double* filt, double tt, double pt, double* sh) {
     double inf_ = 0.0;
     for (int k = threadIdx.x; k < kFilt; k += kIB)
         if (tt >= filt[2 * k] && pt >= filt[2 * k + 1]) inf_ = 1.0;
-    inf_ = breduce(inf_, OpMax(), sh);
+    return breduce(inf_, OpMax(), sh) > 0;
+}
+
+// Ipopt's filter test of a trial (tt = ||c||_1, pt = barrier objective) against the current point (theta, phi,
+// directional derivative dphi, step alpha): (accepted, by the Armijo / f-type rule)
+__device__ void filter_core(const IpmK& K, const double* filt, double theta, double phi, double dphi, double theta_max,
+                            double theta_min, double tt, double pt, double alpha, double* sh, bool& ok, bool& arm) {
+    const bool dominated = filter_dominated(filt, tt, pt, sh);
     const bool finite = isfinite(pt) && isfinite(tt);
-    // in the watchdog, trial points are judged against the iterate where it started (with its full step length)
-    const double theta = S.wd_on ? S.wd_theta : S.theta, phi = S.wd_on ? S.wd_phi : S.phi;
-    const double dphi = S.wd_on ? S.wd_dphi : S.dphi;
-    if (S.wd_on) alpha = S.wd_ap;
     const bool switching = (dphi < 0) && (alpha * pow(clamp_lo(-dphi, 0.0), 2.3) > 1.0 * pow(theta, 1.1)) &&
-                           (theta <= S.theta_min);
+                           (theta <= theta_min);
     // Ipopt's Compare_le(lhs, rhs, base): lhs - rhs <= 10 eps |base| (round-off in phi near an optimum)
     const double tol_phi = 10 * kEps * fabs(phi);
     const bool armijo_ok = (pt - phi) - K.o.armijo * alpha * dphi <= tol_phi;
     const bool suff = (tt - (1 - 1e-5) * theta <= 10 * kEps * theta) || ((pt - phi) + 1e-5 * theta <= tol_phi);
-    ok = finite && (tt <= S.theta_max) && !(inf_ > 0) && (switching ? armijo_ok : suff);
+    ok = finite && (tt <= theta_max) && !dominated && (switching ? armijo_ok : suff);
     arm = switching && armijo_ok;
+}
+
+// solver.py _filter_accept: (accepted, by the Armijo / f-type rule) for a trial with tt = ||g||_1, pt = barrier
+__device__ void filter_accept(const IpmK& K, const Scal& S, const double* filt, double tt, double pt, double alpha,
+                              double* sh, bool& ok, bool& arm) {
+    // in the watchdog, trial points are judged against the iterate where it started (with its full step length)
+    const double theta = S.wd_on ? S.wd_theta : S.theta, phi = S.wd_on ? S.wd_phi : S.phi;
+    const double dphi = S.wd_on ? S.wd_dphi : S.dphi;
+    if (S.wd_on) alpha = S.wd_ap;
+    filter_core(K, filt, theta, phi, dphi, S.theta_max, S.theta_min, tt, pt, alpha, sh, ok, arm);
 }
 
 // x -> full decision vector (fixed entries are already in place)
 __device__ inline void write_full(const IpmK& K, int64_t b, const double* xs, double* v) {
     for (int i = threadIdx.x; i < K.nf; i += kIB) v[b * K.n + K.free[i]] = xs[i] * K.d[i];
+}
+
+// restoration phase: weight zeta D_R,i^2 of the proximity term zeta/2 |D_R (x - x_r)|^2, zeta = sqrt(mu_R),
+// D_R,i = min(1, 1 / |x_r,i|) (Ipopt resto_proximity_weight 1); x_r is the iterate where the phase started (K.x)
+__device__ inline double rs_weight(double mu, double xref) {
+    const double r = clamp_lo(fabs(xref), 1.0);
+    return sqrt(mu) / (r * r);
+}
+__device__ inline double rs_prox(const IpmK& K, int64_t b, int i) {
+    return rs_weight(K.sc[b].rs_mu, K.x[b * K.nf + i]);
 }
 
 // ---------------------------------------------------------------------------------------------------------------
@@ -405,6 +439,7 @@ __global__ void __launch_bounds__(kIB) k_ipm_begin(const IpmK K, int mode, int s
         S.acc = S.err0 <= K.o.acceptable_tol ? S.acc + 1 : 0;
         const bool newly = !S.done && (S.err0 <= K.o.tol || S.acc >= K.o.acceptable_iter);
         S.done = S.done || newly;
+        if (!S.done && S.iters >= K.o.max_iter) S.done = S.stop = 1;  // per-instance budget
     }
     __syncthreads();
     // monotone barrier update: while the barrier sub-problem is solved, decrease mu (at most 5 times)
@@ -459,17 +494,26 @@ __global__ void __launch_bounds__(kIB) k_ipm_kkt(const IpmK K, int mode) {
         const double* hv = K.hv + b * K.nnzh;
         const double* jv = K.jv + b * K.nj;
         const double* sig = K.sig + b * K.nf;
-        const double dw = K.sc[b].dw + (K.lbfgs ? K.sc[b].lsig : 0.0);  // L-BFGS: W = sigma I - low rank (Woodbury)
+        // L-BFGS: W = sigma I - low rank (Woodbury); restoration phase: its own regularisation and proximity term
+        const bool rs = mode == KKT_RSNLP;
+        const double dw = rs ? K.sc[b].rs_dw : K.sc[b].dw + (K.lbfgs ? K.sc[b].lsig : 0.0);
         for (int k = K.kkt_ptr[p]; k < K.kkt_ptr[p + 1]; ++k) {
             const int32_t code = K.kkt_src[k];
             const int idx = code & kSrcMask;
             switch (code >> kSrcShift) {
                 case SRC_W:
-                    if (mode == KKT_NEWTON) v += hv[K.hsel[idx]] * K.d[K.hr[idx]] * K.d[K.hc[idx]];
+                    if (mode == KKT_NEWTON || rs) v += hv[K.hsel[idx]] * K.d[K.hr[idx]] * K.d[K.hc[idx]];
                     break;
                 case SRC_JV: v += jv[idx]; break;
-                case SRC_DIAG: v += mode == KKT_NEWTON ? sig[idx] + dw : (mode == KKT_LSMULT ? 1.0 : sig[idx] + 1.0); break;
-                default: v += idx ? 1.0 : -K.o.delta_c; break;  // unit diagonal of a padding row / -delta_c
+                case SRC_DIAG:
+                    if (rs)
+                        v += sig[idx] + dw + rs_prox(K, b, idx);
+                    else
+                        v += mode == KKT_NEWTON ? sig[idx] + dw : (mode == KKT_LSMULT ? 1.0 : sig[idx] + 1.0);
+                    break;
+                default:  // unit diagonal of a padding row / -delta_c (restoration: - p / zp - n / zn of row idx)
+                    v += idx == kSrcMask ? 1.0 : -K.o.delta_c + (rs ? K.rdc[b * K.m + idx] : 0.0);
+                    break;
             }
         }
         if (p < K.NE_A) {
@@ -488,7 +532,7 @@ __global__ void __launch_bounds__(kIB) k_ipm_kkt(const IpmK K, int mode) {
     if (p < K.nK) {
         const int nf = K.nf;
         double r;
-        if (mode == KKT_NEWTON)
+        if (mode == KKT_NEWTON || mode == KKT_RSNLP)
             r = K.rhs[b * K.nK + p];
         else if (mode == KKT_LSMULT)
             r = p < nf ? -(K.gF[b * nf + p] - K.zl[b * nf + p] + K.zu[b * nf + p]) : 0.0;
@@ -628,24 +672,29 @@ __global__ void __launch_bounds__(kIB) k_ipm_schur(const IpmK K, int factor) {
     for (int c = t; c < np; c += kIB) rb[PA + c] = sv[c];
 }
 
-// Newton step in natural order and the curvature test (solver.py inertia loop); bumps dw where it fails.
-__global__ void __launch_bounds__(kIB) k_ipm_curv(const IpmK K, int slot) {
+// Newton step in natural order and the curvature test (solver.py inertia loop); bumps dw where it fails.  rs: the
+// restoration phase's step (instances in the phase only; its dx in dxr, its own dw, the proximity weights)
+__global__ void __launch_bounds__(kIB) k_ipm_curv(const IpmK K, int slot, int rs) {
     __shared__ Scal S;
     const int64_t b = blockIdx.x;
     const int nf = K.nf;
     load_scal(K, b, S);
+    const bool active = rs ? (bool)S.rs_on : !S.done;
+    const double dwc = rs ? S.rs_dw : S.dw;
     const double* rb = K.rb + b * K.nKp;
-    double* dx = K.dx + b * nf;
+    double* dx = (rs ? K.dxr : K.dx) + b * nf;
     double* dy = K.dy + b * K.m;
     double nonfin = 0.0;
-    for (int i = threadIdx.x; i < K.nK; i += kIB) {
-        const double r = rb[K.pos[i]];
-        if (!isfinite(r)) nonfin = 1.0;
-        if (i < nf)
-            dx[i] = r;
-        else
-            dy[i - nf] = r;
-    }
+    // the phase's solves of the instances outside it are not steps: their dy (main-loop step) stays
+    if (active || !rs)
+        for (int i = threadIdx.x; i < K.nK; i += kIB) {
+            const double r = rb[K.pos[i]];
+            if (!isfinite(r)) nonfin = 1.0;
+            if (i < nf)
+                dx[i] = r;
+            else
+                dy[i - nf] = r;
+        }
     __syncthreads();
     const double* hv = K.hv + b * K.nnzh;
     double quad = 0.0;
@@ -657,7 +706,7 @@ __global__ void __launch_bounds__(kIB) k_ipm_curv(const IpmK K, int slot) {
     const double* sig = K.sig + b * nf;
     double dd = 0.0, nrm = 0.0;
     for (int i = threadIdx.x; i < nf; i += kIB) {
-        dd += (sig[i] + S.dw) * dx[i] * dx[i];
+        dd += (sig[i] + dwc + (rs ? rs_prox(K, b, i) : 0.0)) * dx[i] * dx[i];
         nrm += dx[i] * dx[i];
     }
     {
@@ -674,17 +723,19 @@ __global__ void __launch_bounds__(kIB) k_ipm_curv(const IpmK K, int slot) {
     for (int q = 0; q < K.P; ++q) sing = sing || K.info[b * K.P + q] != 0;
     // L-BFGS: the approximation is positive definite by construction (pairs with s^T y <= 0 are skipped), so only a
     // singular or non-finite factorisation asks for more regularisation
-    const bool weak = K.lbfgs ? false : ((curv <= K.o.curv_min * nrm) || !isfinite(curv));
-    const bool bad = !S.done && (weak || sing || nonfin > 0);
+    const bool weak = (K.lbfgs && !rs) ? false : ((curv <= K.o.curv_min * nrm) || !isfinite(curv));
+    const bool bad = active && (weak || sing || nonfin > 0);
     if (threadIdx.x == 0 && bad) {
-        if (S.dw == 0.0)
-            S.dw = S.dwl > 0 ? clamp_lo(S.dwl / 3, 1e-20) : 1e-4;
+        double& dw = rs ? S.rs_dw : S.dw;
+        const double dwl = rs ? S.rs_dwl : S.dwl;
+        if (dw == 0.0)
+            dw = dwl > 0 ? clamp_lo(dwl / 3, 1e-20) : 1e-4;
         else
-            S.dw = S.dw * 8;
+            dw = dw * 8;
     }
     store_scal(K, b, S);
     if (threadIdx.x == 0) {
-        count_add(K, slot, 0, !S.done);
+        count_add(K, slot, 0, active);
         if (bad) atomicAdd(K.cnt + 4 * slot + 1, 1);
     }
 }
@@ -1054,7 +1105,7 @@ __global__ void __launch_bounds__(kIB) k_ipm_update(const IpmK K, int resto) {
     const bool failed = !S.accepted && !S.done;
     const bool forced = S.forced;
     const bool grow = !S.done && S.accepted && !S.armijo && !forced;
-    const bool reset = failed && resto && m > 0;
+    const bool reset = failed && resto && m > 0;  // resto 1: restoration step, 2: restoration phase
     // watchdog bookkeeping (solver.py): an acceptable point ends it; after watchdog_trial_iter_max unacceptable full
     // steps the iterate returns to where it started, and the next line search starts at half its step
     const bool wd_ok = S.wd_on && S.accepted && !forced;
@@ -1068,7 +1119,7 @@ __global__ void __launch_bounds__(kIB) k_ipm_update(const IpmK K, int resto) {
         filt[2 * k + 1] = S.phi - 1e-5 * S.theta;
     }
     __syncthreads();
-    if (reset)
+    if (reset)  // a fresh filter after a restoration (step or phase, see k_rs_init)
         for (int k = threadIdx.x; k < kFilt; k += kIB) {
             filt[2 * k] = INFINITY;
             filt[2 * k + 1] = -INFINITY;
@@ -1131,6 +1182,8 @@ __global__ void __launch_bounds__(kIB) k_ipm_update(const IpmK K, int resto) {
     }
     if (wd_back)
         for (int j = threadIdx.x; j < m; j += kIB) K.y[b * m + j] = K.wy[b * m + j];
+    else if (reset && resto == 2)  // after the phase: zero multipliers (Ipopt constr_mult_reset_threshold = 0)
+        for (int j = threadIdx.x; j < m; j += kIB) K.y[b * m + j] = 0.0;
     else if (mv)
         for (int j = threadIdx.x; j < m; j += kIB) K.y[b * m + j] = K.y[b * m + j] + alpha * dy[j];
     // the Hessian's multipliers at the new iterate, as k_ipm_begin will form them: the next iteration evaluates
@@ -1141,7 +1194,7 @@ __global__ void __launch_bounds__(kIB) k_ipm_update(const IpmK K, int resto) {
     if (threadIdx.x == 0) {
         if (grow) S.fpos += 1;
         if (reset) {
-            S.reinit = 1;
+            S.reinit = resto == 1;  // the step re-estimates the multipliers by least squares
             S.lcount = S.lhead = S.lprev = 0;  // the quasi-Newton pairs describe the abandoned region
             S.lsig = 1.0;
         }
@@ -1154,6 +1207,469 @@ __global__ void __launch_bounds__(kIB) k_ipm_update(const IpmK K, int resto) {
         if (wd_back) S.mu = S.wd_mu;
     }
     store_scal(K, b, S);
+}
+
+// ---- Ipopt's feasibility-restoration phase (CFX_RESTORATION_PHASE) -------------------------------------------------
+// For the instances whose line search failed:  min rho sum(p + n) + 1/2 sum_i zeta D_R,i^2 (x_i - x_r,i)^2  s.t.
+// c(x) - p + n = 0, p, n >= 0 and the bounds — c the scaled constraints, x_r the iterate where the phase started
+// (K.x) — solved by the interior point itself with its own barrier mu_R, filter and line search.  With dp, dn and
+// the bound multipliers' steps eliminated its Newton system
+//   [[W_c + zeta D_R^2 + Sigma_x + dw, J^T], [J, -(p / zp + n / zn) - delta_c]] [dx; dy] = [r_x; r_c],
+//   dp = (dy + mu_R / p - rho + y) p / zp,   dn = (-dy + mu_R / n - rho - y) n / zn
+// has the original band structure (W_c: the Hessian of y^T c, eval_h with objective factor 0), so band assembly,
+// factorisation, curvature test and callbacks are the main loop's.  The phase iterate is xr (direction dxr), its bound
+// multipliers rzl / rzu; the main iteration's x, zl, zu, y stay untouched until it ends.  It ends when its point is
+// acceptable to the original filter (augmented with the starting point) with ||c||_1 <= required_infeasibility_
+// reduction times the value where it started (Ipopt RestoConvergenceCheck); the original bound multipliers then take
+// a Newton step for complementarity over the phase's whole dx (cut by the fraction to the boundary; all reset to 1
+// above Ipopt's bound_mult_reset_threshold 1000), the constraint multipliers restart from zero (Ipopt's
+// constr_mult_reset_threshold = 0 discards the least-squares estimate) and the filter from empty (k_ipm_update;
+// measured: cfg 5 from 16 perturbed starts converges 13 / 16 with a fresh filter, 9 / 16 keeping the augmented one).
+
+// p, n minimising rho (p + n) - mu (ln p + ln n) on c - p + n = 0 (Ipopt's closed form, evaluated without
+// cancellation)
+__device__ inline void rs_pn(double c, double mu, double rho, double& p, double& n) {
+    const double s = hypot(mu, rho * c);
+    n = c > 0 ? (mu + mu * mu / (s + rho * c)) / (2 * rho) : (mu - rho * c + s) / (2 * rho);
+    p = c < 0 ? (mu + mu * mu / (s - rho * c)) / (2 * rho) : (mu + rho * c + s) / (2 * rho);
+}
+
+// the phase's barrier objective at (x, p, n) with barrier mu: +inf outside the bounds or at p, n <= 0
+__device__ double rs_merit(const IpmK& K, int64_t b, const double* x, const double* p, const double* nn, double mu,
+                           double* sh) {
+    const int nf = K.nf, m = K.m;
+    double prox = 0.0, lin = 0.0, lg = 0.0, bad = 0.0;
+    for (int i = threadIdx.x; i < nf; i += kIB) {
+        const double xref = K.x[b * nf + i], e = x[i] - xref;
+        prox += rs_weight(mu, xref) * e * e;
+    }
+    for (int j = threadIdx.x; j < m; j += kIB) {
+        if (!(p[j] > 0) || !(nn[j] > 0)) bad = 1.0;
+        lin += p[j] + nn[j];
+        lg += log(clamp_lo(p[j], 1e-300)) + log(clamp_lo(nn[j], 1e-300));
+    }
+    {
+        double rv[4] = {prox, lin, lg, bad};
+        const int ro[4] = {0, 0, 0, 1};
+        breduce_n(rv, ro);
+        prox = rv[0];
+        lin = rv[1];
+        lg = rv[2];
+        bad = rv[3];
+    }
+    const double fx = barrier_obj(K, b, x, K.o.resto_penalty * lin + 0.5 * prox, mu, sh);
+    return bad > 0 ? INFINITY : fx - mu * lg;
+}
+
+// enter the phase (the instances whose line search failed; counter [0]: instances in the phase)
+__global__ void __launch_bounds__(kIB) k_rs_init(const IpmK K, int slot) {
+    __shared__ double sh[kIB / 64];
+    __shared__ Scal S;
+    const int64_t b = blockIdx.x;
+    const int nf = K.nf, m = K.m;
+    load_scal(K, b, S);
+    // per-instance budget: the phase's iterations count among the instance's (not the batch's main iterations)
+    const bool failed = !S.accepted && !S.done;
+    const bool go = failed && S.iters < K.o.max_iter;
+    if (failed && !go)  // out of iterations: it stays where it is
+        for (int i = threadIdx.x; i < nf; i += kIB) K.xr[b * nf + i] = K.x[b * nf + i];
+    if (go) {  // block-uniform
+        const double rho = K.o.resto_penalty;
+        const double* c = K.gS + b * m;
+        double cinf = 0.0;
+        for (int j = threadIdx.x; j < m; j += kIB) cinf = max_n(cinf, fabs(c[j]));
+        cinf = breduce(cinf, OpMax(), sh);
+        const double mu = max_n(S.mu, cinf);  // Ipopt: mu_R = max(mu, ||c||_inf)
+        for (int j = threadIdx.x; j < m; j += kIB) {
+            double p, n;
+            rs_pn(c[j], mu, rho, p, n);
+            K.rp[b * m + j] = p;
+            K.rn[b * m + j] = n;
+            K.rzp[b * m + j] = mu / p;
+            K.rzn[b * m + j] = mu / n;
+            K.ry[b * m + j] = 0.0;
+        }
+        for (int i = threadIdx.x; i < nf; i += kIB) {
+            K.xr[b * nf + i] = K.x[b * nf + i];
+            K.rzl[b * nf + i] = K.hasL[i] ? min_n(rho, K.zl[b * nf + i]) : 0.0;
+            K.rzu[b * nf + i] = K.hasU[i] ? min_n(rho, K.zu[b * nf + i]) : 0.0;
+        }
+        double* rf = K.rfilt + b * kFilt * 2;
+        for (int k = threadIdx.x; k < kFilt; k += kIB) {
+            rf[2 * k] = INFINITY;
+            rf[2 * k + 1] = -INFINITY;
+        }
+        if (threadIdx.x == 0) {  // the original filter takes the point where the phase starts
+            double* filt = K.filt + b * kFilt * 2;
+            const int k = S.fpos % kFilt;
+            filt[2 * k] = (1 - 1e-5) * S.theta;
+            filt[2 * k + 1] = S.phi - 1e-5 * S.theta;
+            S.fpos += 1;
+            S.rs_mu = mu;
+            S.rs_th0 = S.theta;
+            S.rs_dw = S.rs_dwl = 0.0;
+            S.rs_it = 0;
+        }
+        __syncthreads();
+        write_full(K, b, K.xr + b * nf, K.vt);
+    }
+    if (threadIdx.x == 0) {
+        S.rs_on = go;
+        S.rs_ok = 0;
+    }
+    store_scal(K, b, S);
+    count_add(K, slot, 0, go);
+}
+
+// after g, J_g at the phase iterate (vt): scaling, the phase's optimality error and barrier update, Sigma, the Newton
+// right-hand side, the eliminated (2,2) block and the multipliers of its constraint Hessian
+__global__ void __launch_bounds__(kIB) k_rs_begin(const IpmK K) {
+    __shared__ double sh[kIB / 64];
+    __shared__ Scal S;
+    const int64_t b = blockIdx.x;
+    const int nf = K.nf, m = K.m;
+    load_scal(K, b, S);
+    if (!S.rs_on) return;  // block-uniform
+    const double rho = K.o.resto_penalty;
+    const double* sg = K.sg + b * m;
+    double* gS = K.gS + b * m;
+    double* jv = K.jv + b * K.nj;
+    const double* jac = K.jac + b * K.nnzj;
+    for (int j = threadIdx.x; j < m; j += kIB) gS[j] = K.graw[b * m + j] * sg[j];
+    for (int q = threadIdx.x; q < K.nj; q += kIB) jv[q] = jac[K.jsel[q]] * K.d[K.jc[q]] * sg[K.jr[q]];
+    __syncthreads();
+    const double* x = K.xr + b * nf;
+    const double* xref = K.x + b * nf;
+    const double* zl = K.rzl + b * nf;
+    const double* zu = K.rzu + b * nf;
+    const double* lbI = K.lbI + b * nf;
+    const double* ubI = K.ubI + b * nf;
+    const double* p = K.rp + b * m;
+    const double* nn = K.rn + b * m;
+    const double* zp = K.rzp + b * m;
+    const double* zn = K.rzn + b * m;
+    const double* y = K.ry + b * m;
+    double* rhs = K.rhs + b * K.nK;
+    double ed = 0.0, ep = 0.0;
+    for (int i = threadIdx.x; i < nf; i += kIB) {
+        double jty = 0.0;
+        for (int k = K.jt_ptr[i]; k < K.jt_ptr[i + 1]; ++k) {
+            const int q = K.jt_idx[k];
+            jty += jv[q] * y[K.jr[q]];
+        }
+        rhs[i] = jty;  // completed below, once mu_R is final
+        ed = max_n(ed, fabs(rs_weight(S.rs_mu, xref[i]) * (x[i] - xref[i]) + jty - zl[i] + zu[i]));
+    }
+    for (int j = threadIdx.x; j < m; j += kIB) {
+        ep = max_n(ep, fabs(gS[j] - p[j] + nn[j]));
+        ed = max_n(ed, max_n(fabs(rho - y[j] - zp[j]), fabs(rho + y[j] - zn[j])));
+    }
+    {
+        double rv[2] = {ed, ep};
+        const int ro[2] = {1, 1};
+        breduce_n(rv, ro);
+        ed = rv[0];
+        ep = rv[1];
+    }
+    // the phase's monotone barrier update (the main loop's rule, on its unscaled errors)
+    double e_mu = INFINITY;
+    for (int pass = 0; pass < 5; ++pass) {
+        const double mu = S.rs_mu;
+        double ecm = 0.0;
+        for (int i = threadIdx.x; i < nf; i += kIB) {
+            if (K.hasL[i]) ecm = max_n(ecm, fabs((x[i] - lbI[i]) * zl[i] - mu));
+            if (K.hasU[i]) ecm = max_n(ecm, fabs((ubI[i] - x[i]) * zu[i] - mu));
+        }
+        for (int j = threadIdx.x; j < m; j += kIB)
+            ecm = max_n(ecm, max_n(fabs(p[j] * zp[j] - mu), fabs(nn[j] * zn[j] - mu)));
+        ecm = breduce(ecm, OpMax(), sh);
+        e_mu = max_n(max_n(ed, ep), ecm);
+        if (!((e_mu <= K.o.kappa_eps * mu) && (mu > K.o.tol / 10))) break;
+        __syncthreads();
+        if (threadIdx.x == 0) S.rs_mu = clamp_lo(min_n(K.o.kappa_mu * mu, pow(mu, K.o.theta_mu)), K.o.tol / 10);
+        __syncthreads();
+    }
+    const double mu = S.rs_mu;
+    // the phase has converged (barrier at its floor, its sub-problem solved) without reaching a point the original
+    // problem accepts: a local minimiser of the infeasibility (Ipopt: "converged to a point of local infeasibility")
+    if (mu <= K.o.tol / 10 && e_mu <= K.o.kappa_eps * mu) {
+        __syncthreads();
+        if (threadIdx.x == 0) S.rs_on = 0;
+        store_scal(K, b, S);
+        return;
+    }
+    double* sig = K.sig + b * nf;
+    for (int i = threadIdx.x; i < nf; i += kIB) {
+        const bool hL = K.hasL[i], hU = K.hasU[i];
+        const double sl = hL ? x[i] - lbI[i] : 1.0, su = hU ? ubI[i] - x[i] : 1.0;
+        sig[i] = (hL ? zl[i] / sl : 0.0) + (hU ? zu[i] / su : 0.0);
+        const double bar = (hL ? mu / sl : 0.0) - (hU ? mu / su : 0.0);
+        rhs[i] = -(rs_weight(mu, xref[i]) * (x[i] - xref[i]) + rhs[i] - bar);
+    }
+    for (int j = threadIdx.x; j < m; j += kIB) {
+        const double Sp = zp[j] / p[j], Sn = zn[j] / nn[j];
+        const double ap = mu / p[j] - rho + y[j], an = mu / nn[j] - rho - y[j];
+        rhs[nf + j] = -(gS[j] - p[j] + nn[j]) + ap / Sp - an / Sn;
+        K.rdc[b * m + j] = -(1.0 / Sp + 1.0 / Sn);
+        K.ysc[b * m + j] = y[j] * sg[j];
+    }
+    if (threadIdx.x == 0) {
+        S.rs_tau = clamp_lo(1.0 - mu, K.o.tau_min);
+        S.rs_dw = 0.0;
+    }
+    store_scal(K, b, S);
+}
+
+// the phase's step: dp, dn and the multiplier steps from (dx, dy), fraction to the boundary, filter quantities at
+// the phase iterate, first trial point
+__global__ void __launch_bounds__(kIB) k_rs_dir(const IpmK K) {
+    __shared__ double sh[kIB / 64];
+    __shared__ Scal S;
+    const int64_t b = blockIdx.x;
+    const int nf = K.nf, m = K.m;
+    load_scal(K, b, S);
+    if (!S.rs_on) return;  // block-uniform
+    const double rho = K.o.resto_penalty, mu = S.rs_mu, tau = S.rs_tau;
+    const double* x = K.xr + b * nf;
+    const double* xref = K.x + b * nf;
+    const double* dx = K.dxr + b * nf;
+    const double* zl = K.rzl + b * nf;
+    const double* zu = K.rzu + b * nf;
+    const double* lbI = K.lbI + b * nf;
+    const double* ubI = K.ubI + b * nf;
+    double* dzl = K.dzl + b * nf;
+    double* dzu = K.dzu + b * nf;
+    const double* p = K.rp + b * m;
+    const double* nn = K.rn + b * m;
+    const double* zp = K.rzp + b * m;
+    const double* zn = K.rzn + b * m;
+    const double* y = K.ry + b * m;
+    const double* dy = K.dy + b * m;
+    double apl = INFINITY, apu = INFINITY, azl = INFINITY, azu = INFINITY, dphi = 0.0, theta = 0.0;
+    for (int i = threadIdx.x; i < nf; i += kIB) {
+        const bool hL = K.hasL[i], hU = K.hasU[i];
+        const double sl = hL ? x[i] - lbI[i] : 1.0, su = hU ? ubI[i] - x[i] : 1.0;
+        const double vzl = hL ? mu / sl - zl[i] - zl[i] / sl * dx[i] : 0.0;
+        const double vzu = hU ? mu / su - zu[i] + zu[i] / su * dx[i] : 0.0;
+        dzl[i] = vzl;
+        dzu[i] = vzu;
+        apl = min_n(apl, step_term(hL, sl, dx[i], tau));
+        apu = min_n(apu, step_term(hU, su, -dx[i], tau));
+        azl = min_n(azl, step_term(hL, zl[i], vzl, tau));
+        azu = min_n(azu, step_term(hU, zu[i], vzu, tau));
+        const double bar = (hL ? mu / sl : 0.0) - (hU ? mu / su : 0.0);
+        dphi += (rs_weight(mu, xref[i]) * (x[i] - xref[i]) - bar) * dx[i];
+    }
+    for (int j = threadIdx.x; j < m; j += kIB) {
+        const double Sp = zp[j] / p[j], Sn = zn[j] / nn[j];
+        const double dpj = (dy[j] + mu / p[j] - rho + y[j]) / Sp;
+        const double dnj = (-dy[j] + mu / nn[j] - rho - y[j]) / Sn;
+        const double dzpj = mu / p[j] - zp[j] - Sp * dpj, dznj = mu / nn[j] - zn[j] - Sn * dnj;
+        K.rdp[b * m + j] = dpj;
+        K.rdn[b * m + j] = dnj;
+        K.rdzp[b * m + j] = dzpj;
+        K.rdzn[b * m + j] = dznj;
+        apl = min_n(apl, min_n(step_term(true, p[j], dpj, tau), step_term(true, nn[j], dnj, tau)));
+        azl = min_n(azl, min_n(step_term(true, zp[j], dzpj, tau), step_term(true, zn[j], dznj, tau)));
+        dphi += (rho - mu / p[j]) * dpj + (rho - mu / nn[j]) * dnj;
+        theta += fabs(K.gS[b * m + j] - p[j] + nn[j]);
+    }
+    {
+        double rv[6] = {apl, apu, azl, azu, dphi, theta};
+        const int ro[6] = {2, 2, 2, 2, 0, 0};
+        breduce_n(rv, ro);
+        apl = rv[0];
+        apu = rv[1];
+        azl = rv[2];
+        azu = rv[3];
+        dphi = rv[4];
+        theta = rv[5];
+    }
+    const double phi = rs_merit(K, b, x, p, nn, mu, sh);
+    const double a_p = min_n(clamp_hi(apl, 1.0), clamp_hi(apu, 1.0));
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        S.rs_dwl = S.rs_dw;
+        S.rs_theta = theta;
+        S.rs_phi = phi;
+        S.rs_dphi = dphi;
+        S.rs_ap = a_p;
+        S.rs_az = min_n(clamp_hi(azl, 1.0), clamp_hi(azu, 1.0));
+        S.rs_alpha = a_p;
+        S.rs_acc = 0;
+        S.rs_arm = 0;
+        if (S.rs_it == 0) {
+            S.rs_tmax = 1e4 * clamp_lo(theta, 1.0);
+            S.rs_tmin = 1e-4 * clamp_lo(theta, 1.0);
+        }
+    }
+    double* xt = K.xt + b * nf;
+    for (int i = threadIdx.x; i < nf; i += kIB) xt[i] = x[i] + a_p * dx[i];
+    for (int j = threadIdx.x; j < m; j += kIB) {
+        K.rpt[b * m + j] = p[j] + a_p * K.rdp[b * m + j];
+        K.rnt[b * m + j] = nn[j] + a_p * K.rdn[b * m + j];
+    }
+    __syncthreads();
+    write_full(K, b, xt, K.vt);
+    store_scal(K, b, S);
+}
+
+// after g (and f) at the phase's trial point: its own filter test.  counter [0]: phase instances not accepted
+__global__ void __launch_bounds__(kIB) k_rs_accept(const IpmK K, int slot) {
+    __shared__ double sh[kIB / 64];
+    __shared__ Scal S;
+    const int64_t b = blockIdx.x;
+    const int nf = K.nf, m = K.m;
+    load_scal(K, b, S);
+    if (S.rs_on && !S.rs_acc) {  // block-uniform
+        const double* sg = K.sg + b * m;
+        const double* gt = K.gt + b * m;
+        const double* pt = K.rpt + b * m;
+        const double* nt = K.rnt + b * m;
+        double tt = 0.0;
+        for (int j = threadIdx.x; j < m; j += kIB) tt += fabs(gt[j] * sg[j] - pt[j] + nt[j]);
+        tt = breduce(tt, OpSum(), sh);
+        const double ph = rs_merit(K, b, K.xt + b * nf, pt, nt, S.rs_mu, sh);
+        bool ok, arm;
+        filter_core(K, K.rfilt + b * kFilt * 2, S.rs_theta, S.rs_phi, S.rs_dphi, S.rs_tmax, S.rs_tmin, tt, ph,
+                    S.rs_alpha, sh, ok, arm);
+        __syncthreads();
+        if (threadIdx.x == 0 && ok) {
+            S.rs_acc = 1;
+            S.rs_arm = arm;
+        }
+    }
+    store_scal(K, b, S);
+    count_add(K, slot, 0, S.rs_on && !S.rs_acc);
+}
+
+// the phase's backtracking: halve its step where no trial was accepted
+__global__ void __launch_bounds__(kIB) k_rs_next_trial(const IpmK K) {
+    __shared__ Scal S;
+    const int64_t b = blockIdx.x;
+    const int nf = K.nf, m = K.m;
+    load_scal(K, b, S);
+    if (!S.rs_on || S.rs_acc) return;  // block-uniform
+    const double a = S.rs_alpha * 0.5;
+    const double* x = K.xr + b * nf;
+    const double* dx = K.dxr + b * nf;
+    double* xt = K.xt + b * nf;
+    for (int i = threadIdx.x; i < nf; i += kIB) xt[i] = x[i] + a * dx[i];
+    for (int j = threadIdx.x; j < m; j += kIB) {
+        K.rpt[b * m + j] = K.rp[b * m + j] + a * K.rdp[b * m + j];
+        K.rnt[b * m + j] = K.rn[b * m + j] + a * K.rdn[b * m + j];
+    }
+    __syncthreads();
+    write_full(K, b, xt, K.vt);
+    if (threadIdx.x == 0) K.sc[b].rs_alpha = a;
+}
+
+// end of a phase iteration: the step (primal-dual, z safeguard), the phase's filter, the exit test on the original
+// problem and, on exit, the original bound multipliers.  A failed line search of the phase ends it unsuccessfully at
+// its current point.  counter [0]: instances still in the phase
+__global__ void __launch_bounds__(kIB) k_rs_update(const IpmK K, int slot) {
+    __shared__ double sh[kIB / 64];
+    __shared__ Scal S;
+    const int64_t b = blockIdx.x;
+    const int nf = K.nf, m = K.m;
+    load_scal(K, b, S);
+    if (S.rs_on && !S.rs_acc) {  // block-uniform
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            S.rs_on = 0;
+            S.iters += 1;  // Ipopt counts the phase's iterations among the solve's
+        }
+    } else if (S.rs_on) {
+        const double a = S.rs_alpha, az = S.rs_az, mu = S.rs_mu;
+        if (threadIdx.x == 0 && !S.rs_arm) {
+            double* rf = K.rfilt + b * kFilt * 2;
+            const int k = S.rs_it % kFilt;
+            rf[2 * k] = (1 - 1e-5) * S.rs_theta;
+            rf[2 * k + 1] = S.rs_phi - 1e-5 * S.rs_theta;
+        }
+        double* x = K.xr + b * nf;
+        double* zl = K.rzl + b * nf;
+        double* zu = K.rzu + b * nf;
+        const double* lbI = K.lbI + b * nf;
+        const double* ubI = K.ubI + b * nf;
+        for (int i = threadIdx.x; i < nf; i += kIB) {
+            const double xi = K.xt[b * nf + i];
+            x[i] = xi;
+            if (K.hasL[i]) {
+                const double sl = xi - lbI[i];
+                zl[i] = clamp_hi(clamp_lo(zl[i] + az * K.dzl[b * nf + i], mu / (1e10 * sl)), 1e10 * mu / sl);
+            }
+            if (K.hasU[i]) {
+                const double su = ubI[i] - xi;
+                zu[i] = clamp_hi(clamp_lo(zu[i] + az * K.dzu[b * nf + i], mu / (1e10 * su)), 1e10 * mu / su);
+            }
+        }
+        for (int j = threadIdx.x; j < m; j += kIB) {
+            const int64_t e = b * m + j;
+            const double p = K.rpt[e], n = K.rnt[e];
+            K.rp[e] = p;
+            K.rn[e] = n;
+            K.ry[e] += a * K.dy[e];
+            K.rzp[e] = clamp_hi(clamp_lo(K.rzp[e] + az * K.rdzp[e], mu / (1e10 * p)), 1e10 * mu / p);
+            K.rzn[e] = clamp_hi(clamp_lo(K.rzn[e] + az * K.rdzn[e], mu / (1e10 * n)), 1e10 * mu / n);
+        }
+        __syncthreads();
+        // exit test on the original problem, from g, f of the accepted trial
+        const double* sg = K.sg + b * m;
+        double th = 0.0;
+        for (int j = threadIdx.x; j < m; j += kIB) th += fabs(K.gt[b * m + j] * sg[j]);
+        th = breduce(th, OpSum(), sh);
+        const double ph = barrier_obj(K, b, x, K.ft[b] * S.sf, S.mu, sh);
+        const bool ok = isfinite(th) && isfinite(ph) && th <= K.o.required_infeasibility_reduction * S.rs_th0 &&
+                        !filter_dominated(K.filt + b * kFilt * 2, th, ph, sh);
+        if (ok) {  // the original bound multipliers: Newton step for complementarity over the phase's dx
+            const double* x0 = K.x + b * nf;
+            double* zl0 = K.zl + b * nf;
+            double* zu0 = K.zu + b * nf;
+            const double mu0 = S.mu, tau0 = S.tau;
+            double al = INFINITY;
+            for (int i = threadIdx.x; i < nf; i += kIB) {
+                const bool hL = K.hasL[i], hU = K.hasU[i];
+                const double sl = hL ? x0[i] - lbI[i] : 1.0, su = hU ? ubI[i] - x0[i] : 1.0, d = x[i] - x0[i];
+                const double vzl = hL ? mu0 / sl - zl0[i] - zl0[i] / sl * d : 0.0;
+                const double vzu = hU ? mu0 / su - zu0[i] + zu0[i] / su * d : 0.0;
+                al = min_n(al, min_n(step_term(hL, zl0[i], vzl, tau0), step_term(hU, zu0[i], vzu, tau0)));
+            }
+            al = clamp_hi(breduce(al, OpMin(), sh), 1.0);
+            double zmax = 0.0;
+            for (int i = threadIdx.x; i < nf; i += kIB) {
+                const bool hL = K.hasL[i], hU = K.hasU[i];
+                const double sl = hL ? x0[i] - lbI[i] : 1.0, su = hU ? ubI[i] - x0[i] : 1.0, d = x[i] - x0[i];
+                if (hL) zl0[i] += al * (mu0 / sl - zl0[i] - zl0[i] / sl * d);
+                if (hU) zu0[i] += al * (mu0 / su - zu0[i] + zu0[i] / su * d);
+                zmax = max_n(zmax, max_n(zl0[i], zu0[i]));
+            }
+            zmax = breduce(zmax, OpMax(), sh);
+            if (zmax > 1e3)
+                for (int i = threadIdx.x; i < nf; i += kIB) {
+                    zl0[i] = K.hasL[i] ? 1.0 : 0.0;
+                    zu0[i] = K.hasU[i] ? 1.0 : 0.0;
+                }
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            S.rs_it += 1;
+            S.iters += 1;
+            if (ok) {
+                S.rs_on = 0;
+                S.rs_ok = 1;
+            } else if (S.iters >= K.o.max_iter) {
+                S.rs_on = 0;
+            }
+        }
+    }
+    store_scal(K, b, S);
+    count_add(K, slot, 0, S.rs_on);
+}
+
+// the phase's iteration limit: the instances still in it leave it, unsuccessfully, at its current point
+__global__ void __launch_bounds__(kIB) k_rs_finish(const IpmK K) {
+    if (threadIdx.x == 0) K.sc[blockIdx.x].rs_on = 0;
 }
 
 // project onto the original bounds (Ipopt honor_original_bounds) and write the final point into vx
@@ -1173,7 +1689,7 @@ __global__ void __launch_bounds__(kIB) k_ipm_out(const IpmK K, double* __restric
     if (yo)
         for (int j = threadIdx.x; j < K.m; j += kIB) yo[b * K.m + j] = K.y[b * K.m + j] * K.sg[b * K.m + j] / S.sf;
     if (threadIdx.x == 0) {
-        if (conv) conv[b] = S.done;
+        if (conv) conv[b] = S.done && !S.stop;
         if (its) its[b] = S.iters;
         if (kkt) kkt[b] = S.err0;
     }
@@ -1512,6 +2028,10 @@ extern "C" void cfx_ipm_default_options(cfx_ipm_options* o) {
     o->watchdog_trial_iter_max = 3;
     o->hessian_approximation = CFX_HESSIAN_EXACT;
     o->limited_memory_max_history = 6;
+    o->restoration = CFX_RESTORATION_PHASE;
+    o->max_resto_iter = 200;
+    o->resto_penalty = 1000.0;
+    o->required_infeasibility_reduction = 0.9;
 }
 
 // CSR of `key` (values in [0, nkeys)) with the sources of each key in increasing source order
@@ -1561,7 +2081,9 @@ extern "C" int cfx_ipm_create(cfx_handle* h, const double* lb, const double* ub,
         (K.o.hessian_approximation != CFX_HESSIAN_EXACT && K.o.hessian_approximation != CFX_HESSIAN_LIMITED_MEMORY) ||
         (K.o.hessian_approximation == CFX_HESSIAN_LIMITED_MEMORY &&
          (K.o.limited_memory_max_history < 1 || K.o.limited_memory_max_history > 16)) ||
-        s->B > 0x7fffffff) {
+        (K.o.restoration != CFX_RESTORATION_STEP && K.o.restoration != CFX_RESTORATION_PHASE) ||
+        K.o.max_resto_iter < 0 || !(K.o.resto_penalty > 0) || !(K.o.required_infeasibility_reduction > 0) ||
+        !(K.o.required_infeasibility_reduction < 1) || s->B > 0x7fffffff) {
         s->err = "cfx_ipm_create: the handle must use CFX_LAYOUT_AOS (or batch 1) and the options must be valid";
         return create_fail(s, CFX_EINVAL);
     }
@@ -1650,7 +2172,7 @@ extern "C" int cfx_ipm_create(cfx_handle* h, const double* lb, const double* ub,
     for (int s2 = 0; s2 < nj; ++s2) er.push_back(nf + jrF[s2]), ec.push_back(jcF[s2]), src.push_back((SRC_JV << kSrcShift) | s2);
     for (int s2 = 0; s2 < nj; ++s2) er.push_back(jcF[s2]), ec.push_back(nf + jrF[s2]), src.push_back((SRC_JV << kSrcShift) | s2);
     for (int i = 0; i < nf; ++i) er.push_back(i), ec.push_back(i), src.push_back((SRC_DIAG << kSrcShift) | i);
-    for (int j = 0; j < m; ++j) er.push_back(nf + j), ec.push_back(nf + j), src.push_back(SRC_DC << kSrcShift);
+    for (int j = 0; j < m; ++j) er.push_back(nf + j), ec.push_back(nf + j), src.push_back((SRC_DC << kSrcShift) | j);
     // one ordering: border = true places the free parameters last (keys of the rows computed without them)
     struct Order {
         std::vector<int32_t> pos;
@@ -1867,7 +2389,7 @@ extern "C" int cfx_ipm_create(cfx_handle* h, const double* lb, const double* ub,
         if (!used[sl]) {
             const int64_t q = sl / nA, l = sl - q * nA;
             flat.push_back(q * nA * ldab + l * ldab + kl + ku);
-            src.push_back((SRC_DC << kSrcShift) | 1);
+            src.push_back((SRC_DC << kSrcShift) | kSrcMask);
         }
     std::vector<int32_t> kptr, kidx, kcode;
     csr(flat, NE, kptr, kidx);
@@ -1962,6 +2484,15 @@ extern "C" int cfx_ipm_create(cfx_handle* h, const double* lb, const double* ub,
         K.Cl = dalloc<double>(s, B * H2 * H2, &rc);
         K.Cp = dalloc<int32_t>(s, B * H2, &rc);
         K.Zb = dalloc<double>(s, H2 * B * nKp, &rc);
+    }
+    K.rsphase = K.o.restoration == CFX_RESTORATION_PHASE && m > 0;
+    if (K.rsphase) {
+        double** rbufs[] = {&K.rp, &K.rdp, &K.rn, &K.rdn, &K.rzp, &K.rdzp, &K.rzn, &K.rdzn, &K.rpt, &K.rnt, &K.ry, &K.rdc};
+        for (double** p : rbufs) *p = dalloc<double>(s, B * m, &rc);
+        K.rzl = dalloc<double>(s, B * nf, &rc);
+        K.rzu = dalloc<double>(s, B * nf, &rc);
+        K.rfilt = dalloc<double>(s, B * kFilt * 2, &rc);
+        K.ofz = dalloc<double>(s, B, &rc);
     }
     K.cnt = dalloc<int32_t>(s, 4 * kSlots, &rc);
     s->d_fv = dalloc<double>(s, B * K.nfix, &rc);
@@ -2077,6 +2608,55 @@ struct Run {
         }
         return CFX_OK;
     }
+    // Ipopt's restoration phase for the instances whose line search failed (k_rs_*): its iterations run the whole
+    // batch's callbacks and factorisations, the kernels act on the instances in the phase only
+    int resto_phase() {
+        IpmK& K = s->K;
+        const dim3 blk(kIB);
+        int32_t c[4];
+        int sl = next_slot();
+        hipLaunchKernelGGL(k_rs_init, g, blk, 0, st, K, sl);
+        IPM_HIP(s, hipGetLastError());
+        IPM_RUN(read(sl, c));
+        s->st.resto_phases++;
+        for (int r = 0; r < K.o.max_resto_iter && c[0] > 0; ++r) {
+            IPM_RUN(eval_full(K.vt));
+            hipLaunchKernelGGL(k_rs_begin, g, blk, 0, st, K);
+            IPM_HIP(s, hipGetLastError());
+            if (!K.lbfgs) {  // W of the phase: the Hessian of y^T c (objective factor 0); L-BFGS runs it without W
+                cfx_internal_msk_stash(s->h, 2);  // vt is the point of eval_full above
+                IPM_CFX(s, cfx_eval_h(s->h, K.vt, K.ofz, K.ysc, K.hv, CFX_DEVICE));
+                s->st.eval_h++;
+            }
+            for (int attempt = 0; attempt < 12; ++attempt) {
+                IPM_RUN(kkt_factor(KKT_RSNLP));
+                sl = next_slot();
+                hipLaunchKernelGGL(k_ipm_curv, g, blk, 0, st, K, sl, 1);
+                IPM_HIP(s, hipGetLastError());
+                IPM_RUN(read(sl, c));
+                if (c[0] == 0 || c[1] == 0) break;
+            }
+            hipLaunchKernelGGL(k_rs_dir, g, blk, 0, st, K);
+            IPM_HIP(s, hipGetLastError());
+            for (int ls = 0; ls < K.o.max_backtrack; ++ls) {
+                IPM_RUN(eval_gf(true));
+                sl = next_slot();
+                hipLaunchKernelGGL(k_rs_accept, g, blk, 0, st, K, sl);
+                IPM_HIP(s, hipGetLastError());
+                IPM_RUN(read(sl, c));
+                if (c[0] == 0) break;
+                hipLaunchKernelGGL(k_rs_next_trial, g, blk, 0, st, K);
+            }
+            sl = next_slot();
+            hipLaunchKernelGGL(k_rs_update, g, blk, 0, st, K, sl);
+            IPM_HIP(s, hipGetLastError());
+            IPM_RUN(read(sl, c));
+            s->st.resto_iterations++;
+        }
+        hipLaunchKernelGGL(k_rs_finish, g, blk, 0, st, K);
+        IPM_HIP(s, hipGetLastError());
+        return CFX_OK;
+    }
     // L-BFGS: after a Newton factorisation of K0, P = K0^-1 Z column by column, C = M - Z^T P, and the Newton
     // solution corrected (rb += P C^-1 Z^T rb)
     int lbfgs_newton() {
@@ -2118,6 +2698,11 @@ static int ipm_solve(cfx_ipm* s, const double* v0, const double* fixed_values, d
     Run R{s, st, dim3((unsigned)B)};
     const dim3 blk(kIB);
     s->st.eval_all = s->st.eval_g_f = s->st.eval_h = s->st.kkt_factor = s->st.iterations = s->st.host_syncs = 0;
+    s->st.resto_phases = s->st.resto_iterations = 0;
+    if (K.rsphase) {  // zero objective factor of the phase's Hessian; the (2,2) block of instances outside it
+        IPM_HIP(s, hipMemsetAsync(K.ofz, 0, B * sizeof(double), st));
+        IPM_HIP(s, hipMemsetAsync(K.rdc, 0, B * K.m * sizeof(double), st));
+    }
     s->slot = 0;
     IPM_HIP(s, hipMemsetAsync(K.cnt, 0, 4 * kSlots * sizeof(int32_t), st));
     IPM_HIP(s, hipMemsetAsync(K.rb, 0, B * K.nKp * sizeof(double), st));  // padding rows of the blocks stay 0
@@ -2167,7 +2752,7 @@ static int ipm_solve(cfx_ipm* s, const double* v0, const double* fixed_values, d
             IPM_RUN(R.kkt_factor(KKT_NEWTON));
             if (K.lbfgs) IPM_RUN(R.lbfgs_newton());
             const int sl = R.next_slot();
-            hipLaunchKernelGGL(k_ipm_curv, R.g, blk, 0, st, K, sl);
+            hipLaunchKernelGGL(k_ipm_curv, R.g, blk, 0, st, K, sl, 0);
             IPM_HIP(s, hipGetLastError());
             IPM_RUN(R.read(sl, c));
             if (c[0] == 0) {
@@ -2205,7 +2790,9 @@ static int ipm_solve(cfx_ipm* s, const double* v0, const double* fixed_values, d
         }
         // failed line searches: a feasibility-restoration step, a fresh filter and least-squares multipliers
         const bool resto = notacc > 0 && K.m > 0;
-        if (resto) {
+        if (resto && K.rsphase) {
+            IPM_RUN(R.resto_phase());
+        } else if (resto) {
             IPM_RUN(R.kkt_factor(KKT_RESTO));
             int sl = R.next_slot();
             hipLaunchKernelGGL(k_ipm_resto_init, R.g, blk, 0, st, K, sl);
@@ -2219,7 +2806,7 @@ static int ipm_solve(cfx_ipm* s, const double* v0, const double* fixed_values, d
             }
             reinit = true;
         }
-        hipLaunchKernelGGL(k_ipm_update, R.g, blk, 0, st, K, (int)resto);
+        hipLaunchKernelGGL(k_ipm_update, R.g, blk, 0, st, K, resto ? (K.rsphase ? 2 : 1) : 0);
         IPM_HIP(s, hipGetLastError());
         s->st.iterations++;
     }

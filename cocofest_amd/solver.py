@@ -57,6 +57,13 @@ class IpmOptions:
     # limited_memory_max_history pairs, Ipopt's defaults)
     hessian_approximation: str = "exact"
     limited_memory_max_history: int = 6
+    # what a failed line search starts: "phase" — Ipopt's feasibility-restoration phase (an NLP over the constraint
+    # violation, cfx_ipm only), "step" — one minimum-norm step on g = 0 (this class's algorithm); None: each solver's
+    # own (NativeIpm "phase", BatchedIpm "step")
+    restoration: str | None = None
+    max_resto_iter: int = 200
+    resto_penalty: float = 1000.0            # Ipopt resto_penalty_parameter (rho)
+    required_infeasibility_reduction: float = 0.9
     verbose: bool = False
 
 
@@ -73,7 +80,9 @@ class Solver:
                     "_hessian_approximation": "hessian_approximation",
                     "_limited_memory_max_history": "limited_memory_max_history", "_max_soc": "max_soc",
                     "_watchdog_shortened_iter_trigger": "watchdog_shortened_iter_trigger",
-                    "_watchdog_trial_iter_max": "watchdog_trial_iter_max"}
+                    "_watchdog_trial_iter_max": "watchdog_trial_iter_max", "_max_resto_iter": "max_resto_iter",
+                    "_resto_penalty_parameter": "resto_penalty",
+                    "_required_infeasibility_reduction": "required_infeasibility_reduction"}
         _IGNORED = {"show_online_optim", "show_options", "_print_level", "_linear_solver", "_nlp_scaling_method",
                     "_check_derivatives_for_naninf", "_c_compile", "_print_timing_statistics", "_output_file",
                     "_constr_viol_tol", "_dual_inf_tol", "_compl_inf_tol"}
@@ -192,6 +201,9 @@ class BatchedIpm:
         self.ocp = ocp
         self.B = batch
         self.opt = options or IpmOptions()
+        if self.opt.restoration not in (None, "step", "phase"):
+            raise ValueError("restoration must be 'phase' or 'step'")
+        self._phase = self.opt.restoration == "phase"  # BatchedIpm's own default is the restoration step
         if self.opt.hessian_approximation != "exact":
             raise ValueError("BatchedIpm: hessian_approximation='limited-memory' is implemented by the native interior "
                              "point (NativeIpm / cfx_ipm) only")
@@ -304,9 +316,10 @@ class BatchedIpm:
         g, f = self._eval_gf(v)
         return g * self.sg, f * self.sf
 
-    def _scaled_hess(self, v, y):
-        """Lagrangian Hessian values over the free variables (triplets hrF >= hcF) of the scaled problem."""
-        hv = self._eval_h(v, y * self.sg, self.sf)
+    def _scaled_hess(self, v, y, of=None):
+        """Lagrangian Hessian values over the free variables (triplets hrF >= hcF) of the scaled problem (objective
+        factor ``of``, default the objective scaling)."""
+        hv = self._eval_h(v, y * self.sg, self.sf if of is None else of)
         return hv[:, self.hselT] * self.d[self.hrF] * self.d[self.hcF]
 
     def _jt_mul(self, jv, y):
@@ -338,12 +351,14 @@ class BatchedIpm:
                              jv * dx[:, self.jcF])
         return torch.cat([top, jd - self.opt.delta_c * dy], dim=1)
 
-    def _kkt_band(self, hv, diag_x, jv):
-        """Band storage (B, nK, ldab) of [[W + diag_x, J^T], [J, -delta_c I]] in the stage-wise order."""
+    def _kkt_band(self, hv, diag_x, jv, diag_y=None):
+        """Band storage (B, nK, ldab) of [[W + diag_x, J^T], [J, -delta_c I + diag_y]] in the stage-wise order."""
         torch = self.torch
         ab = torch.zeros((self.B, self.nK * self.ldab), dtype=torch.float64, device=self.dev)
         self.seg_kkt.add_(ab, torch.cat([hv, hv[:, self.hoff], jv, jv, diag_x], dim=1))
         ab[:, self.idx_dy] -= self.opt.delta_c
+        if diag_y is not None:
+            ab[:, self.idx_dy] += diag_y
         self.calls["kkt_factor"] += 1
         return ab.view(self.B, self.nK, self.ldab)
 
@@ -413,6 +428,7 @@ class BatchedIpm:
                                                                                           device=self.dev)
         delta_w_last = torch.zeros((B,), dtype=torch.float64, device=self.dev)
         done = torch.zeros((B,), dtype=torch.bool, device=self.dev)
+        stopped = torch.zeros((B,), dtype=torch.bool, device=self.dev)
         iters = torch.zeros((B,), dtype=torch.int64, device=self.dev)
         acc_count = torch.zeros((B,), dtype=torch.int64, device=self.dev)
         err0 = torch.full((B,), np.inf, dtype=torch.float64, device=self.dev)
@@ -431,7 +447,9 @@ class BatchedIpm:
         def full(xf):  # scaled free variables -> full decision vector
             return self._full(xf)
 
-        for it in range(opt.max_iter):
+        it = -1
+        while it + 1 < opt.max_iter:
+            it += 1
             vfull = full(x)
             g, jv, f, gF = self._scaled_all(vfull)
             sl = torch.where(hasL, x - lbF, torch.ones_like(x))
@@ -454,6 +472,10 @@ class BatchedIpm:
             acc_count = torch.where(err0 <= opt.acceptable_tol, acc_count + 1, torch.zeros_like(acc_count))
             newly = (~done) & ((err0 <= opt.tol) | (acc_count >= opt.acceptable_iter))
             done = done | newly
+            # an instance whose iterations (restoration-phase ones included) reach max_iter stops, unconverged
+            out_of_iters = (~done) & (iters >= opt.max_iter)
+            stopped = stopped | out_of_iters
+            done = done | out_of_iters
             if bool(done.all()):
                 break
             # barrier update (monotone): while the barrier sub-problem is solved, decrease mu
@@ -592,7 +614,20 @@ class BatchedIpm:
             # Sigma + I, backtracking on ||g||_1 only), then a fresh filter and least-squares multipliers
             x_new = x_acc
             failed = failed & ~done
-            if bool(failed.any()) and m:
+            if bool(failed.any()) and m and self._phase:
+                # Ipopt's restoration phase; its iterations count among the solve's
+                xr, zl, zu, filt, fpos, its_r = self._restoration_phase(failed, x, zl, zu, g, theta, phi, mu, tau,
+                                                                         filt, fpos, iters)
+                x_new = torch.where(failed[:, None], xr, x_acc)
+                iters = iters + its_r
+                # after the phase: zero constraint multipliers (Ipopt's constr_mult_reset_threshold = 0 ignores the
+                # least-squares estimate) and a fresh filter (measured: cfg 5 from 16 perturbed starts converges
+                # 13 / 16 with it against 9 / 16 keeping the augmented filter, scripts/r3/resto_variants.py)
+                y = torch.where(failed[:, None], torch.zeros_like(y), y)
+                filt = torch.where(failed[:, None, None], torch.tensor([np.inf, -np.inf], dtype=torch.float64,
+                                                                       device=self.dev), filt)
+                alpha = torch.where(failed, torch.zeros_like(alpha), alpha)
+            elif bool(failed.any()) and m:
                 xr = self._restoration_step(x, g, jv, sig, tau)
                 x_new = torch.where(failed[:, None], xr, x_acc)
                 filt = torch.where(failed[:, None, None], torch.tensor([np.inf, -np.inf], dtype=torch.float64,
@@ -633,7 +668,8 @@ class BatchedIpm:
         y = y * self.sg / self.sf[:, None]  # multipliers of the unscaled problem
         if self.dev.type == "cuda":
             torch.cuda.synchronize()
-        return IpmResult(v=vfinal.cpu().numpy(), y=y.cpu().numpy(), f=f.cpu().numpy(), converged=done.cpu().numpy(),
+        return IpmResult(v=vfinal.cpu().numpy(), y=y.cpu().numpy(), f=f.cpu().numpy(),
+                         converged=(done & ~stopped).cpu().numpy(),
                          iterations=iters.cpu().numpy(), kkt_error=err0.cpu().numpy(),
                          wall_time=time.perf_counter() - t0, n_callbacks=dict(self.calls))
 
@@ -678,6 +714,200 @@ class BatchedIpm:
                 break
             a = a * 0.5
         return out
+
+    def _restoration_phase(self, on, x, zl, zu, g, theta, phi, mu, tau, filt, fpos, iters):
+        """Ipopt's feasibility-restoration phase for the instances ``on`` (their line search failed):
+        min rho sum(p + n) + 1/2 sum_i zeta D_i^2 (x_i - x_r,i)^2 s.t. c(x) - p + n = 0, p, n >= 0 and the bounds
+        (c the scaled constraints, x_r = x, zeta = sqrt(mu_R), D_i = min(1, 1 / |x_r,i|)), by this interior point
+        with its own barrier mu_R, filter and line search; p, n and the bound multipliers' steps are eliminated, so
+        the Newton system is the original band KKT with W = Hessian of y^T c + zeta D^2 and the (2,2) block
+        -(p / zp + n / zn).  It ends when a point is acceptable to the original filter (augmented with x) with
+        ||c||_1 <= required_infeasibility_reduction * theta, when its own sub-problem has converged (a local
+        minimiser of the infeasibility), after a failed line search of its own, after max_resto_iter iterations, or
+        when the instance's iterations (``iters`` + the phase's) reach max_iter — the budget is per instance: one
+        instance's phase does not use up the batch's main iterations.  On success the original bound multipliers take a Newton step for complementarity over the
+        phase's dx (fraction to the boundary; reset to 1 above 1e3); the caller then restarts the constraint
+        multipliers from zero and the filter from empty.  The executable specification of
+        csrc/cfx_ipm.hip's k_rs_* kernels.  Returns (x_r, zl, zu, filt, fpos, iterations per instance)."""
+        torch = self.torch
+        opt = self.opt
+        B, nf, m = self.B, len(self.free), self.m
+        hasL, hasU = self.hasL, self.hasU
+        lbI, ubI = self._lbI, self._ubI
+        rho = opt.resto_penalty
+        zeros_x = torch.zeros_like(x)
+        on = on & (iters < opt.max_iter)
+        # the original filter takes the point where the phase starts
+        slot = (torch.arange(filt.shape[1], device=self.dev) == (fpos % filt.shape[1])[:, None])[:, :, None]
+        filt = torch.where(on[:, None, None] & slot,
+                           torch.stack([(1 - 1e-5) * theta, phi - 1e-5 * theta], dim=1)[:, None, :], filt)
+        fpos = fpos + on.long()
+        th0 = theta
+        c = g
+        muR = torch.maximum(mu, c.abs().amax(1))
+        sR = torch.hypot(muR[:, None], rho * c)
+        mR = muR[:, None]
+        n = torch.where(c > 0, (mR + mR * mR / (sR + rho * c)) / (2 * rho), (mR - rho * c + sR) / (2 * rho))
+        p = torch.where(c < 0, (mR + mR * mR / (sR - rho * c)) / (2 * rho), (mR + rho * c + sR) / (2 * rho))
+        zp, zn = mR / p, mR / n
+        yR = torch.zeros_like(c)
+        xR = x.clone()
+        xref = x
+        rzl = torch.where(hasL, torch.clamp(zl, max=rho), zeros_x)
+        rzu = torch.where(hasU, torch.clamp(zu, max=rho), zeros_x)
+        rfilt = torch.full((B, filt.shape[1], 2), np.inf, dtype=torch.float64, device=self.dev)
+        rfilt[:, :, 1] = -np.inf
+        its = torch.zeros((B,), dtype=torch.int64, device=self.dev)
+        dwl = torch.zeros((B,), dtype=torch.float64, device=self.dev)
+        tmax = tmin = None
+        dref = torch.clamp(xref.abs(), min=1.0) ** 2
+        of0 = torch.zeros((B,), dtype=torch.float64, device=self.dev)
+
+        def merit(xx, pp, nn, mu_):
+            w = mu_.sqrt()[:, None] / dref
+            prox = (w * (xx - xref) ** 2).sum(1)
+            bad = ((pp <= 0) | (nn <= 0)).any(1)
+            lg = (torch.log(torch.clamp(pp, min=1e-300)) + torch.log(torch.clamp(nn, min=1e-300))).sum(1)
+            fx = self._barrier_obj(rho * (pp + nn).sum(1) + 0.5 * prox, xx, mu_)
+            return torch.where(bad, torch.full_like(fx, np.inf), fx - mu_ * lg)
+
+        for r in range(opt.max_resto_iter):
+            if not bool(on.any()):
+                break
+            vfull = self._full(xR)
+            gS, jv, _, _ = self._scaled_all(vfull)
+            sl = torch.where(hasL, xR - lbI, torch.ones_like(xR))
+            su = torch.where(hasU, ubI - xR, torch.ones_like(xR))
+            jty = self._jt_mul(jv, yR)
+            w = muR.sqrt()[:, None] / dref
+            ed = torch.maximum((w * (xR - xref) + jty - rzl + rzu).abs().amax(1),
+                               torch.maximum((rho - yR - zp).abs().amax(1), (rho + yR - zn).abs().amax(1)))
+            ep = (gS - p + n).abs().amax(1)
+            # the phase's monotone barrier update
+            looping = on.clone()
+            e_last = torch.full_like(muR, np.inf)
+            for _ in range(5):
+                mR = muR[:, None]
+                ecm = torch.maximum(
+                    torch.maximum(torch.where(hasL, (sl * rzl - mR).abs(), zeros_x).amax(1),
+                                  torch.where(hasU, (su * rzu - mR).abs(), zeros_x).amax(1)),
+                    torch.maximum((p * zp - mR).abs().amax(1), (n * zn - mR).abs().amax(1)))
+                e_mu = torch.maximum(torch.maximum(ed, ep), ecm)
+                e_last = torch.where(looping, e_mu, e_last)
+                dec = looping & (e_mu <= opt.kappa_eps * muR) & (muR > opt.tol / 10)
+                looping = dec
+                if not bool(dec.any()):
+                    break
+                muR = torch.where(dec, torch.clamp(torch.minimum(opt.kappa_mu * muR, muR ** opt.theta_mu),
+                                                   min=opt.tol / 10), muR)
+            # its sub-problem solved without a point the original problem accepts: local infeasibility
+            on = on & ~((muR <= opt.tol / 10) & (e_last <= opt.kappa_eps * muR))
+            if not bool(on.any()):
+                break
+            mR = muR[:, None]
+            tauR = torch.clamp(1.0 - muR, min=opt.tau_min)
+            w = muR.sqrt()[:, None] / dref
+            sig = torch.where(hasL, rzl / sl, zeros_x) + torch.where(hasU, rzu / su, zeros_x)
+            bar = torch.where(hasL, mR / sl, zeros_x) - torch.where(hasU, mR / su, zeros_x)
+            Sp, Sn = zp / p, zn / n
+            ap, an = mR / p - rho + yR, mR / n - rho - yR
+            rhs = torch.cat([-(w * (xR - xref) + jty - bar), -(gS - p + n) + ap / Sp - an / Sn], dim=1)
+            dc = -(1.0 / Sp + 1.0 / Sn)
+            W = self._scaled_hess(vfull, yR, of0)
+            dw = torch.zeros((B,), dtype=torch.float64, device=self.dev)
+            for _ in range(12):
+                dxx = sig + dw[:, None] + w
+                K = self.band.factor(self._kkt_band(W, dxx, jv, dc), self.kl, self.ku)
+                sol = self._kkt_solve(K, rhs)
+                dx, dy = sol[:, :nf], sol[:, nf:]
+                curv = self._quad_w(W, dx) + (dxx * dx * dx).sum(1)
+                bad = on & ((curv <= opt.curv_min * (dx * dx).sum(1)) | ~torch.isfinite(curv) |
+                            self.band.singular(K) | ~torch.isfinite(sol).all(1))
+                if not bool(bad.any()):
+                    break
+                first = dw == 0
+                dw = torch.where(bad, torch.where(first, torch.where(dwl > 0, torch.clamp(dwl / 3, min=1e-20),
+                                                                     torch.full_like(dw, 1e-4)), dw * 8), dw)
+            dwl = dw
+            dp, dn = (dy + ap) / Sp, (-dy + an) / Sn
+            dzp, dzn = mR / p - zp - Sp * dp, mR / n - zn - Sn * dn
+            dzl = torch.where(hasL, mR / sl - rzl - rzl / sl * dx, zeros_x)
+            dzu = torch.where(hasU, mR / su - rzu + rzu / su * dx, zeros_x)
+            all_m = torch.ones_like(p, dtype=torch.bool)
+            a_p = torch.minimum(torch.minimum(self._max_step(sl, dx, hasL, tauR), self._max_step(su, -dx, hasU, tauR)),
+                                torch.minimum(self._max_step(p, dp, all_m, tauR), self._max_step(n, dn, all_m, tauR)))
+            a_z = torch.minimum(torch.minimum(self._max_step(rzl, dzl, hasL, tauR), self._max_step(rzu, dzu, hasU, tauR)),
+                                torch.minimum(self._max_step(zp, dzp, all_m, tauR), self._max_step(zn, dzn, all_m, tauR)))
+            thR = (gS - p + n).abs().sum(1)
+            phR = merit(xR, p, n, muR)
+            dphR = ((w * (xR - xref) - bar) * dx).sum(1) + ((rho - mR / p) * dp + (rho - mR / n) * dn).sum(1)
+            if tmax is None:
+                tmax, tmin = 1e4 * torch.clamp(thR, min=1.0), 1e-4 * torch.clamp(thR, min=1.0)
+            alpha = a_p.clone()
+            acc = torch.zeros_like(on)
+            arm_acc = torch.zeros_like(on)
+            x_a, p_a, n_a = xR.clone(), p.clone(), n.clone()
+            g_a = torch.zeros_like(gS)
+            f_a = torch.zeros_like(muR)
+            for _ in range(opt.max_backtrack):
+                xt = xR + alpha[:, None] * dx
+                pt, nt = p + alpha[:, None] * dp, n + alpha[:, None] * dn
+                gt, ft = self._scaled_gf(self._full(xt))
+                ok, arm = self._filter_core((gt - pt + nt).abs().sum(1), merit(xt, pt, nt, muR), thR, phR, dphR, alpha,
+                                            tmax, tmin, rfilt)
+                ok = ok & on & ~acc
+                c1 = ok[:, None]
+                x_a, p_a, n_a = torch.where(c1, xt, x_a), torch.where(c1, pt, p_a), torch.where(c1, nt, n_a)
+                g_a, f_a = torch.where(c1, gt, g_a), torch.where(ok, ft, f_a)
+                arm_acc = torch.where(ok, arm, arm_acc)
+                acc = acc | ok
+                if not bool((on & ~acc).any()):
+                    break
+                alpha = torch.where(acc, alpha, alpha * 0.5)
+            its = its + on.long()
+            on = on & acc  # a failed line search of the phase ends it where it is
+            grow = on & ~arm_acc
+            rslot = (torch.arange(rfilt.shape[1], device=self.dev) == (r % rfilt.shape[1]))[None, :, None]
+            rfilt = torch.where(grow[:, None, None] & rslot,
+                                torch.stack([(1 - 1e-5) * thR, phR - 1e-5 * thR], dim=1)[:, None, :], rfilt)
+            c1 = on[:, None]
+            xR = torch.where(c1, x_a, xR)
+            slN = torch.where(hasL, xR - lbI, torch.ones_like(xR))
+            suN = torch.where(hasU, ubI - xR, torch.ones_like(xR))
+            azc = a_z[:, None]
+            rzl = torch.where(c1 & hasL, torch.clamp(rzl + azc * dzl, min=mR / (1e10 * slN), max=1e10 * mR / slN), rzl)
+            rzu = torch.where(c1 & hasU, torch.clamp(rzu + azc * dzu, min=mR / (1e10 * suN), max=1e10 * mR / suN), rzu)
+            p, n = torch.where(c1, p_a, p), torch.where(c1, n_a, n)
+            yR = torch.where(c1, yR + alpha[:, None] * dy, yR)
+            zp = torch.where(c1, torch.clamp(zp + azc * dzp, min=mR / (1e10 * p), max=1e10 * mR / p), zp)
+            zn = torch.where(c1, torch.clamp(zn + azc * dzn, min=mR / (1e10 * n), max=1e10 * mR / n), zn)
+            # exit test on the original problem at the accepted point
+            th = g_a.abs().sum(1)
+            ph = self._barrier_obj(f_a, xR, mu)
+            dominated = ((th[:, None] >= filt[:, :, 0]) & (ph[:, None] >= filt[:, :, 1])).any(1)
+            done_r = on & torch.isfinite(th) & torch.isfinite(ph) &                 (th <= opt.required_infeasibility_reduction * th0) & ~dominated
+            if bool(done_r.any()):  # the original bound multipliers: Newton step over the phase's whole dx
+                sl0 = torch.where(hasL, x - lbI, torch.ones_like(x))
+                su0 = torch.where(hasU, ubI - x, torch.ones_like(x))
+                d = xR - x
+                m0 = mu[:, None]
+                dzl0 = torch.where(hasL, m0 / sl0 - zl - zl / sl0 * d, zeros_x)
+                dzu0 = torch.where(hasU, m0 / su0 - zu + zu / su0 * d, zeros_x)
+                ad = torch.minimum(self._max_step(zl, dzl0, hasL, tau), self._max_step(zu, dzu0, hasU, tau))[:, None]
+                zl1 = torch.where(hasL, zl + ad * dzl0, zl)
+                zu1 = torch.where(hasU, zu + ad * dzu0, zu)
+                big = torch.maximum(zl1.amax(1), zu1.amax(1)) > 1e3
+                zl1 = torch.where(big[:, None], hasL.to(zl.dtype).expand_as(zl), zl1)
+                zu1 = torch.where(big[:, None], hasU.to(zu.dtype).expand_as(zu), zu1)
+                zl = torch.where(done_r[:, None], zl1, zl)
+                zu = torch.where(done_r[:, None], zu1, zu)
+            if opt.verbose:
+                print(f"  resto {r:3d} on {int(on[0])} acc {int(acc[0])} muR {float(muR[0]):.2e} thR {float(thR[0]):.3e} "
+                      f"th {float(th[0]):.3e} th0 {float(th0[0]):.3e} dom {int(dominated[0])} a {float(alpha[0]):.2e} "
+                      f"ap {float(a_p[0]):.2e} az {float(a_z[0]):.2e} dw {float(dw[0]):.1e} done {int(done_r[0])} ed {float(ed[0]):.2e} "
+                      f"ep {float(ep[0]):.2e} emu {float(e_last[0]):.2e}")
+            on = on & ~done_r & (iters + its < opt.max_iter)
+        return xR, zl, zu, filt, fpos, its
 
     def _kkt_solve(self, K, rhs):
         """Solve with factored KKT K for a natural-order right-hand side (free variables, then g rows)."""
@@ -727,10 +957,13 @@ class BatchedIpm:
 
     def _filter_accept(self, gt, ft, xt, theta, phi, dphi, alpha, mu, theta_max, theta_min, filt):
         """Ipopt acceptance test of a trial point: (accepted, by the Armijo/f-type rule)."""
+        return self._filter_core(gt.abs().sum(1), self._barrier_obj(ft, xt, mu), theta, phi, dphi, alpha, theta_max,
+                                 theta_min, filt)
+
+    def _filter_core(self, tt, pt, theta, phi, dphi, alpha, theta_max, theta_min, filt):
+        """The filter test of a trial (tt = ||c||_1, pt = barrier objective) against the current point."""
         torch = self.torch
         opt = self.opt
-        tt = gt.abs().sum(1)
-        pt = self._barrier_obj(ft, xt, mu)
         finite = torch.isfinite(pt) & torch.isfinite(tt)
         s_phi, s_theta, delta = 2.3, 1.1, 1.0
         switching = (dphi < 0) & (alpha * (-dphi).clamp(min=0) ** s_phi > delta * theta ** s_theta) & (theta <= theta_min)
@@ -780,8 +1013,10 @@ class GpuBandSolver:
 _NATIVE_OPTIONS = ("tol", "max_iter", "acceptable_tol", "acceptable_iter", "mu_init", "bound_relax_factor",
                    "bound_push", "tau_min", "kappa_eps", "kappa_mu", "theta_mu", "s_max", "armijo", "max_backtrack",
                    "delta_c", "curv_min", "max_soc", "kappa_soc", "watchdog_shortened_iter_trigger",
-                   "watchdog_trial_iter_max", "limited_memory_max_history")
+                   "watchdog_trial_iter_max", "limited_memory_max_history", "max_resto_iter", "resto_penalty",
+                   "required_infeasibility_reduction")
 _HESSIAN_APPROXIMATION = {"exact": 0, "limited-memory": 1}
+_RESTORATION = {"step": 0, "phase": 1, None: 1}
 
 
 class NativeIpm:
@@ -806,7 +1041,8 @@ class NativeIpm:
         self.free = np.where(lb != ub)[0]
         self.ipm = _cfx.Ipm(self.h, lb, ub, int(getattr(ocp, "n_params", 0) or 0),
                             {**{k: getattr(self.opt, k) for k in _NATIVE_OPTIONS},
-                             "hessian_approximation": _HESSIAN_APPROXIMATION[self.opt.hessian_approximation]})
+                             "hessian_approximation": _HESSIAN_APPROXIMATION[self.opt.hessian_approximation],
+                             "restoration": _RESTORATION[self.opt.restoration]})
         self.calls = {"eval_all": 0, "eval_h": 0, "eval_g_f": 0, "kkt_factor": 0}
 
     def solve(self, v0=None, fixed_values=None):

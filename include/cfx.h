@@ -331,9 +331,25 @@ typedef struct cfx_ipm_options {
        solve through the Sherman-Morrison-Woodbury identity on the band factors) */
     int32_t hessian_approximation;
     int32_t limited_memory_max_history;
+    /* What a failed line search starts (the instances whose search failed; the others wait):
+       CFX_RESTORATION_PHASE (default) — Ipopt's feasibility-restoration phase, an NLP of its own over the constraint
+       violation, min rho sum(p + n) + zeta/2 |D_R (x - x_r)|^2 s.t. c(x) - p + n = 0, p, n >= 0 and the bounds,
+       solved by the same interior point (own barrier mu_R = max(mu, |c|_inf), filter and line search; p, n and their
+       multipliers eliminated, so its KKT matrix has the original band structure) until a point is acceptable to the
+       original filter with |c|_1 <= required_infeasibility_reduction times the value where it started, or
+       max_resto_iter iterations (the bound multipliers then take a Newton step for complementarity over the phase's
+       dx, the constraint multipliers restart from zero, the filter from empty; the phase's iterations count among the
+       instance's max_iter); CFX_RESTORATION_STEP — one minimum-norm step on c = 0 in the Sigma + I metric,
+       backtracked until |c|_1 decreases, then least-squares multipliers. */
+    int32_t restoration;
+    int32_t max_resto_iter;                  /* 200 */
+    double resto_penalty;                    /* rho, Ipopt resto_penalty_parameter: 1000 */
+    double required_infeasibility_reduction; /* 0.9 */
 } cfx_ipm_options;
 #define CFX_HESSIAN_EXACT 0
 #define CFX_HESSIAN_LIMITED_MEMORY 1
+#define CFX_RESTORATION_STEP 0
+#define CFX_RESTORATION_PHASE 1
 
 typedef struct cfx_ipm_stats {
     int64_t eval_all, eval_g_f, eval_h, kkt_factor, iterations, host_syncs;
@@ -342,6 +358,7 @@ typedef struct cfx_ipm_stats {
        complement; 0: one band) */
     int64_t kkt_n, kkt_kl, kkt_ku, kkt_band_n, kkt_border;
     int64_t kkt_blocks; /* band blocks factored side by side (nested dissection of the stage chain; 1: none) */
+    int64_t resto_phases, resto_iterations; /* restoration phases entered / their iterations (whole batch) */
 } cfx_ipm_stats;
 
 typedef struct cfx_ipm cfx_ipm;

@@ -31,10 +31,11 @@ def _starts(ocp, B, seed, spread=10.0):
     return v0
 
 
-def _both(ocp, B, v0, tol=1e-8, fixed_values=None, max_iter=300):
+def _both(ocp, B, v0, tol=1e-8, fixed_values=None, max_iter=300, restoration="phase"):
     from cocofest_amd.solver import BatchedIpm, IpmOptions, NativeIpm
 
-    opts = IpmOptions(tol=tol, max_iter=max_iter)
+    # the same restoration on both sides (BatchedIpm's own default is the minimum-norm step, NativeIpm's the phase)
+    opts = IpmOptions(tol=tol, max_iter=max_iter, restoration=restoration)
     ref = BatchedIpm(ocp, batch=B, options=opts)
     r_ref = ref.solve(v0, fixed_values=fixed_values)
     ref.close()

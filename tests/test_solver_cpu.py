@@ -141,3 +141,61 @@ def test_safe_slacks_and_watchdog_keep_the_end_game_short():
     assert res.converged.all() and res.iterations[0] <= 60, res.iterations
     lb, ub = ocp.bounds_vector()
     assert np.all(res.v[0] >= lb - 1e-12) and np.all(res.v[0] <= ub + 1e-12)  # final point on the original bounds
+
+
+def test_restoration_phase_reduces_the_infeasibility():
+    """Ipopt's restoration phase (BatchedIpm._restoration_phase, the specification of cfx_ipm's k_rs_* kernels) run
+    directly from badly infeasible points of a Ding2007 pulse-width problem: each instance leaves it successfully with
+    ||c||_1 <= required_infeasibility_reduction * ||c||_1 at the start, inside the bounds, with positive bound
+    multipliers; the closed-form p, n of its start satisfy c - p + n = 0 and 2 rho = mu / p + mu / n."""
+    import torch
+
+    cfg = dict(name="ding2007", stims=[0.0, 0.05, 0.1, 0.15], final_time=0.2, truncation=4, scheme="RK1", m=5,
+               objective={"end_node_tracking": 30}, n_shooting=None)
+    B = 3
+    ocp, pb, ipm = _ipm(cfg, batch=B, tol=1e-8, restoration="phase")
+    rng = np.random.default_rng(4)
+    lb, ub = ocp.bounds_vector()
+    v = np.tile(ocp.initial_guess_vector(), (B, 1))
+    free = lb != ub
+    v[:, free] = np.clip(v[:, free] + rng.uniform(0, 1, (B, free.sum())) * np.minimum(ub[free] - lb[free], 50.0),
+                         lb[free], ub[free])
+    # the solver's state at such a point, as solve() sets it up
+    vt = torch.as_tensor(v)
+    ipm._set_function_scaling(vt)
+    ipm._v_template = vt.clone()
+    x = vt[:, ipm.freeT] / ipm.d
+    lbF, ubF = ipm.lbF.expand(B, -1).clone(), ipm.ubF.expand(B, -1).clone()
+    ipm._lbI, ipm._ubI = lbF, ubF
+    x = torch.where(ipm.hasL, torch.maximum(x, lbF + 1e-2), x)
+    x = torch.where(ipm.hasU, torch.minimum(x, ubF - 1e-2), x)
+    mu = torch.full((B,), 0.1, dtype=torch.float64)
+    zl = torch.where(ipm.hasL, mu[:, None] / (x - lbF), torch.zeros_like(x))
+    zu = torch.where(ipm.hasU, mu[:, None] / (ubF - x), torch.zeros_like(x))
+    g, _, f, _ = ipm._scaled_all(ipm._full(x))
+    theta = g.abs().sum(1)
+    phi = ipm._barrier_obj(f, x, mu)
+    filt = torch.full((B, 64, 2), np.inf, dtype=torch.float64)
+    filt[:, :, 1] = -np.inf
+    on = torch.ones((B,), dtype=torch.bool)
+    xr, zl2, zu2, filt2, fpos2, its = ipm._restoration_phase(on, x, zl, zu, g, theta, phi, mu,
+                                                             torch.full((B,), 0.99, dtype=torch.float64), filt,
+                                                             torch.zeros((B,), dtype=torch.int64),
+                                                             torch.zeros((B,), dtype=torch.int64))
+    gr, _ = ipm._scaled_gf(ipm._full(xr))
+    assert torch.all(its >= 1)
+    assert torch.all(gr.abs().sum(1) <= 0.9 * theta), (gr.abs().sum(1), theta)
+    assert torch.all(xr[:, ipm.hasL] > lbF[:, ipm.hasL]) and torch.all(xr[:, ipm.hasU] < ubF[:, ipm.hasU])
+    assert torch.all(zl2[:, ipm.hasL] > 0) and torch.all(zu2[:, ipm.hasU] > 0)
+    assert torch.all(fpos2 == 1)  # the starting point entered the original filter
+    # Ipopt's closed-form relaxation of the start (restated in k_rs_init / rs_pn)
+    c = g
+    muR = torch.maximum(mu, c.abs().amax(1))[:, None]
+    rho = ipm.opt.resto_penalty
+    s = torch.hypot(muR, rho * c)
+    n = torch.where(c > 0, (muR + muR * muR / (s + rho * c)) / (2 * rho), (muR - rho * c + s) / (2 * rho))
+    p = torch.where(c < 0, (muR + muR * muR / (s - rho * c)) / (2 * rho), (muR + rho * c + s) / (2 * rho))
+    assert torch.all(p > 0) and torch.all(n > 0)
+    np.testing.assert_allclose((c - p + n).numpy(), 0.0, atol=1e-12 * float(c.abs().max()))
+    np.testing.assert_allclose((muR / p + muR / n).numpy(), 2 * rho, rtol=1e-10)
+    ipm.close()
