@@ -20,6 +20,7 @@ ap.add_argument("--amp", type=float, default=0.1)
 ap.add_argument("--max-iter", type=int, default=1000)
 ap.add_argument("--modes", default="phase,step")
 ap.add_argument("--cfg3-batch", type=int, default=0)
+ap.add_argument("--rir", default="0.9", help="required_infeasibility_reduction values (phase runs), comma-separated")
 a = ap.parse_args()
 
 
@@ -33,14 +34,15 @@ def starts(ocp, B, amp, seed=0):
     return v0
 
 
-def run(name, ocp, v0, mode):
-    print(f"# {name} {mode} batch {len(v0)}", file=sys.stderr, flush=True)
-    ipm = NativeIpm(ocp, batch=len(v0), options=IpmOptions(tol=1e-6, max_iter=a.max_iter, restoration=mode))
+def run(name, ocp, v0, mode, rir=0.9):
+    print(f"# {name} {mode} {rir} batch {len(v0)}", file=sys.stderr, flush=True)
+    ipm = NativeIpm(ocp, batch=len(v0), options=IpmOptions(tol=1e-6, max_iter=a.max_iter, restoration=mode,
+                                                            required_infeasibility_reduction=rir))
     res = ipm.solve(v0)
     st = ipm.last_stats
     ipm.close()
     conv = res.converged.astype(bool)
-    print(json.dumps({"problem": name, "restoration": mode, "batch": len(v0), "converged": int(conv.sum()),
+    print(json.dumps({"problem": name, "restoration": mode, "required_infeasibility_reduction": rir, "batch": len(v0), "converged": int(conv.sum()),
                       "wall_s": res.wall_time, "iterations_median": float(np.median(res.iterations)),
                       "iterations_max": int(res.iterations.max()),
                       "f_converged_min": float(res.f[conv].min()) if conv.any() else None,
@@ -54,7 +56,8 @@ if a.cfg5_batch:
     ocp = bench.msk_build(5)
     v0 = starts(ocp, a.cfg5_batch, a.amp)
     for mode in modes:
-        run(f"cfg5_rk4x5_amp{a.amp}", ocp, v0, mode)
+        for rir in ([float(r) for r in a.rir.split(",")] if mode == "phase" else [0.9]):
+            run(f"cfg5_rk4x5_amp{a.amp}", ocp, v0, mode, rir)
 if a.cfg3_batch:  # bench.convergence's random starts
     ocp3 = bench.build_cfg3()
     rng = np.random.default_rng(0)
