@@ -176,7 +176,10 @@ def load_library(path: str | os.PathLike | None = None):
     if not p.exists():
         raise CfxError(ENODEV, f"{p} not found: build it with `make -C cocofest_amd/csrc` (no CPU fallback)")
     lib = C.CDLL(str(p))
+    variant = bool(os.environ.get("CFX_LIB")) and not path  # an A/B build may predate later entry points
     for name, (res, args) in SIGNATURES.items():
+        if variant and not hasattr(lib, name):
+            continue  # calling it raises AttributeError
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args

@@ -706,6 +706,223 @@ __global__ void __launch_bounds__(64) k_band_solve_reg_multi(int n, int kl, int 
 }
 
 // ---------------------------------------------------------------------------------------------------
+// grouped register placement: four instances per wavefront, 16 lanes each (narrow bands, large batches)
+// ---------------------------------------------------------------------------------------------------
+// The register kernel above gives each instance a whole wavefront, but a band with kl <= 7 and ku <= 8 keeps
+// only the 8 + ku <= 16 lanes of its window busy: for the cfg-2 / cfg-3 KKT bands (kl = ku = 5..6) 50 of the 64
+// lanes idle, and once the batch fills the chip the waves queue for the SIMDs.  Here a 16-lane row of the wave
+// owns one instance (instance 4 blockIdx + lane / 16) and runs the same column step on its window, with the
+// cross-lane operations kept inside the row: the group's lane 0 is broadcast with DPP row_newbcast:0, the window
+// slides with DPP row_shl:1 (lane 15 of each row takes 0, as lane 63 does above), the pivot row (now different in
+// each group) is swapped in by selects, and the multipliers are gathered into lanes 1 .. kl by selects.  Same
+// storage, pivots, zero-pivot convention and D-step prefetch discipline as the one-instance kernel.
+__device__ __forceinline__ int g16_first_i(int v) { return __builtin_amdgcn_mov_dpp(v, 0x150, 0xf, 0xf, false); }
+__device__ __forceinline__ double g16_first(double v) {  // the group's lane 0 value (row_newbcast:0)
+    return from32(g16_first_i(lo32(v)), g16_first_i(hi32(v)));
+}
+__device__ __forceinline__ double g16_next(double v) {  // v on group lane + 1, 0.0 on group lane 15 (row_shl:1)
+    return from32(__builtin_amdgcn_mov_dpp(lo32(v), 0x101, 0xf, 0xf, true),
+                  __builtin_amdgcn_mov_dpp(hi32(v), 0x101, 0xf, 0xf, true));
+}
+__device__ __forceinline__ double g16_read(double v, int src) {  // v on lane src (any lane; ds_bpermute)
+    return from32(__builtin_amdgcn_ds_bpermute(src << 2, lo32(v)), __builtin_amdgcn_ds_bpermute(src << 2, hi32(v)));
+}
+constexpr int kG16Klm = 7;  // window rows (kl <= 7); columns 8 + ku <= 16
+
+// x <- U^-1 L^-1 P x for nrhs right-hand sides, one instance per 16-lane group (factors of k_band_lu_reg16 or of
+// any placement: same storage)
+template <int D>
+__device__ __forceinline__ void reg16_solve(int n, int kl, int ku, int nrhs, const double* ab, const int32_t* piv,
+                                            double* xs, bool valid) {
+    const int gl = threadIdx.x & 15, base = threadIdx.x & 48;
+    const int ldab = 2 * kl + ku + 1, kv = kl + ku;
+    double* dsink = block_sink() + threadIdx.x;
+    for (int c = 0; c < nrhs; ++c) {
+        double* x = xs + (int64_t)c * n;
+        if (kl > 0) {
+            auto mult_ok = [&](int j) { return j < n && gl >= 1 && gl <= min(kl, n - 1 - j); };
+            auto mult = [&](int j) { return ab[mult_ok(j) ? j * ldab + kv + gl : 0]; };
+            auto enter_ok = [&](int j) { return gl == kl && j + 1 + kl < n; };
+            auto enter = [&](int j) { return x[enter_ok(j) ? j + 1 + kl : 0]; };
+            auto pivot = [&](int j) { return piv[min(j, n - 1)]; };
+            double xw = (gl <= kl && gl < n) ? x[gl] : 0.0;
+            double lc[D], nx[D];
+            int pj[D];
+            static_for<0, D>([&](auto S_) CFX_INLINE {
+                constexpr int s = decltype(S_)::value;
+                lc[s] = mult(s);
+                nx[s] = enter(s);
+                pj[s] = pivot(s);
+            });
+            auto step = [&](int j, double& lcs, double& nxs, int& pjs, int jpre) CFX_INLINE {
+                double lcv = mult_ok(j) ? lcs : 0.0, nxv = enter_ok(j) ? nxs : 0.0;
+                int pjv = pjs;
+                asm volatile("" : "+v"(lcv), "+v"(nxv), "+v"(pjv)::"memory");
+                lcs = mult(jpre);
+                nxs = enter(jpre);
+                pjs = pivot(jpre);
+                const int p = pjv - j;  // the same in the group's lanes
+                const double a = g16_first(xw), bq = g16_read(xw, base + p);
+                xw = gl == 0 ? bq : (gl == p ? a : xw);
+                const double xj = g16_first(xw);
+                xw -= lcv * xj;
+                *(valid && gl == 0 ? x + j : dsink) = xj;
+                xw = g16_next(xw);
+                if (gl == kl) xw = nxv;
+            };
+            int j0 = 0;
+            for (; j0 + D <= n - 1; j0 += D) {
+                static_for<0, D>([&](auto S_) CFX_INLINE {
+                    constexpr int s = decltype(S_)::value;
+                    step(j0 + s, lc[s], nx[s], pj[s], j0 + s + D);
+                });
+            }
+            static_for<0, D>([&](auto S_) CFX_INLINE {
+                constexpr int s = decltype(S_)::value;
+                if (j0 + s < n - 1) step(j0 + s, lc[s], nx[s], pj[s], n);
+            });
+            if (valid && gl == 0) x[n - 1] = xw;
+            __threadfence();  // the backward pass re-reads what this one stored
+        }
+        auto ucol_ok = [&](int j) { return j >= 0 && gl <= min(kv, j); };
+        auto ucol = [&](int j) { return ab[ucol_ok(j) ? j * ldab + kv - gl : 0]; };
+        auto enter_ok = [&](int j) { return gl == kv && j - 1 - kv >= 0; };
+        auto enter = [&](int j) { return x[enter_ok(j) ? j - 1 - kv : 0]; };
+        double xw = (gl <= kv && n - 1 - gl >= 0) ? x[n - 1 - gl] : 0.0;
+        double uc[D], nx[D];
+        static_for<0, D>([&](auto S_) CFX_INLINE {
+            constexpr int s = decltype(S_)::value;
+            uc[s] = ucol(n - 1 - s);
+            nx[s] = enter(n - 1 - s);
+        });
+        auto step = [&](int j, double& ucs, double& nxs, int jpre) CFX_INLINE {
+            double ucv = ucol_ok(j) ? ucs : 0.0, nxv = enter_ok(j) ? nxs : 0.0;
+            asm volatile("" : "+v"(ucv), "+v"(nxv)::"memory");
+            ucs = ucol(jpre);
+            nxs = enter(jpre);
+            const double xj = g16_first(xw) / g16_first(ucv);
+            *(valid && gl == 0 ? x + j : dsink) = xj;
+            xw -= gl == 0 ? 0.0 : ucv * xj;
+            xw = g16_next(xw);
+            if (gl == kv) xw = nxv;
+        };
+        int j0 = n - 1;
+        for (; j0 - D + 1 >= 0; j0 -= D) {
+            static_for<0, D>([&](auto S_) CFX_INLINE {
+                constexpr int s = decltype(S_)::value;
+                step(j0 - s, uc[s], nx[s], j0 - s - D);
+            });
+        }
+        static_for<0, D>([&](auto S_) CFX_INLINE {
+            constexpr int s = decltype(S_)::value;
+            if (j0 - s >= 0) step(j0 - s, uc[s], nx[s], -1);
+        });
+    }
+}
+
+template <int D>
+__global__ void __launch_bounds__(64) k_band_lu_reg16(int64_t batch, int n, int kl, int ku, int nrhs,
+                                                      double* __restrict__ AB, int32_t* __restrict__ IPIV,
+                                                      double* __restrict__ RHS, int32_t* __restrict__ INFO) {
+    constexpr int KLM = kG16Klm;
+    const int gl = threadIdx.x & 15;
+    const int64_t b0 = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 4);
+    const bool valid = b0 < batch;
+    const int64_t b = valid ? b0 : batch - 1;  // the spare groups of the last wave read a valid instance
+    const int ldab = 2 * kl + ku + 1, kv = kl + ku;
+    double* ab = AB + b * (int64_t)n * ldab;
+    int32_t* piv = IPIV + b * n;
+    const int cofs = gl * (ldab - 1) + kv;  // U(j, j + gl) at ab[j ldab + cofs]
+    const bool uok = gl <= kv;
+    const bool eok = gl >= KLM - kl && gl <= KLM + ku;
+    auto entering_ok = [&](int j) { return eok && j + 1 + KLM < n && j + 1 + gl < n; };
+    auto fetch = [&](int j) { return ab[entering_ok(j) ? (j + 1) * ldab + cofs + KLM : 0]; };
+    double* const sinkb = block_sink();
+    double* dsink = sinkb + threadIdx.x;
+    int32_t* isink = reinterpret_cast<int32_t*>(sinkb + 64 * 2) + threadIdx.x;
+
+    double r[KLM + 1];  // r[i]: row j + i of the window, column j + gl
+    static_for<0, KLM + 1>([&](auto I) CFX_INLINE {
+        constexpr int i = decltype(I)::value;
+        r[i] = (i < n && gl < n && i - gl <= kl && gl - i <= ku) ? ab[gl * ldab + kv + i - gl] : 0.0;
+    });
+    if (valid && gl < min(kv, n))
+        for (int q = 0; q < min(kl, kv - gl); ++q) ab[gl * ldab + q] = 0.0;
+    double nxt[D];
+    static_for<0, D>([&](auto S_) CFX_INLINE { nxt[decltype(S_)::value] = fetch(decltype(S_)::value); });
+    int info = 0;
+
+    auto step = [&](int j, double& pre, int jpre) CFX_INLINE {
+        double ent = entering_ok(j) ? pre : 0.0;
+        asm volatile("" : "+v"(ent)::"memory");
+        pre = fetch(jpre);
+        // pivot: first largest |A(j + i, j)| on the group's lane 0 (column j)
+        double best = fabs(r[0]);
+        int p = 0;
+        static_for<1, KLM + 1>([&](auto I) CFX_INLINE {
+            constexpr int i = decltype(I)::value;
+            const double a = fabs(r[i]);
+            p = a > best ? i : p;
+            best = fmax(best, a);
+        });
+        p = g16_first_i(p);
+        *(valid && gl == 0 ? piv + j : isink) = j + p;
+        static_for<1, KLM + 1>([&](auto I) CFX_INLINE {  // rows 0 and p (group-uniform p) by selects
+            constexpr int i = decltype(I)::value;
+            const bool sw = p == i;
+            const double t = r[0];
+            r[0] = sw ? r[i] : r[0];
+            r[i] = sw ? t : r[i];
+        });
+        const double u = r[0];
+        *(valid && uok && j + gl < n ? ab + j * ldab + cofs : dsink) = u;
+        const double pv = g16_first(u);
+        const double inv = pv != 0.0 ? 1.0 / pv : 0.0;
+        if (pv == 0.0 && info == 0) info = j + 1;
+        double lg = 0.0;  // group lane i gathers L(j + i, j)
+        static_for<1, KLM + 1>([&](auto I) CFX_INLINE {
+            constexpr int i = decltype(I)::value;
+            const double l = g16_first(r[i] * inv);
+            lg = gl == i ? l : lg;
+            r[i] -= l * u;
+        });
+        *(valid && gl >= 1 && gl <= min(kl, n - 1 - j) ? ab + j * ldab + kv + gl : dsink + 64) = lg;
+        static_for<0, KLM>([&](auto I) CFX_INLINE {
+            constexpr int i = decltype(I)::value;
+            r[i] = g16_next(r[i + 1]);
+        });
+        r[KLM] = ent;
+    };
+    int j0 = 0;
+    for (; j0 + D <= n; j0 += D) {
+        static_for<0, D>([&](auto S_) CFX_INLINE {
+            constexpr int s = decltype(S_)::value;
+            step(j0 + s, nxt[s], j0 + s + D);
+        });
+    }
+    static_for<0, D>([&](auto S_) CFX_INLINE {
+        constexpr int s = decltype(S_)::value;
+        if (j0 + s < n) step(j0 + s, nxt[s], n);
+    });
+    if (valid && gl == 0) INFO[b] = info;
+    if (nrhs > 0) {
+        __threadfence();  // the solve reads the factors stored above
+        reg16_solve<D>(n, kl, ku, nrhs, ab, piv, RHS + b * (int64_t)n * nrhs, valid);
+    }
+}
+
+template <int D>
+__global__ void __launch_bounds__(64) k_band_solve_reg16(int64_t batch, int n, int kl, int ku, int nrhs,
+                                                         const double* __restrict__ AB,
+                                                         const int32_t* __restrict__ IPIV, double* __restrict__ RHS) {
+    const int64_t b0 = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 4);
+    const bool valid = b0 < batch;
+    const int64_t b = valid ? b0 : batch - 1;
+    reg16_solve<D>(n, kl, ku, nrhs, AB + b * (int64_t)n * (2 * kl + ku + 1), IPIV + b * n,
+                   RHS + b * (int64_t)n * nrhs, valid);
+}
+
+// ---------------------------------------------------------------------------------------------------
 // lane placement: one lane per instance (large batches of narrow bands)
 // ---------------------------------------------------------------------------------------------------
 // Once the batch alone fills the chip, a wavefront per instance spends every column step on cross-lane
@@ -1024,9 +1241,28 @@ static int reg_chunks(int64_t n, int32_t kl, int32_t ku) {
     return nch;
 }
 
+// Grouped register placement (four instances per wave): windows of at most 16 lanes, batches of at least
+// kGroupBatch instances (CFX_BAND_GROUP=0 / 1 forces it off / on where it fits).
+constexpr int64_t kGroupBatch = 256;
+static bool group_ok(int64_t n, int32_t kl, int32_t ku, int64_t batch) {
+    if (kl > kG16Klm || 8 + ku > 16 || n * (2 * (int64_t)kl + ku + 1) >= ((int64_t)1 << 31)) return false;
+    if (const char* e = std::getenv("CFX_BAND_GROUP")) return *e == '1';
+    return batch >= kGroupBatch;
+}
+
 static hipError_t reg_dispatch(int64_t n, int32_t kl, int32_t ku, int64_t batch, double* ab, int32_t* ipiv,
                                int32_t* info, int32_t nrhs, double* rhs, hipStream_t s, int factor) {
 #define CFX_REG(M, C) launch_reg<M, C>(n, kl, ku, batch, ab, ipiv, info, nrhs, rhs, s, factor)
+    if (group_ok(n, kl, ku, batch)) {
+        const dim3 grid((unsigned)((batch + 3) / 4));
+        if (factor)
+            hipLaunchKernelGGL(k_band_lu_reg16<8>, grid, dim3(64), 0, s, batch, (int)n, kl, ku, nrhs, ab, ipiv, rhs,
+                               info);
+        else
+            hipLaunchKernelGGL(k_band_solve_reg16<8>, grid, dim3(64), 0, s, batch, (int)n, kl, ku, nrhs,
+                               (const double*)ab, (const int32_t*)ipiv, rhs);
+        return hipGetLastError();
+    }
     const int nch = reg_chunks(n, kl, ku);
     if (8 * nch + ku <= 64) {
         switch (nch) {
@@ -1151,7 +1387,7 @@ static int band_launch(int64_t n, int32_t kl, int32_t ku, int64_t batch, double*
     const char* forced = std::getenv("CFX_BAND_PLACEMENT");
     const bool win_ok = lds_win <= (size_t)kBandLds && chunk >= 4;
     // the register solve (one wave per instance) loses to the windowed one once the batch fills the chip
-    const bool reg_ok = reg_chunks(n, kl, ku) > 0 && (factor || batch < 2048 || !win_ok);
+    const bool reg_ok = reg_chunks(n, kl, ku) > 0 && (factor || batch < 2048 || !win_ok || group_ok(n, kl, ku, batch));
     if (forced && *forced == '4' && lane_ok(n, kl, ku))
         placement = 4;
     else if (forced && *forced == '3' && reg_chunks(n, kl, ku) > 0)

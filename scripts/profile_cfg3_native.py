@@ -1,5 +1,6 @@
-"""cfg 3 (Ding2007 pulse width, N = 100, force tracking) native interior point at batch 1, solved `reps` times after
-a warm-up, for a rocprofv3 kernel trace: python scripts/profile_cfg3_native.py [reps]"""
+"""cfg 3 (Ding2007 pulse width, N = 100, force tracking) native interior point at batch B (1: the reference's initial
+guess; > 1: bench.py's random starts), solved `reps` times after a warm-up, for a rocprofv3 kernel trace:
+python scripts/profile_cfg3_native.py [reps] [B]"""
 import json
 import pathlib
 import sys
@@ -14,20 +15,30 @@ from cocofest_amd import ModelMaker, OcpFes, OdeSolver  # noqa: E402
 from cocofest_amd.solver import IpmOptions, NativeIpm  # noqa: E402
 
 reps = int(sys.argv[1]) if len(sys.argv) > 1 else 10
+B = int(sys.argv[2]) if len(sys.argv) > 2 else 1
 ft = json.loads((ROOT / "tests" / "golden" / "ref_formulas.json").read_text())["misc"]["force_tracking"]
 model = ModelMaker.create_model("ding2007", stim_time=[float(v) for v in np.round(np.linspace(0, 1, 31)[:-1], 2)],
                                 sum_stim_truncation=10)
 ocp = OcpFes.prepare_ocp(model=model, final_time=1, pulse_width={"min": model.pd0, "max": 0.0006},
                          objective={"force_tracking": [np.array(ft["time"]), np.array(ft["force"])]},
                          ode_solver=OdeSolver.RK1(n_integration_steps=10))
-ipm = NativeIpm(ocp, batch=1, options=IpmOptions(tol=1e-6, max_iter=300))
-ipm.solve()
+v0 = None
+if B > 1:  # bench.py convergence(): the reference's guess + U(0, 1) x min(range, 10) on every free variable
+    rng = np.random.default_rng(0)
+    v0 = np.tile(ocp.initial_guess_vector(), (B, 1))
+    lb, ub = ocp.bounds_vector()
+    free = lb != ub
+    v0[:, free] = np.clip(v0[:, free] + rng.uniform(0, 1, (B, free.sum())) * np.minimum(ub[free] - lb[free], 10),
+                          lb[free], ub[free])
+ipm = NativeIpm(ocp, batch=B, options=IpmOptions(tol=1e-6, max_iter=300))
+ipm.solve(v0)
 walls = []
 for _ in range(reps):
     t = time.perf_counter()
-    r = ipm.solve()
+    r = ipm.solve(v0)
     walls.append(time.perf_counter() - t)
-print(json.dumps({"wall_s_median": float(np.median(walls)), "wall_s_min": min(walls), "iterations": int(r.iterations[0]),
+print(json.dumps({"batch": B, "wall_s_median": float(np.median(walls)), "wall_s_min": min(walls),
+                  "iterations": int(r.iterations.max()), "converged": int(r.converged.sum()),
                   "callbacks": r.n_callbacks, "stats": {k: (float(v) if not isinstance(v, int) else v)
                                                        for k, v in ipm.last_stats.items()}}))
 ipm.close()

@@ -604,6 +604,46 @@ def test_band_lu_lane_placement(B, n, kl, ku, zero_diag, monkeypatch):
     assert np.max(np.abs(lane[3][pick] - ref)) <= 1e-13 * cond * n * max(1.0, np.abs(ref).max())
 
 
+@pytest.mark.parametrize("B,n,kl,ku,zero_diag", [(1100, 502, 6, 6, True), (257, 60, 7, 8, True), (70, 37, 3, 1, False),
+                                                 (66, 50, 0, 2, False), (65, 9, 5, 2, True), (5, 1, 0, 0, False),
+                                                 (4096, 120, 6, 6, False)])
+def test_band_lu_grouped_register_placement(B, n, kl, ku, zero_diag, monkeypatch):
+    """Four instances per wavefront (16-lane groups, bands with kl <= 7 and ku <= 8; forced with CFX_BAND_GROUP=1)
+    against one instance per wavefront (CFX_BAND_GROUP=0): the same factors, pivots, zero-pivot reports and
+    solutions bit for bit (the same operations per instance), batches that are not a multiple of four included; and
+    numpy's dense solve on a sample."""
+    import torch
+
+    from cocofest_amd import _cfx
+
+    rng = np.random.default_rng(B + n + kl + 7)
+    A, ab = _band_system(rng, B, n, kl, ku, zero_diag=zero_diag)
+    rhs = rng.standard_normal((B, 2, n))
+    monkeypatch.setenv("CFX_BAND_PLACEMENT", "3")
+    outs = {}
+    for grp in ("1", "0"):
+        monkeypatch.setenv("CFX_BAND_GROUP", grp)
+        abt = torch.tensor(ab, device="cuda")
+        ipiv = torch.empty((B, n), dtype=torch.int32, device="cuda")
+        info = torch.empty((B,), dtype=torch.int32, device="cuda")
+        x = torch.tensor(rhs, device="cuda")
+        _cfx.band_lu(abt, ipiv, info, kl, ku, rhs=x)
+        x2 = torch.tensor(rhs[:, 1:], device="cuda")
+        _cfx.band_lu_solve(abt, ipiv, kl, ku, x2)
+        torch.cuda.synchronize()
+        outs[grp] = (abt.cpu().numpy(), ipiv.cpu().numpy(), info.cpu().numpy(), x.cpu().numpy(), x2.cpu().numpy())
+    for a, b in zip(outs["1"], outs["0"]):
+        np.testing.assert_array_equal(a, b)
+    got = outs["1"]
+    ok = got[2] == 0
+    pick = rng.choice(np.where(ok)[0], min(int(ok.sum()), 32), replace=False)
+    if len(pick):
+        ref = np.linalg.solve(A[pick], rhs[pick].transpose(0, 2, 1)).transpose(0, 2, 1)
+        cond = np.linalg.cond(A[pick]).max()
+        assert np.max(np.abs(got[3][pick] - ref)) <= 1e-13 * cond * n * max(1.0, np.abs(ref).max())
+        np.testing.assert_array_equal(got[4][pick], got[3][pick][:, 1:])
+
+
 def test_band_lu_reports_singular_and_bad_arguments():
     import torch
 
