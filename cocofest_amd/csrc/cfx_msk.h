@@ -1047,7 +1047,10 @@ __global__ void __launch_bounds__(256) k_msk_tangents(const MskParams P, const M
 // runs kpb consecutive intervals with the next sub-step's coefficients prefetched during the current one (below).
 constexpr int kMskLdsCols = 16;
 constexpr int kMskLdsLoads = 16;  // coefficient loads in flight per thread while staging
-constexpr int kMskTangentInstances = 32;  // TW: instances per k_msk_tangents_lds block
+#ifndef CFX_MSK_TW
+#define CFX_MSK_TW 32
+#endif
+constexpr int kMskTangentInstances = CFX_MSK_TW;  // TW: instances per k_msk_tangents_lds block (16 or 32)
 
 // Default intervals per k_msk_tangents_lds block: as many as keep >= 4,096 blocks (16 per CU) in flight.
 inline int msk_default_kpb(int64_t B, int N) {
@@ -1078,17 +1081,18 @@ __global__ void __launch_bounds__(32 * kMskLdsCols) k_msk_tangents_lds(const Msk
     // (global_load_lds_dwordx4: lane L of a wave moves 16 B to M0 + 16 L, so one wave instruction fills four
     // TW-double rows), so only the block's first staging waits for HBM and no registers hold the prefetch.  Needs
     // 16-byte rows (B even); otherwise the sub-steps stage through registers one at a time.
-    static_assert(TW == 32, "a 16-lane quarter of a wave moves one TW-double row");
+    static_assert(TW == 16 || TW == 32, "a TW / 2-lane part of a wave moves one TW-double row");
+    constexpr int RPW = 128 / TW;  // rows of TW doubles per wave instruction (64 lanes x 16 B)
     const bool async = (B % 2) == 0;
     const int wave = threadIdx.x / 64, nwave = nthr / 64, L = threadIdx.x % 64;  // full waves only (nz odd: one half)
     auto issue = [&](int kk, int j, int buf) {
         const double* __restrict__ Wk = P.scratch + (int64_t)kk * P.Q * NC * B + (int64_t)j * ST * NC * B;
         double* base = sW + buf * NE;
-        for (int c = wave; wave < nwave && c * 4 * TW < NE; c += nwave) {  // chunk c: rows 4c .. 4c + 3 (st * NC + c)
-            const int row = 4 * c + L / 16, l = (L % 16) * 2;
+        for (int c = wave; wave < nwave && c * RPW * TW < NE; c += nwave) {  // chunk c: rows RPW c .. RPW c + RPW - 1
+            const int row = RPW * c + L / (TW / 2), l = (L % (TW / 2)) * 2;
             if (row * TW < NE && b0 + l < B)
                 __builtin_amdgcn_global_load_lds(Wk + (int64_t)row * B + b0 + l,
-                                                 (__attribute__((address_space(3))) void*)(base + c * 4 * TW), 16, 0, 0);
+                                                 (__attribute__((address_space(3))) void*)(base + c * RPW * TW), 16, 0, 0);
         }
     };
     int buf = 0;

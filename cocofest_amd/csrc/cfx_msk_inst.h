@@ -44,9 +44,8 @@ hipError_t shoot_t(const MskParams& P, const MskGeom* G, const double* V, double
                        XS);
     hipLaunchKernelGGL((k_msk_stagecoef_par<NQ, NM, FAM>), dim3((unsigned)((P.B * P.N * P.Q + kMskBlk - 1) / kMskBlk)),
                        dim3(kMskBlk), 0, s, P, G, V, (const double*)XS);
-    if (P.nz <= kMskLdsCols) {  // coefficients through LDS, one block per 32 instances
-        constexpr int ST = SCHEME == 4 ? 4 : (SCHEME == 2 ? 2 : 1), TW = 32;
-        static_assert(TW == kMskTangentInstances, "cfx_msk_create sizes kpb for this block width");
+    if (P.nz <= kMskLdsCols) {  // coefficients through LDS, one block per TW instances
+        constexpr int ST = SCHEME == 4 ? 4 : (SCHEME == 2 ? 2 : 1), TW = kMskTangentInstances;  // cfx_msk_create's kpb
         const int64_t nbx = (P.B + TW - 1) / TW;
         const int kpb = std::max(1, std::min(P.N, P.kpb));  // intervals per block (cfx_msk_create)
         // two coefficient buffers when B is even (k_msk_tangents_lds): above the default 64 KiB of dynamic LDS for cfg 5

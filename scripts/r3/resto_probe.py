@@ -48,7 +48,8 @@ def run(name, ocp, v0, mode, rir=0.9):
                       "f_converged_min": float(res.f[conv].min()) if conv.any() else None,
                       "f_converged_median": float(np.median(res.f[conv])) if conv.any() else None,
                       "resto_phases": int(st["resto_phases"]), "resto_iterations": int(st["resto_iterations"]),
-                      "eval_all": int(st["eval_all"]), "kkt_factor": int(st["kkt_factor"])}), flush=True)
+                      "eval_all": int(st["eval_all"]), "kkt_factor": int(st["kkt_factor"]),
+                      "failed": np.where(~conv)[0].tolist(), "iterations": res.iterations.tolist()}), flush=True)
 
 
 modes = a.modes.split(",")
