@@ -1047,6 +1047,15 @@ __global__ void __launch_bounds__(256) k_msk_tangents(const MskParams P, const M
 // runs kpb consecutive intervals with the next sub-step's coefficients prefetched during the current one (below).
 constexpr int kMskLdsCols = 16;
 constexpr int kMskLdsLoads = 16;  // coefficient loads in flight per thread while staging
+// J_g stores of the tangent kernel: non-temporal, as the shooting kernel's output stream (cfg 5: 1.533 / 1.535 ->
+// 1.529 / 1.526 ms per g + J_g, alternating builds, profiles/round3/msk_waits/nt_j_ab.jsonl)
+__device__ __forceinline__ void msk_st_j(double* p, double v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    __builtin_nontemporal_store(v, p);
+#else
+    *p = v;
+#endif
+}
 #ifndef CFX_MSK_TW
 #define CFX_MSK_TW 32
 #endif
@@ -1160,11 +1169,11 @@ __global__ void __launch_bounds__(32 * kMskLdsCols) k_msk_tangents_lds(const Msk
 #pragma unroll
             for (int r = 0; r < NX; ++r) {
                 const int pos = G.jpos[r * kMskMaxZ + col];
-                if (pos >= 0) J[(jb + pos) * B + b] = tx[r];
+                if (pos >= 0) msk_st_j(J + (jb + pos) * B + b, tx[r]);
             }
             if (col == 0) {
 #pragma unroll
-                for (int r = 0; r < NX; ++r) J[(jb + G.jneg[r]) * B + b] = -1.0;
+                for (int r = 0; r < NX; ++r) msk_st_j(J + (jb + G.jneg[r]) * B + b, -1.0);
             }
         }
     }
