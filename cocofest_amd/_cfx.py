@@ -29,6 +29,7 @@ RK1, RK2, RK4 = 1, 2, 4
 COLLOCATION_LEGENDRE, COLLOCATION_RADAU = 16, 17
 LAYOUT_AOS, LAYOUT_SOA, LAYOUT_TILED64 = 0, 1, 2
 DEVICE = 1
+KEEP_CONSTANT_JAC = 2
 OBJ_LAGRANGE, OBJ_MAYER, OBJ_MAYER_INV = 0, 1, 2
 MSK_FORCE_LENGTH, MSK_FORCE_VELOCITY, MSK_PASSIVE_FORCE, MSK_RESIDUAL_TORQUE = 1, 2, 4, 8
 VAR_STATE, VAR_CONTROL = 0, 1
@@ -137,6 +138,7 @@ SIGNATURES = {
     "cfx_abi_version": (C.c_int, []),
     "cfx_device_count": (C.c_int, []),
     "cfx_jac_structure": (C.c_int, [_P, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
+    "cfx_jac_constant_mask": (C.c_int, [_P, C.POINTER(C.c_uint8)]),
     "cfx_hess_structure": (C.c_int, [_P, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
     "cfx_eval_g": (C.c_int, [_P, _P, _P, C.c_uint32]),
     "cfx_eval_jac_g": (C.c_int, [_P, _P, _P, C.c_uint32]),
@@ -358,6 +360,13 @@ class Handle:
                                                c.ctypes.data_as(C.POINTER(C.c_int32))))
         return r, c
 
+    def jac_constant_mask(self):
+        """Boolean mask over the J_g values that depend on neither the instance nor the point (cfx_jac_constant_mask):
+        the values ``keep_constant_jac=True`` evaluations leave in place."""
+        m = np.empty(self.nnz_jac, dtype=np.uint8)
+        self._check(self.lib.cfx_jac_constant_mask(self.h, m.ctypes.data_as(C.POINTER(C.c_uint8))))
+        return m.astype(bool)
+
     def hess_structure(self):
         r = np.empty(self.nnz_hess, dtype=np.int32)
         c = np.empty(self.nnz_hess, dtype=np.int32)
@@ -421,11 +430,14 @@ class Handle:
             return (self.batch // 64, n, 64) if n > 1 else (self.batch,)
         return (n, self.batch)
 
-    def eval_all(self, v, g=None, jac=None, f=None, grad=None):
+    def eval_all(self, v, g=None, jac=None, f=None, grad=None, keep_constant_jac=False):
+        """keep_constant_jac: CFX_KEEP_CONSTANT_JAC — the constant J_g values (jac_constant_mask) are not written;
+        ``jac`` (device call) or the handle's staging buffer (host call) must hold them from a full evaluation."""
         (v, g, jac, f, grad), fl = self._buffers(("v", v, self.nv, False), ("g", g, self.ng, True),
                                                   ("jac", jac, self.nnz_jac, True), ("f", f, 1, True),
                                                   ("grad", grad, self.nv, True))
         self._torch_stream(fl)
+        fl |= KEEP_CONSTANT_JAC if keep_constant_jac else 0
         self._check(self.lib.cfx_eval_all(self.h, _ptr(v), _ptr(g), _ptr(jac), _ptr(f), _ptr(grad), fl))
 
     def eval_g(self, v, g=None):
@@ -433,9 +445,9 @@ class Handle:
         self.eval_all(v, g=g)
         return g
 
-    def eval_jac_g(self, v, jac=None):
+    def eval_jac_g(self, v, jac=None, keep_constant_jac=False):
         jac = np.empty(self._shape(self.nnz_jac)) if jac is None else jac
-        self.eval_all(v, jac=jac)
+        self.eval_all(v, jac=jac, keep_constant_jac=keep_constant_jac)
         return jac
 
     def eval_f(self, v, f=None):
@@ -456,7 +468,7 @@ class Handle:
         self._check(self.lib.cfx_eval_h(self.h, _ptr(v), _ptr(obj_factor), _ptr(lam), _ptr(hess), fl))
         return hess
 
-    def eval_all_h(self, v, obj_factor, lam, g=None, jac=None, f=None, grad=None, hess=None):
+    def eval_all_h(self, v, obj_factor, lam, g=None, jac=None, f=None, grad=None, hess=None, keep_constant_jac=False):
         """g, J_g, (f, grad f) and the Lagrangian Hessian at one point (cfx_eval_all_h: one launch on the shooting
         transcriptions).  Returns (g, jac, hess)."""
         if _is_tensor(v):  # device call: the missing outputs on the handle's device
@@ -473,6 +485,7 @@ class Handle:
             ("g", g, self.ng, True), ("jac", jac, self.nnz_jac, True), ("f", f, 1, True),
             ("grad", grad, self.nv, True), ("hess", hess, self.nnz_hess, True))
         self._torch_stream(fl)
+        fl |= KEEP_CONSTANT_JAC if keep_constant_jac else 0
         self._check(self.lib.cfx_eval_all_h(self.h, _ptr(v), _ptr(obj_factor), _ptr(lam), _ptr(g), _ptr(jac),
                                             _ptr(f), _ptr(grad), _ptr(hess), fl))
         return g, jac, hess

@@ -56,6 +56,10 @@ struct cfx_handle {
     int n_htasks = 1, hbs = 1;
     int n_obj = 0;
     std::vector<int32_t> jrow, jcol, hrow, hcol;
+    // J_g values that depend on neither the instance nor the point (cfx_jac_constant_mask), and whether the handle's
+    // own J_g staging buffer (AoS / host outputs) holds them from an earlier full evaluation
+    std::vector<uint8_t> jconst;
+    bool jconst_staged = false;
     // musculoskeletal problems (cfx_msk_create)
     bool msk = false;
     int msk_nq = 0, msk_nm = 0, msk_fam = 0;
@@ -592,6 +596,14 @@ extern "C" int cfx_create(const cfx_problem* p, cfx_handle** out) {
         }
     }
     h->sz.nnz_jac = (int64_t)h->jrow.size();
+    // constant J_g values: the -1 on x_{k+1} of every continuity row and, for the Ding families (calcium affine in
+    // its start value, cfx_kernels.h:integrate), dCn+/dCn0 = cna[m S]
+    h->jconst.assign(h->jrow.size(), 0);
+    if (!colloc)
+        for (int k = 0; k < N; ++k) {
+            for (int r = 0; r < nx; ++r) h->jconst[(size_t)k * nnzk + kp.jneg[r]] = 1;
+            if (!is_int(h->model) && kp.jpos[0][0] >= 0) h->jconst[(size_t)k * nnzk + kp.jpos[0][0]] = 1;
+        }
     auto hput = [&](int r, int c) {
         h->hrow.push_back(r);
         h->hcol.push_back(c);
@@ -849,13 +861,32 @@ extern "C" int cfx_hess_structure(const cfx_handle* h, int32_t* row, int32_t* co
 // ------------------------------------------------------------------------------------------------------
 // evaluation
 // ------------------------------------------------------------------------------------------------------
-static hipError_t launch_shooting(cfx_handle* h, bool derivs, const double* V, double* G, double* J) {
+static hipError_t launch_shooting(cfx_handle* h, bool derivs, const double* V, double* G, double* J, bool keep) {
     if (h->colloc) return launch_colloc(h->model, h->tmax, h->kp, V, G, derivs ? J : nullptr, h->stream);
-    if (is_int(h->model)) return launch_shooting_hmed(h->model, h->scheme, derivs, h->tmax, h->kp, V, G, J, h->stream);
+    KParams kp = h->kp;
+    kp.keepc = keep ? 1 : 0;
+    if (is_int(h->model)) return launch_shooting_hmed(h->model, h->scheme, derivs, h->tmax, kp, V, G, J, h->stream);
     // 16-byte lane accesses need 16-byte aligned buffers (B % NI == 0 keeps every row aligned)
     auto aligned = [](const void* p) { return ((uintptr_t)p & 15u) == 0; };
     const int ni = (aligned(V) && aligned(G) && aligned(J)) ? (derivs ? h->ni : h->ni_g) : 1;
-    return launch_shooting_ding(h->model, h->scheme, derivs, ni, h->kp, V, G, J, h->stream);
+    return launch_shooting_ding(h->model, h->scheme, derivs, ni, kp, V, G, J, h->stream);
+}
+
+// CFX_KEEP_CONSTANT_JAC: skip the constant J_g values when the buffer the kernels write holds them — the caller's
+// buffer on the direct device path (the caller's contract), the handle's staging buffer once a full evaluation has
+// filled it.  Whether the next staged evaluation may skip is recorded here.
+static bool keep_constants(cfx_handle* h, uint32_t flags, const double* J) {
+    if (!J) return false;
+    const bool staged = !(flags & CFX_DEVICE) || is_aos(h, h->sz.nnz_jac);
+    const bool keep = (flags & CFX_KEEP_CONSTANT_JAC) && (!staged || h->jconst_staged);
+    if (staged) h->jconst_staged = true;
+    return keep;
+}
+
+extern "C" int cfx_jac_constant_mask(const cfx_handle* h, uint8_t* mask) {
+    if (!h || !mask) return CFX_EINVAL;
+    std::memcpy(mask, h->jconst.data(), h->jconst.size());
+    return CFX_OK;
 }
 
 // Hmed sliding-window rows of g / J_g (k_slide; nothing for the other families)
@@ -917,7 +948,7 @@ extern "C" int cfx_eval_all(cfx_handle* h, const double* v, double* g, double* j
     double* GR = grad ? stage_out(h, S_GRAD, grad, h->sz.nv, flags, &rc) : nullptr;
     if (rc != CFX_OK) return rc;
     if (G || J) {
-        CFX_HIP(h, launch_shooting(h, J != nullptr, V, G, J));
+        CFX_HIP(h, launch_shooting(h, J != nullptr, V, G, J, keep_constants(h, flags, J)));
         launch_slide(h, V, G, J);
     }
     CFX_HIP(h, launch_objective(h, V, F, GR));
@@ -998,7 +1029,9 @@ extern "C" int cfx_eval_all_h(cfx_handle* h, const double* v, const double* obj_
     double* H = stage_out(h, S_OUT, hess, h->sz.nnz_hess, flags, &rc);
     if (rc != CFX_OK || !G || !J || !H) return rc != CFX_OK ? rc : fail(h, CFX_EINVAL, "cfx_eval_all_h: staging");
     // one launch: the interval's second-order jets carry the g rows and the J_g columns too
-    CFX_HIP(h, launch_hessian(h->model, h->scheme, h->tmax, h->kp, h->d_htasks, h->n_htasks, h->hbs, V, LAM, H, G, J,
+    KParams kp = h->kp;
+    kp.keepc = keep_constants(h, flags, J) ? 1 : 0;
+    CFX_HIP(h, launch_hessian(h->model, h->scheme, h->tmax, kp, h->d_htasks, h->n_htasks, h->hbs, V, LAM, H, G, J,
                               h->stream));
     launch_slide(h, V, G, J);
     CFX_HIP(h, launch_objective(h, V, F, GR));
@@ -1427,6 +1460,9 @@ extern "C" int cfx_msk_create(const cfx_msk_problem* p, cfx_handle** out) {
     h->sz.nv = (int64_t)N * nz + nx + (ns ? p->n_params : 0);
     h->sz.ng = mrow;
     h->sz.nnz_jac = (int64_t)h->jrow.size();
+    h->jconst.assign(h->jrow.size(), 0);  // the -1 on x_{k+1} of every continuity row
+    for (int k = 0; k < N; ++k)
+        for (int r = 0; r < nx; ++r) h->jconst[(size_t)k * nnzk + G.jneg[r]] = 1;
     h->sz.nnz_hess = (int64_t)h->hrow.size();
     h->sz.nx = nx;
     h->sz.nu = nu;
@@ -1489,6 +1525,7 @@ static int msk_eval_all(cfx_handle* h, const double* v, double* g, double* jac, 
     if (rc != CFX_OK) return rc;
     if (G || J) {
         MskParams P = h->mp;
+        P.keepc = keep_constants(h, flags, J) ? 1 : 0;
         if (J) {  // per-stage Jacobian coefficients (and stage values) between the g + J_g launches
             const size_t nw = h->msk_stash ? msk_hess_work_host(h->msk_nq, h->msk_nm, P.nx, P.nz, P.nz * (P.nz + 1) / 2,
                                                                 B, P.N, P.Q)

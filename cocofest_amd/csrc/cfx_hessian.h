@@ -200,7 +200,7 @@ __global__ void __launch_bounds__(256) k_hessian(const KParams P, const HTask* _
                 const int g = sl < bs ? gd[sl] : -1;
                 if (g < 0) continue;
                 if constexpr (LIN) {
-                    if (g == 0 && P.jpos[0][0] >= 0) J[jb + (jo + P.jpos[0][0]) * ES] = P.cna[end];
+                    if (g == 0 && P.jpos[0][0] >= 0 && !P.keepc) J[jb + (jo + P.jpos[0][0]) * ES] = P.cna[end];
                 }
 #pragma unroll
                 for (int r = R0; r < NX; ++r) {
@@ -215,7 +215,7 @@ __global__ void __launch_bounds__(256) k_hessian(const KParams P, const HTask* _
             for (int r = 0; r < NX; ++r) {
                 const double phi = (LIN && r == 0) ? fma(P.cna[end], cn0.v, cnb[end]) : x[r].v;
                 G[lb + (int64_t)(k * P.ngk + r) * ES] = phi - Vat(xn + r);
-                J[jb + (jo + P.jneg[r]) * ES] = -1.0;
+                if (!P.keepc) J[jb + (jo + P.jneg[r]) * ES] = -1.0;
             }
         }
     }

@@ -554,9 +554,10 @@ __device__ __forceinline__ void wave_sync() {
 }
 
 constexpr int kSchurStage = 2048;  // Cc non-zeros / active-slot entries staged in LDS (else read from global)
-// Products Cc(z) * (A^-1 Cr)(., j) of every Cc non-zero z and border column j, formed by all threads at once before
-// the S entries sum them: the per-entry loops otherwise walk their row's non-zeros with one dependent L2 load each
-// (cfg 3 at batch 1: 29.6 us per call, of a ~180 us iteration)
+// Operands (A^-1 Cr)(., j) of every Cc non-zero z and border column j, gathered by all threads at once before the S
+// entries sum their products: the per-entry loops otherwise walk their row's non-zeros with one dependent L2 load each
+// (cfg 3 at batch 1: 29.6 us per call, of a ~180 us iteration).  The sums keep the fused multiply-subtract of the
+// ungathered loop, so the results are bit-identical to it (the interior point's trajectories are sensitive to rounding)
 constexpr int kSchurProd = 1536;
 
 __global__ void __launch_bounds__(kIB) k_ipm_schur(const IpmK K, int factor) {
@@ -588,11 +589,11 @@ __global__ void __launch_bounds__(kIB) k_ipm_schur(const IpmK K, int factor) {
     auto slot = [&](int q, int j) { return staged ? slt[q * np + j] : K.sl[q * np + j]; };
     const bool pstage = staged && K.ncc * np <= kSchurProd && K.ncc <= kSchurProd;
     if (factor) {
-        if (pstage) {  // every product at once (independent loads), then the sums from LDS
+        if (pstage) {  // every operand at once (independent loads), then the sums from LDS
             for (int e = t; e < K.ncc * np; e += kIB) {
                 const int z = e / np, j = e - z * np;
                 const int q = ccq[z], c = slt[q * np + j];
-                prod[e] = c >= 0 ? ccv[z] * X[q * nb + (int64_t)c * nA + cca[z]] : 0.0;
+                prod[e] = c >= 0 ? X[q * nb + (int64_t)c * nA + cca[z]] : 0.0;
             }
             __syncthreads();
         }
@@ -601,10 +602,10 @@ __global__ void __launch_bounds__(kIB) k_ipm_schur(const IpmK K, int factor) {
             double acc = K.Db[b * np * np + e];
             for (int z = K.ccr_ptr[i]; z < K.ccr_ptr[i + 1]; ++z) {
                 if (pstage) {
-                    acc -= prod[z * np + j];
+                    acc = fma(-ccv[z], prod[z * np + j], acc);
                 } else {
                     const int q = cq(z), c = slot(q, j);
-                    if (c >= 0) acc -= cval(z) * X[q * nb + (int64_t)c * nA + ca(z)];
+                    if (c >= 0) acc = fma(-cval(z), X[q * nb + (int64_t)c * nA + ca(z)], acc);
                 }
             }
             S[i][j] = acc;
@@ -652,8 +653,8 @@ __global__ void __launch_bounds__(kIB) k_ipm_schur(const IpmK K, int factor) {
         if (t < np) piv[t] = Sp[t];
         __syncthreads();
     }
-    if (pstage) {  // Cc y products at once (the factor phase's reads of prod are behind the barriers above)
-        for (int z = t; z < K.ncc; z += kIB) prod[z] = ccv[z] * rb[ccq[z] * nA + cca[z]];
+    if (pstage) {  // the y operands of Cc y at once (the factor phase's reads of prod are behind the barriers above)
+        for (int z = t; z < K.ncc; z += kIB) prod[z] = rb[ccq[z] * nA + cca[z]];
         __syncthreads();
     }
     if (t < 64) {  // x_p = S^-1 (r_p - sum_q Cc_q y_q), lane i holding component i (getrs)
@@ -661,7 +662,7 @@ __global__ void __launch_bounds__(kIB) k_ipm_schur(const IpmK K, int factor) {
         if (t < np) {
             x = rb[PA + t];
             for (int z = K.ccr_ptr[t]; z < K.ccr_ptr[t + 1]; ++z)
-                x -= pstage ? prod[z] : cval(z) * rb[cq(z) * nA + ca(z)];
+                x = fma(-cval(z), pstage ? prod[z] : rb[cq(z) * nA + ca(z)], x);
         }
         for (int k = 0; k < np; ++k) {  // row interchanges in order
             const int p = piv[k];
@@ -1985,6 +1986,10 @@ struct cfx_ipm {
     // staging for host inputs / outputs
     double *d_fv = nullptr, *d_yo = nullptr, *d_kkt = nullptr;
     int32_t *d_conv = nullptr, *d_its = nullptr;
+    // J_g's constant values (cfx_jac_constant_mask) stay in K.jac after the first full evaluation: later evaluations
+    // pass CFX_KEEP_CONSTANT_JAC (CFX_IPM_KEEPJ=0 turns it off, for A/B runs)
+    bool keepj = true, jac_filled = false;
+    uint32_t jac_flags() const { return CFX_DEVICE | (keepj && jac_filled ? CFX_KEEP_CONSTANT_JAC : 0u); }
 };
 
 #define IPM_HIP(s, call)                                                         \
@@ -2538,6 +2543,7 @@ extern "C" int cfx_ipm_create(cfx_handle* h, const double* lb, const double* ub,
     }
     if (s->h_pub) std::memset(s->h_pub, 0, 16 * sizeof(int32_t));
     if (const char* e = std::getenv("CFX_IPM_SYNC")) s->poll = std::strcmp(e, "stream") != 0;
+    if (const char* e = std::getenv("CFX_IPM_KEEPJ")) s->keepj = std::atoi(e) != 0;
     if (rc == CFX_OK && hipHostMalloc((void**)&s->h_cnt, 4 * sizeof(int32_t), hipHostMallocDefault) != hipSuccess) {
         rc = CFX_ENOMEM;
         s->err = "hipHostMalloc failed";
@@ -2597,7 +2603,8 @@ struct Run {
         return CFX_OK;
     }
     int eval_full(double* v) {
-        IPM_CFX(s, cfx_eval_all(s->h, v, s->K.graw, s->K.jac, s->K.fraw, s->K.grad, CFX_DEVICE));
+        IPM_CFX(s, cfx_eval_all(s->h, v, s->K.graw, s->K.jac, s->K.fraw, s->K.grad, s->jac_flags()));
+        s->jac_filled = true;
         s->st.eval_all++;
         return CFX_OK;
     }
@@ -2753,7 +2760,8 @@ static int ipm_solve(cfx_ipm* s, const double* v0, const double* fixed_values, d
         // formed them): g, J_g, f, grad f and the Hessian of the new iterate from one call
         const bool fused = it > 0 && !reinit && !K.lbfgs && K.m > 0;
         if (fused) {
-            IPM_CFX(s, cfx_eval_all_h(s->h, K.vx, K.of, K.ysc, K.graw, K.jac, K.fraw, K.grad, K.hv, CFX_DEVICE));
+            IPM_CFX(s, cfx_eval_all_h(s->h, K.vx, K.of, K.ysc, K.graw, K.jac, K.fraw, K.grad, K.hv, s->jac_flags()));
+            s->jac_filled = true;
             s->st.eval_all++;
             s->st.eval_h++;
         } else {

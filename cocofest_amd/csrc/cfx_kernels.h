@@ -52,6 +52,8 @@ struct KParams {
     int32_t n_params;
     int32_t kpt;     // shooting intervals per thread
     int32_t ifast;   // shooting launch: interval chunks on grid.x (fast), instance blocks on grid.y
+    int32_t keepc;   // CFX_KEEP_CONSTANT_JAC: the instance- and point-invariant J_g values (the -1 on x_{k+1}, the
+                     // Ding calcium row's cna) are not stored; the output already holds them (cfx_jac_constant_mask)
     double dt, h;
     // model constants (reciprocals precomputed on the host)
     double inv_tauc, tau2, km_rest, tau1_rest, a_rest, a_scale, pd0, pdt;
@@ -526,7 +528,9 @@ __device__ __forceinline__ void shoot_run(const KParams& P, const double* __rest
                     const int gd = chunk * D + j;
                     if (gd < P.nz) {
                         const int pos = P.jpos[r][gd];
-                        if (pos >= 0) {
+                        // the Ding calcium row's only entry, dCn+/dCn0 = cna[m S], is constant (integrate)
+                        const bool cst = !is_int(MODEL) && r == 0 && gd == 0 && P.keepc;
+                        if (pos >= 0 && !cst) {
                             double t[NI];
 #pragma unroll
                             for (int i = 0; i < NI; ++i) t[i] = st[i].xd[r][j];
@@ -534,7 +538,7 @@ __device__ __forceinline__ void shoot_run(const KParams& P, const double* __rest
                         }
                     }
                 }
-                if (chunk == 0) st_lane_const<NI>(J + jb + (jo + P.jneg[r]) * ES, -1.0);
+                if (chunk == 0 && !P.keepc) st_lane_const<NI>(J + jb + (jo + P.jneg[r]) * ES, -1.0);
             }
         }
 #pragma unroll

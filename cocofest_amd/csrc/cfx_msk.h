@@ -92,6 +92,16 @@ MSK_HD Dep mlog(Dep a) { return a; }
 MSK_HD Dep msqrt(Dep a) { return a; }
 MSK_HD Dep msin(Dep a) { return a; }
 MSK_HD Dep mcos(Dep a) { return a; }
+// sin and cos of one angle from one argument reduction (two separate calls reduce twice)
+MSK_HD void msincos(double x, double* s, double* c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    sincos(x, s, c);
+#else
+    *s = std::sin(x);
+    *c = std::cos(x);
+#endif
+}
+MSK_HD void msincos(Dep a, Dep* s, Dep* c) { *s = *c = a; }
 
 template <int D>
 CFX_HD Dual<D> dchain(const Dual<D>& a, double f0, double f1) {
@@ -108,12 +118,12 @@ CFX_HD Dual<D> mexp(const Dual<D>& a) {
 }
 template <int D>
 CFX_HD Dual<D> mlog(const Dual<D>& a) {
-    return dchain(a, log(a.v), 1.0 / a.v);
+    return dchain(a, log(a.v), drcp(a.v));
 }
 template <int D>
 CFX_HD Dual<D> msqrt(const Dual<D>& a) {
     const double s = sqrt(a.v);
-    return dchain(a, s, 0.5 / s);
+    return dchain(a, s, 0.5 * drcp(s));
 }
 template <int D>
 CFX_HD Dual<D> msin(const Dual<D>& a) {
@@ -122,6 +132,13 @@ CFX_HD Dual<D> msin(const Dual<D>& a) {
 template <int D>
 CFX_HD Dual<D> mcos(const Dual<D>& a) {
     return dchain(a, cos(a.v), -sin(a.v));
+}
+template <int D>
+CFX_HD void msincos(const Dual<D>& a, Dual<D>* s, Dual<D>* c) {
+    double sv, cv;
+    msincos(a.v, &sv, &cv);
+    *s = dchain(a, sv, cv);
+    *c = dchain(a, cv, -sv);
 }
 template <int D>
 CFX_HD Jet<D> mexp(const Jet<D>& a) {
@@ -147,6 +164,13 @@ template <int D>
 CFX_HD Jet<D> mcos(const Jet<D>& a) {
     const double s = sin(a.v), c = cos(a.v);
     return jchain(a, c, -s, -c);
+}
+template <int D>
+CFX_HD void msincos(const Jet<D>& a, Jet<D>* s, Jet<D>* c) {
+    double sv, cv;
+    msincos(a.v, &sv, &cv);
+    *s = jchain(a, sv, cv, -sv);
+    *c = jchain(a, cv, -sv, -cv);
 }
 
 // ---- problem constants ----------------------------------------------------------------------------------------
@@ -183,6 +207,7 @@ struct MskParams {
     int32_t N, m, nx, nu, nz, Q, nnzk, nhk, residual, npw;
     int32_t T, ngk;      // truncation; rows per interval (nx continuity rows, then the Hmed sliding-window rows)
     int32_t kpb;         // k_msk_tangents_lds: consecutive intervals per block (fixed by cfx_msk_create)
+    int32_t keepc;       // CFX_KEEP_CONSTANT_JAC: the -1 on x_{k+1} is not stored (the output holds it already)
     double dt, h;
     // calcium sums [N][Q][NM] at every RK stage time (host, reference operation order); Hmed2018: the per-pulse
     // coefficients r_i exp(-(t - t_i) / tau_c) [N][Q][NM][TMAX] of cs = sum_i coef_i lambda(I_i)
@@ -315,7 +340,8 @@ MSK_HD void msk_frames(const MskGeom& G, const S* q, S (*R)[9], S (*o)[3], S (*z
                           R[j - 1][r * 3 + 2] * G.t[j][2];
             }
         }
-        const S c = mcos(q[j]), s = msin(q[j]);
+        S s, c;
+        msincos(q[j], &s, &c);
         // R_j = Rb Rot_z(q): columns 0 and 1 mix, the axis column 2 is kept (cfx_msk_create expresses every joint
         // as a rotation about its frame's z axis, G.axis[j] == 2)
 #pragma unroll
@@ -759,7 +785,7 @@ __global__ void __launch_bounds__(256) k_msk_shooting(const MskParams P, const M
                     if (pos >= 0) J[(jb + pos) * B + b] = x[r].d[d];
                 }
             }
-        if (blockIdx.z == 0) {
+        if (blockIdx.z == 0 && !P.keepc) {
 #pragma unroll
             for (int r = 0; r < NX; ++r) J[(jb + G.jneg[r]) * B + b] = -1.0;
         }
@@ -1033,7 +1059,7 @@ __global__ void __launch_bounds__(256) k_msk_tangents(const MskParams P, const M
         const int pos = G.jpos[r * kMskMaxZ + col];
         if (pos >= 0) J[(jb + pos) * B + b] = tx[r];
     }
-    if (col == 0) {
+    if (col == 0 && !P.keepc) {
 #pragma unroll
         for (int r = 0; r < NX; ++r) J[(jb + G.jneg[r]) * B + b] = -1.0;
     }
@@ -1171,7 +1197,7 @@ __global__ void __launch_bounds__(32 * kMskLdsCols) k_msk_tangents_lds(const Msk
                 const int pos = G.jpos[r * kMskMaxZ + col];
                 if (pos >= 0) msk_st_j(J + (jb + pos) * B + b, tx[r]);
             }
-            if (col == 0) {
+            if (col == 0 && !P.keepc) {
 #pragma unroll
                 for (int r = 0; r < NX; ++r) msk_st_j(J + (jb + G.jneg[r]) * B + b, -1.0);
             }

@@ -79,6 +79,11 @@ extern "C" {
    g + J_g pass).  Shooting transcriptions, eval_g / eval_jac_g / eval_f / eval_grad_f / eval_all only. */
 #define CFX_LAYOUT_TILED64 2
 #define CFX_DEVICE 1u /* pointers are device pointers; call is asynchronous on the handle stream */
+/* eval_jac_g / eval_all / eval_all_h: the J_g values cfx_jac_constant_mask lists are not written — the output buffer
+   already holds them from an earlier full evaluation (with CFX_DEVICE on a buffer the kernels write directly: the
+   caller's buffer; otherwise the handle's staging buffer, filled by the first evaluation).  Ipopt's TNLP contract
+   asks for every value on every call: callers bound by it leave this flag off. */
+#define CFX_KEEP_CONSTANT_JAC 2u
 
 /* objective terms (fes_ocp.py:531-569) */
 #define CFX_OBJ_LAGRANGE 0 /* weight * dt * (z_k - target_k)^2 summed over the node range */
@@ -170,6 +175,10 @@ int cfx_get_launch_shape(const cfx_handle *h, cfx_launch_shape *out);
 /* ---- sparsity (Ipopt eval_jac_g / eval_h with values == NULL) ---------------------------------- */
 int cfx_jac_structure(const cfx_handle *h, int32_t *row, int32_t *col);  /* nnz_jac entries */
 int cfx_hess_structure(const cfx_handle *h, int32_t *row, int32_t *col); /* nnz_hess, row >= col */
+/* mask[nnz_jac] = 1 for the J_g values that depend on neither the instance nor the point (the -1 on x_{k+1} of every
+   continuity row; for the Ding families also dCn+/dCn0, the calcium state being affine in its start value), i.e. the
+   values CFX_KEEP_CONSTANT_JAC leaves in place (cfg 2: 60 of 100 per instance).  Collocation handles report none. */
+int cfx_jac_constant_mask(const cfx_handle *h, uint8_t *mask);
 
 /* ---- NLP callbacks over the whole batch -------------------------------------------------------- */
 int cfx_eval_g(cfx_handle *h, const double *v, double *g, uint32_t flags);         /* eval_g */
