@@ -15,7 +15,7 @@ import numpy as np
 
 LIB_PATH = pathlib.Path(__file__).with_name("libcfx.so")
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 OK, EINVAL, EHIP, ENOMEM, EUNSUPPORTED, ENODEV = 0, -1, -2, -3, -4, -5
 MODEL_IDS = {
     "ding2003": 0,
@@ -113,7 +113,8 @@ class IpmOptions(C.Structure):
                 ("watchdog_trial_iter_max", C.c_int32), ("hessian_approximation", C.c_int32),
                 ("limited_memory_max_history", C.c_int32), ("restoration", C.c_int32),
                 ("max_resto_iter", C.c_int32), ("resto_penalty", C.c_double),
-                ("required_infeasibility_reduction", C.c_double)]
+                ("required_infeasibility_reduction", C.c_double), ("filter_reset_trigger", C.c_int32),
+                ("max_filter_resets", C.c_int32)]
 
 
 class IpmStats(C.Structure):

@@ -48,7 +48,10 @@ struct Scal {
         theta_r, a_r;
     double wd_theta, wd_phi, wd_dphi, wd_ap, wd_mu;  // watchdog reference: the iterate where it started
     int32_t done, acc, iters, fpos, accepted, armijo, soc, reinit, todo;
-    int32_t wd_short, wd_on, wd_trial, skip_first, forced, pad[2];
+    int32_t wd_short, wd_on, wd_trial, skip_first, forced;
+    int32_t rejf, nsucc, nreset;  // filter reset heuristic: last rejection by the filter, successive such iterations,
+                                  // resets done
+    int32_t pad;
     // limited-memory Hessian (L-BFGS): sigma, pairs held, next ring slot, previous iterate saved
     double lsig;
     int32_t lcount, lhead, lprev, lpad;
@@ -261,7 +264,8 @@ __device__ bool filter_dominated(const double* filt, double tt, double pt, doubl
 // Ipopt's filter test of a trial (tt = ||c||_1, pt = barrier objective) against the current point (theta, phi,
 // directional derivative dphi, step alpha): (accepted, by the Armijo / f-type rule)
 __device__ void filter_core(const IpmK& K, const double* filt, double theta, double phi, double dphi, double theta_max,
-                            double theta_min, double tt, double pt, double alpha, double* sh, bool& ok, bool& arm) {
+                            double theta_min, double tt, double pt, double alpha, double* sh, bool& ok, bool& arm,
+                            bool* rejf = nullptr) {
     const bool dominated = filter_dominated(filt, tt, pt, sh);
     const bool finite = isfinite(pt) && isfinite(tt);
     const bool switching = (dphi < 0) && (alpha * pow(clamp_lo(-dphi, 0.0), 2.3) > 1.0 * pow(theta, 1.1)) &&
@@ -272,16 +276,18 @@ __device__ void filter_core(const IpmK& K, const double* filt, double theta, dou
     const bool suff = (tt - (1 - 1e-5) * theta <= 10 * kEps * theta) || ((pt - phi) + 1e-5 * theta <= tol_phi);
     ok = finite && (tt <= theta_max) && !dominated && (switching ? armijo_ok : suff);
     arm = switching && armijo_ok;
+    // rejected by the filter alone: it passed Ipopt's theta_max and Armijo / sufficient-decrease tests
+    if (rejf) *rejf = finite && (tt <= theta_max) && dominated && (switching ? armijo_ok : suff);
 }
 
 // solver.py _filter_accept: (accepted, by the Armijo / f-type rule) for a trial with tt = ||g||_1, pt = barrier
 __device__ void filter_accept(const IpmK& K, const Scal& S, const double* filt, double tt, double pt, double alpha,
-                              double* sh, bool& ok, bool& arm) {
+                              double* sh, bool& ok, bool& arm, bool* rejf = nullptr) {
     // in the watchdog, trial points are judged against the iterate where it started (with its full step length)
     const double theta = S.wd_on ? S.wd_theta : S.theta, phi = S.wd_on ? S.wd_phi : S.phi;
     const double dphi = S.wd_on ? S.wd_dphi : S.dphi;
     if (S.wd_on) alpha = S.wd_ap;
-    filter_core(K, filt, theta, phi, dphi, S.theta_max, S.theta_min, tt, pt, alpha, sh, ok, arm);
+    filter_core(K, filt, theta, phi, dphi, S.theta_max, S.theta_min, tt, pt, alpha, sh, ok, arm, rejf);
 }
 
 // x -> full decision vector (fixed entries are already in place)
@@ -856,6 +862,7 @@ __global__ void __launch_bounds__(kIB) k_ipm_dir(const IpmK K, int it) {
         S.armijo = 0;
         S.soc = 0;
         S.forced = 0;
+        S.rejf = 0;  // Ipopt's InitThisLineSearch
     }
     double* xacc = K.xacc + b * nf;
     double* xt = K.xt + b * nf;
@@ -883,8 +890,9 @@ __global__ void __launch_bounds__(kIB) k_ipm_accept(const IpmK K, int ls, int sl
     tt = breduce(tt, OpSum(), sh);
     const double* xt = K.xt + b * nf;
     const double pt = barrier_obj(K, b, xt, K.ft[b] * S.sf, S.mu, sh);
-    bool ok, arm;
-    filter_accept(K, S, K.filt + b * kFilt * 2, tt, pt, S.alpha, sh, ok, arm);
+    bool ok, arm, rejf;
+    filter_accept(K, S, K.filt + b * kFilt * 2, tt, pt, S.alpha, sh, ok, arm, &rejf);
+    const bool rej_here = rejf && !S.accepted;
     ok = ok && !S.accepted;
     // a watchdog iteration takes its full step whether or not it is acceptable (no corrections, no backtracking)
     const bool forced = ls == 0 && S.wd_on && !ok && !S.accepted;
@@ -904,6 +912,7 @@ __global__ void __launch_bounds__(kIB) k_ipm_accept(const IpmK K, int ls, int sl
             S.soc = soc;
             S.theta_soc = tt;
         }
+        if (rej_here) S.rejf = 1;
         if (ok) {
             S.armijo = arm;
             S.accepted = 1;
@@ -989,8 +998,9 @@ __global__ void __launch_bounds__(kIB) k_ipm_soc_accept(const IpmK K, int slot) 
     tt = breduce(tt, OpSum(), sh);
     const double* xr = K.xr + b * nf;
     const double pt = barrier_obj(K, b, xr, K.ft[b] * S.sf, S.mu, sh);
-    bool okc, armc;
-    filter_accept(K, S, K.filt + b * kFilt * 2, tt, pt, S.alpha, sh, okc, armc);
+    bool okc, armc, rejfc;
+    filter_accept(K, S, K.filt + b * kFilt * 2, tt, pt, S.alpha, sh, okc, armc, &rejfc);
+    const bool rej_here = rejfc && S.soc && !S.accepted;
     okc = okc && S.soc && (S.a_c >= 0.99);
     if (okc) {
         double* xacc = K.xacc + b * nf;
@@ -1004,6 +1014,7 @@ __global__ void __launch_bounds__(kIB) k_ipm_soc_accept(const IpmK K, int slot) 
             S.armijo = armc;
             S.accepted = 1;
         }
+        if (rej_here) S.rejf = 1;
         S.soc = S.soc && !okc && (S.a_c >= 0.99) && (tt <= K.o.kappa_soc * S.theta_soc);
         S.theta_soc = tt;
     }
@@ -1145,6 +1156,25 @@ __global__ void __launch_bounds__(kIB) k_ipm_update(const IpmK K, int resto) {
     const bool wd_back = forced && wd_trial > K.o.watchdog_trial_iter_max;
     const bool shortened = S.accepted && !forced && S.alpha < S.a_p;
     double* filt = K.filt + b * kFilt * 2;
+    // Ipopt's filter reset heuristic (FilterLSAcceptor::UpdateForNextIteration), before the augmentation
+    int nsucc = S.nsucc;
+    bool freset = false;
+    if (!S.done && S.accepted && !forced && S.nreset < K.o.max_filter_resets) {
+        if (S.rejf) {
+            if (++nsucc >= K.o.filter_reset_trigger) {
+                freset = true;
+                nsucc = 0;
+            }
+        } else {
+            nsucc = 0;
+        }
+    }
+    if (freset)
+        for (int k = threadIdx.x; k < kFilt; k += kIB) {
+            filt[2 * k] = INFINITY;
+            filt[2 * k + 1] = -INFINITY;
+        }
+    __syncthreads();
     if (threadIdx.x == 0 && grow) {
         const int k = S.fpos % kFilt;
         filt[2 * k] = (1 - 1e-5) * S.theta;
@@ -1232,6 +1262,8 @@ __global__ void __launch_bounds__(kIB) k_ipm_update(const IpmK K, int resto) {
         }
         S.alpha = alpha;
         S.iters += step;
+        S.nsucc = nsucc;
+        S.nreset += freset;
         S.wd_trial = wd_trial;
         S.wd_on = S.wd_on && !wd_ok && !wd_back;
         S.wd_short = (wd_ok || wd_back || failed || !shortened) ? 0 : S.wd_short + 1;
@@ -2068,6 +2100,8 @@ extern "C" void cfx_ipm_default_options(cfx_ipm_options* o) {
     o->max_resto_iter = 200;
     o->resto_penalty = 1000.0;
     o->required_infeasibility_reduction = 0.9;
+    o->filter_reset_trigger = 5;
+    o->max_filter_resets = 0;  // Ipopt: 5; off here
 }
 
 // CSR of `key` (values in [0, nkeys)) with the sources of each key in increasing source order

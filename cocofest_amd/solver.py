@@ -64,6 +64,12 @@ class IpmOptions:
     max_resto_iter: int = 200
     resto_penalty: float = 1000.0            # Ipopt resto_penalty_parameter (rho)
     required_infeasibility_reduction: float = 0.9
+    # Ipopt's filter reset heuristic: after filter_reset_trigger successive iterations whose line search last rejected a
+    # trial point because of the filter, the filter is cleared, at most max_filter_resets times (0: off).  Ipopt's
+    # default is 5 resets; off by default here (measured on the fatigue-family RK4 test problem
+    # and cfg 5's multistart)
+    filter_reset_trigger: int = 5
+    max_filter_resets: int = 0
     verbose: bool = False
 
 
@@ -82,7 +88,8 @@ class Solver:
                     "_watchdog_shortened_iter_trigger": "watchdog_shortened_iter_trigger",
                     "_watchdog_trial_iter_max": "watchdog_trial_iter_max", "_max_resto_iter": "max_resto_iter",
                     "_resto_penalty_parameter": "resto_penalty",
-                    "_required_infeasibility_reduction": "required_infeasibility_reduction"}
+                    "_required_infeasibility_reduction": "required_infeasibility_reduction",
+                    "_filter_reset_trigger": "filter_reset_trigger", "_max_filter_resets": "max_filter_resets"}
         _IGNORED = {"show_online_optim", "show_options", "_print_level", "_linear_solver", "_nlp_scaling_method",
                     "_check_derivatives_for_naninf", "_c_compile", "_print_timing_statistics", "_output_file",
                     "_constr_viol_tol", "_dual_inf_tol", "_compl_inf_tol"}
@@ -441,6 +448,9 @@ class BatchedIpm:
         wd_trial = torch.zeros((B,), dtype=torch.int64, device=self.dev)
         skip_first = torch.zeros((B,), dtype=torch.bool, device=self.dev)
         wd = None
+        # Ipopt's filter reset heuristic: successive iterations whose last rejection was the filter's, resets done
+        f_succ = torch.zeros((B,), dtype=torch.int64, device=self.dev)
+        f_resets = torch.zeros((B,), dtype=torch.int64, device=self.dev)
 
         self._v_template = v
 
@@ -550,6 +560,7 @@ class BatchedIpm:
             accepted = done.clone()
             forced = torch.zeros_like(done)
             armijo_step = torch.zeros_like(done)
+            rej_f = torch.zeros_like(done)  # Ipopt's InitThisLineSearch
             x_acc = x.clone()
             dx_acc = dx.clone()
             for ls in range(opt.max_backtrack):
@@ -558,6 +569,7 @@ class BatchedIpm:
                 a_test = torch.where(wd_on, wd["a_p"], alpha) if wd is not None else alpha
                 ok, arm = self._filter_accept(gt, ft, xt, r_theta, r_phi, r_dphi, a_test, mu, theta_max, theta_min,
                                               filt)
+                rej_f = rej_f | (self._rejf & ~accepted)
                 ok = ok & ~accepted
                 if ls == 0:
                     # watchdog iterations take the full step whether or not it is acceptable (no corrections)
@@ -579,6 +591,7 @@ class BatchedIpm:
                         gc, fc = self._scaled_gf(full(xc))
                         okc, armc = self._filter_accept(gc, fc, xc, theta, phi, dphi, alpha, mu, theta_max,
                                                         theta_min, filt)
+                        rej_f = rej_f | (self._rejf & soc_try & ~accepted)
                         okc = okc & soc_try & (a_c >= 0.99)
                         x_acc = torch.where(okc[:, None], xc, x_acc)
                         dx_acc = torch.where(okc[:, None], (xc - x) / alpha.clamp(min=1e-300)[:, None], dx_acc)
@@ -604,6 +617,14 @@ class BatchedIpm:
             shortened = accepted & ~forced & (alpha < a_p)
             wd_short = torch.where(wd_ok | wd_back | failed | ~shortened, torch.zeros_like(wd_short), wd_short + 1)
             skip_first = wd_back.clone()
+            # Ipopt's filter reset heuristic (FilterLSAcceptor::UpdateForNextIteration), before the augmentation
+            upd = (~done) & accepted & ~forced & (f_resets < opt.max_filter_resets)
+            f_succ = torch.where(upd, torch.where(rej_f, f_succ + 1, torch.zeros_like(f_succ)), f_succ)
+            f_reset = upd & rej_f & (f_succ >= opt.filter_reset_trigger)
+            f_succ = torch.where(f_reset, torch.zeros_like(f_succ), f_succ)
+            f_resets = f_resets + f_reset.long()
+            filt = torch.where(f_reset[:, None, None], torch.tensor([np.inf, -np.inf], dtype=torch.float64,
+                                                                    device=self.dev), filt)
             # filter augmentation for h-type (non-Armijo) steps
             grow = (~done) & accepted & ~armijo_step & ~forced
             filt = torch.where(grow[:, None, None] & (torch.arange(filt.shape[1], device=self.dev) ==
@@ -975,6 +996,8 @@ class BatchedIpm:
             ((pt - phi) + 1e-5 * theta <= tol_phi)
         in_filter = ((tt[:, None] >= filt[:, :, 0]) & (pt[:, None] >= filt[:, :, 1])).any(1)
         ok = finite & (tt <= theta_max) & ~in_filter & torch.where(switching, armijo_ok, suff)
+        # rejected by the filter alone (Ipopt's last_rejection_due_to_filter: the other tests passed)
+        self._rejf = finite & (tt <= theta_max) & in_filter & torch.where(switching, armijo_ok, suff)
         return ok, switching & armijo_ok
 
     def close(self):
@@ -1014,7 +1037,7 @@ _NATIVE_OPTIONS = ("tol", "max_iter", "acceptable_tol", "acceptable_iter", "mu_i
                    "bound_push", "tau_min", "kappa_eps", "kappa_mu", "theta_mu", "s_max", "armijo", "max_backtrack",
                    "delta_c", "curv_min", "max_soc", "kappa_soc", "watchdog_shortened_iter_trigger",
                    "watchdog_trial_iter_max", "limited_memory_max_history", "max_resto_iter", "resto_penalty",
-                   "required_infeasibility_reduction")
+                   "required_infeasibility_reduction", "filter_reset_trigger", "max_filter_resets")
 _HESSIAN_APPROXIMATION = {"exact": 0, "limited-memory": 1}
 _RESTORATION = {"step": 0, "phase": 1, None: 1}
 

@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define CFX_ABI_VERSION 4
+#define CFX_ABI_VERSION 5
 
 /* return codes */
 #define CFX_OK 0
@@ -354,6 +354,12 @@ typedef struct cfx_ipm_options {
     int32_t max_resto_iter;                  /* 200 */
     double resto_penalty;                    /* rho, Ipopt resto_penalty_parameter: 1000 */
     double required_infeasibility_reduction; /* 0.9 */
+    /* Ipopt's filter reset heuristic (IpFilterLSAcceptor): when in filter_reset_trigger (5) successive iterations the
+       line search's last rejected trial point was rejected by the filter (it passed the Armijo / sufficient-decrease
+       test), the filter is cleared — at most max_filter_resets times per solve (Ipopt's default 5; default here 0:
+       off) */
+    int32_t filter_reset_trigger;
+    int32_t max_filter_resets;
 } cfx_ipm_options;
 #define CFX_HESSIAN_EXACT 0
 #define CFX_HESSIAN_LIMITED_MEMORY 1
