@@ -548,8 +548,16 @@ __device__ __forceinline__ void shoot_run(const KParams& P, const double* __rest
     }
 }
 
+// CFX_SHOOT_WPE: occupancy hint for the shooting kernel (waves per SIMD the register allocation must allow; A/B builds).
+// Measured with 8 (63 instead of 78 VGPRs, 6 -> 8 waves per SIMD, no spills): cfg 2 0.274 -> 0.277 ms, cfg 3 0.451 ->
+// 0.516 ms (profiles/round3/occupancy/wpe8_ab.jsonl); the default allocation is kept.
+#ifdef CFX_SHOOT_WPE
+#define CFX_SHOOT_ATTR __attribute__((amdgpu_waves_per_eu(CFX_SHOOT_WPE, CFX_SHOOT_WPE)))
+#else
+#define CFX_SHOOT_ATTR
+#endif
 template <int MODEL, int SCHEME, int D, int TMAX, int NI>
-__global__ void __launch_bounds__(256) k_shooting(const KParams P, const double* __restrict__ V,
+__global__ void __launch_bounds__(256) CFX_SHOOT_ATTR k_shooting(const KParams P, const double* __restrict__ V,
                                                   double* __restrict__ G, double* __restrict__ J) {
     const int64_t B = P.B;
     const unsigned bi = P.ifast ? blockIdx.y : blockIdx.x, bk = P.ifast ? blockIdx.x : blockIdx.y;
