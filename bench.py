@@ -360,7 +360,10 @@ def nmpc_section(device, n_windows, dist=None, world=1, rank=0, backend="nccl", 
         out["gathered_force_shape"] = [world] + list(F.shape)
     out.update({"wall_s": wall, "ms_per_horizon": wall / n_windows * 1e3,
                 "scenario_horizons_per_s": world * batch * n_windows / wall, "converged_frac": conv_frac,
-                "iterations_median": float(np.median(its)), "iterations_max": int(its.max())})
+                "iterations_median": float(np.median(its)), "iterations_max": int(its.max()),
+                # the interior point's share of a horizon (NativeIpm.solve wall-clock); the rest is the host's window
+                # bookkeeping (warm start shift, history, fixed values)
+                "solve_ms_per_horizon": float(np.sum(res.solve_wall)) / n_windows * 1e3})
     return out
 
 

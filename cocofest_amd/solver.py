@@ -623,6 +623,7 @@ class BatchedIpm:
             f_reset = upd & rej_f & (f_succ >= opt.filter_reset_trigger)
             f_succ = torch.where(f_reset, torch.zeros_like(f_succ), f_succ)
             f_resets = f_resets + f_reset.long()
+            self.filter_resets = f_resets.cpu().numpy()
             filt = torch.where(f_reset[:, None, None], torch.tensor([np.inf, -np.inf], dtype=torch.float64,
                                                                     device=self.dev), filt)
             # filter augmentation for h-type (non-Armijo) steps

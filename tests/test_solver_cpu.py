@@ -199,3 +199,26 @@ def test_restoration_phase_reduces_the_infeasibility():
     np.testing.assert_allclose((c - p + n).numpy(), 0.0, atol=1e-12 * float(c.abs().max()))
     np.testing.assert_allclose((muR / p + muR / n).numpy(), 2 * rho, rtol=1e-10)
     ipm.close()
+
+
+def test_filter_reset_heuristic():
+    """Ipopt's filter reset heuristic (off by default here): with a trigger of one iteration the filter is cleared
+    whenever the line search's last rejection was the filter's, at most max_filter_resets times; cfg 2 from the zero
+    initial guess (a long backtracking line search) still reaches the forward integration.  Solver.IPOPT maps
+    bioptim-style option names onto it."""
+    from cocofest_amd.solver import IpmOptions, Solver
+
+    cfg = cases.cfg2()
+    _, pb, ipm = _ipm(cfg, batch=1, filter_reset_trigger=1, max_filter_resets=3)
+    res = ipm.solve()
+    assert res.converged.all(), (res.kkt_error, res.iterations)
+    assert 1 <= int(ipm.filter_resets[0]) <= 3, ipm.filter_resets
+    c = O.model_constants("ding2003")
+    traj = O.ivp_integrate("ding2003", c, pb.rows, np.zeros((pb.n_shooting, 0)), 1.0, "RK1", 10)
+    X, _, _ = pb.unpack(res.v)
+    np.testing.assert_allclose(X[0].T, traj[:, ::10], rtol=1e-6, atol=1e-6)
+    _, _, off = _ipm(cfg, batch=1)
+    off.solve()
+    assert int(off.filter_resets[0]) == 0  # the default: off
+    o = Solver.IPOPT(_filter_reset_trigger=2, _max_filter_resets=5).apply(IpmOptions())
+    assert (o.filter_reset_trigger, o.max_filter_resets) == (2, 5)
