@@ -278,43 +278,94 @@ def convergence(device):
     return out
 
 
-def collocation_section(device, steps=50):
-    """The same cfg-2 problem transcribed by direct collocation (OdeSolver.COLLOCATION(4, "legendre"), bioptim's
-    default degree): g + J_g throughput of k_colloc over a device-resident SoA batch, and its algorithmic HBM
-    bandwidth (read v, write g and J_g values)."""
-    import torch
+COLLOCATION_BATCH = 1 << 18
 
+
+def build_collocation():
+    """cfg 2 transcribed by direct collocation (OdeSolver.COLLOCATION(4, "legendre"), bioptim's default degree; the
+    transcription north_star names; the reference accepts it at cocofest/optimization/fes_ocp.py:334-338)."""
     from cocofest_amd import ModelMaker, OcpFes, OdeSolver
 
     model = ModelMaker.create_model("ding2003", stim_time=[round(0.1 * i, 1) for i in range(10)],
                                     sum_stim_truncation=20)
-    ocp = OcpFes.prepare_ocp(model=model, final_time=1, objective={"end_node_tracking": 100},
-                             ode_solver=OdeSolver.COLLOCATION(4, "legendre"), n_shooting=20)
-    B = 1 << 18
-    h = ocp.nlp(batch=B, layout="soa", device=device)
+    return OcpFes.prepare_ocp(model=model, final_time=1, objective={"end_node_tracking": 100},
+                              ode_solver=OdeSolver.COLLOCATION(4, "legendre"), n_shooting=20)
+
+
+def collocation_synthetic(ocp, B, device, seed=7):
+    """Tiled (B / 64, nv, 64) decision vectors of the collocation cfg 2: Cn ~ U(0, 1.5), F ~ U(0, 250) at every node
+    and collocation point."""
+    import torch
+
+    gen = torch.Generator(device=device)
+    gen.manual_seed(seed)
+    v = torch.rand((ocp.nv, B), generator=gen, dtype=torch.float64, device=device)
+    v *= torch.tensor([1.5, 250.0] * (ocp.nv // 2), dtype=torch.float64, device=device)[:, None]
+    return to_tiled(v)
+
+
+def collocation_pmc():
+    """HBM bytes per launch of the collocation g + J_g kernel from the committed PMC summary, if any."""
+    f = ROOT / "profiles" / "pmc_traffic_collocation.json"
+    if not f.exists():
+        return None
+    try:
+        d = json.loads(f.read_text())
+        return d if d.get("batch") == COLLOCATION_BATCH else None
+    except Exception:
+        return None
+
+
+def collocation_section(device, steps=50):
+    """The same cfg-2 problem transcribed by direct collocation: g + J_g throughput of k_colloc over a device-resident
+    batch in 64-instance tiles (the handle's default launch shape: two instances per lane, intervals-fast grid), its
+    roofline (algorithmic HBM bytes — read v, write g and J_g — over the launch time from HIP events on the launch
+    stream), and the fused g + J_g + Hessian launch (cfx_eval_all_h, one kernel) timed the same way."""
+    import torch
+
+    ocp = build_collocation()
+    B = COLLOCATION_BATCH
+    h = ocp.nlp(batch=B, layout="tiled64", device=device)
     dev = f"cuda:{device}"
-    gen = torch.Generator(device=dev)
-    gen.manual_seed(7)
-    v = torch.rand((h.nv, B), generator=gen, dtype=torch.float64, device=dev)
-    v *= torch.tensor([1.5, 250.0] * (h.nv // 2), dtype=torch.float64, device=dev)[:, None]
-    g = torch.empty((h.ng, B), dtype=torch.float64, device=dev)
-    jac = torch.empty((h.nnz_jac, B), dtype=torch.float64, device=dev)
-    for _ in range(5):
-        h.eval_all(v, g=g, jac=jac)
-    torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(steps):
-        h.eval_all(v, g=g, jac=jac)
-    e1.record()
-    torch.cuda.synchronize()
-    ms = e0.elapsed_time(e1) / steps
+    v = collocation_synthetic(ocp, B, dev)
+    g = torch.empty((B // 64, h.ng, 64), dtype=torch.float64, device=dev)
+    jac = torch.empty((B // 64, h.nnz_jac, 64), dtype=torch.float64, device=dev)
+
+    def timed(fn, n):
+        for _ in range(5):
+            fn()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(n):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / n
+
+    ms = timed(lambda: h.eval_all(v, g=g, jac=jac), steps)
     nbytes = 8 * (h.nv + h.ng + h.nnz_jac)
+    achieved = nbytes * B / (ms * 1e-3) / 1e9
+    pmc = collocation_pmc()
+    lam = torch.randn((B // 64, h.ng, 64), dtype=torch.float64, device=dev, generator=torch.Generator(dev).manual_seed(3))
+    of = torch.ones((B,), dtype=torch.float64, device=dev)
+    hs = torch.empty((B // 64, h.nnz_hess, 64), dtype=torch.float64, device=dev)
+    ms_h = timed(lambda: h.eval_all_h(v, of, lam, g=g, jac=jac, hess=hs), max(steps // 5, 5))
+    nbytes_h = 8 * (2 * h.nv + 2 * h.ng + h.nnz_jac + h.nnz_hess)  # + read lambda, write the Hessian values
+    shape = h.launch_shape()
     h.close()
-    return {"workload": "cfg2 by direct collocation, Legendre degree 4 (nv = 202, ng = 200)", "batch": B,
-            "nv": ocp.nv, "ng": int(ocp.n_shooting * ocp.ngk), "nnz_jac": nbytes // 8 - ocp.nv - ocp.n_shooting * ocp.ngk,
-            "ms_per_launch": ms, "instance_evals_per_s": B / (ms * 1e-3),
-            "achieved_GBps": nbytes * B / (ms * 1e-3) / 1e9, "bytes_per_instance": nbytes}
+    return {"workload": "cfg2 by direct collocation, Legendre degree 4 (nv = 202, ng = 200); one launch = g + J_g of "
+                        "every instance", "batch": B, "nv": ocp.nv, "ng": int(ocp.n_shooting * ocp.ngk),
+            "nnz_jac": nbytes // 8 - ocp.nv - ocp.n_shooting * ocp.ngk, "layout": "CFX_LAYOUT_TILED64",
+            "launch_shape": shape, "ms_per_launch": ms, "instance_evals_per_s": B / (ms * 1e-3),
+            "achieved_GBps": achieved, "bytes_per_instance": nbytes,
+            "roofline": {"bound": "hbm", "kernel": "cfx::k_colloc<DING2003, TMAX=1, DEG=4, NI=2>", "achieved": achieved,
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                         "traffic": pmc.get("hbm_bytes_per_launch") if pmc else None,
+                         "traffic_source": pmc.get("source") if pmc else None},
+            "fused_g_jac_hess": {"kernel": "cfx::k_colloc_hess<DING2003, DJ=2, TMAX=1, GJ=true>",
+                                 "ms_per_launch": ms_h, "bytes_per_instance": nbytes_h,
+                                 "achieved_GBps": nbytes_h * B / (ms_h * 1e-3) / 1e9}}
 
 
 def nmpc_section(device, n_windows, dist=None, world=1, rank=0, backend="nccl", batch=64):

@@ -15,7 +15,7 @@ import numpy as np
 
 LIB_PATH = pathlib.Path(__file__).with_name("libcfx.so")
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 OK, EINVAL, EHIP, ENOMEM, EUNSUPPORTED, ENODEV = 0, -1, -2, -3, -4, -5
 MODEL_IDS = {
     "ding2003": 0,
@@ -114,7 +114,12 @@ class IpmOptions(C.Structure):
                 ("limited_memory_max_history", C.c_int32), ("restoration", C.c_int32),
                 ("max_resto_iter", C.c_int32), ("resto_penalty", C.c_double),
                 ("required_infeasibility_reduction", C.c_double), ("filter_reset_trigger", C.c_int32),
-                ("max_filter_resets", C.c_int32)]
+                ("max_filter_resets", C.c_int32), ("max_wall_time", C.c_double), ("print_frequency_time", C.c_double)]
+
+
+# cfx_ipm_get_status values (Ipopt's ApplicationReturnStatus)
+IPM_STATUS = {0: "Solve_Succeeded", 1: "Solved_To_Acceptable_Level", 2: "Infeasible_Problem_Detected",
+              -1: "Maximum_Iterations_Exceeded", -2: "Restoration_Failed", -5: "Maximum_WallTime_Exceeded"}
 
 
 class IpmStats(C.Structure):
@@ -156,6 +161,7 @@ SIGNATURES = {
     "cfx_ipm_create": (C.c_int, [_P, _P, _P, C.c_int32, C.POINTER(IpmOptions), C.POINTER(_P)]),
     "cfx_ipm_solve": (C.c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _P, C.c_uint32]),
     "cfx_ipm_get_stats": (C.c_int, [_P, C.POINTER(IpmStats)]),
+    "cfx_ipm_get_status": (C.c_int, [_P, C.POINTER(C.c_int32)]),
     "cfx_ipm_n_fixed": (C.c_int, [_P]),
     "cfx_ipm_last_error": (C.c_char_p, [_P]),
     "cfx_ipm_destroy": (None, [_P]),
@@ -632,6 +638,14 @@ class Ipm:
         if rc != OK:
             raise CfxError(rc, "cfx_ipm_get_stats")
         return {k: getattr(st, k) for k, _ in IpmStats._fields_}
+
+    def status(self):
+        """(B,) int32: the CFX_IPM_* outcome (IPM_STATUS) of every instance of the last solve."""
+        out = np.empty(self.batch, dtype=np.int32)
+        rc = self.lib.cfx_ipm_get_status(self.s, out.ctypes.data_as(C.POINTER(C.c_int32)))
+        if rc != OK:
+            raise CfxError(rc, "cfx_ipm_get_status")
+        return out
 
     def close(self):
         if getattr(self, "s", None):

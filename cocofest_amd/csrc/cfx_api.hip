@@ -447,9 +447,8 @@ extern "C" int cfx_create(const cfx_problem* p, cfx_handle** out) {
         return create_fail(nullptr, CFX_EUNSUPPORTED, "cfx_create: truncation must be in [1, 32]");
     if (p->layout != CFX_LAYOUT_AOS && p->layout != CFX_LAYOUT_SOA && p->layout != CFX_LAYOUT_TILED64)
         return create_fail(nullptr, CFX_EINVAL, "cfx_create: unknown layout");
-    if (p->layout == CFX_LAYOUT_TILED64 && (p->batch % 64 != 0 || colloc))
-        return create_fail(nullptr, CFX_EUNSUPPORTED,
-                           "cfx_create: CFX_LAYOUT_TILED64 needs batch % 64 == 0 and a shooting transcription");
+    if (p->layout == CFX_LAYOUT_TILED64 && p->batch % 64 != 0)
+        return create_fail(nullptr, CFX_EUNSUPPORTED, "cfx_create: CFX_LAYOUT_TILED64 needs batch % 64 == 0");
     if (!p->stim_rows) return create_fail(nullptr, CFX_EINVAL, "cfx_create: stim_rows is NULL");
     if (p->n_objectives < 0 || (p->n_objectives > 0 && !p->objectives))
         return create_fail(nullptr, CFX_EINVAL, "cfx_create: n_objectives < 0, or objectives is NULL");
@@ -697,17 +696,20 @@ extern "C" int cfx_create(const cfx_problem* p, cfx_handle** out) {
         // With 64-instance tiles the g + J_g pass is fastest at NI = 2 (0.29 vs 0.30 ms at NI = 1, SoA NI = 1:
         // 0.32 ms; scripts/kprobe.py).
         h->ni = (!hmed && p->layout == CFX_LAYOUT_TILED64) ? 2 : 1;
+        // collocation (degrees 1..5, Ding families): two instances per lane whenever the batch pairs up
+        if (colloc) h->ni = (!hmed && deg <= 5 && p->batch % 2 == 0) ? 2 : 1;
         h->ni_g = (!hmed && p->batch % 4 == 0 && p->batch >= (int64_t)256 * 1024) ? 4 : 1;
         if (const char* e = std::getenv("CFX_NI")) {
             const int v = std::atoi(e);
             if (!hmed && (v == 1 || v == 2 || v == 4) && p->batch % v == 0) h->ni = h->ni_g = v;
         }
+        if (colloc && (hmed || deg > 5 || h->ni > 2)) h->ni = h->ni_g = 1;  // what the collocation kernels run
         // intervals per thread: about 40 workgroups per CU (10,240).  Longer chunks read fewer boundary states
         // twice but start every wave in the same phase; cfg 2 at B = 2^20 (20 intervals, 2,048 instance blocks):
         // 0.313 / 0.304 / 0.295 / 0.287 / 0.293 / 0.303 ms at 20 / 10 / 5 / 4 / 2 / 1 intervals per thread
         // (scripts/store_probe.py).
         const int64_t bx = (p->batch + (int64_t)kBlock * h->ni - 1) / ((int64_t)kBlock * h->ni);
-        const int64_t nch = nchunk_of(h->model, h->scheme, h->tmax, nz);
+        const int64_t nch = colloc ? 1 : nchunk_of(h->model, h->scheme, h->tmax, nz);
         int64_t kpt = (int64_t)N * bx * nch / 10240;
         kp.kpt = (int32_t)std::max<int64_t>(1, std::min<int64_t>(N, kpt));
         if (const char* e = std::getenv("CFX_KPT"))  // tuning override
@@ -862,12 +864,15 @@ extern "C" int cfx_hess_structure(const cfx_handle* h, int32_t* row, int32_t* co
 // evaluation
 // ------------------------------------------------------------------------------------------------------
 static hipError_t launch_shooting(cfx_handle* h, bool derivs, const double* V, double* G, double* J, bool keep) {
-    if (h->colloc) return launch_colloc(h->model, h->tmax, h->kp, V, G, derivs ? J : nullptr, h->stream);
+    // 16-byte lane accesses need 16-byte aligned buffers (B % NI == 0 keeps every row aligned)
+    auto aligned = [](const void* p) { return ((uintptr_t)p & 15u) == 0; };
+    if (h->colloc) {
+        const int ni = (aligned(V) && aligned(G) && aligned(J)) ? h->ni : 1;
+        return launch_colloc(h->model, h->tmax, ni, h->kp, V, G, derivs ? J : nullptr, h->stream);
+    }
     KParams kp = h->kp;
     kp.keepc = keep ? 1 : 0;
     if (is_int(h->model)) return launch_shooting_hmed(h->model, h->scheme, derivs, h->tmax, kp, V, G, J, h->stream);
-    // 16-byte lane accesses need 16-byte aligned buffers (B % NI == 0 keeps every row aligned)
-    auto aligned = [](const void* p) { return ((uintptr_t)p & 15u) == 0; };
     const int ni = (aligned(V) && aligned(G) && aligned(J)) ? (derivs ? h->ni : h->ni_g) : 1;
     return launch_shooting_ding(h->model, h->scheme, derivs, ni, kp, V, G, J, h->stream);
 }
@@ -994,8 +999,8 @@ extern "C" int cfx_eval_h(cfx_handle* h, const double* v, const double* obj_fact
     double* H = stage_out(h, S_OUT, hess, h->sz.nnz_hess, flags, &rc);
     if (!H) return rc;
     if (h->colloc)
-        CFX_HIP(h, launch_colloc_hess(h->model, h->tmax, h->kp, h->d_htasks, h->n_htasks, h->hbs, V, LAM, H,
-                                      h->stream));
+        CFX_HIP(h, launch_colloc_hess(h->model, h->tmax, h->kp, h->d_htasks, h->n_htasks, h->hbs, V, LAM, H, nullptr,
+                                      nullptr, h->stream));
     else
         CFX_HIP(h, launch_hessian(h->model, h->scheme, h->tmax, h->kp, h->d_htasks, h->n_htasks, h->hbs, V, LAM, H,
                                   nullptr, nullptr, h->stream));
@@ -1008,7 +1013,7 @@ extern "C" int cfx_eval_all_h(cfx_handle* h, const double* v, const double* obj_
                               double* g, double* jac, double* f, double* grad, double* hess, uint32_t flags) {
     if (!h || !v || !obj_factor || !lambda || !g || !jac || !hess)
         return h ? fail(h, CFX_EINVAL, "cfx_eval_all_h: NULL argument") : CFX_EINVAL;
-    if (h->msk || h->colloc) {  // the callbacks, then the Hessian at the same point
+    if (h->msk) {  // the callbacks, then the Hessian at the same point
         int rc = cfx_eval_all(h, v, g, jac, f, grad, flags);
         if (rc != CFX_OK) return rc;
         if (h->msk) h->stash_same_point = h->msk_stash && h->stash_valid;
@@ -1028,11 +1033,16 @@ extern "C" int cfx_eval_all_h(cfx_handle* h, const double* v, const double* obj_
     double* GR = grad ? stage_out(h, S_GRAD, grad, h->sz.nv, flags, &rc) : nullptr;
     double* H = stage_out(h, S_OUT, hess, h->sz.nnz_hess, flags, &rc);
     if (rc != CFX_OK || !G || !J || !H) return rc != CFX_OK ? rc : fail(h, CFX_EINVAL, "cfx_eval_all_h: staging");
-    // one launch: the interval's second-order jets carry the g rows and the J_g columns too
+    // one launch: shooting — the interval's second-order jets carry the g rows and the J_g columns too; collocation
+    // — task 0 of every interval runs the g + J_g body (defects, continuity) beside its Hessian block
     KParams kp = h->kp;
     kp.keepc = keep_constants(h, flags, J) ? 1 : 0;
-    CFX_HIP(h, launch_hessian(h->model, h->scheme, h->tmax, kp, h->d_htasks, h->n_htasks, h->hbs, V, LAM, H, G, J,
-                              h->stream));
+    if (h->colloc)
+        CFX_HIP(h, launch_colloc_hess(h->model, h->tmax, kp, h->d_htasks, h->n_htasks, h->hbs, V, LAM, H, G, J,
+                                      h->stream));
+    else
+        CFX_HIP(h, launch_hessian(h->model, h->scheme, h->tmax, kp, h->d_htasks, h->n_htasks, h->hbs, V, LAM, H, G, J,
+                                  h->stream));
     launch_slide(h, V, G, J);
     CFX_HIP(h, launch_objective(h, V, F, GR));
     CFX_HIP(h, launch_objective_hess(h, OF, H));

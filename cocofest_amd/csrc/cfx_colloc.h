@@ -36,51 +36,70 @@ constexpr int col_rowlen(int model, int r, int deg, int nu) {
     return deg + 1 + __builtin_popcount(col_xdeps(model, r) & ~(1u << r)) + col_udeps(model, r, nu);
 }
 
-// DEG > 0: the degree is a compile-time constant and every input of the interval (x^0..x^d, x_{k+1}, the
-// controls) is loaded into registers before the first store — on CDNA vmcnt counts stores too, so a load
-// issued after stores waits for them; DEG == 0: any degree, states re-read from memory per point.
-template <int MODEL, int TMAX, int DEG>
-__global__ void __launch_bounds__(256) k_colloc(const KParams P, const double* __restrict__ V, double* __restrict__ G,
-                                                double* __restrict__ J) {
+// One interval of g (defects + continuity) and J_g for NI adjacent instances per lane (16-byte accesses when NI = 2).
+// DEG > 0: the degree is a compile-time constant and every input of the interval (x^1..x^d, x_{k+1}, the controls)
+// is loaded into registers before the first store — on CDNA vmcnt counts stores too, so a load issued after stores
+// waits for them; x^0 is the previous interval's x_{k+1} (xc, carried by the caller's interval loop).  DEG == 0: any
+// degree, NI = 1, states re-read from memory per point.  ES / vb / gb / jb: element stride and the instances' bases
+// of V, G, J (SoA or 64-instance tiles, lay_stride / lay_base).  Shared by k_colloc and the fused g + J_g + Hessian
+// launch (k_colloc_hess<GJ>), so the two write the same bits.
+template <int MODEL, int TMAX, int DEG, int NI>
+__device__ __forceinline__ void colloc_interval(const KParams& P, const double* __restrict__ V, double* __restrict__ G,
+                                                double* __restrict__ J, int k, int64_t ES, int64_t vb, int64_t gb,
+                                                int64_t jb, double (&xc)[nx_of(MODEL)][NI]) {
     constexpr int NX = nx_of(MODEL);
     constexpr bool PW = is_pw(MODEL), HM = is_int(MODEL);
     constexpr int DD = NX + (PW ? 1 : 0);  // directions of the RHS partials: the point's states (+ pulse width)
     constexpr int XS = DEG > 0 ? DEG + 1 : 1;
     constexpr int UN = DEG > 0 ? DEG + 1 : 1;  // unroll factor of the point / basis loops
-    const int64_t B = P.B;
-    const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (b >= B) return;
-    const int k = blockIdx.y;
+    static_assert(DEG > 0 || NI == 1, "the generic-degree body runs one instance per lane");
     const int d = DEG > 0 ? DEG : P.deg;
-    const double* Vb = V + b;
     const int64_t xo = (int64_t)k * P.nz;
-    auto ld = [&](int64_t e) { return Vb[(xo + e) * B]; };
+    auto ld = [&](int64_t e, double(&o)[NI]) { ld_lane<NI>(V + vb + (xo + e) * ES, o); };
 
-    double xs[XS][NX], xn[NX];
+    double xs[XS][NX][NI], xn[NX][NI];
     if constexpr (DEG > 0) {
 #pragma unroll
-        for (int i = 0; i <= DEG; ++i)
+        for (int r = 0; r < NX; ++r)
 #pragma unroll
-            for (int r = 0; r < NX; ++r) xs[i][r] = ld(i * NX + r);
+            for (int n = 0; n < NI; ++n) xs[0][r][n] = xc[r][n];
+#pragma unroll
+        for (int i = 1; i <= DEG; ++i)
+#pragma unroll
+            for (int r = 0; r < NX; ++r) ld(i * NX + r, xs[i][r]);
     }
 #pragma unroll
-    for (int r = 0; r < NX; ++r) xn[r] = Vb[((int64_t)(k + 1) * P.nz + r) * B];
-    auto X = [&](int i, int r) { return DEG > 0 ? xs[i][r] : ld(i * NX + r); };
+    for (int r = 0; r < NX; ++r) ld_lane<NI>(V + vb + ((int64_t)(k + 1) * P.nz + r) * ES, xn[r]);
+    auto X = [&](int i, int r, int n) { return DEG > 0 ? xs[i][r][n] : V[vb + (xo + i * NX + r) * ES]; };
 
-    Amp amp{1.0, 0.0, -1};
-    double lam[TMAX], lamd[TMAX];
+    Amp amp[NI];
+    double lam[NI][TMAX], lamd[NI][TMAX];
+#pragma unroll
+    for (int n = 0; n < NI; ++n) amp[n] = Amp{1.0, 0.0, -1};
     if constexpr (PW) {
-        const double ex = exp(-(ld(P.uoff) - P.pd0) / P.pdt);
-        amp.E = 1.0 - ex;
-        amp.dE = ex / P.pdt;
-        amp.pwdir = NX;
+        double pw[NI];
+        ld(P.uoff, pw);
+#pragma unroll
+        for (int n = 0; n < NI; ++n) {
+            const double ex = exp(-(pw[n] - P.pd0) / P.pdt);
+            amp[n].E = 1.0 - ex;
+            amp[n].dE = ex / P.pdt;
+            amp[n].pwdir = NX;
+        }
     }
     if constexpr (HM) {
 #pragma unroll
         for (int i = 0; i < TMAX; ++i) {
-            const double th = i < P.T ? tanh(P.bs * (ld(P.uoff + i) - P.Is)) : 0.0;
-            lam[i] = i < P.T ? P.ar * (th + P.cr) : 0.0;
-            lamd[i] = i < P.T ? P.ar * P.bs * (1.0 - th * th) : 0.0;
+            double u[NI];
+#pragma unroll
+            for (int n = 0; n < NI; ++n) u[n] = P.Is;
+            if (i < P.T) ld(P.uoff + i, u);
+#pragma unroll
+            for (int n = 0; n < NI; ++n) {
+                const double th = i < P.T ? tanh(P.bs * (u[n] - P.Is)) : 0.0;
+                lam[n][i] = i < P.T ? P.ar * (th + P.cr) : 0.0;
+                lamd[n][i] = i < P.T ? P.ar * P.bs * (1.0 - th * th) : 0.0;
+            }
         }
     }
     int sumrow = 0;
@@ -91,59 +110,89 @@ __global__ void __launch_bounds__(256) k_colloc(const KParams P, const double* _
 
 #pragma unroll UN
     for (int j = 1; j <= d; ++j) {
-        double x[NX];
-#pragma unroll
-        for (int r = 0; r < NX; ++r) x[r] = X(j, r);
         const int q = k * d + j - 1;
-        double cs;
         const double* coef = P.tab + (int64_t)q * (HM ? TMAX : 1);
-        if constexpr (HM) {
-            cs = 0.0;
+        double f[NI][NX], fd[NI][NX][DD];
 #pragma unroll
-            for (int i = 0; i < TMAX; ++i) cs += coef[i] * lam[i];
-        } else {
-            cs = coef[0];
+        for (int n = 0; n < NI; ++n) {
+            double x[NX];
+#pragma unroll
+            for (int r = 0; r < NX; ++r) x[r] = X(j, r, n);
+            double cs;
+            if constexpr (HM) {
+                cs = 0.0;
+#pragma unroll
+                for (int i = 0; i < TMAX; ++i) cs += coef[i] * lam[n][i];
+            } else {
+                cs = coef[0];
+            }
+            double xd[NX][DD], cnd[DD];
+#pragma unroll
+            for (int r = 0; r < NX; ++r)
+#pragma unroll
+                for (int c = 0; c < DD; ++c) xd[r][c] = r == c ? 1.0 : 0.0;
+#pragma unroll
+            for (int c = 0; c < DD; ++c) cnd[c] = c == 0 ? 1.0 : 0.0;
+            rhs_force<MODEL, DD, true>(P, x[0], cnd, x, xd, amp[n], f[n], fd[n]);
+            f[n][0] = P.inv_tauc * (cs - x[0]);
         }
-        double xd[NX][DD], cnd[DD], f[NX], fd[NX][DD];
-#pragma unroll
-        for (int r = 0; r < NX; ++r)
-#pragma unroll
-            for (int c = 0; c < DD; ++c) xd[r][c] = r == c ? 1.0 : 0.0;
-#pragma unroll
-        for (int c = 0; c < DD; ++c) cnd[c] = c == 0 ? 1.0 : 0.0;
-        rhs_force<MODEL, DD, true>(P, x[0], cnd, x, xd, amp, f, fd);
-        f[0] = P.inv_tauc * (cs - x[0]);
         if (G) {
 #pragma unroll
             for (int r = 0; r < NX; ++r) {
-                double poly = 0.0;
+                double t[NI];
+#pragma unroll
+                for (int n = 0; n < NI; ++n) {
+                    double poly = 0.0;
 #pragma unroll UN
-                for (int i = 0; i <= d; ++i) poly = fma(P.colC[i][j], X(i, r), poly);
-                st_nt(G + (go + (j - 1) * NX + r) * B + b, fma(-P.dt, f[r], poly));
+                    for (int i = 0; i <= d; ++i) poly = fma(P.colC[i][j], X(i, r, n), poly);
+                    t[n] = fma(-P.dt, f[n][r], poly);
+                }
+                st_lane<NI>(G + gb + (go + (j - 1) * NX + r) * ES, t);
             }
         }
         if (J) {
             int64_t o = jo + (int64_t)(j - 1) * sumrow;
 #pragma unroll
             for (int r = 0; r < NX; ++r) {
-                const double diag = r == 0 ? -P.inv_tauc : fd[r][r];
 #pragma unroll UN
-                for (int i = 0; i <= d; ++i)
-                    st_nt(J + (o + i) * B + b, i == j ? fma(-P.dt, diag, P.colC[i][j]) : P.colC[i][j]);
+                for (int i = 0; i <= d; ++i) {
+                    double t[NI];
+#pragma unroll
+                    for (int n = 0; n < NI; ++n) {
+                        const double diag = r == 0 ? -P.inv_tauc : fd[n][r][r];
+                        t[n] = i == j ? fma(-P.dt, diag, P.colC[i][j]) : P.colC[i][j];
+                    }
+                    st_lane<NI>(J + jb + (o + i) * ES, t);
+                }
                 o += d + 1;
 #pragma unroll
                 for (int c = 0; c < NX; ++c)
-                    if (c != r && (col_xdeps(MODEL, r) >> c & 1u)) st_nt(J + (o++) * B + b, -P.dt * fd[r][c]);
+                    if (c != r && (col_xdeps(MODEL, r) >> c & 1u)) {
+                        double t[NI];
+#pragma unroll
+                        for (int n = 0; n < NI; ++n) t[n] = -P.dt * fd[n][r][c];
+                        st_lane<NI>(J + jb + (o++) * ES, t);
+                    }
                 if constexpr (HM) {
                     if (r == 0) {
 #pragma unroll
                         for (int i = 0; i < TMAX; ++i)  // register-resident lamd: no dynamic indexing
-                            if (i < P.T) st_nt(J + (o + i) * B + b, -P.dt * P.inv_tauc * coef[i] * lamd[i]);
+                            if (i < P.T) {
+                                double t[NI];
+#pragma unroll
+                                for (int n = 0; n < NI; ++n) t[n] = -P.dt * P.inv_tauc * coef[i] * lamd[n][i];
+                                st_lane<NI>(J + jb + (o + i) * ES, t);
+                            }
                         o += P.T;
                     }
                 }
                 if constexpr (PW) {
-                    if (r == 1) st_nt(J + (o++) * B + b, -P.dt * fd[1][NX]);
+                    if (r == 1) {
+                        double t[NI];
+#pragma unroll
+                        for (int n = 0; n < NI; ++n) t[n] = -P.dt * fd[n][1][NX];
+                        st_lane<NI>(J + jb + (o++) * ES, t);
+                    }
                 }
             }
         }
@@ -152,28 +201,64 @@ __global__ void __launch_bounds__(256) k_colloc(const KParams P, const double* _
 #pragma unroll
     for (int r = 0; r < NX; ++r) {
         if (G) {
-            double e = 0.0;
+            double t[NI];
+#pragma unroll
+            for (int n = 0; n < NI; ++n) {
+                double e = 0.0;
 #pragma unroll UN
-            for (int i = 0; i <= d; ++i) e = fma(P.colD[i], X(i, r), e);
-            st_nt(G + (go + d * NX + r) * B + b, e - xn[r]);
+                for (int i = 0; i <= d; ++i) e = fma(P.colD[i], X(i, r, n), e);
+                t[n] = e - xn[r][n];
+            }
+            st_lane<NI>(G + gb + (go + d * NX + r) * ES, t);
         }
         if (J) {
             const int64_t o = jo + (int64_t)d * sumrow + (int64_t)r * (d + 2);
 #pragma unroll UN
-            for (int i = 0; i <= d; ++i) st_nt(J + (o + i) * B + b, P.colD[i]);
-            st_nt(J + (o + d + 1) * B + b, -1.0);
+            for (int i = 0; i <= d; ++i) st_lane_const<NI>(J + jb + (o + i) * ES, P.colD[i]);
+            st_lane_const<NI>(J + jb + (o + d + 1) * ES, -1.0);
         }
     }
+#pragma unroll
+    for (int r = 0; r < NX; ++r)
+#pragma unroll
+        for (int n = 0; n < NI; ++n) xc[r][n] = xn[r][n];
+}
+
+// g + J_g of the collocation transcription.  Thread = (NI adjacent instances, intervals [k0, k0 + kpt)); grid as the
+// shooting launch (interval chunks on grid.x when P.ifast, instance blocks on grid.y).  Each interval reads its own
+// block (x^0 carried from the previous interval's x_{k+1}) and x_{k+1}^0; no recursion, so the intervals per thread
+// only shape the launch (fewer, longer waves; the carried x^0 is read once).
+template <int MODEL, int TMAX, int DEG, int NI>
+__global__ void __launch_bounds__(256) k_colloc(const KParams P, const double* __restrict__ V, double* __restrict__ G,
+                                                double* __restrict__ J) {
+    constexpr int NX = nx_of(MODEL);
+    const unsigned bi = P.ifast ? blockIdx.y : blockIdx.x, bk = P.ifast ? blockIdx.x : blockIdx.y;
+    const int64_t b0 = ((int64_t)bi * blockDim.x + threadIdx.x) * NI;
+    if (b0 >= P.B) return;
+    const int k0 = bk * P.kpt;
+    const int k1 = min(P.N, k0 + P.kpt);
+    const int64_t ES = lay_stride(P);
+    const int64_t vb = lay_base(P, P.nv_tot, b0), gb = lay_base(P, P.ng_tot, b0), jb = lay_base(P, P.nnz_tot, b0);
+    double xc[NX][NI];
+    if constexpr (DEG > 0) {
+#pragma unroll
+        for (int r = 0; r < NX; ++r) ld_lane<NI>(V + vb + ((int64_t)k0 * P.nz + r) * ES, xc[r]);
+    }
+    for (int k = k0; k < k1; ++k) colloc_interval<MODEL, TMAX, DEG, NI>(P, V, G, J, k, ES, vb, gb, jb, xc);
 }
 
 // Lagrangian Hessian of the collocation defects: sum_{j,r} lambda_{k,j,r} (-dt) d^2 f_r(x_k^j, u_k).  Local
 // directions of a point: its nx states then the nu controls; a task (I, J) carries direction blocks I and J
 // (as k_hessian).  States of different points never meet, so point j's (x, x) and (u, x) entries are written
 // per point; the (u, u) entries are summed over the points in registers and written once.
-template <int MODEL, int DJ, int TMAX>
+// GJ: the same launch also writes g and J_g (cfx_eval_all_h: defects, continuity, Jacobian and Hessian of every
+// interval from one launch, the north star's contract): task 0 of each interval runs the k_colloc body
+// (colloc_interval, generic degree), so its values are k_colloc's bits.
+template <int MODEL, int DJ, int TMAX, bool GJ>
 __global__ void __launch_bounds__(256) k_colloc_hess(const KParams P, const HTask* __restrict__ tasks, int bs,
                                                      const double* __restrict__ V, const double* __restrict__ LAM,
-                                                     double* __restrict__ H) {
+                                                     double* __restrict__ H, double* __restrict__ G,
+                                                     double* __restrict__ J) {
     constexpr int NX = nx_of(MODEL);
     constexpr bool HM = is_int(MODEL);
     using J_t = Jet<DJ>;
@@ -183,8 +268,17 @@ __global__ void __launch_bounds__(256) k_colloc_hess(const KParams P, const HTas
     const int k = blockIdx.y;
     const HTask task = tasks[blockIdx.z];
     const int d = P.deg, nu = P.nu, nzl = NX + P.nu;
-    const double* Vb = V + b;
+    // layout (SoA or 64-instance tiles): element stride ES, per-buffer instance bases
+    const int64_t ES = lay_stride(P), vb = lay_base(P, P.nv_tot, b), lb = lay_base(P, P.ng_tot, b),
+                  hb = lay_base(P, P.nh_tot, b);
+    auto Vat = [&](int64_t e) { return V[vb + e * ES]; };
     const int64_t xo = (int64_t)k * P.nz;
+    if constexpr (GJ) {
+        if (blockIdx.z == 0) {
+            double xc[NX][1];
+            colloc_interval<MODEL, TMAX, 0, 1>(P, V, G, J, k, ES, vb, lb, lay_base(P, P.nnz_tot, b), xc);
+        }
+    }
 
     int gd[DJ];
 #pragma unroll
@@ -202,7 +296,7 @@ __global__ void __launch_bounds__(256) k_colloc_hess(const KParams P, const HTas
     };
     J_t afac = jconst<DJ>(1.0);
     if constexpr (is_pw(MODEL)) {
-        const double pw = Vb[(xo + P.uoff) * B];
+        const double pw = Vat(xo + P.uoff);
         const double ex = exp(-(pw - P.pd0) / P.pdt);
         afac = jchain(seed(pw, NX), 1.0 - ex, ex / P.pdt, -ex / (P.pdt * P.pdt));
     }
@@ -211,7 +305,7 @@ __global__ void __launch_bounds__(256) k_colloc_hess(const KParams P, const HTas
         csh.coef = P.tab;
 #pragma unroll
         for (int i = 0; i < TMAX; ++i) {
-            const double ui = i < P.T ? Vb[(xo + P.uoff + i) * B] : P.Is;
+            const double ui = i < P.T ? Vat(xo + P.uoff + i) : P.Is;
             csh.lamv[i] = i < P.T ? P.ar * (tanh(P.bs * (ui - P.Is)) + P.cr) : 0.0;
         }
 #pragma unroll
@@ -219,7 +313,7 @@ __global__ void __launch_bounds__(256) k_colloc_hess(const KParams P, const HTas
             csh.uidx[s] = -1;
             csh.l1[s] = csh.l2[s] = 0.0;
             if (gd[s] >= NX) {
-                const double th = tanh(P.bs * (Vb[(xo + P.uoff + gd[s] - NX) * B] - P.Is));
+                const double th = tanh(P.bs * (Vat(xo + P.uoff + gd[s] - NX) - P.Is));
                 const double d1 = P.bs * (1.0 - th * th);
                 csh.l1[s] = P.ar * d1;
                 csh.l2[s] = -2.0 * P.ar * P.bs * th * d1;
@@ -239,7 +333,7 @@ __global__ void __launch_bounds__(256) k_colloc_hess(const KParams P, const HTas
     for (int j = 1; j <= d; ++j) {
         J_t x[NX];
 #pragma unroll
-        for (int r = 0; r < NX; ++r) x[r] = seed(Vb[(xo + j * NX + r) * B], r);
+        for (int r = 0; r < NX; ++r) x[r] = seed(Vat(xo + j * NX + r), r);
         J_t f[NX];
         const int q = k * d + j - 1;
         const J_t cs = HM ? csh.eval(q) : jconst<DJ>(P.tab[q]);
@@ -247,7 +341,7 @@ __global__ void __launch_bounds__(256) k_colloc_hess(const KParams P, const HTas
         rhs_force_gen<MODEL>(P, x[0], x, afac, f);
         double w[NX];
 #pragma unroll
-        for (int r = 0; r < NX; ++r) w[r] = -P.dt * LAM[(int64_t)(k * P.ngk + (j - 1) * NX + r) * B + b];
+        for (int r = 0; r < NX; ++r) w[r] = -P.dt * LAM[lb + (int64_t)(k * P.ngk + (j - 1) * NX + r) * ES];
         const int64_t pj = hk + NX + (int64_t)(j - 1) * per_point;
 #pragma unroll
         for (int s1 = 0; s1 < DJ; ++s1) {
@@ -259,9 +353,9 @@ __global__ void __launch_bounds__(256) k_colloc_hess(const KParams P, const HTas
                 for (int r = 0; r < NX; ++r) acc += w[r] * f[r].h[s1 * (s1 + 1) / 2 + s2];
                 const int g1 = gd[s1] > gd[s2] ? gd[s1] : gd[s2], g2 = gd[s1] > gd[s2] ? gd[s2] : gd[s1];
                 if (g1 < NX) {
-                    H[(pj + g1 * (g1 + 1) / 2 + g2) * B + b] = acc;
+                    H[hb + (pj + g1 * (g1 + 1) / 2 + g2) * ES] = acc;
                 } else if (g2 < NX) {
-                    H[(pj + NX * (NX + 1) / 2 + (int64_t)(g1 - NX) * NX + g2) * B + b] = acc;
+                    H[hb + (pj + NX * (NX + 1) / 2 + (int64_t)(g1 - NX) * NX + g2) * ES] = acc;
                 } else {
                     uu[s1 * (s1 + 1) / 2 + s2] += acc;
                 }
@@ -276,17 +370,17 @@ __global__ void __launch_bounds__(256) k_colloc_hess(const KParams P, const HTas
             const int g1 = gd[s1] > gd[s2] ? gd[s1] : gd[s2], g2 = gd[s1] > gd[s2] ? gd[s2] : gd[s1];
             if (g2 >= NX) {
                 const int a = g1 - NX, c = g2 - NX;
-                H[(uu0 + a * (a + 1) / 2 + c) * B + b] = uu[s1 * (s1 + 1) / 2 + s2];
+                H[hb + (uu0 + a * (a + 1) / 2 + c) * ES] = uu[s1 * (s1 + 1) / 2 + s2];
             }
         }
     }
     // the node-state diagonal of interval k (and x_N) carries objective terms only: start from zero
     if (blockIdx.z == 0) {
 #pragma unroll
-        for (int r = 0; r < NX; ++r) H[(hk + r) * B + b] = 0.0;
+        for (int r = 0; r < NX; ++r) H[hb + (hk + r) * ES] = 0.0;
         if (k == P.N - 1) {
 #pragma unroll
-            for (int r = 0; r < NX; ++r) H[((int64_t)P.N * P.nhk + r) * B + b] = 0.0;
+            for (int r = 0; r < NX; ++r) H[hb + ((int64_t)P.N * P.nhk + r) * ES] = 0.0;
         }
     }
 }

@@ -26,6 +26,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <cstdio>
 #include <cstring>
 #include <numeric>
 #include <string>
@@ -56,11 +57,18 @@ struct Scal {
     double lsig;
     int32_t lcount, lhead, lprev, lpad;
     // restoration phase (CFX_RESTORATION_PHASE): its barrier, the original infeasibility where it started, its own
-    // regularisation, line-search and filter quantities; rs_on: in the phase, rs_ok: left it successfully
+    // regularisation, line-search and filter quantities
     double rs_mu, rs_tau, rs_th0, rs_dw, rs_dwl, rs_theta, rs_phi, rs_dphi, rs_alpha, rs_ap, rs_az, rs_tmax, rs_tmin;
-    int32_t rs_on, rs_ok, rs_acc, rs_arm, rs_it;
-    int32_t stop;  // out of iterations (restoration-phase ones included): done, not converged
+    // rs_on: the instance is in the phase (its iterations run in the same launches as the main iterations of the
+    // others); rs_exit: how its phase ended this iteration (RS_*; 0: still running), acted on by k_ipm_update
+    int32_t rs_on, rs_exit, rs_acc, rs_arm, rs_it;
+    int32_t stop;    // done, not converged (status says why)
+    int32_t status;  // CFX_IPM_STATUS_* once done
+    int32_t spad;
 };
+
+// how a restoration phase ended (Scal::rs_exit)
+enum { RS_RUNNING = 0, RS_OK = 1, RS_FAILED = 2, RS_INFEASIBLE = 3, RS_BUDGET = 4 };
 
 struct IpmK {
     int64_t B;
@@ -123,7 +131,8 @@ struct IpmK {
     int rsphase;
     double *rp, *rn, *rzp, *rzn, *rdp, *rdn, *rdzp, *rdzn, *rpt, *rnt, *ry, *rdc;
     double *rzl, *rzu;
-    double *rfilt, *ofz;
+    double* rfilt;
+    unsigned long long* rstat;  // [2] phases entered, phase iterations (summed over the instances)
 };
 
 enum { KKT_NEWTON = 0, KKT_LSMULT = 1, KKT_RESTO = 2, KKT_RSNLP = 3 };
@@ -373,12 +382,17 @@ __global__ void __launch_bounds__(kIB) k_ipm_init(const IpmK K) {
 
 // Iteration start (solver.py solve loop, up to the Newton right-hand side).  mode bit 0: scale the callback
 // outputs of x (g, J_g, f, grad f); bit 1: stop after the scaling (least-squares multipliers come next).
+// Instances in the restoration phase are k_rs_begin's.
 __global__ void __launch_bounds__(kIB) k_ipm_begin(const IpmK K, int mode, int slot) {
     __shared__ double sh[kIB / 64];
     __shared__ Scal S;
     const int64_t b = blockIdx.x;
     const int nf = K.nf, m = K.m;
     load_scal(K, b, S);
+    if (S.rs_on) {  // block-uniform
+        count_add(K, slot, 0, 0);
+        return;
+    }
     double* gS = K.gS + b * m;
     double* jv = K.jv + b * K.nj;
     double* gF = K.gF + b * nf;
@@ -444,8 +458,12 @@ __global__ void __launch_bounds__(kIB) k_ipm_begin(const IpmK K, int mode, int s
         S.err0 = max_n(max_n(e_d, e_p), e_c0);
         S.acc = S.err0 <= K.o.acceptable_tol ? S.acc + 1 : 0;
         const bool newly = !S.done && (S.err0 <= K.o.tol || S.acc >= K.o.acceptable_iter);
+        if (newly) S.status = S.err0 <= K.o.tol ? CFX_IPM_SOLVE_SUCCEEDED : CFX_IPM_SOLVED_TO_ACCEPTABLE_LEVEL;
         S.done = S.done || newly;
-        if (!S.done && S.iters >= K.o.max_iter) S.done = S.stop = 1;  // per-instance budget
+        if (!S.done && S.iters >= K.o.max_iter) {  // per-instance budget
+            S.done = S.stop = 1;
+            S.status = CFX_IPM_MAXIMUM_ITERATIONS_EXCEEDED;
+        }
     }
     __syncthreads();
     // monotone barrier update: while the barrier sub-problem is solved, decrease mu (at most 5 times)
@@ -500,8 +518,9 @@ __global__ void __launch_bounds__(kIB) k_ipm_kkt(const IpmK K, int mode) {
         const double* hv = K.hv + b * K.nnzh;
         const double* jv = K.jv + b * K.nj;
         const double* sig = K.sig + b * K.nf;
-        // L-BFGS: W = sigma I - low rank (Woodbury); restoration phase: its own regularisation and proximity term
-        const bool rs = mode == KKT_RSNLP;
+        // L-BFGS: W = sigma I - low rank (Woodbury); restoration phase (the Newton matrix of an instance in it): its
+        // own regularisation and proximity term
+        const bool rs = mode == KKT_RSNLP || (mode == KKT_NEWTON && K.sc[b].rs_on);
         const double dw = rs ? K.sc[b].rs_dw : K.sc[b].dw + (K.lbfgs ? K.sc[b].lsig : 0.0);
         for (int k = K.kkt_ptr[p]; k < K.kkt_ptr[p + 1]; ++k) {
             const int32_t code = K.kkt_src[k];
@@ -710,20 +729,21 @@ __global__ void __launch_bounds__(kIB) k_ipm_schur(const IpmK K, int factor) {
     for (int c = t; c < np; c += kIB) rb[PA + c] = sv[c];
 }
 
-// Newton step in natural order and the curvature test (solver.py inertia loop); bumps dw where it fails.  rs: the
-// restoration phase's step (instances in the phase only; its dx in dxr, its own dw, the proximity weights)
-__global__ void __launch_bounds__(kIB) k_ipm_curv(const IpmK K, int slot, int rs) {
+// Newton step in natural order and the curvature test (solver.py inertia loop); bumps dw where it fails.  An instance
+// in the restoration phase takes the phase's step (its dx in dxr, its own dw, the proximity weights).  Counters: [0]
+// instances iterating, [1] of them with the wrong inertia, [2] of them in the restoration phase
+__global__ void __launch_bounds__(kIB) k_ipm_curv(const IpmK K, int slot) {
     __shared__ Scal S;
     const int64_t b = blockIdx.x;
     const int nf = K.nf;
     load_scal(K, b, S);
-    const bool active = rs ? (bool)S.rs_on : !S.done;
+    const bool rs = S.rs_on;
+    const bool active = rs ? S.rs_exit == RS_RUNNING : !S.done;
     const double dwc = rs ? S.rs_dw : S.dw;
     const double* rb = K.rb + b * K.nKp;
     double* dx = (rs ? K.dxr : K.dx) + b * nf;
     double* dy = K.dy + b * K.m;
     double nonfin = 0.0;
-    // the phase's solves of the instances outside it are not steps: their dy (main-loop step) stays
     if (active || !rs)
         for (int i = threadIdx.x; i < K.nK; i += kIB) {
             const double r = rb[K.pos[i]];
@@ -775,6 +795,7 @@ __global__ void __launch_bounds__(kIB) k_ipm_curv(const IpmK K, int slot, int rs
     if (threadIdx.x == 0) {
         count_add(K, slot, 0, active);
         if (bad) atomicAdd(K.cnt + 4 * slot + 1, 1);
+        if (rs && active) atomicAdd(K.cnt + 4 * slot + 2, 1);
     }
 }
 
@@ -785,6 +806,7 @@ __global__ void __launch_bounds__(kIB) k_ipm_dir(const IpmK K, int it) {
     const int64_t b = blockIdx.x;
     const int nf = K.nf, m = K.m;
     load_scal(K, b, S);
+    if (S.rs_on) return;  // block-uniform: k_rs_dir's
     const double* x = K.x + b * nf;
     const double* zl = K.zl + b * nf;
     const double* zu = K.zu + b * nf;
@@ -876,13 +898,18 @@ __global__ void __launch_bounds__(kIB) k_ipm_dir(const IpmK K, int it) {
 }
 
 // after g, f at the trial point: filter acceptance (solver.py line search); at ls == 0 the second-order
-// correction set-up.  counters: [0] not accepted, [1] second-order corrections wanted
+// correction set-up.  counters: [0] not accepted (instances in the restoration phase counted after k_rs_accept),
+// [1] second-order corrections wanted
 __global__ void __launch_bounds__(kIB) k_ipm_accept(const IpmK K, int ls, int slot) {
     __shared__ double sh[kIB / 64];
     __shared__ Scal S;
     const int64_t b = blockIdx.x;
     const int nf = K.nf, m = K.m;
     load_scal(K, b, S);
+    if (S.rs_on) {  // block-uniform
+        count_add(K, slot, 0, S.rs_exit == RS_RUNNING && !S.rs_acc);
+        return;
+    }
     const double* sg = K.sg + b * m;
     const double* gt = K.gt + b * m;
     double tt = 0.0;
@@ -934,7 +961,7 @@ __global__ void __launch_bounds__(kIB) k_ipm_next_trial(const IpmK K) {
     __shared__ Scal S;
     const int64_t b = blockIdx.x;
     load_scal(K, b, S);
-    if (S.accepted) return;  // block-uniform
+    if (S.accepted || S.rs_on) return;  // block-uniform
     const double a = S.alpha * 0.5;
     const int nf = K.nf;
     const double* x = K.x + b * nf;
@@ -949,6 +976,7 @@ __global__ void __launch_bounds__(kIB) k_ipm_next_trial(const IpmK K) {
 // second-order correction: rhs [alpha rhs_x; -c_soc] in band order (the factors of the iteration are reused)
 __global__ void __launch_bounds__(kIB) k_ipm_soc_rhs(const IpmK K) {
     const int64_t b = blockIdx.x;
+    if (K.sc[b].rs_on) return;  // block-uniform
     const double a = K.sc[b].alpha;
     const int nf = K.nf;
     for (int i = threadIdx.x; i < K.nK; i += kIB)
@@ -958,6 +986,7 @@ __global__ void __launch_bounds__(kIB) k_ipm_soc_rhs(const IpmK K) {
 // corrected trial x + a_c dx_c (into xr)
 __global__ void __launch_bounds__(kIB) k_ipm_soc_trial(const IpmK K) {
     const int64_t b = blockIdx.x;
+    if (K.sc[b].rs_on) return;  // block-uniform: xr, vt hold the phase's iterate and trial
     const int nf = K.nf;
     const double* x = K.x + b * nf;
     const double* rb = K.rb + b * K.nKp;
@@ -991,6 +1020,10 @@ __global__ void __launch_bounds__(kIB) k_ipm_soc_accept(const IpmK K, int slot) 
     const int64_t b = blockIdx.x;
     const int nf = K.nf, m = K.m;
     load_scal(K, b, S);
+    if (S.rs_on) {  // block-uniform
+        count_add(K, slot, 0, S.rs_exit == RS_RUNNING && !S.rs_acc);
+        return;
+    }
     const double* sg = K.sg + b * m;
     const double* gt = K.gt + b * m;
     double tt = 0.0;
@@ -1139,16 +1172,36 @@ __global__ void __launch_bounds__(kIB) k_ipm_lsmult(const IpmK K) {
     if (threadIdx.x == 0) K.sc[b].reinit = 0;
 }
 
-// end of an iteration: filter augmentation, restoration outcome, primal-dual steps, z safeguard
+// end of an iteration: filter augmentation, restoration outcome, primal-dual steps, z safeguard.  resto 1: the
+// instances whose line search failed took a restoration step (xr); resto 2 (restoration phase): an instance whose phase
+// ended this iteration (k_rs_update / k_rs_begin set rs_exit) returns to the main iteration at the phase's point, or —
+// when the phase failed or found a point of local infeasibility — stops there, as Ipopt's solve does
+// (Restoration_Failed / Infeasible_Problem_Detected); an instance still in the phase (or entering it, k_rs_init) is
+// left alone; an instance whose search failed with its iteration budget spent does not move.
 __global__ void __launch_bounds__(kIB) k_ipm_update(const IpmK K, int resto) {
     __shared__ Scal S;
     const int64_t b = blockIdx.x;
     const int nf = K.nf, m = K.m;
     load_scal(K, b, S);
+    if (S.rs_on && S.rs_exit == RS_RUNNING) return;  // block-uniform
+    const bool phase_end = S.rs_on;
+    const bool rs_stop = phase_end && (S.rs_exit == RS_FAILED || S.rs_exit == RS_INFEASIBLE);
+    if (rs_stop) {
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            S.done = S.stop = 1;
+            S.status = S.rs_exit == RS_FAILED ? CFX_IPM_RESTORATION_FAILED : CFX_IPM_INFEASIBLE_PROBLEM_DETECTED;
+            S.iters += 1;  // the main iteration whose line search failed
+            S.rs_on = 0;
+            S.rs_exit = RS_RUNNING;
+        }
+        store_scal(K, b, S);
+        return;
+    }
     const bool failed = !S.accepted && !S.done;
     const bool forced = S.forced;
     const bool grow = !S.done && S.accepted && !S.armijo && !forced;
-    const bool reset = failed && resto && m > 0;  // resto 1: restoration step, 2: restoration phase
+    const bool reset = resto == 2 ? phase_end : (failed && resto && m > 0);
     // watchdog bookkeeping (solver.py): an acceptable point ends it; after watchdog_trial_iter_max unacceptable full
     // steps the iterate returns to where it started, and the next line search starts at half its step
     const bool wd_ok = S.wd_on && S.accepted && !forced;
@@ -1188,7 +1241,7 @@ __global__ void __launch_bounds__(kIB) k_ipm_update(const IpmK K, int resto) {
         }
     const bool step = !S.done;
     double alpha = S.alpha;
-    if (reset || !step) alpha = 0.0;
+    if (reset || failed || !step) alpha = 0.0;
     double* x = K.x + b * nf;
     double* zl = K.zl + b * nf;
     double* zu = K.zu + b * nf;
@@ -1254,12 +1307,15 @@ __global__ void __launch_bounds__(kIB) k_ipm_update(const IpmK K, int resto) {
     __syncthreads();
     write_full(K, b, x, K.vx);
     if (threadIdx.x == 0) {
+        K.of[b] = S.sf;  // the phase evaluated its Hessian with objective factor 0
         if (grow) S.fpos += 1;
         if (reset) {
             S.reinit = resto == 1;  // the step re-estimates the multipliers by least squares
             S.lcount = S.lhead = S.lprev = 0;  // the quasi-Newton pairs describe the abandoned region
             S.lsig = 1.0;
         }
+        S.rs_on = 0;
+        S.rs_exit = RS_RUNNING;
         S.alpha = alpha;
         S.iters += step;
         S.nsucc = nsucc;
@@ -1289,6 +1345,15 @@ __global__ void __launch_bounds__(kIB) k_ipm_update(const IpmK K, int resto) {
 // above Ipopt's bound_mult_reset_threshold 1000), the constraint multipliers restart from zero (Ipopt's
 // constr_mult_reset_threshold = 0 discards the least-squares estimate) and the filter from empty (k_ipm_update;
 // measured: cfg 5 from 16 perturbed starts converges 13 / 16 with a fresh filter, 9 / 16 keeping the augmented one).
+// A failed line search of the phase, a point of local infeasibility (its own problem converged) or max_resto_iter of
+// its iterations end the solve of that instance, as in Ipopt.
+//
+// Scheduling: an instance's phase iterations run inside the host's main iterations — one host iteration advances every
+// instance by one iteration of its own mode (main or phase), through the same callback launches, factorisations and
+// line-search loop (the k_ipm_* kernels skip the instances in the phase, the k_rs_* kernels the others).  A batch
+// whose instances enter the phase at staggered times therefore costs max over the instances of their iterations, not
+// their sum (round 3 ran each phase as a nested loop over the whole batch with the other instances idle: 512 starts of
+// cfg 5 serialised into an unbounded number of batch-wide iterations).
 
 // p, n minimising rho (p + n) - mu (ln p + ln n) on c - p + n = 0 (Ipopt's closed form, evaluated without
 // cancellation)
@@ -1325,18 +1390,23 @@ __device__ double rs_merit(const IpmK& K, int64_t b, const double* x, const doub
     return bad > 0 ? INFINITY : fx - mu * lg;
 }
 
-// enter the phase (the instances whose line search failed; counter [0]: instances in the phase)
-__global__ void __launch_bounds__(kIB) k_rs_init(const IpmK K, int slot) {
+// enter the phase: the instances in the main iteration whose line search failed (with iterations left: the phase's
+// iterations count among the instance's); their first phase iteration is the next host iteration, at vx = x
+__global__ void __launch_bounds__(kIB) k_rs_init(const IpmK K) {
     __shared__ double sh[kIB / 64];
     __shared__ Scal S;
     const int64_t b = blockIdx.x;
     const int nf = K.nf, m = K.m;
     load_scal(K, b, S);
-    // per-instance budget: the phase's iterations count among the instance's (not the batch's main iterations)
-    const bool failed = !S.accepted && !S.done;
-    const bool go = failed && S.iters < K.o.max_iter;
-    if (failed && !go)  // out of iterations: it stays where it is
-        for (int i = threadIdx.x; i < nf; i += kIB) K.xr[b * nf + i] = K.x[b * nf + i];
+    const bool failed = !S.rs_on && !S.accepted && !S.done;
+    // Ipopt (BacktrackingLineSearch): "Restoration phase called at acceptable point" — the solve ends there, solved to
+    // the acceptable level (err0 is the current point's scaled KKT error)
+    const bool acceptable = failed && S.err0 <= K.o.acceptable_tol;
+    const bool go = failed && !acceptable && S.iters < K.o.max_iter;
+    if (acceptable && threadIdx.x == 0) {
+        S.done = 1;
+        S.status = CFX_IPM_SOLVED_TO_ACCEPTABLE_LEVEL;
+    }
     if (go) {  // block-uniform
         const double rho = K.o.resto_penalty;
         const double* c = K.gS + b * m;
@@ -1352,6 +1422,7 @@ __global__ void __launch_bounds__(kIB) k_rs_init(const IpmK K, int slot) {
             K.rzp[b * m + j] = mu / p;
             K.rzn[b * m + j] = mu / n;
             K.ry[b * m + j] = 0.0;
+            K.ysc[b * m + j] = 0.0;  // the multipliers of its first Hessian (objective factor 0)
         }
         for (int i = threadIdx.x; i < nf; i += kIB) {
             K.xr[b * nf + i] = K.x[b * nf + i];
@@ -1373,27 +1444,29 @@ __global__ void __launch_bounds__(kIB) k_rs_init(const IpmK K, int slot) {
             S.rs_th0 = S.theta;
             S.rs_dw = S.rs_dwl = 0.0;
             S.rs_it = 0;
+            S.rs_on = 1;
+            S.rs_exit = RS_RUNNING;
+            S.soc = 0;
+            S.lcount = S.lhead = S.lprev = 0;  // L-BFGS: no pairs (no Woodbury correction) during the phase
+            S.lsig = 1.0;
+            K.of[b] = 0.0;
+            atomicAdd(K.rstat, 1ull);
         }
         __syncthreads();
-        write_full(K, b, K.xr + b * nf, K.vt);
-    }
-    if (threadIdx.x == 0) {
-        S.rs_on = go;
-        S.rs_ok = 0;
+        write_full(K, b, K.xr + b * nf, K.vx);
     }
     store_scal(K, b, S);
-    count_add(K, slot, 0, go);
 }
 
-// after g, J_g at the phase iterate (vt): scaling, the phase's optimality error and barrier update, Sigma, the Newton
-// right-hand side, the eliminated (2,2) block and the multipliers of its constraint Hessian
+// after g, J_g at the phase iterate (vx = xr): scaling, the phase's optimality error and barrier update, Sigma, the
+// Newton right-hand side, the eliminated (2,2) block and the multipliers of its constraint Hessian
 __global__ void __launch_bounds__(kIB) k_rs_begin(const IpmK K) {
     __shared__ double sh[kIB / 64];
     __shared__ Scal S;
     const int64_t b = blockIdx.x;
     const int nf = K.nf, m = K.m;
     load_scal(K, b, S);
-    if (!S.rs_on) return;  // block-uniform
+    if (!S.rs_on || S.rs_exit != RS_RUNNING) return;  // block-uniform
     const double rho = K.o.resto_penalty;
     const double* sg = K.sg + b * m;
     double* gS = K.gS + b * m;
@@ -1458,7 +1531,7 @@ __global__ void __launch_bounds__(kIB) k_rs_begin(const IpmK K) {
     // problem accepts: a local minimiser of the infeasibility (Ipopt: "converged to a point of local infeasibility")
     if (mu <= K.o.tol / 10 && e_mu <= K.o.kappa_eps * mu) {
         __syncthreads();
-        if (threadIdx.x == 0) S.rs_on = 0;
+        if (threadIdx.x == 0) S.rs_exit = RS_INFEASIBLE;
         store_scal(K, b, S);
         return;
     }
@@ -1492,7 +1565,7 @@ __global__ void __launch_bounds__(kIB) k_rs_dir(const IpmK K) {
     const int64_t b = blockIdx.x;
     const int nf = K.nf, m = K.m;
     load_scal(K, b, S);
-    if (!S.rs_on) return;  // block-uniform
+    if (!S.rs_on || S.rs_exit != RS_RUNNING) return;  // block-uniform
     const double rho = K.o.resto_penalty, mu = S.rs_mu, tau = S.rs_tau;
     const double* x = K.xr + b * nf;
     const double* xref = K.x + b * nf;
@@ -1578,14 +1651,15 @@ __global__ void __launch_bounds__(kIB) k_rs_dir(const IpmK K) {
     store_scal(K, b, S);
 }
 
-// after g (and f) at the phase's trial point: its own filter test.  counter [0]: phase instances not accepted
-__global__ void __launch_bounds__(kIB) k_rs_accept(const IpmK K, int slot) {
+// after g (and f) at the phase's trial point: its own filter test (k_ipm_accept, launched next, counts the phase
+// instances not accepted)
+__global__ void __launch_bounds__(kIB) k_rs_accept(const IpmK K) {
     __shared__ double sh[kIB / 64];
     __shared__ Scal S;
     const int64_t b = blockIdx.x;
     const int nf = K.nf, m = K.m;
     load_scal(K, b, S);
-    if (S.rs_on && !S.rs_acc) {  // block-uniform
+    if (S.rs_on && S.rs_exit == RS_RUNNING && !S.rs_acc) {  // block-uniform
         const double* sg = K.sg + b * m;
         const double* gt = K.gt + b * m;
         const double* pt = K.rpt + b * m;
@@ -1604,7 +1678,6 @@ __global__ void __launch_bounds__(kIB) k_rs_accept(const IpmK K, int slot) {
         }
     }
     store_scal(K, b, S);
-    count_add(K, slot, 0, S.rs_on && !S.rs_acc);
 }
 
 // the phase's backtracking: halve its step where no trial was accepted
@@ -1613,7 +1686,7 @@ __global__ void __launch_bounds__(kIB) k_rs_next_trial(const IpmK K) {
     const int64_t b = blockIdx.x;
     const int nf = K.nf, m = K.m;
     load_scal(K, b, S);
-    if (!S.rs_on || S.rs_acc) return;  // block-uniform
+    if (!S.rs_on || S.rs_exit != RS_RUNNING || S.rs_acc) return;  // block-uniform
     const double a = S.rs_alpha * 0.5;
     const double* x = K.xr + b * nf;
     const double* dx = K.dxr + b * nf;
@@ -1629,21 +1702,24 @@ __global__ void __launch_bounds__(kIB) k_rs_next_trial(const IpmK K) {
 }
 
 // end of a phase iteration: the step (primal-dual, z safeguard), the phase's filter, the exit test on the original
-// problem and, on exit, the original bound multipliers.  A failed line search of the phase ends it unsuccessfully at
-// its current point.  counter [0]: instances still in the phase
-__global__ void __launch_bounds__(kIB) k_rs_update(const IpmK K, int slot) {
+// problem and, on exit, the original bound multipliers; rs_exit records how the phase ended (k_ipm_update acts on it).
+// A failed line search of the phase, or max_resto_iter iterations of it, fail it (Ipopt: Restoration_Failed).  The
+// instances that go on get their next evaluation point (vx = xr) and Hessian multipliers ready.
+__global__ void __launch_bounds__(kIB) k_rs_update(const IpmK K) {
     __shared__ double sh[kIB / 64];
     __shared__ Scal S;
     const int64_t b = blockIdx.x;
     const int nf = K.nf, m = K.m;
     load_scal(K, b, S);
-    if (S.rs_on && !S.rs_acc) {  // block-uniform
+    if (!S.rs_on || S.rs_exit != RS_RUNNING) return;  // block-uniform
+    if (!S.rs_acc) {
         __syncthreads();
         if (threadIdx.x == 0) {
-            S.rs_on = 0;
+            S.rs_exit = RS_FAILED;
             S.iters += 1;  // Ipopt counts the phase's iterations among the solve's
+            atomicAdd(K.rstat + 1, 1ull);
         }
-    } else if (S.rs_on) {
+    } else {
         const double a = S.rs_alpha, az = S.rs_az, mu = S.rs_mu;
         if (threadIdx.x == 0 && !S.rs_arm) {
             double* rf = K.rfilt + b * kFilt * 2;
@@ -1715,25 +1791,39 @@ __global__ void __launch_bounds__(kIB) k_rs_update(const IpmK K, int slot) {
                     zu0[i] = K.hasU[i] ? 1.0 : 0.0;
                 }
         }
+        const bool budget = S.iters + 1 >= K.o.max_iter, limit = S.rs_it + 1 >= K.o.max_resto_iter;
+        if (!ok && !budget && !limit) {  // the phase goes on from xr
+            write_full(K, b, x, K.vx);
+            for (int j = threadIdx.x; j < m; j += kIB) K.ysc[b * m + j] = K.ry[b * m + j] * sg[j];
+        }
         __syncthreads();
         if (threadIdx.x == 0) {
             S.rs_it += 1;
             S.iters += 1;
-            if (ok) {
-                S.rs_on = 0;
-                S.rs_ok = 1;
-            } else if (S.iters >= K.o.max_iter) {
-                S.rs_on = 0;
-            }
+            atomicAdd(K.rstat + 1, 1ull);
+            if (ok)
+                S.rs_exit = RS_OK;
+            else if (budget)
+                S.rs_exit = RS_BUDGET;
+            else if (limit)
+                S.rs_exit = RS_FAILED;
         }
     }
     store_scal(K, b, S);
-    count_add(K, slot, 0, S.rs_on);
 }
 
-// the phase's iteration limit: the instances still in it leave it, unsuccessfully, at its current point
+// after the last host iteration: the instances still in the phase leave it, not converged (a failed phase k_ipm_update
+// has not seen yet stops the instance as it would have)
 __global__ void __launch_bounds__(kIB) k_rs_finish(const IpmK K) {
-    if (threadIdx.x == 0) K.sc[blockIdx.x].rs_on = 0;
+    if (threadIdx.x == 0) {
+        Scal& S = K.sc[blockIdx.x];
+        if (S.rs_on && (S.rs_exit == RS_FAILED || S.rs_exit == RS_INFEASIBLE)) {
+            S.status = S.rs_exit == RS_FAILED ? CFX_IPM_RESTORATION_FAILED : CFX_IPM_INFEASIBLE_PROBLEM_DETECTED;
+            S.done = S.stop = 1;
+        }
+        S.rs_on = 0;
+        S.rs_exit = RS_RUNNING;
+    }
 }
 
 // project onto the original bounds (Ipopt honor_original_bounds) and write the final point into vx
@@ -1747,7 +1837,8 @@ __global__ void __launch_bounds__(kIB) k_ipm_final(const IpmK K) {
 
 // results: y of the unscaled problem, converged / iterations / KKT error
 __global__ void __launch_bounds__(kIB) k_ipm_out(const IpmK K, double* __restrict__ yo, int32_t* __restrict__ conv,
-                                                 int32_t* __restrict__ its, double* __restrict__ kkt) {
+                                                 int32_t* __restrict__ its, double* __restrict__ kkt,
+                                                 int32_t* __restrict__ status, int wall) {
     const int64_t b = blockIdx.x;
     const Scal& S = K.sc[b];
     if (yo)
@@ -1756,6 +1847,10 @@ __global__ void __launch_bounds__(kIB) k_ipm_out(const IpmK K, double* __restric
         if (conv) conv[b] = S.done && !S.stop;
         if (its) its[b] = S.iters;
         if (kkt) kkt[b] = S.err0;
+        // still iterating when the host loop ended: its bound (max_iter host iterations) or max_wall_time
+        if (status)
+            status[b] = S.done ? S.status
+                               : (wall ? CFX_IPM_MAXIMUM_WALLTIME_EXCEEDED : CFX_IPM_MAXIMUM_ITERATIONS_EXCEEDED);
     }
 }
 
@@ -2017,7 +2112,8 @@ struct cfx_ipm {
     hipStream_t stream = nullptr;
     // staging for host inputs / outputs
     double *d_fv = nullptr, *d_yo = nullptr, *d_kkt = nullptr;
-    int32_t *d_conv = nullptr, *d_its = nullptr;
+    int32_t *d_conv = nullptr, *d_its = nullptr, *d_status = nullptr;
+    std::vector<int32_t> h_status;  // CFX_IPM_* status per instance of the last solve (cfx_ipm_get_status)
     // J_g's constant values (cfx_jac_constant_mask) stay in K.jac after the first full evaluation: later evaluations
     // pass CFX_KEEP_CONSTANT_JAC (CFX_IPM_KEEPJ=0 turns it off, for A/B runs)
     bool keepj = true, jac_filled = false;
@@ -2102,6 +2198,8 @@ extern "C" void cfx_ipm_default_options(cfx_ipm_options* o) {
     o->required_infeasibility_reduction = 0.9;
     o->filter_reset_trigger = 5;
     o->max_filter_resets = 0;  // Ipopt: 5; off here
+    o->max_wall_time = 1e20;   // Ipopt max_wall_time
+    o->print_frequency_time = 0.0;
 }
 
 // CSR of `key` (values in [0, nkeys)) with the sources of each key in increasing source order
@@ -2153,7 +2251,8 @@ extern "C" int cfx_ipm_create(cfx_handle* h, const double* lb, const double* ub,
          (K.o.limited_memory_max_history < 1 || K.o.limited_memory_max_history > 16)) ||
         (K.o.restoration != CFX_RESTORATION_STEP && K.o.restoration != CFX_RESTORATION_PHASE) ||
         K.o.max_resto_iter < 0 || !(K.o.resto_penalty > 0) || !(K.o.required_infeasibility_reduction > 0) ||
-        !(K.o.required_infeasibility_reduction < 1) || s->B > 0x7fffffff) {
+        !(K.o.required_infeasibility_reduction < 1) || K.o.filter_reset_trigger < 1 || K.o.max_filter_resets < 0 ||
+        !(K.o.max_wall_time > 0) || !(K.o.print_frequency_time >= 0) || s->B > 0x7fffffff) {
         s->err = "cfx_ipm_create: the handle must use CFX_LAYOUT_AOS (or batch 1) and the options must be valid";
         return create_fail(s, CFX_EINVAL);
     }
@@ -2562,14 +2661,16 @@ extern "C" int cfx_ipm_create(cfx_handle* h, const double* lb, const double* ub,
         K.rzl = dalloc<double>(s, B * nf, &rc);
         K.rzu = dalloc<double>(s, B * nf, &rc);
         K.rfilt = dalloc<double>(s, B * kFilt * 2, &rc);
-        K.ofz = dalloc<double>(s, B, &rc);
     }
+    K.rstat = dalloc<unsigned long long>(s, 2, &rc);
     K.cnt = dalloc<int32_t>(s, 4 * kSlots, &rc);
     s->d_fv = dalloc<double>(s, B * K.nfix, &rc);
     s->d_yo = dalloc<double>(s, B * m, &rc);
     s->d_kkt = dalloc<double>(s, B, &rc);
     s->d_conv = dalloc<int32_t>(s, B, &rc);
     s->d_its = dalloc<int32_t>(s, B, &rc);
+    s->d_status = dalloc<int32_t>(s, B, &rc);
+    s->h_status.assign(B, CFX_IPM_MAXIMUM_ITERATIONS_EXCEEDED);
     if (rc == CFX_OK && (hipHostMalloc((void**)&s->h_pub, 16 * sizeof(int32_t), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
                          hipHostGetDevicePointer((void**)&s->d_pub, s->h_pub, 0) != hipSuccess)) {
         rc = CFX_ENOMEM;
@@ -2680,55 +2781,6 @@ struct Run {
         }
         return CFX_OK;
     }
-    // Ipopt's restoration phase for the instances whose line search failed (k_rs_*): its iterations run the whole
-    // batch's callbacks and factorisations, the kernels act on the instances in the phase only
-    int resto_phase() {
-        IpmK& K = s->K;
-        const dim3 blk(kIB);
-        int32_t c[4];
-        int sl = next_slot();
-        hipLaunchKernelGGL(k_rs_init, g, blk, 0, st, K, sl);
-        IPM_HIP(s, hipGetLastError());
-        IPM_RUN(read(sl, c));
-        s->st.resto_phases++;
-        for (int r = 0; r < K.o.max_resto_iter && c[0] > 0; ++r) {
-            IPM_RUN(eval_full(K.vt));
-            hipLaunchKernelGGL(k_rs_begin, g, blk, 0, st, K);
-            IPM_HIP(s, hipGetLastError());
-            if (!K.lbfgs) {  // W of the phase: the Hessian of y^T c (objective factor 0); L-BFGS runs it without W
-                cfx_internal_msk_stash(s->h, 2);  // vt is the point of eval_full above
-                IPM_CFX(s, cfx_eval_h(s->h, K.vt, K.ofz, K.ysc, K.hv, CFX_DEVICE));
-                s->st.eval_h++;
-            }
-            for (int attempt = 0; attempt < 12; ++attempt) {
-                IPM_RUN(kkt_factor(KKT_RSNLP));
-                sl = next_slot();
-                hipLaunchKernelGGL(k_ipm_curv, g, blk, 0, st, K, sl, 1);
-                IPM_HIP(s, hipGetLastError());
-                IPM_RUN(read(sl, c));
-                if (c[0] == 0 || c[1] == 0) break;
-            }
-            hipLaunchKernelGGL(k_rs_dir, g, blk, 0, st, K);
-            IPM_HIP(s, hipGetLastError());
-            for (int ls = 0; ls < K.o.max_backtrack; ++ls) {
-                IPM_RUN(eval_gf(true));
-                sl = next_slot();
-                hipLaunchKernelGGL(k_rs_accept, g, blk, 0, st, K, sl);
-                IPM_HIP(s, hipGetLastError());
-                IPM_RUN(read(sl, c));
-                if (c[0] == 0) break;
-                hipLaunchKernelGGL(k_rs_next_trial, g, blk, 0, st, K);
-            }
-            sl = next_slot();
-            hipLaunchKernelGGL(k_rs_update, g, blk, 0, st, K, sl);
-            IPM_HIP(s, hipGetLastError());
-            IPM_RUN(read(sl, c));
-            s->st.resto_iterations++;
-        }
-        hipLaunchKernelGGL(k_rs_finish, g, blk, 0, st, K);
-        IPM_HIP(s, hipGetLastError());
-        return CFX_OK;
-    }
     // L-BFGS: after a Newton factorisation of K0, P = K0^-1 Z column by column, C = M - Z^T P, and the Newton
     // solution corrected (rb += P C^-1 Z^T rb)
     int lbfgs_newton() {
@@ -2771,10 +2823,9 @@ static int ipm_solve(cfx_ipm* s, const double* v0, const double* fixed_values, d
     const dim3 blk(kIB);
     s->st.eval_all = s->st.eval_g_f = s->st.eval_h = s->st.kkt_factor = s->st.iterations = s->st.host_syncs = 0;
     s->st.resto_phases = s->st.resto_iterations = 0;
-    if (K.rsphase) {  // zero objective factor of the phase's Hessian; the (2,2) block of instances outside it
-        IPM_HIP(s, hipMemsetAsync(K.ofz, 0, B * sizeof(double), st));
+    IPM_HIP(s, hipMemsetAsync(K.rstat, 0, 2 * sizeof(unsigned long long), st));
+    if (K.rsphase)  // the (2,2) block of instances outside the phase
         IPM_HIP(s, hipMemsetAsync(K.rdc, 0, B * K.m * sizeof(double), st));
-    }
     s->slot = 0;
     IPM_HIP(s, hipMemsetAsync(K.cnt, 0, 4 * kSlots * sizeof(int32_t), st));
     IPM_HIP(s, hipMemsetAsync(K.rb, 0, B * K.nKp * sizeof(double), st));  // padding rows of the blocks stay 0
@@ -2787,11 +2838,29 @@ static int ipm_solve(cfx_ipm* s, const double* v0, const double* fixed_values, d
     hipLaunchKernelGGL(k_ipm_init, R.g, blk, 0, st, K);
     IPM_HIP(s, hipGetLastError());
     IPM_HIP(s, hipMemcpyAsync(K.vt, K.vx, B * K.n * sizeof(double), hipMemcpyDeviceToDevice, st));
-    bool reinit = K.m > 0;
+    bool reinit = K.m > 0, wall_stop = false;
     int32_t c[4];
+    int n_active = (int)B, n_resto = 0;
+    double last_print = 0.0;
+    // One host iteration advances every instance still iterating by one iteration of its own: a main iteration, or
+    // one of the restoration phase (k_rs_*) for the instances in it — the same callback launches, factorisations and
+    // line-search loop serve both (section "Ipopt's feasibility-restoration phase" above).  Every instance's
+    // iterations (phase ones included) count against its max_iter, so max_iter host iterations bound the loop.
     for (int it = 0; it < K.o.max_iter; ++it) {
+        const double elapsed = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        if (elapsed > K.o.max_wall_time) {  // Ipopt max_wall_time: the instances still iterating stop where they are
+            wall_stop = true;
+            break;
+        }
+        if (K.o.print_frequency_time > 0 && it > 0 && elapsed - last_print >= K.o.print_frequency_time) {
+            std::fprintf(stderr, "cfx_ipm: iteration %d, %.1f s: %d of %lld instances iterating, %d in restoration\n", it,
+                         elapsed, n_active, (long long)B, n_resto);
+            std::fflush(stderr);
+            last_print = elapsed;
+        }
         // after an ordinary iteration the multipliers of the Hessian are known before k_ipm_begin (k_ipm_update
-        // formed them): g, J_g, f, grad f and the Hessian of the new iterate from one call
+        // formed them; k_rs_update / k_rs_init for the instances in the restoration phase, objective factor 0): g,
+        // J_g, f, grad f and the Hessian of the new iterate from one call
         const bool fused = it > 0 && !reinit && !K.lbfgs && K.m > 0;
         if (fused) {
             IPM_CFX(s, cfx_eval_all_h(s->h, K.vx, K.of, K.ysc, K.graw, K.jac, K.fraw, K.grad, K.hv, s->jac_flags()));
@@ -2809,6 +2878,7 @@ static int ipm_solve(cfx_ipm* s, const double* v0, const double* fixed_values, d
         } else {
             hipLaunchKernelGGL(k_ipm_begin, R.g, blk, 0, st, K, 1, R.next_slot());
         }
+        if (K.rsphase) hipLaunchKernelGGL(k_rs_begin, R.g, blk, 0, st, K);
         reinit = false;
         IPM_HIP(s, hipGetLastError());
         if (K.lbfgs) {  // quasi-Newton pair of the last step, M (no eval_h: hv stays zero)
@@ -2825,9 +2895,13 @@ static int ipm_solve(cfx_ipm* s, const double* v0, const double* fixed_values, d
             IPM_RUN(R.kkt_factor(KKT_NEWTON));
             if (K.lbfgs) IPM_RUN(R.lbfgs_newton());
             const int sl = R.next_slot();
-            hipLaunchKernelGGL(k_ipm_curv, R.g, blk, 0, st, K, sl, 0);
+            hipLaunchKernelGGL(k_ipm_curv, R.g, blk, 0, st, K, sl);
             IPM_HIP(s, hipGetLastError());
             IPM_RUN(R.read(sl, c));
+            if (attempt == 0) {
+                n_active = c[0];
+                n_resto = c[2];
+            }
             if (c[0] == 0) {
                 all_done = true;
                 break;
@@ -2836,11 +2910,13 @@ static int ipm_solve(cfx_ipm* s, const double* v0, const double* fixed_values, d
         }
         if (all_done) break;
         hipLaunchKernelGGL(k_ipm_dir, R.g, blk, 0, st, K, it);
-        // filter line search with second-order corrections
+        if (K.rsphase) hipLaunchKernelGGL(k_rs_dir, R.g, blk, 0, st, K);
+        // filter line search with second-order corrections (the phase's own filter line search alongside)
         int notacc = 0;
         for (int ls = 0; ls < K.o.max_backtrack; ++ls) {
             IPM_RUN(R.eval_gf(true));
             int sl = R.next_slot();
+            if (K.rsphase) hipLaunchKernelGGL(k_rs_accept, R.g, blk, 0, st, K);
             hipLaunchKernelGGL(k_ipm_accept, R.g, blk, 0, st, K, ls, sl);
             IPM_HIP(s, hipGetLastError());
             IPM_RUN(R.read(sl, c));
@@ -2860,11 +2936,15 @@ static int ipm_solve(cfx_ipm* s, const double* v0, const double* fixed_values, d
                 }
             if (notacc == 0) break;
             hipLaunchKernelGGL(k_ipm_next_trial, R.g, blk, 0, st, K);
+            if (K.rsphase) hipLaunchKernelGGL(k_rs_next_trial, R.g, blk, 0, st, K);
         }
-        // failed line searches: a feasibility-restoration step, a fresh filter and least-squares multipliers
+        // failed line searches: the restoration phase (its iterations for the instances in it; the instances whose
+        // search failed enter it), or a feasibility-restoration step, a fresh filter and least-squares multipliers
         const bool resto = notacc > 0 && K.m > 0;
-        if (resto && K.rsphase) {
-            IPM_RUN(R.resto_phase());
+        if (K.rsphase) {
+            hipLaunchKernelGGL(k_rs_update, R.g, blk, 0, st, K);
+            if (resto) hipLaunchKernelGGL(k_rs_init, R.g, blk, 0, st, K);
+            IPM_HIP(s, hipGetLastError());
         } else if (resto) {
             IPM_RUN(R.kkt_factor(KKT_RESTO));
             int sl = R.next_slot();
@@ -2879,17 +2959,24 @@ static int ipm_solve(cfx_ipm* s, const double* v0, const double* fixed_values, d
             }
             reinit = true;
         }
-        hipLaunchKernelGGL(k_ipm_update, R.g, blk, 0, st, K, resto ? (K.rsphase ? 2 : 1) : 0);
+        hipLaunchKernelGGL(k_ipm_update, R.g, blk, 0, st, K, K.rsphase ? 2 : (resto ? 1 : 0));
         IPM_HIP(s, hipGetLastError());
         s->st.iterations++;
     }
+    if (K.rsphase) hipLaunchKernelGGL(k_rs_finish, R.g, blk, 0, st, K);
     hipLaunchKernelGGL(k_ipm_final, R.g, blk, 0, st, K);
     IPM_CFX(s, cfx_eval_all(s->h, K.vx, K.graw, nullptr, K.fraw, nullptr, CFX_DEVICE));
     s->st.eval_g_f++;
     hipLaunchKernelGGL(k_ipm_out, R.g, blk, 0, st, K, devp ? y_out : (y_out ? s->d_yo : nullptr),
                        devp ? conv_out : (conv_out ? s->d_conv : nullptr), devp ? its_out : (its_out ? s->d_its : nullptr),
-                       devp ? kkt_out : (kkt_out ? s->d_kkt : nullptr));
+                       devp ? kkt_out : (kkt_out ? s->d_kkt : nullptr), s->d_status, (int)wall_stop);
     IPM_HIP(s, hipGetLastError());
+    unsigned long long rstat[2] = {0, 0};
+    IPM_HIP(s, hipMemcpyAsync(rstat, K.rstat, sizeof(rstat), hipMemcpyDeviceToHost, st));
+    IPM_HIP(s, hipMemcpyAsync(s->h_status.data(), s->d_status, B * sizeof(int32_t), hipMemcpyDeviceToHost, st));
+    IPM_HIP(s, hipStreamSynchronize(st));
+    s->st.resto_phases = (int64_t)rstat[0];
+    s->st.resto_iterations = (int64_t)rstat[1];
     if (v_out) IPM_HIP(s, hipMemcpyAsync(v_out, K.vx, B * K.n * sizeof(double), kout, st));
     if (f_out) IPM_HIP(s, hipMemcpyAsync(f_out, K.fraw, B * sizeof(double), kout, st));
     if (!devp) {
@@ -2908,6 +2995,12 @@ extern "C" int cfx_ipm_solve(cfx_ipm* s, const double* v0, const double* fixed_v
     if (!s) return CFX_EINVAL;
     if (!v0) return ipm_fail(s, CFX_EINVAL, "cfx_ipm_solve: v0 is NULL");
     return ipm_solve(s, v0, fixed_values, v, y, f, converged, iterations, kkt_error, flags);
+}
+
+extern "C" int cfx_ipm_get_status(const cfx_ipm* s, int32_t* status) {
+    if (!s || !status) return CFX_EINVAL;
+    std::memcpy(status, s->h_status.data(), s->h_status.size() * sizeof(int32_t));
+    return CFX_OK;
 }
 
 extern "C" int cfx_ipm_get_stats(const cfx_ipm* s, cfx_ipm_stats* out) {

@@ -58,10 +58,12 @@ hipError_t launch_hessian(int model, int scheme, int tmax, const KParams& P, con
                           const double* V, const double* LAM, double* H, double* G, double* J, hipStream_t s);
 
 // direct collocation (cfx_colloc.h, instantiated in cfx_inst_colloc.hip)
-hipError_t launch_colloc(int model, int tmax, const KParams& P, const double* V, double* G, double* J,
+// ni: adjacent instances per lane (1 or 2; the Ding families, degrees 1..5).  launch_colloc_hess with G, J (both or
+// neither): the same launch writes g and J_g too (cfx_eval_all_h)
+hipError_t launch_colloc(int model, int tmax, int ni, const KParams& P, const double* V, double* G, double* J,
                          hipStream_t s);
 hipError_t launch_colloc_hess(int model, int tmax, const KParams& P, const HTask* tasks, int ntasks, int bs,
-                              const double* V, const double* LAM, double* H, hipStream_t s);
+                              const double* V, const double* LAM, double* H, double* G, double* J, hipStream_t s);
 
 template <int MODEL, int SCHEME, int DJ, int TMAX>
 hipError_t launch_hessian_t(const KParams& P, const HTask* tasks, int ntasks, int bs, const double* V,

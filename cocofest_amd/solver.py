@@ -57,9 +57,8 @@ class IpmOptions:
     # limited_memory_max_history pairs, Ipopt's defaults)
     hessian_approximation: str = "exact"
     limited_memory_max_history: int = 6
-    # what a failed line search starts: "phase" — Ipopt's feasibility-restoration phase (an NLP over the constraint
-    # violation, cfx_ipm only), "step" — one minimum-norm step on g = 0 (this class's algorithm); None: each solver's
-    # own (NativeIpm "phase", BatchedIpm "step")
+    # what a failed line search starts: "phase" (default; None means it too) — Ipopt's feasibility-restoration phase,
+    # an NLP over the constraint violation; "step" — one minimum-norm step on g = 0 then least-squares multipliers
     restoration: str | None = None
     max_resto_iter: int = 200
     resto_penalty: float = 1000.0            # Ipopt resto_penalty_parameter (rho)
@@ -70,7 +69,17 @@ class IpmOptions:
     # and cfg 5's multistart)
     filter_reset_trigger: int = 5
     max_filter_resets: int = 0
+    # Ipopt's max_wall_time (s): the instances still iterating stop there (status -5); print_frequency_time (s, 0:
+    # off): the native solver prints a progress line (iteration, instances iterating, in restoration) this often
+    max_wall_time: float = 1e20
+    print_frequency_time: float = 0.0
     verbose: bool = False
+
+    def __post_init__(self):
+        if self.filter_reset_trigger < 1 or self.max_filter_resets < 0:
+            raise ValueError("filter_reset_trigger must be >= 1 and max_filter_resets >= 0")
+        if not self.max_wall_time > 0 or not self.print_frequency_time >= 0:
+            raise ValueError("max_wall_time must be > 0 and print_frequency_time >= 0")
 
 
 class Solver:
@@ -89,7 +98,8 @@ class Solver:
                     "_watchdog_trial_iter_max": "watchdog_trial_iter_max", "_max_resto_iter": "max_resto_iter",
                     "_resto_penalty_parameter": "resto_penalty",
                     "_required_infeasibility_reduction": "required_infeasibility_reduction",
-                    "_filter_reset_trigger": "filter_reset_trigger", "_max_filter_resets": "max_filter_resets"}
+                    "_filter_reset_trigger": "filter_reset_trigger", "_max_filter_resets": "max_filter_resets",
+                    "_max_wall_time": "max_wall_time", "_print_frequency_time": "print_frequency_time"}
         _IGNORED = {"show_online_optim", "show_options", "_print_level", "_linear_solver", "_nlp_scaling_method",
                     "_check_derivatives_for_naninf", "_c_compile", "_print_timing_statistics", "_output_file",
                     "_constr_viol_tol", "_dual_inf_tol", "_compl_inf_tol"}
@@ -167,6 +177,9 @@ class IpmResult:
     kkt_error: np.ndarray
     wall_time: float
     n_callbacks: dict = field(default_factory=dict)
+    # per instance, Ipopt's ApplicationReturnStatus (cocofest_amd._cfx.IPM_STATUS): 0 solved, 1 solved to acceptable
+    # level, 2 local infeasibility, -1 maximum iterations, -2 restoration failed, -5 maximum wall time
+    status: np.ndarray | None = None
 
 
 class _SegmentSum:
@@ -208,9 +221,10 @@ class BatchedIpm:
         self.ocp = ocp
         self.B = batch
         self.opt = options or IpmOptions()
+        self.opt.__post_init__()  # options set after construction (Solver.IPOPT.apply) are checked too
         if self.opt.restoration not in (None, "step", "phase"):
             raise ValueError("restoration must be 'phase' or 'step'")
-        self._phase = self.opt.restoration == "phase"  # BatchedIpm's own default is the restoration step
+        self._phase = self.opt.restoration in (None, "phase")  # the native solver's default too
         if self.opt.hessian_approximation != "exact":
             raise ValueError("BatchedIpm: hessian_approximation='limited-memory' is implemented by the native interior "
                              "point (NativeIpm / cfx_ipm) only")
@@ -436,6 +450,7 @@ class BatchedIpm:
         delta_w_last = torch.zeros((B,), dtype=torch.float64, device=self.dev)
         done = torch.zeros((B,), dtype=torch.bool, device=self.dev)
         stopped = torch.zeros((B,), dtype=torch.bool, device=self.dev)
+        status = torch.full((B,), -1, dtype=torch.int32, device=self.dev)  # Ipopt ApplicationReturnStatus
         iters = torch.zeros((B,), dtype=torch.int64, device=self.dev)
         acc_count = torch.zeros((B,), dtype=torch.int64, device=self.dev)
         err0 = torch.full((B,), np.inf, dtype=torch.float64, device=self.dev)
@@ -460,6 +475,9 @@ class BatchedIpm:
         it = -1
         while it + 1 < opt.max_iter:
             it += 1
+            if time.perf_counter() - t0 > opt.max_wall_time:  # Ipopt max_wall_time
+                status = torch.where(done, status, torch.full_like(status, -5))
+                break
             vfull = full(x)
             g, jv, f, gF = self._scaled_all(vfull)
             sl = torch.where(hasL, x - lbF, torch.ones_like(x))
@@ -481,9 +499,11 @@ class BatchedIpm:
             err0 = torch.maximum(torch.maximum(e_d, e_p), e_c0)
             acc_count = torch.where(err0 <= opt.acceptable_tol, acc_count + 1, torch.zeros_like(acc_count))
             newly = (~done) & ((err0 <= opt.tol) | (acc_count >= opt.acceptable_iter))
+            status = torch.where(newly, torch.where(err0 <= opt.tol, 0, 1).to(status.dtype), status)
             done = done | newly
             # an instance whose iterations (restoration-phase ones included) reach max_iter stops, unconverged
             out_of_iters = (~done) & (iters >= opt.max_iter)
+            status = torch.where(out_of_iters, torch.full_like(status, -1), status)
             stopped = stopped | out_of_iters
             done = done | out_of_iters
             if bool(done.all()):
@@ -636,18 +656,33 @@ class BatchedIpm:
             # Sigma + I, backtracking on ||g||_1 only), then a fresh filter and least-squares multipliers
             x_new = x_acc
             failed = failed & ~done
+            if self._phase:
+                # Ipopt: "Restoration phase called at acceptable point" ends the solve, solved to the acceptable level
+                at_acc = failed & (err0 <= opt.acceptable_tol)
+                status = torch.where(at_acc, torch.ones_like(status), status)
+                done = done | at_acc
+                failed = failed & ~at_acc
             if bool(failed.any()) and m and self._phase:
-                # Ipopt's restoration phase; its iterations count among the solve's
-                xr, zl, zu, filt, fpos, its_r = self._restoration_phase(failed, x, zl, zu, g, theta, phi, mu, tau,
-                                                                         filt, fpos, iters)
-                x_new = torch.where(failed[:, None], xr, x_acc)
-                iters = iters + its_r
+                # Ipopt's restoration phase; its iterations count among the solve's.  An instance whose budget is
+                # spent does not enter it (and does not move); a phase that fails (its line search, max_resto_iter)
+                # or finds a point of local infeasibility stops the instance where it is, as Ipopt's solve stops
+                entered = failed & (iters < opt.max_iter)
+                xr, zl, zu, filt, fpos, its_r, rexit = self._restoration_phase(failed, x, zl, zu, g, theta, phi, mu,
+                                                                                tau, filt, fpos, iters)
+                back = entered & ((rexit == self.RS_OK) | (rexit == self.RS_BUDGET))
+                rstop = entered & ~back
+                x_new = torch.where(back[:, None], xr, x_acc)
+                iters = iters + its_r + rstop.long()  # a stopped instance takes no step below: count its iteration
+                status = torch.where(rstop, torch.where(rexit == self.RS_INFEASIBLE, torch.full_like(status, 2),
+                                                        torch.full_like(status, -2)), status)
+                done = done | rstop
+                stopped = stopped | rstop
                 # after the phase: zero constraint multipliers (Ipopt's constr_mult_reset_threshold = 0 ignores the
                 # least-squares estimate) and a fresh filter (measured: cfg 5 from 16 perturbed starts converges
                 # 13 / 16 with it against 9 / 16 keeping the augmented filter, scripts/r3/resto_variants.py)
-                y = torch.where(failed[:, None], torch.zeros_like(y), y)
-                filt = torch.where(failed[:, None, None], torch.tensor([np.inf, -np.inf], dtype=torch.float64,
-                                                                       device=self.dev), filt)
+                y = torch.where(back[:, None], torch.zeros_like(y), y)
+                filt = torch.where(back[:, None, None], torch.tensor([np.inf, -np.inf], dtype=torch.float64,
+                                                                     device=self.dev), filt)
                 alpha = torch.where(failed, torch.zeros_like(alpha), alpha)
             elif bool(failed.any()) and m:
                 xr = self._restoration_step(x, g, jv, sig, tau)
@@ -693,7 +728,8 @@ class BatchedIpm:
         return IpmResult(v=vfinal.cpu().numpy(), y=y.cpu().numpy(), f=f.cpu().numpy(),
                          converged=(done & ~stopped).cpu().numpy(),
                          iterations=iters.cpu().numpy(), kkt_error=err0.cpu().numpy(),
-                         wall_time=time.perf_counter() - t0, n_callbacks=dict(self.calls))
+                         wall_time=time.perf_counter() - t0, n_callbacks=dict(self.calls),
+                         status=status.cpu().numpy())
 
     def _full(self, xf):
         vv = self._v_template.clone()
@@ -737,6 +773,8 @@ class BatchedIpm:
             a = a * 0.5
         return out
 
+    RS_OK, RS_FAILED, RS_INFEASIBLE, RS_BUDGET = 1, 2, 3, 4  # how a restoration phase ended (cfx_ipm.hip rs_exit)
+
     def _restoration_phase(self, on, x, zl, zu, g, theta, phi, mu, tau, filt, fpos, iters):
         """Ipopt's feasibility-restoration phase for the instances ``on`` (their line search failed):
         min rho sum(p + n) + 1/2 sum_i zeta D_i^2 (x_i - x_r,i)^2 s.t. c(x) - p + n = 0, p, n >= 0 and the bounds
@@ -747,10 +785,14 @@ class BatchedIpm:
         ||c||_1 <= required_infeasibility_reduction * theta, when its own sub-problem has converged (a local
         minimiser of the infeasibility), after a failed line search of its own, after max_resto_iter iterations, or
         when the instance's iterations (``iters`` + the phase's) reach max_iter — the budget is per instance: one
-        instance's phase does not use up the batch's main iterations.  On success the original bound multipliers take a Newton step for complementarity over the
+        instance's phase does not use up the batch's main iterations.  The exit code (RS_*) says which: the caller
+        stops the instances whose phase failed (RS_FAILED: its line search or max_resto_iter) or found local
+        infeasibility (RS_INFEASIBLE), as Ipopt does.  On success the original bound multipliers take a Newton step for complementarity over the
         phase's dx (fraction to the boundary; reset to 1 above 1e3); the caller then restarts the constraint
         multipliers from zero and the filter from empty.  The executable specification of
-        csrc/cfx_ipm.hip's k_rs_* kernels.  Returns (x_r, zl, zu, filt, fpos, iterations per instance)."""
+        csrc/cfx_ipm.hip's k_rs_* kernels (which run each instance's phase iterations inside the host's main
+        iterations instead of a nested loop: the same per-instance arithmetic).  Returns (x_r, zl, zu, filt, fpos,
+        iterations per instance, exit code per instance)."""
         torch = self.torch
         opt = self.opt
         B, nf, m = self.B, len(self.free), self.m
@@ -784,6 +826,7 @@ class BatchedIpm:
         tmax = tmin = None
         dref = torch.clamp(xref.abs(), min=1.0) ** 2
         of0 = torch.zeros((B,), dtype=torch.float64, device=self.dev)
+        rexit = torch.zeros((B,), dtype=torch.int64, device=self.dev)
 
         def merit(xx, pp, nn, mu_):
             w = mu_.sqrt()[:, None] / dref
@@ -823,7 +866,9 @@ class BatchedIpm:
                 muR = torch.where(dec, torch.clamp(torch.minimum(opt.kappa_mu * muR, muR ** opt.theta_mu),
                                                    min=opt.tol / 10), muR)
             # its sub-problem solved without a point the original problem accepts: local infeasibility
-            on = on & ~((muR <= opt.tol / 10) & (e_last <= opt.kappa_eps * muR))
+            infeas = on & (muR <= opt.tol / 10) & (e_last <= opt.kappa_eps * muR)
+            rexit = torch.where(infeas, torch.full_like(rexit, self.RS_INFEASIBLE), rexit)
+            on = on & ~infeas
             if not bool(on.any()):
                 break
             mR = muR[:, None]
@@ -887,7 +932,8 @@ class BatchedIpm:
                     break
                 alpha = torch.where(acc, alpha, alpha * 0.5)
             its = its + on.long()
-            on = on & acc  # a failed line search of the phase ends it where it is
+            rexit = torch.where(on & ~acc, torch.full_like(rexit, self.RS_FAILED), rexit)
+            on = on & acc  # a failed line search of the phase fails it
             grow = on & ~arm_acc
             rslot = (torch.arange(rfilt.shape[1], device=self.dev) == (r % rfilt.shape[1]))[None, :, None]
             rfilt = torch.where(grow[:, None, None] & rslot,
@@ -928,8 +974,13 @@ class BatchedIpm:
                       f"th {float(th[0]):.3e} th0 {float(th0[0]):.3e} dom {int(dominated[0])} a {float(alpha[0]):.2e} "
                       f"ap {float(a_p[0]):.2e} az {float(a_z[0]):.2e} dw {float(dw[0]):.1e} done {int(done_r[0])} ed {float(ed[0]):.2e} "
                       f"ep {float(ep[0]):.2e} emu {float(e_last[0]):.2e}")
-            on = on & ~done_r & (iters + its < opt.max_iter)
-        return xR, zl, zu, filt, fpos, its
+            rexit = torch.where(done_r, torch.full_like(rexit, self.RS_OK), rexit)
+            budget = on & ~done_r & (iters + its >= opt.max_iter)
+            rexit = torch.where(budget, torch.full_like(rexit, self.RS_BUDGET), rexit)
+            on = on & ~done_r & ~budget
+        # max_resto_iter iterations of the phase: Ipopt's Restoration_Failed
+        rexit = torch.where(on, torch.full_like(rexit, self.RS_FAILED), rexit)
+        return xR, zl, zu, filt, fpos, its, rexit
 
     def _kkt_solve(self, K, rhs):
         """Solve with factored KKT K for a natural-order right-hand side (free variables, then g rows)."""
@@ -1038,7 +1089,8 @@ _NATIVE_OPTIONS = ("tol", "max_iter", "acceptable_tol", "acceptable_iter", "mu_i
                    "bound_push", "tau_min", "kappa_eps", "kappa_mu", "theta_mu", "s_max", "armijo", "max_backtrack",
                    "delta_c", "curv_min", "max_soc", "kappa_soc", "watchdog_shortened_iter_trigger",
                    "watchdog_trial_iter_max", "limited_memory_max_history", "max_resto_iter", "resto_penalty",
-                   "required_infeasibility_reduction", "filter_reset_trigger", "max_filter_resets")
+                   "required_infeasibility_reduction", "filter_reset_trigger", "max_filter_resets", "max_wall_time",
+                   "print_frequency_time")
 _HESSIAN_APPROXIMATION = {"exact": 0, "limited-memory": 1}
 _RESTORATION = {"step": 0, "phase": 1, None: 1}
 
@@ -1079,7 +1131,7 @@ class NativeIpm:
         self.calls = {k: int(st[k]) for k in ("eval_all", "eval_h", "eval_g_f", "kkt_factor")}
         self.last_stats = st
         return IpmResult(v=v, y=y, f=f, converged=conv, iterations=its, kkt_error=kkt, wall_time=wall,
-                         n_callbacks=dict(self.calls))
+                         n_callbacks=dict(self.calls), status=self.ipm.status())
 
     def close(self):
         self.ipm.close()

@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define CFX_ABI_VERSION 5
+#define CFX_ABI_VERSION 6
 
 /* return codes */
 #define CFX_OK 0
@@ -76,7 +76,8 @@ extern "C" {
 /* 64-instance tiles: element e of instance b at ((b / 64) * len + e) * 64 + b % 64, len = the per-instance
    length of the buffer (nv, ng, nnz_jac, nv for grad, 1 for f).  batch % 64 == 0.  Keeps each wave's stores
    inside one contiguous tile instead of spreading them over len rows B apart (+6 % on the store-bound
-   g + J_g pass).  Shooting transcriptions, eval_g / eval_jac_g / eval_f / eval_grad_f / eval_all only. */
+   g + J_g pass).  Shooting and collocation transcriptions: eval_g / eval_jac_g / eval_f / eval_grad_f / eval_all /
+   eval_h / eval_all_h (bit-identical to the SoA results). */
 #define CFX_LAYOUT_TILED64 2
 #define CFX_DEVICE 1u /* pointers are device pointers; call is asynchronous on the handle stream */
 /* eval_jac_g / eval_all / eval_all_h: the J_g values cfx_jac_constant_mask lists are not written — the output buffer
@@ -193,8 +194,10 @@ int cfx_eval_all(cfx_handle *h, const double *v, double *g, double *jac, double 
                  uint32_t flags);
 /* g + J_g + eval_h (+ f, grad f when non-NULL) at one point: Ipopt's eval_g / eval_jac_g / eval_h of an
    accepted iterate (IpoptAlgorithm's new point, then the Hessian with the new multipliers).  On the shooting
-   transcriptions ONE launch integrates every interval on second-order jets and writes the three outputs; the
-   collocation and musculoskeletal problems run eval_all then eval_h.  g, jac, hess must be non-NULL. */
+   transcriptions ONE launch integrates every interval on second-order jets and writes the three outputs; on the
+   collocation transcription ONE launch writes every interval's defects, continuity rows, J_g values and Hessian
+   blocks (g and J_g bit-identical to eval_all); the musculoskeletal problems run eval_all then eval_h.  g, jac,
+   hess must be non-NULL. */
 int cfx_eval_all_h(cfx_handle *h, const double *v, const double *obj_factor, const double *lambda, double *g,
                    double *jac, double *f, double *grad, double *hess, uint32_t flags);
 
@@ -340,16 +343,19 @@ typedef struct cfx_ipm_options {
        solve through the Sherman-Morrison-Woodbury identity on the band factors) */
     int32_t hessian_approximation;
     int32_t limited_memory_max_history;
-    /* What a failed line search starts (the instances whose search failed; the others wait):
+    /* What a failed line search starts (for the instances whose search failed):
        CFX_RESTORATION_PHASE (default) — Ipopt's feasibility-restoration phase, an NLP of its own over the constraint
        violation, min rho sum(p + n) + zeta/2 |D_R (x - x_r)|^2 s.t. c(x) - p + n = 0, p, n >= 0 and the bounds,
        solved by the same interior point (own barrier mu_R = max(mu, |c|_inf), filter and line search; p, n and their
        multipliers eliminated, so its KKT matrix has the original band structure) until a point is acceptable to the
-       original filter with |c|_1 <= required_infeasibility_reduction times the value where it started, or
-       max_resto_iter iterations (the bound multipliers then take a Newton step for complementarity over the phase's
-       dx, the constraint multipliers restart from zero, the filter from empty; the phase's iterations count among the
-       instance's max_iter); CFX_RESTORATION_STEP — one minimum-norm step on c = 0 in the Sigma + I metric,
-       backtracked until |c|_1 decreases, then least-squares multipliers. */
+       original filter with |c|_1 <= required_infeasibility_reduction times the value where it started (the bound
+       multipliers then take a Newton step for complementarity over the phase's dx, the constraint multipliers restart
+       from zero, the filter from empty; the phase's iterations count among the instance's max_iter).  A failed line
+       search of the phase, max_resto_iter iterations of it, or a point of local infeasibility stop that instance
+       (status CFX_IPM_RESTORATION_FAILED / CFX_IPM_INFEASIBLE_PROBLEM_DETECTED), as Ipopt's solve stops.  The phase's
+       iterations run inside the same host iterations as the other instances' main iterations (one host iteration
+       advances every instance by one iteration of its own).  CFX_RESTORATION_STEP — one minimum-norm step on c = 0
+       in the Sigma + I metric, backtracked until |c|_1 decreases, then least-squares multipliers. */
     int32_t restoration;
     int32_t max_resto_iter;                  /* 200 */
     double resto_penalty;                    /* rho, Ipopt resto_penalty_parameter: 1000 */
@@ -358,13 +364,27 @@ typedef struct cfx_ipm_options {
        line search's last rejected trial point was rejected by the filter (it passed the Armijo / sufficient-decrease
        test), the filter is cleared — at most max_filter_resets times per solve (Ipopt's default 5; default here 0:
        off) */
-    int32_t filter_reset_trigger;
-    int32_t max_filter_resets;
+    int32_t filter_reset_trigger; /* >= 1 */
+    int32_t max_filter_resets;    /* >= 0 */
+    /* Ipopt's max_wall_time (seconds, default 1e20): the instances still iterating when it is exceeded stop there
+       (status CFX_IPM_MAXIMUM_WALLTIME_EXCEEDED) */
+    double max_wall_time;
+    /* Ipopt's print_frequency_time (seconds, default 0: off): one progress line on stderr at most this often —
+       host iteration, elapsed time, instances still iterating, of them in the restoration phase */
+    double print_frequency_time;
 } cfx_ipm_options;
 #define CFX_HESSIAN_EXACT 0
 #define CFX_HESSIAN_LIMITED_MEMORY 1
 #define CFX_RESTORATION_STEP 0
 #define CFX_RESTORATION_PHASE 1
+
+/* per-instance outcome of a solve (cfx_ipm_get_status), Ipopt's ApplicationReturnStatus values */
+#define CFX_IPM_SOLVE_SUCCEEDED 0
+#define CFX_IPM_SOLVED_TO_ACCEPTABLE_LEVEL 1
+#define CFX_IPM_INFEASIBLE_PROBLEM_DETECTED 2 /* the restoration phase converged to a point of local infeasibility */
+#define CFX_IPM_MAXIMUM_ITERATIONS_EXCEEDED (-1)
+#define CFX_IPM_RESTORATION_FAILED (-2)
+#define CFX_IPM_MAXIMUM_WALLTIME_EXCEEDED (-5)
 
 typedef struct cfx_ipm_stats {
     int64_t eval_all, eval_g_f, eval_h, kkt_factor, iterations, host_syncs;
@@ -373,7 +393,7 @@ typedef struct cfx_ipm_stats {
        complement; 0: one band) */
     int64_t kkt_n, kkt_kl, kkt_ku, kkt_band_n, kkt_border;
     int64_t kkt_blocks; /* band blocks factored side by side (nested dissection of the stage chain; 1: none) */
-    int64_t resto_phases, resto_iterations; /* restoration phases entered / their iterations (whole batch) */
+    int64_t resto_phases, resto_iterations; /* restoration phases entered / their iterations, summed over the instances */
 } cfx_ipm_stats;
 
 typedef struct cfx_ipm cfx_ipm;
@@ -389,6 +409,8 @@ int cfx_ipm_create(cfx_handle *h, const double *lb, const double *ub, int32_t n_
 int cfx_ipm_solve(cfx_ipm *s, const double *v0, const double *fixed_values, double *v, double *y, double *f,
                   int32_t *converged, int32_t *iterations, double *kkt_error, uint32_t flags);
 int cfx_ipm_get_stats(const cfx_ipm *s, cfx_ipm_stats *out);
+/* status [B] (host): CFX_IPM_* outcome of every instance of the last cfx_ipm_solve */
+int cfx_ipm_get_status(const cfx_ipm *s, int32_t *status);
 int cfx_ipm_n_fixed(const cfx_ipm *s);
 const char *cfx_ipm_last_error(const cfx_ipm *s);
 void cfx_ipm_destroy(cfx_ipm *s);

@@ -1,5 +1,13 @@
 """cfg-5 (RK4 x 5) batched interior point from perturbed starts, and the stage-wise Hessian's throughput at batch
-65,536 (RK4 x 1).  Usage: python scripts/msk_multistart_probe.py [--hess-only]"""
+65,536 (RK4 x 1).
+
+Usage: python scripts/msk_multistart_probe.py [--native] [--hess-only] [--runs B:amp,B:amp,...] [--max-iter N]
+                                              [--wall SECONDS] [--jsonl FILE]
+Each run prints one line (converged count, Ipopt status histogram, restoration phases / iterations, wall time); the
+native solver prints a progress line on stderr every 20 s (print_frequency_time)."""
+import argparse
+import collections
+import json
 import pathlib
 import sys
 import time
@@ -11,26 +19,48 @@ ROOT = pathlib.Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT))
 
 import bench  # noqa: E402
+from cocofest_amd._cfx import IPM_STATUS  # noqa: E402
 from cocofest_amd.solver import BatchedIpm, IpmOptions, NativeIpm  # noqa: E402
 
+ap = argparse.ArgumentParser()
+ap.add_argument("--native", action="store_true")
+ap.add_argument("--hess-only", action="store_true")
+ap.add_argument("--runs", default="64:0.1,64:0.3,512:0.1")
+ap.add_argument("--max-iter", type=int, default=1000)
+ap.add_argument("--wall", type=float, default=1e20)
+ap.add_argument("--jsonl", default=None)
+args = ap.parse_args()
+
 ocp = bench.msk_build(5)
-for B, amp in (() if "--hess-only" in sys.argv else ((64, 0.1), (64, 0.3), (512, 0.1))):
+runs = [] if args.hess_only else [(int(r.split(":")[0]), float(r.split(":")[1])) for r in args.runs.split(",")]
+for B, amp in runs:
     rng = np.random.default_rng(0)
     v0 = np.tile(ocp.initial_guess_vector(), (B, 1))
     lb, ub = ocp.bounds_vector()
     free = lb != ub
     span = np.minimum(np.where(np.isfinite(ub - lb), ub - lb, 10.0), 10.0)[free]
     v0[:, free] = np.clip(v0[:, free] + amp * rng.uniform(-1, 1, (B, free.sum())) * span, lb[free], ub[free])
-    cls = NativeIpm if "--native" in sys.argv else BatchedIpm
-    ipm = cls(ocp, batch=B, options=IpmOptions(tol=1e-6, max_iter=1000))
+    cls = NativeIpm if args.native else BatchedIpm
+    ipm = cls(ocp, batch=B, options=IpmOptions(tol=1e-6, max_iter=args.max_iter, max_wall_time=args.wall,
+                                               print_frequency_time=20.0))
     res = ipm.solve(v0)
+    st = dict(getattr(ipm, "last_stats", {}) or {})
     ipm.close()
-    print(f"{cls.__name__} B={B} amp={amp}: wall {res.wall_time:.2f} s, converged {int(res.converged.sum())}/{B}, iterations "
-          f"median {np.median(res.iterations):.0f} max {res.iterations.max()}, f median {np.median(res.f):.4f} "
-          f"min {res.f.min():.4f}", flush=True)
+    hist = collections.Counter(IPM_STATUS.get(int(s), str(s)) for s in res.status)
+    conv = res.converged.astype(bool)
+    rec = dict(solver=cls.__name__, batch=B, amp=amp, max_iter=args.max_iter, wall_s=round(res.wall_time, 3),
+               converged=int(conv.sum()), status=dict(hist), iterations_median=float(np.median(res.iterations)),
+               iterations_max=int(res.iterations.max()), f_converged_min=float(res.f[conv].min()) if conv.any() else None,
+               f_converged_max=float(res.f[conv].max()) if conv.any() else None,
+               resto_phases=st.get("resto_phases"), resto_iterations=st.get("resto_iterations"),
+               host_iterations=st.get("iterations"))
+    print(json.dumps(rec), flush=True)
+    if args.jsonl:
+        with open(args.jsonl, "a") as fh:
+            fh.write(json.dumps(rec) + "\n")
 
 ocp1 = bench.msk_build(1)
-for B in ((4096,) if "--hess-only" in sys.argv else (1, 4096, 65536)):
+for B in ((4096,) if args.hess_only else (() if args.runs else (1, 4096, 65536))):
     h = ocp1.nlp(batch=B, layout="soa", device=0)
     r = torch.rand((h.nv, B), dtype=torch.float64, device="cuda:0", generator=torch.Generator("cuda:0").manual_seed(1))
     lo, hi = ocp1.bounds_vector()

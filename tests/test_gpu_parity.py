@@ -391,7 +391,8 @@ def test_fused_g_jacobian_hessian(name, scheme):
 
 
 def test_fused_callbacks_on_collocation_run_both_passes():
-    """cfx_eval_all_h on a collocation handle (eval_all, then eval_h): the separate callbacks' bits."""
+    """cfx_eval_all_h on a collocation handle (one launch since round 4: task 0 of each interval runs the g + J_g body
+    beside its Hessian block): the separate callbacks' bits."""
     ocp = cases.product_collocation_ocp("ding2007", COL_STIMS, 0.5, 4, degree=3, method="legendre",
                                         objective={"end_node_tracking": 40.0}, n_shooting=5)
     from tests.oracle_handle import oracle_problem_from_ocp

@@ -223,3 +223,40 @@ def test_limited_memory_hessian_cfg3(B):
         res = ocp.solve(Solver.IPOPT(_hessian_approximation="limited-memory", _max_iter=1000, _tol=1e-8))
         assert bool(res.converged[0])
         np.testing.assert_allclose(res.f, r_ex.f, rtol=1e-6, atol=1e-9)
+
+
+def test_native_ipm_infeasible_instance_stops_alone():
+    """One infeasible instance in a batch of feasible ones (cfg 2, 0 DOF, its fixed initial force 5,000 N: every later
+    node's force exceeds its 1,000 N bound).  Its line search fails, its restoration phase converges to a point of local
+    infeasibility and the instance stops there with Ipopt's Infeasible_Problem_Detected (or Restoration_Failed), as the
+    specification does, while the others converge — with the same iterations and points as in a batch of feasible
+    instances only: each instance's phase iterations run inside the same host iterations as the others' main ones and
+    leave them untouched (a failed phase used to be treated like a successful one)."""
+    from cocofest_amd.solver import BatchedIpm, IpmOptions, NativeIpm
+
+    ocp = cases.product_ocp(**cases.cfg2())
+    lb, ub = ocp.bounds_vector()
+    B = 4
+    fixed = np.tile(lb[lb == ub], (B, 1))
+    bad = fixed.copy()
+    bad[2, 1] = 5000.0
+    v0 = np.tile(ocp.initial_guess_vector(), (B, 1))
+    opts = IpmOptions(tol=1e-8, max_iter=300)
+    nat = NativeIpm(ocp, batch=B, options=opts)
+    r_bad = nat.solve(v0, fixed_values=bad)
+    st = dict(nat.last_stats)
+    r_ok = nat.solve(v0, fixed_values=fixed)
+    nat.close()
+    ref = BatchedIpm(ocp, batch=B, options=opts)
+    r_spec = ref.solve(v0, fixed_values=bad)
+    ref.close()
+    print("status", r_bad.status, r_spec.status, "iterations", r_bad.iterations, r_spec.iterations, st)
+    assert list(r_bad.converged) == [True, True, False, True]
+    assert r_bad.status[2] in (2, -2) and r_bad.status[2] == r_spec.status[2]
+    assert r_bad.iterations[2] < opts.max_iter
+    assert st["resto_phases"] >= 1 and st["resto_iterations"] >= 1, st
+    np.testing.assert_array_equal(r_spec.converged, r_bad.converged)
+    keep = [0, 1, 3]
+    np.testing.assert_array_equal(r_bad.iterations[keep], r_ok.iterations[keep])
+    np.testing.assert_array_equal(r_bad.v[keep], r_ok.v[keep])
+    assert np.all(r_bad.status[keep] == 0) and np.all(r_ok.status == 0)

@@ -178,12 +178,13 @@ def test_restoration_phase_reduces_the_infeasibility():
     filt = torch.full((B, 64, 2), np.inf, dtype=torch.float64)
     filt[:, :, 1] = -np.inf
     on = torch.ones((B,), dtype=torch.bool)
-    xr, zl2, zu2, filt2, fpos2, its = ipm._restoration_phase(on, x, zl, zu, g, theta, phi, mu,
-                                                             torch.full((B,), 0.99, dtype=torch.float64), filt,
-                                                             torch.zeros((B,), dtype=torch.int64),
-                                                             torch.zeros((B,), dtype=torch.int64))
+    xr, zl2, zu2, filt2, fpos2, its, rexit = ipm._restoration_phase(on, x, zl, zu, g, theta, phi, mu,
+                                                                    torch.full((B,), 0.99, dtype=torch.float64), filt,
+                                                                    torch.zeros((B,), dtype=torch.int64),
+                                                                    torch.zeros((B,), dtype=torch.int64))
     gr, _ = ipm._scaled_gf(ipm._full(xr))
     assert torch.all(its >= 1)
+    assert torch.all(rexit == ipm.RS_OK)
     assert torch.all(gr.abs().sum(1) <= 0.9 * theta), (gr.abs().sum(1), theta)
     assert torch.all(xr[:, ipm.hasL] > lbF[:, ipm.hasL]) and torch.all(xr[:, ipm.hasU] < ubF[:, ipm.hasU])
     assert torch.all(zl2[:, ipm.hasL] > 0) and torch.all(zu2[:, ipm.hasU] > 0)
