@@ -45,6 +45,10 @@ typedef struct {
     int32_t fv_on, fp_on, residual;
     int32_t N, m, scheme, T;
     double tf;
+    /* the conventions of the revision that wrote the reference's stored reaching-task solutions (fes_oracle.cn_sum
+       legacy_skip_first, fes_oracle.rhs legacy): a window's first pulse left out of the calcium sum once the window
+       holds several, r0 from the Km state of the fatigue models */
+    int32_t legacy;
 } ms_desc;
 
 typedef struct {
@@ -259,14 +263,22 @@ static void msk_rhs(const ms_ctx *c, double t, const double *row, const cx *x, c
         /* muscle ODE (ding2003.py:230-311, ding2003_with_fatigue.py:197-240, ding2007.py:172-188) */
         const cx *xm = x + c->xoff[mu];
         cx *fm = f + c->xoff[mu];
-        const double tauc = cs[0], r0 = cs[5] + cs[1];
+        const int fat = d->model[mu] & 1, pw = d->model[mu] >= 2;
+        const double tauc = cs[0];
+        const cx r0 = (d->legacy && fat) ? xm[4] + cs[1] : cs[5] + cs[1];
+        int skip = -1;
+        if (d->legacy) {
+            int nreal = 0;
+            for (int i = 0; i < d->T; ++i) nreal += row[i] > -1e6;
+            if (nreal > 1) skip = d->T - nreal;
+        }
         cx sum = 0;
         for (int i = 0; i < d->T; ++i) {
-            const double ri = i == 0 ? 1.0 : 1.0 + (r0 - 1.0) * exp(-(row[i] - row[i - 1]) / tauc);
+            if (i == skip) continue;
+            const cx ri = i == 0 ? 1.0 : 1.0 + (r0 - 1.0) * exp(-(row[i] - row[i - 1]) / tauc);
             sum += ri * exp(-(t - row[i]) / tauc);
         }
         fm[0] = (1 / tauc) * sum - xm[0] / tauc;
-        const int fat = d->model[mu] & 1, pw = d->model[mu] >= 2;
         cx A = fat ? xm[2] : (pw ? cs[6] : cs[2]);
         const cx tau1 = fat ? xm[3] : cs[3], km = fat ? xm[4] : cs[5];
         if (pw) A = A * (1 - cexp(-(u[c->uoff[mu]] - cs[7]) / cs[8]));

@@ -33,7 +33,8 @@ class Desc(C.Structure):
                 ("model", _i32 * MUS), ("cst", (_f64 * 13) * MUS), ("npts", _i32 * MUS),
                 ("pt_seg", (_i32 * PTS) * MUS), ("pt_pos", ((_f64 * 3) * PTS) * MUS), ("lopt", _f64 * MUS),
                 ("slack", _f64 * MUS), ("penn", _f64 * MUS), ("fv_on", _i32), ("fp_on", _i32),
-                ("residual", _i32), ("N", _i32), ("m", _i32), ("scheme", _i32), ("T", _i32), ("tf", _f64)]
+                ("residual", _i32), ("N", _i32), ("m", _i32), ("scheme", _i32), ("T", _i32), ("tf", _f64),
+                ("legacy", _i32)]
 
 
 _lib = None
@@ -86,6 +87,7 @@ def describe(pb: M.MskProblem) -> Desc:
     d.fv_on, d.fp_on, d.residual = int(pb.fv_on), int(pb.fp_on), int(pb.residual)
     d.N, d.m, d.scheme, d.T = pb.n_shooting, pb.m, SCHEME[pb.scheme], pb.rows.shape[1]
     d.tf = pb.final_time
+    d.legacy = int(pb.legacy)
     return d
 
 

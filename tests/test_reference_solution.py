@@ -18,8 +18,9 @@ What the stored trajectory says about that revision, measured here (DESIGN.md se
     the current convention the Cn rows miss by 8.6e-3 right after the second pulse.
 With those conventions the oracle's restatement of the whole right-hand side — the biorbd chain, muscle paths and
 length Jacobians, De Groote force-length / force-velocity, the Ding ODEs — reproduces every continuity row of the
-stored solution to 2e-12 on the muscle states and 1e-9 on the joint velocities (Ipopt's converged constraint
-violation), and the marker constraint to its tolerance.  The GPU kernels are then compared with the oracle at the
+stored solution (all 1,500 intervals) to 2e-11 on the muscle states and 1e-9 on the joint velocities (Ipopt's converged
+constraint violation), and the marker constraint to its tolerance; each stored optimum is first-order stationary in
+its per-pulse pulse widths (tests/reaching_kkt.py) and beats the other on its own objective.  The GPU kernels are then compared with the oracle at the
 same trajectory under the current convention (tests marked gpu).
 """
 
@@ -99,6 +100,15 @@ def _residuals(pb, X, U, ks):
                      for k in ks])
 
 
+def all_residuals(pb, X, U):
+    """Every continuity row Phi(x_k, u_k) - x_{k+1}, k = 0 .. N-1, from the plain-C port of the oracle (the numpy
+    restatement's arithmetic; the sample below pins the two together)."""
+    from oracle import c_msk
+
+    g, _ = c_msk.shooting(pb, decision_vector(X, U, pb.nz)[None], want_jac=False, threads=8)
+    return g[0, : N * pb.nx].reshape(N, pb.nx)
+
+
 @pytest.mark.parametrize("objective", ["fatigue", "force"])
 def test_oracle_reproduces_the_reference_solution(objective):
     d = load(objective)
@@ -107,12 +117,15 @@ def test_oracle_reproduces_the_reference_solution(objective):
     assert X.shape == (pb.nx, N + 1) and U.shape == (pb.nu, N)
     assert np.allclose(d["time"], np.arange(N + 1) * FINAL_TIME / N, atol=1e-12)
     R = _residuals(pb, X, U, SAMPLE)
+    # all 1,500 intervals through the C port of the same restatement, equal to the numpy oracle on the sample
+    Rall = all_residuals(pb, X, U)
+    np.testing.assert_allclose(Rall[SAMPLE], R, rtol=0, atol=1e-12 * np.abs(X).max())
     nxm = pb.nxm
-    scale = np.maximum(1.0, np.abs(X[:, [k + 1 for k in SAMPLE]].T))
-    # muscle states: every continuity row to 2e-12 relative (Ipopt met them to machine precision)
-    assert np.max(np.abs(R[:, :nxm]) / scale[:, :nxm]) < 1e-11, np.max(np.abs(R[:, :nxm]) / scale[:, :nxm])
+    scale = np.maximum(1.0, np.abs(X[:, 1:].T))
+    # muscle states: every continuity row of the 1,500 to 2.2e-11 relative (Ipopt met them to machine precision)
+    assert np.max(np.abs(Rall[:, :nxm]) / scale[:, :nxm]) < 5e-11, np.max(np.abs(Rall[:, :nxm]) / scale[:, :nxm])
     # q, qdot: biorbd's forward dynamics against the oracle's chain: 1e-9 (Ipopt's constraint violation)
-    assert np.max(np.abs(R[:, nxm:])) < 1e-8, np.max(np.abs(R[:, nxm:]))
+    assert np.max(np.abs(Rall[:, nxm:])) < 1e-8, np.max(np.abs(Rall[:, nxm:]))
     # the stored optimum satisfies the reaching constraint and the start / end postures of the script
     v = decision_vector(X, U, pb.nz)
     assert np.max(np.abs(M.marker_rows(pb, v))) < 1e-8
@@ -184,11 +197,49 @@ def test_gpu_matches_the_oracle_at_the_reference_solution(objective):
     h.close()
     nx = pb.nx
     gk = g[: N * nx].reshape(N, nx)
-    R = _residuals(pb, X, U, SAMPLE)
+    # every one of the 1,500 intervals against the oracle (its C port; the numpy restatement on the sample)
+    R = all_residuals(pb, X, U)
+    np.testing.assert_allclose(R[SAMPLE], _residuals(pb, X, U, SAMPLE), rtol=0, atol=1e-12 * np.abs(X).max())
     # relative to |Phi| per row, floored at 1e-6 of the row's largest state (a muscle that is not yet stimulated has
     # forces of 1e-8 N, where the last bits of a 1e-13 absolute agreement would read as 1e-7)
     floor = 1e-6 * np.abs(X).max(axis=1)
-    ref_scale = np.maximum(np.abs(R) + np.abs(X[:, [k + 1 for k in SAMPLE]].T), floor)
-    assert np.max(np.abs(gk[SAMPLE] - R) / ref_scale) < 1e-10
+    ref_scale = np.maximum(np.abs(R) + np.abs(X[:, 1:].T), floor)
+    assert np.max(np.abs(gk - R) / ref_scale) < 1e-10
     np.testing.assert_allclose(g[N * nx:], M.marker_rows(pb, v), atol=1e-13)
     assert np.max(np.abs(g[N * nx:])) < 1e-8
+
+
+def test_each_stored_optimum_beats_the_other_on_its_own_objective():
+    """The two stored solutions solve the same constrained problem with different objectives (fes_ocp_dynamics.py:
+    675-693), so each must be at least as good as the other on its own objective, as the product states them:
+    sum_m (a_rest_m / A_m(T))^2 (Mayer, Node.END) and dt sum_k sum_m F_{m,k}^2 (Lagrange, Node.ALL).  Both are feasible
+    for the other's constraints (same bounds, dynamics and marker row).  Measured: 7.8420 vs 7.8921 (fatigue) and
+    30,543 vs 32,078 (force)."""
+    from tests import reaching_kkt as K
+
+    _, _, _, _, model = K.product_bounds("fatigue")
+    dt = FINAL_TIME / N
+    val = {}
+    for data in ("fatigue", "force"):
+        X, _ = trajectory(load(data))
+        val[data] = (sum((mus.a_rest / X[5 * m + 2, N]) ** 2 for m, mus in enumerate(model.muscles_dynamics_model)),
+                     dt * sum(float((X[5 * m + 1] ** 2).sum()) for m in range(len(MUSCLES))))
+    assert val["fatigue"][0] < val["force"][0] and val["force"][1] < val["fatigue"][1], val
+    np.testing.assert_allclose([val["fatigue"][0], val["force"][1]], [7.841959196, 30543.104905], rtol=1e-8)
+
+
+@pytest.mark.parametrize("objective", ["fatigue", "force"])
+def test_reference_optimum_is_stationary_in_the_pulse_widths(objective):
+    """First-order optimality of the stored optimum in its own decision space (per-pulse pulse-width parameters, the
+    dynamics eliminated: tests/reaching_kkt.reduced_stationarity): reduced gradients of the objective, of the marker
+    rows and of the end posture by the discrete adjoint of RK4 x 1 under the stored revision's conventions; least-
+    squares multipliers (4 equality rows, sign-constrained bound multipliers).  The solution is bang-bang (346 / 316
+    of the 360 pulses on a bound), and the remaining dual infeasibility is 1e-3 of the largest reduced-gradient term
+    (Ipopt's own termination test scales it by its multipliers' size)."""
+    from tests import reaching_kkt as K
+
+    r = K.reduced_stationarity(objective, legacy=True)
+    print(r)
+    assert r["at_bounds"] >= 300 and r["pulses"] == 360
+    assert r["dual_inf_rel"] < 3e-3, r
+    assert all(np.isfinite(r["nu"]))
