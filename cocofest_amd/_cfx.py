@@ -16,7 +16,7 @@ import numpy as np
 LIB_PATH = pathlib.Path(__file__).with_name("libcfx.so")
 
 ABI_VERSION = 6
-OK, EINVAL, EHIP, ENOMEM, EUNSUPPORTED, ENODEV = 0, -1, -2, -3, -4, -5
+OK, EINVAL, EHIP, ENOMEM, EUNSUPPORTED, ENODEV, ECALLBACK = 0, -1, -2, -3, -4, -5, -6
 MODEL_IDS = {
     "ding2003": 0,
     "ding2003_with_fatigue": 1,
@@ -130,6 +130,22 @@ class IpmStats(C.Structure):
                 ("resto_iterations", C.c_int64)]
 
 
+# cfx_evaluator / cfx_nlp_desc (cfx_ipm_create_ext): caller-supplied callbacks of an NLP the solver runs on
+EVAL_ALL_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p)
+EVAL_H_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p)
+
+
+class Evaluator(C.Structure):
+    _fields_ = [("ctx", C.c_void_p), ("eval_all", EVAL_ALL_FN), ("eval_h", EVAL_H_FN)]
+
+
+class NlpDesc(C.Structure):
+    _fields_ = [("batch", C.c_int64), ("nv", C.c_int64), ("ng", C.c_int64), ("nnz_jac", C.c_int64),
+                ("nnz_hess", C.c_int64), ("jac_row", C.POINTER(C.c_int32)), ("jac_col", C.POINTER(C.c_int32)),
+                ("hess_row", C.POINTER(C.c_int32)), ("hess_col", C.POINTER(C.c_int32)), ("device", C.c_int32),
+                ("hip_stream", C.c_void_p)]
+
+
 # exported symbols and their signatures (must match include/cfx.h)
 _P = C.c_void_p
 _D = C.POINTER(C.c_double)
@@ -162,6 +178,9 @@ SIGNATURES = {
     "cfx_ipm_solve": (C.c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _P, C.c_uint32]),
     "cfx_ipm_get_stats": (C.c_int, [_P, C.POINTER(IpmStats)]),
     "cfx_ipm_get_status": (C.c_int, [_P, C.POINTER(C.c_int32)]),
+    "cfx_ipm_create_ext": (C.c_int, [C.POINTER(NlpDesc), C.POINTER(Evaluator), _P, _P, C.c_int32,
+                                     C.POINTER(IpmOptions), C.POINTER(_P)]),
+    "cfx_gather_sum": (C.c_int, [C.c_int64, C.c_int64, _P, _P, _P, C.c_int64, _P, _P]),
     "cfx_ipm_n_fixed": (C.c_int, [_P]),
     "cfx_ipm_last_error": (C.c_char_p, [_P]),
     "cfx_ipm_destroy": (None, [_P]),
@@ -608,6 +627,58 @@ class Ipm:
         self.s = s
         self.n_fixed = self.lib.cfx_ipm_n_fixed(self.s)
 
+    @classmethod
+    def external(cls, batch, nv, ng, jac_structure, hess_structure, eval_all, eval_h, lb, ub, n_params=0,
+                 options=None, device=0, stream=0):
+        """The solver over caller-supplied callbacks (cfx_ipm_create_ext): ``eval_all(v, g, jac, f, grad)`` and
+        ``eval_h(v, obj_factor, lam, hess)`` receive device pointers (ints; 0 for an output not wanted) of AoS arrays
+        on ``stream`` and return 0 on success.  Used by the interval-sharded path (distributed.ShardedNativeIpm)."""
+        self = cls.__new__(cls)
+        self.lib = load_library()
+        self.handle = None
+        self.batch, self.nv, self.ng = int(batch), int(nv), int(ng)
+        jr, jc = (np.ascontiguousarray(a, dtype=np.int32) for a in jac_structure)
+        hr, hc = (np.ascontiguousarray(a, dtype=np.int32) for a in hess_structure)
+        i32 = lambda a: a.ctypes.data_as(C.POINTER(C.c_int32))  # noqa: E731
+        desc = NlpDesc(self.batch, self.nv, self.ng, len(jr), len(hr), i32(jr), i32(jc), i32(hr), i32(hc), int(device),
+                       C.c_void_p(int(stream)))
+
+        def _all(ctx, v, g, jac, f, grad):
+            try:
+                return int(eval_all(v or 0, g or 0, jac or 0, f or 0, grad or 0))
+            except Exception as e:  # noqa: BLE001 — reported through CFX_ECALLBACK, re-raised by solve()
+                self._cb_error = e
+                return -1
+
+        def _h(ctx, v, of, lam, hess):
+            try:
+                return int(eval_h(v or 0, of or 0, lam or 0, hess or 0))
+            except Exception as e:  # noqa: BLE001
+                self._cb_error = e
+                return -1
+
+        self._cb = (EVAL_ALL_FN(_all), EVAL_H_FN(_h))  # kept alive with the solver
+        self._cb_error = None
+        ev = Evaluator(None, self._cb[0], self._cb[1])
+        lb = np.ascontiguousarray(lb, dtype=np.float64).reshape(-1)
+        ub = np.ascontiguousarray(ub, dtype=np.float64).reshape(-1)
+        if lb.size != self.nv or ub.size != self.nv:
+            raise CfxError(EINVAL, f"Ipm.external: bounds must hold nv = {self.nv} values")
+        opt = IpmOptions()
+        self.lib.cfx_ipm_default_options(C.byref(opt))
+        for k, v in (options or {}).items():
+            if k not in dict(IpmOptions._fields_):
+                raise CfxError(EINVAL, f"Ipm: unknown option {k!r}")
+            setattr(opt, k, v)
+        s = C.c_void_p()
+        rc = self.lib.cfx_ipm_create_ext(C.byref(desc), C.byref(ev), lb.ctypes.data, ub.ctypes.data, int(n_params),
+                                         C.byref(opt), C.byref(s))
+        if rc != OK:
+            raise CfxError(rc, self.lib.cfx_last_error(None).decode())
+        self.s = s
+        self.n_fixed = self.lib.cfx_ipm_n_fixed(self.s)
+        return self
+
     def solve(self, v0, fixed_values=None):
         """Returns (v, y, f, converged, iterations, kkt_error) as numpy arrays."""
         B = self.batch
@@ -629,6 +700,10 @@ class Ipm:
         rc = self.lib.cfx_ipm_solve(self.s, v0.ctypes.data, None if fv is None else fv.ctypes.data, v.ctypes.data,
                                     y.ctypes.data, f.ctypes.data, conv.ctypes.data, its.ctypes.data, kkt.ctypes.data, 0)
         if rc != OK:
+            err = getattr(self, "_cb_error", None)
+            if err is not None:
+                self._cb_error = None
+                raise CfxError(rc, f"{self.lib.cfx_ipm_last_error(self.s).decode()}: {err!r}") from err
             raise CfxError(rc, self.lib.cfx_ipm_last_error(self.s).decode())
         return v, y, f, conv.astype(bool), its.astype(np.int64), kkt
 

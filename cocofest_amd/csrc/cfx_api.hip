@@ -1621,3 +1621,34 @@ static int msk_integrate(cfx_handle* h, const double* x0, const double* u, doubl
     if ((rc = finish_out(h, S_OUT, TR, traj, nsamp * h->sz.nx, flags)) != CFX_OK) return rc;
     return sync_if_host(h, flags);
 }
+
+// ------------------------------------------------------------------------------------------------------
+// cfx_gather_sum: the fixed gather table that places all-gathered value slices (include/cfx.h)
+// ------------------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_gather_sum(int64_t batch, int64_t n_dst, const int32_t* __restrict__ ptr,
+                                                    const int32_t* __restrict__ idx, const double* __restrict__ src,
+                                                    int64_t src_len, double* __restrict__ dst) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t b = blockIdx.y;
+    if (i >= n_dst || b >= batch) return;
+    double acc = 0.0;
+    for (int32_t s = ptr[i]; s < ptr[i + 1]; ++s) acc += src[b * src_len + idx[s]];
+    dst[b * n_dst + i] = acc;
+}
+
+extern "C" int cfx_gather_sum(int64_t batch, int64_t n_dst, const int32_t* ptr, const int32_t* idx, const double* src,
+                              int64_t src_len, double* dst, void* stream) {
+    if (batch < 1 || n_dst < 0 || src_len < 0 || !ptr || (n_dst && (!idx || !src || !dst)) || batch > kMaxGridY) {
+        g_create_error = "cfx_gather_sum: invalid arguments (batch must be in [1, 65535])";
+        return CFX_EINVAL;
+    }
+    if (n_dst == 0) return CFX_OK;
+    hipLaunchKernelGGL(k_gather_sum, dim3((unsigned)((n_dst + 255) / 256), (unsigned)batch), dim3(256), 0,
+                       (hipStream_t)stream, batch, n_dst, ptr, idx, src, src_len, dst);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        g_create_error = std::string("cfx_gather_sum: ") + hipGetErrorString(e);
+        return CFX_EHIP;
+    }
+    return CFX_OK;
+}

@@ -2118,6 +2118,10 @@ struct cfx_ipm {
     // pass CFX_KEEP_CONSTANT_JAC (CFX_IPM_KEEPJ=0 turns it off, for A/B runs)
     bool keepj = true, jac_filled = false;
     uint32_t jac_flags() const { return CFX_DEVICE | (keepj && jac_filled ? CFX_KEEP_CONSTANT_JAC : 0u); }
+    // cfx_ipm_create_ext: the callbacks come from the caller's evaluator (e.g. interval-sharded over several GPUs)
+    // instead of a libcfx handle
+    bool ext = false;
+    cfx_evaluator ev{};
 };
 
 #define IPM_HIP(s, call)                                                         \
@@ -2144,6 +2148,28 @@ struct cfx_ipm {
             return r_;                                                           \
         }                                                                        \
     } while (0)
+
+// The callbacks at a point (device pointers, AoS): the handle's, or the caller's evaluator (cfx_ipm_create_ext)
+static int ipm_eval_all(cfx_ipm* s, const double* v, double* g, double* jac, double* f, double* grad, uint32_t flags) {
+    if (s->ext) {
+        const int r = s->ev.eval_all(s->ev.ctx, v, g, jac, f, grad);
+        if (r != 0) s->err = "cfx_ipm: the evaluator's eval_all returned " + std::to_string(r);
+        return r != 0 ? CFX_ECALLBACK : CFX_OK;
+    }
+    const int r = cfx_eval_all(s->h, v, g, jac, f, grad, flags);
+    if (r != CFX_OK) s->err = std::string("cfx_eval_all: ") + cfx_last_error(s->h);
+    return r;
+}
+static int ipm_eval_h(cfx_ipm* s, const double* v, const double* of, const double* lam, double* hess) {
+    if (s->ext) {
+        const int r = s->ev.eval_h ? s->ev.eval_h(s->ev.ctx, v, of, lam, hess) : -1;
+        if (r != 0) s->err = "cfx_ipm: the evaluator's eval_h returned " + std::to_string(r);
+        return r != 0 ? CFX_ECALLBACK : CFX_OK;
+    }
+    const int r = cfx_eval_h(s->h, v, of, lam, hess, CFX_DEVICE);
+    if (r != CFX_OK) s->err = std::string("cfx_eval_h: ") + cfx_last_error(s->h);
+    return r;
+}
 
 template <class T>
 static T* dalloc(cfx_ipm* s, size_t n, int* rc) {
@@ -2224,6 +2250,10 @@ static int ipm_fail(cfx_ipm* s, int code, const std::string& msg) {
     return code;
 }
 
+static int ipm_create_common(cfx_ipm* s, const cfx_sizes& sz, int layout, const int32_t* jr_in, const int32_t* jc_in,
+                             const int32_t* hr_in, const int32_t* hc_in, const double* lb, const double* ub,
+                             int32_t n_params, const cfx_ipm_options* opt, cfx_ipm** out);
+
 extern "C" int cfx_ipm_create(cfx_handle* h, const double* lb, const double* ub, int32_t n_params,
                               const cfx_ipm_options* opt, cfx_ipm** out) {
     if (!h || !lb || !ub || !out) return CFX_EINVAL;
@@ -2232,18 +2262,63 @@ extern "C" int cfx_ipm_create(cfx_handle* h, const double* lb, const double* ub,
     s->h = h;
     int layout = 0;
     hipStream_t stream = nullptr;
-    int rc = CFX_OK;
-    if (cfx_internal_info(h, &s->B, &layout, &s->device, &stream) != CFX_OK) {
+    cfx_sizes sz{};
+    if (cfx_internal_info(h, &s->B, &layout, &s->device, &stream) != CFX_OK || cfx_get_sizes(h, &sz) != CFX_OK) {
         s->err = "cfx_ipm_create: bad handle";
         return create_fail(s, CFX_EINVAL);
     }
+    std::vector<int32_t> jr(sz.nnz_jac), jc(sz.nnz_jac), hr(sz.nnz_hess), hc(sz.nnz_hess);
+    if (cfx_jac_structure(h, jr.data(), jc.data()) != CFX_OK || cfx_hess_structure(h, hr.data(), hc.data()) != CFX_OK) {
+        s->err = "cfx_ipm_create: structure query failed";
+        return create_fail(s, CFX_EINVAL);
+    }
+    return ipm_create_common(s, sz, layout, jr.data(), jc.data(), hr.data(), hc.data(), lb, ub, n_params, opt, out);
+}
+
+extern "C" int cfx_ipm_create_ext(const cfx_nlp_desc* nlp, const cfx_evaluator* ev, const double* lb, const double* ub,
+                                  int32_t n_params, const cfx_ipm_options* opt, cfx_ipm** out) {
+    if (!nlp || !ev || !ev->eval_all || !lb || !ub || !out) return CFX_EINVAL;
+    *out = nullptr;
+    cfx_ipm* s = new cfx_ipm();
+    if (nlp->batch < 1 || nlp->nv < 1 || nlp->ng < 0 || nlp->nnz_jac < 0 || nlp->nnz_hess < 0 ||
+        (nlp->nnz_jac && (!nlp->jac_row || !nlp->jac_col)) || (nlp->nnz_hess && (!nlp->hess_row || !nlp->hess_col))) {
+        s->err = "cfx_ipm_create_ext: invalid NLP description";
+        return create_fail(s, CFX_EINVAL);
+    }
+    for (int64_t e = 0; e < nlp->nnz_jac; ++e)
+        if (nlp->jac_row[e] < 0 || nlp->jac_row[e] >= nlp->ng || nlp->jac_col[e] < 0 || nlp->jac_col[e] >= nlp->nv) {
+            s->err = "cfx_ipm_create_ext: Jacobian triplet out of range";
+            return create_fail(s, CFX_EINVAL);
+        }
+    for (int64_t e = 0; e < nlp->nnz_hess; ++e)
+        if (nlp->hess_row[e] < nlp->hess_col[e] || nlp->hess_col[e] < 0 || nlp->hess_row[e] >= nlp->nv) {
+            s->err = "cfx_ipm_create_ext: Hessian triplet out of range or above the diagonal";
+            return create_fail(s, CFX_EINVAL);
+        }
+    s->B = nlp->batch;
+    s->device = nlp->device;
+    s->stream = (hipStream_t)nlp->hip_stream;
+    s->ev = *ev;
+    s->ext = true;
+    cfx_sizes sz{};
+    sz.nv = nlp->nv;
+    sz.ng = nlp->ng;
+    sz.nnz_jac = nlp->nnz_jac;
+    sz.nnz_hess = nlp->nnz_hess;
+    return ipm_create_common(s, sz, CFX_LAYOUT_AOS, nlp->jac_row, nlp->jac_col, nlp->hess_row, nlp->hess_col, lb, ub,
+                             n_params, opt, out);
+}
+
+static int ipm_create_common(cfx_ipm* s, const cfx_sizes& sz, int layout, const int32_t* jr_in, const int32_t* jc_in,
+                             const int32_t* hr_in, const int32_t* hc_in, const double* lb, const double* ub,
+                             int32_t n_params, const cfx_ipm_options* opt, cfx_ipm** out) {
+    int rc = CFX_OK;
     IpmK& K = s->K;
     if (opt)
         K.o = *opt;
     else
         cfx_ipm_default_options(&K.o);
-    cfx_sizes sz{};
-    if (cfx_get_sizes(h, &sz) != CFX_OK || (s->B > 1 && layout != CFX_LAYOUT_AOS) || layout == CFX_LAYOUT_TILED64 ||
+    if ((s->B > 1 && layout != CFX_LAYOUT_AOS) || layout == CFX_LAYOUT_TILED64 ||
         n_params < 0 || n_params > sz.nv || K.o.max_iter < 0 || K.o.max_backtrack < 1 || K.o.max_soc < 0 ||
         K.o.watchdog_shortened_iter_trigger < 0 || K.o.watchdog_trial_iter_max < 0 ||
         (K.o.hessian_approximation != CFX_HESSIAN_EXACT && K.o.hessian_approximation != CFX_HESSIAN_LIMITED_MEMORY) ||
@@ -2289,11 +2364,8 @@ extern "C" int cfx_ipm_create(cfx_handle* h, const double* lb, const double* ub,
         ubF[i] = ubF0[i] + rel * clamp_lo(std::fabs(ubF0[i] * d[i]), 1.0) / d[i];
     }
     // triplets over the free variables (solver.py _build_kkt_maps)
-    std::vector<int32_t> jr(K.nnzj), jc(K.nnzj), hr(K.nnzh), hc(K.nnzh);
-    if (cfx_jac_structure(h, jr.data(), jc.data()) != CFX_OK || cfx_hess_structure(h, hr.data(), hc.data()) != CFX_OK) {
-        s->err = "cfx_ipm_create: structure query failed";
-        return create_fail(s, CFX_EINVAL);
-    }
+    const std::vector<int32_t> jr(jr_in, jr_in + K.nnzj), jc(jc_in, jc_in + K.nnzj), hr(hr_in, hr_in + K.nnzh),
+        hc(hc_in, hc_in + K.nnzh);
     std::vector<int64_t> posF(n, -1);
     for (int i = 0; i < nf; ++i) posF[freev[i]] = i;
     std::vector<int32_t> jsel, jrF, jcF, hsel, hrF, hcF;
@@ -2738,13 +2810,13 @@ struct Run {
         return CFX_OK;
     }
     int eval_full(double* v) {
-        IPM_CFX(s, cfx_eval_all(s->h, v, s->K.graw, s->K.jac, s->K.fraw, s->K.grad, s->jac_flags()));
+        IPM_RUN(ipm_eval_all(s, v, s->K.graw, s->K.jac, s->K.fraw, s->K.grad, s->jac_flags()));
         s->jac_filled = true;
         s->st.eval_all++;
         return CFX_OK;
     }
     int eval_gf(bool with_f) {
-        IPM_CFX(s, cfx_eval_all(s->h, s->K.vt, s->K.gt, nullptr, with_f ? s->K.ft : nullptr, nullptr, CFX_DEVICE));
+        IPM_RUN(ipm_eval_all(s, s->K.vt, s->K.gt, nullptr, with_f ? s->K.ft : nullptr, nullptr, CFX_DEVICE));
         s->st.eval_g_f++;
         return CFX_OK;
     }
@@ -2804,16 +2876,21 @@ static int ipm_solve(cfx_ipm* s, const double* v0, const double* fixed_values, d
     int64_t Bq = 0;
     int layout = 0, dev = 0;
     hipStream_t st = nullptr;
-    if (cfx_internal_info(s->h, &Bq, &layout, &dev, &st) != CFX_OK) return ipm_fail(s, CFX_EINVAL, "bad handle");
+    if (s->ext)
+        st = s->stream;
+    else if (cfx_internal_info(s->h, &Bq, &layout, &dev, &st) != CFX_OK)
+        return ipm_fail(s, CFX_EINVAL, "bad handle");
     IPM_HIP(s, hipSetDevice(s->device));
     s->stream = st;
     // MSK handles: eval_h re-uses the stage data of the eval_all just before it at the same point (switched off
     // again on every exit path)
     struct StashGuard {
         cfx_handle* h;
-        ~StashGuard() { cfx_internal_msk_stash(h, 0); }
+        ~StashGuard() {
+            if (h) cfx_internal_msk_stash(h, 0);
+        }
     } stash_guard{s->h};
-    cfx_internal_msk_stash(s->h, 1);
+    if (s->h) cfx_internal_msk_stash(s->h, 1);
     IpmK& K = s->K;
     const bool devp = flags & CFX_DEVICE;
     const size_t B = (size_t)K.B;
@@ -2861,7 +2938,7 @@ static int ipm_solve(cfx_ipm* s, const double* v0, const double* fixed_values, d
         // after an ordinary iteration the multipliers of the Hessian are known before k_ipm_begin (k_ipm_update
         // formed them; k_rs_update / k_rs_init for the instances in the restoration phase, objective factor 0): g,
         // J_g, f, grad f and the Hessian of the new iterate from one call
-        const bool fused = it > 0 && !reinit && !K.lbfgs && K.m > 0;
+        const bool fused = it > 0 && !reinit && !K.lbfgs && K.m > 0 && !s->ext;
         if (fused) {
             IPM_CFX(s, cfx_eval_all_h(s->h, K.vx, K.of, K.ysc, K.graw, K.jac, K.fraw, K.grad, K.hv, s->jac_flags()));
             s->jac_filled = true;
@@ -2885,8 +2962,8 @@ static int ipm_solve(cfx_ipm* s, const double* v0, const double* fixed_values, d
             hipLaunchKernelGGL(k_lbfgs_update, R.g, blk, 0, st, K);
             IPM_HIP(s, hipGetLastError());
         } else if (!fused) {
-            cfx_internal_msk_stash(s->h, 2);  // K.vx is the point of eval_full above: the MSK stage data may be re-used
-            IPM_CFX(s, cfx_eval_h(s->h, K.vx, K.of, K.ysc, K.hv, CFX_DEVICE));
+            if (s->h) cfx_internal_msk_stash(s->h, 2);  // K.vx is eval_full's point: the MSK stage data may be re-used
+            IPM_RUN(ipm_eval_h(s, K.vx, K.of, K.ysc, K.hv));
             s->st.eval_h++;
         }
         // inertia correction by the curvature test: grow dw until dx^T (W + Sigma + dw) dx > 0
@@ -2965,7 +3042,7 @@ static int ipm_solve(cfx_ipm* s, const double* v0, const double* fixed_values, d
     }
     if (K.rsphase) hipLaunchKernelGGL(k_rs_finish, R.g, blk, 0, st, K);
     hipLaunchKernelGGL(k_ipm_final, R.g, blk, 0, st, K);
-    IPM_CFX(s, cfx_eval_all(s->h, K.vx, K.graw, nullptr, K.fraw, nullptr, CFX_DEVICE));
+    IPM_RUN(ipm_eval_all(s, K.vx, K.graw, nullptr, K.fraw, nullptr, CFX_DEVICE));
     s->st.eval_g_f++;
     hipLaunchKernelGGL(k_ipm_out, R.g, blk, 0, st, K, devp ? y_out : (y_out ? s->d_yo : nullptr),
                        devp ? conv_out : (conv_out ? s->d_conv : nullptr), devp ? its_out : (its_out ? s->d_its : nullptr),

@@ -115,6 +115,49 @@ class IntervalShardedNlp:
         self.cols_local = self.map_v[self.rank]
         self.nv, self.ng = o.nv, o.n_shooting * self.ngk
         self.nnz_jac, self.nnz_hess = len(self._jr), len(self._hr)
+        # placement of the all-gathered slices: one fixed gather-sum table per output (libcfx cfx_gather_sum on a GPU)
+        self._tables = {}
+        if self.dev.type == "cuda":
+            from . import _cfx
+
+            self._lib = _cfx.load_library()
+            maps = {"g": (self.map_g, self.ng), "jac": (self.map_j, self.nnz_jac), "grad": (self.map_v, self.nv),
+                    "hess": (self.map_h, self.nnz_hess)}
+            for name, (mp, width) in maps.items():
+                self._tables[name] = self._gather_table([m.cpu().numpy() for m in mp], width)
+            # selections of this rank's inputs from the full vectors (v columns, lambda rows), and the identity
+            g0 = self.k0 * self.ngk
+            self._tables["v_local"] = self._select_table(self.cols_local.cpu().numpy())
+            self._tables["lam_local"] = self._select_table(np.arange(g0, g0 + self.sub.n_shooting * self.ngk))
+            self._tables["one"] = self._select_table(np.zeros(1, dtype=np.int64))
+
+    def _gather_table(self, maps, width):
+        """CSR (ptr, idx) over the concatenated gathered buffer [rank r's slice at r * pad]: the sources of every
+        destination, in rank order (the index_add_ order)."""
+        pad = max(len(m) for m in maps)
+        dst = np.concatenate([np.asarray(m, np.int64) for m in maps])
+        src = np.concatenate([r * pad + np.arange(len(m)) for r, m in enumerate(maps)])
+        order = np.argsort(dst, kind="stable")
+        ptr = np.zeros(width + 1, dtype=np.int32)
+        np.add.at(ptr, dst + 1, 1)
+        ptr = np.cumsum(ptr).astype(np.int32)
+        T = self.torch
+        return (T.as_tensor(ptr, device=self.dev), T.as_tensor(src[order].astype(np.int32), device=self.dev), pad)
+
+    def _select_table(self, cols):
+        T = self.torch
+        n = len(cols)
+        return (T.as_tensor(np.arange(n + 1, dtype=np.int32), device=self.dev),
+                T.as_tensor(np.asarray(cols, dtype=np.int32), device=self.dev), None)
+
+    def _gather_sum(self, table, src_ptr, src_len, dst_ptr, n_dst):
+        from . import _cfx
+
+        ptr, idx, _ = table
+        rc = self._lib.cfx_gather_sum(self.B, n_dst, ptr.data_ptr(), idx.data_ptr(), src_ptr, src_len, dst_ptr,
+                                      self.torch.cuda.current_stream(self.dev).cuda_stream)
+        if rc != _cfx.OK:
+            raise _cfx.CfxError(rc, self._lib.cfx_last_error(None).decode())
 
     def jac_structure(self):
         return self._jr.astype(np.int32), self._jc.astype(np.int32)
@@ -123,10 +166,9 @@ class IntervalShardedNlp:
         return self._hr.astype(np.int32), self._hc.astype(np.int32)
 
     # ---- exchange -------------------------------------------------------------------------------------
-    def _allgather_place(self, local, maps, width):
-        """All-gather every rank's (B, L_r) slice and index-add it into a (B, width) global array."""
+    def _allgather(self, local, pad):
+        """All-gather every rank's (B, L_r) slice, padded to ``pad``, as one (B, world * pad) tensor on self.dev."""
         torch, dist = self.torch, self.dist
-        pad = max(m.numel() for m in maps)
         # gloo moves host memory only: a rank with device tensors stages the exchange through the host (the
         # nccl / RCCL backend gathers the device buffers directly over xGMI)
         cdev = torch.device("cpu") if (self.dev.type == "cuda" and dist.get_backend(self.group) == "gloo") else self.dev
@@ -134,10 +176,23 @@ class IntervalShardedNlp:
         buf[:, : local.shape[1]] = local.to(cdev)
         out = [torch.empty_like(buf) for _ in range(self.world)]
         dist.all_gather(out, buf, group=self.group)
-        out = [o.to(self.dev) for o in out]
+        return torch.cat([o.to(self.dev) for o in out], dim=1).contiguous()
+
+    def _allgather_place(self, local, maps, width, name=None, dst=None):
+        """All-gather every rank's (B, L_r) slice and sum it into a (B, width) global array: on a GPU with the
+        precomputed table ``name`` (one cfx_gather_sum launch, written into ``dst`` — a tensor or a device pointer —
+        when given), otherwise by an index-add per rank."""
+        torch = self.torch
+        pad = max(m.numel() for m in maps)
+        cat = self._allgather(local, pad)
+        if name in self._tables:
+            out = dst if dst is not None else torch.empty((self.B, width), dtype=torch.float64, device=self.dev)
+            self._gather_sum(self._tables[name], cat.data_ptr(), cat.shape[1],
+                             out if isinstance(out, int) else out.data_ptr(), width)
+            return out
         full = torch.zeros((self.B, width), dtype=torch.float64, device=self.dev)
-        for o, m in zip(out, maps):
-            full.index_add_(1, m, o[:, : m.numel()])
+        for r, m in enumerate(maps):
+            full.index_add_(1, m, cat[:, r * pad: r * pad + m.numel()])
         return full
 
     # ---- callbacks (same signatures as _cfx.Handle, AoS (B, ...) tensors) ------------------------------
@@ -152,15 +207,56 @@ class IntervalShardedNlp:
         dl = torch.empty((self.B, sub.nv), dtype=torch.float64, device=self.dev) if grad is not None else None
         self.h.eval_all(vl, g=gl, jac=jl, f=fl, grad=dl)
         if g is not None:
-            g.copy_(self._allgather_place(gl, self.map_g, self.ng))
+            g.copy_(self._allgather_place(gl, self.map_g, self.ng, "g"))
         if jac is not None:
-            jac.copy_(self._allgather_place(jl, self.map_j, self.nnz_jac))
+            jac.copy_(self._allgather_place(jl, self.map_j, self.nnz_jac, "jac"))
         if f is not None:
-            fs = fl.cpu() if (self.dev.type == "cuda" and self.dist.get_backend(self.group) == "gloo") else fl.clone()
-            self.dist.all_reduce(fs, group=self.group)
-            f.copy_(fs.to(self.dev))
+            f.copy_(self._reduce_f(fl))
         if grad is not None:
-            grad.copy_(self._allgather_place(dl, self.map_v, self.nv))
+            grad.copy_(self._allgather_place(dl, self.map_v, self.nv, "grad"))
+
+    def _reduce_f(self, fl):
+        fs = fl.cpu() if (self.dev.type == "cuda" and self.dist.get_backend(self.group) == "gloo") else fl.clone()
+        self.dist.all_reduce(fs, group=self.group)
+        return fs.to(self.dev)
+
+    # ---- the same callbacks on raw device pointers (AoS, the full problem), for libcfx's own interior point
+    # (cfx_ipm_create_ext, ShardedNativeIpm): inputs selected by the gather table, outputs placed straight into the
+    # solver's buffers
+    def eval_all_ptr(self, v, g, jac, f, grad):
+        torch, sub = self.torch, self.sub
+        vl = torch.empty((self.B, sub.nv), dtype=torch.float64, device=self.dev)
+        self._gather_sum(self._tables["v_local"], v, self.nv, vl.data_ptr(), sub.nv)
+        gl = torch.empty((self.B, sub.n_shooting * self.ngk), dtype=torch.float64, device=self.dev) if (g or jac) \
+            else None
+        jl = torch.empty((self.B, self.h.nnz_jac), dtype=torch.float64, device=self.dev) if jac else None
+        fl = torch.empty((self.B,), dtype=torch.float64, device=self.dev) if f else None
+        dl = torch.empty((self.B, sub.nv), dtype=torch.float64, device=self.dev) if grad else None
+        self.h.eval_all(vl, g=gl, jac=jl, f=fl, grad=dl)
+        if g:
+            self._allgather_place(gl, self.map_g, self.ng, "g", dst=g)
+        if jac:
+            self._allgather_place(jl, self.map_j, self.nnz_jac, "jac", dst=jac)
+        if f:
+            fs = self._reduce_f(fl).contiguous()
+            self._gather_sum(self._tables["one"], fs.data_ptr(), 1, f, 1)
+        if grad:
+            self._allgather_place(dl, self.map_v, self.nv, "grad", dst=grad)
+        return 0
+
+    def eval_h_ptr(self, v, of, lam, hess):
+        torch, sub = self.torch, self.sub
+        vl = torch.empty((self.B, sub.nv), dtype=torch.float64, device=self.dev)
+        self._gather_sum(self._tables["v_local"], v, self.nv, vl.data_ptr(), sub.nv)
+        ngl = sub.n_shooting * self.ngk
+        laml = torch.empty((self.B, ngl), dtype=torch.float64, device=self.dev)
+        self._gather_sum(self._tables["lam_local"], lam, self.ng, laml.data_ptr(), ngl)
+        ofl = torch.empty((self.B,), dtype=torch.float64, device=self.dev)
+        self._gather_sum(self._tables["one"], of, 1, ofl.data_ptr(), 1)
+        hl = torch.empty((self.B, self.h.nnz_hess), dtype=torch.float64, device=self.dev)
+        self.h.eval_h(vl, ofl, laml, hl)
+        self._allgather_place(hl, self.map_h, self.nnz_hess, "hess", dst=hess)
+        return 0
 
     def eval_h(self, v, of, lam, hess):
         torch = self.torch
@@ -169,8 +265,57 @@ class IntervalShardedNlp:
         laml = lam[:, g0: g0 + self.sub.n_shooting * self.ngk].contiguous()
         hl = torch.empty((self.B, self.h.nnz_hess), dtype=torch.float64, device=self.dev)
         self.h.eval_h(vl, of.contiguous(), laml, hl)
-        hess.copy_(self._allgather_place(hl, self.map_h, self.nnz_hess))
+        hess.copy_(self._allgather_place(hl, self.map_h, self.nnz_hess, "hess"))
         return hess
 
     def close(self):
         self.h.close()
+
+
+class ShardedNativeIpm:
+    """libcfx's own interior point (cfx_ipm, csrc/cfx_ipm.hip) over the interval-sharded callbacks of ONE OCP: every
+    rank holds the full KKT system (the band assembly and factorisation run replicated on identical data, as the
+    callbacks' all-gather leaves every rank the full values) and evaluates only its interval slice — the solver reaches
+    its callbacks through cfx_ipm_create_ext, the value slices land in its buffers by one cfx_gather_sum launch each.
+    Same ``solve`` / result as solver.NativeIpm.  SURVEY.md section 8(e); the reference's analogue is CasADi's `map`
+    over intervals with n_threads (cocofest/optimization/fes_ocp.py:122,189)."""
+
+    def __init__(self, ocp, batch: int = 1, options=None, group=None, device=None):
+        import torch
+
+        from . import _cfx
+        from .solver import _HESSIAN_APPROXIMATION, _NATIVE_OPTIONS, _RESTORATION, IpmOptions
+
+        self.torch = torch
+        self.ocp, self.B = ocp, batch
+        self.opt = options or IpmOptions()
+        self.nlp = IntervalShardedNlp(ocp, batch=batch, group=group, device=device)
+        lb, ub = ocp.bounds_vector()
+        self.n, self.m = self.nlp.nv, self.nlp.ng
+        self.ipm = _cfx.Ipm.external(
+            batch, self.nlp.nv, self.nlp.ng, self.nlp.jac_structure(), self.nlp.hess_structure(),
+            self.nlp.eval_all_ptr, self.nlp.eval_h_ptr, lb, ub, int(getattr(ocp, "n_params", 0) or 0),
+            {**{k: getattr(self.opt, k) for k in _NATIVE_OPTIONS},
+             "hessian_approximation": _HESSIAN_APPROXIMATION[self.opt.hessian_approximation],
+             "restoration": _RESTORATION[self.opt.restoration]},
+            device=self.nlp.dev.index, stream=torch.cuda.current_stream(self.nlp.dev).cuda_stream)
+
+    def solve(self, v0=None, fixed_values=None):
+        import time
+
+        from .solver import IpmResult
+
+        t0 = time.perf_counter()
+        if v0 is None:
+            v0 = np.tile(self.ocp.initial_guess_vector(), (self.B, 1))
+        v, y, f, conv, its, kkt = self.ipm.solve(v0, fixed_values)
+        st = self.ipm.stats()
+        self.last_stats = st
+        return IpmResult(v=v, y=y, f=f, converged=conv, iterations=its, kkt_error=kkt,
+                         wall_time=time.perf_counter() - t0,
+                         n_callbacks={k: int(st[k]) for k in ("eval_all", "eval_h", "eval_g_f", "kkt_factor")},
+                         status=self.ipm.status())
+
+    def close(self):
+        self.ipm.close()
+        self.nlp.close()

@@ -50,6 +50,7 @@ extern "C" {
 #define CFX_ENOMEM (-3)
 #define CFX_EUNSUPPORTED (-4)
 #define CFX_ENODEV (-5)
+#define CFX_ECALLBACK (-6) /* a caller-supplied evaluator (cfx_ipm_create_ext) returned non-zero */
 
 /* models (cocofest/models/model_maker.py:9-22) */
 #define CFX_DING2003 0
@@ -408,12 +409,41 @@ int cfx_ipm_create(cfx_handle *h, const double *lb, const double *ub, int32_t n_
    outputs are written asynchronously on the handle's stream; otherwise host pointers. */
 int cfx_ipm_solve(cfx_ipm *s, const double *v0, const double *fixed_values, double *v, double *y, double *f,
                   int32_t *converged, int32_t *iterations, double *kkt_error, uint32_t flags);
+/* The same solver over callbacks the caller provides instead of a libcfx handle — e.g. one OCP's intervals sharded
+   over several GPUs, each rank evaluating its slice and all-gathering the value slices (cocofest_amd/distributed.py,
+   the interval sharding of SURVEY.md section 8(e)).  The NLP is described by its sizes and fixed triplet structures
+   (J_g: ng x nv; Hessian: lower triangle, row >= col); the evaluator's functions are called synchronously from
+   cfx_ipm_solve's host thread with device pointers (AoS [batch][len]) that the solver's kernels on `hip_stream` wrote
+   or read: the evaluator must order its own work after the work queued on that stream, and have finished writing its
+   outputs when it returns (a callback on the same stream satisfies both).  Any output pointer may be NULL (not
+   wanted).  A non-zero return aborts the solve with CFX_ECALLBACK. */
+typedef struct cfx_evaluator {
+    void *ctx;
+    int (*eval_all)(void *ctx, const double *v, double *g, double *jac, double *f, double *grad);
+    int (*eval_h)(void *ctx, const double *v, const double *obj_factor, const double *lambda, double *hess);
+} cfx_evaluator;
+typedef struct cfx_nlp_desc {
+    int64_t batch, nv, ng, nnz_jac, nnz_hess;
+    const int32_t *jac_row, *jac_col, *hess_row, *hess_col; /* host arrays, copied */
+    int32_t device;
+    void *hip_stream;
+} cfx_nlp_desc;
+int cfx_ipm_create_ext(const cfx_nlp_desc *nlp, const cfx_evaluator *ev, const double *lb, const double *ub,
+                       int32_t n_params, const cfx_ipm_options *opt, cfx_ipm **out);
 int cfx_ipm_get_stats(const cfx_ipm *s, cfx_ipm_stats *out);
 /* status [B] (host): CFX_IPM_* outcome of every instance of the last cfx_ipm_solve */
 int cfx_ipm_get_status(const cfx_ipm *s, int32_t *status);
 int cfx_ipm_n_fixed(const cfx_ipm *s);
 const char *cfx_ipm_last_error(const cfx_ipm *s);
 void cfx_ipm_destroy(cfx_ipm *s);
+
+/* ---- placing gathered value slices --------------------------------------------------------------------
+   dst[b][i] = sum over s in [ptr[i], ptr[i+1]) of src[b][idx[s]] for the batch-major (AoS) src [batch][src_len] and
+   dst [batch][n_dst] on `hip_stream` (device pointers; ptr / idx device int32 arrays): the fixed gather table that
+   places every rank's all-gathered value slices of an interval-sharded OCP into the full g / J_g / grad f / Hessian
+   arrays, summing the entries several slices contribute (halo nodes, parameters) in a fixed order (no atomics). */
+int cfx_gather_sum(int64_t batch, int64_t n_dst, const int32_t *ptr, const int32_t *idx, const double *src,
+                   int64_t src_len, double *dst, void *hip_stream);
 
 #ifdef __cplusplus
 }

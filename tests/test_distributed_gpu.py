@@ -76,11 +76,27 @@ def _worker(rank, port, out_dir):
         np.savez(os.path.join(out_dir, f"ipm_r{rank}.npz"), v=res.v, converged=res.converged, f=res.f, v0=v0,
                  iterations=res.iterations, kkt=res.kkt_error)
         ipm.close()
-        if rank == 0:  # the same algorithm on one process-local handle of the whole problem
+        # libcfx's own interior point on the sharded callbacks (cfx_ipm_create_ext; value slices placed by
+        # cfx_gather_sum)
+        from cocofest_amd.distributed import ShardedNativeIpm
+
+        nat = ShardedNativeIpm(ocp, batch=2, options=IpmOptions(tol=1e-6, max_iter=500), device=0)
+        rn = nat.solve(v0)
+        nat.close()
+        np.savez(os.path.join(out_dir, f"native_r{rank}.npz"), v=rn.v, converged=rn.converged, f=rn.f,
+                 iterations=rn.iterations, status=rn.status)
+        if rank == 0:  # the same algorithms on one process-local handle of the whole problem
+            from cocofest_amd.solver import NativeIpm
+
             one = BatchedIpm(ocp, batch=2, options=IpmOptions(tol=1e-6, max_iter=500))
             r1 = one.solve(v0)
             one.close()
             np.savez(os.path.join(out_dir, "ipm_single.npz"), v=r1.v, converged=r1.converged, f=r1.f,
+                     iterations=r1.iterations)
+            one = NativeIpm(ocp, batch=2, options=IpmOptions(tol=1e-6, max_iter=500))
+            r1 = one.solve(v0)
+            one.close()
+            np.savez(os.path.join(out_dir, "native_single.npz"), v=r1.v, converged=r1.converged, f=r1.f,
                      iterations=r1.iterations)
     finally:
         dist.destroy_process_group()
@@ -136,6 +152,26 @@ def test_batched_interior_point_on_interval_sharded_libcfx(sharded_gpu_run):
     ocp = cases.product_ocp(**IPM_CFG)
     lb, ub = ocp.bounds_vector()
     # fixed variables (lb == ub) have zero span: floor it with the variable's own magnitude
+    span = np.where(np.isfinite(ub - lb), ub - lb, 0.0)
+    span = np.maximum(span, np.maximum(1e-12, np.abs(one["v"]).max(axis=0)))
+    assert np.max(np.abs(r0["v"] - one["v"]) / span) < 1e-6
+    np.testing.assert_allclose(r0["f"], one["f"], rtol=1e-7)
+
+
+def test_native_interior_point_on_interval_sharded_libcfx(sharded_gpu_run):
+    """libcfx's own interior point (cfx_ipm through cfx_ipm_create_ext: its callbacks are the 2-rank interval-sharded
+    libcfx slices, all-gathered and placed by one cfx_gather_sum launch per output) converges in lockstep on both
+    ranks, to the single-process cfx_ipm point (cfg 3, from the reference's initial guess and a perturbed start)."""
+    r0 = np.load(sharded_gpu_run / "native_r0.npz")
+    r1 = np.load(sharded_gpu_run / "native_r1.npz")
+    one = np.load(sharded_gpu_run / "native_single.npz")
+    assert one["converged"].all(), one["iterations"]
+    assert r0["converged"].all(), (r0["iterations"], r0["status"])
+    np.testing.assert_array_equal(r0["v"], r1["v"])
+    np.testing.assert_array_equal(r0["iterations"], r1["iterations"])
+    assert np.all(np.abs(r0["iterations"] - one["iterations"]) <= 2), (r0["iterations"], one["iterations"])
+    ocp = cases.product_ocp(**IPM_CFG)
+    lb, ub = ocp.bounds_vector()
     span = np.where(np.isfinite(ub - lb), ub - lb, 0.0)
     span = np.maximum(span, np.maximum(1e-12, np.abs(one["v"]).max(axis=0)))
     assert np.max(np.abs(r0["v"] - one["v"]) / span) < 1e-6
