@@ -14,7 +14,7 @@ import numpy as np
 import pytest
 
 from tests import cases
-from tests.test_gpu_parity import COL_STIMS, _close, _close_g
+from tests.test_gpu_parity import COL_STIMS, _close
 from tests.test_launch_shapes import ENV, _run, _tile, _untile
 
 pytestmark = pytest.mark.gpu
@@ -42,6 +42,12 @@ def _col(name, degree, method, n_shooting=10):
 KPTS = [1, 2, 4, 5, 10]
 
 
+def _close_col_g(v, g, g_ref, degree, what):
+    """Defects are differences of O(|x| / dt)-sized terms: compare against that scale (as test_gpu_parity.py)."""
+    scale = np.abs(v).max(axis=1, keepdims=True) * (degree + 1) ** 2
+    assert np.max(np.abs(g - g_ref) / scale) <= 1e-13, what
+
+
 @pytest.mark.parametrize("degree,method", [(3, "legendre"), (4, "legendre"), (2, "radau"), (6, "legendre")])
 @pytest.mark.parametrize("name", ["ding2003", "ding2003_with_fatigue", "ding2007", "ding2007_with_fatigue",
                                   "hmed2018", "hmed2018_with_fatigue"])
@@ -55,7 +61,7 @@ def test_collocation_launch_shapes_are_bitwise_identical(name, degree, method, m
     (g_ref, j_ref), shape = _run(ocp, v, "soa", monkeypatch, {"CFX_KPT": 1, "CFX_IFAST": 0, "CFX_NI": 1})
     assert (shape["intervals_per_thread"], shape["intervals_fast"], shape["instances_per_lane"]) == (1, 0, 1)
     pick = np.array([0, 1, 63, 64, 255, 256, 511, 512, 700, 1023, 1024, B - 2, B - 1])
-    _close_g(pb, v[pick], g_ref[pick], CO.eval_g(pb, v[pick]), what=f"colloc g {name} {degree}")
+    _close_col_g(v[pick], g_ref[pick], CO.eval_g(pb, v[pick]), degree, f"colloc g {name} {degree}")
     _close(j_ref[pick], CO.eval_jac_g(pb, v[pick]), what=f"colloc J {name} {degree}")
     pairs = not name.startswith("hmed") and degree <= 5  # two instances per lane: Ding families, degrees 1..5
     seen = set()
@@ -124,7 +130,7 @@ def test_collocation_fused_launch_matches_the_separate_callbacks(name):
         np.testing.assert_array_equal(a, b)
     g, j, hh = res["soa"][:3]
     pick = np.array([0, 1, 63, 64, 100, B - 1])
-    _close_g(pb, v[pick], g[pick], CO.eval_g(pb, v[pick]), what=f"fused colloc g {name}")
+    _close_col_g(v[pick], g[pick], CO.eval_g(pb, v[pick]), 4, f"fused colloc g {name}")
     _close(j[pick], CO.eval_jac_g(pb, v[pick]), what=f"fused colloc J {name}")
 
 
@@ -160,5 +166,5 @@ def test_bench_shape_collocation():
     np.testing.assert_array_equal(gp, small.eval_g(vp))
     np.testing.assert_array_equal(jp, small.eval_jac_g(vp))
     small.close()
-    _close_g(pb, vp, gp, CO.eval_g(pb, vp), what="bench colloc g")
+    _close_col_g(vp, gp, CO.eval_g(pb, vp), 4, "bench colloc g")
     _close(jp, CO.eval_jac_g(pb, vp), what="bench colloc J")
