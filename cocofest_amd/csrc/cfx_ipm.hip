@@ -2919,6 +2919,9 @@ static int ipm_solve(cfx_ipm* s, const double* v0, const double* fixed_values, d
     int32_t c[4];
     int n_active = (int)B, n_resto = 0;
     double last_print = 0.0;
+    // some instance may be in the restoration phase: the k_rs_* launches are skipped while none is (the batch-1
+    // latency of an iteration is its chain of launches)
+    bool rs_live = false;
     // One host iteration advances every instance still iterating by one iteration of its own: a main iteration, or
     // one of the restoration phase (k_rs_*) for the instances in it — the same callback launches, factorisations and
     // line-search loop serve both (section "Ipopt's feasibility-restoration phase" above).  Every instance's
@@ -2955,7 +2958,7 @@ static int ipm_solve(cfx_ipm* s, const double* v0, const double* fixed_values, d
         } else {
             hipLaunchKernelGGL(k_ipm_begin, R.g, blk, 0, st, K, 1, R.next_slot());
         }
-        if (K.rsphase) hipLaunchKernelGGL(k_rs_begin, R.g, blk, 0, st, K);
+        if (K.rsphase && rs_live) hipLaunchKernelGGL(k_rs_begin, R.g, blk, 0, st, K);
         reinit = false;
         IPM_HIP(s, hipGetLastError());
         if (K.lbfgs) {  // quasi-Newton pair of the last step, M (no eval_h: hv stays zero)
@@ -2986,14 +2989,15 @@ static int ipm_solve(cfx_ipm* s, const double* v0, const double* fixed_values, d
             if (c[1] == 0) break;
         }
         if (all_done) break;
+        rs_live = n_resto > 0;  // instances iterating in the phase (counted by k_ipm_curv)
         hipLaunchKernelGGL(k_ipm_dir, R.g, blk, 0, st, K, it);
-        if (K.rsphase) hipLaunchKernelGGL(k_rs_dir, R.g, blk, 0, st, K);
+        if (K.rsphase && rs_live) hipLaunchKernelGGL(k_rs_dir, R.g, blk, 0, st, K);
         // filter line search with second-order corrections (the phase's own filter line search alongside)
         int notacc = 0;
         for (int ls = 0; ls < K.o.max_backtrack; ++ls) {
             IPM_RUN(R.eval_gf(true));
             int sl = R.next_slot();
-            if (K.rsphase) hipLaunchKernelGGL(k_rs_accept, R.g, blk, 0, st, K);
+            if (K.rsphase && rs_live) hipLaunchKernelGGL(k_rs_accept, R.g, blk, 0, st, K);
             hipLaunchKernelGGL(k_ipm_accept, R.g, blk, 0, st, K, ls, sl);
             IPM_HIP(s, hipGetLastError());
             IPM_RUN(R.read(sl, c));
@@ -3013,15 +3017,16 @@ static int ipm_solve(cfx_ipm* s, const double* v0, const double* fixed_values, d
                 }
             if (notacc == 0) break;
             hipLaunchKernelGGL(k_ipm_next_trial, R.g, blk, 0, st, K);
-            if (K.rsphase) hipLaunchKernelGGL(k_rs_next_trial, R.g, blk, 0, st, K);
+            if (K.rsphase && rs_live) hipLaunchKernelGGL(k_rs_next_trial, R.g, blk, 0, st, K);
         }
         // failed line searches: the restoration phase (its iterations for the instances in it; the instances whose
         // search failed enter it), or a feasibility-restoration step, a fresh filter and least-squares multipliers
         const bool resto = notacc > 0 && K.m > 0;
         if (K.rsphase) {
-            hipLaunchKernelGGL(k_rs_update, R.g, blk, 0, st, K);
+            if (rs_live) hipLaunchKernelGGL(k_rs_update, R.g, blk, 0, st, K);
             if (resto) hipLaunchKernelGGL(k_rs_init, R.g, blk, 0, st, K);
             IPM_HIP(s, hipGetLastError());
+            rs_live = rs_live || resto;  // entrants (k_rs_init) or instances still in the phase
         } else if (resto) {
             IPM_RUN(R.kkt_factor(KKT_RESTO));
             int sl = R.next_slot();
