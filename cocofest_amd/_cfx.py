@@ -15,7 +15,7 @@ import numpy as np
 
 LIB_PATH = pathlib.Path(__file__).with_name("libcfx.so")
 
-ABI_VERSION = 6
+ABI_VERSION = 7
 OK, EINVAL, EHIP, ENOMEM, EUNSUPPORTED, ENODEV, ECALLBACK = 0, -1, -2, -3, -4, -5, -6
 MODEL_IDS = {
     "ding2003": 0,
@@ -114,7 +114,8 @@ class IpmOptions(C.Structure):
                 ("limited_memory_max_history", C.c_int32), ("restoration", C.c_int32),
                 ("max_resto_iter", C.c_int32), ("resto_penalty", C.c_double),
                 ("required_infeasibility_reduction", C.c_double), ("filter_reset_trigger", C.c_int32),
-                ("max_filter_resets", C.c_int32), ("max_wall_time", C.c_double), ("print_frequency_time", C.c_double)]
+                ("max_filter_resets", C.c_int32), ("max_wall_time", C.c_double), ("print_frequency_time", C.c_double),
+                ("soft_resto_pderror_reduction_factor", C.c_double), ("max_soft_resto_iters", C.c_int32)]
 
 
 # cfx_ipm_get_status values (Ipopt's ApplicationReturnStatus)
@@ -127,7 +128,7 @@ class IpmStats(C.Structure):
                 ("iterations", C.c_int64), ("host_syncs", C.c_int64), ("wall_s", C.c_double),
                 ("kkt_n", C.c_int64), ("kkt_kl", C.c_int64), ("kkt_ku", C.c_int64), ("kkt_band_n", C.c_int64),
                 ("kkt_border", C.c_int64), ("kkt_blocks", C.c_int64), ("resto_phases", C.c_int64),
-                ("resto_iterations", C.c_int64)]
+                ("resto_iterations", C.c_int64), ("soft_steps", C.c_int64)]
 
 
 # cfx_evaluator / cfx_nlp_desc (cfx_ipm_create_ext): caller-supplied callbacks of an NLP the solver runs on

@@ -43,7 +43,7 @@ constexpr int col_rowlen(int model, int r, int deg, int nu) {
 // degree, NI = 1, states re-read from memory per point.  ES / vb / gb / jb: element stride and the instances' bases
 // of V, G, J (SoA or 64-instance tiles, lay_stride / lay_base).  Shared by k_colloc and the fused g + J_g + Hessian
 // launch (k_colloc_hess<GJ>), so the two write the same bits.
-template <int MODEL, int TMAX, int DEG, int NI>
+template <int MODEL, int TMAX, int DEG, int NI, bool PLAIN = false>
 __device__ __forceinline__ void colloc_interval(const KParams& P, const double* __restrict__ V, double* __restrict__ G,
                                                 double* __restrict__ J, int k, int64_t ES, int64_t vb, int64_t gb,
                                                 int64_t jb, double (&xc)[nx_of(MODEL)][NI]) {
@@ -147,7 +147,7 @@ __device__ __forceinline__ void colloc_interval(const KParams& P, const double* 
                     for (int i = 0; i <= d; ++i) poly = fma(P.colC[i][j], X(i, r, n), poly);
                     t[n] = fma(-P.dt, f[n][r], poly);
                 }
-                st_lane<NI>(G + gb + (go + (j - 1) * NX + r) * ES, t);
+                st_lane_p<NI, PLAIN>(G + gb + (go + (j - 1) * NX + r) * ES, t);
             }
         }
         if (J) {
@@ -162,7 +162,7 @@ __device__ __forceinline__ void colloc_interval(const KParams& P, const double* 
                         const double diag = r == 0 ? -P.inv_tauc : fd[n][r][r];
                         t[n] = i == j ? fma(-P.dt, diag, P.colC[i][j]) : P.colC[i][j];
                     }
-                    st_lane<NI>(J + jb + (o + i) * ES, t);
+                    st_lane_p<NI, PLAIN>(J + jb + (o + i) * ES, t);
                 }
                 o += d + 1;
 #pragma unroll
@@ -171,7 +171,7 @@ __device__ __forceinline__ void colloc_interval(const KParams& P, const double* 
                         double t[NI];
 #pragma unroll
                         for (int n = 0; n < NI; ++n) t[n] = -P.dt * fd[n][r][c];
-                        st_lane<NI>(J + jb + (o++) * ES, t);
+                        st_lane_p<NI, PLAIN>(J + jb + (o++) * ES, t);
                     }
                 if constexpr (HM) {
                     if (r == 0) {
@@ -181,7 +181,7 @@ __device__ __forceinline__ void colloc_interval(const KParams& P, const double* 
                                 double t[NI];
 #pragma unroll
                                 for (int n = 0; n < NI; ++n) t[n] = -P.dt * P.inv_tauc * coef[i] * lamd[n][i];
-                                st_lane<NI>(J + jb + (o + i) * ES, t);
+                                st_lane_p<NI, PLAIN>(J + jb + (o + i) * ES, t);
                             }
                         o += P.T;
                     }
@@ -191,7 +191,7 @@ __device__ __forceinline__ void colloc_interval(const KParams& P, const double* 
                         double t[NI];
 #pragma unroll
                         for (int n = 0; n < NI; ++n) t[n] = -P.dt * fd[n][1][NX];
-                        st_lane<NI>(J + jb + (o++) * ES, t);
+                        st_lane_p<NI, PLAIN>(J + jb + (o++) * ES, t);
                     }
                 }
             }
@@ -209,13 +209,21 @@ __device__ __forceinline__ void colloc_interval(const KParams& P, const double* 
                 for (int i = 0; i <= d; ++i) e = fma(P.colD[i], X(i, r, n), e);
                 t[n] = e - xn[r][n];
             }
-            st_lane<NI>(G + gb + (go + d * NX + r) * ES, t);
+            st_lane_p<NI, PLAIN>(G + gb + (go + d * NX + r) * ES, t);
         }
         if (J) {
             const int64_t o = jo + (int64_t)d * sumrow + (int64_t)r * (d + 2);
 #pragma unroll UN
-            for (int i = 0; i <= d; ++i) st_lane_const<NI>(J + jb + (o + i) * ES, P.colD[i]);
-            st_lane_const<NI>(J + jb + (o + d + 1) * ES, -1.0);
+            for (int i = 0; i <= d; ++i) {
+                double t[NI];
+#pragma unroll
+                for (int n = 0; n < NI; ++n) t[n] = P.colD[i];
+                st_lane_p<NI, PLAIN>(J + jb + (o + i) * ES, t);
+            }
+            double m1[NI];
+#pragma unroll
+            for (int n = 0; n < NI; ++n) m1[n] = -1.0;
+            st_lane_p<NI, PLAIN>(J + jb + (o + d + 1) * ES, m1);
         }
     }
 #pragma unroll
@@ -228,7 +236,7 @@ __device__ __forceinline__ void colloc_interval(const KParams& P, const double* 
 // shooting launch (interval chunks on grid.x when P.ifast, instance blocks on grid.y).  Each interval reads its own
 // block (x^0 carried from the previous interval's x_{k+1}) and x_{k+1}^0; no recursion, so the intervals per thread
 // only shape the launch (fewer, longer waves; the carried x^0 is read once).
-template <int MODEL, int TMAX, int DEG, int NI>
+template <int MODEL, int TMAX, int DEG, int NI, bool PLAIN = false>
 __global__ void __launch_bounds__(256) k_colloc(const KParams P, const double* __restrict__ V, double* __restrict__ G,
                                                 double* __restrict__ J) {
     constexpr int NX = nx_of(MODEL);
@@ -244,7 +252,7 @@ __global__ void __launch_bounds__(256) k_colloc(const KParams P, const double* _
 #pragma unroll
         for (int r = 0; r < NX; ++r) ld_lane<NI>(V + vb + ((int64_t)k0 * P.nz + r) * ES, xc[r]);
     }
-    for (int k = k0; k < k1; ++k) colloc_interval<MODEL, TMAX, DEG, NI>(P, V, G, J, k, ES, vb, gb, jb, xc);
+    for (int k = k0; k < k1; ++k) colloc_interval<MODEL, TMAX, DEG, NI, PLAIN>(P, V, G, J, k, ES, vb, gb, jb, xc);
 }
 
 // Lagrangian Hessian of the collocation defects: sum_{j,r} lambda_{k,j,r} (-dt) d^2 f_r(x_k^j, u_k).  Local

@@ -2,10 +2,23 @@
 #include "cfx_colloc.h"
 #include "cfx_launch.h"
 
+#include <cstdlib>
+#include <cstring>
+
 namespace cfx {
 
 // grid as the shooting launch: interval chunks of P.kpt intervals on grid.x when P.ifast (the chunks of one instance
 // block, which write one region of each 64-instance output tile, dispatched together), instance blocks on grid.y
+// CFX_COLLOC_STORE=plain: ordinary instead of non-temporal output stores (store-policy probe, bench's instantiation
+// only; read once per process)
+static bool colloc_plain_stores() {
+    static const bool plain = [] {
+        const char* e = getenv("CFX_COLLOC_STORE");
+        return e && strcmp(e, "plain") == 0;
+    }();
+    return plain;
+}
+
 template <int MODEL, int TMAX, int DEG, int NI>
 static hipError_t colloc_deg(const KParams& P, const double* V, double* G, double* J, hipStream_t s) {
     const int64_t per_block = (int64_t)kBlock * NI;
@@ -13,6 +26,12 @@ static hipError_t colloc_deg(const KParams& P, const double* V, double* G, doubl
     KParams Q = P;
     if (nbi > (unsigned)kMaxGridY) Q.ifast = 0;  // instance blocks must fit grid.y in the intervals-fast order
     dim3 grid(Q.ifast ? nbk : nbi, Q.ifast ? nbi : nbk);
+    if constexpr (MODEL == M_D03 && DEG == 4 && NI == 2) {
+        if (colloc_plain_stores()) {
+            hipLaunchKernelGGL((k_colloc<MODEL, TMAX, DEG, NI, true>), grid, dim3(kBlock), 0, s, Q, V, G, J);
+            return hipGetLastError();
+        }
+    }
     hipLaunchKernelGGL((k_colloc<MODEL, TMAX, DEG, NI>), grid, dim3(kBlock), 0, s, Q, V, G, J);
     return hipGetLastError();
 }

@@ -65,6 +65,10 @@ struct Scal {
     int32_t stop;    // done, not converged (status says why)
     int32_t status;  // CFX_IPM_STATUS_* once done
     int32_t spad;
+    // soft restoration: its step and the primal-dual error at x; taking soft steps, how many, tried this iteration,
+    // the try was accepted by the original filter
+    double soft_a, soft_pd;
+    int32_t soft_on, soft_cnt, soft_try, soft_ok;
 };
 
 // how a restoration phase ended (Scal::rs_exit)
@@ -132,7 +136,11 @@ struct IpmK {
     double *rp, *rn, *rzp, *rzn, *rdp, *rdn, *rdzp, *rdzn, *rpt, *rnt, *ry, *rdc;
     double *rzl, *rzu;
     double* rfilt;
-    unsigned long long* rstat;  // [2] phases entered, phase iterations (summed over the instances)
+    unsigned long long* rstat;  // [3] phases entered, phase iterations, soft steps (summed over the instances)
+    // soft restoration (o.soft_resto_pderror_reduction_factor > 0): the trial point's J_g values and gradient; npd =
+    // nf + m + bounded sides, the number of terms of the primal-dual system error
+    double *jact, *gradt;  // [B][nnzj], [B][n]
+    int npd;
 };
 
 enum { KKT_NEWTON = 0, KKT_LSMULT = 1, KKT_RESTO = 2, KKT_RSNLP = 3 };
@@ -880,7 +888,7 @@ __global__ void __launch_bounds__(kIB) k_ipm_dir(const IpmK K, int it) {
             S.wd_mu = mu;
         }
         S.alpha = alpha0;
-        S.accepted = S.done;
+        S.accepted = S.done || S.soft_on;  // soft-restoration steps replace the line search (k_soft_trial)
         S.armijo = 0;
         S.soc = 0;
         S.forced = 0;
@@ -953,6 +961,7 @@ __global__ void __launch_bounds__(kIB) k_ipm_accept(const IpmK K, int ls, int sl
     if (threadIdx.x == 0) {
         count_add(K, slot, 0, !S.accepted);
         if (S.soc) atomicAdd(K.cnt + 4 * slot + 1, 1);
+        if (S.soft_on && !S.done) atomicAdd(K.cnt + 4 * slot + 2, 1);  // taking soft steps (no line search)
     }
 }
 
@@ -1146,6 +1155,142 @@ __global__ void __launch_bounds__(kIB) k_ipm_resto_accept(const IpmK K, int slot
     count_add(K, slot, 0, todo);
 }
 
+// ---- Ipopt's soft restoration (IpBacktrackingLineSearch::TrySoftRestoStep; solver.py, soft_resto_...) ----------
+// Ipopt's primal-dual system error of the scaled problem at (x, y, zl, zu): (|grad L|_1 + |c|_1 + sum |s z - mu|) / npd.
+// gF / gS: the scaled objective gradient and constraints at x; the scaled J_g values are jac[jsel] d sg (jac_raw) or jv
+__device__ double pd_error(const IpmK& K, int64_t b, const double* x, const double* y, double ay, const double* dy,
+                           const double* zl, const double* zu, double az, const double* dzl, const double* dzu,
+                           const double* gF, const double* jac_raw, const double* jv, const double* gS, double mu) {
+    const int nf = K.nf, m = K.m;
+    const double* lbI = K.lbI + b * nf;
+    const double* ubI = K.ubI + b * nf;
+    const double* sg = K.sg + b * m;
+    double sd = 0.0, sp = 0.0, scl = 0.0, scu = 0.0;
+    for (int i = threadIdx.x; i < nf; i += kIB) {
+        double jty = 0.0;
+        for (int k = K.jt_ptr[i]; k < K.jt_ptr[i + 1]; ++k) {
+            const int s = K.jt_idx[k], r = K.jr[s];
+            const double jvs = jac_raw ? jac_raw[K.jsel[s]] * K.d[K.jc[s]] * sg[r] : jv[s];
+            jty += jvs * (y[r] + ay * dy[r]);
+        }
+        const double l = zl[i] + az * dzl[i], u = zu[i] + az * dzu[i];
+        sd += fabs(gF[i] + jty - l + u);
+        if (K.hasL[i]) scl += fabs((x[i] - lbI[i]) * l - mu);
+        if (K.hasU[i]) scu += fabs((ubI[i] - x[i]) * u - mu);
+    }
+    for (int j = threadIdx.x; j < m; j += kIB) sp += fabs(gS ? gS[j] : 0.0);
+    double rv[4] = {sd, sp, scl, scu};
+    const int ro[4] = {0, 0, 0, 0};
+    breduce_n(rv, ro);
+    return (((rv[0] + rv[1]) + rv[2]) + rv[3]) / K.npd;
+}
+
+// after the line search: the instances taking soft steps count one more (past max_soft_resto_iters their search counts
+// as failed); the candidates — failed searches outside the watchdog, instances taking soft steps — get the trial
+// x + a dx, a = min(a_p, a_z), in xt / vt and the primal-dual error at x.  counters: [0] candidates, [1] instances
+// whose soft steps ran out
+__global__ void __launch_bounds__(kIB) k_soft_trial(const IpmK K, int slot) {
+    __shared__ Scal S;
+    const int64_t b = blockIdx.x;
+    const int nf = K.nf;
+    load_scal(K, b, S);
+    if (S.rs_on || S.done) {  // block-uniform
+        count_add(K, slot, 0, 0);
+        return;
+    }
+    const bool was = S.soft_on;
+    const int cnt = S.soft_cnt + (was ? 1 : 0);
+    const bool over = was && cnt > K.o.max_soft_resto_iters;
+    const bool cand = (!S.accepted && !S.wd_on) || (was && !over);
+    const double a = min_n(S.a_p, S.a_z);
+    double pd = 0.0;
+    if (cand) {
+        const double* x = K.x + b * nf;
+        const double* dx = K.dx + b * nf;
+        double* xt = K.xt + b * nf;
+        for (int i = threadIdx.x; i < nf; i += kIB) xt[i] = x[i] + a * dx[i];
+        __syncthreads();
+        write_full(K, b, xt, K.vt);
+        pd = pd_error(K, b, x, K.y + b * K.m, 0.0, K.dy + b * K.m, K.zl + b * nf, K.zu + b * nf, 0.0, K.dzl + b * nf,
+                      K.dzu + b * nf, K.gF + b * nf, nullptr, K.jv + b * K.nj, K.gS + b * K.m, S.mu);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        if (over) {
+            S.soft_on = 0;
+            S.accepted = 0;  // to the restoration phase
+        }
+        S.soft_cnt = over ? 0 : cnt;
+        S.soft_try = cand;
+        S.soft_a = a;
+        S.soft_pd = pd;
+    }
+    store_scal(K, b, S);
+    if (threadIdx.x == 0) {
+        count_add(K, slot, 0, cand);
+        if (over) atomicAdd(K.cnt + 4 * slot + 1, 1);
+    }
+}
+
+// after eval_all at the soft trial points (gt, jact, ft, gradt): take the step when the original filter accepts it
+// (alpha 0: the sufficient-decrease test) or it cuts the primal-dual error by soft_resto_pderror_reduction_factor;
+// instances whose step the filter did not accept keep taking soft steps, rejected ones go to the restoration phase.
+// counters: [0] not accepted (as k_ipm_accept's: instances in the phase counted by their own line search)
+__global__ void __launch_bounds__(kIB) k_soft_accept(const IpmK K, int slot) {
+    __shared__ double sh[kIB / 64];
+    __shared__ Scal S;
+    const int64_t b = blockIdx.x;
+    const int nf = K.nf, m = K.m;
+    load_scal(K, b, S);
+    if (S.rs_on) {  // block-uniform
+        count_add(K, slot, 0, S.rs_exit == RS_RUNNING && !S.rs_acc);
+        return;
+    }
+    if (S.done || !S.soft_try) {  // block-uniform
+        count_add(K, slot, 0, !S.accepted);
+        return;
+    }
+    const double* sg = K.sg + b * m;
+    const double* gt = K.gt + b * m;
+    const double* xt = K.xt + b * nf;
+    double* gFt = K.sig + b * nf;  // scratch: Sigma is rebuilt by the next k_ipm_begin
+    for (int i = threadIdx.x; i < nf; i += kIB) gFt[i] = K.gradt[b * K.n + K.free[i]] * K.d[i] * S.sf;
+    double* gSt = K.csoc + b * m;  // scratch: set up again by the next line search
+    double tt = 0.0;
+    for (int j = threadIdx.x; j < m; j += kIB) {
+        gSt[j] = gt[j] * sg[j];
+        tt += fabs(gSt[j]);
+    }
+    tt = breduce(tt, OpSum(), sh);
+    const double a = S.soft_a;
+    const double pd = pd_error(K, b, xt, K.y + b * m, a, K.dy + b * m, K.zl + b * nf, K.zu + b * nf, a, K.dzl + b * nf,
+                               K.dzu + b * nf, gFt, K.jact + b * K.nnzj, nullptr, gSt, S.mu);
+    const double pt = barrier_obj(K, b, xt, K.ft[b] * S.sf, S.mu, sh);
+    bool ok, arm;
+    filter_accept(K, S, K.filt + b * kFilt * 2, tt, pt, 0.0, sh, ok, arm);
+    const bool acc = isfinite(pd) && (ok || pd <= K.o.soft_resto_pderror_reduction_factor * S.soft_pd);
+    if (acc) {
+        double* xacc = K.xacc + b * nf;
+        for (int i = threadIdx.x; i < nf; i += kIB) xacc[i] = xt[i];
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        S.accepted = acc;
+        S.armijo = 0;
+        S.forced = 0;
+        S.soft_ok = acc && ok;
+        S.soft_on = acc && !ok;
+        if (!S.soft_on) S.soft_cnt = 0;
+        if (acc) {
+            S.alpha = a;  // primal and dual steps of the same length (k_ipm_update)
+            S.a_z = a;
+            atomicAdd(K.rstat + 2, 1ull);
+        }
+    }
+    store_scal(K, b, S);
+    count_add(K, slot, 0, !S.accepted);
+}
+
 // least-squares multipliers (Ipopt's constr_mult_init), for the instances flagged reinit
 __global__ void __launch_bounds__(kIB) k_ipm_lsmult(const IpmK K) {
     __shared__ Scal S;
@@ -1200,7 +1345,8 @@ __global__ void __launch_bounds__(kIB) k_ipm_update(const IpmK K, int resto) {
     }
     const bool failed = !S.accepted && !S.done;
     const bool forced = S.forced;
-    const bool grow = !S.done && S.accepted && !S.armijo && !forced;
+    // a soft-restoration step augments the filter only when the original filter accepted it (as an h-type step)
+    const bool grow = !S.done && S.accepted && !S.armijo && !forced && (!S.soft_try || S.soft_ok);
     const bool reset = resto == 2 ? phase_end : (failed && resto && m > 0);
     // watchdog bookkeeping (solver.py): an acceptable point ends it; after watchdog_trial_iter_max unacceptable full
     // steps the iterate returns to where it started, and the next line search starts at half its step
@@ -1212,7 +1358,7 @@ __global__ void __launch_bounds__(kIB) k_ipm_update(const IpmK K, int resto) {
     // Ipopt's filter reset heuristic (FilterLSAcceptor::UpdateForNextIteration), before the augmentation
     int nsucc = S.nsucc;
     bool freset = false;
-    if (!S.done && S.accepted && !forced && S.nreset < K.o.max_filter_resets) {
+    if (!S.done && S.accepted && !forced && !S.soft_try && S.nreset < K.o.max_filter_resets) {
         if (S.rejf) {
             if (++nsucc >= K.o.filter_reset_trigger) {
                 freset = true;
@@ -1322,7 +1468,8 @@ __global__ void __launch_bounds__(kIB) k_ipm_update(const IpmK K, int resto) {
         S.nreset += freset;
         S.wd_trial = wd_trial;
         S.wd_on = S.wd_on && !wd_ok && !wd_back;
-        S.wd_short = (wd_ok || wd_back || failed || !shortened) ? 0 : S.wd_short + 1;
+        S.wd_short = (wd_ok || wd_back || failed || !shortened || S.soft_try) ? 0 : S.wd_short + 1;
+        S.soft_try = 0;
         S.skip_first = wd_back;
         if (wd_back) S.mu = S.wd_mu;
     }
@@ -2226,6 +2373,8 @@ extern "C" void cfx_ipm_default_options(cfx_ipm_options* o) {
     o->max_filter_resets = 0;  // Ipopt: 5; off here
     o->max_wall_time = 1e20;   // Ipopt max_wall_time
     o->print_frequency_time = 0.0;
+    o->soft_resto_pderror_reduction_factor = 0.0;  // Ipopt: 0.9999
+    o->max_soft_resto_iters = 10;
 }
 
 // CSR of `key` (values in [0, nkeys)) with the sources of each key in increasing source order
@@ -2327,7 +2476,8 @@ static int ipm_create_common(cfx_ipm* s, const cfx_sizes& sz, int layout, const 
         (K.o.restoration != CFX_RESTORATION_STEP && K.o.restoration != CFX_RESTORATION_PHASE) ||
         K.o.max_resto_iter < 0 || !(K.o.resto_penalty > 0) || !(K.o.required_infeasibility_reduction > 0) ||
         !(K.o.required_infeasibility_reduction < 1) || K.o.filter_reset_trigger < 1 || K.o.max_filter_resets < 0 ||
-        !(K.o.max_wall_time > 0) || !(K.o.print_frequency_time >= 0) || s->B > 0x7fffffff) {
+        !(K.o.max_wall_time > 0) || !(K.o.print_frequency_time >= 0) ||
+        !(K.o.soft_resto_pderror_reduction_factor >= 0) || K.o.max_soft_resto_iters < 0 || s->B > 0x7fffffff) {
         s->err = "cfx_ipm_create: the handle must use CFX_LAYOUT_AOS (or batch 1) and the options must be valid";
         return create_fail(s, CFX_EINVAL);
     }
@@ -2641,6 +2791,7 @@ static int ipm_create_common(cfx_ipm* s, const cfx_sizes& sz, int layout, const 
     csr(std::vector<int64_t>(jrF.begin(), jrF.end()), m, jrwptr, jrwidx);
 
     K.nf = nf;
+    K.npd = nf + m + (int)std::count(hasL.begin(), hasL.end(), 1) + (int)std::count(hasU.begin(), hasU.end(), 1);
     K.nj = nj;
     K.nh = nh;
     K.nK = nK;
@@ -2733,8 +2884,12 @@ static int ipm_create_common(cfx_ipm* s, const cfx_sizes& sz, int layout, const 
         K.rzl = dalloc<double>(s, B * nf, &rc);
         K.rzu = dalloc<double>(s, B * nf, &rc);
         K.rfilt = dalloc<double>(s, B * kFilt * 2, &rc);
+        if (K.o.soft_resto_pderror_reduction_factor > 0) {
+            K.jact = dalloc<double>(s, B * K.nnzj, &rc);
+            K.gradt = dalloc<double>(s, B * n, &rc);
+        }
     }
-    K.rstat = dalloc<unsigned long long>(s, 2, &rc);
+    K.rstat = dalloc<unsigned long long>(s, 3, &rc);
     K.cnt = dalloc<int32_t>(s, 4 * kSlots, &rc);
     s->d_fv = dalloc<double>(s, B * K.nfix, &rc);
     s->d_yo = dalloc<double>(s, B * m, &rc);
@@ -2899,8 +3054,8 @@ static int ipm_solve(cfx_ipm* s, const double* v0, const double* fixed_values, d
     Run R{s, st, dim3((unsigned)B)};
     const dim3 blk(kIB);
     s->st.eval_all = s->st.eval_g_f = s->st.eval_h = s->st.kkt_factor = s->st.iterations = s->st.host_syncs = 0;
-    s->st.resto_phases = s->st.resto_iterations = 0;
-    IPM_HIP(s, hipMemsetAsync(K.rstat, 0, 2 * sizeof(unsigned long long), st));
+    s->st.resto_phases = s->st.resto_iterations = s->st.soft_steps = 0;
+    IPM_HIP(s, hipMemsetAsync(K.rstat, 0, 3 * sizeof(unsigned long long), st));
     if (K.rsphase)  // the (2,2) block of instances outside the phase
         IPM_HIP(s, hipMemsetAsync(K.rdc, 0, B * K.m * sizeof(double), st));
     s->slot = 0;
@@ -2993,7 +3148,7 @@ static int ipm_solve(cfx_ipm* s, const double* v0, const double* fixed_values, d
         hipLaunchKernelGGL(k_ipm_dir, R.g, blk, 0, st, K, it);
         if (K.rsphase && rs_live) hipLaunchKernelGGL(k_rs_dir, R.g, blk, 0, st, K);
         // filter line search with second-order corrections (the phase's own filter line search alongside)
-        int notacc = 0;
+        int notacc = 0, n_soft = 0;
         for (int ls = 0; ls < K.o.max_backtrack; ++ls) {
             IPM_RUN(R.eval_gf(true));
             int sl = R.next_slot();
@@ -3002,6 +3157,7 @@ static int ipm_solve(cfx_ipm* s, const double* v0, const double* fixed_values, d
             IPM_HIP(s, hipGetLastError());
             IPM_RUN(R.read(sl, c));
             notacc = c[0];
+            if (ls == 0) n_soft = c[2];
             if (ls == 0)
                 for (int q = 0; q < K.o.max_soc && c[1] > 0; ++q) {
                     hipLaunchKernelGGL(k_ipm_soc_rhs, R.g, blk, 0, st, K);
@@ -3018,6 +3174,24 @@ static int ipm_solve(cfx_ipm* s, const double* v0, const double* fixed_values, d
             if (notacc == 0) break;
             hipLaunchKernelGGL(k_ipm_next_trial, R.g, blk, 0, st, K);
             if (K.rsphase && rs_live) hipLaunchKernelGGL(k_rs_next_trial, R.g, blk, 0, st, K);
+        }
+        // Ipopt's soft restoration: the failed searches and the instances taking soft steps try the step at the
+        // fraction to the boundary (k_soft_trial counts them; one eval_all at their trial points; k_soft_accept)
+        if (K.jact && (notacc > 0 || n_soft > 0)) {
+            int sl = R.next_slot();
+            hipLaunchKernelGGL(k_soft_trial, R.g, blk, 0, st, K, sl);
+            IPM_HIP(s, hipGetLastError());
+            IPM_RUN(R.read(sl, c));
+            notacc += c[1];  // soft steps exhausted: failed searches from here on
+            if (c[0] > 0) {
+                IPM_RUN(ipm_eval_all(s, K.vt, K.gt, K.jact, K.ft, K.gradt, CFX_DEVICE));
+                s->st.eval_all++;
+                sl = R.next_slot();
+                hipLaunchKernelGGL(k_soft_accept, R.g, blk, 0, st, K, sl);
+                IPM_HIP(s, hipGetLastError());
+                IPM_RUN(R.read(sl, c));
+                notacc = c[0];
+            }
         }
         // failed line searches: the restoration phase (its iterations for the instances in it; the instances whose
         // search failed enter it), or a feasibility-restoration step, a fresh filter and least-squares multipliers
@@ -3053,12 +3227,13 @@ static int ipm_solve(cfx_ipm* s, const double* v0, const double* fixed_values, d
                        devp ? conv_out : (conv_out ? s->d_conv : nullptr), devp ? its_out : (its_out ? s->d_its : nullptr),
                        devp ? kkt_out : (kkt_out ? s->d_kkt : nullptr), s->d_status, (int)wall_stop);
     IPM_HIP(s, hipGetLastError());
-    unsigned long long rstat[2] = {0, 0};
+    unsigned long long rstat[3] = {0, 0, 0};
     IPM_HIP(s, hipMemcpyAsync(rstat, K.rstat, sizeof(rstat), hipMemcpyDeviceToHost, st));
     IPM_HIP(s, hipMemcpyAsync(s->h_status.data(), s->d_status, B * sizeof(int32_t), hipMemcpyDeviceToHost, st));
     IPM_HIP(s, hipStreamSynchronize(st));
     s->st.resto_phases = (int64_t)rstat[0];
     s->st.resto_iterations = (int64_t)rstat[1];
+    s->st.soft_steps = (int64_t)rstat[2];
     if (v_out) IPM_HIP(s, hipMemcpyAsync(v_out, K.vx, B * K.n * sizeof(double), kout, st));
     if (f_out) IPM_HIP(s, hipMemcpyAsync(f_out, K.fraw, B * sizeof(double), kout, st));
     if (!devp) {

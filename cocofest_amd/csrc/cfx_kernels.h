@@ -451,6 +451,20 @@ CFX_HD void st_lane(double* p, const double (&v)[NI]) {
 #endif
     }
 }
+// st_lane with a store policy: PLAIN = ordinary (write-back) 16-byte stores, for the collocation store-policy probe
+template <int NI, bool PLAIN>
+CFX_HD void st_lane_p(double* p, const double (&v)[NI]) {
+    if constexpr (PLAIN) {
+        if constexpr (NI == 1) {
+            *p = v[0];
+        } else {
+#pragma unroll
+            for (int i = 0; i < NI; i += 2) *reinterpret_cast<double2*>(p + i) = make_double2(v[i], v[i + 1]);
+        }
+    } else {
+        st_lane<NI>(p, v);
+    }
+}
 template <int NI>
 CFX_HD void st_lane_const(double* p, double c) {
     double v[NI];

@@ -69,6 +69,14 @@ class IpmOptions:
     # and cfg 5's multistart)
     filter_reset_trigger: int = 5
     max_filter_resets: int = 0
+    # Ipopt's soft restoration (IpBacktrackingLineSearch::TrySoftRestoStep): a failed line search first tries the step
+    # at the smaller of the primal and dual fractions to the boundary, primal and dual together, accepted when the
+    # original filter takes it (at alpha 0: the sufficient-decrease test) or when it cuts the primal-dual system error
+    # (mean of |grad L|, |c| and |s z - mu|) by this factor (Ipopt's default 0.9999; 0: off).  An accepted step the
+    # filter did not take keeps the instance on such steps — no line search — for up to max_soft_resto_iters
+    # iterations, until one satisfies the filter; a rejected one starts the restoration phase.  Phase mode only
+    soft_resto_pderror_reduction_factor: float = 0.0
+    max_soft_resto_iters: int = 10
     # Ipopt's max_wall_time (s): the instances still iterating stop there (status -5); print_frequency_time (s, 0:
     # off): the native solver prints a progress line (iteration, instances iterating, in restoration) this often
     max_wall_time: float = 1e20
@@ -80,6 +88,8 @@ class IpmOptions:
             raise ValueError("filter_reset_trigger must be >= 1 and max_filter_resets >= 0")
         if not self.max_wall_time > 0 or not self.print_frequency_time >= 0:
             raise ValueError("max_wall_time must be > 0 and print_frequency_time >= 0")
+        if not self.soft_resto_pderror_reduction_factor >= 0 or self.max_soft_resto_iters < 0:
+            raise ValueError("soft_resto_pderror_reduction_factor must be >= 0 and max_soft_resto_iters >= 0")
 
 
 class Solver:
@@ -99,7 +109,9 @@ class Solver:
                     "_resto_penalty_parameter": "resto_penalty",
                     "_required_infeasibility_reduction": "required_infeasibility_reduction",
                     "_filter_reset_trigger": "filter_reset_trigger", "_max_filter_resets": "max_filter_resets",
-                    "_max_wall_time": "max_wall_time", "_print_frequency_time": "print_frequency_time"}
+                    "_max_wall_time": "max_wall_time", "_print_frequency_time": "print_frequency_time",
+                    "_soft_resto_pderror_reduction_factor": "soft_resto_pderror_reduction_factor",
+                    "_max_soft_resto_iters": "max_soft_resto_iters"}
         _IGNORED = {"show_online_optim", "show_options", "_print_level", "_linear_solver", "_nlp_scaling_method",
                     "_check_derivatives_for_naninf", "_c_compile", "_print_timing_statistics", "_output_file",
                     "_constr_viol_tol", "_dual_inf_tol", "_compl_inf_tol"}
@@ -466,6 +478,11 @@ class BatchedIpm:
         # Ipopt's filter reset heuristic: successive iterations whose last rejection was the filter's, resets done
         f_succ = torch.zeros((B,), dtype=torch.int64, device=self.dev)
         f_resets = torch.zeros((B,), dtype=torch.int64, device=self.dev)
+        # soft restoration: instances taking soft steps, and how many they have taken
+        soft_on = torch.zeros((B,), dtype=torch.bool, device=self.dev)
+        soft_cnt = torch.zeros((B,), dtype=torch.int64, device=self.dev)
+        soft_fac = opt.soft_resto_pderror_reduction_factor if (m and self._phase) else 0.0
+        self.soft_steps = 0  # soft-restoration steps taken (all instances)
 
         self._v_template = v
 
@@ -577,7 +594,7 @@ class BatchedIpm:
             else:
                 r_theta, r_phi, r_dphi = theta, phi, dphi
             alpha = torch.where(skip_first, 0.5 * a_p, a_p)
-            accepted = done.clone()
+            accepted = done | soft_on  # instances taking soft steps skip the line search (TrySoftRestoStep below)
             forced = torch.zeros_like(done)
             armijo_step = torch.zeros_like(done)
             rej_f = torch.zeros_like(done)  # Ipopt's InitThisLineSearch
@@ -638,7 +655,7 @@ class BatchedIpm:
             wd_short = torch.where(wd_ok | wd_back | failed | ~shortened, torch.zeros_like(wd_short), wd_short + 1)
             skip_first = wd_back.clone()
             # Ipopt's filter reset heuristic (FilterLSAcceptor::UpdateForNextIteration), before the augmentation
-            upd = (~done) & accepted & ~forced & (f_resets < opt.max_filter_resets)
+            upd = (~done) & accepted & ~forced & ~soft_on & (f_resets < opt.max_filter_resets)
             f_succ = torch.where(upd, torch.where(rej_f, f_succ + 1, torch.zeros_like(f_succ)), f_succ)
             f_reset = upd & rej_f & (f_succ >= opt.filter_reset_trigger)
             f_succ = torch.where(f_reset, torch.zeros_like(f_succ), f_succ)
@@ -647,15 +664,39 @@ class BatchedIpm:
             filt = torch.where(f_reset[:, None, None], torch.tensor([np.inf, -np.inf], dtype=torch.float64,
                                                                     device=self.dev), filt)
             # filter augmentation for h-type (non-Armijo) steps
-            grow = (~done) & accepted & ~armijo_step & ~forced
-            filt = torch.where(grow[:, None, None] & (torch.arange(filt.shape[1], device=self.dev) ==
-                                                      (fpos % filt.shape[1])[:, None])[:, :, None],
-                               torch.stack([(1 - 1e-5) * theta, phi - 1e-5 * theta], dim=1)[:, None, :], filt)
-            fpos = fpos + grow.long()
+            grow = (~done) & accepted & ~armijo_step & ~forced & ~soft_on
+            filt, fpos = self._augment_filter(filt, fpos, grow, theta, phi)
             # a failed search: a feasibility-restoration step (minimum-norm Newton step on g = 0 in the metric
             # Sigma + I, backtracking on ||g||_1 only), then a fresh filter and least-squares multipliers
             x_new = x_acc
             failed = failed & ~done
+            soft_acc = torch.zeros_like(done)
+            if soft_fac > 0:
+                # Ipopt's soft restoration, for the failed searches and the instances already taking soft steps
+                was_soft = soft_on & ~done
+                soft_cnt = torch.where(was_soft, soft_cnt + 1, soft_cnt)
+                over = was_soft & (soft_cnt > opt.max_soft_resto_iters)
+                cand = (failed & ~wd_on) | (was_soft & ~over)
+                failed = failed | over
+                if bool(cand.any()):
+                    a_s = torch.minimum(a_p, a_z)
+                    xs = x + a_s[:, None] * dx
+                    ys, zls, zus = y + a_s[:, None] * dy, zl + a_s[:, None] * dzl, zu + a_s[:, None] * dzu
+                    gs, jvs, fs, gFs = self._scaled_all(full(xs))
+                    ok_orig, _ = self._filter_accept(gs, fs, xs, theta, phi, dphi, torch.zeros_like(alpha), mu,
+                                                     theta_max, theta_min, filt)
+                    pd_c = self._pd_error(gF, jv, y, zl, zu, g, x, mu)
+                    pd_t = self._pd_error(gFs, jvs, ys, zls, zus, gs, xs, mu)
+                    soft_acc = cand & torch.isfinite(pd_t) & (ok_orig | (pd_t <= soft_fac * pd_c))
+                    self.soft_steps += int(soft_acc.sum())
+                    failed = (failed | cand) & ~soft_acc
+                    x_new = torch.where(soft_acc[:, None], xs, x_new)
+                    # a step the filter takes ends the soft steps (and augments it, as an h-type step would)
+                    filt, fpos = self._augment_filter(filt, fpos, soft_acc & ok_orig, theta, phi)
+                    soft_on = torch.where(cand, soft_acc & ~ok_orig, soft_on)
+                    wd_short = torch.where(cand, torch.zeros_like(wd_short), wd_short)
+                soft_on = soft_on & ~over
+                soft_cnt = torch.where(soft_on, soft_cnt, torch.zeros_like(soft_cnt))
             if self._phase:
                 # Ipopt: "Restoration phase called at acceptable point" ends the solve, solved to the acceptable level
                 at_acc = failed & (err0 <= opt.acceptable_tol)
@@ -691,9 +732,10 @@ class BatchedIpm:
                                                                        device=self.dev), filt)
                 reinit_y = reinit_y | failed
                 alpha = torch.where(failed, torch.zeros_like(alpha), alpha)  # y and z stay put this iteration
-            alpha_eff = torch.where(failed, alpha, torch.where(accepted, alpha, alpha))
+            if soft_fac > 0 and bool(soft_acc.any()):
+                alpha = torch.where(soft_acc, a_s, alpha)  # the soft step moves y (and z, below) by the same step
             step = (~done)
-            alpha = torch.where(step, alpha_eff, torch.zeros_like(alpha_eff))
+            alpha = torch.where(step, alpha, torch.zeros_like(alpha))
             if opt.verbose:
                 print(f"it {it:3d} f {float(f[0]):.6e} err {float(err0[0]):.3e} e_d {float(e_d[0]):.2e} "
                       f"e_p {float(e_p[0]):.2e} mu {float(mu[0]):.1e} alpha {float(alpha[0]):.2e} "
@@ -703,7 +745,7 @@ class BatchedIpm:
             # updates only where a step is taken and finite (0 * NaN would poison a finished instance for good)
             mv = (alpha > 0) & torch.isfinite(dy).all(1)
             y = torch.where(mv[:, None], y + alpha[:, None] * dy, y)
-            az = torch.where(step & ~failed, a_z, torch.zeros_like(a_z))
+            az = torch.where(step & ~failed, torch.where(soft_acc, alpha, a_z), torch.zeros_like(a_z))
             mz = (az > 0) & torch.isfinite(dzl).all(1) & torch.isfinite(dzu).all(1)
             zl = torch.where(mz[:, None], zl + az[:, None] * dzl, zl)
             zu = torch.where(mz[:, None], zu + az[:, None] * dzu, zu)
@@ -730,6 +772,27 @@ class BatchedIpm:
                          iterations=iters.cpu().numpy(), kkt_error=err0.cpu().numpy(),
                          wall_time=time.perf_counter() - t0, n_callbacks=dict(self.calls),
                          status=status.cpu().numpy())
+
+    def _augment_filter(self, filt, fpos, grow, theta, phi):
+        """Add (theta, phi) of the instances ``grow`` to their filter (a ring of filt.shape[1] pairs)."""
+        torch = self.torch
+        slot = torch.arange(filt.shape[1], device=self.dev) == (fpos % filt.shape[1])[:, None]
+        filt = torch.where(grow[:, None, None] & slot[:, :, None],
+                           torch.stack([(1 - 1e-5) * theta, phi - 1e-5 * theta], dim=1)[:, None, :], filt)
+        return filt, fpos + grow.long()
+
+    def _pd_error(self, gF, jv, y, zl, zu, g, x, mu):
+        """Ipopt's primal-dual system error (IpoptCalculatedQuantities::curr_primal_dual_system_error) of the scaled
+        problem: (||grad L||_1 + ||c||_1 + sum |s z - mu|) over the number of those terms."""
+        torch = self.torch
+        hasL, hasU = self.hasL, self.hasU
+        sl = torch.where(hasL, x - self._lbI, torch.ones_like(x))
+        su = torch.where(hasU, self._ubI - x, torch.ones_like(x))
+        rd = gF + self._jt_mul(jv, y) - zl + zu
+        cl = torch.where(hasL, (sl * zl - mu[:, None]).abs(), torch.zeros_like(x))
+        cu = torch.where(hasU, (su * zu - mu[:, None]).abs(), torch.zeros_like(x))
+        n = x.shape[1] + self.m + int(hasL.sum()) + int(hasU.sum())
+        return (rd.abs().sum(1) + g.abs().sum(1) + cl.sum(1) + cu.sum(1)) / n
 
     def _full(self, xf):
         vv = self._v_template.clone()
@@ -1090,7 +1153,7 @@ _NATIVE_OPTIONS = ("tol", "max_iter", "acceptable_tol", "acceptable_iter", "mu_i
                    "delta_c", "curv_min", "max_soc", "kappa_soc", "watchdog_shortened_iter_trigger",
                    "watchdog_trial_iter_max", "limited_memory_max_history", "max_resto_iter", "resto_penalty",
                    "required_infeasibility_reduction", "filter_reset_trigger", "max_filter_resets", "max_wall_time",
-                   "print_frequency_time")
+                   "print_frequency_time", "soft_resto_pderror_reduction_factor", "max_soft_resto_iters")
 _HESSIAN_APPROXIMATION = {"exact": 0, "limited-memory": 1}
 _RESTORATION = {"step": 0, "phase": 1, None: 1}
 

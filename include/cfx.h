@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define CFX_ABI_VERSION 6
+#define CFX_ABI_VERSION 7
 
 /* return codes */
 #define CFX_OK 0
@@ -373,6 +373,16 @@ typedef struct cfx_ipm_options {
     /* Ipopt's print_frequency_time (seconds, default 0: off): one progress line on stderr at most this often —
        host iteration, elapsed time, instances still iterating, of them in the restoration phase */
     double print_frequency_time;
+    /* Ipopt's soft restoration (IpBacktrackingLineSearch::TrySoftRestoStep; restoration phase only): a failed line
+       search first tries the step at the smaller of the primal and dual fractions to the boundary, primal and dual
+       together; it is taken when the original filter accepts it (sufficient-decrease test) or when it cuts the
+       primal-dual system error (mean of |grad L|, |c| and |s z - mu| over the scaled problem) by
+       soft_resto_pderror_reduction_factor (Ipopt's default 0.9999; default here 0: off).  A step the filter did not
+       accept keeps the instance on such steps, without line search, for up to max_soft_resto_iters (10) iterations
+       until one is accepted by the filter; a rejected one starts the restoration phase.  Each try costs one eval_all
+       at the trial point. */
+    double soft_resto_pderror_reduction_factor; /* >= 0 */
+    int32_t max_soft_resto_iters;               /* >= 0 */
 } cfx_ipm_options;
 #define CFX_HESSIAN_EXACT 0
 #define CFX_HESSIAN_LIMITED_MEMORY 1
@@ -395,6 +405,7 @@ typedef struct cfx_ipm_stats {
     int64_t kkt_n, kkt_kl, kkt_ku, kkt_band_n, kkt_border;
     int64_t kkt_blocks; /* band blocks factored side by side (nested dissection of the stage chain; 1: none) */
     int64_t resto_phases, resto_iterations; /* restoration phases entered / their iterations, summed over the instances */
+    int64_t soft_steps;                     /* soft-restoration steps taken, summed over the instances */
 } cfx_ipm_stats;
 
 typedef struct cfx_ipm cfx_ipm;

@@ -2,11 +2,13 @@
 tiles) at the launch shapes in --shapes (CFX_KPT:CFX_NI:CFX_IFAST triples, '-' = the handle's default) and layouts;
 each shape runs in a child process (cfx_create reads the overrides), alternating --rounds times.  One JSON line per run.
 
-Usage: python scripts/colloc_probe.py [--shapes -:-:-,1:1:0,...] [--layouts tiled64,soa] [--rounds 2] [--steps 200]
+Usage (lists separated by ',' or '+'): python scripts/colloc_probe.py [--shapes -:-:-,1:1:0,...] [--layouts tiled64,soa] [--stores nt,plain]
+                                      [--rounds 2] [--steps 200]
 With --pmc-only: the default shape once, 20 launches (the process rocprofv3 --pmc wraps)."""
 import argparse
 import json
 import os
+import re
 import subprocess
 import sys
 
@@ -16,6 +18,7 @@ sys.path.insert(0, ROOT)
 ap = argparse.ArgumentParser()
 ap.add_argument("--shapes", default="-:-:-")
 ap.add_argument("--layouts", default="tiled64")
+ap.add_argument("--stores", default="nt", help="output store policies: nt (default) and/or plain (CFX_COLLOC_STORE)")
 ap.add_argument("--rounds", type=int, default=1)
 ap.add_argument("--steps", type=int, default=200)
 ap.add_argument("--child", default=None)
@@ -63,17 +66,20 @@ if args.pmc_only:
     print(json.dumps(child("tiled64", 20)), flush=True)
     sys.exit(0)
 for rnd in range(args.rounds):
-    for shape in args.shapes.split(","):
+    for shape in re.split(r"[,+]", args.shapes):
         kpt, ni, ifast = shape.split(":")
         env = dict(os.environ)
         for k, val in (("CFX_KPT", kpt), ("CFX_NI", ni), ("CFX_IFAST", ifast)):
             env.pop(k, None)
             if val != "-":
                 env[k] = val
-        for layout in args.layouts.split(","):
+        for layout, store in [(la, st) for la in re.split(r"[,+]", args.layouts) for st in re.split(r"[,+]", args.stores)]:
+            env.pop("CFX_COLLOC_STORE", None)
+            if store != "nt":
+                env["CFX_COLLOC_STORE"] = store
             r = subprocess.run([sys.executable, __file__, "--child", layout, "--steps", str(args.steps)], env=env,
                                capture_output=True, text=True, timeout=300)
             line = r.stdout.strip().splitlines()[-1] if r.stdout.strip() else json.dumps({"error": r.stderr[-400:]})
             rec = json.loads(line)
-            rec.update(round=rnd, request=shape)
+            rec.update(round=rnd, request=shape, store=store)
             print(json.dumps(rec), flush=True)

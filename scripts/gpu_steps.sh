@@ -10,6 +10,7 @@
 #   bench20          python bench.py --steps 20 --warmup 5 -> bench_k20.json
 #   prof             rocprofv3 --kernel-trace --stats of bench.py --steps 20
 #   multistart:RUNS  scripts/msk_multistart_probe.py --native --runs RUNS (e.g. 64:0.1,512:0.1)
+#   specms:RUNS:SOFT the same with the BatchedIpm specification and soft_resto_pderror_reduction_factor SOFT
 #   py:SCRIPT[:ARGS] python SCRIPT ARGS (ARGS with commas for spaces), stdout to SCRIPT's name .txt
 set -o pipefail
 out=gpurun_out/$1
@@ -40,6 +41,9 @@ for step in "$@"; do
         prof) run 900 prof.log rocprofv3 --kernel-trace --stats -d "$out/prof" -o run -- python3 bench.py --steps 20 ;;
         multistart:*) run 1100 "multistart_${step#multistart:}.log" python3 -u scripts/msk_multistart_probe.py --native \
                           --runs "${step#multistart:}" --jsonl "$out/multistart.jsonl" ;;
+        specms:*) r=${step#specms:}
+                  run 1100 "specms_${r}.log" python3 -u scripts/msk_multistart_probe.py --runs "${r%:*}" \
+                      --soft "${r##*:}" --jsonl "$out/specms.jsonl" ;;
         py:*) spec=${step#py:}
               script=${spec%%:*}
               args=""

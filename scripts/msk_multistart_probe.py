@@ -2,13 +2,14 @@
 65,536 (RK4 x 1).
 
 Usage: python scripts/msk_multistart_probe.py [--native] [--hess-only] [--runs B:amp,B:amp,...] [--max-iter N]
-                                              [--wall SECONDS] [--jsonl FILE]
+                                              [--wall SECONDS] [--soft FACTOR] [--jsonl FILE]
 Each run prints one line (converged count, Ipopt status histogram, restoration phases / iterations, wall time); the
 native solver prints a progress line on stderr every 20 s (print_frequency_time)."""
 import argparse
 import collections
 import json
 import pathlib
+import re
 import sys
 import time
 
@@ -29,10 +30,11 @@ ap.add_argument("--runs", default="64:0.1,64:0.3,512:0.1")
 ap.add_argument("--max-iter", type=int, default=1000)
 ap.add_argument("--wall", type=float, default=1e20)
 ap.add_argument("--jsonl", default=None)
+ap.add_argument("--soft", type=float, default=None, help="soft_resto_pderror_reduction_factor (default: the option's)")
 args = ap.parse_args()
 
 ocp = bench.msk_build(5)
-runs = [] if args.hess_only else [(int(r.split(":")[0]), float(r.split(":")[1])) for r in args.runs.split(",")]
+runs = [] if args.hess_only else [(int(r.split(":")[0]), float(r.split(":")[1])) for r in re.split(r"[,+]", args.runs)]
 for B, amp in runs:
     rng = np.random.default_rng(0)
     v0 = np.tile(ocp.initial_guess_vector(), (B, 1))
@@ -41,8 +43,9 @@ for B, amp in runs:
     span = np.minimum(np.where(np.isfinite(ub - lb), ub - lb, 10.0), 10.0)[free]
     v0[:, free] = np.clip(v0[:, free] + amp * rng.uniform(-1, 1, (B, free.sum())) * span, lb[free], ub[free])
     cls = NativeIpm if args.native else BatchedIpm
-    ipm = cls(ocp, batch=B, options=IpmOptions(tol=1e-6, max_iter=args.max_iter, max_wall_time=args.wall,
-                                               print_frequency_time=20.0))
+    extra = {} if args.soft is None else {"soft_resto_pderror_reduction_factor": args.soft}
+    opts = IpmOptions(tol=1e-6, max_iter=args.max_iter, max_wall_time=args.wall, print_frequency_time=20.0, **extra)
+    ipm = cls(ocp, batch=B, options=opts)
     res = ipm.solve(v0)
     st = dict(getattr(ipm, "last_stats", {}) or {})
     ipm.close()
@@ -53,7 +56,8 @@ for B, amp in runs:
                iterations_max=int(res.iterations.max()), f_converged_min=float(res.f[conv].min()) if conv.any() else None,
                f_converged_max=float(res.f[conv].max()) if conv.any() else None,
                resto_phases=st.get("resto_phases"), resto_iterations=st.get("resto_iterations"),
-               host_iterations=st.get("iterations"))
+               host_iterations=st.get("iterations"), soft=opts.soft_resto_pderror_reduction_factor,
+               soft_steps=getattr(ipm, "soft_steps", st.get("soft_steps")))
     print(json.dumps(rec), flush=True)
     if args.jsonl:
         with open(args.jsonl, "a") as fh:

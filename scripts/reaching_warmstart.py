@@ -1,0 +1,109 @@
+"""Warm-started native solve of the reference's reaching task from its stored optimum.
+
+The product's OcpFesMsk for examples/dynamics/reaching_task/reaching_task_pulse_duration_optimization.py:80-118 (six
+Ding2007-with-fatigue muscles at the stored revision's fatigue rates, 60 pulses at 40 Hz, N = 1,500, RK4 x 1, the hand on
+the target at node 1000, no residual torque) is solved by cfx_ipm starting at the stored states and pulse widths
+(tests/golden/reaching_pulse_duration_*.npz).  The stored point solves the stored revision's NLP (tests/
+test_reference_solution.py); the product states today's reference, whose calcium sum keeps every pulse of the window
+(the stored Cn rows miss by 8.6e-3 after the second pulse under it) and whose pulse width is a control per interval,
+not a parameter per pulse.  So the solve must move; this script measures how far: start and end objective, the
+largest constraint row at the start, the change of every state and pulse width relative to its range, and how many
+pulse widths sit on a bound.  One JSON line per objective.
+
+Usage (GPU): python scripts/reaching_warmstart.py [--objectives fatigue,force] [--max-iter 3000] [--wall 400]"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from tests import test_reference_solution as R  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--objectives", default="fatigue,force")
+ap.add_argument("--max-iter", type=int, default=3000)
+ap.add_argument("--wall", type=float, default=400.0)
+ap.add_argument("--out", default=None, help="append the JSON lines to this file")
+args = ap.parse_args()
+
+
+def build(objective):
+    import cocofest_amd as C
+    from oracle import fes_oracle as O
+
+    models = []
+    for n, c in zip(R.MUSCLES, R.muscle_constants(legacy_rates=True)):
+        mm = C.DingModelPulseWidthFrequencyWithFatigue(muscle_name=n, sum_stim_truncation=R.T)
+        for k in ("alpha_a", "alpha_tau1", "alpha_km", "a_scale"):
+            setattr(mm, k, c[k])
+        models.append(mm)
+    model = C.FesMskModel(biorbd_path=str(R.GOLDEN / "biomod_arm26.json"), muscles_model=models, stim_time=R.STIMS,
+                          activate_force_length_relationship=True, activate_force_velocity_relationship=True,
+                          activate_residual_torque=False)
+    cl = C.ConstraintList()
+    cl.add(C.ConstraintFcn.SUPERIMPOSE_MARKERS, first_marker="COM_hand", second_marker="reaching_target", phase=0,
+           node=R.MARKER_NODE, axes=[C.Axis.X, C.Axis.Y])
+    return C.OcpFesMsk.prepare_ocp(model=model, final_time=R.FINAL_TIME, n_shooting=R.N,
+                                   pulse_width={"min": O.model_constants("ding2007")["pd0"], "max": 0.0006},
+                                   objective={f"minimize_muscle_{objective}": True},
+                                   msk_info={"with_residual_torque": False, "bound_type": "start_end",
+                                             "bound_data": [[0, 5], [0, 5]], "custom_constraint": cl},
+                                   ode_solver=C.OdeSolver.RK4(n_integration_steps=1),
+                                   apply_custom_constraint=True)
+
+
+def run(objective):
+    from cocofest_amd.solver import IpmOptions, NativeIpm
+
+    ocp = build(objective)
+    X, U = R.trajectory(R.load(objective))
+    nm = len(R.MUSCLES)
+    nx, nz = ocp.nx, ocp.nx + ocp.nu
+    assert ocp.nu == nm, ocp.nu
+    v0 = R.decision_vector(X, U[:nm], nz)
+    lb, ub = ocp.bounds_vector()
+    v0 = np.clip(v0, lb, ub)  # the stored widths sit 1e-8 outside (Ipopt's bound_relax_factor)
+    h = ocp.nlp(batch=1, layout="aos")
+    g0 = h.eval_g(v0[None])[0]
+    f0 = float(h.eval_f(v0[None])[0])
+    h.close()
+    t0 = time.perf_counter()
+    ipm = NativeIpm(ocp, batch=1, options=IpmOptions(tol=1e-6, max_iter=args.max_iter, max_wall_time=args.wall,
+                                                      print_frequency_time=30.0))
+    res = ipm.solve(v0[None])
+    st = dict(ipm.last_stats)
+    ipm.close()
+    wall = time.perf_counter() - t0
+    v = res.v[0]
+    span = np.where(np.isfinite(ub - lb) & (ub > lb), ub - lb, np.maximum(1.0, np.abs(v0)))
+    body0, body = v0[: R.N * nz].reshape(R.N, nz), v[: R.N * nz].reshape(R.N, nz)
+    dstate = np.abs(body[:, :nx] - body0[:, :nx]) / span[: R.N * nz].reshape(R.N, nz)[:, :nx]
+    pw0, pw = body0[:, nx:], body[:, nx:]
+    pwlo, pwhi = lb[nx], ub[nx]
+    pidx = R.pulse_index()
+    spread = max(float(np.ptp(pw[pidx == i], axis=0).max()) for i in range(int(pidx.max()) + 1))
+    out = {"objective": objective, "status": int(res.status[0]), "converged": bool(res.converged[0]),
+           "iterations": int(res.iterations[0]), "wall_s": wall, "kkt_error": float(res.kkt_error[0]),
+           "f_start": f0, "f_end": float(res.f[0]), "g_start_max": float(np.abs(g0).max()),
+           "g_start_rows_over_1e-6": int((np.abs(g0) > 1e-6).sum()),
+           "dstate_rel_max": float(dstate.max()), "dstate_rel_median": float(np.median(dstate)),
+           "dpw_rel_max": float(np.abs(pw - pw0).max() / (pwhi - pwlo)),
+           "dpw_rel_median": float(np.median(np.abs(pw - pw0)) / (pwhi - pwlo)),
+           "pw_at_bounds_start": int(((pw0 <= pwlo + 1e-9) | (pw0 >= pwhi - 1e-9)).sum()),
+           "pw_at_bounds_end": int(((pw <= pwlo + 1e-9) | (pw >= pwhi - 1e-9)).sum()), "pw_total": int(pw.size),
+           "pw_spread_within_pulse_max_rel": spread / (pwhi - pwlo),
+           "resto_phases": int(st.get("resto_phases", 0)), "kkt_layout": st.get("layout")}
+    line = json.dumps(out)
+    print(line, flush=True)
+    if args.out:
+        with open(args.out, "a") as fh:
+            fh.write(line + "\n")
+
+
+for obj in args.objectives.split(","):
+    run(obj)

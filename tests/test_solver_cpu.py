@@ -223,3 +223,37 @@ def test_filter_reset_heuristic():
     assert int(off.filter_resets[0]) == 0  # the default: off
     o = Solver.IPOPT(_filter_reset_trigger=2, _max_filter_resets=5).apply(IpmOptions())
     assert (o.filter_reset_trigger, o.max_filter_resets) == (2, 5)
+
+
+def test_soft_restoration_steps():
+    """Ipopt's soft restoration (IpmOptions.soft_resto_pderror_reduction_factor, Ipopt's TrySoftRestoStep) on cfg 2 from
+    the zero guess and 7 starts perturbed by 30 % of each range: failed line searches take soft steps (primal and dual
+    at the fraction to the boundary, accepted by the filter or by a primal-dual error decrease), and every start still
+    reaches the forward integration, as without them."""
+    cfg = cases.cfg2()
+    out = {}
+    for fac in (0.0, 0.9999):
+        ocp, pb, ipm = _ipm(cfg, batch=8, soft_resto_pderror_reduction_factor=fac, max_iter=300)
+        rng = np.random.default_rng(1)
+        v0 = np.tile(ocp.initial_guess_vector(), (8, 1))
+        lb, ub = ocp.bounds_vector()
+        free = lb != ub
+        span = np.minimum(np.where(np.isfinite(ub - lb), ub - lb, 10.0), 10.0)[free]
+        v0[1:, free] = np.clip(v0[1:, free] + 0.3 * rng.uniform(-1, 1, (7, free.sum())) * span, lb[free], ub[free])
+        out[fac] = (ipm.solve(v0), ipm.soft_steps)
+    (r0, n0), (r1, n1) = out[0.0], out[0.9999]
+    assert n0 == 0 and n1 > 0, (n0, n1)
+    assert r0.converged.all() and r1.converged.all()
+    np.testing.assert_allclose(r1.f, r0.f, rtol=1e-8)
+    np.testing.assert_allclose(r1.v, r0.v, rtol=1e-6, atol=1e-6)
+
+
+def test_soft_restoration_options_are_validated():
+    from cocofest_amd.solver import IpmOptions, Solver, apply_solver
+
+    with pytest.raises(ValueError):
+        IpmOptions(soft_resto_pderror_reduction_factor=-1.0)
+    with pytest.raises(ValueError):
+        IpmOptions(max_soft_resto_iters=-1)
+    o = apply_solver(IpmOptions(), Solver.IPOPT(_soft_resto_pderror_reduction_factor=0.9999, _max_soft_resto_iters=3))
+    assert (o.soft_resto_pderror_reduction_factor, o.max_soft_resto_iters) == (0.9999, 3)
