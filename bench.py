@@ -346,6 +346,11 @@ def collocation_section(device, steps=50):
     ms = timed(lambda: h.eval_all(v, g=g, jac=jac), steps)
     nbytes = 8 * (h.nv + h.ng + h.nnz_jac)
     achieved = nbytes * B / (ms * 1e-3) / 1e9
+    # the caller that keeps the constant J_g values (cfx_jac_constant_mask: C off the point's own state, the calcium
+    # row, D and -1 — 48 of 56 per interval) in its buffer: CFX_KEEP_CONSTANT_JAC skips their stores
+    n_const = int(h.jac_constant_mask().sum())
+    ms_keep = timed(lambda: h.eval_all(v, g=g, jac=jac, keep_constant_jac=True), steps)
+    nbytes_keep = 8 * (h.nv + h.ng + h.nnz_jac - n_const)
     pmc = collocation_pmc()
     lam = torch.randn((B // 64, h.ng, 64), dtype=torch.float64, device=dev, generator=torch.Generator(dev).manual_seed(3))
     of = torch.ones((B,), dtype=torch.float64, device=dev)
@@ -363,6 +368,9 @@ def collocation_section(device, steps=50):
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                          "traffic": pmc.get("hbm_bytes_per_launch") if pmc else None,
                          "traffic_source": pmc.get("source") if pmc else None},
+            "jac_constants_kept": {"constant_values": n_const, "ms_per_launch": ms_keep,
+                                   "bytes_per_instance": nbytes_keep, "instance_evals_per_s": B / (ms_keep * 1e-3),
+                                   "achieved_GBps": nbytes_keep * B / (ms_keep * 1e-3) / 1e9},
             "fused_g_jac_hess": {"kernel": "cfx::k_colloc_hess<DING2003, DJ=2, TMAX=1, GJ=true>",
                                  "ms_per_launch": ms_h, "bytes_per_instance": nbytes_h,
                                  "achieved_GBps": nbytes_h * B / (ms_h * 1e-3) / 1e9}}

@@ -527,6 +527,7 @@ extern "C" int cfx_create(const cfx_problem* p, cfx_handle** out) {
     const int nhk = colloc ? nx + deg * per_point + nu * (nu + 1) / 2 : nz * (nz + 1) / 2;
     KParams& kp = h->kp;
     int nnzk = 0;
+    std::vector<uint8_t> ccst;  // collocation: constant J_g values, in triplet order
     if (!colloc) {
         // structural sparsity of dPhi/d(x_k, u_k), as CasADi derives it symbolically: dependency bitmasks
         // pushed through the RHS and the RK stages (identical for every interval)
@@ -551,25 +552,28 @@ extern "C" int cfx_create(const cfx_problem* p, cfx_handle** out) {
         }
     } else {
         // collocation (cfx_colloc.h): defect rows [x^0_r..x^d_r, other states of point j, controls], then
-        // continuity rows [x^0_r..x^d_r, -1 on x_{k+1}^0_r]
+        // continuity rows [x^0_r..x^d_r, -1 on x_{k+1}^0_r].  Constant values (ccst): the basis coefficients C[i][j]
+        // off the point's own state, the whole calcium row (its right-hand side (cs - cn) / tau_c is linear in cn),
+        // every continuity value D[i] and -1
         for (int k = 0; k < N; ++k) {
             const size_t before = h->jrow.size();
-            auto put = [&](int row, int col) {
+            auto put = [&](int row, int col, bool cst) {
                 h->jrow.push_back(row);
                 h->jcol.push_back(col);
+                ccst.push_back(cst);
             };
             for (int j = 1; j <= deg; ++j)
                 for (int r = 0; r < nx; ++r) {
                     const int row = k * ngk + (j - 1) * nx + r;
-                    for (int i = 0; i <= deg; ++i) put(row, k * nz + i * nx + r);
+                    for (int i = 0; i <= deg; ++i) put(row, k * nz + i * nx + r, r == 0 || i != j);
                     for (int c = 0; c < nx; ++c)
-                        if (c != r && (col_xdeps(h->model, r) >> c & 1u)) put(row, k * nz + j * nx + c);
-                    for (int c = 0; c < col_udeps(h->model, r, nu); ++c) put(row, k * nz + uoff + c);
+                        if (c != r && (col_xdeps(h->model, r) >> c & 1u)) put(row, k * nz + j * nx + c, false);
+                    for (int c = 0; c < col_udeps(h->model, r, nu); ++c) put(row, k * nz + uoff + c, false);
                 }
             for (int r = 0; r < nx; ++r) {
                 const int row = k * ngk + deg * nx + r;
-                for (int i = 0; i <= deg; ++i) put(row, k * nz + i * nx + r);
-                put(row, (k + 1) * nz + r);
+                for (int i = 0; i <= deg; ++i) put(row, k * nz + i * nx + r, true);
+                put(row, (k + 1) * nz + r, true);
             }
             nnzk = (int)(h->jrow.size() - before);
         }
@@ -598,6 +602,7 @@ extern "C" int cfx_create(const cfx_problem* p, cfx_handle** out) {
     // constant J_g values: the -1 on x_{k+1} of every continuity row and, for the Ding families (calcium affine in
     // its start value, cfx_kernels.h:integrate), dCn+/dCn0 = cna[m S]
     h->jconst.assign(h->jrow.size(), 0);
+    std::copy(ccst.begin(), ccst.end(), h->jconst.begin());
     if (!colloc)
         for (int k = 0; k < N; ++k) {
             for (int r = 0; r < nx; ++r) h->jconst[(size_t)k * nnzk + kp.jneg[r]] = 1;
@@ -866,12 +871,12 @@ extern "C" int cfx_hess_structure(const cfx_handle* h, int32_t* row, int32_t* co
 static hipError_t launch_shooting(cfx_handle* h, bool derivs, const double* V, double* G, double* J, bool keep) {
     // 16-byte lane accesses need 16-byte aligned buffers (B % NI == 0 keeps every row aligned)
     auto aligned = [](const void* p) { return ((uintptr_t)p & 15u) == 0; };
-    if (h->colloc) {
-        const int ni = (aligned(V) && aligned(G) && aligned(J)) ? h->ni : 1;
-        return launch_colloc(h->model, h->tmax, ni, h->kp, V, G, derivs ? J : nullptr, h->stream);
-    }
     KParams kp = h->kp;
     kp.keepc = keep ? 1 : 0;
+    if (h->colloc) {
+        const int ni = (aligned(V) && aligned(G) && aligned(J)) ? h->ni : 1;
+        return launch_colloc(h->model, h->tmax, ni, kp, V, G, derivs ? J : nullptr, h->stream);
+    }
     if (is_int(h->model)) return launch_shooting_hmed(h->model, h->scheme, derivs, h->tmax, kp, V, G, J, h->stream);
     const int ni = (aligned(V) && aligned(G) && aligned(J)) ? (derivs ? h->ni : h->ni_g) : 1;
     return launch_shooting_ding(h->model, h->scheme, derivs, ni, kp, V, G, J, h->stream);

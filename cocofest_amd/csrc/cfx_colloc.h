@@ -156,6 +156,8 @@ __device__ __forceinline__ void colloc_interval(const KParams& P, const double* 
             for (int r = 0; r < NX; ++r) {
 #pragma unroll UN
                 for (int i = 0; i <= d; ++i) {
+                    // CFX_KEEP_CONSTANT_JAC: only the point's own non-calcium states vary (cfx_jac_constant_mask)
+                    if (P.keepc && (r == 0 || i != j)) continue;
                     double t[NI];
 #pragma unroll
                     for (int n = 0; n < NI; ++n) {
@@ -211,7 +213,7 @@ __device__ __forceinline__ void colloc_interval(const KParams& P, const double* 
             }
             st_lane_p<NI, PLAIN>(G + gb + (go + d * NX + r) * ES, t);
         }
-        if (J) {
+        if (J && !P.keepc) {
             const int64_t o = jo + (int64_t)d * sumrow + (int64_t)r * (d + 2);
 #pragma unroll UN
             for (int i = 0; i <= d; ++i) {

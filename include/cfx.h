@@ -179,7 +179,9 @@ int cfx_jac_structure(const cfx_handle *h, int32_t *row, int32_t *col);  /* nnz_
 int cfx_hess_structure(const cfx_handle *h, int32_t *row, int32_t *col); /* nnz_hess, row >= col */
 /* mask[nnz_jac] = 1 for the J_g values that depend on neither the instance nor the point (the -1 on x_{k+1} of every
    continuity row; for the Ding families also dCn+/dCn0, the calcium state being affine in its start value), i.e. the
-   values CFX_KEEP_CONSTANT_JAC leaves in place (cfg 2: 60 of 100 per instance).  Collocation handles report none. */
+   values CFX_KEEP_CONSTANT_JAC leaves in place (cfg 2: 60 of 100 per instance).  Collocation: the basis coefficients
+   C[i][j] off the point's own state, the whole calcium row (linear in cn), every continuity value D[i] and -1 (cfg 2
+   at degree 4: 48 of 56 per interval). */
 int cfx_jac_constant_mask(const cfx_handle *h, uint8_t *mask);
 
 /* ---- NLP callbacks over the whole batch -------------------------------------------------------- */

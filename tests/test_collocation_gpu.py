@@ -168,3 +168,52 @@ def test_bench_shape_collocation():
     small.close()
     _close_col_g(vp, gp, CO.eval_g(pb, vp), 4, "bench colloc g")
     _close(jp, CO.eval_jac_g(pb, vp), what="bench colloc J")
+
+
+@pytest.mark.parametrize("name,degree", [("ding2003", 4), ("ding2007_with_fatigue", 3), ("hmed2018", 2)])
+def test_collocation_keep_constant(name, degree):
+    """The constant collocation J_g values (cfx_jac_constant_mask): the basis coefficients C[i][j] off the point's own
+    state, the whole calcium row (its right-hand side (cs - cn) / tau_c is linear in cn), the continuity values D[i]
+    and the -1 — 48 of 56 per interval for Ding2003 at degree 4.  With CFX_KEEP_CONSTANT_JAC the g + J_g launch (two
+    instances per lane where it applies) and the fused g + J_g + Hessian launch leave them in place and write every
+    other value bit for bit (tests/test_constant_jac.py's check); the mask's values equal the oracle's."""
+    import torch
+
+    from oracle import fes_collocation as CO
+    from tests.test_constant_jac import _keep_check
+
+    ocp, pb = _col(name, degree, "legendre")
+    B = 256
+    h = ocp.nlp(batch=B, layout="soa")
+    mask = h.jac_constant_mask()
+    N = pb.n_shooting
+    if name == "ding2003":
+        assert (h.nnz_jac // N, int(mask.sum()) // N) == (56, 48)
+    v1, v2 = (cases.random_collocation_decision(pb, B, seed=s) for s in (5, 6))
+    d1, d2 = (torch.tensor(np.ascontiguousarray(v.T), device="cuda") for v in (v1, v2))
+
+    def full(j, v=d2):
+        j = torch.empty((h.nnz_jac, B), dtype=torch.float64, device="cuda") if j is None else j
+        h.eval_all(v, jac=j)
+        return j
+
+    def keep(j):
+        h.eval_all(d2, jac=j, keep_constant_jac=True)
+
+    a = _keep_check(h, full, keep, mask)
+    b = full(None, d1).cpu().numpy()
+    np.testing.assert_array_equal(a[mask], b[mask])  # constant over instances and points
+    np.testing.assert_array_equal(a[mask], np.broadcast_to(a[mask][:, :1], a[mask].shape))
+    _close(a[:, :3].T, CO.eval_jac_g(pb, v2[:3]), what=f"colloc J {name} {degree}")
+    of = torch.linspace(0.5, 1.5, B, dtype=torch.float64, device="cuda")
+    lam = torch.randn((h.ng, B), dtype=torch.float64, device="cuda")
+
+    def full_h(j):
+        _, j, _ = h.eval_all_h(d2, of, lam, jac=j)
+        return j
+
+    def keep_h(j):
+        h.eval_all_h(d2, of, lam, jac=j, keep_constant_jac=True)
+
+    _keep_check(h, full_h, keep_h, mask)
+    h.close()

@@ -210,3 +210,4 @@ def test_msk_keep_constant():
     a = _keep_check(h, full, keep, mask)
     assert np.all(a[mask] == -1.0)
     h.close()
+
