@@ -69,6 +69,8 @@ struct Scal {
     // the try was accepted by the original filter
     double soft_a, soft_pd;
     int32_t soft_on, soft_cnt, soft_try, soft_ok;
+    int32_t rs_rr;  // the phase's last iteration reset p, n (Ipopt's RestoRestorationPhase) instead of stepping
+    int32_t rpad;
 };
 
 // how a restoration phase ended (Scal::rs_exit)
@@ -1591,6 +1593,7 @@ __global__ void __launch_bounds__(kIB) k_rs_init(const IpmK K) {
             S.rs_th0 = S.theta;
             S.rs_dw = S.rs_dwl = 0.0;
             S.rs_it = 0;
+            S.rs_rr = 0;
             S.rs_on = 1;
             S.rs_exit = RS_RUNNING;
             S.soc = 0;
@@ -1850,8 +1853,10 @@ __global__ void __launch_bounds__(kIB) k_rs_next_trial(const IpmK K) {
 
 // end of a phase iteration: the step (primal-dual, z safeguard), the phase's filter, the exit test on the original
 // problem and, on exit, the original bound multipliers; rs_exit records how the phase ended (k_ipm_update acts on it).
-// A failed line search of the phase, or max_resto_iter iterations of it, fail it (Ipopt: Restoration_Failed).  The
-// instances that go on get their next evaluation point (vx = xr) and Hessian multipliers ready.
+// A failed line search of the phase is answered as Ipopt's RestoRestorationPhase does: x stays, p and n take their
+// closed form at x (the phase's own constraints c - p + n = 0 then hold), the phase's filter takes the point; a second
+// failed search in a row, or max_resto_iter iterations, fail the phase (Ipopt: Restoration_Failed).  The instances
+// that go on get their next evaluation point (vx = xr) and Hessian multipliers ready.
 __global__ void __launch_bounds__(kIB) k_rs_update(const IpmK K) {
     __shared__ double sh[kIB / 64];
     __shared__ Scal S;
@@ -1859,12 +1864,42 @@ __global__ void __launch_bounds__(kIB) k_rs_update(const IpmK K) {
     const int nf = K.nf, m = K.m;
     load_scal(K, b, S);
     if (!S.rs_on || S.rs_exit != RS_RUNNING) return;  // block-uniform
-    if (!S.rs_acc) {
+    if (!S.rs_acc && S.rs_rr) {
         __syncthreads();
         if (threadIdx.x == 0) {
             S.rs_exit = RS_FAILED;
             S.iters += 1;  // Ipopt counts the phase's iterations among the solve's
             atomicAdd(K.rstat + 1, 1ull);
+        }
+    } else if (!S.rs_acc) {  // Ipopt's restoration of the restoration phase
+        const double rho = K.o.resto_penalty, mu = S.rs_mu;
+        for (int j = threadIdx.x; j < m; j += kIB) {
+            double p, n;
+            rs_pn(K.gS[b * m + j], mu, rho, p, n);
+            K.rp[b * m + j] = p;
+            K.rn[b * m + j] = n;
+            K.rzp[b * m + j] = mu / p;
+            K.rzn[b * m + j] = mu / n;
+        }
+        const bool budget = S.iters + 1 >= K.o.max_iter, limit = S.rs_it + 1 >= K.o.max_resto_iter;
+        if (!budget && !limit) {
+            write_full(K, b, K.xr + b * nf, K.vx);
+            for (int j = threadIdx.x; j < m; j += kIB) K.ysc[b * m + j] = K.ry[b * m + j] * K.sg[b * m + j];
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            double* rf = K.rfilt + b * kFilt * 2;
+            const int k = S.rs_it % kFilt;
+            rf[2 * k] = (1 - 1e-5) * S.rs_theta;
+            rf[2 * k + 1] = S.rs_phi - 1e-5 * S.rs_theta;
+            S.rs_rr = 1;
+            S.rs_it += 1;
+            S.iters += 1;
+            atomicAdd(K.rstat + 1, 1ull);
+            if (budget)
+                S.rs_exit = RS_BUDGET;
+            else if (limit)
+                S.rs_exit = RS_FAILED;
         }
     } else {
         const double a = S.rs_alpha, az = S.rs_az, mu = S.rs_mu;
@@ -1945,6 +1980,7 @@ __global__ void __launch_bounds__(kIB) k_rs_update(const IpmK K) {
         }
         __syncthreads();
         if (threadIdx.x == 0) {
+            S.rs_rr = 0;
             S.rs_it += 1;
             S.iters += 1;
             atomicAdd(K.rstat + 1, 1ull);

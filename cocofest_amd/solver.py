@@ -872,8 +872,8 @@ class BatchedIpm:
         th0 = theta
         c = g
         muR = torch.maximum(mu, c.abs().amax(1))
-        sR = torch.hypot(muR[:, None], rho * c)
         mR = muR[:, None]
+        sR = torch.hypot(mR, rho * c)
         n = torch.where(c > 0, (mR + mR * mR / (sR + rho * c)) / (2 * rho), (mR - rho * c + sR) / (2 * rho))
         p = torch.where(c < 0, (mR + mR * mR / (sR - rho * c)) / (2 * rho), (mR + rho * c + sR) / (2 * rho))
         zp, zn = mR / p, mR / n
@@ -890,6 +890,14 @@ class BatchedIpm:
         dref = torch.clamp(xref.abs(), min=1.0) ** 2
         of0 = torch.zeros((B,), dtype=torch.float64, device=self.dev)
         rexit = torch.zeros((B,), dtype=torch.int64, device=self.dev)
+        rr_last = torch.zeros_like(on)  # the last phase iteration reset p, n (Ipopt's RestoRestorationPhase)
+
+        def pn_closed_form(cc, muR_):
+            mR_ = muR_[:, None]
+            s_ = torch.hypot(mR_, rho * cc)
+            nn_ = torch.where(cc > 0, (mR_ + mR_ * mR_ / (s_ + rho * cc)) / (2 * rho), (mR_ - rho * cc + s_) / (2 * rho))
+            pp_ = torch.where(cc < 0, (mR_ + mR_ * mR_ / (s_ - rho * cc)) / (2 * rho), (mR_ + rho * cc + s_) / (2 * rho))
+            return pp_, nn_
 
         def merit(xx, pp, nn, mu_):
             w = mu_.sqrt()[:, None] / dref
@@ -995,13 +1003,25 @@ class BatchedIpm:
                     break
                 alpha = torch.where(acc, alpha, alpha * 0.5)
             its = its + on.long()
-            rexit = torch.where(on & ~acc, torch.full_like(rexit, self.RS_FAILED), rexit)
-            on = on & acc  # a failed line search of the phase fails it
-            grow = on & ~arm_acc
+            # a failed line search of the phase: Ipopt's RestoRestorationPhase — x stays, p and n take their closed
+            # form at x (the phase's constraints then hold) and the phase's filter takes the point (below); a second
+            # failed search in a row fails the phase
+            lsfail = on & ~acc
+            rexit = torch.where(lsfail & rr_last, torch.full_like(rexit, self.RS_FAILED), rexit)
+            on = on & ~(lsfail & rr_last)
+            rr = lsfail & ~rr_last
+            if bool(rr.any()):
+                pN, nN = pn_closed_form(gS, muR)
+                c2 = rr[:, None]
+                p, n = torch.where(c2, pN, p), torch.where(c2, nN, n)
+                zp, zn = torch.where(c2, mR / p, zp), torch.where(c2, mR / n, zn)
+            rr_last = rr
+            grow = on & ~arm_acc  # h-type steps, and the points the reset starts from
             rslot = (torch.arange(rfilt.shape[1], device=self.dev) == (r % rfilt.shape[1]))[None, :, None]
             rfilt = torch.where(grow[:, None, None] & rslot,
                                 torch.stack([(1 - 1e-5) * thR, phR - 1e-5 * thR], dim=1)[:, None, :], rfilt)
-            c1 = on[:, None]
+            stepped = on & acc
+            c1 = stepped[:, None]
             xR = torch.where(c1, x_a, xR)
             slN = torch.where(hasL, xR - lbI, torch.ones_like(xR))
             suN = torch.where(hasU, ubI - xR, torch.ones_like(xR))
@@ -1016,7 +1036,8 @@ class BatchedIpm:
             th = g_a.abs().sum(1)
             ph = self._barrier_obj(f_a, xR, mu)
             dominated = ((th[:, None] >= filt[:, :, 0]) & (ph[:, None] >= filt[:, :, 1])).any(1)
-            done_r = on & torch.isfinite(th) & torch.isfinite(ph) &                 (th <= opt.required_infeasibility_reduction * th0) & ~dominated
+            done_r = stepped & torch.isfinite(th) & torch.isfinite(ph) & \
+                (th <= opt.required_infeasibility_reduction * th0) & ~dominated
             if bool(done_r.any()):  # the original bound multipliers: Newton step over the phase's whole dx
                 sl0 = torch.where(hasL, x - lbI, torch.ones_like(x))
                 su0 = torch.where(hasU, ubI - x, torch.ones_like(x))
