@@ -32,6 +32,7 @@ DEVICE = 1
 KEEP_CONSTANT_JAC = 2
 OBJ_LAGRANGE, OBJ_MAYER, OBJ_MAYER_INV = 0, 1, 2
 MSK_FORCE_LENGTH, MSK_FORCE_VELOCITY, MSK_PASSIVE_FORCE, MSK_RESIDUAL_TORQUE = 1, 2, 4, 8
+MSK_PULSE_WIDTH_PER_PULSE, MSK_LEGACY_CALCIUM = 16, 32
 VAR_STATE, VAR_CONTROL = 0, 1
 
 
@@ -115,7 +116,8 @@ class IpmOptions(C.Structure):
                 ("max_resto_iter", C.c_int32), ("resto_penalty", C.c_double),
                 ("required_infeasibility_reduction", C.c_double), ("filter_reset_trigger", C.c_int32),
                 ("max_filter_resets", C.c_int32), ("max_wall_time", C.c_double), ("print_frequency_time", C.c_double),
-                ("soft_resto_pderror_reduction_factor", C.c_double), ("max_soft_resto_iters", C.c_int32)]
+                ("soft_resto_pderror_reduction_factor", C.c_double), ("max_soft_resto_iters", C.c_int32),
+                ("resto_failure_restart", C.c_int32)]
 
 
 # cfx_ipm_get_status values (Ipopt's ApplicationReturnStatus)

@@ -73,6 +73,10 @@ struct cfx_handle {
     int msk_ns = 0;                // Hmed: sliding-window rows per interval (0: none)
     MskMarker* d_mk = nullptr;     // marker superimpositions (cfx_msk_marker_pair)
     int n_mk = 0;
+    int32_t* d_ties = nullptr;     // CFX_MSK_PULSE_WIDTH_PER_PULSE: rows v[a] - v[b], [n_ties][2]
+    int n_ties = 0;
+    int64_t tie_row0 = 0, tie_j0 = 0;  // their first g row and J_g value
+    double* d_cs1 = nullptr;       // CFX_MSK_LEGACY_CALCIUM: d cs / d Km per stage and muscle
     DevBuf main[S_COUNT], stage[S_COUNT];
     std::string err;
 };
@@ -801,7 +805,8 @@ extern "C" void cfx_destroy(cfx_handle* h) {
     }
     for (void* p : {(void*)h->d_tab, (void*)h->d_rest, (void*)h->d_cna, (void*)h->d_htasks, (void*)h->d_obj,
                     (void*)h->d_targets, (void*)h->d_sl_param, (void*)h->d_sl_joff, (void*)h->d_hdiag,
-                    (void*)h->d_geom, (void*)h->d_mobj, (void*)h->d_msk_imin, (void*)h->d_mk})
+                    (void*)h->d_geom, (void*)h->d_mobj, (void*)h->d_msk_imin, (void*)h->d_mk, (void*)h->d_ties,
+                    (void*)h->d_cs1})
         if (p) (void)hipFree(p);
     if (h->own_stream) (void)hipStreamDestroy(h->own_stream);
     delete h;
@@ -1127,6 +1132,9 @@ extern "C" int cfx_msk_create(const cfx_msk_problem* p, cfx_handle** out) {
     const int fam = hmed ? 4 + (model - CFX_HMED2018) + (p->truncation > 10 ? 2 : 0) : model;
     if (p->n_params < 0 || (p->n_params > 0 && (!hmed || !p->last_stim_idx || !p->param_offset)))
         return bad("intensity parameters need Hmed2018 muscles, last_stim_idx and param_offset");
+    if ((p->flags & CFX_MSK_LEGACY_CALCIUM) && hmed) return bad("CFX_MSK_LEGACY_CALCIUM needs Ding2003 / Ding2007 muscles");
+    if ((p->flags & CFX_MSK_PULSE_WIDTH_PER_PULSE) && !(model == CFX_DING2007 || model == CFX_DING2007_FATIGUE))
+        return bad("CFX_MSK_PULSE_WIDTH_PER_PULSE needs Ding2007 muscles (pulse-width controls)");
     for (int m = 0; m < nm; ++m) {
         const cfx_msk_muscle& mu = p->muscles[m];
         if (mu.model != model) return bad("every muscle must use the same model family");
@@ -1267,14 +1275,29 @@ extern "C" int cfx_msk_create(const cfx_msk_problem* p, cfx_handle** out) {
     const int Q = m * S;
     const int TM = hmed ? (T > 10 ? 20 : 10) : 1;  // Hmed: per-pulse coefficients, padded to the kernel's TMAX
     std::vector<double> cs((size_t)N * Q * nm * TM, 0.0);
+    // CFX_MSK_LEGACY_CALCIUM (the revision that stored the reaching-task solutions, tests/test_reference_solution.py):
+    // a window's first pulse is left out once the window holds several, and the fatigue models' r0 is Km + r0_km, so
+    // cs = table(r0 = km_rest + r0_km) + (Km - km_rest) cs1 with cs1 = sum_{i >= 1} exp(-(t_i - t_{i-1}) / tau_c)
+    // exp(-(t - t_i) / tau_c) over the pulses kept
+    const bool legacy = (p->flags & CFX_MSK_LEGACY_CALCIUM) != 0;
+    std::vector<double> cs1(legacy && fat ? (size_t)N * Q * nm : 0, 0.0);
     for (int k = 0; k < N; ++k) {
         const double* row = p->stim_rows + (size_t)k * T;
+        int skip = -1;
+        if (legacy) {
+            int nreal = 0;
+            for (int i = 0; i < T; ++i) nreal += row[i] > -1e6;
+            if (nreal > 1) skip = T - nreal;
+        }
         for (int mi = 0; mi < nm; ++mi) {
             const cfx_constants& c = p->muscles[mi].constants;
             const double r0 = c.km_rest + c.r0_km_relationship;
-            std::vector<double> ri(T);
-            for (int i = 0; i < T; ++i)
+            std::vector<double> ri(T), di(T, 0.0);
+            for (int i = 0; i < T; ++i) {
                 ri[i] = i == 0 ? 1.0 : 1.0 + (r0 - 1.0) * std::exp(-(row[i] - row[i - 1]) / c.tauc);
+                if (i > 0) di[i] = std::exp(-(row[i] - row[i - 1]) / c.tauc);
+                if (i == skip) ri[i] = di[i] = 0.0;
+            }
             for (int j = 0; j < m; ++j)
                 for (int st = 0; st < S; ++st) {
                     double t = k * dt + j * hh;
@@ -1286,9 +1309,14 @@ extern "C" int cfx_msk_create(const cfx_msk_problem* p, cfx_handle** out) {
                         for (int i = 0; i < T; ++i) cs[(kq * nm + mi) * TM + i] = ri[i] * std::exp(-(t - row[i]) / c.tauc);
                         continue;
                     }
-                    double sum = 0.0;
-                    for (int i = 0; i < T; ++i) sum = sum + ri[i] * std::exp(-(t - row[i]) / c.tauc);
+                    double sum = 0.0, sum1 = 0.0;
+                    for (int i = 0; i < T; ++i) {
+                        if (i == skip) continue;
+                        sum = sum + ri[i] * std::exp(-(t - row[i]) / c.tauc);
+                        sum1 = sum1 + di[i] * std::exp(-(t - row[i]) / c.tauc);
+                    }
                     cs[kq * nm + mi] = sum;
+                    if (!cs1.empty()) cs1[kq * nm + mi] = sum1;
                 }
         }
     }
@@ -1306,6 +1334,7 @@ extern "C" int cfx_msk_create(const cfx_msk_problem* p, cfx_handle** out) {
     {
         MskParams Ph = P;
         Ph.cs = cs.data();
+        Ph.cs1 = cs1.empty() ? nullptr : cs1.data();
         msk_dep_pattern(nq, nm, fam, p->scheme, Ph, G, dep.data());
     }
     for (int e = 0; e < kMskMaxX * kMskMaxZ; ++e) G.jpos[e] = -1;
@@ -1376,6 +1405,26 @@ extern "C" int cfx_msk_create(const cfx_msk_problem* p, cfx_handle** out) {
             }
         mrow += d.nrow;
     }
+    // CFX_MSK_PULSE_WIDTH_PER_PULSE: interval k following the same pulse as interval k - 1 (same last stimulation
+    // time in its window) keeps its pulse widths: rows u_k[m] - u_{k-1}[m] (+1, -1; constant J_g values), after the
+    // marker rows — the decision space of per-pulse pulse-width parameters, with band-local rows
+    std::vector<int32_t> ties;  // [n][2] decision indices (v[a] - v[b])
+    const int64_t tie_row0 = mrow, tie_j0 = (int64_t)h->jrow.size();
+    if (p->flags & CFX_MSK_PULSE_WIDTH_PER_PULSE)
+        for (int k = 1; k < N; ++k)
+            if (p->stim_rows[(size_t)k * T + T - 1] == p->stim_rows[(size_t)(k - 1) * T + T - 1])
+                for (int mi = 0; mi < nm; ++mi) {
+                    ties.push_back(k * nz + nx + mi);
+                    ties.push_back((k - 1) * nz + nx + mi);
+                    h->jrow.push_back((int32_t)mrow);
+                    h->jcol.push_back(k * nz + nx + mi);
+                    h->jrow.push_back((int32_t)mrow);
+                    h->jcol.push_back((k - 1) * nz + nx + mi);
+                    ++mrow;
+                }
+    h->n_ties = (int)(ties.size() / 2);
+    h->tie_row0 = tie_row0;
+    h->tie_j0 = tie_j0;
     // ---- Hessian: dense lower triangle of every interval block, then the diagonal of x_N (and, for marker pairs at
     // node N, the q_N pairs off the diagonal)
     const int nhk = nz * (nz + 1) / 2;
@@ -1478,6 +1527,7 @@ extern "C" int cfx_msk_create(const cfx_msk_problem* p, cfx_handle** out) {
     h->jconst.assign(h->jrow.size(), 0);  // the -1 on x_{k+1} of every continuity row
     for (int k = 0; k < N; ++k)
         for (int r = 0; r < nx; ++r) h->jconst[(size_t)k * nnzk + G.jneg[r]] = 1;
+    for (int64_t e = 0; e < 2 * (int64_t)h->n_ties; ++e) h->jconst[(size_t)(tie_j0 + e)] = 1;
     h->sz.nnz_hess = (int64_t)h->hrow.size();
     h->sz.nx = nx;
     h->sz.nu = nu;
@@ -1502,12 +1552,37 @@ extern "C" int cfx_msk_create(const cfx_msk_problem* p, cfx_handle** out) {
         !upload((void**)&h->d_sl_param, sl_param.data(), sl_param.size() * sizeof(int32_t)) ||
         !upload((void**)&h->d_sl_joff, sl_joff.data(), sl_joff.size() * sizeof(int32_t)) ||
         !upload((void**)&h->d_msk_imin, imin.data(), imin.size() * sizeof(double)) ||
-        !upload((void**)&h->d_mk, mks.data(), mks.size() * sizeof(MskMarker)))
+        !upload((void**)&h->d_mk, mks.data(), mks.size() * sizeof(MskMarker)) ||
+        !upload((void**)&h->d_ties, ties.data(), ties.size() * sizeof(int32_t)) ||
+        !upload((void**)&h->d_cs1, cs1.data(), cs1.size() * sizeof(double)))
         return create_fail(h, CFX_ENOMEM, "cfx_msk_create: device allocation/upload failed");
     P.cs = h->d_tab;
+    P.cs1 = cs1.empty() ? nullptr : h->d_cs1;
     P.rest = h->d_rest;
     *out = h;
     return CFX_OK;
+}
+
+// per-pulse pulse-width rows v[a] - v[b] (CFX_MSK_PULSE_WIDTH_PER_PULSE): SoA, thread = (instance, row)
+static __global__ void __launch_bounds__(256) k_msk_ties(int64_t B, int n, const int32_t* __restrict__ ties,
+                                                         int64_t row0, int64_t j0, int keepc,
+                                                         const double* __restrict__ V, double* __restrict__ G,
+                                                         double* __restrict__ J) {
+    const int64_t item = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (item >= B * n) return;
+    const int64_t b = item % B, t = item / B;
+    if (G) G[(row0 + t) * B + b] = V[(int64_t)ties[2 * t] * B + b] - V[(int64_t)ties[2 * t + 1] * B + b];
+    if (J && !keepc) {
+        J[(j0 + 2 * t) * B + b] = 1.0;
+        J[(j0 + 2 * t + 1) * B + b] = -1.0;
+    }
+}
+static hipError_t launch_msk_ties(cfx_handle* h, const double* V, double* G, double* J, int keepc) {
+    if (!h->n_ties || (!G && !J)) return hipSuccess;
+    const int64_t items = h->mp.B * h->n_ties;
+    hipLaunchKernelGGL(k_msk_ties, dim3((unsigned)((items + 255) / 256)), dim3(256), 0, h->stream, h->mp.B, h->n_ties,
+                       (const int32_t*)h->d_ties, h->tie_row0, h->tie_j0, keepc, V, G, J);
+    return hipGetLastError();
 }
 
 // marker superimposition rows / their Hessian terms (k_msk_markers, one thread per instance)
@@ -1557,6 +1632,7 @@ static int msk_eval_all(cfx_handle* h, const double* v, double* g, double* jac, 
                                (const double*)h->d_msk_imin, (int64_t)P.N * P.nz + P.nx, V, G, J);
         }
         CFX_HIP(h, launch_msk_markers(h, V, G, J, nullptr, nullptr));
+        CFX_HIP(h, launch_msk_ties(h, V, G, J, P.keepc));
         if (J) {
             h->stash_valid = h->msk_stash;
             h->stash_same_point = false;

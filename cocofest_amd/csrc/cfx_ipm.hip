@@ -1332,7 +1332,10 @@ __global__ void __launch_bounds__(kIB) k_ipm_update(const IpmK K, int resto) {
     load_scal(K, b, S);
     if (S.rs_on && S.rs_exit == RS_RUNNING) return;  // block-uniform
     const bool phase_end = S.rs_on;
-    const bool rs_stop = phase_end && (S.rs_exit == RS_FAILED || S.rs_exit == RS_INFEASIBLE);
+    // a failed phase stops the instance (Ipopt: Restoration_Failed) unless resto_failure_restart (an extension) sends
+    // it back to the main iteration from the phase's last point, as a successful phase would
+    const bool rs_stop = phase_end && (S.rs_exit == RS_INFEASIBLE ||
+                                       (S.rs_exit == RS_FAILED && !K.o.resto_failure_restart));
     if (rs_stop) {
         __syncthreads();
         if (threadIdx.x == 0) {
@@ -2411,6 +2414,7 @@ extern "C" void cfx_ipm_default_options(cfx_ipm_options* o) {
     o->print_frequency_time = 0.0;
     o->soft_resto_pderror_reduction_factor = 0.0;  // Ipopt: 0.9999
     o->max_soft_resto_iters = 10;
+    o->resto_failure_restart = 0;
 }
 
 // CSR of `key` (values in [0, nkeys)) with the sources of each key in increasing source order

@@ -212,6 +212,9 @@ struct MskParams {
     // calcium sums [N][Q][NM] at every RK stage time (host, reference operation order); Hmed2018: the per-pulse
     // coefficients r_i exp(-(t - t_i) / tau_c) [N][Q][NM][TMAX] of cs = sum_i coef_i lambda(I_i)
     const double* cs;
+    // CFX_MSK_LEGACY_CALCIUM (fatigue families): d cs / d Km [N][Q][NM] — the stored revision's r0 = Km + r0_km
+    // makes cs affine in the Km state, cs = table + (Km - km_rest) cs1; nullptr: today's r0 = km_rest + r0_km
+    const double* cs1;
     const double* rest;  // rest state [nx] (IVP default x0)
     double* scratch;     // k_msk_stagecoef_par -> k_msk_tangents: per-stage Jacobian coefficients [N][Q][NC][B]
 };
@@ -304,6 +307,12 @@ MSK_HD void msk_stage_cs(const double* __restrict__ tab, int64_t kq, const doubl
 #pragma unroll
         for (int mu = 0; mu < NM; ++mu) cs[mu] = tab[kq * NM + mu];
     }
+}
+
+// legacy calcium: the stage's d cs / d Km per muscle (nullptr when off)
+template <int NM>
+MSK_HD const double* msk_cs1(const MskParams& P, int64_t kq) {
+    return P.cs1 ? P.cs1 + kq * NM : nullptr;
 }
 
 // ---- small vector helpers ---------------------------------------------------------------------------------------
@@ -633,7 +642,8 @@ MSK_HD void msk_skeleton(const MskGeom& G, const SQ* q, const SV* qd, const SV* 
 
 // FesMskModel.muscle_dynamic for one state: f = dx/dt.  cs[m]: calcium sum of muscle m at this stage time.
 template <int NQ, int NM, int FAM, class S>
-MSK_HD void msk_rhs(const MskGeom& G, int residual, const double* cs, const S* x, const S* u, S* f) {
+MSK_HD void msk_rhs(const MskGeom& G, int residual, const double* cs, const double* cs1, const S* x, const S* u,
+                    S* f) {
     constexpr int NXM = msk_nxm<FAM>();
     constexpr bool FAT = (FAM & 1) != 0, PW = msk_pw<FAM>();
     constexpr int XQ = NM * NXM, XQD = XQ + NQ;
@@ -660,6 +670,7 @@ MSK_HD void msk_rhs(const MskGeom& G, int residual, const double* cs, const S* x
             A = x[mu * NXM + 2];
             tau1 = x[mu * NXM + 3];
             km = x[mu * NXM + 4];
+            if (cs1) f[mu * NXM] = f[mu * NXM] + (km - C.km_rest) * (cs1[mu] * C.inv_tauc);  // legacy r0 = Km + r0_km
         }
         S Aeff = A;
         if constexpr (PW) Aeff = A * (1.0 - mexp(-(u[mu] - C.pd0) * C.inv_pdt));
@@ -687,44 +698,50 @@ MSK_HD void msk_interval(const MskParams& P, const MskGeom& G, int k, S* x, cons
     constexpr int NMC = NM;
     const double h = P.h;
     for (int j = 0; j < P.m; ++j) {
-        double csv[ST * NMC];  // the stage sums of this sub-step
+        double csv[ST * NMC], csv1[ST * NMC];  // the stage sums of this sub-step (and their d / d Km, legacy)
 #pragma unroll
-        for (int st = 0; st < ST; ++st) msk_stage_cs<NM, FAM>(P.cs, (int64_t)k * P.Q + j * ST + st, lam, csv + st * NMC);
+        for (int st = 0; st < ST; ++st) {
+            msk_stage_cs<NM, FAM>(P.cs, (int64_t)k * P.Q + j * ST + st, lam, csv + st * NMC);
+            if (P.cs1)
+#pragma unroll
+                for (int mu = 0; mu < NM; ++mu) csv1[st * NMC + mu] = P.cs1[((int64_t)k * P.Q + j * ST + st) * NM + mu];
+        }
         const double* cs = csv;
+        const double* c1 = P.cs1 ? csv1 : nullptr;
         if constexpr (SCHEME == 1) {
             S f[NX];
-            msk_rhs<NQ, NM, FAM>(G, P.residual, cs, x, u, f);
+            msk_rhs<NQ, NM, FAM>(G, P.residual, cs, c1, x, u, f);
 #pragma unroll
             for (int r = 0; r < NX; ++r) x[r] = x[r] + h * f[r];
         } else if constexpr (SCHEME == 2) {
             S f[NX], xs[NX];
-            msk_rhs<NQ, NM, FAM>(G, P.residual, cs, x, u, f);
+            msk_rhs<NQ, NM, FAM>(G, P.residual, cs, c1, x, u, f);
 #pragma unroll
             for (int r = 0; r < NX; ++r) xs[r] = x[r] + (0.5 * h) * f[r];
-            msk_rhs<NQ, NM, FAM>(G, P.residual, cs + NMC, xs, u, f);
+            msk_rhs<NQ, NM, FAM>(G, P.residual, cs + NMC, c1 ? c1 + NMC : nullptr, xs, u, f);
 #pragma unroll
             for (int r = 0; r < NX; ++r) x[r] = x[r] + h * f[r];
         } else {
             S acc[NX], xs[NX], f[NX];
-            msk_rhs<NQ, NM, FAM>(G, P.residual, cs, x, u, f);
+            msk_rhs<NQ, NM, FAM>(G, P.residual, cs, c1, x, u, f);
 #pragma unroll
             for (int r = 0; r < NX; ++r) {
                 acc[r] = f[r];
                 xs[r] = x[r] + (0.5 * h) * f[r];
             }
-            msk_rhs<NQ, NM, FAM>(G, P.residual, cs + NMC, xs, u, f);
+            msk_rhs<NQ, NM, FAM>(G, P.residual, cs + NMC, c1 ? c1 + NMC : nullptr, xs, u, f);
 #pragma unroll
             for (int r = 0; r < NX; ++r) {
                 acc[r] = acc[r] + 2.0 * f[r];
                 xs[r] = x[r] + (0.5 * h) * f[r];
             }
-            msk_rhs<NQ, NM, FAM>(G, P.residual, cs + 2 * NMC, xs, u, f);
+            msk_rhs<NQ, NM, FAM>(G, P.residual, cs + 2 * NMC, c1 ? c1 + 2 * NMC : nullptr, xs, u, f);
 #pragma unroll
             for (int r = 0; r < NX; ++r) {
                 acc[r] = acc[r] + 2.0 * f[r];
                 xs[r] = x[r] + h * f[r];
             }
-            msk_rhs<NQ, NM, FAM>(G, P.residual, cs + 3 * NMC, xs, u, f);
+            msk_rhs<NQ, NM, FAM>(G, P.residual, cs + 3 * NMC, c1 ? c1 + 3 * NMC : nullptr, xs, u, f);
 #pragma unroll
             for (int r = 0; r < NX; ++r) x[r] = x[r] + (h / 6.0) * (acc[r] + f[r]);
         }
@@ -844,8 +861,9 @@ __device__ __forceinline__ void msk_muscle_coef(const MskMuscleConst& C, const d
 
 // One RK stage: the RHS value f(xs, u) and the stage coefficients written to Ws[c * B].
 template <int NQ, int NM, int FAM>
-__device__ __forceinline__ void msk_stage(const MskGeom& G, int residual, const double* cs, const double* xs,
-                                          const double* u, double* f, double* __restrict__ Ws, int64_t B) {
+__device__ __forceinline__ void msk_stage(const MskGeom& G, int residual, const double* cs, const double* cs1,
+                                          const double* xs, const double* u, double* f, double* __restrict__ Ws,
+                                          int64_t B) {
     constexpr int NXM = msk_nxm<FAM>(), XQ = NM * NXM, XQD = XQ + NQ, ND = 2 * NQ;
     constexpr bool FAT = (FAM & 1) != 0, PW = msk_pw<FAM>();
     constexpr int NUI = msk_nui<NM, FAM>(), OM = 6 + ND, ODQ = NM * OM, OB = ODQ + NQ * ND, OMI = OB + NQ * NM;
@@ -874,6 +892,7 @@ __device__ __forceinline__ void msk_stage(const MskGeom& G, int residual, const 
         f[mu * NXM] = (cs[mu] - xm[0]) * C.inv_tauc;
         f[mu * NXM + 1] = base * mult[mu].v;
         if constexpr (FAT) {
+            if (cs1) f[mu * NXM] = f[mu * NXM] + (xm[4] - C.km_rest) * (cs1[mu] * C.inv_tauc);
             f[mu * NXM + 2] = C.alpha_a * xm[1] - (xm[2] - C.a_fat_rest) * C.inv_tau_fat;
             f[mu * NXM + 3] = C.alpha_tau1 * xm[1] - (xm[3] - C.tau1_rest) * C.inv_tau_fat;
             f[mu * NXM + 4] = C.alpha_km * xm[1] - (xm[4] - C.km_rest) * C.inv_tau_fat;
@@ -931,8 +950,10 @@ __device__ __forceinline__ void msk_stage(const MskGeom& G, int residual, const 
 // tk = (df/dx, df/du)(stage) . (t, tu) for one tangent column, from the stored stage coefficients.
 // dcs: Hmed, the stage's d cs_mu / d(column) (zero unless the column is one of the muscle's intensities).
 template <int NQ, int NM, int FAM>
+// cs1: legacy calcium, the stage's d cs / d Km (nullptr: off)
 __device__ __forceinline__ void msk_tangent(const MskGeom& G, int residual, const double* __restrict__ Ws, int64_t B,
-                                            const double* t, const double* tu, const double* dcs, double* tk) {
+                                            const double* t, const double* tu, const double* dcs, const double* cs1,
+                                            double* tk) {
     constexpr int NXM = msk_nxm<FAM>(), XQ = NM * NXM, XQD = XQ + NQ, ND = 2 * NQ;
     constexpr bool FAT = (FAM & 1) != 0, PW = msk_pw<FAM>();
     constexpr int NUI = msk_nui<NM, FAM>(), OM = 6 + ND, ODQ = NM * OM, OB = ODQ + NQ * ND, OMI = OB + NQ * NM;
@@ -943,6 +964,8 @@ __device__ __forceinline__ void msk_tangent(const MskGeom& G, int residual, cons
         const double* c = Ws + (int64_t)mu * OM * B;
         tk[o] = -C.inv_tauc * t[o];
         if constexpr (msk_hmed<FAM>()) tk[o] += C.inv_tauc * dcs[mu];
+        if constexpr (FAT)
+            if (cs1) tk[o] += (cs1[mu] * C.inv_tauc) * t[o + 4];
         double s = c[0] * t[o] + c[B] * t[o + 1];
         if constexpr (FAT) s += c[2 * B] * t[o + 2] + c[3 * B] * t[o + 3] + c[4 * B] * t[o + 4];
         if constexpr (PW) s += c[5 * B] * tu[mu];
@@ -1040,7 +1063,8 @@ __global__ void __launch_bounds__(256) k_msk_tangents(const MskParams P, const M
         for (int st = 0; st < ST; ++st) {
             double tk[NX], dcs[NM];
             msk_icol_dcs<NM, FAM>(P, ic, (int64_t)k * P.Q + j * ST + st, dcs);
-            msk_tangent<NQ, NM, FAM>(G, residual, Wk + (int64_t)(j * ST + st) * NC * B, B, txs, tu, dcs, tk);
+            msk_tangent<NQ, NM, FAM>(G, residual, Wk + (int64_t)(j * ST + st) * NC * B, B, txs, tu, dcs,
+                                     msk_cs1<NM>(P, (int64_t)k * P.Q + j * ST + st), tk);
             const double cst = (ST == 4 && st == 2) ? h : 0.5 * h;
 #pragma unroll
             for (int r = 0; r < NX; ++r) {
@@ -1177,7 +1201,8 @@ __global__ void __launch_bounds__(32 * kMskLdsCols) k_msk_tangents_lds(const Msk
             for (int st = 0; st < ST; ++st) {
                 double tk[NX], dcs[NM];
                 msk_icol_dcs<NM, FAM>(P, ic, (int64_t)k * P.Q + j * ST + st, dcs);
-                msk_tangent<NQ, NM, FAM>(G, residual, sWb + st * NC * TW + lane, TW, txs, tu, dcs, tk);
+                msk_tangent<NQ, NM, FAM>(G, residual, sWb + st * NC * TW + lane, TW, txs, tu, dcs,
+                                         msk_cs1<NM>(P, (int64_t)k * P.Q + j * ST + st), tk);
                 const double cst = (ST == 4 && st == 2) ? h : 0.5 * h;
 #pragma unroll
                 for (int r = 0; r < NX; ++r) {
@@ -1227,7 +1252,7 @@ __device__ __forceinline__ double rk_a(int s) {
 // a = (df/dx)^T w at the stage whose coefficients are Ws (the transpose of msk_tangent's state part)
 template <int NQ, int NM, int FAM>
 __device__ __forceinline__ void msk_tangent_T(const MskGeom& G, const double* __restrict__ Ws, int64_t B,
-                                              const double* w, double* a) {
+                                              const double* cs1, const double* w, double* a) {
     constexpr int NXM = msk_nxm<FAM>(), XQ = NM * NXM, XQD = XQ + NQ, ND = 2 * NQ, NX = XQ + 2 * NQ;
     constexpr bool FAT = (FAM & 1) != 0;
     constexpr int OM = 6 + ND, ODQ = NM * OM, OB = ODQ + NQ * ND;
@@ -1246,6 +1271,7 @@ __device__ __forceinline__ void msk_tangent_T(const MskGeom& G, const double* __
             a[o + 2] += c[2 * B] * w1 - C.inv_tau_fat * w[o + 2];
             a[o + 3] += c[3 * B] * w1 - C.inv_tau_fat * w[o + 3];
             a[o + 4] += c[4 * B] * w1 - C.inv_tau_fat * w[o + 4];
+            if (cs1) a[o + 4] += (cs1[mu] * C.inv_tauc) * w[o];
         }
 #pragma unroll
         for (int e = 0; e < ND; ++e) a[XQ + e] += c[(6 + e) * B] * w1;
@@ -1301,7 +1327,8 @@ __global__ void __launch_bounds__(256) k_msk_htan(const MskParams P, const MskGe
             for (int r = 0; r < NX; ++r) ts[(int64_t)r * nz * B] = txs[r];
             double tk[NX], dcs[NM];
             msk_icol_dcs<NM, FAM>(P, ic, (int64_t)k * Q + slot, dcs);
-            msk_tangent<NQ, NM, FAM>(G, P.residual, Wk + (int64_t)slot * NC * B, B, txs, tu, dcs, tk);
+            msk_tangent<NQ, NM, FAM>(G, P.residual, Wk + (int64_t)slot * NC * B, B, txs, tu, dcs,
+                                     msk_cs1<NM>(P, (int64_t)k * Q + slot), tk);
             const double cst = (ST == 4 && st == 2) ? h : 0.5 * h;
 #pragma unroll
             for (int r = 0; r < NX; ++r) {
@@ -1348,7 +1375,7 @@ __global__ void __launch_bounds__(256) k_msk_hadj(const MskParams P, const MskGe
                 mu[r] = wb * xb[r] + wa * yb[r];
                 MU[(((int64_t)k * Q + slot) * NX + r) * B + b] = mu[r];
             }
-            msk_tangent_T<NQ, NM, FAM>(G, Wk + (int64_t)slot * NC * B, B, mu, yb);
+            msk_tangent_T<NQ, NM, FAM>(G, Wk + (int64_t)slot * NC * B, B, msk_cs1<NM>(P, (int64_t)k * Q + slot), mu, yb);
 #pragma unroll
             for (int r = 0; r < NX; ++r) xn[r] += yb[r];
         }
@@ -1454,7 +1481,7 @@ __global__ void __launch_bounds__(256) k_msk_hpair(const MskParams P, const MskG
     } else {
         msk_stage_cs<NM, FAM>(P.cs, kq, nullptr, csl);
     }
-    msk_rhs<NQ, NM, FAM>(G, P.residual, csl, x, u, f);
+    msk_rhs<NQ, NM, FAM>(G, P.residual, csl, msk_cs1<NM>(P, kq), x, u, f);
     const int hi = I == J ? 0 : 1;  // Jet<2> second-order slots: (0,0), (1,0), (1,1)
     double acc = 0.0;
 #pragma unroll
@@ -1558,7 +1585,7 @@ __global__ void __launch_bounds__(256) k_msk_values(const MskParams P, const Msk
             for (int r = 0; r < NX; ++r) XS[(kq * NX + r) * B + b] = xs[r];
             double f[NX], csl[NM];
             msk_stage_cs<NM, FAM>(P.cs, kq, lam, csl);
-            msk_rhs<NQ, NM, FAM>(G, residual, csl, xs, u, f);
+            msk_rhs<NQ, NM, FAM>(G, residual, csl, msk_cs1<NM>(P, kq), xs, u, f);
             const double cst = (ST == 4 && st == 2) ? h : 0.5 * h;
 #pragma unroll
             for (int r = 0; r < NX; ++r) {
@@ -1609,7 +1636,7 @@ __global__ void __launch_bounds__(256) k_msk_stagecoef_par(const MskParams P, co
     } else {
         msk_stage_cs<NM, FAM>(P.cs, kq, nullptr, csl);
     }
-    msk_stage<NQ, NM, FAM>(G, P.residual, csl, xs, u, f, P.scratch + kq * NC * B + b, B);
+    msk_stage<NQ, NM, FAM>(G, P.residual, csl, msk_cs1<NM>(P, kq), xs, u, f, P.scratch + kq * NC * B + b, B);
 }
 
 // one stage's term T_q^T (G_q T_q[:, a]) of k_msk_hproj (thread = instance, column a, interval-stage kq)
@@ -1701,6 +1728,7 @@ __global__ void __launch_bounds__(256) k_msk_ivp(const MskParams P, const MskGeo
         for (int j = 0; j < P.m; ++j) {
             MskParams Pj = P1;
             Pj.cs = P.cs + (int64_t)j * (P.Q / P.m) * msk_cs_stride<NM, FAM>();  // sub-step j's stages inside interval k
+            if (P.cs1) Pj.cs1 = P.cs1 + (int64_t)j * (P.Q / P.m) * NM;
             msk_interval<NQ, NM, FAM, SCHEME>(Pj, G, k, x, u, lam);
             ++row;
 #pragma unroll

@@ -249,7 +249,7 @@ class FesMskModel:
                  stim_time: list = None, previous_stim: dict = None,
                  activate_force_length_relationship: bool = False, activate_force_velocity_relationship: bool = False,
                  activate_passive_force_relationship: bool = False, activate_residual_torque: bool = False,
-                 parameters=None, external_force_set=None):
+                 parameters=None, external_force_set=None, legacy_calcium: bool = False):
         if parameters is not None or external_force_set is not None:
             raise NotImplementedError("FesMskModel: parameters / external forces are not supported")
         self._model_sanity(muscles_model, activate_force_length_relationship, activate_force_velocity_relationship)
@@ -271,6 +271,9 @@ class FesMskModel:
         self.activate_residual_torque = activate_residual_torque
         self.parameters_list = parameters
         self.external_forces_set = external_force_set
+        # extension: the calcium-sum conventions of the revision that stored the reaching-task solutions (a window's
+        # first pulse left out once it holds several; the fatigue models' r0 from the Km state), CFX_MSK_LEGACY_CALCIUM
+        self.legacy_calcium = bool(legacy_calcium)
 
     @staticmethod
     def _model_sanity(muscles_model, activate_force_length_relationship, activate_force_velocity_relationship):
@@ -351,6 +354,8 @@ class FesMskModel:
             f |= _cfx.MSK_PASSIVE_FORCE
         if self.activate_residual_torque:
             f |= _cfx.MSK_RESIDUAL_TORQUE
+        if getattr(self, "legacy_calcium", False):
+            f |= _cfx.MSK_LEGACY_CALCIUM
         return f
 
 
@@ -369,7 +374,7 @@ class FesMskOcp:
 
     def __init__(self, model: FesMskModel, n_shooting, final_time, ode_solver, rows, objectives, x_bounds, x_init,
                  u_bounds, u_init, state_names, control_names, n_threads=1, use_sx=True, n_params=0, p_bounds=None,
-                 p_init=None, param_names=(), last_stim_idx=None, param_offset=None, marker_pairs=()):
+                 p_init=None, param_names=(), last_stim_idx=None, param_offset=None, marker_pairs=(), per_pulse=False):
         self.model = model
         self.n_shooting = n_shooting
         self.final_time = final_time
@@ -390,6 +395,8 @@ class FesMskOcp:
         self.param_offset = param_offset
         # SUPERIMPOSE_MARKERS rows after every interval's rows (cfx_msk_marker_pair dicts + marker names)
         self.marker_pairs = list(marker_pairs)
+        # pulse_width["per_pulse"]: the intervals that follow one pulse share its widths (rows after the marker rows)
+        self.per_pulse = bool(per_pulse)
 
     @property
     def n_marker_rows(self) -> int:
@@ -446,7 +453,8 @@ class FesMskOcp:
         return _cfx.MskHandle(
             chain=self.model.cfx_chain(), muscles=self.model.cfx_muscles(), scheme=self.ode_solver.scheme,
             n_steps=self.ode_solver.n_integration_steps, n_shooting=self.n_shooting, truncation=self.truncation,
-            final_time=float(self.final_time), stim_rows=self.stim_rows, batch=batch, flags=self.model.cfx_flags(),
+            final_time=float(self.final_time), stim_rows=self.stim_rows, batch=batch,
+            flags=self.model.cfx_flags() | (_cfx.MSK_PULSE_WIDTH_PER_PULSE if self.per_pulse else 0),
             layout={"aos": _cfx.LAYOUT_AOS, "soa": _cfx.LAYOUT_SOA}[layout], objectives=self.objectives,
             device=device, n_params=self.n_params, last_stim_idx=self.last_stim_idx, param_offset=self.param_offset,
             marker_pairs=self.marker_pairs)
@@ -467,7 +475,9 @@ class OcpFesMsk:
                     control_type: ControlType = ControlType.CONSTANT, n_threads: int = 1, external_forces: dict = None,
                     n_shooting: int | None = None, apply_custom_constraint: bool = False) -> FesMskOcp:
         """Same arguments as the reference (fes_ocp_dynamics.py:158-251).  Extensions: ``n_shooting`` overrides the
-        LCM node count of ``OcpFes.prepare_n_shooting``; ``apply_custom_constraint`` enforces
+        LCM node count of ``OcpFes.prepare_n_shooting``; ``pulse_width["per_pulse"]`` makes the intervals that follow
+        one pulse share its widths (the per-pulse parameters of the revision that stored the reaching-task solutions,
+        as band-local equality rows); ``apply_custom_constraint`` enforces
         ``msk_info["custom_constraint"]``.  The reference accepts that constraint list but never applies it: its
         ``_prepare_optimization_problem`` calls ``_build_constraints`` without it (fes_ocp_dynamics.py:107; the
         parameter is read at 424-450), so by default it is ignored here too, with a warning."""
@@ -521,8 +531,11 @@ class OcpFesMsk:
                 warnings.warn("msk_info['custom_constraint'] is not applied, as in the reference "
                               "(fes_ocp_dynamics.py:107 builds the constraints without it); pass "
                               "apply_custom_constraint=True to enforce it", stacklevel=2)
+        per_pulse = bool(pulse_width.get("per_pulse"))
+        if per_pulse and not isinstance(muscles[0], DingModelPulseWidthFrequency):
+            raise ValueError("pulse_width['per_pulse'] needs pulse-width (Ding2007) muscles")
         return FesMskOcp(model, n, final_time, ode_solver, rows, terms, x_bounds, x_init, u_bounds, u_init,
-                         state_names, control_names, n_threads, use_sx, marker_pairs=pairs, **par)
+                         state_names, control_names, n_threads, use_sx, marker_pairs=pairs, per_pulse=per_pulse, **par)
 
     @staticmethod
     def _build_constraints(model, n, custom_constraint) -> list:
@@ -581,7 +594,8 @@ class OcpFesMsk:
     @staticmethod
     def _fill_msk_dict(pulse_width, pulse_intensity, objective, msk_info):
         """fes_ocp_dynamics.py:253-301."""
-        dpw = {"fixed": None, "min": None, "max": None, "bimapping": False, "same_for_all_muscles": False}
+        dpw = {"fixed": None, "min": None, "max": None, "bimapping": False, "same_for_all_muscles": False,
+               "per_pulse": False}
         dobj = {"force_tracking": None, "end_node_tracking": None, "custom": None, "q_tracking": None,
                 "minimize_muscle_fatigue": False, "minimize_muscle_force": False, "minimize_residual_torque": False}
         dmsk = {"bound_type": None, "bound_data": None, "with_residual_torque": False, "custom_constraint": None}

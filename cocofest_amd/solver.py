@@ -77,6 +77,10 @@ class IpmOptions:
     # iterations, until one satisfies the filter; a rejected one starts the restoration phase.  Phase mode only
     soft_resto_pderror_reduction_factor: float = 0.0
     max_soft_resto_iters: int = 10
+    # extension (not Ipopt): a failed restoration phase restarts the main iteration from the phase's last point (zero
+    # constraint multipliers, empty filter) instead of stopping the instance with Restoration_Failed; the iteration
+    # budget still bounds it.  Off by default (Ipopt's behaviour); DESIGN.md section 5 has the multistart numbers
+    resto_failure_restart: bool = False
     # Ipopt's max_wall_time (s): the instances still iterating stop there (status -5); print_frequency_time (s, 0:
     # off): the native solver prints a progress line (iteration, instances iterating, in restoration) this often
     max_wall_time: float = 1e20
@@ -710,7 +714,8 @@ class BatchedIpm:
                 entered = failed & (iters < opt.max_iter)
                 xr, zl, zu, filt, fpos, its_r, rexit = self._restoration_phase(failed, x, zl, zu, g, theta, phi, mu,
                                                                                 tau, filt, fpos, iters)
-                back = entered & ((rexit == self.RS_OK) | (rexit == self.RS_BUDGET))
+                back = entered & ((rexit == self.RS_OK) | (rexit == self.RS_BUDGET) |
+                                  ((rexit == self.RS_FAILED) & bool(opt.resto_failure_restart)))
                 rstop = entered & ~back
                 x_new = torch.where(back[:, None], xr, x_acc)
                 iters = iters + its_r + rstop.long()  # a stopped instance takes no step below: count its iteration
@@ -1174,7 +1179,8 @@ _NATIVE_OPTIONS = ("tol", "max_iter", "acceptable_tol", "acceptable_iter", "mu_i
                    "delta_c", "curv_min", "max_soc", "kappa_soc", "watchdog_shortened_iter_trigger",
                    "watchdog_trial_iter_max", "limited_memory_max_history", "max_resto_iter", "resto_penalty",
                    "required_infeasibility_reduction", "filter_reset_trigger", "max_filter_resets", "max_wall_time",
-                   "print_frequency_time", "soft_resto_pderror_reduction_factor", "max_soft_resto_iters")
+                   "print_frequency_time", "soft_resto_pderror_reduction_factor", "max_soft_resto_iters",
+                   "resto_failure_restart")
 _HESSIAN_APPROXIMATION = {"exact": 0, "limited-memory": 1}
 _RESTORATION = {"step": 0, "phase": 1, None: 1}
 

@@ -227,6 +227,14 @@ int cfx_integrate(cfx_handle *h, const double *x0, const double *u, double *traj
 #define CFX_MSK_FORCE_VELOCITY 2u /* hill_coefficients.py:66-96 */
 #define CFX_MSK_PASSIVE_FORCE 4u  /* hill_coefficients.py:99-126 */
 #define CFX_MSK_RESIDUAL_TORQUE 8u
+/* Ding2007 muscles: consecutive intervals that follow the same pulse share their pulse widths — rows
+   u_k[m] - u_{k-1}[m] = 0 after the marker rows (the decision space of the per-pulse pulse-duration parameters of the
+   revision that stored examples/dynamics/reaching_task/result_file/*.pkl, with band-local rows) */
+#define CFX_MSK_PULSE_WIDTH_PER_PULSE 16u
+/* Ding muscles: that revision's calcium sum — a window's first pulse left out once it holds several, and the fatigue
+   models' r0 = Km + r0_km_relationship read from the Km state (today: km_rest + r0_km_relationship, ding2003.py:230-252;
+   tests/test_reference_solution.py measures both) */
+#define CFX_MSK_LEGACY_CALCIUM 32u
 /* objective kind for MSK problems: weight * (target_value / z_k)^2 at the nodes of the range
    (CustomObjective.minimize_overall_muscle_fatigue, cocofest/custom_objectives.py:80-101: a_rest / A) */
 #define CFX_OBJ_MAYER_INV 2
@@ -354,7 +362,8 @@ typedef struct cfx_ipm_options {
        original filter with |c|_1 <= required_infeasibility_reduction times the value where it started (the bound
        multipliers then take a Newton step for complementarity over the phase's dx, the constraint multipliers restart
        from zero, the filter from empty; the phase's iterations count among the instance's max_iter).  A failed line
-       search of the phase, max_resto_iter iterations of it, or a point of local infeasibility stop that instance
+       search of the phase resets p and n to their closed form at the phase's point (Ipopt's RestoRestorationPhase);
+       a second one in a row, max_resto_iter iterations of it, or a point of local infeasibility stop that instance
        (status CFX_IPM_RESTORATION_FAILED / CFX_IPM_INFEASIBLE_PROBLEM_DETECTED), as Ipopt's solve stops.  The phase's
        iterations run inside the same host iterations as the other instances' main iterations (one host iteration
        advances every instance by one iteration of its own).  CFX_RESTORATION_STEP — one minimum-norm step on c = 0
@@ -385,6 +394,10 @@ typedef struct cfx_ipm_options {
        at the trial point. */
     double soft_resto_pderror_reduction_factor; /* >= 0 */
     int32_t max_soft_resto_iters;               /* >= 0 */
+    /* extension, not Ipopt (default 0): a failed restoration phase (its line search failed twice in a row, or
+       max_resto_iter) restarts the main iteration from the phase's last point — zero constraint multipliers, an
+       empty filter — instead of stopping the instance with CFX_IPM_RESTORATION_FAILED */
+    int32_t resto_failure_restart;
 } cfx_ipm_options;
 #define CFX_HESSIAN_EXACT 0
 #define CFX_HESSIAN_LIMITED_MEMORY 1

@@ -12,6 +12,7 @@
 #   multistart:RUNS  scripts/msk_multistart_probe.py --native --runs RUNS (e.g. 64:0.1,512:0.1)
 #   specms:RUNS:SOFT the same with the BatchedIpm specification and soft_resto_pderror_reduction_factor SOFT
 #   py:SCRIPT[:ARGS] python SCRIPT ARGS (ARGS with commas for spaces), stdout to SCRIPT's name .txt
+#   bin:PATH[:ARGS]  a binary built here (e.g. scripts/micro/bin/colloc_bw), stdout to its name .txt
 set -o pipefail
 out=gpurun_out/$1
 shift
@@ -50,6 +51,12 @@ for step in "$@"; do
               [ "$spec" != "$script" ] && args=${spec#*:}
               # shellcheck disable=SC2086
               run 900 "$(basename "$script" .py).txt" python3 -u "$script" ${args//,/ } ;;
+        bin:*) spec=${step#bin:}
+               exe=${spec%%:*}
+               args=""
+               [ "$spec" != "$exe" ] && args=${spec#*:}
+               # shellcheck disable=SC2086
+               run 300 "$(basename "$exe").txt" "$exe" ${args//,/ } ;;
         *) echo "unknown step $step"; exit 2 ;;
     esac
 done

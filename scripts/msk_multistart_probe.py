@@ -2,7 +2,7 @@
 65,536 (RK4 x 1).
 
 Usage: python scripts/msk_multistart_probe.py [--native] [--hess-only] [--runs B:amp,B:amp,...] [--max-iter N]
-                                              [--wall SECONDS] [--soft FACTOR] [--jsonl FILE]
+                                              [--wall SECONDS] [--soft FACTOR] [--restart] [--jsonl FILE]
 Each run prints one line (converged count, Ipopt status histogram, restoration phases / iterations, wall time); the
 native solver prints a progress line on stderr every 20 s (print_frequency_time)."""
 import argparse
@@ -31,6 +31,7 @@ ap.add_argument("--max-iter", type=int, default=1000)
 ap.add_argument("--wall", type=float, default=1e20)
 ap.add_argument("--jsonl", default=None)
 ap.add_argument("--soft", type=float, default=None, help="soft_resto_pderror_reduction_factor (default: the option's)")
+ap.add_argument("--restart", action="store_true", help="resto_failure_restart (extension: a failed phase restarts)")
 args = ap.parse_args()
 
 ocp = bench.msk_build(5)
@@ -44,6 +45,8 @@ for B, amp in runs:
     v0[:, free] = np.clip(v0[:, free] + amp * rng.uniform(-1, 1, (B, free.sum())) * span, lb[free], ub[free])
     cls = NativeIpm if args.native else BatchedIpm
     extra = {} if args.soft is None else {"soft_resto_pderror_reduction_factor": args.soft}
+    if args.restart:
+        extra["resto_failure_restart"] = True
     opts = IpmOptions(tol=1e-6, max_iter=args.max_iter, max_wall_time=args.wall, print_frequency_time=20.0, **extra)
     ipm = cls(ocp, batch=B, options=opts)
     res = ipm.solve(v0)
@@ -57,6 +60,7 @@ for B, amp in runs:
                f_converged_max=float(res.f[conv].max()) if conv.any() else None,
                resto_phases=st.get("resto_phases"), resto_iterations=st.get("resto_iterations"),
                host_iterations=st.get("iterations"), soft=opts.soft_resto_pderror_reduction_factor,
+               restart=opts.resto_failure_restart,
                soft_steps=getattr(ipm, "soft_steps", st.get("soft_steps")))
     print(json.dumps(rec), flush=True)
     if args.jsonl:

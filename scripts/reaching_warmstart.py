@@ -6,11 +6,14 @@ the target at node 1000, no residual torque) is solved by cfx_ipm starting at th
 (tests/golden/reaching_pulse_duration_*.npz).  The stored point solves the stored revision's NLP (tests/
 test_reference_solution.py); the product states today's reference, whose calcium sum keeps every pulse of the window
 (the stored Cn rows miss by 8.6e-3 after the second pulse under it) and whose pulse width is a control per interval,
-not a parameter per pulse.  So the solve must move; this script measures how far: start and end objective, the
-largest constraint row at the start, the change of every state and pulse width relative to its range, and how many
-pulse widths sit on a bound.  One JSON line per objective.
+not a parameter per pulse.  By default the product runs the stored revision's conventions (FesMskModel(
+legacy_calcium=True), pulse_width["per_pulse"]: tests/test_reference_solution.py::legacy_product), where the stored
+point is feasible; --current runs today's.  The script measures how far the solve moves: start and end objective,
+the largest constraint row at the start, the change of every state and pulse width relative to its range, and how
+many pulse widths sit on a bound.  One JSON line per objective.
 
-Usage (GPU): python scripts/reaching_warmstart.py [--objectives fatigue,force] [--max-iter 3000] [--wall 400]"""
+Usage (GPU): python scripts/reaching_warmstart.py [--objectives fatigue,force] [--max-iter 3000] [--wall 400]
+             [--current]"""
 import argparse
 import json
 import os
@@ -29,6 +32,8 @@ ap.add_argument("--objectives", default="fatigue,force")
 ap.add_argument("--max-iter", type=int, default=3000)
 ap.add_argument("--wall", type=float, default=400.0)
 ap.add_argument("--out", default=None, help="append the JSON lines to this file")
+ap.add_argument("--current", action="store_true",
+                help="today's calcium conventions and per-interval widths instead of the stored revision's")
 args = ap.parse_args()
 
 
@@ -60,7 +65,7 @@ def build(objective):
 def run(objective):
     from cocofest_amd.solver import IpmOptions, NativeIpm
 
-    ocp = build(objective)
+    ocp = build(objective) if args.current else R.legacy_product(objective)
     X, U = R.trajectory(R.load(objective))
     nm = len(R.MUSCLES)
     nx, nz = ocp.nx, ocp.nx + ocp.nu
@@ -87,7 +92,8 @@ def run(objective):
     pwlo, pwhi = lb[nx], ub[nx]
     pidx = R.pulse_index()
     spread = max(float(np.ptp(pw[pidx == i], axis=0).max()) for i in range(int(pidx.max()) + 1))
-    out = {"objective": objective, "status": int(res.status[0]), "converged": bool(res.converged[0]),
+    out = {"objective": objective, "conventions": "current" if args.current else "stored revision (legacy, per pulse)",
+           "status": int(res.status[0]), "converged": bool(res.converged[0]),
            "iterations": int(res.iterations[0]), "wall_s": wall, "kkt_error": float(res.kkt_error[0]),
            "f_start": f0, "f_end": float(res.f[0]), "g_start_max": float(np.abs(g0).max()),
            "g_start_rows_over_1e-6": int((np.abs(g0) > 1e-6).sum()),

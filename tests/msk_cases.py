@@ -67,9 +67,10 @@ def cfg5(**kw):
 
 
 def product_ocp(model, biomod, muscles, scheme, m, fv, residual, fatigue, qdot_end, truncation, bound=(5, 90),
-                passive=False, markers=(), bound_type="start_end"):
+                passive=False, markers=(), bound_type="start_end", legacy=False):
     """``markers``: SUPERIMPOSE_MARKERS constraints as dicts first, second, node (int or "end"), axes (indices),
-    passed through msk_info["custom_constraint"] with apply_custom_constraint=True."""
+    passed through msk_info["custom_constraint"] with apply_custom_constraint=True.  ``legacy``: the stored
+    reaching-task revision's calcium sum (FesMskModel(legacy_calcium=True), CFX_MSK_LEGACY_CALCIUM)."""
     import cocofest_amd as C
 
     pint = None
@@ -79,7 +80,8 @@ def product_ocp(model, biomod, muscles, scheme, m, fv, residual, fatigue, qdot_e
     mm = C.FesMskModel(biorbd_path=biomod_path(biomod),
                        muscles_model=[cls(muscle_name=n, sum_stim_truncation=truncation) for n in muscles],
                        stim_time=list(STIMS), activate_force_length_relationship=fv,
-                       activate_force_velocity_relationship=fv, activate_residual_torque=residual)
+                       activate_force_velocity_relationship=fv, activate_residual_torque=residual,
+                       legacy_calcium=legacy)
     obj = {}
     if qdot_end:
         ol = C.ObjectiveList()
@@ -110,13 +112,13 @@ def product_ocp(model, biomod, muscles, scheme, m, fv, residual, fatigue, qdot_e
 
 
 def oracle_problem(model, biomod, muscles, scheme, m, fv, residual, fatigue, qdot_end, truncation, bound=(5, 90),
-                   passive=False, markers=(), bound_type="start_end"):
+                   passive=False, markers=(), bound_type="start_end", legacy=False):
     bm = json.loads(pathlib.Path(biomod_path(biomod)).read_text())
     n = O.prepare_n_shooting(STIMS, 1)
     tab = O.stim_table(STIMS, n, 1, truncation)
     mus = [M.MskMuscle(model=model, name=nm, c=O.model_constants(model)) for nm in muscles]
     pb = M.MskProblem(bm=bm, muscles=mus, rows=tab.rows, n_shooting=n, final_time=1.0, scheme=scheme, m=m, fv_on=fv,
-                      fp_on=passive, residual=residual)
+                      fp_on=passive, residual=residual, legacy=legacy)
     if _hmed(model):  # one block of n_stim intensity parameters per muscle; node k's window ends at its last pulse
         pb.n_params = len(STIMS) * len(muscles)
         pb.param_offset = [i * len(STIMS) for i in range(len(muscles))]

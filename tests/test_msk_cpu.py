@@ -321,3 +321,25 @@ def test_c_port_matches_numpy_oracle(kw):
         k = pb.n_shooting - 1
         Jr = M.continuity_jacobian(pb, v[b], k)
         np.testing.assert_allclose(J[b, k], Jr, rtol=1e-11, atol=1e-12 * np.abs(Jr).max())
+
+
+def test_legacy_calcium_and_per_pulse_flags():
+    """Extensions for the stored reaching-task revision: FesMskModel(legacy_calcium=True) sets CFX_MSK_LEGACY_CALCIUM,
+    pulse_width["per_pulse"] sets CFX_MSK_PULSE_WIDTH_PER_PULSE on the handle (Ding2007 muscles only)."""
+    from cocofest_amd import _cfx
+    from tests import msk_cases as MC
+    from tests import test_reference_solution as R
+
+    ocp = MC.product_ocp(**MC.cfg5(legacy=True))
+    assert ocp.model.cfx_flags() & _cfx.MSK_LEGACY_CALCIUM and not ocp.per_pulse
+    assert not MC.product_ocp(**MC.cfg5()).model.cfx_flags() & _cfx.MSK_LEGACY_CALCIUM
+    assert R.legacy_product().per_pulse
+    with pytest.raises(ValueError, match="per_pulse"):
+        import cocofest_amd as C
+
+        mm = C.FesMskModel(biorbd_path=MC.biomod_path("arm26_biceps_triceps"),
+                           muscles_model=[C.DingModelFrequencyWithFatigue(muscle_name="BIClong")],
+                           stim_time=[0.0, 0.1], activate_force_length_relationship=True,
+                           activate_force_velocity_relationship=True)
+        C.OcpFesMsk.prepare_ocp(model=mm, final_time=0.2, pulse_width={"per_pulse": True},
+                                msk_info={"bound_type": "start", "bound_data": [0, 5]})

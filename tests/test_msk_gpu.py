@@ -41,6 +41,11 @@ CASES = {
     "rotated_xy_d07f": MC.cfg5(biomod=MC.rotated_biomod(("x", "y"))),
     "rotated_yx_d03_residual": MC.cfg5(biomod=MC.rotated_biomod(("y", "x")), model="ding2003", fatigue=False,
                                        residual=True, m=2),
+    # the stored reaching-task revision's calcium sum (CFX_MSK_LEGACY_CALCIUM: a window's first pulse left out once
+    # it holds several; r0 from the Km state — cn_dot affine in Km, one more J_g entry per muscle)
+    "cfg5_legacy": MC.cfg5(legacy=True),
+    "d03f_rk2_legacy": MC.cfg5(model="ding2003_with_fatigue", scheme="RK2", m=2, legacy=True),
+    "d07_rk1_legacy": MC.cfg5(model="ding2007", scheme="RK1", m=3, fatigue=False, legacy=True),
 }
 
 
@@ -146,7 +151,7 @@ def _lagrangian_block_fd(pb, v, lam_k, k, rel=1e-4):
 
 
 @pytest.mark.parametrize("case", ["cfg5_d07f_rk4", "d07_rk1_residual", "d03_rk4_residual", "d07f_rk2", "d07f_passive",
-                                  "biceps_1dof_d07f", "arm26_6muscles_d03_rk1"])
+                                  "biceps_1dof_d07f", "arm26_6muscles_d03_rk1", "cfg5_legacy", "d03f_rk2_legacy"])
 def test_msk_hessian_matches_oracle(case):
     """Stage-wise Hessian (stage tangents, adjoints swept back through m sub-steps, per-stage pair Hessians) against
     finite differences of the oracle's complex-step gradients, on two instances of a batch of three."""
