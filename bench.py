@@ -316,20 +316,36 @@ def collocation_pmc():
         return None
 
 
+def collocation_pattern_ceiling():
+    """The collocation kernel's traffic pattern with no arithmetic (scripts/micro/colloc_bw.hip, committed run):
+    ms per launch by variant, or None."""
+    f = ROOT / "profiles" / "round4" / "collocation" / "colloc_bw.jsonl"
+    try:
+        return {d["variant"]: d["ms"] for d in map(json.loads, f.read_text().splitlines()) if d.get("batch") ==
+                COLLOCATION_BATCH}
+    except Exception:
+        return None
+
+
 def collocation_section(device, steps=50):
     """The same cfg-2 problem transcribed by direct collocation: g + J_g throughput of k_colloc over a device-resident
-    batch in 64-instance tiles (the handle's default launch shape: two instances per lane, intervals-fast grid), its
-    roofline (algorithmic HBM bytes — read v, write g and J_g — over the launch time from HIP events on the launch
-    stream), and the fused g + J_g + Hessian launch (cfx_eval_all_h, one kernel) timed the same way."""
+    SoA batch (the handle's default launch shape: two instances per lane, intervals-fast grid; 64-instance tiles timed
+    beside it), its roofline (algorithmic HBM bytes — read v, write g and J_g — over the launch time from HIP events on
+    the launch stream) against the pattern's own ceiling (the same traffic with no arithmetic), and the fused g + J_g +
+    Hessian launch (cfx_eval_all_h, one kernel) timed the same way."""
     import torch
 
     ocp = build_collocation()
     B = COLLOCATION_BATCH
-    h = ocp.nlp(batch=B, layout="tiled64", device=device)
     dev = f"cuda:{device}"
-    v = collocation_synthetic(ocp, B, dev)
-    g = torch.empty((B // 64, h.ng, 64), dtype=torch.float64, device=dev)
-    jac = torch.empty((B // 64, h.nnz_jac, 64), dtype=torch.float64, device=dev)
+    vt = collocation_synthetic(ocp, B, dev)
+    ht = ocp.nlp(batch=B, layout="tiled64", device=device)
+    gt = torch.empty((B // 64, ht.ng, 64), dtype=torch.float64, device=dev)
+    jt = torch.empty((B // 64, ht.nnz_jac, 64), dtype=torch.float64, device=dev)
+    h = ocp.nlp(batch=B, layout="soa", device=device)
+    v = vt.transpose(1, 2).reshape(B, h.nv).T.contiguous()  # tiles -> SoA (nv, B)
+    g = torch.empty((h.ng, B), dtype=torch.float64, device=dev)
+    jac = torch.empty((h.nnz_jac, B), dtype=torch.float64, device=dev)
 
     def timed(fn, n):
         for _ in range(5):
@@ -343,6 +359,9 @@ def collocation_section(device, steps=50):
         torch.cuda.synchronize()
         return e0.elapsed_time(e1) / n
 
+    ms_tiled = timed(lambda: ht.eval_all(vt, g=gt, jac=jt), steps)
+    ht.close()
+    del gt, jt
     ms = timed(lambda: h.eval_all(v, g=g, jac=jac), steps)
     nbytes = 8 * (h.nv + h.ng + h.nnz_jac)
     achieved = nbytes * B / (ms * 1e-3) / 1e9
@@ -352,18 +371,24 @@ def collocation_section(device, steps=50):
     ms_keep = timed(lambda: h.eval_all(v, g=g, jac=jac, keep_constant_jac=True), steps)
     nbytes_keep = 8 * (h.nv + h.ng + h.nnz_jac - n_const)
     pmc = collocation_pmc()
-    lam = torch.randn((B // 64, h.ng, 64), dtype=torch.float64, device=dev, generator=torch.Generator(dev).manual_seed(3))
+    lam = torch.randn((h.ng, B), dtype=torch.float64, device=dev, generator=torch.Generator(dev).manual_seed(3))
     of = torch.ones((B,), dtype=torch.float64, device=dev)
-    hs = torch.empty((B // 64, h.nnz_hess, 64), dtype=torch.float64, device=dev)
+    hs = torch.empty((h.nnz_hess, B), dtype=torch.float64, device=dev)
     ms_h = timed(lambda: h.eval_all_h(v, of, lam, g=g, jac=jac, hess=hs), max(steps // 5, 5))
     nbytes_h = 8 * (2 * h.nv + 2 * h.ng + h.nnz_jac + h.nnz_hess)  # + read lambda, write the Hessian values
     shape = h.launch_shape()
     h.close()
+    ceil = collocation_pattern_ceiling()
     return {"workload": "cfg2 by direct collocation, Legendre degree 4 (nv = 202, ng = 200); one launch = g + J_g of "
                         "every instance", "batch": B, "nv": ocp.nv, "ng": int(ocp.n_shooting * ocp.ngk),
-            "nnz_jac": nbytes // 8 - ocp.nv - ocp.n_shooting * ocp.ngk, "layout": "CFX_LAYOUT_TILED64",
+            "nnz_jac": nbytes // 8 - ocp.nv - ocp.n_shooting * ocp.ngk, "layout": "CFX_LAYOUT_SOA",
             "launch_shape": shape, "ms_per_launch": ms, "instance_evals_per_s": B / (ms * 1e-3),
             "achieved_GBps": achieved, "bytes_per_instance": nbytes,
+            "tiled64_ms_per_launch": ms_tiled,
+            "pattern_ceiling": None if not ceil else {
+                "source": "scripts/micro/colloc_bw.hip (profiles/round4/collocation/colloc_bw.jsonl): the same reads "
+                          "and stores, no arithmetic", "soa_nt_ms": ceil.get("soa_nt"), "tiled_nt_ms": ceil.get("tiled_nt"),
+                "kernel_over_pattern_soa": ceil["soa_nt"] / ms if ceil.get("soa_nt") else None},
             "roofline": {"bound": "hbm", "kernel": "cfx::k_colloc<DING2003, TMAX=1, DEG=4, NI=2>", "achieved": achieved,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                          "traffic": pmc.get("hbm_bytes_per_launch") if pmc else None,
@@ -572,13 +597,21 @@ def msk_throughput(local, dist, world, rank, backend, steps=10, B=1 << 16):
            "kernels": "k_msk_values + k_msk_stagecoef_par + k_msk_tangents_lds (compute-bound: FP64 VALU, see profiles/)"}
     pmc = msk_pmc()
     if pmc and pmc.get("batch") == B:
-        # compute-bound: the VALU issue rate of the step's three kernels (committed SQ_INSTS_VALU per step over the
-        # step's kernel time measured here) against the measured FP64 FMA issue peak
-        achieved = pmc["valu_wave_instr_per_step"] / (out["kernel_ms_per_step"] * 1e-3)
+        # compute-bound: the FP64 instruction issue rate of the step's three kernels (committed SQ_INSTS_VALU_{FMA,
+        # MUL,ADD,TRANS}_F64 per step over the step's kernel time measured here) against the measured FP64 FMA issue
+        # peak; the all-VALU rate beside it (an upper bound on FP64-pipe use)
+        f64 = pmc.get("f64_wave_instr_per_step")
+        valu = pmc.get("valu_wave_instr_per_step")
+        t = out["kernel_ms_per_step"] * 1e-3
+        achieved = (f64 if f64 else valu) / t
+        traffic = pmc.get("hbm_bytes_per_step")
         out["roofline"] = {"bound": "fp64_valu", "achieved": achieved, "peak": FP64_FMA_ISSUE_PEAK,
-                           "unit": "VALU wave-instr/s", "frac": achieved / FP64_FMA_ISSUE_PEAK,
-                           "traffic": pmc.get("hbm_bytes_per_step"), "per_kernel": pmc.get("kernels"),
-                           "source": pmc.get("source")}
+                           "unit": "FP64 wave-instr/s" if f64 else "VALU wave-instr/s",
+                           "frac": achieved / FP64_FMA_ISSUE_PEAK,
+                           "valu_frac": valu / t / FP64_FMA_ISSUE_PEAK if valu else None,
+                           "traffic": traffic, "traffic_over_algorithmic": traffic / (nbytes * B) if traffic else None,
+                           "traffic_GBps": traffic / t / 1e9 if traffic else None,
+                           "per_kernel": pmc.get("kernels"), "source": pmc.get("source")}
     h.close()
     return out, ocp
 

@@ -238,9 +238,9 @@ __device__ __forceinline__ void colloc_interval(const KParams& P, const double* 
 // shooting launch (interval chunks on grid.x when P.ifast, instance blocks on grid.y).  Each interval reads its own
 // block (x^0 carried from the previous interval's x_{k+1}) and x_{k+1}^0; no recursion, so the intervals per thread
 // only shape the launch (fewer, longer waves; the carried x^0 is read once).
-template <int MODEL, int TMAX, int DEG, int NI, bool PLAIN = false>
-__global__ void __launch_bounds__(256) k_colloc(const KParams P, const double* __restrict__ V, double* __restrict__ G,
-                                                double* __restrict__ J) {
+template <int MODEL, int TMAX, int DEG, int NI, bool PLAIN>
+__device__ __forceinline__ void colloc_thread(const KParams& P, const double* __restrict__ V, double* __restrict__ G,
+                                              double* __restrict__ J) {
     constexpr int NX = nx_of(MODEL);
     const unsigned bi = P.ifast ? blockIdx.y : blockIdx.x, bk = P.ifast ? blockIdx.x : blockIdx.y;
     const int64_t b0 = ((int64_t)bi * blockDim.x + threadIdx.x) * NI;
@@ -255,6 +255,18 @@ __global__ void __launch_bounds__(256) k_colloc(const KParams P, const double* _
         for (int r = 0; r < NX; ++r) ld_lane<NI>(V + vb + ((int64_t)k0 * P.nz + r) * ES, xc[r]);
     }
     for (int k = k0; k < k1; ++k) colloc_interval<MODEL, TMAX, DEG, NI, PLAIN>(P, V, G, J, k, ES, vb, gb, jb, xc);
+}
+template <int MODEL, int TMAX, int DEG, int NI, bool PLAIN = false>
+__global__ void __launch_bounds__(256) k_colloc(const KParams P, const double* __restrict__ V, double* __restrict__ G,
+                                                double* __restrict__ J) {
+    colloc_thread<MODEL, TMAX, DEG, NI, PLAIN>(P, V, G, J);
+}
+// occupancy probe (CFX_COLLOC_STORE=w4 / w4plain): the same thread body held to 128 VGPRs (4 waves per SIMD; the
+// default instantiation of the bench's shape takes 198 VGPRs, 2 waves)
+template <int MODEL, int TMAX, int DEG, int NI, bool PLAIN>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k_colloc_w4(
+    const KParams P, const double* __restrict__ V, double* __restrict__ G, double* __restrict__ J) {
+    colloc_thread<MODEL, TMAX, DEG, NI, PLAIN>(P, V, G, J);
 }
 
 // Lagrangian Hessian of the collocation defects: sum_{j,r} lambda_{k,j,r} (-dt) d^2 f_r(x_k^j, u_k).  Local

@@ -9,14 +9,15 @@ namespace cfx {
 
 // grid as the shooting launch: interval chunks of P.kpt intervals on grid.x when P.ifast (the chunks of one instance
 // block, which write one region of each 64-instance output tile, dispatched together), instance blocks on grid.y
-// CFX_COLLOC_STORE=plain: ordinary instead of non-temporal output stores (store-policy probe, bench's instantiation
-// only; read once per process)
-static bool colloc_plain_stores() {
-    static const bool plain = [] {
+// CFX_COLLOC_STORE (probe of the bench's instantiation only, read once per process): "plain" — ordinary instead of
+// non-temporal output stores; "w4" / "w4plain" — the kernel held to 4 waves per SIMD.  Returns bit 0 plain, bit 1 w4
+static int colloc_variant() {
+    static const int v = [] {
         const char* e = getenv("CFX_COLLOC_STORE");
-        return e && strcmp(e, "plain") == 0;
+        if (!e) return 0;
+        return (strstr(e, "plain") ? 1 : 0) | (strncmp(e, "w4", 2) == 0 ? 2 : 0);
     }();
-    return plain;
+    return v;
 }
 
 template <int MODEL, int TMAX, int DEG, int NI>
@@ -27,9 +28,14 @@ static hipError_t colloc_deg(const KParams& P, const double* V, double* G, doubl
     if (nbi > (unsigned)kMaxGridY) Q.ifast = 0;  // instance blocks must fit grid.y in the intervals-fast order
     dim3 grid(Q.ifast ? nbk : nbi, Q.ifast ? nbi : nbk);
     if constexpr (MODEL == M_D03 && DEG == 4 && NI == 2) {
-        if (colloc_plain_stores()) {
-            hipLaunchKernelGGL((k_colloc<MODEL, TMAX, DEG, NI, true>), grid, dim3(kBlock), 0, s, Q, V, G, J);
-            return hipGetLastError();
+        switch (colloc_variant()) {
+            case 1: hipLaunchKernelGGL((k_colloc<MODEL, TMAX, DEG, NI, true>), grid, dim3(kBlock), 0, s, Q, V, G, J);
+                    return hipGetLastError();
+            case 2: hipLaunchKernelGGL((k_colloc_w4<MODEL, TMAX, DEG, NI, false>), grid, dim3(kBlock), 0, s, Q, V, G, J);
+                    return hipGetLastError();
+            case 3: hipLaunchKernelGGL((k_colloc_w4<MODEL, TMAX, DEG, NI, true>), grid, dim3(kBlock), 0, s, Q, V, G, J);
+                    return hipGetLastError();
+            default: break;
         }
     }
     hipLaunchKernelGGL((k_colloc<MODEL, TMAX, DEG, NI>), grid, dim3(kBlock), 0, s, Q, V, G, J);

@@ -521,8 +521,9 @@ __global__ void __launch_bounds__(kIB) k_ipm_begin(const IpmK K, int mode, int s
 //   RESTO : [[Sigma + I, J^T], [J, -delta_c]], rhs [0; -g]            (restoration step)
 __global__ void __launch_bounds__(kIB) k_ipm_kkt(const IpmK K, int mode) {
     const int64_t b = blockIdx.x;
-    const int64_t p = (int64_t)blockIdx.y * kIB + threadIdx.x;
     const int64_t NE = K.NE_tot;
+    // grid-stride over the entries: grid.y is capped at kMaxY (a 1,500-interval MSK KKT matrix has ~18 M entries)
+    for (int64_t p = (int64_t)blockIdx.y * kIB + threadIdx.x; p < NE || p < K.nK; p += (int64_t)gridDim.y * kIB) {
     if (p < NE) {
         double v = 0.0;
         const double* hv = K.hv + b * K.nnzh;
@@ -574,6 +575,7 @@ __global__ void __launch_bounds__(kIB) k_ipm_kkt(const IpmK K, int mode) {
         else
             r = p < nf ? 0.0 : -K.gS[b * K.m + (p - nf)];
         K.rb[b * K.nKp + K.pos[p]] = r;
+    }
     }
 }
 
@@ -2790,7 +2792,7 @@ static int ipm_create_common(cfx_ipm* s, const cfx_sizes& sz, int layout, const 
     }
     const int64_t ncc = ccq.size();
     const int64_t NE_A = P * nA * ldab, NE = NE_A + P * na * nA + ncc + npb * npb;
-    if (nh >= (1 << kSrcShift) || nj >= (1 << kSrcShift) || NE >= INT32_MAX || (NE + kIB - 1) / kIB > kMaxY) {
+    if (nh >= (1 << kSrcShift) || nj >= (1 << kSrcShift) || NE >= INT32_MAX) {
         s->err = "cfx_ipm_create: KKT band too large";
         return create_fail(s, CFX_EUNSUPPORTED);
     }
@@ -3017,7 +3019,8 @@ struct Run {
     }
     int kkt_factor(int mode) {
         const IpmK& K = s->K;
-        hipLaunchKernelGGL(k_ipm_kkt, dim3((unsigned)K.B, (unsigned)((K.NE_tot + kIB - 1) / kIB)), dim3(kIB), 0, st,
+        const int64_t nblk = (std::max<int64_t>(K.NE_tot, K.nK) + kIB - 1) / kIB;
+        hipLaunchKernelGGL(k_ipm_kkt, dim3((unsigned)K.B, (unsigned)std::min<int64_t>(nblk, kMaxY)), dim3(kIB), 0, st,
                            K, mode);
         IPM_HIP(s, hipGetLastError());
         if (K.np) {  // blocks + border: factor the blocks, A_q^-1 [Cr_q | r_q] (parallel right-hand sides), Schur

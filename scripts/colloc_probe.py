@@ -4,7 +4,7 @@ each shape runs in a child process (cfx_create reads the overrides), alternating
 
 Usage (lists separated by ',' or '+'): python scripts/colloc_probe.py [--shapes -:-:-,1:1:0,...] [--layouts tiled64,soa] [--stores nt,plain]
                                       [--rounds 2] [--steps 200]
-With --pmc-only: the default shape once, 20 launches (the process rocprofv3 --pmc wraps)."""
+With --pmc-only: the default shape once on the first of --layouts, 20 launches (the process rocprofv3 --pmc wraps)."""
 import argparse
 import json
 import os
@@ -62,8 +62,8 @@ def child(layout, steps):
 if args.child:
     print(json.dumps(child(args.child, args.steps)), flush=True)
     sys.exit(0)
-if args.pmc_only:
-    print(json.dumps(child("tiled64", 20)), flush=True)
+if args.pmc_only:  # the bench's layout (SoA), 20 launches
+    print(json.dumps(child(re.split(r"[,+]", args.layouts)[0], 20)), flush=True)
     sys.exit(0)
 for rnd in range(args.rounds):
     for shape in re.split(r"[,+]", args.shapes):

@@ -13,6 +13,9 @@
 #   specms:RUNS:SOFT the same with the BatchedIpm specification and soft_resto_pderror_reduction_factor SOFT
 #   py:SCRIPT[:ARGS] python SCRIPT ARGS (ARGS with commas for spaces), stdout to SCRIPT's name .txt
 #   bin:PATH[:ARGS]  a binary built here (e.g. scripts/micro/bin/colloc_bw), stdout to its name .txt
+#   env:NAME=VALUE   export NAME=VALUE for the steps after it (e.g. env:CFX_LIB=cocofest_amd/libcfx_recip.so)
+#   pmc:CTRS[@LABEL]:SCRIPT[:ARGS]  rocprofv3 --pmc CTRS ('+'-separated, one pass; FETCH_SIZE and WRITE_SIZE each
+#                    alone) over python3 SCRIPT ARGS -> pmc_[LABEL_]<first counter>/
 set -o pipefail
 out=gpurun_out/$1
 shift
@@ -57,6 +60,21 @@ for step in "$@"; do
                [ "$spec" != "$exe" ] && args=${spec#*:}
                # shellcheck disable=SC2086
                run 300 "$(basename "$exe").txt" "$exe" ${args//,/ } ;;
+        pmc:*) spec=${step#pmc:}
+               ctr=${spec%%:*}
+               rest=${spec#*:}
+               script=${rest%%:*}
+               args=""
+               [ "$rest" != "$script" ] && args=${rest#*:}
+               # shellcheck disable=SC2086
+               tag=${ctr%%+*}
+               if [[ "$ctr" == *@* ]]; then tag="${ctr#*@}_${tag%%@*}"; ctr=${ctr%%@*}; fi
+               # shellcheck disable=SC2086
+               run 180 "pmc_${tag}.log" timeout -s KILL 150 rocprofv3 --pmc ${ctr//+/ } -d "$out/pmc_${tag}" -o run -- \
+                   python3 "$script" ${args//,/ } ;;
+        env:*) kv=${step#env:}
+               export "${kv%%=*}=${kv#*=}"
+               echo "== export ${kv%%=*}=${kv#*=}" ;;
         *) echo "unknown step $step"; exit 2 ;;
     esac
 done

@@ -4,7 +4,7 @@
 // interval), write 10 g rows and 56 J_g values — 1,616 B read and 10,560 B written per instance, the kernel's
 // algorithmic bytes.  Same grid as k_colloc's default shape (thread = 2 adjacent instances x 1 interval, interval
 // chunks on grid.x), SoA or 64-instance tiles, non-temporal or plain 16-byte stores; plus a pure write stream and a
-// pure read stream of the same byte counts.  Prints one line per variant: ms per launch and TB/s of the algorithmic
+// pure read stream over the J_g buffer.  Prints one line per variant: ms per launch and TB/s of the algorithmic
 // bytes (12,176 B per instance).
 //   hipcc -O3 --offload-arch=gfx950 scripts/micro/colloc_bw.hip -o /tmp/colloc_bw && /tmp/colloc_bw
 #include <hip/hip_runtime.h>
@@ -113,7 +113,7 @@ int main(int argc, char** argv) {
     CHECK(hipMalloc(&J, sizeof(double) * EJ * B));
     CHECK(hipMalloc(&out, sizeof(double)));
     CHECK(hipMemset(V, 0, sizeof(double) * EV * B));
-    const double bytes = 8.0 * (EV + EG + EJ) * (double)B, wbytes = 8.0 * (EG + EJ) * (double)B;
+    const double bytes = 8.0 * (EV + EG + EJ) * (double)B;
     const dim3 grid(N, (unsigned)((B / 2 + 255) / 256));
     auto report = [&](const char* name, double ms, double nbytes) {
         std::printf("{\"variant\": \"%s\", \"batch\": %lld, \"ms\": %.4f, \"TBps\": %.3f, \"frac_8TBps\": %.3f}\n", name,
@@ -127,13 +127,15 @@ int main(int argc, char** argv) {
            bytes);
     report("tiled_plain",
            timed([&] { hipLaunchKernelGGL((k_pattern<true, false>), grid, dim3(256), 0, 0, V, G, J, B); }, reps), bytes);
-    const int64_t w2 = (int64_t)(wbytes / 16);
-    report("wstream_nt (write bytes only)",
-           timed([&] { hipLaunchKernelGGL((k_wstream<true>), dim3(4096), dim3(256), 0, 0, J, w2, 1.0); }, reps), wbytes);
-    report("wstream_plain (write bytes only)",
-           timed([&] { hipLaunchKernelGGL((k_wstream<false>), dim3(4096), dim3(256), 0, 0, J, w2, 1.0); }, reps), wbytes);
-    report("rstream (J buffer, write bytes)",
-           timed([&] { hipLaunchKernelGGL(k_rstream, dim3(4096), dim3(256), 0, 0, J, w2, out); }, reps), wbytes);
+    // pure streams over the J buffer alone (its EJ * B doubles: the bulk of the written bytes)
+    const int64_t w2 = (int64_t)EJ * B / 2;
+    const double jbytes = 8.0 * EJ * (double)B;
+    report("wstream_nt (J bytes)",
+           timed([&] { hipLaunchKernelGGL((k_wstream<true>), dim3(4096), dim3(256), 0, 0, J, w2, 1.0); }, reps), jbytes);
+    report("wstream_plain (J bytes)",
+           timed([&] { hipLaunchKernelGGL((k_wstream<false>), dim3(4096), dim3(256), 0, 0, J, w2, 1.0); }, reps), jbytes);
+    report("rstream (J bytes)",
+           timed([&] { hipLaunchKernelGGL(k_rstream, dim3(4096), dim3(256), 0, 0, J, w2, out); }, reps), jbytes);
     CHECK(hipFree(V));
     CHECK(hipFree(G));
     CHECK(hipFree(J));

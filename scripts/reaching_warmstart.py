@@ -32,6 +32,10 @@ ap.add_argument("--objectives", default="fatigue,force")
 ap.add_argument("--max-iter", type=int, default=3000)
 ap.add_argument("--wall", type=float, default=400.0)
 ap.add_argument("--out", default=None, help="append the JSON lines to this file")
+ap.add_argument("--mu-init", type=float, default=1e-9, help="warm start: Ipopt's mu_init (default 1e-9)")
+ap.add_argument("--bound-push", type=float, default=1e-9, help="warm start: Ipopt's bound_push (default 1e-9)")
+ap.add_argument("--bound-relax", type=float, default=1e-8,
+                help="Ipopt's bound_relax_factor (its default 1e-8, as the stored solve used)")
 ap.add_argument("--current", action="store_true",
                 help="today's calcium conventions and per-interval widths instead of the stored revision's")
 args = ap.parse_args()
@@ -72,19 +76,25 @@ def run(objective):
     assert ocp.nu == nm, ocp.nu
     v0 = R.decision_vector(X, U[:nm], nz)
     lb, ub = ocp.bounds_vector()
-    v0 = np.clip(v0, lb, ub)  # the stored widths sit 1e-8 outside (Ipopt's bound_relax_factor)
     h = ocp.nlp(batch=1, layout="aos")
-    g0 = h.eval_g(v0[None])[0]
+    g0 = h.eval_g(v0[None])[0]  # the stored point as it is (its widths sit 1e-8 outside: Ipopt's bound_relax_factor)
     f0 = float(h.eval_f(v0[None])[0])
     h.close()
     t0 = time.perf_counter()
+    # Ipopt-style warm start: a small barrier and bound push, the relaxed bounds of the stored solve
     ipm = NativeIpm(ocp, batch=1, options=IpmOptions(tol=1e-6, max_iter=args.max_iter, max_wall_time=args.wall,
-                                                      print_frequency_time=30.0))
+                                                      print_frequency_time=30.0, mu_init=args.mu_init,
+                                                      bound_push=args.bound_push,
+                                                      bound_relax_factor=args.bound_relax))
     res = ipm.solve(v0[None])
     st = dict(ipm.last_stats)
     ipm.close()
     wall = time.perf_counter() - t0
     v = res.v[0]
+    h = ocp.nlp(batch=1, layout="aos")
+    g1 = h.eval_g(v[None])[0]
+    h.close()
+    nrow = R.N * ocp.nx
     span = np.where(np.isfinite(ub - lb) & (ub > lb), ub - lb, np.maximum(1.0, np.abs(v0)))
     body0, body = v0[: R.N * nz].reshape(R.N, nz), v[: R.N * nz].reshape(R.N, nz)
     dstate = np.abs(body[:, :nx] - body0[:, :nx]) / span[: R.N * nz].reshape(R.N, nz)[:, :nx]
@@ -96,6 +106,7 @@ def run(objective):
            "status": int(res.status[0]), "converged": bool(res.converged[0]),
            "iterations": int(res.iterations[0]), "wall_s": wall, "kkt_error": float(res.kkt_error[0]),
            "f_start": f0, "f_end": float(res.f[0]), "g_start_max": float(np.abs(g0).max()),
+           "g_end_max_continuity": float(np.abs(g1[:nrow]).max()), "g_end_max_other": float(np.abs(g1[nrow:]).max()),
            "g_start_rows_over_1e-6": int((np.abs(g0) > 1e-6).sum()),
            "dstate_rel_max": float(dstate.max()), "dstate_rel_median": float(np.median(dstate)),
            "dpw_rel_max": float(np.abs(pw - pw0).max() / (pwhi - pwlo)),
@@ -103,7 +114,9 @@ def run(objective):
            "pw_at_bounds_start": int(((pw0 <= pwlo + 1e-9) | (pw0 >= pwhi - 1e-9)).sum()),
            "pw_at_bounds_end": int(((pw <= pwlo + 1e-9) | (pw >= pwhi - 1e-9)).sum()), "pw_total": int(pw.size),
            "pw_spread_within_pulse_max_rel": spread / (pwhi - pwlo),
-           "resto_phases": int(st.get("resto_phases", 0)), "kkt_layout": st.get("layout")}
+           "resto_phases": int(st.get("resto_phases", 0)), "kkt_n": st.get("kkt_n"), "kkt_kl": st.get("kkt_kl"),
+           "kkt_blocks": st.get("kkt_blocks"), "mu_init": args.mu_init, "bound_push": args.bound_push,
+           "bound_relax_factor": args.bound_relax, "s_per_iteration": wall / max(1, int(res.iterations[0]))}
     line = json.dumps(out)
     print(line, flush=True)
     if args.out:

@@ -135,39 +135,51 @@ def test_collocation_fused_launch_matches_the_separate_callbacks(name):
 
 
 def test_bench_shape_collocation():
-    """bench.py's collocation launch: cfg 2 by direct collocation (Legendre degree 4), B = 2^18, 64-instance tiles,
-    the handle's default shape, on the bench's synthetic batch: sampled instances bit for bit against a small AoS
-    handle (trivial shape) and against the oracle; the fused launch at the same shape against the separate passes."""
+    """bench.py's collocation launches: cfg 2 by direct collocation (Legendre degree 4), B = 2^18, SoA (the roofline
+    line) and 64-instance tiles (timed beside it), the handle's default shape, on the bench's synthetic batch: sampled
+    instances bit for bit against a small AoS handle (trivial shape) and against the oracle."""
     import torch
 
     import bench
     from oracle import fes_collocation as CO
     from tests.oracle_handle import oracle_problem_from_ocp
+    from tests.test_launch_shapes import _picks
 
     ocp = bench.build_collocation()
     pb = oracle_problem_from_ocp(ocp)
     B = bench.COLLOCATION_BATCH
-    v = bench.collocation_synthetic(ocp, B, device="cuda:0")
-    h = ocp.nlp(batch=B, layout="tiled64")
-    shape = h.launch_shape()
-    assert shape["instances_per_lane"] == 2, shape
-    g = torch.empty((B // 64, h.ng, 64), dtype=torch.float64, device="cuda")
-    j = torch.empty((B // 64, h.nnz_jac, 64), dtype=torch.float64, device="cuda")
-    h.eval_all(v, g=g, jac=j)
-    torch.cuda.synchronize()
-    from tests.test_launch_shapes import _picks
-
+    vt = bench.collocation_synthetic(ocp, B, device="cuda:0")
     pick = _picks(B, n_random=24)
     t, e = pick // 64, pick % 64
-    gp, jp, vp = g[t, :, e].cpu().numpy(), j[t, :, e].cpu().numpy(), v[t, :, e].cpu().numpy()
-    h.close()
-    del g, j
+    vp = vt[t, :, e].cpu().numpy()
     small = ocp.nlp(batch=len(pick), layout="aos")
-    np.testing.assert_array_equal(gp, small.eval_g(vp))
-    np.testing.assert_array_equal(jp, small.eval_jac_g(vp))
+    g_ref, j_ref = small.eval_g(vp), small.eval_jac_g(vp)
     small.close()
-    _close_col_g(vp, gp, CO.eval_g(pb, vp), 4, "bench colloc g")
-    _close(jp, CO.eval_jac_g(pb, vp), what="bench colloc J")
+    _close_col_g(vp, g_ref, CO.eval_g(pb, vp), 4, "bench colloc g")
+    _close(j_ref, CO.eval_jac_g(pb, vp), what="bench colloc J")
+    for layout in ("tiled64", "soa"):
+        h = ocp.nlp(batch=B, layout=layout)
+        shape = h.launch_shape()
+        assert shape["instances_per_lane"] == 2, (layout, shape)
+        if layout == "tiled64":
+            g = torch.empty((B // 64, h.ng, 64), dtype=torch.float64, device="cuda")
+            j = torch.empty((B // 64, h.nnz_jac, 64), dtype=torch.float64, device="cuda")
+            h.eval_all(vt, g=g, jac=j)
+            torch.cuda.synchronize()
+            gp, jp = g[t, :, e].cpu().numpy(), j[t, :, e].cpu().numpy()
+        else:
+            v = vt.transpose(1, 2).reshape(B, h.nv).T.contiguous()
+            g = torch.empty((h.ng, B), dtype=torch.float64, device="cuda")
+            j = torch.empty((h.nnz_jac, B), dtype=torch.float64, device="cuda")
+            h.eval_all(v, g=g, jac=j)
+            torch.cuda.synchronize()
+            idx = torch.as_tensor(pick, device="cuda")
+            gp, jp = g[:, idx].T.cpu().numpy(), j[:, idx].T.cpu().numpy()
+            del v
+        h.close()
+        del g, j
+        np.testing.assert_array_equal(gp, g_ref)
+        np.testing.assert_array_equal(jp, j_ref)
 
 
 @pytest.mark.parametrize("name,degree", [("ding2003", 4), ("ding2007_with_fatigue", 3), ("hmed2018", 2)])
