@@ -257,3 +257,27 @@ def test_soft_restoration_options_are_validated():
         IpmOptions(max_soft_resto_iters=-1)
     o = apply_solver(IpmOptions(), Solver.IPOPT(_soft_resto_pderror_reduction_factor=0.9999, _max_soft_resto_iters=3))
     assert (o.soft_resto_pderror_reduction_factor, o.max_soft_resto_iters) == (0.9999, 3)
+
+
+@pytest.mark.parametrize("restart", [False, True])
+def test_failed_restoration_stops_or_restarts(restart):
+    """An infeasible instance (cfg 2 with its fixed initial force at 5,000 N: every later force exceeds its 1,000 N
+    bound) beside a feasible one.  With Ipopt's exits its restoration phase ends it (Infeasible_Problem_Detected or
+    Restoration_Failed); with the resto_failure_restart extension a failed phase sends it back to the main iteration
+    instead, so it never ends with Restoration_Failed.  The feasible instance converges to the same point either way."""
+    cfg = cases.cfg2()
+    ocp, pb, ipm = _ipm(cfg, batch=2, tol=1e-8, max_iter=120, resto_failure_restart=restart)
+    lb, ub = ocp.bounds_vector()
+    fixed = np.tile(lb[lb == ub], (2, 1))
+    fixed[1, 1] = 5000.0
+    res = ipm.solve(np.tile(ocp.initial_guess_vector(), (2, 1)), fixed_values=fixed)
+    assert res.converged[0] and not res.converged[1], (res.status, res.iterations)
+    assert res.status[0] == 0
+    if restart:
+        assert res.status[1] in (2, -1), res.status
+    else:
+        assert res.status[1] in (2, -2), res.status
+    c = O.model_constants("ding2003")
+    traj = O.ivp_integrate("ding2003", c, pb.rows, np.zeros((pb.n_shooting, 0)), 1.0, "RK1", 10)
+    X, _, _ = pb.unpack(res.v)
+    np.testing.assert_allclose(X[0].T, traj[:, ::10], rtol=1e-6, atol=1e-6)
