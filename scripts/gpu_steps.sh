@@ -14,6 +14,8 @@
 #   py:SCRIPT[:ARGS] python SCRIPT ARGS (ARGS with commas for spaces), stdout to SCRIPT's name .txt
 #   bin:PATH[:ARGS]  a binary built here (e.g. scripts/micro/bin/colloc_bw), stdout to its name .txt
 #   env:NAME=VALUE   export NAME=VALUE for the steps after it (e.g. env:CFX_LIB=cocofest_amd/libcfx_recip.so)
+#   limit:SECONDS    time limit of the py: steps after it (default 900)
+#   trace:SCRIPT[:ARGS]  rocprofv3 --kernel-trace --stats (CSV) over python3 SCRIPT ARGS -> trace_<script>/
 #   pmc:CTRS[@LABEL]:SCRIPT[:ARGS]  rocprofv3 --pmc CTRS ('+'-separated, one pass; FETCH_SIZE and WRITE_SIZE each
 #                    alone) over python3 SCRIPT ARGS -> pmc_[LABEL_]<first counter>/
 set -o pipefail
@@ -33,6 +35,7 @@ run() {  # run LIMIT LOGNAME CMD...
         exit $rc
     fi
 }
+pylim=900
 for step in "$@"; do
     case "$step" in
         tests) run 600 pytest_gpu.log python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread ;;
@@ -53,7 +56,7 @@ for step in "$@"; do
               args=""
               [ "$spec" != "$script" ] && args=${spec#*:}
               # shellcheck disable=SC2086
-              run 900 "$(basename "$script" .py).txt" python3 -u "$script" ${args//,/ } ;;
+              run "$pylim" "$(basename "$script" .py).txt" python3 -u "$script" ${args//,/ } ;;
         bin:*) spec=${step#bin:}
                exe=${spec%%:*}
                args=""
@@ -72,6 +75,15 @@ for step in "$@"; do
                # shellcheck disable=SC2086
                run 180 "pmc_${tag}.log" timeout -s KILL 150 rocprofv3 --pmc ${ctr//+/ } -d "$out/pmc_${tag}" -o run -- \
                    python3 "$script" ${args//,/ } ;;
+        limit:*) pylim=${step#limit:} ;;
+        trace:*) spec=${step#trace:}
+                 script=${spec%%:*}
+                 args=""
+                 [ "$spec" != "$script" ] && args=${spec#*:}
+                 name=$(basename "$script" .py)
+                 # shellcheck disable=SC2086
+                 run "$pylim" "trace_${name}.log" rocprofv3 --kernel-trace --stats --output-format csv \
+                     -d "$out/trace_${name}" -o run -- python3 -u "$script" ${args//,/ } ;;
         env:*) kv=${step#env:}
                export "${kv%%=*}=${kv#*=}"
                echo "== export ${kv%%=*}=${kv#*=}" ;;
