@@ -1179,6 +1179,391 @@ __global__ void __launch_bounds__(256) k_band_transpose(const T* __restrict__ sr
 }
 
 // ---------------------------------------------------------------------------------------------------
+// panel placement: single wide bands, factored NB columns at a time
+// ---------------------------------------------------------------------------------------------------
+// The global placement's column step is five barrier-separated phases over L2 (pivot search, swap, scale,
+// update): ≈ 13 µs per column for the 1,500-interval MSK KKT (n = 119,640, kl = ku = 108), 1.5 s per
+// factorisation.  Here, per panel of NB columns j0 .. j0 + NB - 1:
+//  1. the panel (its rows j0 .. j0 + NB - 1 + kl) is factored in LDS with ONE barrier per column: every wave
+//     finds the pivot itself (no broadcast), and every element of the active block is rewritten into the
+//     other of two buffers with the row interchange folded into its source row;
+//  2. the trailing columns j0 + NB .. ju (ju <= j0 + NB - 1 + kv) take the panel's interchanges and
+//     elimination at once: U12 = L11^-1 P A12 by one thread per column, A22 -= L21 U12 by one wave per column
+//     with the lanes over rows (band-storage columns are contiguous).  The multipliers of this step are the
+//     panel's with its later interchanges applied — Lt(r, k) = L(sigma_k(r), k), sigma_k(r) the row that held
+//     at step k what ends in row r — while the stored multipliers stay position-based (dgbtf2's, what every
+//     solve kernel reads).
+// Every element receives the same operations in the same order as in the column step (the interchanges
+// commute with the eliminations they are moved past), so factors, pivots and zero-pivot reports equal the
+// global placement's (tested bit for bit).  Fill rows (storage rows < kl) are zeroed lazily, as columns
+// enter the trailing reach.
+#ifdef CFX_BAND_PROF
+__device__ unsigned long long g_panel_prof[8];  // phase clocks of instance 0, thread 0 (micro build only)
+#define PANEL_STAMP(i)                                                  \
+    do {                                                                \
+        if (blockIdx.x == 0 && t == 0) {                                \
+            const unsigned long long now_ = wall_clock64();             \
+            prof[i] += now_ - last_;                                    \
+            last_ = now_;                                               \
+        }                                                               \
+    } while (0)
+#else
+#define PANEL_STAMP(i) \
+    do {               \
+    } while (0)
+#endif
+template <int NB, int NT>
+__global__ void __launch_bounds__(NT) k_band_lu_panel(int n, int kl, int ku, double* __restrict__ AB,
+                                                      int32_t* __restrict__ IPIV, int32_t* __restrict__ INFO) {
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    constexpr int NW = NT / 64, US = NB + 1;  // US: column stride of the trailing-column images (conflict-free)
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const int ldab = 2 * kl + ku + 1, kv = kl + ku, PR = NB + kl, WT = max(kv, 1);
+    double* const ab = AB + (int64_t)blockIdx.x * n * ldab;
+    int32_t* const piv = IPIV + (int64_t)blockIdx.x * n;
+    double* const P0 = smem;               // panel buffers, column-major [c][r], stride PR
+    double* const P1 = P0 + NB * PR;
+    double* const Lt = P1 + NB * PR;       // blocked multipliers, row-major [r][k], stride US
+    double* const Ut = Lt + PR * US;       // trailing columns' top rows, interchanged, then U12: [c'][k]
+    double* const To = Ut + WT * US;       // trailing columns' top rows as they were (for rows moved down)
+    int* const q = reinterpret_cast<int*>(To + WT * US);  // panel row r ends up holding original row q[r]
+    int* const sp = q + PR;                                // pivot row of each panel step (panel-relative)
+    auto at = [&](int i, int j) -> double& { return ab[(int64_t)j * ldab + kv + i - j]; };
+    int info = 0, ju = 0, zhi = -1;
+#ifdef CFX_BAND_PROF
+    unsigned long long prof[8] = {}, last_ = wall_clock64();
+#endif
+    for (int j0 = 0; j0 < n; j0 += NB) {
+        const int w = min(NB, n - j0), pr = min(w + kl, n - j0);
+        // fill rows of the columns entering the reach of this panel's rows (no earlier step touched them)
+        const int zend = min(j0 + w - 1 + kv, n - 1);
+        for (int64_t e = t; e < (int64_t)(zend - zhi) * kl; e += NT)
+            ab[(int64_t)(zhi + 1 + e / kl) * ldab + e % kl] = 0.0;
+        zhi = max(zhi, zend);
+        __syncthreads();
+        PANEL_STAMP(0);
+        for (int e = t; e < w * pr; e += NT) {
+            const int c = e / pr, r = e - c * pr;
+            P0[c * PR + r] = (r - c <= kl && c - r <= kv) ? at(j0 + r, j0 + c) : 0.0;
+        }
+        __syncthreads();
+        PANEL_STAMP(1);
+        // 1. the panel: step jj reads one buffer and writes the active block (rows, columns >= jj) to the other
+        for (int jj = 0; jj < w; ++jj) {
+            const double* S = (jj & 1) ? P1 : P0;
+            double* T = (jj & 1) ? P0 : P1;
+            const int rmax = min(pr - 1, jj + kl);  // rows of the column step (km); below: zeros in column jj
+            double av = -1.0;
+            int ai = jj;
+            for (int r = jj + lane; r <= rmax; r += 64) {
+                const double v = fabs(S[jj * PR + r]);
+                if (v > av) {
+                    av = v;
+                    ai = r;
+                }
+            }
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) {
+                const double ov = __shfl_xor(av, off);
+                const int oi = __shfl_xor(ai, off);
+                if (ov > av || (ov == av && oi < ai)) {
+                    av = ov;
+                    ai = oi;
+                }
+            }
+            const int pj = ai;
+            const double pv = S[jj * PR + pj];
+            const int m = pr - jj;
+            if (pv != 0.0) {
+                const double inv = 1.0 / pv;
+                for (int e = t; e < (w - jj) * m; e += NT) {
+                    const int c = jj + e / m, r = jj + e % m;
+                    const int s = r == jj ? pj : (r == pj ? jj : r);
+                    double v;
+                    if (r > rmax)
+                        v = S[c * PR + r];
+                    else if (c == jj)
+                        v = r == jj ? pv : S[jj * PR + s] * inv;
+                    else if (r == jj)
+                        v = S[c * PR + pj];
+                    else
+                        v = S[c * PR + s] - (S[jj * PR + s] * inv) * S[c * PR + pj];
+                    T[c * PR + r] = v;
+                }
+                ju = max(ju, min(j0 + ku + pj, n - 1));
+            } else {
+                for (int e = t; e < (w - jj) * m; e += NT) {
+                    const int c = jj + e / m, r = jj + e % m;
+                    T[c * PR + r] = S[c * PR + r];
+                }
+                if (info == 0) info = j0 + jj + 1;
+            }
+            if (t == 0) sp[jj] = pj;
+            __syncthreads();
+        }
+        PANEL_STAMP(2);
+        // the panel back to the band (element (r, c) is final after step min(r, c), in that step's output
+        // buffer), the pivots, the blocked multipliers and the composed interchanges
+        int spr[NB];
+#pragma unroll
+        for (int i = 0; i < NB; ++i) spr[i] = i < w ? sp[i] : i;
+        auto sigma = [&](int r, int k) {  // interchanges w - 1 .. k + 1 undone
+            int s = r;
+#pragma unroll
+            for (int i = NB - 1; i >= 0; --i)
+                if (i > k && i < w) s = s == i ? spr[i] : (s == spr[i] ? i : s);
+            return s;
+        };
+        for (int e = t; e < w * pr; e += NT) {
+            const int c = e / pr, r = e - c * pr;
+            const double* F = (min(r, c) & 1) ? P0 : P1;
+            if (r - c <= kl && c - r <= kv) at(j0 + r, j0 + c) = F[c * PR + r];
+            const int k = e % w, rr = e / w;
+            Lt[rr * US + k] = rr > k ? ((k & 1) ? P0 : P1)[k * PR + sigma(rr, k)] : 0.0;
+        }
+        for (int r = t; r < pr; r += NT) q[r] = sigma(r, -1);
+        if (t < w) piv[j0 + t] = j0 + sp[t];
+        const int c0 = j0 + w, wt = ju - c0 + 1;  // trailing columns c0 .. ju
+        __syncthreads();
+        PANEL_STAMP(3);
+        if (wt > 0) {
+            // 2a. the trailing columns' top rows, interchanged (Ut) and as they were (To)
+            for (int e = t; e < wt * w; e += NT) {
+                const int cc = e / w, k = e - cc * w, c = c0 + cc, i = j0 + q[k];
+                Ut[cc * US + k] = c - i <= kv ? at(i, c) : 0.0;
+                To[cc * US + k] = c - (j0 + k) <= kv ? at(j0 + k, c) : 0.0;
+            }
+            __syncthreads();
+            PANEL_STAMP(4);
+            // 2b. U12 = L11^-1 (P A12), one thread per column, in the column step's order
+            for (int cc = t; cc < wt; cc += NT) {
+                double x[NB];
+#pragma unroll
+                for (int k = 0; k < NB; ++k) x[k] = k < w ? Ut[cc * US + k] : 0.0;
+#pragma unroll
+                for (int k = 0; k < NB; ++k)
+#pragma unroll
+                    for (int r = k + 1; r < NB; ++r)
+                        if (r < w) x[r] -= Lt[r * US + k] * x[k];
+#pragma unroll
+                for (int k = 0; k < NB; ++k)
+                    if (k < w) Ut[cc * US + k] = x[k];
+            }
+            __syncthreads();
+            PANEL_STAMP(5);
+            // 2c. A22 -= L21 U12 (rows w .. pr - 1: rows moved down start from their original top row), one wave
+            // per column, lanes over rows; the wave also stores the column's U12 rows
+            for (int h0 = 0; h0 < max(pr - w, 1); h0 += 128) {
+                const int r0 = w + h0 + lane, r1 = r0 + 64;
+                const bool ok0 = r0 < pr, ok1 = r1 < pr;
+                const int q0 = ok0 ? q[r0] : r0, q1 = ok1 ? q[r1] : r1;
+                double l0[NB], l1[NB];
+#pragma unroll
+                for (int k = 0; k < NB; ++k) {
+                    l0[k] = ok0 ? Lt[r0 * US + k] : 0.0;
+                    l1[k] = ok1 ? Lt[r1 * US + k] : 0.0;
+                }
+                constexpr int CG = 4;  // columns in flight per wave
+                for (int cb = wave; cb < wt; cb += NW * CG) {
+                    double y0[CG], y1[CG];
+#pragma unroll
+                    for (int g = 0; g < CG; ++g) {
+                        const int cc = cb + g * NW, c = c0 + cc;
+                        const bool okc = cc < wt;
+                        y0[g] = okc && ok0 ? (q0 != r0 ? To[cc * US + q0] : at(j0 + r0, c)) : 0.0;
+                        y1[g] = okc && ok1 ? (q1 != r1 ? To[cc * US + q1] : at(j0 + r1, c)) : 0.0;
+                    }
+#pragma unroll
+                    for (int g = 0; g < CG; ++g) {
+                        const int cc = cb + g * NW, c = c0 + cc;
+                        if (cc >= wt) break;
+                        const double* uc = Ut + cc * US;
+                        if (h0 == 0 && lane < w && c - (j0 + lane) <= kv) at(j0 + lane, c) = uc[lane];
+#pragma unroll
+                        for (int k = 0; k < NB; ++k)
+                            if (k < w) {
+                                const double u = uc[k];
+                                y0[g] -= l0[k] * u;
+                                y1[g] -= l1[k] * u;
+                            }
+                        if (ok0) at(j0 + r0, c) = y0[g];
+                        if (ok1) at(j0 + r1, c) = y1[g];
+                    }
+                }
+            }
+        }
+        // (the next panel's first barrier orders these stores before its loads)
+        PANEL_STAMP(6);
+    }
+#ifdef CFX_BAND_PROF
+    if (blockIdx.x == 0 && t == 0)
+        for (int i = 0; i < 8; ++i) g_panel_prof[i] = prof[i];
+#endif
+    if (t == 0) INFO[blockIdx.x] = info;
+}
+
+// Solves with the factors of any placement for single wide bands: one wavefront runs the substitution's
+// dependent chain with its window in registers (as the register placement's solve), the other waves stream
+// the band columns it needs into LDS ahead of it, CH columns per buffer, one barrier per CH columns — the
+// global placement's substitutions pay two barriers and an L2 round trip per column instead.
+// Forward pass: x <- L^-1 P x, lane i + 64 f holding x[j + i + 64 f] (i + 64 f <= kl < 64 KF); per column the
+// buffer holds the multipliers L(j + i, j) at slot i (zero outside 1 .. min(kl, n - 1 - j)), the pivot row
+// and x[j + 1 + kl], the element entering the window.
+template <int KF, int NT>
+__global__ void __launch_bounds__(NT) k_band_fwd_stream(int n, int kl, int ku, int nrhs,
+                                                        const double* __restrict__ AB,
+                                                        const int32_t* __restrict__ IPIV, double* RHS) {
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    constexpr int CW = 64 * KF, CH = 128 / KF, NP = NT - 64;
+    const int t = threadIdx.x, lane = t & 63;
+    const int ldab = 2 * kl + ku + 1, kv = kl + ku, fk = kl >> 6, lk = kl & 63;
+    const double* const ab = AB + (int64_t)blockIdx.x * n * ldab;
+    const int32_t* const piv = IPIV + (int64_t)blockIdx.x * n;
+    double* const M = smem;                // [buffer][column][slot]
+    double* const X = M + 2 * CH * CW;     // [buffer][column]
+    int* const Pv = reinterpret_cast<int*>(X + 2 * CH);
+    double* dsink = block_sink() + lane;
+    const int steps = n - 1, nch = (steps + CH - 1) / CH;
+    if (kl == 0 || steps <= 0) return;
+    for (int c = 0; c < nrhs; ++c) {
+        double* x = RHS + ((int64_t)blockIdx.x * nrhs + c) * n;
+        auto produce = [&](int ci) {
+            const int b = ci & 1, jb = ci * CH, tp = t - 64;
+#pragma unroll 8
+            for (int e = tp; e < CH * CW; e += NP) {
+                const int jj = e / CW, i = e - jj * CW, j = jb + jj;
+                M[(b * CH + jj) * CW + i] =
+                    (j < steps && i >= 1 && i <= min(kl, n - 1 - j)) ? ab[(int64_t)j * ldab + kv + i] : 0.0;
+            }
+            for (int jj = tp; jj < CH; jj += NP) {
+                const int j = jb + jj;
+                Pv[b * CH + jj] = j < steps ? piv[j] - j : 0;
+                X[b * CH + jj] = j + 1 + kl < n ? x[j + 1 + kl] : 0.0;
+            }
+        };
+        double xw[KF];
+        if (t < 64) {
+#pragma unroll
+            for (int f = 0; f < KF; ++f) {
+                const int i = lane + 64 * f;
+                xw[f] = (i <= kl && i < n) ? x[i] : 0.0;
+            }
+        } else {
+            produce(0);
+        }
+        __syncthreads();
+        for (int ci = 0; ci < nch; ++ci) {
+            if (t < 64) {
+                const int b = ci & 1, jb = ci * CH, cnt = min(CH, steps - jb);
+                const double* Mb = M + b * CH * CW;
+                for (int jj = 0; jj < cnt; ++jj) {
+                    const int j = jb + jj;
+                    double lc[KF];
+#pragma unroll
+                    for (int f = 0; f < KF; ++f) lc[f] = Mb[jj * CW + lane + 64 * f];
+                    const int p = __builtin_amdgcn_readfirstlane(Pv[b * CH + jj]);
+                    const double nxv = X[b * CH + jj];
+                    if (p != 0) {
+                        const int fp = p >> 6, lp = p & 63;
+                        double src = xw[0];
+#pragma unroll
+                        for (int f = 1; f < KF; ++f)
+                            if (f == fp) src = xw[f];
+                        const double a = lane_read(xw[0], 0), bv = lane_read(src, lp);
+                        xw[0] = lane == 0 ? bv : xw[0];
+#pragma unroll
+                        for (int f = 0; f < KF; ++f)
+                            if (f == fp) xw[f] = lane == lp ? a : xw[f];
+                    }
+                    const double xj = lane_read(xw[0], 0);
+#pragma unroll
+                    for (int f = 0; f < KF; ++f) xw[f] -= lc[f] * xj;
+                    *(lane == 0 ? x + j : dsink) = xj;
+                    slide<KF>(xw);
+#pragma unroll
+                    for (int f = 0; f < KF; ++f)
+                        if (f == fk && lane == lk) xw[f] = nxv;
+                }
+            } else if (ci + 1 < nch) {
+                produce(ci + 1);
+            }
+            __syncthreads();
+        }
+        if (t == 0) x[n - 1] = xw[0];
+        __syncthreads();
+    }
+}
+
+// Backward pass: x <- U^-1 x, lane i + 64 k holding x[j - i - 64 k] (i + 64 k <= kv < 64 KB); per column the
+// buffer holds U(j - i, j) at slot i (zero past min(kv, j)) and x[j - 1 - kv].
+template <int KB, int NT>
+__global__ void __launch_bounds__(NT) k_band_bwd_stream(int n, int kl, int ku, int nrhs,
+                                                        const double* __restrict__ AB, double* RHS) {
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    constexpr int CW = 64 * KB, CH = 128 / KB, NP = NT - 64;
+    const int t = threadIdx.x, lane = t & 63;
+    const int ldab = 2 * kl + ku + 1, kv = kl + ku, fk = kv >> 6, lk = kv & 63;
+    const double* const ab = AB + (int64_t)blockIdx.x * n * ldab;
+    double* const U = smem;
+    double* const X = U + 2 * CH * CW;
+    double* dsink = block_sink() + lane;
+    const int nch = (n + CH - 1) / CH;
+    for (int c = 0; c < nrhs; ++c) {
+        double* x = RHS + ((int64_t)blockIdx.x * nrhs + c) * n;
+        auto produce = [&](int ci) {  // chunk ci: columns n - 1 - ci CH downwards
+            const int b = ci & 1, jb = n - 1 - ci * CH, tp = t - 64;
+#pragma unroll 8
+            for (int e = tp; e < CH * CW; e += NP) {
+                const int jj = e / CW, i = e - jj * CW, j = jb - jj;
+                U[(b * CH + jj) * CW + i] = (j >= 0 && i <= min(kv, j)) ? ab[(int64_t)j * ldab + kv - i] : 0.0;
+            }
+            for (int jj = tp; jj < CH; jj += NP) {
+                const int j = jb - jj;
+                X[b * CH + jj] = j - 1 - kv >= 0 ? x[j - 1 - kv] : 0.0;
+            }
+        };
+        double xw[KB];
+        if (t < 64) {
+#pragma unroll
+            for (int k = 0; k < KB; ++k) {
+                const int i = lane + 64 * k;
+                xw[k] = (i <= kv && n - 1 - i >= 0) ? x[n - 1 - i] : 0.0;
+            }
+        } else {
+            produce(0);
+        }
+        __syncthreads();
+        for (int ci = 0; ci < nch; ++ci) {
+            if (t < 64) {
+                const int b = ci & 1, jb = n - 1 - ci * CH, cnt = min(CH, jb + 1);
+                const double* Ub = U + b * CH * CW;
+                for (int jj = 0; jj < cnt; ++jj) {
+                    const int j = jb - jj;
+                    double uc[KB];
+#pragma unroll
+                    for (int k = 0; k < KB; ++k) uc[k] = Ub[jj * CW + lane + 64 * k];
+                    const double nxv = X[b * CH + jj];
+                    const double xj = lane_read(xw[0], 0) / lane_read(uc[0], 0);
+                    *(lane == 0 ? x + j : dsink) = xj;
+#pragma unroll
+                    for (int k = 0; k < KB; ++k) {  // one fused multiply-subtract per element, as the column kernels
+                        const double u = (k == 0 && lane == 0) ? 0.0 : uc[k];
+                        xw[k] -= u * xj;
+                    }
+                    slide<KB>(xw);
+#pragma unroll
+                    for (int k = 0; k < KB; ++k)
+                        if (k == fk && lane == lk) xw[k] = nxv;
+                }
+            } else if (ci + 1 < nch) {
+                produce(ci + 1);
+            }
+            __syncthreads();
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------------
 // dispatch
 // ---------------------------------------------------------------------------------------------------
 // Raise a kernel's dynamic-LDS limit above 64 KiB only when a launch needs more than it was last raised to (one
@@ -1363,6 +1748,80 @@ static hipError_t lane_dispatch(int64_t n, int32_t kl, int32_t ku, int64_t batch
 #undef CFX_LANE
 }
 
+// Panel placement (single bands too wide for LDS and registers: what the global placement would take): LDS bytes of
+// k_band_lu_panel<nb>; the panel width that fits (16, else 8, else 0: not applicable).
+static size_t panel_lds(int nb, int32_t kl, int32_t ku) {
+    const int64_t pr = nb + (int64_t)kl, wt = std::max<int64_t>((int64_t)kl + ku, 1);
+    return (size_t)(8 * (2 * nb * pr + pr * (nb + 1) + 2 * wt * (nb + 1)) + 4 * (pr + nb));
+}
+static int panel_nb(int32_t kl, int32_t ku) {
+    if (panel_lds(16, kl, ku) <= (size_t)kBandLds) return 16;
+    if (panel_lds(8, kl, ku) <= (size_t)kBandLds) return 8;
+    return 0;
+}
+// streamed solves: window registers per lane (forward kl < 64 KF, backward kl + ku < 64 KB)
+static bool stream_ok(int32_t kl, int32_t ku) { return kl <= 255 && kl + ku <= 511; }
+constexpr int kStreamNT = 512;
+
+template <int KF>
+static hipError_t launch_fwd(int64_t n, int32_t kl, int32_t ku, int64_t batch, const double* ab, const int32_t* ipiv,
+                             int32_t nrhs, double* rhs, hipStream_t s) {
+    constexpr int CH = 128 / KF;
+    const size_t lds = (size_t)2 * CH * 64 * KF * 8 + (size_t)2 * CH * 8 + (size_t)2 * CH * 4;
+    hipError_t e = allow_lds(&k_band_fwd_stream<KF, kStreamNT>, lds);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL((k_band_fwd_stream<KF, kStreamNT>), dim3((unsigned)batch), dim3(kStreamNT), lds, s, (int)n, kl,
+                       ku, nrhs, ab, ipiv, rhs);
+    return hipGetLastError();
+}
+template <int KB>
+static hipError_t launch_bwd(int64_t n, int32_t kl, int32_t ku, int64_t batch, const double* ab, int32_t nrhs,
+                             double* rhs, hipStream_t s) {
+    constexpr int CH = 128 / KB;
+    const size_t lds = (size_t)2 * CH * 64 * KB * 8 + (size_t)2 * CH * 8;
+    hipError_t e = allow_lds(&k_band_bwd_stream<KB, kStreamNT>, lds);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL((k_band_bwd_stream<KB, kStreamNT>), dim3((unsigned)batch), dim3(kStreamNT), lds, s, (int)n, kl,
+                       ku, nrhs, ab, rhs);
+    return hipGetLastError();
+}
+
+static hipError_t launch_panel(int64_t n, int32_t kl, int32_t ku, int64_t batch, double* ab, int32_t* ipiv,
+                               int32_t* info, int32_t nrhs, double* rhs, hipStream_t s, int factor) {
+    hipError_t e = hipSuccess;
+    if (factor) {
+        const int nb = panel_nb(kl, ku);
+        const size_t lds = panel_lds(nb, kl, ku);
+        if (nb == 16) {
+            if ((e = allow_lds(&k_band_lu_panel<16, 512>, lds)) != hipSuccess) return e;
+            hipLaunchKernelGGL((k_band_lu_panel<16, 512>), dim3((unsigned)batch), dim3(512), lds, s, (int)n, kl, ku, ab,
+                               ipiv, info);
+        } else {
+            if ((e = allow_lds(&k_band_lu_panel<8, 512>, lds)) != hipSuccess) return e;
+            hipLaunchKernelGGL((k_band_lu_panel<8, 512>), dim3((unsigned)batch), dim3(512), lds, s, (int)n, kl, ku, ab,
+                               ipiv, info);
+        }
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
+    if (nrhs < 1) return hipSuccess;
+    if (!stream_ok(kl, ku)) {  // the global placement's substitutions
+        hipLaunchKernelGGL((k_band_lu<false, 1024>), dim3((unsigned)batch), dim3(1024), 0, s, (int)n, kl, ku, nrhs, ab,
+                           ipiv, rhs, info, 0);
+        return hipGetLastError();
+    }
+    if (kl > 0) {
+        e = kl < 64 ? launch_fwd<1>(n, kl, ku, batch, ab, ipiv, nrhs, rhs, s)
+                    : (kl < 128 ? launch_fwd<2>(n, kl, ku, batch, ab, ipiv, nrhs, rhs, s)
+                                : launch_fwd<4>(n, kl, ku, batch, ab, ipiv, nrhs, rhs, s));
+        if (e != hipSuccess) return e;
+    }
+    const int kv = kl + ku;
+    return kv < 64    ? launch_bwd<1>(n, kl, ku, batch, ab, nrhs, rhs, s)
+           : kv < 128 ? launch_bwd<2>(n, kl, ku, batch, ab, nrhs, rhs, s)
+           : kv < 256 ? launch_bwd<4>(n, kl, ku, batch, ab, nrhs, rhs, s)
+                      : launch_bwd<8>(n, kl, ku, batch, ab, nrhs, rhs, s);
+}
+
 static int band_launch(int64_t n, int32_t kl, int32_t ku, int64_t batch, double* ab, int32_t* ipiv, int32_t* info,
                        int32_t nrhs, double* rhs, void* stream, int factor) {
     if (n < 1 || n > (1 << 24) || kl < 0 || ku < 0 || kl >= n || ku >= n || batch < 1 || batch > 0x7fffffff ||
@@ -1379,9 +1838,10 @@ static int band_launch(int64_t n, int32_t kl, int32_t ku, int64_t batch, double*
     const size_t lds_full = (size_t)(n * ldab + n * nrhs) * sizeof(double) + (size_t)n * sizeof(int32_t);
     // placement: the register kernels whenever the window fits a wavefront's registers; otherwise small
     // batches keep the whole band resident when it fits LDS (latency-bound), larger ones use the window,
-    // and bands too wide for both run on the global copy.  CFX_BAND_PLACEMENT=0..3 forces one (where it
-    // fits; 4: the lane placement); CFX_BAND_FULL forces resident / global.  Batches of >= kLaneBatch narrow
-    // bands take the lane placement.
+    // and bands too wide for both take the panel kernels (the global copy where even those do not fit).
+    // CFX_BAND_PLACEMENT=0..5 forces one (where it fits; 1: resident, else global; 2: global; 4: lane; 5:
+    // panel); CFX_BAND_FULL forces resident / global.  Batches of >= kLaneBatch narrow bands take the lane
+    // placement.
     int placement;
     const bool force_full = std::getenv("CFX_BAND_FULL") != nullptr;
     const char* forced = std::getenv("CFX_BAND_PLACEMENT");
@@ -1396,20 +1856,27 @@ static int band_launch(int64_t n, int32_t kl, int32_t ku, int64_t batch, double*
         placement = 4;
     else if (forced && *forced == '0' && win_ok)
         placement = 0;
-    else if (forced && (*forced == '1' || *forced == '2'))
+    else if (forced && *forced == '1')
         placement = lds_full <= (size_t)kBandLds ? 1 : 2;
+    else if (forced && *forced == '2')
+        placement = 2;
+    else if (forced && *forced == '5' && panel_nb(kl, ku) > 0)
+        placement = 5;
     else if (!force_full && !forced && reg_ok)
         placement = 3;
     else if (!force_full && !(batch < 128 && lds_full <= (size_t)kBandLds) && win_ok)
         placement = 0;
     else
         placement = lds_full <= (size_t)kBandLds ? 1 : 2;
+    if (placement == 2 && !force_full && !forced && panel_nb(kl, ku) > 0) placement = 5;
     const size_t lds = placement == 0 ? lds_win : (placement == 1 ? lds_full : 0);
     // threads per instance: enough lanes for the rank-1 update of the trailing km x (kl + ku) block
     const int64_t work = (int64_t)kl * (kl + ku);
     const hipStream_t s = (hipStream_t)stream;
     hipError_t e;
-    if (placement == 4)
+    if (placement == 5)
+        e = launch_panel(n, kl, ku, batch, ab, ipiv, info, nrhs, rhs, s, factor);
+    else if (placement == 4)
         e = lane_dispatch(n, kl, ku, batch, ab, ipiv, info, nrhs, rhs, s, factor);
     else if (placement == 3)
         e = reg_dispatch(n, kl, ku, batch, ab, ipiv, info, nrhs, rhs, s, factor);

@@ -3131,8 +3131,13 @@ static int ipm_solve(cfx_ipm* s, const double* v0, const double* fixed_values, d
             break;
         }
         if (K.o.print_frequency_time > 0 && it > 0 && elapsed - last_print >= K.o.print_frequency_time) {
-            std::fprintf(stderr, "cfx_ipm: iteration %d, %.1f s: %d of %lld instances iterating, %d in restoration\n", it,
-                         elapsed, n_active, (long long)B, n_resto);
+            Scal s0{};  // instance 0's optimality error, barrier, infeasibility and last step (one small read)
+            IPM_HIP(s, hipMemcpyAsync(&s0, K.sc, sizeof(Scal), hipMemcpyDeviceToHost, st));
+            IPM_HIP(s, hipStreamSynchronize(st));
+            std::fprintf(stderr,
+                         "cfx_ipm: iteration %d, %.1f s: %d of %lld instances iterating, %d in restoration; instance 0: "
+                         "error %.3e, mu %.1e, theta %.3e, alpha %.2e\n",
+                         it, elapsed, n_active, (long long)B, n_resto, s0.err0, s0.mu, s0.theta, s0.alpha);
             std::fflush(stderr);
             last_print = elapsed;
         }

@@ -1026,7 +1026,8 @@ __device__ __forceinline__ void msk_icol_dcs(const MskParams& P, const MskICol& 
 
 template <int NQ, int NM, int FAM, int SCHEME>
 __global__ void __launch_bounds__(256) k_msk_tangents(const MskParams P, const MskGeom* __restrict__ GG,
-                                                      const double* __restrict__ V, double* __restrict__ J) {
+                                                      const double* __restrict__ V, double* __restrict__ J,
+                                                      int flat) {
     constexpr int NXM = msk_nxm<FAM>(), NX = NM * NXM + 2 * NQ;
     constexpr int NUMAX = msk_numax<NQ, NM, FAM>();
     constexpr int NC = msk_ncoef<NQ, NM>();
@@ -1035,11 +1036,22 @@ __global__ void __launch_bounds__(256) k_msk_tangents(const MskParams P, const M
     const int nz = P.nz;
     // block = 256 consecutive instances x one column.  Workgroups are dispatched round-robin over the 8 XCDs
     // (blockIdx % 8), each with its own L2: the nz column blocks of one instance range are given ids of the same
-    // residue, so they run on one XCD, together, and read the range's coefficients from that XCD's L2.
-    const unsigned L = blockIdx.x, slot = L >> 3;
-    const int col = (int)(slot % (unsigned)nz);
-    const int64_t range = (int64_t)(slot / (unsigned)nz) * 8 + (L & 7);
-    const int64_t b = range * blockDim.x + threadIdx.x;
+    // residue, so they run on one XCD, together, and read the range's coefficients from that XCD's L2.  Small
+    // batches (flat): thread = (instance, column), the columns of an instance side by side — at batch 1 the
+    // per-column blocks left 255 of 256 lanes and 7 of 8 ranges idle (33 ms per call for the 1,500-interval
+    // reaching task, 40 columns).
+    int col;
+    int64_t b;
+    if (flat) {
+        const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+        col = (int)(e % nz);
+        b = e / nz;
+    } else {
+        const unsigned L = blockIdx.x, slot = L >> 3;
+        col = (int)(slot % (unsigned)nz);
+        const int64_t range = (int64_t)(slot / (unsigned)nz) * 8 + (L & 7);
+        b = range * blockDim.x + threadIdx.x;
+    }
     if (b >= B) return;
     const int k = blockIdx.y;
     const MskGeom& G = *GG;

@@ -61,9 +61,11 @@ hipError_t shoot_t(const MskParams& P, const MskGeom* G, const double* V, double
                            dim3(TW * P.nz), lds, s, P, G, V, J, kpb);
         return hipGetLastError();
     }
+    const int flat = P.B < kMskBlk;  // (instance, column) threads: batches below one block per column
     const int64_t ranges8 = ((P.B + kMskBlk - 1) / kMskBlk + 7) / 8 * 8;  // instance ranges, padded to 8 XCDs
-    const unsigned gt = (unsigned)(ranges8 * P.nz);
-    hipLaunchKernelGGL((k_msk_tangents<NQ, NM, FAM, SCHEME>), dim3(gt, (unsigned)P.N), dim3(kMskBlk), 0, s, P, G, V, J);
+    const unsigned gt = flat ? (unsigned)((P.B * P.nz + kMskBlk - 1) / kMskBlk) : (unsigned)(ranges8 * P.nz);
+    hipLaunchKernelGGL((k_msk_tangents<NQ, NM, FAM, SCHEME>), dim3(gt, (unsigned)P.N), dim3(kMskBlk), 0, s, P, G, V, J,
+                       flat);
     return hipGetLastError();
 }
 

@@ -229,7 +229,7 @@ int cfx_integrate(cfx_handle *h, const double *x0, const double *u, double *traj
 #define CFX_MSK_RESIDUAL_TORQUE 8u
 /* Ding2007 muscles: consecutive intervals that follow the same pulse share their pulse widths — rows
    u_k[m] - u_{k-1}[m] = 0 after the marker rows (the decision space of the per-pulse pulse-duration parameters of the
-   revision that stored examples/dynamics/reaching_task/result_file/*.pkl, with band-local rows) */
+   revision that stored examples/dynamics/reaching_task/result_file pickles, with band-local rows) */
 #define CFX_MSK_PULSE_WIDTH_PER_PULSE 16u
 /* Ding muscles: that revision's calcium sum — a window's first pulse left out once it holds several, and the fatigue
    models' r0 = Km + r0_km_relationship read from the Km state (today: km_rest + r0_km_relationship, ding2003.py:230-252;

@@ -1,0 +1,70 @@
+// Phase clocks of the panel band LU (k_band_lu_panel, cocofest_amd/csrc/cfx_band.hip built with CFX_BAND_PROF):
+// one factorisation of a random single band (n, kl, ku), thread 0's wall clock (s_memrealtime, 100 MHz) summed
+// per phase over the panels: fill zeroing, panel load, panel steps, write-back + blocked multipliers, trailing
+// loads, U12, A22 update.  Prints one JSON line with the per-panel microseconds of each phase.
+//   hipcc -O3 -std=c++17 --offload-arch=gfx950 scripts/micro/band_panel_prof.hip -o scripts/micro/bin/band_panel_prof
+//   scripts/micro/bin/band_panel_prof [n kl ku reps]
+#define CFX_BAND_PROF 1
+#include "../../cocofest_amd/csrc/cfx_band.hip"
+
+#include <cstdio>
+#include <random>
+#include <vector>
+
+thread_local std::string g_create_error;
+
+#define CK(x)                                                                                    \
+    do {                                                                                         \
+        hipError_t e_ = (x);                                                                     \
+        if (e_ != hipSuccess) {                                                                  \
+            std::fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e_));                         \
+            std::exit(1);                                                                        \
+        }                                                                                        \
+    } while (0)
+
+int main(int argc, char** argv) {
+    const int n = argc > 1 ? std::atoi(argv[1]) : 119640, kl = argc > 2 ? std::atoi(argv[2]) : 108,
+              ku = argc > 3 ? std::atoi(argv[3]) : 108, reps = argc > 4 ? std::atoi(argv[4]) : 3;
+    const int ldab = 2 * kl + ku + 1, kv = kl + ku;
+    std::vector<double> h((size_t)n * ldab, 0.0);
+    std::mt19937_64 rng(7);
+    std::normal_distribution<double> nd;
+    for (int j = 0; j < n; ++j)
+        for (int i = std::max(0, j - ku); i <= std::min(n - 1, j + kl); ++i)
+            h[(size_t)j * ldab + kv + i - j] = nd(rng) + (i == j ? 4.0 * kv : 0.0);
+    double* ab;
+    int32_t *ipiv, *info;
+    CK(hipMalloc(&ab, h.size() * sizeof(double)));
+    CK(hipMalloc(&ipiv, (size_t)n * sizeof(int32_t)));
+    CK(hipMalloc(&info, sizeof(int32_t)));
+    setenv("CFX_BAND_PLACEMENT", "5", 1);
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    for (int r = 0; r < reps; ++r) {
+        CK(hipMemcpy(ab, h.data(), h.size() * sizeof(double), hipMemcpyHostToDevice));
+        CK(hipEventRecord(a));
+        if (cfx_band_lu(n, kl, ku, 1, ab, ipiv, info, 0, nullptr, nullptr) != 0) {
+            std::fprintf(stderr, "cfx_band_lu: %s\n", g_create_error.c_str());
+            return 1;
+        }
+        CK(hipEventRecord(b));
+        CK(hipEventSynchronize(b));
+        float ms = 0;
+        CK(hipEventElapsedTime(&ms, a, b));
+        unsigned long long p[8];
+        CK(hipMemcpyFromSymbol(p, HIP_SYMBOL(cfx::g_panel_prof), sizeof(p)));
+        const int nb = cfx::panel_nb(kl, ku), panels = (n + nb - 1) / nb;
+        const char* names[7] = {"zero_fill", "panel_load", "panel_steps", "writeback_lt", "trail_load", "u12",
+                                "a22"};
+        std::printf("{\"n\": %d, \"kl\": %d, \"ku\": %d, \"nb\": %d, \"ms\": %.3f, \"us_per_panel\": %.3f", n, kl, ku,
+                    nb, ms, 1e3 * ms / panels);
+        double tot = 0;
+        for (int i = 0; i < 7; ++i) {
+            std::printf(", \"%s\": %.3f", names[i], p[i] * 0.01 / panels);  // 100 MHz ticks -> us per panel
+            tot += p[i] * 0.01 / panels;
+        }
+        std::printf(", \"sum_us\": %.3f}\n", tot);
+    }
+    return 0;
+}

@@ -534,6 +534,52 @@ def test_band_lu_small_and_windowed_paths_agree(B, n, kl, ku, monkeypatch):
     np.testing.assert_allclose(outs[0][3], outs[0][2][:, :1], rtol=1e-10, atol=1e-12)
 
 
+@pytest.mark.parametrize("B,n,kl,ku,zero_diag", [(1, 300, 40, 40, False), (2, 200, 70, 2, False), (1, 7, 3, 1, False),
+                                                 (1, 1000, 108, 108, True), (3, 150, 0, 5, False),
+                                                 (1, 500, 130, 140, False), (1, 64, 63, 63, False),
+                                                 (2, 90, 20, 20, True), (1, 450, 200, 200, False)])
+def test_band_lu_panel_placement(B, n, kl, ku, zero_diag, monkeypatch):
+    """The panel placement (single wide bands: blocked factorisation, streamed one-wave solves; CFX_BAND_PLACEMENT=5)
+    against the global placement (=2), whose column step it reorders: the same factors, pivots and zero-pivot
+    reports bit for bit, the same solutions, factors of one solved by the other's kernels; numpy's dense solve.
+    kl = ku = 200: the 8-column panel (the 16-column one exceeds LDS)."""
+    import torch
+
+    from cocofest_amd import _cfx
+
+    rng = np.random.default_rng(B + n + kl + 11)
+    A, ab = _band_system(rng, B, n, kl, ku, zero_diag=zero_diag)
+    rhs = rng.standard_normal((B, 2, n))
+    singular = B > 1 and kl > 0
+    if singular:
+        ab[1, n // 3, :] = 0.0  # a zero column in instance 1: info = n // 3 + 1, later columns still factored
+    outs = {}
+    for pl in ("5", "2"):
+        monkeypatch.setenv("CFX_BAND_PLACEMENT", pl)
+        abt = torch.tensor(ab, device="cuda")
+        ipiv = torch.empty((B, n), dtype=torch.int32, device="cuda")
+        info = torch.empty((B,), dtype=torch.int32, device="cuda")
+        x = torch.tensor(rhs, device="cuda")
+        _cfx.band_lu(abt, ipiv, info, kl, ku, rhs=x)
+        monkeypatch.setenv("CFX_BAND_PLACEMENT", "2" if pl == "5" else "5")  # solve with the other placement
+        x2 = torch.tensor(rhs[:, 1:], device="cuda")
+        _cfx.band_lu_solve(abt, ipiv, kl, ku, x2)
+        torch.cuda.synchronize()
+        outs[pl] = (abt.cpu().numpy(), ipiv.cpu().numpy(), info.cpu().numpy(), x.cpu().numpy(), x2.cpu().numpy())
+    pan, glo = outs["5"], outs["2"]
+    np.testing.assert_array_equal(pan[1], glo[1])
+    np.testing.assert_array_equal(pan[2], glo[2])
+    np.testing.assert_array_equal(pan[0], glo[0])
+    ok = pan[2] == 0
+    assert ok.sum() == B - (1 if singular else 0)
+    np.testing.assert_array_equal(pan[3][ok], glo[3][ok])
+    np.testing.assert_array_equal(pan[4][ok], pan[3][ok][:, 1:])
+    np.testing.assert_array_equal(glo[4][ok], glo[3][ok][:, 1:])
+    ref = np.linalg.solve(A[ok], rhs[ok].transpose(0, 2, 1)).transpose(0, 2, 1)
+    cond = np.linalg.cond(A[ok]).max()
+    assert np.max(np.abs(pan[3][ok] - ref)) <= 1e-13 * cond * n * max(1.0, np.abs(ref).max())
+
+
 @pytest.mark.parametrize("n", [60, 502])
 def test_band_lu_large_batch_factor_then_solve(n):
     """From 2048 instances on, cfx_band_lu factors with the register kernel while cfx_band_lu_solve may pick the
