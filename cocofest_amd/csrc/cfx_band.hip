@@ -1184,19 +1184,20 @@ __global__ void __launch_bounds__(256) k_band_transpose(const T* __restrict__ sr
 // The global placement's column step is five barrier-separated phases over L2 (pivot search, swap, scale,
 // update): ≈ 13 µs per column for the 1,500-interval MSK KKT (n = 119,640, kl = ku = 108), 1.5 s per
 // factorisation.  Here, per panel of NB columns j0 .. j0 + NB - 1:
-//  1. the panel (its rows j0 .. j0 + NB - 1 + kl) is factored in LDS with ONE barrier per column: every wave
-//     finds the pivot itself (no broadcast), and every element of the active block is rewritten into the
-//     other of two buffers with the row interchange folded into its source row;
+//  1. the panel (its rows j0 .. j0 + NB - 1 + kl) is factored in one wavefront's registers, no LDS round trip
+//     and no barrier per column (an LDS version with one barrier per column spent ≈ 1 µs per column);
 //  2. the trailing columns j0 + NB .. ju (ju <= j0 + NB - 1 + kv) take the panel's interchanges and
-//     elimination at once: U12 = L11^-1 P A12 by one thread per column, A22 -= L21 U12 by one wave per column
-//     with the lanes over rows (band-storage columns are contiguous).  The multipliers of this step are the
-//     panel's with its later interchanges applied — Lt(r, k) = L(sigma_k(r), k), sigma_k(r) the row that held
-//     at step k what ends in row r — while the stored multipliers stay position-based (dgbtf2's, what every
-//     solve kernel reads).
+//     elimination at once, one wave per column with the lanes over the panel's rows (band-storage columns are
+//     contiguous): row r starts from original row q[r] (the interchanges composed), and for k = 0 .. NB - 1 the
+//     final U12 element of row k is broadcast (readlane) and subtracted times Lt(r, k) — U12 = L11^-1 P A12 in
+//     the lanes above NB, A22 -= L21 U12 below, no LDS image and no barrier; the column loads run one group
+//     ahead.  Lt(r, k) = L(sigma_k(r), k) are the panel's multipliers with its later interchanges applied,
+//     sigma_k(r) the row that held at step k what ends in row r; the stored multipliers stay position-based
+//     (dgbtf2's, what every solve kernel reads).
 // Every element receives the same operations in the same order as in the column step (the interchanges
 // commute with the eliminations they are moved past), so factors, pivots and zero-pivot reports equal the
 // global placement's (tested bit for bit).  Fill rows (storage rows < kl) are zeroed lazily, as columns
-// enter the trailing reach.
+// enter the trailing reach.  RH: 64-row chunks per lane (NB + kl <= 64 RH).
 #ifdef CFX_BAND_PROF
 __device__ unsigned long long g_panel_prof[8];  // phase clocks of instance 0, thread 0 (micro build only)
 #define PANEL_STAMP(i)                                                  \
@@ -1212,23 +1213,44 @@ __device__ unsigned long long g_panel_prof[8];  // phase clocks of instance 0, t
     do {               \
     } while (0)
 #endif
-template <int NB, int NT>
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v) {
+    return from32(__builtin_amdgcn_mov_dpp(lo32(v), CTRL, 0xf, 0xf, false),
+                  __builtin_amdgcn_mov_dpp(hi32(v), CTRL, 0xf, 0xf, false));
+}
+// max over the wave (every lane gets it): quad swaps, half-row and row mirrors (each lane then holds its
+// 16-lane row's max), then the four rows through readlane
+__device__ __forceinline__ double wave_max(double v) {
+    v = fmax(v, dpp_d<0xB1>(v));   // quad_perm [1, 0, 3, 2]
+    v = fmax(v, dpp_d<0x4E>(v));   // quad_perm [2, 3, 0, 1]
+    v = fmax(v, dpp_d<0x141>(v));  // row_half_mirror
+    v = fmax(v, dpp_d<0x140>(v));  // row_mirror
+    return fmax(fmax(lane_read(v, 0), lane_read(v, 16)), fmax(lane_read(v, 32), lane_read(v, 48)));
+}
+__device__ __forceinline__ int wave_min_i(int v) {
+    v = min(v, __builtin_amdgcn_mov_dpp(v, 0xB1, 0xf, 0xf, false));
+    v = min(v, __builtin_amdgcn_mov_dpp(v, 0x4E, 0xf, 0xf, false));
+    v = min(v, __builtin_amdgcn_mov_dpp(v, 0x141, 0xf, 0xf, false));
+    v = min(v, __builtin_amdgcn_mov_dpp(v, 0x140, 0xf, 0xf, false));
+    return min(min(__builtin_amdgcn_readlane(v, 0), __builtin_amdgcn_readlane(v, 16)),
+               min(__builtin_amdgcn_readlane(v, 32), __builtin_amdgcn_readlane(v, 48)));
+}
+
+template <int NB, int RH, int NT>
 __global__ void __launch_bounds__(NT) k_band_lu_panel(int n, int kl, int ku, double* __restrict__ AB,
                                                       int32_t* __restrict__ IPIV, int32_t* __restrict__ INFO) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
-    constexpr int NW = NT / 64, US = NB + 1;  // US: column stride of the trailing-column images (conflict-free)
+    constexpr int NW = NT / 64, US = NB + 1, CG = RH >= 4 ? 2 : 4;  // US: row stride of Lt (conflict-free); CG: columns per load group
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-    const int ldab = 2 * kl + ku + 1, kv = kl + ku, PR = NB + kl, WT = max(kv, 1);
+    const int ldab = 2 * kl + ku + 1, kv = kl + ku, PR = NB + kl;
     double* const ab = AB + (int64_t)blockIdx.x * n * ldab;
     int32_t* const piv = IPIV + (int64_t)blockIdx.x * n;
-    double* const P0 = smem;               // panel buffers, column-major [c][r], stride PR
-    double* const P1 = P0 + NB * PR;
-    double* const Lt = P1 + NB * PR;       // blocked multipliers, row-major [r][k], stride US
-    double* const Ut = Lt + PR * US;       // trailing columns' top rows, interchanged, then U12: [c'][k]
-    double* const To = Ut + WT * US;       // trailing columns' top rows as they were (for rows moved down)
-    int* const q = reinterpret_cast<int*>(To + WT * US);  // panel row r ends up holding original row q[r]
+    double* const P0 = smem;               // the panel, column-major [c][r], stride PR
+    double* const Lt = P0 + NB * PR;       // blocked multipliers, row-major [r][k], stride US
+    int* const q = reinterpret_cast<int*>(Lt + PR * US);  // panel row r ends up holding original row q[r]
     int* const sp = q + PR;                                // pivot row of each panel step (panel-relative)
-    auto at = [&](int i, int j) -> double& { return ab[(int64_t)j * ldab + kv + i - j]; };
+    int* const snz = sp + NB;                              // its pivot was non-zero
+    auto at = [&](int i, int j) CFX_INLINE -> double& { return ab[(int64_t)j * ldab + kv + i - j]; };
     int info = 0, ju = 0, zhi = -1;
 #ifdef CFX_BAND_PROF
     unsigned long long prof[8] = {}, last_ = wall_clock64();
@@ -1248,66 +1270,97 @@ __global__ void __launch_bounds__(NT) k_band_lu_panel(int n, int kl, int ku, dou
         }
         __syncthreads();
         PANEL_STAMP(1);
-        // 1. the panel: step jj reads one buffer and writes the active block (rows, columns >= jj) to the other
-        for (int jj = 0; jj < w; ++jj) {
-            const double* S = (jj & 1) ? P1 : P0;
-            double* T = (jj & 1) ? P0 : P1;
-            const int rmax = min(pr - 1, jj + kl);  // rows of the column step (km); below: zeros in column jj
-            double av = -1.0;
-            int ai = jj;
-            for (int r = jj + lane; r <= rmax; r += 64) {
-                const double v = fabs(S[jj * PR + r]);
-                if (v > av) {
-                    av = v;
-                    ai = r;
+        // 1. the panel, in wavefront 0's registers (lane: rows lane + 64 h; no LDS and no barrier per column): per
+        //    step the pivot (DPP reductions), the pivot row and row jj broadcast by readlane, and every row of the
+        //    active block rewritten in place with the interchange folded into its source row — the column step's
+        //    expressions, operand for operand
+        if (wave == 0) {
+            double pa[RH][NB];
+#pragma unroll
+            for (int h = 0; h < RH; ++h)
+#pragma unroll
+                for (int c = 0; c < NB; ++c) {
+                    const int r = lane + 64 * h;
+                    pa[h][c] = (r < pr && c < w) ? P0[c * PR + r] : 0.0;
+                }
+#pragma unroll
+            for (int jj = 0; jj < NB; ++jj) {
+                if (jj < w) {
+                    const int rmax = min(pr - 1, jj + kl);  // rows of the column step (km)
+                    double av = -1.0;
+                    int ai = jj;
+#pragma unroll
+                    for (int h = 0; h < RH; ++h) {  // first row of the largest |A(r, jj)| (NaN never wins)
+                        const int r = lane + 64 * h;
+                        const double v = fabs(pa[h][jj]);
+                        if (r >= jj && r <= rmax && v > av) {
+                            av = v;
+                            ai = r;
+                        }
+                    }
+                    const double amax = wave_max(av);
+                    const int pj = wave_min_i(av == amax ? ai : 0x7fffffff), ph = pj >> 6, pl = pj & 63;
+                    double u[NB], rj[NB];  // the pivot row and row jj, columns jj .. NB - 1
+#pragma unroll
+                    for (int c = 0; c < NB; ++c) {  // (full-range loops: unrolled before jj is, registers throughout)
+                        if (c >= jj) {
+                            double src = pa[0][c];
+#pragma unroll
+                            for (int h = 1; h < RH; ++h)
+                                if (ph == h) src = pa[h][c];
+                            u[c] = lane_read(src, pl);
+                            rj[c] = lane_read(pa[0][c], jj);
+                        }
+                    }
+                    const double pv = u[jj];
+                    const bool nz = pv != 0.0;
+                    const double inv = nz ? 1.0 / pv : 0.0;
+#pragma unroll
+                    for (int h = 0; h < RH; ++h) {
+                        const int r = lane + 64 * h;
+                        const bool isp = r == pj && r != jj;  // row pj takes row jj's elements
+                        const bool elim = nz && r > jj && r <= rmax;
+                        const double l = elim ? (isp ? rj[jj] : pa[h][jj]) * inv : 0.0;
+#pragma unroll
+                        for (int c = 0; c < NB; ++c) {
+                            if (c >= jj) {
+                                const double srcv = isp ? rj[c] : pa[h][c];
+                                double nv = pa[h][c];
+                                if (nz && r == jj)
+                                    nv = u[c];
+                                else if (elim)
+                                    nv = c == jj ? l : srcv - l * u[c];
+                                pa[h][c] = nv;
+                            }
+                        }
+                    }
+                    if (lane == 0) {
+                        sp[jj] = pj;
+                        snz[jj] = nz;
+                    }
                 }
             }
 #pragma unroll
-            for (int off = 32; off > 0; off >>= 1) {
-                const double ov = __shfl_xor(av, off);
-                const int oi = __shfl_xor(ai, off);
-                if (ov > av || (ov == av && oi < ai)) {
-                    av = ov;
-                    ai = oi;
+            for (int h = 0; h < RH; ++h)
+#pragma unroll
+                for (int c = 0; c < NB; ++c) {
+                    const int r = lane + 64 * h;
+                    if (r < pr && c < w) P0[c * PR + r] = pa[h][c];
                 }
-            }
-            const int pj = ai;
-            const double pv = S[jj * PR + pj];
-            const int m = pr - jj;
-            if (pv != 0.0) {
-                const double inv = 1.0 / pv;
-                for (int e = t; e < (w - jj) * m; e += NT) {
-                    const int c = jj + e / m, r = jj + e % m;
-                    const int s = r == jj ? pj : (r == pj ? jj : r);
-                    double v;
-                    if (r > rmax)
-                        v = S[c * PR + r];
-                    else if (c == jj)
-                        v = r == jj ? pv : S[jj * PR + s] * inv;
-                    else if (r == jj)
-                        v = S[c * PR + pj];
-                    else
-                        v = S[c * PR + s] - (S[jj * PR + s] * inv) * S[c * PR + pj];
-                    T[c * PR + r] = v;
-                }
-                ju = max(ju, min(j0 + ku + pj, n - 1));
-            } else {
-                for (int e = t; e < (w - jj) * m; e += NT) {
-                    const int c = jj + e / m, r = jj + e % m;
-                    T[c * PR + r] = S[c * PR + r];
-                }
-                if (info == 0) info = j0 + jj + 1;
-            }
-            if (t == 0) sp[jj] = pj;
-            __syncthreads();
+        }
+        __syncthreads();
+        for (int jj = 0; jj < w; ++jj) {  // LAPACK's column reach and first zero pivot, in every thread
+            if (snz[jj])
+                ju = max(ju, min(j0 + ku + sp[jj], n - 1));
+            else if (info == 0)
+                info = j0 + jj + 1;
         }
         PANEL_STAMP(2);
-        // the panel back to the band (element (r, c) is final after step min(r, c), in that step's output
-        // buffer), the pivots, the blocked multipliers and the composed interchanges
+        // the panel back to the band, the pivots, the blocked multipliers and the composed interchanges
         int spr[NB];
 #pragma unroll
         for (int i = 0; i < NB; ++i) spr[i] = i < w ? sp[i] : i;
-        auto sigma = [&](int r, int k) {  // interchanges w - 1 .. k + 1 undone
+        auto sigma = [&](int r, int k) CFX_INLINE {  // interchanges w - 1 .. k + 1 undone
             int s = r;
 #pragma unroll
             for (int i = NB - 1; i >= 0; --i)
@@ -1316,80 +1369,68 @@ __global__ void __launch_bounds__(NT) k_band_lu_panel(int n, int kl, int ku, dou
         };
         for (int e = t; e < w * pr; e += NT) {
             const int c = e / pr, r = e - c * pr;
-            const double* F = (min(r, c) & 1) ? P0 : P1;
-            if (r - c <= kl && c - r <= kv) at(j0 + r, j0 + c) = F[c * PR + r];
-            const int k = e % w, rr = e / w;
-            Lt[rr * US + k] = rr > k ? ((k & 1) ? P0 : P1)[k * PR + sigma(rr, k)] : 0.0;
+            if (r - c <= kl && c - r <= kv) at(j0 + r, j0 + c) = P0[c * PR + r];
+        }
+        for (int e = t; e < NB * pr; e += NT) {
+            const int k = e % NB, rr = e / NB;
+            Lt[rr * US + k] = (rr > k && k < w) ? P0[k * PR + sigma(rr, k)] : 0.0;
         }
         for (int r = t; r < pr; r += NT) q[r] = sigma(r, -1);
         if (t < w) piv[j0 + t] = j0 + sp[t];
         const int c0 = j0 + w, wt = ju - c0 + 1;  // trailing columns c0 .. ju
-        __syncthreads();
+        // LDS only (Lt, q): the panel's global stores are read again only after the next panel's first barrier
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
         PANEL_STAMP(3);
+        // 2. trailing columns, one wave each; lane holds rows lane + 64 h of the column
         if (wt > 0) {
-            // 2a. the trailing columns' top rows, interchanged (Ut) and as they were (To)
-            for (int e = t; e < wt * w; e += NT) {
-                const int cc = e / w, k = e - cc * w, c = c0 + cc, i = j0 + q[k];
-                Ut[cc * US + k] = c - i <= kv ? at(i, c) : 0.0;
-                To[cc * US + k] = c - (j0 + k) <= kv ? at(j0 + k, c) : 0.0;
+            double lr[RH][NB];
+            int qr[RH];
+#pragma unroll
+            for (int h = 0; h < RH; ++h) {
+                const int r = lane + 64 * h;
+                qr[h] = r < pr ? q[r] : -1;
+#pragma unroll
+                for (int k = 0; k < NB; ++k) lr[h][k] = r < pr ? Lt[r * US + k] : 0.0;
             }
-            __syncthreads();
-            PANEL_STAMP(4);
-            // 2b. U12 = L11^-1 (P A12), one thread per column, in the column step's order
-            for (int cc = t; cc < wt; cc += NT) {
-                double x[NB];
+            auto load = [&](int cc, double (&x)[RH]) CFX_INLINE {
+                const int c = c0 + cc;
 #pragma unroll
-                for (int k = 0; k < NB; ++k) x[k] = k < w ? Ut[cc * US + k] : 0.0;
+                for (int h = 0; h < RH; ++h)
+                    x[h] = (cc < wt && qr[h] >= 0 && c - (j0 + qr[h]) <= kv) ? at(j0 + qr[h], c) : 0.0;
+            };
+            double cur[CG][RH], nxt[CG][RH];
 #pragma unroll
-                for (int k = 0; k < NB; ++k)
+            for (int g = 0; g < CG; ++g) load(wave + g * NW, cur[g]);
+            for (int cb = wave; cb < wt; cb += NW * CG) {
 #pragma unroll
-                    for (int r = k + 1; r < NB; ++r)
-                        if (r < w) x[r] -= Lt[r * US + k] * x[k];
+                for (int g = 0; g < CG; ++g) load(cb + (g + CG) * NW, nxt[g]);
 #pragma unroll
-                for (int k = 0; k < NB; ++k)
-                    if (k < w) Ut[cc * US + k] = x[k];
-            }
-            __syncthreads();
-            PANEL_STAMP(5);
-            // 2c. A22 -= L21 U12 (rows w .. pr - 1: rows moved down start from their original top row), one wave
-            // per column, lanes over rows; the wave also stores the column's U12 rows
-            for (int h0 = 0; h0 < max(pr - w, 1); h0 += 128) {
-                const int r0 = w + h0 + lane, r1 = r0 + 64;
-                const bool ok0 = r0 < pr, ok1 = r1 < pr;
-                const int q0 = ok0 ? q[r0] : r0, q1 = ok1 ? q[r1] : r1;
-                double l0[NB], l1[NB];
+                for (int g = 0; g < CG; ++g) {
+                    const int cc = cb + g * NW, c = c0 + cc;
+                    double (&x)[RH] = cur[g];
 #pragma unroll
-                for (int k = 0; k < NB; ++k) {
-                    l0[k] = ok0 ? Lt[r0 * US + k] : 0.0;
-                    l1[k] = ok1 ? Lt[r1 * US + k] : 0.0;
-                }
-                constexpr int CG = 4;  // columns in flight per wave
-                for (int cb = wave; cb < wt; cb += NW * CG) {
-                    double y0[CG], y1[CG];
+                    for (int k = 0; k < NB; ++k) {
+                        if (k < w) {  // (uniform; no break: the loop stays fully unrolled, lr in registers)
+                            const double xk = lane_read(x[0], k);  // row k: final (U12) once steps 0 .. k - 1 are in
+                            x[0] = lane > k ? x[0] - lr[0][k] * xk : x[0];
 #pragma unroll
-                    for (int g = 0; g < CG; ++g) {
-                        const int cc = cb + g * NW, c = c0 + cc;
-                        const bool okc = cc < wt;
-                        y0[g] = okc && ok0 ? (q0 != r0 ? To[cc * US + q0] : at(j0 + r0, c)) : 0.0;
-                        y1[g] = okc && ok1 ? (q1 != r1 ? To[cc * US + q1] : at(j0 + r1, c)) : 0.0;
+                            for (int h = 1; h < RH; ++h) x[h] -= lr[h][k] * xk;
+                        }
                     }
+                    if (cc < wt) {
 #pragma unroll
-                    for (int g = 0; g < CG; ++g) {
-                        const int cc = cb + g * NW, c = c0 + cc;
-                        if (cc >= wt) break;
-                        const double* uc = Ut + cc * US;
-                        if (h0 == 0 && lane < w && c - (j0 + lane) <= kv) at(j0 + lane, c) = uc[lane];
-#pragma unroll
-                        for (int k = 0; k < NB; ++k)
-                            if (k < w) {
-                                const double u = uc[k];
-                                y0[g] -= l0[k] * u;
-                                y1[g] -= l1[k] * u;
-                            }
-                        if (ok0) at(j0 + r0, c) = y0[g];
-                        if (ok1) at(j0 + r1, c) = y1[g];
+                        for (int h = 0; h < RH; ++h) {
+                            const int r = lane + 64 * h;
+                            if (r < pr && (r >= w || c - (j0 + r) <= kv)) at(j0 + r, c) = x[h];
+                        }
                     }
                 }
+#pragma unroll
+                for (int g = 0; g < CG; ++g)
+#pragma unroll
+                    for (int h = 0; h < RH; ++h) cur[g][h] = nxt[g][h];
             }
         }
         // (the next panel's first barrier orders these stores before its loads)
@@ -1748,16 +1789,16 @@ static hipError_t lane_dispatch(int64_t n, int32_t kl, int32_t ku, int64_t batch
 #undef CFX_LANE
 }
 
-// Panel placement (single bands too wide for LDS and registers: what the global placement would take): LDS bytes of
-// k_band_lu_panel<nb>; the panel width that fits (16, else 8, else 0: not applicable).
-static size_t panel_lds(int nb, int32_t kl, int32_t ku) {
-    const int64_t pr = nb + (int64_t)kl, wt = std::max<int64_t>((int64_t)kl + ku, 1);
-    return (size_t)(8 * (2 * nb * pr + pr * (nb + 1) + 2 * wt * (nb + 1)) + 4 * (pr + nb));
+// Panel placement (single bands too wide for LDS and registers: what the global placement would take): 16-column
+// panels with the panel's rows (16 + kl <= 256) in at most four 64-row chunks per lane; LDS bytes of k_band_lu_panel.
+constexpr int kPanelNB = 16;
+static size_t panel_lds(int32_t kl) {
+    const int64_t pr = kPanelNB + (int64_t)kl;
+    return (size_t)(8 * (kPanelNB * pr + pr * (kPanelNB + 1)) + 4 * (pr + 2 * kPanelNB));
 }
-static int panel_nb(int32_t kl, int32_t ku) {
-    if (panel_lds(16, kl, ku) <= (size_t)kBandLds) return 16;
-    if (panel_lds(8, kl, ku) <= (size_t)kBandLds) return 8;
-    return 0;
+static int panel_rh(int32_t kl) {  // 64-row chunks per lane, 0: not applicable
+    const int64_t pr = kPanelNB + (int64_t)kl;
+    return (pr <= 256 && panel_lds(kl) <= (size_t)kBandLds) ? (int)((pr + 63) / 64) : 0;
 }
 // streamed solves: window registers per lane (forward kl < 64 KF, backward kl + ku < 64 KB)
 static bool stream_ok(int32_t kl, int32_t ku) { return kl <= 255 && kl + ku <= 511; }
@@ -1786,22 +1827,28 @@ static hipError_t launch_bwd(int64_t n, int32_t kl, int32_t ku, int64_t batch, c
     return hipGetLastError();
 }
 
+template <int RH>
+static hipError_t launch_panel_rh(int64_t n, int32_t kl, int32_t ku, int64_t batch, double* ab, int32_t* ipiv,
+                                  int32_t* info, hipStream_t s) {
+    const size_t lds = panel_lds(kl);
+    hipError_t e = allow_lds(&k_band_lu_panel<kPanelNB, RH, 512>, lds);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL((k_band_lu_panel<kPanelNB, RH, 512>), dim3((unsigned)batch), dim3(512), lds, s, (int)n, kl, ku,
+                       ab, ipiv, info);
+    return hipGetLastError();
+}
+
 static hipError_t launch_panel(int64_t n, int32_t kl, int32_t ku, int64_t batch, double* ab, int32_t* ipiv,
                                int32_t* info, int32_t nrhs, double* rhs, hipStream_t s, int factor) {
     hipError_t e = hipSuccess;
     if (factor) {
-        const int nb = panel_nb(kl, ku);
-        const size_t lds = panel_lds(nb, kl, ku);
-        if (nb == 16) {
-            if ((e = allow_lds(&k_band_lu_panel<16, 512>, lds)) != hipSuccess) return e;
-            hipLaunchKernelGGL((k_band_lu_panel<16, 512>), dim3((unsigned)batch), dim3(512), lds, s, (int)n, kl, ku, ab,
-                               ipiv, info);
-        } else {
-            if ((e = allow_lds(&k_band_lu_panel<8, 512>, lds)) != hipSuccess) return e;
-            hipLaunchKernelGGL((k_band_lu_panel<8, 512>), dim3((unsigned)batch), dim3(512), lds, s, (int)n, kl, ku, ab,
-                               ipiv, info);
+        switch (panel_rh(kl)) {
+            case 1: e = launch_panel_rh<1>(n, kl, ku, batch, ab, ipiv, info, s); break;
+            case 2: e = launch_panel_rh<2>(n, kl, ku, batch, ab, ipiv, info, s); break;
+            case 3: e = launch_panel_rh<3>(n, kl, ku, batch, ab, ipiv, info, s); break;
+            default: e = launch_panel_rh<4>(n, kl, ku, batch, ab, ipiv, info, s); break;
         }
-        if ((e = hipGetLastError()) != hipSuccess) return e;
+        if (e != hipSuccess) return e;
     }
     if (nrhs < 1) return hipSuccess;
     if (!stream_ok(kl, ku)) {  // the global placement's substitutions
@@ -1860,7 +1907,7 @@ static int band_launch(int64_t n, int32_t kl, int32_t ku, int64_t batch, double*
         placement = lds_full <= (size_t)kBandLds ? 1 : 2;
     else if (forced && *forced == '2')
         placement = 2;
-    else if (forced && *forced == '5' && panel_nb(kl, ku) > 0)
+    else if (forced && *forced == '5' && panel_rh(kl) > 0)
         placement = 5;
     else if (!force_full && !forced && reg_ok)
         placement = 3;
@@ -1868,7 +1915,7 @@ static int band_launch(int64_t n, int32_t kl, int32_t ku, int64_t batch, double*
         placement = 0;
     else
         placement = lds_full <= (size_t)kBandLds ? 1 : 2;
-    if (placement == 2 && !force_full && !forced && panel_nb(kl, ku) > 0) placement = 5;
+    if (placement == 2 && !force_full && !forced && panel_rh(kl) > 0) placement = 5;
     const size_t lds = placement == 0 ? lds_win : (placement == 1 ? lds_full : 0);
     // threads per instance: enough lanes for the rank-1 update of the trailing km x (kl + ku) block
     const int64_t work = (int64_t)kl * (kl + ku);

@@ -54,7 +54,7 @@ int main(int argc, char** argv) {
         CK(hipEventElapsedTime(&ms, a, b));
         unsigned long long p[8];
         CK(hipMemcpyFromSymbol(p, HIP_SYMBOL(cfx::g_panel_prof), sizeof(p)));
-        const int nb = cfx::panel_nb(kl, ku), panels = (n + nb - 1) / nb;
+        const int nb = cfx::kPanelNB, panels = (n + nb - 1) / nb;
         const char* names[7] = {"zero_fill", "panel_load", "panel_steps", "writeback_lt", "trail_load", "u12",
                                 "a22"};
         std::printf("{\"n\": %d, \"kl\": %d, \"ku\": %d, \"nb\": %d, \"ms\": %.3f, \"us_per_panel\": %.3f", n, kl, ku,

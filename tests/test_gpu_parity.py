@@ -542,7 +542,7 @@ def test_band_lu_panel_placement(B, n, kl, ku, zero_diag, monkeypatch):
     """The panel placement (single wide bands: blocked factorisation, streamed one-wave solves; CFX_BAND_PLACEMENT=5)
     against the global placement (=2), whose column step it reorders: the same factors, pivots and zero-pivot
     reports bit for bit, the same solutions, factors of one solved by the other's kernels; numpy's dense solve.
-    kl = ku = 200: the 8-column panel (the 16-column one exceeds LDS)."""
+    kl = ku = 200: four 64-row chunks per lane."""
     import torch
 
     from cocofest_amd import _cfx
