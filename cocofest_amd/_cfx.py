@@ -15,7 +15,7 @@ import numpy as np
 
 LIB_PATH = pathlib.Path(__file__).with_name("libcfx.so")
 
-ABI_VERSION = 7
+ABI_VERSION = 8
 OK, EINVAL, EHIP, ENOMEM, EUNSUPPORTED, ENODEV, ECALLBACK = 0, -1, -2, -3, -4, -5, -6
 MODEL_IDS = {
     "ding2003": 0,
@@ -117,7 +117,10 @@ class IpmOptions(C.Structure):
                 ("required_infeasibility_reduction", C.c_double), ("filter_reset_trigger", C.c_int32),
                 ("max_filter_resets", C.c_int32), ("max_wall_time", C.c_double), ("print_frequency_time", C.c_double),
                 ("soft_resto_pderror_reduction_factor", C.c_double), ("max_soft_resto_iters", C.c_int32),
-                ("resto_failure_restart", C.c_int32)]
+                ("resto_failure_restart", C.c_int32), ("constr_viol_tol", C.c_double),
+                ("dual_inf_tol", C.c_double), ("compl_inf_tol", C.c_double),
+                ("acceptable_constr_viol_tol", C.c_double), ("acceptable_dual_inf_tol", C.c_double),
+                ("acceptable_compl_inf_tol", C.c_double)]
 
 
 # cfx_ipm_get_status values (Ipopt's ApplicationReturnStatus)

@@ -1185,7 +1185,9 @@ __global__ void __launch_bounds__(256) k_band_transpose(const T* __restrict__ sr
 // update): ≈ 13 µs per column for the 1,500-interval MSK KKT (n = 119,640, kl = ku = 108), 1.5 s per
 // factorisation.  Here, per panel of NB columns j0 .. j0 + NB - 1:
 //  1. the panel (its rows j0 .. j0 + NB - 1 + kl) is factored in one wavefront's registers, no LDS round trip
-//     and no barrier per column (an LDS version with one barrier per column spent ≈ 1 µs per column);
+//     and no barrier per column (an LDS version with one barrier per column spent ≈ 1 µs per column), and with
+//     look-ahead: wavefront 0 takes the next panel's columns of step 2 first and factors that panel while the
+//     other waves finish step 2 for the current one;
 //  2. the trailing columns j0 + NB .. ju (ju <= j0 + NB - 1 + kv) take the panel's interchanges and
 //     elimination at once, one wave per column with the lanes over the panel's rows (band-storage columns are
 //     contiguous): row r starts from original row q[r] (the interchanges composed), and for k = 0 .. NB - 1 the
@@ -1240,123 +1242,174 @@ template <int NB, int RH, int NT>
 __global__ void __launch_bounds__(NT) k_band_lu_panel(int n, int kl, int ku, double* __restrict__ AB,
                                                       int32_t* __restrict__ IPIV, int32_t* __restrict__ INFO) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
-    constexpr int NW = NT / 64, US = NB + 1, CG = RH >= 4 ? 2 : 4;  // US: row stride of Lt (conflict-free); CG: columns per load group
+    constexpr int NW = NT / 64, US = NB + 1, CG = RH >= 3 ? 2 : 4;  // US: row stride of Lt (conflict-free); CG: columns per load group
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
     const int ldab = 2 * kl + ku + 1, kv = kl + ku, PR = NB + kl;
     double* const ab = AB + (int64_t)blockIdx.x * n * ldab;
     int32_t* const piv = IPIV + (int64_t)blockIdx.x * n;
-    double* const P0 = smem;               // the panel, column-major [c][r], stride PR
+    double* const P0 = smem;               // the factored panel, column-major [c][r], stride PR
     double* const Lt = P0 + NB * PR;       // blocked multipliers, row-major [r][k], stride US
     int* const q = reinterpret_cast<int*>(Lt + PR * US);  // panel row r ends up holding original row q[r]
     int* const sp = q + PR;                                // pivot row of each panel step (panel-relative)
     int* const snz = sp + NB;                              // its pivot was non-zero
     auto at = [&](int i, int j) CFX_INLINE -> double& { return ab[(int64_t)j * ldab + kv + i - j]; };
-    int info = 0, ju = 0, zhi = -1;
-#ifdef CFX_BAND_PROF
-    unsigned long long prof[8] = {}, last_ = wall_clock64();
-#endif
-    for (int j0 = 0; j0 < n; j0 += NB) {
-        const int w = min(NB, n - j0), pr = min(w + kl, n - j0);
-        // fill rows of the columns entering the reach of this panel's rows (no earlier step touched them)
-        const int zend = min(j0 + w - 1 + kv, n - 1);
-        for (int64_t e = t; e < (int64_t)(zend - zhi) * kl; e += NT)
+    // fill rows (storage rows < kl) of columns zhi + 1 .. zend, as columns enter the reach of a panel's rows
+    auto zero_fill = [&](int zhi, int zend, int tid, int nthr) CFX_INLINE {
+        for (int64_t e = tid; e < (int64_t)(zend - zhi) * kl; e += nthr)
             ab[(int64_t)(zhi + 1 + e / kl) * ldab + e % kl] = 0.0;
-        zhi = max(zhi, zend);
-        __syncthreads();
-        PANEL_STAMP(0);
-        for (int e = t; e < w * pr; e += NT) {
-            const int c = e / pr, r = e - c * pr;
-            P0[c * PR + r] = (r - c <= kl && c - r <= kv) ? at(j0 + r, j0 + c) : 0.0;
+    };
+    // 1. panel j0p (width wp, rows prp) in wavefront 0's registers (lane: rows lane + 64 h; no LDS and no barrier per
+    //    column): per step the pivot (DPP reductions), the pivot row and row jj broadcast by readlane, and every row
+    //    of the active block rewritten in place with the interchange folded into its source row — the column step's
+    //    expressions, operand for operand.  Leaves the factored panel in P0 and the pivots in sp / snz.
+    auto factor_panel = [&](int j0p, int wp, int prp) CFX_INLINE {
+        double pa[RH][NB];
+#pragma unroll
+        for (int h = 0; h < RH; ++h)
+#pragma unroll
+            for (int c = 0; c < NB; ++c) {
+                const int r = lane + 64 * h;
+                pa[h][c] = (r < prp && c < wp && r - c <= kl && c - r <= kv) ? at(j0p + r, j0p + c) : 0.0;
+            }
+#pragma unroll
+        for (int jj = 0; jj < NB; ++jj) {
+            if (jj < wp) {
+                const int rmax = min(prp - 1, jj + kl);  // rows of the column step (km)
+                double av = -1.0;
+                int ai = jj;
+#pragma unroll
+                for (int h = 0; h < RH; ++h) {  // first row of the largest |A(r, jj)| (NaN never wins)
+                    const int r = lane + 64 * h;
+                    const double v = fabs(pa[h][jj]);
+                    if (r >= jj && r <= rmax && v > av) {
+                        av = v;
+                        ai = r;
+                    }
+                }
+                const double amax = wave_max(av);
+                const int pj = wave_min_i(av == amax ? ai : 0x7fffffff), ph = pj >> 6, pl = pj & 63;
+                double u[NB], rj[NB];  // the pivot row and row jj, columns jj .. NB - 1
+#pragma unroll
+                for (int c = 0; c < NB; ++c) {  // (full-range loops: unrolled before jj is, registers throughout)
+                    if (c >= jj) {
+                        double src = pa[0][c];
+#pragma unroll
+                        for (int h = 1; h < RH; ++h)
+                            if (ph == h) src = pa[h][c];
+                        u[c] = lane_read(src, pl);
+                        rj[c] = lane_read(pa[0][c], jj);
+                    }
+                }
+                const double pv = u[jj];
+                const bool nz = pv != 0.0;
+                const double inv = nz ? 1.0 / pv : 0.0;
+#pragma unroll
+                for (int h = 0; h < RH; ++h) {
+                    const int r = lane + 64 * h;
+                    const bool isp = r == pj && r != jj;  // row pj takes row jj's elements
+                    const bool elim = nz && r > jj && r <= rmax;
+                    const double l = elim ? (isp ? rj[jj] : pa[h][jj]) * inv : 0.0;
+#pragma unroll
+                    for (int c = 0; c < NB; ++c) {
+                        if (c >= jj) {
+                            const double srcv = isp ? rj[c] : pa[h][c];
+                            double nv = pa[h][c];
+                            if (nz && r == jj)
+                                nv = u[c];
+                            else if (elim)
+                                nv = c == jj ? l : srcv - l * u[c];
+                            pa[h][c] = nv;
+                        }
+                    }
+                }
+                if (lane == 0) {
+                    sp[jj] = pj;
+                    snz[jj] = nz;
+                }
+            }
         }
-        __syncthreads();
-        PANEL_STAMP(1);
-        // 1. the panel, in wavefront 0's registers (lane: rows lane + 64 h; no LDS and no barrier per column): per
-        //    step the pivot (DPP reductions), the pivot row and row jj broadcast by readlane, and every row of the
-        //    active block rewritten in place with the interchange folded into its source row — the column step's
-        //    expressions, operand for operand
-        if (wave == 0) {
-            double pa[RH][NB];
+#pragma unroll
+        for (int h = 0; h < RH; ++h)
+#pragma unroll
+            for (int c = 0; c < NB; ++c) {
+                const int r = lane + 64 * h;
+                if (r < prp && c < wp) P0[c * PR + r] = pa[h][c];
+            }
+    };
+    // 2. trailing columns c0 + cc (cc = cb, cb + stride, ... < ce) of panel j0 (width w, rows pr), one wave each: lane
+    //    holds rows lane + 64 h; row r starts from original row q[r], and for k = 0 .. w - 1 the final U12 element of
+    //    row k is broadcast (readlane) and subtracted times Lt(r, k) (zero for r <= k); the loads run one group ahead
+    auto trail = [&](int j0, int w, int pr, int c0, int cb0, int ce, int stride) CFX_INLINE {
+        double lr[RH][NB];
+        int qr[RH];
+#pragma unroll
+        for (int h = 0; h < RH; ++h) {
+            const int r = lane + 64 * h;
+            qr[h] = r < pr ? q[r] : -1;
+#pragma unroll
+            for (int k = 0; k < NB; ++k) lr[h][k] = r < pr ? Lt[r * US + k] : 0.0;
+        }
+        auto load = [&](int cc, double (&x)[RH]) CFX_INLINE {
+            const int c = c0 + cc;
 #pragma unroll
             for (int h = 0; h < RH; ++h)
+                x[h] = (cc < ce && qr[h] >= 0 && c - (j0 + qr[h]) <= kv) ? at(j0 + qr[h], c) : 0.0;
+        };
+        double cur[CG][RH], nxt[CG][RH];
 #pragma unroll
-                for (int c = 0; c < NB; ++c) {
-                    const int r = lane + 64 * h;
-                    pa[h][c] = (r < pr && c < w) ? P0[c * PR + r] : 0.0;
+        for (int g = 0; g < CG; ++g) load(cb0 + g * stride, cur[g]);
+        for (int cb = cb0; cb < ce; cb += stride * CG) {
+#pragma unroll
+            for (int g = 0; g < CG; ++g) load(cb + (g + CG) * stride, nxt[g]);
+#pragma unroll
+            for (int g = 0; g < CG; ++g) {
+                const int cc = cb + g * stride, c = c0 + cc;
+                double (&x)[RH] = cur[g];
+#pragma unroll
+                for (int k = 0; k < NB; ++k) {
+                    if (k < w) {  // (uniform; no break: the loop stays fully unrolled, lr in registers)
+                        const double xk = lane_read(x[0], k);  // row k: final (U12) once steps 0 .. k - 1 are in
+#pragma unroll
+                        for (int h = 0; h < RH; ++h) x[h] -= lr[h][k] * xk;
+                    }
                 }
-#pragma unroll
-            for (int jj = 0; jj < NB; ++jj) {
-                if (jj < w) {
-                    const int rmax = min(pr - 1, jj + kl);  // rows of the column step (km)
-                    double av = -1.0;
-                    int ai = jj;
-#pragma unroll
-                    for (int h = 0; h < RH; ++h) {  // first row of the largest |A(r, jj)| (NaN never wins)
-                        const int r = lane + 64 * h;
-                        const double v = fabs(pa[h][jj]);
-                        if (r >= jj && r <= rmax && v > av) {
-                            av = v;
-                            ai = r;
-                        }
-                    }
-                    const double amax = wave_max(av);
-                    const int pj = wave_min_i(av == amax ? ai : 0x7fffffff), ph = pj >> 6, pl = pj & 63;
-                    double u[NB], rj[NB];  // the pivot row and row jj, columns jj .. NB - 1
-#pragma unroll
-                    for (int c = 0; c < NB; ++c) {  // (full-range loops: unrolled before jj is, registers throughout)
-                        if (c >= jj) {
-                            double src = pa[0][c];
-#pragma unroll
-                            for (int h = 1; h < RH; ++h)
-                                if (ph == h) src = pa[h][c];
-                            u[c] = lane_read(src, pl);
-                            rj[c] = lane_read(pa[0][c], jj);
-                        }
-                    }
-                    const double pv = u[jj];
-                    const bool nz = pv != 0.0;
-                    const double inv = nz ? 1.0 / pv : 0.0;
+                if (cc < ce) {
 #pragma unroll
                     for (int h = 0; h < RH; ++h) {
                         const int r = lane + 64 * h;
-                        const bool isp = r == pj && r != jj;  // row pj takes row jj's elements
-                        const bool elim = nz && r > jj && r <= rmax;
-                        const double l = elim ? (isp ? rj[jj] : pa[h][jj]) * inv : 0.0;
-#pragma unroll
-                        for (int c = 0; c < NB; ++c) {
-                            if (c >= jj) {
-                                const double srcv = isp ? rj[c] : pa[h][c];
-                                double nv = pa[h][c];
-                                if (nz && r == jj)
-                                    nv = u[c];
-                                else if (elim)
-                                    nv = c == jj ? l : srcv - l * u[c];
-                                pa[h][c] = nv;
-                            }
-                        }
-                    }
-                    if (lane == 0) {
-                        sp[jj] = pj;
-                        snz[jj] = nz;
+                        if (r < pr && (r >= w || c - (j0 + r) <= kv)) at(j0 + r, c) = x[h];
                     }
                 }
             }
 #pragma unroll
-            for (int h = 0; h < RH; ++h)
+            for (int g = 0; g < CG; ++g)
 #pragma unroll
-                for (int c = 0; c < NB; ++c) {
-                    const int r = lane + 64 * h;
-                    if (r < pr && c < w) P0[c * PR + r] = pa[h][c];
-                }
+                for (int h = 0; h < RH; ++h) cur[g][h] = nxt[g][h];
         }
+    };
+    int info = 0, ju = 0, zhi = -1;
+#ifdef CFX_BAND_PROF
+    unsigned long long prof[8] = {}, last_ = wall_clock64();
+#endif
+    {  // prologue: the first panel
+        const int w0 = min(NB, n), zend = min(w0 - 1 + kv, n - 1);
+        zero_fill(zhi, zend, t, NT);
+        zhi = zend;
         __syncthreads();
-        for (int jj = 0; jj < w; ++jj) {  // LAPACK's column reach and first zero pivot, in every thread
+        if (wave == 0) factor_panel(0, w0, min(w0 + kl, n));
+        __syncthreads();
+    }
+    for (int j0 = 0; j0 < n; j0 += NB) {
+        const int w = min(NB, n - j0), pr = min(w + kl, n - j0);
+        // the factored panel (P0, sp, snz): LAPACK's column reach and first zero pivot in every thread; the panel back
+        // to the band, the pivots, the blocked multipliers and the composed interchanges
+        for (int jj = 0; jj < w; ++jj) {
             if (snz[jj])
                 ju = max(ju, min(j0 + ku + sp[jj], n - 1));
             else if (info == 0)
                 info = j0 + jj + 1;
         }
         PANEL_STAMP(2);
-        // the panel back to the band, the pivots, the blocked multipliers and the composed interchanges
         int spr[NB];
 #pragma unroll
         for (int i = 0; i < NB; ++i) spr[i] = i < w ? sp[i] : i;
@@ -1377,63 +1430,29 @@ __global__ void __launch_bounds__(NT) k_band_lu_panel(int n, int kl, int ku, dou
         }
         for (int r = t; r < pr; r += NT) q[r] = sigma(r, -1);
         if (t < w) piv[j0 + t] = j0 + sp[t];
-        const int c0 = j0 + w, wt = ju - c0 + 1;  // trailing columns c0 .. ju
-        // LDS only (Lt, q): the panel's global stores are read again only after the next panel's first barrier
+        // LDS only (Lt, q; P0 and sp free after it): the panel's global stores are read again only after the next
+        // full barrier
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
         __builtin_amdgcn_s_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
         PANEL_STAMP(3);
-        // 2. trailing columns, one wave each; lane holds rows lane + 64 h of the column
-        if (wt > 0) {
-            double lr[RH][NB];
-            int qr[RH];
-#pragma unroll
-            for (int h = 0; h < RH; ++h) {
-                const int r = lane + 64 * h;
-                qr[h] = r < pr ? q[r] : -1;
-#pragma unroll
-                for (int k = 0; k < NB; ++k) lr[h][k] = r < pr ? Lt[r * US + k] : 0.0;
+        // 2. the trailing columns c0 .. ju, with look-ahead: wavefront 0 updates the next panel's columns, zeroes the
+        //    fill rows entering that panel's reach, re-reads the panel and factors it (step 1) while the other waves
+        //    update the rest
+        const int c0 = j0 + w, wt = ju - c0 + 1, jn = c0, wn = min(NB, n - jn);
+        const int zend = wn > 0 ? min(jn + wn - 1 + kv, n - 1) : zhi;
+        if (wave == 0) {
+            if (wn > 0) {
+                if (wt > 0) trail(j0, w, pr, c0, 0, min(wn, wt), 1);
+                zero_fill(zhi, zend, lane, 64);
+                __threadfence_block();  // this wave's stores before its loads of the next panel
+                factor_panel(jn, wn, min(wn + kl, n - jn));
             }
-            auto load = [&](int cc, double (&x)[RH]) CFX_INLINE {
-                const int c = c0 + cc;
-#pragma unroll
-                for (int h = 0; h < RH; ++h)
-                    x[h] = (cc < wt && qr[h] >= 0 && c - (j0 + qr[h]) <= kv) ? at(j0 + qr[h], c) : 0.0;
-            };
-            double cur[CG][RH], nxt[CG][RH];
-#pragma unroll
-            for (int g = 0; g < CG; ++g) load(wave + g * NW, cur[g]);
-            for (int cb = wave; cb < wt; cb += NW * CG) {
-#pragma unroll
-                for (int g = 0; g < CG; ++g) load(cb + (g + CG) * NW, nxt[g]);
-#pragma unroll
-                for (int g = 0; g < CG; ++g) {
-                    const int cc = cb + g * NW, c = c0 + cc;
-                    double (&x)[RH] = cur[g];
-#pragma unroll
-                    for (int k = 0; k < NB; ++k) {
-                        if (k < w) {  // (uniform; no break: the loop stays fully unrolled, lr in registers)
-                            const double xk = lane_read(x[0], k);  // row k: final (U12) once steps 0 .. k - 1 are in
-                            x[0] = lane > k ? x[0] - lr[0][k] * xk : x[0];
-#pragma unroll
-                            for (int h = 1; h < RH; ++h) x[h] -= lr[h][k] * xk;
-                        }
-                    }
-                    if (cc < wt) {
-#pragma unroll
-                        for (int h = 0; h < RH; ++h) {
-                            const int r = lane + 64 * h;
-                            if (r < pr && (r >= w || c - (j0 + r) <= kv)) at(j0 + r, c) = x[h];
-                        }
-                    }
-                }
-#pragma unroll
-                for (int g = 0; g < CG; ++g)
-#pragma unroll
-                    for (int h = 0; h < RH; ++h) cur[g][h] = nxt[g][h];
-            }
+        } else if (wt > wn) {
+            trail(j0, w, pr, c0, wn + wave - 1, wt, NW - 1);
         }
-        // (the next panel's first barrier orders these stores before its loads)
+        zhi = max(zhi, zend);
+        __syncthreads();
         PANEL_STAMP(6);
     }
 #ifdef CFX_BAND_PROF
@@ -1455,7 +1474,7 @@ __global__ void __launch_bounds__(NT) k_band_fwd_stream(int n, int kl, int ku, i
                                                         const double* __restrict__ AB,
                                                         const int32_t* __restrict__ IPIV, double* RHS) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
-    constexpr int CW = 64 * KF, CH = 128 / KF, NP = NT - 64;
+    constexpr int CW = 64 * KF, CH = 128 / KF, NP = NT - 64, SD = 4;
     const int t = threadIdx.x, lane = t & 63;
     const int ldab = 2 * kl + ku + 1, kv = kl + ku, fk = kl >> 6, lk = kl & 63;
     const double* const ab = AB + (int64_t)blockIdx.x * n * ldab;
@@ -1497,33 +1516,51 @@ __global__ void __launch_bounds__(NT) k_band_fwd_stream(int n, int kl, int ku, i
             if (t < 64) {
                 const int b = ci & 1, jb = ci * CH, cnt = min(CH, steps - jb);
                 const double* Mb = M + b * CH * CW;
-                for (int jj = 0; jj < cnt; ++jj) {
-                    const int j = jb + jj;
-                    double lc[KF];
+                // the buffer's reads run SD steps ahead of their use (a register ring, unrolled)
+                auto fetch = [&](int jj, double (&lc)[KF], int& p, double& nx) CFX_INLINE {
+                    const int jc = min(jj, CH - 1);
 #pragma unroll
-                    for (int f = 0; f < KF; ++f) lc[f] = Mb[jj * CW + lane + 64 * f];
-                    const int p = __builtin_amdgcn_readfirstlane(Pv[b * CH + jj]);
-                    const double nxv = X[b * CH + jj];
-                    if (p != 0) {
-                        const int fp = p >> 6, lp = p & 63;
-                        double src = xw[0];
+                    for (int f = 0; f < KF; ++f) lc[f] = Mb[jc * CW + lane + 64 * f];
+                    p = Pv[b * CH + jc];
+                    nx = X[b * CH + jc];
+                };
+                double lr[SD][KF], nr[SD];
+                int pr[SD];
 #pragma unroll
-                        for (int f = 1; f < KF; ++f)
-                            if (f == fp) src = xw[f];
-                        const double a = lane_read(xw[0], 0), bv = lane_read(src, lp);
-                        xw[0] = lane == 0 ? bv : xw[0];
+                for (int s = 0; s < SD; ++s) fetch(s, lr[s], pr[s], nr[s]);
+                for (int jj0 = 0; jj0 < cnt; jj0 += SD) {
 #pragma unroll
-                        for (int f = 0; f < KF; ++f)
-                            if (f == fp) xw[f] = lane == lp ? a : xw[f];
+                    for (int s = 0; s < SD; ++s) {
+                        const int jj = jj0 + s, j = jb + jj;
+                        if (jj < cnt) {
+                            double lc[KF];
+#pragma unroll
+                            for (int f = 0; f < KF; ++f) lc[f] = lr[s][f];
+                            const int p = __builtin_amdgcn_readfirstlane(pr[s]);
+                            const double nxv = nr[s];
+                            fetch(jj + SD, lr[s], pr[s], nr[s]);
+                            if (p != 0) {
+                                const int fp = p >> 6, lp = p & 63;
+                                double src = xw[0];
+#pragma unroll
+                                for (int f = 1; f < KF; ++f)
+                                    if (f == fp) src = xw[f];
+                                const double a = lane_read(xw[0], 0), bv = lane_read(src, lp);
+                                xw[0] = lane == 0 ? bv : xw[0];
+#pragma unroll
+                                for (int f = 0; f < KF; ++f)
+                                    if (f == fp) xw[f] = lane == lp ? a : xw[f];
+                            }
+                            const double xj = lane_read(xw[0], 0);
+#pragma unroll
+                            for (int f = 0; f < KF; ++f) xw[f] -= lc[f] * xj;
+                            *(lane == 0 ? x + j : dsink) = xj;
+                            slide<KF>(xw);
+#pragma unroll
+                            for (int f = 0; f < KF; ++f)
+                                if (f == fk && lane == lk) xw[f] = nxv;
+                        }
                     }
-                    const double xj = lane_read(xw[0], 0);
-#pragma unroll
-                    for (int f = 0; f < KF; ++f) xw[f] -= lc[f] * xj;
-                    *(lane == 0 ? x + j : dsink) = xj;
-                    slide<KF>(xw);
-#pragma unroll
-                    for (int f = 0; f < KF; ++f)
-                        if (f == fk && lane == lk) xw[f] = nxv;
                 }
             } else if (ci + 1 < nch) {
                 produce(ci + 1);
@@ -1541,7 +1578,7 @@ template <int KB, int NT>
 __global__ void __launch_bounds__(NT) k_band_bwd_stream(int n, int kl, int ku, int nrhs,
                                                         const double* __restrict__ AB, double* RHS) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
-    constexpr int CW = 64 * KB, CH = 128 / KB, NP = NT - 64;
+    constexpr int CW = 64 * KB, CH = 128 / KB, NP = NT - 64, SD = 4;
     const int t = threadIdx.x, lane = t & 63;
     const int ldab = 2 * kl + ku + 1, kv = kl + ku, fk = kv >> 6, lk = kv & 63;
     const double* const ab = AB + (int64_t)blockIdx.x * n * ldab;
@@ -1578,23 +1615,38 @@ __global__ void __launch_bounds__(NT) k_band_bwd_stream(int n, int kl, int ku, i
             if (t < 64) {
                 const int b = ci & 1, jb = n - 1 - ci * CH, cnt = min(CH, jb + 1);
                 const double* Ub = U + b * CH * CW;
-                for (int jj = 0; jj < cnt; ++jj) {
-                    const int j = jb - jj;
-                    double uc[KB];
+                auto fetch = [&](int jj, double (&uc)[KB], double& nx) CFX_INLINE {
+                    const int jc = min(jj, CH - 1);
 #pragma unroll
-                    for (int k = 0; k < KB; ++k) uc[k] = Ub[jj * CW + lane + 64 * k];
-                    const double nxv = X[b * CH + jj];
-                    const double xj = lane_read(xw[0], 0) / lane_read(uc[0], 0);
-                    *(lane == 0 ? x + j : dsink) = xj;
+                    for (int k = 0; k < KB; ++k) uc[k] = Ub[jc * CW + lane + 64 * k];
+                    nx = X[b * CH + jc];
+                };
+                double ur[SD][KB], nr[SD];
 #pragma unroll
-                    for (int k = 0; k < KB; ++k) {  // one fused multiply-subtract per element, as the column kernels
-                        const double u = (k == 0 && lane == 0) ? 0.0 : uc[k];
-                        xw[k] -= u * xj;
+                for (int s = 0; s < SD; ++s) fetch(s, ur[s], nr[s]);
+                for (int jj0 = 0; jj0 < cnt; jj0 += SD) {
+#pragma unroll
+                    for (int s = 0; s < SD; ++s) {
+                        const int jj = jj0 + s, j = jb - jj;
+                        if (jj < cnt) {
+                            double uc[KB];
+#pragma unroll
+                            for (int k = 0; k < KB; ++k) uc[k] = ur[s][k];
+                            const double nxv = nr[s];
+                            fetch(jj + SD, ur[s], nr[s]);
+                            const double xj = lane_read(xw[0], 0) / lane_read(uc[0], 0);
+                            *(lane == 0 ? x + j : dsink) = xj;
+#pragma unroll
+                            for (int k = 0; k < KB; ++k) {  // one fused multiply-subtract per element, as the column kernels
+                                const double u = (k == 0 && lane == 0) ? 0.0 : uc[k];
+                                xw[k] -= u * xj;
+                            }
+                            slide<KB>(xw);
+#pragma unroll
+                            for (int k = 0; k < KB; ++k)
+                                if (k == fk && lane == lk) xw[k] = nxv;
+                        }
                     }
-                    slide<KB>(xw);
-#pragma unroll
-                    for (int k = 0; k < KB; ++k)
-                        if (k == fk && lane == lk) xw[k] = nxv;
                 }
             } else if (ci + 1 < nch) {
                 produce(ci + 1);

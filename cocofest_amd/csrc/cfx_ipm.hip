@@ -52,7 +52,7 @@ struct Scal {
     int32_t wd_short, wd_on, wd_trial, skip_first, forced;
     int32_t rejf, nsucc, nreset;  // filter reset heuristic: last rejection by the filter, successive such iterations,
                                   // resets done
-    int32_t pad;
+    int32_t acc_ok;  // the iterate meets Ipopt's acceptable-level tests (k_ipm_begin)
     // limited-memory Hessian (L-BFGS): sigma, pairs held, next ring slot, previous iterate saved
     double lsig;
     int32_t lcount, lhead, lprev, lpad;
@@ -426,7 +426,8 @@ __global__ void __launch_bounds__(kIB) k_ipm_begin(const IpmK K, int mode, int s
     const double* lbI = K.lbI + b * nf;
     const double* ubI = K.ubI + b * nf;
     double* rhs = K.rhs + b * K.nK;
-    double szl = 0, szu = 0, sy = 0, ed = 0, ep = 0, ecl = 0, ecu = 0;
+    double szl = 0, szu = 0, sy = 0, ed = 0, ep = 0, ecl = 0, ecu = 0, edu = 0, epu = 0;
+    const double* sg = K.sg + b * m;
     for (int i = threadIdx.x; i < nf; i += kIB) {
         double jty = 0.0;
         for (int k = K.jt_ptr[i]; k < K.jt_ptr[i + 1]; ++k) {
@@ -441,16 +442,18 @@ __global__ void __launch_bounds__(kIB) k_ipm_begin(const IpmK K, int mode, int s
         const double cl = K.hasL[i] ? (x[i] - lbI[i]) * zl[i] : 0.0;
         const double cu = K.hasU[i] ? (ubI[i] - x[i]) * zu[i] : 0.0;
         ed = max_n(ed, fabs(rd));
+        edu = max_n(edu, fabs(rd) / K.d[i]);
         ecl = max_n(ecl, fabs(cl));
         ecu = max_n(ecu, fabs(cu));
     }
     for (int j = threadIdx.x; j < m; j += kIB) {
         sy += fabs(y[j]);
         ep = max_n(ep, fabs(gS[j]));
+        epu = max_n(epu, fabs(gS[j]) / sg[j]);
     }
     {
-        double rv[7] = {szl, szu, sy, ed, ep, ecl, ecu};
-        const int ro[7] = {0, 0, 0, 1, 1, 1, 1};
+        double rv[9] = {szl, szu, sy, ed, ep, ecl, ecu, edu, epu};
+        const int ro[9] = {0, 0, 0, 1, 1, 1, 1, 1, 1};
         breduce_n(rv, ro);
         szl = rv[0];
         szu = rv[1];
@@ -459,6 +462,8 @@ __global__ void __launch_bounds__(kIB) k_ipm_begin(const IpmK K, int mode, int s
         ep = rv[4];
         ecl = rv[5];
         ecu = rv[6];
+        edu = rv[7];
+        epu = rv[8];
     }
     const double smax = K.o.s_max;
     const double sd = clamp_lo((szl + szu + sy) / (2.0 * nf + m), smax) / smax;
@@ -466,9 +471,16 @@ __global__ void __launch_bounds__(kIB) k_ipm_begin(const IpmK K, int mode, int s
     const double e_d = ed / sd, e_p = m ? ep : 0.0, e_c0 = max_n(ecl, ecu) / sc;
     if (threadIdx.x == 0) {
         S.err0 = max_n(max_n(e_d, e_p), e_c0);
-        S.acc = S.err0 <= K.o.acceptable_tol ? S.acc + 1 : 0;
-        const bool newly = !S.done && (S.err0 <= K.o.tol || S.acc >= K.o.acceptable_iter);
-        if (newly) S.status = S.err0 <= K.o.tol ? CFX_IPM_SOLVE_SUCCEEDED : CFX_IPM_SOLVED_TO_ACCEPTABLE_LEVEL;
+        // Ipopt's unscaled tests (IpOptErrorConv): constraint violation, dual infeasibility (x = d x_s, the multipliers
+        // of the scaled problem over sf), complementarity with mu = 0
+        const double e_pu = m ? epu : 0.0, e_du = edu / S.sf, e_cu = max_n(ecl, ecu) / S.sf;
+        const bool conv = S.err0 <= K.o.tol && e_pu <= K.o.constr_viol_tol && e_du <= K.o.dual_inf_tol &&
+                          e_cu <= K.o.compl_inf_tol;
+        S.acc_ok = S.err0 <= K.o.acceptable_tol && e_pu <= K.o.acceptable_constr_viol_tol &&
+                   e_du <= K.o.acceptable_dual_inf_tol && e_cu <= K.o.acceptable_compl_inf_tol;
+        S.acc = S.acc_ok ? S.acc + 1 : 0;
+        const bool newly = !S.done && (conv || S.acc >= K.o.acceptable_iter);
+        if (newly) S.status = conv ? CFX_IPM_SOLVE_SUCCEEDED : CFX_IPM_SOLVED_TO_ACCEPTABLE_LEVEL;
         S.done = S.done || newly;
         if (!S.done && S.iters >= K.o.max_iter) {  // per-instance budget
             S.done = S.stop = 1;
@@ -1555,7 +1567,7 @@ __global__ void __launch_bounds__(kIB) k_rs_init(const IpmK K) {
     const bool failed = !S.rs_on && !S.accepted && !S.done;
     // Ipopt (BacktrackingLineSearch): "Restoration phase called at acceptable point" — the solve ends there, solved to
     // the acceptable level (err0 is the current point's scaled KKT error)
-    const bool acceptable = failed && S.err0 <= K.o.acceptable_tol;
+    const bool acceptable = failed && S.acc_ok;
     const bool go = failed && !acceptable && S.iters < K.o.max_iter;
     if (acceptable && threadIdx.x == 0) {
         S.done = 1;
@@ -2417,6 +2429,12 @@ extern "C" void cfx_ipm_default_options(cfx_ipm_options* o) {
     o->soft_resto_pderror_reduction_factor = 0.0;  // Ipopt: 0.9999
     o->max_soft_resto_iters = 10;
     o->resto_failure_restart = 0;
+    o->constr_viol_tol = 1e-4;
+    o->dual_inf_tol = 1.0;
+    o->compl_inf_tol = 1e-4;
+    o->acceptable_constr_viol_tol = 0.01;
+    o->acceptable_dual_inf_tol = 1e10;
+    o->acceptable_compl_inf_tol = 0.01;
 }
 
 // CSR of `key` (values in [0, nkeys)) with the sources of each key in increasing source order
@@ -2519,7 +2537,10 @@ static int ipm_create_common(cfx_ipm* s, const cfx_sizes& sz, int layout, const 
         K.o.max_resto_iter < 0 || !(K.o.resto_penalty > 0) || !(K.o.required_infeasibility_reduction > 0) ||
         !(K.o.required_infeasibility_reduction < 1) || K.o.filter_reset_trigger < 1 || K.o.max_filter_resets < 0 ||
         !(K.o.max_wall_time > 0) || !(K.o.print_frequency_time >= 0) ||
-        !(K.o.soft_resto_pderror_reduction_factor >= 0) || K.o.max_soft_resto_iters < 0 || s->B > 0x7fffffff) {
+        !(K.o.soft_resto_pderror_reduction_factor >= 0) || K.o.max_soft_resto_iters < 0 || s->B > 0x7fffffff ||
+        !(K.o.constr_viol_tol > 0) || !(K.o.dual_inf_tol > 0) || !(K.o.compl_inf_tol > 0) ||
+        !(K.o.acceptable_constr_viol_tol > 0) || !(K.o.acceptable_dual_inf_tol > 0) ||
+        !(K.o.acceptable_compl_inf_tol > 0)) {
         s->err = "cfx_ipm_create: the handle must use CFX_LAYOUT_AOS (or batch 1) and the options must be valid";
         return create_fail(s, CFX_EINVAL);
     }

@@ -85,6 +85,16 @@ class IpmOptions:
     # off): the native solver prints a progress line (iteration, instances iterating, in restoration) this often
     max_wall_time: float = 1e20
     print_frequency_time: float = 0.0
+    # Ipopt's termination tests on the unscaled problem (IpOptErrorConv), beside tol on the scaled error: converged
+    # needs max|g| <= constr_viol_tol, max|grad L| <= dual_inf_tol and max|s z| <= compl_inf_tol; the acceptable level
+    # (acceptable_tol held acceptable_iter iterations, or a restoration phase called at an acceptable point) the
+    # acceptable_* ones.  Ipopt's defaults
+    constr_viol_tol: float = 1e-4
+    dual_inf_tol: float = 1.0
+    compl_inf_tol: float = 1e-4
+    acceptable_constr_viol_tol: float = 1e-2
+    acceptable_dual_inf_tol: float = 1e10
+    acceptable_compl_inf_tol: float = 1e-2
     verbose: bool = False
 
     def __post_init__(self):
@@ -94,6 +104,10 @@ class IpmOptions:
             raise ValueError("max_wall_time must be > 0 and print_frequency_time >= 0")
         if not self.soft_resto_pderror_reduction_factor >= 0 or self.max_soft_resto_iters < 0:
             raise ValueError("soft_resto_pderror_reduction_factor must be >= 0 and max_soft_resto_iters >= 0")
+        for k in ("constr_viol_tol", "dual_inf_tol", "compl_inf_tol", "acceptable_constr_viol_tol",
+                  "acceptable_dual_inf_tol", "acceptable_compl_inf_tol"):
+            if not getattr(self, k) > 0:
+                raise ValueError(f"{k} must be > 0")
 
 
 class Solver:
@@ -115,10 +129,13 @@ class Solver:
                     "_filter_reset_trigger": "filter_reset_trigger", "_max_filter_resets": "max_filter_resets",
                     "_max_wall_time": "max_wall_time", "_print_frequency_time": "print_frequency_time",
                     "_soft_resto_pderror_reduction_factor": "soft_resto_pderror_reduction_factor",
-                    "_max_soft_resto_iters": "max_soft_resto_iters"}
+                    "_max_soft_resto_iters": "max_soft_resto_iters", "_constr_viol_tol": "constr_viol_tol",
+                    "_dual_inf_tol": "dual_inf_tol", "_compl_inf_tol": "compl_inf_tol",
+                    "_acceptable_constr_viol_tol": "acceptable_constr_viol_tol",
+                    "_acceptable_dual_inf_tol": "acceptable_dual_inf_tol",
+                    "_acceptable_compl_inf_tol": "acceptable_compl_inf_tol"}
         _IGNORED = {"show_online_optim", "show_options", "_print_level", "_linear_solver", "_nlp_scaling_method",
-                    "_check_derivatives_for_naninf", "_c_compile", "_print_timing_statistics", "_output_file",
-                    "_constr_viol_tol", "_dual_inf_tol", "_compl_inf_tol"}
+                    "_check_derivatives_for_naninf", "_c_compile", "_print_timing_statistics", "_output_file"}
 
         def __init__(self, show_online_optim: bool = False, show_options: dict | None = None, **kwargs):
             self._tol = 1e-6
@@ -518,9 +535,17 @@ class BatchedIpm:
             e_p = g.abs().amax(1) if m else torch.zeros_like(mu)
             e_c0 = torch.maximum(compl_l.abs().amax(1), compl_u.abs().amax(1)) / sc
             err0 = torch.maximum(torch.maximum(e_d, e_p), e_c0)
-            acc_count = torch.where(err0 <= opt.acceptable_tol, acc_count + 1, torch.zeros_like(acc_count))
-            newly = (~done) & ((err0 <= opt.tol) | (acc_count >= opt.acceptable_iter))
-            status = torch.where(newly, torch.where(err0 <= opt.tol, 0, 1).to(status.dtype), status)
+            # Ipopt's unscaled tests: x = d x_s, g = g_s / sg, the multipliers of the scaled problem over sf
+            e_pu = (g / self.sg).abs().amax(1) if m else torch.zeros_like(mu)
+            e_du = (rd / self.d).abs().amax(1) / self.sf
+            e_cu = torch.maximum(compl_l.abs().amax(1), compl_u.abs().amax(1)) / self.sf
+            conv = (err0 <= opt.tol) & (e_pu <= opt.constr_viol_tol) & (e_du <= opt.dual_inf_tol) & \
+                (e_cu <= opt.compl_inf_tol)
+            acc_ok = (err0 <= opt.acceptable_tol) & (e_pu <= opt.acceptable_constr_viol_tol) & \
+                (e_du <= opt.acceptable_dual_inf_tol) & (e_cu <= opt.acceptable_compl_inf_tol)
+            acc_count = torch.where(acc_ok, acc_count + 1, torch.zeros_like(acc_count))
+            newly = (~done) & (conv | (acc_count >= opt.acceptable_iter))
+            status = torch.where(newly, torch.where(conv, 0, 1).to(status.dtype), status)
             done = done | newly
             # an instance whose iterations (restoration-phase ones included) reach max_iter stops, unconverged
             out_of_iters = (~done) & (iters >= opt.max_iter)
@@ -703,7 +728,7 @@ class BatchedIpm:
                 soft_cnt = torch.where(soft_on, soft_cnt, torch.zeros_like(soft_cnt))
             if self._phase:
                 # Ipopt: "Restoration phase called at acceptable point" ends the solve, solved to the acceptable level
-                at_acc = failed & (err0 <= opt.acceptable_tol)
+                at_acc = failed & acc_ok
                 status = torch.where(at_acc, torch.ones_like(status), status)
                 done = done | at_acc
                 failed = failed & ~at_acc
@@ -1180,7 +1205,8 @@ _NATIVE_OPTIONS = ("tol", "max_iter", "acceptable_tol", "acceptable_iter", "mu_i
                    "watchdog_trial_iter_max", "limited_memory_max_history", "max_resto_iter", "resto_penalty",
                    "required_infeasibility_reduction", "filter_reset_trigger", "max_filter_resets", "max_wall_time",
                    "print_frequency_time", "soft_resto_pderror_reduction_factor", "max_soft_resto_iters",
-                   "resto_failure_restart")
+                   "resto_failure_restart", "constr_viol_tol", "dual_inf_tol", "compl_inf_tol",
+                   "acceptable_constr_viol_tol", "acceptable_dual_inf_tol", "acceptable_compl_inf_tol")
 _HESSIAN_APPROXIMATION = {"exact": 0, "limited-memory": 1}
 _RESTORATION = {"step": 0, "phase": 1, None: 1}
 

@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define CFX_ABI_VERSION 7
+#define CFX_ABI_VERSION 8
 
 /* return codes */
 #define CFX_OK 0
@@ -398,6 +398,12 @@ typedef struct cfx_ipm_options {
        max_resto_iter) restarts the main iteration from the phase's last point — zero constraint multipliers, an
        empty filter — instead of stopping the instance with CFX_IPM_RESTORATION_FAILED */
     int32_t resto_failure_restart;
+    /* Ipopt's termination tests on the UNSCALED problem, beside tol on the scaled error (ABI 8): converged needs
+       max|g| <= constr_viol_tol (1e-4), max|grad L| <= dual_inf_tol (1), max|s z| <= compl_inf_tol (1e-4); the
+       acceptable level (acceptable_tol for acceptable_iter iterations, and a restoration phase called at an acceptable
+       point) needs the acceptable_* ones (0.01, 1e10, 0.01) */
+    double constr_viol_tol, dual_inf_tol, compl_inf_tol;
+    double acceptable_constr_viol_tol, acceptable_dual_inf_tol, acceptable_compl_inf_tol;
 } cfx_ipm_options;
 #define CFX_HESSIAN_EXACT 0
 #define CFX_HESSIAN_LIMITED_MEMORY 1

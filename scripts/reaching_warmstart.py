@@ -88,6 +88,7 @@ def run(objective):
                                                       bound_relax_factor=args.bound_relax))
     res = ipm.solve(v0[None])
     st = dict(ipm.last_stats)
+    g_solver = ipm.h.eval_g(res.v)[0]  # the solver's own handle, at the returned point
     ipm.close()
     wall = time.perf_counter() - t0
     v = res.v[0]
@@ -107,6 +108,8 @@ def run(objective):
            "iterations": int(res.iterations[0]), "wall_s": wall, "kkt_error": float(res.kkt_error[0]),
            "f_start": f0, "f_end": float(res.f[0]), "g_start_max": float(np.abs(g0).max()),
            "g_end_max_continuity": float(np.abs(g1[:nrow]).max()), "g_end_max_other": float(np.abs(g1[nrow:]).max()),
+           "g_end_max_solver_handle": float(np.abs(g_solver).max()),
+           "g_end_argmax_row": int(np.abs(g1).argmax()), "ng": int(g1.size),
            "g_start_rows_over_1e-6": int((np.abs(g0) > 1e-6).sum()),
            "dstate_rel_max": float(dstate.max()), "dstate_rel_median": float(np.median(dstate)),
            "dpw_rel_max": float(np.abs(pw - pw0).max() / (pwhi - pwlo)),
@@ -117,6 +120,8 @@ def run(objective):
            "resto_phases": int(st.get("resto_phases", 0)), "kkt_n": st.get("kkt_n"), "kkt_kl": st.get("kkt_kl"),
            "kkt_blocks": st.get("kkt_blocks"), "mu_init": args.mu_init, "bound_push": args.bound_push,
            "bound_relax_factor": args.bound_relax, "s_per_iteration": wall / max(1, int(res.iterations[0]))}
+    if args.out:  # the end point, for a later look
+        np.savez(os.path.splitext(args.out)[0] + f"_{objective}.npz", v=res.v[0], g=g1)
     line = json.dumps(out)
     print(line, flush=True)
     if args.out:
@@ -124,5 +129,5 @@ def run(objective):
             fh.write(line + "\n")
 
 
-for obj in args.objectives.split(","):
+for obj in args.objectives.replace("+", ",").split(","):
     run(obj)

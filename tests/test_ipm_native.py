@@ -292,3 +292,27 @@ def test_native_ipm_soft_restoration_matches_the_specification():
     print("soft steps", soft_ref, st["soft_steps"], "iterations", r_ref.iterations, r_nat.iterations)
     assert soft_ref > 0 and st["soft_steps"] == soft_ref, (soft_ref, st)
     _compare(ocp, r_ref, r_nat, it_slack=0)
+
+
+def test_native_ipm_unscaled_termination_tests():
+    """Ipopt's unscaled termination tests in the native solver, as in the specification (test_solver_cpu.py::
+    test_unscaled_termination_tests): a complementarity tolerance no interior point reaches keeps cfg 2 iterating
+    past its scaled convergence until max_iter, at the same point; Ipopt's defaults converge as before."""
+    from cocofest_amd.solver import IpmOptions, NativeIpm
+
+    ocp = cases.product_ocp(**cases.cfg2())
+    v0 = _starts(ocp, 1, 0)
+    nat = NativeIpm(ocp, batch=1, options=IpmOptions(tol=1e-6))
+    base = nat.solve(v0)
+    nat.close()
+    assert base.converged[0] and base.status[0] == 0
+    it0 = int(base.iterations[0])
+    nat = NativeIpm(ocp, batch=1, options=IpmOptions(tol=1e-6, compl_inf_tol=1e-300, acceptable_compl_inf_tol=1e-300,
+                                                     max_iter=it0 + 5))
+    res = nat.solve(v0)
+    nat.close()
+    assert not res.converged[0] and res.status[0] == -1 and int(res.iterations[0]) == it0 + 5, (res.status,
+                                                                                                  res.iterations)
+    lb, ub = ocp.bounds_vector()
+    span = np.where(np.isfinite(ub - lb), ub - lb, np.maximum(np.abs(base.v).max(0), 1.0))
+    assert np.max(np.abs(res.v - base.v) / np.maximum(span, 1e-12)) < 1e-6

@@ -281,3 +281,29 @@ def test_failed_restoration_stops_or_restarts(restart):
     traj = O.ivp_integrate("ding2003", c, pb.rows, np.zeros((pb.n_shooting, 0)), 1.0, "RK1", 10)
     X, _, _ = pb.unpack(res.v)
     np.testing.assert_allclose(X[0].T, traj[:, ::10], rtol=1e-6, atol=1e-6)
+
+
+def test_unscaled_termination_tests():
+    """Ipopt's termination also checks the UNSCALED problem (IpOptErrorConv: constr_viol_tol, dual_inf_tol,
+    compl_inf_tol beside tol on the scaled error).  A complementarity tolerance below anything an interior point
+    reaches (its s z stay positive) keeps the solver iterating past its scaled convergence, here until max_iter, at
+    the same point; Solver.IPOPT maps the options and IpmOptions validates them."""
+    from cocofest_amd.solver import IpmOptions, Solver, apply_solver
+
+    cfg = cases.cfg2(n_shooting=None)
+    ocp, pb, ipm = _ipm(cfg, batch=1, tol=1e-6)
+    base = ipm.solve()
+    assert base.converged.all() and base.status[0] == 0
+    it0 = int(base.iterations[0])
+    ocp, pb, tight = _ipm(cfg, batch=1, tol=1e-6, compl_inf_tol=1e-300, acceptable_compl_inf_tol=1e-300,
+                          max_iter=it0 + 5)
+    res = tight.solve()
+    assert not res.converged[0] and res.status[0] == -1 and int(res.iterations[0]) == it0 + 5, (res.status,
+                                                                                                  res.iterations)
+    np.testing.assert_allclose(res.v, base.v, rtol=1e-6, atol=1e-6)  # it stays at the optimum meanwhile
+    for k in ("constr_viol_tol", "dual_inf_tol", "compl_inf_tol", "acceptable_constr_viol_tol",
+              "acceptable_dual_inf_tol", "acceptable_compl_inf_tol"):
+        with pytest.raises(ValueError):
+            IpmOptions(**{k: 0.0})
+    o = apply_solver(IpmOptions(), Solver.IPOPT(_constr_viol_tol=1e-6, _dual_inf_tol=0.5, _compl_inf_tol=1e-5))
+    assert (o.constr_viol_tol, o.dual_inf_tol, o.compl_inf_tol) == (1e-6, 0.5, 1e-5)
