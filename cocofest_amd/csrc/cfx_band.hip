@@ -1201,10 +1201,11 @@ __global__ void __launch_bounds__(256) k_band_transpose(const T* __restrict__ sr
 // global placement's (tested bit for bit).  Fill rows (storage rows < kl) are zeroed lazily, as columns
 // enter the trailing reach.  RH: 64-row chunks per lane (NB + kl <= 64 RH).
 #ifdef CFX_BAND_PROF
-__device__ unsigned long long g_panel_prof[8];  // phase clocks of instance 0, thread 0 (micro build only)
+// phase clocks of instance 0 (micro build only): [0, 8) thread 0 (wavefront 0), [8, 16) thread 64 (wavefront 1)
+__device__ unsigned long long g_panel_prof[16];
 #define PANEL_STAMP(i)                                                  \
     do {                                                                \
-        if (blockIdx.x == 0 && t == 0) {                                \
+        if (blockIdx.x == 0 && (t == 0 || t == 64)) {                   \
             const unsigned long long now_ = wall_clock64();             \
             prof[i] += now_ - last_;                                    \
             last_ = now_;                                               \
@@ -1242,7 +1243,11 @@ template <int NB, int RH, int NT>
 __global__ void __launch_bounds__(NT) k_band_lu_panel(int n, int kl, int ku, double* __restrict__ AB,
                                                       int32_t* __restrict__ IPIV, int32_t* __restrict__ INFO) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
+#ifdef CFX_PANEL_CG  // (micro builds: columns per load group)
+    constexpr int NW = NT / 64, US = NB + 1, CG = CFX_PANEL_CG;
+#else
     constexpr int NW = NT / 64, US = NB + 1, CG = RH >= 3 ? 2 : 4;  // US: row stride of Lt (conflict-free); CG: columns per load group
+#endif
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
     const int ldab = 2 * kl + ku + 1, kv = kl + ku, PR = NB + kl;
     double* const ab = AB + (int64_t)blockIdx.x * n * ldab;
@@ -1361,18 +1366,28 @@ __global__ void __launch_bounds__(NT) k_band_lu_panel(int n, int kl, int ku, dou
         for (int cb = cb0; cb < ce; cb += stride * CG) {
 #pragma unroll
             for (int g = 0; g < CG; ++g) load(cb + (g + CG) * stride, nxt[g]);
+            // the CG columns' chains interleaved step by step (row k of each: final U12 once steps 0 .. k - 1 are in);
+            // full panels without the k < w test, so that the whole update is one block for the scheduler
+            auto step = [&](int k) CFX_INLINE {
+#pragma unroll
+                for (int g = 0; g < CG; ++g) {
+                    const double xk = lane_read(cur[g][0], k);
+#pragma unroll
+                    for (int h = 0; h < RH; ++h) cur[g][h] -= lr[h][k] * xk;
+                }
+            };
+            if (w == NB) {
+#pragma unroll
+                for (int k = 0; k < NB; ++k) step(k);
+            } else {
+#pragma unroll
+                for (int k = 0; k < NB; ++k)
+                    if (k < w) step(k);  // (uniform; no break: the loop stays fully unrolled, lr in registers)
+            }
 #pragma unroll
             for (int g = 0; g < CG; ++g) {
                 const int cc = cb + g * stride, c = c0 + cc;
                 double (&x)[RH] = cur[g];
-#pragma unroll
-                for (int k = 0; k < NB; ++k) {
-                    if (k < w) {  // (uniform; no break: the loop stays fully unrolled, lr in registers)
-                        const double xk = lane_read(x[0], k);  // row k: final (U12) once steps 0 .. k - 1 are in
-#pragma unroll
-                        for (int h = 0; h < RH; ++h) x[h] -= lr[h][k] * xk;
-                    }
-                }
                 if (cc < ce) {
 #pragma unroll
                     for (int h = 0; h < RH; ++h) {
@@ -1444,12 +1459,15 @@ __global__ void __launch_bounds__(NT) k_band_lu_panel(int n, int kl, int ku, dou
         if (wave == 0) {
             if (wn > 0) {
                 if (wt > 0) trail(j0, w, pr, c0, 0, min(wn, wt), 1);
+                PANEL_STAMP(4);
                 zero_fill(zhi, zend, lane, 64);
                 __threadfence_block();  // this wave's stores before its loads of the next panel
                 factor_panel(jn, wn, min(wn + kl, n - jn));
+                PANEL_STAMP(5);
             }
         } else if (wt > wn) {
             trail(j0, w, pr, c0, wn + wave - 1, wt, NW - 1);
+            PANEL_STAMP(4);
         }
         zhi = max(zhi, zend);
         __syncthreads();
@@ -1458,6 +1476,8 @@ __global__ void __launch_bounds__(NT) k_band_lu_panel(int n, int kl, int ku, dou
 #ifdef CFX_BAND_PROF
     if (blockIdx.x == 0 && t == 0)
         for (int i = 0; i < 8; ++i) g_panel_prof[i] = prof[i];
+    if (blockIdx.x == 0 && t == 64)
+        for (int i = 0; i < 8; ++i) g_panel_prof[8 + i] = prof[i];
 #endif
     if (t == 0) INFO[blockIdx.x] = info;
 }

@@ -1,7 +1,7 @@
 // Phase clocks of the panel band LU (k_band_lu_panel, cocofest_amd/csrc/cfx_band.hip built with CFX_BAND_PROF):
 // one factorisation of a random single band (n, kl, ku), thread 0's wall clock (s_memrealtime, 100 MHz) summed
-// per phase over the panels: fill zeroing, panel load, panel steps, write-back + blocked multipliers, trailing
-// loads, U12, A22 update.  Prints one JSON line with the per-panel microseconds of each phase.
+// per phase over the panels (look-ahead kernel: write-back, own trailing columns, the next panel's factorisation,
+// barrier wait), for wavefront 0 and wavefront 1.  Prints one JSON line with the per-panel microseconds of each phase.
 //   hipcc -O3 -std=c++17 --offload-arch=gfx950 scripts/micro/band_panel_prof.hip -o scripts/micro/bin/band_panel_prof
 //   scripts/micro/bin/band_panel_prof [n kl ku reps]
 #define CFX_BAND_PROF 1
@@ -52,18 +52,21 @@ int main(int argc, char** argv) {
         CK(hipEventSynchronize(b));
         float ms = 0;
         CK(hipEventElapsedTime(&ms, a, b));
-        unsigned long long p[8];
+        unsigned long long p[16];
         CK(hipMemcpyFromSymbol(p, HIP_SYMBOL(cfx::g_panel_prof), sizeof(p)));
         const int nb = cfx::kPanelNB, panels = (n + nb - 1) / nb;
-        const char* names[7] = {"zero_fill", "panel_load", "panel_steps", "writeback_lt", "trail_load", "u12",
-                                "a22"};
+        // per panel: [2] reach / first zero pivot, [3] write-back + blocked multipliers + LDS barrier, [4] own trailing
+        // columns, [5] (wavefront 0) fill rows + next panel re-read + its factorisation, [6] wait at the closing barrier
+        const char* names[5] = {"reach", "writeback_lt", "trail", "lookahead_factor", "barrier_wait"};
+        const int ids[5] = {2, 3, 4, 5, 6};
         std::printf("{\"n\": %d, \"kl\": %d, \"ku\": %d, \"nb\": %d, \"ms\": %.3f, \"us_per_panel\": %.3f", n, kl, ku,
                     nb, ms, 1e3 * ms / panels);
         double tot = 0;
-        for (int i = 0; i < 7; ++i) {
-            std::printf(", \"%s\": %.3f", names[i], p[i] * 0.01 / panels);  // 100 MHz ticks -> us per panel
-            tot += p[i] * 0.01 / panels;
-        }
+        for (int w = 0; w < 2; ++w)
+            for (int i = 0; i < 5; ++i) {
+                std::printf(", \"w%d_%s\": %.3f", w, names[i], p[8 * w + ids[i]] * 0.01 / panels);  // 100 MHz ticks
+                if (w == 0) tot += p[ids[i]] * 0.01 / panels;
+            }
         std::printf(", \"sum_us\": %.3f}\n", tot);
     }
     return 0;
