@@ -1293,39 +1293,47 @@ __global__ void __launch_bounds__(NT) k_band_lu_panel(int n, int kl, int ku, dou
                 }
                 const double amax = wave_max(av);
                 const int pj = wave_min_i(av == amax ? ai : 0x7fffffff), ph = pj >> 6, pl = pj & 63;
-                double u[NB], rj[NB];  // the pivot row and row jj, columns jj .. NB - 1
+                double u[NB];  // the pivot row, columns jj .. NB - 1 (uniform: readlane)
 #pragma unroll
-                for (int c = 0; c < NB; ++c) {  // (full-range loops: unrolled before jj is, registers throughout)
-                    if (c >= jj) {
-                        double src = pa[0][c];
+                for (int h = 0; h < RH; ++h)
+                    if (ph == h) {  // (uniform branch: one register's readlanes)
 #pragma unroll
-                        for (int h = 1; h < RH; ++h)
-                            if (ph == h) src = pa[h][c];
-                        u[c] = lane_read(src, pl);
-                        rj[c] = lane_read(pa[0][c], jj);
+                        for (int c = 0; c < NB; ++c)  // (full-range loops: unrolled before jj is, registers throughout)
+                            if (c >= jj) u[c] = lane_read(pa[h][c], pl);
                     }
-                }
                 const double pv = u[jj];
                 const bool nz = pv != 0.0;
                 const double inv = nz ? 1.0 / pv : 0.0;
+                // the ordinary rows jj < r <= rmax (not pj): l = A(r, jj) / pv, A(r, c) -= l u(c); the others keep
+                // their values (l = 0: an exact no-op for finite pivot rows)
 #pragma unroll
                 for (int h = 0; h < RH; ++h) {
                     const int r = lane + 64 * h;
-                    const bool isp = r == pj && r != jj;  // row pj takes row jj's elements
-                    const bool elim = nz && r > jj && r <= rmax;
-                    const double l = elim ? (isp ? rj[jj] : pa[h][jj]) * inv : 0.0;
+                    const bool elim = nz && r > jj && r <= rmax && r != pj;
+                    const double l = elim ? pa[h][jj] * inv : 0.0;
 #pragma unroll
-                    for (int c = 0; c < NB; ++c) {
-                        if (c >= jj) {
-                            const double srcv = isp ? rj[c] : pa[h][c];
-                            double nv = pa[h][c];
-                            if (nz && r == jj)
-                                nv = u[c];
-                            else if (elim)
-                                nv = c == jj ? l : srcv - l * u[c];
-                            pa[h][c] = nv;
+                    for (int c = 0; c < NB; ++c)
+                        if (c > jj) pa[h][c] -= l * u[c];
+                    pa[h][jj] = elim ? l : pa[h][jj];
+                }
+                if (nz && pj != jj) {  // row pj takes row jj's elements, eliminated (uniform values, one lane)
+                    double rj[NB];
+#pragma unroll
+                    for (int c = 0; c < NB; ++c)
+                        if (c >= jj) rj[c] = lane_read(pa[0][c], jj);
+                    const double lp = rj[jj] * inv;
+#pragma unroll
+                    for (int h = 0; h < RH; ++h)
+                        if (ph == h) {
+#pragma unroll
+                            for (int c = 0; c < NB; ++c)
+                                if (c >= jj) pa[h][c] = lane == pl ? (c == jj ? lp : rj[c] - lp * u[c]) : pa[h][c];
                         }
-                    }
+                }
+                if (nz) {  // row jj takes the pivot row
+#pragma unroll
+                    for (int c = 0; c < NB; ++c)
+                        if (c >= jj) pa[0][c] = lane == jj ? u[c] : pa[0][c];
                 }
                 if (lane == 0) {
                     sp[jj] = pj;
