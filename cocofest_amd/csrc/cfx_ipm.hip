@@ -410,6 +410,8 @@ __global__ void __launch_bounds__(kIB) k_ipm_begin(const IpmK K, int mode, int s
         const double* sg = K.sg + b * m;
         const double* jac = K.jac + b * K.nnzj;
         for (int j = threadIdx.x; j < m; j += kIB) gS[j] = K.graw[b * m + j] * sg[j];
+        // (unrolled: several gathers in flight per thread — one instance of ~10^6 J_g entries is one block's loop)
+#pragma unroll 8
         for (int s = threadIdx.x; s < K.nj; s += kIB) jv[s] = jac[K.jsel[s]] * K.d[K.jc[s]] * sg[K.jr[s]];
         for (int i = threadIdx.x; i < nf; i += kIB) gF[i] = K.grad[b * K.n + K.free[i]] * K.d[i] * S.sf;
         if (threadIdx.x == 0) S.fS = K.fraw[b] * S.sf;
@@ -430,6 +432,7 @@ __global__ void __launch_bounds__(kIB) k_ipm_begin(const IpmK K, int mode, int s
     const double* sg = K.sg + b * m;
     for (int i = threadIdx.x; i < nf; i += kIB) {
         double jty = 0.0;
+#pragma unroll 4
         for (int k = K.jt_ptr[i]; k < K.jt_ptr[i + 1]; ++k) {
             const int s = K.jt_idx[k];
             jty += jv[s] * y[K.jr[s]];
@@ -780,7 +783,8 @@ __global__ void __launch_bounds__(kIB) k_ipm_curv(const IpmK K, int slot) {
     __syncthreads();
     const double* hv = K.hv + b * K.nnzh;
     double quad = 0.0;
-    for (int s = threadIdx.x; s < K.nh; s += kIB) {
+#pragma unroll 8
+    for (int s = threadIdx.x; s < K.nh; s += kIB) {  // (sums in the same order; gathers in flight)
         const int r = K.hr[s], c = K.hc[s];
         const double w = hv[K.hsel[s]] * K.d[r] * K.d[c];
         quad += w * dx[r] * dx[c] * (K.hoff[s] ? 2.0 : 1.0);
@@ -1184,6 +1188,7 @@ __device__ double pd_error(const IpmK& K, int64_t b, const double* x, const doub
     double sd = 0.0, sp = 0.0, scl = 0.0, scu = 0.0;
     for (int i = threadIdx.x; i < nf; i += kIB) {
         double jty = 0.0;
+#pragma unroll 4
         for (int k = K.jt_ptr[i]; k < K.jt_ptr[i + 1]; ++k) {
             const int s = K.jt_idx[k], r = K.jr[s];
             const double jvs = jac_raw ? jac_raw[K.jsel[s]] * K.d[K.jc[s]] * sg[r] : jv[s];
@@ -1640,6 +1645,7 @@ __global__ void __launch_bounds__(kIB) k_rs_begin(const IpmK K) {
     double* jv = K.jv + b * K.nj;
     const double* jac = K.jac + b * K.nnzj;
     for (int j = threadIdx.x; j < m; j += kIB) gS[j] = K.graw[b * m + j] * sg[j];
+#pragma unroll 8
     for (int q = threadIdx.x; q < K.nj; q += kIB) jv[q] = jac[K.jsel[q]] * K.d[K.jc[q]] * sg[K.jr[q]];
     __syncthreads();
     const double* x = K.xr + b * nf;
@@ -1657,6 +1663,7 @@ __global__ void __launch_bounds__(kIB) k_rs_begin(const IpmK K) {
     double ed = 0.0, ep = 0.0;
     for (int i = threadIdx.x; i < nf; i += kIB) {
         double jty = 0.0;
+#pragma unroll 4
         for (int k = K.jt_ptr[i]; k < K.jt_ptr[i + 1]; ++k) {
             const int q = K.jt_idx[k];
             jty += jv[q] * y[K.jr[q]];
@@ -2101,6 +2108,7 @@ __global__ void __launch_bounds__(kIB) k_lbfgs_update(const IpmK K) {
         double sy = 0.0, ss = 0.0, yy = 0.0;
         for (int i = threadIdx.x; i < nf; i += kIB) {
             double jty = 0.0, jtyp = 0.0;
+#pragma unroll 4
             for (int k = K.jt_ptr[i]; k < K.jt_ptr[i + 1]; ++k) {
                 const int t = K.jt_idx[k];
                 const double yk = y[K.jr[t]];
