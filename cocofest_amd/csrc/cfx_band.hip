@@ -1491,36 +1491,20 @@ __global__ void __launch_bounds__(NT) k_band_lu_panel(int n, int kl, int ku, dou
 }
 
 // Solves with the factors of any placement for single wide bands: one wavefront runs the substitution's
-// dependent chain with its window in registers, the other waves stream the band columns it needs into LDS ahead
-// of it, CH columns per buffer, one barrier per CH columns — the global placement's substitutions pay two barriers
-// and an L2 round trip per column instead.  The window does not slide: slot s (lane s % 64 of register s / 64) holds
-// x[g] for the g = s mod W of the current window, so a step touches one slot's lane (readlane / select) and no DPP
-// shift runs on the chain; the producers store each column's multipliers already rotated into their slots.
-// Forward pass: x <- L^-1 P x over the window [j, j + W), W = 64 KF > kl; per column the buffer holds L(j + i, j) at
-// slot (j + i) mod W (zero outside i = 1 .. min(kl, n - 1 - j)), the pivot row and x[j + W], the element entering
-// the slot step j frees.
-template <int KF>
-__device__ __forceinline__ double slot_get(const double (&xw)[KF], int f) {  // register f (uniform)
-    double v = xw[0];
-#pragma unroll
-    for (int k = 1; k < KF; ++k) v = f == k ? xw[k] : v;
-    return v;
-}
-template <int KF>
-__device__ __forceinline__ void slot_set(double (&xw)[KF], int f, int l, double v) {  // lane l of register f
-    const int lane = threadIdx.x & 63;
-#pragma unroll
-    for (int k = 0; k < KF; ++k) xw[k] = (k == f && lane == l) ? v : xw[k];
-}
-
+// dependent chain with its window in registers (as the register placement's solve), the other waves stream
+// the band columns it needs into LDS ahead of it, CH columns per buffer, one barrier per CH columns — the
+// global placement's substitutions pay two barriers and an L2 round trip per column instead.
+// Forward pass: x <- L^-1 P x, lane i + 64 f holding x[j + i + 64 f] (i + 64 f <= kl < 64 KF); per column the
+// buffer holds the multipliers L(j + i, j) at slot i (zero outside 1 .. min(kl, n - 1 - j)), the pivot row
+// and x[j + 1 + kl], the element entering the window.
 template <int KF, int NT>
 __global__ void __launch_bounds__(NT) k_band_fwd_stream(int n, int kl, int ku, int nrhs,
                                                         const double* __restrict__ AB,
                                                         const int32_t* __restrict__ IPIV, double* RHS) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
-    constexpr int CW = 64 * KF, W = CW, CH = 128 / KF, NP = NT - 64, SD = 4;
+    constexpr int CW = 64 * KF, CH = 128 / KF, NP = NT - 64, SD = 4;
     const int t = threadIdx.x, lane = t & 63;
-    const int ldab = 2 * kl + ku + 1, kv = kl + ku;
+    const int ldab = 2 * kl + ku + 1, kv = kl + ku, fk = kl >> 6, lk = kl & 63;
     const double* const ab = AB + (int64_t)blockIdx.x * n * ldab;
     const int32_t* const piv = IPIV + (int64_t)blockIdx.x * n;
     double* const M = smem;                // [buffer][column][slot]
@@ -1535,14 +1519,14 @@ __global__ void __launch_bounds__(NT) k_band_fwd_stream(int n, int kl, int ku, i
             const int b = ci & 1, jb = ci * CH, tp = t - 64;
 #pragma unroll 8
             for (int e = tp; e < CH * CW; e += NP) {
-                const int jj = e / CW, sl = e - jj * CW, j = jb + jj, i = (sl - j) & (W - 1);
-                M[(b * CH + jj) * CW + sl] =
+                const int jj = e / CW, i = e - jj * CW, j = jb + jj;
+                M[(b * CH + jj) * CW + i] =
                     (j < steps && i >= 1 && i <= min(kl, n - 1 - j)) ? ab[(int64_t)j * ldab + kv + i] : 0.0;
             }
             for (int jj = tp; jj < CH; jj += NP) {
                 const int j = jb + jj;
                 Pv[b * CH + jj] = j < steps ? piv[j] - j : 0;
-                X[b * CH + jj] = j + W < n ? x[j + W] : 0.0;
+                X[b * CH + jj] = j + 1 + kl < n ? x[j + 1 + kl] : 0.0;
             }
         };
         double xw[KF];
@@ -1550,7 +1534,7 @@ __global__ void __launch_bounds__(NT) k_band_fwd_stream(int n, int kl, int ku, i
 #pragma unroll
             for (int f = 0; f < KF; ++f) {
                 const int i = lane + 64 * f;
-                xw[f] = i < n ? x[i] : 0.0;
+                xw[f] = (i <= kl && i < n) ? x[i] : 0.0;
             }
         } else {
             produce(0);
@@ -1583,18 +1567,26 @@ __global__ void __launch_bounds__(NT) k_band_fwd_stream(int n, int kl, int ku, i
                             const int p = __builtin_amdgcn_readfirstlane(pr[s]);
                             const double nxv = nr[s];
                             fetch(jj + SD, lr[s], pr[s], nr[s]);
-                            const int o = j & (W - 1), fo = o >> 6, lo = o & 63;
-                            if (p != 0) {  // rows j and j + p
-                                const int q = (o + p) & (W - 1), fq = q >> 6, lq = q & 63;
-                                const double a = lane_read(slot_get(xw, fo), lo), bv = lane_read(slot_get(xw, fq), lq);
-                                slot_set(xw, fo, lo, bv);
-                                slot_set(xw, fq, lq, a);
+                            if (p != 0) {
+                                const int fp = p >> 6, lp = p & 63;
+                                double src = xw[0];
+#pragma unroll
+                                for (int f = 1; f < KF; ++f)
+                                    if (f == fp) src = xw[f];
+                                const double a = lane_read(xw[0], 0), bv = lane_read(src, lp);
+                                xw[0] = lane == 0 ? bv : xw[0];
+#pragma unroll
+                                for (int f = 0; f < KF; ++f)
+                                    if (f == fp) xw[f] = lane == lp ? a : xw[f];
                             }
-                            const double xj = lane_read(slot_get(xw, fo), lo);
+                            const double xj = lane_read(xw[0], 0);
 #pragma unroll
                             for (int f = 0; f < KF; ++f) xw[f] -= lc[f] * xj;
                             *(lane == 0 ? x + j : dsink) = xj;
-                            slot_set(xw, fo, lo, nxv);  // x[j + W] into the freed slot
+                            slide<KF>(xw);
+#pragma unroll
+                            for (int f = 0; f < KF; ++f)
+                                if (f == fk && lane == lk) xw[f] = nxv;
                         }
                     }
                 }
@@ -1603,24 +1595,20 @@ __global__ void __launch_bounds__(NT) k_band_fwd_stream(int n, int kl, int ku, i
             }
             __syncthreads();
         }
-        if (t < 64) {
-            const int o = (n - 1) & (W - 1);
-            const double xl = lane_read(slot_get(xw, o >> 6), o & 63);
-            if (t == 0) x[n - 1] = xl;
-        }
+        if (t == 0) x[n - 1] = xw[0];
         __syncthreads();
     }
 }
 
-// Backward pass: x <- U^-1 x over the window (j - W, j], W = 64 KB > kv, slot s holding x[g] for g = s mod W; per
-// column the buffer holds U(j - i, j) at slot (j - i) mod W (i = 0: the diagonal; zero past min(kv, j)) and x[j - W].
+// Backward pass: x <- U^-1 x, lane i + 64 k holding x[j - i - 64 k] (i + 64 k <= kv < 64 KB); per column the
+// buffer holds U(j - i, j) at slot i (zero past min(kv, j)) and x[j - 1 - kv].
 template <int KB, int NT>
 __global__ void __launch_bounds__(NT) k_band_bwd_stream(int n, int kl, int ku, int nrhs,
                                                         const double* __restrict__ AB, double* RHS) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
-    constexpr int CW = 64 * KB, W = CW, CH = 128 / KB, NP = NT - 64, SD = 4;
+    constexpr int CW = 64 * KB, CH = 128 / KB, NP = NT - 64, SD = 4;
     const int t = threadIdx.x, lane = t & 63;
-    const int ldab = 2 * kl + ku + 1, kv = kl + ku;
+    const int ldab = 2 * kl + ku + 1, kv = kl + ku, fk = kv >> 6, lk = kv & 63;
     const double* const ab = AB + (int64_t)blockIdx.x * n * ldab;
     double* const U = smem;
     double* const X = U + 2 * CH * CW;
@@ -1632,20 +1620,20 @@ __global__ void __launch_bounds__(NT) k_band_bwd_stream(int n, int kl, int ku, i
             const int b = ci & 1, jb = n - 1 - ci * CH, tp = t - 64;
 #pragma unroll 8
             for (int e = tp; e < CH * CW; e += NP) {
-                const int jj = e / CW, sl = e - jj * CW, j = jb - jj, i = (j - sl) & (W - 1);
-                U[(b * CH + jj) * CW + sl] = (j >= 0 && i <= min(kv, j)) ? ab[(int64_t)j * ldab + kv - i] : 0.0;
+                const int jj = e / CW, i = e - jj * CW, j = jb - jj;
+                U[(b * CH + jj) * CW + i] = (j >= 0 && i <= min(kv, j)) ? ab[(int64_t)j * ldab + kv - i] : 0.0;
             }
             for (int jj = tp; jj < CH; jj += NP) {
                 const int j = jb - jj;
-                X[b * CH + jj] = j - W >= 0 ? x[j - W] : 0.0;
+                X[b * CH + jj] = j - 1 - kv >= 0 ? x[j - 1 - kv] : 0.0;
             }
         };
         double xw[KB];
         if (t < 64) {
 #pragma unroll
             for (int k = 0; k < KB; ++k) {
-                const int sl = lane + 64 * k, g = (n - 1) - ((n - 1 - sl) & (W - 1));
-                xw[k] = g >= 0 ? x[g] : 0.0;
+                const int i = lane + 64 * k;
+                xw[k] = (i <= kv && n - 1 - i >= 0) ? x[n - 1 - i] : 0.0;
             }
         } else {
             produce(0);
@@ -1674,15 +1662,17 @@ __global__ void __launch_bounds__(NT) k_band_bwd_stream(int n, int kl, int ku, i
                             for (int k = 0; k < KB; ++k) uc[k] = ur[s][k];
                             const double nxv = nr[s];
                             fetch(jj + SD, ur[s], nr[s]);
-                            const int o = j & (W - 1), fo = o >> 6, lo = o & 63;
-                            const double xj = lane_read(slot_get(xw, fo), lo) / lane_read(slot_get(uc, fo), lo);
+                            const double xj = lane_read(xw[0], 0) / lane_read(uc[0], 0);
                             *(lane == 0 ? x + j : dsink) = xj;
 #pragma unroll
                             for (int k = 0; k < KB; ++k) {  // one fused multiply-subtract per element, as the column kernels
-                                const double u = (k == fo && lane == lo) ? 0.0 : uc[k];
+                                const double u = (k == 0 && lane == 0) ? 0.0 : uc[k];
                                 xw[k] -= u * xj;
                             }
-                            slot_set(xw, fo, lo, nxv);  // x[j - W] into the freed slot
+                            slide<KB>(xw);
+#pragma unroll
+                            for (int k = 0; k < KB; ++k)
+                                if (k == fk && lane == lk) xw[k] = nxv;
                         }
                     }
                 }
