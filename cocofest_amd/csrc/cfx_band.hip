@@ -1258,6 +1258,9 @@ __global__ void __launch_bounds__(NT) k_band_lu_panel(int n, int kl, int ku, dou
     int* const sp = q + PR;                                // pivot row of each panel step (panel-relative)
     int* const snz = sp + NB;                              // its pivot was non-zero
     auto at = [&](int i, int j) CFX_INLINE -> double& { return ab[(int64_t)j * ldab + kv + i - j]; };
+#ifdef CFX_BAND_PROF
+    unsigned long long prof[8] = {}, last_ = wall_clock64();
+#endif
     // fill rows (storage rows < kl) of columns zhi + 1 .. zend, as columns enter the reach of a panel's rows
     auto zero_fill = [&](int zhi, int zend, int tid, int nthr) CFX_INLINE {
         for (int64_t e = tid; e < (int64_t)(zend - zhi) * kl; e += nthr)
@@ -1276,6 +1279,7 @@ __global__ void __launch_bounds__(NT) k_band_lu_panel(int n, int kl, int ku, dou
                 const int r = lane + 64 * h;
                 pa[h][c] = (r < prp && c < wp && r - c <= kl && c - r <= kv) ? at(j0p + r, j0p + c) : 0.0;
             }
+        PANEL_STAMP(0);
 #pragma unroll
         for (int jj = 0; jj < NB; ++jj) {
             if (jj < wp) {
@@ -1341,6 +1345,7 @@ __global__ void __launch_bounds__(NT) k_band_lu_panel(int n, int kl, int ku, dou
                 }
             }
         }
+        PANEL_STAMP(1);
 #pragma unroll
         for (int h = 0; h < RH; ++h)
 #pragma unroll
@@ -1348,6 +1353,7 @@ __global__ void __launch_bounds__(NT) k_band_lu_panel(int n, int kl, int ku, dou
                 const int r = lane + 64 * h;
                 if (r < prp && c < wp) P0[c * PR + r] = pa[h][c];
             }
+        PANEL_STAMP(7);
     };
     // 2. trailing columns c0 + cc (cc = cb, cb + stride, ... < ce) of panel j0 (width w, rows pr), one wave each: lane
     //    holds rows lane + 64 h; row r starts from original row q[r], and for k = 0 .. w - 1 the final U12 element of
@@ -1411,9 +1417,6 @@ __global__ void __launch_bounds__(NT) k_band_lu_panel(int n, int kl, int ku, dou
         }
     };
     int info = 0, ju = 0, zhi = -1;
-#ifdef CFX_BAND_PROF
-    unsigned long long prof[8] = {}, last_ = wall_clock64();
-#endif
     {  // prologue: the first panel
         const int w0 = min(NB, n), zend = min(w0 - 1 + kv, n - 1);
         zero_fill(zhi, zend, t, NT);

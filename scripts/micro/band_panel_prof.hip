@@ -57,13 +57,14 @@ int main(int argc, char** argv) {
         const int nb = cfx::kPanelNB, panels = (n + nb - 1) / nb;
         // per panel: [2] reach / first zero pivot, [3] write-back + blocked multipliers + LDS barrier, [4] own trailing
         // columns, [5] (wavefront 0) fill rows + next panel re-read + its factorisation, [6] wait at the closing barrier
-        const char* names[5] = {"reach", "writeback_lt", "trail", "lookahead_factor", "barrier_wait"};
-        const int ids[5] = {2, 3, 4, 5, 6};
+        const char* names[8] = {"reach", "writeback_lt", "trail", "lookahead_rest", "barrier_wait", "panel_fence_load",
+                                "panel_steps", "panel_store"};
+        const int ids[8] = {2, 3, 4, 5, 6, 0, 1, 7};
         std::printf("{\"n\": %d, \"kl\": %d, \"ku\": %d, \"nb\": %d, \"ms\": %.3f, \"us_per_panel\": %.3f", n, kl, ku,
                     nb, ms, 1e3 * ms / panels);
         double tot = 0;
         for (int w = 0; w < 2; ++w)
-            for (int i = 0; i < 5; ++i) {
+            for (int i = 0; i < 8; ++i) {
                 std::printf(", \"w%d_%s\": %.3f", w, names[i], p[8 * w + ids[i]] * 0.01 / panels);  // 100 MHz ticks
                 if (w == 0) tot += p[ids[i]] * 0.01 / panels;
             }
