@@ -43,7 +43,6 @@ args = ap.parse_args()
 
 def build(objective):
     import cocofest_amd as C
-    from oracle import fes_oracle as O
 
     models = []
     for n, c in zip(R.MUSCLES, R.muscle_constants(legacy_rates=True)):
@@ -58,7 +57,7 @@ def build(objective):
     cl.add(C.ConstraintFcn.SUPERIMPOSE_MARKERS, first_marker="COM_hand", second_marker="reaching_target", phase=0,
            node=R.MARKER_NODE, axes=[C.Axis.X, C.Axis.Y])
     return C.OcpFesMsk.prepare_ocp(model=model, final_time=R.FINAL_TIME, n_shooting=R.N,
-                                   pulse_width={"min": O.model_constants("ding2007")["pd0"], "max": 0.0006},
+                                   pulse_width={"min": C.DingModelPulseWidthFrequency().pd0, "max": 0.0006},
                                    objective={f"minimize_muscle_{objective}": True},
                                    msk_info={"with_residual_torque": False, "bound_type": "start_end",
                                              "bound_data": [[0, 5], [0, 5]], "custom_constraint": cl},
