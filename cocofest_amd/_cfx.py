@@ -15,7 +15,7 @@ import numpy as np
 
 LIB_PATH = pathlib.Path(__file__).with_name("libcfx.so")
 
-ABI_VERSION = 8
+ABI_VERSION = 9
 OK, EINVAL, EHIP, ENOMEM, EUNSUPPORTED, ENODEV, ECALLBACK = 0, -1, -2, -3, -4, -5, -6
 MODEL_IDS = {
     "ding2003": 0,
@@ -120,7 +120,9 @@ class IpmOptions(C.Structure):
                 ("resto_failure_restart", C.c_int32), ("constr_viol_tol", C.c_double),
                 ("dual_inf_tol", C.c_double), ("compl_inf_tol", C.c_double),
                 ("acceptable_constr_viol_tol", C.c_double), ("acceptable_dual_inf_tol", C.c_double),
-                ("acceptable_compl_inf_tol", C.c_double)]
+                ("acceptable_compl_inf_tol", C.c_double), ("warm_start_bound_push", C.c_double),
+                ("warm_start_bound_frac", C.c_double), ("warm_start_mult_bound_push", C.c_double),
+                ("warm_start_init_point", C.c_int32), ("honor_original_bounds", C.c_int32)]
 
 
 # cfx_ipm_get_status values (Ipopt's ApplicationReturnStatus)
@@ -133,7 +135,8 @@ class IpmStats(C.Structure):
                 ("iterations", C.c_int64), ("host_syncs", C.c_int64), ("wall_s", C.c_double),
                 ("kkt_n", C.c_int64), ("kkt_kl", C.c_int64), ("kkt_ku", C.c_int64), ("kkt_band_n", C.c_int64),
                 ("kkt_border", C.c_int64), ("kkt_blocks", C.c_int64), ("resto_phases", C.c_int64),
-                ("resto_iterations", C.c_int64), ("soft_steps", C.c_int64)]
+                ("resto_iterations", C.c_int64), ("soft_steps", C.c_int64), ("kkt_chain_nodes", C.c_int64),
+                ("kkt_chain_sp", C.c_int64)]
 
 
 # cfx_evaluator / cfx_nlp_desc (cfx_ipm_create_ext): caller-supplied callbacks of an NLP the solver runs on
@@ -184,6 +187,10 @@ SIGNATURES = {
     "cfx_ipm_solve": (C.c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _P, C.c_uint32]),
     "cfx_ipm_get_stats": (C.c_int, [_P, C.POINTER(IpmStats)]),
     "cfx_ipm_get_status": (C.c_int, [_P, C.POINTER(C.c_int32)]),
+    "cfx_ipm_set_warm_start": (C.c_int, [_P, _P, _P, _P, C.c_uint32]),
+    "cfx_ipm_get_bound_multipliers": (C.c_int, [_P, _P, _P, C.c_uint32]),
+    "cfx_btri_factor": (C.c_int, [C.c_int64, C.c_int32, C.c_int32, _P, _P, _P, _P, _P, _P]),
+    "cfx_btri_solve": (C.c_int, [C.c_int64, C.c_int32, C.c_int32, _P, _P, _P, _P, C.c_int32, _P, _P, _P]),
     "cfx_ipm_create_ext": (C.c_int, [C.POINTER(NlpDesc), C.POINTER(Evaluator), _P, _P, C.c_int32,
                                      C.POINTER(IpmOptions), C.POINTER(_P)]),
     "cfx_gather_sum": (C.c_int, [C.c_int64, C.c_int64, _P, _P, _P, C.c_int64, _P, _P]),
@@ -712,6 +719,28 @@ class Ipm:
                 raise CfxError(rc, f"{self.lib.cfx_ipm_last_error(self.s).decode()}: {err!r}") from err
             raise CfxError(rc, self.lib.cfx_ipm_last_error(self.s).decode())
         return v, y, f, conv.astype(bool), its.astype(np.int64), kkt
+
+    def set_warm_start(self, y, z_l, z_u):
+        """Ipopt's warm_start_init_point inputs (cfx_ipm_set_warm_start): y (B, ng) constraint multipliers, z_l / z_u
+        (B, nv) bound multipliers of the unscaled problem; used by solves with the warm_start_init_point option."""
+        B = self.batch
+        y = np.ascontiguousarray(y, dtype=np.float64)
+        zl = np.ascontiguousarray(z_l, dtype=np.float64)
+        zu = np.ascontiguousarray(z_u, dtype=np.float64)
+        if y.size != B * self.ng or zl.size != B * self.nv or zu.size != B * self.nv:
+            raise CfxError(EINVAL, "Ipm.set_warm_start: y must hold batch * ng values, z_l / z_u batch * nv")
+        rc = self.lib.cfx_ipm_set_warm_start(self.s, y.ctypes.data, zl.ctypes.data, zu.ctypes.data, 0)
+        if rc != OK:
+            raise CfxError(rc, self.lib.cfx_ipm_last_error(self.s).decode())
+
+    def bound_multipliers(self):
+        """(z_l, z_u), each (B, nv): the last solve's bound multipliers of the unscaled problem."""
+        zl = np.empty((self.batch, self.nv))
+        zu = np.empty((self.batch, self.nv))
+        rc = self.lib.cfx_ipm_get_bound_multipliers(self.s, zl.ctypes.data, zu.ctypes.data, 0)
+        if rc != OK:
+            raise CfxError(rc, self.lib.cfx_ipm_last_error(self.s).decode())
+        return zl, zu
 
     def stats(self):
         st = IpmStats()

@@ -27,3 +27,13 @@ int cfx_band_solve_multi(int64_t n, int32_t kl, int32_t ku, int64_t batch, int32
 // following cfx_eval_h re-uses them only when the caller has declared, with on = 2 right before it, that the point
 // is the one of that eval_all (cfx_ipm_solve, which does not move K.vx in between).  Any other eval_h recomputes.
 int cfx_internal_msk_stash(cfx_handle* h, int on);
+
+// block-tridiagonal (stage chain) factorisation and solves by block cyclic reduction (cfx_chain.hip): node size sp
+// (a multiple of 16, <= 128); D / L / U [M][sp][sp] per instance at `stride`, work Cl / Cr at `wstride`; right-hand
+// side c of instance b at R + b r_inst + c r_rhs (node k at + k sp), scratch T of the same shape
+int cfx_chain_sp_ok(int32_t sp);
+int cfx_chain_factor_s(int64_t batch, int32_t M, int32_t sp, double* D, double* L, double* U, int64_t stride,
+                       double* Cl, double* Cr, int64_t wstride, int32_t* info, void* stream);
+int cfx_chain_solve_s(int64_t batch, int32_t M, int32_t sp, const double* D, const double* L, const double* U,
+                      int64_t stride, const double* Cl, const double* Cr, int64_t wstride, int32_t nrhs, double* R,
+                      int64_t r_inst, int64_t r_rhs, double* T, int64_t t_inst, int64_t t_rhs, void* stream);

@@ -91,6 +91,12 @@ struct IpmK {
     const int32_t *jrw_ptr, *jrw_idx;  // triplets of each constraint row (row scaling)
     const int32_t *kkt_ptr, *kkt_src;  // sources of each band-storage entry
     const int32_t* pos;                // KKT unknown (free variables, then rows) -> band order
+    // Stage-chain layout (chain = 1): the unknowns grouped by stage into cM nodes of csp (padded) unknowns, the KKT
+    // matrix block tridiagonal and factored by block cyclic reduction (cfx_chain.hip); P = 1 and nA = cM csp, the
+    // band storage `ab` holds [D | L | U] ([3][cM][csp][csp] per instance, NE_A entries), cw the reduction's work
+    // ([B][2][cM][csp][csp]), ct its solve scratch ([B][max(na, 1)][nA]); a border (np > 0) as below.
+    int chain, cM, csp;
+    double *cw, *ct;
     // KKT layout.  P = 1, np = 0: one band of nA = nK unknowns (factor + solve in one launch).  Otherwise the
     // unknowns split into P diagonal band blocks of nA rows each (padded with unit rows) and a dense border of np
     // unknowns — Hmed intensity parameters, whose sliding windows couple most stages, and the separators between
@@ -337,9 +343,14 @@ __global__ void __launch_bounds__(kIB) k_ipm_fix(const IpmK K, const double* __r
 
 // after eval_all at the starting point: gradient-based scaling (solver.py _set_function_scaling), bound push,
 // z = mu / s, y = 0, empty filter
-__global__ void __launch_bounds__(kIB) k_ipm_init(const IpmK K) {
+// Warm start (Ipopt warm_start_init_point; ws = the unscaled multipliers of cfx_ipm_set_warm_start, else NULL): y and
+// the bound multipliers from them (scaled problem: y_s = sf y / s_g, z_s = sf d z, z raised to
+// warm_start_mult_bound_push), x pushed by warm_start_bound_push / warm_start_bound_frac, no least-squares step.
+__global__ void __launch_bounds__(kIB) k_ipm_init(const IpmK K, const double* __restrict__ wy,
+                                                  const double* __restrict__ wzl, const double* __restrict__ wzu) {
     __shared__ double sh[kIB / 64];
     const int64_t b = blockIdx.x;
+    const bool warm = wy != nullptr;
     const double* grad = K.grad + b * K.n;
     const double* jac = K.jac + b * K.nnzj;
     double gmax = 0.0;
@@ -352,27 +363,37 @@ __global__ void __launch_bounds__(kIB) k_ipm_init(const IpmK K) {
             const int s = K.jrw_idx[k];
             rmax = max_n(rmax, fabs(jac[K.jsel[s]] * K.d[K.jc[s]]));
         }
-        K.sg[b * K.m + r] = clamp_hi(100.0 / clamp_lo(rmax, 1e-300), 1.0);
-        K.y[b * K.m + r] = 0.0;
+        const double sgr = clamp_hi(100.0 / clamp_lo(rmax, 1e-300), 1.0);
+        K.sg[b * K.m + r] = sgr;
+        K.y[b * K.m + r] = warm ? sf * wy[b * K.m + r] / sgr : 0.0;
     }
     const double mu = K.o.mu_init;
+    const double push = warm ? K.o.warm_start_bound_push : K.o.bound_push;
+    const double frac = warm ? K.o.warm_start_bound_frac : 0.5;
     for (int i = threadIdx.x; i < K.nf; i += kIB) {
         double xi = K.vx[b * K.n + K.free[i]] / K.d[i];
         const bool hL = K.hasL[i], hU = K.hasU[i];
         const double lb = K.lbF[i], ub = K.ubF[i];
         K.lbI[b * K.nf + i] = lb;
         K.ubI[b * K.nf + i] = ub;
-        double pl = K.o.bound_push * clamp_lo(hL ? fabs(lb) : 1.0, 1.0);
-        double pu = K.o.bound_push * clamp_lo(hU ? fabs(ub) : 1.0, 1.0);
+        double pl = push * clamp_lo(hL ? fabs(lb) : 1.0, 1.0);
+        double pu = push * clamp_lo(hU ? fabs(ub) : 1.0, 1.0);
         const double width = (hL && hU) ? ub - lb : INFINITY;
-        pl = min_n(pl, 0.5 * width);
-        pu = min_n(pu, 0.5 * width);
+        pl = min_n(pl, frac * width);
+        pu = min_n(pu, frac * width);
         if (hL) xi = max_n(xi, lb + pl);
         if (hU) xi = min_n(xi, ub - pu);
         const double sl = hL ? xi - lb : 1.0, su = hU ? ub - xi : 1.0;
         K.x[b * K.nf + i] = xi;
-        K.zl[b * K.nf + i] = hL ? mu / sl : 0.0;
-        K.zu[b * K.nf + i] = hU ? mu / su : 0.0;
+        if (warm) {
+            const int64_t e = b * K.n + K.free[i];
+            const double zs = sf * K.d[i];
+            K.zl[b * K.nf + i] = hL ? max_n(zs * wzl[e], K.o.warm_start_mult_bound_push) : 0.0;
+            K.zu[b * K.nf + i] = hU ? max_n(zs * wzu[e], K.o.warm_start_mult_bound_push) : 0.0;
+        } else {
+            K.zl[b * K.nf + i] = hL ? mu / sl : 0.0;
+            K.zu[b * K.nf + i] = hU ? mu / su : 0.0;
+        }
         K.vx[b * K.n + K.free[i]] = xi * K.d[i];
     }
     for (int k = threadIdx.x; k < kFilt; k += kIB) {
@@ -385,7 +406,7 @@ __global__ void __launch_bounds__(kIB) k_ipm_init(const IpmK K) {
         S.sf = sf;
         S.lsig = 1.0;  // Ipopt limited_memory_init_val
         S.err0 = INFINITY;
-        S.reinit = K.m > 0;
+        S.reinit = K.m > 0 && !warm;
         K.sc[b] = S;
     }
 }
@@ -2034,10 +2055,18 @@ __global__ void __launch_bounds__(kIB) k_rs_finish(const IpmK K) {
 }
 
 // project onto the original bounds (Ipopt honor_original_bounds) and write the final point into vx
-__global__ void __launch_bounds__(kIB) k_ipm_final(const IpmK K) {
+// (honor_original_bounds only), and the bound multipliers of the unscaled problem (z_l, z_u [B][n]; 0 at fixed ones)
+__global__ void __launch_bounds__(kIB) k_ipm_final(const IpmK K, double* __restrict__ zlo, double* __restrict__ zuo) {
     const int64_t b = blockIdx.x;
     double* x = K.x + b * K.nf;
-    for (int i = threadIdx.x; i < K.nf; i += kIB) x[i] = min_n(max_n(x[i], K.lbF0[i]), K.ubF0[i]);
+    if (K.o.honor_original_bounds)
+        for (int i = threadIdx.x; i < K.nf; i += kIB) x[i] = min_n(max_n(x[i], K.lbF0[i]), K.ubF0[i]);
+    const double sf = K.sc[b].sf;
+    for (int j = threadIdx.x; j < K.nfix; j += kIB) zlo[b * K.n + K.fixed[j]] = zuo[b * K.n + K.fixed[j]] = 0.0;
+    for (int i = threadIdx.x; i < K.nf; i += kIB) {
+        zlo[b * K.n + K.free[i]] = K.zl[b * K.nf + i] / (sf * K.d[i]);
+        zuo[b * K.n + K.free[i]] = K.zu[b * K.nf + i] / (sf * K.d[i]);
+    }
     __syncthreads();
     write_full(K, b, x, K.vx);
 }
@@ -2320,6 +2349,9 @@ struct cfx_ipm {
     hipStream_t stream = nullptr;
     // staging for host inputs / outputs
     double *d_fv = nullptr, *d_yo = nullptr, *d_kkt = nullptr;
+    // warm start inputs (cfx_ipm_set_warm_start; allocated on first use) and the last solve's bound multipliers
+    double *d_wy = nullptr, *d_wzl = nullptr, *d_wzu = nullptr, *d_zlo = nullptr, *d_zuo = nullptr;
+    bool warm_set = false;
     int32_t *d_conv = nullptr, *d_its = nullptr, *d_status = nullptr;
     std::vector<int32_t> h_status;  // CFX_IPM_* status per instance of the last solve (cfx_ipm_get_status)
     // J_g's constant values (cfx_jac_constant_mask) stay in K.jac after the first full evaluation: later evaluations
@@ -2443,6 +2475,11 @@ extern "C" void cfx_ipm_default_options(cfx_ipm_options* o) {
     o->acceptable_constr_viol_tol = 0.01;
     o->acceptable_dual_inf_tol = 1e10;
     o->acceptable_compl_inf_tol = 0.01;
+    o->warm_start_bound_push = 1e-3;
+    o->warm_start_bound_frac = 1e-3;
+    o->warm_start_mult_bound_push = 1e-3;
+    o->warm_start_init_point = 0;
+    o->honor_original_bounds = 0;  // Ipopt 3.14's default
 }
 
 // CSR of `key` (values in [0, nkeys)) with the sources of each key in increasing source order
@@ -2453,6 +2490,137 @@ static void csr(const std::vector<int64_t>& key, int64_t nkeys, std::vector<int3
     idx.assign(key.size(), 0);
     std::vector<int32_t> fill(ptr.begin(), ptr.end() - 1);
     for (size_t s = 0; s < key.size(); ++s) idx[fill[key[s]]++] = (int32_t)s;
+}
+
+// Stage-chain grouping of the KKT unknowns (IpmK::chain; cfx_chain.hip).  A node width w over the ORIGINAL variable
+// index (node(v) = v / w; for a shooting transcription w = nx + nu puts x_k and u_k in node k) is searched from the
+// smallest that can work; a constraint row belongs to the node of its last free column.  Accepted when every Jacobian
+// and Hessian entry couples equal or adjacent nodes (block tridiagonal) and the rows of each node match one-to-one to
+// variables of that node through Jacobian entries (Kuhn's augmenting paths, rows in index order, so a continuity row
+// takes the state its -I falls on): rows left unmatched (a marker row on states already claimed by continuity rows,
+// the continuity row of a fixed end state), rows without free columns and the parameters go to the dense border.
+// With that matching every contiguous range of nodes has a constraint block of full structural row rank, so the
+// pivot blocks of the cyclic reduction are nonsingular KKT matrices.
+struct ChainPlan {
+    bool ok = false;
+    int M = 0, sp = 0, nb = 0, width = 0;
+    std::vector<int32_t> pos;  // KKT unknown (free variables, then rows) -> slot (node k: k sp + local; border: M sp + j)
+};
+static ChainPlan chain_plan(int nf, int m, const std::vector<int32_t>& freev, const std::vector<uint8_t>& par,
+                            const std::vector<int32_t>& jrF, const std::vector<int32_t>& jcF,
+                            const std::vector<int32_t>& hrF, const std::vector<int32_t>& hcF, int max_border) {
+    ChainPlan best;
+    const int nj = (int)jrF.size(), nh = (int)hrF.size();
+    std::vector<int64_t> rmin(m, INT64_MAX), rmax(m, -1);
+    for (int s = 0; s < nj; ++s) {
+        const int c = jcF[s];
+        if (par[c]) continue;
+        rmin[jrF[s]] = std::min<int64_t>(rmin[jrF[s]], freev[c]);
+        rmax[jrF[s]] = std::max<int64_t>(rmax[jrF[s]], freev[c]);
+    }
+    int64_t span = 0, vmax = 0;
+    for (int r = 0; r < m; ++r)
+        if (rmax[r] >= 0) span = std::max(span, rmax[r] - rmin[r]);
+    for (int s = 0; s < nh; ++s)
+        if (!par[hrF[s]] && !par[hcF[s]]) span = std::max<int64_t>(span, std::abs((int64_t)freev[hrF[s]] - freev[hcF[s]]));
+    for (int i = 0; i < nf; ++i)
+        if (!par[i]) vmax = std::max<int64_t>(vmax, freev[i]);
+    // Jacobian entries of each row over non-parameter columns (CSR)
+    std::vector<int32_t> rptr(m + 1, 0), rcol;
+    for (int s = 0; s < nj; ++s)
+        if (!par[jcF[s]]) rptr[jrF[s] + 1]++;
+    for (int r = 0; r < m; ++r) rptr[r + 1] += rptr[r];
+    rcol.resize(rptr[m]);
+    {
+        std::vector<int32_t> fill(rptr.begin(), rptr.end() - 1);
+        for (int s = 0; s < nj; ++s)
+            if (!par[jcF[s]]) rcol[fill[jrF[s]]++] = jcF[s];
+    }
+    for (int64_t w = std::max<int64_t>(1, (span + 2) / 2); w <= span + 1; ++w) {
+        const int M = (int)(vmax / w) + 1;
+        auto vnode = [&](int i) { return (int)(freev[i] / w); };
+        bool tri = true;
+        for (int r = 0; r < m && tri; ++r)
+            if (rmax[r] >= 0 && rmin[r] / w < rmax[r] / w - 1) tri = false;
+        for (int s = 0; s < nh && tri; ++s)
+            if (!par[hrF[s]] && !par[hcF[s]] && std::abs(vnode(hrF[s]) - vnode(hcF[s])) > 1) tri = false;
+        if (!tri) continue;
+        // rows of each node in index order; Kuhn's matching of rows to variables of the same node
+        std::vector<int32_t> match_var(nf, -1), match_row(m, -1), rnode(m, -1);
+        std::vector<std::vector<int32_t>> nrows(M);
+        for (int r = 0; r < m; ++r)
+            if (rmax[r] >= 0) {
+                rnode[r] = (int)(rmax[r] / w);
+                nrows[rnode[r]].push_back(r);
+            }
+        std::vector<int32_t> seen(nf, -1);
+        int stamp = 0;
+        std::vector<std::pair<int32_t, int32_t>> stack;  // (row, next entry)
+        for (int k = 0; k < M; ++k)
+            for (int r0 : nrows[k]) {
+                ++stamp;
+                // iterative DFS for an augmenting path from row r0
+                stack.assign(1, {r0, rptr[r0]});
+                std::vector<int32_t> path_var;
+                bool found = false;
+                while (!stack.empty() && !found) {
+                    auto& [r, e] = stack.back();
+                    if (e >= rptr[r + 1]) {
+                        stack.pop_back();
+                        if (!path_var.empty()) path_var.pop_back();
+                        continue;
+                    }
+                    const int v = rcol[e++];
+                    if (vnode(v) != k || seen[v] == stamp) continue;
+                    seen[v] = stamp;
+                    path_var.push_back(v);
+                    if (match_var[v] < 0) {
+                        found = true;
+                    } else {
+                        stack.push_back({match_var[v], rptr[match_var[v]]});
+                    }
+                }
+                if (found)  // flip the path: row stack[d] takes path_var[d]
+                    for (size_t d = 0; d < stack.size(); ++d) {
+                        const int r = stack[d].first, v = path_var[d];
+                        match_var[v] = r;
+                        match_row[r] = v;
+                    }
+            }
+        std::vector<int32_t> cnt(M, 0);
+        int nb = 0;
+        for (int i = 0; i < nf; ++i) par[i] ? ++nb : ++cnt[vnode(i)];
+        for (int r = 0; r < m; ++r) match_row[r] >= 0 ? ++cnt[rnode[r]] : ++nb;
+        int smax = 0;
+        for (int k = 0; k < M; ++k) smax = std::max(smax, cnt[k]);
+        const int sp = (smax + 15) / 16 * 16;
+        if (nb > max_border || !cfx_chain_sp_ok(sp) || M < 2) continue;
+        ChainPlan cp;
+        cp.ok = true;
+        cp.M = M;
+        cp.sp = sp;
+        cp.nb = nb;
+        cp.width = (int)w;
+        cp.pos.assign(nf + m, -1);
+        std::fill(cnt.begin(), cnt.end(), 0);
+        int j = 0;
+        for (int i = 0; i < nf; ++i) {
+            if (par[i])
+                cp.pos[i] = M * sp + j++;
+            else {
+                const int k = vnode(i);
+                cp.pos[i] = k * sp + cnt[k]++;
+            }
+        }
+        for (int r = 0; r < m; ++r) {
+            if (match_row[r] >= 0)
+                cp.pos[nf + r] = rnode[r] * sp + cnt[rnode[r]]++;
+            else
+                cp.pos[nf + r] = M * sp + j++;
+        }
+        return cp;
+    }
+    return best;
 }
 
 // a failed cfx_ipm_create: the message goes to cfx_last_error(NULL), as for cfx_create
@@ -2548,7 +2716,8 @@ static int ipm_create_common(cfx_ipm* s, const cfx_sizes& sz, int layout, const 
         !(K.o.soft_resto_pderror_reduction_factor >= 0) || K.o.max_soft_resto_iters < 0 || s->B > 0x7fffffff ||
         !(K.o.constr_viol_tol > 0) || !(K.o.dual_inf_tol > 0) || !(K.o.compl_inf_tol > 0) ||
         !(K.o.acceptable_constr_viol_tol > 0) || !(K.o.acceptable_dual_inf_tol > 0) ||
-        !(K.o.acceptable_compl_inf_tol > 0)) {
+        !(K.o.acceptable_compl_inf_tol > 0) || !(K.o.warm_start_bound_push > 0) || !(K.o.warm_start_bound_frac > 0) ||
+        !(K.o.warm_start_bound_frac <= 0.5) || !(K.o.warm_start_mult_bound_push > 0)) {
         s->err = "cfx_ipm_create: the handle must use CFX_LAYOUT_AOS (or batch 1) and the options must be valid";
         return create_fail(s, CFX_EINVAL);
     }
@@ -2759,9 +2928,20 @@ static int ipm_create_common(cfx_ipm* s, const cfx_sizes& sz, int layout, const 
     // scripts/gpu_nmpc_nd.sh), 2 blocks up to batch 512 (cfg 3, 256 starts: 22.9 vs 27.5 ms; scripts/gpu_cfg3_nd.sh);
     // larger batches fill the chip with one band per instance.
     Cut cut;
+    // Stage-chain layout (block cyclic reduction, cfx_chain.hip): by default for bands the register placement cannot
+    // hold (the reaching task: n = 119,640, kl = 108, where the band factorisation is one workgroup's 119,640-column
+    // chain) at small batches; CFX_IPM_KKT=chain / band forces it on (where a grouping exists) / off.
+    ChainPlan cp;
+    {
+        const char* ke = std::getenv("CFX_IPM_KKT");
+        const bool force_chain = ke && std::strcmp(ke, "chain") == 0, no_chain = ke && std::strcmp(ke, "band") == 0;
+        const bool wide = !cfx_band_reg_ok(nAb, (int32_t)ord.kl, (int32_t)ord.ku) && s->B <= 64 && nK >= 4096;
+        if (force_chain || (wide && !no_chain)) cp = chain_plan(nf, m, freev, par, jrF, jcF, hrF, hcF, kMaxBorder);
+    }
+    const bool chain = cp.ok;
     int64_t nd_batch = 512;
     if (const char* e = std::getenv("CFX_IPM_ND_BATCH")) nd_batch = std::atoll(e);  // tuning override
-    if (s->B <= nd_batch && nAb >= 48) {
+    if (!chain && s->B <= nd_batch && nAb >= 48) {
         int pmax = (int)std::min<int64_t>(std::min(8, nAb / 24), std::max<int64_t>(2, 128 / s->B));
         if (const char* e = std::getenv("CFX_IPM_PARTS")) pmax = std::min(pmax, std::atoi(e));  // tuning override
         for (int P = pmax; P >= 2 && cut.P == 1; --P) {
@@ -2772,16 +2952,19 @@ static int ipm_create_common(cfx_ipm* s, const cfx_sizes& sz, int layout, const 
         }
     }
     const int P = cut.P;
-    const int64_t kl = P > 1 ? cut.kl : ord.kl, ku = P > 1 ? cut.ku : ord.ku;
-    const int64_t nA = P > 1 ? cut.nA : nAb, npb = (P > 1 ? cut.nsep : 0) + nparb;
+    const int64_t kl = chain ? 0 : (P > 1 ? cut.kl : ord.kl), ku = chain ? 0 : (P > 1 ? cut.ku : ord.ku);
+    const int64_t csp = cp.sp, cM = cp.M;
+    const int64_t nA = chain ? cM * csp : (P > 1 ? cut.nA : nAb);
+    const int64_t npb = chain ? cp.nb : (P > 1 ? cut.nsep : 0) + nparb;
     const int64_t nKp = P * nA + npb;
     // natural unknown -> slot in rb
     std::vector<int32_t> pos(nK);
     for (int i = 0; i < nK; ++i) {
         const int v = ord.pos[i];
-        pos[i] = v < nAb ? (P > 1 ? cut.slot[v] : v) : (int32_t)(P * nA + (P > 1 ? cut.nsep : 0) + (v - nAb));
+        pos[i] = chain ? cp.pos[i]
+                       : (v < nAb ? (P > 1 ? cut.slot[v] : v) : (int32_t)(P * nA + (P > 1 ? cut.nsep : 0) + (v - nAb)));
     }
-    const int64_t ldab = 2 * kl + ku + 1;
+    const int64_t ldab = chain ? 0 : 2 * kl + ku + 1;
     const int64_t PA = P * nA;
     // border structure: active columns of each block, Cc non-zeros by border row
     std::vector<std::vector<uint8_t>> isact(P, std::vector<uint8_t>(npb, 0));
@@ -2820,7 +3003,7 @@ static int ipm_create_common(cfx_ipm* s, const cfx_sizes& sz, int layout, const 
         }
     }
     const int64_t ncc = ccq.size();
-    const int64_t NE_A = P * nA * ldab, NE = NE_A + P * na * nA + ncc + npb * npb;
+    const int64_t NE_A = chain ? 3 * cM * csp * csp : P * nA * ldab, NE = NE_A + P * na * nA + ncc + npb * npb;
     if (nh >= (1 << kSrcShift) || nj >= (1 << kSrcShift) || NE >= INT32_MAX) {
         s->err = "cfx_ipm_create: KKT band too large";
         return create_fail(s, CFX_EUNSUPPORTED);
@@ -2830,7 +3013,14 @@ static int ipm_create_common(cfx_ipm* s, const cfx_sizes& sz, int layout, const 
     std::vector<int64_t> flat(er.size());
     for (size_t e = 0; e < er.size(); ++e) {
         const int64_t r = pos[er[e]], c = pos[ec[e]];
-        if (r < PA && c < PA) {  // same block (dissection guarantees it)
+        if (r < PA && c < PA && chain) {  // [D | L | U] of the stage chain (the grouping makes |kr - kc| <= 1)
+            const int64_t kr = r / csp, kc = c / csp, area = kc == kr ? 0 : (kc == kr - 1 ? 1 : 2);
+            if (std::abs(kr - kc) > 1) {
+                s->err = "cfx_ipm_create: stage-chain grouping is not block tridiagonal";
+                return create_fail(s, CFX_EUNSUPPORTED);
+            }
+            flat[e] = area * cM * csp * csp + kr * csp * csp + (r - kr * csp) * csp + (c - kc * csp);
+        } else if (r < PA && c < PA) {  // same block (dissection guarantees it)
             const int64_t q = r / nA, lr = r - q * nA, lc = c - q * nA;
             flat[e] = q * nA * ldab + lc * ldab + kl + ku + lr - lc;
         } else if (r < PA) {
@@ -2849,8 +3039,13 @@ static int ipm_create_common(cfx_ipm* s, const cfx_sizes& sz, int layout, const 
         if (pos[i] < PA) used[pos[i]] = true;
     for (int64_t sl = 0; sl < PA; ++sl)
         if (!used[sl]) {
-            const int64_t q = sl / nA, l = sl - q * nA;
-            flat.push_back(q * nA * ldab + l * ldab + kl + ku);
+            if (chain) {
+                const int64_t k = sl / csp, l = sl - k * csp;
+                flat.push_back(k * csp * csp + l * csp + l);
+            } else {
+                const int64_t q = sl / nA, l = sl - q * nA;
+                flat.push_back(q * nA * ldab + l * ldab + kl + ku);
+            }
             src.push_back((SRC_DC << kSrcShift) | kSrcMask);
         }
     std::vector<int32_t> kptr, kidx, kcode;
@@ -2925,6 +3120,13 @@ static int ipm_create_common(cfx_ipm* s, const cfx_sizes& sz, int layout, const 
     K.ft = dalloc<double>(s, B, &rc);
     K.of = dalloc<double>(s, B, &rc);
     K.ab = dalloc<double>(s, B * NE_A, &rc);
+    K.chain = chain ? 1 : 0;
+    K.cM = (int)cM;
+    K.csp = (int)csp;
+    if (chain) {
+        K.cw = dalloc<double>(s, B * 2 * cM * csp * csp, &rc);
+        K.ct = dalloc<double>(s, B * std::max(na, 1) * nA, &rc);
+    }
     K.Xb = dalloc<double>(s, B * P * na * nA, &rc);
     K.Ccb = dalloc<double>(s, B * ncc, &rc);
     K.Db = dalloc<double>(s, B * npb * npb, &rc);
@@ -2965,6 +3167,8 @@ static int ipm_create_common(cfx_ipm* s, const cfx_sizes& sz, int layout, const 
     s->d_fv = dalloc<double>(s, B * K.nfix, &rc);
     s->d_yo = dalloc<double>(s, B * m, &rc);
     s->d_kkt = dalloc<double>(s, B, &rc);
+    s->d_zlo = dalloc<double>(s, B * n, &rc);
+    s->d_zuo = dalloc<double>(s, B * n, &rc);
     s->d_conv = dalloc<int32_t>(s, B, &rc);
     s->d_its = dalloc<int32_t>(s, B, &rc);
     s->d_status = dalloc<int32_t>(s, B, &rc);
@@ -2988,6 +3192,8 @@ static int ipm_create_common(cfx_ipm* s, const cfx_sizes& sz, int layout, const 
     s->st.kkt_band_n = nA;
     s->st.kkt_border = npb;
     s->st.kkt_blocks = P;
+    s->st.kkt_chain_nodes = chain ? cM : 0;
+    s->st.kkt_chain_sp = chain ? csp : 0;
     *out = s;
     return CFX_OK;
 }
@@ -3046,13 +3252,35 @@ struct Run {
         s->st.eval_g_f++;
         return CFX_OK;
     }
+    // stage chain (IpmK::chain): the block cyclic reduction of [D | L | U] in ab; solves of nrhs right-hand sides at
+    // R + b r_inst + c r_rhs (the chain part, nA entries, of rb-shaped or Xb arrays)
+    int chain_factor() {
+        const IpmK& K = s->K;
+        const int64_t nb = (int64_t)K.cM * K.csp * K.csp;
+        return cfx_chain_factor_s(K.B, K.cM, K.csp, K.ab, K.ab + nb, K.ab + 2 * nb, K.NE_A, K.cw, K.cw + nb, 2 * nb,
+                                  K.info, st);
+    }
+    int chain_solve(double* R, int64_t r_inst, int64_t r_rhs, int nrhs) {
+        const IpmK& K = s->K;
+        const int64_t nb = (int64_t)K.cM * K.csp * K.csp;
+        return cfx_chain_solve_s(K.B, K.cM, K.csp, K.ab, K.ab + nb, K.ab + 2 * nb, K.NE_A, K.cw, K.cw + nb, 2 * nb,
+                                 nrhs, R, r_inst, r_rhs, K.ct, (int64_t)nrhs * K.nA, K.nA, st);
+    }
     int kkt_factor(int mode) {
         const IpmK& K = s->K;
         const int64_t nblk = (std::max<int64_t>(K.NE_tot, K.nK) + kIB - 1) / kIB;
         hipLaunchKernelGGL(k_ipm_kkt, dim3((unsigned)K.B, (unsigned)std::min<int64_t>(nblk, kMaxY)), dim3(kIB), 0, st,
                            K, mode);
         IPM_HIP(s, hipGetLastError());
-        if (K.np) {  // blocks + border: factor the blocks, A_q^-1 [Cr_q | r_q] (parallel right-hand sides), Schur
+        if (K.chain) {  // stage chain: block cyclic reduction, then (border) A^-1 [Cr | r] and the Schur complement
+            IPM_BAND(s, chain_factor());
+            if (K.np) IPM_BAND(s, chain_solve(K.Xb, (int64_t)K.na * K.nA, K.nA, K.na));
+            IPM_BAND(s, chain_solve(K.rb, K.nKp, 0, 1));
+            if (K.np) {
+                hipLaunchKernelGGL(k_ipm_schur, g, dim3(kIB), 0, st, K, 1);
+                IPM_HIP(s, hipGetLastError());
+            }
+        } else if (K.np) {  // blocks + border: factor the blocks, A_q^-1 [Cr_q | r_q] (parallel right-hand sides), Schur
             const int64_t BP = K.B * K.P, nb = (int64_t)K.na * K.nA;
             IPM_BAND(s, cfx_band_lu(K.nA, K.kl, K.ku, BP, K.ab, K.ipiv, K.info, 0, nullptr, st));
             IPM_BAND(s, cfx_band_solve_multi(K.nA, K.kl, K.ku, BP, K.P, K.ab, K.ipiv, K.Xb, K.P * nb, nb, K.nA, K.na,
@@ -3070,7 +3298,13 @@ struct Run {
     int resolve(double* into = nullptr) {
         IpmK K = s->K;
         if (into) K.rb = into;
-        if (K.np) {
+        if (K.chain) {
+            IPM_BAND(s, chain_solve(K.rb, K.nKp, 0, 1));
+            if (K.np) {
+                hipLaunchKernelGGL(k_ipm_schur, g, dim3(kIB), 0, st, K, 0);
+                IPM_HIP(s, hipGetLastError());
+            }
+        } else if (K.np) {
             IPM_BAND(s, cfx_band_solve_multi(K.nA, K.kl, K.ku, K.B * K.P, K.P, K.ab, K.ipiv, nullptr, 0, 0, 0, 0,
                                              K.rb, K.nKp, K.nA, st));
             hipLaunchKernelGGL(k_ipm_schur, g, dim3(kIB), 0, st, K, 0);
@@ -3139,10 +3373,14 @@ static int ipm_solve(cfx_ipm* s, const double* v0, const double* fixed_values, d
         IPM_HIP(s, hipMemcpyAsync(s->d_fv, fixed_values, B * K.nfix * sizeof(double), kin, st));
     hipLaunchKernelGGL(k_ipm_fix, R.g, blk, 0, st, K, (const double*)(fixed_values && K.nfix ? s->d_fv : nullptr));
     IPM_RUN(R.eval_full(K.vx));
-    hipLaunchKernelGGL(k_ipm_init, R.g, blk, 0, st, K);
+    const bool warm = K.o.warm_start_init_point != 0;
+    if (warm && !s->warm_set)
+        return ipm_fail(s, CFX_EINVAL, "cfx_ipm_solve: warm_start_init_point needs cfx_ipm_set_warm_start first");
+    hipLaunchKernelGGL(k_ipm_init, R.g, blk, 0, st, K, warm ? (const double*)s->d_wy : nullptr,
+                       warm ? (const double*)s->d_wzl : nullptr, warm ? (const double*)s->d_wzu : nullptr);
     IPM_HIP(s, hipGetLastError());
     IPM_HIP(s, hipMemcpyAsync(K.vt, K.vx, B * K.n * sizeof(double), hipMemcpyDeviceToDevice, st));
-    bool reinit = K.m > 0, wall_stop = false;
+    bool reinit = K.m > 0 && !warm, wall_stop = false;
     int32_t c[4];
     int n_active = (int)B, n_resto = 0;
     double last_print = 0.0;
@@ -3297,7 +3535,7 @@ static int ipm_solve(cfx_ipm* s, const double* v0, const double* fixed_values, d
         s->st.iterations++;
     }
     if (K.rsphase) hipLaunchKernelGGL(k_rs_finish, R.g, blk, 0, st, K);
-    hipLaunchKernelGGL(k_ipm_final, R.g, blk, 0, st, K);
+    hipLaunchKernelGGL(k_ipm_final, R.g, blk, 0, st, K, s->d_zlo, s->d_zuo);
     IPM_RUN(ipm_eval_all(s, K.vx, K.graw, nullptr, K.fraw, nullptr, CFX_DEVICE));
     s->st.eval_g_f++;
     hipLaunchKernelGGL(k_ipm_out, R.g, blk, 0, st, K, devp ? y_out : (y_out ? s->d_yo : nullptr),
@@ -3329,6 +3567,38 @@ extern "C" int cfx_ipm_solve(cfx_ipm* s, const double* v0, const double* fixed_v
     if (!s) return CFX_EINVAL;
     if (!v0) return ipm_fail(s, CFX_EINVAL, "cfx_ipm_solve: v0 is NULL");
     return ipm_solve(s, v0, fixed_values, v, y, f, converged, iterations, kkt_error, flags);
+}
+
+extern "C" int cfx_ipm_set_warm_start(cfx_ipm* s, const double* y, const double* z_l, const double* z_u,
+                                      uint32_t flags) {
+    if (!s) return CFX_EINVAL;
+    if ((s->K.m && !y) || !z_l || !z_u) return ipm_fail(s, CFX_EINVAL, "cfx_ipm_set_warm_start: NULL input");
+    IPM_HIP(s, hipSetDevice(s->device));
+    int rc = CFX_OK;
+    const size_t B = (size_t)s->K.B;
+    if (!s->d_wy) {
+        s->d_wy = dalloc<double>(s, B * s->K.m, &rc);
+        s->d_wzl = dalloc<double>(s, B * s->K.n, &rc);
+        s->d_wzu = dalloc<double>(s, B * s->K.n, &rc);
+        if (rc != CFX_OK) return rc;
+    }
+    const hipMemcpyKind k = (flags & CFX_DEVICE) ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
+    if (s->K.m) IPM_HIP(s, hipMemcpy(s->d_wy, y, B * s->K.m * sizeof(double), k));
+    IPM_HIP(s, hipMemcpy(s->d_wzl, z_l, B * s->K.n * sizeof(double), k));
+    IPM_HIP(s, hipMemcpy(s->d_wzu, z_u, B * s->K.n * sizeof(double), k));
+    s->warm_set = true;
+    return CFX_OK;
+}
+
+extern "C" int cfx_ipm_get_bound_multipliers(cfx_ipm* s, double* z_l, double* z_u, uint32_t flags) {
+    if (!s || !z_l || !z_u) return CFX_EINVAL;
+    IPM_HIP(s, hipSetDevice(s->device));
+    const size_t bytes = (size_t)s->K.B * s->K.n * sizeof(double);
+    const hipMemcpyKind k = (flags & CFX_DEVICE) ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
+    if (s->stream) IPM_HIP(s, hipStreamSynchronize(s->stream));
+    IPM_HIP(s, hipMemcpy(z_l, s->d_zlo, bytes, k));
+    IPM_HIP(s, hipMemcpy(z_u, s->d_zuo, bytes, k));
+    return CFX_OK;
 }
 
 extern "C" int cfx_ipm_get_status(const cfx_ipm* s, int32_t* status) {

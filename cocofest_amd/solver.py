@@ -95,6 +95,17 @@ class IpmOptions:
     acceptable_constr_viol_tol: float = 1e-2
     acceptable_dual_inf_tol: float = 1e10
     acceptable_compl_inf_tol: float = 1e-2
+    # Ipopt's honor_original_bounds (3.14's default "no"): with bound_relax_factor > 0, True moves the returned point
+    # into the original bounds, False returns the iterate as it is (the reference's stored reaching-task widths sit
+    # 1e-8 outside their bounds: its Ipopt returned the iterate)
+    honor_original_bounds: bool = False
+    # Ipopt's warm start (NativeIpm: solve(..., warm_start=(y, z_l, z_u))): no least-squares multipliers; x pushed from
+    # its bounds by warm_start_bound_push max(1, |bound|) (at most warm_start_bound_frac of the range), bound
+    # multipliers raised to warm_start_mult_bound_push; mu starts at mu_init
+    warm_start_init_point: bool = False
+    warm_start_bound_push: float = 1e-3
+    warm_start_bound_frac: float = 1e-3
+    warm_start_mult_bound_push: float = 1e-3
     verbose: bool = False
 
     def __post_init__(self):
@@ -791,7 +802,8 @@ class BatchedIpm:
                 zl, zu = torch.where(c, wd["zl"], zl), torch.where(c, wd["zu"], zu)
                 mu = torch.where(wd_back, wd["mu"], mu)
             iters = iters + step.long()
-        x = torch.minimum(torch.maximum(x, self.lbF0), self.ubF0)  # inf bounds leave x as is
+        if opt.honor_original_bounds:
+            x = torch.minimum(torch.maximum(x, self.lbF0), self.ubF0)  # inf bounds leave x as is
         vfinal = full(x)
         g, f = self._eval_gf(vfinal)
         y = y * self.sg / self.sf[:, None]  # multipliers of the unscaled problem
@@ -1206,7 +1218,8 @@ _NATIVE_OPTIONS = ("tol", "max_iter", "acceptable_tol", "acceptable_iter", "mu_i
                    "required_infeasibility_reduction", "filter_reset_trigger", "max_filter_resets", "max_wall_time",
                    "print_frequency_time", "soft_resto_pderror_reduction_factor", "max_soft_resto_iters",
                    "resto_failure_restart", "constr_viol_tol", "dual_inf_tol", "compl_inf_tol",
-                   "acceptable_constr_viol_tol", "acceptable_dual_inf_tol", "acceptable_compl_inf_tol")
+                   "acceptable_constr_viol_tol", "acceptable_dual_inf_tol", "acceptable_compl_inf_tol",
+                   "warm_start_bound_push", "warm_start_bound_frac", "warm_start_mult_bound_push")
 _HESSIAN_APPROXIMATION = {"exact": 0, "limited-memory": 1}
 _RESTORATION = {"step": 0, "phase": 1, None: 1}
 
@@ -1234,14 +1247,23 @@ class NativeIpm:
         self.ipm = _cfx.Ipm(self.h, lb, ub, int(getattr(ocp, "n_params", 0) or 0),
                             {**{k: getattr(self.opt, k) for k in _NATIVE_OPTIONS},
                              "hessian_approximation": _HESSIAN_APPROXIMATION[self.opt.hessian_approximation],
-                             "restoration": _RESTORATION[self.opt.restoration]})
+                             "restoration": _RESTORATION[self.opt.restoration],
+                             "warm_start_init_point": int(self.opt.warm_start_init_point),
+                             "honor_original_bounds": int(self.opt.honor_original_bounds)})
         self.calls = {"eval_all": 0, "eval_h": 0, "eval_g_f": 0, "kkt_factor": 0}
 
-    def solve(self, v0=None, fixed_values=None):
+    def solve(self, v0=None, fixed_values=None, warm_start=None):
+        """``warm_start``: (y, z_l, z_u) multipliers of the unscaled problem ((B, ng), (B, nv), (B, nv)) for a solve
+        with ``warm_start_init_point``; ``last_bound_multipliers`` holds the solve's (z_l, z_u) afterwards."""
         t0 = time.perf_counter()
         if v0 is None:
             v0 = np.tile(self.ocp.initial_guess_vector(), (self.B, 1))
+        if warm_start is not None:
+            self.ipm.set_warm_start(*warm_start)
+        elif self.opt.warm_start_init_point:
+            raise ValueError("NativeIpm.solve: warm_start_init_point needs warm_start=(y, z_l, z_u)")
         v, y, f, conv, its, kkt = self.ipm.solve(v0, fixed_values)
+        self.last_bound_multipliers = self.ipm.bound_multipliers()
         wall = time.perf_counter() - t0
         st = self.ipm.stats()
         self.calls = {k: int(st[k]) for k in ("eval_all", "eval_h", "eval_g_f", "kkt_factor")}

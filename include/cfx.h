@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define CFX_ABI_VERSION 8
+#define CFX_ABI_VERSION 9
 
 /* return codes */
 #define CFX_OK 0
@@ -316,6 +316,22 @@ int cfx_band_lu(int64_t n, int32_t kl, int32_t ku, int64_t batch, double *ab, in
 int cfx_band_lu_solve(int64_t n, int32_t kl, int32_t ku, int64_t batch, const double *ab, const int32_t *ipiv,
                       int32_t nrhs, double *rhs, void *hip_stream);
 
+/* ---- block-tridiagonal (stage chain) systems: block cyclic reduction ----------------------------------------
+   The interior point's KKT matrix of ONE large OCP grouped by stage (cfx_ipm: the free variables of node k and the
+   constraint rows arriving at it) is block tridiagonal; its sequential band factorisation (above) leaves the chip
+   idle, so cfx_ipm factors it by block cyclic reduction instead (MUMPS' role in Ipopt for
+   reaching_task_pulse_duration_optimization.py:117 of the reference).  B independent systems of M diagonal blocks,
+   sp x sp each (sp a multiple of 16, <= 128), row-major, device pointers:
+     D [B][M][sp][sp] diagonal blocks, L [B][M][sp][sp] blocks (k, k-1) (L[.][0] unused), U [B][M][sp][sp] blocks
+     (k, k+1) (U[.][M-1] unused), work [2][B][M][sp][sp];  info [B]: 0, or the 1-based unknown of a zero pivot
+   cfx_btri_factor overwrites D / L / U with the factors (no pivoting across blocks: each pivot block is inverted with
+   partial pivoting, so the systems must have nonsingular pivot blocks, as the KKT matrices cfx_ipm groups do);
+   cfx_btri_solve solves rhs [B][nrhs][M sp] in place (scratch: same shape).  On `hip_stream`. */
+int cfx_btri_factor(int64_t batch, int32_t M, int32_t sp, double *D, double *L, double *U, double *work,
+                    int32_t *info, void *hip_stream);
+int cfx_btri_solve(int64_t batch, int32_t M, int32_t sp, const double *D, const double *L, const double *U,
+                   const double *work, int32_t nrhs, double *rhs, double *scratch, void *hip_stream);
+
 /* ---- batched interior-point solver ---------------------------------------------------------------
    Replaces the solver role of `ocp.solve(Solver.IPOPT(...))` (bioptim's Ipopt interface; called e.g. at
    examples/getting_started/frequency_optimization.py:22 and examples/getting_started/pulse_duration_optimization.py:41
@@ -404,6 +420,16 @@ typedef struct cfx_ipm_options {
        point) needs the acceptable_* ones (0.01, 1e10, 0.01) */
     double constr_viol_tol, dual_inf_tol, compl_inf_tol;
     double acceptable_constr_viol_tol, acceptable_dual_inf_tol, acceptable_compl_inf_tol;
+    /* Ipopt's warm start (ABI 9): with warm_start_init_point (default 0) the solve starts from the multipliers given
+       by cfx_ipm_set_warm_start instead of least-squares multipliers and z = mu / s: x is pushed from its bounds by
+       warm_start_bound_push max(1, |bound|) capped at warm_start_bound_frac of the range (1e-3, 1e-3), the bound
+       multipliers are raised to at least warm_start_mult_bound_push (1e-3; scaled problem), the barrier starts at
+       mu_init */
+    double warm_start_bound_push, warm_start_bound_frac, warm_start_mult_bound_push;
+    int32_t warm_start_init_point;
+    /* Ipopt's honor_original_bounds (ABI 9; default 0, Ipopt 3.14's): 1 moves the returned point into the original
+       bounds when bound_relax_factor relaxed them; 0 returns the iterate as it is (within the relaxed bounds) */
+    int32_t honor_original_bounds;
 } cfx_ipm_options;
 #define CFX_HESSIAN_EXACT 0
 #define CFX_HESSIAN_LIMITED_MEMORY 1
@@ -427,6 +453,8 @@ typedef struct cfx_ipm_stats {
     int64_t kkt_blocks; /* band blocks factored side by side (nested dissection of the stage chain; 1: none) */
     int64_t resto_phases, resto_iterations; /* restoration phases entered / their iterations, summed over the instances */
     int64_t soft_steps;                     /* soft-restoration steps taken, summed over the instances */
+    /* stage-chain KKT layout (ABI 9; cfx_btri_*): nodes and their padded size (0: a band layout above) */
+    int64_t kkt_chain_nodes, kkt_chain_sp;
 } cfx_ipm_stats;
 
 typedef struct cfx_ipm cfx_ipm;
@@ -441,6 +469,13 @@ int cfx_ipm_create(cfx_handle *h, const double *lb, const double *ub, int32_t n_
    outputs are written asynchronously on the handle's stream; otherwise host pointers. */
 int cfx_ipm_solve(cfx_ipm *s, const double *v0, const double *fixed_values, double *v, double *y, double *f,
                   int32_t *converged, int32_t *iterations, double *kkt_error, uint32_t flags);
+/* Ipopt's warm_start_init_point inputs (ABI 9) for the following cfx_ipm_solve calls with the option set: y [B][ng]
+   constraint multipliers and z_l, z_u [B][nv] bound multipliers of the UNSCALED problem, Ipopt's sign convention
+   (grad f + J^T y - z_l + z_u = 0, z >= 0; entries of fixed variables and of missing bounds are ignored).  Host
+   pointers, or device pointers with CFX_DEVICE; copied.  cfx_ipm_get_bound_multipliers returns the last solve's
+   z_l, z_u [B][nv] in that form (0 at fixed variables). */
+int cfx_ipm_set_warm_start(cfx_ipm *s, const double *y, const double *z_l, const double *z_u, uint32_t flags);
+int cfx_ipm_get_bound_multipliers(cfx_ipm *s, double *z_l, double *z_u, uint32_t flags);
 /* The same solver over callbacks the caller provides instead of a libcfx handle — e.g. one OCP's intervals sharded
    over several GPUs, each rank evaluating its slice and all-gathering the value slices (cocofest_amd/distributed.py,
    the interval sharding of SURVEY.md section 8(e)).  The NLP is described by its sizes and fixed triplet structures
