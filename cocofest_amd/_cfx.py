@@ -122,7 +122,8 @@ class IpmOptions(C.Structure):
                 ("acceptable_constr_viol_tol", C.c_double), ("acceptable_dual_inf_tol", C.c_double),
                 ("acceptable_compl_inf_tol", C.c_double), ("warm_start_bound_push", C.c_double),
                 ("warm_start_bound_frac", C.c_double), ("warm_start_mult_bound_push", C.c_double),
-                ("warm_start_init_point", C.c_int32), ("honor_original_bounds", C.c_int32)]
+                ("warm_start_init_point", C.c_int32), ("honor_original_bounds", C.c_int32),
+                ("range_scaling", C.c_int32)]
 
 
 # cfx_ipm_get_status values (Ipopt's ApplicationReturnStatus)

@@ -80,9 +80,15 @@ constexpr int kNT = 256;  // threads per workgroup (4 waves)
 // i - h exists), U_i <- D_i^-1 U_i (when node i + h exists).  A zero pivot sets info[b] (0-based slot + 1) if unset.
 template <int SP>
 __global__ void __launch_bounds__(kNT) k_chain_elim(Chain C, int first, int step, int h, int32_t* __restrict__ info) {
+    // In-place Gauss-Jordan with partial pivoting (first largest |A(r, k)|, r >= k; columns unscrambled at the end),
+    // the matrix in registers: thread t owns row t % SP and the columns cg + G c (cg = t / SP, G = kNT / SP groups).
+    // Per pivot column three barriers: the column (double-buffered, written by its owners at the end of the previous
+    // step) -> wave 0's argmax -> the pivot row and row k through LDS -> every thread updates its own entries.
+    constexpr int G = kNT / SP, CW = (SP + G - 1) / G, SPP = G * CW;  // SPP: columns padded to the groups
     __shared__ double A[SP][SP + 1];
-    __shared__ double col[SP];
-    __shared__ int piv[SP];
+    __shared__ double colv[2][SP];
+    __shared__ double rowp[SPP], rowk[SPP];
+    __shared__ int piv[SP], perm[SP];
     __shared__ int s_p;
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
     const int i = first + step * blockIdx.x;
@@ -90,58 +96,106 @@ __global__ void __launch_bounds__(kNT) k_chain_elim(Chain C, int first, int step
     if (i >= C.M) return;
     constexpr int64_t NB = (int64_t)SP * SP;
     double* D = C.D + b * C.stride + i * NB;
-    for (int e = t; e < SP * SP; e += kNT) A[e / SP][e % SP] = D[e];
+    const int row = t % SP, cg = min(t / SP, G - 1);
+    const bool own = t < G * SP;  // threads past G SP groups own nothing (they shadow the last group, never store)
+    double a[CW];
+#pragma unroll
+    for (int c = 0; c < CW; ++c) {
+        const int j = cg + G * c;
+        a[c] = j < SP ? D[(int64_t)row * SP + j] : 0.0;
+    }
+    if (own && cg == 0) colv[0][row] = a[0];                           // column 0
+    for (int j = SP + t; j < SPP; j += kNT) rowp[j] = rowk[j] = 0.0;  // padding columns stay zero
     __syncthreads();
     int sing = 0;
-    // in-place Gauss-Jordan with partial pivoting (first largest |A(r, k)|, r >= k), columns unscrambled at the end
-    for (int k = 0; k < SP; ++k) {
-        if (wave == 0) {
-            double av = -1.0;
-            int ai = SP;
-            for (int r = k + lane; r < SP; r += 64) {
-                const double v = fabs(A[r][k]);
-                if (v > av) av = v, ai = r;
-            }
+    {
+#pragma unroll 1
+        for (int k = 0; k < SP; ++k) {
+            const int par = k & 1;
+            if (wave == 0) {
+                double av = -1.0;
+                int ai = SP;
+                for (int r = k + lane; r < SP; r += 64) {
+                    const double v = fabs(colv[par][r]);
+                    if (v > av) av = v, ai = r;
+                }
 #pragma unroll
-            for (int o = 32; o > 0; o >>= 1) {
-                const double ov = __shfl_xor(av, o);
-                const int oi = __shfl_xor(ai, o);
-                if (ov > av || (ov == av && oi < ai)) av = ov, ai = oi;
+                for (int o = 32; o > 0; o >>= 1) {
+                    const double ov = __shfl_xor(av, o);
+                    const int oi = __shfl_xor(ai, o);
+                    if (ov > av || (ov == av && oi < ai)) av = ov, ai = oi;
+                }
+                if (lane == 0) s_p = piv[k] = ai;
             }
-            if (lane == 0) s_p = piv[k] = ai;
+            __syncthreads();
+            const int p = s_p;
+            if (own && (row == p || row == k)) {
+                double* dst = row == p ? rowp : rowk;
+#pragma unroll
+                for (int c = 0; c < CW; ++c) dst[cg + G * c] = a[c];
+            }
+            __syncthreads();
+            const double pv = colv[par][p];
+            if (pv == 0.0 && !sing) sing = k + 1;
+            const double inv = pv != 0.0 ? 1.0 / pv : 0.0;
+            // row p now holds the old row k (its column-k value colv[k]); row k the scaled pivot row.  Branch-free:
+            // all LDS reads first, then selects
+            const bool isk = row == k, isp = row == p && p != k;
+            const double f = colv[par][isp ? k : row];
+            double pr[CW], rk[CW];
+#pragma unroll
+            for (int c = 0; c < CW; ++c) pr[c] = rowp[cg + G * c];
+#pragma unroll
+            for (int c = 0; c < CW; ++c) rk[c] = rowk[cg + G * c];
+            const int kn = k + 1;
+            double nxt = 0.0;
+#pragma unroll
+            for (int c = 0; c < CW; ++c) {
+                const int j = cg + G * c;
+                const double prc = (j == k ? 1.0 : pr[c]) * inv;
+                const double src = isp ? rk[c] : a[c];
+                const double upd = (j == k ? 0.0 : src) - f * prc;
+                a[c] = isk ? prc : upd;
+                nxt = (j == kn) ? a[c] : nxt;
+            }
+            // the next pivot column, by its owners, into the other buffer
+            if (own && kn < SP && cg == kn % G) colv[par ^ 1][row] = nxt;
+            __syncthreads();
         }
-        __syncthreads();
-        const int p = s_p;
-        if (p != k)
-            for (int j = t; j < SP; j += kNT) {
-                const double s = A[k][j];
-                A[k][j] = A[p][j];
-                A[p][j] = s;
-            }
-        __syncthreads();
-        for (int r = t; r < SP; r += kNT) col[r] = A[r][k];
-        __syncthreads();
-        const double pv = col[k];
-        if (pv == 0.0 && !sing) sing = k + 1;
-        const double inv = pv != 0.0 ? 1.0 / pv : 0.0;
-        for (int j = t; j < SP; j += kNT) A[k][j] = (j == k ? 1.0 : A[k][j]) * inv;
-        __syncthreads();
-        for (int e = t; e < SP * SP; e += kNT) {
-            const int r = e / SP, j = e - (e / SP) * SP;
-            if (r != k) A[r][j] = (j == k ? 0.0 : A[r][j]) - col[r] * A[k][j];
+    }
+    // columns: final column j is the eliminated matrix's column perm[j] (the interchanges undone in reverse order)
+    if (t == 0) {
+        for (int j = 0; j < SP; ++j) perm[j] = j;
+        for (int k = SP - 1; k >= 0; --k) {
+            const int q = piv[k], tmp = perm[k];
+            perm[k] = perm[q];
+            perm[q] = tmp;
         }
-        __syncthreads();
     }
-    for (int k = SP - 1; k >= 0; --k) {
-        const int p = piv[k];
-        if (p != k)
-            for (int r = t; r < SP; r += kNT) {
-                const double s = A[r][k];
-                A[r][k] = A[r][p];
-                A[r][p] = s;
-            }
-        __syncthreads();
+    if (own) {
+#pragma unroll
+        for (int c = 0; c < CW; ++c) {
+            const int j = cg + G * c;
+            if (j < SP) A[row][j] = a[c];
+        }
     }
+    __syncthreads();
+    if (own) {
+#pragma unroll
+        for (int c = 0; c < CW; ++c) {
+            const int j = cg + G * c;
+            if (j < SP) a[c] = A[row][perm[j]];
+        }
+    }
+    __syncthreads();
+    if (own) {
+#pragma unroll
+        for (int c = 0; c < CW; ++c) {
+            const int j = cg + G * c;
+            if (j < SP) A[row][j] = a[c];
+        }
+    }
+    __syncthreads();
     if (t == 0 && sing && info && info[b] == 0) info[b] = (int32_t)(i * SP + sing);
     for (int e = t; e < SP * SP; e += kNT) D[e] = A[e / SP][e % SP];
     // X_i = D_i^-1 L_i, Y_i = D_i^-1 U_i in place: a wave owns whole column blocks J (read into registers first)

@@ -42,6 +42,7 @@ constexpr int kFilt = 64;   // filter entries per instance (a ring, as solver.py
 constexpr int kSlots = 64;  // counter ring: one 4-int slot per host read
 constexpr int kMaxY = 65535;
 constexpr int kMaxBorder = 32;  // free parameters handled as a dense border
+constexpr int kWideParts = 128;  // blocks per instance of the wide-instance reductions (IpmK::wide)
 
 // per-instance scalars of the iteration
 struct Scal {
@@ -97,6 +98,12 @@ struct IpmK {
     // ([B][2][cM][csp][csp]), ct its solve scratch ([B][max(na, 1)][nA]); a border (np > 0) as below.
     int chain, cM, csp;
     double *cw, *ct;
+    // Wide instances (wide = 1: small batches of large NLPs, e.g. the reaching task's 2.4 M J_g values in one instance):
+    // the gather loops of k_ipm_begin (J_g scaling, J^T y), k_ipm_curv (unpacking, x^T W x) and the border's back
+    // substitution run as grids of many blocks per instance (k_wide_*) instead of one block's serial loop; gj [B][nf]
+    // holds grad f + J^T y, part [B][kWideParts][2] the per-block partial sums, reduced in a fixed order
+    int wide;
+    double *gj, *part;
     // KKT layout.  P = 1, np = 0: one band of nA = nK unknowns (factor + solve in one launch).  Otherwise the
     // unknowns split into P diagonal band blocks of nA rows each (padded with unit rows) and a dense border of np
     // unknowns — Hmed intensity parameters, whose sliding windows couple most stages, and the separators between
@@ -430,11 +437,13 @@ __global__ void __launch_bounds__(kIB) k_ipm_begin(const IpmK K, int mode, int s
     if (mode & 1) {
         const double* sg = K.sg + b * m;
         const double* jac = K.jac + b * K.nnzj;
-        for (int j = threadIdx.x; j < m; j += kIB) gS[j] = K.graw[b * m + j] * sg[j];
-        // (unrolled: several gathers in flight per thread — one instance of ~10^6 J_g entries is one block's loop)
+        if (!K.wide) {  // (wide: k_wide_scale did these)
+            for (int j = threadIdx.x; j < m; j += kIB) gS[j] = K.graw[b * m + j] * sg[j];
+            // (unrolled: several gathers in flight per thread — one instance of ~10^6 J_g entries is one block's loop)
 #pragma unroll 8
-        for (int s = threadIdx.x; s < K.nj; s += kIB) jv[s] = jac[K.jsel[s]] * K.d[K.jc[s]] * sg[K.jr[s]];
-        for (int i = threadIdx.x; i < nf; i += kIB) gF[i] = K.grad[b * K.n + K.free[i]] * K.d[i] * S.sf;
+            for (int s = threadIdx.x; s < K.nj; s += kIB) jv[s] = jac[K.jsel[s]] * K.d[K.jc[s]] * sg[K.jr[s]];
+            for (int i = threadIdx.x; i < nf; i += kIB) gF[i] = K.grad[b * K.n + K.free[i]] * K.d[i] * S.sf;
+        }
         if (threadIdx.x == 0) S.fS = K.fraw[b] * S.sf;
         __syncthreads();
         if (mode & 2) {
@@ -452,13 +461,18 @@ __global__ void __launch_bounds__(kIB) k_ipm_begin(const IpmK K, int mode, int s
     double szl = 0, szu = 0, sy = 0, ed = 0, ep = 0, ecl = 0, ecu = 0, edu = 0, epu = 0;
     const double* sg = K.sg + b * m;
     for (int i = threadIdx.x; i < nf; i += kIB) {
-        double jty = 0.0;
+        double gj;
+        if (K.wide) {  // k_wide_jty, the same sum in the same order
+            gj = K.gj[b * nf + i];
+        } else {
+            double jty = 0.0;
 #pragma unroll 4
-        for (int k = K.jt_ptr[i]; k < K.jt_ptr[i + 1]; ++k) {
-            const int s = K.jt_idx[k];
-            jty += jv[s] * y[K.jr[s]];
+            for (int k = K.jt_ptr[i]; k < K.jt_ptr[i + 1]; ++k) {
+                const int s = K.jt_idx[k];
+                jty += jv[s] * y[K.jr[s]];
+            }
+            gj = gF[i] + jty;
         }
-        const double gj = gF[i] + jty;
         rhs[i] = gj;  // completed below, once mu is final
         const double rd = gj - zl[i] + zu[i];
         szl += fabs(zl[i]);
@@ -633,7 +647,7 @@ constexpr int kSchurStage = 2048;  // Cc non-zeros / active-slot entries staged 
 // ungathered loop, so the results are bit-identical to it (the interior point's trajectories are sensitive to rounding)
 constexpr int kSchurProd = 1536;
 
-__global__ void __launch_bounds__(kIB) k_ipm_schur(const IpmK K, int factor) {
+__global__ void __launch_bounds__(kIB) k_ipm_schur(const IpmK K, int factor, int back = 1) {
     __shared__ double S[kMaxBorder][kMaxBorder + 1];
     __shared__ double sv[kMaxBorder];
     __shared__ int piv[kMaxBorder];
@@ -757,6 +771,10 @@ __global__ void __launch_bounds__(kIB) k_ipm_schur(const IpmK K, int factor) {
         if (t < np) sv[t] = x;
     }
     __syncthreads();
+    if (!back) {  // k_wide_border_back does the blocks
+        for (int c = t; c < np; c += kIB) rb[PA + c] = sv[c];
+        return;
+    }
     for (int e = t; e < PA; e += kIB) {
         const int q = e / nA, a = e - (e / nA) * nA;
         double acc = rb[e];
@@ -777,6 +795,112 @@ __global__ void __launch_bounds__(kIB) k_ipm_schur(const IpmK K, int factor) {
     for (int c = t; c < np; c += kIB) rb[PA + c] = sv[c];
 }
 
+
+// ---- wide instances (IpmK::wide): the long gather loops of one instance over a grid of blocks ----------------
+// grid (B, ceil(max(nj, m, nf) / kIB)): the scaled callback outputs of k_ipm_begin's mode bit 0 (gS, jv, gF)
+__global__ void __launch_bounds__(kIB) k_wide_scale(const IpmK K) {
+    const int64_t b = blockIdx.x;
+    if (K.sc[b].rs_on) return;
+    const int64_t p = (int64_t)blockIdx.y * kIB + threadIdx.x;
+    const int m = K.m, nf = K.nf;
+    const double* sg = K.sg + b * m;
+    if (p < K.nj) K.jv[b * K.nj + p] = K.jac[b * K.nnzj + K.jsel[p]] * K.d[K.jc[p]] * sg[K.jr[p]];
+    if (p < m) K.gS[b * m + p] = K.graw[b * m + p] * sg[p];
+    if (p < nf) K.gF[b * nf + p] = K.grad[b * K.n + K.free[p]] * K.d[p] * K.sc[b].sf;
+}
+
+// grid (B, ceil(nf / kIB)): gj = grad f + J^T y per free variable, k_ipm_begin's sum in its order
+__global__ void __launch_bounds__(kIB) k_wide_jty(const IpmK K) {
+    const int64_t b = blockIdx.x;
+    if (K.sc[b].rs_on) return;
+    const int i = blockIdx.y * kIB + threadIdx.x;
+    if (i >= K.nf) return;
+    const double* jv = K.jv + b * K.nj;
+    const double* y = K.y + b * K.m;
+    double jty = 0.0;
+#pragma unroll 4
+    for (int k = K.jt_ptr[i]; k < K.jt_ptr[i + 1]; ++k) {
+        const int s = K.jt_idx[k];
+        jty += jv[s] * y[K.jr[s]];
+    }
+    K.gj[b * K.nf + i] = K.gF[b * K.nf + i] + jty;
+}
+
+// grid (B, kWideParts): the Newton step in natural order (dx / dxr, dy) from rb, and a non-finite flag per block
+__global__ void __launch_bounds__(kIB) k_wide_unpack(const IpmK K) {
+    __shared__ double sh[kIB / 64];
+    const int64_t b = blockIdx.x;
+    const Scal& S = K.sc[b];
+    const bool rs = S.rs_on;
+    const bool active = rs ? S.rs_exit == RS_RUNNING : !S.done;
+    const int nf = K.nf;
+    const double* rb = K.rb + b * K.nKp;
+    double* dx = (rs ? K.dxr : K.dx) + b * nf;
+    double* dy = K.dy + b * K.m;
+    const int64_t per = (K.nK + kWideParts - 1) / kWideParts;
+    const int64_t lo = blockIdx.y * per, hi = std::min<int64_t>(K.nK, lo + per);
+    double nonfin = 0.0;
+    if (active || !rs)
+        for (int64_t i = lo + threadIdx.x; i < hi; i += kIB) {
+            const double r = rb[K.pos[i]];
+            if (!isfinite(r)) nonfin = 1.0;
+            if (i < nf)
+                dx[i] = r;
+            else
+                dy[i - nf] = r;
+        }
+    nonfin = breduce(nonfin, OpMax(), sh);
+    if (threadIdx.x == 0) K.part[(b * kWideParts + blockIdx.y) * 2 + 1] = nonfin;
+}
+
+// grid (B, kWideParts): partial sums of dx^T W dx over contiguous ranges of the Hessian entries
+__global__ void __launch_bounds__(kIB) k_wide_quad(const IpmK K) {
+    __shared__ double sh[kIB / 64];
+    const int64_t b = blockIdx.x;
+    const bool rs = K.sc[b].rs_on;
+    const double* dx = (rs ? K.dxr : K.dx) + b * K.nf;
+    const double* hv = K.hv + b * K.nnzh;
+    const int64_t per = (K.nh + kWideParts - 1) / kWideParts;
+    const int64_t lo = blockIdx.y * per, hi = std::min<int64_t>(K.nh, lo + per);
+    double quad = 0.0;
+#pragma unroll 8
+    for (int64_t s = lo + threadIdx.x; s < hi; s += kIB) {
+        const int r = K.hr[s], c = K.hc[s];
+        const double w = hv[K.hsel[s]] * K.d[r] * K.d[c];
+        quad += w * dx[r] * dx[c] * (K.hoff[s] ? 2.0 : 1.0);
+    }
+    quad = breduce(quad, OpSum(), sh);
+    if (threadIdx.x == 0) K.part[(b * kWideParts + blockIdx.y) * 2] = quad;
+}
+
+// grid (B, ceil(P nA / kIB)): the chain's back substitution of the border, x_A = y_A - (A^-1 Cr) x_p (k_ipm_schur's
+// last loop, same order per entry), after k_ipm_schur with back = 0 left x_p in rb's border slots
+__global__ void __launch_bounds__(kIB) k_wide_border_back(const IpmK K) {
+    const int64_t b = blockIdx.x;
+    const int64_t PA = (int64_t)K.P * K.nA;
+    const int64_t e = (int64_t)blockIdx.y * kIB + threadIdx.x;
+    if (e >= PA) return;
+    const int nA = K.nA, na = K.na, np = K.np;
+    const int64_t nb = (int64_t)na * nA;
+    const double* X = K.Xb + b * K.P * nb;
+    double* rb = K.rb + b * K.nKp;
+    const int q = (int)(e / nA), a = (int)(e - (int64_t)q * nA);
+    double acc = rb[e];
+    for (int c0 = 0; c0 < na; c0 += 4) {
+        double xv[4], sk[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int c = c0 + u, k = c < na ? K.act[q * na + c] : -1;
+            xv[u] = k >= 0 ? X[q * nb + (int64_t)c * nA + a] : 0.0;
+            sk[u] = k >= 0 ? rb[PA + k] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) acc -= xv[u] * sk[u];
+    }
+    rb[e] = acc;
+    (void)np;
+}
+
 // Newton step in natural order and the curvature test (solver.py inertia loop); bumps dw where it fails.  An instance
 // in the restoration phase takes the phase's step (its dx in dxr, its own dw, the proximity weights).  Counters: [0]
 // instances iterating, [1] of them with the wrong inertia, [2] of them in the restoration phase
@@ -791,24 +915,33 @@ __global__ void __launch_bounds__(kIB) k_ipm_curv(const IpmK K, int slot) {
     const double* rb = K.rb + b * K.nKp;
     double* dx = (rs ? K.dxr : K.dx) + b * nf;
     double* dy = K.dy + b * K.m;
-    double nonfin = 0.0;
-    if (active || !rs)
-        for (int i = threadIdx.x; i < K.nK; i += kIB) {
-            const double r = rb[K.pos[i]];
-            if (!isfinite(r)) nonfin = 1.0;
-            if (i < nf)
-                dx[i] = r;
-            else
-                dy[i - nf] = r;
+    double nonfin = 0.0, quad = 0.0;
+    if (K.wide) {  // k_wide_unpack / k_wide_quad: partial sums of the blocks, in block order
+        const double* pt = K.part + b * kWideParts * 2;
+        for (int q = 0; q < kWideParts; ++q) {
+            quad += pt[2 * q];
+            nonfin = max_n(nonfin, pt[2 * q + 1]);
         }
-    __syncthreads();
-    const double* hv = K.hv + b * K.nnzh;
-    double quad = 0.0;
+        quad /= kIB;  // every thread holds the full sum; the reduction below adds kIB copies
+        nonfin = threadIdx.x == 0 ? nonfin : 0.0;
+    } else {
+        if (active || !rs)
+            for (int i = threadIdx.x; i < K.nK; i += kIB) {
+                const double r = rb[K.pos[i]];
+                if (!isfinite(r)) nonfin = 1.0;
+                if (i < nf)
+                    dx[i] = r;
+                else
+                    dy[i - nf] = r;
+            }
+        __syncthreads();
+        const double* hv = K.hv + b * K.nnzh;
 #pragma unroll 8
-    for (int s = threadIdx.x; s < K.nh; s += kIB) {  // (sums in the same order; gathers in flight)
-        const int r = K.hr[s], c = K.hc[s];
-        const double w = hv[K.hsel[s]] * K.d[r] * K.d[c];
-        quad += w * dx[r] * dx[c] * (K.hoff[s] ? 2.0 : 1.0);
+        for (int s = threadIdx.x; s < K.nh; s += kIB) {  // (sums in the same order; gathers in flight)
+            const int r = K.hr[s], c = K.hc[s];
+            const double w = hv[K.hsel[s]] * K.d[r] * K.d[c];
+            quad += w * dx[r] * dx[c] * (K.hoff[s] ? 2.0 : 1.0);
+        }
     }
     const double* sig = K.sig + b * nf;
     double dd = 0.0, nrm = 0.0;
@@ -2352,6 +2485,7 @@ struct cfx_ipm {
     // warm start inputs (cfx_ipm_set_warm_start; allocated on first use) and the last solve's bound multipliers
     double *d_wy = nullptr, *d_wzl = nullptr, *d_wzu = nullptr, *d_zlo = nullptr, *d_zuo = nullptr;
     bool warm_set = false;
+    bool trace = false;  // CFX_IPM_TRACE=1: one stderr line per iteration (instance 0)
     int32_t *d_conv = nullptr, *d_its = nullptr, *d_status = nullptr;
     std::vector<int32_t> h_status;  // CFX_IPM_* status per instance of the last solve (cfx_ipm_get_status)
     // J_g's constant values (cfx_jac_constant_mask) stay in K.jac after the first full evaluation: later evaluations
@@ -2480,6 +2614,7 @@ extern "C" void cfx_ipm_default_options(cfx_ipm_options* o) {
     o->warm_start_mult_bound_push = 1e-3;
     o->warm_start_init_point = 0;
     o->honor_original_bounds = 0;  // Ipopt 3.14's default
+    o->range_scaling = 1;
 }
 
 // CSR of `key` (values in [0, nkeys)) with the sources of each key in increasing source order
@@ -2747,7 +2882,7 @@ static int ipm_create_common(cfx_ipm* s, const cfx_sizes& sz, int layout, const 
         hasL[i] = std::isfinite(l);
         hasU[i] = std::isfinite(u);
         const double w = u - l;
-        d[i] = (std::isfinite(w) && w < 1.0) ? w : 1.0;
+        d[i] = (K.o.range_scaling && std::isfinite(w) && w < 1.0) ? w : 1.0;
         lbF0[i] = l / d[i];
         ubF0[i] = u / d[i];
         lbF[i] = lbF0[i] - rel * clamp_lo(std::fabs(lbF0[i] * d[i]), 1.0) / d[i];
@@ -3120,6 +3255,10 @@ static int ipm_create_common(cfx_ipm* s, const cfx_sizes& sz, int layout, const 
     K.ft = dalloc<double>(s, B, &rc);
     K.of = dalloc<double>(s, B, &rc);
     K.ab = dalloc<double>(s, B * NE_A, &rc);
+    K.wide = s->B <= 16 && (int64_t)nj + nh >= 262144;
+    if (const char* e = std::getenv("CFX_IPM_WIDE")) K.wide = std::atoi(e) != 0;  // tuning / A-B override
+    K.gj = dalloc<double>(s, B * nf, &rc);
+    K.part = dalloc<double>(s, B * kWideParts * 2, &rc);
     K.chain = chain ? 1 : 0;
     K.cM = (int)cM;
     K.csp = (int)csp;
@@ -3181,6 +3320,7 @@ static int ipm_create_common(cfx_ipm* s, const cfx_sizes& sz, int layout, const 
     if (s->h_pub) std::memset(s->h_pub, 0, 16 * sizeof(int32_t));
     if (const char* e = std::getenv("CFX_IPM_SYNC")) s->poll = std::strcmp(e, "stream") != 0;
     if (const char* e = std::getenv("CFX_IPM_KEEPJ")) s->keepj = std::atoi(e) != 0;
+    if (const char* e = std::getenv("CFX_IPM_TRACE")) s->trace = std::atoi(e) != 0;
     if (rc == CFX_OK && hipHostMalloc((void**)&s->h_cnt, 4 * sizeof(int32_t), hipHostMallocDefault) != hipSuccess) {
         rc = CFX_ENOMEM;
         s->err = "hipHostMalloc failed";
@@ -3252,6 +3392,44 @@ struct Run {
         s->st.eval_g_f++;
         return CFX_OK;
     }
+    // Schur complement of the border; wide instances: its back substitution of the blocks as a grid
+    int schur(const IpmK& K, int factor) {
+        hipLaunchKernelGGL(k_ipm_schur, g, dim3(kIB), 0, st, K, factor, K.wide ? 0 : 1);
+        if (K.wide) {
+            const int64_t PA = (int64_t)K.P * K.nA;
+            hipLaunchKernelGGL(k_wide_border_back, dim3((unsigned)K.B, (unsigned)((PA + kIB - 1) / kIB)), dim3(kIB), 0,
+                               st, K);
+        }
+        IPM_HIP(s, hipGetLastError());
+        return CFX_OK;
+    }
+    // k_ipm_begin, after the wide-instance grids it reads (scaling when mode bit 0; J^T y unless it stops after the
+    // scaling, mode bit 1)
+    int begin(int mode, int slot) {
+        const IpmK& K = s->K;
+        if (K.wide) {
+            const int64_t n = std::max<int64_t>(std::max<int64_t>(K.nj, K.m), K.nf);
+            if (mode & 1)
+                hipLaunchKernelGGL(k_wide_scale, dim3((unsigned)K.B, (unsigned)((n + kIB - 1) / kIB)), dim3(kIB), 0,
+                                   st, K);
+            if (!(mode & 2))
+                hipLaunchKernelGGL(k_wide_jty, dim3((unsigned)K.B, (unsigned)((K.nf + kIB - 1) / kIB)), dim3(kIB), 0,
+                                   st, K);
+        }
+        hipLaunchKernelGGL(k_ipm_begin, g, dim3(kIB), 0, st, K, mode, slot);
+        IPM_HIP(s, hipGetLastError());
+        return CFX_OK;
+    }
+    int curv(int slot) {
+        const IpmK& K = s->K;
+        if (K.wide) {
+            hipLaunchKernelGGL(k_wide_unpack, dim3((unsigned)K.B, kWideParts), dim3(kIB), 0, st, K);
+            hipLaunchKernelGGL(k_wide_quad, dim3((unsigned)K.B, kWideParts), dim3(kIB), 0, st, K);
+        }
+        hipLaunchKernelGGL(k_ipm_curv, g, dim3(kIB), 0, st, K, slot);
+        IPM_HIP(s, hipGetLastError());
+        return CFX_OK;
+    }
     // stage chain (IpmK::chain): the block cyclic reduction of [D | L | U] in ab; solves of nrhs right-hand sides at
     // R + b r_inst + c r_rhs (the chain part, nA entries, of rb-shaped or Xb arrays)
     int chain_factor() {
@@ -3276,17 +3454,13 @@ struct Run {
             IPM_BAND(s, chain_factor());
             if (K.np) IPM_BAND(s, chain_solve(K.Xb, (int64_t)K.na * K.nA, K.nA, K.na));
             IPM_BAND(s, chain_solve(K.rb, K.nKp, 0, 1));
-            if (K.np) {
-                hipLaunchKernelGGL(k_ipm_schur, g, dim3(kIB), 0, st, K, 1);
-                IPM_HIP(s, hipGetLastError());
-            }
+            if (K.np) IPM_RUN(schur(K, 1));
         } else if (K.np) {  // blocks + border: factor the blocks, A_q^-1 [Cr_q | r_q] (parallel right-hand sides), Schur
             const int64_t BP = K.B * K.P, nb = (int64_t)K.na * K.nA;
             IPM_BAND(s, cfx_band_lu(K.nA, K.kl, K.ku, BP, K.ab, K.ipiv, K.info, 0, nullptr, st));
             IPM_BAND(s, cfx_band_solve_multi(K.nA, K.kl, K.ku, BP, K.P, K.ab, K.ipiv, K.Xb, K.P * nb, nb, K.nA, K.na,
                                              K.rb, K.nKp, K.nA, st));
-            hipLaunchKernelGGL(k_ipm_schur, g, dim3(kIB), 0, st, K, 1);
-            IPM_HIP(s, hipGetLastError());
+            IPM_RUN(schur(K, 1));
         } else {
             IPM_BAND(s, cfx_band_lu(K.nK, K.kl, K.ku, K.B, K.ab, K.ipiv, K.info, 1, K.rb, st));
         }
@@ -3300,15 +3474,11 @@ struct Run {
         if (into) K.rb = into;
         if (K.chain) {
             IPM_BAND(s, chain_solve(K.rb, K.nKp, 0, 1));
-            if (K.np) {
-                hipLaunchKernelGGL(k_ipm_schur, g, dim3(kIB), 0, st, K, 0);
-                IPM_HIP(s, hipGetLastError());
-            }
+            if (K.np) IPM_RUN(schur(K, 0));
         } else if (K.np) {
             IPM_BAND(s, cfx_band_solve_multi(K.nA, K.kl, K.ku, K.B * K.P, K.P, K.ab, K.ipiv, nullptr, 0, 0, 0, 0,
                                              K.rb, K.nKp, K.nA, st));
-            hipLaunchKernelGGL(k_ipm_schur, g, dim3(kIB), 0, st, K, 0);
-            IPM_HIP(s, hipGetLastError());
+            IPM_RUN(schur(K, 0));
         } else {
             IPM_BAND(s, cfx_band_lu_solve(K.nK, K.kl, K.ku, K.B, K.ab, K.ipiv, 1, K.rb, st));
         }
@@ -3397,6 +3567,16 @@ static int ipm_solve(cfx_ipm* s, const double* v0, const double* fixed_values, d
             wall_stop = true;
             break;
         }
+        if (s->trace && it > 0) {  // CFX_IPM_TRACE=1: instance 0's iterate every iteration (diagnostics)
+            Scal s0{};
+            IPM_HIP(s, hipMemcpyAsync(&s0, K.sc, sizeof(Scal), hipMemcpyDeviceToHost, st));
+            IPM_HIP(s, hipStreamSynchronize(st));
+            std::fprintf(stderr,
+                         "cfx_ipm trace %d: iters %d f %.10e err %.3e mu %.3e theta %.3e alpha %.3e a_z %.3e dw %.2e "
+                         "resto %d soft %d wd %d acc %d\n",
+                         it, s0.iters, s0.fS / s0.sf, s0.err0, s0.mu, s0.theta, s0.alpha, s0.a_z, s0.dwl, s0.rs_on,
+                         s0.soft_on, s0.wd_on, s0.acc);
+        }
         if (K.o.print_frequency_time > 0 && it > 0 && elapsed - last_print >= K.o.print_frequency_time) {
             Scal s0{};  // instance 0's optimality error, barrier, infeasibility and last step (one small read)
             IPM_HIP(s, hipMemcpyAsync(&s0, K.sc, sizeof(Scal), hipMemcpyDeviceToHost, st));
@@ -3421,12 +3601,12 @@ static int ipm_solve(cfx_ipm* s, const double* v0, const double* fixed_values, d
             IPM_RUN(R.eval_full(K.vx));
         }
         if (reinit) {  // least-squares multipliers for the flagged instances (start, after a restoration)
-            hipLaunchKernelGGL(k_ipm_begin, R.g, blk, 0, st, K, 3, 0);
+            IPM_RUN(R.begin(3, 0));
             IPM_RUN(R.kkt_factor(KKT_LSMULT));
             hipLaunchKernelGGL(k_ipm_lsmult, R.g, blk, 0, st, K);
-            hipLaunchKernelGGL(k_ipm_begin, R.g, blk, 0, st, K, 0, R.next_slot());
+            IPM_RUN(R.begin(0, R.next_slot()));
         } else {
-            hipLaunchKernelGGL(k_ipm_begin, R.g, blk, 0, st, K, 1, R.next_slot());
+            IPM_RUN(R.begin(1, R.next_slot()));
         }
         if (K.rsphase && rs_live) hipLaunchKernelGGL(k_rs_begin, R.g, blk, 0, st, K);
         reinit = false;
@@ -3445,7 +3625,7 @@ static int ipm_solve(cfx_ipm* s, const double* v0, const double* fixed_values, d
             IPM_RUN(R.kkt_factor(KKT_NEWTON));
             if (K.lbfgs) IPM_RUN(R.lbfgs_newton());
             const int sl = R.next_slot();
-            hipLaunchKernelGGL(k_ipm_curv, R.g, blk, 0, st, K, sl);
+            IPM_RUN(R.curv(sl));
             IPM_HIP(s, hipGetLastError());
             IPM_RUN(R.read(sl, c));
             if (attempt == 0) {

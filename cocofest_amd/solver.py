@@ -99,6 +99,9 @@ class IpmOptions:
     # into the original bounds, False returns the iterate as it is (the reference's stored reaching-task widths sit
     # 1e-8 outside their bounds: its Ipopt returned the iterate)
     honor_original_bounds: bool = False
+    # variable scaling by the bound range (x = d x~, d = ub - lb when below 1: pulse widths ~1e-4 s become O(1)); an
+    # extension — Ipopt scales only f and g (nlp_scaling_method gradient-based), which range_scaling=False reproduces
+    range_scaling: bool = True
     # Ipopt's warm start (NativeIpm: solve(..., warm_start=(y, z_l, z_u))): no least-squares multipliers; x pushed from
     # its bounds by warm_start_bound_push max(1, |bound|) (at most warm_start_bound_frac of the range), bound
     # multipliers raised to warm_start_mult_bound_push; mu starts at mu_init
@@ -288,7 +291,8 @@ class BatchedIpm:
         # Variable scaling (x = d * x~): variables whose bound range is below 1 (pulse widths ~1e-4 s, fatigue
         # time constants) are mapped to O(1); the iteration works in x~, bounds and derivatives follow.
         width = self.ubF - self.lbF
-        self.d = torch.where(torch.isfinite(width) & (width < 1.0), width, torch.ones_like(width))
+        self.d = torch.where(torch.isfinite(width) & (width < 1.0) & bool(self.opt.range_scaling), width,
+                             torch.ones_like(width))
         self.lbF, self.ubF = self.lbF / self.d, self.ubF / self.d
         # Ipopt's bound_relax_factor: the iteration sees the bounds relaxed by eps * max(1, |bound|) (in the user's
         # units, as Ipopt), meant for bounds the solution touches only asymptotically (a fatigue state a hair above
@@ -1249,7 +1253,8 @@ class NativeIpm:
                              "hessian_approximation": _HESSIAN_APPROXIMATION[self.opt.hessian_approximation],
                              "restoration": _RESTORATION[self.opt.restoration],
                              "warm_start_init_point": int(self.opt.warm_start_init_point),
-                             "honor_original_bounds": int(self.opt.honor_original_bounds)})
+                             "honor_original_bounds": int(self.opt.honor_original_bounds),
+                             "range_scaling": int(self.opt.range_scaling)})
         self.calls = {"eval_all": 0, "eval_h": 0, "eval_g_f": 0, "kkt_factor": 0}
 
     def solve(self, v0=None, fixed_values=None, warm_start=None):

@@ -430,6 +430,10 @@ typedef struct cfx_ipm_options {
     /* Ipopt's honor_original_bounds (ABI 9; default 0, Ipopt 3.14's): 1 moves the returned point into the original
        bounds when bound_relax_factor relaxed them; 0 returns the iterate as it is (within the relaxed bounds) */
     int32_t honor_original_bounds;
+    /* variable scaling by the bound range (ABI 9; default 1, an extension): variables whose range ub - lb is below 1
+       (pulse widths ~1e-4 s) are iterated as x / (ub - lb).  0: no variable scaling — Ipopt's behaviour (its
+       gradient-based nlp scaling scales f and g only), which changes the scaled termination test */
+    int32_t range_scaling;
 } cfx_ipm_options;
 #define CFX_HESSIAN_EXACT 0
 #define CFX_HESSIAN_LIMITED_MEMORY 1
