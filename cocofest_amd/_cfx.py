@@ -123,7 +123,8 @@ class IpmOptions(C.Structure):
                 ("acceptable_compl_inf_tol", C.c_double), ("warm_start_bound_push", C.c_double),
                 ("warm_start_bound_frac", C.c_double), ("warm_start_mult_bound_push", C.c_double),
                 ("warm_start_init_point", C.c_int32), ("honor_original_bounds", C.c_int32),
-                ("range_scaling", C.c_int32)]
+                ("range_scaling", C.c_int32), ("bound_mult_init_method", C.c_int32),
+                ("bound_mult_init_val", C.c_double)]
 
 
 # cfx_ipm_get_status values (Ipopt's ApplicationReturnStatus)

@@ -397,6 +397,9 @@ __global__ void __launch_bounds__(kIB) k_ipm_init(const IpmK K, const double* __
             const double zs = sf * K.d[i];
             K.zl[b * K.nf + i] = hL ? max_n(zs * wzl[e], K.o.warm_start_mult_bound_push) : 0.0;
             K.zu[b * K.nf + i] = hU ? max_n(zs * wzu[e], K.o.warm_start_mult_bound_push) : 0.0;
+        } else if (K.o.bound_mult_init_method == 0) {  // Ipopt's "constant"
+            K.zl[b * K.nf + i] = hL ? K.o.bound_mult_init_val : 0.0;
+            K.zu[b * K.nf + i] = hU ? K.o.bound_mult_init_val : 0.0;
         } else {
             K.zl[b * K.nf + i] = hL ? mu / sl : 0.0;
             K.zu[b * K.nf + i] = hU ? mu / su : 0.0;
@@ -2615,6 +2618,8 @@ extern "C" void cfx_ipm_default_options(cfx_ipm_options* o) {
     o->warm_start_init_point = 0;
     o->honor_original_bounds = 0;  // Ipopt 3.14's default
     o->range_scaling = 1;
+    o->bound_mult_init_method = 1;  // mu-based (Ipopt's default is constant, 1)
+    o->bound_mult_init_val = 1.0;
 }
 
 // CSR of `key` (values in [0, nkeys)) with the sources of each key in increasing source order
@@ -2852,7 +2857,8 @@ static int ipm_create_common(cfx_ipm* s, const cfx_sizes& sz, int layout, const 
         !(K.o.constr_viol_tol > 0) || !(K.o.dual_inf_tol > 0) || !(K.o.compl_inf_tol > 0) ||
         !(K.o.acceptable_constr_viol_tol > 0) || !(K.o.acceptable_dual_inf_tol > 0) ||
         !(K.o.acceptable_compl_inf_tol > 0) || !(K.o.warm_start_bound_push > 0) || !(K.o.warm_start_bound_frac > 0) ||
-        !(K.o.warm_start_bound_frac <= 0.5) || !(K.o.warm_start_mult_bound_push > 0)) {
+        !(K.o.warm_start_bound_frac <= 0.5) || !(K.o.warm_start_mult_bound_push > 0) ||
+        (K.o.bound_mult_init_method != 0 && K.o.bound_mult_init_method != 1) || !(K.o.bound_mult_init_val > 0)) {
         s->err = "cfx_ipm_create: the handle must use CFX_LAYOUT_AOS (or batch 1) and the options must be valid";
         return create_fail(s, CFX_EINVAL);
     }

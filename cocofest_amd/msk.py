@@ -374,7 +374,8 @@ class FesMskOcp:
 
     def __init__(self, model: FesMskModel, n_shooting, final_time, ode_solver, rows, objectives, x_bounds, x_init,
                  u_bounds, u_init, state_names, control_names, n_threads=1, use_sx=True, n_params=0, p_bounds=None,
-                 p_init=None, param_names=(), last_stim_idx=None, param_offset=None, marker_pairs=(), per_pulse=False):
+                 p_init=None, param_names=(), last_stim_idx=None, param_offset=None, marker_pairs=(), per_pulse=False,
+                 per_pulse_bounds="all"):
         self.model = model
         self.n_shooting = n_shooting
         self.final_time = final_time
@@ -395,8 +396,10 @@ class FesMskOcp:
         self.param_offset = param_offset
         # SUPERIMPOSE_MARKERS rows after every interval's rows (cfx_msk_marker_pair dicts + marker names)
         self.marker_pairs = list(marker_pairs)
-        # pulse_width["per_pulse"]: the intervals that follow one pulse share its widths (rows after the marker rows)
+        # pulse_width["per_pulse"]: the intervals that follow one pulse share its widths (rows after the marker rows);
+        # per_pulse_bounds: "all" (every interval's copy bounded) or "first" (the pulse's first interval; bounds_vector)
         self.per_pulse = bool(per_pulse)
+        self.per_pulse_bounds = per_pulse_bounds
 
     @property
     def n_marker_rows(self) -> int:
@@ -441,9 +444,32 @@ class FesMskOcp:
     def param_offset_blocks(self):
         return sorted(set(int(o) for o in self.param_offset)) if self.n_params else []
 
+    def tied_intervals(self):
+        """pulse_width["per_pulse"]: the intervals k >= 1 that follow the same pulse as k - 1 (same last stimulation
+        time in the window: the tie rows u_k - u_{k-1} = 0 of CFX_MSK_PULSE_WIDTH_PER_PULSE, cfx_api.hip)."""
+        if not self.per_pulse:
+            return np.zeros(self.n_shooting, dtype=bool)
+        last = np.asarray(self.stim_rows, dtype=float).reshape(self.n_shooting + 1, -1)[:, -1]
+        return np.concatenate([[False], last[1: self.n_shooting] == last[: self.n_shooting - 1]])
+
     def bounds_vector(self):
-        return (self.pack(self.x_bounds[0], self.u_bounds[0], self.p_bounds[0]),
-                self.pack(self.x_bounds[1], self.u_bounds[1], self.p_bounds[1]))
+        """(lb, ub) over the decision vector.  pulse_width["per_pulse"] with per_pulse_bounds "first": the bounds of a
+        pulse's width bind on the pulse's first interval only, as on the stored revision's per-pulse PARAMETER (one
+        bound per pulse; the tie-row statement otherwise has a copy per interval, 25 copies of one active bound tied by
+        24 rows: degenerate multipliers); the copies' bounds are moved one range outwards (never active while the tie
+        rows hold; finite, so the range scaling of the variable is unchanged).  "all" (default) bounds every copy —
+        the iterates then stay inside the range even where the tie rows do not yet hold (DESIGN.md section 9 has the
+        solves of both)."""
+        lb = self.pack(self.x_bounds[0], self.u_bounds[0], self.p_bounds[0])
+        ub = self.pack(self.x_bounds[1], self.u_bounds[1], self.p_bounds[1])
+        tied = self.tied_intervals()
+        if tied.any() and self.per_pulse_bounds == "first":
+            nm = len(self.model.muscles_dynamics_model)
+            cols = (np.nonzero(tied)[0][:, None] * self.nzb + self.nx + np.arange(nm)[None, :]).ravel()
+            w = ub[cols] - lb[cols]
+            lb[cols] -= w
+            ub[cols] += w
+        return lb, ub
 
     def initial_guess_vector(self):
         return self.pack(self.x_init, self.u_init, self.p_init)
@@ -534,8 +560,12 @@ class OcpFesMsk:
         per_pulse = bool(pulse_width.get("per_pulse"))
         if per_pulse and not isinstance(muscles[0], DingModelPulseWidthFrequency):
             raise ValueError("pulse_width['per_pulse'] needs pulse-width (Ding2007) muscles")
+        ppb = pulse_width.get("per_pulse_bounds", "all")
+        if ppb not in ("all", "first"):
+            raise ValueError("pulse_width['per_pulse_bounds'] must be 'all' or 'first'")
         return FesMskOcp(model, n, final_time, ode_solver, rows, terms, x_bounds, x_init, u_bounds, u_init,
-                         state_names, control_names, n_threads, use_sx, marker_pairs=pairs, per_pulse=per_pulse, **par)
+                         state_names, control_names, n_threads, use_sx, marker_pairs=pairs, per_pulse=per_pulse,
+                         per_pulse_bounds=ppb, **par)
 
     @staticmethod
     def _build_constraints(model, n, custom_constraint) -> list:

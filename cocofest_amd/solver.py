@@ -102,6 +102,10 @@ class IpmOptions:
     # variable scaling by the bound range (x = d x~, d = ub - lb when below 1: pulse widths ~1e-4 s become O(1)); an
     # extension — Ipopt scales only f and g (nlp_scaling_method gradient-based), which range_scaling=False reproduces
     range_scaling: bool = True
+    # Ipopt's bound_mult_init_method: "mu-based" (z = mu_init / slack; the default here) or "constant" (Ipopt's
+    # default: z = bound_mult_init_val)
+    bound_mult_init_method: str = "mu-based"
+    bound_mult_init_val: float = 1.0
     # Ipopt's warm start (NativeIpm: solve(..., warm_start=(y, z_l, z_u))): no least-squares multipliers; x pushed from
     # its bounds by warm_start_bound_push max(1, |bound|) (at most warm_start_bound_frac of the range), bound
     # multipliers raised to warm_start_mult_bound_push; mu starts at mu_init
@@ -490,8 +494,12 @@ class BatchedIpm:
         mu = torch.full((B,), opt.mu_init, dtype=torch.float64, device=self.dev)
         sl = torch.where(hasL, x - lbF, torch.ones_like(x))
         su = torch.where(hasU, ubF - x, torch.ones_like(x))
-        zl = torch.where(hasL, mu[:, None] / sl, torch.zeros_like(x))
-        zu = torch.where(hasU, mu[:, None] / su, torch.zeros_like(x))
+        if opt.bound_mult_init_method == "constant":  # Ipopt's default
+            zl = torch.where(hasL, torch.full_like(x, opt.bound_mult_init_val), torch.zeros_like(x))
+            zu = torch.where(hasU, torch.full_like(x, opt.bound_mult_init_val), torch.zeros_like(x))
+        else:
+            zl = torch.where(hasL, mu[:, None] / sl, torch.zeros_like(x))
+            zu = torch.where(hasU, mu[:, None] / su, torch.zeros_like(x))
         y = torch.zeros((B, m), dtype=torch.float64, device=self.dev)
         reinit_y = torch.ones((B,), dtype=torch.bool, device=self.dev) if m else torch.zeros((B,), dtype=torch.bool,
                                                                                           device=self.dev)
@@ -1254,7 +1262,9 @@ class NativeIpm:
                              "restoration": _RESTORATION[self.opt.restoration],
                              "warm_start_init_point": int(self.opt.warm_start_init_point),
                              "honor_original_bounds": int(self.opt.honor_original_bounds),
-                             "range_scaling": int(self.opt.range_scaling)})
+                             "range_scaling": int(self.opt.range_scaling),
+                             "bound_mult_init_method": {"constant": 0, "mu-based": 1}[self.opt.bound_mult_init_method],
+                             "bound_mult_init_val": float(self.opt.bound_mult_init_val)})
         self.calls = {"eval_all": 0, "eval_h": 0, "eval_g_f": 0, "kkt_factor": 0}
 
     def solve(self, v0=None, fixed_values=None, warm_start=None):

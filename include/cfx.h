@@ -434,6 +434,10 @@ typedef struct cfx_ipm_options {
        (pulse widths ~1e-4 s) are iterated as x / (ub - lb).  0: no variable scaling — Ipopt's behaviour (its
        gradient-based nlp scaling scales f and g only), which changes the scaled termination test */
     int32_t range_scaling;
+    /* Ipopt's bound_mult_init_method (ABI 9): 0 "constant" (Ipopt's default: z = bound_mult_init_val, 1), 1
+       "mu-based" (z = mu_init / slack; this library's default) */
+    int32_t bound_mult_init_method;
+    double bound_mult_init_val;
 } cfx_ipm_options;
 #define CFX_HESSIAN_EXACT 0
 #define CFX_HESSIAN_LIMITED_MEMORY 1

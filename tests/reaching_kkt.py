@@ -147,3 +147,127 @@ def reduced_stationarity(objective="fatigue", data=None, legacy=True, w_end=1.0,
             "dual_inf_rel": float(np.abs(res).max() / scale),
             "dual_inf_rel_free": float(np.abs(res[free]).max() / scale) if free.any() else 0.0,
             "dual_inf_rel_free_median": float(np.median(np.abs(res[free])) / scale) if free.any() else 0.0}
+
+
+def adjoint_multipliers(ocp, v, lb, ub, pulse_bounds="all"):
+    """Ipopt warm-start multipliers (y, z_l, z_u, report) of the legacy product's NLP at the point v, from the PRODUCT's
+    J_g and grad f (libcfx, GPU): the continuity-row multipliers by the discrete adjoint of the RK4 x 1 transcription
+    (y_{c_{k-1}} = df/dx_k + A_k^T y_{c_k} + marker terms; free at the fixed end states), the marker and end-state
+    multipliers and the per-pulse bound multipliers by least squares over the 360 pulse-width sums with their signs
+    enforced (reduced_stationarity's problem), the bound multiplier of each pulse on its first interval
+    (pulse_bounds "first", FesMskOcp.bounds_vector) or spread over its copies ("all"), the tie-row multipliers by the
+    recursion along each pulse.  NLP rows [N nx continuity | 2 marker rows | tie rows], decision [x_k, u_k]_k, x_N."""
+    N, nx, nu = R.N, ocp.nx, ocp.nu
+    nz = nx + nu
+    h = ocp.nlp(batch=1, layout="aos")
+    jr, jc = h.jac_structure()
+    jv = h.eval_jac_g(v[None])[0]
+    gf = h.eval_grad_f(v[None])[0]
+    ng = h.ng
+    h.close()
+    fixed = lb == ub
+    # interval blocks A_k = dPhi_k/dx_k, B_k = dPhi_k/du_k
+    cont = jr < N * nx
+    k = jr[cont] // nx
+    loc = jc[cont] - k * nz
+    inb = (loc >= 0) & (loc < nz)
+    J = np.zeros((N, nx, nz))
+    np.add.at(J, (k[inb], jr[cont][inb] - k[inb] * nx, loc[inb]), jv[cont][inb])
+    A, Bu = J[:, :, :nx], J[:, :, nx:]
+    # marker rows (N nx, N nx + 1): entries on node MARKER_NODE's states
+    mrow = [N * nx, N * nx + 1]
+    seeds = []  # (N + 1, nx) seeds of the adjoint recursion
+    s0 = np.zeros((N + 1, nx))
+    s0[:N] = gf[: N * nz].reshape(N, nz)[:, :nx]
+    s0[N] = gf[N * nz: N * nz + nx]
+    xN_fixed = fixed[N * nz: N * nz + nx]
+    s0[N][xN_fixed] = 0.0
+    seeds.append(s0)
+    for r in mrow:
+        s = np.zeros((N + 1, nx))
+        sel = jr == r
+        node = jc[sel] // nz
+        assert np.all(node == R.MARKER_NODE)
+        s[R.MARKER_NODE, jc[sel] - R.MARKER_NODE * nz] = jv[sel]
+        seeds.append(s)
+    end_idx = np.nonzero(xN_fixed)[0]
+    for i in end_idx:
+        s = np.zeros((N + 1, nx))
+        s[N, i] = 1.0
+        seeds.append(s)
+    S = np.stack(seeds, axis=-1)  # (N + 1, nx, ns)
+    lam = np.zeros((N + 1, nx, S.shape[-1]))  # lam[k] = multiplier of the continuity row into x_k (k >= 1)
+    lam[N] = S[N]
+    for kk in range(N - 1, 0, -1):
+        lam[kk] = S[kk] + A[kk].T @ lam[kk + 1]
+    gu = gf[: N * nz].reshape(N, nz)[:, nx:]
+    G = np.einsum("kxu,kxs->kus", Bu, lam[1:])  # (N, nu, ns): d/du_k of (f, marker rows, end states) via x
+    G[:, :, 0] += gu
+    pidx = R.pulse_index()
+    npulse = int(pidx.max()) + 1
+    Gp = np.zeros((npulse, nu, G.shape[-1]))
+    np.add.at(Gp, pidx, G)
+    Gp = Gp.reshape(npulse * nu, -1)
+    u = v[: N * nz].reshape(N, nz)[:, nx:]
+    ulo = lb[: N * nz].reshape(N, nz)[:, nx:]
+    uhi = ub[: N * nz].reshape(N, nz)[:, nx:]
+    first = np.array([np.nonzero(pidx == p)[0][0] for p in range(npulse)])
+    P = u[first].reshape(-1)
+    rng_u = (uhi - ulo)[first].reshape(-1)
+    tolb = 1e-6 * rng_u
+    at_lo = P <= ulo[first].reshape(-1) + tolb
+    at_hi = P >= uhi[first].reshape(-1) - tolb
+    sign = np.where(at_lo, 1.0, np.where(at_hi, -1.0, 0.0))
+    keep = sign != 0
+    for _ in range(50):  # least squares for nu and the pulse totals Z, wrong-signed Z dropped (reaching_kkt.py)
+        idx = np.nonzero(keep)[0]
+        Am = np.concatenate([Gp[:, 1:], -np.eye(len(P))[:, idx]], axis=1)
+        sol, *_ = np.linalg.lstsq(Am, -Gp[:, 0], rcond=None)
+        Z = np.zeros(len(P))
+        Z[idx] = sol[Gp.shape[1] - 1:]
+        wrong = keep & (Z * sign < 0)
+        if not wrong.any():
+            break
+        keep &= ~wrong
+    nu_ = sol[: Gp.shape[1] - 1]
+    resid = Gp[:, 0] + Gp[:, 1:] @ nu_ - Z
+    coef = np.concatenate([[1.0], nu_])
+    lamc = lam @ coef  # (N + 1, nx)
+    y = np.zeros(ng)
+    y[: N * nx] = lamc[1:].reshape(-1)
+    y[mrow] = nu_[:2]
+    # per-interval width multipliers: the pulse total on its first interval (the only one whose bounds bind,
+    # FesMskOcp.bounds_vector); tie rows by the recursion along the pulse
+    g = (G @ coef)  # (N, nu): stationarity of u_k without the tie rows and bounds
+    Zp = Z.reshape(npulse, nu)
+    zk = np.zeros((N, nu))
+    for p in range(npulse):
+        ks = np.nonzero(pidx == p)[0]
+        if pulse_bounds == "first":
+            zk[ks[0]] = Zp[p]
+        else:  # every copy's bound binds: the total spread evenly
+            zk[ks] = Zp[p] / len(ks)
+    tie = jr >= N * nx + 2
+    tie_rows = np.unique(jr[tie])
+    # tie row -> (later interval k, muscle m, sign of its entry on u_k)
+    kpos = {}
+    for r, c, val in zip(jr[tie], jc[tie], jv[tie]):
+        kpos.setdefault(int(r), []).append((int(c // nz), int(c % nz - nx), float(val)))
+    tval = np.zeros((N + 1, nu))  # multiplier of the tie row written +u_k - u_{k-1}
+    for kk in range(N):
+        if kk + 1 < N and pidx[kk + 1] == pidx[kk]:
+            tval[kk + 1] = g[kk] + tval[kk] - zk[kk]
+    for r in tie_rows:
+        (ka, ma, va), (kb, mb, vb) = kpos[int(r)]
+        kl, ml, vl = (ka, ma, va) if ka > kb else (kb, mb, vb)
+        y[r] = tval[kl, ml] * vl
+    zl = np.zeros(v.size)
+    zu = np.zeros(v.size)
+    ucols = (np.arange(N)[:, None] * nz + nx + np.arange(nu)[None, :])
+    zl[ucols] = np.maximum(zk, 0.0)
+    zu[ucols] = np.maximum(-zk, 0.0)
+    scale = np.abs(Gp[:, 0]).max()
+    rep = {"nu_marker": [float(a) for a in nu_[:2]], "nu_end": [float(a) for a in nu_[2:]],
+           "pulses_at_bounds": int((sign != 0).sum()), "pulses_sign_kept": int(keep.sum()),
+           "reduced_dual_inf_rel": float(np.abs(resid).max() / scale)}
+    return y, zl, zu, rep

@@ -245,7 +245,7 @@ def test_reference_optimum_is_stationary_in_the_pulse_widths(objective):
     assert all(np.isfinite(r["nu"]))
 
 
-def legacy_product(objective="fatigue", per_pulse=True):
+def legacy_product(objective="fatigue", per_pulse=True, pulse_bounds="all"):
     """The product's OcpFesMsk for the stored revision: FesMskModel(legacy_calcium=True) (CFX_MSK_LEGACY_CALCIUM),
     its fatigue rates, pulse widths per pulse (pulse_width["per_pulse"], CFX_MSK_PULSE_WIDTH_PER_PULSE), no residual
     torque (the script's with_residual_torque=False), the hand on the target at node 1000."""
@@ -265,7 +265,7 @@ def legacy_product(objective="fatigue", per_pulse=True):
            node=MARKER_NODE, axes=[C.Axis.X, C.Axis.Y])
     return C.OcpFesMsk.prepare_ocp(model=model, final_time=FINAL_TIME, n_shooting=N,
                                    pulse_width={"min": O.model_constants("ding2007")["pd0"], "max": 0.0006,
-                                                "per_pulse": per_pulse},
+                                                "per_pulse": per_pulse, "per_pulse_bounds": pulse_bounds},
                                    objective={f"minimize_muscle_{objective}": True},
                                    msk_info={"with_residual_torque": False, "bound_type": "start_end",
                                              "bound_data": [[0, 5], [0, 5]], "custom_constraint": cl},
