@@ -26,6 +26,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <map>
 #include <mutex>
 #include <string>
 #include <type_traits>
@@ -1692,13 +1693,20 @@ __global__ void __launch_bounds__(NT) k_band_bwd_stream(int n, int kl, int ku, i
 // ---------------------------------------------------------------------------------------------------
 // Raise a kernel's dynamic-LDS limit above 64 KiB only when a launch needs more than it was last raised to (one
 // attribute call per kernel and size, not one per launch).
+// The limit raised so far is kept per kernel ADDRESS: several instantiations share one function-pointer type
+// (k_band_fwd_stream<1/2/4>, k_band_bwd_stream<KB>, k_band_lu_panel<RH>), so a per-type static would skip the attribute
+// call for an instantiation that was never raised.
+static std::mutex g_lds_mutex;
+static std::map<const void*, size_t> g_lds_raised;
 template <class K>
 static hipError_t allow_lds(K kernel, size_t bytes) {
-    static size_t raised = 65536;  // one per kernel instantiation (K is the kernel's type; one address per type here)
+    const void* fn = reinterpret_cast<const void*>(kernel);
+    std::lock_guard<std::mutex> lock(g_lds_mutex);
+    auto it = g_lds_raised.find(fn);
+    const size_t raised = it == g_lds_raised.end() ? 65536 : it->second;
     if (bytes <= raised) return hipSuccess;
-    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kernel),
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
-    if (e == hipSuccess) raised = bytes;
+    const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+    if (e == hipSuccess) g_lds_raised[fn] = bytes;
     return e;
 }
 

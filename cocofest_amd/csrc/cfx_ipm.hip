@@ -2184,6 +2184,7 @@ __global__ void __launch_bounds__(kIB) k_rs_finish(const IpmK K) {
         if (S.rs_on && (S.rs_exit == RS_FAILED || S.rs_exit == RS_INFEASIBLE)) {
             S.status = S.rs_exit == RS_FAILED ? CFX_IPM_RESTORATION_FAILED : CFX_IPM_INFEASIBLE_PROBLEM_DETECTED;
             S.done = S.stop = 1;
+            S.iters += 1;  // the iteration k_ipm_update's stop path counts (solver.py: rstop.long()), ADVICE round 4
         }
         S.rs_on = 0;
         S.rs_exit = RS_RUNNING;

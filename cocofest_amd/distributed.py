@@ -223,16 +223,34 @@ class IntervalShardedNlp:
     # ---- the same callbacks on raw device pointers (AoS, the full problem), for libcfx's own interior point
     # (cfx_ipm_create_ext, ShardedNativeIpm): inputs selected by the gather table, outputs placed straight into the
     # solver's buffers
+    def _agree(self, ok: bool) -> bool:
+        """True when every rank's local evaluation succeeded (one MAX all-reduce of a failure flag): the callbacks run
+        their collectives only when all ranks reached them, so a rank whose evaluation raised makes every rank's
+        callback fail at the same call instead of leaving the others blocked in an all-gather."""
+        torch, dist = self.torch, self.dist
+        cdev = torch.device("cpu") if (self.dev.type != "cuda" or dist.get_backend(self.group) == "gloo") else self.dev
+        flag = torch.tensor([0 if ok else 1], dtype=torch.int32, device=cdev)
+        dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=self.group)
+        return int(flag.item()) == 0
+
     def eval_all_ptr(self, v, g, jac, f, grad):
         torch, sub = self.torch, self.sub
-        vl = torch.empty((self.B, sub.nv), dtype=torch.float64, device=self.dev)
-        self._gather_sum(self._tables["v_local"], v, self.nv, vl.data_ptr(), sub.nv)
-        gl = torch.empty((self.B, sub.n_shooting * self.ngk), dtype=torch.float64, device=self.dev) if (g or jac) \
-            else None
-        jl = torch.empty((self.B, self.h.nnz_jac), dtype=torch.float64, device=self.dev) if jac else None
-        fl = torch.empty((self.B,), dtype=torch.float64, device=self.dev) if f else None
-        dl = torch.empty((self.B, sub.nv), dtype=torch.float64, device=self.dev) if grad else None
-        self.h.eval_all(vl, g=gl, jac=jl, f=fl, grad=dl)
+        err = None
+        try:
+            vl = torch.empty((self.B, sub.nv), dtype=torch.float64, device=self.dev)
+            self._gather_sum(self._tables["v_local"], v, self.nv, vl.data_ptr(), sub.nv)
+            gl = torch.empty((self.B, sub.n_shooting * self.ngk), dtype=torch.float64, device=self.dev) \
+                if (g or jac) else None
+            jl = torch.empty((self.B, self.h.nnz_jac), dtype=torch.float64, device=self.dev) if jac else None
+            fl = torch.empty((self.B,), dtype=torch.float64, device=self.dev) if f else None
+            dl = torch.empty((self.B, sub.nv), dtype=torch.float64, device=self.dev) if grad else None
+            self.h.eval_all(vl, g=gl, jac=jl, f=fl, grad=dl)
+        except Exception as e:  # noqa: BLE001 — every rank learns of it below, then re-raised through the solver
+            err = e
+        if not self._agree(err is None):
+            if err is not None:
+                raise err
+            raise RuntimeError("interval-sharded eval_all: another rank's evaluation failed")
         if g:
             self._allgather_place(gl, self.map_g, self.ng, "g", dst=g)
         if jac:
@@ -246,15 +264,23 @@ class IntervalShardedNlp:
 
     def eval_h_ptr(self, v, of, lam, hess):
         torch, sub = self.torch, self.sub
-        vl = torch.empty((self.B, sub.nv), dtype=torch.float64, device=self.dev)
-        self._gather_sum(self._tables["v_local"], v, self.nv, vl.data_ptr(), sub.nv)
-        ngl = sub.n_shooting * self.ngk
-        laml = torch.empty((self.B, ngl), dtype=torch.float64, device=self.dev)
-        self._gather_sum(self._tables["lam_local"], lam, self.ng, laml.data_ptr(), ngl)
-        ofl = torch.empty((self.B,), dtype=torch.float64, device=self.dev)
-        self._gather_sum(self._tables["one"], of, 1, ofl.data_ptr(), 1)
-        hl = torch.empty((self.B, self.h.nnz_hess), dtype=torch.float64, device=self.dev)
-        self.h.eval_h(vl, ofl, laml, hl)
+        err = None
+        try:
+            vl = torch.empty((self.B, sub.nv), dtype=torch.float64, device=self.dev)
+            self._gather_sum(self._tables["v_local"], v, self.nv, vl.data_ptr(), sub.nv)
+            ngl = sub.n_shooting * self.ngk
+            laml = torch.empty((self.B, ngl), dtype=torch.float64, device=self.dev)
+            self._gather_sum(self._tables["lam_local"], lam, self.ng, laml.data_ptr(), ngl)
+            ofl = torch.empty((self.B,), dtype=torch.float64, device=self.dev)
+            self._gather_sum(self._tables["one"], of, 1, ofl.data_ptr(), 1)
+            hl = torch.empty((self.B, self.h.nnz_hess), dtype=torch.float64, device=self.dev)
+            self.h.eval_h(vl, ofl, laml, hl)
+        except Exception as e:  # noqa: BLE001
+            err = e
+        if not self._agree(err is None):
+            if err is not None:
+                raise err
+            raise RuntimeError("interval-sharded eval_h: another rank's evaluation failed")
         self._allgather_place(hl, self.map_h, self.nnz_hess, "hess", dst=hess)
         return 0
 
@@ -289,6 +315,11 @@ class ShardedNativeIpm:
         self.torch = torch
         self.ocp, self.B = ocp, batch
         self.opt = options or IpmOptions()
+        # max_wall_time reads each rank's own clock at the top of each iteration: ranks could stop at different
+        # iterations, and one left inside a callback's collective would wait forever — refused here
+        if self.opt.max_wall_time < 1e19:
+            raise ValueError("ShardedNativeIpm: max_wall_time must stay unset (each rank would stop on its own clock); "
+                             "bound the solve with max_iter")
         self.nlp = IntervalShardedNlp(ocp, batch=batch, group=group, device=device)
         lb, ub = ocp.bounds_vector()
         self.n, self.m = self.nlp.nv, self.nlp.ng

@@ -36,9 +36,12 @@ def _worker(rank, port, out_dir):
     from cocofest_amd.solver import BatchedIpm, IpmOptions
     from tests.oracle_handle import oracle_problem_from_ocp
 
+    import datetime
+
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.cuda.set_device(0)
-    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    # a rank left waiting in a collective fails after 60 s instead of hanging the test
+    dist.init_process_group("gloo", rank=rank, world_size=WORLD, timeout=datetime.timedelta(seconds=60))
     try:
         B = 3
         for ci, cfg in enumerate(CFGS):
@@ -85,6 +88,31 @@ def _worker(rank, port, out_dir):
         nat.close()
         np.savez(os.path.join(out_dir, f"native_r{rank}.npz"), v=rn.v, converged=rn.converged, f=rn.f,
                  iterations=rn.iterations, status=rn.status)
+        # a per-rank wall clock is refused; one rank's failing evaluation fails every rank's solve
+        try:
+            ShardedNativeIpm(ocp, batch=2, options=IpmOptions(max_wall_time=10.0), device=0)
+            wall_refused = False
+        except ValueError:
+            wall_refused = True
+        nat = ShardedNativeIpm(ocp, batch=2, options=IpmOptions(tol=1e-6, max_iter=50), device=0)
+        if rank == 1:
+            calls = {"n": 0}
+            orig = nat.nlp.h.eval_all
+
+            def failing(*a, **k):
+                calls["n"] += 1
+                if calls["n"] == 3:
+                    raise RuntimeError("injected evaluation failure")
+                return orig(*a, **k)
+
+            nat.nlp.h.eval_all = failing
+        failed, msg = False, ""
+        try:
+            nat.solve(v0)
+        except Exception as e:  # noqa: BLE001
+            failed, msg = True, str(e)
+        nat.close()
+        np.savez(os.path.join(out_dir, f"fail_r{rank}.npz"), wall_refused=wall_refused, failed=failed, msg=msg)
         if rank == 0:  # the same algorithms on one process-local handle of the whole problem
             from cocofest_amd.solver import NativeIpm
 
@@ -176,3 +204,15 @@ def test_native_interior_point_on_interval_sharded_libcfx(sharded_gpu_run):
     span = np.maximum(span, np.maximum(1e-12, np.abs(one["v"]).max(axis=0)))
     assert np.max(np.abs(r0["v"] - one["v"]) / span) < 1e-6
     np.testing.assert_allclose(r0["f"], one["f"], rtol=1e-7)
+
+
+def test_sharded_native_ipm_fails_on_every_rank_together(sharded_gpu_run):
+    """ShardedNativeIpm refuses a finite max_wall_time (each rank would stop on its own clock), and a
+    rank whose local evaluation raises makes every rank's solve fail at the same callback — rank 0, whose evaluation
+    succeeded, raises too instead of waiting in the next all-gather (the process group's 60 s timeout would fail the
+    run otherwise)."""
+    for r in range(WORLD):
+        d = np.load(sharded_gpu_run / f"fail_r{r}.npz")
+        assert bool(d["wall_refused"]) and bool(d["failed"]), (r, str(d["msg"]))
+    assert "injected evaluation failure" in str(np.load(sharded_gpu_run / "fail_r1.npz")["msg"])
+    assert "another rank" in str(np.load(sharded_gpu_run / "fail_r0.npz")["msg"])
