@@ -44,6 +44,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline sample budget (0: skip)")
     ap.add_argument("--no-solve", action="store_true", help="skip the wall-clock-to-convergence section")
     ap.add_argument("--no-msk", action="store_true", help="skip the cfg-5 musculoskeletal section")
+    ap.add_argument("--no-reaching", action="store_true",
+                    help="skip the 1,500-interval reaching-task solve (wall-clock to convergence, ~30 s)")
     ap.add_argument("--nmpc-horizons", type=int, default=200, help="cfg-4 NMPC horizons (0: skip)")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="process-group backend; gloo (ranks may share a GPU) rehearses the N > 1 path on one card")
@@ -632,6 +634,71 @@ def msk_section(device, tp, ocp1, cpu_seconds=0.0):
     return out
 
 
+REACHING_MUSCLES = ["BIClong", "BICshort", "TRIlong", "TRIlat", "TRImed", "BRA"]
+
+
+def build_reaching(objective="fatigue"):
+    """The reference's reaching task (examples/dynamics/reaching_task/reaching_task_pulse_duration_optimization.py:
+    27-118) as the product states its stored revision (tests/test_reference_solution.py::legacy_product): arm26 with
+    six Ding2007-with-fatigue muscles (fibre-type and PCSA proportions, the stored revision's fatigue rates x 10), 60
+    pulses at 40 Hz over 1.5 s, N = 1,500, RK4 x 1, the hand on the target at node 1000, per-pulse widths, no residual
+    torque.  Data only from tests/golden (the bioMod as parsed JSON)."""
+    import cocofest_amd as C
+
+    root = os.path.dirname(os.path.abspath(__file__))
+    alpha_a_prop = [0.607, 0.607, 0.465, 0.465, 0.465, 0.457]
+    a_scale_prop = [12.7 / 28.3, 12.7 / 28.3, 1.0, 1.0, 1.0, 11.6 / 28.3]
+    stims = [float(s) for s in np.round(np.linspace(0, 1.5, 61), 3)[:-1]]
+    models = []
+    for i, n in enumerate(REACHING_MUSCLES):
+        mm = C.DingModelPulseWidthFrequencyWithFatigue(muscle_name=n, sum_stim_truncation=60)
+        mm.alpha_a = mm.alpha_a * alpha_a_prop[i] * 10.0
+        mm.alpha_tau1 = mm.alpha_tau1 * 10.0
+        mm.alpha_km = mm.alpha_km * 10.0
+        mm.a_scale = mm.a_scale * a_scale_prop[i]
+        models.append(mm)
+    model = C.FesMskModel(biorbd_path=os.path.join(root, "tests", "golden", "biomod_arm26.json"), muscles_model=models,
+                          stim_time=stims, activate_force_length_relationship=True,
+                          activate_force_velocity_relationship=True, activate_residual_torque=False,
+                          legacy_calcium=True)
+    cl = C.ConstraintList()
+    cl.add(C.ConstraintFcn.SUPERIMPOSE_MARKERS, first_marker="COM_hand", second_marker="reaching_target", phase=0,
+           node=1000, axes=[C.Axis.X, C.Axis.Y])
+    return C.OcpFesMsk.prepare_ocp(model=model, final_time=1.5, n_shooting=1500,
+                                   pulse_width={"min": C.DingModelPulseWidthFrequency().pd0, "max": 0.0006,
+                                                "per_pulse": True},
+                                   objective={f"minimize_muscle_{objective}": True},
+                                   msk_info={"with_residual_torque": False, "bound_type": "start_end",
+                                             "bound_data": [[0, 5], [0, 5]], "custom_constraint": cl},
+                                   ode_solver=C.OdeSolver.RK4(n_integration_steps=1), apply_custom_constraint=True)
+
+
+def reaching_section(device, wall_limit=150.0):
+    """Wall-clock to convergence of the one reference OCP with a timed reference solve: the fatigue objective of the
+    reaching task from the product's default initial guess (the reference script's own start), Ipopt's termination
+    tests at tol 1e-6, bound_relax_factor 1e-8; the stage-chain KKT layout (block cyclic reduction).  Beside it the
+    reference's own time_to_optimize (sol.real_time_to_optimize, cocofest/result/pickle.py:32; unknown hardware, an
+    older revision, use_sx=False)."""
+    from cocofest_amd.solver import IpmOptions, NativeIpm
+
+    root = os.path.dirname(os.path.abspath(__file__))
+    ref_t = float(np.load(os.path.join(root, "tests", "golden", "reaching_pulse_duration_fatigue.npz"))["time_to_optimize"])
+    ocp = build_reaching("fatigue")
+    ipm = NativeIpm(ocp, batch=1, device=device,
+                    options=IpmOptions(tol=1e-6, max_iter=5000, bound_relax_factor=1e-8, max_wall_time=wall_limit))
+    res = ipm.solve()
+    st = dict(ipm.last_stats)
+    ipm.close()
+    return {"objective": "fatigue (minimize_muscle_fatigue)", "start": "product default initial guess",
+            "wall_s": res.wall_time, "iterations": int(res.iterations[0]), "status": int(res.status[0]),
+            "converged": bool(res.converged[0]), "f": float(res.f[0]), "f_stored_reference_optimum": 7.841959196,
+            "kkt_layout": {"chain_nodes": int(st["kkt_chain_nodes"]), "node_size": int(st["kkt_chain_sp"]),
+                           "border": int(st["kkt_border"]), "kkt_unknowns": int(st["kkt_n"])},
+            "s_per_iteration": res.wall_time / max(1, int(res.iterations[0])),
+            "reference_time_to_optimize_s": ref_t, "reference_over_product": ref_t / res.wall_time,
+            "note": "reference timing on unknown hardware with an older revision (use_sx=False); stated as context"}
+
+
 def main():
     args = parse()
     import torch
@@ -713,6 +780,7 @@ def main():
         ivp = ivp_section(local) if (world == 1 and not args.no_solve) else None
         col = collocation_section(local) if (world == 1 and not args.no_solve) else None
         c3 = cfg3_section(local, args.cpu_seconds / 4) if (world == 1 and not args.no_solve) else None
+        reach = reaching_section(local) if (world == 1 and not args.no_solve and not args.no_reaching) else None
         msk = msk_tp
         if msk_tp is not None and world == 1 and not args.no_solve:
             msk = msk_section(local, msk_tp, msk_ocp, cpu_seconds=args.cpu_seconds / 2)
@@ -756,6 +824,7 @@ def main():
             "cfg3_callbacks": c3,
             "nmpc": nm,
             "msk": msk,
+            "reaching": reach,
         }
     h.close()
     if dist:
