@@ -391,7 +391,7 @@ def collocation_section(device, steps=50):
                 "source": "scripts/micro/colloc_bw.hip (profiles/round4/collocation/colloc_bw.jsonl): the same reads "
                           "and stores, no arithmetic", "soa_nt_ms": ceil.get("soa_nt"), "tiled_nt_ms": ceil.get("tiled_nt"),
                 "kernel_over_pattern_soa": ceil["soa_nt"] / ms if ceil.get("soa_nt") else None},
-            "roofline": {"bound": "hbm", "kernel": "cfx::k_colloc<DING2003, TMAX=1, DEG=4, NI=2>", "achieved": achieved,
+            "roofline": {"bound": "hbm", "kernel": "cfx::k_colloc_soa<DING2003, TMAX=1, DEG=4, NI=2> (its own name in traces since round 5)", "achieved": achieved,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                          "traffic": pmc.get("hbm_bytes_per_launch") if pmc else None,
                          "traffic_source": pmc.get("source") if pmc else None},

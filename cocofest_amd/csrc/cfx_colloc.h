@@ -261,6 +261,19 @@ __global__ void __launch_bounds__(256) k_colloc(const KParams P, const double* _
                                                 double* __restrict__ J) {
     colloc_thread<MODEL, TMAX, DEG, NI, PLAIN>(P, V, G, J);
 }
+// The bench's launch shapes under names of their own (one kernel name mixed the SoA, tiled and
+// keep-constant launches in the traces, so no roofline fraction could be recomputed per launch): the same body.
+#define CFX_COLLOC_NAMED(NAME)                                                                                        \
+    template <int MODEL, int TMAX, int DEG, int NI>                                                                 \
+    __global__ void __launch_bounds__(256) NAME(const KParams P, const double* __restrict__ V,                       \
+                                                double* __restrict__ G, double* __restrict__ J) {                   \
+        colloc_thread<MODEL, TMAX, DEG, NI, false>(P, V, G, J);                                                     \
+    }
+CFX_COLLOC_NAMED(k_colloc_soa)
+CFX_COLLOC_NAMED(k_colloc_tiles)
+CFX_COLLOC_NAMED(k_colloc_soa_keepj)
+CFX_COLLOC_NAMED(k_colloc_tiles_keepj)
+#undef CFX_COLLOC_NAMED
 // occupancy probe (CFX_COLLOC_STORE=w4 / w4plain): the same thread body held to 128 VGPRs (4 waves per SIMD; the
 // default instantiation of the bench's shape takes 198 VGPRs, 2 waves)
 template <int MODEL, int TMAX, int DEG, int NI, bool PLAIN>

@@ -37,6 +37,16 @@ static hipError_t colloc_deg(const KParams& P, const double* V, double* G, doubl
                     return hipGetLastError();
             default: break;
         }
+        // the bench's shape: one kernel name per layout and J_g form (traces attribute each launch)
+        if (J) {
+            if (Q.tiled)
+                hipLaunchKernelGGL((Q.keepc ? k_colloc_tiles_keepj<MODEL, TMAX, DEG, NI> : k_colloc_tiles<MODEL, TMAX, DEG, NI>),
+                                   grid, dim3(kBlock), 0, s, Q, V, G, J);
+            else
+                hipLaunchKernelGGL((Q.keepc ? k_colloc_soa_keepj<MODEL, TMAX, DEG, NI> : k_colloc_soa<MODEL, TMAX, DEG, NI>),
+                                   grid, dim3(kBlock), 0, s, Q, V, G, J);
+            return hipGetLastError();
+        }
     }
     hipLaunchKernelGGL((k_colloc<MODEL, TMAX, DEG, NI>), grid, dim3(kBlock), 0, s, Q, V, G, J);
     return hipGetLastError();

@@ -107,6 +107,12 @@ static double timed(F f, int reps) {
 int main(int argc, char** argv) {
     const int64_t B = argc > 1 ? std::atoll(argv[1]) : (1 << 18);
     const int reps = argc > 2 ? std::atoi(argv[2]) : 200;
+    // bounds (round 4's fault: a write stream sized (EG + EJ) B over the EJ B buffer): the pattern kernels write
+    // instance pairs b, b + 1 < B of every element row, the streams 16-byte pairs below w2
+    if (B < 2 || B % 2 != 0) {
+        std::printf("batch must be even and >= 2\n");
+        return 1;
+    }
     double *V, *G, *J, *out;
     CHECK(hipMalloc(&V, sizeof(double) * EV * B));
     CHECK(hipMalloc(&G, sizeof(double) * EG * B));
@@ -130,6 +136,10 @@ int main(int argc, char** argv) {
     // pure streams over the J buffer alone (its EJ * B doubles: the bulk of the written bytes)
     const int64_t w2 = (int64_t)EJ * B / 2;
     const double jbytes = 8.0 * EJ * (double)B;
+    if (2 * w2 > (int64_t)EJ * B) {  // every stream element pair inside the J allocation
+        std::printf("stream bounds: %lld doubles over a %lld-double buffer\n", (long long)(2 * w2), (long long)EJ * B);
+        return 1;
+    }
     report("wstream_nt (J bytes)",
            timed([&] { hipLaunchKernelGGL((k_wstream<true>), dim3(4096), dim3(256), 0, 0, J, w2, 1.0); }, reps), jbytes);
     report("wstream_plain (J bytes)",
