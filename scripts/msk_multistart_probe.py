@@ -32,6 +32,8 @@ ap.add_argument("--wall", type=float, default=1e20)
 ap.add_argument("--jsonl", default=None)
 ap.add_argument("--soft", type=float, default=None, help="soft_resto_pderror_reduction_factor (default: the option's)")
 ap.add_argument("--restart", action="store_true", help="resto_failure_restart (extension: a failed phase restarts)")
+ap.add_argument("--opt", action="append", default=[], help="extra IpmOptions key=value (repeatable)")
+ap.add_argument("--label", default="")
 args = ap.parse_args()
 
 ocp = bench.msk_build(5)
@@ -47,6 +49,10 @@ for B, amp in runs:
     extra = {} if args.soft is None else {"soft_resto_pderror_reduction_factor": args.soft}
     if args.restart:
         extra["resto_failure_restart"] = True
+    for kv in args.opt:
+        k, val = kv.split("=", 1)
+        cur = getattr(IpmOptions, k)
+        extra[k] = type(cur)(val) if not isinstance(cur, bool) else val.lower() in ("1", "true", "yes")
     opts = IpmOptions(tol=1e-6, max_iter=args.max_iter, max_wall_time=args.wall, print_frequency_time=20.0, **extra)
     ipm = cls(ocp, batch=B, options=opts)
     res = ipm.solve(v0)
@@ -54,7 +60,7 @@ for B, amp in runs:
     ipm.close()
     hist = collections.Counter(IPM_STATUS.get(int(s), str(s)) for s in res.status)
     conv = res.converged.astype(bool)
-    rec = dict(solver=cls.__name__, batch=B, amp=amp, max_iter=args.max_iter, wall_s=round(res.wall_time, 3),
+    rec = dict(label=args.label, options={k: v for k, v in extra.items()}, solver=cls.__name__, batch=B, amp=amp, max_iter=args.max_iter, wall_s=round(res.wall_time, 3),
                converged=int(conv.sum()), status=dict(hist), iterations_median=float(np.median(res.iterations)),
                iterations_max=int(res.iterations.max()), f_converged_min=float(res.f[conv].min()) if conv.any() else None,
                f_converged_max=float(res.f[conv].max()) if conv.any() else None,
