@@ -316,6 +316,28 @@ MSK_HD const double* msk_cs1(const MskParams& P, int64_t kq) {
 }
 
 // ---- small vector helpers ---------------------------------------------------------------------------------------
+// c ? a : b field by field: a conditional on whole dual numbers is lowered to a copy from a selected address, which
+// keeps the operands in scratch memory
+MSK_HD double msel(bool c, double a, double b) { return c ? a : b; }
+MSK_HD Dep msel(bool c, Dep a, Dep b) { return c ? a : b; }
+template <int D>
+CFX_HD Dual<D> msel(bool c, const Dual<D>& a, const Dual<D>& b) {
+    Dual<D> r;
+    r.v = c ? a.v : b.v;
+#pragma unroll
+    for (int i = 0; i < D; ++i) r.d[i] = c ? a.d[i] : b.d[i];
+    return r;
+}
+template <int D>
+CFX_HD Jet<D> msel(bool c, const Jet<D>& a, const Jet<D>& b) {
+    Jet<D> r;
+    r.v = c ? a.v : b.v;
+#pragma unroll
+    for (int i = 0; i < D; ++i) r.g[i] = c ? a.g[i] : b.g[i];
+#pragma unroll
+    for (int i = 0; i < Jet<D>::H; ++i) r.h[i] = c ? a.h[i] : b.h[i];
+    return r;
+}
 template <class S>
 MSK_HD void cross3(const S* a, const S* b, S* r) {
     r[0] = a[1] * b[2] - a[2] * b[1];
@@ -373,17 +395,42 @@ MSK_HD void msk_point(const S (*R)[9], const S (*o)[3], const S (*z)[3], int f, 
     for (int k = 0; k < NQ; ++k)
 #pragma unroll
         for (int e = 0; e < 3; ++e) dP[k][e] = Num<S>::c(0.0);
+    if constexpr (std::is_same<S, double>::value) {
 #pragma unroll
-    for (int j = 0; j < NQ; ++j) {
-        if (f == j) {
+        for (int j = 0; j < NQ; ++j) {
+            if (f == j) {
 #pragma unroll
-            for (int e = 0; e < 3; ++e) P[e] = o[j][e] + R[j][e * 3] * p[0] + R[j][e * 3 + 1] * p[1] + R[j][e * 3 + 2] * p[2];
+                for (int e = 0; e < 3; ++e)
+                    P[e] = o[j][e] + R[j][e * 3] * p[0] + R[j][e * 3 + 1] * p[1] + R[j][e * 3 + 2] * p[2];
 #pragma unroll
-            for (int k = 0; k <= j; ++k) {
-                S r[3] = {P[0] - o[k][0], P[1] - o[k][1], P[2] - o[k][2]};
-                cross3(z[k], r, dP[k]);
+                for (int k = 0; k <= j; ++k) {
+                    S r[3] = {P[0] - o[k][0], P[1] - o[k][1], P[2] - o[k][2]};
+                    cross3(z[k], r, dP[k]);
+                }
             }
         }
+        return;
+    }
+    // dual numbers: every frame's transform is formed and the point's own selected (f is wave-uniform) — with a
+    // branch per frame the compiler merged the branches into copies from R[f] / o[f], f a run-time index, which kept
+    // the frames in scratch memory
+#pragma unroll
+    for (int j = 0; j < NQ; ++j) {
+        const bool own = f == j;
+#pragma unroll
+        for (int e = 0; e < 3; ++e) {
+            const S Pj = o[j][e] + R[j][e * 3] * p[0] + R[j][e * 3 + 1] * p[1] + R[j][e * 3 + 2] * p[2];
+            P[e] = msel(own, Pj, P[e]);
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < NQ; ++k) {
+        const bool above = k <= f;
+        const S r[3] = {P[0] - o[k][0], P[1] - o[k][1], P[2] - o[k][2]};
+        S c[3];
+        cross3(z[k], r, c);
+#pragma unroll
+        for (int e = 0; e < 3; ++e) dP[k][e] = msel(above, c[e], dP[k][e]);
     }
 }
 
@@ -409,7 +456,7 @@ MSK_HD S hill_fv(const S& vel) {
 template <class S>
 MSK_HD S hill_fp(const S& nl) {
     const S fp = (mexp(4.0 * (nl - 1.0) / 0.6) - 1.0) / (exp(4.0) - 1.0);
-    return value(fp) > 0.0 ? fp : Num<S>::c(0.0);
+    return msel(value(fp) > 0.0, fp, Num<S>::c(0.0));
 }
 
 // Promotion of a q-only quantity (SQ) to the (q, qdot) scalar (SV): identity when both are the same type, else
@@ -431,6 +478,8 @@ template <class SV, class SQ>
 MSK_HD SV up(const SQ& a) {
     if constexpr (std::is_same<SV, SQ>::value) {
         return a;
+    } else if constexpr (std::is_same<SQ, double>::value) {
+        return Num<SV>::c(a);
     } else {
         return dual_up<DualN<SV>::n>(a);
     }
@@ -486,8 +535,8 @@ MSK_HD void msk_skeleton(const MskGeom& G, const SQ* q, const SV* qd, const SV* 
             JLu[k] = up<SV>(JL[k]);
             vel = vel + JLu[k] * qd[k];
         }
-        const SV fl = G.fl_on ? up<SV>(hill_fl(nl)) : Num<SV>::c(1.0);
-        const SV fv = G.fv_on ? hill_fv(vel) : Num<SV>::c(1.0);
+        const SV fl = msel(G.fl_on, up<SV>(hill_fl(nl)), Num<SV>::c(1.0));
+        const SV fv = msel(G.fv_on, hill_fv(vel), Num<SV>::c(1.0));
         mult[mu] = G.fp_on ? fl * fv + up<SV>(hill_fp(nl)) : fl * fv;
         // ---- joint torque -J_L^T F (dynamical_model.py:331-332)
 #pragma unroll
@@ -653,7 +702,7 @@ MSK_HD void msk_rhs(const MskGeom& G, int residual, const double* cs, const doub
     for (int mu = 0; mu < NM; ++mu) F[mu] = x[mu * NXM + 1];
 #pragma unroll
     for (int k = 0; k < NQ; ++k) taur[k] = residual ? u[NUI + k] : Num<S>::c(0.0);
-    msk_skeleton<NQ, NM>(G, x + XQ, x + XQD, F, residual ? taur : nullptr, mult, qdd, nullptr, nullptr);
+    msk_skeleton<NQ, NM>(G, x + XQ, x + XQD, F, taur, mult, qdd, nullptr, nullptr);
 #pragma unroll
     for (int mu = 0; mu < NM; ++mu) {
         const MskMuscleConst& C = G.mc[mu];
@@ -690,62 +739,72 @@ MSK_HD void msk_rhs(const MskGeom& G, int residual, const double* cs, const doub
 }
 
 // Phi_m(x, u) over interval k: m RK sub-steps (bioptim convention: constant control, RK4 stage times
-// t, t + h/2, t + h/2, t + h).  x is overwritten with the end state.
-template <int NQ, int NM, int FAM, int SCHEME, class S>
-MSK_HD void msk_interval(const MskParams& P, const MskGeom& G, int k, S* x, const S* u, const double* lam) {
+// t, t + h/2, t + h/2, t + h).  x is overwritten with the end state.  LEG: legacy calcium (P.cs1 set) — a compile-time
+// choice, because a pointer chosen at run time between the local stage array and null kept the array in scratch memory.
+template <int NQ, int NM, int FAM, int SCHEME, bool LEG, class S>
+MSK_HD void msk_interval_t(const MskParams& P, const MskGeom& G, int k, S* x, const S* u, const double* lam) {
     constexpr int NX = NM * msk_nxm<FAM>() + 2 * NQ;
     constexpr int ST = SCHEME == 4 ? 4 : (SCHEME == 2 ? 2 : 1);
     constexpr int NMC = NM;
     const double h = P.h;
     for (int j = 0; j < P.m; ++j) {
-        double csv[ST * NMC], csv1[ST * NMC];  // the stage sums of this sub-step (and their d / d Km, legacy)
+        double csv[ST * NMC], csv1[LEG ? ST * NMC : 1];  // the stage sums of this sub-step (and their d / d Km)
 #pragma unroll
         for (int st = 0; st < ST; ++st) {
             msk_stage_cs<NM, FAM>(P.cs, (int64_t)k * P.Q + j * ST + st, lam, csv + st * NMC);
-            if (P.cs1)
+            if constexpr (LEG)
 #pragma unroll
                 for (int mu = 0; mu < NM; ++mu) csv1[st * NMC + mu] = P.cs1[((int64_t)k * P.Q + j * ST + st) * NM + mu];
         }
         const double* cs = csv;
-        const double* c1 = P.cs1 ? csv1 : nullptr;
+        auto c1s = [&](int st) -> const double* {
+            if constexpr (LEG) return csv1 + st * NMC;
+            return nullptr;
+        };
         if constexpr (SCHEME == 1) {
             S f[NX];
-            msk_rhs<NQ, NM, FAM>(G, P.residual, cs, c1, x, u, f);
+            msk_rhs<NQ, NM, FAM>(G, P.residual, cs, c1s(0), x, u, f);
 #pragma unroll
             for (int r = 0; r < NX; ++r) x[r] = x[r] + h * f[r];
         } else if constexpr (SCHEME == 2) {
             S f[NX], xs[NX];
-            msk_rhs<NQ, NM, FAM>(G, P.residual, cs, c1, x, u, f);
+            msk_rhs<NQ, NM, FAM>(G, P.residual, cs, c1s(0), x, u, f);
 #pragma unroll
             for (int r = 0; r < NX; ++r) xs[r] = x[r] + (0.5 * h) * f[r];
-            msk_rhs<NQ, NM, FAM>(G, P.residual, cs + NMC, c1 ? c1 + NMC : nullptr, xs, u, f);
+            msk_rhs<NQ, NM, FAM>(G, P.residual, cs + NMC, c1s(1), xs, u, f);
 #pragma unroll
             for (int r = 0; r < NX; ++r) x[r] = x[r] + h * f[r];
         } else {
             S acc[NX], xs[NX], f[NX];
-            msk_rhs<NQ, NM, FAM>(G, P.residual, cs, c1, x, u, f);
+            msk_rhs<NQ, NM, FAM>(G, P.residual, cs, c1s(0), x, u, f);
 #pragma unroll
             for (int r = 0; r < NX; ++r) {
                 acc[r] = f[r];
                 xs[r] = x[r] + (0.5 * h) * f[r];
             }
-            msk_rhs<NQ, NM, FAM>(G, P.residual, cs + NMC, c1 ? c1 + NMC : nullptr, xs, u, f);
+            msk_rhs<NQ, NM, FAM>(G, P.residual, cs + NMC, c1s(1), xs, u, f);
 #pragma unroll
             for (int r = 0; r < NX; ++r) {
                 acc[r] = acc[r] + 2.0 * f[r];
                 xs[r] = x[r] + (0.5 * h) * f[r];
             }
-            msk_rhs<NQ, NM, FAM>(G, P.residual, cs + 2 * NMC, c1 ? c1 + 2 * NMC : nullptr, xs, u, f);
+            msk_rhs<NQ, NM, FAM>(G, P.residual, cs + 2 * NMC, c1s(2), xs, u, f);
 #pragma unroll
             for (int r = 0; r < NX; ++r) {
                 acc[r] = acc[r] + 2.0 * f[r];
                 xs[r] = x[r] + h * f[r];
             }
-            msk_rhs<NQ, NM, FAM>(G, P.residual, cs + 3 * NMC, c1 ? c1 + 3 * NMC : nullptr, xs, u, f);
+            msk_rhs<NQ, NM, FAM>(G, P.residual, cs + 3 * NMC, c1s(3), xs, u, f);
 #pragma unroll
             for (int r = 0; r < NX; ++r) x[r] = x[r] + (h / 6.0) * (acc[r] + f[r]);
         }
     }
+}
+
+template <int NQ, int NM, int FAM, int SCHEME, class S>
+MSK_HD void msk_interval(const MskParams& P, const MskGeom& G, int k, S* x, const S* u, const double* lam) {
+    if (P.cs1) msk_interval_t<NQ, NM, FAM, SCHEME, true>(P, G, k, x, u, lam);
+    else msk_interval_t<NQ, NM, FAM, SCHEME, false>(P, G, k, x, u, lam);
 }
 
 // ---- g + J_g: thread = (instance, interval, chunk of D Jacobian directions) ---------------------------------
@@ -859,51 +918,9 @@ __device__ __forceinline__ void msk_muscle_coef(const MskMuscleConst& C, const d
     c[5] = PW ? mult * s * A * dE : 0.0;
 }
 
-// One RK stage: the RHS value f(xs, u) and the stage coefficients written to Ws[c * B].
-template <int NQ, int NM, int FAM>
-__device__ __forceinline__ void msk_stage(const MskGeom& G, int residual, const double* cs, const double* cs1,
-                                          const double* xs, const double* u, double* f, double* __restrict__ Ws,
-                                          int64_t B) {
-    constexpr int NXM = msk_nxm<FAM>(), XQ = NM * NXM, XQD = XQ + NQ, ND = 2 * NQ;
-    constexpr bool FAT = (FAM & 1) != 0, PW = msk_pw<FAM>();
-    constexpr int NUI = msk_nui<NM, FAM>(), OM = 6 + ND, ODQ = NM * OM, OB = ODQ + NQ * ND, OMI = OB + NQ * NM;
-    using S = Dual<ND>;
-    Dual<NQ> q[NQ];  // q-only quantities carry the nq q-directions, the rest all 2 nq (msk_skeleton)
-    S qd[NQ], F[NM], taur[NQ], mult[NM], qdd[NQ];
-#pragma unroll
-    for (int k = 0; k < NQ; ++k) {
-        q[k] = dconst<NQ>(xs[XQ + k]);
-        qd[k] = dconst<ND>(xs[XQD + k]);
-        q[k].d[k] = 1.0;
-        qd[k].d[NQ + k] = 1.0;
-        taur[k] = dconst<ND>(residual ? u[NUI + k] : 0.0);
-    }
-#pragma unroll
-    for (int mu = 0; mu < NM; ++mu) F[mu] = dconst<ND>(xs[mu * NXM + 1]);
-    double Mv[NQ][NQ], JLv[NM][NQ];
-    msk_skeleton<NQ, NM>(G, q, qd, F, residual ? taur : nullptr, mult, qdd, Mv, JLv);
-#pragma unroll
-    for (int mu = 0; mu < NM; ++mu) {
-        const MskMuscleConst& C = G.mc[mu];
-        const double* xm = xs + mu * NXM;
-        double c[6], base, pw = 0.0;
-        if constexpr (PW) pw = u[mu];  // (a plain ternary would still index u out of range for NM > NQ)
-        msk_muscle_coef<FAM>(C, xm, pw, mult[mu].v, c, base);
-        f[mu * NXM] = (cs[mu] - xm[0]) * C.inv_tauc;
-        f[mu * NXM + 1] = base * mult[mu].v;
-        if constexpr (FAT) {
-            if (cs1) f[mu * NXM] = f[mu * NXM] + (xm[4] - C.km_rest) * (cs1[mu] * C.inv_tauc);
-            f[mu * NXM + 2] = C.alpha_a * xm[1] - (xm[2] - C.a_fat_rest) * C.inv_tau_fat;
-            f[mu * NXM + 3] = C.alpha_tau1 * xm[1] - (xm[3] - C.tau1_rest) * C.inv_tau_fat;
-            f[mu * NXM + 4] = C.alpha_km * xm[1] - (xm[4] - C.km_rest) * C.inv_tau_fat;
-        }
-#pragma unroll
-        for (int e = 0; e < 6; ++e) Ws[(mu * OM + e) * B] = c[e];
-#pragma unroll
-        for (int d = 0; d < ND; ++d) Ws[(mu * OM + 6 + d) * B] = base * mult[mu].d[d];
-    }
-    // M^-1 (symmetric positive definite, NQ <= 4: Gauss-Jordan without pivoting)
-    double Mi[NQ][NQ];
+// M^-1 (symmetric positive definite, NQ <= 4: Gauss-Jordan without pivoting)
+template <int NQ>
+__device__ __forceinline__ void msk_spd_inverse(const double (*Mv)[NQ], double (*Mi)[NQ]) {
     if constexpr (NQ == 1) {
         Mi[0][0] = 1.0 / Mv[0][0];
     } else if constexpr (NQ == 2) {
@@ -929,6 +946,53 @@ __device__ __forceinline__ void msk_stage(const MskGeom& G, int residual, const 
                 }
         }
     }
+}
+
+// One RK stage: the RHS value f(xs, u) and the stage coefficients written to Ws[c * B].
+template <int NQ, int NM, int FAM>
+__device__ __forceinline__ void msk_stage(const MskGeom& G, int residual, const double* cs, const double* cs1,
+                                          const double* xs, const double* u, double* f, double* __restrict__ Ws,
+                                          int64_t B) {
+    constexpr int NXM = msk_nxm<FAM>(), XQ = NM * NXM, XQD = XQ + NQ, ND = 2 * NQ;
+    constexpr bool FAT = (FAM & 1) != 0, PW = msk_pw<FAM>();
+    constexpr int NUI = msk_nui<NM, FAM>(), OM = 6 + ND, ODQ = NM * OM, OB = ODQ + NQ * ND, OMI = OB + NQ * NM;
+    using S = Dual<ND>;
+    Dual<NQ> q[NQ];  // q-only quantities carry the nq q-directions, the rest all 2 nq (msk_skeleton)
+    S qd[NQ], F[NM], taur[NQ], mult[NM], qdd[NQ];
+#pragma unroll
+    for (int k = 0; k < NQ; ++k) {
+        q[k] = dconst<NQ>(xs[XQ + k]);
+        qd[k] = dconst<ND>(xs[XQD + k]);
+        q[k].d[k] = 1.0;
+        qd[k].d[NQ + k] = 1.0;
+        taur[k] = dconst<ND>(residual ? u[NUI + k] : 0.0);
+    }
+#pragma unroll
+    for (int mu = 0; mu < NM; ++mu) F[mu] = dconst<ND>(xs[mu * NXM + 1]);
+    double Mv[NQ][NQ], JLv[NM][NQ];
+    msk_skeleton<NQ, NM>(G, q, qd, F, taur, mult, qdd, Mv, JLv);
+#pragma unroll
+    for (int mu = 0; mu < NM; ++mu) {
+        const MskMuscleConst& C = G.mc[mu];
+        const double* xm = xs + mu * NXM;
+        double c[6], base, pw = 0.0;
+        if constexpr (PW) pw = u[mu];  // (a plain ternary would still index u out of range for NM > NQ)
+        msk_muscle_coef<FAM>(C, xm, pw, mult[mu].v, c, base);
+        f[mu * NXM] = (cs[mu] - xm[0]) * C.inv_tauc;
+        f[mu * NXM + 1] = base * mult[mu].v;
+        if constexpr (FAT) {
+            if (cs1) f[mu * NXM] = f[mu * NXM] + (xm[4] - C.km_rest) * (cs1[mu] * C.inv_tauc);
+            f[mu * NXM + 2] = C.alpha_a * xm[1] - (xm[2] - C.a_fat_rest) * C.inv_tau_fat;
+            f[mu * NXM + 3] = C.alpha_tau1 * xm[1] - (xm[3] - C.tau1_rest) * C.inv_tau_fat;
+            f[mu * NXM + 4] = C.alpha_km * xm[1] - (xm[4] - C.km_rest) * C.inv_tau_fat;
+        }
+#pragma unroll
+        for (int e = 0; e < 6; ++e) Ws[(mu * OM + e) * B] = c[e];
+#pragma unroll
+        for (int d = 0; d < ND; ++d) Ws[(mu * OM + 6 + d) * B] = base * mult[mu].d[d];
+    }
+    double Mi[NQ][NQ];
+    msk_spd_inverse<NQ>(Mv, Mi);
 #pragma unroll
     for (int i = 0; i < NQ; ++i) {
         f[XQ + i] = xs[XQD + i];
@@ -944,6 +1008,76 @@ __device__ __forceinline__ void msk_stage(const MskGeom& G, int residual, const 
         }
 #pragma unroll
         for (int k = 0; k < NQ; ++k) Ws[(OMI + i * NQ + k) * B] = Mi[i][k];
+    }
+}
+
+// msk_stage split by derivative direction (k_msk_stagecoef_split): HALF 0 carries the nq q-directions through
+// everything (SQ = SV = Dual<nq>) and writes the coefficients that need them (the muscle coefficients, the q half of
+// d(base mult) and d qdd, -M^-1 J_L, M^-1); HALF 1 carries the nq qdot-directions only through the velocity-dependent
+// part (SQ = double: the frames, geometry and M are plain values) and writes the qdot half.  Each direction is the same
+// chain-rule expression as in msk_stage's Dual<2 nq> (per-direction arithmetic does not depend on how many directions
+// travel together), at about 3/5 of its registers.
+template <int NQ, int NM, int FAM, int HALF>
+__device__ __forceinline__ void msk_stage_half(const MskGeom& G, int residual, const double* xs, const double* u,
+                                               double* __restrict__ Ws, int64_t B) {
+    constexpr int NXM = msk_nxm<FAM>(), XQ = NM * NXM, XQD = XQ + NQ, ND = 2 * NQ;
+    constexpr int NUI = msk_nui<NM, FAM>(), OM = 6 + ND, ODQ = NM * OM, OB = ODQ + NQ * ND, OMI = OB + NQ * NM;
+    constexpr bool PW = msk_pw<FAM>();
+    using SV = Dual<NQ>;
+    using SQ = typename std::conditional<HALF == 0, Dual<NQ>, double>::type;
+    SQ q[NQ];
+    SV qd[NQ], F[NM], taur[NQ], mult[NM], qdd[NQ];
+#pragma unroll
+    for (int k = 0; k < NQ; ++k) {
+        if constexpr (HALF == 0) {
+            q[k] = dconst<NQ>(xs[XQ + k]);
+            q[k].d[k] = 1.0;
+            qd[k] = dconst<NQ>(xs[XQD + k]);
+        } else {
+            q[k] = xs[XQ + k];
+            qd[k] = dconst<NQ>(xs[XQD + k]);
+            qd[k].d[k] = 1.0;
+        }
+        taur[k] = dconst<NQ>(residual ? u[NUI + k] : 0.0);
+    }
+#pragma unroll
+    for (int mu = 0; mu < NM; ++mu) F[mu] = dconst<NQ>(xs[mu * NXM + 1]);
+    double Mv[NQ][NQ], JLv[NM][NQ];
+    msk_skeleton<NQ, NM>(G, q, qd, F, taur, mult, qdd, Mv, JLv);
+    constexpr int D0 = HALF == 0 ? 0 : NQ;  // the directions' slots among msk_stage's 2 nq
+#pragma unroll
+    for (int mu = 0; mu < NM; ++mu) {
+        const MskMuscleConst& C = G.mc[mu];
+        const double* xm = xs + mu * NXM;
+        double c[6], base, pw = 0.0;
+        if constexpr (PW) pw = u[mu];
+        msk_muscle_coef<FAM>(C, xm, pw, mult[mu].v, c, base);
+        if constexpr (HALF == 0) {
+#pragma unroll
+            for (int e = 0; e < 6; ++e) Ws[(mu * OM + e) * B] = c[e];
+        }
+#pragma unroll
+        for (int d = 0; d < NQ; ++d) Ws[(mu * OM + 6 + D0 + d) * B] = base * mult[mu].d[d];
+    }
+#pragma unroll
+    for (int i = 0; i < NQ; ++i)
+#pragma unroll
+        for (int d = 0; d < NQ; ++d) Ws[(ODQ + i * ND + D0 + d) * B] = qdd[i].d[d];
+    if constexpr (HALF == 0) {
+        double Mi[NQ][NQ];
+        msk_spd_inverse<NQ>(Mv, Mi);
+#pragma unroll
+        for (int i = 0; i < NQ; ++i) {
+#pragma unroll
+            for (int mu = 0; mu < NM; ++mu) {
+                double bsum = 0.0;
+#pragma unroll
+                for (int k = 0; k < NQ; ++k) bsum += Mi[i][k] * JLv[mu][k];
+                Ws[(OB + i * NM + mu) * B] = -bsum;
+            }
+#pragma unroll
+            for (int k = 0; k < NQ; ++k) Ws[(OMI + i * NQ + k) * B] = Mi[i][k];
+        }
     }
 }
 
@@ -1649,6 +1783,40 @@ __global__ void __launch_bounds__(256) k_msk_stagecoef_par(const MskParams P, co
         msk_stage_cs<NM, FAM>(P.cs, kq, nullptr, csl);
     }
     msk_stage<NQ, NM, FAM>(G, P.residual, csl, msk_cs1<NM>(P, kq), xs, u, f, P.scratch + kq * NC * B + b, B);
+}
+
+// k_msk_stagecoef_par with the derivative directions split over two threads (blockIdx.y: 0 the q-directions, 1 the
+// qdot-directions; msk_stage_half): the same coefficients, each from the same expression, at fewer registers per
+// thread.  The stage's calcium sum enters f only, which neither half forms.
+#ifndef CFX_MSK_SPLIT_WAVES
+#define CFX_MSK_SPLIT_WAVES 2  // waves per SIMD the split kernel is compiled for (the q half takes 272 registers free)
+#endif
+template <int NQ, int NM, int FAM>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CFX_MSK_SPLIT_WAVES, CFX_MSK_SPLIT_WAVES)))
+k_msk_stagecoef_split(const MskParams P, const MskGeom* __restrict__ GG,
+                                                             const double* __restrict__ V,
+                                                             const double* __restrict__ XS) {
+    constexpr int NXM = msk_nxm<FAM>(), NX = NM * NXM + 2 * NQ;
+    constexpr int NUMAX = msk_numax<NQ, NM, FAM>();
+    constexpr int NC = msk_ncoef<NQ, NM>();
+    const int64_t B = P.B;
+    const int64_t item = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (item >= B * P.N * P.Q) return;
+    const int64_t b = item % B, kq = item / B;
+    const int k = (int)(kq / P.Q);
+    const MskGeom& G = *GG;
+    const int64_t zb = (int64_t)k * P.nz;
+    double xs[NX], u[NUMAX];
+#pragma unroll
+    for (int r = 0; r < NX; ++r) xs[r] = XS[(kq * NX + r) * B + b];
+#pragma unroll
+    for (int i = 0; i < NUMAX; ++i) {
+        const int dc = msk_udec<NM, FAM>(i, P.T, P.nu);
+        u[i] = dc >= 0 ? V[(zb + NX + dc) * B + b] : 0.0;
+    }
+    double* Ws = P.scratch + kq * NC * B + b;
+    if (blockIdx.y == 0) msk_stage_half<NQ, NM, FAM, 0>(G, P.residual, xs, u, Ws, B);
+    else msk_stage_half<NQ, NM, FAM, 1>(G, P.residual, xs, u, Ws, B);
 }
 
 // one stage's term T_q^T (G_q T_q[:, a]) of k_msk_hproj (thread = instance, column a, interval-stage kq)

@@ -4,6 +4,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <string>
 
 #include "cfx_msk_launch.h"
 
@@ -26,6 +27,23 @@ void dep_t(const MskParams& P, const MskGeom& G, uint64_t* dep) {
     for (int r = 0; r < NX; ++r) dep[r] = x[r].m;
 }
 
+// Stage coefficients: one thread per stage (k_msk_stagecoef_par, the default) or per stage and half of the derivative
+// directions (k_msk_stagecoef_split, CFX_MSK_STAGE=split).  cfg 5 at B = 65,536 (profiles/round5/msk_stage/): 0.563 vs
+// 0.553 ms per call, g + J_g 1.405-1.426 vs 1.409-1.424 ms over three runs each — the halves' extra value work eats
+// what the second wave per SIMD gains, so the simpler kernel stays the default.
+inline bool msk_stage_split() {  // read at every launch, so a test can compare both kernels in one process
+    const char* e = std::getenv("CFX_MSK_STAGE");
+    return e && std::string(e) == "split";
+}
+template <int NQ, int NM, int FAM>
+void msk_stagecoef(const MskParams& P, const MskGeom* G, const double* V, const double* XS, hipStream_t s) {
+    const unsigned g = (unsigned)((P.B * P.N * P.Q + kMskBlk - 1) / kMskBlk);
+    if (msk_stage_split())
+        hipLaunchKernelGGL((k_msk_stagecoef_split<NQ, NM, FAM>), dim3(g, 2), dim3(kMskBlk), 0, s, P, G, V, XS);
+    else
+        hipLaunchKernelGGL((k_msk_stagecoef_par<NQ, NM, FAM>), dim3(g), dim3(kMskBlk), 0, s, P, G, V, XS);
+}
+
 template <int NQ, int NM, int FAM, int SCHEME>
 hipError_t shoot_t(const MskParams& P, const MskGeom* G, const double* V, double* Gout, double* J, bool keep_xs,
                    hipStream_t s) {
@@ -42,8 +60,7 @@ hipError_t shoot_t(const MskParams& P, const MskGeom* G, const double* V, double
     (void)keep_xs;  // the stage values are always left in XS
     hipLaunchKernelGGL((k_msk_values<NQ, NM, FAM, SCHEME>), dim3(gx, (unsigned)P.N), dim3(kMskBlk), 0, s, P, G, V, Gout,
                        XS);
-    hipLaunchKernelGGL((k_msk_stagecoef_par<NQ, NM, FAM>), dim3((unsigned)((P.B * P.N * P.Q + kMskBlk - 1) / kMskBlk)),
-                       dim3(kMskBlk), 0, s, P, G, V, (const double*)XS);
+    msk_stagecoef<NQ, NM, FAM>(P, G, V, XS, s);
     if (P.nz <= kMskLdsCols) {  // coefficients through LDS, one block per TW instances
         constexpr int ST = SCHEME == 4 ? 4 : (SCHEME == 2 ? 2 : 1), TW = kMskTangentInstances;  // cfx_msk_create's kpb
         const int64_t nbx = (P.B + TW - 1) / TW;
@@ -92,8 +109,7 @@ hipError_t hess_t(const MskParams& P, const MskGeom* G, const int16_t* tasks, in
     if (!reuse) {  // stage values and coefficients (reuse: left by the g + J_g launch at this point)
         hipLaunchKernelGGL((k_msk_values<NQ, NM, FAM, SCHEME>), dim3(gx, (unsigned)P.N), dim3(kMskBlk), 0, s, Pw, G, V,
                            (double*)nullptr, XS);
-        hipLaunchKernelGGL((k_msk_stagecoef_par<NQ, NM, FAM>), flat(BNQ), dim3(kMskBlk), 0, s, Pw, G, V,
-                           (const double*)XS);
+        msk_stagecoef<NQ, NM, FAM>(Pw, G, V, XS, s);
     }
     hipLaunchKernelGGL((k_msk_htan<NQ, NM, FAM, SCHEME>), flat(P.B * P.N * P.nz), dim3(kMskBlk), 0, s, Pw, G, V, TS);
     hipLaunchKernelGGL((k_msk_hadj<NQ, NM, FAM, SCHEME>), flat(P.B * P.N), dim3(kMskBlk), 0, s, Pw, G, LAM, MU);

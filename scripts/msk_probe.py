@@ -59,6 +59,7 @@ def main():
     ap.add_argument("--batch", type=int, nargs="+", default=[4096, 65536])
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--libs", nargs="*", default=[])
+    ap.add_argument("--dump", default=None, help="save g and J_g of the first batch's first 256 instances here (.npz), for A/B comparisons")
     a = ap.parse_args()
     from cocofest_amd import _cfx
 
@@ -74,6 +75,8 @@ def main():
             g = torch.empty((h.ng, B), dtype=torch.float64, device="cuda")
             j = torch.empty((h.nnz_jac, B), dtype=torch.float64, device="cuda")
             t_gj = timeit(lambda: h.eval_all(v, g=g, jac=j), a.reps)
+            if a.dump and B == a.batch[0]:
+                np.savez(a.dump, g=g[:, :256].cpu().numpy(), j=j[:, :256].cpu().numpy())
             t_g = timeit(lambda: h.eval_all(v, g=g), a.reps)
             row = dict(lib=lib or "default", batch=B, nnz_jac=h.nnz_jac, ms_g_jac=t_gj, ms_g=t_g,
                        evals_per_s=B / t_gj * 1e3, GBps=B * 8 * (h.nv + h.ng + h.nnz_jac) / t_gj / 1e6)

@@ -445,6 +445,33 @@ def test_msk_small_and_large_batch_paths_agree(case):
         assert np.max(np.abs(a - b_) / scale) < 1e-12
 
 
+@pytest.mark.parametrize("case", ["cfg5_d07f_rk4", "d07_rk1_residual"])
+def test_msk_stage_kernels_split_by_direction_agree(case, monkeypatch):
+    """k_msk_stagecoef_split (CFX_MSK_STAGE=split: the q- and qdot-directions of each stage in two threads) gives the
+    coefficients of k_msk_stagecoef_par from the same per-direction expressions: g bit-identical, J_g and the
+    Lagrangian Hessian to rounding (the compiler may contract the two kernels' sums differently)."""
+    cfg = CASES[case]
+    ocp = MC.product_ocp(**cfg)
+    pb = MC.oracle_problem(**cfg)
+    B = 64
+    V = MC.random_decision(pb, B, seed=7)
+    lam = np.random.default_rng(8).normal(size=(B, pb.ng))
+    of = np.linspace(0.2, 1.5, B)
+    out = {}
+    for mode in ("par", "split"):
+        monkeypatch.setenv("CFX_MSK_STAGE", mode)
+        h = ocp.nlp(batch=B, layout="aos")
+        g, jac = np.empty((B, h.ng)), np.empty((B, h.nnz_jac))
+        h.eval_all(V.copy(), g=g, jac=jac)
+        hv = h.eval_h(V.copy(), of.copy(), lam.copy())
+        h.close()
+        out[mode] = (g, jac, hv)
+    np.testing.assert_array_equal(out["par"][0], out["split"][0])
+    for a, b_ in zip(out["par"][1:], out["split"][1:]):
+        scale = np.abs(a) + 1e-9 * np.abs(a).max()
+        assert np.max(np.abs(a - b_) / scale) < 1e-12
+
+
 def test_msk_hmed_interior_point_converges():
     """The reference's Hmed MSK case (tests/shard2/test_fes_dynamics.py:104-183: arm26 biceps / triceps, Hmed2018 with
     fatigue, residual torque minimised, elbow 5 -> 120 deg, intensities in [I_min, 130]) at RK4 x 5 (RK4 x 1 is unstable
