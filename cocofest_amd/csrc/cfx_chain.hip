@@ -74,127 +74,172 @@ __device__ __forceinline__ void store_tile(double* __restrict__ C, int I, int J,
     for (int r = 0; r < 4; ++r) C[(16 * I + (lane >> 4) + 4 * r) * SP + 16 * J + (lane & 15)] = v[r];
 }
 
+// Maximum of v over the 64 lanes (every lane gets it): DPP max-scan within rows of 16 lanes, row broadcasts to
+// lane 63, readlane.  Lanes a shift leaves without a source keep their own value.
+#define CFX_DPP_MAX(v, CTRL, RM, BM)                                                                              \
+    do {                                                                                                          \
+        const int lo_ = __double2loint(v), hi_ = __double2hiint(v);                                               \
+        const int slo_ = __builtin_amdgcn_update_dpp(lo_, lo_, CTRL, RM, BM, false);                              \
+        const int shi_ = __builtin_amdgcn_update_dpp(hi_, hi_, CTRL, RM, BM, false);                              \
+        v = fmax(v, __hiloint2double(shi_, slo_));                                                                \
+    } while (0)
+__device__ __forceinline__ double wave_max(double v) {
+    CFX_DPP_MAX(v, 0x111, 0xf, 0xf);  // row_shr:1
+    CFX_DPP_MAX(v, 0x112, 0xf, 0xf);  // row_shr:2
+    CFX_DPP_MAX(v, 0x114, 0xf, 0xf);  // row_shr:4
+    CFX_DPP_MAX(v, 0x118, 0xf, 0xf);  // row_shr:8  (lane 15 of each row: the row's maximum)
+    CFX_DPP_MAX(v, 0x142, 0xa, 0xf);  // row_bcast:15 into rows 1 and 3
+    CFX_DPP_MAX(v, 0x143, 0xc, 0xf);  // row_bcast:31 into rows 2 and 3 (lane 63: the wave's maximum)
+    const int lo = __builtin_amdgcn_readlane(__double2loint(v), 63), hi = __builtin_amdgcn_readlane(__double2hiint(v), 63);
+    return __hiloint2double(hi, lo);
+}
+
 constexpr int kNT = 256;  // threads per workgroup (4 waves)
 
 // Eliminate nodes i = first + step * blockIdx.x (instance blockIdx.y): D_i <- D_i^-1, L_i <- D_i^-1 L_i (when node
 // i - h exists), U_i <- D_i^-1 U_i (when node i + h exists).  A zero pivot sets info[b] (0-based slot + 1) if unset.
 template <int SP>
 __global__ void __launch_bounds__(kNT) k_chain_elim(Chain C, int first, int step, int h, int32_t* __restrict__ info) {
-    // In-place Gauss-Jordan with partial pivoting (first largest |A(r, k)|, r >= k; columns unscrambled at the end),
-    // the matrix in registers: thread t owns row t % SP and the columns cg + G c (cg = t / SP, G = kNT / SP groups).
-    // Per pivot column three barriers: the column (double-buffered, written by its owners at the end of the previous
-    // step) -> wave 0's argmax -> the pivot row and row k through LDS -> every thread updates its own entries.
-    constexpr int G = kNT / SP, CW = (SP + G - 1) / G, SPP = G * CW;  // SPP: columns padded to the groups
+    // In-place Gauss-Jordan with partial pivoting (largest |A(r, k)| over the rows not yet pivots, ties to the lowest
+    // row) without moving rows: step k pivots on physical row P_k, which is logical row k, so the array ends as
+    // (Q D)^-1 = D^-1 Q^T with Q the row order P, i.e. D^-1[k][j] = array[P_k][s_j], s_j the step at which row j was
+    // pivot (undone through LDS at the end).  The matrix sits in registers as 16 x 16 interleaved tiles: thread
+    // t = 16 tr + tc owns rows tr + 16 i and columns tc + 16 j (i, j < T = SP / 16), so a rank-1 step reads T
+    // multipliers and T pivot-row values from LDS for its T^2 entries, and every entry takes the same two multiplies
+    // and one FMA (selects per entry cost more than the arithmetic; the row-per-thread layout with explicit row swaps
+    // took 205 us per 80 x 80 block, this one ...).  Per pivot column: every wave finds the pivot itself (one 64-bit
+    // key per row, DPP max reduction, no barrier), the owners of row p stage it in LDS, barrier, every thread updates
+    // its tile and the owners of column k + 1 stage that column for the next step, barrier.
+    constexpr int T = SP / 16;
+    static_assert(SP % 16 == 0 && SP <= 128 && kNT == 256, "16 x 16 thread tiles; 7-bit row index in the pivot key");
     __shared__ double A[SP][SP + 1];
     __shared__ double colv[2][SP];
-    __shared__ double rowp[SPP], rowk[SPP];
-    __shared__ int piv[SP], perm[SP];
-    __shared__ int s_p;
+    __shared__ double rowp[SP];
+    __shared__ int prow[SP], pstep[SP];  // P_k (row pivoted at step k), s_j (step at which row j was pivot)
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
     const int i = first + step * blockIdx.x;
     const int64_t b = blockIdx.y;
     if (i >= C.M) return;
     constexpr int64_t NB = (int64_t)SP * SP;
     double* D = C.D + b * C.stride + i * NB;
-    const int row = t % SP, cg = min(t / SP, G - 1);
-    const bool own = t < G * SP;  // threads past G SP groups own nothing (they shadow the last group, never store)
-    double a[CW];
-#pragma unroll
-    for (int c = 0; c < CW; ++c) {
-        const int j = cg + G * c;
-        a[c] = j < SP ? D[(int64_t)row * SP + j] : 0.0;
+    // the survivors' pre-update couplings for this level's Schur update (k_chain_upd) and the solves:
+    // Cl_i = U_{i-h}, Cr_i = L_{i+h}; nothing else touches those blocks until k_chain_upd runs
+    if (i - h >= 0 || i + h < C.M) {
+        const double* Us = C.U + b * C.stride + (int64_t)(i - h) * NB;
+        const double* Ls = C.L + b * C.stride + (int64_t)(i + h) * NB;
+        double* Cl = C.Cl + b * C.wstride + i * NB;
+        double* Cr = C.Cr + b * C.wstride + i * NB;
+        const bool cl = i - h >= 0, cr = i + h < C.M;
+        for (int e = t; e < SP * SP; e += kNT) {
+            if (cl) Cl[e] = Us[e];
+            if (cr) Cr[e] = Ls[e];
+        }
     }
-    if (own && cg == 0) colv[0][row] = a[0];                           // column 0
-    for (int j = SP + t; j < SPP; j += kNT) rowp[j] = rowk[j] = 0.0;  // padding columns stay zero
+    const int tr = t >> 4, tc = t & 15;
+    double a[T][T];
+#pragma unroll
+    for (int ii = 0; ii < T; ++ii)
+#pragma unroll
+        for (int jj = 0; jj < T; ++jj) a[ii][jj] = D[(int64_t)(tr + 16 * ii) * SP + tc + 16 * jj];
+    if (tc == 0) {
+#pragma unroll
+        for (int ii = 0; ii < T; ++ii) colv[0][tr + 16 * ii] = a[ii][0];  // column 0
+    }
     __syncthreads();
     int sing = 0;
-    {
+    bool used0 = false, used1 = false;  // rows lane and lane + 64 already pivots (every wave tracks them)
 #pragma unroll 1
-        for (int k = 0; k < SP; ++k) {
-            const int par = k & 1;
-            if (wave == 0) {
-                double av = -1.0;
-                int ai = SP;
-                for (int r = k + lane; r < SP; r += 64) {
-                    const double v = fabs(colv[par][r]);
-                    if (v > av) av = v, ai = r;
-                }
+    for (int k = 0; k < SP; ++k) {
+        const int par = k & 1;
+        // pivot search: key = |v| with its 7 low mantissa bits replaced by 127 - r (the order of non-negative doubles
+        // is the order of their bits), -1 for rows already pivots; the wave maximum is the largest |v|, ties to the
+        // lowest r
+        double key = -1.0;
+        const double v0 = lane < SP ? colv[par][lane] : 0.0, v1 = lane + 64 < SP ? colv[par][lane + 64] : 0.0;
+        double fcol[T];  // this thread's rows of column k (issued with the pivot search's reads)
 #pragma unroll
-                for (int o = 32; o > 0; o >>= 1) {
-                    const double ov = __shfl_xor(av, o);
-                    const int oi = __shfl_xor(ai, o);
-                    if (ov > av || (ov == av && oi < ai)) av = ov, ai = oi;
-                }
-                if (lane == 0) s_p = piv[k] = ai;
-            }
-            __syncthreads();
-            const int p = s_p;
-            if (own && (row == p || row == k)) {
-                double* dst = row == p ? rowp : rowk;
-#pragma unroll
-                for (int c = 0; c < CW; ++c) dst[cg + G * c] = a[c];
-            }
-            __syncthreads();
-            const double pv = colv[par][p];
-            if (pv == 0.0 && !sing) sing = k + 1;
-            const double inv = pv != 0.0 ? 1.0 / pv : 0.0;
-            // row p now holds the old row k (its column-k value colv[k]); row k the scaled pivot row.  Branch-free:
-            // all LDS reads first, then selects
-            const bool isk = row == k, isp = row == p && p != k;
-            const double f = colv[par][isp ? k : row];
-            double pr[CW], rk[CW];
-#pragma unroll
-            for (int c = 0; c < CW; ++c) pr[c] = rowp[cg + G * c];
-#pragma unroll
-            for (int c = 0; c < CW; ++c) rk[c] = rowk[cg + G * c];
-            const int kn = k + 1;
-            double nxt = 0.0;
-#pragma unroll
-            for (int c = 0; c < CW; ++c) {
-                const int j = cg + G * c;
-                const double prc = (j == k ? 1.0 : pr[c]) * inv;
-                const double src = isp ? rk[c] : a[c];
-                const double upd = (j == k ? 0.0 : src) - f * prc;
-                a[c] = isk ? prc : upd;
-                nxt = (j == kn) ? a[c] : nxt;
-            }
-            // the next pivot column, by its owners, into the other buffer
-            if (own && kn < SP && cg == kn % G) colv[par ^ 1][row] = nxt;
-            __syncthreads();
+        for (int ii = 0; ii < T; ++ii) fcol[ii] = colv[par][tr + 16 * ii];
+        if (lane < SP && !used0) {
+            const uint64_t bits = (uint64_t)__double_as_longlong(fabs(v0));
+            key = __longlong_as_double((long long)((bits & ~0x7Full) | (uint64_t)(127 - lane)));
         }
-    }
-    // columns: final column j is the eliminated matrix's column perm[j] (the interchanges undone in reverse order)
-    if (t == 0) {
-        for (int j = 0; j < SP; ++j) perm[j] = j;
-        for (int k = SP - 1; k >= 0; --k) {
-            const int q = piv[k], tmp = perm[k];
-            perm[k] = perm[q];
-            perm[q] = tmp;
+        if (lane + 64 < SP && !used1) {
+            const uint64_t bits = (uint64_t)__double_as_longlong(fabs(v1));
+            key = fmax(key, __longlong_as_double((long long)((bits & ~0x7Full) | (uint64_t)(63 - lane))));
         }
-    }
-    if (own) {
+        key = wave_max(key);
+        const int p = 127 - (int)((uint64_t)__double_as_longlong(key) & 0x7Full);
+        used0 = used0 || p == lane;
+        used1 = used1 || p == lane + 64;
+        if (t == 0) prow[k] = p, pstep[p] = k;
+        const double pvl = p < 64 ? v0 : v1;  // the pivot value, from the lane that holds it
+        const int pl = p & 63;
+        const double pv = __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(pvl), pl),
+                                           __builtin_amdgcn_readlane(__double2loint(pvl), pl));
+        if (pv == 0.0 && !sing) sing = k + 1;
+        const double inv = pv != 0.0 ? 1.0 / pv : 0.0;
+        // row p to LDS (its owners: tr == p % 16).  ip, k and every tile index are wave-uniform: the branches below
+        // pick a register statically instead of a select chain over the tile (measured: the chains cost 30 of 92 us)
+        const int ip = p >> 4;
 #pragma unroll
-        for (int c = 0; c < CW; ++c) {
-            const int j = cg + G * c;
-            if (j < SP) A[row][j] = a[c];
+        for (int ii = 0; ii < T; ++ii)
+            if (ii == ip && tr == (p & 15)) {
+#pragma unroll
+                for (int jj = 0; jj < T; ++jj) rowp[tc + 16 * jj] = a[ii][jj];
+            }
+        __syncthreads();
+        // every row r -= A(r, k) x the scaled pivot row; then column k becomes -A(r, k) / pv and row p the scaled
+        // pivot row (column k: 1 / pv)
+        double prc[T];
+#pragma unroll
+        for (int jj = 0; jj < T; ++jj) {
+            const int c = tc + 16 * jj;
+            prc[jj] = (c == k ? 1.0 : rowp[c]) * inv;
         }
+#pragma unroll
+        for (int ii = 0; ii < T; ++ii)
+#pragma unroll
+            for (int jj = 0; jj < T; ++jj) a[ii][jj] = fma(-fcol[ii], prc[jj], a[ii][jj]);
+        const int jk = k >> 4;
+#pragma unroll
+        for (int jj = 0; jj < T; ++jj)
+            if (jj == jk) {
+                const bool own = tc == (k & 15);
+#pragma unroll
+                for (int ii = 0; ii < T; ++ii) a[ii][jj] = own ? -fcol[ii] * prc[jj] : a[ii][jj];
+            }
+#pragma unroll
+        for (int ii = 0; ii < T; ++ii)
+            if (ii == ip) {
+                const bool own = tr == (p & 15);
+#pragma unroll
+                for (int jj = 0; jj < T; ++jj) a[ii][jj] = own ? prc[jj] : a[ii][jj];
+            }
+        // the next pivot column, by its owners, into the other buffer
+        const int kn = k + 1, jn = kn >> 4;
+#pragma unroll
+        for (int jj = 0; jj < T; ++jj)
+            if (jj == jn && kn < SP && tc == (kn & 15)) {
+#pragma unroll
+                for (int ii = 0; ii < T; ++ii) colv[par ^ 1][tr + 16 * ii] = a[ii][jj];
+            }
+        __syncthreads();
     }
+    // D^-1[r][c] = array[P_r][s_c]
+#pragma unroll
+    for (int ii = 0; ii < T; ++ii)
+#pragma unroll
+        for (int jj = 0; jj < T; ++jj) A[tr + 16 * ii][tc + 16 * jj] = a[ii][jj];
     __syncthreads();
-    if (own) {
 #pragma unroll
-        for (int c = 0; c < CW; ++c) {
-            const int j = cg + G * c;
-            if (j < SP) a[c] = A[row][perm[j]];
-        }
-    }
+    for (int ii = 0; ii < T; ++ii)
+#pragma unroll
+        for (int jj = 0; jj < T; ++jj) a[ii][jj] = A[prow[tr + 16 * ii]][pstep[tc + 16 * jj]];
     __syncthreads();
-    if (own) {
 #pragma unroll
-        for (int c = 0; c < CW; ++c) {
-            const int j = cg + G * c;
-            if (j < SP) A[row][j] = a[c];
-        }
-    }
+    for (int ii = 0; ii < T; ++ii)
+#pragma unroll
+        for (int jj = 0; jj < T; ++jj) A[tr + 16 * ii][tc + 16 * jj] = a[ii][jj];
     __syncthreads();
     if (t == 0 && sing && info && info[b] == 0) info[b] = (int32_t)(i * SP + sing);
     for (int e = t; e < SP * SP; e += kNT) D[e] = A[e / SP][e % SP];
@@ -217,76 +262,91 @@ __global__ void __launch_bounds__(kNT) k_chain_elim(Chain C, int first, int step
 }
 
 // Survivors p = 2 h blockIdx.x of level h (instance blockIdx.y) take the Schur complement of their eliminated
-// neighbours i = p + h and j = p - h.  The pre-update U_p / L_p are copied to Cl_i / Cr_j first; every product reads
-// its left operand from those copies, so the in-place updates of U_p / L_p never race with their reads.
+// neighbours i = p + h and j = p - h, in three workgroups per survivor (blockIdx.z):
+//   0: D_p -= Cl_i X_i + Cr_j Y_j      1: U_p <- -Cl_i Y_i (zero without node p + 2h)      2: L_p <- -Cr_j X_j
+// where Cl_i / Cr_j are the pre-update U_p / L_p, copied by the elimination kernel of this level — so no workgroup
+// reads what another writes.  Each product stages its two operands in LDS (the left operand read by every tile, the
+// right one too when both fit: SP <= 96) and spreads its 16 x 16 output tiles over the four waves; the sums run in
+// the order of one K loop per product, products in the order above.  (Round 5 first version: one workgroup per
+// survivor, left operands read from global memory per MFMA, output column blocks per wave — 115 us per tail level
+// for SP = 80, where the FP64 matrix cores need ~7.)
+template <int SP>
+constexpr bool chain_b_in_lds() {
+    return 2 * SP * (SP + 1) * 8 <= 150 * 1024;
+}
+template <int SP>
+constexpr size_t chain_upd_lds() {
+    return (size_t)(chain_b_in_lds<SP>() ? 2 : 1) * SP * (SP + 1) * sizeof(double);
+}
 template <int SP>
 __global__ void __launch_bounds__(kNT) k_chain_upd(Chain C, int h) {
-    const int t = threadIdx.x, wave = t >> 6;
-    const int p = 2 * h * blockIdx.x;
+    constexpr int T16 = SP / 16, NT = T16 * T16, TPW = (NT + 3) / 4;  // output tiles, per wave
+    constexpr int LD = SP + 1;
+    constexpr bool BL = chain_b_in_lds<SP>();
+    extern __shared__ double sm[];
+    double* sA = sm;
+    double* sB = sm + SP * LD;
+    const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
+    const int p = 2 * h * blockIdx.x, part = blockIdx.z;
     const int64_t b = blockIdx.y;
     if (p >= C.M) return;
     constexpr int64_t NB = (int64_t)SP * SP;
     const int i = p + h, j = p - h;
     const bool hi = i < C.M, hj = j >= 0;
     const bool hyi = hi && i + h < C.M;  // Y_i exists (node i + h = p + 2h)
-    double* Dp = C.D + b * C.stride + p * NB;
-    double* Up = C.U + b * C.stride + p * NB;
-    double* Lp = C.L + b * C.stride + p * NB;
-    double* Cli = hi ? C.Cl + b * C.wstride + i * NB : nullptr;
-    double* Crj = hj ? C.Cr + b * C.wstride + j * NB : nullptr;
-    for (int e = t; e < SP * SP; e += kNT) {
-        if (hi) Cli[e] = Up[e];
-        if (hj) Crj[e] = Lp[e];
-    }
-    __threadfence_block();
-    __syncthreads();
-    const double* Xi = hi ? C.L + b * C.stride + i * NB : nullptr;
-    const double* Yi = hyi ? C.U + b * C.stride + i * NB : nullptr;
-    const double* Xj = hj ? C.L + b * C.stride + j * NB : nullptr;
-    const double* Yj = hj ? C.U + b * C.stride + j * NB : nullptr;
-    auto cl_at = [&](int r, int c) { return Cli[r * SP + c]; };
-    auto cr_at = [&](int r, int c) { return Crj[r * SP + c]; };
-    for (int J = wave; J < SP / 16; J += kNT / 64) {
-        double breg[SP / 4];
-        d4 accD[SP / 16];
+    if ((part == 0 && !hi && !hj) || (part == 1 && !hi) || (part == 2 && !hj)) return;
+    const double* Cli = hi ? C.Cl + b * C.wstride + i * NB : nullptr;
+    const double* Crj = hj ? C.Cr + b * C.wstride + j * NB : nullptr;
+    d4 acc[TPW];
 #pragma unroll
-        for (int I = 0; I < SP / 16; ++I) accD[I] = d4{0.0, 0.0, 0.0, 0.0};
-        if (hi) {  // D_p -= U_p X_i
-            load_bcol<SP>(Xi, J, breg);
-#pragma unroll
-            for (int I = 0; I < SP / 16; ++I) accD[I] = tile_mm<SP>(cl_at, breg, I, accD[I]);
+    for (int q = 0; q < TPW; ++q) acc[q] = d4{0.0, 0.0, 0.0, 0.0};
+    // acc[q] += A Bm over the wave's tiles q (tile wave + 4 q: I = tile / T16, J = tile % T16)
+    auto product = [&](const double* __restrict__ Ag, const double* __restrict__ Bg) {
+        __syncthreads();  // the previous product's readers are done with the buffers
+        for (int e = t; e < SP * SP; e += kNT) {
+            const int r = e / SP, c = e - r * SP;
+            sA[r * LD + c] = Ag[e];
+            if constexpr (BL) sB[r * LD + c] = Bg[e];
         }
-        if (hj) {  // D_p -= L_p Y_j
-            load_bcol<SP>(Yj, J, breg);
+        __syncthreads();
 #pragma unroll
-            for (int I = 0; I < SP / 16; ++I) accD[I] = tile_mm<SP>(cr_at, breg, I, accD[I]);
-        }
-        if (hi || hj) {
-            const int lane = t & 63;
+        for (int q = 0; q < TPW; ++q) {
+            const int tile = wave + 4 * q;
+            if (tile < NT) {
+                const int I = tile / T16, J = tile % T16;
+                const int ra = 16 * I + (lane & 15), kq = lane >> 4, cb = 16 * J + (lane & 15);
+                d4 a = acc[q];
 #pragma unroll
-            for (int I = 0; I < SP / 16; ++I)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int64_t e = (16 * I + (lane >> 4) + 4 * r) * SP + 16 * J + (lane & 15);
-                    Dp[e] -= accD[I][r];
+                for (int kk = 0; kk < SP / 4; ++kk) {
+                    const double bv = BL ? sB[(4 * kk + kq) * LD + cb] : Bg[(4 * kk + kq) * SP + cb];
+                    a = __builtin_amdgcn_mfma_f64_16x16x4f64(sA[ra * LD + 4 * kk + kq], bv, a, 0, 0, 0);
                 }
-        }
-        if (hi) {  // U_p <- -U_p Y_i (zero when node p + 2h does not exist)
-            if (hyi) load_bcol<SP>(Yi, J, breg);
-#pragma unroll 1
-            for (int I = 0; I < SP / 16; ++I) {
-                d4 acc = {0.0, 0.0, 0.0, 0.0};
-                if (hyi) acc = tile_mm<SP>(cl_at, breg, I, acc);
-                store_tile<SP>(Up, I, J, -acc);
+                acc[q] = a;
             }
         }
-        if (hj) {  // L_p <- -L_p X_j
-            load_bcol<SP>(Xj, J, breg);
-#pragma unroll 1
-            for (int I = 0; I < SP / 16; ++I) {
-                d4 acc = {0.0, 0.0, 0.0, 0.0};
-                acc = tile_mm<SP>(cr_at, breg, I, acc);
-                store_tile<SP>(Lp, I, J, -acc);
+    };
+    double* out;
+    if (part == 0) {
+        if (hi) product(Cli, C.L + b * C.stride + i * NB);  // Cl_i X_i
+        if (hj) product(Crj, C.U + b * C.stride + j * NB);  // Cr_j Y_j
+        out = C.D + b * C.stride + p * NB;
+    } else if (part == 1) {
+        if (hyi) product(Cli, C.U + b * C.stride + i * NB);  // Cl_i Y_i
+        out = C.U + b * C.stride + p * NB;
+    } else {
+        product(Crj, C.L + b * C.stride + j * NB);  // Cr_j X_j
+        out = C.L + b * C.stride + p * NB;
+    }
+#pragma unroll
+    for (int q = 0; q < TPW; ++q) {
+        const int tile = wave + 4 * q;
+        if (tile < NT) {
+            const int I = tile / T16, J = tile % T16;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int64_t e = (16 * I + (lane >> 4) + 4 * r) * SP + 16 * J + (lane & 15);
+                if (part == 0) out[e] -= acc[q][r];
+                else out[e] = -acc[q][r];
             }
         }
     }
@@ -391,11 +451,17 @@ static int levels(int M) {
 template <int SP>
 static hipError_t factor_sp(const Chain& C, int64_t B, int32_t* info, hipStream_t s) {
     const int L = levels(C.M);
+    if (chain_upd_lds<SP>() > 65536) {  // above the default dynamic LDS limit: raised once per kernel
+        static const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_chain_upd<SP>),
+                                                        hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                        (int)chain_upd_lds<SP>());
+        if (e != hipSuccess) return e;
+    }
     for (int l = 0; l < L; ++l) {
         const int h = 1 << l;
         const int ne = (C.M - h + 2 * h - 1) / (2 * h), ns = (C.M + 2 * h - 1) / (2 * h);
         hipLaunchKernelGGL(k_chain_elim<SP>, dim3((unsigned)ne, (unsigned)B), dim3(kNT), 0, s, C, h, 2 * h, h, info);
-        hipLaunchKernelGGL(k_chain_upd<SP>, dim3((unsigned)ns, (unsigned)B), dim3(kNT), 0, s, C, h);
+        hipLaunchKernelGGL(k_chain_upd<SP>, dim3((unsigned)ns, (unsigned)B, 3), dim3(kNT), chain_upd_lds<SP>(), s, C, h);
     }
     hipLaunchKernelGGL(k_chain_elim<SP>, dim3(1, (unsigned)B), dim3(kNT), 0, s, C, 0, 1, 1 << L, info);
     return hipGetLastError();

@@ -30,6 +30,8 @@ int main(int argc, char** argv) {
     CK(hipEventCreate(&a));
     CK(hipEventCreate(&b));
     const cfx_chain::Chain C{d, d + nb, d + 2 * nb, w, w + nb, 0, 0, M};
+    CK(hipFuncSetAttribute(reinterpret_cast<const void*>(&cfx_chain::k_chain_upd<SP>),
+                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)cfx_chain::chain_upd_lds<SP>()));
     for (int rep = 0; rep < 3; ++rep) {
         CK(hipMemcpy(d, h.data(), 3 * nb * sizeof(double), hipMemcpyHostToDevice));
         float tot = 0;
@@ -42,7 +44,7 @@ int main(int argc, char** argv) {
             CK(hipEventSynchronize(b));
             CK(hipEventElapsedTime(&te, a, b));
             CK(hipEventRecord(a));
-            hipLaunchKernelGGL(cfx_chain::k_chain_upd<SP>, dim3(ns, 1), dim3(256), 0, 0, C, hh);
+            hipLaunchKernelGGL(cfx_chain::k_chain_upd<SP>, dim3(ns, 1, 3), dim3(256), cfx_chain::chain_upd_lds<SP>(), 0, C, hh);
             CK(hipEventRecord(b));
             CK(hipEventSynchronize(b));
             CK(hipEventElapsedTime(&tu, a, b));
