@@ -20,15 +20,17 @@
 // v_mfma_f64_16x16x4f64), and each survivor p = 0 mod 2h takes the Schur complement of its two eliminated neighbours
 // i = p + h, j = p - h:
 //     D_p -= U_p X_i + L_p Y_j,   U_p <- -U_p Y_i  (now coupling to p + 2h),   L_p <- -L_p X_j  (to p - 2h)
-// four SP x SP x SP products on the matrix cores.  The pre-update U_p, L_p are kept (Cl_i, Cr_j) for the solves.
+// four SP x SP x SP products on the matrix cores.  The updated couplings go to work slots (cur_u / cur_l below), so
+// the pre-update U_p, L_p stay in place for the solves.
 // After the last level node 0 alone remains and is inverted.  Level 0 of the reaching task (M = 1,501, SP = 80) runs
 // 750 eliminations side by side: the chip is full where the band factorisation ran one workgroup.
-// Solve: forward over the levels (t_i = D_i^-1 r_i, r_p -= Cl_i t_i + Cr_j t_j), x_0 = D_0^-1 r_0, backward
+// Solve: forward over the levels (t_i = D_i^-1 r_i, r_p -= U_p t_i + L_p t_j), x_0 = D_0^-1 r_0, backward
 // (x_i = t_i - X_i x_{i-h} - Y_i x_{i+h}).
 //
 // Storage (per instance, instance stride `stride` doubles): D [M][SP][SP], L [M][SP][SP], U [M][SP][SP], row-major.
-// After the factorisation D_k holds D_k^-1 of the level where node k was eliminated, L_k / U_k of an eliminated node
-// hold X_k / Y_k; work (per instance `wstride`): Cl [M][SP][SP], Cr [M][SP][SP].
+// Work (per instance `wstride`): Cl [M][SP][SP], Cr [M][SP][SP].  After the factorisation D_k holds D_k^-1 of the
+// level where node k was eliminated, and node k's couplings at that level (cur_u / cur_l: in U / L for level 0, in
+// Cl / Cr above) hold X_k / Y_k.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -47,6 +49,22 @@ struct Chain {
     int64_t stride, wstride;
     int M;
 };
+
+// Where node k's couplings live at the start of level h (h = 1: the input blocks; after level h / 2 the Schur update
+// wrote them to the work slot of the node it eliminated: U_k to Cl[k + h/2], L_k to Cr[k - h/2]).  A node eliminated
+// at level h keeps X_k = D_k^-1 L_k, Y_k = D_k^-1 U_k in those same places, and the pre-update couplings a survivor's
+// solve step needs stay where they are — no block is copied.  Work slot Cl[x] (Cr[x]) is written at one level only,
+// the one at which x is eliminated.
+template <int SP>
+__device__ __forceinline__ double* cur_u(const Chain& C, int64_t b, int k, int h) {
+    constexpr int64_t NB = (int64_t)SP * SP;
+    return h == 1 ? C.U + b * C.stride + k * NB : C.Cl + b * C.wstride + (k + h / 2) * NB;
+}
+template <int SP>
+__device__ __forceinline__ double* cur_l(const Chain& C, int64_t b, int k, int h) {
+    constexpr int64_t NB = (int64_t)SP * SP;
+    return h == 1 ? C.L + b * C.stride + k * NB : C.Cr + b * C.wstride + (k - h / 2) * NB;
+}
 
 // One 16 x 16 tile of C = A B over K = SP (A row-major lda, B row-major ldb), B's column block in registers:
 // breg[kk] = B[4 kk + (lane >> 4)][16 J + (lane & 15)].  v_mfma_f64_16x16x4f64: lane l holds A[l & 15][l >> 4] and
@@ -122,19 +140,6 @@ __global__ void __launch_bounds__(kNT) k_chain_elim(Chain C, int first, int step
     if (i >= C.M) return;
     constexpr int64_t NB = (int64_t)SP * SP;
     double* D = C.D + b * C.stride + i * NB;
-    // the survivors' pre-update couplings for this level's Schur update (k_chain_upd) and the solves:
-    // Cl_i = U_{i-h}, Cr_i = L_{i+h}; nothing else touches those blocks until k_chain_upd runs
-    if (i - h >= 0 || i + h < C.M) {
-        const double* Us = C.U + b * C.stride + (int64_t)(i - h) * NB;
-        const double* Ls = C.L + b * C.stride + (int64_t)(i + h) * NB;
-        double* Cl = C.Cl + b * C.wstride + i * NB;
-        double* Cr = C.Cr + b * C.wstride + i * NB;
-        const bool cl = i - h >= 0, cr = i + h < C.M;
-        for (int e = t; e < SP * SP; e += kNT) {
-            if (cl) Cl[e] = Us[e];
-            if (cr) Cr[e] = Ls[e];
-        }
-    }
     const int tr = t >> 4, tc = t & 15;
     double a[T][T];
 #pragma unroll
@@ -243,29 +248,30 @@ __global__ void __launch_bounds__(kNT) k_chain_elim(Chain C, int first, int step
     __syncthreads();
     if (t == 0 && sing && info && info[b] == 0) info[b] = (int32_t)(i * SP + sing);
     for (int e = t; e < SP * SP; e += kNT) D[e] = A[e / SP][e % SP];
-    // X_i = D_i^-1 L_i, Y_i = D_i^-1 U_i in place: a wave owns whole column blocks J (read into registers first)
+    // X_i = D_i^-1 L_i, Y_i = D_i^-1 U_i in place: items (side, column block J) over the waves, each read into
+    // registers before its tiles are stored
     auto a_at = [&](int r, int c) { return A[r][c]; };
-    for (int side = 0; side < 2; ++side) {
-        if (side == 0 ? i - h < 0 : i + h >= C.M) continue;
-        double* Bm = (side == 0 ? C.L : C.U) + b * C.stride + i * NB;
-        for (int J = wave; J < SP / 16; J += kNT / 64) {
-            double breg[SP / 4];
-            load_bcol<SP>(Bm, J, breg);
+    const bool xl = i - h >= 0, yu = i + h < C.M;
+    for (int it = wave; it < 2 * (SP / 16); it += kNT / 64) {
+        const int side = it / (SP / 16), J = it % (SP / 16);
+        if (side == 0 ? !xl : !yu) continue;
+        double* Bm = side == 0 ? cur_l<SP>(C, b, i, h) : cur_u<SP>(C, b, i, h);
+        double breg[SP / 4];
+        load_bcol<SP>(Bm, J, breg);
 #pragma unroll 1
-            for (int I = 0; I < SP / 16; ++I) {
-                d4 acc = {0.0, 0.0, 0.0, 0.0};
-                acc = tile_mm<SP>(a_at, breg, I, acc);
-                store_tile<SP>(Bm, I, J, acc);
-            }
+        for (int I = 0; I < SP / 16; ++I) {
+            d4 acc = {0.0, 0.0, 0.0, 0.0};
+            acc = tile_mm<SP>(a_at, breg, I, acc);
+            store_tile<SP>(Bm, I, J, acc);
         }
     }
 }
 
 // Survivors p = 2 h blockIdx.x of level h (instance blockIdx.y) take the Schur complement of their eliminated
 // neighbours i = p + h and j = p - h, in three workgroups per survivor (blockIdx.z):
-//   0: D_p -= Cl_i X_i + Cr_j Y_j      1: U_p <- -Cl_i Y_i (zero without node p + 2h)      2: L_p <- -Cr_j X_j
-// where Cl_i / Cr_j are the pre-update U_p / L_p, copied by the elimination kernel of this level — so no workgroup
-// reads what another writes.  Each product stages its two operands in LDS (the left operand read by every tile, the
+//   0: D_p -= U_p X_i + L_p Y_j      1: U_p' = -U_p Y_i (zero without node p + 2h)      2: L_p' = -L_p X_j
+// with U_p' / L_p' written to the work slots Cl[i] / Cr[j] (cur_u / cur_l), so no workgroup reads what another
+// writes and U_p / L_p stay for the solves.  Each product stages its two operands in LDS (the left operand read by every tile, the
 // right one too when both fit: SP <= 96) and spreads its 16 x 16 output tiles over the four waves; the sums run in
 // the order of one K loop per product, products in the order above.  (Round 5 first version: one workgroup per
 // survivor, left operands read from global memory per MFMA, output column blocks per wave — 115 us per tail level
@@ -295,8 +301,8 @@ __global__ void __launch_bounds__(kNT) k_chain_upd(Chain C, int h) {
     const bool hi = i < C.M, hj = j >= 0;
     const bool hyi = hi && i + h < C.M;  // Y_i exists (node i + h = p + 2h)
     if ((part == 0 && !hi && !hj) || (part == 1 && !hi) || (part == 2 && !hj)) return;
-    const double* Cli = hi ? C.Cl + b * C.wstride + i * NB : nullptr;
-    const double* Crj = hj ? C.Cr + b * C.wstride + j * NB : nullptr;
+    const double* Up = hi ? cur_u<SP>(C, b, p, h) : nullptr;  // the pre-update couplings (stay in place)
+    const double* Lp = hj ? cur_l<SP>(C, b, p, h) : nullptr;
     d4 acc[TPW];
 #pragma unroll
     for (int q = 0; q < TPW; ++q) acc[q] = d4{0.0, 0.0, 0.0, 0.0};
@@ -327,15 +333,15 @@ __global__ void __launch_bounds__(kNT) k_chain_upd(Chain C, int h) {
     };
     double* out;
     if (part == 0) {
-        if (hi) product(Cli, C.L + b * C.stride + i * NB);  // Cl_i X_i
-        if (hj) product(Crj, C.U + b * C.stride + j * NB);  // Cr_j Y_j
+        if (hi) product(Up, cur_l<SP>(C, b, i, h));  // U_p X_i
+        if (hj) product(Lp, cur_u<SP>(C, b, j, h));  // L_p Y_j
         out = C.D + b * C.stride + p * NB;
     } else if (part == 1) {
-        if (hyi) product(Cli, C.U + b * C.stride + i * NB);  // Cl_i Y_i
-        out = C.U + b * C.stride + p * NB;
+        if (hyi) product(Up, cur_u<SP>(C, b, i, h));  // U_p Y_i
+        out = C.Cl + b * C.wstride + i * NB;            // = cur_u(p, 2h)
     } else {
-        product(Crj, C.L + b * C.stride + j * NB);  // Cr_j X_j
-        out = C.L + b * C.stride + p * NB;
+        product(Lp, cur_l<SP>(C, b, j, h));  // L_p X_j
+        out = C.Cr + b * C.wstride + j * NB;  // = cur_l(p, 2h)
     }
 #pragma unroll
     for (int q = 0; q < TPW; ++q) {
@@ -400,8 +406,8 @@ __global__ void __launch_bounds__(kNT) k_chain_fwd(Chain C, Rhs X, int h) {
     __syncthreads();
     if (t < SP && (hi || hj)) {
         double acc = R[(int64_t)p * SP + t];
-        if (hi) acc -= row_dot<SP>(C.Cl + b * C.wstride + i * NB, t, ti);
-        if (hj) acc -= row_dot<SP>(C.Cr + b * C.wstride + j * NB, t, tj);
+        if (hi) acc -= row_dot<SP>(cur_u<SP>(C, b, p, h), t, ti);
+        if (hj) acc -= row_dot<SP>(cur_l<SP>(C, b, p, h), t, tj);
         R[(int64_t)p * SP + t] = acc;
     }
 }
@@ -426,7 +432,6 @@ __global__ void __launch_bounds__(kNT) k_chain_bwd(Chain C, Rhs X, int h) {
     const int i = h + 2 * h * blockIdx.x;
     const int64_t b = blockIdx.z, c = blockIdx.y;
     if (i >= C.M) return;
-    constexpr int64_t NB = (int64_t)SP * SP;
     const bool hr = i + h < C.M;
     double* R = X.R + b * X.r_inst + c * X.r_rhs;
     const double* T = X.T + b * X.t_inst + c * X.t_rhs;
@@ -436,8 +441,8 @@ __global__ void __launch_bounds__(kNT) k_chain_bwd(Chain C, Rhs X, int h) {
     }
     __syncthreads();
     if (t < SP) {
-        double acc = T[(int64_t)i * SP + t] - row_dot<SP>(C.L + b * C.stride + i * NB, t, xl);
-        if (hr) acc -= row_dot<SP>(C.U + b * C.stride + i * NB, t, xr);
+        double acc = T[(int64_t)i * SP + t] - row_dot<SP>(cur_l<SP>(C, b, i, h), t, xl);
+        if (hr) acc -= row_dot<SP>(cur_u<SP>(C, b, i, h), t, xr);
         R[(int64_t)i * SP + t] = acc;
     }
 }

@@ -324,7 +324,7 @@ int cfx_band_lu_solve(int64_t n, int32_t kl, int32_t ku, int64_t batch, const do
    sp x sp each (sp a multiple of 16, <= 128), row-major, device pointers:
      D [B][M][sp][sp] diagonal blocks, L [B][M][sp][sp] blocks (k, k-1) (L[.][0] unused), U [B][M][sp][sp] blocks
      (k, k+1) (U[.][M-1] unused), work [2][B][M][sp][sp];  info [B]: 0, or the 1-based unknown of a zero pivot
-   cfx_btri_factor overwrites D / L / U with the factors (no pivoting across blocks: each pivot block is inverted with
+   cfx_btri_factor overwrites D / L / U and fills work with the factors (no pivoting across blocks: each pivot block is inverted with
    partial pivoting, so the systems must have nonsingular pivot blocks, as the KKT matrices cfx_ipm groups do);
    cfx_btri_solve solves rhs [B][nrhs][M sp] in place (scratch: same shape).  On `hip_stream`. */
 int cfx_btri_factor(int64_t batch, int32_t M, int32_t sp, double *D, double *L, double *U, double *work,
