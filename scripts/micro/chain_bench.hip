@@ -53,6 +53,24 @@ int main(int argc, char** argv) {
         }
         if (rep == 2) printf("total %.3f ms\n", tot);
     }
+    // one solve with one right-hand side (after the last factorisation above)
+    {
+        double *rr, *tt;
+        CK(hipMalloc(&rr, (size_t)M * SP * sizeof(double)));
+        CK(hipMalloc(&tt, (size_t)M * SP * sizeof(double)));
+        std::vector<double> hr((size_t)M * SP, 1.0);
+        CK(hipMemcpy(rr, hr.data(), hr.size() * sizeof(double), hipMemcpyHostToDevice));
+        const cfx_chain::Rhs X{rr, 0, 0, tt, 0, 0};
+        float ts = 0;
+        for (int rep = 0; rep < 2; ++rep) {
+            CK(hipEventRecord(a));
+            CK(cfx_chain::solve_sp<SP>(C, 1, X, 1, 0));
+            CK(hipEventRecord(b));
+            CK(hipEventSynchronize(b));
+            CK(hipEventElapsedTime(&ts, a, b));
+        }
+        printf("one solve (1 rhs): %.1f us\n", ts * 1e3);
+    }
     // the pivot block alone: one workgroup, no neighbours (h = M)
     float t1;
     CK(hipEventRecord(a));
