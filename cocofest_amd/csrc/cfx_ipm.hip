@@ -43,6 +43,8 @@ constexpr int kSlots = 64;  // counter ring: one 4-int slot per host read
 constexpr int kMaxY = 65535;
 constexpr int kMaxBorder = 32;  // free parameters handled as a dense border
 constexpr int kWideParts = 128;  // blocks per instance of the wide-instance reductions (IpmK::wide)
+constexpr int kWP = 16;          // partial values per block (IpmK::wpart)
+constexpr int kWF = 12;          // decisions per instance (IpmK::wflag)
 
 // per-instance scalars of the iteration
 struct Scal {
@@ -104,6 +106,9 @@ struct IpmK {
     // holds grad f + J^T y, part [B][kWideParts][2] the per-block partial sums, reduced in a fixed order
     int wide;
     double *gj, *part;
+    // wpart [B][kWideParts][kWP]: per-block partials of the split barrier-algebra kernels (k_w*_a), reduced by the
+    // one-block kernel in breduce_n's fixed order; wflag [B][kWF]: that kernel's decisions for the k_w*_c loops
+    double *wpart, *wflag;
     // KKT layout.  P = 1, np = 0: one band of nA = nK unknowns (factor + solve in one launch).  Otherwise the
     // unknowns split into P diagonal band blocks of nA rows each (padded with unit rows) and a dense border of np
     // unknowns — Hmed intensity parameters, whose sliding windows couple most stages, and the separators between
@@ -214,6 +219,28 @@ __device__ void breduce_n(double (&v)[N], const int (&op)[N]) {
         for (int w = 1; w < kIB / 64; ++w) r = apply(i, r, shn[w][i]);
         v[i] = r;
     }
+}
+
+// Wide instances: a block of a k_w*_a grid (B, kWideParts) stores its partials of N reductions; the one-block
+// kernel that follows reduces the kWideParts partials of each (thread q holding partial q) in breduce_n's order, so
+// the values are reproducible (their order differs from the one-block loops': the wide path is its own
+// deterministic sum).
+__device__ inline double red_identity(int op) { return op == 0 ? 0.0 : (op == 1 ? -INFINITY : INFINITY); }
+template <int N>
+__device__ void wide_put(const IpmK& K, int64_t b, double (&v)[N], const int (&op)[N]) {
+    static_assert(N <= kWP, "partials per block");
+    breduce_n(v, op);
+    if (threadIdx.x == 0)
+#pragma unroll
+        for (int k = 0; k < N; ++k) K.wpart[(b * kWideParts + blockIdx.y) * kWP + k] = v[k];
+}
+template <int N>
+__device__ void wide_get(const IpmK& K, int64_t b, double (&v)[N], const int (&op)[N]) {
+    static_assert(kWideParts <= kIB, "a partial per thread");
+#pragma unroll
+    for (int k = 0; k < N; ++k)
+        v[k] = threadIdx.x < kWideParts ? K.wpart[(b * kWideParts + threadIdx.x) * kWP + k] : red_identity(op[k]);
+    breduce_n(v, op);
 }
 
 // counter slot: thread 0 of block 0 clears the next slot (the next counting kernel runs after this one)
@@ -462,7 +489,15 @@ __global__ void __launch_bounds__(kIB) k_ipm_begin(const IpmK K, int mode, int s
     const double* ubI = K.ubI + b * nf;
     double* rhs = K.rhs + b * K.nK;
     double szl = 0, szu = 0, sy = 0, ed = 0, ep = 0, ecl = 0, ecu = 0, edu = 0, epu = 0;
+    double pLmax = -INFINITY, pLmin = INFINITY, pUmax = -INFINITY, pUmin = INFINITY;  // (wide: k_wbegin_a's)
     const double* sg = K.sg + b * m;
+    if (K.wide) {
+        double rv[13];
+        const int ro[13] = {0, 0, 0, 1, 1, 1, 1, 1, 1, 1, 2, 1, 2};
+        wide_get(K, b, rv, ro);
+        szl = rv[0], szu = rv[1], sy = rv[2], ed = rv[3], ep = rv[4], ecl = rv[5], ecu = rv[6], edu = rv[7],
+        epu = rv[8], pLmax = rv[9], pLmin = rv[10], pUmax = rv[11], pUmin = rv[12];
+    } else {
     for (int i = threadIdx.x; i < nf; i += kIB) {
         double gj;
         if (K.wide) {  // k_wide_jty, the same sum in the same order
@@ -506,6 +541,7 @@ __global__ void __launch_bounds__(kIB) k_ipm_begin(const IpmK K, int mode, int s
         edu = rv[7];
         epu = rv[8];
     }
+    }
     const double smax = K.o.s_max;
     const double sd = clamp_lo((szl + szu + sy) / (2.0 * nf + m), smax) / smax;
     const double sc = clamp_lo((szl + szu) / (2.0 * nf), smax) / smax;
@@ -533,12 +569,16 @@ __global__ void __launch_bounds__(kIB) k_ipm_begin(const IpmK K, int mode, int s
     for (int pass = 0; pass < 5; ++pass) {
         const double mu = S.mu;
         double ecm = 0.0;
+        if (K.wide) {  // max_i |p_i - mu| = max(p_max - mu, mu - p_min), exactly (fl(p - mu) is monotone in p)
+            ecm = max_n(max_n(max_n(ecm, pLmax - mu), max_n(mu - pLmin, pUmax - mu)), mu - pUmin) / sc;
+        } else {
         for (int i = threadIdx.x; i < nf; i += kIB) {
             const double cl = K.hasL[i] ? (x[i] - lbI[i]) * zl[i] - mu : 0.0;
             const double cu = K.hasU[i] ? (ubI[i] - x[i]) * zu[i] - mu : 0.0;
             ecm = max_n(ecm, max_n(fabs(cl), fabs(cu)));
         }
         ecm = breduce(ecm, OpMax(), sh) / sc;
+        }
         const double e_mu = max_n(max_n(e_d, e_p), ecm);
         const bool dec = !S.done && (e_mu <= K.o.kappa_eps * mu) && (mu > K.o.tol / 10);
         if (!dec) break;
@@ -548,6 +588,7 @@ __global__ void __launch_bounds__(kIB) k_ipm_begin(const IpmK K, int mode, int s
     }
     const double mu = S.mu;
     double* sig = K.sig + b * nf;
+    if (!K.wide) {  // (wide: k_wbegin_c)
     for (int i = threadIdx.x; i < nf; i += kIB) {
         const bool hL = K.hasL[i], hU = K.hasU[i];
         const double sl = hL ? x[i] - lbI[i] : 1.0, su = hU ? ubI[i] - x[i] : 1.0;
@@ -558,6 +599,7 @@ __global__ void __launch_bounds__(kIB) k_ipm_begin(const IpmK K, int mode, int s
     for (int j = threadIdx.x; j < m; j += kIB) {
         rhs[nf + j] = -gS[j];
         K.ysc[b * m + j] = y[j] * K.sg[b * m + j];
+    }
     }
     if (threadIdx.x == 0) {
         S.tau = clamp_lo(1.0 - mu, K.o.tau_min);
@@ -904,6 +946,246 @@ __global__ void __launch_bounds__(kIB) k_wide_border_back(const IpmK K) {
     (void)np;
 }
 
+// ---- wide instances: k_ipm_begin / k_ipm_dir / k_ipm_accept / k_ipm_update split into a grid pass that forms the
+// per-block partials (k_w*_a, grid (B, kWideParts), strided loops), the one-block kernel (its scalar logic on the reduced
+// values, unchanged) and a grid pass over the elementwise updates that depend on them (k_w*_c, grid (B, ceil(max(nf,
+// m) / kIB)), reading the decisions the one-block kernel left in K.sc / K.wflag).  The one-block kernels' own loops
+// over ~10^5 variables were 0.5-1.4 ms each on the reaching task.
+#define WIDE_LOOP(i, n) for (int i = blockIdx.y * kIB + threadIdx.x; i < (n); i += kWideParts * kIB)
+
+// k_ipm_begin's sums and maxima (9) and the extremes of the complementarity products (4), from which the monotone
+// mu update's max_i |(x - l) z - mu| follows exactly for any mu (fl(p - mu) is monotone in p)
+__global__ void __launch_bounds__(kIB) k_wbegin_a(const IpmK K) {
+    const int64_t b = blockIdx.x;
+    if (K.sc[b].rs_on) return;
+    const int nf = K.nf, m = K.m;
+    const double* x = K.x + b * nf;
+    const double* zl = K.zl + b * nf;
+    const double* zu = K.zu + b * nf;
+    const double* y = K.y + b * m;
+    const double* lbI = K.lbI + b * nf;
+    const double* ubI = K.ubI + b * nf;
+    const double* gS = K.gS + b * m;
+    const double* sg = K.sg + b * m;
+    double* rhs = K.rhs + b * K.nK;
+    double szl = 0, szu = 0, sy = 0, ed = 0, ep = 0, ecl = 0, ecu = 0, edu = 0, epu = 0;
+    double pLmax = -INFINITY, pLmin = INFINITY, pUmax = -INFINITY, pUmin = INFINITY;
+    WIDE_LOOP(i, nf) {
+        const double gj = K.gj[b * nf + i];
+        rhs[i] = gj;
+        const double rd = gj - zl[i] + zu[i];
+        szl += fabs(zl[i]);
+        szu += fabs(zu[i]);
+        const double cl = K.hasL[i] ? (x[i] - lbI[i]) * zl[i] : 0.0;
+        const double cu = K.hasU[i] ? (ubI[i] - x[i]) * zu[i] : 0.0;
+        ed = max_n(ed, fabs(rd));
+        edu = max_n(edu, fabs(rd) / K.d[i]);
+        ecl = max_n(ecl, fabs(cl));
+        ecu = max_n(ecu, fabs(cu));
+        if (K.hasL[i]) pLmax = max_n(pLmax, cl), pLmin = min_n(pLmin, cl);
+        if (K.hasU[i]) pUmax = max_n(pUmax, cu), pUmin = min_n(pUmin, cu);
+    }
+    WIDE_LOOP(j, m) {
+        sy += fabs(y[j]);
+        ep = max_n(ep, fabs(gS[j]));
+        epu = max_n(epu, fabs(gS[j]) / sg[j]);
+    }
+    double rv[13] = {szl, szu, sy, ed, ep, ecl, ecu, edu, epu, pLmax, pLmin, pUmax, pUmin};
+    const int ro[13] = {0, 0, 0, 1, 1, 1, 1, 1, 1, 1, 2, 1, 2};
+    wide_put(K, b, rv, ro);
+}
+
+// k_ipm_begin's Newton right-hand side and Sigma at the final mu (k_ipm_begin stored it)
+__global__ void __launch_bounds__(kIB) k_wbegin_c(const IpmK K) {
+    const int64_t b = blockIdx.x;
+    if (K.sc[b].rs_on) return;
+    const int nf = K.nf, m = K.m;
+    const int i = blockIdx.y * kIB + threadIdx.x;
+    const double mu = K.sc[b].mu;
+    double* rhs = K.rhs + b * K.nK;
+    if (i < nf) {
+        const double xi = K.x[b * nf + i];
+        const bool hL = K.hasL[i], hU = K.hasU[i];
+        const double sl = hL ? xi - K.lbI[b * nf + i] : 1.0, su = hU ? K.ubI[b * nf + i] - xi : 1.0;
+        K.sig[b * nf + i] = (hL ? K.zl[b * nf + i] / sl : 0.0) + (hU ? K.zu[b * nf + i] / su : 0.0);
+        const double bar = (hL ? mu / sl : 0.0) - (hU ? mu / su : 0.0);
+        rhs[i] = -(rhs[i] - bar);
+    }
+    if (i < m) {
+        rhs[nf + i] = -K.gS[b * m + i];
+        K.ysc[b * m + i] = K.y[b * m + i] * K.sg[b * m + i];
+    }
+}
+
+// k_ipm_dir's loops: dz, the fraction-to-the-boundary minima, grad phi . dx, ||c||_1 and the barrier terms at x
+__global__ void __launch_bounds__(kIB) k_wdir_a(const IpmK K) {
+    const int64_t b = blockIdx.x;
+    if (K.sc[b].rs_on) return;
+    const int nf = K.nf, m = K.m;
+    const double mu = K.sc[b].mu, tau = K.sc[b].tau, smin = slack_min(mu);
+    const double* x = K.x + b * nf;
+    const double* zl = K.zl + b * nf;
+    const double* zu = K.zu + b * nf;
+    const double* dx = K.dx + b * nf;
+    const double* gF = K.gF + b * nf;
+    const double* lbI = K.lbI + b * nf;
+    const double* ubI = K.ubI + b * nf;
+    double apl = INFINITY, apu = INFINITY, azl = INFINITY, azu = INFINITY, dphi = 0.0, theta = 0.0;
+    double sL = 0.0, sU = 0.0, bad = 0.0;
+    WIDE_LOOP(i, nf) {
+        const bool hL = K.hasL[i], hU = K.hasU[i];
+        const double sl = hL ? x[i] - lbI[i] : 1.0, su = hU ? ubI[i] - x[i] : 1.0;
+        const double vzl = hL ? mu / sl - zl[i] - zl[i] / sl * dx[i] : 0.0;
+        const double vzu = hU ? mu / su - zu[i] + zu[i] / su * dx[i] : 0.0;
+        K.dzl[b * nf + i] = vzl;
+        K.dzu[b * nf + i] = vzu;
+        apl = min_n(apl, step_term(hL, sl, dx[i], tau));
+        apu = min_n(apu, step_term(hU, su, -dx[i], tau));
+        azl = min_n(azl, step_term(hL, zl[i], vzl, tau));
+        azu = min_n(azu, step_term(hU, zu[i], vzu, tau));
+        const double bar = (hL ? mu / sl : 0.0) - (hU ? mu / su : 0.0);
+        dphi += (gF[i] - bar) * dx[i];
+        if (hL) {  // barrier_obj's terms
+            const double s2 = x[i] - moved_lb(lbI[i], sl, smin);
+            if (s2 <= 0) bad = 1.0;
+            sL += log(clamp_lo(s2, 1e-300));
+        }
+        if (hU) {
+            const double s2 = moved_ub(ubI[i], su, smin) - x[i];
+            if (s2 <= 0) bad = 1.0;
+            sU += log(clamp_lo(s2, 1e-300));
+        }
+    }
+    WIDE_LOOP(j, m) theta += fabs(K.gS[b * m + j]);
+    double rv[9] = {apl, apu, azl, azu, dphi, theta, sL, sU, bad};
+    const int ro[9] = {2, 2, 2, 2, 0, 0, 0, 0, 1};
+    wide_put(K, b, rv, ro);
+}
+
+// k_ipm_dir's first trial point x + alpha0 dx (alpha0: S.alpha as k_ipm_dir left it)
+__global__ void __launch_bounds__(kIB) k_wdir_c(const IpmK K) {
+    const int64_t b = blockIdx.x;
+    if (K.sc[b].rs_on) return;
+    const int nf = K.nf;
+    const int i = blockIdx.y * kIB + threadIdx.x;
+    if (i >= nf) return;
+    const double a0 = K.sc[b].alpha, xi = K.x[b * nf + i];
+    const double xt = xi + a0 * K.dx[b * nf + i];
+    K.xacc[b * nf + i] = xi;
+    K.xt[b * nf + i] = xt;
+    K.vt[b * K.n + K.free[i]] = xt * K.d[i];
+}
+
+// k_ipm_accept's ||c(x_t)||_1 and the barrier terms at the trial point
+__global__ void __launch_bounds__(kIB) k_wacc_a(const IpmK K) {
+    const int64_t b = blockIdx.x;
+    if (K.sc[b].rs_on) return;
+    const int nf = K.nf, m = K.m;
+    const double mu = K.sc[b].mu, smin = slack_min(mu);
+    const double* xt = K.xt + b * nf;
+    const double* lbI = K.lbI + b * nf;
+    const double* ubI = K.ubI + b * nf;
+    double tt = 0.0, sL = 0.0, sU = 0.0, bad = 0.0;
+    WIDE_LOOP(j, m) tt += fabs(K.gt[b * m + j] * K.sg[b * m + j]);
+    WIDE_LOOP(i, nf) {
+        if (K.hasL[i]) {
+            double sl = xt[i] - lbI[i];
+            sl = xt[i] - moved_lb(lbI[i], sl, smin);
+            if (sl <= 0) bad = 1.0;
+            sL += log(clamp_lo(sl, 1e-300));
+        }
+        if (K.hasU[i]) {
+            double su = ubI[i] - xt[i];
+            su = moved_ub(ubI[i], su, smin) - xt[i];
+            if (su <= 0) bad = 1.0;
+            sU += log(clamp_lo(su, 1e-300));
+        }
+    }
+    double rv[4] = {tt, sL, sU, bad};
+    const int ro[4] = {0, 0, 0, 1};
+    wide_put(K, b, rv, ro);
+}
+
+// k_ipm_accept's second-order-correction right-hand side (wflag[1]) and the accepted point (wflag[2])
+__global__ void __launch_bounds__(kIB) k_wacc_c(const IpmK K) {
+    const int64_t b = blockIdx.x;
+    const double* wf = K.wflag + b * kWF;
+    if (wf[0] == 0.0) return;
+    const int nf = K.nf, m = K.m;
+    const int i = blockIdx.y * kIB + threadIdx.x;
+    if (wf[1] != 0.0 && i < m) K.csoc[b * m + i] = wf[3] * K.gS[b * m + i] + K.gt[b * m + i] * K.sg[b * m + i];
+    if (wf[2] != 0.0 && i < nf) K.xacc[b * nf + i] = K.xt[b * nf + i];
+}
+
+// k_ipm_update's non-finite checks of the step
+__global__ void __launch_bounds__(kIB) k_wupd_a(const IpmK K) {
+    const int64_t b = blockIdx.x;
+    const int nf = K.nf, m = K.m;
+    double nfy = 0.0, nfz = 0.0;
+    WIDE_LOOP(j, m)
+    if (!isfinite(K.dy[b * m + j])) nfy = 1.0;
+    WIDE_LOOP(i, nf)
+    if (!isfinite(K.dzl[b * nf + i]) || !isfinite(K.dzu[b * nf + i])) nfz = 1.0;
+    double rv[2] = {nfy, nfz};
+    const int ro[2] = {1, 1};
+    wide_put(K, b, rv, ro);
+}
+
+// k_ipm_update's step of x, the bound multipliers (with Ipopt's kappa_sigma safeguard) and the moved bounds, the
+// constraint multipliers, and the decision vector; wflag: [0] go, [1] step, [2] reset, [3] mz, [4] az, [5] mu,
+// [6] back to the watchdog iterate, [7] y update (0 none, 1 watchdog, 2 zero, 3 alpha dy), [8] alpha
+__global__ void __launch_bounds__(kIB) k_wupd_c(const IpmK K) {
+    const int64_t b = blockIdx.x;
+    const double* wf = K.wflag + b * kWF;
+    if (wf[0] == 0.0) return;
+    const int nf = K.nf, m = K.m;
+    const int i = blockIdx.y * kIB + threadIdx.x;
+    const bool step = wf[1] != 0.0, reset = wf[2] != 0.0, mz = wf[3] != 0.0, wd_back = wf[6] != 0.0;
+    const double az = wf[4], mu = wf[5], smin = slack_min(mu);
+    if (i < nf) {
+        const int64_t e = b * nf + i;
+        const double* xnew = reset ? K.xr : K.xacc;
+        double xi = step ? xnew[e] : K.x[e];
+        double l = K.zl[e], u = K.zu[e];
+        if (mz) {
+            l = l + az * K.dzl[e];
+            u = u + az * K.dzu[e];
+        }
+        if (K.hasL[i]) {
+            const double lbv = moved_lb(K.lbI[e], xi - K.lbI[e], smin);
+            K.lbI[e] = lbv;
+            const double sl = xi - lbv;
+            l = clamp_hi(clamp_lo(l, mu / (1e10 * sl)), 1e10 * mu / sl);
+        }
+        if (K.hasU[i]) {
+            const double ubv = moved_ub(K.ubI[e], K.ubI[e] - xi, smin);
+            K.ubI[e] = ubv;
+            const double su = ubv - xi;
+            u = clamp_hi(clamp_lo(u, mu / (1e10 * su)), 1e10 * mu / su);
+        }
+        if (wd_back) {
+            xi = K.wx[e];
+            l = K.wzl[e];
+            u = K.wzu[e];
+        }
+        K.x[e] = xi;
+        K.zl[e] = l;
+        K.zu[e] = u;
+        K.vx[b * K.n + K.free[i]] = xi * K.d[i];
+    }
+    if (i < m) {
+        const int64_t e = b * m + i;
+        const int ym = (int)wf[7];
+        double yv = K.y[e];
+        if (ym == 1) yv = K.wy[e];
+        else if (ym == 2) yv = 0.0;
+        else if (ym == 3) yv = yv + wf[8] * K.dy[e];
+        K.y[e] = yv;
+        K.ysc[e] = yv * K.sg[e];
+    }
+}
+#undef WIDE_LOOP
+
 // Newton step in natural order and the curvature test (solver.py inertia loop); bumps dw where it fails.  An instance
 // in the restoration phase takes the phase's step (its dx in dxr, its own dw, the proximity weights).  Counters: [0]
 // instances iterating, [1] of them with the wrong inertia, [2] of them in the restoration phase
@@ -1003,6 +1285,14 @@ __global__ void __launch_bounds__(kIB) k_ipm_dir(const IpmK K, int it) {
     const double* lbI = K.lbI + b * nf;
     const double* ubI = K.ubI + b * nf;
     double apl = INFINITY, apu = INFINITY, azl = INFINITY, azu = INFINITY, dphi = 0.0, theta = 0.0;
+    double phi;
+    if (K.wide) {  // k_wdir_a's partials
+        double rv[9];
+        const int ro[9] = {2, 2, 2, 2, 0, 0, 0, 0, 1};
+        wide_get(K, b, rv, ro);
+        apl = rv[0], apu = rv[1], azl = rv[2], azu = rv[3], dphi = rv[4], theta = rv[5];
+        phi = rv[8] > 0 ? INFINITY : S.fS - mu * (rv[6] + rv[7]);
+    } else {
     for (int i = threadIdx.x; i < nf; i += kIB) {
         const bool hL = K.hasL[i], hU = K.hasU[i];
         const double sl = hL ? x[i] - lbI[i] : 1.0, su = hU ? ubI[i] - x[i] : 1.0;
@@ -1029,7 +1319,8 @@ __global__ void __launch_bounds__(kIB) k_ipm_dir(const IpmK K, int it) {
         dphi = rv[4];
         theta = rv[5];
     }
-    const double phi = barrier_obj(K, b, x, S.fS, mu, sh);
+    phi = barrier_obj(K, b, x, S.fS, mu, sh);
+    }
     const double a_p = min_n(clamp_hi(apl, 1.0), clamp_hi(apu, 1.0));
     // watchdog start (Ipopt StartWatchDog): remember this iterate and its line-search reference values
     const int trig = K.o.watchdog_shortened_iter_trigger;
@@ -1071,14 +1362,16 @@ __global__ void __launch_bounds__(kIB) k_ipm_dir(const IpmK K, int it) {
         S.forced = 0;
         S.rejf = 0;  // Ipopt's InitThisLineSearch
     }
-    double* xacc = K.xacc + b * nf;
-    double* xt = K.xt + b * nf;
-    for (int i = threadIdx.x; i < nf; i += kIB) {
-        xacc[i] = x[i];
-        xt[i] = x[i] + alpha0 * dx[i];
+    if (!K.wide) {  // (wide: k_wdir_c)
+        double* xacc = K.xacc + b * nf;
+        double* xt = K.xt + b * nf;
+        for (int i = threadIdx.x; i < nf; i += kIB) {
+            xacc[i] = x[i];
+            xt[i] = x[i] + alpha0 * dx[i];
+        }
+        __syncthreads();
+        write_full(K, b, xt, K.vt);
     }
-    __syncthreads();
-    write_full(K, b, xt, K.vt);
     store_scal(K, b, S);
 }
 
@@ -1093,15 +1386,24 @@ __global__ void __launch_bounds__(kIB) k_ipm_accept(const IpmK K, int ls, int sl
     load_scal(K, b, S);
     if (S.rs_on) {  // block-uniform
         count_add(K, slot, 0, S.rs_exit == RS_RUNNING && !S.rs_acc);
+        if (K.wide && threadIdx.x == 0) K.wflag[b * kWF] = 0.0;  // k_wacc_c: nothing to do
         return;
     }
     const double* sg = K.sg + b * m;
     const double* gt = K.gt + b * m;
-    double tt = 0.0;
-    for (int j = threadIdx.x; j < m; j += kIB) tt += fabs(gt[j] * sg[j]);
-    tt = breduce(tt, OpSum(), sh);
+    double tt = 0.0, pt;
     const double* xt = K.xt + b * nf;
-    const double pt = barrier_obj(K, b, xt, K.ft[b] * S.sf, S.mu, sh);
+    if (K.wide) {  // k_wacc_a's partials
+        double rv[4];
+        const int ro[4] = {0, 0, 0, 1};
+        wide_get(K, b, rv, ro);
+        tt = rv[0];
+        pt = rv[3] > 0 ? INFINITY : K.ft[b] * S.sf - S.mu * (rv[1] + rv[2]);
+    } else {
+        for (int j = threadIdx.x; j < m; j += kIB) tt += fabs(gt[j] * sg[j]);
+        tt = breduce(tt, OpSum(), sh);
+        pt = barrier_obj(K, b, xt, K.ft[b] * S.sf, S.mu, sh);
+    }
     bool ok, arm, rejf;
     filter_accept(K, S, K.filt + b * kFilt * 2, tt, pt, S.alpha, sh, ok, arm, &rejf);
     const bool rej_here = rejf && !S.accepted;
@@ -1109,14 +1411,24 @@ __global__ void __launch_bounds__(kIB) k_ipm_accept(const IpmK K, int ls, int sl
     // a watchdog iteration takes its full step whether or not it is acceptable (no corrections, no backtracking)
     const bool forced = ls == 0 && S.wd_on && !ok && !S.accepted;
     bool soc = false;
-    if (ls == 0) {
-        soc = !S.accepted && !ok && !forced && (tt >= S.theta) && !S.skip_first;
-        double* cs = K.csoc + b * m;
-        for (int j = threadIdx.x; j < m; j += kIB) cs[j] = S.alpha * K.gS[b * m + j] + gt[j] * sg[j];
-    }
-    if (ok || forced) {
-        double* xacc = K.xacc + b * nf;
-        for (int i = threadIdx.x; i < nf; i += kIB) xacc[i] = xt[i];
+    if (ls == 0) soc = !S.accepted && !ok && !forced && (tt >= S.theta) && !S.skip_first;
+    if (K.wide) {  // (k_wacc_c)
+        if (threadIdx.x == 0) {
+            double* wf = K.wflag + b * kWF;
+            wf[0] = 1.0;
+            wf[1] = ls == 0;
+            wf[2] = ok || forced;
+            wf[3] = S.alpha;
+        }
+    } else {
+        if (ls == 0) {
+            double* cs = K.csoc + b * m;
+            for (int j = threadIdx.x; j < m; j += kIB) cs[j] = S.alpha * K.gS[b * m + j] + gt[j] * sg[j];
+        }
+        if (ok || forced) {
+            double* xacc = K.xacc + b * nf;
+            for (int i = threadIdx.x; i < nf; i += kIB) xacc[i] = xt[i];
+        }
     }
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -1208,6 +1520,7 @@ __global__ void __launch_bounds__(kIB) k_ipm_soc_accept(const IpmK K, int slot) 
     load_scal(K, b, S);
     if (S.rs_on) {  // block-uniform
         count_add(K, slot, 0, S.rs_exit == RS_RUNNING && !S.rs_acc);
+        if (K.wide && threadIdx.x == 0) K.wflag[b * kWF] = 0.0;  // k_wacc_c: nothing to do
         return;
     }
     const double* sg = K.sg + b * m;
@@ -1506,6 +1819,7 @@ __global__ void __launch_bounds__(kIB) k_ipm_update(const IpmK K, int resto) {
     const int64_t b = blockIdx.x;
     const int nf = K.nf, m = K.m;
     load_scal(K, b, S);
+    if (K.wide && threadIdx.x == 0) K.wflag[b * kWF] = 0.0;  // k_wupd_c: nothing to do unless set below
     if (S.rs_on && S.rs_exit == RS_RUNNING) return;  // block-uniform
     const bool phase_end = S.rs_on;
     // a failed phase stops the instance (Ipopt: Restoration_Failed) unless resto_failure_restart (an extension) sends
@@ -1576,11 +1890,17 @@ __global__ void __launch_bounds__(kIB) k_ipm_update(const IpmK K, int resto) {
     const double* dzu = K.dzu + b * nf;
     const double* dy = K.dy + b * m;
     double nfy = 0.0, nfz = 0.0;
-    for (int j = threadIdx.x; j < m; j += kIB)
-        if (!isfinite(dy[j])) nfy = 1.0;
-    for (int i = threadIdx.x; i < nf; i += kIB)
-        if (!isfinite(dzl[i]) || !isfinite(dzu[i])) nfz = 1.0;
-    {
+    if (K.wide) {  // k_wupd_a's partials
+        double rv[2];
+        const int ro[2] = {1, 1};
+        wide_get(K, b, rv, ro);
+        nfy = rv[0];
+        nfz = rv[1];
+    } else {
+        for (int j = threadIdx.x; j < m; j += kIB)
+            if (!isfinite(dy[j])) nfy = 1.0;
+        for (int i = threadIdx.x; i < nf; i += kIB)
+            if (!isfinite(dzl[i]) || !isfinite(dzu[i])) nfz = 1.0;
         double rv[2] = {nfy, nfz};
         const int ro[2] = {1, 1};
         breduce_n(rv, ro);
@@ -1594,6 +1914,20 @@ __global__ void __launch_bounds__(kIB) k_ipm_update(const IpmK K, int resto) {
     const double mu = S.mu, smin = slack_min(mu);
     double* lbI = K.lbI + b * nf;
     double* ubI = K.ubI + b * nf;
+    if (K.wide) {  // (k_wupd_c)
+        if (threadIdx.x == 0) {
+            double* wf = K.wflag + b * kWF;
+            wf[1] = step;
+            wf[2] = reset;
+            wf[3] = mz;
+            wf[4] = az;
+            wf[5] = mu;
+            wf[6] = wd_back;
+            wf[7] = wd_back ? 1 : ((reset && resto == 2) ? 2 : (mv ? 3 : 0));
+            wf[8] = alpha;
+            wf[0] = 1.0;
+        }
+    } else {
     for (int i = threadIdx.x; i < nf; i += kIB) {
         double xi = step ? xnew[i] : x[i];
         x[i] = xi;
@@ -1633,6 +1967,7 @@ __global__ void __launch_bounds__(kIB) k_ipm_update(const IpmK K, int resto) {
     for (int j = threadIdx.x; j < m; j += kIB) K.ysc[b * m + j] = K.y[b * m + j] * K.sg[b * m + j];
     __syncthreads();
     write_full(K, b, x, K.vx);
+    }
     if (threadIdx.x == 0) {
         K.of[b] = S.sf;  // the phase evaluated its Hessian with objective factor 0
         if (grow) S.fpos += 1;
@@ -3266,6 +3601,8 @@ static int ipm_create_common(cfx_ipm* s, const cfx_sizes& sz, int layout, const 
     if (const char* e = std::getenv("CFX_IPM_WIDE")) K.wide = std::atoi(e) != 0;  // tuning / A-B override
     K.gj = dalloc<double>(s, B * nf, &rc);
     K.part = dalloc<double>(s, B * kWideParts * 2, &rc);
+    K.wpart = dalloc<double>(s, B * kWideParts * kWP, &rc);
+    K.wflag = dalloc<double>(s, B * kWF, &rc);
     K.chain = chain ? 1 : 0;
     K.cM = (int)cM;
     K.csp = (int)csp;
@@ -3419,13 +3756,22 @@ struct Run {
             if (mode & 1)
                 hipLaunchKernelGGL(k_wide_scale, dim3((unsigned)K.B, (unsigned)((n + kIB - 1) / kIB)), dim3(kIB), 0,
                                    st, K);
-            if (!(mode & 2))
+            if (!(mode & 2)) {
                 hipLaunchKernelGGL(k_wide_jty, dim3((unsigned)K.B, (unsigned)((K.nf + kIB - 1) / kIB)), dim3(kIB), 0,
                                    st, K);
+                hipLaunchKernelGGL(k_wbegin_a, wa(), dim3(kIB), 0, st, K);
+            }
         }
         hipLaunchKernelGGL(k_ipm_begin, g, dim3(kIB), 0, st, K, mode, slot);
+        if (K.wide && !(mode & 2)) hipLaunchKernelGGL(k_wbegin_c, wc(), dim3(kIB), 0, st, K);
         IPM_HIP(s, hipGetLastError());
         return CFX_OK;
+    }
+    // wide instances: the partials grid and the elementwise grid of the split kernels
+    dim3 wa() const { return dim3((unsigned)s->K.B, kWideParts); }
+    dim3 wc() const {
+        const int64_t n = std::max<int64_t>(s->K.nf, s->K.m);
+        return dim3((unsigned)s->K.B, (unsigned)((n + kIB - 1) / kIB));
     }
     int curv(int slot) {
         const IpmK& K = s->K;
@@ -3647,7 +3993,9 @@ static int ipm_solve(cfx_ipm* s, const double* v0, const double* fixed_values, d
         }
         if (all_done) break;
         rs_live = n_resto > 0;  // instances iterating in the phase (counted by k_ipm_curv)
+        if (K.wide) hipLaunchKernelGGL(k_wdir_a, R.wa(), blk, 0, st, K);
         hipLaunchKernelGGL(k_ipm_dir, R.g, blk, 0, st, K, it);
+        if (K.wide) hipLaunchKernelGGL(k_wdir_c, R.wc(), blk, 0, st, K);
         if (K.rsphase && rs_live) hipLaunchKernelGGL(k_rs_dir, R.g, blk, 0, st, K);
         // filter line search with second-order corrections (the phase's own filter line search alongside)
         int notacc = 0, n_soft = 0;
@@ -3655,7 +4003,9 @@ static int ipm_solve(cfx_ipm* s, const double* v0, const double* fixed_values, d
             IPM_RUN(R.eval_gf(true));
             int sl = R.next_slot();
             if (K.rsphase && rs_live) hipLaunchKernelGGL(k_rs_accept, R.g, blk, 0, st, K);
+            if (K.wide) hipLaunchKernelGGL(k_wacc_a, R.wa(), blk, 0, st, K);
             hipLaunchKernelGGL(k_ipm_accept, R.g, blk, 0, st, K, ls, sl);
+            if (K.wide) hipLaunchKernelGGL(k_wacc_c, R.wc(), blk, 0, st, K);
             IPM_HIP(s, hipGetLastError());
             IPM_RUN(R.read(sl, c));
             notacc = c[0];
@@ -3717,7 +4067,9 @@ static int ipm_solve(cfx_ipm* s, const double* v0, const double* fixed_values, d
             }
             reinit = true;
         }
+        if (K.wide) hipLaunchKernelGGL(k_wupd_a, R.wa(), blk, 0, st, K);
         hipLaunchKernelGGL(k_ipm_update, R.g, blk, 0, st, K, K.rsphase ? 2 : (resto ? 1 : 0));
+        if (K.wide) hipLaunchKernelGGL(k_wupd_c, R.wc(), blk, 0, st, K);
         IPM_HIP(s, hipGetLastError());
         s->st.iterations++;
     }
