@@ -1490,6 +1490,20 @@ extern "C" int cfx_msk_create(const cfx_msk_problem* p, cfx_handle** out) {
                 tasks.push_back((int16_t)J);
                 tasks.push_back((int16_t)t);
             }
+        // k_msk_hpair's groups: pairs without q, with one q (swapped to come first), with two
+        std::vector<int16_t> grp[3];
+        for (size_t e = 0; e < tasks.size(); e += 3) {
+            int16_t I = tasks[e], J = tasks[e + 1];
+            const int g = (int)is_q(I) + (int)is_q(J);
+            if (g == 1 && !is_q(I)) std::swap(I, J);
+            grp[g].insert(grp[g].end(), {I, J, tasks[e + 2]});
+        }
+        tasks.clear();
+        for (int g = 0; g < 3; ++g) {
+            tasks.insert(tasks.end(), grp[g].begin(), grp[g].end());
+            if (g < 2) h->mp.hgrp[g] = (int32_t)(grp[g].size() / 3);
+        }
+        h->mp.hgrp[2] = (int32_t)(grp[2].size() / 3);
     }
     h->n_htasks = (int)(tasks.size() / 3);
 

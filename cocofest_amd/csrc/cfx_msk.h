@@ -208,6 +208,8 @@ struct MskParams {
     int32_t T, ngk;      // truncation; rows per interval (nx continuity rows, then the Hmed sliding-window rows)
     int32_t kpb;         // k_msk_tangents_lds: consecutive intervals per block (fixed by cfx_msk_create)
     int32_t keepc;       // CFX_KEEP_CONSTANT_JAC: the -1 on x_{k+1} is not stored (the output holds it already)
+    int32_t hgrp[3];     // k_msk_hpair's task groups (cfx_msk_create orders the tasks so): pairs without q, with one
+                         // q (listed first), with two
     double dt, h;
     // calcium sums [N][Q][NM] at every RK stage time (host, reference operation order); Hmed2018: the per-pulse
     // coefficients r_i exp(-(t - t_i) / tau_c) [N][Q][NM][TMAX] of cs = sum_i coef_i lambda(I_i)
@@ -474,12 +476,20 @@ CFX_HD Dual<B> dual_up(const Dual<A>& a) {
     for (int i = 0; i < A; ++i) r.d[i] = a.d[i];
     return r;
 }
+template <class T>
+struct IsJet : std::false_type {};
+template <int D>
+struct IsJet<Jet<D>> : std::true_type {};
 template <class SV, class SQ>
 MSK_HD SV up(const SQ& a) {
     if constexpr (std::is_same<SV, SQ>::value) {
         return a;
     } else if constexpr (std::is_same<SQ, double>::value) {
         return Num<SV>::c(a);
+    } else if constexpr (IsJet<SV>::value) {  // Dual<1> in the pair's first direction, no second derivatives
+        SV r = Num<SV>::c(a.v);
+        r.g[0] = a.d[0];
+        return r;
     } else {
         return dual_up<DualN<SV>::n>(a);
     }
@@ -690,9 +700,11 @@ MSK_HD void msk_skeleton(const MskGeom& G, const SQ* q, const SV* qd, const SV* 
 }
 
 // FesMskModel.muscle_dynamic for one state: f = dx/dt.  cs[m]: calcium sum of muscle m at this stage time.
-template <int NQ, int NM, int FAM, class S>
-MSK_HD void msk_rhs(const MskGeom& G, int residual, const double* cs, const double* cs1, const S* x, const S* u,
-                    S* f) {
+// q (SQ) may carry fewer derivative directions than the rest of the state (k_msk_hpair: the frames of a pair that does
+// not involve q are plain values)
+template <int NQ, int NM, int FAM, class S, class SQ>
+MSK_HD void msk_rhs_q(const MskGeom& G, int residual, const double* cs, const double* cs1, const S* x, const SQ* q,
+                      const S* u, S* f) {
     constexpr int NXM = msk_nxm<FAM>();
     constexpr bool FAT = (FAM & 1) != 0, PW = msk_pw<FAM>();
     constexpr int XQ = NM * NXM, XQD = XQ + NQ;
@@ -701,8 +713,11 @@ MSK_HD void msk_rhs(const MskGeom& G, int residual, const double* cs, const doub
 #pragma unroll
     for (int mu = 0; mu < NM; ++mu) F[mu] = x[mu * NXM + 1];
 #pragma unroll
-    for (int k = 0; k < NQ; ++k) taur[k] = residual ? u[NUI + k] : Num<S>::c(0.0);
-    msk_skeleton<NQ, NM>(G, x + XQ, x + XQD, F, taur, mult, qdd, nullptr, nullptr);
+    for (int k = 0; k < NQ; ++k) {
+        if (residual) taur[k] = u[NUI + k];
+        else taur[k] = Num<S>::c(0.0);
+    }
+    msk_skeleton<NQ, NM>(G, q, x + XQD, F, taur, mult, qdd, nullptr, nullptr);
 #pragma unroll
     for (int mu = 0; mu < NM; ++mu) {
         const MskMuscleConst& C = G.mc[mu];
@@ -736,6 +751,12 @@ MSK_HD void msk_rhs(const MskGeom& G, int residual, const double* cs, const doub
         f[XQ + k] = x[XQD + k];
         f[XQD + k] = qdd[k];
     }
+}
+
+template <int NQ, int NM, int FAM, class S>
+MSK_HD void msk_rhs(const MskGeom& G, int residual, const double* cs, const double* cs1, const S* x, const S* u,
+                    S* f) {
+    msk_rhs_q<NQ, NM, FAM>(G, residual, cs, cs1, x, x + NM * msk_nxm<FAM>(), u, f);
 }
 
 // Phi_m(x, u) over interval k: m RK sub-steps (bioptim convention: constant control, RK4 stage times
@@ -1531,8 +1552,15 @@ __global__ void __launch_bounds__(256) k_msk_hadj(const MskParams P, const MskGe
 }
 
 // GQ[k][q][t][b] = d^2(mu_q^T f)/dY_I dY_J at stage q for coordinate pair t = (I, J) of (x, u); tasks holds
-// (I, J, t) triples of the structurally non-zero pairs (cfx_msk_create)
-template <int NQ, int NM, int FAM>
+// (I, J, t) triples of the structurally non-zero pairs (cfx_msk_create), in three groups launched apart (VAR):
+//   0  neither coordinate is a q: the frames, muscle geometry and mass matrix are plain values (their derivatives in
+//      both directions vanish);
+//   1  I is a q, J not: they carry the I direction only (Dual<1>, promoted with zero second derivatives — the frames
+//      depend on q alone, so their d2/dI dJ and d2/dJ2 vanish and d2/dI2, which does, is not the entry asked for);
+//   2  both are q: Jet<2> throughout.
+// Each entry is the same chain-rule sum as with Jet<2> frames (the dropped terms are exact zeros); the six-muscle arm's
+// Jet<2> frames spilled 235 registers per thread.
+template <int NQ, int NM, int FAM, int VAR>
 __global__ void __launch_bounds__(256) k_msk_hpair(const MskParams P, const MskGeom* __restrict__ GG,
                                                    const int16_t* __restrict__ tasks, int ntasks, int npair,
                                                    const double* __restrict__ V, const double* __restrict__ XS,
@@ -1573,7 +1601,7 @@ __global__ void __launch_bounds__(256) k_msk_hpair(const MskParams P, const MskG
     }
     auto owner = [](int e) { return e < NM * NXM ? e / NXM : ((e >= NX && e < NX + NPW) ? e - NX : -1); };
     const int mI = owner(I), mJ = owner(J);
-    if (mI >= 0 && mI == mJ) {
+    if (VAR == 0 && mI >= 0 && mI == mJ) {
         const int mu = mI, o = mu * NXM;
         const MskMuscleConst& C = G.mc[mu];
         auto seed = [&](int e, double v) {
@@ -1627,7 +1655,24 @@ __global__ void __launch_bounds__(256) k_msk_hpair(const MskParams P, const MskG
     } else {
         msk_stage_cs<NM, FAM>(P.cs, kq, nullptr, csl);
     }
-    msk_rhs<NQ, NM, FAM>(G, P.residual, csl, msk_cs1<NM>(P, kq), x, u, f);
+    if constexpr (VAR == 2) {
+        msk_rhs<NQ, NM, FAM>(G, P.residual, csl, msk_cs1<NM>(P, kq), x, u, f);
+    } else if constexpr (VAR == 1) {
+        constexpr int XQ = NM * NXM;
+        Dual<1> q[NQ];
+#pragma unroll
+        for (int k = 0; k < NQ; ++k) {
+            q[k] = dconst<1>(x[XQ + k].v);
+            q[k].d[0] = XQ + k == I ? 1.0 : 0.0;
+        }
+        msk_rhs_q<NQ, NM, FAM>(G, P.residual, csl, msk_cs1<NM>(P, kq), x, q, u, f);
+    } else {
+        constexpr int XQ = NM * NXM;
+        double q[NQ];
+#pragma unroll
+        for (int k = 0; k < NQ; ++k) q[k] = x[XQ + k].v;
+        msk_rhs_q<NQ, NM, FAM>(G, P.residual, csl, msk_cs1<NM>(P, kq), x, q, u, f);
+    }
     const int hi = I == J ? 0 : 1;  // Jet<2> second-order slots: (0,0), (1,0), (1,1)
     double acc = 0.0;
 #pragma unroll

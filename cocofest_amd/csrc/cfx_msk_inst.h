@@ -113,8 +113,19 @@ hipError_t hess_t(const MskParams& P, const MskGeom* G, const int16_t* tasks, in
     }
     hipLaunchKernelGGL((k_msk_htan<NQ, NM, FAM, SCHEME>), flat(P.B * P.N * P.nz), dim3(kMskBlk), 0, s, Pw, G, V, TS);
     hipLaunchKernelGGL((k_msk_hadj<NQ, NM, FAM, SCHEME>), flat(P.B * P.N), dim3(kMskBlk), 0, s, Pw, G, LAM, MU);
-    hipLaunchKernelGGL((k_msk_hpair<NQ, NM, FAM>), flat(BNQ * ntasks), dim3(kMskBlk), 0, s, Pw, G, tasks,
-                       ntasks, npair, V, (const double*)XS, (const double*)MU, GQ);
+    {  // the three task groups (k_msk_hpair), each its own instantiation and register allocation
+        const int16_t* tg = tasks;
+        const int n0 = P.hgrp[0], n1 = P.hgrp[1], n2 = ntasks - n0 - n1;
+        if (n0 > 0)
+            hipLaunchKernelGGL((k_msk_hpair<NQ, NM, FAM, 0>), flat(BNQ * n0), dim3(kMskBlk), 0, s, Pw, G, tg, n0, npair,
+                               V, (const double*)XS, (const double*)MU, GQ);
+        if (n1 > 0)
+            hipLaunchKernelGGL((k_msk_hpair<NQ, NM, FAM, 1>), flat(BNQ * n1), dim3(kMskBlk), 0, s, Pw, G, tg + 3 * n0,
+                               n1, npair, V, (const double*)XS, (const double*)MU, GQ);
+        if (n2 > 0)
+            hipLaunchKernelGGL((k_msk_hpair<NQ, NM, FAM, 2>), flat(BNQ * n2), dim3(kMskBlk), 0, s, Pw, G,
+                               tg + 3 * (n0 + n1), n2, npair, V, (const double*)XS, (const double*)MU, GQ);
+    }
     if (small) {
         double* HQ = GQ + BNQ * npair;
         hipLaunchKernelGGL((k_msk_hproj_stage<NQ, NM, FAM>), flat(BNQ * P.nz), dim3(kMskBlk), 0, s, Pw,
