@@ -74,7 +74,13 @@ struct Scal {
     int32_t soft_on, soft_cnt, soft_try, soft_ok;
     int32_t rs_rr;  // the phase's last iteration reset p, n (Ipopt's RestoRestorationPhase) instead of stepping
     int32_t rpad;
+    // Ipopt's structural-degeneracy test of the Hessian (PDPerturbationHandler, degen_iters_max = 3): hdeg 0 not yet
+    // determined, 1 not degenerate (an iteration's first trial with dw = 0 passed), 2 degenerate (the first
+    // kDegenIters iterations all needed dw > 0): from then on each iteration's first trial is dw = max(1e-20, dw_last / 3)
+    // instead of 0; degit counts those iterations
+    int32_t hdeg, degit;
 };
+constexpr int kDegenIters = 3;  // Ipopt degen_iters_max
 
 // how a restoration phase ended (Scal::rs_exit)
 enum { RS_RUNNING = 0, RS_OK = 1, RS_FAILED = 2, RS_INFEASIBLE = 3, RS_BUDGET = 4 };
@@ -103,7 +109,8 @@ struct IpmK {
     // Wide instances (wide = 1: small batches of large NLPs, e.g. the reaching task's 2.4 M J_g values in one instance):
     // the gather loops of k_ipm_begin (J_g scaling, J^T y), k_ipm_curv (unpacking, x^T W x) and the border's back
     // substitution run as grids of many blocks per instance (k_wide_*) instead of one block's serial loop; gj [B][nf]
-    // holds grad f + J^T y, part [B][kWideParts][2] the per-block partial sums, reduced in a fixed order
+    // holds grad f + J^T y, part [B][kWideParts][4] the per-block partial sums (x^T W x, non-finite, x^T (Sigma +
+    // dw) x, |x|^2), reduced in a fixed order
     int wide;
     double *gj, *part;
     // wpart [B][kWideParts][kWP]: per-block partials of the split barrier-algebra kernels (k_w*_a), reduced by the
@@ -603,7 +610,8 @@ __global__ void __launch_bounds__(kIB) k_ipm_begin(const IpmK K, int mode, int s
     }
     if (threadIdx.x == 0) {
         S.tau = clamp_lo(1.0 - mu, K.o.tau_min);
-        S.dw = 0.0;
+        // Ipopt's first trial: dw = 0, or straight from the last one when the Hessian is known to be degenerate
+        S.dw = S.hdeg == 2 ? (S.dwl > 0 ? clamp_lo(S.dwl / 3, 1e-20) : 1e-4) : 0.0;
         K.of[b] = S.sf;
     }
     store_scal(K, b, S);
@@ -873,7 +881,6 @@ __global__ void __launch_bounds__(kIB) k_wide_jty(const IpmK K) {
 
 // grid (B, kWideParts): the Newton step in natural order (dx / dxr, dy) from rb, and a non-finite flag per block
 __global__ void __launch_bounds__(kIB) k_wide_unpack(const IpmK K) {
-    __shared__ double sh[kIB / 64];
     const int64_t b = blockIdx.x;
     const Scal& S = K.sc[b];
     const bool rs = S.rs_on;
@@ -884,18 +891,30 @@ __global__ void __launch_bounds__(kIB) k_wide_unpack(const IpmK K) {
     double* dy = K.dy + b * K.m;
     const int64_t per = (K.nK + kWideParts - 1) / kWideParts;
     const int64_t lo = blockIdx.y * per, hi = std::min<int64_t>(K.nK, lo + per);
-    double nonfin = 0.0;
+    double nonfin = 0.0, dd = 0.0, nrm = 0.0;
+    const double dwc = rs ? S.rs_dw : S.dw;
+    const double* sig = K.sig + b * nf;
     if (active || !rs)
         for (int64_t i = lo + threadIdx.x; i < hi; i += kIB) {
             const double r = rb[K.pos[i]];
             if (!isfinite(r)) nonfin = 1.0;
-            if (i < nf)
+            if (i < nf) {
                 dx[i] = r;
-            else
+                dd += (sig[i] + dwc + (rs ? rs_prox(K, b, (int)i) : 0.0)) * r * r;  // k_ipm_curv's terms
+                nrm += r * r;
+            } else {
                 dy[i - nf] = r;
+            }
         }
-    nonfin = breduce(nonfin, OpMax(), sh);
-    if (threadIdx.x == 0) K.part[(b * kWideParts + blockIdx.y) * 2 + 1] = nonfin;
+    double rv[3] = {nonfin, dd, nrm};
+    const int ro[3] = {1, 0, 0};
+    breduce_n(rv, ro);
+    if (threadIdx.x == 0) {
+        double* pp = K.part + (b * kWideParts + blockIdx.y) * 4;
+        pp[1] = rv[0];
+        pp[2] = rv[1];
+        pp[3] = rv[2];
+    }
 }
 
 // grid (B, kWideParts): partial sums of dx^T W dx over contiguous ranges of the Hessian entries
@@ -915,7 +934,7 @@ __global__ void __launch_bounds__(kIB) k_wide_quad(const IpmK K) {
         quad += w * dx[r] * dx[c] * (K.hoff[s] ? 2.0 : 1.0);
     }
     quad = breduce(quad, OpSum(), sh);
-    if (threadIdx.x == 0) K.part[(b * kWideParts + blockIdx.y) * 2] = quad;
+    if (threadIdx.x == 0) K.part[(b * kWideParts + blockIdx.y) * 4] = quad;
 }
 
 // grid (B, ceil(P nA / kIB)): the chain's back substitution of the border, x_A = y_A - (A^-1 Cr) x_p (k_ipm_schur's
@@ -1200,15 +1219,15 @@ __global__ void __launch_bounds__(kIB) k_ipm_curv(const IpmK K, int slot) {
     const double* rb = K.rb + b * K.nKp;
     double* dx = (rs ? K.dxr : K.dx) + b * nf;
     double* dy = K.dy + b * K.m;
-    double nonfin = 0.0, quad = 0.0;
-    if (K.wide) {  // k_wide_unpack / k_wide_quad: partial sums of the blocks, in block order
-        const double* pt = K.part + b * kWideParts * 2;
-        for (int q = 0; q < kWideParts; ++q) {
-            quad += pt[2 * q];
-            nonfin = max_n(nonfin, pt[2 * q + 1]);
+    double nonfin = 0.0, quad = 0.0, dd = 0.0, nrm = 0.0;
+    if (K.wide) {  // k_wide_unpack / k_wide_quad: partial sums of the blocks (thread q holds block q's)
+        if (threadIdx.x < kWideParts) {
+            const double* pt = K.part + (b * kWideParts + threadIdx.x) * 4;
+            quad = pt[0];
+            nonfin = pt[1];
+            dd = pt[2];
+            nrm = pt[3];
         }
-        quad /= kIB;  // every thread holds the full sum; the reduction below adds kIB copies
-        nonfin = threadIdx.x == 0 ? nonfin : 0.0;
     } else {
         if (active || !rs)
             for (int i = threadIdx.x; i < K.nK; i += kIB) {
@@ -1229,11 +1248,11 @@ __global__ void __launch_bounds__(kIB) k_ipm_curv(const IpmK K, int slot) {
         }
     }
     const double* sig = K.sig + b * nf;
-    double dd = 0.0, nrm = 0.0;
-    for (int i = threadIdx.x; i < nf; i += kIB) {
-        dd += (sig[i] + dwc + (rs ? rs_prox(K, b, i) : 0.0)) * dx[i] * dx[i];
-        nrm += dx[i] * dx[i];
-    }
+    if (!K.wide)
+        for (int i = threadIdx.x; i < nf; i += kIB) {
+            dd += (sig[i] + dwc + (rs ? rs_prox(K, b, i) : 0.0)) * dx[i] * dx[i];
+            nrm += dx[i] * dx[i];
+        }
     {
         double rv[4] = {quad, dd, nrm, nonfin};
         const int ro[4] = {0, 0, 0, 1};
@@ -1257,6 +1276,13 @@ __global__ void __launch_bounds__(kIB) k_ipm_curv(const IpmK K, int slot) {
             dw = dwl > 0 ? clamp_lo(dwl / 3, 1e-20) : 1e-4;
         else
             dw = dw * 8;
+    }
+    if (threadIdx.x == 0 && active && !bad && !rs && S.hdeg == 0) {  // the iteration's trial passed: degeneracy test
+        if (S.dw == 0.0) {
+            S.hdeg = 1;
+        } else if (++S.degit >= kDegenIters) {
+            S.hdeg = 2;
+        }
     }
     store_scal(K, b, S);
     if (threadIdx.x == 0) {
@@ -3600,7 +3626,7 @@ static int ipm_create_common(cfx_ipm* s, const cfx_sizes& sz, int layout, const 
     K.wide = s->B <= 16 && (int64_t)nj + nh >= 262144;
     if (const char* e = std::getenv("CFX_IPM_WIDE")) K.wide = std::atoi(e) != 0;  // tuning / A-B override
     K.gj = dalloc<double>(s, B * nf, &rc);
-    K.part = dalloc<double>(s, B * kWideParts * 2, &rc);
+    K.part = dalloc<double>(s, B * kWideParts * 4, &rc);
     K.wpart = dalloc<double>(s, B * kWideParts * kWP, &rc);
     K.wflag = dalloc<double>(s, B * kWF, &rc);
     K.chain = chain ? 1 : 0;

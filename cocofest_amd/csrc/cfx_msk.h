@@ -1721,7 +1721,9 @@ __global__ void __launch_bounds__(256) k_msk_hproj(const MskParams P, const doub
 #pragma unroll
         for (int c = 0; c < NZ; ++c) {
             if (c < a || c >= nz) continue;
-            double sacc = c >= NX ? w[c] : 0.0;
+            double sacc = 0.0;  // w[c] for the control rows (T_q's identity), picked without a run-time register index
+#pragma unroll
+            for (int e = NX; e < NZ; ++e) sacc = e == c ? w[e] : sacc;
 #pragma unroll
             for (int I = 0; I < NX; ++I) sacc += ts[((int64_t)I * nz + c) * B] * w[I];
             out[c] += sacc;
@@ -1901,7 +1903,9 @@ __global__ void __launch_bounds__(256) k_msk_hproj_stage(const MskParams P, cons
 #pragma unroll
     for (int c = 0; c < NZ; ++c) {
         if (c < a || c >= nz) continue;
-        double sacc = c >= NX ? w[c] : 0.0;
+        double sacc = 0.0;  // w[c] for the control rows, picked without a run-time register index
+#pragma unroll
+        for (int e = NX; e < NZ; ++e) sacc = e == c ? w[e] : sacc;
 #pragma unroll
         for (int I = 0; I < NX; ++I) sacc += ts[((int64_t)I * nz + c) * B] * w[I];
         hq[(int64_t)(c * (c + 1) / 2 + a) * B] = sacc;
