@@ -3439,7 +3439,15 @@ static int ipm_create_common(cfx_ipm* s, const cfx_sizes& sz, int layout, const 
         const char* ke = std::getenv("CFX_IPM_KKT");
         const bool force_chain = ke && std::strcmp(ke, "chain") == 0, no_chain = ke && std::strcmp(ke, "band") == 0;
         const bool wide = !cfx_band_reg_ok(nAb, (int32_t)ord.kl, (int32_t)ord.ku) && s->B <= 64 && nK >= 4096;
-        if (force_chain || (wide && !no_chain)) cp = chain_plan(nf, m, freev, par, jrF, jcF, hrF, hcF, kMaxBorder);
+        if (force_chain || (wide && !no_chain)) {
+            cp = chain_plan(nf, m, freev, par, jrF, jcF, hrF, hcF, kMaxBorder);
+        } else if (!no_chain && s->B <= 4) {
+            // a few short chains (<= 16 nodes: <= 4 reduction levels) also beat nested dissection at batch 1 once
+            // the pivot blocks are fast: cfg 5 (11 nodes of 32) 136 vs 229 ms per solve; cfg 3 (101 nodes of 16,
+            // 7 levels) stays with dissection, 13.7 vs 10.1 ms (profiles/round5/b1/b1_layouts_r5end.jsonl)
+            cp = chain_plan(nf, m, freev, par, jrF, jcF, hrF, hcF, kMaxBorder);
+            if (cp.ok && cp.M > 16) cp = ChainPlan{};
+        }
     }
     const bool chain = cp.ok;
     int64_t nd_batch = 512;
