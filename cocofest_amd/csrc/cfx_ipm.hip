@@ -72,7 +72,7 @@ struct Scal {
     // the try was accepted by the original filter
     double soft_a, soft_pd;
     int32_t soft_on, soft_cnt, soft_try, soft_ok;
-    int32_t rs_rr;  // the phase's last iteration reset p, n (Ipopt's RestoRestorationPhase) instead of stepping
+    int32_t rs_rr;  // consecutive phase iterations that reset p, n (Ipopt's RestoRestorationPhase) instead of stepping
     int32_t rpad;
     // Ipopt's structural-degeneracy test of the Hessian (PDPerturbationHandler, degen_iters_max = 3): hdeg 0 not yet
     // determined, 1 not degenerate (an iteration's first trial with dw = 0 passed), 2 degenerate (the first
@@ -2393,6 +2393,11 @@ __global__ void __launch_bounds__(kIB) k_rs_next_trial(const IpmK K) {
     if (threadIdx.x == 0) K.sc[b].rs_alpha = a;
 }
 
+// consecutive p, n resets after which a phase whose line search keeps failing gives up (Ipopt has no such bound: its
+// RestoRestorationPhase always succeeds and the phase runs on to max_resto_iter); CFX_RS_RR_MAX for experiments
+__device__ __constant__ int g_rs_rr_max = 1;
+__device__ inline int rs_rr_max() { return g_rs_rr_max; }
+
 // end of a phase iteration: the step (primal-dual, z safeguard), the phase's filter, the exit test on the original
 // problem and, on exit, the original bound multipliers; rs_exit records how the phase ended (k_ipm_update acts on it).
 // A failed line search of the phase is answered as Ipopt's RestoRestorationPhase does: x stays, p and n take their
@@ -2406,7 +2411,7 @@ __global__ void __launch_bounds__(kIB) k_rs_update(const IpmK K) {
     const int nf = K.nf, m = K.m;
     load_scal(K, b, S);
     if (!S.rs_on || S.rs_exit != RS_RUNNING) return;  // block-uniform
-    if (!S.rs_acc && S.rs_rr) {
+    if (!S.rs_acc && S.rs_rr >= rs_rr_max()) {
         __syncthreads();
         if (threadIdx.x == 0) {
             S.rs_exit = RS_FAILED;
@@ -2434,7 +2439,7 @@ __global__ void __launch_bounds__(kIB) k_rs_update(const IpmK K) {
             const int k = S.rs_it % kFilt;
             rf[2 * k] = (1 - 1e-5) * S.rs_theta;
             rf[2 * k + 1] = S.rs_phi - 1e-5 * S.rs_theta;
-            S.rs_rr = 1;
+            S.rs_rr += 1;
             S.rs_it += 1;
             S.iters += 1;
             atomicAdd(K.rstat + 1, 1ull);
@@ -3205,6 +3210,10 @@ static int ipm_create_common(cfx_ipm* s, const cfx_sizes& sz, int layout, const 
         K.o = *opt;
     else
         cfx_ipm_default_options(&K.o);
+    if (const char* e = std::getenv("CFX_RS_RR_MAX")) {  // experiment override (see rs_rr_max)
+        const int v = std::max(1, std::atoi(e));
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_rs_rr_max), &v, sizeof(int)) != hipSuccess) return CFX_EHIP;
+    }
     if ((s->B > 1 && layout != CFX_LAYOUT_AOS) || layout == CFX_LAYOUT_TILED64 ||
         n_params < 0 || n_params > sz.nv || K.o.max_iter < 0 || K.o.max_backtrack < 1 || K.o.max_soc < 0 ||
         K.o.watchdog_shortened_iter_trigger < 0 || K.o.watchdog_trial_iter_max < 0 ||
