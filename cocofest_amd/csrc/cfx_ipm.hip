@@ -106,6 +106,10 @@ struct IpmK {
     // ([B][2][cM][csp][csp]), ct its solve scratch ([B][max(na, 1)][nA]); a border (np > 0) as below.
     int chain, cM, csp;
     double *cw, *ct;
+    // chain: the band-storage positions with a source (the rest of [D | L | U] is zero and is cleared by a memset, not
+    // by one thread per entry: 28.8 M entries of which ~1 in 6 has a source for the reaching task)
+    const int32_t* nzpos;
+    int64_t nnzA;
     // Wide instances (wide = 1: small batches of large NLPs, e.g. the reaching task's 2.4 M J_g values in one instance):
     // the gather loops of k_ipm_begin (J_g scaling, J^T y), k_ipm_curv (unpacking, x^T W x) and the border's back
     // substitution run as grids of many blocks per instance (k_wide_*) instead of one block's serial loop; gj [B][nf]
@@ -622,63 +626,73 @@ __global__ void __launch_bounds__(kIB) k_ipm_begin(const IpmK K, int mode, int s
 //   NEWTON: [[W + Sigma + dw, J^T], [J, -delta_c]], rhs as k_ipm_begin left it
 //   LSMULT: [[I, J^T], [J, -delta_c]], rhs [-(grad f - zl + zu); 0]   (least-squares multipliers)
 //   RESTO : [[Sigma + I, J^T], [J, -delta_c]], rhs [0; -g]            (restoration step)
+// one band-storage entry of the KKT matrix (p < NE_tot) from its sources
+__device__ inline void kkt_entry(const IpmK& K, int64_t b, int64_t p, int mode) {
+    double v = 0.0;
+    const double* hv = K.hv + b * K.nnzh;
+    const double* jv = K.jv + b * K.nj;
+    const double* sig = K.sig + b * K.nf;
+    // L-BFGS: W = sigma I - low rank (Woodbury); restoration phase (the Newton matrix of an instance in it): its
+    // own regularisation and proximity term
+    const bool rs = mode == KKT_RSNLP || (mode == KKT_NEWTON && K.sc[b].rs_on);
+    const double dw = rs ? K.sc[b].rs_dw : K.sc[b].dw + (K.lbfgs ? K.sc[b].lsig : 0.0);
+    for (int k = K.kkt_ptr[p]; k < K.kkt_ptr[p + 1]; ++k) {
+        const int32_t code = K.kkt_src[k];
+        const int idx = code & kSrcMask;
+        switch (code >> kSrcShift) {
+            case SRC_W:
+                if (mode == KKT_NEWTON || rs) v += hv[K.hsel[idx]] * K.d[K.hr[idx]] * K.d[K.hc[idx]];
+                break;
+            case SRC_JV: v += jv[idx]; break;
+            case SRC_DIAG:
+                if (rs)
+                    v += sig[idx] + dw + rs_prox(K, b, idx);
+                else
+                    v += mode == KKT_NEWTON ? sig[idx] + dw : (mode == KKT_LSMULT ? 1.0 : sig[idx] + 1.0);
+                break;
+            default:  // unit diagonal of a padding row / -delta_c (restoration: - p / zp - n / zn of row idx)
+                v += idx == kSrcMask ? 1.0 : -K.o.delta_c + (rs ? K.rdc[b * K.m + idx] : 0.0);
+                break;
+        }
+    }
+    if (p < K.NE_A) {
+        K.ab[b * K.NE_A + p] = v;
+    } else {  // the border: Cr (active columns per block, as right-hand sides), Cc non-zeros, D
+        const int64_t nb = (int64_t)K.P * K.na * K.nA;
+        int64_t q = p - K.NE_A;
+        if (q < nb)
+            K.Xb[b * nb + q] = v;
+        else if ((q -= nb) < K.ncc)
+            K.Ccb[b * K.ncc + q] = v;
+        else
+            K.Db[b * K.np * K.np + (q - K.ncc)] = v;
+    }
+}
+
+// the permuted right-hand side entry p < nK
+__device__ inline void kkt_rhs(const IpmK& K, int64_t b, int64_t p, int mode) {
+    const int nf = K.nf;
+    double r;
+    if (mode == KKT_NEWTON || mode == KKT_RSNLP)
+        r = K.rhs[b * K.nK + p];
+    else if (mode == KKT_LSMULT)
+        r = p < nf ? -(K.gF[b * nf + p] - K.zl[b * nf + p] + K.zu[b * nf + p]) : 0.0;
+    else
+        r = p < nf ? 0.0 : -K.gS[b * K.m + (p - nf)];
+    K.rb[b * K.nKp + K.pos[p]] = r;
+}
+
 __global__ void __launch_bounds__(kIB) k_ipm_kkt(const IpmK K, int mode) {
     const int64_t b = blockIdx.x;
-    const int64_t NE = K.NE_tot;
-    // grid-stride over the entries: grid.y is capped at kMaxY (a 1,500-interval MSK KKT matrix has ~18 M entries)
-    for (int64_t p = (int64_t)blockIdx.y * kIB + threadIdx.x; p < NE || p < K.nK; p += (int64_t)gridDim.y * kIB) {
-    if (p < NE) {
-        double v = 0.0;
-        const double* hv = K.hv + b * K.nnzh;
-        const double* jv = K.jv + b * K.nj;
-        const double* sig = K.sig + b * K.nf;
-        // L-BFGS: W = sigma I - low rank (Woodbury); restoration phase (the Newton matrix of an instance in it): its
-        // own regularisation and proximity term
-        const bool rs = mode == KKT_RSNLP || (mode == KKT_NEWTON && K.sc[b].rs_on);
-        const double dw = rs ? K.sc[b].rs_dw : K.sc[b].dw + (K.lbfgs ? K.sc[b].lsig : 0.0);
-        for (int k = K.kkt_ptr[p]; k < K.kkt_ptr[p + 1]; ++k) {
-            const int32_t code = K.kkt_src[k];
-            const int idx = code & kSrcMask;
-            switch (code >> kSrcShift) {
-                case SRC_W:
-                    if (mode == KKT_NEWTON || rs) v += hv[K.hsel[idx]] * K.d[K.hr[idx]] * K.d[K.hc[idx]];
-                    break;
-                case SRC_JV: v += jv[idx]; break;
-                case SRC_DIAG:
-                    if (rs)
-                        v += sig[idx] + dw + rs_prox(K, b, idx);
-                    else
-                        v += mode == KKT_NEWTON ? sig[idx] + dw : (mode == KKT_LSMULT ? 1.0 : sig[idx] + 1.0);
-                    break;
-                default:  // unit diagonal of a padding row / -delta_c (restoration: - p / zp - n / zn of row idx)
-                    v += idx == kSrcMask ? 1.0 : -K.o.delta_c + (rs ? K.rdc[b * K.m + idx] : 0.0);
-                    break;
-            }
+    // chain with a source list (nzpos): entries t < nnzA are the positions with sources in [D | L | U] (the rest was
+    // cleared), then the border's; otherwise every entry.  grid-stride: grid.y is capped at kMaxY
+    const int64_t NE = K.nzpos ? K.nnzA + (K.NE_tot - K.NE_A) : K.NE_tot;
+    for (int64_t t = (int64_t)blockIdx.y * kIB + threadIdx.x; t < NE || t < K.nK; t += (int64_t)gridDim.y * kIB) {
+        if (t < NE) {
+            const int64_t p = K.nzpos ? (t < K.nnzA ? (int64_t)K.nzpos[t] : K.NE_A + (t - K.nnzA)) : t;
+            kkt_entry(K, b, p, mode);
         }
-        if (p < K.NE_A) {
-            K.ab[b * K.NE_A + p] = v;
-        } else {  // the border: Cr (active columns per block, as right-hand sides), Cc non-zeros, D
-            const int64_t nb = (int64_t)K.P * K.na * K.nA;
-            int64_t q = p - K.NE_A;
-            if (q < nb)
-                K.Xb[b * nb + q] = v;
-            else if ((q -= nb) < K.ncc)
-                K.Ccb[b * K.ncc + q] = v;
-            else
-                K.Db[b * K.np * K.np + (q - K.ncc)] = v;
-        }
-    }
-    if (p < K.nK) {
-        const int nf = K.nf;
-        double r;
-        if (mode == KKT_NEWTON || mode == KKT_RSNLP)
-            r = K.rhs[b * K.nK + p];
-        else if (mode == KKT_LSMULT)
-            r = p < nf ? -(K.gF[b * nf + p] - K.zl[b * nf + p] + K.zu[b * nf + p]) : 0.0;
-        else
-            r = p < nf ? 0.0 : -K.gS[b * K.m + (p - nf)];
-        K.rb[b * K.nKp + K.pos[p]] = r;
-    }
+        if (t < K.nK) kkt_rhs(K, b, t, mode);
     }
 }
 
@@ -3621,6 +3635,15 @@ static int ipm_create_common(cfx_ipm* s, const cfx_sizes& sz, int layout, const 
     K.jrw_idx = dupload(s, jrwidx, &rc);
     K.kkt_ptr = dupload(s, kptr, &rc);
     K.kkt_src = dupload(s, kcode, &rc);
+    K.nzpos = nullptr;
+    K.nnzA = 0;
+    if (chain) {  // the [D | L | U] positions with a source (k_ipm_kkt); the others stay zero after a memset
+        std::vector<int32_t> nzp;
+        for (int64_t p = 0; p < NE_A; ++p)
+            if (kptr[p + 1] > kptr[p]) nzp.push_back((int32_t)p);
+        K.nnzA = (int64_t)nzp.size();
+        if (!nzp.empty()) K.nzpos = dupload(s, nzp, &rc);
+    }
     K.pos = dupload(s, pos, &rc);
     const size_t B = (size_t)s->B;
     double** fbufs[] = {&K.x,   &K.zl,  &K.zu, &K.dx,  &K.dzl, &K.dzu, &K.xt, &K.xacc, &K.xr,
@@ -3842,7 +3865,9 @@ struct Run {
     }
     int kkt_factor(int mode) {
         const IpmK& K = s->K;
-        const int64_t nblk = (std::max<int64_t>(K.NE_tot, K.nK) + kIB - 1) / kIB;
+        const int64_t NE = K.nzpos ? K.nnzA + (K.NE_tot - K.NE_A) : K.NE_tot;
+        if (K.nzpos) IPM_HIP(s, hipMemsetAsync(K.ab, 0, (size_t)K.B * K.NE_A * sizeof(double), st));
+        const int64_t nblk = (std::max<int64_t>(NE, K.nK) + kIB - 1) / kIB;
         hipLaunchKernelGGL(k_ipm_kkt, dim3((unsigned)K.B, (unsigned)std::min<int64_t>(nblk, kMaxY)), dim3(kIB), 0, st,
                            K, mode);
         IPM_HIP(s, hipGetLastError());
