@@ -413,26 +413,24 @@ MSK_HD void msk_point(const S (*R)[9], const S (*o)[3], const S (*z)[3], int f, 
         }
         return;
     }
-    // dual numbers: every frame's transform is formed and the point's own selected (f is wave-uniform) — with a
-    // branch per frame the compiler merged the branches into copies from R[f] / o[f], f a run-time index, which kept
-    // the frames in scratch memory
+    // dual numbers: the point's own frame only, one branch per frame (f is wave-uniform).  Each branch ends in an
+    // inline-asm marker of its own: without it the compiler merged the branches' identical tails into copies from
+    // R[f] / o[f] with f a run-time index, which kept the frames in scratch memory
 #pragma unroll
     for (int j = 0; j < NQ; ++j) {
-        const bool own = f == j;
+        if (f == j) {
 #pragma unroll
-        for (int e = 0; e < 3; ++e) {
-            const S Pj = o[j][e] + R[j][e * 3] * p[0] + R[j][e * 3 + 1] * p[1] + R[j][e * 3 + 2] * p[2];
-            P[e] = msel(own, Pj, P[e]);
+            for (int e = 0; e < 3; ++e)
+                P[e] = o[j][e] + R[j][e * 3] * p[0] + R[j][e * 3 + 1] * p[1] + R[j][e * 3 + 2] * p[2];
+#pragma unroll
+            for (int k = 0; k <= j; ++k) {
+                const S r[3] = {P[0] - o[k][0], P[1] - o[k][1], P[2] - o[k][2]};
+                cross3(z[k], r, dP[k]);
+            }
+#if defined(__HIP_DEVICE_COMPILE__)
+            asm volatile("; msk_point frame %0" ::"n"(j));
+#endif
         }
-    }
-#pragma unroll
-    for (int k = 0; k < NQ; ++k) {
-        const bool above = k <= f;
-        const S r[3] = {P[0] - o[k][0], P[1] - o[k][1], P[2] - o[k][2]};
-        S c[3];
-        cross3(z[k], r, c);
-#pragma unroll
-        for (int e = 0; e < 3; ++e) dP[k][e] = msel(above, c[e], dP[k][e]);
     }
 }
 
