@@ -316,3 +316,29 @@ def test_native_ipm_unscaled_termination_tests():
     lb, ub = ocp.bounds_vector()
     span = np.where(np.isfinite(ub - lb), ub - lb, np.maximum(np.abs(base.v).max(0), 1.0))
     assert np.max(np.abs(res.v - base.v) / np.maximum(span, 1e-12)) < 1e-6
+
+
+@pytest.mark.parametrize("B", [1, 4])
+def test_native_ipm_wide_split_kernels_reach_the_same_optimum(B, monkeypatch):
+    """The wide-instance path (IpmK::wide: the long loops of k_ipm_begin / dir / accept / update / curv as grids of
+    partial sums, the one-block kernels on the reduced values, grids over the elementwise updates — chosen for the
+    reaching task's 120,000 unknowns) forced on a small problem (CFX_IPM_WIDE=1) against the one-block kernels: the
+    same optimum; the sums run in another fixed order, so the path may differ by rounding."""
+    from cocofest_amd.solver import IpmOptions, NativeIpm
+
+    cfg = dict(cases.cfg3(), objective=TRACK)
+    ocp = cases.product_ocp(**cfg)
+    v0 = _starts(ocp, B, 3)
+    out = {}
+    for wide in ("0", "1"):
+        monkeypatch.setenv("CFX_IPM_WIDE", wide)
+        nat = NativeIpm(ocp, batch=B, options=IpmOptions(tol=1e-8, max_iter=300))
+        out[wide] = nat.solve(v0)
+        nat.close()
+    a, b = out["0"], out["1"]
+    assert a.converged.all() and b.converged.all(), (a.status, b.status)
+    np.testing.assert_allclose(b.f, a.f, rtol=1e-8, atol=1e-10)
+    lb, ub = ocp.bounds_vector()
+    span = np.where(np.isfinite(ub - lb), ub - lb, 1.0)
+    assert np.max(np.abs(b.v - a.v) / np.maximum(span, 1e-12)) < 1e-5
+    assert np.all(np.abs(b.iterations - a.iterations) <= 5), (a.iterations, b.iterations)
