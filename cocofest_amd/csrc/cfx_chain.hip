@@ -360,12 +360,18 @@ __global__ void __launch_bounds__(kNT) k_chain_upd(Chain C, int h) {
 
 // y = M x for an SP x SP row-major matrix and an LDS vector, rows over threads [t0, t0 + SP)
 template <int SP>
+// (four interleaved partial sums: the single chain of sp dependent FMAs was the solve kernels' latency)
 __device__ __forceinline__ double row_dot(const double* __restrict__ Mx, int r, const double* x) {
-    double acc = 0.0;
+    double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
     const double* row = Mx + (int64_t)r * SP;
-#pragma unroll 8
-    for (int k = 0; k < SP; ++k) acc = fma(row[k], x[k], acc);
-    return acc;
+#pragma unroll 4
+    for (int k = 0; k < SP; k += 4) {
+        a0 = fma(row[k], x[k], a0);
+        a1 = fma(row[k + 1], x[k + 1], a1);
+        a2 = fma(row[k + 2], x[k + 2], a2);
+        a3 = fma(row[k + 3], x[k + 3], a3);
+    }
+    return (a0 + a1) + (a2 + a3);
 }
 
 struct Rhs {
@@ -404,10 +410,17 @@ __global__ void __launch_bounds__(kNT) k_chain_fwd(Chain C, Rhs X, int h) {
         if (hj) tj[t - 128] = row_dot<SP>(C.D + b * C.stride + j * NB, t - 128, vj);
     }
     __syncthreads();
+    // the two coupling products in the two thread halves, summed through LDS (vi / vj are free again)
+    if (t < SP) {
+        if (hi) vi[t] = row_dot<SP>(cur_u<SP>(C, b, p, h), t, ti);
+    } else if (t >= 128 && t < 128 + SP) {
+        if (hj) vj[t - 128] = row_dot<SP>(cur_l<SP>(C, b, p, h), t - 128, tj);
+    }
+    __syncthreads();
     if (t < SP && (hi || hj)) {
         double acc = R[(int64_t)p * SP + t];
-        if (hi) acc -= row_dot<SP>(cur_u<SP>(C, b, p, h), t, ti);
-        if (hj) acc -= row_dot<SP>(cur_l<SP>(C, b, p, h), t, tj);
+        if (hi) acc -= vi[t];
+        if (hj) acc -= vj[t];
         R[(int64_t)p * SP + t] = acc;
     }
 }
@@ -440,9 +453,13 @@ __global__ void __launch_bounds__(kNT) k_chain_bwd(Chain C, Rhs X, int h) {
         xr[r] = hr ? R[(int64_t)(i + h) * SP + r] : 0.0;
     }
     __syncthreads();
+    __shared__ double yl[SP], yr[SP];
+    if (t < SP) yl[t] = row_dot<SP>(cur_l<SP>(C, b, i, h), t, xl);
+    else if (t >= 128 && t < 128 + SP && hr) yr[t - 128] = row_dot<SP>(cur_u<SP>(C, b, i, h), t - 128, xr);
+    __syncthreads();
     if (t < SP) {
-        double acc = T[(int64_t)i * SP + t] - row_dot<SP>(cur_l<SP>(C, b, i, h), t, xl);
-        if (hr) acc -= row_dot<SP>(cur_u<SP>(C, b, i, h), t, xr);
+        double acc = T[(int64_t)i * SP + t] - yl[t];
+        if (hr) acc -= yr[t];
         R[(int64_t)i * SP + t] = acc;
     }
 }
