@@ -276,19 +276,24 @@ __global__ void __launch_bounds__(kNT) k_chain_elim(Chain C, int first, int step
 // the order of one K loop per product, products in the order above.  (Round 5 first version: one workgroup per
 // survivor, left operands read from global memory per MFMA, output column blocks per wave — 115 us per tail level
 // for SP = 80, where the FP64 matrix cores need ~7.)
+// BLDS: the right operand staged in LDS too (when both fit: SP <= 96).  The launcher stages it only for levels with
+// fewer than kUpdGlobalB survivors: at the wide levels the doubled LDS halves the workgroups per CU, and reading the
+// right operand from L2 is faster (reaching task, micro: level 0 249 -> 155 us, level 1 108 -> 86 us; the tail
+// levels the other way, 35 vs 48 us)
+constexpr int kUpdGlobalB = 256;
 template <int SP>
-constexpr bool chain_b_in_lds() {
+constexpr bool chain_b_fits() {
     return 2 * SP * (SP + 1) * 8 <= 150 * 1024;
 }
-template <int SP>
+template <int SP, bool BLDS>
 constexpr size_t chain_upd_lds() {
-    return (size_t)(chain_b_in_lds<SP>() ? 2 : 1) * SP * (SP + 1) * sizeof(double);
+    return (size_t)(BLDS ? 2 : 1) * SP * (SP + 1) * sizeof(double);
 }
-template <int SP>
+template <int SP, bool BLDS>
 __global__ void __launch_bounds__(kNT) k_chain_upd(Chain C, int h) {
     constexpr int T16 = SP / 16, NT = T16 * T16, TPW = (NT + 3) / 4;  // output tiles, per wave
     constexpr int LD = SP + 1;
-    constexpr bool BL = chain_b_in_lds<SP>();
+    constexpr bool BL = BLDS && chain_b_fits<SP>();
     extern __shared__ double sm[];
     double* sA = sm;
     double* sB = sm + SP * LD;
@@ -473,17 +478,21 @@ static int levels(int M) {
 template <int SP>
 static hipError_t factor_sp(const Chain& C, int64_t B, int32_t* info, hipStream_t s) {
     const int L = levels(C.M);
-    if (chain_upd_lds<SP>() > 65536) {  // above the default dynamic LDS limit: raised once per kernel
-        static const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_chain_upd<SP>),
+    constexpr bool FITS = chain_b_fits<SP>();
+    if (chain_upd_lds<SP, FITS>() > 65536) {  // above the default dynamic LDS limit: raised once per kernel
+        static const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_chain_upd<SP, FITS>),
                                                         hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                        (int)chain_upd_lds<SP>());
+                                                        (int)chain_upd_lds<SP, FITS>());
         if (e != hipSuccess) return e;
     }
     for (int l = 0; l < L; ++l) {
         const int h = 1 << l;
         const int ne = (C.M - h + 2 * h - 1) / (2 * h), ns = (C.M + 2 * h - 1) / (2 * h);
         hipLaunchKernelGGL(k_chain_elim<SP>, dim3((unsigned)ne, (unsigned)B), dim3(kNT), 0, s, C, h, 2 * h, h, info);
-        hipLaunchKernelGGL(k_chain_upd<SP>, dim3((unsigned)ns, (unsigned)B, 3), dim3(kNT), chain_upd_lds<SP>(), s, C, h);
+        if (FITS && ns < kUpdGlobalB)
+            k_chain_upd<SP, FITS><<<dim3((unsigned)ns, (unsigned)B, 3), dim3(kNT), chain_upd_lds<SP, FITS>(), s>>>(C, h);
+        else
+            k_chain_upd<SP, false><<<dim3((unsigned)ns, (unsigned)B, 3), dim3(kNT), chain_upd_lds<SP, false>(), s>>>(C, h);
     }
     hipLaunchKernelGGL(k_chain_elim<SP>, dim3(1, (unsigned)B), dim3(kNT), 0, s, C, 0, 1, 1 << L, info);
     return hipGetLastError();

@@ -30,8 +30,8 @@ int main(int argc, char** argv) {
     CK(hipEventCreate(&a));
     CK(hipEventCreate(&b));
     const cfx_chain::Chain C{d, d + nb, d + 2 * nb, w, w + nb, 0, 0, M};
-    CK(hipFuncSetAttribute(reinterpret_cast<const void*>(&cfx_chain::k_chain_upd<SP>),
-                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)cfx_chain::chain_upd_lds<SP>()));
+    CK(hipFuncSetAttribute(reinterpret_cast<const void*>(&cfx_chain::k_chain_upd<SP, true>),
+                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)cfx_chain::chain_upd_lds<SP, true>()));
     for (int rep = 0; rep < 3; ++rep) {
         CK(hipMemcpy(d, h.data(), 3 * nb * sizeof(double), hipMemcpyHostToDevice));
         float tot = 0;
@@ -44,7 +44,10 @@ int main(int argc, char** argv) {
             CK(hipEventSynchronize(b));
             CK(hipEventElapsedTime(&te, a, b));
             CK(hipEventRecord(a));
-            hipLaunchKernelGGL(cfx_chain::k_chain_upd<SP>, dim3(ns, 1, 3), dim3(256), cfx_chain::chain_upd_lds<SP>(), 0, C, hh);
+            if (ns < cfx_chain::kUpdGlobalB)
+                cfx_chain::k_chain_upd<SP, true><<<dim3(ns, 1, 3), dim3(256), cfx_chain::chain_upd_lds<SP, true>(), 0>>>(C, hh);
+            else
+                cfx_chain::k_chain_upd<SP, false><<<dim3(ns, 1, 3), dim3(256), cfx_chain::chain_upd_lds<SP, false>(), 0>>>(C, hh);
             CK(hipEventRecord(b));
             CK(hipEventSynchronize(b));
             CK(hipEventElapsedTime(&tu, a, b));
