@@ -15,7 +15,7 @@ import numpy as np
 
 LIB_PATH = pathlib.Path(__file__).with_name("libcfx.so")
 
-ABI_VERSION = 9
+ABI_VERSION = 10
 OK, EINVAL, EHIP, ENOMEM, EUNSUPPORTED, ENODEV, ECALLBACK = 0, -1, -2, -3, -4, -5, -6
 MODEL_IDS = {
     "ding2003": 0,
@@ -124,7 +124,7 @@ class IpmOptions(C.Structure):
                 ("warm_start_bound_frac", C.c_double), ("warm_start_mult_bound_push", C.c_double),
                 ("warm_start_init_point", C.c_int32), ("honor_original_bounds", C.c_int32),
                 ("range_scaling", C.c_int32), ("bound_mult_init_method", C.c_int32),
-                ("bound_mult_init_val", C.c_double)]
+                ("bound_mult_init_val", C.c_double), ("inertia_test", C.c_int32)]
 
 
 # cfx_ipm_get_status values (Ipopt's ApplicationReturnStatus)
@@ -193,6 +193,7 @@ SIGNATURES = {
     "cfx_ipm_get_bound_multipliers": (C.c_int, [_P, _P, _P, C.c_uint32]),
     "cfx_btri_factor": (C.c_int, [C.c_int64, C.c_int32, C.c_int32, _P, _P, _P, _P, _P, _P]),
     "cfx_btri_solve": (C.c_int, [C.c_int64, C.c_int32, C.c_int32, _P, _P, _P, _P, C.c_int32, _P, _P, _P]),
+    "cfx_btri_inertia": (C.c_int, [C.c_int64, C.c_int32, C.c_int32, _P, _P, _P]),
     "cfx_ipm_create_ext": (C.c_int, [C.POINTER(NlpDesc), C.POINTER(Evaluator), _P, _P, C.c_int32,
                                      C.POINTER(IpmOptions), C.POINTER(_P)]),
     "cfx_gather_sum": (C.c_int, [C.c_int64, C.c_int64, _P, _P, _P, C.c_int64, _P, _P]),

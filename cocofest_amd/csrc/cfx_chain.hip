@@ -37,6 +37,7 @@
 #include <string>
 
 #include "../../include/cfx.h"
+#include "cfx_inertia.h"
 #include "cfx_internal.h"
 
 namespace cfx_chain {
@@ -515,6 +516,41 @@ static hipError_t solve_sp(const Chain& C, int64_t B, const Rhs& X, int nrhs, hi
     return hipGetLastError();
 }
 
+// Negative eigenvalues of the factored symmetric block-tridiagonal matrix (the interior point's inertia correction,
+// cfx_inertia.h), added to neg[b]: block cyclic reduction is a sequence of congruences, so the matrix's inertia is the
+// sum of its pivot blocks' (node k at its elimination level), and node k's D slot holds that block's inverse, whose
+// inertia is the block's.  One workgroup per node (grid M x batch); the inverse is symmetrised on its way to LDS.
+template <int SP>
+constexpr size_t chain_inertia_lds() {
+    return (size_t)SP * (SP + 1) * sizeof(double);
+}
+template <int SP>
+__global__ void __launch_bounds__(kNT) k_chain_inertia(Chain C, int32_t* __restrict__ neg) {
+    extern __shared__ double A[];
+    constexpr int64_t NB = (int64_t)SP * SP;
+    const int64_t b = blockIdx.y;
+    const double* D = C.D + b * C.stride + blockIdx.x * NB;
+    for (int e = threadIdx.x; e < SP * SP; e += kNT) {
+        const int r = e / SP, c = e % SP;
+        A[r * (SP + 1) + c] = 0.5 * (D[r * SP + c] + D[c * SP + r]);
+    }
+    __syncthreads();
+    const int cnt = cfx_inertia::sym_neg_count(A, SP + 1, SP);
+    if (threadIdx.x == 0 && cnt) atomicAdd(neg + b, cnt);
+}
+
+template <int SP>
+static hipError_t inertia_sp(const Chain& C, int64_t B, int32_t* neg, hipStream_t s) {
+    if (chain_inertia_lds<SP>() > 65536) {
+        static const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_chain_inertia<SP>),
+                                                        hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                        (int)chain_inertia_lds<SP>());
+        if (e != hipSuccess) return e;
+    }
+    k_chain_inertia<SP><<<dim3((unsigned)C.M, (unsigned)B), dim3(kNT), chain_inertia_lds<SP>(), s>>>(C, neg);
+    return hipGetLastError();
+}
+
 #define CFX_CHAIN_SP(F, ...)                                     \
     switch (sp) {                                                \
         case 16: e = F<16>(__VA_ARGS__); break;                  \
@@ -572,6 +608,22 @@ int cfx_chain_solve_s(int64_t batch, int32_t M, int32_t sp, const double* D, con
     return CFX_OK;
 }
 
+int cfx_chain_inertia_s(int64_t batch, int32_t M, int32_t sp, const double* D, int64_t stride, int32_t* neg,
+                        void* stream) {
+    if (batch < 1 || batch > 65535 || M < 1 || !cfx_chain_sp_ok(sp) || !D || !neg) {
+        g_create_error = "cfx_chain_inertia: invalid argument";
+        return CFX_EINVAL;
+    }
+    const cfx_chain::Chain C{const_cast<double*>(D), nullptr, nullptr, nullptr, nullptr, stride, 0, M};
+    hipError_t e;
+    CFX_CHAIN_SP(cfx_chain::inertia_sp, C, batch, neg, (hipStream_t)stream)
+    if (e != hipSuccess) {
+        g_create_error = std::string("cfx_chain_inertia: ") + hipGetErrorString(e);
+        return CFX_EHIP;
+    }
+    return CFX_OK;
+}
+
 // ---- C ABI (include/cfx.h): contiguous layout [batch][M][sp][sp] per array ------------------------------------
 extern "C" int cfx_btri_factor(int64_t batch, int32_t M, int32_t sp, double* D, double* L, double* U, double* work,
                                int32_t* info, void* stream) {
@@ -592,4 +644,16 @@ extern "C" int cfx_btri_solve(int64_t batch, int32_t M, int32_t sp, const double
     const int64_t st = (int64_t)M * sp * sp, nv = (int64_t)M * sp;
     return cfx_chain_solve_s(batch, M, sp, D, L, U, st, work, work + batch * st, st, nrhs, rhs, nrhs * nv, nv, scratch,
                              nrhs * nv, nv, stream);
+}
+
+extern "C" int cfx_btri_inertia(int64_t batch, int32_t M, int32_t sp, const double* D, int32_t* neg, void* stream) {
+    if (!neg || batch < 1 || batch > 65535) {
+        g_create_error = "cfx_btri_inertia: invalid argument";
+        return CFX_EINVAL;
+    }
+    if (hipMemsetAsync(neg, 0, batch * sizeof(int32_t), (hipStream_t)stream) != hipSuccess) {
+        g_create_error = "cfx_btri_inertia: hipMemsetAsync failed";
+        return CFX_EHIP;
+    }
+    return cfx_chain_inertia_s(batch, M, sp, D, (int64_t)M * sp * sp, neg, stream);
 }

@@ -37,3 +37,7 @@ int cfx_chain_factor_s(int64_t batch, int32_t M, int32_t sp, double* D, double* 
 int cfx_chain_solve_s(int64_t batch, int32_t M, int32_t sp, const double* D, const double* L, const double* U,
                       int64_t stride, const double* Cl, const double* Cr, int64_t wstride, int32_t nrhs, double* R,
                       int64_t r_inst, int64_t r_rhs, double* T, int64_t t_inst, int64_t t_rhs, void* stream);
+// negative eigenvalues of the symmetric block-tridiagonal matrix factored by cfx_chain_factor_s (its D slots), added
+// to neg[b] (zero pivots add 1 << 20)
+int cfx_chain_inertia_s(int64_t batch, int32_t M, int32_t sp, const double* D, int64_t stride, int32_t* neg,
+                        void* stream);

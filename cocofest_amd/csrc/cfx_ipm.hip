@@ -33,6 +33,7 @@
 #include <vector>
 
 #include "../../include/cfx.h"
+#include "cfx_inertia.h"
 #include "cfx_internal.h"
 
 namespace {
@@ -146,6 +147,9 @@ struct IpmK {
     // [B][P][na][nA] Cr -> A^-1 Cr (active columns), [B][ncc] Cc non-zeros, [B][np][np] D, LU of the Schur complement
     double *Xb, *Ccb, *Db, *Sf;
     int32_t* Sp;  // [B][np] its pivots
+    // inertia test (o.inertia_test, stage chain): [B] negative eigenvalues of the last factorisation (the chain's pivot
+    // blocks by cfx_chain_inertia_s, the border's Schur complement by k_ipm_schur); null: the curvature test
+    int32_t* inert;
     int32_t *ipiv, *info;                                                   // [B][P][nA], [B][P]
     double* filt;                                                           // [B][kFilt][2]
     Scal* sc;                                                               // [B]
@@ -765,6 +769,16 @@ __global__ void __launch_bounds__(kIB) k_ipm_schur(const IpmK K, int factor, int
             S[i][j] = acc;
         }
         __syncthreads();
+        if (K.inert) {  // inertia test: the border's share of the KKT matrix's negative eigenvalues (Haynsworth)
+            __shared__ double S2[kMaxBorder * (kMaxBorder + 1)];
+            for (int e = t; e < np * np; e += kIB) {
+                const int i = e / np, j = e - (e / np) * np;
+                S2[i * (kMaxBorder + 1) + j] = 0.5 * (S[i][j] + S[j][i]);
+            }
+            __syncthreads();
+            const int cnt = cfx_inertia::sym_neg_count(S2, kMaxBorder + 1, np);
+            if (t == 0 && cnt) atomicAdd(K.inert + b, cnt);
+        }
         if (t < 64) {  // LU with partial pivoting (first largest |S(i, k)|, i >= k) in one wavefront
             int sing = 0;
             for (int k = 0; k < np; ++k) {
@@ -1281,7 +1295,10 @@ __global__ void __launch_bounds__(kIB) k_ipm_curv(const IpmK K, int slot) {
     for (int q = 0; q < K.P; ++q) sing = sing || K.info[b * K.P + q] != 0;
     // L-BFGS: the approximation is positive definite by construction (pairs with s^T y <= 0 are skipped), so only a
     // singular or non-finite factorisation asks for more regularisation
-    const bool weak = (K.lbfgs && !rs) ? false : ((curv <= K.o.curv_min * nrm) || !isfinite(curv));
+    // (inertia test: the factorisation's negative eigenvalues must number the constraints, Ipopt's inertia correction)
+    const bool weak = (K.lbfgs && !rs) ? false
+                      : K.inert        ? (K.inert[b] != K.m || !isfinite(curv))
+                                       : ((curv <= K.o.curv_min * nrm) || !isfinite(curv));
     const bool bad = active && (weak || sing || nonfin > 0);
     if (threadIdx.x == 0 && bad) {
         double& dw = rs ? S.rs_dw : S.dw;
@@ -3001,6 +3018,7 @@ extern "C" void cfx_ipm_default_options(cfx_ipm_options* o) {
     o->range_scaling = 1;
     o->bound_mult_init_method = 1;  // mu-based (Ipopt's default is constant, 1)
     o->bound_mult_init_val = 1.0;
+    o->inertia_test = 0;
 }
 
 // CSR of `key` (values in [0, nkeys)) with the sources of each key in increasing source order
@@ -3243,7 +3261,8 @@ static int ipm_create_common(cfx_ipm* s, const cfx_sizes& sz, int layout, const 
         !(K.o.acceptable_constr_viol_tol > 0) || !(K.o.acceptable_dual_inf_tol > 0) ||
         !(K.o.acceptable_compl_inf_tol > 0) || !(K.o.warm_start_bound_push > 0) || !(K.o.warm_start_bound_frac > 0) ||
         !(K.o.warm_start_bound_frac <= 0.5) || !(K.o.warm_start_mult_bound_push > 0) ||
-        (K.o.bound_mult_init_method != 0 && K.o.bound_mult_init_method != 1) || !(K.o.bound_mult_init_val > 0)) {
+        (K.o.bound_mult_init_method != 0 && K.o.bound_mult_init_method != 1) || !(K.o.bound_mult_init_val > 0) ||
+        (K.o.inertia_test != 0 && K.o.inertia_test != 1)) {
         s->err = "cfx_ipm_create: the handle must use CFX_LAYOUT_AOS (or batch 1) and the options must be valid";
         return create_fail(s, CFX_EINVAL);
     }
@@ -3672,8 +3691,10 @@ static int ipm_create_common(cfx_ipm* s, const cfx_sizes& sz, int layout, const 
     K.chain = chain ? 1 : 0;
     K.cM = (int)cM;
     K.csp = (int)csp;
+    K.inert = nullptr;
     if (chain) {
         K.cw = dalloc<double>(s, B * 2 * cM * csp * csp, &rc);
+        if (K.o.inertia_test) K.inert = dalloc<int32_t>(s, B, &rc);
         K.ct = dalloc<double>(s, B * std::max(na, 1) * nA, &rc);
     }
     K.Xb = dalloc<double>(s, B * P * na * nA, &rc);
@@ -3873,6 +3894,10 @@ struct Run {
         IPM_HIP(s, hipGetLastError());
         if (K.chain) {  // stage chain: block cyclic reduction, then (border) A^-1 [Cr | r] and the Schur complement
             IPM_BAND(s, chain_factor());
+            if (K.inert) {  // the inertia: the chain's pivot blocks here, the border's Schur complement in k_ipm_schur
+                IPM_HIP(s, hipMemsetAsync(K.inert, 0, (size_t)K.B * sizeof(int32_t), st));
+                IPM_BAND(s, cfx_chain_inertia_s(K.B, K.cM, K.csp, K.ab, K.NE_A, K.inert, st));
+            }
             if (K.np) IPM_BAND(s, chain_solve(K.Xb, (int64_t)K.na * K.nA, K.nA, K.na));
             IPM_BAND(s, chain_solve(K.rb, K.nKp, 0, 1));
             if (K.np) IPM_RUN(schur(K, 1));

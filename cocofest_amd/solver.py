@@ -106,6 +106,9 @@ class IpmOptions:
     # default: z = bound_mult_init_val)
     bound_mult_init_method: str = "mu-based"
     bound_mult_init_val: float = 1.0
+    # inertia correction (NativeIpm, stage-chain layout): False the curvature test above; True Ipopt's test on the KKT
+    # matrix's inertia (exactly m negative eigenvalues, else dw grows), counted from the chain's pivot blocks
+    inertia_test: bool = False
     # Ipopt's warm start (NativeIpm: solve(..., warm_start=(y, z_l, z_u))): no least-squares multipliers; x pushed from
     # its bounds by warm_start_bound_push max(1, |bound|) (at most warm_start_bound_frac of the range), bound
     # multipliers raised to warm_start_mult_bound_push; mu starts at mu_init
@@ -1231,7 +1234,7 @@ _NATIVE_OPTIONS = ("tol", "max_iter", "acceptable_tol", "acceptable_iter", "mu_i
                    "print_frequency_time", "soft_resto_pderror_reduction_factor", "max_soft_resto_iters",
                    "resto_failure_restart", "constr_viol_tol", "dual_inf_tol", "compl_inf_tol",
                    "acceptable_constr_viol_tol", "acceptable_dual_inf_tol", "acceptable_compl_inf_tol",
-                   "warm_start_bound_push", "warm_start_bound_frac", "warm_start_mult_bound_push")
+                   "warm_start_bound_push", "warm_start_bound_frac", "warm_start_mult_bound_push", "inertia_test")
 _HESSIAN_APPROXIMATION = {"exact": 0, "limited-memory": 1}
 _RESTORATION = {"step": 0, "phase": 1, None: 1}
 

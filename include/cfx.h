@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define CFX_ABI_VERSION 9
+#define CFX_ABI_VERSION 10
 
 /* return codes */
 #define CFX_OK 0
@@ -331,6 +331,11 @@ int cfx_btri_factor(int64_t batch, int32_t M, int32_t sp, double *D, double *L, 
                     int32_t *info, void *hip_stream);
 int cfx_btri_solve(int64_t batch, int32_t M, int32_t sp, const double *D, const double *L, const double *U,
                    const double *work, int32_t nrhs, double *rhs, double *scratch, void *hip_stream);
+/* (ABI 10) the inertia of a SYMMETRIC system factored by cfx_btri_factor: neg [B] receives its number of negative
+   eigenvalues (each pivot block counted by a Bunch-Kaufman LDL^T of its inverse; block cyclic reduction is a sequence
+   of congruences, so the counts add up to the matrix's), plus 1 << 20 per zero pivot.  The count MUMPS reports to
+   Ipopt for its inertia correction (IpPDPerturbationHandler). */
+int cfx_btri_inertia(int64_t batch, int32_t M, int32_t sp, const double *D, int32_t *neg, void *hip_stream);
 
 /* ---- batched interior-point solver ---------------------------------------------------------------
    Replaces the solver role of `ocp.solve(Solver.IPOPT(...))` (bioptim's Ipopt interface; called e.g. at
@@ -438,6 +443,11 @@ typedef struct cfx_ipm_options {
        "mu-based" (z = mu_init / slack; this library's default) */
     int32_t bound_mult_init_method;
     double bound_mult_init_val;
+    /* inertia correction (ABI 10): 0 (default) the curvature test (dx^T (W + Sigma + dw) dx >= curv_min |dx|^2); 1
+       Ipopt's test on the KKT matrix's inertia — the factorisation must have exactly m negative eigenvalues (m
+       constraints), else dw grows — counted for the stage-chain layout (cfx_btri_inertia's count on the chain plus a
+       Bunch-Kaufman LDL^T of the border's Schur complement; other layouts keep the curvature test) */
+    int32_t inertia_test;
 } cfx_ipm_options;
 #define CFX_HESSIAN_EXACT 0
 #define CFX_HESSIAN_LIMITED_MEMORY 1

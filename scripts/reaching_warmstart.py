@@ -52,6 +52,7 @@ ap.add_argument("--bound-relax", type=float, default=1e-8,
                 help="Ipopt's bound_relax_factor (its default 1e-8, as the stored solve used)")
 ap.add_argument("--tol", type=float, default=1e-6)
 ap.add_argument("--curv-min", type=float, default=None, help="the inertia-free curvature test's threshold")
+ap.add_argument("--inertia-test", type=int, default=0, help="1: Ipopt's inertia correction (chain pivot-block inertias)")
 ap.add_argument("--bound-mult-init", default="mu-based", choices=["mu-based", "constant"],
                 help="Ipopt's bound_mult_init_method (its default: constant 1)")
 ap.add_argument("--ipopt-defaults", action="store_true",
@@ -115,6 +116,8 @@ def run(objective):
     kw["bound_mult_init_method"] = args.bound_mult_init
     if args.ipopt_defaults:
         kw.update(bound_mult_init_method="constant", soft_resto_pderror_reduction_factor=0.9999, max_filter_resets=5)
+    if args.inertia_test:
+        kw["inertia_test"] = True
     if args.curv_min is not None:
         kw["curv_min"] = args.curv_min
     if warm:

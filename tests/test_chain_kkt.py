@@ -90,6 +90,57 @@ def test_btri_reports_a_singular_pivot_block():
     assert info[0] == 5 * 16 + 1, info
 
 
+def _sym_system(B, M, sp, seed):
+    """Symmetric indefinite block-tridiagonal systems shaped like the interior point's KKT nodes: each diagonal block
+    [[H, J^T], [J, -1e-3 I]] with H symmetric indefinite and J of full row rank, couplings L_k = U_{k-1}^T."""
+    rng = np.random.default_rng(seed)
+    nr = sp // 3
+    D = np.zeros((B, M, sp, sp))
+    for b in range(B):
+        for k in range(M):
+            H = rng.normal(size=(sp - nr, sp - nr))
+            H = H + H.T + rng.uniform(-2, 6) * np.eye(sp - nr)
+            J = rng.normal(size=(nr, sp - nr))
+            D[b, k, : sp - nr, : sp - nr] = H
+            D[b, k, sp - nr:, : sp - nr] = J
+            D[b, k, : sp - nr, sp - nr:] = J.T
+            D[b, k, sp - nr:, sp - nr:] = -1e-3 * np.eye(nr)
+    U = 0.5 * rng.normal(size=(B, M, sp, sp))
+    U[:, M - 1] = 0.0
+    L = np.zeros_like(U)
+    L[:, 1:] = np.transpose(U[:, :-1], (0, 1, 3, 2))
+    return D, L, U
+
+
+@pytest.mark.parametrize("sp,M,B", [(16, 37, 2), (48, 16, 2), (80, 33, 1), (128, 6, 1)])
+def test_btri_inertia_counts_negative_eigenvalues(sp, M, B):
+    """cfx_btri_inertia after cfx_btri_factor: the number of negative eigenvalues of the symmetric system (Bunch-Kaufman
+    LDL^T of every pivot block's inverse, summed over the reduction's levels) equals numpy's eigvalsh count."""
+    import torch
+
+    from cocofest_amd import _cfx
+
+    lib = _cfx.load_library()
+    D, L, U = _sym_system(B, M, sp, seed=sp + 7 * M)
+    t = lambda a: torch.tensor(np.ascontiguousarray(a), dtype=torch.float64, device="cuda")  # noqa: E731
+    dD, dL, dU = t(D), t(L), t(U)
+    work = torch.zeros(2 * B * M * sp * sp, dtype=torch.float64, device="cuda")
+    info = torch.zeros(B, dtype=torch.int32, device="cuda")
+    neg = torch.full((B,), -7, dtype=torch.int32, device="cuda")
+    st = torch.cuda.current_stream().cuda_stream
+    assert lib.cfx_btri_factor(B, M, sp, dD.data_ptr(), dL.data_ptr(), dU.data_ptr(), work.data_ptr(),
+                               info.data_ptr(), st) == 0, lib.cfx_last_error(None)
+    assert lib.cfx_btri_inertia(B, M, sp, dD.data_ptr(), neg.data_ptr(), st) == 0, lib.cfx_last_error(None)
+    torch.cuda.synchronize()
+    assert np.all(info.cpu().numpy() == 0)
+    got = neg.cpu().numpy()
+    for b in range(B):
+        A = _dense(D, L, U, b)
+        ev = np.linalg.eigvalsh(A)
+        assert np.abs(ev).min() > 1e-8 * np.abs(ev).max()  # well away from singular: the count is unambiguous
+        assert got[b] == int((ev < 0).sum()), (b, got[b], int((ev < 0).sum()))
+
+
 def _solve(ocp, B, v0, kkt, monkeypatch, **opt):
     from cocofest_amd.solver import IpmOptions, NativeIpm
 
@@ -201,3 +252,34 @@ def test_chain_layout_reaching_task_first_iterates(monkeypatch):
     span = np.where(np.isfinite(ub - lb) & (ub > lb), ub - lb, np.maximum(1.0, np.abs(v0[0])))
     assert np.max(np.abs(rc.v - rb.v) / span) < 1e-9
     np.testing.assert_array_equal(rc.iterations, rb.iterations)
+
+
+def test_inertia_test_reaches_the_curvature_tests_optimum(monkeypatch):
+    """inertia_test=True (Ipopt's inertia correction from the chain's pivot-block inertias and the border's Schur
+    complement) lands on the curvature test's KKT point: cfg 3 (batch 4, no border) and Hmed with its intensity
+    parameters in the border (batch 4)."""
+    import json
+    import pathlib
+
+    ft = json.loads((pathlib.Path(__file__).parent / "golden" / "ref_formulas.json").read_text())["misc"]["force_tracking"]
+    ocp = cases.product_ocp(**dict(cases.cfg3(), objective={"force_tracking": [np.array(ft["time"]),
+                                                                                 np.array(ft["force"])]}))
+    v0 = _starts(ocp, 4, 0)
+    ri, _ = _solve(ocp, 4, v0, "chain", monkeypatch, inertia_test=True)
+    rc, _ = _solve(ocp, 4, v0, "chain", monkeypatch)
+    _compare(ocp, ri, rc, it_slack=10)
+    cfg = dict(name="hmed2018", stims=[0.0, 0.1, 0.2, 0.3, 0.4], final_time=0.5, truncation=5, scheme="RK1", m=5,
+               objective={"end_node_tracking": 60}, n_shooting=None)
+    ocp = cases.product_ocp(**cfg)
+    rng = np.random.default_rng(5)
+    v0 = np.tile(ocp.initial_guess_vector(), (4, 1))
+    lb, ub = ocp.bounds_vector()
+    free = lb != ub
+    v0[:, free] = np.clip(v0[:, free] + rng.uniform(0, 10, (4, free.sum())), lb[free], ub[free])
+    ri, si = _solve(ocp, 4, v0, "chain", monkeypatch, inertia_test=True)
+    rc, _ = _solve(ocp, 4, v0, "chain", monkeypatch)
+    assert si["kkt_border"] >= 5, si
+    # the intensity valley is flat (test_ipm_native.py): a different regularisation path ends elsewhere on it, at the
+    # same f (measured: intensities 1.4 % of their range apart)
+    assert ri.converged.all() and rc.converged.all(), (ri.status, rc.status)
+    np.testing.assert_allclose(ri.f, rc.f, rtol=1e-8, atol=1e-10)
