@@ -59,6 +59,8 @@ def main():
     ap.add_argument("--batch", type=int, nargs="+", default=[4096, 65536])
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--libs", nargs="*", default=[])
+    ap.add_argument("--reaching", action="store_true",
+                    help="the 1,500-interval reaching task (6 muscles, tests/test_reference_solution.py) instead of cfg 5")
     ap.add_argument("--dump", default=None, help="save g and J_g of the first batch's first 256 instances here (.npz), for A/B comparisons")
     a = ap.parse_args()
     from cocofest_amd import _cfx
@@ -68,7 +70,13 @@ def main():
         if lib:
             _cfx._lib = None
             os.environ["CFX_LIB"] = lib
-        ocp = build()
+        if a.reaching:
+            sys.path.insert(0, str(ROOT))
+            from tests import test_reference_solution as R
+
+            ocp = R.legacy_product("fatigue")
+        else:
+            ocp = build()
         for B in a.batch:
             h = ocp.nlp(batch=B, layout="soa")
             v = synthetic(ocp, B)
@@ -78,7 +86,7 @@ def main():
             if a.dump and B == a.batch[0]:
                 np.savez(a.dump, g=g[:, :256].cpu().numpy(), j=j[:, :256].cpu().numpy())
             t_g = timeit(lambda: h.eval_all(v, g=g), a.reps)
-            row = dict(lib=lib or "default", batch=B, nnz_jac=h.nnz_jac, ms_g_jac=t_gj, ms_g=t_g,
+            row = dict(lib=lib or "default", geom_lds=os.environ.get("CFX_MSK_GEOM_LDS", ""), batch=B, nnz_jac=h.nnz_jac, ms_g_jac=t_gj, ms_g=t_g,
                        evals_per_s=B / t_gj * 1e3, GBps=B * 8 * (h.nv + h.ng + h.nnz_jac) / t_gj / 1e6)
             if B <= 4096:
                 lam = torch.randn((h.ng, B), dtype=torch.float64, device="cuda")
