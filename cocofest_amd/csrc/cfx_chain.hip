@@ -134,7 +134,9 @@ __global__ void __launch_bounds__(kNT) k_chain_elim(Chain C, int first, int step
     __shared__ double A[SP][SP + 1];
     __shared__ double colv[2][SP];
     __shared__ double rowp[SP];
-    __shared__ int prow[SP], pstep[SP];  // P_k (row pivoted at step k), s_j (step at which row j was pivot)
+    // P_k (row pivoted at step k), s_j (step at which row j was pivot); bytes, so that three workgroups' LDS fit a CU
+    // at SP = 80 with the allocation granularity
+    __shared__ uint8_t prow[SP], pstep[SP];
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
     const int i = first + step * blockIdx.x;
     const int64_t b = blockIdx.y;
@@ -177,7 +179,7 @@ __global__ void __launch_bounds__(kNT) k_chain_elim(Chain C, int first, int step
         const int p = 127 - (int)((uint64_t)__double_as_longlong(key) & 0x7Full);
         used0 = used0 || p == lane;
         used1 = used1 || p == lane + 64;
-        if (t == 0) prow[k] = p, pstep[p] = k;
+        if (t == 0) prow[k] = (uint8_t)p, pstep[p] = (uint8_t)k;
         const double pvl = p < 64 ? v0 : v1;  // the pivot value, from the lane that holds it
         const int pl = p & 63;
         const double pv = __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(pvl), pl),
