@@ -1772,8 +1772,10 @@ __global__ void __launch_bounds__(256) k_msk_values(const MskParams P, const Msk
 #pragma unroll
         for (int st = 0; st < ST; ++st) {
             const int64_t kq = (int64_t)k * Q + j * ST + st;
+            if (XS) {  // (null: g only)
 #pragma unroll
-            for (int r = 0; r < NX; ++r) XS[(kq * NX + r) * B + b] = xs[r];
+                for (int r = 0; r < NX; ++r) XS[(kq * NX + r) * B + b] = xs[r];
+            }
             double f[NX], csl[NM];
             msk_stage_cs<NM, FAM>(P.cs, kq, lam, csl);
             msk_rhs<NQ, NM, FAM>(G, residual, csl, msk_cs1<NM>(P, kq), xs, u, f);

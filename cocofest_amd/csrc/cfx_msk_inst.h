@@ -48,9 +48,15 @@ template <int NQ, int NM, int FAM, int SCHEME>
 hipError_t shoot_t(const MskParams& P, const MskGeom* G, const double* V, double* Gout, double* J, bool keep_xs,
                    hipStream_t s) {
     const unsigned gx = (unsigned)((P.B + kMskBlk - 1) / kMskBlk);
-    if (!J) {  // g only: the value recursion without derivative directions
-        hipLaunchKernelGGL((k_msk_shooting<NQ, NM, FAM, SCHEME, 0>), dim3(gx, (unsigned)P.N), dim3(kMskBlk), 0, s, P, G,
-                           V, Gout, J);
+    if (!J) {  // g only: the value recursion of the g + J_g path without storing the stage inputs (CFX_MSK_G=dual: the
+               // generic interval in Dual<0>, the previous kernel)
+        const char* e = std::getenv("CFX_MSK_G");
+        if (e && std::string(e) == "dual")
+            hipLaunchKernelGGL((k_msk_shooting<NQ, NM, FAM, SCHEME, 0>), dim3(gx, (unsigned)P.N), dim3(kMskBlk), 0, s, P,
+                               G, V, Gout, J);
+        else
+            hipLaunchKernelGGL((k_msk_values<NQ, NM, FAM, SCHEME>), dim3(gx, (unsigned)P.N), dim3(kMskBlk), 0, s, P, G, V,
+                               Gout, (double*)nullptr);
         return hipGetLastError();
     }
     // g + J_g: the value recursion (stage inputs XS), every stage's coefficients in its own thread, then one
