@@ -15,7 +15,7 @@ import numpy as np
 
 LIB_PATH = pathlib.Path(__file__).with_name("libcfx.so")
 
-ABI_VERSION = 10
+ABI_VERSION = 11
 OK, EINVAL, EHIP, ENOMEM, EUNSUPPORTED, ENODEV, ECALLBACK = 0, -1, -2, -3, -4, -5, -6
 MODEL_IDS = {
     "ding2003": 0,
@@ -124,7 +124,17 @@ class IpmOptions(C.Structure):
                 ("warm_start_bound_frac", C.c_double), ("warm_start_mult_bound_push", C.c_double),
                 ("warm_start_init_point", C.c_int32), ("honor_original_bounds", C.c_int32),
                 ("range_scaling", C.c_int32), ("bound_mult_init_method", C.c_int32),
-                ("bound_mult_init_val", C.c_double), ("inertia_test", C.c_int32)]
+                ("bound_mult_init_val", C.c_double), ("inertia_test", C.c_int32),
+                # ABI 11: Ipopt's barrier-parameter strategies, NLP scaling method, bound_frac
+                ("mu_strategy", C.c_int32), ("adaptive_mu_globalization", C.c_int32), ("mu_max_fact", C.c_double),
+                ("mu_max", C.c_double), ("mu_min", C.c_double), ("adaptive_mu_monotone_init_factor", C.c_double),
+                ("sigma_max", C.c_double), ("sigma_min", C.c_double),
+                ("quality_function_section_sigma_tol", C.c_double), ("quality_function_section_qf_tol", C.c_double),
+                ("quality_function_max_section_steps", C.c_int32), ("mu_change_resets_filter", C.c_int32),
+                ("filter_margin_fact", C.c_double), ("filter_max_margin", C.c_double),
+                ("monotone_mu_floor", C.c_int32), ("nlp_scaling_method", C.c_int32),
+                ("nlp_scaling_max_gradient", C.c_double), ("nlp_scaling_min_value", C.c_double),
+                ("bound_frac", C.c_double)]
 
 
 # cfx_ipm_get_status values (Ipopt's ApplicationReturnStatus)
@@ -138,7 +148,7 @@ class IpmStats(C.Structure):
                 ("kkt_n", C.c_int64), ("kkt_kl", C.c_int64), ("kkt_ku", C.c_int64), ("kkt_band_n", C.c_int64),
                 ("kkt_border", C.c_int64), ("kkt_blocks", C.c_int64), ("resto_phases", C.c_int64),
                 ("resto_iterations", C.c_int64), ("soft_steps", C.c_int64), ("kkt_chain_nodes", C.c_int64),
-                ("kkt_chain_sp", C.c_int64)]
+                ("kkt_chain_sp", C.c_int64), ("mu_mode_switches", C.c_int64)]
 
 
 # cfx_evaluator / cfx_nlp_desc (cfx_ipm_create_ext): caller-supplied callbacks of an NLP the solver runs on

@@ -44,7 +44,7 @@ constexpr int kSlots = 64;  // counter ring: one 4-int slot per host read
 constexpr int kMaxY = 65535;
 constexpr int kMaxBorder = 32;  // free parameters handled as a dense border
 constexpr int kWideParts = 128;  // blocks per instance of the wide-instance reductions (IpmK::wide)
-constexpr int kWP = 16;          // partial values per block (IpmK::wpart)
+constexpr int kWP = 20;          // partial values per block (IpmK::wpart)
 constexpr int kWF = 12;          // decisions per instance (IpmK::wflag)
 
 // per-instance scalars of the iteration
@@ -80,6 +80,11 @@ struct Scal {
     // kDegenIters iterations all needed dw > 0): from then on each iteration's first trial is dw = max(1e-20, dw_last / 3)
     // instead of 0; degit counts those iterations
     int32_t hdeg, degit;
+    // adaptive barrier parameter (o.mu_strategy == CFX_MU_ADAPTIVE; IpAdaptiveMuUpdate): free-mu mode, insertions into
+    // the globalisation filter (its ring position), mu_max (set at the first iteration), this iteration's average
+    // complementarity and the squared 2-norms of the scaled dual / primal infeasibility (the quality function's terms)
+    int32_t mfree, mfpos;
+    double mu_max, avgc, qd, qp;
 };
 constexpr int kDegenIters = 3;  // Ipopt degen_iters_max
 
@@ -171,11 +176,17 @@ struct IpmK {
     double *rp, *rn, *rzp, *rzn, *rdp, *rdn, *rdzp, *rdzn, *rpt, *rnt, *ry, *rdc;
     double *rzl, *rzu;
     double* rfilt;
-    unsigned long long* rstat;  // [3] phases entered, phase iterations, soft steps (summed over the instances)
+    unsigned long long* rstat;  // [4] phases entered, phase iterations, soft steps, switches of the adaptive mu update
+                                // to its monotone mode (summed over the instances)
     // soft restoration (o.soft_resto_pderror_reduction_factor > 0): the trial point's J_g values and gradient; npd =
     // nf + m + bounded sides, the number of terms of the primal-dual system error
     double *jact, *gradt;  // [B][nnzj], [B][n]
     int npd;
+    // adaptive barrier parameter (adapt = o.mu_strategy == CFX_MU_ADAPTIVE): the (f, ||c||_1) filter of its
+    // globalisation [B][kFilt][2], the unit-centering part of the Newton right-hand side 1 / s_L - 1 / s_U [B][nf] (the
+    // affine part stays in rhs) and its solution in band order [B][nKp]; ncomp = the bounded sides
+    int adapt, ncomp;
+    double *mfilt, *rhsmu, *rbc;
 };
 
 enum { KKT_NEWTON = 0, KKT_LSMULT = 1, KKT_RESTO = 2, KKT_RSNLP = 3 };
@@ -405,20 +416,23 @@ __global__ void __launch_bounds__(kIB) k_ipm_init(const IpmK K, const double* __
     double gmax = 0.0;
     for (int i = threadIdx.x; i < K.nf; i += kIB) gmax = max_n(gmax, fabs(grad[K.free[i]] * K.d[i]));
     gmax = breduce(gmax, OpMax(), sh);
-    const double sf = clamp_hi(100.0 / clamp_lo(gmax, 1e-300), 1.0);
+    // Ipopt's gradient-based scaling: min(1, max_gradient / max |gradient|), at least nlp_scaling_min_value; none: 1
+    const bool scl = K.o.nlp_scaling_method != 0;
+    const double gm = K.o.nlp_scaling_max_gradient, smin = K.o.nlp_scaling_min_value;
+    const double sf = scl ? clamp_lo(clamp_hi(gm / clamp_lo(gmax, 1e-300), 1.0), smin) : 1.0;
     for (int r = threadIdx.x; r < K.m; r += kIB) {
         double rmax = 0.0;
         for (int k = K.jrw_ptr[r]; k < K.jrw_ptr[r + 1]; ++k) {
             const int s = K.jrw_idx[k];
             rmax = max_n(rmax, fabs(jac[K.jsel[s]] * K.d[K.jc[s]]));
         }
-        const double sgr = clamp_hi(100.0 / clamp_lo(rmax, 1e-300), 1.0);
+        const double sgr = scl ? clamp_lo(clamp_hi(gm / clamp_lo(rmax, 1e-300), 1.0), smin) : 1.0;
         K.sg[b * K.m + r] = sgr;
         K.y[b * K.m + r] = warm ? sf * wy[b * K.m + r] / sgr : 0.0;
     }
     const double mu = K.o.mu_init;
     const double push = warm ? K.o.warm_start_bound_push : K.o.bound_push;
-    const double frac = warm ? K.o.warm_start_bound_frac : 0.5;
+    const double frac = warm ? K.o.warm_start_bound_frac : K.o.bound_frac;
     for (int i = threadIdx.x; i < K.nf; i += kIB) {
         double xi = K.vx[b * K.n + K.free[i]] / K.d[i];
         const bool hL = K.hasL[i], hU = K.hasU[i];
@@ -451,11 +465,14 @@ __global__ void __launch_bounds__(kIB) k_ipm_init(const IpmK K, const double* __
     for (int k = threadIdx.x; k < kFilt; k += kIB) {
         K.filt[(b * kFilt + k) * 2] = INFINITY;
         K.filt[(b * kFilt + k) * 2 + 1] = -INFINITY;
+        if (K.adapt) K.mfilt[(b * kFilt + k) * 2] = K.mfilt[(b * kFilt + k) * 2 + 1] = INFINITY;
     }
     if (threadIdx.x == 0) {
         Scal S{};
         S.mu = mu;
         S.sf = sf;
+        S.mfree = K.adapt;  // Ipopt's adaptive update starts in the free mode
+        S.mu_max = -1.0;
         S.lsig = 1.0;  // Ipopt limited_memory_init_val
         S.err0 = INFINITY;
         S.reinit = K.m > 0 && !warm;
@@ -505,13 +522,16 @@ __global__ void __launch_bounds__(kIB) k_ipm_begin(const IpmK K, int mode, int s
     double* rhs = K.rhs + b * K.nK;
     double szl = 0, szu = 0, sy = 0, ed = 0, ep = 0, ecl = 0, ecu = 0, edu = 0, epu = 0;
     double pLmax = -INFINITY, pLmin = INFINITY, pUmax = -INFINITY, pUmin = INFINITY;  // (wide: k_wbegin_a's)
+    // the adaptive update's sums: complementarity (its average), ||c||_1, |grad L|^2, |c|^2
+    double scl = 0, scu = 0, th = 0, rd2 = 0, g2 = 0;
     const double* sg = K.sg + b * m;
     if (K.wide) {
-        double rv[13];
-        const int ro[13] = {0, 0, 0, 1, 1, 1, 1, 1, 1, 1, 2, 1, 2};
+        double rv[18];
+        const int ro[18] = {0, 0, 0, 1, 1, 1, 1, 1, 1, 1, 2, 1, 2, 0, 0, 0, 0, 0};
         wide_get(K, b, rv, ro);
         szl = rv[0], szu = rv[1], sy = rv[2], ed = rv[3], ep = rv[4], ecl = rv[5], ecu = rv[6], edu = rv[7],
         epu = rv[8], pLmax = rv[9], pLmin = rv[10], pUmax = rv[11], pUmin = rv[12];
+        scl = rv[13], scu = rv[14], th = rv[15], rd2 = rv[16], g2 = rv[17];
     } else {
     for (int i = threadIdx.x; i < nf; i += kIB) {
         double gj;
@@ -536,15 +556,20 @@ __global__ void __launch_bounds__(kIB) k_ipm_begin(const IpmK K, int mode, int s
         edu = max_n(edu, fabs(rd) / K.d[i]);
         ecl = max_n(ecl, fabs(cl));
         ecu = max_n(ecu, fabs(cu));
+        scl += cl;
+        scu += cu;
+        rd2 += rd * rd;
     }
     for (int j = threadIdx.x; j < m; j += kIB) {
         sy += fabs(y[j]);
         ep = max_n(ep, fabs(gS[j]));
         epu = max_n(epu, fabs(gS[j]) / sg[j]);
+        th += fabs(gS[j]);
+        g2 += gS[j] * gS[j];
     }
     {
-        double rv[9] = {szl, szu, sy, ed, ep, ecl, ecu, edu, epu};
-        const int ro[9] = {0, 0, 0, 1, 1, 1, 1, 1, 1};
+        double rv[14] = {szl, szu, sy, ed, ep, ecl, ecu, edu, epu, scl, scu, th, rd2, g2};
+        const int ro[14] = {0, 0, 0, 1, 1, 1, 1, 1, 1, 0, 0, 0, 0, 0};
         breduce_n(rv, ro);
         szl = rv[0];
         szu = rv[1];
@@ -555,6 +580,11 @@ __global__ void __launch_bounds__(kIB) k_ipm_begin(const IpmK K, int mode, int s
         ecu = rv[6];
         edu = rv[7];
         epu = rv[8];
+        scl = rv[9];
+        scu = rv[10];
+        th = rv[11];
+        rd2 = rv[12];
+        g2 = rv[13];
     }
     }
     const double smax = K.o.s_max;
@@ -580,8 +610,61 @@ __global__ void __launch_bounds__(kIB) k_ipm_begin(const IpmK K, int mode, int s
         }
     }
     __syncthreads();
-    // monotone barrier update: while the barrier sub-problem is solved, decrease mu (at most 5 times)
-    for (int pass = 0; pass < 5; ++pass) {
+    // Adaptive strategy (IpAdaptiveMuUpdate; solver.py BatchedIpm.solve): the globalisation decides the mode — a
+    // free-mode iterate not acceptable to the (f, ||c||_1) filter switches to the monotone mode at mu =
+    // adaptive_mu_monotone_init_factor * average complementarity; a monotone-mode one acceptable to it returns to the
+    // free mode; acceptable iterates enter the filter.  Free-mode mu comes from k_mu_oracle after the factorisation.
+    __shared__ int s_mono;
+    const double mu_prev = S.mu;
+    int passes = 5;  // the monotone strategy's fast decrease (mu_allow_fast_monotone_decrease)
+    if (threadIdx.x == 0) s_mono = !S.done;
+    if (K.adapt) {
+        passes = 1;
+        if (threadIdx.x == 0 && !S.done) {
+            const double avg = K.ncomp ? (scl + scu) / K.ncomp : 0.0;
+            S.avgc = avg;
+            S.qd = rd2;
+            S.qp = m ? g2 : 0.0;
+            const double thc = m ? th : 0.0;
+            if (S.mu_max < 0) S.mu_max = K.o.mu_max > 0 ? K.o.mu_max : K.o.mu_max_fact * avg;
+            double* mf = K.mfilt + b * kFilt * 2;
+            bool ok = true;  // IpFilter::Acceptable: f <= f_i or theta < theta_i for every entry
+            if (K.o.adaptive_mu_globalization == CFX_MU_GLOBAL_OBJ_CONSTR_FILTER)
+                for (int k = 0; k < kFilt; ++k)
+                    if (!(S.fS <= mf[2 * k] || thc < mf[2 * k + 1])) {
+                        ok = false;
+                        break;
+                    }
+            if (ok) {  // RememberCurrentPointAsAccepted: the entries it dominates leave, then the first free slot
+                const double margin = K.o.filter_margin_fact * clamp_hi(thc, K.o.filter_max_margin);
+                const double fe = S.fS - margin, te = thc - margin;
+                int slot = -1;
+                for (int k = 0; k < kFilt; ++k) {
+                    if (fe <= mf[2 * k] && te <= mf[2 * k + 1]) mf[2 * k] = mf[2 * k + 1] = INFINITY;
+                    if (slot < 0 && isinf(mf[2 * k]) && isinf(mf[2 * k + 1])) slot = k;
+                }
+                if (slot < 0) slot = S.mfpos % kFilt;
+                mf[2 * slot] = fe;
+                mf[2 * slot + 1] = te;
+                S.mfpos += 1;
+            }
+            s_mono = 0;
+            if (S.mfree && !ok) {  // to the monotone mode
+                S.mfree = 0;
+                S.mu = min_n(clamp_lo(K.o.adaptive_mu_monotone_init_factor * avg, K.o.mu_min), S.mu_max);
+                atomicAdd(K.rstat + 3, 1ull);
+            } else if (!S.mfree && ok) {  // back to the free mode
+                S.mfree = 1;
+            } else {
+                s_mono = !S.mfree;
+            }
+        }
+    }
+    __syncthreads();
+    // floor of the monotone mu: tol / 10, or Ipopt's min(tol, compl_inf_tol) / (barrier_tol_factor + 1)
+    const double mufl = K.o.monotone_mu_floor ? min_n(K.o.tol, K.o.compl_inf_tol) / (K.o.kappa_eps + 1.0) : K.o.tol / 10;
+    // monotone barrier update: while the barrier sub-problem is solved, decrease mu (at most `passes` times)
+    for (int pass = 0; pass < passes && s_mono; ++pass) {
         const double mu = S.mu;
         double ecm = 0.0;
         if (K.wide) {  // max_i |p_i - mu| = max(p_max - mu, mu - p_min), exactly (fl(p - mu) is monotone in p)
@@ -595,21 +678,34 @@ __global__ void __launch_bounds__(kIB) k_ipm_begin(const IpmK K, int mode, int s
         ecm = breduce(ecm, OpMax(), sh) / sc;
         }
         const double e_mu = max_n(max_n(e_d, e_p), ecm);
-        const bool dec = !S.done && (e_mu <= K.o.kappa_eps * mu) && (mu > K.o.tol / 10);
+        const bool dec = !S.done && (e_mu <= K.o.kappa_eps * mu) && (mu > mufl);
         if (!dec) break;
         __syncthreads();
-        if (threadIdx.x == 0) S.mu = clamp_lo(min_n(K.o.kappa_mu * mu, pow(mu, K.o.theta_mu)), K.o.tol / 10);
+        if (threadIdx.x == 0) S.mu = clamp_lo(min_n(K.o.kappa_mu * mu, pow(mu, K.o.theta_mu)), mufl);
         __syncthreads();
     }
     const double mu = S.mu;
+    // Ipopt restarts the line search's filter whenever mu changes (linesearch_->Reset()): every free-mode iteration of
+    // the adaptive strategy, a changed mu of either strategy (the monotone one only with mu_change_resets_filter)
+    const bool ls_reset = !S.done && (K.adapt ? (S.mfree || mu != mu_prev) : (K.o.mu_change_resets_filter && mu != mu_prev));
+    if (ls_reset)
+        for (int k = threadIdx.x; k < kFilt; k += kIB) {
+            K.filt[(b * kFilt + k) * 2] = INFINITY;
+            K.filt[(b * kFilt + k) * 2 + 1] = -INFINITY;
+        }
     double* sig = K.sig + b * nf;
     if (!K.wide) {  // (wide: k_wbegin_c)
     for (int i = threadIdx.x; i < nf; i += kIB) {
         const bool hL = K.hasL[i], hU = K.hasU[i];
         const double sl = hL ? x[i] - lbI[i] : 1.0, su = hU ? ubI[i] - x[i] : 1.0;
         sig[i] = (hL ? zl[i] / sl : 0.0) + (hU ? zu[i] / su : 0.0);
-        const double bar = (hL ? mu / sl : 0.0) - (hU ? mu / su : 0.0);
-        rhs[i] = -(rhs[i] - bar);
+        if (K.adapt) {  // rhs = -(grad f + J^T y) + mu (1 / s_L - 1 / s_U): the affine part and the unit centering
+            rhs[i] = -rhs[i];
+            K.rhsmu[b * nf + i] = (hL ? 1.0 / sl : 0.0) - (hU ? 1.0 / su : 0.0);
+        } else {
+            const double bar = (hL ? mu / sl : 0.0) - (hU ? mu / su : 0.0);
+            rhs[i] = -(rhs[i] - bar);
+        }
     }
     for (int j = threadIdx.x; j < m; j += kIB) {
         rhs[nf + j] = -gS[j];
@@ -677,8 +773,13 @@ __device__ inline void kkt_entry(const IpmK& K, int64_t b, int64_t p, int mode) 
 __device__ inline void kkt_rhs(const IpmK& K, int64_t b, int64_t p, int mode) {
     const int nf = K.nf;
     double r;
-    if (mode == KKT_NEWTON || mode == KKT_RSNLP)
+    if (mode == KKT_NEWTON || mode == KKT_RSNLP) {
         r = K.rhs[b * K.nK + p];
+        // adaptive strategy: the monotone-mode instances' mu term (free-mode ones solve mu = 0 here, k_mu_oracle adds
+        // mu times the centering solution)
+        if (K.adapt && mode == KKT_NEWTON && p < nf && !K.sc[b].rs_on && !K.sc[b].mfree)
+            r += K.sc[b].mu * K.rhsmu[b * nf + p];
+    }
     else if (mode == KKT_LSMULT)
         r = p < nf ? -(K.gF[b * nf + p] - K.zl[b * nf + p] + K.zu[b * nf + p]) : 0.0;
     else
@@ -1017,6 +1118,7 @@ __global__ void __launch_bounds__(kIB) k_wbegin_a(const IpmK K) {
     double* rhs = K.rhs + b * K.nK;
     double szl = 0, szu = 0, sy = 0, ed = 0, ep = 0, ecl = 0, ecu = 0, edu = 0, epu = 0;
     double pLmax = -INFINITY, pLmin = INFINITY, pUmax = -INFINITY, pUmin = INFINITY;
+    double scl = 0, scu = 0, th = 0, rd2 = 0, g2 = 0;
     WIDE_LOOP(i, nf) {
         const double gj = K.gj[b * nf + i];
         rhs[i] = gj;
@@ -1031,14 +1133,19 @@ __global__ void __launch_bounds__(kIB) k_wbegin_a(const IpmK K) {
         ecu = max_n(ecu, fabs(cu));
         if (K.hasL[i]) pLmax = max_n(pLmax, cl), pLmin = min_n(pLmin, cl);
         if (K.hasU[i]) pUmax = max_n(pUmax, cu), pUmin = min_n(pUmin, cu);
+        scl += cl;
+        scu += cu;
+        rd2 += rd * rd;
     }
     WIDE_LOOP(j, m) {
         sy += fabs(y[j]);
         ep = max_n(ep, fabs(gS[j]));
         epu = max_n(epu, fabs(gS[j]) / sg[j]);
+        th += fabs(gS[j]);
+        g2 += gS[j] * gS[j];
     }
-    double rv[13] = {szl, szu, sy, ed, ep, ecl, ecu, edu, epu, pLmax, pLmin, pUmax, pUmin};
-    const int ro[13] = {0, 0, 0, 1, 1, 1, 1, 1, 1, 1, 2, 1, 2};
+    double rv[18] = {szl, szu, sy, ed, ep, ecl, ecu, edu, epu, pLmax, pLmin, pUmax, pUmin, scl, scu, th, rd2, g2};
+    const int ro[18] = {0, 0, 0, 1, 1, 1, 1, 1, 1, 1, 2, 1, 2, 0, 0, 0, 0, 0};
     wide_put(K, b, rv, ro);
 }
 
@@ -1055,8 +1162,13 @@ __global__ void __launch_bounds__(kIB) k_wbegin_c(const IpmK K) {
         const bool hL = K.hasL[i], hU = K.hasU[i];
         const double sl = hL ? xi - K.lbI[b * nf + i] : 1.0, su = hU ? K.ubI[b * nf + i] - xi : 1.0;
         K.sig[b * nf + i] = (hL ? K.zl[b * nf + i] / sl : 0.0) + (hU ? K.zu[b * nf + i] / su : 0.0);
-        const double bar = (hL ? mu / sl : 0.0) - (hU ? mu / su : 0.0);
-        rhs[i] = -(rhs[i] - bar);
+        if (K.adapt) {  // the affine part and the unit centering (k_ipm_begin)
+            rhs[i] = -rhs[i];
+            K.rhsmu[b * nf + i] = (hL ? 1.0 / sl : 0.0) - (hU ? 1.0 / su : 0.0);
+        } else {
+            const double bar = (hL ? mu / sl : 0.0) - (hU ? mu / su : 0.0);
+            rhs[i] = -(rhs[i] - bar);
+        }
     }
     if (i < m) {
         rhs[nf + i] = -K.gS[b * m + i];
@@ -1323,6 +1435,157 @@ __global__ void __launch_bounds__(kIB) k_ipm_curv(const IpmK K, int slot) {
     }
 }
 
+// ---- adaptive barrier parameter: Ipopt's quality-function mu oracle (IpQualityFunctionMuOracle::CalculateMu,
+// 2-norm-squared, no centrality or balancing term; recalled, see solver.py BatchedIpm._mu_oracle, its specification)
+// For the free-mode instances the Newton step is affine in mu: rb holds the solution of the affine right-hand side
+// (mu = 0, kkt_rhs), rbc that of the unit centering [1 / s_L - 1 / s_U; 0] with the same factors, and the step for
+// mu = sigma * avgc is rb + mu rbc.
+
+// the unit-centering right-hand side in band order (zero for the other instances, so rbc stays bounded)
+__global__ void __launch_bounds__(kIB) k_mu_cen_rhs(const IpmK K) {
+    const int64_t b = blockIdx.x;
+    const bool on = !K.sc[b].done && !K.sc[b].rs_on && K.sc[b].mfree;
+    for (int i = threadIdx.x; i < K.nK; i += kIB)
+        K.rbc[b * K.nKp + K.pos[i]] = (on && i < K.nf) ? K.rhsmu[b * K.nf + i] : 0.0;
+}
+
+// the quality function at mu: predicted (1 - a_d)^2 |grad L|^2 / n_x + (1 - a_p)^2 |c|^2 / m + |(s + a_p ds)(z + a_d
+// dz)|^2 / n_bounds after the step of mu, a_p / a_d its fractions to the boundary (tau = max(tau_min, 1 - mu))
+__device__ double mu_quality(const IpmK& K, int64_t b, const Scal& S, double mu) {
+    const int nf = K.nf;
+    const double tau = clamp_lo(1.0 - mu, K.o.tau_min);
+    const double* x = K.x + b * nf;
+    const double* zl = K.zl + b * nf;
+    const double* zu = K.zu + b * nf;
+    const double* lbI = K.lbI + b * nf;
+    const double* ubI = K.ubI + b * nf;
+    const double* ra = K.rb + b * K.nKp;
+    const double* rc = K.rbc + b * K.nKp;
+    double apl = INFINITY, apu = INFINITY, azl = INFINITY, azu = INFINITY;
+    for (int i = threadIdx.x; i < nf; i += kIB) {
+        const int q = K.pos[i];
+        const double dx = ra[q] + mu * rc[q];
+        const bool hL = K.hasL[i], hU = K.hasU[i];
+        const double sl = hL ? x[i] - lbI[i] : 1.0, su = hU ? ubI[i] - x[i] : 1.0;
+        const double vzl = hL ? mu / sl - zl[i] - zl[i] / sl * dx : 0.0;
+        const double vzu = hU ? mu / su - zu[i] + zu[i] / su * dx : 0.0;
+        apl = min_n(apl, step_term(hL, sl, dx, tau));
+        apu = min_n(apu, step_term(hU, su, -dx, tau));
+        azl = min_n(azl, step_term(hL, zl[i], vzl, tau));
+        azu = min_n(azu, step_term(hU, zu[i], vzu, tau));
+    }
+    {
+        double rv[4] = {apl, apu, azl, azu};
+        const int ro[4] = {2, 2, 2, 2};
+        breduce_n(rv, ro);
+        apl = rv[0], apu = rv[1], azl = rv[2], azu = rv[3];
+    }
+    const double ap = min_n(clamp_hi(apl, 1.0), clamp_hi(apu, 1.0));
+    const double ad = min_n(clamp_hi(azl, 1.0), clamp_hi(azu, 1.0));
+    double cs = 0.0;
+    for (int i = threadIdx.x; i < nf; i += kIB) {
+        const int q = K.pos[i];
+        const double dx = ra[q] + mu * rc[q];
+        const bool hL = K.hasL[i], hU = K.hasU[i];
+        if (hL) {
+            const double sl = x[i] - lbI[i];
+            const double t = (sl + ap * dx) * (zl[i] + ad * (mu / sl - zl[i] - zl[i] / sl * dx));
+            cs += t * t;
+        }
+        if (hU) {
+            const double su = ubI[i] - x[i];
+            const double t = (su - ap * dx) * (zu[i] + ad * (mu / su - zu[i] + zu[i] / su * dx));
+            cs += t * t;
+        }
+    }
+    {
+        double rv[1] = {cs};
+        const int ro[1] = {0};
+        breduce_n(rv, ro);
+        cs = rv[0];
+    }
+    double val = (1.0 - ad) * (1.0 - ad) * S.qd / (nf > 0 ? nf : 1);
+    if (K.m) val += (1.0 - ap) * (1.0 - ap) * S.qp / K.m;
+    if (K.ncomp) val += cs / K.ncomp;
+    return val;
+}
+
+// sigma by golden section over log sigma (CalculateMu / PerformGoldenSection), mu = sigma * avgc within [mu_min, mu_max];
+// then the Newton step rb += mu rbc, mu and tau stored
+__global__ void __launch_bounds__(kIB) k_mu_oracle(const IpmK K) {
+    __shared__ Scal S;
+    const int64_t b = blockIdx.x;
+    load_scal(K, b, S);
+    if (S.done || S.rs_on || !S.mfree) return;  // block-uniform
+    const double avg = S.avgc;
+    const bool safe = avg > 0;
+    const double avgs = safe ? avg : 1.0;
+    auto Q = [&](double sig) { return mu_quality(K, b, S, sig * avg); };
+    const double s1m = 1.0 - max_n(1e-4, K.o.quality_function_section_sigma_tol);
+    const double q1m = Q(s1m), q1 = Q(1.0);
+    const bool up = q1m > q1;  // the quality decreases beyond sigma = 1
+    const double s_hi = up ? clamp_hi(S.mu_max / avgs, K.o.sigma_max) : clamp_lo(K.o.mu_min / avgs, K.o.sigma_min);
+    const double lo = up ? 1.0 : s_hi;
+    const double hi = up ? s_hi : max_n(s_hi, s1m);
+    double q_lo = up ? q1 : -1.0, q_hi = up ? -1.0 : q1m;  // -1: not evaluated
+    double sig;
+    if (lo >= hi) {
+        sig = up ? hi : lo;
+    } else {
+        const double g = (3.0 - sqrt(5.0)) / 2.0;
+        double a = log(lo), bb = log(hi);
+        const double a0 = a, b0 = bb;
+        double m1 = a + g * (bb - a), m2 = a + (1.0 - g) * (bb - a);
+        double qm1 = Q(exp(m1)), qm2 = Q(exp(m2));
+        for (int k = 0; k < K.o.quality_function_max_section_steps; ++k) {
+            double qmin = INFINITY, qmax = -INFINITY;
+            const double qs[4] = {q_lo, q_hi, qm1, qm2};
+            for (int t = 0; t < 4; ++t)
+                if (qs[t] >= 0) qmin = fmin(qmin, qs[t]), qmax = fmax(qmax, qs[t]);
+            if (!(exp(bb) - exp(a) >= K.o.quality_function_section_sigma_tol * exp(bb)) ||
+                !(1.0 - qmin / qmax >= K.o.quality_function_section_qf_tol))
+                break;
+            if (qm1 > qm2) {  // the minimum is in [m1, b]
+                a = m1;
+                q_lo = qm1;
+                m1 = m2;
+                qm1 = qm2;
+                m2 = a + (1.0 - g) * (bb - a);
+                qm2 = Q(exp(m2));
+            } else {
+                bb = m2;
+                q_hi = qm2;
+                m2 = m1;
+                qm2 = qm1;
+                m1 = a + g * (bb - a);
+                qm1 = Q(exp(m1));
+            }
+        }
+        double best = qm1 < qm2 ? m1 : m2;
+        const double qbest = qm1 < qm2 ? qm1 : qm2;
+        const bool hi_end = bb == b0, lo_end = a == a0 && !hi_end;  // an end point never moved competes
+        if (hi_end || lo_end) {
+            double qe = hi_end ? q_hi : q_lo;
+            if (qe < 0) qe = Q(exp(hi_end ? bb : a));
+            if (qe < qbest) best = hi_end ? bb : a;
+        }
+        sig = exp(best);
+    }
+    const double mu = safe ? clamp_lo(min_n(sig * avg, S.mu_max), K.o.mu_min) : K.o.mu_min;
+    __syncthreads();
+    double* rb = K.rb + b * K.nKp;
+    const double* rc = K.rbc + b * K.nKp;
+    for (int i = threadIdx.x; i < K.nK; i += kIB) {
+        const int q = K.pos[i];
+        rb[q] += mu * rc[q];
+    }
+    if (threadIdx.x == 0) {
+        S.mu = mu;
+        S.tau = clamp_lo(1.0 - mu, K.o.tau_min);
+    }
+    store_scal(K, b, S);
+}
+
 // dz, fraction to the boundary, filter quantities at x, first trial point (solver.py, after the inertia loop)
 __global__ void __launch_bounds__(kIB) k_ipm_dir(const IpmK K, int it) {
     __shared__ double sh[kIB / 64];
@@ -1532,10 +1795,13 @@ __global__ void __launch_bounds__(kIB) k_ipm_next_trial(const IpmK K) {
 __global__ void __launch_bounds__(kIB) k_ipm_soc_rhs(const IpmK K) {
     const int64_t b = blockIdx.x;
     if (K.sc[b].rs_on) return;  // block-uniform
-    const double a = K.sc[b].alpha;
+    const double a = K.sc[b].alpha, mu = K.sc[b].mu;
     const int nf = K.nf;
-    for (int i = threadIdx.x; i < K.nK; i += kIB)
-        K.rb[b * K.nKp + K.pos[i]] = i < nf ? K.rhs[b * K.nK + i] * a : -K.csoc[b * K.m + (i - nf)];
+    for (int i = threadIdx.x; i < K.nK; i += kIB) {
+        // (adaptive: rhs holds the affine part, the final mu's term added)
+        const double rx = i < nf ? (K.adapt ? K.rhs[b * K.nK + i] + mu * K.rhsmu[b * nf + i] : K.rhs[b * K.nK + i]) : 0.0;
+        K.rb[b * K.nKp + K.pos[i]] = i < nf ? rx * a : -K.csoc[b * K.m + (i - nf)];
+    }
 }
 
 // corrected trial x + a_c dx_c (into xr)
@@ -2764,29 +3030,32 @@ __global__ void __launch_bounds__(kIB) k_lbfgs_zcols(const IpmK K) {
     }
 }
 
-// C = M - Z^T P and its LU (partial pivoting, one wavefront, lanes over columns)
+// C = M - Z^T P and its LU with partial pivoting, in place in Cl (2 hmax <= 128: the whole block, a barrier per
+// pivot step; the pivot search by wavefront 0, two rows per lane)
 __global__ void __launch_bounds__(kIB) k_lbfgs_factor(const IpmK K) {
-    constexpr int HM2 = 32;
     __shared__ Scal S;
-    __shared__ double C[HM2][HM2 + 1];
-    __shared__ int piv[HM2];
+    __shared__ int piv_s;
     const int64_t b = blockIdx.x;
     load_scal(K, b, S);
     const int H2 = 2 * K.hmax, t = threadIdx.x;
     const double* Mb = K.Mm + b * H2 * H2;
+    double* C = K.Cl + b * H2 * H2;
+    int32_t* piv = K.Cp + b * H2;
     for (int e = t; e < H2 * H2; e += kIB) {
         const int r = e / H2, c = e - (e / H2) * H2;
         const double* P = K.Zb + ((int64_t)c * K.B + b) * K.nKp;
         double acc = 0.0;
         if ((r % K.hmax) < S.lcount && (c % K.hmax) < S.lcount)
             for (int i = 0; i < K.nf; ++i) acc += lb_z(K, S, b, r, i) * P[K.pos[i]];
-        C[r][c] = Mb[e] - acc;
+        C[e] = Mb[e] - acc;
     }
     __syncthreads();
-    if (t < 64) {
-        for (int k = 0; k < H2; ++k) {
-            double a = (t >= k && t < H2) ? fabs(C[t][k]) : -1.0;
-            int idx = t;
+    for (int k = 0; k < H2; ++k) {
+        if (t < 64) {  // argmax |C[r][k]| over r >= k (first index on ties), rows t and t + 64
+            double a = -1.0;
+            int idx = H2;
+            for (int r = t; r < H2; r += 64)
+                if (r >= k && fabs(C[r * H2 + k]) > a) a = fabs(C[r * H2 + k]), idx = r;
             for (int o = 32; o > 0; o >>= 1) {
                 const double a2 = __shfl_xor(a, o, 64);
                 const int i2 = __shfl_xor(idx, o, 64);
@@ -2795,65 +3064,74 @@ __global__ void __launch_bounds__(kIB) k_lbfgs_factor(const IpmK K) {
                     idx = i2;
                 }
             }
-            const int p = idx;
-            if (t == 0) piv[k] = p;
-            if (p != k && t < H2) {
-                const double tmp = C[k][t];
-                C[k][t] = C[p][t];
-                C[p][t] = tmp;
+            if (t == 0) {
+                piv_s = idx;
+                piv[k] = idx;
             }
-            wave_sync();
-            const double pv = C[k][k];
-            const double inv = pv != 0.0 ? 1.0 / pv : 0.0;
-            if (t > k && t < H2) C[t][k] *= inv;
-            wave_sync();
-            if (t > k && t < H2) {
-                const double ukt = C[k][t];
-                for (int i = k + 1; i < H2; ++i) C[i][t] -= C[i][k] * ukt;
-            }
-            wave_sync();
         }
+        __syncthreads();
+        const int p = piv_s;
+        if (p != k)
+            for (int c = t; c < H2; c += kIB) {
+                const double tmp = C[k * H2 + c];
+                C[k * H2 + c] = C[p * H2 + c];
+                C[p * H2 + c] = tmp;
+            }
+        __syncthreads();
+        const double pv = C[k * H2 + k];
+        const double inv = pv != 0.0 ? 1.0 / pv : 0.0;
+        for (int r = k + 1 + t; r < H2; r += kIB) C[r * H2 + k] *= inv;
+        __syncthreads();
+        const int n1 = H2 - k - 1;
+        for (int e = t; e < n1 * n1; e += kIB) {
+            const int r = k + 1 + e / n1, c = k + 1 + e % n1;
+            C[r * H2 + c] -= C[r * H2 + k] * C[k * H2 + c];
+        }
+        __syncthreads();
     }
-    __syncthreads();
-    for (int e = t; e < H2 * H2; e += kIB) K.Cl[b * H2 * H2 + e] = C[e / H2][e - (e / H2) * H2];
-    if (t < H2) K.Cp[b * H2 + t] = piv[t];
 }
 
-// rb (= K0^-1 r, band order) += P C^-1 Z^T rb
+// rb (= K0^-1 r, band order) += P C^-1 Z^T rb   (2 hmax <= 128 values in LDS)
 __global__ void __launch_bounds__(kIB) k_lbfgs_apply(const IpmK K) {
-    constexpr int HM2 = 32;
+    constexpr int HM2 = 128;
     __shared__ Scal S;
     __shared__ double w[HM2];
     const int64_t b = blockIdx.x;
     load_scal(K, b, S);
     const int H2 = 2 * K.hmax, t = threadIdx.x;
     double* rb = K.rb + b * K.nKp;
-    if (t < 64) {
-        double v = 0.0;  // lane r: (Z^T u)_r
-        if (t < H2 && (t % K.hmax) < S.lcount)
+    if (t < H2) {  // (Z^T u)_t
+        double v = 0.0;
+        if ((t % K.hmax) < S.lcount)
             for (int i = 0; i < K.nf; ++i) v += lb_z(K, S, b, t, i) * rb[K.pos[i]];
-        const double* L = K.Cl + b * H2 * H2;
-        const int32_t* pv = K.Cp + b * H2;
-        for (int k = 0; k < H2; ++k) {  // row interchanges, unit lower, upper (getrs)
-            const int p = pv[k];
-            if (p != k) {
-                const double vk = __shfl(v, k, 64), vp = __shfl(v, p, 64);
-                if (t == k) v = vp;
-                if (t == p) v = vk;
-            }
-        }
-        for (int k = 0; k < H2; ++k) {
-            const double vk = __shfl(v, k, 64);
-            if (t > k && t < H2) v -= L[t * H2 + k] * vk;
-        }
-        for (int k = H2 - 1; k >= 0; --k) {
-            if (t == k) v = v / L[k * H2 + k];
-            const double vk = __shfl(v, k, 64);
-            if (t < k) v -= L[t * H2 + k] * vk;
-        }
-        if (t < H2) w[t] = v;
+        w[t] = v;
     }
     __syncthreads();
+    const double* L = K.Cl + b * H2 * H2;
+    const int32_t* pv = K.Cp + b * H2;
+    if (t == 0)  // row interchanges (getrs), in order
+        for (int k = 0; k < H2; ++k) {
+            const int p = pv[k];
+            if (p != k) {
+                const double tmp = w[k];
+                w[k] = w[p];
+                w[p] = tmp;
+            }
+        }
+    __syncthreads();
+    for (int k = 0; k < H2; ++k) {  // unit lower
+        const double wk = w[k];
+        __syncthreads();
+        if (t > k && t < H2) w[t] -= L[t * H2 + k] * wk;
+        __syncthreads();
+    }
+    for (int k = H2 - 1; k >= 0; --k) {  // upper
+        if (t == 0) w[k] = w[k] / L[k * H2 + k];
+        __syncthreads();
+        const double wk = w[k];
+        if (t < k) w[t] -= L[t * H2 + k] * wk;
+        __syncthreads();
+    }
     for (int e = t; e < K.nKp; e += kIB) {
         double acc = 0.0;
         for (int q = 0; q < H2; ++q)
@@ -3019,6 +3297,25 @@ extern "C" void cfx_ipm_default_options(cfx_ipm_options* o) {
     o->bound_mult_init_method = 1;  // mu-based (Ipopt's default is constant, 1)
     o->bound_mult_init_val = 1.0;
     o->inertia_test = 0;
+    o->mu_strategy = CFX_MU_MONOTONE;
+    o->adaptive_mu_globalization = CFX_MU_GLOBAL_OBJ_CONSTR_FILTER;
+    o->mu_max_fact = 1000.0;
+    o->mu_max = -1.0;  // mu_max_fact * the first iterate's average complementarity
+    o->mu_min = 1e-11;
+    o->adaptive_mu_monotone_init_factor = 0.8;
+    o->sigma_max = 100.0;
+    o->sigma_min = 1e-6;
+    o->quality_function_section_sigma_tol = 1e-2;
+    o->quality_function_section_qf_tol = 0.0;
+    o->quality_function_max_section_steps = 8;
+    o->mu_change_resets_filter = 0;  // Ipopt: resets (the adaptive strategy here always does)
+    o->filter_margin_fact = 1e-5;
+    o->filter_max_margin = 1.0;
+    o->monotone_mu_floor = 0;  // tol / 10 (Ipopt: min(tol, compl_inf_tol) / (kappa_eps + 1))
+    o->nlp_scaling_method = 1;  // gradient-based
+    o->nlp_scaling_max_gradient = 100.0;
+    o->nlp_scaling_min_value = 1e-8;
+    o->bound_frac = 0.5;  // Ipopt: 0.01
 }
 
 // CSR of `key` (values in [0, nkeys)) with the sources of each key in increasing source order
@@ -3251,7 +3548,7 @@ static int ipm_create_common(cfx_ipm* s, const cfx_sizes& sz, int layout, const 
         K.o.watchdog_shortened_iter_trigger < 0 || K.o.watchdog_trial_iter_max < 0 ||
         (K.o.hessian_approximation != CFX_HESSIAN_EXACT && K.o.hessian_approximation != CFX_HESSIAN_LIMITED_MEMORY) ||
         (K.o.hessian_approximation == CFX_HESSIAN_LIMITED_MEMORY &&
-         (K.o.limited_memory_max_history < 1 || K.o.limited_memory_max_history > 16)) ||
+         (K.o.limited_memory_max_history < 1 || K.o.limited_memory_max_history > 64)) ||
         (K.o.restoration != CFX_RESTORATION_STEP && K.o.restoration != CFX_RESTORATION_PHASE) ||
         K.o.max_resto_iter < 0 || !(K.o.resto_penalty > 0) || !(K.o.required_infeasibility_reduction > 0) ||
         !(K.o.required_infeasibility_reduction < 1) || K.o.filter_reset_trigger < 1 || K.o.max_filter_resets < 0 ||
@@ -3262,7 +3559,19 @@ static int ipm_create_common(cfx_ipm* s, const cfx_sizes& sz, int layout, const 
         !(K.o.acceptable_compl_inf_tol > 0) || !(K.o.warm_start_bound_push > 0) || !(K.o.warm_start_bound_frac > 0) ||
         !(K.o.warm_start_bound_frac <= 0.5) || !(K.o.warm_start_mult_bound_push > 0) ||
         (K.o.bound_mult_init_method != 0 && K.o.bound_mult_init_method != 1) || !(K.o.bound_mult_init_val > 0) ||
-        (K.o.inertia_test != 0 && K.o.inertia_test != 1)) {
+        (K.o.inertia_test != 0 && K.o.inertia_test != 1) ||
+        (K.o.mu_strategy != CFX_MU_MONOTONE && K.o.mu_strategy != CFX_MU_ADAPTIVE) ||
+        (K.o.adaptive_mu_globalization != CFX_MU_GLOBAL_OBJ_CONSTR_FILTER &&
+         K.o.adaptive_mu_globalization != CFX_MU_GLOBAL_NEVER_MONOTONE) ||
+        !(K.o.mu_min > 0) || !(K.o.mu_max_fact > 0) || !(K.o.sigma_min > 0) || !(K.o.sigma_min <= 1) ||
+        !(K.o.sigma_max >= 1) || !(K.o.adaptive_mu_monotone_init_factor > 0) ||
+        K.o.quality_function_max_section_steps < 0 || !(K.o.quality_function_section_sigma_tol > 0) ||
+        !(K.o.quality_function_section_sigma_tol < 1) || !(K.o.quality_function_section_qf_tol >= 0) ||
+        !(K.o.filter_margin_fact > 0) || !(K.o.filter_max_margin > 0) ||
+        (K.o.mu_change_resets_filter != 0 && K.o.mu_change_resets_filter != 1) ||
+        (K.o.monotone_mu_floor != 0 && K.o.monotone_mu_floor != 1) ||
+        (K.o.nlp_scaling_method != 0 && K.o.nlp_scaling_method != 1) || !(K.o.nlp_scaling_max_gradient > 0) ||
+        !(K.o.nlp_scaling_min_value > 0) || !(K.o.bound_frac > 0) || !(K.o.bound_frac <= 0.5)) {
         s->err = "cfx_ipm_create: the handle must use CFX_LAYOUT_AOS (or batch 1) and the options must be valid";
         return create_fail(s, CFX_EINVAL);
     }
@@ -3732,7 +4041,16 @@ static int ipm_create_common(cfx_ipm* s, const cfx_sizes& sz, int layout, const 
             K.gradt = dalloc<double>(s, B * n, &rc);
         }
     }
-    K.rstat = dalloc<unsigned long long>(s, 3, &rc);
+    K.rstat = dalloc<unsigned long long>(s, 4, &rc);
+    K.adapt = K.o.mu_strategy == CFX_MU_ADAPTIVE;
+    K.ncomp = 0;
+    for (int i = 0; i < nf; ++i) K.ncomp += (int)hasL[i] + (int)hasU[i];
+    K.mfilt = K.rhsmu = K.rbc = nullptr;
+    if (K.adapt) {
+        K.mfilt = dalloc<double>(s, B * kFilt * 2, &rc);
+        K.rhsmu = dalloc<double>(s, B * nf, &rc);
+        K.rbc = dalloc<double>(s, B * nKp, &rc);
+    }
     K.cnt = dalloc<int32_t>(s, 4 * kSlots, &rc);
     s->d_fv = dalloc<double>(s, B * K.nfix, &rc);
     s->d_yo = dalloc<double>(s, B * m, &rc);
@@ -3930,6 +4248,22 @@ struct Run {
         }
         return CFX_OK;
     }
+    // adaptive mu: the unit-centering solve with the factors just made, then the quality-function oracle of the
+    // free-mode instances, which leaves their combined Newton step in rb (k_mu_oracle)
+    int mu_oracle() {
+        const IpmK& K = s->K;
+        hipLaunchKernelGGL(k_mu_cen_rhs, g, dim3(kIB), 0, st, K);
+        IPM_HIP(s, hipGetLastError());
+        IPM_RUN(resolve(K.rbc));
+        if (K.lbfgs) {  // the Woodbury correction of the centering solution too
+            IpmK K2 = K;
+            K2.rb = K.rbc;
+            hipLaunchKernelGGL(k_lbfgs_apply, g, dim3(kIB), 0, st, K2);
+        }
+        hipLaunchKernelGGL(k_mu_oracle, g, dim3(kIB), 0, st, K);
+        IPM_HIP(s, hipGetLastError());
+        return CFX_OK;
+    }
     // L-BFGS: after a Newton factorisation of K0, P = K0^-1 Z column by column, C = M - Z^T P, and the Newton
     // solution corrected (rb += P C^-1 Z^T rb)
     int lbfgs_newton() {
@@ -3977,12 +4311,13 @@ static int ipm_solve(cfx_ipm* s, const double* v0, const double* fixed_values, d
     const dim3 blk(kIB);
     s->st.eval_all = s->st.eval_g_f = s->st.eval_h = s->st.kkt_factor = s->st.iterations = s->st.host_syncs = 0;
     s->st.resto_phases = s->st.resto_iterations = s->st.soft_steps = 0;
-    IPM_HIP(s, hipMemsetAsync(K.rstat, 0, 3 * sizeof(unsigned long long), st));
+    IPM_HIP(s, hipMemsetAsync(K.rstat, 0, 4 * sizeof(unsigned long long), st));
     if (K.rsphase)  // the (2,2) block of instances outside the phase
         IPM_HIP(s, hipMemsetAsync(K.rdc, 0, B * K.m * sizeof(double), st));
     s->slot = 0;
     IPM_HIP(s, hipMemsetAsync(K.cnt, 0, 4 * kSlots * sizeof(int32_t), st));
     IPM_HIP(s, hipMemsetAsync(K.rb, 0, B * K.nKp * sizeof(double), st));  // padding rows of the blocks stay 0
+    if (K.adapt) IPM_HIP(s, hipMemsetAsync(K.rbc, 0, B * K.nKp * sizeof(double), st));
     if (K.lbfgs) IPM_HIP(s, hipMemsetAsync(K.hv, 0, B * K.nnzh * sizeof(double), st));  // W enters as sigma I
     IPM_HIP(s, hipMemcpyAsync(K.vx, v0, B * K.n * sizeof(double), kin, st));
     if (fixed_values && K.nfix)
@@ -4019,9 +4354,9 @@ static int ipm_solve(cfx_ipm* s, const double* v0, const double* fixed_values, d
             IPM_HIP(s, hipStreamSynchronize(st));
             std::fprintf(stderr,
                          "cfx_ipm trace %d: iters %d f %.10e err %.3e mu %.3e theta %.3e alpha %.3e a_z %.3e dw %.2e "
-                         "resto %d soft %d wd %d acc %d\n",
+                         "resto %d soft %d wd %d acc %d free %d avgc %.3e\n",
                          it, s0.iters, s0.fS / s0.sf, s0.err0, s0.mu, s0.theta, s0.alpha, s0.a_z, s0.dwl, s0.rs_on,
-                         s0.soft_on, s0.wd_on, s0.acc);
+                         s0.soft_on, s0.wd_on, s0.acc, s0.mfree, s0.avgc);
         }
         if (K.o.print_frequency_time > 0 && it > 0 && elapsed - last_print >= K.o.print_frequency_time) {
             Scal s0{};  // instance 0's optimality error, barrier, infeasibility and last step (one small read)
@@ -4070,6 +4405,7 @@ static int ipm_solve(cfx_ipm* s, const double* v0, const double* fixed_values, d
         for (int attempt = 0; attempt < 12; ++attempt) {
             IPM_RUN(R.kkt_factor(KKT_NEWTON));
             if (K.lbfgs) IPM_RUN(R.lbfgs_newton());
+            if (K.adapt) IPM_RUN(R.mu_oracle());
             const int sl = R.next_slot();
             IPM_RUN(R.curv(sl));
             IPM_HIP(s, hipGetLastError());
@@ -4174,13 +4510,14 @@ static int ipm_solve(cfx_ipm* s, const double* v0, const double* fixed_values, d
                        devp ? conv_out : (conv_out ? s->d_conv : nullptr), devp ? its_out : (its_out ? s->d_its : nullptr),
                        devp ? kkt_out : (kkt_out ? s->d_kkt : nullptr), s->d_status, (int)wall_stop);
     IPM_HIP(s, hipGetLastError());
-    unsigned long long rstat[3] = {0, 0, 0};
+    unsigned long long rstat[4] = {0, 0, 0, 0};
     IPM_HIP(s, hipMemcpyAsync(rstat, K.rstat, sizeof(rstat), hipMemcpyDeviceToHost, st));
     IPM_HIP(s, hipMemcpyAsync(s->h_status.data(), s->d_status, B * sizeof(int32_t), hipMemcpyDeviceToHost, st));
     IPM_HIP(s, hipStreamSynchronize(st));
     s->st.resto_phases = (int64_t)rstat[0];
     s->st.resto_iterations = (int64_t)rstat[1];
     s->st.soft_steps = (int64_t)rstat[2];
+    s->st.mu_mode_switches = (int64_t)rstat[3];
     if (v_out) IPM_HIP(s, hipMemcpyAsync(v_out, K.vx, B * K.n * sizeof(double), kout, st));
     if (f_out) IPM_HIP(s, hipMemcpyAsync(f_out, K.fraw, B * sizeof(double), kout, st));
     if (!devp) {

@@ -310,7 +310,7 @@ class ShardedNativeIpm:
         import torch
 
         from . import _cfx
-        from .solver import _HESSIAN_APPROXIMATION, _NATIVE_OPTIONS, _RESTORATION, IpmOptions
+        from .solver import IpmOptions, native_options
 
         self.torch = torch
         self.ocp, self.B = ocp, batch
@@ -326,9 +326,7 @@ class ShardedNativeIpm:
         self.ipm = _cfx.Ipm.external(
             batch, self.nlp.nv, self.nlp.ng, self.nlp.jac_structure(), self.nlp.hess_structure(),
             self.nlp.eval_all_ptr, self.nlp.eval_h_ptr, lb, ub, int(getattr(ocp, "n_params", 0) or 0),
-            {**{k: getattr(self.opt, k) for k in _NATIVE_OPTIONS},
-             "hessian_approximation": _HESSIAN_APPROXIMATION[self.opt.hessian_approximation],
-             "restoration": _RESTORATION[self.opt.restoration]},
+            native_options(self.opt),
             device=self.nlp.dev.index, stream=torch.cuda.current_stream(self.nlp.dev).cuda_stream)
 
     def solve(self, v0=None, fixed_values=None):

@@ -107,7 +107,8 @@ class IpmOptions:
     bound_mult_init_method: str = "mu-based"
     bound_mult_init_val: float = 1.0
     # inertia correction (NativeIpm, stage-chain layout): False the curvature test above; True Ipopt's test on the KKT
-    # matrix's inertia (exactly m negative eigenvalues, else dw grows), counted from the chain's pivot blocks
+    # matrix's inertia (exactly m negative eigenvalues, else dw grows), counted from the chain's pivot blocks.  Layouts
+    # without an inertia count (NativeIpm's band layouts, every BatchedIpm solve) keep the curvature test
     inertia_test: bool = False
     # Ipopt's warm start (NativeIpm: solve(..., warm_start=(y, z_l, z_u))): no least-squares multipliers; x pushed from
     # its bounds by warm_start_bound_push max(1, |bound|) (at most warm_start_bound_frac of the range), bound
@@ -116,7 +117,70 @@ class IpmOptions:
     warm_start_bound_push: float = 1e-3
     warm_start_bound_frac: float = 1e-3
     warm_start_mult_bound_push: float = 1e-3
+    # cold-start push: x_L + min(bound_push max(1, |x_L|), bound_frac (x_U - x_L)) (Ipopt's bound_frac is 0.01; this
+    # library's 0.5 pushes narrow-range variables to at most the middle of their range)
+    bound_frac: float = 0.5
+    # Ipopt's barrier-parameter strategy (IpAdaptiveMuUpdate / IpMonotoneMuUpdate).  "monotone": Fiacco-McCormick, mu
+    # decreased while the barrier problem's error is below kappa_eps mu (this library's default); "adaptive" (bioptim's
+    # Solver.IPOPT default, recalled — external/bioptim is not in the reference tree): the free-mu mode of Nocedal,
+    # Waechter & Waltz (2009) — every iteration mu = sigma * (average complementarity), sigma minimising Ipopt's quality
+    # function (mu_oracle "quality-function": the predicted 2-norm-squared dual infeasibility, primal infeasibility and
+    # complementarity after a step of mu's direction, golden-section search over log sigma); globalised by
+    # adaptive_mu_globalization: "obj-constr-filter" (Ipopt's default: an iterate not acceptable to a filter of the
+    # (f, ||c||_1) of the accepted free-mode iterates switches to the monotone mode at mu = adaptive_mu_monotone_init_factor
+    # * average complementarity, which returns to the free mode once an iterate is acceptable again) or
+    # "never-monotone-mode".  "kkt-error" globalisation and the probing / loqo oracles are not restated
+    mu_strategy: str = "monotone"
+    mu_oracle: str = "quality-function"
+    adaptive_mu_globalization: str = "obj-constr-filter"
+    mu_max_fact: float = 1000.0  # mu_max = mu_max_fact * average complementarity at the first iteration (mu_max <= 0)
+    mu_max: float = -1.0
+    mu_min: float = 1e-11
+    adaptive_mu_monotone_init_factor: float = 0.8
+    sigma_max: float = 100.0
+    sigma_min: float = 1e-6
+    quality_function_max_section_steps: int = 8
+    quality_function_section_sigma_tol: float = 1e-2
+    quality_function_section_qf_tol: float = 0.0
+    filter_margin_fact: float = 1e-5
+    filter_max_margin: float = 1.0
+    # Ipopt resets the line search's filter whenever the barrier parameter changes (linesearch_->Reset() in both mu
+    # updates: the filter's phi values belong to the old barrier function).  The adaptive strategy always does; for the
+    # monotone strategy this flag (off in this library's profile, which keeps the filter across mu decreases)
+    mu_change_resets_filter: bool = False
+    # floor of the monotone mu update: "library" tol / 10; "ipopt" min(tol, compl_inf_tol) / (kappa_eps + 1)
+    monotone_mu_floor: str = "library"
+    # Ipopt's nlp_scaling_method: "gradient-based" (f and each row of g scaled so that their largest gradient entry at
+    # the starting point is at most nlp_scaling_max_gradient, factors at least nlp_scaling_min_value) or "none"
+    nlp_scaling_method: str = "gradient-based"
+    nlp_scaling_max_gradient: float = 100.0
+    nlp_scaling_min_value: float = 1e-8
     verbose: bool = False
+
+    # Ipopt 3.14's defaults where bioptim's Solver.IPOPT leaves them, bioptim's values where it sets them (recalled, see
+    # DESIGN.md "Solver profiles"): the options Solver.IPOPT() applies by default.  Everything not listed keeps its
+    # IpmOptions default, which equals Ipopt's (tol on the unscaled problem, watchdog, second-order corrections, ...)
+    IPOPT_PROFILE = dict(
+        tol=1e-6, max_iter=1000, acceptable_tol=1e-6, acceptable_iter=15, mu_init=0.1,  # bioptim
+        mu_strategy="adaptive",  # bioptim (Ipopt's own default is "monotone")
+        limited_memory_max_history=50,  # bioptim (Ipopt: 6)
+        bound_relax_factor=1e-8, bound_push=1e-2, bound_frac=1e-2, honor_original_bounds=False,
+        range_scaling=False, bound_mult_init_method="constant", bound_mult_init_val=1.0,
+        max_resto_iter=3_000_000, max_filter_resets=5, filter_reset_trigger=5,
+        soft_resto_pderror_reduction_factor=0.9999, max_soft_resto_iters=10, resto_failure_restart=False,
+        mu_change_resets_filter=True, monotone_mu_floor="ipopt", nlp_scaling_method="gradient-based",
+        inertia_test=True)
+
+    @classmethod
+    def ipopt(cls, **overrides) -> "IpmOptions":
+        """The Ipopt / bioptim profile (IPOPT_PROFILE) with ``overrides``."""
+        return cls(**{**cls.IPOPT_PROFILE, **overrides})
+
+    def mu_floor(self) -> float:
+        """Lower bound of the monotone barrier parameter."""
+        if self.monotone_mu_floor == "ipopt":
+            return min(self.tol, self.compl_inf_tol) / (self.kappa_eps + 1.0)
+        return self.tol / 10
 
     def __post_init__(self):
         if self.filter_reset_trigger < 1 or self.max_filter_resets < 0:
@@ -129,15 +193,38 @@ class IpmOptions:
                   "acceptable_dual_inf_tol", "acceptable_compl_inf_tol"):
             if not getattr(self, k) > 0:
                 raise ValueError(f"{k} must be > 0")
+        choices = {"mu_strategy": ("monotone", "adaptive"), "mu_oracle": ("quality-function",),
+                   "adaptive_mu_globalization": ("obj-constr-filter", "never-monotone-mode"),
+                   "monotone_mu_floor": ("library", "ipopt"), "nlp_scaling_method": ("gradient-based", "none"),
+                   "bound_mult_init_method": ("constant", "mu-based"),
+                   "hessian_approximation": ("exact", "limited-memory")}
+        for k, allowed in choices.items():
+            if getattr(self, k) not in allowed:
+                raise ValueError(f"{k} must be one of {allowed} (got {getattr(self, k)!r}; Ipopt's other choices are not "
+                                 "restated here)")
+        if not (self.mu_min > 0 and self.mu_max_fact > 0 and 0 < self.sigma_min <= 1 <= self.sigma_max and
+                0 < self.adaptive_mu_monotone_init_factor and self.quality_function_max_section_steps >= 0 and
+                0 < self.quality_function_section_sigma_tol < 1 and self.quality_function_section_qf_tol >= 0 and
+                self.filter_margin_fact > 0 and self.filter_max_margin > 0):
+            raise ValueError("invalid adaptive barrier-parameter options")
+        if not (self.nlp_scaling_max_gradient > 0 and self.nlp_scaling_min_value > 0):
+            raise ValueError("nlp_scaling_max_gradient and nlp_scaling_min_value must be > 0")
+        if not (0 < self.bound_frac <= 0.5 and self.bound_push > 0):
+            raise ValueError("bound_push must be > 0 and 0 < bound_frac <= 0.5")
 
 
 class Solver:
     """bioptim's solver namespace as cocofest uses it: ``ocp.solve(Solver.IPOPT(_max_iter=..., _tol=...,
     _hessian_approximation="limited-memory"))`` (examples/getting_started/frequency_optimization.py:22,
     pulse_duration_optimization.py:41).  The options map onto the native interior point's (IpmOptions); the
-    ones that only steer Ipopt's own output or its external linear solver are accepted and ignored."""
+    ones that only steer Ipopt's own output or its external linear solver are accepted and ignored.
+
+    ``profile`` names the option set the explicit options start from: "ipopt" (the default — IpmOptions.IPOPT_PROFILE,
+    Ipopt 3.14's defaults with bioptim's Solver.IPOPT values where bioptim sets them, so a cocofest script is solved
+    with the reference's solver settings) or "cfx" (this library's tuned set, the IpmOptions defaults)."""
 
     class IPOPT:
+        _PROFILES = ("ipopt", "cfx")
         _OPTIONS = {"_tol": "tol", "_max_iter": "max_iter", "_acceptable_tol": "acceptable_tol",
                     "_acceptable_iter": "acceptable_iter", "_mu_init": "mu_init",
                     "_bound_relax_factor": "bound_relax_factor", "_bound_push": "bound_push",
@@ -154,23 +241,45 @@ class Solver:
                     "_dual_inf_tol": "dual_inf_tol", "_compl_inf_tol": "compl_inf_tol",
                     "_acceptable_constr_viol_tol": "acceptable_constr_viol_tol",
                     "_acceptable_dual_inf_tol": "acceptable_dual_inf_tol",
-                    "_acceptable_compl_inf_tol": "acceptable_compl_inf_tol"}
-        _IGNORED = {"show_online_optim", "show_options", "_print_level", "_linear_solver", "_nlp_scaling_method",
-                    "_check_derivatives_for_naninf", "_c_compile", "_print_timing_statistics", "_output_file"}
+                    "_acceptable_compl_inf_tol": "acceptable_compl_inf_tol",
+                    "_mu_strategy": "mu_strategy", "_mu_oracle": "mu_oracle",
+                    "_adaptive_mu_globalization": "adaptive_mu_globalization", "_mu_max_fact": "mu_max_fact",
+                    "_mu_max": "mu_max", "_mu_min": "mu_min", "_nlp_scaling_method": "nlp_scaling_method",
+                    "_nlp_scaling_max_gradient": "nlp_scaling_max_gradient", "_bound_frac": "bound_frac",
+                    "_bound_mult_init_method": "bound_mult_init_method", "_bound_mult_init_val": "bound_mult_init_val",
+                    "_honor_original_bounds": "honor_original_bounds",
+                    "_warm_start_init_point": "warm_start_init_point", "_warm_start_bound_push": "warm_start_bound_push",
+                    "_warm_start_bound_frac": "warm_start_bound_frac",
+                    "_warm_start_mult_bound_push": "warm_start_mult_bound_push"}
+        _IGNORED = {"show_online_optim", "show_options", "_print_level", "_linear_solver",
+                    "_check_derivatives_for_naninf", "_c_compile", "_print_timing_statistics", "_output_file",
+                    "_warm_start_slack_bound_push", "_warm_start_slack_bound_frac"}
+        # Ipopt's yes / no options
+        _YESNO = {"_honor_original_bounds", "_warm_start_init_point"}
 
-        def __init__(self, show_online_optim: bool = False, show_options: dict | None = None, **kwargs):
-            self._tol = 1e-6
-            self._max_iter = 1000
+        def __init__(self, show_online_optim: bool = False, show_options: dict | None = None, profile: str = "ipopt",
+                     **kwargs):
+            if profile not in self._PROFILES:
+                raise ValueError(f"Solver.IPOPT: profile must be one of {self._PROFILES}")
+            self.profile = profile
+            base = IpmOptions.ipopt() if profile == "ipopt" else IpmOptions()
+            self._tol = base.tol
+            self._max_iter = 1000  # bioptim's _max_iter, in either profile
             self._hessian_approximation = "exact"
-            self._limited_memory_max_history = 6
+            self._limited_memory_max_history = base.limited_memory_max_history
             self._print_level = 5
             self._linear_solver = "mumps"
             for k, v in kwargs.items():
                 if k not in self._OPTIONS and k not in self._IGNORED:
                     raise TypeError(f"Solver.IPOPT: unknown option {k!r}")
+                if k in self._YESNO and isinstance(v, str):
+                    if v not in ("yes", "no"):
+                        raise ValueError(f"Solver.IPOPT: {k} must be 'yes' or 'no'")
+                    v = v == "yes"
                 setattr(self, k, v)
             if self._hessian_approximation not in ("exact", "limited-memory"):
                 raise ValueError("hessian_approximation must be 'exact' or 'limited-memory'")
+            self.options()  # validates every option now (unknown choices raise ValueError)
 
         # bioptim's setters
         def set_maximum_iterations(self, n: int):
@@ -202,11 +311,28 @@ class Solver:
         def max_iter(self):
             return self._max_iter
 
+        def set_mu_strategy(self, value: str):
+            self._mu_strategy = value
+            self.options()
+
+        def set_nlp_scaling_method(self, value: str):
+            self._nlp_scaling_method = value
+            self.options()
+
         def apply(self, opts: "IpmOptions") -> "IpmOptions":
+            """The profile's options, then the explicit ones, onto ``opts`` (fields neither sets keep their value)."""
+            if self.profile == "ipopt":
+                for name, v in IpmOptions.IPOPT_PROFILE.items():
+                    setattr(opts, name, v)
             for k, name in self._OPTIONS.items():
                 if hasattr(self, k):
                     setattr(opts, name, getattr(self, k))
+            opts.__post_init__()
             return opts
+
+        def options(self) -> "IpmOptions":
+            """The IpmOptions this solver object stands for."""
+            return self.apply(IpmOptions())
 
 
 def apply_solver(opts: "IpmOptions", solver) -> "IpmOptions":
@@ -279,9 +405,14 @@ class BatchedIpm:
         if self.opt.restoration not in (None, "step", "phase"):
             raise ValueError("restoration must be 'phase' or 'step'")
         self._phase = self.opt.restoration in (None, "phase")  # the native solver's default too
+        # what only the native interior point implements is refused here rather than silently ignored
         if self.opt.hessian_approximation != "exact":
             raise ValueError("BatchedIpm: hessian_approximation='limited-memory' is implemented by the native interior "
                              "point (NativeIpm / cfx_ipm) only")
+        if self.opt.warm_start_init_point:
+            raise ValueError("BatchedIpm: warm_start_init_point is implemented by NativeIpm only")
+        # (inertia_test: the band factorisation here has no inertia count, so the curvature test stands in for it, as
+        # on NativeIpm's band layouts)
         self.dev = torch.device(torch_device) if torch_device is not None else torch.device("cuda", device)
         self.h = handle if handle is not None else ocp.nlp(batch=batch, layout="aos", device=device)
         h = self.h
@@ -409,14 +540,22 @@ class BatchedIpm:
         return (t * (1.0 + self.hoff.to(t.dtype))).sum(1)
 
     def _set_function_scaling(self, v):
+        """Ipopt's gradient-based NLP scaling at the starting point: s = min(1, max_gradient / max |grad|), at least
+        nlp_scaling_min_value; nlp_scaling_method "none": s = 1."""
         torch = self.torch
         g, jac, f, grad = self._eval_all(v)
+        opt = self.opt
+        if opt.nlp_scaling_method == "none":
+            self.sf = torch.ones((self.B,), dtype=torch.float64, device=self.dev)
+            self.sg = torch.ones((self.B, self.m), dtype=torch.float64, device=self.dev)
+            return
         gF = grad[:, self.freeT] * self.d
         ja = (jac[:, self.jselT] * self.d[self.jcF]).abs()
         rmax = torch.zeros((self.B, self.m), dtype=torch.float64, device=self.dev)
         rmax.scatter_reduce_(1, self.jrF.expand(self.B, -1), ja, reduce="amax")
-        self.sf = torch.clamp(100.0 / torch.clamp(gF.abs().amax(1), min=1e-300), max=1.0)
-        self.sg = torch.clamp(100.0 / torch.clamp(rmax, min=1e-300), max=1.0)
+        gm, lo = opt.nlp_scaling_max_gradient, opt.nlp_scaling_min_value
+        self.sf = torch.clamp(torch.clamp(gm / torch.clamp(gF.abs().amax(1), min=1e-300), max=1.0), min=lo)
+        self.sg = torch.clamp(torch.clamp(gm / torch.clamp(rmax, min=1e-300), max=1.0), min=lo)
 
     def _kkt_matvec(self, hv, diag_x, jv, dx, dy):
         """[[W + diag_x, J^T], [J, -delta_c I]] [dx; dy] from the triplets (the residual of iterative refinement)."""
@@ -490,8 +629,8 @@ class BatchedIpm:
         pu = opt.bound_push * torch.clamp(torch.where(hasU, ubF.abs(), torch.ones_like(ubF)), min=1.0)
         both = hasL & hasU
         width = torch.where(both, ubF - lbF, torch.full_like(lbF, np.inf))
-        pl = torch.minimum(pl, 0.5 * width)
-        pu = torch.minimum(pu, 0.5 * width)
+        pl = torch.minimum(pl, opt.bound_frac * width)
+        pu = torch.minimum(pu, opt.bound_frac * width)
         x = torch.where(hasL, torch.maximum(x, lbF + pl), x)
         x = torch.where(hasU, torch.minimum(x, ubF - pu), x)
         mu = torch.full((B,), opt.mu_init, dtype=torch.float64, device=self.dev)
@@ -530,6 +669,14 @@ class BatchedIpm:
         soft_cnt = torch.zeros((B,), dtype=torch.int64, device=self.dev)
         soft_fac = opt.soft_resto_pderror_reduction_factor if (m and self._phase) else 0.0
         self.soft_steps = 0  # soft-restoration steps taken (all instances)
+        # adaptive barrier update: free-mu mode per instance, the (f, theta) filter of its globalisation, mu_max
+        adaptive = opt.mu_strategy == "adaptive"
+        mfree = torch.full((B,), adaptive, dtype=torch.bool, device=self.dev)
+        mfilt = torch.full((B, 64, 2), np.inf, dtype=torch.float64, device=self.dev)
+        mfpos = torch.zeros((B,), dtype=torch.int64, device=self.dev)
+        mu_max = torch.full((B,), -1.0, dtype=torch.float64, device=self.dev)
+        self.mode_switches = torch.zeros((B,), dtype=torch.int64, device=self.dev)  # free -> monotone switches
+        mufl = opt.mu_floor()
 
         self._v_template = v
 
@@ -580,24 +727,67 @@ class BatchedIpm:
             done = done | out_of_iters
             if bool(done.all()):
                 break
-            # barrier update (monotone): while the barrier sub-problem is solved, decrease mu
-            for _ in range(5):
+            # barrier update.  Adaptive strategy (IpAdaptiveMuUpdate): the globalisation decides the mode first — a
+            # free-mode iterate not acceptable to the (f, theta) filter switches to the monotone mode, a monotone-mode
+            # iterate acceptable to it returns to the free mode; acceptable iterates enter the filter.  The free mode's
+            # mu comes from the quality-function oracle once the KKT matrix is factored (below)
+            mu_prev = mu
+            mono = ~done
+            max_passes = 5  # the monotone strategy's fast decrease (mu_allow_fast_monotone_decrease)
+            if adaptive:
+                zB = torch.zeros_like(mu)
+                theta_c = g.abs().sum(1) if m else zB
+                ncomp = int(hasL.sum()) + int(hasU.sum())
+                avg = (compl_l.sum(1) + compl_u.sum(1)) / max(ncomp, 1)
+                mu_max = torch.where(mu_max < 0, torch.full_like(mu_max, opt.mu_max) if opt.mu_max > 0 else
+                                     opt.mu_max_fact * avg, mu_max)
+                act = ~done
+                ok = (torch.ones_like(done) if opt.adaptive_mu_globalization == "never-monotone-mode"
+                      else self._mfilter_ok(mfilt, f, theta_c))
+                to_mono = act & mfree & ~ok
+                back = act & ~mfree & ok
+                mfilt, mfpos = self._mfilter_add(mfilt, mfpos, act & ok, f, theta_c)
+                mfree = (mfree | back) & ~to_mono
+                mu = torch.where(to_mono, torch.minimum(torch.clamp(opt.adaptive_mu_monotone_init_factor * avg,
+                                                                    min=opt.mu_min), mu_max), mu)
+                self.mode_switches = self.mode_switches + to_mono.long()
+                mono = act & ~mfree & ~to_mono
+                max_passes = 1
+            # monotone update: while the barrier sub-problem is solved, decrease mu
+            for _ in range(max_passes):
                 e_cmu = torch.maximum((compl_l - torch.where(hasL, mu[:, None], 0 * mu[:, None])).abs().amax(1),
                                       (compl_u - torch.where(hasU, mu[:, None], 0 * mu[:, None])).abs().amax(1)) / sc
                 e_mu = torch.maximum(torch.maximum(e_d, e_p), e_cmu)
-                dec = (~done) & (e_mu <= opt.kappa_eps * mu) & (mu > opt.tol / 10)
+                dec = mono & (e_mu <= opt.kappa_eps * mu) & (mu > mufl)
                 if not bool(dec.any()):
                     break
-                mu = torch.where(dec, torch.clamp(torch.minimum(opt.kappa_mu * mu, mu ** opt.theta_mu), min=opt.tol / 10),
-                                 mu)
-            tau = torch.clamp(1.0 - mu, min=opt.tau_min)
+                mu = torch.where(dec, torch.clamp(torch.minimum(opt.kappa_mu * mu, mu ** opt.theta_mu), min=mufl), mu)
+            # Ipopt restarts the line search's filter whenever mu changes (and so in every free-mode iteration)
+            reset_ls = (~done) & (mu != mu_prev) & bool(adaptive or opt.mu_change_resets_filter)
+            if adaptive:
+                reset_ls = reset_ls | (mfree & ~done)
+            if bool(reset_ls.any()):
+                filt = torch.where(reset_ls[:, None, None], torch.tensor([np.inf, -np.inf], dtype=torch.float64,
+                                                                         device=self.dev), filt)
 
             W = self._scaled_hess(vfull, y)
             sig = torch.where(hasL, zl / sl, torch.zeros_like(x)) + torch.where(hasU, zu / su, torch.zeros_like(x))
-            bar = torch.where(hasL, mu[:, None] / sl, torch.zeros_like(x)) - torch.where(hasU, mu[:, None] / su,
-                                                                                         torch.zeros_like(x))
-            rhs_x = -(gF + jty - bar)
-            rhs = torch.cat([rhs_x, -g], dim=1)
+            if adaptive:
+                # the Newton step is affine in mu: rhs = [-(grad f + J^T y) + mu cen; -c], cen = 1 / s_L - 1 / s_U.  The
+                # free-mode instances solve mu = 0 and cen alone, the oracle picks mu, the step is their combination
+                cen_x = torch.where(hasL, 1.0 / sl, torch.zeros_like(x)) - torch.where(hasU, 1.0 / su, torch.zeros_like(x))
+                rhs_ax = -(gF + jty)
+                osel = mfree & ~done
+                murhs = torch.where(osel, torch.zeros_like(mu), mu)
+                rhs = torch.cat([rhs_ax + murhs[:, None] * cen_x, -g], dim=1)
+                rhs_c = torch.cat([cen_x, torch.zeros_like(g)], dim=1)
+                rd2 = (rd * rd).sum(1)
+                c2 = (g * g).sum(1) if m else zB
+            else:
+                bar = torch.where(hasL, mu[:, None] / sl, torch.zeros_like(x)) - torch.where(hasU, mu[:, None] / su,
+                                                                                             torch.zeros_like(x))
+                rhs_x = -(gF + jty - bar)
+                rhs = torch.cat([rhs_x, -g], dim=1)
             # inertia correction by curvature test: increase delta_w until dx^T (W + Sigma + dw) dx > 0
             dw = torch.zeros((B,), dtype=torch.float64, device=self.dev)
             for attempt in range(12):
@@ -606,6 +796,14 @@ class BatchedIpm:
                 sol = self._kkt_solve(K, rhs)
                 for _ in range(opt.refine):
                     sol = sol + self._kkt_solve(K, rhs - self._kkt_matvec(W, dxx, jv, sol[:, :nf], sol[:, nf:]))
+                if adaptive and bool(osel.any()):
+                    solc = self._kkt_solve(K, rhs_c)
+                    for _ in range(opt.refine):
+                        solc = solc + self._kkt_solve(K, rhs_c - self._kkt_matvec(W, dxx, jv, solc[:, :nf],
+                                                                                  solc[:, nf:]))
+                    mu_o = self._mu_oracle(osel, sl, su, zl, zu, sol[:, :nf], solc[:, :nf], rd2, c2, avg, mu_max)
+                    mu = torch.where(osel, mu_o, mu)
+                    sol = torch.where(osel[:, None], sol + mu[:, None] * solc, sol)
                 dx, dy = sol[:, :nf], sol[:, nf:]
                 curv = self._quad_w(W, dx) + (dxx * dx * dx).sum(1)
                 # a zero pivot (LAPACK info != 0) or a non-finite solution counts as wrong inertia: more delta_w
@@ -618,6 +816,11 @@ class BatchedIpm:
                                                                      torch.clamp(delta_w_last / 3, min=1e-20),
                                                                      torch.full_like(dw, 1e-4)), dw * 8), dw)
             delta_w_last = dw
+            tau = torch.clamp(1.0 - mu, min=opt.tau_min)
+            if adaptive:  # the final mu's barrier gradient and Newton right-hand side (line search, corrections)
+                bar = torch.where(hasL, mu[:, None] / sl, torch.zeros_like(x)) - torch.where(hasU, mu[:, None] / su,
+                                                                                             torch.zeros_like(x))
+                rhs_x = rhs_ax + mu[:, None] * cen_x
             dzl = torch.where(hasL, mu[:, None] / sl - zl - zl / sl * dx, torch.zeros_like(x))
             dzu = torch.where(hasU, mu[:, None] / su - zu + zu / su * dx, torch.zeros_like(x))
             # fraction to the boundary
@@ -837,6 +1040,123 @@ class BatchedIpm:
         filt = torch.where(grow[:, None, None] & slot[:, :, None],
                            torch.stack([(1 - 1e-5) * theta, phi - 1e-5 * theta], dim=1)[:, None, :], filt)
         return filt, fpos + grow.long()
+
+    # ---- adaptive barrier parameter (Ipopt's IpAdaptiveMuUpdate, IpQualityFunctionMuOracle; recalled) -------------
+    @staticmethod
+    def _mfilter_ok(mfilt, f, theta):
+        """Acceptable to the mu globalisation's filter (IpFilter::Acceptable): against every entry (f_i, theta_i),
+        f <= f_i or theta < theta_i (empty entries are +inf)."""
+        return ((f[:, None] <= mfilt[:, :, 0]) | (theta[:, None] < mfilt[:, :, 1])).all(1)
+
+    def _mfilter_add(self, mfilt, mfpos, on, f, theta):
+        """RememberCurrentPointAsAccepted: (f - margin, theta - margin), margin = filter_margin_fact
+        min(filter_max_margin, theta), enters the filter of the instances ``on``; entries it dominates leave it.  A ring
+        of mfilt.shape[1] slots: the first free slot, else slot mfpos."""
+        torch = self.torch
+        opt = self.opt
+        margin = opt.filter_margin_fact * torch.clamp(theta, max=opt.filter_max_margin)
+        fe, te = f - margin, theta - margin
+        dom = on[:, None] & (fe[:, None] <= mfilt[:, :, 0]) & (te[:, None] <= mfilt[:, :, 1])
+        mfilt = torch.where(dom[:, :, None], torch.full_like(mfilt, np.inf), mfilt)
+        free_slot = torch.isinf(mfilt[:, :, 0]) & torch.isinf(mfilt[:, :, 1])
+        nslot = mfilt.shape[1]
+        first = torch.where(free_slot.any(1), free_slot.long().argmax(1), mfpos % nslot)
+        slot = torch.arange(nslot, device=self.dev)[None, :] == first[:, None]
+        mfilt = torch.where((on[:, None] & slot)[:, :, None], torch.stack([fe, te], 1)[:, None, :], mfilt)
+        return mfilt, mfpos + on.long()
+
+    def _mu_oracle(self, sel, sl, su, zl, zu, dxa, dxc, rd2, c2, avg, mu_max):
+        """Ipopt's quality-function mu oracle (QualityFunctionMuOracle::CalculateMu, 2-norm-squared, no centrality or
+        balancing term) for the instances ``sel``.  The step for mu = sigma avg (avg: the average complementarity) is
+        dx = dxa + mu dxc (affine and unit-centering solutions of the factored KKT system), dz as in the iteration; the
+        quality of sigma is the predicted (1 - a_d)^2 |grad L|^2 / n_x + (1 - a_p)^2 |c|^2 / m + |(s + a_p ds)(z + a_d
+        dz)|^2 / n_bounds, a_p / a_d the fractions to the boundary (tau = max(tau_min, 1 - mu)).  sigma: if q(1 - 1e-2)
+        > q(1) a golden-section search over log sigma in [1, min(sigma_max, mu_max / avg)], else over
+        [max(sigma_min, mu_min / avg), 1 - 1e-2] (quality_function_max_section_steps sections, stopping once the
+        bracket is within quality_function_section_sigma_tol of its upper end); the best of the two inner points, or
+        of an end point never moved.  Returns mu per instance (the others: anything)."""
+        torch = self.torch
+        opt = self.opt
+        hasL, hasU = self.hasL, self.hasU
+        nd = max(int(sl.shape[1]), 1)
+        nc = int(hasL.sum()) + int(hasU.sum())
+        z = torch.zeros_like(sl)
+
+        def q(sig):
+            mu = (sig * avg)[:, None]
+            dx = dxa + mu * dxc
+            dzl = torch.where(hasL, mu / sl - zl - zl / sl * dx, z)
+            dzu = torch.where(hasU, mu / su - zu + zu / su * dx, z)
+            tau = torch.clamp(1.0 - mu[:, 0], min=opt.tau_min)
+            ap = torch.minimum(self._max_step(sl, dx, hasL, tau), self._max_step(su, -dx, hasU, tau))
+            ad = torch.minimum(self._max_step(zl, dzl, hasL, tau), self._max_step(zu, dzu, hasU, tau))
+            a, d = ap[:, None], ad[:, None]
+            cl = torch.where(hasL, (sl + a * dx) * (zl + d * dzl), z)
+            cu = torch.where(hasU, (su - a * dx) * (zu + d * dzu), z)
+            val = (1.0 - ad) ** 2 * rd2 / nd
+            if self.m:
+                val = val + (1.0 - ap) ** 2 * c2 / self.m
+            if nc:
+                val = val + ((cl * cl).sum(1) + (cu * cu).sum(1)) / nc
+            return val
+
+        ones = torch.ones_like(avg)
+        s1m = 1.0 - max(1e-4, opt.quality_function_section_sigma_tol)
+        safe = avg > 0
+        avgs = torch.where(safe, avg, ones)
+        q1m, q1 = q(s1m * ones), q(ones)
+        up = q1m > q1  # the quality decreases beyond sigma = 1
+        s_hi = torch.where(up, torch.clamp(mu_max / avgs, max=opt.sigma_max), torch.clamp(opt.mu_min / avgs,
+                                                                                           min=opt.sigma_min))
+        # bracket [lo, hi] in sigma, with the known end values (-1: unknown)
+        lo = torch.where(up, ones, s_hi)
+        hi = torch.where(up, s_hi, torch.maximum(s_hi, s1m * ones))
+        q_lo = torch.where(up, q1, -ones)
+        q_hi = torch.where(up, -ones, q1m)
+        trivial = lo >= hi
+        sig_triv = torch.where(up, hi, lo)
+        a, b = torch.log(lo), torch.log(torch.maximum(hi, lo))
+        a0, b0 = a.clone(), b.clone()
+        gfac = (3.0 - np.sqrt(5.0)) / 2.0
+        m1, m2 = a + gfac * (b - a), a + (1.0 - gfac) * (b - a)
+        qm1, qm2 = q(torch.exp(m1)), q(torch.exp(m2))
+        live = sel & ~trivial
+        for _ in range(opt.quality_function_max_section_steps):
+            qs = torch.stack([q_lo, q_hi, qm1, qm2], 1)
+            known = qs >= 0
+            qmin = torch.where(known, qs, torch.full_like(qs, np.inf)).amin(1)
+            qmax = torch.where(known, qs, torch.full_like(qs, -np.inf)).amax(1)
+            live = live & (torch.exp(b) - torch.exp(a) >= opt.quality_function_section_sigma_tol * torch.exp(b)) & \
+                (1.0 - qmin / qmax >= opt.quality_function_section_qf_tol)
+            if not bool(live.any()):
+                break
+            right = qm1 > qm2  # the minimum is in [m1, b]
+            na = torch.where(right, m1, a)
+            nq_lo = torch.where(right, qm1, q_lo)
+            nb = torch.where(right, b, m2)
+            nq_hi = torch.where(right, q_hi, qm2)
+            nm1 = torch.where(right, m2, na + gfac * (nb - na))
+            nm2 = torch.where(right, na + (1.0 - gfac) * (nb - na), m1)
+            qn = q(torch.exp(torch.where(right, nm2, nm1)))
+            nqm1 = torch.where(right, qm2, qn)
+            nqm2 = torch.where(right, qn, qm1)
+            c = live
+            a, b, q_lo, q_hi = (torch.where(c, new, old) for new, old in ((na, a), (nb, b), (nq_lo, q_lo), (nq_hi, q_hi)))
+            m1, m2, qm1, qm2 = (torch.where(c, new, old) for new, old in ((nm1, m1), (nm2, m2), (nqm1, qm1), (nqm2, qm2)))
+        best = torch.where(qm1 < qm2, m1, m2)
+        qbest = torch.where(qm1 < qm2, qm1, qm2)
+        # an end point never moved competes with the inner points (its value computed if unknown)
+        hi_end = b == b0
+        lo_end = (a == a0) & ~hi_end
+        q_end = torch.where(hi_end, q_hi, q_lo)
+        need = (hi_end | lo_end) & (q_end < 0)
+        if bool((need & sel & ~trivial).any()):
+            q_end = torch.where(need, q(torch.exp(torch.where(hi_end, b, a))), q_end)
+        take = (hi_end | lo_end) & (q_end < qbest)
+        best = torch.where(take, torch.where(hi_end, b, a), best)
+        sig = torch.where(trivial, sig_triv, torch.exp(best))
+        mu = torch.clamp(torch.minimum(sig * avg, mu_max), min=opt.mu_min)
+        return torch.where(safe, mu, torch.full_like(mu, opt.mu_min))
 
     def _pd_error(self, gF, jv, y, zl, zu, g, x, mu):
         """Ipopt's primal-dual system error (IpoptCalculatedQuantities::curr_primal_dual_system_error) of the scaled
@@ -1234,9 +1554,33 @@ _NATIVE_OPTIONS = ("tol", "max_iter", "acceptable_tol", "acceptable_iter", "mu_i
                    "print_frequency_time", "soft_resto_pderror_reduction_factor", "max_soft_resto_iters",
                    "resto_failure_restart", "constr_viol_tol", "dual_inf_tol", "compl_inf_tol",
                    "acceptable_constr_viol_tol", "acceptable_dual_inf_tol", "acceptable_compl_inf_tol",
-                   "warm_start_bound_push", "warm_start_bound_frac", "warm_start_mult_bound_push", "inertia_test")
+                   "warm_start_bound_push", "warm_start_bound_frac", "warm_start_mult_bound_push", "inertia_test",
+                   "mu_max_fact", "mu_max", "mu_min", "adaptive_mu_monotone_init_factor", "sigma_max", "sigma_min",
+                   "quality_function_section_sigma_tol", "quality_function_section_qf_tol",
+                   "quality_function_max_section_steps", "mu_change_resets_filter", "filter_margin_fact",
+                   "filter_max_margin", "nlp_scaling_max_gradient", "nlp_scaling_min_value", "bound_frac",
+                   "warm_start_init_point", "honor_original_bounds", "range_scaling", "bound_mult_init_val")
 _HESSIAN_APPROXIMATION = {"exact": 0, "limited-memory": 1}
 _RESTORATION = {"step": 0, "phase": 1, None: 1}
+_ENUMS = {"hessian_approximation": _HESSIAN_APPROXIMATION, "restoration": _RESTORATION,
+          "bound_mult_init_method": {"constant": 0, "mu-based": 1}, "mu_strategy": {"monotone": 0, "adaptive": 1},
+          "adaptive_mu_globalization": {"obj-constr-filter": 0, "never-monotone-mode": 1},
+          "monotone_mu_floor": {"library": 0, "ipopt": 1}, "nlp_scaling_method": {"none": 0, "gradient-based": 1}}
+
+
+def native_options(opt: IpmOptions) -> dict:
+    """cfx_ipm_options fields of ``opt`` (NativeIpm and distributed.ShardedNativeIpm: one mapping, so that the same
+    IpmOptions give the same algorithm in both).  BatchedIpm-only options (refine) are refused."""
+    opt.__post_init__()
+    if opt.refine:
+        raise ValueError("the native interior point has no iterative refinement (refine > 0): BatchedIpm only")
+    out = {}
+    for k in _NATIVE_OPTIONS:
+        v = getattr(opt, k)
+        out[k] = int(v) if isinstance(v, bool) else v
+    for k, table in _ENUMS.items():
+        out[k] = table[getattr(opt, k)]
+    return out
 
 
 class NativeIpm:
@@ -1252,22 +1596,13 @@ class NativeIpm:
         self.ocp = ocp
         self.B = batch
         self.opt = options or IpmOptions()
-        if self.opt.refine:
-            raise ValueError("NativeIpm: iterative refinement (refine > 0) is only available in BatchedIpm")
+        nopt = native_options(self.opt)
         self.h = ocp.nlp(batch=batch, layout="aos", device=device)
         self.n, self.m = self.h.nv, self.h.ng
         lb, ub = ocp.bounds_vector()
         self.fixed = np.where(lb == ub)[0]
         self.free = np.where(lb != ub)[0]
-        self.ipm = _cfx.Ipm(self.h, lb, ub, int(getattr(ocp, "n_params", 0) or 0),
-                            {**{k: getattr(self.opt, k) for k in _NATIVE_OPTIONS},
-                             "hessian_approximation": _HESSIAN_APPROXIMATION[self.opt.hessian_approximation],
-                             "restoration": _RESTORATION[self.opt.restoration],
-                             "warm_start_init_point": int(self.opt.warm_start_init_point),
-                             "honor_original_bounds": int(self.opt.honor_original_bounds),
-                             "range_scaling": int(self.opt.range_scaling),
-                             "bound_mult_init_method": {"constant": 0, "mu-based": 1}[self.opt.bound_mult_init_method],
-                             "bound_mult_init_val": float(self.opt.bound_mult_init_val)})
+        self.ipm = _cfx.Ipm(self.h, lb, ub, int(getattr(ocp, "n_params", 0) or 0), nopt)
         self.calls = {"eval_all": 0, "eval_h": 0, "eval_g_f": 0, "kkt_factor": 0}
 
     def solve(self, v0=None, fixed_values=None, warm_start=None):

@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define CFX_ABI_VERSION 10
+#define CFX_ABI_VERSION 11
 
 /* return codes */
 #define CFX_OK 0
@@ -371,7 +371,7 @@ typedef struct cfx_ipm_options {
     int32_t watchdog_trial_iter_max;
     /* Ipopt's hessian_approximation: CFX_HESSIAN_EXACT (the callbacks' eval_h) or CFX_HESSIAN_LIMITED_MEMORY (no
        eval_h: an L-BFGS approximation of the Lagrangian Hessian from the last limited_memory_max_history (6, at
-       most 16) steps, compact form sigma I - low rank, sigma = s^T y / s^T s; the low-rank part enters every Newton
+       most 64) steps, compact form sigma I - low rank, sigma = s^T y / s^T s; the low-rank part enters every Newton
        solve through the Sherman-Morrison-Woodbury identity on the band factors) */
     int32_t hessian_approximation;
     int32_t limited_memory_max_history;
@@ -448,11 +448,45 @@ typedef struct cfx_ipm_options {
        constraints), else dw grows — counted for the stage-chain layout (cfx_btri_inertia's count on the chain plus a
        Bunch-Kaufman LDL^T of the border's Schur complement; other layouts keep the curvature test) */
     int32_t inertia_test;
+    /* Ipopt's barrier-parameter strategy (ABI 11).  mu_strategy CFX_MU_MONOTONE (default): Fiacco-McCormick, mu
+       decreased while the barrier problem's scaled error is below kappa_eps mu.  CFX_MU_ADAPTIVE (bioptim's
+       Solver.IPOPT setting): Ipopt's free-mu mode — each iteration the KKT matrix is factored once and solved for the
+       affine (mu = 0) and unit-centering right-hand sides; mu = sigma * (average complementarity) with sigma minimising
+       Ipopt's quality function (predicted 2-norm-squared dual / primal infeasibility and complementarity after the step,
+       golden section over log sigma within [sigma_min, sigma_max] and [mu_min, mu_max], at most
+       quality_function_max_section_steps sections); the Newton step is the solutions' combination.  Globalisation
+       (adaptive_mu_globalization): CFX_MU_GLOBAL_OBJ_CONSTR_FILTER — an iterate not acceptable to a filter of the
+       (f, ||c||_1) of accepted iterates (margin filter_margin_fact min(filter_max_margin, ||c||_1)) switches to the
+       monotone mode at mu = adaptive_mu_monotone_init_factor * average complementarity, an acceptable one returns to the
+       free mode; CFX_MU_GLOBAL_NEVER_MONOTONE — always free.  mu_max <= 0: mu_max_fact times the first iterate's
+       average complementarity. */
+    int32_t mu_strategy;
+    int32_t adaptive_mu_globalization;
+    double mu_max_fact, mu_max, mu_min, adaptive_mu_monotone_init_factor;
+    double sigma_max, sigma_min, quality_function_section_sigma_tol, quality_function_section_qf_tol;
+    int32_t quality_function_max_section_steps;
+    /* Ipopt resets the line search's filter whenever mu changes (ABI 11; the adaptive strategy always does, the
+       monotone strategy when this is 1; default 0) */
+    int32_t mu_change_resets_filter;
+    double filter_margin_fact, filter_max_margin;
+    /* floor of the monotone mu: 0 (default) tol / 10; 1 Ipopt's min(tol, compl_inf_tol) / (kappa_eps + 1) */
+    int32_t monotone_mu_floor;
+    /* Ipopt's nlp_scaling_method (ABI 11): 1 gradient-based (default: f and each row of g scaled at the starting point
+       by min(1, nlp_scaling_max_gradient / max |gradient|), at least nlp_scaling_min_value), 0 none */
+    int32_t nlp_scaling_method;
+    double nlp_scaling_max_gradient, nlp_scaling_min_value;
+    /* cold-start push from the bounds: min(bound_push max(1, |bound|), bound_frac (ub - lb)); Ipopt's bound_frac is
+       0.01, this library's default 0.5 (ABI 11) */
+    double bound_frac;
 } cfx_ipm_options;
 #define CFX_HESSIAN_EXACT 0
 #define CFX_HESSIAN_LIMITED_MEMORY 1
 #define CFX_RESTORATION_STEP 0
 #define CFX_RESTORATION_PHASE 1
+#define CFX_MU_MONOTONE 0
+#define CFX_MU_ADAPTIVE 1
+#define CFX_MU_GLOBAL_OBJ_CONSTR_FILTER 0
+#define CFX_MU_GLOBAL_NEVER_MONOTONE 1
 
 /* per-instance outcome of a solve (cfx_ipm_get_status), Ipopt's ApplicationReturnStatus values */
 #define CFX_IPM_SOLVE_SUCCEEDED 0
@@ -473,6 +507,8 @@ typedef struct cfx_ipm_stats {
     int64_t soft_steps;                     /* soft-restoration steps taken, summed over the instances */
     /* stage-chain KKT layout (ABI 9; cfx_btri_*): nodes and their padded size (0: a band layout above) */
     int64_t kkt_chain_nodes, kkt_chain_sp;
+    /* (ABI 11) adaptive mu strategy: switches from its free mode to its monotone mode, summed over the instances */
+    int64_t mu_mode_switches;
 } cfx_ipm_stats;
 
 typedef struct cfx_ipm cfx_ipm;

@@ -31,11 +31,11 @@ def _starts(ocp, B, seed, spread=10.0):
     return v0
 
 
-def _both(ocp, B, v0, tol=1e-8, fixed_values=None, max_iter=300, restoration="phase"):
+def _both(ocp, B, v0, tol=1e-8, fixed_values=None, max_iter=300, restoration="phase", **extra):
     from cocofest_amd.solver import BatchedIpm, IpmOptions, NativeIpm
 
     # the same restoration on both sides (BatchedIpm's own default is the minimum-norm step, NativeIpm's the phase)
-    opts = IpmOptions(tol=tol, max_iter=max_iter, restoration=restoration)
+    opts = IpmOptions(tol=tol, max_iter=max_iter, restoration=restoration, **extra)
     ref = BatchedIpm(ocp, batch=B, options=opts)
     r_ref = ref.solve(v0, fixed_values=fixed_values)
     ref.close()
@@ -219,10 +219,11 @@ def test_limited_memory_hessian_cfg3(B):
     lb, ub = ocp.bounds_vector()
     span = np.where(np.isfinite(ub - lb), ub - lb, np.maximum(np.abs(r_ex.v).max(0), 1.0))
     assert np.max(np.abs(r_lm.v - r_ex.v) / np.maximum(span, 1e-12)) < 1e-4
-    if B == 1:  # the bioptim-style entry: ocp.solve(Solver.IPOPT(...))
+    if B == 1:  # the bioptim-style entry: ocp.solve(Solver.IPOPT(...)), the facade's Ipopt / bioptim profile
         res = ocp.solve(Solver.IPOPT(_hessian_approximation="limited-memory", _max_iter=1000, _tol=1e-8))
-        assert bool(res.converged[0])
-        np.testing.assert_allclose(res.f, r_ex.f, rtol=1e-6, atol=1e-9)
+        ex = ocp.solve(Solver.IPOPT(_max_iter=1000, _tol=1e-8))
+        assert bool(res.converged[0]) and bool(ex.converged[0])
+        np.testing.assert_allclose(res.f, ex.f, rtol=1e-6, atol=1e-9)
 
 
 def test_native_ipm_infeasible_instance_stops_alone():
@@ -342,3 +343,64 @@ def test_native_ipm_wide_split_kernels_reach_the_same_optimum(B, monkeypatch):
     span = np.where(np.isfinite(ub - lb), ub - lb, 1.0)
     assert np.max(np.abs(b.v - a.v) / np.maximum(span, 1e-12)) < 1e-5
     assert np.all(np.abs(b.iterations - a.iterations) <= 5), (a.iterations, b.iterations)
+
+
+@pytest.mark.parametrize("case,glob", [(c, "obj-constr-filter") for c in ("cfg3", "hmed", "fatigue_rk4", "cfg2_zero")] +
+                         [("cfg3", "never-monotone-mode")])
+def test_native_adaptive_mu_matches_the_specification(case, glob):
+    """Ipopt's adaptive barrier-parameter strategy (mu_strategy "adaptive", bioptim's Solver.IPOPT setting: the
+    quality-function oracle on the affine and centering solutions of one factorisation, golden section over log
+    sigma; obj-constr-filter globalisation with its monotone fallback, or never-monotone-mode) in the native kernels
+    (k_ipm_begin's mode decision, k_mu_cen_rhs, k_mu_oracle) against BatchedIpm's restatement: the same KKT points from
+    the same starts, iteration counts within a few (reduction orders differ), on shooting problems with free pulse
+    widths, intensities with parameters and sliding windows, the fatigue families at RK4, and cfg 2 from the zero
+    initial guess (least-squares multipliers, restoration)."""
+    t = np.linspace(0, 1, 11)
+    if case == "cfg3":
+        ocp = cases.product_ocp(**dict(cases.cfg3(), objective=TRACK))
+        B, v0 = 4, None
+    elif case == "hmed":
+        ocp = cases.product_ocp(name="hmed2018", stims=[0.0, 0.1, 0.2, 0.3, 0.4], final_time=0.5, truncation=5,
+                                scheme="RK1", m=5, objective={"force_tracking": [t, 40 * t]}, n_shooting=None)
+        B, v0 = 2, None
+    elif case == "fatigue_rk4":
+        ocp = cases.product_ocp(name="ding2007_with_fatigue", stims=[0.0, 0.05, 0.1, 0.15], final_time=0.2,
+                                truncation=4, scheme="RK4", m=3, objective={"force_tracking": [t, 40 * t]},
+                                n_shooting=None)
+        B, v0 = 2, None
+    else:
+        ocp = cases.product_ocp(**cases.cfg2())
+        B, v0 = 1, None
+    v0 = _starts(ocp, B, 2) if v0 is None else v0
+    r_ref, r_nat = _both(ocp, B, v0, mu_strategy="adaptive", adaptive_mu_globalization=glob)
+    print(case, glob, "iterations", r_ref.iterations, r_nat.iterations, "f", r_ref.f, r_nat.f)
+    _compare(ocp, r_ref, r_nat, it_slack=6)
+
+
+def test_solver_ipopt_profile_solves_cfg3_on_the_gpu():
+    """ocp.solve(Solver.IPOPT()) — the facade's default Ipopt / bioptim profile (adaptive mu, Ipopt's bound push,
+    constant bound multipliers, bound relaxation, no range scaling, Ipopt's inertia test where the layout counts it) —
+    converges on cfg 3 from the reference's initial guess to the library profile's optimum (same f to 1e-6: the bound
+    relaxation of 1e-8 moves it slightly), with Ipopt's Solve_Succeeded; and the limited-memory Hessian with bioptim's
+    50 pairs (the native L-BFGS kernels hold up to 64)."""
+    from cocofest_amd import Solver
+    from cocofest_amd.solver import IpmOptions, NativeIpm
+
+    ocp = cases.product_ocp(**dict(cases.cfg3(), objective=TRACK))
+    res = ocp.solve(Solver.IPOPT())
+    out = {}
+    for name, o in (("library", {}), ("library, relaxed bounds", dict(bound_relax_factor=1e-8)),
+                    ("library, relaxed, adaptive", dict(bound_relax_factor=1e-8, mu_strategy="adaptive"))):
+        lib = NativeIpm(ocp, batch=1, options=IpmOptions(tol=1e-6, max_iter=1000, **o))
+        out[name] = lib.solve()
+        lib.close()
+        print(name, out[name].iterations, out[name].f, out[name].status)
+    print("ipopt profile", res.iterations, res.f, res.status)
+    assert res.status[0] == 0 and all(r.status[0] == 0 for r in out.values())
+    # Ipopt's bound relaxation (1e-8 of each width bound) moves the optimum of this width-bound-active problem by
+    # ~2e-4 of f; the profile lands on the relaxed problem's optimum
+    np.testing.assert_allclose(res.f, out["library, relaxed bounds"].f, rtol=1e-6)
+    lm = ocp.solve(Solver.IPOPT(_hessian_approximation="limited-memory"))
+    print("ipopt profile, limited memory (50 pairs)", lm.iterations, lm.f, lm.status)
+    assert lm.status[0] in (0, 1)
+    np.testing.assert_allclose(lm.f, res.f, rtol=1e-6)
