@@ -12,8 +12,12 @@
 // U_k = block (k, k+1).  cfx_ipm builds this grouping from the callbacks' triplets (rows matched one-to-one to a
 // variable of their node; rows that cannot be matched — marker rows, end conditions on fixed states — go to a small
 // dense border, solved by its Schur complement as for the Hmed parameters).  With that matching every principal
-// submatrix over a contiguous range of nodes is a KKT matrix whose constraint block has full row rank, so the pivot
-// blocks below are nonsingular for any Hessian: no pivoting across blocks is needed.
+// submatrix over a contiguous range of nodes is a KKT matrix whose constraint block has full structural row rank, so
+// the pivot blocks below are structurally nonsingular and the factorisation pivots within each block only.  That is
+// not numerical nonsingularity: a block [W_k J_k^T; J_k -dc] whose W_k is singular on null(J_k) is (nearly) singular,
+// and no pivoting across blocks rescues it.  An exactly zero pivot, or a column with no finite pivot candidate, is
+// reported in info (the interior point then raises its regularisation dw); the inertia test (cfx_btri_inertia) counts
+// such blocks' eigenvalues, the default curvature test sees them only through the step they produce.
 //
 // Block cyclic reduction (log2 M levels).  Level l (h = 2^l) eliminates the nodes i = h mod 2h, every one
 // independently:  D_i^-1 (Gauss-Jordan with partial pivoting in LDS), X_i = D_i^-1 L_i, Y_i = D_i^-1 U_i (FP64 MFMA,
@@ -176,7 +180,13 @@ __global__ void __launch_bounds__(kNT) k_chain_elim(Chain C, int first, int step
             key = fmax(key, __longlong_as_double((long long)((bits & ~0x7Full) | (uint64_t)(63 - lane))));
         }
         key = wave_max(key);
-        const int p = 127 - (int)((uint64_t)__double_as_longlong(key) & 0x7Full);
+        int p = 127 - (int)((uint64_t)__double_as_longlong(key) & 0x7Full);
+        if (!(key >= 0.0)) {  // (wave-uniform) no finite candidate — every unused row NaN / Inf: singular; the lowest
+                              // unused row keeps the indices in range
+            const unsigned long long m0 = __ballot(lane < SP && !used0), m1 = __ballot(lane + 64 < SP && !used1);
+            p = m0 ? __ffsll((long long)m0) - 1 : 64 + __ffsll((long long)m1) - 1;
+            if (!sing) sing = k + 1;
+        }
         used0 = used0 || p == lane;
         used1 = used1 || p == lane + 64;
         if (t == 0) prow[k] = (uint8_t)p, pstep[p] = (uint8_t)k;
@@ -478,16 +488,24 @@ static int levels(int M) {
     return L;
 }
 
+// the dynamic LDS limit of one k_chain_upd instantiation raised (once) when it needs more than the default 64 KiB
+template <int SP, bool BL>
+static hipError_t allow_upd_lds() {
+    if (chain_upd_lds<SP, BL>() <= 65536) return hipSuccess;
+    static const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_chain_upd<SP, BL>),
+                                                    hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                    (int)chain_upd_lds<SP, BL>());
+    return e;
+}
+
 template <int SP>
 static hipError_t factor_sp(const Chain& C, int64_t B, int32_t* info, hipStream_t s) {
     const int L = levels(C.M);
     constexpr bool FITS = chain_b_fits<SP>();
-    if (chain_upd_lds<SP, FITS>() > 65536) {  // above the default dynamic LDS limit: raised once per kernel
-        static const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_chain_upd<SP, FITS>),
-                                                        hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                        (int)chain_upd_lds<SP, FITS>());
-        if (e != hipSuccess) return e;
-    }
+    // both instantiations the levels below can launch (SP = 96 without BLDS needs 74,496 B)
+    hipError_t e = allow_upd_lds<SP, FITS>();
+    if (e == hipSuccess) e = allow_upd_lds<SP, false>();
+    if (e != hipSuccess) return e;
     for (int l = 0; l < L; ++l) {
         const int h = 1 << l;
         const int ne = (C.M - h + 2 * h - 1) / (2 * h), ns = (C.M + 2 * h - 1) / (2 * h);

@@ -62,6 +62,15 @@ ap.add_argument("--pulse-bounds", default="all", choices=["all", "first"],
                 help="per-pulse widths: bounds on every interval's copy (all) or on the pulse's first interval (first)")
 ap.add_argument("--range-scaling", type=int, default=1,
                 help="1: the product's variable scaling by the bound range (default); 0: none, as Ipopt")
+ap.add_argument("--profile", default="script", choices=["script", "ipopt", "cfx"],
+                help="ipopt: Solver.IPOPT()'s Ipopt / bioptim profile (IpmOptions.ipopt: adaptive mu, Ipopt's bound push, "
+                     "constant bound multipliers, no range scaling, ...) with only tol / max_iter / wall and the warm "
+                     "start taken from this script; cfx: the library profile (IpmOptions()) likewise; script: this "
+                     "script's own flags")
+ap.add_argument("--mu-strategy", default=None, choices=["monotone", "adaptive"], help="override Ipopt's mu_strategy")
+ap.add_argument("--trace", action="store_true", help="CFX_IPM_TRACE=1 (one stderr line per iteration)")
+ap.add_argument("--hessian", default=None, choices=["exact", "limited-memory"], help="Ipopt's hessian_approximation")
+ap.add_argument("--lm-history", type=int, default=None, help="limited_memory_max_history")
 ap.add_argument("--current", action="store_true",
                 help="today's calcium conventions and per-interval widths instead of the stored revision's")
 args = ap.parse_args()
@@ -127,6 +136,18 @@ def run(objective):
     elif args.mu_init:
         kw["mu_init"] = args.mu_init
     t_mult = time.perf_counter() - t0
+    if args.profile != "script":  # a named profile: only the solve's budget and the warm start from this script
+        keep = {k: kw[k] for k in ("tol", "max_iter", "max_wall_time", "print_frequency_time", "warm_start_init_point",
+                                   "mu_init", "warm_start_bound_push", "warm_start_mult_bound_push") if k in kw}
+        kw = {**(IpmOptions.IPOPT_PROFILE if args.profile == "ipopt" else {}), **keep}
+    if args.mu_strategy:
+        kw["mu_strategy"] = args.mu_strategy
+    if args.hessian:
+        kw["hessian_approximation"] = args.hessian
+    if args.lm_history:
+        kw["limited_memory_max_history"] = args.lm_history
+    if args.trace:
+        os.environ["CFX_IPM_TRACE"] = "1"
     ipm = NativeIpm(ocp, batch=1, options=IpmOptions(**kw))
     t1 = time.perf_counter()
     res = ipm.solve(v0[None], warm_start=(y[None], zl[None], zu[None]) if warm else None)
@@ -161,6 +182,7 @@ def run(objective):
            "resto_phases": int(st.get("resto_phases", 0)), "kkt_chain_nodes": st.get("kkt_chain_nodes"),
            "kkt_n": st.get("kkt_n"), "s_per_iteration": (t2 - t1) / max(1, int(res.iterations[0])),
            "reference_time_to_optimize_s": float(d["time_to_optimize"]), "pulse_bounds": args.pulse_bounds,
+           "profile": args.profile, "mu_mode_switches": int(st.get("mu_mode_switches", 0)),
            **{k: kw[k] for k in kw if k != "tol"},
            **rep}
     if args.out:  # the end point, for a later look

@@ -76,7 +76,7 @@ def _marker_jacobian(pb, X):
     return out
 
 
-def reduced_stationarity(objective="fatigue", data=None, legacy=True, w_end=1.0, threads=8):
+def reduced_stationarity(objective="fatigue", data=None, legacy=True, w_end=1.0, threads=8, _keep=None):
     """First-order optimality in the space of the decisions that remain once the dynamics are solved: the 360
     per-pulse pulse widths p.  The stored states are the forward integration of p (their continuity rows hold to
     1e-12 / 1e-9), so the stored point is a KKT point of the reference's NLP iff
@@ -122,6 +122,7 @@ def reduced_stationarity(objective="fatigue", data=None, legacy=True, w_end=1.0,
     G = np.zeros((len(MUSCLES), int(pidx.max()) + 1, 5))
     for k in range(N):
         G[:, pidx[k]] += grad_pw[k]
+    G_seconds = G.reshape(-1, 5).copy()  # per second of pulse width (the stored revision's parameter unit)
     G = G.reshape(-1, 5) * (pwhi - pwlo)  # per unit of the pulse-width range
     P = np.stack([d[f"pulse_duration_{n}"] for n in MUSCLES]).ravel()
     at_lo = P <= pwlo + 1e-12
@@ -141,6 +142,9 @@ def reduced_stationarity(objective="fatigue", data=None, legacy=True, w_end=1.0,
     res = G[:, 0] + G[:, 1:] @ sol[:4] - z
     free = sign == 0
     scale = np.abs(G[:, 0]).max()
+    if _keep is not None:  # (ipopt_termination_audit's inputs)
+        _keep.update(G_seconds=G_seconds, sign=sign, nu_ls=sol[:4].copy(), z_ls=z / (pwhi - pwlo), J=J, X=X, v=v,
+                     seeds=seeds, pb=pb, pwlo=pwlo, pwhi=pwhi, P=P, xlo=xlo, xhi=xhi)
     return {"objective": objective, "data": data or objective, "legacy": legacy, "w_end": w_end,
             "pulses": len(P), "at_bounds": int((~free).sum()), "active_kept": int(keep.sum()),
             "grad_f_max": float(scale), "nu": [float(x) for x in sol[:4]],
@@ -271,3 +275,75 @@ def adjoint_multipliers(ocp, v, lb, ub, pulse_bounds="all"):
            "pulses_at_bounds": int((sign != 0).sum()), "pulses_sign_kept": int(keep.sum()),
            "reduced_dual_inf_rel": float(np.abs(resid).max() / scale)}
     return y, zl, zu, rep
+
+
+def ipopt_termination_audit(objective="fatigue", legacy=True, threads=8):
+    """Ipopt's termination tests (IpOptErrorConv: CurrentIsOptimal / CurrentIsAcceptable) at a stored optimum, in the
+    stored revision's NLP — per-pulse pulse-width parameters in SECONDS (VariableScaling 1, fes_ocp_dynamics.py:373),
+    the script's Solver.IPOPT(_max_iter=10000) (reaching_task_pulse_duration_optimization.py:117) with bioptim's tol =
+    acceptable_tol = 1e-6 (recalled).  In the reduced space of reduced_stationarity every multiplier is fixed by the 4
+    equality multipliers nu (the continuity multipliers are their adjoint) and the 360 per-pulse bound multipliers z, so
+    the best achievable dual infeasibility is a small problem:
+      * least squares with the signs of z enforced (reduced_stationarity's multipliers), and
+      * the linear program  min_{nu, z} max_j |g_j + G_j nu - z_j|  (z_j >= 0 at the lower bound, <= 0 at the upper,
+        0 off the bounds): d*, the smallest max-norm unscaled dual infeasibility ANY multipliers give.
+    Ipopt's scaled error uses its gradient-based NLP scaling (s_f = 1 at the script's initial guess: the objective's
+    gradient there is far below nlp_scaling_max_gradient 100 — 2 / a_rest for the fatigue Mayer term at A = a_rest, 0 for
+    the force term at F = 0; the continuity rows' factors s_g from the interval Jacobians at that guess) and the
+    multiplier scaling s_d = max(s_max, (|y_s|_1 + |z_s|_1) / (m + n_z)) / s_max, s_max = 100.  Returns the numbers."""
+    from scipy.optimize import linprog
+
+    from oracle import c_msk
+
+    keep = {}
+    base = reduced_stationarity(objective, legacy=legacy, threads=threads, _keep=keep)
+    G, sign = keep["G_seconds"], keep["sign"]
+    pb, X, seeds, J = keep["pb"], keep["X"], keep["seeds"], keep["J"]
+    n_p = G.shape[0]
+    # least squares (signs enforced), converted to seconds
+    nu_ls, z_ls = keep["nu_ls"], keep["z_ls"]
+    r_ls = G[:, 0] + G[:, 1:] @ nu_ls - z_ls
+    # the linear program over (nu, z, t)
+    nv = 4 + n_p + 1
+    c = np.zeros(nv)
+    c[-1] = 1.0
+    A = np.zeros((2 * n_p, nv))
+    A[:n_p, :4], A[:n_p, 4:4 + n_p], A[:n_p, -1] = G[:, 1:], -np.eye(n_p), -1.0
+    A[n_p:, :4], A[n_p:, 4:4 + n_p], A[n_p:, -1] = -G[:, 1:], np.eye(n_p), -1.0
+    b = np.concatenate([-G[:, 0], G[:, 0]])
+    bounds = [(None, None)] * 4 + [((0, None) if s_ > 0 else ((None, 0) if s_ < 0 else (0, 0))) for s_ in sign] + \
+        [(0, None)]
+    lp = linprog(c, A_ub=A, b_ub=b, bounds=bounds, method="highs")
+    nu_lp, z_lp, dstar = lp.x[:4], lp.x[4:4 + n_p], float(lp.x[-1])
+    # Ipopt's constraint scaling of the continuity rows at the script's initial guess (states at rest, widths at their
+    # initial value: the product's initial guess for this problem)
+    ocp = R.legacy_product(objective)
+    v0 = ocp.initial_guess_vector()
+    _, J0 = c_msk.shooting(pb, v0[None], want_g=False, threads=threads)
+    J0 = J0[0]  # (N, nx, nz): dPhi_k/d(x_k, u_k); the -1 on x_{k+1} as well
+    sg = np.minimum(1.0, 100.0 / np.maximum(np.maximum(np.abs(J0).max(2), 1.0), 1e-300)).reshape(-1)
+    sg = np.maximum(sg, 1e-8)
+    N, nx = R.N, pb.nx
+
+    def scaled_error(nu, z, dinf):
+        coef = np.concatenate([[1.0], nu])
+        lam = seeds[R.N] @ coef
+        ys = [lam]
+        for k in range(N - 1, 0, -1):  # continuity multipliers: the adjoint (the row into x_k)
+            lam = J[k][:, :nx].T @ lam + seeds[k] @ coef
+            ys.append(lam)
+        y = np.concatenate(ys[::-1])  # rows 1..N-1, N (N - 1 + 1 blocks of nx)
+        y_s = np.abs(y) / sg          # scaled problem's multipliers (s_f = 1): y / s_g (row k: into x_{k+1})
+        n_rows = y.size + 2
+        lo, hi = keep["xlo"], keep["xhi"]
+        n_z = int(np.isfinite(lo[:, 1:]).sum() + np.isfinite(hi[:, 1:]).sum()) + 2 * n_p
+        s_d = max(100.0, (y_s.sum() + np.abs(nu[:2]).sum() + np.abs(z).sum()) / (n_rows + n_z)) / 100.0
+        return dinf / s_d, s_d
+
+    err_ls, sd_ls = scaled_error(nu_ls, z_ls, float(np.abs(r_ls).max()))
+    err_lp, sd_lp = scaled_error(nu_lp, z_lp, dstar)
+    return {**base, "dual_inf_unscaled_ls": float(np.abs(r_ls).max()), "dual_inf_unscaled_min_lp": dstar,
+            "lp_status": int(lp.status), "s_d_ls": sd_ls, "s_d_lp": sd_lp, "scaled_error_ls": err_ls,
+            "scaled_error_lp": err_lp, "s_g_min": float(sg.min()), "s_g_median": float(np.median(sg)),
+            "wrong_signed_or_free_pulses_ls": int((np.abs(r_ls) > 1e-6 * np.abs(G[:, 0]).max()).sum()),
+            "tol": 1e-6, "acceptable_tol": 1e-6, "dual_inf_tol": 1.0}

@@ -83,6 +83,33 @@ def test_btri_matches_dense_solve(sp, M, B):
         assert err < 1e-11 and res < 1e-14, (b, err, res)
 
 
+def test_btri_wide_levels_at_sp96():
+    """sp = 96 with M = 520 nodes: level 0 has 260 survivors, so its Schur updates take the variant with the right
+    operand in L2 (k_chain_upd<96, false>, 74,496 B of LDS: above the 64 KiB default, raised like the staged variant's —
+    ADVICE round 5); the solution is checked by its block residual (the dense matrix would be 20 GB)."""
+    sp, M, B = 96, 520, 1
+    D, L, U = _system(B, M, sp, seed=9)
+    rng = np.random.default_rng(2)
+    rhs = rng.normal(size=(B, 1, M * sp))
+    x, info = _btri(D, L, U, rhs)
+    assert np.all(info == 0)
+    X = x[0, 0].reshape(M, sp)
+    R = np.einsum("kij,kj->ki", D[0], X)
+    R[1:] += np.einsum("kij,kj->ki", L[0, 1:], X[:-1])
+    R[:-1] += np.einsum("kij,kj->ki", U[0, :-1], X[1:])
+    res = np.abs(R.reshape(-1) - rhs[0, 0]).max() / (np.abs(D).max() * np.abs(X).max())
+    assert res < 1e-14, res
+
+
+def test_btri_reports_a_non_finite_pivot_block():
+    """A pivot block of NaN has no finite pivot candidate in any column: reported singular at its first column, and the
+    pivot search keeps its row indices in range (the empty search used to decode row 127)."""
+    D, L, U = _system(2, 8, 16, seed=4)
+    D[1, 5] = np.nan
+    _, info = _btri(D, L, U, np.ones((2, 1, 8 * 16)))
+    assert info[0] == 0 and info[1] == 5 * 16 + 1, info
+
+
 def test_btri_reports_a_singular_pivot_block():
     D, L, U = _system(1, 8, 16, seed=3)
     D[0, 5] = 0.0  # node 5 is eliminated at level 0: its block has no pivot at all
