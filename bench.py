@@ -116,7 +116,7 @@ FP64_FMA_ISSUE_PEAK = 5.18e11  # wave-instr/s, measured (profiles/round1/micro_f
 
 def msk_pmc():
     """VALU wave-instructions per cfg-5 g + J_g step (k_msk_values + k_msk_stagecoef_par + k_msk_tangents_lds,
-    B = 65,536) from the committed rocprofv3 SQ pass (profiles/msk_pmc.json, scripts/r3/gpu_msk_prof.sh), if any."""
+    B = 65,536) from the committed rocprofv3 SQ pass (profiles/msk_pmc.json; the round-3 driver scripts/r3/gpu_msk_prof.sh is in git history at 4131d45), if any."""
     f = ROOT / "profiles" / "msk_pmc.json"
     if not f.exists():
         return None
@@ -252,7 +252,10 @@ def keep_constant_section(h, v, g, jac, steps=50):
 
 def convergence(device):
     """Second half of the BASELINE metric: wall-clock to an Ipopt-equivalent KKT point (tol 1e-6) of the batched
-    interior-point driver over libcfx (cocofest_amd/solver.py), single instance and multi-start batch."""
+    interior-point driver over libcfx (cocofest_amd/solver.py), single instance and multi-start batch.  Each case under
+    this library's profile (IpmOptions(): monotone mu; the keys without suffix, as in earlier rounds) and under the
+    facade's default, the Ipopt / bioptim profile the reference solves with (Solver.IPOPT(): adaptive mu, Ipopt's bound
+    push / multipliers / relaxation; keys "..._ipopt_profile")."""
     from cocofest_amd.solver import IpmOptions, NativeIpm
 
     out = {}
@@ -268,15 +271,19 @@ def convergence(device):
             free = lb != ub
             v0[:, free] = np.clip(v0[:, free] + rng.uniform(0, 1, (B, free.sum())) * np.minimum(ub[free] - lb[free], 10),
                                   lb[free], ub[free])
-        ipm = NativeIpm(ocp, batch=B, device=device, options=IpmOptions(tol=1e-6, max_iter=300))
-        ipm.solve(v0[:, :] if B > 1 else None)  # warm-up (kernel loading, allocator)
-        ipm.calls = {k: 0 for k in ipm.calls}
-        res = ipm.solve(v0 if B > 1 else None)
-        ipm.close()
-        out[name] = {"batch": B, "wall_s": res.wall_time, "converged": int(res.converged.sum()),
-                     "iterations_max": int(res.iterations.max()), "iterations_median": float(np.median(res.iterations)),
-                     "solves_per_s": float(res.converged.sum() / res.wall_time), "callbacks": res.n_callbacks,
-                     "nv": ipm.n, "ng": ipm.m}
+        for suffix, opts in (("", IpmOptions(tol=1e-6, max_iter=300)),
+                             ("_ipopt_profile", IpmOptions.ipopt(tol=1e-6, max_iter=300))):
+            ipm = NativeIpm(ocp, batch=B, device=device, options=opts)
+            ipm.solve(v0[:, :] if B > 1 else None)  # warm-up (kernel loading, allocator)
+            ipm.calls = {k: 0 for k in ipm.calls}
+            res = ipm.solve(v0 if B > 1 else None)
+            ipm.close()
+            out[name + suffix] = {"batch": B, "wall_s": res.wall_time, "converged": int(res.converged.sum()),
+                                  "iterations_max": int(res.iterations.max()),
+                                  "iterations_median": float(np.median(res.iterations)),
+                                  "solves_per_s": float(res.converged.sum() / res.wall_time),
+                                  "callbacks": res.n_callbacks, "nv": ipm.n, "ng": ipm.m,
+                                  "mu_strategy": opts.mu_strategy, "f_median": float(np.median(res.f))}
     return out
 
 
@@ -626,11 +633,13 @@ def msk_section(device, tp, ocp1, cpu_seconds=0.0):
 
     out = dict(tp)
     out["cpu_baseline"] = msk_cpu_baseline(ocp1, cpu_seconds) if cpu_seconds > 0 else None
-    ipm = NativeIpm(msk_build(5), batch=1, device=device, options=IpmOptions(tol=1e-6, max_iter=1000))
-    res = ipm.solve()
-    ipm.close()
-    out["convergence_rk4x5"] = {"wall_s": res.wall_time, "converged": int(res.converged.sum()),
-                                "iterations": int(res.iterations.max()), "f": float(res.f[0])}
+    for key, opts in (("convergence_rk4x5", IpmOptions(tol=1e-6, max_iter=1000)),
+                      ("convergence_rk4x5_ipopt_profile", IpmOptions.ipopt(tol=1e-6, max_iter=1000))):
+        ipm = NativeIpm(msk_build(5), batch=1, device=device, options=opts)
+        res = ipm.solve()
+        ipm.close()
+        out[key] = {"wall_s": res.wall_time, "converged": int(res.converged.sum()), "status": int(res.status[0]),
+                    "iterations": int(res.iterations.max()), "f": float(res.f[0])}
     return out
 
 
@@ -676,27 +685,38 @@ def build_reaching(objective="fatigue"):
 def reaching_section(device, wall_limit=150.0):
     """Wall-clock to convergence of the one reference OCP with a timed reference solve: the fatigue objective of the
     reaching task from the product's default initial guess (the reference script's own start), Ipopt's termination
-    tests at tol 1e-6, bound_relax_factor 1e-8; the stage-chain KKT layout (block cyclic reduction).  Beside it the
-    reference's own time_to_optimize (sol.real_time_to_optimize, cocofest/result/pickle.py:32; unknown hardware, an
-    older revision, use_sx=False)."""
+    tests at tol 1e-6; the stage-chain KKT layout (block cyclic reduction).  Headline: the reference's own solver
+    settings — the script's Solver.IPOPT(_max_iter=10000) through the facade's Ipopt / bioptim profile (adaptive mu,
+    bound_relax_factor 1e-8, ...); beside it this library's profile (monotone mu).  And the reference's own
+    time_to_optimize (sol.real_time_to_optimize, cocofest/result/pickle.py:32; unknown hardware, an older revision,
+    use_sx=False) — a max_iter iterate, not a converged solve (tests/test_reaching_termination.py)."""
+    from cocofest_amd import Solver
     from cocofest_amd.solver import IpmOptions, NativeIpm
 
     root = os.path.dirname(os.path.abspath(__file__))
     ref_t = float(np.load(os.path.join(root, "tests", "golden", "reaching_pulse_duration_fatigue.npz"))["time_to_optimize"])
     ocp = build_reaching("fatigue")
-    ipm = NativeIpm(ocp, batch=1, device=device,
-                    options=IpmOptions(tol=1e-6, max_iter=5000, bound_relax_factor=1e-8, max_wall_time=wall_limit))
-    res = ipm.solve()
-    st = dict(ipm.last_stats)
-    ipm.close()
+    out = {}
+    for key, opts in (("ipopt_profile", Solver.IPOPT(_max_iter=10000, _max_wall_time=wall_limit).options()),
+                      ("library_profile", IpmOptions(tol=1e-6, max_iter=5000, bound_relax_factor=1e-8,
+                                                     max_wall_time=wall_limit))):
+        ipm = NativeIpm(ocp, batch=1, device=device, options=opts)
+        res = ipm.solve()
+        st = dict(ipm.last_stats)
+        ipm.close()
+        out[key] = {"wall_s": res.wall_time, "iterations": int(res.iterations[0]), "status": int(res.status[0]),
+                    "converged": bool(res.converged[0]), "f": float(res.f[0]), "mu_strategy": opts.mu_strategy,
+                    "s_per_iteration": res.wall_time / max(1, int(res.iterations[0])),
+                    "reference_over_product": ref_t / res.wall_time}
+    head = out["ipopt_profile"]
     return {"objective": "fatigue (minimize_muscle_fatigue)", "start": "product default initial guess",
-            "wall_s": res.wall_time, "iterations": int(res.iterations[0]), "status": int(res.status[0]),
-            "converged": bool(res.converged[0]), "f": float(res.f[0]), "f_stored_reference_optimum": 7.841959196,
+            "solver": "Solver.IPOPT(_max_iter=10000) (the reference script's call; the facade's Ipopt / bioptim profile)",
+            **head, "library_profile": out["library_profile"], "f_stored_reference_iterate": 7.841959196,
             "kkt_layout": {"chain_nodes": int(st["kkt_chain_nodes"]), "node_size": int(st["kkt_chain_sp"]),
                            "border": int(st["kkt_border"]), "kkt_unknowns": int(st["kkt_n"])},
-            "s_per_iteration": res.wall_time / max(1, int(res.iterations[0])),
-            "reference_time_to_optimize_s": ref_t, "reference_over_product": ref_t / res.wall_time,
-            "note": "reference timing on unknown hardware with an older revision (use_sx=False); stated as context"}
+            "reference_time_to_optimize_s": ref_t,
+            "note": "reference timing on unknown hardware with an older revision (use_sx=False), ending at its max_iter "
+                    "(tests/test_reaching_termination.py); stated as context"}
 
 
 def main():

@@ -979,7 +979,7 @@ class BatchedIpm:
                 stopped = stopped | rstop
                 # after the phase: zero constraint multipliers (Ipopt's constr_mult_reset_threshold = 0 ignores the
                 # least-squares estimate) and a fresh filter (measured: cfg 5 from 16 perturbed starts converges
-                # 13 / 16 with it against 9 / 16 keeping the augmented filter, scripts/r3/resto_variants.py)
+                # 13 / 16 with it against 9 / 16 keeping the augmented filter; round-3 probe, in git history at 4131d45)
                 y = torch.where(back[:, None], torch.zeros_like(y), y)
                 filt = torch.where(back[:, None, None], torch.tensor([np.inf, -np.inf], dtype=torch.float64,
                                                                      device=self.dev), filt)

@@ -34,6 +34,8 @@ ap.add_argument("--soft", type=float, default=None, help="soft_resto_pderror_red
 ap.add_argument("--restart", action="store_true", help="resto_failure_restart (extension: a failed phase restarts)")
 ap.add_argument("--opt", action="append", default=[], help="extra IpmOptions key=value (repeatable)")
 ap.add_argument("--label", default="")
+ap.add_argument("--profile", default="cfx", choices=["cfx", "ipopt"],
+                help="ipopt: the facade's Ipopt / bioptim profile (IpmOptions.ipopt) under the options above")
 args = ap.parse_args()
 
 ocp = bench.msk_build(5)
@@ -53,14 +55,17 @@ for B, amp in runs:
         k, val = kv.split("=", 1)
         cur = getattr(IpmOptions, k)
         extra[k] = type(cur)(val) if not isinstance(cur, bool) else val.lower() in ("1", "true", "yes")
-    opts = IpmOptions(tol=1e-6, max_iter=args.max_iter, max_wall_time=args.wall, print_frequency_time=20.0, **extra)
+    base = dict(tol=1e-6, max_iter=args.max_iter, max_wall_time=args.wall, print_frequency_time=20.0, **extra)
+    opts = IpmOptions.ipopt(**base) if args.profile == "ipopt" else IpmOptions(**base)
     ipm = cls(ocp, batch=B, options=opts)
     res = ipm.solve(v0)
     st = dict(getattr(ipm, "last_stats", {}) or {})
     ipm.close()
     hist = collections.Counter(IPM_STATUS.get(int(s), str(s)) for s in res.status)
     conv = res.converged.astype(bool)
-    rec = dict(label=args.label, options={k: v for k, v in extra.items()}, solver=cls.__name__, batch=B, amp=amp, max_iter=args.max_iter, wall_s=round(res.wall_time, 3),
+    rec = dict(label=args.label, profile=args.profile, mu_strategy=opts.mu_strategy,
+               mu_mode_switches=st.get("mu_mode_switches"),
+               options={k: v for k, v in extra.items()}, solver=cls.__name__, batch=B, amp=amp, max_iter=args.max_iter, wall_s=round(res.wall_time, 3),
                converged=int(conv.sum()), status=dict(hist), iterations_median=float(np.median(res.iterations)),
                iterations_max=int(res.iterations.max()), f_converged_min=float(res.f[conv].min()) if conv.any() else None,
                f_converged_max=float(res.f[conv].max()) if conv.any() else None,

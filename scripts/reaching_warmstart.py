@@ -71,6 +71,9 @@ ap.add_argument("--mu-strategy", default=None, choices=["monotone", "adaptive"],
 ap.add_argument("--trace", action="store_true", help="CFX_IPM_TRACE=1 (one stderr line per iteration)")
 ap.add_argument("--hessian", default=None, choices=["exact", "limited-memory"], help="Ipopt's hessian_approximation")
 ap.add_argument("--lm-history", type=int, default=None, help="limited_memory_max_history")
+ap.add_argument("--n-shooting", type=int, default=None,
+                help="a coarser grid of the same task (a multiple of 60; from the reference start only, no comparison "
+                     "with the stored optimum)")
 ap.add_argument("--current", action="store_true",
                 help="today's calcium conventions and per-interval widths instead of the stored revision's")
 args = ap.parse_args()
@@ -194,5 +197,37 @@ def run(objective):
             fh.write(line + "\n")
 
 
+def run_coarse(objective):
+    """The task on a coarser grid (legacy conventions), from the product's initial guess."""
+    from cocofest_amd.solver import IpmOptions, NativeIpm
+
+    ocp = R.legacy_product(objective, n_shooting=args.n_shooting)
+    base = dict(tol=args.tol, max_iter=args.max_iter, max_wall_time=args.wall, print_frequency_time=30.0)
+    kw = {**(IpmOptions.IPOPT_PROFILE if args.profile == "ipopt" else {}), **base}
+    if args.mu_strategy:
+        kw["mu_strategy"] = args.mu_strategy
+    if args.hessian:
+        kw["hessian_approximation"] = args.hessian
+    ipm = NativeIpm(ocp, batch=1, options=IpmOptions(**kw))
+    t1 = time.perf_counter()
+    res = ipm.solve()
+    t2 = time.perf_counter()
+    st = dict(ipm.last_stats)
+    ipm.close()
+    h = ocp.nlp(batch=1, layout="aos")
+    g1 = h.eval_g(res.v)[0]
+    h.close()
+    out = {"objective": objective, "n_shooting": args.n_shooting, "profile": args.profile,
+           "mu_strategy": kw.get("mu_strategy", "monotone"), "status": int(res.status[0]),
+           "iterations": int(res.iterations[0]), "solve_wall_s": t2 - t1, "f_end": float(res.f[0]),
+           "g_end_max": float(np.abs(g1).max()), "resto_phases": int(st.get("resto_phases", 0)),
+           "mu_mode_switches": int(st.get("mu_mode_switches", 0)), "kkt_chain_nodes": st.get("kkt_chain_nodes")}
+    line = json.dumps(out)
+    print(line, flush=True)
+    if args.out:
+        with open(args.out, "a") as fh:
+            fh.write(line + "\n")
+
+
 for obj in args.objectives.replace("+", ",").split(","):
-    run(obj)
+    run_coarse(obj) if args.n_shooting else run(obj)

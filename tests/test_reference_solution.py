@@ -245,10 +245,11 @@ def test_reference_optimum_is_stationary_in_the_pulse_widths(objective):
     assert all(np.isfinite(r["nu"]))
 
 
-def legacy_product(objective="fatigue", per_pulse=True, pulse_bounds="all"):
+def legacy_product(objective="fatigue", per_pulse=True, pulse_bounds="all", n_shooting=None):
     """The product's OcpFesMsk for the stored revision: FesMskModel(legacy_calcium=True) (CFX_MSK_LEGACY_CALCIUM),
     its fatigue rates, pulse widths per pulse (pulse_width["per_pulse"], CFX_MSK_PULSE_WIDTH_PER_PULSE), no residual
-    torque (the script's with_residual_torque=False), the hand on the target at node 1000."""
+    torque (the script's with_residual_torque=False), the hand on the target at node 1000 (at t = 1 s: node
+    n_shooting * 2 / 3 on a coarser grid of ``n_shooting`` intervals, a multiple of 60)."""
     import cocofest_amd as C
 
     models = []
@@ -262,8 +263,8 @@ def legacy_product(objective="fatigue", per_pulse=True, pulse_bounds="all"):
                           activate_residual_torque=False, legacy_calcium=True)
     cl = C.ConstraintList()
     cl.add(C.ConstraintFcn.SUPERIMPOSE_MARKERS, first_marker="COM_hand", second_marker="reaching_target", phase=0,
-           node=MARKER_NODE, axes=[C.Axis.X, C.Axis.Y])
-    return C.OcpFesMsk.prepare_ocp(model=model, final_time=FINAL_TIME, n_shooting=N,
+           node=MARKER_NODE if n_shooting is None else (2 * n_shooting) // 3, axes=[C.Axis.X, C.Axis.Y])
+    return C.OcpFesMsk.prepare_ocp(model=model, final_time=FINAL_TIME, n_shooting=n_shooting or N,
                                    pulse_width={"min": O.model_constants("ding2007")["pd0"], "max": 0.0006,
                                                 "per_pulse": per_pulse, "per_pulse_bounds": pulse_bounds},
                                    objective={f"minimize_muscle_{objective}": True},
