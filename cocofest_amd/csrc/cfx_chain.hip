@@ -97,49 +97,57 @@ __device__ __forceinline__ void store_tile(double* __restrict__ C, int I, int J,
     for (int r = 0; r < 4; ++r) C[(16 * I + (lane >> 4) + 4 * r) * SP + 16 * J + (lane & 15)] = v[r];
 }
 
-// Maximum of v over the 64 lanes (every lane gets it): DPP max-scan within rows of 16 lanes, row broadcasts to
-// lane 63, readlane.  Lanes a shift leaves without a source keep their own value.
-#define CFX_DPP_MAX(v, CTRL, RM, BM)                                                                              \
-    do {                                                                                                          \
-        const int lo_ = __double2loint(v), hi_ = __double2hiint(v);                                               \
-        const int slo_ = __builtin_amdgcn_update_dpp(lo_, lo_, CTRL, RM, BM, false);                              \
-        const int shi_ = __builtin_amdgcn_update_dpp(hi_, hi_, CTRL, RM, BM, false);                              \
-        v = fmax(v, __hiloint2double(shi_, slo_));                                                                \
+// Maximum of a 32-bit integer over the 64 lanes (every lane gets it): DPP max-scan within rows of 16 lanes, row
+// broadcasts to lane 63, readlane; lanes a shift leaves without a source keep their own value.  (Round 5 reduced a
+// 64-bit |v| key: two DPP moves and an FP64 max per step.)
+#define CFX_DPP_IMAX(v, CTRL, RM, BM)                                                        \
+    do {                                                                                    \
+        const int s_ = __builtin_amdgcn_update_dpp(v, v, CTRL, RM, BM, false);               \
+        v = v > s_ ? v : s_;                                                                \
     } while (0)
-__device__ __forceinline__ double wave_max(double v) {
-    CFX_DPP_MAX(v, 0x111, 0xf, 0xf);  // row_shr:1
-    CFX_DPP_MAX(v, 0x112, 0xf, 0xf);  // row_shr:2
-    CFX_DPP_MAX(v, 0x114, 0xf, 0xf);  // row_shr:4
-    CFX_DPP_MAX(v, 0x118, 0xf, 0xf);  // row_shr:8  (lane 15 of each row: the row's maximum)
-    CFX_DPP_MAX(v, 0x142, 0xa, 0xf);  // row_bcast:15 into rows 1 and 3
-    CFX_DPP_MAX(v, 0x143, 0xc, 0xf);  // row_bcast:31 into rows 2 and 3 (lane 63: the wave's maximum)
-    const int lo = __builtin_amdgcn_readlane(__double2loint(v), 63), hi = __builtin_amdgcn_readlane(__double2hiint(v), 63);
-    return __hiloint2double(hi, lo);
+__device__ __forceinline__ int wave_imax(int v) {
+    CFX_DPP_IMAX(v, 0x111, 0xf, 0xf);  // row_shr:1
+    CFX_DPP_IMAX(v, 0x112, 0xf, 0xf);  // row_shr:2
+    CFX_DPP_IMAX(v, 0x114, 0xf, 0xf);  // row_shr:4
+    CFX_DPP_IMAX(v, 0x118, 0xf, 0xf);  // row_shr:8
+    CFX_DPP_IMAX(v, 0x142, 0xa, 0xf);  // row_bcast:15
+    CFX_DPP_IMAX(v, 0x143, 0xc, 0xf);  // row_bcast:31
+    return __builtin_amdgcn_readlane(v, 63);
+}
+
+// 32-bit pivot key of a candidate row r with value v: the high word of |v| (sign, exponent, 20 mantissa bits; ordered
+// like |v| for finite values) with its 7 low bits replaced by 127 - r; -1 for a non-finite value.  The maximum picks the
+// largest |v| to within 2^-13 relative (threshold pivoting at 0.9999), ties to the lowest row.
+__device__ __forceinline__ int pivot_key(double v, int r) {
+    const int hi = __double2hiint(v) & 0x7fffffff;
+    return hi >= 0x7ff00000 ? -1 : ((hi & ~0x7f) | (127 - r));
 }
 
 constexpr int kNT = 256;  // threads per workgroup (4 waves)
+
+__device__ __forceinline__ double readlane_d(double v, int l) {
+    return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), l), __builtin_amdgcn_readlane(__double2loint(v), l));
+}
 
 // Eliminate nodes i = first + step * blockIdx.x (instance blockIdx.y): D_i <- D_i^-1, L_i <- D_i^-1 L_i (when node
 // i - h exists), U_i <- D_i^-1 U_i (when node i + h exists).  A zero pivot sets info[b] (0-based slot + 1) if unset.
 template <int SP>
 __global__ void __launch_bounds__(kNT) k_chain_elim(Chain C, int first, int step, int h, int32_t* __restrict__ info) {
-    // In-place Gauss-Jordan with partial pivoting (largest |A(r, k)| over the rows not yet pivots, ties to the lowest
-    // row) without moving rows: step k pivots on physical row P_k, which is logical row k, so the array ends as
-    // (Q D)^-1 = D^-1 Q^T with Q the row order P, i.e. D^-1[k][j] = array[P_k][s_j], s_j the step at which row j was
-    // pivot (undone through LDS at the end).  The matrix sits in registers as 16 x 16 interleaved tiles: thread
-    // t = 16 tr + tc owns rows tr + 16 i and columns tc + 16 j (i, j < T = SP / 16), so a rank-1 step reads T
-    // multipliers and T pivot-row values from LDS for its T^2 entries, and every entry takes the same two multiplies
-    // and one FMA (selects per entry cost more than the arithmetic; the row-per-thread layout with explicit row swaps
-    // took 205 us per 80 x 80 block, this one ...).  Per pivot column: every wave finds the pivot itself (one 64-bit
-    // key per row, DPP max reduction, no barrier), the owners of row p stage it in LDS, barrier, every thread updates
-    // its tile and the owners of column k + 1 stage that column for the next step, barrier.
+    // Blocked in-place Gauss-Jordan with partial pivoting (largest |A(r, k)| over the rows not yet pivots, to within
+    // pivot_key's 2^-13, ties to the lowest row) without moving rows: step k pivots on physical row P_k, so the array
+    // ends as (Q D)^-1 = D^-1 Q^T, D^-1[k][j] = array[P_k][s_j] with s_j the step at which row j was pivot (undone at the
+    // end).  The matrix sits in LDS; the SP columns go in panels of 16.  Panel j: wavefront 0 runs its 16 pivot steps
+    // on the panel's columns alone, in registers (lane l holds rows l and l + 64; DPP pivot search, the pivot row by
+    // readlane, no LDS and no barrier per step).  The composite of the 16 steps acts on every other column as
+    // M <- Z + W V, W the processed panel columns (SP x 16), V the 16 pivot rows before the panel, Z the column with
+    // those rows zeroed — a rank-16 update on v_mfma_f64_16x16x4f64, each wave owning whole 16-column blocks (it reads
+    // V of its blocks before writing them: no barrier between).  Two barriers per panel instead of two per column
+    // (round 5's column-by-column version, register tiles: 83 us per 80 x 80 block, issue- and barrier-bound).
     constexpr int T = SP / 16;
-    static_assert(SP % 16 == 0 && SP <= 128 && kNT == 256, "16 x 16 thread tiles; 7-bit row index in the pivot key");
-    __shared__ double A[SP][SP + 1];
-    __shared__ double colv[2][SP];
-    __shared__ double rowp[SP];
-    // P_k (row pivoted at step k), s_j (step at which row j was pivot); bytes, so that three workgroups' LDS fit a CU
-    // at SP = 80 with the allocation granularity
+    static_assert(SP % 16 == 0 && SP <= 128 && kNT == 256, "16-column panels; 7-bit row index in the pivot key");
+    constexpr int LDA = SP + 1;
+    __shared__ double A[SP * LDA];
+    // P_k (row pivoted at step k), s_j (step at which row j was pivot); bytes
     __shared__ uint8_t prow[SP], pstep[SP];
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
     const int i = first + step * blockIdx.x;
@@ -147,123 +155,119 @@ __global__ void __launch_bounds__(kNT) k_chain_elim(Chain C, int first, int step
     if (i >= C.M) return;
     constexpr int64_t NB = (int64_t)SP * SP;
     double* D = C.D + b * C.stride + i * NB;
+    for (int e = t; e < SP * SP; e += kNT) A[(e / SP) * LDA + e % SP] = D[e];
+    for (int r = t; r < SP; r += kNT) pstep[r] = 255;
+    __syncthreads();
+    int sing = 0;                       // (wave 0)
+    bool used0 = false, used1 = false;  // (wave 0) rows lane and lane + 64 already pivots
+    const bool has0 = lane < SP, has1 = lane + 64 < SP;
+#pragma unroll 1
+    for (int j = 0; j < T; ++j) {
+        if (wave == 0) {
+            double a0[16], a1[16];
+#pragma unroll
+            for (int c = 0; c < 16; ++c) {
+                a0[c] = has0 ? A[lane * LDA + 16 * j + c] : 0.0;
+                a1[c] = has1 ? A[(lane + 64) * LDA + 16 * j + c] : 0.0;
+            }
+#pragma unroll
+            for (int kk = 0; kk < 16; ++kk) {
+                const int k = 16 * j + kk;
+                int key = -1;
+                if (has0 && !used0) key = pivot_key(a0[kk], lane);
+                if (has1 && !used1) {
+                    const int k1 = pivot_key(a1[kk], lane + 64);
+                    key = key > k1 ? key : k1;
+                }
+                key = wave_imax(key);
+                int p;
+                if (key >= 0) {
+                    p = 127 - (key & 0x7f);
+                } else {  // no finite candidate: singular; the lowest unused row keeps the indices in range
+                    const unsigned long long m0 = __ballot(has0 && !used0), m1 = __ballot(has1 && !used1);
+                    p = m0 ? __ffsll((long long)m0) - 1 : 64 + __ffsll((long long)m1) - 1;
+                    if (!sing) sing = k + 1;
+                }
+                used0 = used0 || p == lane;
+                used1 = used1 || p == lane + 64;
+                if (lane == 0) prow[k] = (uint8_t)p, pstep[p] = (uint8_t)k;
+                double prv[16];  // the pivot row's panel values (wave-uniform)
+                if (p < 64) {
+#pragma unroll
+                    for (int c = 0; c < 16; ++c) prv[c] = readlane_d(a0[c], p);
+                } else {
+#pragma unroll
+                    for (int c = 0; c < 16; ++c) prv[c] = readlane_d(a1[c], p - 64);
+                }
+                const double pv = prv[kk];
+                if (pv == 0.0 && !sing) sing = k + 1;
+                const double inv = pv != 0.0 ? 1.0 / pv : 0.0;
+                double sc[16];  // the scaled pivot row, column k replaced by 1 / pv
+#pragma unroll
+                for (int c = 0; c < 16; ++c) sc[c] = c == kk ? inv : prv[c] * inv;
+                // every row r -= A(r, k) x the scaled pivot row; column k -> -A(r, k) / pv; row p -> the scaled row
+                const bool ip0 = lane == p, ip1 = lane + 64 == p;
+                const double m0 = a0[kk], m1 = a1[kk];
+#pragma unroll
+                for (int c = 0; c < 16; ++c) {
+                    if (c == kk) continue;
+                    a0[c] = ip0 ? sc[c] : fma(-m0, sc[c], a0[c]);
+                    a1[c] = ip1 ? sc[c] : fma(-m1, sc[c], a1[c]);
+                }
+                a0[kk] = ip0 ? inv : -m0 * inv;
+                a1[kk] = ip1 ? inv : -m1 * inv;
+            }
+#pragma unroll
+            for (int c = 0; c < 16; ++c) {
+                if (has0) A[lane * LDA + 16 * j + c] = a0[c];
+                if (has1) A[(lane + 64) * LDA + 16 * j + c] = a1[c];
+            }
+        }
+        __syncthreads();
+        // the other column blocks: M <- Z + W V (wave w: blocks w, w + 4, ... other than j)
+        for (int q = wave; q < T - 1; q += kNT / 64) {
+            const int Jc = q < j ? q : q + 1;
+            double breg[4];  // V[4 kk + lane / 16][16 Jc + lane % 16]: pivot row of step 16 j + 4 kk + lane / 16
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk) breg[kk] = A[prow[16 * j + 4 * kk + (lane >> 4)] * LDA + 16 * Jc + (lane & 15)];
+#pragma unroll 1
+            for (int I = 0; I < T; ++I) {
+                d4 acc;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int row = 16 * I + (lane >> 4) + 4 * r;
+                    const int ps = pstep[row];
+                    const bool piv = ps >= 16 * j && ps < 16 * j + 16;  // a pivot row of this panel: zeroed (Z)
+                    acc[r] = piv ? 0.0 : A[row * LDA + 16 * Jc + (lane & 15)];
+                }
+#pragma unroll
+                for (int kk = 0; kk < 4; ++kk)
+                    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(A[(16 * I + (lane & 15)) * LDA + 16 * j + 4 * kk + (lane >> 4)],
+                                                               breg[kk], acc, 0, 0, 0);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) A[(16 * I + (lane >> 4) + 4 * r) * LDA + 16 * Jc + (lane & 15)] = acc[r];
+            }
+        }
+        __syncthreads();
+    }
+    // D^-1[r][c] = array[P_r][s_c]
     const int tr = t >> 4, tc = t & 15;
     double a[T][T];
 #pragma unroll
     for (int ii = 0; ii < T; ++ii)
 #pragma unroll
-        for (int jj = 0; jj < T; ++jj) a[ii][jj] = D[(int64_t)(tr + 16 * ii) * SP + tc + 16 * jj];
-    if (tc == 0) {
-#pragma unroll
-        for (int ii = 0; ii < T; ++ii) colv[0][tr + 16 * ii] = a[ii][0];  // column 0
-    }
-    __syncthreads();
-    int sing = 0;
-    bool used0 = false, used1 = false;  // rows lane and lane + 64 already pivots (every wave tracks them)
-#pragma unroll 1
-    for (int k = 0; k < SP; ++k) {
-        const int par = k & 1;
-        // pivot search: key = |v| with its 7 low mantissa bits replaced by 127 - r (the order of non-negative doubles
-        // is the order of their bits), -1 for rows already pivots; the wave maximum is the largest |v|, ties to the
-        // lowest r
-        double key = -1.0;
-        const double v0 = lane < SP ? colv[par][lane] : 0.0, v1 = lane + 64 < SP ? colv[par][lane + 64] : 0.0;
-        double fcol[T];  // this thread's rows of column k (issued with the pivot search's reads)
-#pragma unroll
-        for (int ii = 0; ii < T; ++ii) fcol[ii] = colv[par][tr + 16 * ii];
-        if (lane < SP && !used0) {
-            const uint64_t bits = (uint64_t)__double_as_longlong(fabs(v0));
-            key = __longlong_as_double((long long)((bits & ~0x7Full) | (uint64_t)(127 - lane)));
-        }
-        if (lane + 64 < SP && !used1) {
-            const uint64_t bits = (uint64_t)__double_as_longlong(fabs(v1));
-            key = fmax(key, __longlong_as_double((long long)((bits & ~0x7Full) | (uint64_t)(63 - lane))));
-        }
-        key = wave_max(key);
-        int p = 127 - (int)((uint64_t)__double_as_longlong(key) & 0x7Full);
-        if (!(key >= 0.0)) {  // (wave-uniform) no finite candidate — every unused row NaN / Inf: singular; the lowest
-                              // unused row keeps the indices in range
-            const unsigned long long m0 = __ballot(lane < SP && !used0), m1 = __ballot(lane + 64 < SP && !used1);
-            p = m0 ? __ffsll((long long)m0) - 1 : 64 + __ffsll((long long)m1) - 1;
-            if (!sing) sing = k + 1;
-        }
-        used0 = used0 || p == lane;
-        used1 = used1 || p == lane + 64;
-        if (t == 0) prow[k] = (uint8_t)p, pstep[p] = (uint8_t)k;
-        const double pvl = p < 64 ? v0 : v1;  // the pivot value, from the lane that holds it
-        const int pl = p & 63;
-        const double pv = __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(pvl), pl),
-                                           __builtin_amdgcn_readlane(__double2loint(pvl), pl));
-        if (pv == 0.0 && !sing) sing = k + 1;
-        const double inv = pv != 0.0 ? 1.0 / pv : 0.0;
-        // row p to LDS (its owners: tr == p % 16).  ip, k and every tile index are wave-uniform: the branches below
-        // pick a register statically instead of a select chain over the tile (measured: the chains cost 30 of 92 us)
-        const int ip = p >> 4;
-#pragma unroll
-        for (int ii = 0; ii < T; ++ii)
-            if (ii == ip && tr == (p & 15)) {
-#pragma unroll
-                for (int jj = 0; jj < T; ++jj) rowp[tc + 16 * jj] = a[ii][jj];
-            }
-        __syncthreads();
-        // every row r -= A(r, k) x the scaled pivot row; then column k becomes -A(r, k) / pv and row p the scaled
-        // pivot row (column k: 1 / pv)
-        double prc[T];
-#pragma unroll
-        for (int jj = 0; jj < T; ++jj) {
-            const int c = tc + 16 * jj;
-            prc[jj] = (c == k ? 1.0 : rowp[c]) * inv;
-        }
-#pragma unroll
-        for (int ii = 0; ii < T; ++ii)
-#pragma unroll
-            for (int jj = 0; jj < T; ++jj) a[ii][jj] = fma(-fcol[ii], prc[jj], a[ii][jj]);
-        const int jk = k >> 4;
-#pragma unroll
-        for (int jj = 0; jj < T; ++jj)
-            if (jj == jk) {
-                const bool own = tc == (k & 15);
-#pragma unroll
-                for (int ii = 0; ii < T; ++ii) a[ii][jj] = own ? -fcol[ii] * prc[jj] : a[ii][jj];
-            }
-#pragma unroll
-        for (int ii = 0; ii < T; ++ii)
-            if (ii == ip) {
-                const bool own = tr == (p & 15);
-#pragma unroll
-                for (int jj = 0; jj < T; ++jj) a[ii][jj] = own ? prc[jj] : a[ii][jj];
-            }
-        // the next pivot column, by its owners, into the other buffer
-        const int kn = k + 1, jn = kn >> 4;
-#pragma unroll
-        for (int jj = 0; jj < T; ++jj)
-            if (jj == jn && kn < SP && tc == (kn & 15)) {
-#pragma unroll
-                for (int ii = 0; ii < T; ++ii) colv[par ^ 1][tr + 16 * ii] = a[ii][jj];
-            }
-        __syncthreads();
-    }
-    // D^-1[r][c] = array[P_r][s_c]
-#pragma unroll
-    for (int ii = 0; ii < T; ++ii)
-#pragma unroll
-        for (int jj = 0; jj < T; ++jj) A[tr + 16 * ii][tc + 16 * jj] = a[ii][jj];
+        for (int jj = 0; jj < T; ++jj) a[ii][jj] = A[prow[tr + 16 * ii] * LDA + pstep[tc + 16 * jj]];
     __syncthreads();
 #pragma unroll
     for (int ii = 0; ii < T; ++ii)
 #pragma unroll
-        for (int jj = 0; jj < T; ++jj) a[ii][jj] = A[prow[tr + 16 * ii]][pstep[tc + 16 * jj]];
-    __syncthreads();
-#pragma unroll
-    for (int ii = 0; ii < T; ++ii)
-#pragma unroll
-        for (int jj = 0; jj < T; ++jj) A[tr + 16 * ii][tc + 16 * jj] = a[ii][jj];
+        for (int jj = 0; jj < T; ++jj) A[(tr + 16 * ii) * LDA + tc + 16 * jj] = a[ii][jj];
     __syncthreads();
     if (t == 0 && sing && info && info[b] == 0) info[b] = (int32_t)(i * SP + sing);
-    for (int e = t; e < SP * SP; e += kNT) D[e] = A[e / SP][e % SP];
+    for (int e = t; e < SP * SP; e += kNT) D[e] = A[(e / SP) * LDA + e % SP];
     // X_i = D_i^-1 L_i, Y_i = D_i^-1 U_i in place: items (side, column block J) over the waves, each read into
     // registers before its tiles are stored
-    auto a_at = [&](int r, int c) { return A[r][c]; };
+    auto a_at = [&](int r, int c) { return A[r * LDA + c]; };
     const bool xl = i - h >= 0, yu = i + h < C.M;
     for (int it = wave; it < 2 * (SP / 16); it += kNT / 64) {
         const int side = it / (SP / 16), J = it % (SP / 16);
