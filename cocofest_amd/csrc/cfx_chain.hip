@@ -97,30 +97,34 @@ __device__ __forceinline__ void store_tile(double* __restrict__ C, int I, int J,
     for (int r = 0; r < 4; ++r) C[(16 * I + (lane >> 4) + 4 * r) * SP + 16 * J + (lane & 15)] = v[r];
 }
 
-// Maximum of a 32-bit integer over the 64 lanes (every lane gets it): DPP max-scan within rows of 16 lanes, row
-// broadcasts to lane 63, readlane; lanes a shift leaves without a source keep their own value.  (Round 5 reduced a
-// 64-bit |v| key: two DPP moves and an FP64 max per step.)
-#define CFX_DPP_IMAX(v, CTRL, RM, BM)                                                        \
-    do {                                                                                    \
-        const int s_ = __builtin_amdgcn_update_dpp(v, v, CTRL, RM, BM, false);               \
-        v = v > s_ ? v : s_;                                                                \
-    } while (0)
-__device__ __forceinline__ int wave_imax(int v) {
-    CFX_DPP_IMAX(v, 0x111, 0xf, 0xf);  // row_shr:1
-    CFX_DPP_IMAX(v, 0x112, 0xf, 0xf);  // row_shr:2
-    CFX_DPP_IMAX(v, 0x114, 0xf, 0xf);  // row_shr:4
-    CFX_DPP_IMAX(v, 0x118, 0xf, 0xf);  // row_shr:8
-    CFX_DPP_IMAX(v, 0x142, 0xa, 0xf);  // row_bcast:15
-    CFX_DPP_IMAX(v, 0x143, 0xc, 0xf);  // row_bcast:31
-    return __builtin_amdgcn_readlane(v, 63);
+// Pivot key of a candidate row r with value v: |v| with its 7 low mantissa bits replaced by 127 - r (non-negative
+// doubles order like their bits), -1 for a non-finite value.  The wave maximum picks the largest |v| (to 2^-45), ties
+// to the lowest row.  (A 32-bit key of the high word, 2^-13, took one instruction less per DPP step but moved the
+// reaching task's iteration path measurably; not kept.)
+__device__ __forceinline__ double pivot_key(double v, int r) {
+    const uint64_t bits = (uint64_t)__double_as_longlong(fabs(v));
+    if (bits >= 0x7ff0000000000000ull) return -1.0;
+    return __longlong_as_double((long long)((bits & ~0x7Full) | (uint64_t)(127 - r)));
 }
 
-// 32-bit pivot key of a candidate row r with value v: the high word of |v| (sign, exponent, 20 mantissa bits; ordered
-// like |v| for finite values) with its 7 low bits replaced by 127 - r; -1 for a non-finite value.  The maximum picks the
-// largest |v| to within 2^-13 relative (threshold pivoting at 0.9999), ties to the lowest row.
-__device__ __forceinline__ int pivot_key(double v, int r) {
-    const int hi = __double2hiint(v) & 0x7fffffff;
-    return hi >= 0x7ff00000 ? -1 : ((hi & ~0x7f) | (127 - r));
+// Maximum of v over the 64 lanes (every lane gets it): DPP max-scan within rows of 16 lanes, row broadcasts to lane 63,
+// readlane.  Lanes a shift leaves without a source keep their own value.
+#define CFX_DPP_MAX(v, CTRL, RM, BM)                                                                              \
+    do {                                                                                                          \
+        const int lo_ = __double2loint(v), hi_ = __double2hiint(v);                                               \
+        const int slo_ = __builtin_amdgcn_update_dpp(lo_, lo_, CTRL, RM, BM, false);                              \
+        const int shi_ = __builtin_amdgcn_update_dpp(hi_, hi_, CTRL, RM, BM, false);                              \
+        v = fmax(v, __hiloint2double(shi_, slo_));                                                                \
+    } while (0)
+__device__ __forceinline__ double wave_max(double v) {
+    CFX_DPP_MAX(v, 0x111, 0xf, 0xf);  // row_shr:1
+    CFX_DPP_MAX(v, 0x112, 0xf, 0xf);  // row_shr:2
+    CFX_DPP_MAX(v, 0x114, 0xf, 0xf);  // row_shr:4
+    CFX_DPP_MAX(v, 0x118, 0xf, 0xf);  // row_shr:8  (lane 15 of each row: the row's maximum)
+    CFX_DPP_MAX(v, 0x142, 0xa, 0xf);  // row_bcast:15 into rows 1 and 3
+    CFX_DPP_MAX(v, 0x143, 0xc, 0xf);  // row_bcast:31 into rows 2 and 3 (lane 63: the wave's maximum)
+    const int lo = __builtin_amdgcn_readlane(__double2loint(v), 63), hi = __builtin_amdgcn_readlane(__double2hiint(v), 63);
+    return __hiloint2double(hi, lo);
 }
 
 constexpr int kNT = 256;  // threads per workgroup (4 waves)
@@ -134,7 +138,7 @@ __device__ __forceinline__ double readlane_d(double v, int l) {
 template <int SP>
 __global__ void __launch_bounds__(kNT) k_chain_elim(Chain C, int first, int step, int h, int32_t* __restrict__ info) {
     // Blocked in-place Gauss-Jordan with partial pivoting (largest |A(r, k)| over the rows not yet pivots, to within
-    // pivot_key's 2^-13, ties to the lowest row) without moving rows: step k pivots on physical row P_k, so the array
+    // pivot_key's 2^-45, ties to the lowest row) without moving rows: step k pivots on physical row P_k, so the array
     // ends as (Q D)^-1 = D^-1 Q^T, D^-1[k][j] = array[P_k][s_j] with s_j the step at which row j was pivot (undone at the
     // end).  The matrix sits in LDS; the SP columns go in panels of 16.  Panel j: wavefront 0 runs its 16 pivot steps
     // on the panel's columns alone, in registers (lane l holds rows l and l + 64; DPP pivot search, the pivot row by
@@ -173,16 +177,13 @@ __global__ void __launch_bounds__(kNT) k_chain_elim(Chain C, int first, int step
 #pragma unroll
             for (int kk = 0; kk < 16; ++kk) {
                 const int k = 16 * j + kk;
-                int key = -1;
+                double key = -1.0;
                 if (has0 && !used0) key = pivot_key(a0[kk], lane);
-                if (has1 && !used1) {
-                    const int k1 = pivot_key(a1[kk], lane + 64);
-                    key = key > k1 ? key : k1;
-                }
-                key = wave_imax(key);
+                if (has1 && !used1) key = fmax(key, pivot_key(a1[kk], lane + 64));
+                key = wave_max(key);
                 int p;
-                if (key >= 0) {
-                    p = 127 - (key & 0x7f);
+                if (key >= 0.0) {
+                    p = 127 - (int)((uint64_t)__double_as_longlong(key) & 0x7Full);
                 } else {  // no finite candidate: singular; the lowest unused row keeps the indices in range
                     const unsigned long long m0 = __ballot(has0 && !used0), m1 = __ballot(has1 && !used1);
                     p = m0 ? __ffsll((long long)m0) - 1 : 64 + __ffsll((long long)m1) - 1;

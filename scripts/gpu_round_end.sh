@@ -1,6 +1,6 @@
 # Round-end check: every GPU test, smoke(), the default bench line.  Stops at the first failure or GPU fault.
 set -o pipefail
-out=gpurun_out/round_end
+out=gpurun_out/${1:-round_end}
 mkdir -p $out
 check() { if grep -q "HSA_STATUS_ERROR" $1; then echo "GPU fault in $1"; exit 3; fi; }
 timeout -k 10 1000 python -u -m pytest -q --tb=short -m gpu --timeout 300 --timeout-method thread tests > $out/pytest.log 2>&1; rc=$?; check $out/pytest.log; tail -5 $out/pytest.log; [ $rc -eq 0 ] || exit $rc

@@ -185,7 +185,7 @@ def run(objective):
            "resto_phases": int(st.get("resto_phases", 0)), "kkt_chain_nodes": st.get("kkt_chain_nodes"),
            "kkt_n": st.get("kkt_n"), "s_per_iteration": (t2 - t1) / max(1, int(res.iterations[0])),
            "reference_time_to_optimize_s": float(d["time_to_optimize"]), "pulse_bounds": args.pulse_bounds,
-           "profile": args.profile, "mu_mode_switches": int(st.get("mu_mode_switches", 0)),
+           "profile": args.profile, "mu_mode_switches": int(st.get("mu_mode_switches", 0)), "lib": os.environ.get("CFX_LIB", "libcfx.so"),
            **{k: kw[k] for k in kw if k != "tol"},
            **rep}
     if args.out:  # the end point, for a later look
