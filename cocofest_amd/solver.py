@@ -995,7 +995,14 @@ class BatchedIpm:
                 alpha = torch.where(soft_acc, a_s, alpha)  # the soft step moves y (and z, below) by the same step
             step = (~done)
             alpha = torch.where(step, alpha, torch.zeros_like(alpha))
-            if opt.verbose:
+            if opt.verbose:  # (and the variable whose bound cuts the primal step most: fraction to the boundary)
+                rl = torch.where(hasL & (dx < 0), -tau[:, None] * sl / dx, torch.full_like(dx, np.inf))
+                ru = torch.where(hasU & (dx > 0), tau[:, None] * su / dx, torch.full_like(dx, np.inf))
+                rr = torch.minimum(rl, ru)[0]
+                jb = int(rr.argmin())
+                print(f"    blocking v[{int(self.free[jb])}] ({'lower' if bool(rl[0, jb] <= ru[0, jb]) else 'upper'}) "
+                      f"ratio {float(rr[jb]):.2e} x {float(x[0, jb] * self.d[jb]):.4e} dx {float(dx[0, jb] * self.d[jb]):.3e}; "
+                      f"ratios < 1e-2: {int((rr < 1e-2).sum())}")
                 print(f"it {it:3d} f {float(f[0]):.6e} err {float(err0[0]):.3e} e_d {float(e_d[0]):.2e} "
                       f"e_p {float(e_p[0]):.2e} mu {float(mu[0]):.1e} alpha {float(alpha[0]):.2e} "
                       f"a_p {float(a_p[0]):.2e} dw {float(dw[0]):.1e} "
