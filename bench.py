@@ -115,8 +115,9 @@ FP64_FMA_ISSUE_PEAK = 5.18e11  # wave-instr/s, measured (profiles/round1/micro_f
 
 
 def msk_pmc():
-    """VALU wave-instructions per cfg-5 g + J_g step (k_msk_values + k_msk_stagecoef_par + k_msk_tangents_lds,
-    B = 65,536) from the committed rocprofv3 SQ pass (profiles/msk_pmc.json; the round-3 driver scripts/r3/gpu_msk_prof.sh is in git history at 4131d45), if any."""
+    """HBM bytes and VALU wave-instructions per cfg-5 g + J_g step (k_msk_values + k_msk_stage_tangents at B = 65,536)
+    from the committed rocprofv3 passes (profiles/msk_pmc.json, written by scripts/summarize_msk_pmc.py from
+    scripts/gpu_msk_pmc.sh), if any."""
     f = ROOT / "profiles" / "msk_pmc.json"
     if not f.exists():
         return None

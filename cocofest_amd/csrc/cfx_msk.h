@@ -19,6 +19,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include <type_traits>
 
 #include "cfx_dual.h"
@@ -1864,6 +1866,167 @@ k_msk_stagecoef_split(const MskParams P, const MskGeom* __restrict__ GG,
     double* Ws = P.scratch + kq * NC * B + b;
     if (blockIdx.y == 0) msk_stage_half<NQ, NM, FAM, 0>(G, P.residual, xs, u, Ws, B);
     else msk_stage_half<NQ, NM, FAM, 1>(G, P.residual, xs, u, Ws, B);
+}
+
+// g + J_g's stage coefficients and tangent columns in one launch (k_msk_stagecoef_par followed by k_msk_tangents_lds,
+// without the coefficients' round trip through HBM: 1.1 GB written and 0.76 GB read back per cfg-5 call at B = 65,536,
+// and the tangent blocks' waits at every hand-off).  Block = TW instances x ki consecutive intervals, 256 threads:
+//   phase A: thread = (instance, interval, stage) task, msk_stage from the stage inputs XS into LDS sW[ki][Q][NC][TW]
+//            (the stage kernel's expression, so the coefficients are the same numbers);
+//   phase B: thread = (instance, CPT columns), the RK recursion of each column through the LDS coefficients — every
+//            coefficient read from LDS once per stage for all the thread's columns (they share the instance).
+// The stage body sets the register allocation (one wave per SIMD, as the stage kernel runs), so a 256-thread block
+// covers TW x nz <= 16 TW (instance, column) pairs with CPT = TW / 16 columns per thread: TW = 32 where one interval's
+// coefficients fit in LDS at 32 instances, else TW = 16 (RK4 x 5: 20 stages x 36 coefficients x 32 x 8 B = 184 KB).
+// keep: the coefficients are also stored to P.scratch (the interior point's Hessian at the same point reuses them,
+// cfx_api.hip msk_stash).
+constexpr int kMskFusedThreads = 256;
+constexpr size_t kMskFusedMaxLds = 160 * 1024;
+
+template <int NQ, int NM, int FAM>
+__device__ __forceinline__ void msk_stage_task(const MskParams& P, const MskGeom& G, const double* __restrict__ V,
+                                               const double* __restrict__ XS, int64_t b, int64_t kq,
+                                               double* __restrict__ Ws, int64_t ws) {
+    constexpr int NXM = msk_nxm<FAM>(), NX = NM * NXM + 2 * NQ;
+    constexpr int NUMAX = msk_numax<NQ, NM, FAM>();
+    const int64_t B = P.B;
+    const int k = (int)(kq / P.Q);
+    const int64_t zb = (int64_t)k * P.nz;
+    double xs[NX], u[NUMAX], f[NX], csl[NM];
+#pragma unroll
+    for (int r = 0; r < NX; ++r) xs[r] = XS[(kq * NX + r) * B + b];
+#pragma unroll
+    for (int i = 0; i < NUMAX; ++i) {
+        const int dc = msk_udec<NM, FAM>(i, P.T, P.nu);
+        u[i] = dc >= 0 ? V[(zb + NX + dc) * B + b] : 0.0;
+    }
+    if constexpr (msk_hmed<FAM>()) {  // cs enters f only, which is not used here
+#pragma unroll
+        for (int mu = 0; mu < NM; ++mu) csl[mu] = 0.0;
+    } else {
+        msk_stage_cs<NM, FAM>(P.cs, kq, nullptr, csl);
+    }
+    msk_stage<NQ, NM, FAM>(G, P.residual, csl, msk_cs1<NM>(P, kq), xs, u, f, Ws, ws);
+}
+
+template <int NQ, int NM, int FAM, int SCHEME, int TW>
+__global__ void __launch_bounds__(kMskFusedThreads) k_msk_stage_tangents(const MskParams P, const MskGeom* __restrict__ GG,
+                                                                        const double* __restrict__ V,
+                                                                        const double* __restrict__ XS,
+                                                                        double* __restrict__ J, int ki, int keep) {
+    constexpr int NXM = msk_nxm<FAM>(), NX = NM * NXM + 2 * NQ;
+    constexpr int NUMAX = msk_numax<NQ, NM, FAM>();
+    constexpr int NC = msk_ncoef<NQ, NM>();
+    constexpr int ST = SCHEME == 4 ? 4 : (SCHEME == 2 ? 2 : 1);
+    constexpr int CPT = TW * kMskLdsCols / kMskFusedThreads;
+    static_assert(CPT >= 1 && TW * kMskLdsCols == CPT * kMskFusedThreads, "phase B: CPT columns per thread");
+    extern __shared__ double sW[];  // [ki][Q][NC][TW]
+    const int64_t B = P.B;
+    const int nz = P.nz, Q = P.Q;
+    const int64_t b0 = (int64_t)blockIdx.x * TW;
+    const int k0 = blockIdx.y * ki, nk = min(ki, P.N - k0);
+    const MskGeom& G = *GG;
+    // phase A: the block's stage coefficients (lanes past the batch end leave their slots unset; their columns are
+    // carried through them below but never stored)
+    const int ntask = TW * nk * Q;
+    for (int t = threadIdx.x; t < ntask; t += kMskFusedThreads) {
+        const int l = t % TW, kql = t / TW;  // kql = local interval * Q + stage
+        const int64_t b = b0 + l;
+        if (b < B) msk_stage_task<NQ, NM, FAM>(P, G, V, XS, b, (int64_t)k0 * Q + kql, sW + kql * NC * TW + l, TW);
+    }
+    __syncthreads();
+    if (keep) {
+        const int ne = nk * Q * NC * TW;
+        double* __restrict__ Wg = P.scratch + (int64_t)k0 * Q * NC * B + b0;
+        for (int e = threadIdx.x; e < ne; e += kMskFusedThreads) {
+            const int l = e % TW, row = e / TW;
+            if (b0 + l < B) Wg[(int64_t)row * B + l] = sW[e];
+        }
+    }
+    // phase B: thread = instance lane, columns col0 + g (kMskFusedThreads / TW)
+    const int lane = threadIdx.x % TW, col0 = threadIdx.x / TW;
+    constexpr int CSTEP = kMskFusedThreads / TW;
+    const int64_t b = b0 + lane;
+    const int residual = P.residual;
+    const double h = P.h;
+    for (int kl = 0; kl < nk; ++kl) {
+        const int k = k0 + kl;
+        double tx[CPT][NX], tu[CPT][NUMAX];
+        MskICol ic[CPT];
+#pragma unroll
+        for (int g = 0; g < CPT; ++g) {
+            const int col = col0 + g * CSTEP;
+#pragma unroll
+            for (int r = 0; r < NX; ++r) tx[g][r] = r == col ? 1.0 : 0.0;
+#pragma unroll
+            for (int i = 0; i < NUMAX; ++i) {
+                const int dc = msk_udec<NM, FAM>(i, P.T, P.nu);
+                tu[g][i] = dc >= 0 && NX + dc == col ? 1.0 : 0.0;
+            }
+            ic[g] = msk_icol<NM, FAM>(P, G, V, (int64_t)k * nz, b, b < B && col < nz, col);
+        }
+        for (int j = 0; j < P.m; ++j) {
+            double tacc[CPT][NX], txs[CPT][NX];
+#pragma unroll
+            for (int g = 0; g < CPT; ++g)
+#pragma unroll
+                for (int r = 0; r < NX; ++r) txs[g][r] = tx[g][r];
+#pragma unroll
+            for (int st = 0; st < ST; ++st) {
+                const int64_t kq = (int64_t)k * Q + j * ST + st;
+                const double* __restrict__ sWb = sW + (kl * Q + j * ST + st) * NC * TW + lane;
+                double cw[NC];  // the stage's coefficients of this instance, read once for the CPT columns
+#pragma unroll
+                for (int c = 0; c < NC; ++c) cw[c] = sWb[c * TW];
+                const double* cs1 = msk_cs1<NM>(P, kq);
+                const double cst = (ST == 4 && st == 2) ? h : 0.5 * h;
+#pragma unroll
+                for (int g = 0; g < CPT; ++g) {
+                    double tk[NX], dcs[NM];
+                    msk_icol_dcs<NM, FAM>(P, ic[g], kq, dcs);
+                    msk_tangent<NQ, NM, FAM>(G, residual, cw, 1, txs[g], tu[g], dcs, cs1, tk);
+#pragma unroll
+                    for (int r = 0; r < NX; ++r) {
+                        if (ST == 4) {
+                            if (st == 0) tacc[g][r] = tk[r];
+                            else if (st < 3) tacc[g][r] = tacc[g][r] + 2.0 * tk[r];
+                        }
+                        if (st + 1 < ST) txs[g][r] = tx[g][r] + cst * tk[r];
+                        else tx[g][r] = ST == 4 ? tx[g][r] + (h / 6.0) * (tacc[g][r] + tk[r]) : tx[g][r] + h * tk[r];
+                    }
+                }
+            }
+        }
+        if (b < B) {
+            const int64_t jb = (int64_t)k * P.nnzk;
+#pragma unroll
+            for (int g = 0; g < CPT; ++g) {
+                const int col = col0 + g * CSTEP;
+                if (col >= nz) continue;
+#pragma unroll
+                for (int r = 0; r < NX; ++r) {
+                    const int pos = G.jpos[r * kMskMaxZ + col];
+                    if (pos >= 0) msk_st_j(J + (jb + pos) * B + b, tx[g][r]);
+                }
+                if (col == 0 && !P.keepc) {
+#pragma unroll
+                    for (int r = 0; r < NX; ++r) msk_st_j(J + (jb + G.jneg[r]) * B + b, -1.0);
+                }
+            }
+        }
+    }
+}
+
+// intervals per k_msk_stage_tangents block: enough (instance, interval, stage) tasks to fill the block once, within
+// the LDS; 0 when even one interval's coefficients do not fit (the unfused path then runs)
+inline int msk_fused_ki(int N, int Q, int NC, int TW) {
+    const size_t per = (size_t)Q * NC * TW * sizeof(double);
+    if (per > kMskFusedMaxLds) return 0;
+    int ki = std::max(1, kMskFusedThreads / (TW * Q));
+    ki = std::min(ki, N);
+    while (ki > 1 && (size_t)ki * per > kMskFusedMaxLds) --ki;
+    while (ki > 1 && N % ki != 0 && (N + ki - 1) / ki == (N + ki - 2) / (ki - 1)) --ki;  // same groups, fewer idle
+    return ki;
 }
 
 // one stage's term T_q^T (G_q T_q[:, a]) of k_msk_hproj (thread = instance, column a, interval-stage kq)

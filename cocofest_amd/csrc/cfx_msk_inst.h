@@ -35,6 +35,17 @@ inline bool msk_stage_split() {  // read at every launch, so a test can compare 
     const char* e = std::getenv("CFX_MSK_STAGE");
     return e && std::string(e) == "split";
 }
+// g + J_g: the stage coefficients and tangents fused (k_msk_stage_tangents) or the two-kernel path through the
+// scratch buffer.  The fused launch holds one block of four waves per CU, so it needs many blocks: cfg 5 at B = 65,536
+// 1.325-1.331 vs 1.371-1.374 ms, at 16,384 0.365 vs 0.381 ms, but at 8,192 0.206 vs 0.204 ms and at batch 1 0.078 vs
+// 0.051 ms (profiles/round6/msk_fused/).  CFX_MSK_TANGENTS=fused|split forces either (read at every launch).
+constexpr int64_t kMskFusedMinBlocks = 2048;  // 8 per CU
+inline int msk_tangent_mode() {  // 0: by size, 1: fused, 2: two kernels
+    const char* e = std::getenv("CFX_MSK_TANGENTS");
+    if (e && std::string(e) == "fused") return 1;
+    if (e && std::string(e) == "split") return 2;
+    return 0;
+}
 template <int NQ, int NM, int FAM>
 void msk_stagecoef(const MskParams& P, const MskGeom* G, const double* V, const double* XS, hipStream_t s) {
     const unsigned g = (unsigned)((P.B * P.N * P.Q + kMskBlk - 1) / kMskBlk);
@@ -42,6 +53,26 @@ void msk_stagecoef(const MskParams& P, const MskGeom* G, const double* V, const 
         hipLaunchKernelGGL((k_msk_stagecoef_split<NQ, NM, FAM>), dim3(g, 2), dim3(kMskBlk), 0, s, P, G, V, XS);
     else
         hipLaunchKernelGGL((k_msk_stagecoef_par<NQ, NM, FAM>), dim3(g), dim3(kMskBlk), 0, s, P, G, V, XS);
+}
+
+// stage coefficients and tangents in one launch (k_msk_stage_tangents); keep: the Hessian that follows at this point
+// reuses the coefficients, so they are stored as well
+template <int NQ, int NM, int FAM, int SCHEME, int TW>
+hipError_t msk_fused(const MskParams& P, const MskGeom* G, const double* V, const double* XS, double* J, int ki,
+                     bool keep, hipStream_t s) {
+    constexpr int NC = msk_ncoef<NQ, NM>();
+    const size_t lds = (size_t)ki * P.Q * NC * TW * sizeof(double);
+    static size_t raised = 65536;  // one per instantiation
+    if (lds > raised) {
+        const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_msk_stage_tangents<NQ, NM, FAM, SCHEME, TW>),
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+        raised = lds;
+    }
+    hipLaunchKernelGGL((k_msk_stage_tangents<NQ, NM, FAM, SCHEME, TW>),
+                       dim3((unsigned)((P.B + TW - 1) / TW), (unsigned)((P.N + ki - 1) / ki)), dim3(kMskFusedThreads),
+                       lds, s, P, G, V, XS, J, ki, keep ? 1 : 0);
+    return hipGetLastError();
 }
 
 template <int NQ, int NM, int FAM, int SCHEME>
@@ -63,9 +94,20 @@ hipError_t shoot_t(const MskParams& P, const MskGeom* G, const double* V, double
     // thread per Jacobian column
     constexpr int NC = msk_ncoef<NQ, NM>();
     double* XS = P.scratch + P.B * P.N * P.Q * NC;
-    (void)keep_xs;  // the stage values are always left in XS
     hipLaunchKernelGGL((k_msk_values<NQ, NM, FAM, SCHEME>), dim3(gx, (unsigned)P.N), dim3(kMskBlk), 0, s, P, G, V, Gout,
                        XS);
+    const int mode = msk_tangent_mode();
+    const bool fuse = P.nz <= kMskLdsCols && mode != 2;
+    auto enough = [&](int tw, int ki) {
+        return mode == 1 || (P.B + tw - 1) / tw * ((P.N + ki - 1) / ki) >= kMskFusedMinBlocks;
+    };
+    const int ki32 = fuse ? msk_fused_ki(P.N, P.Q, NC, 32) : 0;
+    if (ki32 > 0 && enough(32, ki32)) return msk_fused<NQ, NM, FAM, SCHEME, 32>(P, G, V, XS, J, ki32, keep_xs, s);
+    if constexpr (SCHEME == 4) {  // 16-instance blocks for long RK4 intervals (RK4 x 5); RK1 / RK2 that long run unfused
+        const int ki16 = fuse && ki32 == 0 ? msk_fused_ki(P.N, P.Q, NC, 16) : 0;
+        if (ki16 > 0 && enough(16, ki16))
+            return msk_fused<NQ, NM, FAM, SCHEME, 16>(P, G, V, XS, J, ki16, keep_xs, s);
+    }
     msk_stagecoef<NQ, NM, FAM>(P, G, V, XS, s);
     if (P.nz <= kMskLdsCols) {  // coefficients through LDS, one block per TW instances
         constexpr int ST = SCHEME == 4 ? 4 : (SCHEME == 2 ? 2 : 1), TW = kMskTangentInstances;  // cfx_msk_create's kpb

@@ -32,7 +32,8 @@ inline size_t msk_hess_work_host(int nq, int nm, int nx, int nz, int ntasks, int
 }
 
 // g (+ J_g when J != nullptr; P.scratch then points at a msk_shoot_work_host buffer, whose XS region keeps the stage
-// values, so that a launch_msk_hessian at the same point can skip the recursion: reuse).  keep_xs: unused.
+// values, so that a launch_msk_hessian at the same point can skip the recursion: reuse).  keep_xs: a Hessian at this
+// point will reuse the stage data, so the fused stage/tangent kernel stores the coefficients too.
 hipError_t launch_msk_shooting(int nq, int nm, int fam, int scheme, const MskParams& P, const MskGeom* G,
                                const double* V, double* Gout, double* J, bool keep_xs, hipStream_t s);
 hipError_t launch_msk_hessian(int nq, int nm, int fam, int scheme, const MskParams& P, const MskGeom* G,

@@ -1,5 +1,6 @@
-"""Summarize rocprofv3 --pmc passes over scripts/msk_probe.py --batch 65536 (cfg 5 g + J_g: k_msk_values,
-k_msk_stagecoef_par, k_msk_tangents_lds) into profiles/msk_pmc.json, the file bench.py's `msk.roofline` reads.
+"""Summarize rocprofv3 --pmc passes over scripts/msk_probe.py --batch 65536 (cfg 5 g + J_g: k_msk_values and the
+fused k_msk_stage_tangents, or k_msk_stagecoef_par + k_msk_tangents_lds under CFX_MSK_TANGENTS=split) into
+profiles/msk_pmc.json, the file bench.py's `msk.roofline` reads.
 
 Per kernel and dispatch (averaged over the dispatches of the batch's g + J_g calls): HBM bytes from FETCH_SIZE and
 WRITE_SIZE (separate passes, KiB; FETCH_SIZE doubled on gfx950 as MI355X_MICROARCH.md prescribes), all VALU
@@ -12,7 +13,8 @@ import sqlite3
 import statistics
 import sys
 
-KERNELS = {"k_msk_values": "values", "k_msk_stagecoef_par": "stagecoef", "k_msk_tangents_lds": "tangents"}
+KERNELS = {"k_msk_values": "values", "k_msk_stagecoef_par": "stagecoef", "k_msk_tangents_lds": "tangents",
+           "k_msk_stage_tangents": "fused"}
 F64 = ["SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_TRANS_F64"]
 
 
@@ -49,6 +51,8 @@ def main(src, dst="profiles/msk_pmc.json"):
     m, names = collect(src, filt="pmc_")
     kernels, step = {}, {"hbm": 0.0, "valu": 0.0, "f64": 0.0}
     for key in KERNELS:
+        if key not in names:  # not launched in this run
+            continue
         fetch, write = m.get((key, "FETCH_SIZE")), m.get((key, "WRITE_SIZE"))
         hbm = None if fetch is None or write is None else (2 * fetch + write) * 1024.0
         f64 = {c.split("_")[3].lower(): m.get((key, c)) for c in F64}

@@ -472,6 +472,53 @@ def test_msk_stage_kernels_split_by_direction_agree(case, monkeypatch):
         assert np.max(np.abs(a - b_) / scale) < 1e-12
 
 
+@pytest.mark.parametrize("case", ["cfg5_d07f_rk4", "d07_rk1_residual", "d07f_rk2", "hmed_f_rk4_residual", "cfg5_legacy",
+                                  "biceps_1dof_d07f", "cfg5_rk4x5"])
+def test_msk_fused_stage_tangents_match_the_two_kernel_path(case, monkeypatch):
+    """k_msk_stage_tangents (the stage coefficients and tangent columns of g + J_g in one launch, the coefficients kept
+    in LDS; by default only at large batches, forced here) against k_msk_stagecoef_par + k_msk_tangents_lds
+    (CFX_MSK_TANGENTS=split, through the scratch buffer): the same expressions, so g and J_g agree to the bit; a batch
+    that leaves the last 32-instance block partly empty, and the Hessian that follows (it recomputes the stage data
+    outside the interior point).  RK4 x 5 (20 stages per interval) runs the 16-instance blocks."""
+    cfg = MC.cfg5(m=5) if case == "cfg5_rk4x5" else CASES[case]
+    ocp = MC.product_ocp(**cfg)
+    pb = MC.oracle_problem(**cfg)
+    B = 45
+    V = MC.random_decision(pb, B, seed=11)
+    lam = np.random.default_rng(12).normal(size=(B, pb.ng))
+    of = np.linspace(0.2, 1.5, B)
+    out = {}
+    for mode in ("fused", "split"):
+        monkeypatch.setenv("CFX_MSK_TANGENTS", mode)
+        h = ocp.nlp(batch=B, layout="aos")
+        g, jac = np.empty((B, h.ng)), np.empty((B, h.nnz_jac))
+        h.eval_all(V.copy(), g=g, jac=jac)
+        hv = h.eval_h(V.copy(), of.copy(), lam.copy())
+        h.close()
+        out[mode] = (g, jac, hv)
+    for a, b_ in zip(out["fused"], out["split"]):
+        np.testing.assert_array_equal(a, b_)
+
+
+def test_msk_fused_stage_tangents_in_the_interior_point(monkeypatch):
+    """Inside the interior point the fused launch also stores the coefficients for the Hessian at the same point
+    (cfx_api.hip msk_stash): cfg 5 (RK4 x 5, as test_msk_cfg5_interior_point_converges) solved with the fused and the
+    two-kernel path takes the same iterations to the same point."""
+    from cocofest_amd.solver import IpmOptions, NativeIpm
+
+    ocp = MC.product_ocp(**MC.cfg5(m=5))
+    res = {}
+    for mode in ("fused", "split"):
+        monkeypatch.setenv("CFX_MSK_TANGENTS", mode)
+        nat = NativeIpm(ocp, batch=4, options=IpmOptions(tol=1e-6, max_iter=1000))
+        res[mode] = nat.solve()
+        nat.close()
+    a, b_ = res["fused"], res["split"]
+    assert a.converged.all(), (a.status, a.iterations)
+    np.testing.assert_array_equal(a.iterations, b_.iterations)
+    np.testing.assert_array_equal(a.v, b_.v)
+
+
 def test_msk_hmed_interior_point_converges():
     """The reference's Hmed MSK case (tests/shard2/test_fes_dynamics.py:104-183: arm26 biceps / triceps, Hmed2018 with
     fatigue, residual torque minimised, elbow 5 -> 120 deg, intensities in [I_min, 130]) at RK4 x 5 (RK4 x 1 is unstable
