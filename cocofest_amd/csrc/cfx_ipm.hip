@@ -187,6 +187,7 @@ struct IpmK {
     // affine part stays in rhs) and its solution in band order [B][nKp]; ncomp = the bounded sides
     int adapt, ncomp;
     double *mfilt, *rhsmu, *rbc;
+    double* mgs;  // wide instances: k_wmu_ctl's golden-section state [B][kGS]
 };
 
 enum { KKT_NEWTON = 0, KKT_LSMULT = 1, KKT_RESTO = 2, KKT_RSNLP = 3 };
@@ -1584,6 +1585,301 @@ __global__ void __launch_bounds__(kIB) k_mu_oracle(const IpmK K) {
         S.tau = clamp_lo(1.0 - mu, K.o.tau_min);
     }
     store_scal(K, b, S);
+}
+
+// ---- adaptive mu on wide instances (IpmK::wide): k_mu_oracle's golden section as a state machine over rounds of
+// three launches — the candidates' partial step-fraction minima over a grid (k_wmu_min), the partial complementarity
+// sums with every block reducing those minima in wide_get's order (k_wmu_sum), the one-block control step that forms
+// the quality values and advances the section (k_wmu_ctl) — so that a quality evaluation is a grid pass instead of
+// one block's loop over the instance (9.6 ms per call on the reaching task, 65 % of an iteration's kernels).  The
+// decisions are k_mu_oracle's, over the wide path's own deterministic sums.  State [B][kGS] (MG_*); phase 0 nothing to
+// do, 1 the pair Q(s1m), Q(1) pending, 2 the pair Q(e^m1), Q(e^m2), 3 one section point (MG_WHICH 1: m1, 2: m2), 4 the
+// end point, 5 done (k_wmu_apply adds mu rbc to rb).  Rounds after phase 5 return at once.
+constexpr int kGS = 24;
+enum {
+    MG_PHASE = 0, MG_NC, MG_C0, MG_C1, MG_A, MG_BB, MG_A0, MG_B0, MG_M1, MG_M2, MG_QM1, MG_QM2, MG_QLO, MG_QHI, MG_K,
+    MG_QBEST, MG_BEST, MG_WHICH, MG_EP, MG_MU
+};
+
+// grid (B, ceil(nK / kIB)): k_mu_cen_rhs elementwise
+__global__ void __launch_bounds__(kIB) k_wmu_cen_rhs(const IpmK K) {
+    const int64_t b = blockIdx.x;
+    const int i = blockIdx.y * kIB + threadIdx.x;
+    if (i >= K.nK) return;
+    const bool on = !K.sc[b].done && !K.sc[b].rs_on && K.sc[b].mfree;
+    K.rbc[b * K.nKp + K.pos[i]] = (on && i < K.nf) ? K.rhsmu[b * K.nf + i] : 0.0;
+}
+
+__global__ void __launch_bounds__(kIB) k_wmu_init(const IpmK K) {
+    const int64_t b = blockIdx.x;
+    if (threadIdx.x != 0) return;
+    const Scal& S = K.sc[b];
+    double* st = K.mgs + b * kGS;
+    if (S.done || S.rs_on || !S.mfree) {
+        st[MG_PHASE] = 0.0;
+        return;
+    }
+    st[MG_PHASE] = 1.0;
+    st[MG_NC] = 2.0;
+    st[MG_C0] = 1.0 - max_n(1e-4, K.o.quality_function_section_sigma_tol);
+    st[MG_C1] = 1.0;
+}
+
+// the candidates' mu = sigma avgc (at most two)
+__device__ inline int wmu_cands(const IpmK& K, int64_t b, double (&mu)[2]) {
+    const double* st = K.mgs + b * kGS;
+    const int ph = (int)st[MG_PHASE];
+    if (ph < 1 || ph > 4) return 0;
+    const double avg = K.sc[b].avgc;
+    const int nc = (int)st[MG_NC];
+    mu[0] = st[MG_C0] * avg;
+    mu[1] = nc > 1 ? st[MG_C1] * avg : mu[0];
+    return nc;
+}
+
+// grid (B, kWideParts): partial minima of the candidates' primal / dual fractions to the boundary (mu_quality's first
+// loop), wpart slots 0..7
+__global__ void __launch_bounds__(kIB) k_wmu_min(const IpmK K) {
+    const int64_t b = blockIdx.x;
+    double mu[2];
+    const int nc = wmu_cands(K, b, mu);
+    if (nc == 0) return;
+    const int nf = K.nf;
+    const double tau[2] = {clamp_lo(1.0 - mu[0], K.o.tau_min), clamp_lo(1.0 - mu[1], K.o.tau_min)};
+    const double* x = K.x + b * nf;
+    const double* zl = K.zl + b * nf;
+    const double* zu = K.zu + b * nf;
+    const double* lbI = K.lbI + b * nf;
+    const double* ubI = K.ubI + b * nf;
+    const double* ra = K.rb + b * K.nKp;
+    const double* rc = K.rbc + b * K.nKp;
+    double v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = INFINITY;
+    for (int i = blockIdx.y * kIB + threadIdx.x; i < nf; i += kWideParts * kIB) {
+        const int q = K.pos[i];
+        const double a = ra[q], c = rc[q];
+        const bool hL = K.hasL[i], hU = K.hasU[i];
+        const double sl = hL ? x[i] - lbI[i] : 1.0, su = hU ? ubI[i] - x[i] : 1.0;
+        const double zli = zl[i], zui = zu[i];
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            const double dx = a + mu[t] * c;
+            const double vzl = hL ? mu[t] / sl - zli - zli / sl * dx : 0.0;
+            const double vzu = hU ? mu[t] / su - zui + zui / su * dx : 0.0;
+            v[4 * t] = min_n(v[4 * t], step_term(hL, sl, dx, tau[t]));
+            v[4 * t + 1] = min_n(v[4 * t + 1], step_term(hU, su, -dx, tau[t]));
+            v[4 * t + 2] = min_n(v[4 * t + 2], step_term(hL, zli, vzl, tau[t]));
+            v[4 * t + 3] = min_n(v[4 * t + 3], step_term(hU, zui, vzu, tau[t]));
+        }
+    }
+    const int ro[8] = {2, 2, 2, 2, 2, 2, 2, 2};
+    wide_put(K, b, v, ro);
+}
+
+// the candidates' (a_p, a_d) from k_wmu_min's partials (every block and the control kernel the same values)
+__device__ inline void wmu_fractions(const IpmK& K, int64_t b, double (&ap)[2], double (&ad)[2]) {
+    double v[8];
+    const int ro[8] = {2, 2, 2, 2, 2, 2, 2, 2};
+    wide_get(K, b, v, ro);
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+        ap[t] = min_n(clamp_hi(v[4 * t], 1.0), clamp_hi(v[4 * t + 1], 1.0));
+        ad[t] = min_n(clamp_hi(v[4 * t + 2], 1.0), clamp_hi(v[4 * t + 3], 1.0));
+    }
+}
+
+// grid (B, kWideParts): partial sums of the predicted complementarity (mu_quality's second loop), wpart slots 8, 9
+__global__ void __launch_bounds__(kIB) k_wmu_sum(const IpmK K) {
+    const int64_t b = blockIdx.x;
+    double mu[2];
+    if (wmu_cands(K, b, mu) == 0) return;  // (block-uniform)
+    double ap[2], ad[2];
+    wmu_fractions(K, b, ap, ad);
+    const int nf = K.nf;
+    const double* x = K.x + b * nf;
+    const double* zl = K.zl + b * nf;
+    const double* zu = K.zu + b * nf;
+    const double* lbI = K.lbI + b * nf;
+    const double* ubI = K.ubI + b * nf;
+    const double* ra = K.rb + b * K.nKp;
+    const double* rc = K.rbc + b * K.nKp;
+    double cs[2] = {0.0, 0.0};
+    for (int i = blockIdx.y * kIB + threadIdx.x; i < nf; i += kWideParts * kIB) {
+        const int q = K.pos[i];
+        const bool hL = K.hasL[i], hU = K.hasU[i];
+        if (!hL && !hU) continue;
+        const double a = ra[q], c = rc[q];
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            const double dx = a + mu[t] * c;
+            if (hL) {
+                const double sl = x[i] - lbI[i];
+                const double u = (sl + ap[t] * dx) * (zl[i] + ad[t] * (mu[t] / sl - zl[i] - zl[i] / sl * dx));
+                cs[t] += u * u;
+            }
+            if (hU) {
+                const double su = ubI[i] - x[i];
+                const double u = (su - ap[t] * dx) * (zu[i] + ad[t] * (mu[t] / su - zu[i] + zu[i] / su * dx));
+                cs[t] += u * u;
+            }
+        }
+    }
+    const int ro[2] = {0, 0};
+    breduce_n(cs, ro);
+    if (threadIdx.x == 0) {
+        double* pp = K.wpart + (b * kWideParts + blockIdx.y) * kWP;
+        pp[8] = cs[0];
+        pp[9] = cs[1];
+    }
+}
+
+// one block per instance: the candidates' quality values and one step of k_mu_oracle's section
+__global__ void __launch_bounds__(kIB) k_wmu_ctl(const IpmK K) {
+    const int64_t b = blockIdx.x;
+    double mu[2];
+    const int nc = wmu_cands(K, b, mu);
+    if (nc == 0) return;  // (block-uniform)
+    double ap[2], ad[2];
+    wmu_fractions(K, b, ap, ad);
+    double cs[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+        cs[t] = threadIdx.x < kWideParts ? K.wpart[(b * kWideParts + threadIdx.x) * kWP + 8 + t] : 0.0;
+    const int ro[2] = {0, 0};
+    breduce_n(cs, ro);
+    if (threadIdx.x != 0) return;
+    const Scal& S = K.sc[b];
+    const int nf = K.nf;
+    double Qv[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+        double val = (1.0 - ad[t]) * (1.0 - ad[t]) * S.qd / (nf > 0 ? nf : 1);
+        if (K.m) val += (1.0 - ap[t]) * (1.0 - ap[t]) * S.qp / K.m;
+        if (K.ncomp) val += cs[t] / K.ncomp;
+        Qv[t] = val;
+    }
+    double* st = K.mgs + b * kGS;
+    const int ph = (int)st[MG_PHASE];
+    const double avg = S.avgc;
+    const bool safe = avg > 0;
+    const double avgs = safe ? avg : 1.0;
+    const double g = (3.0 - sqrt(5.0)) / 2.0;
+    bool fin = false;
+    double sig = 0.0;
+    auto request = [&](double m, int which) {
+        st[MG_NC] = 1.0;
+        st[MG_C0] = exp(m);
+        st[MG_WHICH] = which;
+    };
+    if (ph == 1) {  // Q(1 - sigma_tol), Q(1): which way the quality decreases
+        const double s1m = st[MG_C0], q1m = Qv[0], q1 = Qv[1];
+        const bool up = q1m > q1;
+        const double s_hi = up ? clamp_hi(S.mu_max / avgs, K.o.sigma_max) : clamp_lo(K.o.mu_min / avgs, K.o.sigma_min);
+        const double lo = up ? 1.0 : s_hi;
+        const double hi = up ? s_hi : max_n(s_hi, s1m);
+        st[MG_QLO] = up ? q1 : -1.0;
+        st[MG_QHI] = up ? -1.0 : q1m;
+        if (lo >= hi) {
+            sig = up ? hi : lo;
+            fin = true;
+        } else {
+            const double a = log(lo), bb = log(hi);
+            st[MG_A] = st[MG_A0] = a;
+            st[MG_BB] = st[MG_B0] = bb;
+            st[MG_M1] = a + g * (bb - a);
+            st[MG_M2] = a + (1.0 - g) * (bb - a);
+            st[MG_NC] = 2.0;
+            st[MG_C0] = exp(st[MG_M1]);
+            st[MG_C1] = exp(st[MG_M2]);
+            st[MG_K] = 0.0;
+            st[MG_PHASE] = 2.0;
+        }
+    } else if (ph == 2 || ph == 3) {
+        if (ph == 2) {
+            st[MG_QM1] = Qv[0];
+            st[MG_QM2] = Qv[1];
+        } else {
+            st[(int)st[MG_WHICH] == 1 ? MG_QM1 : MG_QM2] = Qv[0];
+        }
+        double a = st[MG_A], bb = st[MG_BB], m1 = st[MG_M1], m2 = st[MG_M2];
+        double qm1 = st[MG_QM1], qm2 = st[MG_QM2], q_lo = st[MG_QLO], q_hi = st[MG_QHI];
+        const int k = (int)st[MG_K];
+        bool stop = k >= K.o.quality_function_max_section_steps;
+        if (!stop) {
+            double qmin = INFINITY, qmax = -INFINITY;
+            const double qs[4] = {q_lo, q_hi, qm1, qm2};
+            for (int t = 0; t < 4; ++t)
+                if (qs[t] >= 0) qmin = fmin(qmin, qs[t]), qmax = fmax(qmax, qs[t]);
+            stop = !(exp(bb) - exp(a) >= K.o.quality_function_section_sigma_tol * exp(bb)) ||
+                   !(1.0 - qmin / qmax >= K.o.quality_function_section_qf_tol);
+        }
+        if (!stop) {
+            if (qm1 > qm2) {  // the minimum is in [m1, b]
+                a = m1;
+                q_lo = qm1;
+                m1 = m2;
+                qm1 = qm2;
+                m2 = a + (1.0 - g) * (bb - a);
+                request(m2, 2);
+            } else {
+                bb = m2;
+                q_hi = qm2;
+                m2 = m1;
+                qm2 = qm1;
+                m1 = a + g * (bb - a);
+                request(m1, 1);
+            }
+            st[MG_A] = a, st[MG_BB] = bb, st[MG_M1] = m1, st[MG_M2] = m2;
+            st[MG_QM1] = qm1, st[MG_QM2] = qm2, st[MG_QLO] = q_lo, st[MG_QHI] = q_hi;
+            st[MG_K] = k + 1;
+            st[MG_PHASE] = 3.0;
+        } else {
+            double best = qm1 < qm2 ? m1 : m2;
+            const double qbest = qm1 < qm2 ? qm1 : qm2;
+            const bool hi_end = bb == st[MG_B0], lo_end = a == st[MG_A0] && !hi_end;  // an end point never moved
+            if (hi_end || lo_end) {
+                const double qe = hi_end ? q_hi : q_lo, ep = hi_end ? bb : a;
+                if (qe < 0) {
+                    st[MG_BEST] = best;
+                    st[MG_QBEST] = qbest;
+                    st[MG_EP] = ep;
+                    request(ep, 0);
+                    st[MG_PHASE] = 4.0;
+                } else {
+                    if (qe < qbest) best = ep;
+                    sig = exp(best);
+                    fin = true;
+                }
+            } else {
+                sig = exp(best);
+                fin = true;
+            }
+        }
+    } else if (ph == 4) {
+        double best = st[MG_BEST];
+        if (Qv[0] < st[MG_QBEST]) best = st[MG_EP];
+        sig = exp(best);
+        fin = true;
+    }
+    if (fin) {
+        const double m = safe ? clamp_lo(min_n(sig * avg, S.mu_max), K.o.mu_min) : K.o.mu_min;
+        st[MG_MU] = m;
+        st[MG_PHASE] = 5.0;
+        K.sc[b].mu = m;
+        K.sc[b].tau = clamp_lo(1.0 - m, K.o.tau_min);
+    }
+}
+
+// grid (B, ceil(nK / kIB)): the Newton step rb += mu rbc of the instances whose section finished
+__global__ void __launch_bounds__(kIB) k_wmu_apply(const IpmK K) {
+    const int64_t b = blockIdx.x;
+    const double* st = K.mgs + b * kGS;
+    if ((int)st[MG_PHASE] != 5) return;
+    const int i = blockIdx.y * kIB + threadIdx.x;
+    if (i >= K.nK) return;
+    const int q = K.pos[i];
+    K.rb[b * K.nKp + q] += st[MG_MU] * K.rbc[b * K.nKp + q];
 }
 
 // dz, fraction to the boundary, filter quantities at x, first trial point (solver.py, after the inertia loop)
@@ -4045,8 +4341,9 @@ static int ipm_create_common(cfx_ipm* s, const cfx_sizes& sz, int layout, const 
     K.adapt = K.o.mu_strategy == CFX_MU_ADAPTIVE;
     K.ncomp = 0;
     for (int i = 0; i < nf; ++i) K.ncomp += (int)hasL[i] + (int)hasU[i];
-    K.mfilt = K.rhsmu = K.rbc = nullptr;
+    K.mfilt = K.rhsmu = K.rbc = K.mgs = nullptr;
     if (K.adapt) {
+        K.mgs = dalloc<double>(s, B * kGS, &rc);
         K.mfilt = dalloc<double>(s, B * kFilt * 2, &rc);
         K.rhsmu = dalloc<double>(s, B * nf, &rc);
         K.rbc = dalloc<double>(s, B * nKp, &rc);
@@ -4252,7 +4549,9 @@ struct Run {
     // free-mode instances, which leaves their combined Newton step in rb (k_mu_oracle)
     int mu_oracle() {
         const IpmK& K = s->K;
-        hipLaunchKernelGGL(k_mu_cen_rhs, g, dim3(kIB), 0, st, K);
+        const dim3 gk((unsigned)K.B, (unsigned)((K.nK + kIB - 1) / kIB));
+        if (K.wide) hipLaunchKernelGGL(k_wmu_cen_rhs, gk, dim3(kIB), 0, st, K);
+        else hipLaunchKernelGGL(k_mu_cen_rhs, g, dim3(kIB), 0, st, K);
         IPM_HIP(s, hipGetLastError());
         IPM_RUN(resolve(K.rbc));
         if (K.lbfgs) {  // the Woodbury correction of the centering solution too
@@ -4260,7 +4559,21 @@ struct Run {
             K2.rb = K.rbc;
             hipLaunchKernelGGL(k_lbfgs_apply, g, dim3(kIB), 0, st, K2);
         }
-        hipLaunchKernelGGL(k_mu_oracle, g, dim3(kIB), 0, st, K);
+        if (!K.wide) {
+            hipLaunchKernelGGL(k_mu_oracle, g, dim3(kIB), 0, st, K);
+            IPM_HIP(s, hipGetLastError());
+            return CFX_OK;
+        }
+        // wide instances: the section's rounds (the pair at sigma = 1, the first pair of section points, one point per
+        // section step, the end point), each a no-op once the instance's section has finished
+        hipLaunchKernelGGL(k_wmu_init, g, dim3(64), 0, st, K);
+        const int rounds = K.o.quality_function_max_section_steps + 3;
+        for (int r = 0; r < rounds; ++r) {
+            hipLaunchKernelGGL(k_wmu_min, wa(), dim3(kIB), 0, st, K);
+            hipLaunchKernelGGL(k_wmu_sum, wa(), dim3(kIB), 0, st, K);
+            hipLaunchKernelGGL(k_wmu_ctl, g, dim3(kIB), 0, st, K);
+        }
+        hipLaunchKernelGGL(k_wmu_apply, gk, dim3(kIB), 0, st, K);
         IPM_HIP(s, hipGetLastError());
         return CFX_OK;
     }

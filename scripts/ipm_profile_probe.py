@@ -15,6 +15,8 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--profile", default="ipopt", choices=["ipopt", "cfx"])
 ap.add_argument("--batch", type=int, default=4096)
 ap.add_argument("--opt", action="append", default=[])
+ap.add_argument("--guess", action="store_true", help="start every instance at the reference's initial guess")
+ap.add_argument("--reps", type=int, default=1, help="timed solves (after one warm-up)")
 args = ap.parse_args()
 extra = {}
 for kv in args.opt:
@@ -29,13 +31,15 @@ rng = np.random.default_rng(0)
 v0 = np.tile(ocp.initial_guess_vector(), (B, 1))
 lb, ub = ocp.bounds_vector()
 free = lb != ub
-v0[:, free] = np.clip(v0[:, free] + rng.uniform(0, 1, (B, free.sum())) * np.minimum(ub[free] - lb[free], 10), lb[free],
-                      ub[free])
+if not args.guess:
+    v0[:, free] = np.clip(v0[:, free] + rng.uniform(0, 1, (B, free.sum())) * np.minimum(ub[free] - lb[free], 10),
+                          lb[free], ub[free])
 ipm = NativeIpm(ocp, batch=B, options=opts)
 ipm.solve(v0)
 t = time.perf_counter()
-r = ipm.solve(v0)
-dt = time.perf_counter() - t
+for _ in range(args.reps):
+    r = ipm.solve(v0)
+dt = (time.perf_counter() - t) / args.reps
 st = ipm.last_stats
 ipm.close()
 print({"profile": args.profile, "extra": extra, "batch": B, "wall_s": dt, "iterations_max": int(r.iterations.max()),

@@ -319,12 +319,13 @@ def test_native_ipm_unscaled_termination_tests():
     assert np.max(np.abs(res.v - base.v) / np.maximum(span, 1e-12)) < 1e-6
 
 
-@pytest.mark.parametrize("B", [1, 4])
-def test_native_ipm_wide_split_kernels_reach_the_same_optimum(B, monkeypatch):
+@pytest.mark.parametrize("B,mu", [(1, "monotone"), (4, "monotone"), (1, "adaptive"), (4, "adaptive")])
+def test_native_ipm_wide_split_kernels_reach_the_same_optimum(B, mu, monkeypatch):
     """The wide-instance path (IpmK::wide: the long loops of k_ipm_begin / dir / accept / update / curv as grids of
     partial sums, the one-block kernels on the reduced values, grids over the elementwise updates — chosen for the
-    reaching task's 120,000 unknowns) forced on a small problem (CFX_IPM_WIDE=1) against the one-block kernels: the
-    same optimum; the sums run in another fixed order, so the path may differ by rounding."""
+    reaching task's 120,000 unknowns; under adaptive mu also the quality-function oracle as rounds of grid passes,
+    k_wmu_*) forced on a small problem (CFX_IPM_WIDE=1) against the one-block kernels: the same optimum; the sums run
+    in another fixed order, so the path may differ by rounding."""
     from cocofest_amd.solver import IpmOptions, NativeIpm
 
     cfg = dict(cases.cfg3(), objective=TRACK)
@@ -333,7 +334,7 @@ def test_native_ipm_wide_split_kernels_reach_the_same_optimum(B, monkeypatch):
     out = {}
     for wide in ("0", "1"):
         monkeypatch.setenv("CFX_IPM_WIDE", wide)
-        nat = NativeIpm(ocp, batch=B, options=IpmOptions(tol=1e-8, max_iter=300))
+        nat = NativeIpm(ocp, batch=B, options=IpmOptions(tol=1e-8, max_iter=300, mu_strategy=mu))
         out[wide] = nat.solve(v0)
         nat.close()
     a, b = out["0"], out["1"]
