@@ -188,6 +188,7 @@ struct IpmK {
     int adapt, ncomp;
     double *mfilt, *rhsmu, *rbc;
     double* mgs;  // wide instances: k_wmu_ctl's golden-section state [B][kGS]
+    int mu_block;  // 1: the small-instance oracle in the whole block (CFX_IPM_MU_ORACLE=block, tests / A-B)
 };
 
 enum { KKT_NEWTON = 0, KKT_LSMULT = 1, KKT_RESTO = 2, KKT_RSNLP = 3 };
@@ -621,34 +622,36 @@ __global__ void __launch_bounds__(kIB) k_ipm_begin(const IpmK K, int mode, int s
     if (threadIdx.x == 0) s_mono = !S.done;
     if (K.adapt) {
         passes = 1;
-        if (threadIdx.x == 0 && !S.done) {
+        static_assert(kFilt == 64, "the globalisation filter: one entry per lane of wavefront 0");
+        if (threadIdx.x < 64 && !S.done) {  // (S.done is block-uniform)
+            const int k = threadIdx.x;
             const double avg = K.ncomp ? (scl + scu) / K.ncomp : 0.0;
-            S.avgc = avg;
-            S.qd = rd2;
-            S.qp = m ? g2 : 0.0;
             const double thc = m ? th : 0.0;
-            if (S.mu_max < 0) S.mu_max = K.o.mu_max > 0 ? K.o.mu_max : K.o.mu_max_fact * avg;
             double* mf = K.mfilt + b * kFilt * 2;
-            bool ok = true;  // IpFilter::Acceptable: f <= f_i or theta < theta_i for every entry
-            if (K.o.adaptive_mu_globalization == CFX_MU_GLOBAL_OBJ_CONSTR_FILTER)
-                for (int k = 0; k < kFilt; ++k)
-                    if (!(S.fS <= mf[2 * k] || thc < mf[2 * k + 1])) {
-                        ok = false;
-                        break;
-                    }
+            const double fk = mf[2 * k], tk = mf[2 * k + 1];
+            // IpFilter::Acceptable: f <= f_i or theta < theta_i for every entry
+            const bool okk = K.o.adaptive_mu_globalization != CFX_MU_GLOBAL_OBJ_CONSTR_FILTER || S.fS <= fk || thc < tk;
+            const bool ok = __ballot(!okk) == 0ull;
             if (ok) {  // RememberCurrentPointAsAccepted: the entries it dominates leave, then the first free slot
                 const double margin = K.o.filter_margin_fact * clamp_hi(thc, K.o.filter_max_margin);
                 const double fe = S.fS - margin, te = thc - margin;
-                int slot = -1;
-                for (int k = 0; k < kFilt; ++k) {
-                    if (fe <= mf[2 * k] && te <= mf[2 * k + 1]) mf[2 * k] = mf[2 * k + 1] = INFINITY;
-                    if (slot < 0 && isinf(mf[2 * k]) && isinf(mf[2 * k + 1])) slot = k;
+                const bool dom = fe <= fk && te <= tk;
+                const unsigned long long fr = __ballot(dom || (isinf(fk) && isinf(tk)));
+                const int slot = fr ? __ffsll((long long)fr) - 1 : S.mfpos % kFilt;
+                if (k == slot) {
+                    mf[2 * k] = fe;
+                    mf[2 * k + 1] = te;
+                } else if (dom) {
+                    mf[2 * k] = mf[2 * k + 1] = INFINITY;
                 }
-                if (slot < 0) slot = S.mfpos % kFilt;
-                mf[2 * slot] = fe;
-                mf[2 * slot + 1] = te;
-                S.mfpos += 1;
             }
+            __builtin_amdgcn_wave_barrier();  // every lane has read S.fS / S.mfpos before lane 0 updates S
+            if (k == 0) {
+            if (ok) S.mfpos += 1;
+            S.avgc = avg;
+            S.qd = rd2;
+            S.qp = m ? g2 : 0.0;
+            if (S.mu_max < 0) S.mu_max = K.o.mu_max > 0 ? K.o.mu_max : K.o.mu_max_fact * avg;
             s_mono = 0;
             if (S.mfree && !ok) {  // to the monotone mode
                 S.mfree = 0;
@@ -658,6 +661,7 @@ __global__ void __launch_bounds__(kIB) k_ipm_begin(const IpmK K, int mode, int s
                 S.mfree = 1;
             } else {
                 s_mono = !S.mfree;
+            }
             }
         }
     }
@@ -1511,71 +1515,262 @@ __device__ double mu_quality(const IpmK& K, int64_t b, const Scal& S, double mu)
     return val;
 }
 
-// sigma by golden section over log sigma (CalculateMu / PerformGoldenSection), mu = sigma * avgc within [mu_min, mu_max];
-// then the Newton step rb += mu rbc, mu and tau stored
+// Small instances (nf <= 64 kMuWave): the oracle in wavefront 0 alone, each lane's elements (i = lane + 64 e) and
+// their reciprocals held in registers across the section's evaluations, the reductions lane butterflies — no block
+// barriers — and no division per evaluation: min_i (-tau s_i / ds_i) over ds_i < 0 is formed as tau / max_i (-ds_i
+// (1 / s_i)) (cfg 3 at batch 1: 77 us per call with the block's loops, of which ~13 quality evaluations of four
+// divisions per element).  Its own rounding (and another reduction order), so its decisions may differ from the
+// block path's in the last bits of a quality value.
+constexpr int kMuWave = 6;
+struct MuLane {
+    double a[kMuWave], c[kMuWave], sl[kMuWave], su[kMuWave], zl[kMuWave], zu[kMuWave];
+    double isl[kMuWave], isu[kMuWave], izl[kMuWave], izu[kMuWave];  // 1 / s, 1 / z
+    bool hL[kMuWave], hU[kMuWave];
+};
+__device__ __forceinline__ void mu_lane_load(const IpmK& K, int64_t b, MuLane& E) {
+    const int nf = K.nf, lane = threadIdx.x;
+#pragma unroll
+    for (int e = 0; e < kMuWave; ++e) {
+        const int i = lane + 64 * e;
+        const bool in = i < nf;
+        const int q = in ? K.pos[i] : 0;
+        E.hL[e] = in && K.hasL[i];
+        E.hU[e] = in && K.hasU[i];
+        E.a[e] = in ? K.rb[b * K.nKp + q] : 0.0;
+        E.c[e] = in ? K.rbc[b * K.nKp + q] : 0.0;
+        const double x = in ? K.x[b * nf + i] : 0.0;
+        E.sl[e] = E.hL[e] ? x - K.lbI[b * nf + i] : 1.0;
+        E.su[e] = E.hU[e] ? K.ubI[b * nf + i] - x : 1.0;
+        E.zl[e] = E.hL[e] ? K.zl[b * nf + i] : 1.0;
+        E.zu[e] = E.hU[e] ? K.zu[b * nf + i] : 1.0;
+        E.isl[e] = 1.0 / E.sl[e];
+        E.isu[e] = 1.0 / E.su[e];
+        E.izl[e] = 1.0 / E.zl[e];
+        E.izu[e] = 1.0 / E.zu[e];
+    }
+}
+// wave reduction by DPP (row_shr scans within rows of 16 lanes, row broadcasts, readlane 63): lanes a shift leaves
+// without a source combine with the identity.  (__shfl_xor lowers to ds_bpermute, an LDS round trip per step.)
+#define CFX_DPP_OP(v, op, id, CTRL, RM, BM)                                                                      \
+    do {                                                                                                        \
+        const int slo_ = __builtin_amdgcn_update_dpp(__double2loint(id), __double2loint(v), CTRL, RM, BM, false); \
+        const int shi_ = __builtin_amdgcn_update_dpp(__double2hiint(id), __double2hiint(v), CTRL, RM, BM, false); \
+        v = op(v, __hiloint2double(shi_, slo_));                                                                \
+    } while (0)
+template <class Op>
+__device__ __forceinline__ double wreduce(double v, Op op, double id) {
+    CFX_DPP_OP(v, op, id, 0x111, 0xf, 0xf);  // row_shr:1
+    CFX_DPP_OP(v, op, id, 0x112, 0xf, 0xf);  // row_shr:2
+    CFX_DPP_OP(v, op, id, 0x114, 0xf, 0xf);  // row_shr:4
+    CFX_DPP_OP(v, op, id, 0x118, 0xf, 0xf);  // row_shr:8 (lane 15 of each row: the row's value)
+    CFX_DPP_OP(v, op, id, 0x142, 0xa, 0xf);  // row_bcast:15 into rows 1 and 3
+    CFX_DPP_OP(v, op, id, 0x143, 0xc, 0xf);  // row_bcast:31 into rows 2 and 3 (lane 63: the wave's)
+    return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), 63), __builtin_amdgcn_readlane(__double2loint(v), 63));
+}
+// -ds / s where the step shrinks a positive quantity (has, ds < 0), else 0
+__device__ __forceinline__ double shrink_rate(bool has, double ds, double inv_s) { return (has && ds < 0) ? -ds * inv_s : 0.0; }
+__device__ __forceinline__ double step_from_rate(double r, double tau) { return r > 0 ? tau / r : (r != r ? r : INFINITY); }
+// the wave's maximum of non-negative rates by v_max_f64 steps, NaN if any lane holds one (fmax would drop it)
+__device__ __forceinline__ double wmax_rate(double r) {
+    const bool nan = __ballot(r != r) != 0ull;
+    const double v = wreduce(r, [](double a, double c) { return fmax(a, c); }, 0.0);
+    return nan ? __longlong_as_double(0x7ff8000000000000ll) : v;
+}
+__device__ __forceinline__ double mu_quality_w(const IpmK& K, const MuLane& E, const Scal& S, double mu) {
+    const int nf = K.nf;
+    const double tau = clamp_lo(1.0 - mu, K.o.tau_min);
+    // the primal and the dual fraction to the boundary: min over both sides = tau / the larger shrink rate
+    double rp = 0.0, rz = 0.0;
+#pragma unroll
+    for (int e = 0; e < kMuWave; ++e) {
+        if (threadIdx.x + 64 * e >= nf) break;
+        const double dx = E.a[e] + mu * E.c[e];
+        const bool hL = E.hL[e], hU = E.hU[e];
+        const double vzl = mu * E.isl[e] - E.zl[e] - E.zl[e] * E.isl[e] * dx;
+        const double vzu = mu * E.isu[e] - E.zu[e] + E.zu[e] * E.isu[e] * dx;
+        rp = max_n(rp, max_n(shrink_rate(hL, dx, E.isl[e]), shrink_rate(hU, -dx, E.isu[e])));
+        rz = max_n(rz, max_n(shrink_rate(hL, vzl, E.izl[e]), shrink_rate(hU, vzu, E.izu[e])));
+    }
+    const double ap = clamp_hi(step_from_rate(wmax_rate(rp), tau), 1.0);
+    const double ad = clamp_hi(step_from_rate(wmax_rate(rz), tau), 1.0);
+    double cs = 0.0;
+#pragma unroll
+    for (int e = 0; e < kMuWave; ++e) {
+        if (threadIdx.x + 64 * e >= nf) break;
+        const double dx = E.a[e] + mu * E.c[e];
+        if (E.hL[e]) {
+            const double t = (E.sl[e] + ap * dx) * (E.zl[e] + ad * (mu * E.isl[e] - E.zl[e] - E.zl[e] * E.isl[e] * dx));
+            cs += t * t;
+        }
+        if (E.hU[e]) {
+            const double t = (E.su[e] - ap * dx) * (E.zu[e] + ad * (mu * E.isu[e] - E.zu[e] + E.zu[e] * E.isu[e] * dx));
+            cs += t * t;
+        }
+    }
+    cs = wreduce(cs, OpSum(), 0.0);
+    double val = (1.0 - ad) * (1.0 - ad) * S.qd / (nf > 0 ? nf : 1);
+    if (K.m) val += (1.0 - ap) * (1.0 - ap) * S.qp / K.m;
+    if (K.ncomp) val += cs / K.ncomp;
+    return val;
+}
+
+// sigma from the quality function Q(sigma) by the golden section over log sigma (CalculateMu / PerformGoldenSection),
+// as a state machine that asks for one or two quality values at a time (so each caller evaluates Q at one call site:
+// the inlined evaluation appears once in the code, and the wide path can run each request as grid passes).  phase 1:
+// Q(1 - sigma_tol), Q(1) pending; 2: Q(e^m1), Q(e^m2); 3: one section point (which 1: m1, 2: m2); 4: the end point;
+// 5: done, mu = sigma avgc within [mu_min, mu_max].
+struct MuSec {
+    int phase, nc, which, k;
+    double c0, c1, a, bb, a0, b0, m1, m2, qm1, qm2, q_lo, q_hi, qbest, best, ep, mu;
+};
+__device__ __forceinline__ void musec_start(MuSec& M, const IpmK& K) {
+    M.phase = 1;
+    M.nc = 2;
+    M.c0 = 1.0 - max_n(1e-4, K.o.quality_function_section_sigma_tol);
+    M.c1 = 1.0;
+}
+__device__ __forceinline__ void musec_step(MuSec& M, const IpmK& K, const Scal& S, const double (&Qv)[2]) {
+    const double avg = S.avgc;
+    const bool safe = avg > 0;
+    const double avgs = safe ? avg : 1.0;
+    const double g = (3.0 - sqrt(5.0)) / 2.0;
+    bool fin = false;
+    double sig = 0.0;
+    // the next request: one point e^m (which: the section point it becomes, 1 m1, 2 m2, 0 the end point)
+    int req = -1;
+    double rm = 0.0;
+    if (M.phase == 1) {  // which way the quality decreases from sigma = 1
+        const double s1m = M.c0, q1m = Qv[0], q1 = Qv[1];
+        const bool up = q1m > q1;
+        const double s_hi = up ? clamp_hi(S.mu_max / avgs, K.o.sigma_max) : clamp_lo(K.o.mu_min / avgs, K.o.sigma_min);
+        const double lo = up ? 1.0 : s_hi;
+        const double hi = up ? s_hi : max_n(s_hi, s1m);
+        M.q_lo = up ? q1 : -1.0;  // -1: not evaluated
+        M.q_hi = up ? -1.0 : q1m;
+        if (lo >= hi) {
+            sig = up ? hi : lo;
+            fin = true;
+        } else {
+            M.a = M.a0 = log(lo);
+            M.bb = M.b0 = log(hi);
+            M.m1 = M.a + g * (M.bb - M.a);
+            M.m2 = M.a + (1.0 - g) * (M.bb - M.a);
+            M.nc = 2;
+            M.c0 = exp(M.m1);
+            M.c1 = exp(M.m2);
+            M.k = 0;
+            M.phase = 2;
+        }
+    } else if (M.phase == 2 || M.phase == 3) {
+        // (value selects throughout, no field chosen by a branch: that form keeps M out of registers)
+        const bool two = M.phase == 2, w1 = M.which == 1;
+        M.qm1 = two || w1 ? Qv[0] : M.qm1;
+        M.qm2 = two ? Qv[1] : (w1 ? M.qm2 : Qv[0]);
+        bool stop = M.k >= K.o.quality_function_max_section_steps;
+        if (!stop) {
+            double qmin = INFINITY, qmax = -INFINITY;
+            const double qs[4] = {M.q_lo, M.q_hi, M.qm1, M.qm2};
+            for (int t = 0; t < 4; ++t)
+                if (qs[t] >= 0) qmin = fmin(qmin, qs[t]), qmax = fmax(qmax, qs[t]);
+            stop = !(exp(M.bb) - exp(M.a) >= K.o.quality_function_section_sigma_tol * exp(M.bb)) ||
+                   !(1.0 - qmin / qmax >= K.o.quality_function_section_qf_tol);
+        }
+        if (!stop) {
+            // the minimum is in [m1, b] (right): a = m1, q_lo = qm1, m1 = m2, qm1 = qm2, m2 = a + (1 - g)(b - a) asked
+            // for; else b = m2, q_hi = qm2, m2 = m1, qm2 = qm1, m1 = a + g (b - a) asked for
+            const bool right = M.qm1 > M.qm2;
+            const double a = right ? M.m1 : M.a, bb = right ? M.bb : M.m2;
+            const double m1 = right ? M.m2 : a + g * (bb - a);
+            const double m2 = right ? a + (1.0 - g) * (bb - a) : M.m1;
+            M.q_lo = right ? M.qm1 : M.q_lo;
+            M.q_hi = right ? M.q_hi : M.qm2;
+            const double qm1 = right ? M.qm2 : M.qm1, qm2 = right ? M.qm2 : M.qm1;
+            M.a = a, M.bb = bb, M.m1 = m1, M.m2 = m2, M.qm1 = qm1, M.qm2 = qm2;
+            rm = right ? m2 : m1;
+            req = right ? 2 : 1;
+            M.k += 1;
+            M.phase = 3;
+        } else {
+            double best = M.qm1 < M.qm2 ? M.m1 : M.m2;
+            const double qbest = M.qm1 < M.qm2 ? M.qm1 : M.qm2;
+            const bool hi_end = M.bb == M.b0, lo_end = M.a == M.a0 && !hi_end;  // an end point never moved competes
+            if (hi_end || lo_end) {
+                const double qe = hi_end ? M.q_hi : M.q_lo, ep = hi_end ? M.bb : M.a;
+                if (qe < 0) {
+                    M.best = best;
+                    M.qbest = qbest;
+                    M.ep = ep;
+                    rm = ep, req = 0;
+                    M.phase = 4;
+                } else {
+                    if (qe < qbest) best = ep;
+                    sig = exp(best);
+                    fin = true;
+                }
+            } else {
+                sig = exp(best);
+                fin = true;
+            }
+        }
+    } else if (M.phase == 4) {
+        sig = exp(Qv[0] < M.qbest ? M.ep : M.best);
+        fin = true;
+    }
+    if (req >= 0) {
+        M.nc = 1;
+        M.c0 = exp(rm);
+        M.which = req;
+    }
+    if (fin) {
+        M.mu = safe ? clamp_lo(min_n(sig * avg, S.mu_max), K.o.mu_min) : K.o.mu_min;
+        M.phase = 5;
+    }
+}
+// the section driven to its end by one evaluation site (every thread of the caller runs the same decisions)
+template <class QF>
+__device__ __forceinline__ double mu_section(const IpmK& K, const Scal& S, QF Q) {
+    MuSec M;
+    musec_start(M, K);
+#pragma unroll 1
+    while (M.phase != 5) {
+        double q0 = 0.0, q1 = 0.0;
+#pragma unroll 1
+        for (int c = 0; c < M.nc; ++c) {
+            const double q = Q((c == 0 ? M.c0 : M.c1) * S.avgc);
+            q0 = c == 0 ? q : q0;
+            q1 = c == 0 ? q1 : q;
+        }
+        const double Qv[2] = {q0, q1};
+        musec_step(M, K, S, Qv);
+    }
+    return M.mu;
+}
+
+// mu = sigma avgc within [mu_min, mu_max] from mu_section; then the Newton step rb += mu rbc, mu and tau stored
 __global__ void __launch_bounds__(kIB) k_mu_oracle(const IpmK K) {
     __shared__ Scal S;
     const int64_t b = blockIdx.x;
     load_scal(K, b, S);
     if (S.done || S.rs_on || !S.mfree) return;  // block-uniform
-    const double avg = S.avgc;
-    const bool safe = avg > 0;
-    const double avgs = safe ? avg : 1.0;
-    auto Q = [&](double sig) { return mu_quality(K, b, S, sig * avg); };
-    const double s1m = 1.0 - max_n(1e-4, K.o.quality_function_section_sigma_tol);
-    const double q1m = Q(s1m), q1 = Q(1.0);
-    const bool up = q1m > q1;  // the quality decreases beyond sigma = 1
-    const double s_hi = up ? clamp_hi(S.mu_max / avgs, K.o.sigma_max) : clamp_lo(K.o.mu_min / avgs, K.o.sigma_min);
-    const double lo = up ? 1.0 : s_hi;
-    const double hi = up ? s_hi : max_n(s_hi, s1m);
-    double q_lo = up ? q1 : -1.0, q_hi = up ? -1.0 : q1m;  // -1: not evaluated
-    double sig;
-    if (lo >= hi) {
-        sig = up ? hi : lo;
-    } else {
-        const double g = (3.0 - sqrt(5.0)) / 2.0;
-        double a = log(lo), bb = log(hi);
-        const double a0 = a, b0 = bb;
-        double m1 = a + g * (bb - a), m2 = a + (1.0 - g) * (bb - a);
-        double qm1 = Q(exp(m1)), qm2 = Q(exp(m2));
-        for (int k = 0; k < K.o.quality_function_max_section_steps; ++k) {
-            double qmin = INFINITY, qmax = -INFINITY;
-            const double qs[4] = {q_lo, q_hi, qm1, qm2};
-            for (int t = 0; t < 4; ++t)
-                if (qs[t] >= 0) qmin = fmin(qmin, qs[t]), qmax = fmax(qmax, qs[t]);
-            if (!(exp(bb) - exp(a) >= K.o.quality_function_section_sigma_tol * exp(bb)) ||
-                !(1.0 - qmin / qmax >= K.o.quality_function_section_qf_tol))
-                break;
-            if (qm1 > qm2) {  // the minimum is in [m1, b]
-                a = m1;
-                q_lo = qm1;
-                m1 = m2;
-                qm1 = qm2;
-                m2 = a + (1.0 - g) * (bb - a);
-                qm2 = Q(exp(m2));
-            } else {
-                bb = m2;
-                q_hi = qm2;
-                m2 = m1;
-                qm2 = qm1;
-                m1 = a + g * (bb - a);
-                qm1 = Q(exp(m1));
-            }
-        }
-        double best = qm1 < qm2 ? m1 : m2;
-        const double qbest = qm1 < qm2 ? qm1 : qm2;
-        const bool hi_end = bb == b0, lo_end = a == a0 && !hi_end;  // an end point never moved competes
-        if (hi_end || lo_end) {
-            double qe = hi_end ? q_hi : q_lo;
-            if (qe < 0) qe = Q(exp(hi_end ? bb : a));
-            if (qe < qbest) best = hi_end ? bb : a;
-        }
-        sig = exp(best);
-    }
-    const double mu = safe ? clamp_lo(min_n(sig * avg, S.mu_max), K.o.mu_min) : K.o.mu_min;
-    __syncthreads();
     double* rb = K.rb + b * K.nKp;
     const double* rc = K.rbc + b * K.nKp;
+    if (K.nf <= 64 * kMuWave && !K.mu_block) {  // wavefront 0 alone (block-uniform branch; the other waves leave)
+        if (threadIdx.x >= 64) return;
+        MuLane E;
+        mu_lane_load(K, b, E);
+        const double mu = mu_section(K, S, [&](double m) { return mu_quality_w(K, E, S, m); });
+        for (int i = threadIdx.x; i < K.nK; i += 64) {
+            const int q = K.pos[i];
+            rb[q] += mu * rc[q];
+        }
+        if (threadIdx.x == 0) {
+            K.sc[b].mu = mu;
+            K.sc[b].tau = clamp_lo(1.0 - mu, K.o.tau_min);
+        }
+        return;
+    }
+    const double mu = mu_section(K, S, [&](double m) { return mu_quality(K, b, S, m); });
+    __syncthreads();
     for (int i = threadIdx.x; i < K.nK; i += kIB) {
         const int q = K.pos[i];
         rb[q] += mu * rc[q];
@@ -1587,19 +1782,28 @@ __global__ void __launch_bounds__(kIB) k_mu_oracle(const IpmK K) {
     store_scal(K, b, S);
 }
 
-// ---- adaptive mu on wide instances (IpmK::wide): k_mu_oracle's golden section as a state machine over rounds of
-// three launches — the candidates' partial step-fraction minima over a grid (k_wmu_min), the partial complementarity
-// sums with every block reducing those minima in wide_get's order (k_wmu_sum), the one-block control step that forms
-// the quality values and advances the section (k_wmu_ctl) — so that a quality evaluation is a grid pass instead of
-// one block's loop over the instance (9.6 ms per call on the reaching task, 65 % of an iteration's kernels).  The
-// decisions are k_mu_oracle's, over the wide path's own deterministic sums.  State [B][kGS] (MG_*); phase 0 nothing to
-// do, 1 the pair Q(s1m), Q(1) pending, 2 the pair Q(e^m1), Q(e^m2), 3 one section point (MG_WHICH 1: m1, 2: m2), 4 the
-// end point, 5 done (k_wmu_apply adds mu rbc to rb).  Rounds after phase 5 return at once.
+// ---- adaptive mu on wide instances (IpmK::wide): the section's requests (MuSec) as rounds of three launches — the
+// candidates' partial step-fraction minima over a grid (k_wmu_min), the partial complementarity sums with every block
+// reducing those minima in wide_get's order (k_wmu_sum), the one-block step of the machine on the quality values
+// (k_wmu_ctl) — so that a quality evaluation is a grid pass instead of one block's loop over the instance (9.6 ms per
+// call on the reaching task, 65 % of an iteration's kernels).  State [B][kGS] (musec_load / musec_store); rounds after
+// the machine's phase 5 return at once, and k_wmu_apply adds mu rbc to rb.
 constexpr int kGS = 24;
-enum {
-    MG_PHASE = 0, MG_NC, MG_C0, MG_C1, MG_A, MG_BB, MG_A0, MG_B0, MG_M1, MG_M2, MG_QM1, MG_QM2, MG_QLO, MG_QHI, MG_K,
-    MG_QBEST, MG_BEST, MG_WHICH, MG_EP, MG_MU
-};
+enum { MG_PHASE = 0, MG_NC, MG_C0, MG_C1, MG_MU };  // MuSec's fields in st[]: these first, the rest after
+__device__ inline MuSec musec_load(const double* st) {
+    MuSec M;
+    M.phase = (int)st[MG_PHASE], M.nc = (int)st[MG_NC], M.c0 = st[MG_C0], M.c1 = st[MG_C1], M.mu = st[MG_MU];
+    M.which = (int)st[5], M.k = (int)st[6], M.a = st[7], M.bb = st[8], M.a0 = st[9], M.b0 = st[10], M.m1 = st[11];
+    M.m2 = st[12], M.qm1 = st[13], M.qm2 = st[14], M.q_lo = st[15], M.q_hi = st[16], M.qbest = st[17], M.best = st[18];
+    M.ep = st[19];
+    return M;
+}
+__device__ inline void musec_store(const MuSec& M, double* st) {
+    st[MG_PHASE] = M.phase, st[MG_NC] = M.nc, st[MG_C0] = M.c0, st[MG_C1] = M.c1, st[MG_MU] = M.mu;
+    st[5] = M.which, st[6] = M.k, st[7] = M.a, st[8] = M.bb, st[9] = M.a0, st[10] = M.b0, st[11] = M.m1;
+    st[12] = M.m2, st[13] = M.qm1, st[14] = M.qm2, st[15] = M.q_lo, st[16] = M.q_hi, st[17] = M.qbest, st[18] = M.best;
+    st[19] = M.ep;
+}
 
 // grid (B, ceil(nK / kIB)): k_mu_cen_rhs elementwise
 __global__ void __launch_bounds__(kIB) k_wmu_cen_rhs(const IpmK K) {
@@ -1619,10 +1823,9 @@ __global__ void __launch_bounds__(kIB) k_wmu_init(const IpmK K) {
         st[MG_PHASE] = 0.0;
         return;
     }
-    st[MG_PHASE] = 1.0;
-    st[MG_NC] = 2.0;
-    st[MG_C0] = 1.0 - max_n(1e-4, K.o.quality_function_section_sigma_tol);
-    st[MG_C1] = 1.0;
+    MuSec M{};
+    musec_start(M, K);
+    musec_store(M, st);
 }
 
 // the candidates' mu = sigma avgc (at most two)
@@ -1760,114 +1963,12 @@ __global__ void __launch_bounds__(kIB) k_wmu_ctl(const IpmK K) {
         Qv[t] = val;
     }
     double* st = K.mgs + b * kGS;
-    const int ph = (int)st[MG_PHASE];
-    const double avg = S.avgc;
-    const bool safe = avg > 0;
-    const double avgs = safe ? avg : 1.0;
-    const double g = (3.0 - sqrt(5.0)) / 2.0;
-    bool fin = false;
-    double sig = 0.0;
-    auto request = [&](double m, int which) {
-        st[MG_NC] = 1.0;
-        st[MG_C0] = exp(m);
-        st[MG_WHICH] = which;
-    };
-    if (ph == 1) {  // Q(1 - sigma_tol), Q(1): which way the quality decreases
-        const double s1m = st[MG_C0], q1m = Qv[0], q1 = Qv[1];
-        const bool up = q1m > q1;
-        const double s_hi = up ? clamp_hi(S.mu_max / avgs, K.o.sigma_max) : clamp_lo(K.o.mu_min / avgs, K.o.sigma_min);
-        const double lo = up ? 1.0 : s_hi;
-        const double hi = up ? s_hi : max_n(s_hi, s1m);
-        st[MG_QLO] = up ? q1 : -1.0;
-        st[MG_QHI] = up ? -1.0 : q1m;
-        if (lo >= hi) {
-            sig = up ? hi : lo;
-            fin = true;
-        } else {
-            const double a = log(lo), bb = log(hi);
-            st[MG_A] = st[MG_A0] = a;
-            st[MG_BB] = st[MG_B0] = bb;
-            st[MG_M1] = a + g * (bb - a);
-            st[MG_M2] = a + (1.0 - g) * (bb - a);
-            st[MG_NC] = 2.0;
-            st[MG_C0] = exp(st[MG_M1]);
-            st[MG_C1] = exp(st[MG_M2]);
-            st[MG_K] = 0.0;
-            st[MG_PHASE] = 2.0;
-        }
-    } else if (ph == 2 || ph == 3) {
-        if (ph == 2) {
-            st[MG_QM1] = Qv[0];
-            st[MG_QM2] = Qv[1];
-        } else {
-            st[(int)st[MG_WHICH] == 1 ? MG_QM1 : MG_QM2] = Qv[0];
-        }
-        double a = st[MG_A], bb = st[MG_BB], m1 = st[MG_M1], m2 = st[MG_M2];
-        double qm1 = st[MG_QM1], qm2 = st[MG_QM2], q_lo = st[MG_QLO], q_hi = st[MG_QHI];
-        const int k = (int)st[MG_K];
-        bool stop = k >= K.o.quality_function_max_section_steps;
-        if (!stop) {
-            double qmin = INFINITY, qmax = -INFINITY;
-            const double qs[4] = {q_lo, q_hi, qm1, qm2};
-            for (int t = 0; t < 4; ++t)
-                if (qs[t] >= 0) qmin = fmin(qmin, qs[t]), qmax = fmax(qmax, qs[t]);
-            stop = !(exp(bb) - exp(a) >= K.o.quality_function_section_sigma_tol * exp(bb)) ||
-                   !(1.0 - qmin / qmax >= K.o.quality_function_section_qf_tol);
-        }
-        if (!stop) {
-            if (qm1 > qm2) {  // the minimum is in [m1, b]
-                a = m1;
-                q_lo = qm1;
-                m1 = m2;
-                qm1 = qm2;
-                m2 = a + (1.0 - g) * (bb - a);
-                request(m2, 2);
-            } else {
-                bb = m2;
-                q_hi = qm2;
-                m2 = m1;
-                qm2 = qm1;
-                m1 = a + g * (bb - a);
-                request(m1, 1);
-            }
-            st[MG_A] = a, st[MG_BB] = bb, st[MG_M1] = m1, st[MG_M2] = m2;
-            st[MG_QM1] = qm1, st[MG_QM2] = qm2, st[MG_QLO] = q_lo, st[MG_QHI] = q_hi;
-            st[MG_K] = k + 1;
-            st[MG_PHASE] = 3.0;
-        } else {
-            double best = qm1 < qm2 ? m1 : m2;
-            const double qbest = qm1 < qm2 ? qm1 : qm2;
-            const bool hi_end = bb == st[MG_B0], lo_end = a == st[MG_A0] && !hi_end;  // an end point never moved
-            if (hi_end || lo_end) {
-                const double qe = hi_end ? q_hi : q_lo, ep = hi_end ? bb : a;
-                if (qe < 0) {
-                    st[MG_BEST] = best;
-                    st[MG_QBEST] = qbest;
-                    st[MG_EP] = ep;
-                    request(ep, 0);
-                    st[MG_PHASE] = 4.0;
-                } else {
-                    if (qe < qbest) best = ep;
-                    sig = exp(best);
-                    fin = true;
-                }
-            } else {
-                sig = exp(best);
-                fin = true;
-            }
-        }
-    } else if (ph == 4) {
-        double best = st[MG_BEST];
-        if (Qv[0] < st[MG_QBEST]) best = st[MG_EP];
-        sig = exp(best);
-        fin = true;
-    }
-    if (fin) {
-        const double m = safe ? clamp_lo(min_n(sig * avg, S.mu_max), K.o.mu_min) : K.o.mu_min;
-        st[MG_MU] = m;
-        st[MG_PHASE] = 5.0;
-        K.sc[b].mu = m;
-        K.sc[b].tau = clamp_lo(1.0 - m, K.o.tau_min);
+    MuSec M = musec_load(st);
+    musec_step(M, K, S, Qv);
+    musec_store(M, st);
+    if (M.phase == 5) {
+        K.sc[b].mu = M.mu;
+        K.sc[b].tau = clamp_lo(1.0 - M.mu, K.o.tau_min);
     }
 }
 
@@ -4288,6 +4389,7 @@ static int ipm_create_common(cfx_ipm* s, const cfx_sizes& sz, int layout, const 
     K.of = dalloc<double>(s, B, &rc);
     K.ab = dalloc<double>(s, B * NE_A, &rc);
     K.wide = s->B <= 16 && (int64_t)nj + nh >= 262144;
+    K.mu_block = std::getenv("CFX_IPM_MU_ORACLE") && std::string(std::getenv("CFX_IPM_MU_ORACLE")) == "block";
     if (const char* e = std::getenv("CFX_IPM_WIDE")) K.wide = std::atoi(e) != 0;  // tuning / A-B override
     K.gj = dalloc<double>(s, B * nf, &rc);
     K.part = dalloc<double>(s, B * kWideParts * 4, &rc);

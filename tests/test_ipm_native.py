@@ -346,6 +346,27 @@ def test_native_ipm_wide_split_kernels_reach_the_same_optimum(B, mu, monkeypatch
     assert np.all(np.abs(b.iterations - a.iterations) <= 5), (a.iterations, b.iterations)
 
 
+@pytest.mark.parametrize("B", [1, 3])
+def test_native_adaptive_mu_oracle_wave_and_block_paths_agree(B, monkeypatch):
+    """The quality-function oracle of small instances runs in one wavefront (registers, no block barriers, shrink rates
+    instead of per-element divisions: its own rounding); CFX_IPM_MU_ORACLE=block runs the whole-block loops that larger
+    instances use.  Both reach cfg 3's optimum under the Ipopt profile, with iteration counts within a few."""
+    from cocofest_amd.solver import IpmOptions, NativeIpm
+
+    ocp = cases.product_ocp(**dict(cases.cfg3(), objective=TRACK))
+    v0 = _starts(ocp, B, 5)
+    out = {}
+    for mode in ("wave", "block"):
+        monkeypatch.setenv("CFX_IPM_MU_ORACLE", mode)
+        nat = NativeIpm(ocp, batch=B, options=IpmOptions.ipopt(tol=1e-8, max_iter=300))
+        out[mode] = nat.solve(v0)
+        nat.close()
+    a, b = out["wave"], out["block"]
+    assert a.converged.all() and b.converged.all(), (a.status, b.status)
+    np.testing.assert_allclose(a.f, b.f, rtol=1e-8, atol=1e-10)
+    assert np.all(np.abs(a.iterations - b.iterations) <= 5), (a.iterations, b.iterations)
+
+
 @pytest.mark.parametrize("case,glob", [(c, "obj-constr-filter") for c in ("cfg3", "hmed", "fatigue_rk4", "cfg2_zero")] +
                          [("cfg3", "never-monotone-mode")])
 def test_native_adaptive_mu_matches_the_specification(case, glob):
