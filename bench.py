@@ -44,6 +44,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline sample budget (0: skip)")
     ap.add_argument("--no-solve", action="store_true", help="skip the wall-clock-to-convergence section")
     ap.add_argument("--no-msk", action="store_true", help="skip the cfg-5 musculoskeletal section")
+    ap.add_argument("--no-multistart", action="store_true", help="skip the cfg-5 512-start restoration-robustness run")
     ap.add_argument("--no-reaching", action="store_true",
                     help="skip the 1,500-interval reaching-task solve (wall-clock to convergence, ~30 s)")
     ap.add_argument("--nmpc-horizons", type=int, default=200, help="cfg-4 NMPC horizons (0: skip)")
@@ -626,7 +627,7 @@ def msk_throughput(local, dist, world, rank, backend, steps=10, B=1 << 16):
     return out, ocp
 
 
-def msk_section(device, tp, ocp1, cpu_seconds=0.0):
+def msk_section(device, tp, ocp1, cpu_seconds=0.0, multistart=True):
     """The N = 1 extras of the cfg-5 section: the C port's CPU baseline on a bounded sample of the same workload,
     and the batched interior point's wall-clock to convergence at RK4 x 5 (the default RK4 x 1 is infeasible for
     Ding2007's tau_c)."""
@@ -641,6 +642,40 @@ def msk_section(device, tp, ocp1, cpu_seconds=0.0):
         ipm.close()
         out[key] = {"wall_s": res.wall_time, "converged": int(res.converged.sum()), "status": int(res.status[0]),
                     "iterations": int(res.iterations.max()), "f": float(res.f[0])}
+    if multistart:
+        out["multistart_512"] = msk_multistart(device)
+    return out
+
+
+def msk_multistart(device, B=512, amp=0.1):
+    """Restoration robustness: cfg 5 at RK4 x 5 from B starts perturbed by +-amp of each free
+    variable's range (capped at 10; seed 0; scripts/msk_multistart_probe.py's starts), max_iter 1000, tol 1e-6, under
+    the facade's Ipopt / bioptim profile, the same with Ipopt's mu_max option at 0.1 (= mu_init: the adaptive update never
+    raises the barrier above its start), and this library's monotone profile."""
+    from cocofest_amd._cfx import IPM_STATUS
+    from cocofest_amd.solver import IpmOptions, NativeIpm
+
+    ocp = msk_build(5)
+    rng = np.random.default_rng(0)
+    v0 = np.tile(ocp.initial_guess_vector(), (B, 1))
+    lb, ub = ocp.bounds_vector()
+    free = lb != ub
+    span = np.minimum(np.where(np.isfinite(ub - lb), ub - lb, 10.0), 10.0)[free]
+    v0[:, free] = np.clip(v0[:, free] + amp * rng.uniform(-1, 1, (B, free.sum())) * span, lb[free], ub[free])
+    out = {"starts": B, "amplitude": amp, "max_iter": 1000}
+    for key, opts in (("ipopt_profile", IpmOptions.ipopt(tol=1e-6, max_iter=1000)),
+                      ("ipopt_profile_mu_max_0.1", IpmOptions.ipopt(tol=1e-6, max_iter=1000, mu_max=0.1)),
+                      ("library_profile", IpmOptions(tol=1e-6, max_iter=1000))):
+        ipm = NativeIpm(ocp, batch=B, device=device, options=opts)
+        res = ipm.solve(v0)
+        ipm.close()
+        conv = res.converged.astype(bool)
+        hist = {}
+        for st in res.status:
+            k = IPM_STATUS.get(int(st), str(int(st)))
+            hist[k] = hist.get(k, 0) + 1
+        out[key] = {"converged": int(conv.sum()), "rate": float(conv.mean()), "status": hist, "wall_s": res.wall_time,
+                    "f_converged": [float(res.f[conv].min()), float(res.f[conv].max())] if conv.any() else None}
     return out
 
 
@@ -804,7 +839,7 @@ def main():
         reach = reaching_section(local) if (world == 1 and not args.no_solve and not args.no_reaching) else None
         msk = msk_tp
         if msk_tp is not None and world == 1 and not args.no_solve:
-            msk = msk_section(local, msk_tp, msk_ocp, cpu_seconds=args.cpu_seconds / 2)
+            msk = msk_section(local, msk_tp, msk_ocp, cpu_seconds=args.cpu_seconds / 2, multistart=not args.no_multistart)
         out = {
             "metric": METRIC,
             "value": value,

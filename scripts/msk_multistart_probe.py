@@ -34,6 +34,10 @@ ap.add_argument("--soft", type=float, default=None, help="soft_resto_pderror_red
 ap.add_argument("--restart", action="store_true", help="resto_failure_restart (extension: a failed phase restarts)")
 ap.add_argument("--opt", action="append", default=[], help="extra IpmOptions key=value (repeatable)")
 ap.add_argument("--label", default="")
+ap.add_argument("--dump", default=None, help="save every start's status / iterations / f of the last run here (.npz)")
+ap.add_argument("--first", type=int, default=None,
+                help="swap start FIRST with start 0 (CFX_IPM_TRACE=1 traces instance 0; the batch, and so the KKT "
+                     "layout and every instance's path, is otherwise unchanged)")
 ap.add_argument("--profile", default="cfx", choices=["cfx", "ipopt"],
                 help="ipopt: the facade's Ipopt / bioptim profile (IpmOptions.ipopt) under the options above")
 args = ap.parse_args()
@@ -47,6 +51,8 @@ for B, amp in runs:
     free = lb != ub
     span = np.minimum(np.where(np.isfinite(ub - lb), ub - lb, 10.0), 10.0)[free]
     v0[:, free] = np.clip(v0[:, free] + amp * rng.uniform(-1, 1, (B, free.sum())) * span, lb[free], ub[free])
+    if args.first is not None:
+        v0[[0, args.first]] = v0[[args.first, 0]]
     cls = NativeIpm if args.native else BatchedIpm
     extra = {} if args.soft is None else {"soft_resto_pderror_reduction_factor": args.soft}
     if args.restart:
@@ -74,6 +80,9 @@ for B, amp in runs:
                restart=opts.resto_failure_restart,
                soft_steps=getattr(ipm, "soft_steps", st.get("soft_steps")))
     print(json.dumps(rec), flush=True)
+    if args.dump:
+        np.savez(args.dump, status=res.status, iterations=res.iterations, f=res.f, converged=res.converged,
+                 kkt_error=res.kkt_error)
     if args.jsonl:
         with open(args.jsonl, "a") as fh:
             fh.write(json.dumps(rec) + "\n")
