@@ -13,17 +13,36 @@
 
 namespace cfx_inertia {
 
-// max |v| over the 64 lanes with its lane-supplied index (ties to the lowest index); every lane gets both
+// The largest of the 64 lanes' non-negative candidates v (each with its row idx), ties to the lowest row; every lane
+// gets both.  Two DPP reductions (the maximum, then the lowest row holding it) instead of a shuffle butterfly of
+// pairs (__shfl_xor is an LDS permute per step).  A NaN candidate never wins (as `v > best` comparisons).
+#define CFX_INERTIA_DPP(x, OP, ID, CTRL, RM, BM)                                                                  \
+    do {                                                                                                         \
+        const int slo_ = __builtin_amdgcn_update_dpp(__double2loint(ID), __double2loint(x), CTRL, RM, BM, false);  \
+        const int shi_ = __builtin_amdgcn_update_dpp(__double2hiint(ID), __double2hiint(x), CTRL, RM, BM, false);  \
+        x = OP(x, __hiloint2double(shi_, slo_));                                                                  \
+    } while (0)
+__device__ __forceinline__ double inertia_wave_max(double x) {
+    CFX_INERTIA_DPP(x, fmax, -1.0, 0x111, 0xf, 0xf);
+    CFX_INERTIA_DPP(x, fmax, -1.0, 0x112, 0xf, 0xf);
+    CFX_INERTIA_DPP(x, fmax, -1.0, 0x114, 0xf, 0xf);
+    CFX_INERTIA_DPP(x, fmax, -1.0, 0x118, 0xf, 0xf);
+    CFX_INERTIA_DPP(x, fmax, -1.0, 0x142, 0xa, 0xf);
+    CFX_INERTIA_DPP(x, fmax, -1.0, 0x143, 0xc, 0xf);
+    return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(x), 63), __builtin_amdgcn_readlane(__double2loint(x), 63));
+}
 __device__ __forceinline__ void wave_argmax(double& v, int& idx) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        const double v2 = __shfl_xor(v, o, 64);
-        const int i2 = __shfl_xor(idx, o, 64);
-        if (v2 > v || (v2 == v && i2 < idx)) {
-            v = v2;
-            idx = i2;
-        }
-    }
+    const double best = inertia_wave_max(v == v ? v : -1.0);
+    double r = (v == best) ? (double)idx : 1e9;  // rows are small integers: exact in a double
+    CFX_INERTIA_DPP(r, fmin, 1e9, 0x111, 0xf, 0xf);
+    CFX_INERTIA_DPP(r, fmin, 1e9, 0x112, 0xf, 0xf);
+    CFX_INERTIA_DPP(r, fmin, 1e9, 0x114, 0xf, 0xf);
+    CFX_INERTIA_DPP(r, fmin, 1e9, 0x118, 0xf, 0xf);
+    CFX_INERTIA_DPP(r, fmin, 1e9, 0x142, 0xa, 0xf);
+    CFX_INERTIA_DPP(r, fmin, 1e9, 0x143, 0xc, 0xf);
+    const double rr = __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(r), 63), __builtin_amdgcn_readlane(__double2loint(r), 63));
+    v = best;
+    idx = (int)rr;
 }
 
 // Negative eigenvalues of the symmetric n x n matrix A (LDS, row stride ld, n <= 128; destroyed), by the whole
@@ -82,15 +101,26 @@ __device__ __forceinline__ int sym_neg_count(double* A, int ld, int n) {
             }
             __syncthreads();
         }
-        const int m = n - k - s;
+        // the trailing update: thread (ty, tx) of a 16 x 16 grid (nt = 256) takes rows k + s + ty + 16 u and columns
+        // k + s + tx + 16 w, so no element index is divided (generic blocks: one element per thread and stride)
+        const int k0 = k + s, m = n - k0;
+        const bool grid16 = nt == 256;
+        const int tx = t & 15, ty = t >> 4;
         if (s == 1) {
             const double d = A[k * ld + k];
             if (t == 0) ctl[2] += d < 0.0 ? 1 : (d == 0.0 ? kZeroPivot : 0);
             if (d != 0.0) {
                 const double inv = 1.0 / d;
-                for (int e = t; e < m * m; e += nt) {
-                    const int i = k + 1 + e / m, j = k + 1 + e % m;
-                    A[i * ld + j] = fma(-A[i * ld + k] * inv, A[k * ld + j], A[i * ld + j]);
+                if (grid16) {
+                    for (int i = k0 + ty; i < n; i += 16) {
+                        const double f = -A[i * ld + k] * inv;
+                        for (int j = k0 + tx; j < n; j += 16) A[i * ld + j] = fma(f, A[k * ld + j], A[i * ld + j]);
+                    }
+                } else {
+                    for (int e = t; e < m * m; e += nt) {
+                        const int i = k0 + e / m, j = k0 + e % m;
+                        A[i * ld + j] = fma(-A[i * ld + k] * inv, A[k * ld + j], A[i * ld + j]);
+                    }
                 }
             }
         } else {
@@ -99,11 +129,21 @@ __device__ __forceinline__ int sym_neg_count(double* A, int ld, int n) {
             if (t == 0) ctl[2] += det < 0.0 ? 1 : (det == 0.0 ? kZeroPivot : (a + c < 0.0 ? 2 : 0));
             if (det != 0.0) {
                 const double id = 1.0 / det;
-                for (int e = t; e < m * m; e += nt) {
-                    const int i = k + 2 + e / m, j = k + 2 + e % m;
-                    const double li0 = A[i * ld + k], li1 = A[i * ld + k + 1];
-                    const double w0 = (c * li0 - b * li1) * id, w1 = (a * li1 - b * li0) * id;  // [li0 li1] E^-1
+                auto upd = [&](int i, int j, double w0, double w1) {
                     A[i * ld + j] -= w0 * A[k * ld + j] + w1 * A[(k + 1) * ld + j];
+                };
+                if (grid16) {
+                    for (int i = k0 + ty; i < n; i += 16) {
+                        const double li0 = A[i * ld + k], li1 = A[i * ld + k + 1];
+                        const double w0 = (c * li0 - b * li1) * id, w1 = (a * li1 - b * li0) * id;  // [li0 li1] E^-1
+                        for (int j = k0 + tx; j < n; j += 16) upd(i, j, w0, w1);
+                    }
+                } else {
+                    for (int e = t; e < m * m; e += nt) {
+                        const int i = k0 + e / m, j = k0 + e % m;
+                        const double li0 = A[i * ld + k], li1 = A[i * ld + k + 1];
+                        upd(i, j, (c * li0 - b * li1) * id, (a * li1 - b * li0) * id);
+                    }
                 }
             }
         }
