@@ -1241,12 +1241,13 @@ __global__ void __launch_bounds__(kIB) k_wdir_c(const IpmK K) {
 }
 
 // k_ipm_accept's ||c(x_t)||_1 and the barrier terms at the trial point
-__global__ void __launch_bounds__(kIB) k_wacc_a(const IpmK K) {
+// (soc: the second-order-corrected trial in xr, for k_ipm_soc_accept)
+__global__ void __launch_bounds__(kIB) k_wacc_a(const IpmK K, int soc) {
     const int64_t b = blockIdx.x;
     if (K.sc[b].rs_on) return;
     const int nf = K.nf, m = K.m;
     const double mu = K.sc[b].mu, smin = slack_min(mu);
-    const double* xt = K.xt + b * nf;
+    const double* xt = (soc ? K.xr : K.xt) + b * nf;
     const double* lbI = K.lbI + b * nf;
     const double* ubI = K.ubI + b * nf;
     double tt = 0.0, sL = 0.0, sU = 0.0, bad = 0.0;
@@ -1279,6 +1280,82 @@ __global__ void __launch_bounds__(kIB) k_wacc_c(const IpmK K) {
     const int i = blockIdx.y * kIB + threadIdx.x;
     if (wf[1] != 0.0 && i < m) K.csoc[b * m + i] = wf[3] * K.gS[b * m + i] + K.gt[b * m + i] * K.sg[b * m + i];
     if (wf[2] != 0.0 && i < nf) K.xacc[b * nf + i] = K.xt[b * nf + i];
+}
+
+// the line search's backtracking and second-order corrections on wide instances (their one-block kernels loop over the
+// instance: k_ipm_next_trial 86 us, k_ipm_soc_trial 0.66 ms, k_ipm_soc_accept 0.51 ms, k_ipm_soc_rhs 0.30 ms per call
+// on the reaching task, ~1.3 ms of an iteration under the Ipopt profile)
+// grid (B, ceil(nf / kIB)): k_ipm_next_trial's trial x + (alpha / 2) dx; k_wnext_b halves alpha after it
+__global__ void __launch_bounds__(kIB) k_wnext_a(const IpmK K) {
+    const int64_t b = blockIdx.x;
+    if (K.sc[b].accepted || K.sc[b].rs_on) return;
+    const int nf = K.nf, i = blockIdx.y * kIB + threadIdx.x;
+    if (i >= nf) return;
+    const double a = K.sc[b].alpha * 0.5;
+    const double xt = K.x[b * nf + i] + a * K.dx[b * nf + i];
+    K.xt[b * nf + i] = xt;
+    K.vt[b * K.n + K.free[i]] = xt * K.d[i];
+}
+__global__ void __launch_bounds__(kIB) k_wnext_b(const IpmK K) {
+    const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= K.B || K.sc[b].accepted || K.sc[b].rs_on) return;
+    K.sc[b].alpha = K.sc[b].alpha * 0.5;
+}
+// grid (B, ceil(nK / kIB)): k_ipm_soc_rhs elementwise
+__global__ void __launch_bounds__(kIB) k_wsoc_rhs(const IpmK K) {
+    const int64_t b = blockIdx.x;
+    if (K.sc[b].rs_on) return;
+    const int nf = K.nf, i = blockIdx.y * kIB + threadIdx.x;
+    if (i >= K.nK) return;
+    const double a = K.sc[b].alpha, mu = K.sc[b].mu;
+    const double rx = i < nf ? (K.adapt ? K.rhs[b * K.nK + i] + mu * K.rhsmu[b * nf + i] : K.rhs[b * K.nK + i]) : 0.0;
+    K.rb[b * K.nKp + K.pos[i]] = i < nf ? rx * a : -K.csoc[b * K.m + (i - nf)];
+}
+// k_ipm_soc_trial: partial fractions to the boundary of the corrected step (grid (B, kWideParts)), then every block of
+// a grid over the variables reduces them (the same a_c in each) and forms its part of the trial
+__global__ void __launch_bounds__(kIB) k_wsoct_a(const IpmK K) {
+    const int64_t b = blockIdx.x;
+    if (K.sc[b].rs_on) return;
+    const int nf = K.nf;
+    const double* x = K.x + b * nf;
+    const double* rb = K.rb + b * K.nKp;
+    const double tau = K.sc[b].tau;
+    const double* lbI = K.lbI + b * nf;
+    const double* ubI = K.ubI + b * nf;
+    double apl = INFINITY, apu = INFINITY;
+    WIDE_LOOP(i, nf) {
+        const double d = rb[K.pos[i]];
+        if (K.hasL[i]) apl = min_n(apl, step_term(true, x[i] - lbI[i], d, tau));
+        if (K.hasU[i]) apu = min_n(apu, step_term(true, ubI[i] - x[i], -d, tau));
+    }
+    double rv[2] = {apl, apu};
+    const int ro[2] = {2, 2};
+    wide_put(K, b, rv, ro);
+}
+__global__ void __launch_bounds__(kIB) k_wsoct_c(const IpmK K) {
+    const int64_t b = blockIdx.x;
+    if (K.sc[b].rs_on) return;  // (block-uniform)
+    double rv[2];
+    const int ro[2] = {2, 2};
+    wide_get(K, b, rv, ro);
+    const double a_c = min_n(clamp_hi(rv[0], 1.0), clamp_hi(rv[1], 1.0));
+    const int nf = K.nf, i = blockIdx.y * kIB + threadIdx.x;
+    if (i < nf) {
+        const double xr = K.x[b * nf + i] + a_c * K.rb[b * K.nKp + K.pos[i]];
+        K.xr[b * nf + i] = xr;
+        K.vt[b * K.n + K.free[i]] = xr * K.d[i];
+    }
+    if (blockIdx.y == 0 && threadIdx.x == 0) K.sc[b].a_c = a_c;
+}
+// k_ipm_soc_accept's elementwise part: the correction's constraint values (wflag[1]) and the accepted point (wflag[2])
+__global__ void __launch_bounds__(kIB) k_wsoca_c(const IpmK K) {
+    const int64_t b = blockIdx.x;
+    const double* wf = K.wflag + b * kWF;
+    if (wf[0] == 0.0) return;
+    const int nf = K.nf, m = K.m;
+    const int i = blockIdx.y * kIB + threadIdx.x;
+    if (wf[1] != 0.0 && i < m) K.csoc[b * m + i] = wf[3] * K.csoc[b * m + i] + K.gt[b * m + i] * K.sg[b * m + i];
+    if (wf[2] != 0.0 && i < nf) K.xacc[b * nf + i] = K.xr[b * nf + i];
 }
 
 // k_ipm_update's non-finite checks of the step
@@ -2245,21 +2322,39 @@ __global__ void __launch_bounds__(kIB) k_ipm_soc_accept(const IpmK K, int slot) 
     }
     const double* sg = K.sg + b * m;
     const double* gt = K.gt + b * m;
-    double tt = 0.0;
-    for (int j = threadIdx.x; j < m; j += kIB) tt += fabs(gt[j] * sg[j]);
-    tt = breduce(tt, OpSum(), sh);
+    double tt = 0.0, pt;
     const double* xr = K.xr + b * nf;
-    const double pt = barrier_obj(K, b, xr, K.ft[b] * S.sf, S.mu, sh);
+    if (K.wide) {  // k_wacc_a's partials (soc = 1)
+        double rv[4];
+        const int ro[4] = {0, 0, 0, 1};
+        wide_get(K, b, rv, ro);
+        tt = rv[0];
+        pt = rv[3] > 0 ? INFINITY : K.ft[b] * S.sf - S.mu * (rv[1] + rv[2]);
+    } else {
+        for (int j = threadIdx.x; j < m; j += kIB) tt += fabs(gt[j] * sg[j]);
+        tt = breduce(tt, OpSum(), sh);
+        pt = barrier_obj(K, b, xr, K.ft[b] * S.sf, S.mu, sh);
+    }
     bool okc, armc, rejfc;
     filter_accept(K, S, K.filt + b * kFilt * 2, tt, pt, S.alpha, sh, okc, armc, &rejfc);
     const bool rej_here = rejfc && S.soc && !S.accepted;
     okc = okc && S.soc && (S.a_c >= 0.99);
-    if (okc) {
-        double* xacc = K.xacc + b * nf;
-        for (int i = threadIdx.x; i < nf; i += kIB) xacc[i] = xr[i];
+    if (K.wide) {  // (k_wsoca_c)
+        if (threadIdx.x == 0) {
+            double* wf = K.wflag + b * kWF;
+            wf[0] = 1.0;
+            wf[1] = 1.0;
+            wf[2] = okc;
+            wf[3] = S.a_c;
+        }
+    } else {
+        if (okc) {
+            double* xacc = K.xacc + b * nf;
+            for (int i = threadIdx.x; i < nf; i += kIB) xacc[i] = xr[i];
+        }
+        double* cs = K.csoc + b * m;
+        for (int j = threadIdx.x; j < m; j += kIB) cs[j] = S.a_c * cs[j] + gt[j] * sg[j];
     }
-    double* cs = K.csoc + b * m;
-    for (int j = threadIdx.x; j < m; j += kIB) cs[j] = S.a_c * cs[j] + gt[j] * sg[j];
     __syncthreads();
     if (threadIdx.x == 0) {
         if (okc) {
@@ -4573,6 +4668,7 @@ struct Run {
     }
     // wide instances: the partials grid and the elementwise grid of the split kernels
     dim3 wa() const { return dim3((unsigned)s->K.B, kWideParts); }
+    dim3 wk() const { return dim3((unsigned)s->K.B, (unsigned)((s->K.nK + kIB - 1) / kIB)); }
     dim3 wc() const {
         const int64_t n = std::max<int64_t>(s->K.nf, s->K.m);
         return dim3((unsigned)s->K.B, (unsigned)((n + kIB - 1) / kIB));
@@ -4847,7 +4943,7 @@ static int ipm_solve(cfx_ipm* s, const double* v0, const double* fixed_values, d
             IPM_RUN(R.eval_gf(true));
             int sl = R.next_slot();
             if (K.rsphase && rs_live) hipLaunchKernelGGL(k_rs_accept, R.g, blk, 0, st, K);
-            if (K.wide) hipLaunchKernelGGL(k_wacc_a, R.wa(), blk, 0, st, K);
+            if (K.wide) hipLaunchKernelGGL(k_wacc_a, R.wa(), blk, 0, st, K, 0);
             hipLaunchKernelGGL(k_ipm_accept, R.g, blk, 0, st, K, ls, sl);
             if (K.wide) hipLaunchKernelGGL(k_wacc_c, R.wc(), blk, 0, st, K);
             IPM_HIP(s, hipGetLastError());
@@ -4856,19 +4952,32 @@ static int ipm_solve(cfx_ipm* s, const double* v0, const double* fixed_values, d
             if (ls == 0) n_soft = c[2];
             if (ls == 0)
                 for (int q = 0; q < K.o.max_soc && c[1] > 0; ++q) {
-                    hipLaunchKernelGGL(k_ipm_soc_rhs, R.g, blk, 0, st, K);
+                    if (K.wide) hipLaunchKernelGGL(k_wsoc_rhs, R.wk(), blk, 0, st, K);
+                    else hipLaunchKernelGGL(k_ipm_soc_rhs, R.g, blk, 0, st, K);
                     IPM_RUN(R.resolve());
                     if (K.lbfgs) hipLaunchKernelGGL(k_lbfgs_apply, R.g, blk, 0, st, K);
-                    hipLaunchKernelGGL(k_ipm_soc_trial, R.g, blk, 0, st, K);
+                    if (K.wide) {
+                        hipLaunchKernelGGL(k_wsoct_a, R.wa(), blk, 0, st, K);
+                        hipLaunchKernelGGL(k_wsoct_c, R.wc(), blk, 0, st, K);
+                    } else {
+                        hipLaunchKernelGGL(k_ipm_soc_trial, R.g, blk, 0, st, K);
+                    }
                     IPM_RUN(R.eval_gf(true));
                     sl = R.next_slot();
+                    if (K.wide) hipLaunchKernelGGL(k_wacc_a, R.wa(), blk, 0, st, K, 1);
                     hipLaunchKernelGGL(k_ipm_soc_accept, R.g, blk, 0, st, K, sl);
+                    if (K.wide) hipLaunchKernelGGL(k_wsoca_c, R.wc(), blk, 0, st, K);
                     IPM_HIP(s, hipGetLastError());
                     IPM_RUN(R.read(sl, c));
                     notacc = c[0];
                 }
             if (notacc == 0) break;
-            hipLaunchKernelGGL(k_ipm_next_trial, R.g, blk, 0, st, K);
+            if (K.wide) {
+                hipLaunchKernelGGL(k_wnext_a, R.wc(), blk, 0, st, K);
+                hipLaunchKernelGGL(k_wnext_b, dim3((unsigned)((K.B + kIB - 1) / kIB)), blk, 0, st, K);
+            } else {
+                hipLaunchKernelGGL(k_ipm_next_trial, R.g, blk, 0, st, K);
+            }
             if (K.rsphase && rs_live) hipLaunchKernelGGL(k_rs_next_trial, R.g, blk, 0, st, K);
         }
         // Ipopt's soft restoration: the failed searches and the instances taking soft steps try the step at the
