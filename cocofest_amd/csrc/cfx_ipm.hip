@@ -1425,6 +1425,95 @@ __global__ void __launch_bounds__(kIB) k_wupd_c(const IpmK K) {
         K.ysc[e] = yv * K.sg[e];
     }
 }
+// ---- wide instances in the restoration phase: k_rs_begin's loops over the instance as grids (one block's loops over the
+// reaching task's 2.4 M J_g values and 10^5 variables were ~7 ms per call)
+// grid (B, ceil(max(nj, m) / kIB)): the scaled constraint values and J_g values of the phase's instances
+__global__ void __launch_bounds__(kIB) k_wrs_scale(const IpmK K) {
+    const int64_t b = blockIdx.x;
+    if (!K.sc[b].rs_on || K.sc[b].rs_exit != RS_RUNNING) return;
+    const int64_t p = (int64_t)blockIdx.y * kIB + threadIdx.x;
+    const int m = K.m;
+    const double* sg = K.sg + b * m;
+    if (p < K.nj) K.jv[b * K.nj + p] = K.jac[b * K.nnzj + K.jsel[p]] * K.d[K.jc[p]] * sg[K.jr[p]];
+    if (p < m) K.gS[b * m + p] = K.graw[b * m + p] * sg[p];
+}
+// grid (B, kWideParts): J^T y into rhs (k_rs_begin's sum in its order), the phase's dual and primal errors, and the
+// extremes of its complementarity products, from which max_i |p_i - mu| follows exactly for any mu
+__global__ void __launch_bounds__(kIB) k_wrs_a(const IpmK K) {
+    const int64_t b = blockIdx.x;
+    if (!K.sc[b].rs_on || K.sc[b].rs_exit != RS_RUNNING) return;
+    const int nf = K.nf, m = K.m;
+    const double rho = K.o.resto_penalty, mu = K.sc[b].rs_mu;
+    const double* jv = K.jv + b * K.nj;
+    const double* x = K.xr + b * nf;
+    const double* xref = K.x + b * nf;
+    const double* zl = K.rzl + b * nf;
+    const double* zu = K.rzu + b * nf;
+    const double* lbI = K.lbI + b * nf;
+    const double* ubI = K.ubI + b * nf;
+    const double* p = K.rp + b * m;
+    const double* nn = K.rn + b * m;
+    const double* zp = K.rzp + b * m;
+    const double* zn = K.rzn + b * m;
+    const double* y = K.ry + b * m;
+    const double* gS = K.gS + b * m;
+    double* rhs = K.rhs + b * K.nK;
+    double ed = 0.0, ep = 0.0, pmax = -INFINITY, pmin = INFINITY;
+    WIDE_LOOP(i, nf) {
+        double jty = 0.0;
+#pragma unroll 4
+        for (int k = K.jt_ptr[i]; k < K.jt_ptr[i + 1]; ++k) {
+            const int q = K.jt_idx[k];
+            jty += jv[q] * y[K.jr[q]];
+        }
+        rhs[i] = jty;
+        ed = max_n(ed, fabs(rs_weight(mu, xref[i]) * (x[i] - xref[i]) + jty - zl[i] + zu[i]));
+        if (K.hasL[i]) {
+            const double pr = (x[i] - lbI[i]) * zl[i];
+            pmax = max_n(pmax, pr), pmin = min_n(pmin, pr);
+        }
+        if (K.hasU[i]) {
+            const double pr = (ubI[i] - x[i]) * zu[i];
+            pmax = max_n(pmax, pr), pmin = min_n(pmin, pr);
+        }
+    }
+    WIDE_LOOP(j, m) {
+        ep = max_n(ep, fabs(gS[j] - p[j] + nn[j]));
+        ed = max_n(ed, max_n(fabs(rho - y[j] - zp[j]), fabs(rho + y[j] - zn[j])));
+        const double pp = p[j] * zp[j], pn = nn[j] * zn[j];
+        pmax = max_n(pmax, max_n(pp, pn)), pmin = min_n(pmin, min_n(pp, pn));
+    }
+    double rv[4] = {ed, ep, pmax, pmin};
+    const int ro[4] = {1, 1, 1, 2};
+    wide_put(K, b, rv, ro);
+}
+// grid (B, ceil(max(nf, m) / kIB)): k_rs_begin's Newton system of the phase at its final mu (instances it kept going)
+__global__ void __launch_bounds__(kIB) k_wrs_c(const IpmK K) {
+    const int64_t b = blockIdx.x;
+    if (!K.sc[b].rs_on || K.sc[b].rs_exit != RS_RUNNING) return;
+    const int nf = K.nf, m = K.m, i = blockIdx.y * kIB + threadIdx.x;
+    const double rho = K.o.resto_penalty, mu = K.sc[b].rs_mu;
+    double* rhs = K.rhs + b * K.nK;
+    if (i < nf) {
+        const int64_t e = b * nf + i;
+        const double xi = K.xr[e], xref = K.x[e];
+        const bool hL = K.hasL[i], hU = K.hasU[i];
+        const double sl = hL ? xi - K.lbI[e] : 1.0, su = hU ? K.ubI[e] - xi : 1.0;
+        K.sig[e] = (hL ? K.rzl[e] / sl : 0.0) + (hU ? K.rzu[e] / su : 0.0);
+        const double bar = (hL ? mu / sl : 0.0) - (hU ? mu / su : 0.0);
+        rhs[i] = -(rs_weight(mu, xref) * (xi - xref) + rhs[i] - bar);
+    }
+    if (i < m) {
+        const int64_t e = b * m + i;
+        const double p = K.rp[e], nn = K.rn[e], y = K.ry[e];
+        const double Sp = K.rzp[e] / p, Sn = K.rzn[e] / nn;
+        const double ap = mu / p - rho + y, an = mu / nn - rho - y;
+        rhs[nf + i] = -(K.gS[e] - p + nn) + ap / Sp - an / Sn;
+        K.rdc[e] = -(1.0 / Sp + 1.0 / Sn);
+        K.ysc[e] = y * K.sg[e];
+    }
+}
+
 #undef WIDE_LOOP
 
 // Newton step in natural order and the curvature test (solver.py inertia loop); bumps dw where it fails.  An instance
@@ -2951,9 +3040,11 @@ __global__ void __launch_bounds__(kIB) k_rs_begin(const IpmK K) {
     double* gS = K.gS + b * m;
     double* jv = K.jv + b * K.nj;
     const double* jac = K.jac + b * K.nnzj;
-    for (int j = threadIdx.x; j < m; j += kIB) gS[j] = K.graw[b * m + j] * sg[j];
+    if (!K.wide) {  // (wide: k_wrs_scale)
+        for (int j = threadIdx.x; j < m; j += kIB) gS[j] = K.graw[b * m + j] * sg[j];
 #pragma unroll 8
-    for (int q = threadIdx.x; q < K.nj; q += kIB) jv[q] = jac[K.jsel[q]] * K.d[K.jc[q]] * sg[K.jr[q]];
+        for (int q = threadIdx.x; q < K.nj; q += kIB) jv[q] = jac[K.jsel[q]] * K.d[K.jc[q]] * sg[K.jr[q]];
+    }
     __syncthreads();
     const double* x = K.xr + b * nf;
     const double* xref = K.x + b * nf;
@@ -2967,7 +3058,13 @@ __global__ void __launch_bounds__(kIB) k_rs_begin(const IpmK K) {
     const double* zn = K.rzn + b * m;
     const double* y = K.ry + b * m;
     double* rhs = K.rhs + b * K.nK;
-    double ed = 0.0, ep = 0.0;
+    double ed = 0.0, ep = 0.0, pmax = -INFINITY, pmin = INFINITY;
+    if (K.wide) {  // k_wrs_a's partials
+        double rv[4];
+        const int ro[4] = {1, 1, 1, 2};
+        wide_get(K, b, rv, ro);
+        ed = rv[0], ep = rv[1], pmax = rv[2], pmin = rv[3];
+    } else {
     for (int i = threadIdx.x; i < nf; i += kIB) {
         double jty = 0.0;
 #pragma unroll 4
@@ -2989,11 +3086,15 @@ __global__ void __launch_bounds__(kIB) k_rs_begin(const IpmK K) {
         ed = rv[0];
         ep = rv[1];
     }
+    }
     // the phase's monotone barrier update (the main loop's rule, on its unscaled errors)
     double e_mu = INFINITY;
     for (int pass = 0; pass < 5; ++pass) {
         const double mu = S.rs_mu;
         double ecm = 0.0;
+        if (K.wide) {  // max_i |p_i - mu| = max(p_max - mu, mu - p_min), exactly (fl(p - mu) is monotone in p)
+            ecm = max_n(max_n(ecm, pmax - mu), mu - pmin);
+        } else {
         for (int i = threadIdx.x; i < nf; i += kIB) {
             if (K.hasL[i]) ecm = max_n(ecm, fabs((x[i] - lbI[i]) * zl[i] - mu));
             if (K.hasU[i]) ecm = max_n(ecm, fabs((ubI[i] - x[i]) * zu[i] - mu));
@@ -3001,6 +3102,7 @@ __global__ void __launch_bounds__(kIB) k_rs_begin(const IpmK K) {
         for (int j = threadIdx.x; j < m; j += kIB)
             ecm = max_n(ecm, max_n(fabs(p[j] * zp[j] - mu), fabs(nn[j] * zn[j] - mu)));
         ecm = breduce(ecm, OpMax(), sh);
+        }
         e_mu = max_n(max_n(ed, ep), ecm);
         if (!((e_mu <= K.o.kappa_eps * mu) && (mu > K.o.tol / 10))) break;
         __syncthreads();
@@ -3017,6 +3119,7 @@ __global__ void __launch_bounds__(kIB) k_rs_begin(const IpmK K) {
         return;
     }
     double* sig = K.sig + b * nf;
+    if (!K.wide)  // (wide: k_wrs_c)
     for (int i = threadIdx.x; i < nf; i += kIB) {
         const bool hL = K.hasL[i], hU = K.hasU[i];
         const double sl = hL ? x[i] - lbI[i] : 1.0, su = hU ? ubI[i] - x[i] : 1.0;
@@ -3024,6 +3127,7 @@ __global__ void __launch_bounds__(kIB) k_rs_begin(const IpmK K) {
         const double bar = (hL ? mu / sl : 0.0) - (hU ? mu / su : 0.0);
         rhs[i] = -(rs_weight(mu, xref[i]) * (x[i] - xref[i]) + rhs[i] - bar);
     }
+    if (!K.wide)
     for (int j = threadIdx.x; j < m; j += kIB) {
         const double Sp = zp[j] / p[j], Sn = zn[j] / nn[j];
         const double ap = mu / p[j] - rho + y[j], an = mu / nn[j] - rho - y[j];
@@ -4900,7 +5004,15 @@ static int ipm_solve(cfx_ipm* s, const double* v0, const double* fixed_values, d
         } else {
             IPM_RUN(R.begin(1, R.next_slot()));
         }
-        if (K.rsphase && rs_live) hipLaunchKernelGGL(k_rs_begin, R.g, blk, 0, st, K);
+        if (K.rsphase && rs_live) {
+            if (K.wide) {
+                const int64_t nsc = std::max<int64_t>(K.nj, K.m);
+                hipLaunchKernelGGL(k_wrs_scale, dim3((unsigned)K.B, (unsigned)((nsc + kIB - 1) / kIB)), blk, 0, st, K);
+                hipLaunchKernelGGL(k_wrs_a, R.wa(), blk, 0, st, K);
+            }
+            hipLaunchKernelGGL(k_rs_begin, R.g, blk, 0, st, K);
+            if (K.wide) hipLaunchKernelGGL(k_wrs_c, R.wc(), blk, 0, st, K);
+        }
         reinit = false;
         IPM_HIP(s, hipGetLastError());
         if (K.lbfgs) {  // quasi-Newton pair of the last step, M (no eval_h: hv stays zero)
