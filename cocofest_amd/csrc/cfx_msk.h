@@ -1742,6 +1742,9 @@ __global__ void __launch_bounds__(256) k_msk_hproj(const MskParams P, const doub
 // thread, so the latency is one double recursion plus one Dual stage.  Small batches also split the Hessian
 // projection: k_msk_hproj_stage gives every (stage, column) its own thread and k_msk_hproj_sum adds the stages up in
 // the order k_msk_hproj does.
+// Small batches (msk_values_grid: B below one block) take a flat grid, thread = (interval, instance) with the instances
+// fastest, so a wavefront carries 64 intervals instead of one live lane per block (the reaching task at batch 1: 1,500
+// single-lane blocks); every thread runs the same code on the same data either way.
 template <int NQ, int NM, int FAM, int SCHEME>
 __global__ void __launch_bounds__(256) k_msk_values(const MskParams P, const MskGeom* __restrict__ GG,
                                                     const double* __restrict__ V, double* __restrict__ Gout,
@@ -1750,9 +1753,11 @@ __global__ void __launch_bounds__(256) k_msk_values(const MskParams P, const Msk
     constexpr int NUMAX = msk_numax<NQ, NM, FAM>();
     constexpr int ST = SCHEME == 4 ? 4 : (SCHEME == 2 ? 2 : 1);
     const int64_t B = P.B;
-    const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (b >= B) return;
-    const int k = blockIdx.y;
+    const bool flat = gridDim.y == 1 && P.N > 1;  // (msk_values_grid)
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t b = flat ? e % B : e;
+    const int k = flat ? (int)(e / B) : (int)blockIdx.y;
+    if (b >= B || k >= P.N) return;
     const MskGeom& G = *GG;
     const int nz = P.nz, nu = P.nu, Q = P.Q, residual = P.residual;
     const int64_t zb = (int64_t)k * nz;

@@ -13,6 +13,12 @@ namespace cfx {
 
 constexpr int kMskBlk = 256;
 
+// k_msk_values' grid: (instance blocks, interval) or, below one block of instances, flat over (interval, instance)
+inline dim3 msk_values_grid(const MskParams& P) {
+    if (P.B < kMskBlk && P.N > 1) return dim3((unsigned)((P.B * P.N + kMskBlk - 1) / kMskBlk), 1u);
+    return dim3((unsigned)((P.B + kMskBlk - 1) / kMskBlk), (unsigned)P.N);
+}
+
 template <int NQ, int NM, int FAM, int SCHEME>
 void dep_t(const MskParams& P, const MskGeom& G, uint64_t* dep) {
     constexpr int NX = NM * msk_nxm<FAM>() + 2 * NQ;
@@ -86,7 +92,7 @@ hipError_t shoot_t(const MskParams& P, const MskGeom* G, const double* V, double
             hipLaunchKernelGGL((k_msk_shooting<NQ, NM, FAM, SCHEME, 0>), dim3(gx, (unsigned)P.N), dim3(kMskBlk), 0, s, P,
                                G, V, Gout, J);
         else
-            hipLaunchKernelGGL((k_msk_values<NQ, NM, FAM, SCHEME>), dim3(gx, (unsigned)P.N), dim3(kMskBlk), 0, s, P, G, V,
+            hipLaunchKernelGGL((k_msk_values<NQ, NM, FAM, SCHEME>), msk_values_grid(P), dim3(kMskBlk), 0, s, P, G, V,
                                Gout, (double*)nullptr);
         return hipGetLastError();
     }
@@ -94,7 +100,7 @@ hipError_t shoot_t(const MskParams& P, const MskGeom* G, const double* V, double
     // thread per Jacobian column
     constexpr int NC = msk_ncoef<NQ, NM>();
     double* XS = P.scratch + P.B * P.N * P.Q * NC;
-    hipLaunchKernelGGL((k_msk_values<NQ, NM, FAM, SCHEME>), dim3(gx, (unsigned)P.N), dim3(kMskBlk), 0, s, P, G, V, Gout,
+    hipLaunchKernelGGL((k_msk_values<NQ, NM, FAM, SCHEME>), msk_values_grid(P), dim3(kMskBlk), 0, s, P, G, V, Gout,
                        XS);
     const int mode = msk_tangent_mode();
     const bool fuse = P.nz <= kMskLdsCols && mode != 2;
@@ -155,7 +161,7 @@ hipError_t hess_t(const MskParams& P, const MskGeom* G, const int16_t* tasks, in
     auto flat = [](int64_t items) { return dim3((unsigned)((items + kMskBlk - 1) / kMskBlk)); };
     const bool small = P.B <= kMskSmallBatch;
     if (!reuse) {  // stage values and coefficients (reuse: left by the g + J_g launch at this point)
-        hipLaunchKernelGGL((k_msk_values<NQ, NM, FAM, SCHEME>), dim3(gx, (unsigned)P.N), dim3(kMskBlk), 0, s, Pw, G, V,
+        hipLaunchKernelGGL((k_msk_values<NQ, NM, FAM, SCHEME>), msk_values_grid(P), dim3(kMskBlk), 0, s, Pw, G, V,
                            (double*)nullptr, XS);
         msk_stagecoef<NQ, NM, FAM>(Pw, G, V, XS, s);
     }
