@@ -2080,6 +2080,73 @@ __global__ void __launch_bounds__(256) k_msk_hproj_stage(const MskParams P, cons
     }
 }
 
+// k_msk_hproj_stage with each stage's pair Hessian G_q and tangents T_q staged in LDS: a block takes kMskHpS
+// consecutive stages of one instance, thread = (stage slot, column a).  Every column of a stage read the stage's G_q and
+// T_q from the cache on its own (~1,500 loads a thread; 452 us per call for the reaching task at batch 1); here they are
+// read from HBM once per stage (193 us).  The same sums in the same order as k_msk_hproj_stage; the entries agree to
+// rounding (the compiler forms the two kernels' multiply-adds differently), and the chaotic reaching solve follows
+// another path.
+constexpr int kMskHpS = 3;  // stages per block (LDS: 3 x (nz (nz + 1) / 2 + NX nz) doubles, 52 KB at nz = 40)
+inline size_t msk_hproj_lds(int nx, int nz) { return (size_t)kMskHpS * ((size_t)nz * (nz + 1) / 2 + (size_t)nx * nz) * 8; }
+template <int NQ, int NM, int FAM>
+__global__ void __launch_bounds__(kMskHpS * kMskMaxZ) k_msk_hproj_stage_lds(const MskParams P, const double* __restrict__ TS,
+                                                                            const double* __restrict__ GQ, int ntasks,
+                                                                            double* __restrict__ HQ) {
+    constexpr int NX = NM * msk_nxm<FAM>() + 2 * NQ;
+    constexpr int NZ = NX + (msk_pw<FAM>() ? NM : 0) + NQ;
+    extern __shared__ double sh[];  // [kMskHpS][ntasks] G, then [kMskHpS][NX nz] T
+    const int64_t B = P.B;
+    const int nz = P.nz;
+    const int64_t b = blockIdx.y;
+    const int64_t nkq = (int64_t)P.N * P.Q, kq0 = (int64_t)blockIdx.x * kMskHpS;
+    const int ns = (int)min((int64_t)kMskHpS, nkq - kq0);
+    double* sG = sh;
+    double* sT = sh + kMskHpS * ntasks;
+    const int nt = NX * nz;
+    for (int e = threadIdx.x; e < ns * ntasks; e += blockDim.x) {
+        const int sl = e / ntasks, t = e - sl * ntasks;
+        sG[e] = GQ[((kq0 + sl) * ntasks + t) * B + b];
+    }
+    for (int e = threadIdx.x; e < ns * nt; e += blockDim.x) {
+        const int sl = e / nt, t = e - sl * nt;
+        sT[e] = TS[((kq0 + sl) * nt + t) * B + b];
+    }
+    __syncthreads();
+    const int sl = threadIdx.x / nz, a = threadIdx.x - sl * nz;
+    if (sl >= ns) return;
+    const int64_t kq = kq0 + sl;
+    const double* ts = sT + sl * nt;
+    const double* gq = sG + sl * ntasks;
+    double ta[NZ], w[NZ];
+#pragma unroll
+    for (int I = 0; I < NX; ++I) ta[I] = ts[I * nz + a];
+#pragma unroll
+    for (int I = NX; I < NZ; ++I) ta[I] = I == a ? 1.0 : 0.0;
+#pragma unroll
+    for (int I = 0; I < NZ; ++I) w[I] = 0.0;
+#pragma unroll
+    for (int I = 0; I < NZ; ++I)
+#pragma unroll
+        for (int J = I; J < NZ; ++J) {
+            if (J >= nz) continue;
+            const int t = I * nz - I * (I - 1) / 2 + (J - I);
+            const double g = gq[t];
+            w[I] += g * ta[J];
+            if (J != I) w[J] += g * ta[I];
+        }
+    double* __restrict__ hq = HQ + kq * P.nhk * B + b;
+#pragma unroll
+    for (int c = 0; c < NZ; ++c) {
+        if (c < a || c >= nz) continue;
+        double sacc = 0.0;
+#pragma unroll
+        for (int e = NX; e < NZ; ++e) sacc = e == c ? w[e] : sacc;
+#pragma unroll
+        for (int I = 0; I < NX; ++I) sacc += ts[I * nz + c] * w[I];
+        hq[(int64_t)(c * (c + 1) / 2 + a) * B] = sacc;
+    }
+}
+
 // H[k][e] = sum over the interval's stages of HQ, in stage order (thread = instance, entry, interval)
 static __global__ void __launch_bounds__(256) k_msk_hproj_sum(const MskParams P, const double* __restrict__ HQ,
                                                        double* __restrict__ H) {

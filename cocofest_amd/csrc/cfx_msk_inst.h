@@ -182,8 +182,16 @@ hipError_t hess_t(const MskParams& P, const MskGeom* G, const int16_t* tasks, in
     }
     if (small) {
         double* HQ = GQ + BNQ * npair;
-        hipLaunchKernelGGL((k_msk_hproj_stage<NQ, NM, FAM>), flat(BNQ * P.nz), dim3(kMskBlk), 0, s, Pw,
-                           (const double*)TS, (const double*)GQ, npair, HQ);
+        const size_t lds = msk_hproj_lds(NX, P.nz);
+        if (lds <= 65536 && std::getenv("CFX_MSK_HPROJ") == nullptr) {  // stages staged in LDS (CFX_MSK_HPROJ: the old kernel)
+            const int64_t nkq = (int64_t)P.N * P.Q;
+            hipLaunchKernelGGL((k_msk_hproj_stage_lds<NQ, NM, FAM>),
+                               dim3((unsigned)((nkq + kMskHpS - 1) / kMskHpS), (unsigned)P.B), dim3(kMskHpS * kMskMaxZ), lds,
+                               s, Pw, (const double*)TS, (const double*)GQ, npair, HQ);
+        } else {
+            hipLaunchKernelGGL((k_msk_hproj_stage<NQ, NM, FAM>), flat(BNQ * P.nz), dim3(kMskBlk), 0, s, Pw,
+                               (const double*)TS, (const double*)GQ, npair, HQ);
+        }
         hipLaunchKernelGGL(k_msk_hproj_sum, flat(P.B * P.N * P.nhk), dim3(kMskBlk), 0, s, Pw, (const double*)HQ, H);
     } else {
         hipLaunchKernelGGL((k_msk_hproj<NQ, NM, FAM>), flat(P.B * P.N * P.nz), dim3(kMskBlk), 0, s, Pw,
