@@ -64,12 +64,13 @@ def test_warm_start_holds_the_stored_fatigue_optimum():
 
 def test_solve_from_the_reference_start_converges():
     """The full 1,500-interval fatigue solve through the product (ocp.solve(Solver.IPOPT(profile="cfx",
-    _bound_relax_factor=1e-8)): ~770 iterations / ~7 s on one MI355X) from the reference's start: Solve_Succeeded;
-    the oracle's C port confirms every continuity row (within Ipopt's constr_viol_tol 1e-4) and the marker rows; the
-    fatigue objective is below the stored iterate's 7.84196 (the stored point is no KKT point; this is one).  The
-    library profile because its path has been stable across builds (692-1,060 iterations in rounds 5-6); under the
-    Ipopt profile (adaptive mu) the same solve took 751 iterations with round 5's pivot kernel, 2,635 with round 6's,
-    and did not finish in 3,000 with a coarser pivot key — bench.py's reaching section reports it."""
+    _bound_relax_factor=1e-8)): 771-1,046 iterations / 5-7 s on one MI355X in round 6's builds) from the reference's
+    start: Solve_Succeeded; the oracle's C port confirms every continuity row (within Ipopt's constr_viol_tol 1e-4) and
+    the marker rows; the fatigue objective is below the stored iterate's 7.84196 (the stored point is no KKT point; this
+    is one).  The library profile because its path has stayed within the 3,000-iteration budget across builds
+    (692-1,060 iterations in rounds 5-6); under the Ipopt profile (adaptive mu) the same solve took 751 iterations with
+    round 5's pivot kernel, 2,635 or 981 with round 6's builds, and did not finish in 3,000 with a coarser pivot key —
+    bench.py's reaching section reports it."""
     from cocofest_amd import Solver
     from oracle import c_msk
     from oracle import fes_msk as M
