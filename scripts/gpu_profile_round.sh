@@ -2,7 +2,7 @@
 # usage: bash scripts/gpu_profile_round.sh <tag>
 set -o pipefail
 tag=$1
-cd /root/repo
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
 out=gpurun_out/$tag
 mkdir -p $out
 export TMPDIR=/tmp
